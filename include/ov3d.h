@@ -1,0 +1,112 @@
+/*
+ * ov3d.h — C ABI of libov3d_hip.so, the MI355X (gfx950) kernels of the
+ * open-vocabulary 3D detection hot path.
+ *
+ * Conventions:
+ *   - plain pointers to DEVICE memory, sizes as int; the caller (PyTorch)
+ *     allocates every output and workspace, the library owns no memory;
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream);
+ *     every entry point is stream-ordered and asynchronous (no host sync),
+ *     so it can be captured into a hipGraph;
+ *   - return 0 on success, OV3D_EINVAL on a bad argument, OV3D_ELAUNCH on a
+ *     HIP launch error.  The library never prints and never exit()s (the
+ *     upstream pointnet2 wrappers print and call exit(-1) on CUDA errors).
+ *
+ * Each entry point names the reference interface it replaces.
+ */
+#ifndef OV3D_H_
+#define OV3D_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OV3D_OK 0
+#define OV3D_EINVAL (-1)
+#define OV3D_ELAUNCH (-2)
+
+/* Library version / build tag (host-only, no device work). */
+const char* ov3d_version(void);
+
+/* Iterative furthest-point sampling.
+ * Replaces third_party.pointnet2.pointnet2_utils.furthest_point_sample
+ * (called at models/model_3detr.py:174 and inside PointnetSAModuleVotes,
+ * models/model_3detr.py:355-361, 385-391).
+ *   xyz      (B,N,3) f32      idx_out (B,M) int32, idx_out[:,0] = 0
+ *   new_xyz_out (B,M,3) f32 or NULL: fused gather_operation of the samples
+ *   workspace: B*N floats (only used when N > 20480), may be NULL otherwise.
+ * Tie rule = the upstream 512-thread tree reduction. */
+int ov3d_fps(const float* xyz, int B, int N, int M, int32_t* idx_out, float* new_xyz_out,
+             float* workspace, void* stream);
+
+/* Ball query: first S point indices (ascending) with |p - c|^2 < radius^2,
+ * padded with the first hit, zeros if none.
+ * Replaces pointnet2_utils.ball_query (QueryAndGroup, model_3detr.py:355-361).
+ *   xyz (B,N,3), new_xyz (B,M,3) f32  ->  idx_out (B,M,S) int32 */
+int ov3d_ball_query(const float* xyz, const float* new_xyz, int B, int N, int M, float radius,
+                    int S, int32_t* idx_out, void* stream);
+
+/* QueryAndGroup output with use_xyz=True (pointnet2_utils.QueryAndGroup.forward):
+ *   out[:, 0:3]   = (xyz[idx] - new_xyz) (/ radius if normalize)
+ *   out[:, 3:3+C] = features[:, :, idx]           (features may be NULL, C = 0)
+ *   xyz (B,N,3) f32, new_xyz (B,M,3), features (B,C,N), idx (B,M,S) -> out (B,3+C,M,S) */
+int ov3d_group_fwd(const float* xyz, const float* new_xyz, const float* features,
+                   const int32_t* idx, int B, int C, int N, int M, int S, float radius,
+                   int normalize, float* out, void* stream);
+
+/* Backward of the feature part of ov3d_group_fwd (grouping_operation backward):
+ *   grad_out (B,3+C,M,S) -> grad_features (B,C,N); the callee zero-fills
+ *   grad_features on the stream, then scatter-adds. */
+int ov3d_group_bwd(const float* grad_out, const int32_t* idx, int B, int C, int N, int M, int S,
+                   float* grad_features, void* stream);
+
+/* gather_operation (pointnet2_utils): features (B,C,N), idx (B,M) -> out (B,C,M) */
+int ov3d_gather_fwd(const float* features, const int32_t* idx, int B, int C, int N, int M,
+                    float* out, void* stream);
+/* gather_operation backward: grad_out (B,C,M) -> grad_features (B,C,N) (zero-filled here) */
+int ov3d_gather_bwd(const float* grad_out, const int32_t* idx, int B, int C, int N, int M,
+                    float* grad_features, void* stream);
+
+/* 3D generalized IoU, (B,K1) predicted vs (B,K2) GT boxes given as corners
+ * (B,K,8,3) f32 with up = -Y.  Replaces utils/box_util.py:717-737:
+ *   mode OV3D_GIOU_CYTHON (0): generalized_box3d_iou_cython (box_util.py:624-714)
+ *        + utils/box_intersection.pyx (double-precision clipping); with
+ *        k2_bug != 0 the rotated intersection is evaluated only for
+ *        k2 < min(4, nums[b]) (box_intersection.pyx:180, K2 = rect2.shape[2]).
+ *   mode OV3D_GIOU_TENSOR (1): generalized_box3d_iou_tensor (box_util.py:517-618),
+ *        float32 clipping, all k2 < nums[b].
+ *   rotated == 0: axis-aligned (x,z) rectangle intersection (box_util.py:695-696).
+ * nums (B,) int32 = number of valid GT boxes per scene, or NULL (= K2).
+ * out (B,K1,K2) f32. */
+#define OV3D_GIOU_CYTHON 0
+#define OV3D_GIOU_TENSOR 1
+int ov3d_giou3d(const float* corners1, const float* corners2, const int32_t* nums, int B, int K1,
+                int K2, int mode, int rotated, int k2_bug, float* out, void* stream);
+
+/* Backward of the axis-aligned (rotated == 0) GIoU w.r.t. corners1:
+ * grad_out (B,K1,K2) -> grad_corners1 (B,K1,8,3) (overwritten). */
+int ov3d_giou3d_bwd_aligned(const float* corners1, const float* corners2, const int32_t* nums,
+                            int B, int K1, int K2, const float* grad_out, float* grad_corners1,
+                            void* stream);
+
+/* Greedy 3D NMS, batched over scenes.  Replaces utils/nms.py:79-162
+ * (nms_3d_faster / nms_3d_faster_samecls) as called per scene by
+ * utils/ap_calculator.py:153-190.
+ *   boxes (B,K,stride) f64 rows [x1,y1,z1,x2,y2,z2,score(,cls)], stride 7|8
+ *   valid (B,K) uint8 or NULL: rows with 0 do not take part (nonempty mask)
+ *   keep_out (B,K) uint8 (1 = picked).  samecls: suppress only same class.
+ * Ties in score: larger index first (== np.argsort(kind="stable")).  K <= 512. */
+int ov3d_nms3d(const double* boxes, const uint8_t* valid, int B, int K, int stride, double thr,
+               int old_type, int samecls, uint8_t* keep_out, void* stream);
+
+/* NMS box table straight from predicted corners (ap_calculator.py:153-190):
+ *   corners (B,K,8,3) f32, obj (B,K) f32, cls (B,K) int64 -> boxes (B,K,8) f64 */
+int ov3d_nms_boxes_from_corners(const float* corners, const float* obj, const int64_t* cls, int B,
+                                int K, double* boxes_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OV3D_H_ */

@@ -1,0 +1,100 @@
+"""ctypes binding of ``lib/libov3d_hip.so`` (the C ABI declared in include/ov3d.h).
+
+This is the only door from Python to the hot-path kernels.  There is no CPU
+fallback: if the library is missing, or a tensor is not on a ROCm device, the
+call raises.  Pointers are ``tensor.data_ptr()``; the stream is torch's current
+HIP stream on the tensor's device, so every op is stream-ordered with the
+surrounding torch work and capturable into a hipGraph.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libov3d_hip.so")
+
+OV3D_GIOU_CYTHON = 0
+OV3D_GIOU_TENSOR = 1
+
+_lib = None
+
+# name -> argtypes ("p" pointer, "i" int, "f" float, "d" double)
+_SIGS = {
+    "ov3d_fps": "piiipppp",
+    "ov3d_ball_query": "ppiiifipp",
+    "ov3d_group_fwd": "ppppiiiiifipp",
+    "ov3d_group_bwd": "ppiiiiipp",
+    "ov3d_gather_fwd": "ppiiiipp",
+    "ov3d_gather_bwd": "ppiiiipp",
+    "ov3d_giou3d": "pppiiiiiipp",
+    "ov3d_giou3d_bwd_aligned": "pppiiippp",
+    "ov3d_nms3d": "ppiiidiipp",
+    "ov3d_nms_boxes_from_corners": "pppiipp",
+}
+EXPORTS = tuple(_SIGS) + ("ov3d_version",)
+
+_CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "f": ctypes.c_float, "d": ctypes.c_double}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libov3d_hip.so (raises if it was not built: run __graft_entry__.build())."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(
+                f"{LIB_PATH} not found: the HIP extension is required (no CPU fallback); "
+                "build it with `make -C open-vocabulary-3d-object-detection_amd/csrc`")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, sig in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = [_CT[c] for c in sig]
+            fn.restype = ctypes.c_int
+        lib.ov3d_version.argtypes = []
+        lib.ov3d_version.restype = ctypes.c_char_p
+        _lib = lib
+    return _lib
+
+
+def version():
+    return load().ov3d_version().decode()
+
+
+def _stream(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def check(t, name, dtype=None, ndim=None):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a tensor")
+    if t.device.type != "cuda":
+        raise NativeError(f"{name}: ov3d kernels run on the ROCm device only (got {t.device})")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if ndim is not None and t.dim() != ndim:
+        raise ValueError(f"{name}: expected {ndim}-d tensor, got shape {tuple(t.shape)}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    return t
+
+
+def call(name, *args, like):
+    """Invoke `name` with args (+ the current stream of `like`); raise on nonzero status."""
+    fn = getattr(load(), name)
+    conv = []
+    for a in args:
+        if isinstance(a, torch.Tensor) or a is None:
+            conv.append(_ptr(a))
+        else:
+            conv.append(a)
+    rc = fn(*conv, _stream(like))
+    if rc != 0:
+        raise NativeError(f"{name} failed with status {rc}")

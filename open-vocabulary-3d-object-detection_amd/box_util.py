@@ -1,0 +1,134 @@
+"""Box geometry and 3D GIoU on the ov3d HIP kernels (mirror of the hot-path
+parts of reference utils/box_util.py).
+
+``generalized_box3d_iou`` keeps the reference signature (box_util.py:717-724)
+and its dispatch: ``needs_grad=False`` -> the Cython semantics
+(box_util.py:624-714 + box_intersection.pyx, including the K2 bug, Q1, unless
+``k2_bug=False``), ``needs_grad=True`` -> the TorchScript semantics
+(box_util.py:517-618) with an analytic HIP backward for the axis-aligned case.
+Both run on the device (the reference copies rectangles to the host and loops
+in Cython, box_util.py:684-698).
+"""
+import numpy as np
+import torch
+from torch.autograd import Function
+
+from . import _native as nat
+
+
+# ----------------------------------------------------------------- geometry
+def flip_axis_to_camera_tensor(pc):
+    """depth (X right, Y fwd, Z up) -> camera (X right, Y down, Z fwd): (x, -z, y)"""
+    return torch.stack([pc[..., 0], -pc[..., 2], pc[..., 1]], dim=-1)
+
+
+def flip_axis_to_camera_np(pc):
+    pc2 = pc.copy()
+    pc2[..., [0, 1, 2]] = pc2[..., [0, 2, 1]]
+    pc2[..., 1] *= -1
+    return pc2
+
+
+# corner sign pattern of reference get_3d_box_batch_tensor (box_util.py:337-345)
+_SX = (1, 1, -1, -1, 1, 1, -1, -1)
+_SY = (1, 1, 1, 1, -1, -1, -1, -1)
+_SZ = (1, -1, -1, 1, 1, -1, -1, 1)
+
+
+def get_3d_box_batch_tensor(box_size, angle, center):
+    """(…,3) size (l,w,h), (…) yaw about camera Y, (…,3) center -> (…,8,3) corners.
+
+    corner = R_y(angle) @ (sx*l/2, sy*h/2, sz*w/2) + center (box_util.py:313-352)."""
+    l = box_size[..., 0:1] / 2
+    w = box_size[..., 1:2] / 2
+    h = box_size[..., 2:3] / 2
+    sx = torch.tensor(_SX, dtype=box_size.dtype, device=box_size.device)
+    sy = torch.tensor(_SY, dtype=box_size.dtype, device=box_size.device)
+    sz = torch.tensor(_SZ, dtype=box_size.dtype, device=box_size.device)
+    lx, ly, lz = l * sx, h * sy, w * sz
+    c = torch.cos(angle)[..., None]
+    s = torch.sin(angle)[..., None]
+    x = lx * c + lz * s + center[..., 0:1]
+    y = ly + center[..., 1:2]
+    z = lz * c - lx * s + center[..., 2:3]
+    return torch.stack([x, y, z], dim=-1)
+
+
+def roty_batch_np(t):
+    out = np.zeros(tuple(t.shape) + (3, 3))
+    c, s = np.cos(t), np.sin(t)
+    out[..., 0, 0] = c
+    out[..., 0, 2] = s
+    out[..., 1, 1] = 1
+    out[..., 2, 0] = -s
+    out[..., 2, 2] = c
+    return out
+
+
+def get_3d_box_batch_np(box_size, angle, center):
+    R = roty_batch_np(angle)
+    l, w, h = box_size[..., 0:1], box_size[..., 1:2], box_size[..., 2:3]
+    corners = np.zeros(tuple(angle.shape) + (8, 3))
+    corners[..., :, 0] = np.concatenate([s * l / 2 for s in _SX], -1)
+    corners[..., :, 1] = np.concatenate([s * h / 2 for s in _SY], -1)
+    corners[..., :, 2] = np.concatenate([s * w / 2 for s in _SZ], -1)
+    nd = len(angle.shape)
+    corners = np.matmul(corners, np.transpose(R, tuple(range(nd)) + (nd + 1, nd)))
+    return corners + np.expand_dims(center, -2)
+
+
+# --------------------------------------------------------------------- GIoU
+def _prep(corners1, corners2, nums_k2):
+    c1 = nat.check(corners1.detach().float().contiguous(), "corners1", torch.float32, 4)
+    c2 = nat.check(corners2.detach().float().contiguous(), "corners2", torch.float32, 4)
+    if c1.shape[0] != c2.shape[0] or c1.shape[2:] != (8, 3) or c2.shape[2:] != (8, 3):
+        raise ValueError("corners must be (B,K,8,3) with matching B")
+    nums = None
+    if nums_k2 is not None:
+        nums = nat.check(nums_k2.to(device=c1.device, dtype=torch.int32).contiguous(), "nums_k2",
+                         torch.int32, 1)
+    return c1, c2, nums
+
+
+def giou3d_raw(corners1, corners2, nums_k2, mode, rotated, k2_bug=True):
+    c1, c2, nums = _prep(corners1, corners2, nums_k2)
+    B, K1 = c1.shape[:2]
+    K2 = c2.shape[1]
+    out = torch.empty((B, K1, K2), dtype=torch.float32, device=c1.device)
+    nat.call("ov3d_giou3d", c1, c2, nums, B, K1, K2, int(mode), int(bool(rotated)),
+             int(bool(k2_bug)), out, like=c1)
+    return out
+
+
+class _GIoUAligned(Function):
+    @staticmethod
+    def forward(ctx, corners1, corners2, nums_k2):
+        c1, c2, nums = _prep(corners1, corners2, nums_k2)
+        ctx.save_for_backward(c1, c2, nums if nums is not None else torch.empty(0))
+        ctx.has_nums = nums is not None
+        return giou3d_raw(c1, c2, nums, nat.OV3D_GIOU_TENSOR, False)
+
+    @staticmethod
+    def backward(ctx, g):
+        c1, c2, nums = ctx.saved_tensors
+        nums = nums if ctx.has_nums else None
+        g = nat.check(g.float().contiguous(), "grad", torch.float32, 3)
+        B, K1, K2 = g.shape
+        gc1 = torch.empty_like(c1)
+        nat.call("ov3d_giou3d_bwd_aligned", c1, c2, nums, B, K1, K2, g, gc1, like=g)
+        return gc1, None, None
+
+
+def generalized_box3d_iou(corners1, corners2, nums_k2, rotated_boxes=True,
+                          return_inter_vols_only=False, needs_grad=False, k2_bug=True):
+    """(B,K1,8,3), (B,K2,8,3), (B,) -> (B,K1,K2) generalized IoU."""
+    if return_inter_vols_only:
+        raise NotImplementedError("return_inter_vols_only is not on the training path")
+    if needs_grad:
+        if rotated_boxes:
+            raise NotImplementedError(
+                "differentiable rotated GIoU (loss_giou_weight > 0 with rotated GT) is not "
+                "implemented yet; the reference evaluates it with a Python triple loop")
+        return _GIoUAligned.apply(corners1, corners2, nums_k2)
+    with torch.no_grad():
+        return giou3d_raw(corners1, corners2, nums_k2, nat.OV3D_GIOU_CYTHON, rotated_boxes, k2_bug)

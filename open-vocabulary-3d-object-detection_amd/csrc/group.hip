@@ -1,0 +1,236 @@
+// Ball query, grouping and gather for gfx950.
+//
+// Replaces the un-vendored third_party.pointnet2 ops used by
+// PointnetSAModuleVotes / QueryAndGroup (models/model_3detr.py:355-361, 385-391):
+// ball_query, grouping_operation (+ backward), gather_operation (+ backward).
+//
+// Ball query = one wave64 per centroid.  Each lane owns 4 consecutive points of a
+// 256-point chunk (3 x 16-B loads per lane, one coalesced 3 KiB wave read), four
+// ballots give the in-radius masks, and popcounts of the masks below the lane give
+// every hit its slot -- so the output is the first S in-radius indices in
+// ascending order exactly as the upstream sequential scan produces them, and the
+// wave stops at the first chunk that fills S slots.
+#include "common.h"
+
+namespace {
+
+constexpr int kBQWavesPerBlock = 4;
+
+template <bool ALIGNED>
+__device__ __forceinline__ void load4(const float* __restrict__ p, int k0, int N, float (&x)[4],
+                                      float (&y)[4], float (&z)[4]) {
+    if (ALIGNED && k0 + 3 < N) {
+        const float4* q = reinterpret_cast<const float4*>(p + 3 * (size_t)k0);
+        const float4 a = q[0], b = q[1], c = q[2];
+        x[0] = a.x; y[0] = a.y; z[0] = a.z;
+        x[1] = a.w; y[1] = b.x; z[1] = b.y;
+        x[2] = b.z; y[2] = b.w; z[2] = c.x;
+        x[3] = c.y; y[3] = c.z; z[3] = c.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = k0 + j;
+            if (k < N) { x[j] = p[3 * k]; y[j] = p[3 * k + 1]; z[j] = p[3 * k + 2]; }
+            else { x[j] = 0.f; y[j] = 0.f; z[j] = 0.f; }
+        }
+    }
+}
+
+template <bool ALIGNED>
+__global__ __launch_bounds__(64 * kBQWavesPerBlock) void ball_query_kernel(
+    const float* __restrict__ xyz, const float* __restrict__ new_xyz, int B, int N, int M, float r2,
+    int S, int32_t* __restrict__ idx) {
+    const int gw = blockIdx.x * kBQWavesPerBlock + (threadIdx.x >> 6);
+    if (gw >= B * M) return;  // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const int b = gw / M;
+    const float* __restrict__ p = xyz + (size_t)b * N * 3;
+    const float cx = new_xyz[(size_t)gw * 3], cy = new_xyz[(size_t)gw * 3 + 1],
+                cz = new_xyz[(size_t)gw * 3 + 2];
+    int32_t* __restrict__ out = idx + (size_t)gw * S;
+    const unsigned long long below = lanemask_lt();
+    int cnt = 0;
+    int first = 0;
+    for (int base = 0; base < N && cnt < S; base += 256) {
+        const int k0 = base + 4 * lane;
+        float x[4], y[4], z[4];
+        load4<ALIGNED>(p, k0, N, x, y, z);
+        bool hit[4];
+        unsigned long long m[4];
+        int tot = 0, pre = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float dx = cx - x[j], dy = cy - y[j], dz = cz - z[j];
+            const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+            hit[j] = (k0 + j < N) && (d2 < r2);
+            m[j] = __ballot(hit[j]);
+            tot += __popcll(m[j]);
+            pre += __popcll(m[j] & below);
+        }
+        if (tot == 0) continue;
+        if (cnt == 0) {
+            int f = 0x7fffffff;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (m[j]) { const int c = base + 4 * (__ffsll((long long)m[j]) - 1) + j; f = c < f ? c : f; }
+            first = f;
+        }
+        int pos = cnt + pre;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (hit[j]) {
+                if (pos < S) out[pos] = k0 + j;
+                ++pos;
+            }
+        }
+        cnt += tot;
+    }
+    const int filled = cnt < S ? cnt : S;
+    const int fill = cnt > 0 ? first : 0;
+    for (int s = filled + lane; s < S; s += 64) out[s] = fill;
+}
+
+// out (B,3+C,M,S): thread per (b, m, s)
+__global__ __launch_bounds__(256) void group_fwd_kernel(
+    const float* __restrict__ xyz, const float* __restrict__ new_xyz,
+    const float* __restrict__ feats, const int32_t* __restrict__ idx, int B, int C, int N, int M,
+    int S, float radius, int normalize, float* __restrict__ out) {
+    const long long MS = (long long)M * S;
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long long)B * MS) return;
+    const int b = (int)(t / MS);
+    const long long ms = t - (long long)b * MS;
+    const int m = (int)(ms / S);
+    const int k = idx[t];
+    const float* c = new_xyz + ((size_t)b * M + m) * 3;
+    const float* q = xyz + ((size_t)b * N + k) * 3;
+    float* o = out + (size_t)b * (3 + C) * MS + ms;
+    float gx = q[0] - c[0], gy = q[1] - c[1], gz = q[2] - c[2];
+    if (normalize) { gx = gx / radius; gy = gy / radius; gz = gz / radius; }
+    o[0] = gx;
+    o[MS] = gy;
+    o[2 * MS] = gz;
+    if (feats) {
+        const float* f = feats + (size_t)b * C * N + k;
+        float* of = o + 3 * MS;
+        for (int ch = 0; ch < C; ++ch) of[(size_t)ch * MS] = f[(size_t)ch * N];
+    }
+}
+
+__global__ __launch_bounds__(256) void group_bwd_kernel(const float* __restrict__ gout,
+                                                        const int32_t* __restrict__ idx, int B,
+                                                        int C, int N, int M, int S,
+                                                        float* __restrict__ gfeat) {
+    const long long MS = (long long)M * S;
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long long)B * MS) return;
+    const int b = (int)(t / MS);
+    const long long ms = t - (long long)b * MS;
+    const int k = idx[t];
+    const float* g = gout + (size_t)b * (3 + C) * MS + 3 * MS + ms;
+    float* d = gfeat + (size_t)b * C * N + k;
+    for (int ch = 0; ch < C; ++ch) atomicAdd(d + (size_t)ch * N, g[(size_t)ch * MS]);
+}
+
+// (B,C,N),(B,M) -> (B,C,M): thread per output element
+__global__ __launch_bounds__(256) void gather_fwd_kernel(const float* __restrict__ f,
+                                                         const int32_t* __restrict__ idx, int B,
+                                                         int C, int N, int M,
+                                                         float* __restrict__ out) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long long)B * C * M) return;
+    const int m = (int)(t % M);
+    const long long bc = t / M;
+    const int b = (int)(bc / C);
+    out[t] = f[bc * N + idx[(size_t)b * M + m]];
+}
+
+__global__ __launch_bounds__(256) void gather_bwd_kernel(const float* __restrict__ g,
+                                                         const int32_t* __restrict__ idx, int B,
+                                                         int C, int N, int M,
+                                                         float* __restrict__ gf) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long long)B * C * M) return;
+    const int m = (int)(t % M);
+    const long long bc = t / M;
+    const int b = (int)(bc / C);
+    atomicAdd(gf + bc * N + idx[(size_t)b * M + m], g[t]);
+}
+
+}  // namespace
+
+extern "C" int ov3d_ball_query(const float* xyz, const float* new_xyz, int B, int N, int M,
+                               float radius, int S, int32_t* idx_out, void* stream) {
+    if (B < 0 || N < 0 || M < 0 || S <= 0 || !xyz || !new_xyz || !idx_out) return OV3D_EINVAL;
+    if ((long long)B * M == 0) return OV3D_OK;
+    const float r2 = radius * radius;
+    const int blocks = ov3d_cdiv((long long)B * M, kBQWavesPerBlock);
+    hipStream_t s = ov3d_stream(stream);
+    const bool aligned = (reinterpret_cast<uintptr_t>(xyz) % 16 == 0) && (N % 4 == 0);
+    if (aligned)
+        hipLaunchKernelGGL(ball_query_kernel<true>, dim3(blocks), dim3(64 * kBQWavesPerBlock), 0, s,
+                           xyz, new_xyz, B, N, M, r2, S, idx_out);
+    else
+        hipLaunchKernelGGL(ball_query_kernel<false>, dim3(blocks), dim3(64 * kBQWavesPerBlock), 0, s,
+                           xyz, new_xyz, B, N, M, r2, S, idx_out);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_group_fwd(const float* xyz, const float* new_xyz, const float* features,
+                              const int32_t* idx, int B, int C, int N, int M, int S, float radius,
+                              int normalize, float* out, void* stream) {
+    if (B < 0 || C < 0 || N <= 0 || M < 0 || S <= 0 || !xyz || !new_xyz || !idx || !out)
+        return OV3D_EINVAL;
+    if (C > 0 && !features) return OV3D_EINVAL;
+    const long long total = (long long)B * M * S;
+    if (total == 0) return OV3D_OK;
+    hipLaunchKernelGGL(group_fwd_kernel, dim3(ov3d_cdiv(total, 256)), dim3(256), 0,
+                       ov3d_stream(stream), xyz, new_xyz, C > 0 ? features : nullptr, idx, B, C, N,
+                       M, S, radius, normalize, out);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_group_bwd(const float* grad_out, const int32_t* idx, int B, int C, int N, int M,
+                              int S, float* grad_features, void* stream) {
+    if (B < 0 || C < 0 || N <= 0 || M < 0 || S <= 0 || !grad_out || !idx || !grad_features)
+        return OV3D_EINVAL;
+    hipStream_t s = ov3d_stream(stream);
+    if ((long long)B * C * N > 0 &&
+        hipMemsetAsync(grad_features, 0, sizeof(float) * (size_t)B * C * N, s) != hipSuccess)
+        return OV3D_ELAUNCH;
+    const long long total = (long long)B * M * S;
+    if (total == 0 || C == 0) return OV3D_OK;
+    hipLaunchKernelGGL(group_bwd_kernel, dim3(ov3d_cdiv(total, 256)), dim3(256), 0, s, grad_out,
+                       idx, B, C, N, M, S, grad_features);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_gather_fwd(const float* features, const int32_t* idx, int B, int C, int N,
+                               int M, float* out, void* stream) {
+    if (B < 0 || C < 0 || N <= 0 || M < 0 || !features || !idx || !out) return OV3D_EINVAL;
+    const long long total = (long long)B * C * M;
+    if (total == 0) return OV3D_OK;
+    hipLaunchKernelGGL(gather_fwd_kernel, dim3(ov3d_cdiv(total, 256)), dim3(256), 0,
+                       ov3d_stream(stream), features, idx, B, C, N, M, out);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_gather_bwd(const float* grad_out, const int32_t* idx, int B, int C, int N,
+                               int M, float* grad_features, void* stream) {
+    if (B < 0 || C < 0 || N <= 0 || M < 0 || !grad_out || !idx || !grad_features)
+        return OV3D_EINVAL;
+    hipStream_t s = ov3d_stream(stream);
+    if ((long long)B * C * N > 0 &&
+        hipMemsetAsync(grad_features, 0, sizeof(float) * (size_t)B * C * N, s) != hipSuccess)
+        return OV3D_ELAUNCH;
+    const long long total = (long long)B * C * M;
+    if (total == 0) return OV3D_OK;
+    hipLaunchKernelGGL(gather_bwd_kernel, dim3(ov3d_cdiv(total, 256)), dim3(256), 0, s, grad_out,
+                       idx, B, C, N, M, grad_features);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}

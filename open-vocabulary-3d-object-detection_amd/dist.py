@@ -1,0 +1,148 @@
+"""Distributed helpers (API mirror of reference utils/dist.py:8-176) on
+torch.distributed; on ROCm the "nccl" backend is RCCL over xGMI.
+
+Same function names and semantics as the reference, plus
+``all_reduce_coalesced`` (one collective for many scalars: the reference issues
+one all-reduce for num_boxes, one for the loss and one for the stacked loss
+dict every step, criterion.py:425 and engine.py:104-105).  One process per GPU;
+the rendezvous comes from the environment (torchrun) or ``init_distributed``.
+"""
+import os
+import pickle
+
+import torch
+import torch.distributed as dist
+
+
+def is_distributed():
+    return dist.is_available() and dist.is_initialized()
+
+
+def get_rank():
+    return dist.get_rank() if is_distributed() else 0
+
+
+def is_primary():
+    return get_rank() == 0
+
+
+def get_world_size():
+    return dist.get_world_size() if is_distributed() else 1
+
+
+def barrier():
+    if is_distributed():
+        dist.barrier()
+
+
+def setup_print_for_distributed(is_primary_rank):
+    import builtins
+    builtin_print = builtins.print
+
+    def _print(*args, **kwargs):
+        force = kwargs.pop("force", False)
+        if is_primary_rank or force:
+            builtin_print(*args, **kwargs)
+
+    builtins.print = _print
+
+
+def init_distributed(gpu_id, global_rank, world_size, dist_url, dist_backend):
+    """reference dist.py:51-64 (dist_url e.g. tcp://127.0.0.1:12345 or env://)."""
+    if torch.cuda.is_available() and dist_backend == "nccl":
+        torch.cuda.set_device(gpu_id)
+    dist.init_process_group(backend=dist_backend, init_method=dist_url, world_size=world_size,
+                            rank=global_rank)
+    dist.barrier()
+    setup_print_for_distributed(is_primary())
+
+
+def init_from_env(backend=None):
+    """torchrun-style init (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* in the env)."""
+    if is_distributed():
+        return get_rank(), get_world_size(), int(os.environ.get("LOCAL_RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend, init_method="env://", world_size=world, rank=rank)
+    return rank, world, local
+
+
+def all_reduce_sum(tensor):
+    if not is_distributed():
+        return tensor
+    squeeze = tensor.ndim == 0
+    if squeeze:
+        tensor = tensor[None]
+    dist.all_reduce(tensor)
+    return tensor.squeeze(0) if squeeze else tensor
+
+
+def all_reduce_average(tensor):
+    return all_reduce_sum(tensor) / get_world_size()
+
+
+def all_reduce_coalesced(tensors, average=True):
+    """All-reduce a list of scalar / small tensors with ONE collective."""
+    if not is_distributed():
+        return list(tensors)
+    flat = torch.cat([t.detach().reshape(-1).float() for t in tensors])
+    dist.all_reduce(flat)
+    if average:
+        flat /= get_world_size()
+    out, off = [], 0
+    for t in tensors:
+        n = t.numel()
+        out.append(flat[off: off + n].view(t.shape))
+        off += n
+    return out
+
+
+def reduce_dict(input_dict, average=True):
+    """reference dist.py:82-108: sorted keys, one stacked all-reduce."""
+    if get_world_size() < 2:
+        return input_dict
+    with torch.no_grad():
+        names = sorted(input_dict.keys())
+        values = torch.stack([input_dict[k] for k in names], dim=0)
+        dist.all_reduce(values)
+        if average:
+            values /= get_world_size()
+        return {k: v for k, v in zip(names, values)}
+
+
+def all_gather_pickle(data, device):
+    world = get_world_size()
+    if world == 1:
+        return [data]
+    buf = torch.frombuffer(bytearray(pickle.dumps(data)), dtype=torch.uint8).to(device)
+    size = torch.tensor([buf.numel()], device=device)
+    sizes = [torch.zeros_like(size) for _ in range(world)]
+    dist.all_gather(sizes, size)
+    sizes = [int(s.item()) for s in sizes]
+    mx = max(sizes)
+    if buf.numel() < mx:
+        buf = torch.cat([buf, torch.zeros(mx - buf.numel(), dtype=torch.uint8, device=device)])
+    bufs = [torch.empty((mx,), dtype=torch.uint8, device=device) for _ in range(world)]
+    dist.all_gather(bufs, buf)
+    return [pickle.loads(b.cpu().numpy().tobytes()[:s]) for b, s in zip(bufs, sizes)]
+
+
+def all_gather_dict(data):
+    if not isinstance(data, dict):
+        raise TypeError("all_gather_dict expects a dict of tensors")
+    out = {}
+    for k, v in data.items():
+        if isinstance(v, torch.Tensor):
+            if is_distributed():
+                v = v.contiguous()
+                parts = [torch.empty_like(v) for _ in range(get_world_size())]
+                dist.all_gather(parts, v)
+                v = torch.cat(parts, dim=0)
+            out[k] = v
+    return out

@@ -1,0 +1,68 @@
+"""MLP building blocks (mirror of reference models/helpers.py).
+
+``GenericMLP`` keeps the reference's ``layers`` Sequential indexing
+(conv/linear, [norm], activation, [dropout], ..., out conv, [norm], [act]) so
+state-dict keys such as ``mlp_heads.center_head.layers.0.weight`` load
+unchanged (reference models/helpers.py:45-112).
+"""
+import copy
+
+import torch.nn as nn
+
+NORM_DICT = {
+    "bn1d": nn.BatchNorm1d,
+    "id": nn.Identity,
+    "ln": nn.LayerNorm,
+}
+
+ACTIVATION_DICT = {
+    "relu": nn.ReLU,
+    "gelu": nn.GELU,
+}
+
+
+class GenericMLP(nn.Module):
+    def __init__(self, input_dim, hidden_dims, output_dim, norm_fn_name=None, activation="relu",
+                 use_conv=False, dropout=None, hidden_use_bias=False, output_use_bias=True,
+                 output_use_activation=False, output_use_norm=False, weight_init_name=None):
+        super().__init__()
+        act = ACTIVATION_DICT[activation]
+        if norm_fn_name == "ln" and use_conv:
+            norm = lambda c: nn.GroupNorm(1, c)  # noqa: E731  (reference: LayerNorm over conv channels)
+        elif norm_fn_name is not None:
+            norm = NORM_DICT[norm_fn_name]
+        else:
+            norm = None
+        if dropout is not None and not isinstance(dropout, list):
+            dropout = [dropout] * len(hidden_dims)
+
+        def proj(cin, cout, bias):
+            return nn.Conv1d(cin, cout, 1, bias=bias) if use_conv else nn.Linear(cin, cout, bias=bias)
+
+        mods = []
+        cin = input_dim
+        for i, h in enumerate(hidden_dims):
+            mods.append(proj(cin, h, hidden_use_bias))
+            if norm is not None:
+                mods.append(norm(h))
+            mods.append(act())
+            if dropout is not None:
+                mods.append(nn.Dropout(p=dropout[i]))
+            cin = h
+        mods.append(proj(cin, output_dim, output_use_bias))
+        if output_use_norm:
+            mods.append(norm(output_dim))
+        if output_use_activation:
+            mods.append(act())
+        self.layers = nn.Sequential(*mods)
+        if weight_init_name is not None:
+            for p in self.parameters():
+                if p.dim() > 1:
+                    nn.init.xavier_uniform_(p)
+
+    def forward(self, x):
+        return self.layers(x)
+
+
+def get_clones(module, n):
+    return nn.ModuleList([copy.deepcopy(module) for _ in range(n)])

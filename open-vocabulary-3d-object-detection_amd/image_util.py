@@ -1,0 +1,77 @@
+"""3D box -> 2D image box projection for the RegionCLIP alignment branch
+(mirror of reference utils/image_util.py:117-146, 238-298 as used by
+criterion.py:366-396), batched over scenes and decoder layers on the device.
+
+Reference quirk Q4 reproduced: the predicted *full* size is used as the
+half-extent (image_util.py:124-127 receives size_unnormalized), and the box is
+returned as [min v, min u, max v, max u] (x/y swapped, image_util.py:131-133)
+before the [w, h, w, h] clamp of criterion.py:389-391.
+"""
+import torch
+
+
+class Boxes:
+    """Minimal stand-in for detectron2.structures.Boxes (used only if detectron2 is absent)."""
+
+    def __init__(self, tensor):
+        self.tensor = tensor
+
+
+class Instances:
+    """Minimal stand-in for detectron2.structures.Instances."""
+
+    def __init__(self, image_size, **fields):
+        self.image_size = image_size
+        for k, v in fields.items():
+            setattr(self, k, v)
+
+
+def _structures():
+    try:  # the real RegionCLIP stack, when installed
+        from detectron2.structures import Boxes as B2, Instances as I2
+        return B2, I2
+    except Exception:  # pragma: no cover - detectron2 is absent in this image
+        return Boxes, Instances
+
+
+def project_boxes_2d(center, size, heading, Rtilt, K, img_h, img_w):
+    """center/size (B,Q,3), heading (B,Q), Rtilt/K (B,3,3), img_h/img_w (B,) -> (B,Q,4)."""
+    c = torch.cos(-heading)[..., None]
+    s = torch.sin(-heading)[..., None]
+    l, w, h = size[..., 0:1], size[..., 1:2], size[..., 2:3]
+    sx = torch.tensor([-1, 1, 1, -1, -1, 1, 1, -1], dtype=size.dtype, device=size.device)
+    sy = torch.tensor([1, 1, -1, -1, 1, 1, -1, -1], dtype=size.dtype, device=size.device)
+    sz = torch.tensor([1, 1, 1, 1, -1, -1, -1, -1], dtype=size.dtype, device=size.device)
+    xc, yc, zc = l * sx, w * sy, h * sz                               # (B,Q,8)
+    X = c * xc - s * yc + center[..., 0:1]                            # rotz(-heading) @ corners
+    Y = s * xc + c * yc + center[..., 1:2]
+    Z = zc + center[..., 2:3]
+    P = torch.stack([X, Y, Z], dim=-1)                                # (B,Q,8,3) upright depth
+    Rt = Rtilt.float()[:, None, None]                                 # (B,1,1,3,3)
+    D = (Rt.transpose(-1, -2) @ P[..., None]).squeeze(-1)             # Rtilt^T @ p
+    cam = torch.stack([D[..., 0], -D[..., 2], D[..., 1]], dim=-1)     # flip_axis_to_camera
+    uvw = (K.float()[:, None, None] @ cam[..., None]).squeeze(-1)
+    u = uvw[..., 0] / uvw[..., 2]
+    v = uvw[..., 1] / uvw[..., 2]
+    umin, umax = u.min(dim=-1).values, u.max(dim=-1).values
+    vmin, vmax = v.min(dim=-1).values, v.max(dim=-1).values
+    box = torch.stack([vmin, umin, vmax, umax], dim=-1)               # Q4 swap
+    wf = img_w.to(box.dtype)[:, None]
+    hf = img_h.to(box.dtype)[:, None]
+    lim = torch.stack([wf, hf, wf, hf], dim=-1)
+    return torch.minimum(torch.clamp_min(box, 0), lim)
+
+
+def clip_batch(images_1d, img_h, img_w, boxes):
+    """Build the per-image list that ``clip.inference`` consumes (criterion.py:371-396):
+    image (3,H,W) view of the padded 1-D buffer and Instances(gt_boxes=Boxes(boxes))."""
+    B2, I2 = _structures()
+    hs = img_h.tolist()
+    ws = img_w.tolist()
+    out = []
+    for b in range(boxes.shape[0]):
+        H, W = int(hs[b]), int(ws[b])
+        img = images_1d[b, : H * W * 3].view(H, W, 3)
+        out.append({"image": img.permute(2, 0, 1).contiguous(),
+                    "instances": I2((H, W), gt_boxes=B2(boxes[b]))})
+    return out

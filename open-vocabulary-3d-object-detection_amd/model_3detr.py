@@ -1,0 +1,230 @@
+"""3DETR with open-vocabulary classification head (mirror of reference
+models/model_3detr.py), on the ov3d HIP kernels for sampling / grouping.
+
+API kept identical for main.py / engine.py:
+  * ``build_3detr(args, dataset_config) -> (Model3DETR, BoxProcessor)``
+    (model_3detr.py:421-438);
+  * ``Model3DETR.forward(inputs, encoder_only=False)`` returning
+    ``{"outputs": {13 keys}, "aux_outputs": [7 dicts]}`` (model_3detr.py:317-350);
+  * state-dict keys of the reference (pre_encoder.mlp_module.layer*, encoder.layers.*,
+    decoder.layers.*, mlp_heads.*, pos_embedding.gauss_B, ...).
+Reference quirks reproduced by default:
+  * Q6: ``sem_cls_head`` = Linear(640, T, bias=False) holding the frozen text
+    embedding; logits are raw dot products;
+  * Q8: the reference reshapes the (L*B, T, Q) transposed logits straight to
+    (L, B, Q, T) (model_3detr.py:238, 253), which scrambles the (query, class)
+    layout; ``cls_logits_layout="reference"`` keeps that, ``"fixed"`` undoes it.
+"""
+import math
+from functools import partial
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import pointnet2_utils as pu
+from .helpers import GenericMLP
+from .pc_util import scale_points, shift_scale_points
+from .pointnet2_modules import PointnetSAModuleVotes
+from .position_embedding import PositionEmbeddingCoordsSine
+from .transformer import (MaskedTransformerEncoder, TransformerDecoder, TransformerDecoderLayer,
+                          TransformerEncoder, TransformerEncoderLayer)
+
+
+class BoxProcessor:
+    """Head outputs -> boxes (reference model_3detr.py:19-69)."""
+
+    def __init__(self, dataset_config):
+        self.dataset_config = dataset_config
+
+    def compute_predicted_center(self, center_offset, query_xyz, point_cloud_dims):
+        center_unnormalized = query_xyz + center_offset
+        return shift_scale_points(center_unnormalized, src_range=point_cloud_dims), center_unnormalized
+
+    def compute_predicted_size(self, size_normalized, point_cloud_dims):
+        scene_scale = torch.clamp(point_cloud_dims[1] - point_cloud_dims[0], min=1e-1)
+        return scale_points(size_normalized, mult_factor=scene_scale)
+
+    def compute_predicted_angle(self, angle_logits, angle_residual):
+        if angle_logits.shape[-1] == 1:
+            # no-rotation datasets: keep the heads in the graph (DDP), angle = 0
+            return (angle_logits * 0 + angle_residual * 0).squeeze(-1).clamp(min=0)
+        per_cls = 2 * np.pi / self.dataset_config.num_angle_bin
+        cls = angle_logits.argmax(dim=-1).detach()
+        angle = per_cls * cls + angle_residual.gather(2, cls.unsqueeze(-1)).squeeze(-1)
+        return torch.where(angle > np.pi, angle - 2 * np.pi, angle)
+
+    def compute_objectness_and_cls_prob(self, cls_logits):
+        if cls_logits.shape[-1] != self.dataset_config.num_semcls + 1:
+            raise ValueError("class logits must have num_semcls + 1 entries")
+        prob = torch.softmax(cls_logits, dim=-1)
+        return prob[..., :-1], 1 - prob[..., -1]
+
+    def box_parametrization_to_corners(self, box_center_unnorm, box_size_unnorm, box_angle):
+        return self.dataset_config.box_parametrization_to_corners(box_center_unnorm, box_size_unnorm,
+                                                                  box_angle)
+
+
+class Model3DETR(nn.Module):
+    def __init__(self, pre_encoder, encoder, decoder, dataset_config, text_embedding, encoder_dim=256,
+                 decoder_dim=256, position_embedding="fourier", mlp_dropout=0.3, num_queries=256,
+                 cls_logits_layout="reference"):
+        super().__init__()
+        self.pre_encoder = pre_encoder
+        self.encoder = encoder
+        self.class_num = dataset_config.num_semcls + 1
+        hidden = [encoder_dim] if hasattr(encoder, "masking_radius") else [encoder_dim, encoder_dim]
+        self.encoder_to_decoder_projection = GenericMLP(
+            input_dim=encoder_dim, hidden_dims=hidden, output_dim=decoder_dim, norm_fn_name="bn1d",
+            activation="relu", use_conv=True, output_use_activation=True, output_use_norm=True,
+            output_use_bias=False)
+        self.pos_embedding = PositionEmbeddingCoordsSine(d_pos=decoder_dim, pos_type=position_embedding,
+                                                         normalize=True)
+        self.query_projection = GenericMLP(input_dim=decoder_dim, hidden_dims=[decoder_dim],
+                                           output_dim=decoder_dim, use_conv=True,
+                                           output_use_activation=True, hidden_use_bias=True)
+        self.decoder = decoder
+        self._build_heads(dataset_config, decoder_dim, mlp_dropout, text_embedding)
+        self.num_queries = num_queries
+        self.box_processor = BoxProcessor(dataset_config)
+        if cls_logits_layout not in ("reference", "fixed"):
+            raise ValueError(cls_logits_layout)
+        self.cls_logits_layout = cls_logits_layout
+
+    def _build_heads(self, cfg, dim, dropout, text_embedding):
+        mlp = partial(GenericMLP, norm_fn_name="bn1d", activation="relu", use_conv=True,
+                      hidden_dims=[dim, dim], dropout=dropout, input_dim=dim)
+        sem = nn.Linear(cfg.clip_embed_length, self.class_num, bias=False)
+        if tuple(sem.weight.shape) != tuple(text_embedding.shape):
+            raise ValueError(f"text embedding {tuple(text_embedding.shape)} != {tuple(sem.weight.shape)}")
+        sem.weight = nn.Parameter(text_embedding.float().clone(), requires_grad=False)
+        self.mlp_heads = nn.ModuleDict([
+            ("visual_embed_head", mlp(output_dim=cfg.clip_embed_length)),
+            ("sem_cls_head", sem),
+            ("center_head", mlp(output_dim=3)),
+            ("size_head", mlp(output_dim=3)),
+            ("angle_cls_head", mlp(output_dim=cfg.num_angle_bin)),
+            ("angle_residual_head", mlp(output_dim=cfg.num_angle_bin)),
+        ])
+
+    # ------------------------------------------------------------------ encoder
+    def get_query_embeddings(self, encoder_xyz, point_cloud_dims):
+        _, query_xyz = pu.furthest_point_sample_gather(encoder_xyz, self.num_queries)
+        query_embed = self.query_projection(self.pos_embedding(query_xyz, input_range=point_cloud_dims))
+        return query_xyz, query_embed
+
+    @staticmethod
+    def _break_up_pc(pc):
+        xyz = pc[..., 0:3].contiguous()
+        feats = pc[..., 3:].transpose(1, 2).contiguous() if pc.size(-1) > 3 else None
+        return xyz, feats
+
+    def run_encoder(self, point_clouds):
+        xyz, feats = self._break_up_pc(point_clouds)
+        pre_xyz, pre_feats, pre_inds = self.pre_encoder(xyz, feats)
+        enc_xyz, enc_feats, enc_inds = self.encoder(pre_feats.permute(2, 0, 1), xyz=pre_xyz)
+        if enc_inds is None:
+            enc_inds = pre_inds
+        else:
+            enc_inds = torch.gather(pre_inds.long(), 1, enc_inds.long())
+        return enc_xyz, enc_feats, enc_inds
+
+    # -------------------------------------------------------------------- heads
+    def get_box_predictions(self, query_xyz, point_cloud_dims, box_features):
+        L, Q, B, C = box_features.shape
+        feats = box_features.permute(0, 2, 3, 1).reshape(L * B, C, Q)
+        heads = self.mlp_heads
+        visual = heads["visual_embed_head"](feats).transpose(1, 2)          # (LB, Q, 640)
+        logits = heads["sem_cls_head"](visual)                              # (LB, Q, T)
+        if self.cls_logits_layout == "reference":
+            logits = logits.transpose(1, 2).reshape(L, B, Q, -1)            # Q8
+        else:
+            logits = logits.reshape(L, B, Q, -1)
+        center_offset = (heads["center_head"](feats).sigmoid().transpose(1, 2) - 0.5).reshape(L, B, Q, -1)
+        size_norm = heads["size_head"](feats).sigmoid().transpose(1, 2).reshape(L, B, Q, -1)
+        angle_logits = heads["angle_cls_head"](feats).transpose(1, 2).reshape(L, B, Q, -1)
+        angle_res_norm = heads["angle_residual_head"](feats).transpose(1, 2).reshape(L, B, Q, -1)
+        angle_res = angle_res_norm * (np.pi / angle_res_norm.shape[-1])
+        visual = visual.reshape(L, B, Q, -1)
+        bp = self.box_processor
+        outs = []
+        for l in range(L):
+            center_n, center_u = bp.compute_predicted_center(center_offset[l], query_xyz, point_cloud_dims)
+            angle = bp.compute_predicted_angle(angle_logits[l], angle_res[l])
+            size_u = bp.compute_predicted_size(size_norm[l], point_cloud_dims)
+            corners = bp.box_parametrization_to_corners(center_u, size_u, angle)
+            with torch.no_grad():
+                sem_prob, obj_prob = bp.compute_objectness_and_cls_prob(logits[l])
+            outs.append({
+                "visual_embeds": visual[l],
+                "sem_cls_logits": logits[l],
+                "center_normalized": center_n.contiguous(),
+                "center_unnormalized": center_u,
+                "size_normalized": size_norm[l],
+                "size_unnormalized": size_u,
+                "angle_logits": angle_logits[l],
+                "angle_residual": angle_res[l],
+                "angle_residual_normalized": angle_res_norm[l],
+                "angle_continuous": angle,
+                "objectness_prob": obj_prob,
+                "sem_cls_prob": sem_prob,
+                "box_corners": corners,
+            })
+        return {"outputs": outs[-1], "aux_outputs": outs[:-1]}
+
+    def forward(self, inputs, encoder_only=False):
+        pc = inputs["point_clouds"]
+        enc_xyz, enc_feats, _ = self.run_encoder(pc)
+        enc_feats = self.encoder_to_decoder_projection(enc_feats.permute(1, 2, 0)).permute(2, 0, 1)
+        if encoder_only:
+            return enc_xyz, enc_feats.transpose(0, 1)
+        dims = [inputs["point_cloud_dims_min"].float(), inputs["point_cloud_dims_max"].float()]
+        query_xyz, query_embed = self.get_query_embeddings(enc_xyz, dims)
+        enc_pos = self.pos_embedding(enc_xyz, input_range=dims).permute(2, 0, 1)
+        query_embed = query_embed.permute(2, 0, 1)
+        tgt = torch.zeros_like(query_embed)
+        box_features = self.decoder(tgt, enc_feats, query_pos=query_embed, pos=enc_pos)[0]
+        return self.get_box_predictions(query_xyz, dims, box_features)
+
+
+# ---------------------------------------------------------------- builders
+def build_preencoder(args):
+    return PointnetSAModuleVotes(radius=0.2, nsample=64, npoint=args.preenc_npoints,
+                                 mlp=[3 * int(args.use_color), 64, 128, args.enc_dim],
+                                 normalize_xyz=True)
+
+
+def build_encoder(args):
+    layer = TransformerEncoderLayer(d_model=args.enc_dim, nhead=args.enc_nhead,
+                                    dim_feedforward=args.enc_ffn_dim, dropout=args.enc_dropout,
+                                    activation=args.enc_activation)
+    if args.enc_type == "vanilla":
+        return TransformerEncoder(encoder_layer=layer, num_layers=args.enc_nlayers)
+    if args.enc_type == "masked":
+        interim = PointnetSAModuleVotes(radius=0.4, nsample=32, npoint=args.preenc_npoints // 2,
+                                        mlp=[args.enc_dim, 256, 256, args.enc_dim], normalize_xyz=True)
+        return MaskedTransformerEncoder(encoder_layer=layer, num_layers=3,
+                                        interim_downsampling=interim,
+                                        masking_radius=[math.pow(x, 2) for x in (0.4, 0.8, 1.2)])
+    raise ValueError(f"Unknown encoder type {args.enc_type}")
+
+
+def build_decoder(args):
+    layer = TransformerDecoderLayer(d_model=args.dec_dim, nhead=args.dec_nhead,
+                                    dim_feedforward=args.dec_ffn_dim, dropout=args.dec_dropout)
+    return TransformerDecoder(layer, num_layers=args.dec_nlayers, return_intermediate=True)
+
+
+def load_text_embed(args):
+    """reference model_3detr.py:417-419 (weights_only load: a plain tensor file)."""
+    return torch.load(args.clip_embed_path, map_location="cpu", weights_only=True).float()
+
+
+def build_3detr(args, dataset_config, text_embedding=None):
+    if text_embedding is None:
+        text_embedding = load_text_embed(args)
+    model = Model3DETR(build_preencoder(args), build_encoder(args), build_decoder(args), dataset_config,
+                       text_embedding, encoder_dim=args.enc_dim, decoder_dim=args.dec_dim,
+                       mlp_dropout=args.mlp_dropout, num_queries=args.nqueries,
+                       cls_logits_layout=getattr(args, "cls_logits_layout", "reference"))
+    return model, BoxProcessor(dataset_config)

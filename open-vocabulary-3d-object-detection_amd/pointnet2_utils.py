@@ -1,0 +1,158 @@
+"""Drop-in for ``third_party.pointnet2.pointnet2_utils`` (un-vendored upstream,
+imported at models/model_3detr.py:9 of the reference) on the HIP kernels of
+libov3d_hip.so.
+
+Same names, argument meaning and return types as the upstream module:
+``furthest_point_sample(xyz, npoint) -> int32 (B, npoint)``,
+``gather_operation``, ``ball_query``, ``grouping_operation``, ``QueryAndGroup``.
+Semantics: SURVEY.md Appendix A (FPS tie rule: DESIGN.md §FPS).
+"""
+import torch
+import torch.nn as nn
+from torch.autograd import Function
+
+from . import _native as nat
+
+
+def _f32(t, name, ndim):
+    return nat.check(t.contiguous() if t.dtype == torch.float32 else t.float().contiguous(), name,
+                     torch.float32, ndim)
+
+
+def _i32(t, name, ndim):
+    return nat.check(t.to(torch.int32).contiguous(), name, torch.int32, ndim)
+
+
+class FurthestPointSampling(Function):
+    @staticmethod
+    def forward(ctx, xyz, npoint):
+        xyz = _f32(xyz, "xyz", 3)
+        B, N, _ = xyz.shape
+        idx = torch.empty((B, npoint), dtype=torch.int32, device=xyz.device)
+        ws = torch.empty((B, N), dtype=torch.float32, device=xyz.device) if N > 20480 else None
+        nat.call("ov3d_fps", xyz, B, N, int(npoint), idx, None, ws, like=xyz)
+        ctx.mark_non_differentiable(idx)
+        return idx
+
+    @staticmethod
+    def backward(ctx, g):
+        return None, None
+
+
+furthest_point_sample = FurthestPointSampling.apply
+
+
+def furthest_point_sample_gather(xyz, npoint):
+    """FPS with the gather fused into the sampling kernel: returns
+    (idx int32 (B,npoint), new_xyz (B,npoint,3)).  Equals
+    (furthest_point_sample(xyz, n), gather_operation(xyz^T, idx)^T) bit for bit."""
+    with torch.no_grad():
+        xyz = _f32(xyz.detach(), "xyz", 3)
+        B, N, _ = xyz.shape
+        idx = torch.empty((B, npoint), dtype=torch.int32, device=xyz.device)
+        new_xyz = torch.empty((B, npoint, 3), dtype=torch.float32, device=xyz.device)
+        ws = torch.empty((B, N), dtype=torch.float32, device=xyz.device) if N > 20480 else None
+        nat.call("ov3d_fps", xyz, B, N, int(npoint), idx, new_xyz, ws, like=xyz)
+    return idx, new_xyz
+
+
+class GatherOperation(Function):
+    @staticmethod
+    def forward(ctx, features, idx):
+        features = _f32(features, "features", 3)
+        idx = _i32(idx, "idx", 2)
+        B, C, N = features.shape
+        M = idx.shape[1]
+        out = torch.empty((B, C, M), dtype=torch.float32, device=features.device)
+        nat.call("ov3d_gather_fwd", features, idx, B, C, N, M, out, like=features)
+        ctx.save_for_backward(idx)
+        ctx.N = N
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        g = _f32(g, "grad", 3)
+        B, C, M = g.shape
+        gf = torch.empty((B, C, ctx.N), dtype=torch.float32, device=g.device)
+        nat.call("ov3d_gather_bwd", g, idx, B, C, ctx.N, M, gf, like=g)
+        return gf, None
+
+
+gather_operation = GatherOperation.apply
+
+
+def ball_query(radius, nsample, xyz, new_xyz):
+    """-> int32 (B, npoint, nsample): first nsample in-radius indices, ascending."""
+    xyz = _f32(xyz.detach(), "xyz", 3)
+    new_xyz = _f32(new_xyz.detach(), "new_xyz", 3)
+    B, N, _ = xyz.shape
+    M = new_xyz.shape[1]
+    idx = torch.empty((B, M, nsample), dtype=torch.int32, device=xyz.device)
+    nat.call("ov3d_ball_query", xyz, new_xyz, B, N, M, float(radius), int(nsample), idx, like=xyz)
+    return idx
+
+
+class _Group(Function):
+    """Fused QueryAndGroup body: (xyz[idx]-new_xyz)[/r] ++ features[idx]."""
+
+    @staticmethod
+    def forward(ctx, xyz, new_xyz, features, idx, radius, normalize):
+        B, N, _ = xyz.shape
+        _, M, S = idx.shape
+        C = 0 if features is None else features.shape[1]
+        out = torch.empty((B, 3 + C, M, S), dtype=torch.float32, device=xyz.device)
+        nat.call("ov3d_group_fwd", xyz, new_xyz, features, idx, B, C, N, M, S, float(radius),
+                 int(bool(normalize)), out, like=xyz)
+        ctx.save_for_backward(idx)
+        ctx.shape = (B, C, N, M, S)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        B, C, N, M, S = ctx.shape
+        if C == 0 or not ctx.needs_input_grad[2]:
+            return None, None, None, None, None, None
+        g = _f32(g, "grad", 4)
+        gf = torch.empty((B, C, N), dtype=torch.float32, device=g.device)
+        nat.call("ov3d_group_bwd", g, idx, B, C, N, M, S, gf, like=g)
+        return None, None, gf, None, None, None
+
+
+def grouping_operation(features, idx):
+    """(B,C,N), (B,M,S) -> (B,C,M,S) (differentiable w.r.t. features)."""
+    features = _f32(features, "features", 3)
+    idx = _i32(idx, "idx", 3)
+    B, C, N = features.shape
+    # the fused kernel needs an xyz/new_xyz pair; a zero pair makes channels 0:3 zero
+    z = torch.zeros((B, N, 3), dtype=torch.float32, device=features.device)
+    zc = torch.zeros((B, idx.shape[1], 3), dtype=torch.float32, device=features.device)
+    return _Group.apply(z, zc, features, idx, 1.0, False)[:, 3:]
+
+
+class QueryAndGroup(nn.Module):
+    """pointnet2_utils.QueryAndGroup with use_xyz=True (the only mode the
+    reference builds: models/model_3detr.py:355-361, 385-391)."""
+
+    def __init__(self, radius, nsample, use_xyz=True, ret_grouped_xyz=False, normalize_xyz=False,
+                 sample_uniformly=False, ret_unique_cnt=False):
+        super().__init__()
+        if not use_xyz or sample_uniformly or ret_unique_cnt:
+            raise NotImplementedError("only use_xyz=True grouping is on the reference path")
+        self.radius, self.nsample = radius, nsample
+        self.use_xyz, self.ret_grouped_xyz, self.normalize_xyz = use_xyz, ret_grouped_xyz, normalize_xyz
+
+    def forward(self, xyz, new_xyz, features=None):
+        if xyz.requires_grad or new_xyz.requires_grad:
+            raise NotImplementedError("gradients w.r.t. point coordinates are not on the path")
+        idx = ball_query(self.radius, self.nsample, xyz, new_xyz)
+        xyz = _f32(xyz, "xyz", 3)
+        new_xyz = _f32(new_xyz, "new_xyz", 3)
+        if features is not None:
+            features = features if features.dtype == torch.float32 else features.float()
+            features = nat.check(features.contiguous(), "features", torch.float32, 3)
+        out = _Group.apply(xyz, new_xyz, features, idx, self.radius, self.normalize_xyz)
+        if self.ret_grouped_xyz:
+            return out, out[:, :3]
+        return out

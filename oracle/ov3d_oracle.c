@@ -1,0 +1,418 @@
+/*
+ * ov3d_oracle.c — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference hot-path kernels, used as the parity
+ * checker for the HIP library (libov3d_hip.so) and as the "port" CPU
+ * baseline in bench.py.  Nothing in the product package links or calls this
+ * file; only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+ * load it.
+ *
+ * Floating-point contract: compiled with -O2 -ffp-contract=off; every
+ * fused multiply-add that the HIP kernels use is written here as an explicit
+ * fmaf(), so the two implementations round identically (bit-exact indices,
+ * bit-exact GIoU/NMS arithmetic).
+ *
+ * Sources restated (file:line under the reference tree):
+ *   FPS / ball query / grouping : un-vendored third_party/pointnet2 (imported at
+ *       models/model_3detr.py:8-9); semantics from SURVEY.md Appendix A.1-A.3.
+ *       PARITY UNPINNED by the reference (no sources, no fixtures): the tie
+ *       rule below emulates the upstream 512-thread tree reduction exactly.
+ *   GIoU  : utils/box_util.py:624-714 (Cython dispatch) + utils/box_intersection.pyx:
+ *       13-70 (polygon_clip_unnest, double precision Python floats), 166-198
+ *       (box_intersection, K2 = rect2.shape[2] bug), and utils/box_util.py:517-618
+ *       (TorchScript path, float32, all K2).
+ *   NMS   : utils/nms.py:79-162 (nms_3d_faster / nms_3d_faster_samecls).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ FPS */
+
+/* Largest power of two <= n, capped at 512 — upstream opt_n_threads(). */
+static int fps_block_size(int n) {
+    int bs = 1;
+    while (bs * 2 <= n && bs < 512) bs *= 2;
+    return bs;
+}
+
+static uint32_t bitrev(uint32_t v, int bits) {
+    uint32_t r = 0;
+    for (int i = 0; i < bits; ++i) r |= ((v >> i) & 1u) << (bits - 1 - i);
+    return r;
+}
+
+/* Tie-break rank of point k: the upstream kernel gives point k to thread
+ * t = k mod bs (strict '>' inside a thread keeps the lowest k), then reduces
+ * over threads with a halving tree that keeps the lower slot on ties.  The
+ * winner among equal maxima is the thread with the smallest bit-reversed id,
+ * then the smallest k.  rank(k) orders exactly that way; smaller wins. */
+uint32_t ov3d_fps_rank_cpu(int k, int n) {
+    int bs = fps_block_size(n);
+    int bits = 0;
+    while ((1 << bits) < bs) ++bits;
+    uint32_t t = (uint32_t)(k & (bs - 1));
+    uint32_t i = (uint32_t)(k >> bits);
+    return (bitrev(t, bits) << 23) | i;
+}
+
+int ov3d_fps_cpu(const float* xyz, int B, int N, int M, int32_t* idx_out) {
+    if (B < 0 || N <= 0 || M < 0) return -1;
+    float* temp = (float*)malloc(sizeof(float) * (size_t)N);
+    uint32_t* rank = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)N);
+    unsigned char* skip = (unsigned char*)malloc((size_t)N);
+    if (!temp || !rank || !skip) { free(temp); free(rank); free(skip); return -2; }
+    for (int k = 0; k < N; ++k) rank[k] = ov3d_fps_rank_cpu(k, N);
+    for (int b = 0; b < B; ++b) {
+        const float* p = xyz + (size_t)b * N * 3;
+        int32_t* idx = idx_out + (size_t)b * M;
+        for (int k = 0; k < N; ++k) {
+            temp[k] = 1e10f;
+            float x = p[3 * k], y = p[3 * k + 1], z = p[3 * k + 2];
+            float mag = fmaf(z, z, fmaf(y, y, x * x));
+            skip[k] = ((double)mag <= 1e-3);   /* float vs double literal */
+        }
+        if (M == 0) continue;
+        int old = 0;
+        idx[0] = 0;
+        for (int j = 1; j < M; ++j) {
+            float x1 = p[3 * old], y1 = p[3 * old + 1], z1 = p[3 * old + 2];
+            uint64_t best = 0; /* key 0 == "no candidate" -> index 0 */
+            int besti = 0;
+            for (int k = 0; k < N; ++k) {
+                if (skip[k]) continue;
+                float dx = p[3 * k] - x1, dy = p[3 * k + 1] - y1, dz = p[3 * k + 2] - z1;
+                float d = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                float d2 = fminf(d, temp[k]);
+                temp[k] = d2;
+                uint32_t bits;
+                memcpy(&bits, &d2, 4);
+                uint64_t key = ((uint64_t)bits << 32) | (uint64_t)(~rank[k]);
+                if (key > best) { best = key; besti = k; }
+            }
+            old = besti;
+            idx[j] = old;
+        }
+    }
+    free(temp); free(rank); free(skip);
+    return 0;
+}
+
+/* ------------------------------------------------------------ ball query */
+
+int ov3d_ball_query_cpu(const float* xyz, const float* new_xyz, int B, int N, int M,
+                        float radius, int S, int32_t* idx_out) {
+    if (B < 0 || N < 0 || M < 0 || S <= 0) return -1;
+    const float r2 = radius * radius;
+    for (int b = 0; b < B; ++b) {
+        const float* p = xyz + (size_t)b * N * 3;
+        for (int j = 0; j < M; ++j) {
+            const float* c = new_xyz + ((size_t)b * M + j) * 3;
+            int32_t* idx = idx_out + ((size_t)b * M + j) * S;
+            for (int l = 0; l < S; ++l) idx[l] = 0;
+            int cnt = 0;
+            for (int k = 0; k < N && cnt < S; ++k) {
+                float dx = c[0] - p[3 * k], dy = c[1] - p[3 * k + 1], dz = c[2] - p[3 * k + 2];
+                float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                if (d2 < r2) {
+                    if (cnt == 0)
+                        for (int l = 0; l < S; ++l) idx[l] = k;
+                    idx[cnt++] = k;
+                }
+            }
+        }
+    }
+    return 0;
+}
+
+/* features (B,C,N), idx (B,M,S) -> out (B,C,M,S) */
+int ov3d_group_cpu(const float* feats, const int32_t* idx, int B, int C, int N, int M, int S,
+                   float* out) {
+    for (int b = 0; b < B; ++b)
+        for (int c = 0; c < C; ++c)
+            for (int j = 0; j < M; ++j)
+                for (int s = 0; s < S; ++s) {
+                    int k = idx[((size_t)b * M + j) * S + s];
+                    out[(((size_t)b * C + c) * M + j) * S + s] =
+                        (k >= 0 && k < N) ? feats[((size_t)b * C + c) * N + k] : 0.f;
+                }
+    return 0;
+}
+
+/* ------------------------------------------------------------------ GIoU */
+
+typedef struct { double x, y; } pt_d;
+typedef struct { float x, y; } pt_f;
+
+/* Sutherland–Hodgman in double, as the Cython polygon_clip_unnest evaluates it
+ * (untyped Python floats: box_intersection.pyx:13-23, 27-70). */
+static int clip_double(const pt_d* subj, int ns, const pt_d* clip, int nc, pt_d* out) {
+    pt_d in[16], cur[16];
+    int nout = ns;
+    for (int i = 0; i < ns; ++i) cur[i] = subj[i];
+    pt_d cp1 = clip[nc - 1];
+    for (int ci = 0; ci < nc; ++ci) {
+        pt_d cp2 = clip[ci];
+        int nin = nout;
+        for (int i = 0; i < nin; ++i) in[i] = cur[i];
+        nout = 0;
+        if (nin == 0) break;
+        pt_d s = in[nin - 1];
+        for (int ii = 0; ii < nin; ++ii) {
+            pt_d e = in[ii];
+            int e_in = (cp2.x - cp1.x) * (e.y - cp1.y) > (cp2.y - cp1.y) * (e.x - cp1.x);
+            int s_in = (cp2.x - cp1.x) * (s.y - cp1.y) > (cp2.y - cp1.y) * (s.x - cp1.x);
+            if (e_in || s_in) {
+                if (e_in != s_in) {
+                    double dc0 = cp1.x - cp2.x, dc1 = cp1.y - cp2.y;
+                    double dp0 = s.x - e.x, dp1 = s.y - e.y;
+                    double n1 = cp1.x * cp2.y - cp1.y * cp2.x;
+                    double n2 = s.x * e.y - s.y * e.x;
+                    double n3 = 1.0 / (dc0 * dp1 - dc1 * dp0);
+                    pt_d q = {(n1 * dp0 - n2 * dc0) * n3, (n1 * dp1 - n2 * dc1) * n3};
+                    if (nout < 16) cur[nout++] = q;
+                }
+                if (e_in && nout < 16) cur[nout++] = e;
+            }
+            s = e;
+        }
+        cp1 = cp2;
+        if (nout == 0) break;
+    }
+    for (int i = 0; i < nout; ++i) out[i] = cur[i];
+    return nout;
+}
+
+/* Same algorithm on float32 scalars: the TorchScript path (box_util.py:387-440)
+ * evaluates every step as a float32 0-d tensor op. */
+static int clip_float(const pt_f* subj, int ns, const pt_f* clip, int nc, pt_f* out) {
+    pt_f in[16], cur[16];
+    int nout = ns;
+    for (int i = 0; i < ns; ++i) cur[i] = subj[i];
+    pt_f cp1 = clip[nc - 1];
+    for (int ci = 0; ci < nc; ++ci) {
+        pt_f cp2 = clip[ci];
+        int nin = nout;
+        for (int i = 0; i < nin; ++i) in[i] = cur[i];
+        nout = 0;
+        if (nin == 0) break;
+        pt_f s = in[nin - 1];
+        for (int ii = 0; ii < nin; ++ii) {
+            pt_f e = in[ii];
+            int e_in = (cp2.x - cp1.x) * (e.y - cp1.y) > (cp2.y - cp1.y) * (e.x - cp1.x);
+            int s_in = (cp2.x - cp1.x) * (s.y - cp1.y) > (cp2.y - cp1.y) * (s.x - cp1.x);
+            if (e_in || s_in) {
+                if (e_in != s_in) {
+                    float dc0 = cp1.x - cp2.x, dc1 = cp1.y - cp2.y;
+                    float dp0 = s.x - e.x, dp1 = s.y - e.y;
+                    float n1 = cp1.x * cp2.y - cp1.y * cp2.x;
+                    float n2 = s.x * e.y - s.y * e.x;
+                    float n3 = 1.0f / (dc0 * dp1 - dc1 * dp0);
+                    pt_f q = {(n1 * dp0 - n2 * dc0) * n3, (n1 * dp1 - n2 * dc1) * n3};
+                    if (nout < 16) cur[nout++] = q;
+                }
+                if (e_in && nout < 16) cur[nout++] = e;
+            }
+            s = e;
+        }
+        cp1 = cp2;
+        if (nout == 0) break;
+    }
+    for (int i = 0; i < nout; ++i) out[i] = cur[i];
+    return nout;
+}
+
+/* 0.5*|dot(xs, roll(ys,1)) - dot(ys, roll(xs,1))| with float accumulation */
+static float shoelace_f(const float* xs, const float* ys, int n) {
+    float s1 = 0.f, s2 = 0.f;
+    for (int i = 0; i < n; ++i) {
+        int im = (i + n - 1) % n;
+        s1 = s1 + xs[i] * ys[im];
+        s2 = s2 + ys[i] * xs[im];
+    }
+    return 0.5f * fabsf(s1 - s2);
+}
+
+/* rect[i] = (corner[3-i].x, corner[3-i].z): box_util.py:656-661 */
+static void rect_of(const float* c, float* rx, float* rz) {
+    for (int i = 0; i < 4; ++i) { rx[i] = c[(3 - i) * 3 + 0]; rz[i] = c[(3 - i) * 3 + 2]; }
+}
+
+static float box_vol(const float* c) { /* box3d_vol_tensor, box_util.py:443-463 */
+    const float EPS = 1e-6f;
+    float d[3];
+    float a, b, cc;
+    for (int i = 0; i < 3; ++i) d[i] = c[0 * 3 + i] - c[1 * 3 + i];
+    a = sqrtf(fmaxf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2], EPS));
+    for (int i = 0; i < 3; ++i) d[i] = c[1 * 3 + i] - c[2 * 3 + i];
+    b = sqrtf(fmaxf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2], EPS));
+    for (int i = 0; i < 3; ++i) d[i] = c[0 * 3 + i] - c[4 * 3 + i];
+    cc = sqrtf(fmaxf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2], EPS));
+    return a * b * cc;
+}
+
+/* mode 0: Cython path (double clip, K2 < min(4,nums) bug when cython_k2_bug);
+ * mode 1: TorchScript path (float clip, all k2 < nums). */
+int ov3d_giou3d_cpu(const float* corners1, const float* corners2, const int32_t* nums,
+                    int B, int K1, int K2, int mode, int rotated, int cython_k2_bug,
+                    float* out) {
+    const float EPS = 1e-8f;
+    for (int b = 0; b < B; ++b) {
+        int nk = nums ? nums[b] : K2;
+        for (int k1 = 0; k1 < K1; ++k1) {
+            const float* c1 = corners1 + (((size_t)b * K1 + k1) * 8) * 3;
+            float r1x[4], r1z[4];
+            rect_of(c1, r1x, r1z);
+            float v1 = fmaxf(box_vol(c1), EPS);
+            float mn1[3], mx1[3];
+            for (int a = 0; a < 3; ++a) { mn1[a] = INFINITY; mx1[a] = -INFINITY; }
+            for (int v = 0; v < 8; ++v)
+                for (int a = 0; a < 3; ++a) {
+                    float val = c1[v * 3 + a];
+                    if (a == 1) val = -val;
+                    if (val < mn1[a]) mn1[a] = val;
+                    if (val > mx1[a]) mx1[a] = val;
+                }
+            for (int k2 = 0; k2 < K2; ++k2) {
+                const float* c2 = corners2 + (((size_t)b * K2 + k2) * 8) * 3;
+                float* o = out + ((size_t)b * K1 + k1) * K2 + k2;
+                /* height on -Y */
+                float ymax = fminf(c1[0 * 3 + 1], c2[0 * 3 + 1]);
+                float ymin = fmaxf(c1[4 * 3 + 1], c2[4 * 3 + 1]);
+                float height = fmaxf(ymax - ymin, 0.f);
+                float r2x[4], r2z[4];
+                rect_of(c2, r2x, r2z);
+                float ltx = fmaxf(r1x[1], r2x[1]), ltz = fmaxf(r1z[1], r2z[1]);
+                float rbx = fminf(r1x[3], r2x[3]), rbz = fminf(r1z[3], r2z[3]);
+                float whx = fmaxf(rbx - ltx, 0.f), whz = fmaxf(rbz - ltz, 0.f);
+                float non_rot = whx * whz;
+                if (k2 >= nk) non_rot = 0.f;
+                /* enclosing box (Y flipped), box_util.py:466-514 */
+                float mn2[3], mx2[3];
+                for (int a = 0; a < 3; ++a) { mn2[a] = INFINITY; mx2[a] = -INFINITY; }
+                for (int v = 0; v < 8; ++v)
+                    for (int a = 0; a < 3; ++a) {
+                        float val = c2[v * 3 + a];
+                        if (a == 1) val = -val;
+                        if (val < mn2[a]) mn2[a] = val;
+                        if (val > mx2[a]) mx2[a] = val;
+                    }
+                float al_xmin = fminf(mn1[0], mn2[0]);
+                float al_ymin = fmaxf(mx1[1], mx2[1]);
+                float al_zmin = fminf(mn1[2], mn2[2]);
+                float al_xmax = fmaxf(mx1[0], mx2[0]);
+                float al_ymax = fminf(mn1[1], mn2[1]);
+                float al_zmax = fmaxf(mx1[2], mx2[2]);
+                float enc = fabsf(al_xmax - al_xmin) * fabsf(al_ymax - al_ymin) * fabsf(al_zmax - al_zmin);
+                float v2 = fmaxf(box_vol(c2), EPS);
+                float sum_vols = v1 + v2;
+                float good = (enc > 2e-8f && sum_vols > 4e-8f) ? 1.f : 0.f;
+
+                float inter_area;
+                if (rotated) {
+                    inter_area = 0.f;
+                    int limit = nk;
+                    if (mode == 0 && cython_k2_bug && limit > 4) limit = 4; /* K2 = rect2.shape[2] */
+                    if (k2 < limit && non_rot != 0.f) {
+                        if (mode == 0) {
+                            pt_d s[4], c[4], res[16];
+                            for (int i = 0; i < 4; ++i) {
+                                s[i].x = r1x[i]; s[i].y = r1z[i];
+                                c[i].x = r2x[i]; c[i].y = r2z[i];
+                            }
+                            int n = clip_double(s, 4, c, 4, res);
+                            if (n > 0) {
+                                float xs[16], ys[16];
+                                for (int i = 0; i < n; ++i) { xs[i] = (float)res[i].x; ys[i] = (float)res[i].y; }
+                                inter_area = shoelace_f(xs, ys, n);
+                            }
+                        } else {
+                            pt_f s[4], c[4], res[16];
+                            for (int i = 0; i < 4; ++i) {
+                                s[i].x = r1x[i]; s[i].y = r1z[i];
+                                c[i].x = r2x[i]; c[i].y = r2z[i];
+                            }
+                            int n = clip_float(s, 4, c, 4, res);
+                            if (n > 0) {
+                                float xs[16], ys[16];
+                                for (int i = 0; i < n; ++i) { xs[i] = res[i].x; ys[i] = res[i].y; }
+                                inter_area = shoelace_f(xs, ys, n);
+                            }
+                        }
+                    }
+                } else {
+                    inter_area = non_rot;
+                }
+                float inter_vol = inter_area * height;
+                float uni = fmaxf(sum_vols - inter_vol, EPS);
+                float iou = inter_vol / uni;
+                float second = -(1.f - uni / enc);
+                float g = (iou + second) * good;
+                if (k2 >= nk) g = g * 0.f;
+                *o = g;
+            }
+        }
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------- NMS */
+
+static double np_max(double a, double b) { return (isnan(a) || isnan(b)) ? NAN : (a > b ? a : b); }
+static double np_min(double a, double b) { return (isnan(a) || isnan(b)) ? NAN : (a < b ? a : b); }
+
+static const double* g_scores;
+static int g_stride;
+static int cmp_desc(const void* pa, const void* pb) {
+    int a = *(const int*)pa, b = *(const int*)pb;
+    double sa = g_scores[(size_t)a * g_stride + 6], sb = g_scores[(size_t)b * g_stride + 6];
+    if (sa > sb) return -1;
+    if (sa < sb) return 1;
+    return (a > b) ? -1 : (a < b ? 1 : 0); /* ties: larger index first (stable argsort) */
+}
+
+/* boxes (K, stride) float64 [x1,y1,z1,x2,y2,z2,score(,cls)]; returns #picks,
+ * pick_out[0..n) in pick order, keep_out[K] (0/1) if non-null. */
+int ov3d_nms3d_cpu(const double* boxes, int K, int stride, double thr, int old_type, int samecls,
+                   int32_t* pick_out, uint8_t* keep_out) {
+    if (K < 0 || stride < 7 || (samecls && stride < 8)) return -1;
+    int* order = (int*)malloc(sizeof(int) * (size_t)(K > 0 ? K : 1));
+    unsigned char* sup = (unsigned char*)calloc((size_t)(K > 0 ? K : 1), 1);
+    double* area = (double*)malloc(sizeof(double) * (size_t)(K > 0 ? K : 1));
+    for (int i = 0; i < K; ++i) {
+        const double* p = boxes + (size_t)i * stride;
+        order[i] = i;
+        area[i] = (p[3] - p[0]) * (p[4] - p[1]) * (p[5] - p[2]);
+    }
+    g_scores = boxes; g_stride = stride;
+    qsort(order, (size_t)K, sizeof(int), cmp_desc);
+    int n = 0;
+    if (keep_out) memset(keep_out, 0, (size_t)K);
+    for (int pi = 0; pi < K; ++pi) {
+        int i = order[pi];
+        if (sup[i]) continue;
+        pick_out[n++] = i;
+        if (keep_out) keep_out[i] = 1;
+        const double* a = boxes + (size_t)i * stride;
+        for (int qi = pi + 1; qi < K; ++qi) {
+            int j = order[qi];
+            if (sup[j]) continue;
+            const double* c = boxes + (size_t)j * stride;
+            double xx1 = np_max(a[0], c[0]), yy1 = np_max(a[1], c[1]), zz1 = np_max(a[2], c[2]);
+            double xx2 = np_min(a[3], c[3]), yy2 = np_min(a[4], c[4]), zz2 = np_min(a[5], c[5]);
+            double l = np_max(0.0, xx2 - xx1), w = np_max(0.0, yy2 - yy1), h = np_max(0.0, zz2 - zz1);
+            double o;
+            if (old_type) {
+                o = (l * w * h) / area[j];
+            } else {
+                double inter = l * w * h;
+                o = inter / (area[i] + area[j] - inter);
+            }
+            if (samecls) o = o * (double)(a[7] == c[7]);
+            if (o > thr) sup[j] = 1;
+        }
+    }
+    free(order); free(sup); free(area);
+    return n;
+}

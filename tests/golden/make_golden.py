@@ -1,0 +1,234 @@
+"""Generate the golden parity fixtures from the REFERENCE code (run here, where
+/root/reference exists; the outputs are committed and travel to the GPU box).
+
+    python tests/golden/make_golden.py
+
+Fixtures (tests/golden/*.npz):
+  giou.npz        reference generalized_box3d_iou: Cython path (box_util.py:624-714,
+                  compiled box_intersection.pyx) and TorchScript path (517-618),
+                  rotated / axis-aligned, nums in {1,4,5,40,64}; plus d(sum(G*giou))/dcorners1
+                  of the TorchScript axis-aligned path (autograd).
+  nms.npz         reference nms_3d_faster_samecls / nms_3d_faster (utils/nms.py) picks on
+                  tie-free scores, K in {8, 128, 256}, old_type both.
+  geometry.npz    reference box_parametrization_to_corners (sunrgbd.py:145-148) and
+                  project_box_3d_cuda + clamp (image_util.py:117-134, criterion.py:383-391).
+  model_sun.npz   reference Model3DETR (vanilla encoder, SUN config, reduced widths) +
+                  SetCriterion with a fixed fake RegionCLIP: state dict, inputs, outputs of all
+                  decoder layers, the 56-entry loss dict, parameter gradients.  The un-vendored
+                  pointnet2 is the oracle restatement (oracle/pointnet2_ref.py).
+  model_scannet.npz  same for the masked encoder + colour + ScanNet config + differentiable GIoU.
+"""
+import argparse
+import os
+import sys
+import tempfile
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, ROOT)
+
+from ref_loader import load_reference  # noqa: E402
+from fake_clip import FakeRegionCLIP  # noqa: E402
+import ov3d_import  # noqa: E402
+
+ov3d = ov3d_import.load()
+from ov3d_amd import synthetic  # noqa: E402
+
+
+def rand_boxes(rs, cfg, B, K, rotated=True):
+    c = torch.tensor(rs.uniform([-2, 1, -0.5], [2, 5, 1.5], (B, K, 3)), dtype=torch.float32)
+    s = torch.tensor(rs.uniform(0.3, 2.0, (B, K, 3)), dtype=torch.float32)
+    a = torch.tensor(rs.uniform(-np.pi, np.pi, (B, K)) if rotated else np.zeros((B, K)),
+                     dtype=torch.float32)
+    return c, s, a, cfg.box_parametrization_to_corners(c, s, a)
+
+
+def gen_giou(R):
+    bu = R["box_util"]
+    cfg = R["sunrgbd"].SunrgbdDatasetConfig()
+    rs = np.random.RandomState(1234)
+    B, K1, K2 = 5, 32, 64
+    out = {}
+    for tag, rot in (("rot", True), ("aligned", False)):
+        _, _, _, c1 = rand_boxes(rs, cfg, B, K1, rot)
+        _, _, _, c2 = rand_boxes(rs, cfg, B, K2, rot)
+        c2[:, :12] = c1[:, :12] + torch.tensor(rs.uniform(-0.2, 0.2, (B, 12, 1, 3)), dtype=torch.float32)
+        nums = torch.tensor([1, 4, 5, 40, 64])
+        out[f"{tag}_c1"] = c1.numpy()
+        out[f"{tag}_c2"] = c2.numpy()
+        out[f"{tag}_nums"] = nums.numpy().astype(np.int32)
+        for rflag in (True, False):
+            key = f"{tag}_{'r' if rflag else 'a'}"
+            out[key + "_cython"] = bu.generalized_box3d_iou(c1, c2, nums, rotated_boxes=rflag,
+                                                            needs_grad=False).numpy()
+            out[key + "_tensor"] = bu.generalized_box3d_iou_tensor_jit(c1, c2, nums, rflag, False).numpy()
+    # autograd of the differentiable axis-aligned path
+    _, _, _, c1 = rand_boxes(rs, cfg, 3, 16, False)
+    _, _, _, c2 = rand_boxes(rs, cfg, 3, 8, False)
+    c2[:, :6] = c1[:, :6] + torch.tensor(rs.uniform(-0.3, 0.3, (3, 6, 1, 3)), dtype=torch.float32)
+    nums = torch.tensor([8, 3, 6])
+    G = torch.tensor(rs.randn(3, 16, 8), dtype=torch.float32)
+    c1g = c1.clone().requires_grad_(True)
+    g = bu.generalized_box3d_iou(c1g, c2, nums, rotated_boxes=False, needs_grad=True)
+    (g * G).sum().backward()
+    out.update(grad_c1=c1.numpy(), grad_c2=c2.numpy(), grad_nums=nums.numpy().astype(np.int32),
+               grad_G=G.numpy(), grad_giou=g.detach().numpy(), grad_dc1=c1g.grad.numpy())
+    np.savez_compressed(os.path.join(HERE, "giou.npz"), **out)
+
+
+def gen_nms(R):
+    nms = R["nms"]
+    rs = np.random.RandomState(77)
+    out = {}
+    for i, K in enumerate((8, 128, 256)):
+        lo = rs.uniform(-3, 3, (K, 3))
+        sz = rs.uniform(0.2, 1.5, (K, 3))
+        boxes = np.zeros((K, 8))
+        boxes[:, 0:3] = lo
+        boxes[:, 3:6] = lo + sz
+        boxes[:, 6] = rs.permutation(K) / K + rs.uniform(0, 1e-4, K)  # tie-free
+        boxes[:, 7] = rs.randint(0, 4, K)
+        out[f"boxes{i}"] = boxes
+        for old in (False, True):
+            out[f"samecls{i}_{int(old)}"] = np.array(nms.nms_3d_faster_samecls(boxes, 0.25, old), np.int32)
+            out[f"any{i}_{int(old)}"] = np.array(nms.nms_3d_faster(boxes[:, :7], 0.25, old), np.int32)
+    np.savez_compressed(os.path.join(HERE, "nms.npz"), **out)
+
+
+def gen_geometry(R):
+    cfg = R["sunrgbd"].SunrgbdDatasetConfig()
+    iu = R["image_util"]
+    rs = np.random.RandomState(5)
+    c, s, a, corners = rand_boxes(rs, cfg, 2, 16, True)
+    Rtilt = torch.tensor(np.array([[0.99, 0.05, 0.1], [-0.05, 0.99, 0.0], [-0.1, 0.0, 0.99]]),
+                         dtype=torch.float32)
+    K = torch.tensor([[529.5, 0, 365.0], [0, 529.5, 265.0], [0, 0, 1]], dtype=torch.float32)
+    c_img = c.clone()
+    c_img[..., 1] += 2.0  # in front of the camera
+    boxes2d = []
+    for b in range(2):
+        calib = iu.SUNRGBD_Calibration_cuda(Rtilt, K)
+        bx = iu.project_box_3d_cuda(calib, c_img[b], s[b], a[b])
+        mx = torch.broadcast_to(torch.tensor([[730, 530, 730, 530]]), bx.size())
+        boxes2d.append(torch.minimum(torch.clamp_min(bx, 0), mx))
+    np.savez_compressed(os.path.join(HERE, "geometry.npz"), center=c.numpy(), size=s.numpy(),
+                        angle=a.numpy(), corners=corners.numpy(), center_img=c_img.numpy(),
+                        Rtilt=Rtilt.numpy(), K=K.numpy(), boxes2d=torch.stack(boxes2d).numpy())
+
+
+MODEL_KEYS = ("box_corners", "sem_cls_logits", "visual_embeds", "center_normalized", "size_normalized",
+              "angle_logits", "angle_residual_normalized", "objectness_prob", "sem_cls_prob",
+              "angle_continuous", "center_unnormalized", "size_unnormalized")
+GRAD_PARAMS = ("pre_encoder.mlp_module.layer0.conv.weight", "pre_encoder.mlp_module.layer2.bn.bn.weight",
+               "encoder.layers.0.self_attn.in_proj_weight", "encoder.layers.2.linear2.weight",
+               "encoder_to_decoder_projection.layers.0.weight", "query_projection.layers.0.weight",
+               "decoder.layers.0.multihead_attn.in_proj_weight", "decoder.layers.7.linear1.weight",
+               "decoder.norm.weight", "mlp_heads.visual_embed_head.layers.0.weight",
+               "mlp_heads.center_head.layers.8.weight", "mlp_heads.angle_cls_head.layers.8.bias",
+               "mlp_heads.size_head.layers.4.weight")
+
+
+def model_args(**kw):
+    a = dict(model_name="3detr", enc_type="vanilla", enc_nlayers=3, enc_dim=64, enc_ffn_dim=64,
+             enc_dropout=0.0, enc_nhead=4, enc_activation="relu", dec_nlayers=8, dec_dim=64,
+             dec_ffn_dim=64, dec_dropout=0.0, dec_nhead=4, mlp_dropout=0.0, preenc_npoints=256,
+             nqueries=32, use_color=False, matcher_giou_cost=3.0, matcher_cls_cost=1.0,
+             matcher_center_cost=5.0, matcher_objectness_cost=5.0, loss_giou_weight=0.0,
+             loss_sem_cls_weight=1.0, loss_no_object_weight=0.1, loss_angle_cls_weight=0.1,
+             loss_angle_reg_weight=0.5, loss_center_weight=5.0, loss_size_weight=1.0,
+             loss_2dalignment_weight=2e-4)
+    a.update(kw)
+    return argparse.Namespace(**a)
+
+
+def small_images(batch, B, H=24, W=32):
+    rs = np.random.RandomState(3)
+    batch["image"] = torch.tensor(rs.uniform(0, 255, (B, H * W * 3)), dtype=torch.float32)
+    batch["image_height"] = torch.full((B,), H, dtype=torch.int64)
+    batch["image_width"] = torch.full((B,), W, dtype=torch.int64)
+    batch["calib_Rtilt"] = torch.eye(3).repeat(B, 1, 1)
+    f = 529.5 * W / 730
+    batch["calib_K"] = torch.tensor([[f, 0, W / 2], [0, f, H / 2], [0, 0, 1]], dtype=torch.float32).repeat(B, 1, 1)
+    return batch
+
+
+def run_model_fixture(R, name, args, cfg, batch, text):
+    tmp = tempfile.mkdtemp()
+    args.clip_embed_path = os.path.join(tmp, "text.pth")
+    torch.save(text, args.clip_embed_path)
+    torch.manual_seed(2024)
+    model, _ = R["model_3detr"].build_3detr(args, cfg)
+    model.train()
+    sd = {k: v.detach().clone().numpy() for k, v in model.state_dict().items()}
+    inputs = {"point_clouds": batch["point_clouds"], "point_cloud_dims_min": batch["point_cloud_dims_min"],
+              "point_cloud_dims_max": batch["point_cloud_dims_max"]}
+    out = model(inputs)
+    crit = R["criterion"].build_criterion(args, cfg)
+    clip = FakeRegionCLIP()
+    targets = dict(batch)
+    loss, ld = crit(out, targets, clip=clip)
+    loss.backward()
+    named = dict(model.named_parameters())
+    fx = {"sd/" + k: v for k, v in sd.items()}
+    fx.update({"in/" + k: v.numpy() for k, v in batch.items()})
+    layers = [out["outputs"]] + out["aux_outputs"]
+    for li, lay in enumerate(layers):
+        for k in MODEL_KEYS:
+            if k == "visual_embeds" and li not in (0, len(layers) - 1):
+                continue  # 640-d rows: keep the fixture small (pinned by the alignment loss anyway)
+            fx[f"out/{li}/{k}"] = lay[k].detach().numpy()
+    fx["loss"] = np.float32(loss.item())
+    for k, v in ld.items():
+        fx["ld/" + k] = np.float32(v.item())
+    for p in GRAD_PARAMS:
+        if p in named and named[p].grad is not None:
+            fx["grad/" + p] = named[p].grad.numpy()
+    fx["text"] = text.numpy()
+    fx["args"] = np.array(repr(sorted(vars(args).items())))
+    np.savez_compressed(os.path.join(HERE, name), **fx)
+    print(name, "loss", loss.item(), "keys", len(ld), "clip calls", clip.calls)
+
+
+def gen_model_sun(R):
+    cfg = R["sunrgbd"].SunrgbdDatasetConfig()
+    batch = synthetic.make_batch(2, seed=5, num_points=2048)
+    batch = small_images(batch, 2)
+    run_model_fixture(R, "model_sun.npz", model_args(), cfg, batch, synthetic.text_embedding(21, 640))
+
+
+def gen_model_scannet(R):
+    import datasets.scannet as scannet  # reference module (stubs installed by load_reference)
+    cfg = scannet.ScannetDatasetConfig()
+    batch = synthetic.make_batch(2, seed=9, num_points=4096, use_color=True)
+    # ScanNet boxes are axis aligned: zero every angle and rebuild the corners
+    B = 2
+    batch["gt_box_angles"].zero_()
+    batch["gt_angle_class_label"].zero_()
+    batch["gt_angle_residual_label"].zero_()
+    batch["gt_box_sem_cls_label"].clamp_(max=17)
+    corners = cfg.box_parametrization_to_corners_np(batch["gt_box_centers"].numpy(),
+                                                   batch["gt_box_sizes"].numpy(),
+                                                   np.zeros((B, 64), np.float32))
+    batch["gt_box_corners"] = torch.tensor(corners, dtype=torch.float32)
+    batch = small_images(batch, B)
+    args = model_args(enc_type="masked", use_color=True, preenc_npoints=512, nqueries=64,
+                      matcher_giou_cost=2.0, matcher_center_cost=0.0, matcher_objectness_cost=0.0,
+                      loss_giou_weight=1.0, loss_no_object_weight=0.25, loss_2dalignment_weight=0.0)
+    run_model_fixture(R, "model_scannet.npz", args, cfg, batch, synthetic.text_embedding(19, 640, seed=8))
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(8)
+    R = load_reference()
+    gen_giou(R)
+    gen_nms(R)
+    gen_geometry(R)
+    gen_model_sun(R)
+    gen_model_scannet(R)
+    for f in sorted(os.listdir(HERE)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(HERE, f)))
