@@ -86,6 +86,28 @@ def check(t, name, dtype=None, ndim=None):
     return t
 
 
+# Optional per-launch timing (bench.py): HIP events recorded on the launch stream.
+_TIMING = {}
+
+
+def timing_enable(names):
+    _TIMING.clear()
+    for n in names:
+        _TIMING[n] = []
+
+
+def timing_collect():
+    """-> {name: [{"ms": float, "shape": (int args...)}]}; synchronises the events."""
+    out = {}
+    for n, recs in _TIMING.items():
+        out[n] = []
+        for ev0, ev1, shape in recs:
+            ev1.synchronize()
+            out[n].append({"ms": ev0.elapsed_time(ev1), "shape": shape})
+    _TIMING.clear()
+    return out
+
+
 def call(name, *args, like):
     """Invoke `name` with args (+ the current stream of `like`); raise on nonzero status."""
     fn = getattr(load(), name)
@@ -95,6 +117,15 @@ def call(name, *args, like):
             conv.append(_ptr(a))
         else:
             conv.append(a)
+    rec = _TIMING.get(name)
+    if rec is not None:
+        stream = torch.cuda.current_stream(like.device)
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
     rc = fn(*conv, _stream(like))
+    if rec is not None:
+        ev1.record(stream)
+        rec.append((ev0, ev1, tuple(a for a in args if isinstance(a, int))[:3]))
     if rc != 0:
         raise NativeError(f"{name} failed with status {rc}")

@@ -1,0 +1,186 @@
+"""HIP kernels (libov3d_hip.so, called through the C ABI via the product
+wrappers) against the CPU oracle: bit-exact for indices / integer outputs /
+the no-contraction float kernels, and against the reference fixtures."""
+import numpy as np
+import pytest
+import torch
+
+from helpers import fixture, ov3d
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def scene_batch(B, N, seed, uniform=False):
+    from ov3d_amd import synthetic
+    return synthetic.make_batch(B, seed=seed, num_points=N, uniform_volume=uniform)["point_clouds"]
+
+
+# ------------------------------------------------------------------- FPS
+@pytest.mark.parametrize("B,N,M", [(8, 20000, 2048), (8, 2048, 128), (2, 40000, 1024),
+                                   (3, 2048, 1024), (2, 1000, 64), (4, 300, 17), (2, 37, 37),
+                                   (1, 1, 4), (2, 20480, 8), (2, 20481, 8)])
+def test_fps_bit_exact(cuda, B, N, M):
+    from ov3d_amd import pointnet2_utils as pu
+    xyz = scene_batch(B, N, seed=N + M) if N >= 64 else torch.rand(B, N, 3)
+    ref = O.fps(xyz.numpy(), M)
+    xg = xyz.to(cuda)
+    idx = pu.furthest_point_sample(xg, M)
+    np.testing.assert_array_equal(idx.cpu().numpy(), ref)
+    idx2, new_xyz = pu.furthest_point_sample_gather(xg, M)
+    np.testing.assert_array_equal(idx2.cpu().numpy(), ref)
+    np.testing.assert_array_equal(new_xyz.cpu().numpy(),
+                                  np.take_along_axis(xyz.numpy(), ref[..., None].astype(np.int64), 1))
+
+
+@pytest.mark.parametrize("N", [700, 5000])
+def test_fps_ties_and_skipped_points(cuda, N):
+    """integer grid -> exact distance ties; origin points -> the |p|^2 <= 1e-3 skip."""
+    from ov3d_amd import pointnet2_utils as pu
+    rs = np.random.RandomState(N)
+    xyz = rs.randint(-4, 5, size=(2, N, 3)).astype(np.float32)
+    xyz[:, rs.choice(N, N // 8, replace=False)] = 0.0
+    xyz[:, 7] = 1e-2  # |p|^2 = 3e-4 <= 1e-3 -> never selected
+    ref = O.fps(xyz, 200)
+    got = pu.furthest_point_sample(torch.from_numpy(xyz).to(cuda), 200).cpu().numpy()
+    np.testing.assert_array_equal(got, ref)
+    assert not (got[:, 1:] == 7).any()
+
+
+# ------------------------------------------------------------ ball query
+@pytest.mark.parametrize("B,N,M,r,S,uniform", [(8, 20000, 2048, 0.2, 64, False),
+                                               (8, 20000, 2048, 0.2, 64, True),
+                                               (4, 2048, 1024, 0.4, 32, False),
+                                               (2, 1001, 100, 0.3, 16, False),
+                                               (2, 500, 64, 0.05, 8, True)])
+def test_ball_query_bit_exact(cuda, B, N, M, r, S, uniform):
+    from ov3d_amd import pointnet2_utils as pu
+    xyz = scene_batch(B, N, seed=3 * N + M, uniform=uniform)
+    xn = xyz.numpy()
+    cen = xn[:, np.random.RandomState(1).choice(N, M, replace=False)].copy()
+    cen[:, 0] += 100.0  # one centroid with no neighbour at all
+    ref = O.ball_query(xn, cen, r, S)
+    got = pu.ball_query(r, S, xyz.to(cuda), torch.from_numpy(cen).to(cuda)).cpu().numpy()
+    np.testing.assert_array_equal(got, ref)
+
+
+# -------------------------------------------------------------- grouping
+@pytest.mark.parametrize("C", [0, 3, 256])
+def test_group_fwd_bwd(cuda, C):
+    from ov3d_amd import pointnet2_utils as pu
+    B, N, M, S, r = 2, 2048, 256, 32, 0.4
+    xyz = scene_batch(B, N, seed=11)
+    new_xyz = xyz[:, :M].clone()
+    feats = torch.randn(B, C, N) if C else None
+    grouper = pu.QueryAndGroup(r, S, use_xyz=True, ret_grouped_xyz=True, normalize_xyz=True)
+    fg = feats.to(cuda).requires_grad_(True) if C else None
+    out, gxyz = grouper(xyz.to(cuda), new_xyz.to(cuda), fg)
+    idx = O.ball_query(xyz.numpy(), new_xyz.numpy(), r, S)
+    exp_xyz = (O.group(xyz.transpose(1, 2).contiguous().numpy(), idx) - new_xyz.transpose(1, 2).numpy()[..., None]) / np.float32(r)
+    np.testing.assert_array_equal(out[:, :3].cpu().numpy(), exp_xyz.astype(np.float32))
+    if C:
+        np.testing.assert_array_equal(out[:, 3:].detach().cpu().numpy(), O.group(feats.numpy(), idx))
+        g = torch.randn_like(out)
+        out.backward(g)
+        ref = torch.zeros(B, C, N, dtype=torch.float64)
+        gi = torch.from_numpy(idx).long().view(B, 1, M * S).expand(B, C, M * S)
+        ref.scatter_add_(2, gi, g[:, 3:].double().cpu().reshape(B, C, M * S))
+        np.testing.assert_allclose(fg.grad.cpu().numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
+
+
+def test_gather_fwd_bwd(cuda):
+    from ov3d_amd import pointnet2_utils as pu
+    f = torch.randn(2, 5, 300, device=cuda, requires_grad=True)
+    idx = torch.randint(0, 300, (2, 40), device=cuda, dtype=torch.int32)
+    out = pu.gather_operation(f, idx)
+    ref = torch.gather(f.detach(), 2, idx.long()[:, None].expand(2, 5, 40))
+    assert torch.equal(out.detach(), ref)
+    g = torch.randn_like(out)
+    out.backward(g)
+    exp = torch.zeros(2, 5, 300, device=cuda).scatter_add_(2, idx.long()[:, None].expand(2, 5, 40), g)
+    torch.testing.assert_close(f.grad, exp)
+
+
+# ------------------------------------------------------------------ GIoU
+@pytest.mark.parametrize("tag", ["rot", "aligned"])
+@pytest.mark.parametrize("rflag", [True, False])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_giou_vs_oracle_and_reference(cuda, tag, rflag, mode):
+    from ov3d_amd.box_util import giou3d_raw
+    fx = fixture("giou.npz")
+    c1, c2, nums = fx[f"{tag}_c1"], fx[f"{tag}_c2"], fx[f"{tag}_nums"]
+    got = giou3d_raw(torch.from_numpy(c1).to(cuda), torch.from_numpy(c2).to(cuda),
+                     torch.from_numpy(nums).to(cuda), mode, rflag).cpu().numpy()
+    np.testing.assert_array_equal(got, O.giou3d(c1, c2, nums, mode=mode, rotated=rflag))
+    ref = fx[f"{tag}_{'r' if rflag else 'a'}_{'cython' if mode == 0 else 'tensor'}"]
+    np.testing.assert_allclose(got, ref, rtol=0, atol=2e-6)
+
+
+def test_giou_large_batch_vs_oracle(cuda):
+    """BASELINE shapes: 8 decoder layers x B=8, 128 predictions x 64 GT slots."""
+    from ov3d_amd.box_util import generalized_box3d_iou
+    from ov3d_amd.dataset_config import SunrgbdDatasetConfig
+    cfg = SunrgbdDatasetConfig()
+    g = torch.Generator().manual_seed(0)
+    P, Q, G = 64, 128, 64
+    def boxes(n):
+        c = torch.rand(P, n, 3, generator=g) * torch.tensor([4.0, 4.0, 2.0]) - torch.tensor([2.0, -1.0, 0.5])
+        s = torch.rand(P, n, 3, generator=g) * 1.7 + 0.3
+        a = torch.rand(P, n, generator=g) * 6.28 - 3.14
+        return cfg.box_parametrization_to_corners(c, s, a)
+    c1, c2 = boxes(Q), boxes(G)
+    nums = torch.randint(1, 11, (P,), generator=g)
+    got = generalized_box3d_iou(c1.to(cuda), c2.to(cuda), nums.to(cuda)).cpu().numpy()
+    np.testing.assert_array_equal(got, O.giou3d(c1.numpy(), c2.numpy(), nums.numpy()))
+
+
+def test_giou_backward_matches_reference_autograd(cuda):
+    from ov3d_amd.box_util import generalized_box3d_iou
+    fx = fixture("giou.npz")
+    c1 = torch.from_numpy(fx["grad_c1"]).to(cuda).requires_grad_(True)
+    g = generalized_box3d_iou(c1, torch.from_numpy(fx["grad_c2"]).to(cuda),
+                              torch.from_numpy(fx["grad_nums"]).to(cuda), rotated_boxes=False,
+                              needs_grad=True)
+    np.testing.assert_allclose(g.detach().cpu().numpy(), fx["grad_giou"], atol=2e-6)
+    (g * torch.from_numpy(fx["grad_G"]).to(cuda)).sum().backward()
+    np.testing.assert_allclose(c1.grad.cpu().numpy(), fx["grad_dc1"], rtol=1e-4, atol=1e-5)
+
+
+# ------------------------------------------------------------------- NMS
+@pytest.mark.parametrize("i", [0, 1, 2])
+@pytest.mark.parametrize("old", [False, True])
+def test_nms_matches_reference(cuda, i, old):
+    from ov3d_amd import nms
+    fx = fixture("nms.npz")
+    boxes = fx[f"boxes{i}"]
+    assert nms.nms_3d_faster_samecls(boxes, 0.25, old) == fx[f"samecls{i}_{int(old)}"].tolist()
+    assert nms.nms_3d_faster(boxes[:, :7], 0.25, old) == fx[f"any{i}_{int(old)}"].tolist()
+
+
+def test_nms_batched_vs_oracle_with_ties_and_valid_mask(cuda):
+    from ov3d_amd import nms
+    rs = np.random.RandomState(9)
+    B, K = 8, 256
+    lo = rs.uniform(-2, 2, (B, K, 3))
+    boxes = np.concatenate([lo, lo + rs.uniform(0.3, 1.5, (B, K, 3)),
+                            rs.randint(0, 6, (B, K, 1)) / 5.0, rs.randint(0, 3, (B, K, 1))], 2)
+    valid = rs.rand(B, K) > 0.2
+    keep = nms.nms3d_batched(torch.from_numpy(boxes).to(cuda), 0.25,
+                             valid=torch.from_numpy(valid).to(cuda)).cpu().numpy()
+    for b in range(B):
+        sub = np.nonzero(valid[b])[0]
+        _, k = O.nms3d(boxes[b, sub], 0.25)
+        exp = np.zeros(K, np.uint8)
+        exp[sub] = k
+        np.testing.assert_array_equal(keep[b], exp)
+
+
+def test_nms_boxes_from_corners(cuda):
+    from ov3d_amd import nms
+    corners = torch.randn(2, 16, 8, 3, device=cuda)
+    obj = torch.rand(2, 16, device=cuda)
+    cls = torch.randint(0, 5, (2, 16), device=cuda)
+    t = nms.nms_boxes_from_corners(corners, obj, cls)
+    c64 = corners.double()
+    exp = torch.cat([c64.min(2).values, c64.max(2).values, obj.double()[..., None], cls.double()[..., None]], -1)
+    assert torch.equal(t, exp)

@@ -1,0 +1,74 @@
+"""The product model + criterion on the GPU (HIP sampling / grouping / GIoU
+kernels) against the REFERENCE fixtures (fp32, within 1e-3 relative), and the
+full BASELINE-size training step through size-independent properties."""
+import numpy as np
+import pytest
+import torch
+
+from fake_clip import FakeRegionCLIP
+from helpers import batch_from_fixture, build_model_from_fixture, fixture, fixture_prefix, rel_err
+
+pytestmark = pytest.mark.gpu
+
+CASES = [("model_sun.npz", "sunrgbd"), ("model_scannet.npz", "scannet")]
+
+
+def _no_tf32():
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+
+
+@pytest.mark.parametrize("name,ds", CASES)
+def test_model_matches_reference_on_gpu(cuda, name, ds):
+    from ov3d_amd.criterion import build_criterion
+    _no_tf32()
+    fx = fixture(name)
+    model, cfg, args = build_model_from_fixture(fx, cuda, ds)
+    model.train()
+    batch = batch_from_fixture(fx, cuda)
+    out = model({k: batch[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")})
+    layers = [out["outputs"]] + out["aux_outputs"]
+    for li, lay in enumerate(layers):
+        for k, ref in fixture_prefix(fx, f"out/{li}/").items():
+            assert rel_err(lay[k].detach().cpu().numpy(), ref) < 1e-3, (li, k)
+    crit = build_criterion(args, cfg).to(cuda)
+    loss, ld = crit(out, dict(batch), clip=FakeRegionCLIP())
+    for k, v in fixture_prefix(fx, "ld/").items():
+        assert abs(ld[k].item() - float(v)) <= 1e-3 * max(abs(float(v)), 1e-3), k
+    loss.backward()
+    named = dict(model.named_parameters())
+    for k, g in fixture_prefix(fx, "grad/").items():
+        assert rel_err(named[k].grad.cpu().numpy(), g) < 1e-3, k
+
+
+def test_full_size_train_step_properties(cuda):
+    """BASELINE config 2 shapes (B=8, 20000 pts, 128 queries, 256-d, 8 decoder layers)."""
+    import ov3d_amd
+    from ov3d_amd import synthetic
+    from ov3d_amd.dataset_config import SunrgbdDatasetConfig
+    from bench import default_args
+    args = default_args()
+    cfg = SunrgbdDatasetConfig()
+    torch.manual_seed(0)
+    model, _ = ov3d_amd.build_model(args, cfg, text_embedding=synthetic.text_embedding())
+    model = model.to(cuda).train()
+    crit = ov3d_amd.build_criterion(args, cfg).to(cuda)
+    batch = synthetic.make_batch(8, seed=1, device=cuda)
+    inputs = {k: batch[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")}
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = model(inputs)
+    loss, ld = crit(out, batch)
+    assert torch.isfinite(loss) and len(ld) == 48  # 6 weighted+cardinality keys x 8 (no 2D branch)
+    loss.backward()
+    gn = torch.nn.utils.clip_grad_norm_(model.parameters(), 0.1)
+    assert torch.isfinite(gn)
+    # sampling invariants at full size
+    from ov3d_amd import pointnet2_utils as pu
+    idx, nx = pu.furthest_point_sample_gather(batch["point_clouds"], 2048)
+    assert (idx[:, 0] == 0).all()
+    for b in range(8):
+        assert torch.unique(idx[b]).numel() == 2048
+    bq = pu.ball_query(0.2, 64, batch["point_clouds"], nx)
+    d = ((batch["point_clouds"][torch.arange(8, device=cuda)[:, None, None], bq.long()] - nx[:, :, None]) ** 2).sum(-1)
+    assert (d < 0.2 ** 2 + 1e-6).all()
+    assert (bq[..., 1:] >= bq[..., :1]).all()   # padded with the first hit, ascending
