@@ -110,14 +110,15 @@ class SetCriterion(nn.Module):
         tot = all_reduce_average(nactual_gt.sum())
         angles = targets["gt_box_angles"]
         # one host sync for all data-dependent scalars
-        stats = torch.stack([tot.float(), nactual_gt.sum().float(), (angles > 0).any().float()]).tolist()
+        stats = torch.cat([torch.stack([tot.float(), (angles > 0).any().float()]),
+                           nactual_gt.float()]).tolist()
         num_boxes = max(stats[0], 1.0)
-        num_boxes_replica = int(stats[1])
-        rotated = bool(stats[2])
+        rotated = bool(stats[1])
+        nact = [int(v) for v in stats[2:]]
+        num_boxes_replica = sum(nact)
         targets["nactual_gt"] = nactual_gt
         targets["num_boxes"] = num_boxes
         targets["num_boxes_replica"] = num_boxes_replica
-        nact = nactual_gt.tolist()
 
         def cat(key):
             return torch.cat([o[key] for o in layers], dim=0)    # (L*B, ...)

@@ -131,6 +131,12 @@ class Model3DETR(nn.Module):
 
     # -------------------------------------------------------------------- heads
     def get_box_predictions(self, query_xyz, point_cloud_dims, box_features):
+        """Heads for all L decoder layers at once (the reference loops over layers,
+        model_3detr.py:264-306); evaluated in fp32 like the reference, even under autocast."""
+        with torch.autocast(device_type=box_features.device.type, enabled=False):
+            return self._box_predictions(query_xyz.float(), point_cloud_dims, box_features.float())
+
+    def _box_predictions(self, query_xyz, point_cloud_dims, box_features):
         L, Q, B, C = box_features.shape
         feats = box_features.permute(0, 2, 3, 1).reshape(L * B, C, Q)
         heads = self.mlp_heads
@@ -146,30 +152,38 @@ class Model3DETR(nn.Module):
         angle_res_norm = heads["angle_residual_head"](feats).transpose(1, 2).reshape(L, B, Q, -1)
         angle_res = angle_res_norm * (np.pi / angle_res_norm.shape[-1])
         visual = visual.reshape(L, B, Q, -1)
+
+        # BoxProcessor over the stacked (L*B) batch: dims repeated per layer
+        dims = [point_cloud_dims[0].repeat(L, 1), point_cloud_dims[1].repeat(L, 1)]
         bp = self.box_processor
-        outs = []
-        for l in range(L):
-            center_n, center_u = bp.compute_predicted_center(center_offset[l], query_xyz, point_cloud_dims)
-            angle = bp.compute_predicted_angle(angle_logits[l], angle_res[l])
-            size_u = bp.compute_predicted_size(size_norm[l], point_cloud_dims)
-            corners = bp.box_parametrization_to_corners(center_u, size_u, angle)
-            with torch.no_grad():
-                sem_prob, obj_prob = bp.compute_objectness_and_cls_prob(logits[l])
-            outs.append({
-                "visual_embeds": visual[l],
-                "sem_cls_logits": logits[l],
-                "center_normalized": center_n.contiguous(),
-                "center_unnormalized": center_u,
-                "size_normalized": size_norm[l],
-                "size_unnormalized": size_u,
-                "angle_logits": angle_logits[l],
-                "angle_residual": angle_res[l],
-                "angle_residual_normalized": angle_res_norm[l],
-                "angle_continuous": angle,
-                "objectness_prob": obj_prob,
-                "sem_cls_prob": sem_prob,
-                "box_corners": corners,
-            })
+        center_n, center_u = bp.compute_predicted_center(center_offset.reshape(L * B, Q, 3),
+                                                         query_xyz.repeat(L, 1, 1), dims)
+        angle = bp.compute_predicted_angle(angle_logits.reshape(L * B, Q, -1),
+                                           angle_res.reshape(L * B, Q, -1))
+        size_u = bp.compute_predicted_size(size_norm.reshape(L * B, Q, 3), dims)
+        corners = bp.box_parametrization_to_corners(center_u, size_u, angle)
+        with torch.no_grad():
+            sem_prob, obj_prob = bp.compute_objectness_and_cls_prob(logits)
+        center_n = center_n.view(L, B, Q, 3)
+        center_u = center_u.view(L, B, Q, 3)
+        size_u = size_u.view(L, B, Q, 3)
+        angle = angle.view(L, B, Q)
+        corners = corners.view(L, B, Q, 8, 3)
+        outs = [{
+            "visual_embeds": visual[l],
+            "sem_cls_logits": logits[l],
+            "center_normalized": center_n[l],
+            "center_unnormalized": center_u[l],
+            "size_normalized": size_norm[l],
+            "size_unnormalized": size_u[l],
+            "angle_logits": angle_logits[l],
+            "angle_residual": angle_res[l],
+            "angle_residual_normalized": angle_res_norm[l],
+            "angle_continuous": angle[l],
+            "objectness_prob": obj_prob[l],
+            "sem_cls_prob": sem_prob[l],
+            "box_corners": corners[l],
+        } for l in range(L)]
         return {"outputs": outs[-1], "aux_outputs": outs[:-1]}
 
     def forward(self, inputs, encoder_only=False):

@@ -8,7 +8,6 @@ checkpoints load: ``mlp_module.layer{i}.conv.weight``,
 """
 
 import torch.nn as nn
-import torch.nn.functional as F
 
 from . import pointnet2_utils as pu
 
@@ -78,8 +77,9 @@ class PointnetSAModuleVotes(nn.Module):
             new_xyz = new_xyz.contiguous()
         grouped, _ = self.grouper(xyz, new_xyz, features)
         new_features = self.mlp_module(grouped)
-        new_features = F.max_pool2d(new_features, kernel_size=[1, new_features.size(3)])
-        return new_xyz, new_features.squeeze(-1), inds
+        # max over nsample (== F.max_pool2d(kernel [1, nsample]) of the reference); amax runs as one
+        # reduction instead of PyTorch's generic pooling kernel
+        return new_xyz, new_features.amax(dim=3), inds
 
 
 __all__ = ["PointnetSAModuleVotes", "SharedMLP"]

@@ -77,7 +77,7 @@ def test_group_fwd_bwd(cuda, C):
     out, gxyz = grouper(xyz.to(cuda), new_xyz.to(cuda), fg)
     idx = O.ball_query(xyz.numpy(), new_xyz.numpy(), r, S)
     exp_xyz = (O.group(xyz.transpose(1, 2).contiguous().numpy(), idx) - new_xyz.transpose(1, 2).numpy()[..., None]) / np.float32(r)
-    np.testing.assert_array_equal(out[:, :3].cpu().numpy(), exp_xyz.astype(np.float32))
+    np.testing.assert_array_equal(out[:, :3].detach().cpu().numpy(), exp_xyz.astype(np.float32))
     if C:
         np.testing.assert_array_equal(out[:, 3:].detach().cpu().numpy(), O.group(feats.numpy(), idx))
         g = torch.randn_like(out)
