@@ -48,19 +48,24 @@ int ov3d_fps(const float* xyz, int B, int N, int M, int32_t* idx_out, float* new
 int ov3d_ball_query(const float* xyz, const float* new_xyz, int B, int N, int M, float radius,
                     int S, int32_t* idx_out, void* stream);
 
-/* QueryAndGroup output with use_xyz=True (pointnet2_utils.QueryAndGroup.forward):
- *   out[:, 0:3]   = (xyz[idx] - new_xyz) (/ radius if normalize)
- *   out[:, 3:3+C] = features[:, :, idx]           (features may be NULL, C = 0)
- *   xyz (B,N,3) f32, new_xyz (B,M,3), features (B,C,N), idx (B,M,S) -> out (B,3+C,M,S) */
+/* QueryAndGroup output with use_xyz=True (pointnet2_utils.QueryAndGroup.forward),
+ * written as channels-last rows (the GEMM layout of the SA MLP):
+ *   out[b,m,s, 0:3]   = (xyz[b,idx] - new_xyz[b,m]) (/ radius if normalize)
+ *   out[b,m,s, 3:3+C] = features[b, :, idx]          (features may be NULL, C = 0)
+ * features element (b, n, c) lives at features[b*feat_sb + n*feat_sn + c*feat_sc]
+ * ((B,C,N) contiguous: sb = C*N, sn = 1, sc = N; seq-first (N,B,C): sb = C, sn = B*C, sc = 1).
+ *   xyz (B,N,3) f32, new_xyz (B,M,3), idx (B,M,S) int32 -> out (B,M,S,3+C) f32 */
 int ov3d_group_fwd(const float* xyz, const float* new_xyz, const float* features,
-                   const int32_t* idx, int B, int C, int N, int M, int S, float radius,
-                   int normalize, float* out, void* stream);
+                   long long feat_sb, long long feat_sn, long long feat_sc, const int32_t* idx,
+                   int B, int C, int N, int M, int S, float radius, int normalize, float* out,
+                   void* stream);
 
 /* Backward of the feature part of ov3d_group_fwd (grouping_operation backward):
- *   grad_out (B,3+C,M,S) -> grad_features (B,C,N); the callee zero-fills
- *   grad_features on the stream, then scatter-adds. */
+ *   grad_out (B,M,S,3+C) -> grad_features (B*C*N elements, same strides as the forward);
+ *   the callee zero-fills grad_features on the stream, then scatter-adds. */
 int ov3d_group_bwd(const float* grad_out, const int32_t* idx, int B, int C, int N, int M, int S,
-                   float* grad_features, void* stream);
+                   long long feat_sb, long long feat_sn, long long feat_sc, float* grad_features,
+                   void* stream);
 
 /* gather_operation (pointnet2_utils): features (B,C,N), idx (B,M) -> out (B,C,M) */
 int ov3d_gather_fwd(const float* features, const int32_t* idx, int B, int C, int N, int M,

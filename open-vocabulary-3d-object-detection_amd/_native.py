@@ -19,12 +19,12 @@ OV3D_GIOU_TENSOR = 1
 
 _lib = None
 
-# name -> argtypes ("p" pointer, "i" int, "f" float, "d" double)
+# name -> argtypes ("p" pointer, "i" int, "l" long long, "f" float, "d" double)
 _SIGS = {
     "ov3d_fps": "piiipppp",
     "ov3d_ball_query": "ppiiifipp",
-    "ov3d_group_fwd": "ppppiiiiifipp",
-    "ov3d_group_bwd": "ppiiiiipp",
+    "ov3d_group_fwd": "ppplllpiiiiifipp",
+    "ov3d_group_bwd": "ppiiiiilllpp",
     "ov3d_gather_fwd": "ppiiiipp",
     "ov3d_gather_bwd": "ppiiiipp",
     "ov3d_giou3d": "pppiiiiiipp",
@@ -34,7 +34,8 @@ _SIGS = {
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version",)
 
-_CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "f": ctypes.c_float, "d": ctypes.c_double}
+_CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_longlong, "f": ctypes.c_float,
+       "d": ctypes.c_double}
 
 
 class NativeError(RuntimeError):
@@ -70,6 +71,14 @@ def _stream(t):
 
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def check_device(t, name):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a tensor")
+    if t.device.type != "cuda":
+        raise NativeError(f"{name}: ov3d kernels run on the ROCm device only (got {t.device})")
+    return t
 
 
 def check(t, name, dtype=None, ndim=None):

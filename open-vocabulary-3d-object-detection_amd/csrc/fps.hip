@@ -5,12 +5,13 @@
 //
 // Design (one 1024-thread workgroup = 16 waves per scene, the scene's points
 // held in registers for the whole run):
-//   * point k lives in thread (k mod 1024), slot (k / 1024): PPT slots per thread,
-//     coordinates + running min-distance in VGPRs (4 regs per slot);
-//   * per iteration: VALU distance update + per-thread argmax, wave64 u64 max
-//     reduction with shuffles, one LDS slot per wave (double-buffered by
-//     iteration parity -> ONE barrier per iteration), every thread reduces the
-//     16 wave slots and reads the winner's coordinates from LDS;
+//   * PPT slots per thread, coordinates + running min-distance in VGPRs
+//     (4 regs per slot), points grouped into one spatial cluster per wave;
+//   * per iteration: waves whose cluster cannot get closer skip (exact), the
+//     others do the VALU distance update + per-thread argmax + DPP reduction;
+//     one LDS slot per wave (double-buffered by iteration parity -> ONE barrier
+//     per iteration), every wave reduces the 16 wave slots and reads the
+//     winner's coordinates from LDS;
 //   * the winner's coordinates are carried through the reduction, so there is
 //     no dependent global load on the serial chain; new_xyz (gather_operation)
 //     is written in the same loop.
@@ -89,67 +90,6 @@ __device__ __forceinline__ Pick block_pick(unsigned long long key, float bx, flo
     return p;
 }
 
-template <int PPT>
-__global__ __launch_bounds__(kThreads) void fps_reg_kernel(const float* __restrict__ xyz, int N,
-                                                           int M, int L,
-                                                           int32_t* __restrict__ idx,
-                                                           float* __restrict__ new_xyz) {
-    __shared__ unsigned long long s_key[2][kWaves];
-    __shared__ float4 s_xyz[2][kWaves];
-    const int b = blockIdx.x;
-    const int tid = threadIdx.x;
-    const float* __restrict__ p = xyz + (size_t)b * N * 3;
-    idx += (size_t)b * M;
-    if (new_xyz) new_xyz += (size_t)b * M * 3;
-
-    float px[PPT], py[PPT], pz[PPT], td[PPT];
-#pragma unroll
-    for (int i = 0; i < PPT; ++i) {
-        const int k = tid + i * kThreads;
-        if (k < N) {
-            const float x = p[3 * k], y = p[3 * k + 1], z = p[3 * k + 2];
-            const float mag = fmaf(z, z, fmaf(y, y, x * x));
-            px[i] = x; py[i] = y; pz[i] = z;
-            td[i] = ((double)mag <= 1e-3) ? -1.f : 1e10f;  // -1: never a candidate
-        } else {
-            px[i] = 0.f; py[i] = 0.f; pz[i] = 0.f; td[i] = -1.f;
-        }
-    }
-    const float x0 = p[0], y0 = p[1], z0 = p[2];
-    float x1 = x0, y1 = y0, z1 = z0;
-    if (tid == 0) {
-        idx[0] = 0;
-        if (new_xyz) { new_xyz[0] = x0; new_xyz[1] = y0; new_xyz[2] = z0; }
-    }
-    for (int j = 1; j < M; ++j) {
-        float best = -1.f, bx = 0.f, by = 0.f, bz = 0.f;
-        int bi = 0;
-#pragma unroll
-        for (int i = 0; i < PPT; ++i) {
-            const float dx = px[i] - x1, dy = py[i] - y1, dz = pz[i] - z1;
-            const float d = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-            const float d2 = fminf(d, td[i]);
-            td[i] = d2;
-            const bool gt = d2 > best;
-            best = gt ? d2 : best;
-            bi = gt ? i : bi;
-            bx = gt ? px[i] : bx;
-            by = gt ? py[i] : by;
-            bz = gt ? pz[i] : bz;
-        }
-        unsigned long long key = 0ull;
-        if (best >= 0.f)
-            key = ((unsigned long long)__float_as_uint(best) << 32) |
-                  (unsigned long long)(~fps_rank((uint32_t)(tid + bi * kThreads), L));
-        const Pick pk = block_pick(key, bx, by, bz, j & 1, s_key, s_xyz, x0, y0, z0, L);
-        x1 = pk.x; y1 = pk.y; z1 = pk.z;
-        if (tid == 0) {
-            idx[j] = pk.k;
-            if (new_xyz) { new_xyz[3 * j] = pk.x; new_xyz[3 * j + 1] = pk.y; new_xyz[3 * j + 2] = pk.z; }
-        }
-    }
-}
-
 // Large-N path (N > kThreads * kMaxPPT): running distances in a global workspace.
 __global__ __launch_bounds__(kThreads) void fps_global_kernel(const float* __restrict__ xyz, int N,
                                                               int M, int L, float* __restrict__ temp,
@@ -203,10 +143,319 @@ __global__ __launch_bounds__(kThreads) void fps_global_kernel(const float* __res
     }
 }
 
+// ---------------------------------------------------------------------------
+// Spatially culled FPS (N <= kThreads * kMaxPPT).
+//
+// Setup (once per launch, one workgroup per scene): scene bbox -> 16^3 Morton
+// cell code per point -> LDS counting sort -> wave w owns sorted positions
+// [w*64*PPT, (w+1)*64*PPT), i.e. a compact spatial cluster; each thread sorts
+// its PPT slots by tie-break rank so that strict '>' inside the thread keeps the
+// upstream tie rule; per-wave bounding box.
+// Iteration: a wave updates its points only if the new sample can be closer
+// than the wave's current max running distance: lb = |gap(new, wave bbox)|^2 is
+// evaluated with the same monotone float ops as the point distances, so
+// lb >= wave_tmax implies min(d, temp) == temp for every point of the wave
+// (exact skip, results unchanged).  Skipping waves re-publish their cached
+// best.  ~1/4 of the waves update per iteration on SUN scenes (measured in the
+// DESIGN.md simulation), the rest cost ~15 VALU ops.
+// Reductions: DPP row reductions + readlane, 32-bit keys (distance bits, then
+// min rank only when distances tie).
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ int dpp_mov(int v) {
+    return __builtin_amdgcn_update_dpp(v, v, CTRL, ROWS, 0xf, false);
+}
+
+// every lane of each 16-lane row gets the row's max / min
+__device__ __forceinline__ int row_max_i32(int v) {
+    v = max(v, dpp_mov<0xb1>(v));   // quad_perm(1,0,3,2)
+    v = max(v, dpp_mov<0x4e>(v));   // quad_perm(2,3,0,1)
+    v = max(v, dpp_mov<0x141>(v));  // row_half_mirror
+    v = max(v, dpp_mov<0x140>(v));  // row_mirror
+    return v;
+}
+
+__device__ __forceinline__ uint32_t row_min_u32(uint32_t v) {
+    v = min(v, (uint32_t)dpp_mov<0xb1>((int)v));
+    v = min(v, (uint32_t)dpp_mov<0x4e>((int)v));
+    v = min(v, (uint32_t)dpp_mov<0x141>((int)v));
+    v = min(v, (uint32_t)dpp_mov<0x140>((int)v));
+    return v;
+}
+
+// wave64 reductions: rows, then row_bcast15 / row_bcast31 fold rows into lane 63
+__device__ __forceinline__ int wave_max_i32(int v) {
+    v = row_max_i32(v);
+    v = max(v, dpp_mov<0x142, 0xa>(v));  // row_bcast:15 into rows 1, 3
+    v = max(v, dpp_mov<0x143, 0xc>(v));  // row_bcast:31 into rows 2, 3
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    v = row_min_u32(v);
+    v = min(v, (uint32_t)dpp_mov<0x142, 0xa>((int)v));
+    v = min(v, (uint32_t)dpp_mov<0x143, 0xc>((int)v));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+__device__ __forceinline__ float wave_fmin(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fminf(v, __shfl_xor(v, off));
+    return v;
+}
+__device__ __forceinline__ float wave_fmax(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+    return v;
+}
+
+__device__ __forceinline__ uint32_t spread3(uint32_t x) {  // 4 bits -> every 3rd bit
+    x &= 0xf;
+    x = (x | (x << 4)) & 0x0c3;
+    x = (x | (x << 2)) & 0x249;
+    return x;
+}
+
+constexpr int kCells = 4096;
+constexpr int kMaxOutLDS = 8192;  // deferred outputs: M <= 8192 on the culled path
+
 template <int PPT>
-void launch_reg(const float* xyz, int B, int N, int M, int L, int32_t* idx, float* nx,
-                hipStream_t s) {
-    hipLaunchKernelGGL(fps_reg_kernel<PPT>, dim3(B), dim3(kThreads), 0, s, xyz, N, M, L, idx, nx);
+__global__ __launch_bounds__(kThreads) void fps_cull_kernel(const float* __restrict__ xyz, int N,
+                                                            int M, int L,
+                                                            int32_t* __restrict__ idx,
+                                                            float* __restrict__ new_xyz) {
+    constexpr int PW = PPT * 64;
+    __shared__ uint32_t s_hist[kCells];
+    __shared__ uint16_t s_perm[kThreads * PPT];
+    __shared__ uint16_t s_out[kMaxOutLDS];     // winner position per iteration (outputs deferred)
+    __shared__ float s_red[6][kWaves];
+    __shared__ uint32_t s_scan[kWaves];
+    __shared__ float4 s_pub[2][kWaves];         // per-wave best: x, y, z, distance bits
+    __shared__ int s_pos[2][kWaves];            // per-wave best: sorted position
+
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int w = tid >> 6;
+    const float* __restrict__ p = xyz + (size_t)b * N * 3;
+    idx += (size_t)b * M;
+    if (new_xyz) new_xyz += (size_t)b * M * 3;
+
+    // ---- (a) scene bbox
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int k = tid; k < N; k += kThreads)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float v = p[3 * k + a];
+            lo[a] = fminf(lo[a], v);
+            hi[a] = fmaxf(hi[a], v);
+        }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = wave_fmin(lo[a]);
+        hi[a] = wave_fmax(hi[a]);
+    }
+    if (lane == 0)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) { s_red[a][w] = lo[a]; s_red[3 + a][w] = hi[a]; }
+    for (int i = tid; i < kCells; i += kThreads) s_hist[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        float l = s_red[a][0], h = s_red[3 + a][0];
+        for (int q = 1; q < kWaves; ++q) { l = fminf(l, s_red[a][q]); h = fmaxf(h, s_red[3 + a][q]); }
+        lo[a] = l;
+        hi[a] = 16.f / fmaxf(h - l, 1e-6f);  // cell scale
+    }
+
+    // ---- (b) cell codes + LDS counting sort (order inside a cell is irrelevant:
+    //          ties are decided by rank, never by layout)
+    uint32_t cp[PPT];
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+        const int k = tid + i * kThreads;
+        cp[i] = 0xffffffffu;
+        if (k < N) {
+            uint32_t q[3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const int c = (int)((p[3 * k + a] - lo[a]) * hi[a]);
+                q[a] = (uint32_t)min(max(c, 0), 15);
+            }
+            const uint32_t code = spread3(q[0]) | (spread3(q[1]) << 1) | (spread3(q[2]) << 2);
+            const uint32_t old = atomicAdd(&s_hist[code], 1u);
+            cp[i] = (code << 16) | old;
+        }
+    }
+    __syncthreads();
+    {   // exclusive scan of the 4096 cell counts: 4 per thread
+        uint32_t v[4], sum = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { v[q] = s_hist[4 * tid + q]; sum += v[q]; }
+        uint32_t inc = sum;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t o = __shfl_up(inc, off);
+            if (lane >= off) inc += o;
+        }
+        if (lane == 63) s_scan[w] = inc;
+        __syncthreads();
+        uint32_t base = 0;
+        for (int q = 0; q < w; ++q) base += s_scan[q];
+        uint32_t run = base + inc - sum;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { s_hist[4 * tid + q] = run; run += v[q]; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PPT; ++i)
+        if (cp[i] != 0xffffffffu)
+            s_perm[s_hist[cp[i] >> 16] + (cp[i] & 0xffffu)] = (uint16_t)(tid + i * kThreads);
+    __syncthreads();
+
+    // ---- (c) this thread's slots: wave w, positions w*PW + i*64 + lane, sorted by rank
+    uint32_t rk[PPT];
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+        const int pos = w * PW + i * 64 + lane;
+        rk[i] = pos < N ? fps_rank(s_perm[pos], L) : 0xffffffffu;
+    }
+#pragma unroll
+    for (int pass = 0; pass < PPT; ++pass)
+#pragma unroll
+        for (int i = pass & 1; i + 1 < PPT; i += 2) {
+            const uint32_t a = rk[i], c = rk[i + 1];
+            rk[i] = min(a, c);
+            rk[i + 1] = max(a, c);
+        }
+    float px[PPT], py[PPT], pz[PPT], td[PPT];
+    float wlo[3] = {INFINITY, INFINITY, INFINITY}, whi[3] = {-INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+        const int pos = w * PW + i * 64 + lane;
+        if (rk[i] != 0xffffffffu) {
+            const int k = fps_unrank(rk[i], L);
+            s_perm[pos] = (uint16_t)k;
+            const float x = p[3 * k], y = p[3 * k + 1], z = p[3 * k + 2];
+            const float mag = fmaf(z, z, fmaf(y, y, x * x));
+            px[i] = x; py[i] = y; pz[i] = z;
+            const bool skip = (double)mag <= 1e-3;
+            td[i] = skip ? -1.f : 1e10f;
+            if (!skip) {
+                wlo[0] = fminf(wlo[0], x); wlo[1] = fminf(wlo[1], y); wlo[2] = fminf(wlo[2], z);
+                whi[0] = fmaxf(whi[0], x); whi[1] = fmaxf(whi[1], y); whi[2] = fmaxf(whi[2], z);
+            }
+        } else {
+            px[i] = 0.f; py[i] = 0.f; pz[i] = 0.f; td[i] = -1.f;
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        wlo[a] = wave_fmin(wlo[a]);
+        whi[a] = wave_fmax(whi[a]);
+    }
+    const float x0 = p[0], y0 = p[1], z0 = p[2];
+    float x1 = x0, y1 = y0, z1 = z0;
+    // wave cache: best distance (float bits), its sorted position and coordinates
+    float wtmax = INFINITY;
+    int wdist = __float_as_int(-1.f);
+    int wpos = 0;
+    float wx = 0.f, wy = 0.f, wz = 0.f;
+
+    for (int j = 1; j < M; ++j) {
+        const int buf = j & 1;
+        const float gx = fmaxf(fmaxf(wlo[0] - x1, x1 - whi[0]), 0.f);
+        const float gy = fmaxf(fmaxf(wlo[1] - y1, y1 - whi[1]), 0.f);
+        const float gz = fmaxf(fmaxf(wlo[2] - z1, z1 - whi[2]), 0.f);
+        const float lb = fmaf(gz, gz, fmaf(gy, gy, gx * gx));
+        if (lb < wtmax) {  // wave-uniform
+            float best = -1.f;
+            int bi = 0;
+#pragma unroll
+            for (int i = 0; i < PPT; ++i) {
+                const float dx = px[i] - x1, dy = py[i] - y1, dz = pz[i] - z1;
+                const float d = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                const float d2 = fminf(d, td[i]);
+                td[i] = d2;
+                const bool gt = d2 > best;
+                best = gt ? d2 : best;
+                bi = gt ? i : bi;
+            }
+            const int bb = __float_as_int(best);
+            const int wm = wave_max_i32(bb);
+            wdist = wm;
+            wtmax = __int_as_float(wm);
+            if (wm >= 0) {
+                const unsigned long long cand = __ballot(bb == wm);
+                int wl;
+                if (__popcll(cand) == 1) {
+                    wl = __ffsll((long long)cand) - 1;
+                } else {  // distance tie inside the wave: smallest rank wins
+                    uint32_t my = 0xffffffffu;
+                    if (bb == wm) my = fps_rank(s_perm[w * PW + bi * 64 + lane], L);
+                    const uint32_t mr = wave_min_u32(my);
+                    wl = __ffsll((long long)__ballot(my == mr)) - 1;
+                }
+                const int bis = __builtin_amdgcn_readlane(bi, wl);
+                float sx = 0.f, sy = 0.f, sz = 0.f;
+#pragma unroll
+                for (int i = 0; i < PPT; ++i)
+                    if (i == bis) { sx = px[i]; sy = py[i]; sz = pz[i]; }
+                wx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sx), wl));
+                wy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sy), wl));
+                wz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sz), wl));
+                wpos = w * PW + bis * 64 + wl;
+            }
+        }
+        if (lane == 0) {
+            s_pub[buf][w] = make_float4(wx, wy, wz, __int_as_float(wdist));
+            s_pos[buf][w] = wpos;
+        }
+        // only LDS is shared inside the loop: wait for LDS, not for global memory
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        const float4 v = lane < kWaves ? s_pub[buf][lane] : make_float4(0.f, 0.f, 0.f, __int_as_float(INT_MIN));
+        const int vp = lane < kWaves ? s_pos[buf][lane] : 0;
+        const int dv = __float_as_int(v.w);
+        const int dm = __builtin_amdgcn_readlane(row_max_i32(dv), 0);
+        int pj;
+        if (dm < 0) {  // no candidate anywhere: upstream keeps thread 0's besti = 0
+            pj = 0xffff;
+            x1 = x0; y1 = y0; z1 = z0;
+        } else {
+            const unsigned long long cand = __ballot(lane < kWaves && dv == dm);
+            int ws;
+            if (__popcll(cand) == 1) {
+                ws = __ffsll((long long)cand) - 1;
+            } else {  // distance tie across waves: smallest rank wins
+                const uint32_t r = (lane < kWaves && dv == dm) ? fps_rank(s_perm[vp], L) : 0xffffffffu;
+                const uint32_t rm = __builtin_amdgcn_readlane(row_min_u32(r), 0);
+                ws = __ffsll((long long)__ballot(r == rm && lane < kWaves)) - 1;
+            }
+            x1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.x), ws));
+            y1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.y), ws));
+            z1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.z), ws));
+            pj = __builtin_amdgcn_readlane(vp, ws);
+        }
+        if (tid == 0) s_out[j] = (uint16_t)pj;
+    }
+    __syncthreads();
+    // ---- deferred outputs: indices + gathered coordinates, coalesced
+    for (int j = tid; j < M; j += kThreads) {
+        int k = 0;
+        if (j > 0 && s_out[j] != 0xffff) k = s_perm[s_out[j]];
+        idx[j] = k;
+        if (new_xyz) {
+            new_xyz[3 * j] = p[3 * k];
+            new_xyz[3 * j + 1] = p[3 * k + 1];
+            new_xyz[3 * j + 2] = p[3 * k + 2];
+        }
+    }
+}
+
+template <int PPT>
+void launch_cull(const float* xyz, int B, int N, int M, int L, int32_t* idx, float* nx,
+                 hipStream_t s) {
+    hipLaunchKernelGGL(fps_cull_kernel<PPT>, dim3(B), dim3(kThreads), 0, s, xyz, N, M, L, idx, nx);
 }
 
 }  // namespace
@@ -220,18 +469,14 @@ extern "C" int ov3d_fps(const float* xyz, int B, int N, int M, int32_t* idx_out,
     while (bs * 2 <= N && bs < 512) { bs *= 2; ++L; }
     hipStream_t s = ov3d_stream(stream);
     const int ppt = (N + kThreads - 1) / kThreads;
-    if (ppt <= kMaxPPT) {
-        if (ppt <= 1) launch_reg<1>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
-        else if (ppt <= 2) launch_reg<2>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
-        else if (ppt <= 3) launch_reg<3>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
-        else if (ppt <= 4) launch_reg<4>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
-        else if (ppt <= 6) launch_reg<6>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
-        else if (ppt <= 8) launch_reg<8>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
-        else if (ppt <= 10) launch_reg<10>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
-        else if (ppt <= 12) launch_reg<12>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
-        else if (ppt <= 16) launch_reg<16>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
-
-        else launch_reg<20>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
+    if (ppt <= kMaxPPT && M <= kMaxOutLDS) {
+        if (ppt <= 1) launch_cull<1>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
+        else if (ppt <= 2) launch_cull<2>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
+        else if (ppt <= 4) launch_cull<4>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
+        else if (ppt <= 8) launch_cull<8>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
+        else if (ppt <= 12) launch_cull<12>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
+        else if (ppt <= 16) launch_cull<16>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
+        else launch_cull<20>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
     } else {
         if (!workspace) return OV3D_EINVAL;
         hipLaunchKernelGGL(fps_global_kernel, dim3(B), dim3(kThreads), 0, s, xyz, N, M, L, workspace,

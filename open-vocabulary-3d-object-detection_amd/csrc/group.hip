@@ -90,46 +90,46 @@ __global__ __launch_bounds__(64 * kBQWavesPerBlock) void ball_query_kernel(
     for (int s = filled + lane; s < S; s += 64) out[s] = fill;
 }
 
-// out (B,3+C,M,S): thread per (b, m, s)
+// out (B,M,S,3+C) channels-last rows: thread per output element (row, channel);
+// features addressed through (sb, sn, sc) element strides, so both the reference
+// (B,C,N) layout and the encoder's seq-first (N,B,C) layout are read in place.
 __global__ __launch_bounds__(256) void group_fwd_kernel(
     const float* __restrict__ xyz, const float* __restrict__ new_xyz,
-    const float* __restrict__ feats, const int32_t* __restrict__ idx, int B, int C, int N, int M,
-    int S, float radius, int normalize, float* __restrict__ out) {
-    const long long MS = (long long)M * S;
+    const float* __restrict__ feats, long long sb, long long sn, long long sc,
+    const int32_t* __restrict__ idx, int B, int C, int N, int M, int S, float radius,
+    int normalize, float* __restrict__ out) {
+    const int CW = 3 + C;
     const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (long long)B * MS) return;
-    const int b = (int)(t / MS);
-    const long long ms = t - (long long)b * MS;
-    const int m = (int)(ms / S);
-    const int k = idx[t];
-    const float* c = new_xyz + ((size_t)b * M + m) * 3;
-    const float* q = xyz + ((size_t)b * N + k) * 3;
-    float* o = out + (size_t)b * (3 + C) * MS + ms;
-    float gx = q[0] - c[0], gy = q[1] - c[1], gz = q[2] - c[2];
-    if (normalize) { gx = gx / radius; gy = gy / radius; gz = gz / radius; }
-    o[0] = gx;
-    o[MS] = gy;
-    o[2 * MS] = gz;
-    if (feats) {
-        const float* f = feats + (size_t)b * C * N + k;
-        float* of = o + 3 * MS;
-        for (int ch = 0; ch < C; ++ch) of[(size_t)ch * MS] = f[(size_t)ch * N];
+    const long long rows = (long long)B * M * S;
+    if (t >= rows * CW) return;
+    const long long row = t / CW;
+    const int c = (int)(t - row * CW);
+    const int b = (int)(row / ((long long)M * S));
+    const int m = (int)((row / S) % M);
+    const int k = idx[row];
+    float v;
+    if (c < 3) {
+        v = xyz[((size_t)b * N + k) * 3 + c] - new_xyz[((size_t)b * M + m) * 3 + c];
+        if (normalize) v = v / radius;
+    } else {
+        v = feats[b * sb + k * sn + (c - 3) * sc];
     }
+    out[t] = v;
 }
 
 __global__ __launch_bounds__(256) void group_bwd_kernel(const float* __restrict__ gout,
                                                         const int32_t* __restrict__ idx, int B,
-                                                        int C, int N, int M, int S,
+                                                        int C, int M, int S, long long sb,
+                                                        long long sn, long long sc,
                                                         float* __restrict__ gfeat) {
-    const long long MS = (long long)M * S;
     const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (long long)B * MS) return;
-    const int b = (int)(t / MS);
-    const long long ms = t - (long long)b * MS;
-    const int k = idx[t];
-    const float* g = gout + (size_t)b * (3 + C) * MS + 3 * MS + ms;
-    float* d = gfeat + (size_t)b * C * N + k;
-    for (int ch = 0; ch < C; ++ch) atomicAdd(d + (size_t)ch * N, g[(size_t)ch * MS]);
+    const long long rows = (long long)B * M * S;
+    if (t >= rows * C) return;
+    const long long row = t / C;
+    const int c = (int)(t - row * C);
+    const int b = (int)(row / ((long long)M * S));
+    const int k = idx[row];
+    atomicAdd(gfeat + b * sb + k * sn + c * sc, gout[row * (3 + C) + 3 + c]);
 }
 
 // (B,C,N),(B,M) -> (B,C,M): thread per output element
@@ -178,32 +178,35 @@ extern "C" int ov3d_ball_query(const float* xyz, const float* new_xyz, int B, in
 }
 
 extern "C" int ov3d_group_fwd(const float* xyz, const float* new_xyz, const float* features,
+                              long long feat_sb, long long feat_sn, long long feat_sc,
                               const int32_t* idx, int B, int C, int N, int M, int S, float radius,
                               int normalize, float* out, void* stream) {
     if (B < 0 || C < 0 || N <= 0 || M < 0 || S <= 0 || !xyz || !new_xyz || !idx || !out)
         return OV3D_EINVAL;
     if (C > 0 && !features) return OV3D_EINVAL;
-    const long long total = (long long)B * M * S;
+    const long long total = (long long)B * M * S * (3 + C);
     if (total == 0) return OV3D_OK;
     hipLaunchKernelGGL(group_fwd_kernel, dim3(ov3d_cdiv(total, 256)), dim3(256), 0,
-                       ov3d_stream(stream), xyz, new_xyz, C > 0 ? features : nullptr, idx, B, C, N,
-                       M, S, radius, normalize, out);
+                       ov3d_stream(stream), xyz, new_xyz, C > 0 ? features : nullptr, feat_sb,
+                       feat_sn, feat_sc, idx, B, C, N, M, S, radius, normalize, out);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }
 
 extern "C" int ov3d_group_bwd(const float* grad_out, const int32_t* idx, int B, int C, int N, int M,
-                              int S, float* grad_features, void* stream) {
+                              int S, long long feat_sb, long long feat_sn, long long feat_sc,
+                              float* grad_features, void* stream) {
     if (B < 0 || C < 0 || N <= 0 || M < 0 || S <= 0 || !grad_out || !idx || !grad_features)
         return OV3D_EINVAL;
     hipStream_t s = ov3d_stream(stream);
+    // grad_features spans B*C*N elements whatever the stride order
     if ((long long)B * C * N > 0 &&
         hipMemsetAsync(grad_features, 0, sizeof(float) * (size_t)B * C * N, s) != hipSuccess)
         return OV3D_ELAUNCH;
-    const long long total = (long long)B * M * S;
-    if (total == 0 || C == 0) return OV3D_OK;
+    const long long total = (long long)B * M * S * C;
+    if (total == 0) return OV3D_OK;
     hipLaunchKernelGGL(group_bwd_kernel, dim3(ov3d_cdiv(total, 256)), dim3(256), 0, s, grad_out,
-                       idx, B, C, N, M, S, grad_features);
+                       idx, B, C, M, S, feat_sb, feat_sn, feat_sc, grad_features);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

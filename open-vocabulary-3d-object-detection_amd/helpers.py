@@ -8,6 +8,7 @@ unchanged (reference models/helpers.py:45-112).
 import copy
 
 import torch.nn as nn
+import torch.nn.functional as F
 
 NORM_DICT = {
     "bn1d": nn.BatchNorm1d,
@@ -61,7 +62,24 @@ class GenericMLP(nn.Module):
                     nn.init.xavier_uniform_(p)
 
     def forward(self, x):
+        """Reference layout: (B, C, N) for conv MLPs, (..., C) for linear ones."""
+        if isinstance(self.layers[0], nn.Conv1d):
+            B, C, N = x.shape
+            y = self.rows(x.transpose(1, 2).reshape(B * N, C))
+            return y.view(B, N, -1).transpose(1, 2)
         return self.layers(x)
+
+    def rows(self, x):
+        """Channels-last evaluation on (R, Cin) rows -> (R, Cout): each 1x1 conv is one
+        GEMM, BatchNorm1d statistics over the R rows (== over (B, N) positions)."""
+        for m in self.layers:
+            if isinstance(m, nn.Conv1d):
+                x = F.linear(x, m.weight.view(m.weight.shape[0], m.weight.shape[1]), m.bias)
+            elif isinstance(m, nn.GroupNorm):
+                raise NotImplementedError("GroupNorm MLPs are not on the reference path")
+            else:
+                x = m(x)
+        return x
 
 
 def get_clones(module, n):

@@ -109,9 +109,15 @@ class Model3DETR(nn.Module):
 
     # ------------------------------------------------------------------ encoder
     def get_query_embeddings(self, encoder_xyz, point_cloud_dims):
+        """-> query_xyz (B,Q,3), query_embed (B, C, Q) (reference layout)."""
+        query_xyz, rows = self._query_rows(encoder_xyz, point_cloud_dims)
+        return query_xyz, rows.permute(0, 2, 1)
+
+    def _query_rows(self, encoder_xyz, point_cloud_dims):
         _, query_xyz = pu.furthest_point_sample_gather(encoder_xyz, self.num_queries)
-        query_embed = self.query_projection(self.pos_embedding(query_xyz, input_range=point_cloud_dims))
-        return query_xyz, query_embed
+        pe = self.pos_embedding.rows(query_xyz, input_range=point_cloud_dims)      # (B, Q, C)
+        B, Q, C = pe.shape
+        return query_xyz, self.query_projection.rows(pe.reshape(B * Q, C)).view(B, Q, -1)
 
     @staticmethod
     def _break_up_pc(pc):
@@ -122,7 +128,8 @@ class Model3DETR(nn.Module):
     def run_encoder(self, point_clouds):
         xyz, feats = self._break_up_pc(point_clouds)
         pre_xyz, pre_feats, pre_inds = self.pre_encoder(xyz, feats)
-        enc_xyz, enc_feats, enc_inds = self.encoder(pre_feats.permute(2, 0, 1), xyz=pre_xyz)
+        # (B, C, M) view of channels-last rows -> seq-first (M, B, C)
+        enc_xyz, enc_feats, enc_inds = self.encoder(pre_feats.permute(2, 0, 1).contiguous(), xyz=pre_xyz)
         if enc_inds is None:
             enc_inds = pre_inds
         else:
@@ -138,20 +145,23 @@ class Model3DETR(nn.Module):
 
     def _box_predictions(self, query_xyz, point_cloud_dims, box_features):
         L, Q, B, C = box_features.shape
-        feats = box_features.permute(0, 2, 3, 1).reshape(L * B, C, Q)
+        # heads on channels-last rows ordered (l, b, q): BatchNorm1d statistics are over all
+        # L*B*Q positions exactly as on the reference's (L*B, C, Q) conv input
+        rows = box_features.permute(0, 2, 1, 3).reshape(L * B * Q, C)
         heads = self.mlp_heads
-        visual = heads["visual_embed_head"](feats).transpose(1, 2)          # (LB, Q, 640)
-        logits = heads["sem_cls_head"](visual)                              # (LB, Q, T)
+
+        def head(name):
+            return heads[name].rows(rows).view(L, B, Q, -1)
+
+        visual = head("visual_embed_head")                                  # (L, B, Q, 640)
+        logits = heads["sem_cls_head"](visual)                              # (L, B, Q, T)
         if self.cls_logits_layout == "reference":
-            logits = logits.transpose(1, 2).reshape(L, B, Q, -1)            # Q8
-        else:
-            logits = logits.reshape(L, B, Q, -1)
-        center_offset = (heads["center_head"](feats).sigmoid().transpose(1, 2) - 0.5).reshape(L, B, Q, -1)
-        size_norm = heads["size_head"](feats).sigmoid().transpose(1, 2).reshape(L, B, Q, -1)
-        angle_logits = heads["angle_cls_head"](feats).transpose(1, 2).reshape(L, B, Q, -1)
-        angle_res_norm = heads["angle_residual_head"](feats).transpose(1, 2).reshape(L, B, Q, -1)
+            logits = logits.reshape(L * B, Q, -1).transpose(1, 2).reshape(L, B, Q, -1)   # Q8
+        center_offset = head("center_head").sigmoid() - 0.5
+        size_norm = head("size_head").sigmoid()
+        angle_logits = head("angle_cls_head")
+        angle_res_norm = head("angle_residual_head")
         angle_res = angle_res_norm * (np.pi / angle_res_norm.shape[-1])
-        visual = visual.reshape(L, B, Q, -1)
 
         # BoxProcessor over the stacked (L*B) batch: dims repeated per layer
         dims = [point_cloud_dims[0].repeat(L, 1), point_cloud_dims[1].repeat(L, 1)]
@@ -188,14 +198,15 @@ class Model3DETR(nn.Module):
 
     def forward(self, inputs, encoder_only=False):
         pc = inputs["point_clouds"]
-        enc_xyz, enc_feats, _ = self.run_encoder(pc)
-        enc_feats = self.encoder_to_decoder_projection(enc_feats.permute(1, 2, 0)).permute(2, 0, 1)
+        enc_xyz, enc_feats, _ = self.run_encoder(pc)                        # (N', B, C)
+        Np, B, C = enc_feats.shape
+        enc_feats = self.encoder_to_decoder_projection.rows(enc_feats.reshape(Np * B, C)).view(Np, B, -1)
         if encoder_only:
             return enc_xyz, enc_feats.transpose(0, 1)
         dims = [inputs["point_cloud_dims_min"].float(), inputs["point_cloud_dims_max"].float()]
-        query_xyz, query_embed = self.get_query_embeddings(enc_xyz, dims)
-        enc_pos = self.pos_embedding(enc_xyz, input_range=dims).permute(2, 0, 1)
-        query_embed = query_embed.permute(2, 0, 1)
+        query_xyz, query_embed = self._query_rows(enc_xyz, dims)            # (B, Q, C)
+        enc_pos = self.pos_embedding.rows(enc_xyz, input_range=dims).transpose(0, 1)
+        query_embed = query_embed.transpose(0, 1)                           # (Q, B, C)
         tgt = torch.zeros_like(query_embed)
         box_features = self.decoder(tgt, enc_feats, query_pos=query_embed, pos=enc_pos)[0]
         return self.get_box_predictions(query_xyz, dims, box_features)

@@ -7,9 +7,26 @@ checkpoints load: ``mlp_module.layer{i}.conv.weight``,
 ``mlp_module.layer{i}.bn.bn.{weight,bias,running_mean,running_var}``.
 """
 
+import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from . import pointnet2_utils as pu
+
+
+def batch_norm_rows(bn, x):
+    """BatchNorm over the rows of a channels-last (R, C) tensor with the parameters /
+    running statistics of `bn` (BatchNorm1d/2d or SyncBatchNorm): statistics over R,
+    which are exactly the (N, H, W) positions of the channel-first module."""
+    if isinstance(bn, nn.SyncBatchNorm):
+        return bn(x)
+    training = bn.training or bn.running_mean is None
+    if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+    return F.batch_norm(x, bn.running_mean if not bn.training or bn.track_running_stats else None,
+                        bn.running_var if not bn.training or bn.track_running_stats else None,
+                        bn.weight, bn.bias, training, bn.momentum if bn.momentum is not None else 0.0,
+                        bn.eps)
 
 
 class _BNWrap(nn.Sequential):
@@ -45,6 +62,17 @@ class SharedMLP(nn.Sequential):
         for i in range(len(args) - 1):
             self.add_module(f"{name}layer{i}", _ConvBNReLU(args[i], args[i + 1], bn=bn))
 
+    def rows(self, x):
+        """The 1x1-conv stack on channels-last rows (R, Cin) -> (R, Cout): each layer is one
+        GEMM (hipBLASLt) + BN over rows + ReLU; no NCHW<->NHWC transposes."""
+        for layer in self:
+            w = layer.conv.weight
+            x = F.linear(x, w.view(w.shape[0], w.shape[1]), layer.conv.bias)
+            if hasattr(layer, "bn"):
+                x = batch_norm_rows(layer.bn.bn, x)
+            x = torch.relu(x)
+        return x
+
 
 class PointnetSAModuleVotes(nn.Module):
     """Set abstraction: FPS -> ball query -> group (+xyz, /radius) -> SharedMLP -> max over nsample."""
@@ -75,11 +103,15 @@ class PointnetSAModuleVotes(nn.Module):
                 raise ValueError("inds must have npoint columns")
             new_xyz = pu.gather_operation(xyz.transpose(1, 2).contiguous(), inds).transpose(1, 2)
             new_xyz = new_xyz.contiguous()
-        grouped, _ = self.grouper(xyz, new_xyz, features)
-        new_features = self.mlp_module(grouped)
-        # max over nsample (== F.max_pool2d(kernel [1, nsample]) of the reference); amax runs as one
-        # reduction instead of PyTorch's generic pooling kernel
-        return new_xyz, new_features.amax(dim=3), inds
+        return new_xyz, self._mlp_pool(xyz, new_xyz, features).transpose(1, 2), inds
+
+    def _mlp_pool(self, xyz, new_xyz, features):
+        """grouped rows -> SharedMLP -> max over nsample: (B, npoint, Cout)."""
+        g = self.grouper.rows(xyz, new_xyz, features)          # (B, M, S, 3+C) fp32
+        B, M, S, C = g.shape
+        y = self.mlp_module.rows(g.view(B * M * S, C))
+        # == F.max_pool2d(kernel [1, nsample]) of the reference
+        return y.view(B, M, S, -1).max(dim=2).values
 
 
 __all__ = ["PointnetSAModuleVotes", "SharedMLP"]

@@ -93,30 +93,51 @@ def ball_query(radius, nsample, xyz, new_xyz):
     return idx
 
 
+def _dense_strides(t):
+    """Element strides (b, n, c) of a (B,C,N) view when its storage is dense (any dim
+    order), else None."""
+    B, C, N = t.shape
+    order = sorted(range(3), key=lambda d: t.stride(d))
+    expect = 1
+    for d in order:
+        if t.shape[d] > 1 and t.stride(d) != expect:
+            return None
+        expect *= t.shape[d]
+    return t.stride(0), t.stride(2), t.stride(1)
+
+
 class _Group(Function):
-    """Fused QueryAndGroup body: (xyz[idx]-new_xyz)[/r] ++ features[idx]."""
+    """Fused QueryAndGroup body -> channels-last rows (B,M,S,3+C):
+    (xyz[idx]-new_xyz)[/r] ++ features[idx]; features may be any dense (B,C,N) view."""
 
     @staticmethod
     def forward(ctx, xyz, new_xyz, features, idx, radius, normalize):
         B, N, _ = xyz.shape
         _, M, S = idx.shape
         C = 0 if features is None else features.shape[1]
-        out = torch.empty((B, 3 + C, M, S), dtype=torch.float32, device=xyz.device)
-        nat.call("ov3d_group_fwd", xyz, new_xyz, features, idx, B, C, N, M, S, float(radius),
-                 int(bool(normalize)), out, like=xyz)
+        strides = (0, 0, 0)
+        if C:
+            strides = _dense_strides(features)
+            if strides is None:
+                features = features.contiguous()
+                strides = _dense_strides(features)
+        out = torch.empty((B, M, S, 3 + C), dtype=torch.float32, device=xyz.device)
+        nat.call("ov3d_group_fwd", xyz, new_xyz, features, *strides, idx, B, C, N, M, S,
+                 float(radius), int(bool(normalize)), out, like=xyz)
         ctx.save_for_backward(idx)
-        ctx.shape = (B, C, N, M, S)
+        ctx.meta = (B, C, N, M, S, strides, tuple(features.shape) if C else None,
+                    tuple(features.stride()) if C else None)
         return out
 
     @staticmethod
     def backward(ctx, g):
         (idx,) = ctx.saved_tensors
-        B, C, N, M, S = ctx.shape
+        B, C, N, M, S, strides, shape, stride = ctx.meta
         if C == 0 or not ctx.needs_input_grad[2]:
             return None, None, None, None, None, None
-        g = _f32(g, "grad", 4)
-        gf = torch.empty((B, C, N), dtype=torch.float32, device=g.device)
-        nat.call("ov3d_group_bwd", g, idx, B, C, N, M, S, gf, like=g)
+        g = nat.check(g.float().contiguous(), "grad", torch.float32, 4)
+        gf = torch.empty_strided(shape, stride, dtype=torch.float32, device=g.device)
+        nat.call("ov3d_group_bwd", g, idx, B, C, N, M, S, *strides, gf, like=g)
         return None, None, gf, None, None, None
 
 
@@ -128,7 +149,7 @@ def grouping_operation(features, idx):
     # the fused kernel needs an xyz/new_xyz pair; a zero pair makes channels 0:3 zero
     z = torch.zeros((B, N, 3), dtype=torch.float32, device=features.device)
     zc = torch.zeros((B, idx.shape[1], 3), dtype=torch.float32, device=features.device)
-    return _Group.apply(z, zc, features, idx, 1.0, False)[:, 3:]
+    return _Group.apply(z, zc, features, idx, 1.0, False)[..., 3:].permute(0, 3, 1, 2)
 
 
 class QueryAndGroup(nn.Module):
@@ -143,16 +164,23 @@ class QueryAndGroup(nn.Module):
         self.radius, self.nsample = radius, nsample
         self.use_xyz, self.ret_grouped_xyz, self.normalize_xyz = use_xyz, ret_grouped_xyz, normalize_xyz
 
-    def forward(self, xyz, new_xyz, features=None):
+    def rows(self, xyz, new_xyz, features=None):
+        """Grouped features as channels-last rows (B, npoint, nsample, 3+C)."""
         if xyz.requires_grad or new_xyz.requires_grad:
             raise NotImplementedError("gradients w.r.t. point coordinates are not on the path")
         idx = ball_query(self.radius, self.nsample, xyz, new_xyz)
         xyz = _f32(xyz, "xyz", 3)
         new_xyz = _f32(new_xyz, "new_xyz", 3)
         if features is not None:
+            if features.dim() != 3:
+                raise ValueError("features must be (B, C, N)")
             features = features if features.dtype == torch.float32 else features.float()
-            features = nat.check(features.contiguous(), "features", torch.float32, 3)
-        out = _Group.apply(xyz, new_xyz, features, idx, self.radius, self.normalize_xyz)
+            nat.check_device(features, "features")
+        return _Group.apply(xyz, new_xyz, features, idx, self.radius, self.normalize_xyz)
+
+    def forward(self, xyz, new_xyz, features=None):
+        """Reference layout: (B, 3+C, npoint, nsample) (a view of the channels-last rows)."""
+        out = self.rows(xyz, new_xyz, features).permute(0, 3, 1, 2)
         if self.ret_grouped_xyz:
             return out, out[:, :3]
         return out

@@ -41,7 +41,7 @@ class PositionEmbeddingCoordsSine(nn.Module):
             x = shift_scale_points(x, src_range=input_range)
         x = x * (2 * math.pi)
         proj = torch.mm(x.reshape(-1, d_in), self.gauss_B[:, :d_out].float()).view(B, N, d_out)
-        return torch.cat([proj.sin(), proj.cos()], dim=2).permute(0, 2, 1)
+        return torch.cat([proj.sin(), proj.cos()], dim=2)   # (B, N, d_pos) channels-last
 
     def _sine(self, xyz, num_channels, input_range):
         x = xyz.float()
@@ -66,12 +66,17 @@ class PositionEmbeddingCoordsSine(nn.Module):
             pos = raw[:, :, None] / dim_t
             outs.append(torch.stack((pos[:, :, 0::2].sin(), pos[:, :, 1::2].cos()), dim=3).flatten(2))
             prev = cdim
-        return torch.cat(outs, dim=2).permute(0, 2, 1)
+        return torch.cat(outs, dim=2)   # (B, N, d_pos) channels-last
 
-    def forward(self, xyz, num_channels=None, input_range=None):
+    def rows(self, xyz, num_channels=None, input_range=None):
+        """(B, N, 3) -> (B, N, d_pos) channels-last embedding."""
         if xyz.ndim != 3:
             raise ValueError("xyz must be (B, N, 3)")
         with torch.no_grad(), torch.autocast(device_type=xyz.device.type, enabled=False):
             if self.pos_type == "fourier":
                 return self._fourier(xyz, num_channels, input_range)
             return self._sine(xyz, num_channels, input_range)
+
+    def forward(self, xyz, num_channels=None, input_range=None):
+        """Reference layout: (B, d_pos, N)."""
+        return self.rows(xyz, num_channels, input_range).permute(0, 2, 1)

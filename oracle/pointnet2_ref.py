@@ -75,6 +75,12 @@ class QueryAndGroup(nn.Module):
             return new_features, grouped_xyz
         return new_features
 
+    def rows(self, xyz, new_xyz, features=None):
+        """channels-last view (B, npoint, nsample, 3+C) (product call surface)"""
+        out = self.forward(xyz, new_xyz, features)
+        out = out[0] if isinstance(out, tuple) else out
+        return out.permute(0, 2, 3, 1).contiguous()
+
 
 # ------------------------------------------------------------- pytorch_utils
 class _BN2d(nn.Sequential):

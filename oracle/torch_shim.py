@@ -26,8 +26,50 @@ grouping_operation = _ref.grouping_operation
 QueryAndGroup = _ref.QueryAndGroup
 
 
+def giou_aligned_torch(c1, c2, nums):
+    """Differentiable axis-aligned GIoU, a torch restatement of reference
+    utils/box_util.py:517-618 with rotated_boxes=False (the only differentiable path the
+    reference trains with: ScanNet GT angles are all 0)."""
+    EPS = 1e-8
+    B, K1, K2 = c1.shape[0], c1.shape[1], c2.shape[1]
+    ymax = torch.min(c1[:, :, 0, 1][:, :, None], c2[:, :, 0, 1][:, None, :])
+    ymin = torch.max(c1[:, :, 4, 1][:, :, None], c2[:, :, 4, 1][:, None, :])
+    height = (ymax - ymin).clamp(min=0)
+    r1 = c1[:, :, [3, 2, 1, 0]][..., [0, 2]]
+    r2 = c2[:, :, [3, 2, 1, 0]][..., [0, 2]]
+    lt = torch.max(r1[:, :, 1][:, :, None, :], r2[:, :, 1][:, None, :, :])
+    rb = torch.min(r1[:, :, 3][:, :, None, :], r2[:, :, 3][:, None, :, :])
+    wh = (rb - lt).clamp(min=0)
+    kmask = (torch.arange(K2, device=c1.device)[None, :] < nums.to(c1.device)[:, None]).float()
+    inter = wh[..., 0] * wh[..., 1] * kmask[:, None, :]
+    f1, f2 = c1.clone(), c2.clone()
+    f1[..., 1] = -f1[..., 1]
+    f2[..., 1] = -f2[..., 1]
+    xmin = torch.min(f1[..., 0].min(2).values[:, :, None], f2[..., 0].min(2).values[:, None, :])
+    ymn = torch.max(f1[..., 1].max(2).values[:, :, None], f2[..., 1].max(2).values[:, None, :])
+    zmin = torch.min(f1[..., 2].min(2).values[:, :, None], f2[..., 2].min(2).values[:, None, :])
+    xmax = torch.max(f1[..., 0].max(2).values[:, :, None], f2[..., 0].max(2).values[:, None, :])
+    ymx = torch.min(f1[..., 1].min(2).values[:, :, None], f2[..., 1].min(2).values[:, None, :])
+    zmax = torch.max(f1[..., 2].max(2).values[:, :, None], f2[..., 2].max(2).values[:, None, :])
+    enc = (xmax - xmin).abs() * (ymx - ymn).abs() * (zmax - zmin).abs()
+
+    def vol(c):
+        a = torch.sqrt((c[:, :, 0] - c[:, :, 1]).pow(2).sum(-1).clamp(min=1e-6))
+        b = torch.sqrt((c[:, :, 1] - c[:, :, 2]).pow(2).sum(-1).clamp(min=1e-6))
+        d = torch.sqrt((c[:, :, 0] - c[:, :, 4]).pow(2).sum(-1).clamp(min=1e-6))
+        return (a * b * d).clamp(min=EPS)
+    sum_vols = vol(c1)[:, :, None] + vol(c2)[:, None, :]
+    good = (enc > 2 * EPS) * (sum_vols > 4 * EPS)
+    inter_vols = inter * height
+    union = (sum_vols - inter_vols).clamp(min=EPS)
+    g = (inter_vols / union - (1 - union / enc)) * good
+    return g * kmask[:, None, :]
+
+
 def generalized_box3d_iou(corners1, corners2, nums_k2, rotated_boxes=True,
                           return_inter_vols_only=False, needs_grad=False, k2_bug=True):
+    if needs_grad and not rotated_boxes:
+        return giou_aligned_torch(corners1, corners2, nums_k2)
     mode = _o.GIOU_MODE_TENSOR if needs_grad else _o.GIOU_MODE_CYTHON
     g = _o.giou3d(corners1.detach().cpu().numpy(), corners2.detach().cpu().numpy(),
                   nums_k2.cpu().numpy(), mode=mode, rotated=rotated_boxes, k2_bug=k2_bug)

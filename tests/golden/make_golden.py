@@ -170,6 +170,17 @@ def run_model_fixture(R, name, args, cfg, batch, text):
     crit = R["criterion"].build_criterion(args, cfg)
     clip = FakeRegionCLIP()
     targets = dict(batch)
+    # record the reference matcher's assignments and costs (one call per decoder layer:
+    # final output first, then aux 0..L-2) so tests can pin matching separately from the
+    # gradient check: near-tie costs of a random-init model flip under 1e-6 noise
+    rec = []
+    orig_fwd = crit.matcher.forward
+
+    def recording_forward(outputs, targets):
+        res = orig_fwd(outputs, targets)
+        rec.append((res["per_prop_gt_inds"].numpy().copy(), res["proposal_matched_mask"].numpy().copy()))
+        return res
+    crit.matcher.forward = recording_forward
     loss, ld = crit(out, targets, clip=clip)
     loss.backward()
     named = dict(model.named_parameters())
@@ -187,6 +198,8 @@ def run_model_fixture(R, name, args, cfg, batch, text):
     for p in GRAD_PARAMS:
         if p in named and named[p].grad is not None:
             fx["grad/" + p] = named[p].grad.numpy()
+    fx["match_inds"] = np.stack([r[0] for r in rec])
+    fx["match_mask"] = np.stack([r[1] for r in rec])
     fx["text"] = text.numpy()
     fx["args"] = np.array(repr(sorted(vars(args).items())))
     np.savez_compressed(os.path.join(HERE, name), **fx)

@@ -53,3 +53,26 @@ def rel_err(a, b):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-12))
+
+
+def pin_matcher(crit, fx, device):
+    """Use the reference's recorded Hungarian assignments (fixture) instead of re-solving:
+    isolates gradient parity from near-tie flips of a random-init model's matching costs."""
+    L, B, Q = fx["match_inds"].shape
+    inds = torch.from_numpy(fx["match_inds"].reshape(L * B, Q)).to(device)
+    mask = torch.from_numpy(fx["match_mask"].reshape(L * B, Q)).to(device)
+    crit.matcher.forward = lambda cost, nact: {"assignments": [], "per_prop_gt_inds": inds,
+                                               "proposal_matched_mask": mask}
+    return crit
+
+
+# Gradient tolerance per parameter group.  The reference fixture model is random-init, so
+# many ReLU pre-activations sit at ~0; a 1e-5 relative change of the SA output (different
+# GEMM/BN accumulation order) flips a few ReLU masks in the encoder / projection and moves
+# those gradients by up to a few 1e-2 relative.  Parameters downstream of every ReLU
+# boundary that matters (last decoder layer, decoder norm, heads) are held to 1e-3; the
+# SA module's own backward is pinned separately on identical inputs
+# (test_sa_module_matches_reference_semantics).
+def grad_tol(name):
+    strict = ("decoder.layers.7.", "decoder.norm.", "mlp_heads.")
+    return 1e-3 if name.startswith(strict) else 5e-2
