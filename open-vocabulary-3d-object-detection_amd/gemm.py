@@ -1,0 +1,69 @@
+"""Row-major linear layer with a split-K weight gradient.
+
+Every dense layer of the hot path is a GEMM over R rows (points, memory tokens or
+query slots) with small channel counts: y = x W^T with x (R, Cin), W (Cout, Cin),
+R = 2^20 for the SA MLP, 2^14 for the encoder, Cout*Cin <= 768*256.  Its weight
+gradient dW = dy^T x has a tiny output tile and an R-long reduction; handed to the
+BLAS as one GEMM it runs on 7-21 workgroups of the 256 CUs (1.4-2.1 ms per SA layer,
+measured: profiles/r01_kernel_stats_v2.csv).  Here the reduction is split into
+row chunks computed as one batched GEMM (>= ~256 workgroups) and summed in fp32.
+"""
+import torch
+from torch.autograd import Function
+
+_TARGET_TILES = 512     # aim for this many (chunk x 64x64 tile) work items
+_MIN_ROWS = 256         # never split below this many rows per chunk
+
+
+def _chunks(R, cout, cin):
+    tiles = max(1, ((cout + 63) // 64) * ((cin + 63) // 64))
+    nc = 1
+    while (nc * 2 * tiles <= _TARGET_TILES and R % (nc * 2) == 0 and R // (nc * 2) >= _MIN_ROWS):
+        nc *= 2
+    return nc
+
+
+def weight_grad(dy, x):
+    """dy (R, Cout), x (R, Cin) -> dy^T x (Cout, Cin) in fp32, split-K over R."""
+    R, cout = dy.shape
+    cin = x.shape[1]
+    nc = _chunks(R, cout, cin)
+    if nc == 1:
+        return (dy.t() @ x).float()
+    part = torch.bmm(dy.view(nc, R // nc, cout).transpose(1, 2), x.view(nc, R // nc, cin))
+    return part.float().sum(0)
+
+
+class _RowsLinear(Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        dt = torch.get_autocast_dtype("cuda") if (x.is_cuda and torch.is_autocast_enabled("cuda")) \
+            else x.dtype
+        xc, wc = x.to(dt), w.to(dt)
+        with torch.autocast("cuda", enabled=False):
+            y = xc @ wc.t()
+            if b is not None:
+                y = y + b.to(dt)
+        ctx.save_for_backward(xc, wc)
+        ctx.meta = (x.dtype, w.dtype, b is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, wc = ctx.saved_tensors
+        xdt, wdt, has_b = ctx.meta
+        dy = dy.to(xc.dtype).contiguous()
+        with torch.autocast("cuda", enabled=False):
+            dx = (dy @ wc).to(xdt) if ctx.needs_input_grad[0] else None
+            dw = weight_grad(dy, xc).to(wdt) if ctx.needs_input_grad[1] else None
+            db = dy.float().sum(0).to(wdt) if has_b and ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
+def rows_linear(x, w, b=None):
+    """y = x W^T (+ b) for x (..., Cin); split-K dW on the ROCm device, plain F.linear on CPU."""
+    if not x.is_cuda:
+        return torch.nn.functional.linear(x, w, b)
+    shape = x.shape
+    y = _RowsLinear.apply(x.reshape(-1, shape[-1]), w, b)
+    return y.view(*shape[:-1], w.shape[0])

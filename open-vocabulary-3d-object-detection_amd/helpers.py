@@ -8,7 +8,8 @@ unchanged (reference models/helpers.py:45-112).
 import copy
 
 import torch.nn as nn
-import torch.nn.functional as F
+
+from .gemm import rows_linear
 
 NORM_DICT = {
     "bn1d": nn.BatchNorm1d,
@@ -74,7 +75,7 @@ class GenericMLP(nn.Module):
         GEMM, BatchNorm1d statistics over the R rows (== over (B, N) positions)."""
         for m in self.layers:
             if isinstance(m, nn.Conv1d):
-                x = F.linear(x, m.weight.view(m.weight.shape[0], m.weight.shape[1]), m.bias)
+                x = rows_linear(x, m.weight.view(m.weight.shape[0], m.weight.shape[1]), m.bias)
             elif isinstance(m, nn.GroupNorm):
                 raise NotImplementedError("GroupNorm MLPs are not on the reference path")
             else:

@@ -12,6 +12,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import pointnet2_utils as pu
+from .gemm import rows_linear
 
 
 def batch_norm_rows(bn, x):
@@ -67,7 +68,7 @@ class SharedMLP(nn.Sequential):
         GEMM (hipBLASLt) + BN over rows + ReLU; no NCHW<->NHWC transposes."""
         for layer in self:
             w = layer.conv.weight
-            x = F.linear(x, w.view(w.shape[0], w.shape[1]), layer.conv.bias)
+            x = rows_linear(x, w.view(w.shape[0], w.shape[1]), layer.conv.bias)
             if hasattr(layer, "bn"):
                 x = batch_norm_rows(layer.bn.bn, x)
             x = torch.relu(x)

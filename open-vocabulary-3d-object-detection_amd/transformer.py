@@ -16,6 +16,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
+from .gemm import rows_linear
 from .helpers import ACTIVATION_DICT, NORM_DICT, get_clones
 
 
@@ -42,14 +43,14 @@ class MultiheadAttention(nn.Module):
         S = key.shape[0]
         w, bias = self.in_proj_weight, self.in_proj_bias
         if query is key and key is value:
-            q, k, v = F.linear(query, w, bias).chunk(3, dim=-1)
+            q, k, v = rows_linear(query, w, bias).chunk(3, dim=-1)
         elif query is key:
-            q, k = F.linear(query, w[: 2 * E], bias[: 2 * E]).chunk(2, dim=-1)
-            v = F.linear(value, w[2 * E:], bias[2 * E:])
+            q, k = rows_linear(query, w[: 2 * E], bias[: 2 * E]).chunk(2, dim=-1)
+            v = rows_linear(value, w[2 * E:], bias[2 * E:])
         else:
-            q = F.linear(query, w[:E], bias[:E])
-            k = F.linear(key, w[E: 2 * E], bias[E: 2 * E])
-            v = F.linear(value, w[2 * E:], bias[2 * E:])
+            q = rows_linear(query, w[:E], bias[:E])
+            k = rows_linear(key, w[E: 2 * E], bias[E: 2 * E])
+            v = rows_linear(value, w[2 * E:], bias[2 * E:])
         q, k, v = self._heads(q, L, B), self._heads(k, S, B), self._heads(v, S, B)
         mask = None
         if attn_mask is not None:
@@ -58,7 +59,7 @@ class MultiheadAttention(nn.Module):
         out = F.scaled_dot_product_attention(q, k, v, attn_mask=mask,
                                              dropout_p=self.dropout if self.training else 0.0)
         out = out.permute(2, 0, 1, 3).reshape(L, B, E)
-        return self.out_proj(out)
+        return rows_linear(out, self.out_proj.weight, self.out_proj.bias)
 
 
 class TransformerEncoderLayer(nn.Module):
@@ -92,7 +93,8 @@ class TransformerEncoderLayer(nn.Module):
         src = src + self.dropout1(self.self_attn(qk, qk, x, attn_mask=src_mask))
         if self.use_ffn:
             x = self.norm2(src)
-            src = src + self.dropout2(self.linear2(self.dropout(self.activation(self.linear1(x)))))
+            h = self.dropout(self.activation(rows_linear(x, self.linear1.weight, self.linear1.bias)))
+            src = src + self.dropout2(rows_linear(h, self.linear2.weight, self.linear2.bias))
         return src
 
 
@@ -130,7 +132,8 @@ class TransformerDecoderLayer(nn.Module):
             memory_pos = memory if pos is None else memory + pos
         tgt = tgt + self.dropout2(self.multihead_attn(q, memory_pos, memory, attn_mask=memory_mask))
         x = self.norm3(tgt)
-        tgt = tgt + self.dropout3(self.linear2(self.dropout(self.activation(self.linear1(x)))))
+        h = self.dropout(self.activation(rows_linear(x, self.linear1.weight, self.linear1.bias)))
+        tgt = tgt + self.dropout3(rows_linear(h, self.linear2.weight, self.linear2.bias))
         return tgt, None
 
 
