@@ -11,8 +11,8 @@ nqueries=128, text embedding 21x640) already resident in HBM.  BASELINE.json
 metric: scenes/sec (train step); weak scaling (8 scenes per GPU), DDP over RCCL.
 
 Rank 0 prints ONE JSON line.  It carries a `roofline` object for the dominant
-hand-written kernel (ov3d_fps, timed with HIP events on its own stream inside
-the timed region) and a `cpu_baseline` (the CPU port of the same step: the
+hand-written kernel (ov3d_fps, timed with HIP events on its launch stream; inside
+the timed region in eager mode, right after it when the step replays hipGraphs) and a `cpu_baseline` (the CPU port of the same step: the
 oracle's C restatement for the index kernels + PyTorch-CPU dense layers, a
 bounded sample, rank 0 only, N=1 only).
 """
@@ -73,16 +73,29 @@ def build(args, device, ddp=False):
     return model, crit, opt
 
 
-def train_step(model, crit, opt, batch, args, amp_dtype):
+def train_step(model, crit, opt, batch, args, amp_dtype, graphed=None):
     opt.zero_grad(set_to_none=True)
     inputs = {k: batch[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")}
-    with torch.autocast("cuda", dtype=amp_dtype, enabled=amp_dtype is not None):
-        out = model(inputs)
+    if graphed is not None:
+        out = graphed(inputs)          # replays the captured forward (and, in backward, backward)
+    else:
+        with torch.autocast("cuda", dtype=amp_dtype, enabled=amp_dtype is not None):
+            out = model(inputs)
     loss, _ = crit(out, batch)
     loss.backward()
     torch.nn.utils.clip_grad_norm_(model.parameters(), args.clip_gradient)
     opt.step()
     return loss
+
+
+def fps_launch_timings(pool, cli, reps=5):
+    """Inside graph replays the kernel is not reachable by host events; time the same launch
+    (pre-encoder FPS on the step's batch, same stream) right after the timed region."""
+    from ov3d_amd import _native, pointnet2_utils as pu
+    _native.timing_enable(["ov3d_fps"])
+    for i in range(reps):
+        pu.furthest_point_sample_gather(pool[i % len(pool)]["point_clouds"], 2048)
+    return _native.timing_collect()
 
 
 def cpu_baseline(args, batch_size=1, steps=2):
@@ -138,6 +151,7 @@ def main():
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled")
+    p.add_argument("--no-graph", action="store_true", help="eager forward/backward (no hipGraph)")
     cli = p.parse_args()
 
     ov3d = ov3d_import.load()
@@ -151,21 +165,26 @@ def main():
     pool = [synthetic.make_batch(cli.batch, seed=1000 * rank + i, num_points=cli.points, device=device)
             for i in range(cli.pool)]
 
+    graphed = None
+    if world == 1 and not cli.no_graph:
+        from ov3d_amd.graphs import GraphedModel
+        graphed = GraphedModel(model, pool[0], amp_dtype=amp)
     for i in range(cli.warmup):
-        train_step(model, crit, opt, pool[i % cli.pool], args, amp)
+        train_step(model, crit, opt, pool[i % cli.pool], args, amp, graphed)
     torch.cuda.synchronize()
     dist.barrier()
 
-    _native.timing_enable(["ov3d_fps"])
+    if graphed is None:
+        _native.timing_enable(["ov3d_fps"])
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
     for i in range(cli.steps):
-        loss = train_step(model, crit, opt, pool[i % cli.pool], args, amp)
+        loss = train_step(model, crit, opt, pool[i % cli.pool], args, amp, graphed)
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
-    timings = _native.timing_collect()
+    timings = _native.timing_collect() if graphed is None else fps_launch_timings(pool, cli)
     el = torch.tensor([elapsed], device=device, dtype=torch.float64)
     if world > 1:
         torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)

@@ -134,7 +134,8 @@ class SetCriterion(nn.Module):
                                       k2_bug=self.giou_k2_bug)
         center_norm = cat("center_normalized").float()
         gt_centers = rep(targets["gt_box_centers_normalized"]).float()
-        center_dist = torch.cdist(center_norm, gt_centers, p=1)
+        # == torch.cdist(p=1) (criterion.py:357-360) as one broadcast kernel chain
+        center_dist = (center_norm[:, :, None, :] - gt_centers[:, None, :, :]).abs().sum(-1)
         gt_labels = rep(targets["gt_box_sem_cls_label"])
         cost = self.matcher.cost(cat("sem_cls_prob").float(), cat("objectness_prob").float(),
                                  center_dist, gious, gt_labels)

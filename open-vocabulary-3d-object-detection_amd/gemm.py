@@ -31,7 +31,7 @@ def weight_grad(dy, x):
     if nc == 1:
         return (dy.t() @ x).float()
     part = torch.bmm(dy.view(nc, R // nc, cout).transpose(1, 2), x.view(nc, R // nc, cin))
-    return part.float().sum(0)
+    return torch.sum(part, dim=0, dtype=torch.float32)
 
 
 class _RowsLinear(Function):
@@ -56,7 +56,8 @@ class _RowsLinear(Function):
         with torch.autocast("cuda", enabled=False):
             dx = (dy @ wc).to(xdt) if ctx.needs_input_grad[0] else None
             dw = weight_grad(dy, xc).to(wdt) if ctx.needs_input_grad[1] else None
-            db = dy.float().sum(0).to(wdt) if has_b and ctx.needs_input_grad[2] else None
+            db = torch.sum(dy, dim=0, dtype=torch.float32).to(wdt) \
+                if has_b and ctx.needs_input_grad[2] else None
         return dx, dw, db
 
 

@@ -73,3 +73,35 @@ def test_full_size_train_step_properties(cuda):
     d = ((batch["point_clouds"][torch.arange(8, device=cuda)[:, None, None], bq.long()] - nx[:, :, None]) ** 2).sum(-1)
     assert (d < 0.2 ** 2 + 1e-6).all()
     assert (bq[..., 1:] >= bq[..., :1]).all()   # padded with the first hit, ascending
+
+
+def test_graphed_step_equals_eager(cuda):
+    """hipGraph replay of forward+backward gives the eager results (dropout off)."""
+    import copy
+    import ov3d_amd
+    from ov3d_amd import synthetic
+    from ov3d_amd.dataset_config import SunrgbdDatasetConfig
+    from ov3d_amd.graphs import GraphedModel
+    from bench import default_args
+    args = default_args(enc_dropout=0.0, dec_dropout=0.0, mlp_dropout=0.0, preenc_npoints=512,
+                        nqueries=64)
+    cfg = SunrgbdDatasetConfig()
+    torch.manual_seed(0)
+    model, _ = ov3d_amd.build_model(args, cfg, text_embedding=synthetic.text_embedding())
+    model = model.to(cuda).train()
+    twin = copy.deepcopy(model)
+    crit = ov3d_amd.build_criterion(args, cfg).to(cuda)
+    batch = synthetic.make_batch(2, seed=4, num_points=4096, device=cuda)
+    inputs = {k: batch[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")}
+    graphed = GraphedModel(twin, batch, amp_dtype=None, warmup_iters=1)
+    # warm-up iterations ran the BN updates on `twin`: align the eager model's buffers
+    model.load_state_dict(twin.state_dict())
+    loss_e, _ = crit(model(inputs), dict(batch))
+    loss_e.backward()
+    loss_g, _ = crit(graphed(inputs), dict(batch))
+    loss_g.backward()
+    assert abs(loss_e.item() - loss_g.item()) <= 1e-5 * abs(loss_e.item())
+    ge = dict(model.named_parameters())
+    for n, p in twin.named_parameters():
+        if p.grad is not None:
+            torch.testing.assert_close(p.grad, ge[n].grad, rtol=1e-4, atol=1e-6)
