@@ -33,6 +33,18 @@ def flip_axis_to_camera_np(pc):
 _SX = (1, 1, -1, -1, 1, 1, -1, -1)
 _SY = (1, 1, 1, 1, -1, -1, -1, -1)
 _SZ = (1, -1, -1, 1, 1, -1, -1, 1)
+_SIGN_CACHE = {}
+
+
+def _corner_signs(dtype, device):
+    """(3, 8) sign table, one device copy per (dtype, device): no H2D copy per call, so the
+    forward stays capturable in a hipGraph."""
+    key = (dtype, device)
+    t = _SIGN_CACHE.get(key)
+    if t is None:
+        t = torch.tensor((_SX, _SY, _SZ), dtype=dtype, device=device)
+        _SIGN_CACHE[key] = t
+    return t
 
 
 def get_3d_box_batch_tensor(box_size, angle, center):
@@ -42,9 +54,7 @@ def get_3d_box_batch_tensor(box_size, angle, center):
     l = box_size[..., 0:1] / 2
     w = box_size[..., 1:2] / 2
     h = box_size[..., 2:3] / 2
-    sx = torch.tensor(_SX, dtype=box_size.dtype, device=box_size.device)
-    sy = torch.tensor(_SY, dtype=box_size.dtype, device=box_size.device)
-    sz = torch.tensor(_SZ, dtype=box_size.dtype, device=box_size.device)
+    sx, sy, sz = _corner_signs(box_size.dtype, box_size.device)
     lx, ly, lz = l * sx, h * sy, w * sz
     c = torch.cos(angle)[..., None]
     s = torch.sin(angle)[..., None]
