@@ -1,0 +1,147 @@
+"""Data-parallel path on CPU: world_size 2 over gloo (the GPU path is the same code on
+RCCL).  Covers the reference utils/dist.py API mirror and one DDP training step whose
+averaged gradients must equal the single-process gradients on the whole batch
+(the reference's num_boxes all-reduce, criterion.py:425, makes the box-normalised
+losses batch-split invariant)."""
+import json
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from helpers import ROOT, batch_from_fixture, build_model_from_fixture, fixture, ov3d, rel_err
+
+WORLD = 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _init(rank, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(WORLD), LOCAL_RANK=str(rank))
+    from ov3d_amd import dist
+    r, w, _ = dist.init_from_env(backend="gloo")
+    assert (r, w) == (rank, WORLD)
+    return dist
+
+
+def _collectives(rank, port, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    import ov3d_import
+    ov3d_import.load()
+    dist = _init(rank, port)
+    res = {}
+    res["sum"] = dist.all_reduce_sum(torch.tensor(float(rank + 1))).item()
+    res["avg"] = dist.all_reduce_average(torch.tensor([2.0 * rank, 4.0])).tolist()
+    co = dist.all_reduce_coalesced([torch.tensor(1.0 + rank), torch.full((2, 2), 3.0 * rank)])
+    res["co0"] = co[0].item()
+    res["co1"] = co[1].tolist()
+    rd = dist.reduce_dict({"b": torch.tensor(float(rank)), "a": torch.tensor(10.0 * rank)})
+    res["rd"] = {k: v.item() for k, v in rd.items()}
+    res["gather"] = dist.all_gather_pickle({"rank": rank, "pay": "x" * (5 + 100 * rank)}, "cpu")
+    res["gdict"] = dist.all_gather_dict({"t": torch.full((1, 3), float(rank))})["t"].tolist()
+    with open(os.path.join(out_dir, f"coll{rank}.json"), "w") as f:
+        json.dump(res, f)
+    dist.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_collectives_world2():
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_collectives, args=(_free_port(), d), nprocs=WORLD, join=True)
+        for rank in range(WORLD):
+            with open(os.path.join(d, f"coll{rank}.json")) as f:
+                r = json.load(f)
+            assert r["sum"] == 3.0
+            assert r["avg"] == [1.0, 4.0]
+            assert r["co0"] == 1.5 and r["co1"] == [[1.5, 1.5], [1.5, 1.5]]
+            assert r["rd"] == {"a": 5.0, "b": 0.5}
+            assert [g["rank"] for g in r["gather"]] == [0, 1]
+            assert len(r["gather"][1]["pay"]) == 105
+            assert r["gdict"] == [[0.0] * 3, [1.0] * 3]
+
+
+def _step(model, crit, batch):
+    out = model({k: batch[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")})
+    loss, ld = crit(out, batch)
+    loss.backward()
+    return loss
+
+
+def _ddp_rank(rank, port, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    torch.set_num_threads(2)
+    from oracle import torch_shim
+    from helpers import batch_from_fixture as bff, build_model_from_fixture as bmf, fixture as fxl, ov3d as pkg
+    _init(rank, port)
+    torch_shim.install(pkg)
+    from ov3d_amd.criterion import build_criterion
+    fx = fxl("model_sun.npz")
+    model, cfg, args = bmf(fx, "cpu", "sunrgbd")
+    args.loss_2dalignment_weight = 0.0
+    model.eval()     # running-stat BN, no dropout: per-scene independent forward
+    ddp = torch.nn.parallel.DistributedDataParallel(model)
+    crit = build_criterion(args, cfg)
+    batch = {k: v[rank: rank + 1] for k, v in bff(fx, "cpu").items()}
+    loss = _step(ddp, crit, batch)
+    grads = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+    torch.save({"loss": loss.detach(), "grads": grads}, os.path.join(out_dir, f"ddp{rank}.pt"))
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+@pytest.fixture()
+def shim():
+    from oracle import torch_shim
+    saved = torch_shim.install(ov3d)
+    yield
+    torch_shim.uninstall(saved)
+
+
+def test_ddp_gradients_equal_rank_average(shim, monkeypatch):
+    """DDP step == the mean of the per-scene gradients, each computed with the GLOBAL
+    average num_boxes (what criterion.py:425's all_reduce_average yields on every rank).
+    Other loss terms are per-rank means (reference semantics), so the comparison target
+    is the rank average, not a single whole-batch step."""
+    from ov3d_amd import criterion as crit_mod
+    torch.set_num_threads(4)
+    fx = fixture("model_sun.npz")
+    full = batch_from_fixture(fx, "cpu")
+    nbox = full["gt_box_present"].sum(dim=1)
+    monkeypatch.setattr(crit_mod, "all_reduce_average", lambda t: nbox.sum() / WORLD)
+    ref, losses = {}, []
+    for r in range(WORLD):
+        model, cfg, args = build_model_from_fixture(fx, "cpu", "sunrgbd")
+        args.loss_2dalignment_weight = 0.0
+        model.eval()
+        crit = crit_mod.build_criterion(args, cfg)
+        losses.append(_step(model, crit, {k: v[r: r + 1] for k, v in full.items()}).item())
+        for n, p in model.named_parameters():
+            if p.grad is not None:
+                ref[n] = ref.get(n, 0) + p.grad / WORLD
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_ddp_rank, args=(_free_port(), d), nprocs=WORLD, join=True)
+        res = [torch.load(os.path.join(d, f"ddp{r}.pt"), weights_only=True) for r in range(WORLD)]
+    assert set(res[0]["grads"]) == set(ref)
+    checked = 0
+    for n, g in ref.items():
+        g0, g1 = res[0]["grads"][n], res[1]["grads"][n]
+        assert torch.equal(g0, g1), n          # DDP leaves identical gradients on every rank
+        if g.abs().max() > 1e-8:
+            assert rel_err(g0.numpy(), g.numpy()) < 1e-4, n
+            checked += 1
+    assert checked > 50
+    for r in range(WORLD):
+        assert abs(res[r]["loss"].item() - losses[r]) <= 1e-5 * abs(losses[r])
