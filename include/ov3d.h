@@ -83,18 +83,34 @@ int ov3d_gather_bwd(const float* grad_out, const int32_t* idx, int B, int C, int
  *   mode OV3D_GIOU_TENSOR (1): generalized_box3d_iou_tensor (box_util.py:517-618),
  *        float32 clipping, all k2 < nums[b].
  *   rotated == 0: axis-aligned (x,z) rectangle intersection (box_util.py:695-696).
+ * rotated_dev: optional DEVICE int32 flag that overrides `rotated` when non-NULL
+ *   (the reference decides rotated = any(gt_box_angles > 0) on the host,
+ *   criterion.py:317-330; reading it on the device keeps the step sync-free).
  * nums (B,) int32 = number of valid GT boxes per scene, or NULL (= K2).
  * out (B,K1,K2) f32. */
 #define OV3D_GIOU_CYTHON 0
 #define OV3D_GIOU_TENSOR 1
 int ov3d_giou3d(const float* corners1, const float* corners2, const int32_t* nums, int B, int K1,
-                int K2, int mode, int rotated, int k2_bug, float* out, void* stream);
+                int K2, int mode, int rotated, const int32_t* rotated_dev, int k2_bug, float* out,
+                void* stream);
 
 /* Backward of the axis-aligned (rotated == 0) GIoU w.r.t. corners1:
  * grad_out (B,K1,K2) -> grad_corners1 (B,K1,8,3) (overwritten). */
 int ov3d_giou3d_bwd_aligned(const float* corners1, const float* corners2, const int32_t* nums,
                             int B, int K1, int K2, const float* grad_out, float* grad_corners1,
                             void* stream);
+
+/* Hungarian matching for a stack of P problems, one workgroup each.
+ * Replaces the host loop of criterion.py:77-86 (scipy.optimize.linear_sum_assignment
+ * on final_cost[b, :, :nactual_gt[b]]) with scipy 1.15's algorithm restated
+ * exactly (Crouse shortest augmenting path, float64 path costs, the same
+ * tie rule), so assignments are identical to scipy's for the same costs.
+ *   cost (P,Q,G) f32, nactual (P,) int32 (columns 0..nactual-1 are used)
+ *   -> gt_inds (P,Q) int64 (0 where unmatched), matched (P,Q) f32 (1/0),
+ *      status (P,) int32 or NULL: 0 ok, -1 NaN/-inf cost (scipy raises
+ *      ValueError), -2 infeasible.  Q and G <= 1024. */
+int ov3d_hungarian(const float* cost, const int32_t* nactual, int P, int Q, int G, int64_t* gt_inds,
+                   float* matched, int32_t* status, void* stream);
 
 /* Greedy 3D NMS, batched over scenes.  Replaces utils/nms.py:79-162
  * (nms_3d_faster / nms_3d_faster_samecls) as called per scene by

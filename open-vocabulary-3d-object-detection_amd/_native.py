@@ -27,8 +27,9 @@ _SIGS = {
     "ov3d_group_bwd": "ppiiiiilllpp",
     "ov3d_gather_fwd": "ppiiiipp",
     "ov3d_gather_bwd": "ppiiiipp",
-    "ov3d_giou3d": "pppiiiiiipp",
+    "ov3d_giou3d": "pppiiiiipipp",
     "ov3d_giou3d_bwd_aligned": "pppiiippp",
+    "ov3d_hungarian": "ppiiippp",
     "ov3d_nms3d": "ppiiidiipp",
     "ov3d_nms_boxes_from_corners": "pppiipp",
 }

@@ -101,11 +101,17 @@ def _prep(corners1, corners2, nums_k2):
 
 
 def giou3d_raw(corners1, corners2, nums_k2, mode, rotated, k2_bug=True):
+    """rotated: bool, or a device int32 scalar tensor read by the kernel (no host sync)."""
     c1, c2, nums = _prep(corners1, corners2, nums_k2)
     B, K1 = c1.shape[:2]
     K2 = c2.shape[1]
     out = torch.empty((B, K1, K2), dtype=torch.float32, device=c1.device)
-    nat.call("ov3d_giou3d", c1, c2, nums, B, K1, K2, int(mode), int(bool(rotated)),
+    flag = None
+    if isinstance(rotated, torch.Tensor):
+        flag = nat.check(rotated.to(device=c1.device, dtype=torch.int32).reshape(1).contiguous(),
+                         "rotated", torch.int32, 1)
+        rotated = False
+    nat.call("ov3d_giou3d", c1, c2, nums, B, K1, K2, int(mode), int(bool(rotated)), flag,
              int(bool(k2_bug)), out, like=c1)
     return out
 
@@ -131,10 +137,14 @@ class _GIoUAligned(Function):
 
 def generalized_box3d_iou(corners1, corners2, nums_k2, rotated_boxes=True,
                           return_inter_vols_only=False, needs_grad=False, k2_bug=True):
-    """(B,K1,8,3), (B,K2,8,3), (B,) -> (B,K1,K2) generalized IoU."""
+    """(B,K1,8,3), (B,K2,8,3), (B,) -> (B,K1,K2) generalized IoU.
+
+    rotated_boxes may be a device flag tensor (criterion: any(gt_box_angles > 0))."""
     if return_inter_vols_only:
         raise NotImplementedError("return_inter_vols_only is not on the training path")
     if needs_grad:
+        if isinstance(rotated_boxes, torch.Tensor):
+            rotated_boxes = bool(rotated_boxes.item())    # host sync: ScanNet-style GIoU loss only
         if rotated_boxes:
             raise NotImplementedError(
                 "differentiable rotated GIoU (loss_giou_weight > 0 with rotated GT) is not "

@@ -11,9 +11,9 @@ values, total = sum over layers.
 Restructured for the device (results equal per layer):
   * one GIoU launch for all L decoder layers (the reference runs the Cython
     kernel 8x on the host after a device->host copy each time);
-  * one cost-matrix device->host copy for all L x B Hungarian problems
-    (scipy ``linear_sum_assignment`` on the first nactual columns, exactly as
-    criterion.py:76-86) and one host->device copy of the assignments;
+  * one device Hungarian launch for all L x B problems (ov3d_hungarian: scipy's
+    ``linear_sum_assignment`` algorithm and tie rule on the first nactual columns,
+    criterion.py:76-86) — no device->host copy, no synchronisation in the step;
   * the per-layer losses are computed as (L*B, Q) tensors and reduced per layer;
   * the RegionCLIP call (criterion.py:379-398) only runs when
     loss_2dalignment_weight > 0: the reference calls it unconditionally but only
@@ -24,8 +24,8 @@ import numpy as np
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
-from scipy.optimize import linear_sum_assignment
 
+from .assignment import Assignments, hungarian
 from .box_util import generalized_box3d_iou
 from .dist import all_reduce_average
 from .image_util import clip_batch, project_boxes_2d
@@ -62,25 +62,11 @@ class Matcher(nn.Module):
 
     @torch.no_grad()
     def forward(self, cost, nactual):
-        """cost (P,Q,G) device tensor, nactual list[int] (len P) -> inds (P,Q) int64, mask (P,Q) f32"""
-        P, Q, _ = cost.shape
-        dev = cost.device
-        c = cost.float().cpu().numpy()
-        inds = np.zeros((P, Q), dtype=np.int64)
-        mask = np.zeros((P, Q), dtype=np.float32)
-        assignments = []
-        for p in range(P):
-            n = int(nactual[p])
-            if n > 0:
-                r, col = linear_sum_assignment(c[p, :, :n])
-                inds[p, r] = col
-                mask[p, r] = 1
-                assignments.append((r, col))
-            else:
-                assignments.append(())
-        return {"assignments": assignments,
-                "per_prop_gt_inds": torch.from_numpy(inds).to(dev, non_blocking=True),
-                "proposal_matched_mask": torch.from_numpy(mask).to(dev, non_blocking=True)}
+        """cost (P,Q,G) device tensor, nactual (P,) int device tensor (or list)
+        -> per_prop_gt_inds (P,Q) int64, proposal_matched_mask (P,Q) f32, on the device."""
+        inds, mask, status = hungarian(cost, nactual)
+        return {"assignments": Assignments(inds, mask), "per_prop_gt_inds": inds,
+                "proposal_matched_mask": mask, "status": status}
 
 
 class SetCriterion(nn.Module):
@@ -107,18 +93,14 @@ class SetCriterion(nn.Module):
         L = len(layers)
         present = targets["gt_box_present"]
         nactual_gt = present.sum(axis=1).long()
-        tot = all_reduce_average(nactual_gt.sum())
-        angles = targets["gt_box_angles"]
-        # one host sync for all data-dependent scalars
-        stats = torch.cat([torch.stack([tot.float(), (angles > 0).any().float()]),
-                           nactual_gt.float()]).tolist()
-        num_boxes = max(stats[0], 1.0)
-        rotated = bool(stats[1])
-        nact = [int(v) for v in stats[2:]]
-        num_boxes_replica = sum(nact)
+        # No host synchronisation in the step: num_boxes stays a device scalar, the
+        # rotated switch (criterion.py:317-330, Q2) is a device flag read by the GIoU
+        # kernel, and the matcher runs on the device.
+        num_boxes = torch.clamp(all_reduce_average(nactual_gt.sum()), min=1)
+        rotated = (targets["gt_box_angles"] > 0).any().to(torch.int32)
         targets["nactual_gt"] = nactual_gt
         targets["num_boxes"] = num_boxes
-        targets["num_boxes_replica"] = num_boxes_replica
+        targets["num_boxes_replica"] = nactual_gt.sum()
 
         def cat(key):
             return torch.cat([o[key] for o in layers], dim=0)    # (L*B, ...)
@@ -139,7 +121,7 @@ class SetCriterion(nn.Module):
         gt_labels = rep(targets["gt_box_sem_cls_label"])
         cost = self.matcher.cost(cat("sem_cls_prob").float(), cat("objectness_prob").float(),
                                  center_dist, gious, gt_labels)
-        asg = self.matcher(cost, nact * L)
+        asg = self.matcher(cost, rep(nactual_gt))
         inds, mask = asg["per_prop_gt_inds"], asg["proposal_matched_mask"]
 
         per = {}  # key -> (L,) tensor of unweighted per-layer losses
@@ -151,31 +133,28 @@ class SetCriterion(nn.Module):
             nll = F.cross_entropy(logits.transpose(2, 1), lab, reduction="none")   # (LB,Q)
             wt = self.semcls_percls_weights[lab]
             per["loss_sem_cls"] = (nll * wt).view(L, -1).sum(1) / wt.view(L, -1).sum(1)
-        if num_boxes_replica > 0:
-            # reference key "loss_angle" has no weight entry -> always computed
-            nb = self.dataset_config.num_angle_bin
-            a_logits = cat("angle_logits").float()
-            a_res = cat("angle_residual_normalized").float()
-            gl = torch.gather(rep(targets["gt_angle_class_label"]), 1, inds)
-            gr = torch.gather(rep(targets["gt_angle_residual_label"]).float() / (np.pi / nb), 1, inds)
-            ce = F.cross_entropy(a_logits.transpose(2, 1), gl, reduction="none")
-            per["loss_angle_cls"] = (ce * mask).view(L, -1).sum(1) / num_boxes
-            res_gt_cls = torch.gather(a_res, 2, gl.unsqueeze(-1)).squeeze(-1)
-            hub = huber_loss(res_gt_cls - gr, delta=1.0)
-            per["loss_angle_reg"] = (hub * mask).view(L, -1).sum(1) / num_boxes
-            if self._computed("loss_center"):
-                cl = torch.gather(center_dist, 2, inds.unsqueeze(-1)).squeeze(-1)
-                per["loss_center"] = (cl * mask).view(L, -1).sum(1) / num_boxes
-            if self._computed("loss_size"):
-                gs = rep(targets["gt_box_sizes_normalized"]).float()
-                gsz = torch.gather(gs, 1, inds.unsqueeze(-1).expand(-1, -1, gs.shape[-1]))
-                sl = F.l1_loss(cat("size_normalized").float(), gsz, reduction="none").sum(-1)
-                per["loss_size"] = (sl * mask).view(L, -1).sum(1) / num_boxes
-        else:
-            z = torch.zeros(L, device=present.device)
-            for k in ("loss_angle_cls", "loss_angle_reg", "loss_center", "loss_size"):
-                if k.startswith("loss_angle") or self._computed(k):
-                    per[k] = z
+        # The reference computes these only when the replica has GT boxes
+        # (criterion.py:184, 250) and reports zeros otherwise; with no boxes every
+        # proposal is unmatched, so the masked sums below are exactly 0 as well.
+        # reference key "loss_angle" has no weight entry -> always computed
+        nb = self.dataset_config.num_angle_bin
+        a_logits = cat("angle_logits").float()
+        a_res = cat("angle_residual_normalized").float()
+        gl = torch.gather(rep(targets["gt_angle_class_label"]), 1, inds)
+        gr = torch.gather(rep(targets["gt_angle_residual_label"]).float() / (np.pi / nb), 1, inds)
+        ce = F.cross_entropy(a_logits.transpose(2, 1), gl, reduction="none")
+        per["loss_angle_cls"] = (ce * mask).view(L, -1).sum(1) / num_boxes
+        res_gt_cls = torch.gather(a_res, 2, gl.unsqueeze(-1)).squeeze(-1)
+        hub = huber_loss(res_gt_cls - gr, delta=1.0)
+        per["loss_angle_reg"] = (hub * mask).view(L, -1).sum(1) / num_boxes
+        if self._computed("loss_center"):
+            cl = torch.gather(center_dist, 2, inds.unsqueeze(-1)).squeeze(-1)
+            per["loss_center"] = (cl * mask).view(L, -1).sum(1) / num_boxes
+        if self._computed("loss_size"):
+            gs = rep(targets["gt_box_sizes_normalized"]).float()
+            gsz = torch.gather(gs, 1, inds.unsqueeze(-1).expand(-1, -1, gs.shape[-1]))
+            sl = F.l1_loss(cat("size_normalized").float(), gsz, reduction="none").sum(-1)
+            per["loss_size"] = (sl * mask).view(L, -1).sum(1) / num_boxes
         if self._computed("loss_giou"):
             gl = torch.gather(1 - gious, 2, inds.unsqueeze(-1)).squeeze(-1)
             per["loss_giou"] = (gl * mask).view(L, -1).sum(1) / num_boxes

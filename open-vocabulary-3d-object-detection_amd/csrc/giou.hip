@@ -100,8 +100,10 @@ __device__ __forceinline__ void minmax_flip(const float* c, float* mn, float* mx
 __global__ __launch_bounds__(256) void giou_kernel(const float* __restrict__ corners1,
                                                    const float* __restrict__ corners2,
                                                    const int32_t* __restrict__ nums, int B, int K1,
-                                                   int K2, int mode, int rotated, int k2_bug,
-                                                   float* __restrict__ out) {
+                                                   int K2, int mode, int rotated_host,
+                                                   const int32_t* __restrict__ rotated_dev,
+                                                   int k2_bug, float* __restrict__ out) {
+    const int rotated = rotated_dev ? (*rotated_dev != 0) : rotated_host;
     const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (long long)B * K1 * K2) return;
     const int k2 = (int)(t % K2);
@@ -331,14 +333,14 @@ __global__ __launch_bounds__(128) void giou_bwd_aligned_kernel(
 }  // namespace
 
 extern "C" int ov3d_giou3d(const float* corners1, const float* corners2, const int32_t* nums, int B,
-                           int K1, int K2, int mode, int rotated, int k2_bug, float* out,
-                           void* stream) {
+                           int K1, int K2, int mode, int rotated, const int32_t* rotated_dev,
+                           int k2_bug, float* out, void* stream) {
     if (B < 0 || K1 < 0 || K2 < 0 || !corners1 || !corners2 || !out) return OV3D_EINVAL;
     if (mode != OV3D_GIOU_CYTHON && mode != OV3D_GIOU_TENSOR) return OV3D_EINVAL;
     const long long total = (long long)B * K1 * K2;
     if (total == 0) return OV3D_OK;
     hipLaunchKernelGGL(giou_kernel, dim3(ov3d_cdiv(total, 256)), dim3(256), 0, ov3d_stream(stream),
-                       corners1, corners2, nums, B, K1, K2, mode, rotated, k2_bug, out);
+                       corners1, corners2, nums, B, K1, K2, mode, rotated, rotated_dev, k2_bug, out);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

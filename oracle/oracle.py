@@ -39,7 +39,8 @@ def lib():
         L.ov3d_group_cpu.argtypes = [P, P, i, i, i, i, i, P]
         L.ov3d_giou3d_cpu.argtypes = [P, P, P, i, i, i, i, i, i, P]
         L.ov3d_nms3d_cpu.argtypes = [P, i, i, ctypes.c_double, i, i, P, P]
-        for f in (L.ov3d_fps_cpu, L.ov3d_ball_query_cpu, L.ov3d_group_cpu,
+        L.ov3d_lsap_cpu.argtypes = [P, i, i, i, P]
+        for f in (L.ov3d_lsap_cpu, L.ov3d_fps_cpu, L.ov3d_ball_query_cpu, L.ov3d_group_cpu,
                   L.ov3d_giou3d_cpu, L.ov3d_nms3d_cpu):
             f.restype = ctypes.c_int
         _LIB = L
@@ -113,3 +114,17 @@ def nms3d(boxes, overlap_threshold, old_type=False, samecls=True):
                              int(bool(samecls)), _p(picks), _p(keep))
     assert n >= 0, n
     return picks[:n].tolist(), keep[:K]
+
+
+def lsap(cost):
+    """scipy.optimize.linear_sum_assignment restated (criterion.py:79): cost (Q, n) float32
+    -> gt_of_q (Q,) int32, -1 where unmatched."""
+    c = np.ascontiguousarray(cost, dtype=np.float32)
+    nq, ng = c.shape
+    out = np.empty(nq, dtype=np.int32)
+    rc = lib().ov3d_lsap_cpu(_p(c), nq, ng, ng, _p(out))
+    if rc == -1:
+        raise ValueError("matrix contains invalid numeric entries")
+    if rc:
+        raise ValueError("cost matrix is infeasible")
+    return out

@@ -416,3 +416,93 @@ int ov3d_nms3d_cpu(const double* boxes, int K, int stride, double thr, int old_t
     free(order); free(sup); free(area);
     return n;
 }
+
+/* ----------------------------------------------------- Hungarian (LSAP) */
+/* Restates scipy.optimize.linear_sum_assignment (scipy 1.15.3, the version in
+ * this image; the reference calls it at criterion.py:79 on final_cost[b, :, :n],
+ * a float32 (Q, n) slice converted to float64).  scipy's algorithm is Crouse's
+ * shortest-augmenting-path LSAP (rectangular_lsap.cpp): a tall matrix is
+ * transposed so rows <= cols; one Dijkstra search per row over the remaining
+ * columns, kept in a list initialised in DESCENDING column order and shrunk by
+ * swap-with-last removal; the next column is the first minimum of the path
+ * costs in list order, replaced by a later equal-cost column whenever that one
+ * is unassigned (so: the LAST unassigned minimum if any, else the FIRST
+ * minimum).  Path costs r = ((minVal + c) - u[i]) - v[j] in double.
+ * Tie behaviour therefore matches scipy exactly.
+ *
+ * cost: element (q, g) at cost[q*ld + g], q < nq, g < ng.
+ * Output: gt_of_q[q] = matched g or -1 for all q < nq.  Returns 0, or -1 for
+ * NaN / -inf entries (scipy raises ValueError), -2 if infeasible.          */
+int ov3d_lsap_cpu(const float* cost, int nq, int ng, int ld, int32_t* gt_of_q) {
+    for (int q = 0; q < nq; q++) gt_of_q[q] = -1;
+    if (nq == 0 || ng == 0) return 0;
+    for (int q = 0; q < nq; q++)
+        for (int g = 0; g < ng; g++) {
+            double c = cost[(size_t)q * ld + g];
+            if (c != c || c == -INFINITY) return -1;
+        }
+    const int tr = ng < nq;             /* rows = gts, cols = queries */
+    const int nr = tr ? ng : nq, nc = tr ? nq : ng;
+#define COST(i, j) ((double)(tr ? cost[(size_t)(j) * ld + (i)] : cost[(size_t)(i) * ld + (j)]))
+    double* u = calloc(nr, sizeof(double));
+    double* v = calloc(nc, sizeof(double));
+    double* spc = malloc(nc * sizeof(double));
+    int* path = malloc(nc * sizeof(int));
+    int* col4row = malloc(nr * sizeof(int));
+    int* row4col = malloc(nc * sizeof(int));
+    char* SR = malloc(nr);
+    char* SC = malloc(nc);
+    int* rem = malloc(nc * sizeof(int));
+    int rc = 0;
+    for (int i = 0; i < nr; i++) col4row[i] = -1;
+    for (int j = 0; j < nc; j++) { row4col[j] = -1; path[j] = -1; }
+    for (int cur = 0; cur < nr && rc == 0; cur++) {
+        double minv = 0;
+        int nrem = nc;
+        for (int t = 0; t < nc; t++) rem[t] = nc - 1 - t;
+        memset(SR, 0, nr);
+        memset(SC, 0, nc);
+        for (int j = 0; j < nc; j++) spc[j] = INFINITY;
+        int i = cur, sink = -1;
+        while (sink < 0) {
+            int best = -1;
+            double lo = INFINITY;
+            SR[i] = 1;
+            for (int t = 0; t < nrem; t++) {
+                int j = rem[t];
+                double r = minv + COST(i, j) - u[i] - v[j];
+                if (r < spc[j]) { path[j] = i; spc[j] = r; }
+                if (spc[j] < lo || (spc[j] == lo && row4col[j] < 0)) { lo = spc[j]; best = t; }
+            }
+            minv = lo;
+            if (minv == INFINITY) { rc = -2; break; }
+            int j = rem[best];
+            if (row4col[j] < 0) sink = j; else i = row4col[j];
+            SC[j] = 1;
+            rem[best] = rem[--nrem];
+        }
+        if (rc) break;
+        u[cur] += minv;
+        for (int r = 0; r < nr; r++)
+            if (SR[r] && r != cur) u[r] += minv - spc[col4row[r]];
+        for (int j = 0; j < nc; j++)
+            if (SC[j]) v[j] -= minv - spc[j];
+        for (int j = sink;;) {
+            int r = path[j];
+            row4col[j] = r;
+            int nj = col4row[r];
+            col4row[r] = j;
+            j = nj;
+            if (r == cur) break;
+        }
+    }
+#undef COST
+    if (rc == 0) {
+        for (int r = 0; r < nr; r++) {
+            if (tr) gt_of_q[col4row[r]] = r;
+            else gt_of_q[r] = col4row[r];
+        }
+    }
+    free(u); free(v); free(spc); free(path); free(col4row); free(row4col); free(SR); free(SC); free(rem);
+    return rc;
+}

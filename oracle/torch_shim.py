@@ -4,6 +4,7 @@ heads, criterion) can be checked against the reference fixtures in the CPU
 test suite.  Tests inject them explicitly (monkeypatch); the product never
 imports this module.
 """
+import numpy as np
 import torch
 
 from . import oracle as _o
@@ -68,12 +69,31 @@ def giou_aligned_torch(c1, c2, nums):
 
 def generalized_box3d_iou(corners1, corners2, nums_k2, rotated_boxes=True,
                           return_inter_vols_only=False, needs_grad=False, k2_bug=True):
+    rotated_boxes = bool(rotated_boxes)      # the product passes a device flag tensor
     if needs_grad and not rotated_boxes:
         return giou_aligned_torch(corners1, corners2, nums_k2)
     mode = _o.GIOU_MODE_TENSOR if needs_grad else _o.GIOU_MODE_CYTHON
     g = _o.giou3d(corners1.detach().cpu().numpy(), corners2.detach().cpu().numpy(),
                   nums_k2.cpu().numpy(), mode=mode, rotated=rotated_boxes, k2_bug=k2_bug)
     return torch.from_numpy(g).to(corners1.device)
+
+
+def hungarian(cost, nactual):
+    """CPU stand-in for ov3d_amd.assignment.hungarian: oracle LSAP (scipy restated)."""
+    c = cost.detach().float().cpu().numpy()
+    n = [int(v) for v in (nactual.tolist() if isinstance(nactual, torch.Tensor) else nactual)]
+    P, Q, _ = c.shape
+    inds = np.zeros((P, Q), dtype=np.int64)
+    mask = np.zeros((P, Q), dtype=np.float32)
+    for p in range(P):
+        if n[p] > 0:
+            g = _o.lsap(c[p, :, :n[p]])
+            hit = g >= 0
+            inds[p, hit] = g[hit]
+            mask[p, hit] = 1
+    dev = cost.device
+    return (torch.from_numpy(inds).to(dev), torch.from_numpy(mask).to(dev),
+            torch.zeros(P, dtype=torch.int32, device=dev))
 
 
 def install(pkg):
@@ -89,10 +109,12 @@ def install(pkg):
         grouping_operation=grouping_operation, QueryAndGroup=QueryAndGroup)
     saved = [(pkg.pointnet2_modules, "pu", pkg.pointnet2_modules.pu),
              (pkg.model_3detr, "pu", pkg.model_3detr.pu),
-             (pkg.criterion, "generalized_box3d_iou", pkg.criterion.generalized_box3d_iou)]
+             (pkg.criterion, "generalized_box3d_iou", pkg.criterion.generalized_box3d_iou),
+             (pkg.criterion, "hungarian", pkg.criterion.hungarian)]
     pkg.pointnet2_modules.pu = shim
     pkg.model_3detr.pu = shim
     pkg.criterion.generalized_box3d_iou = generalized_box3d_iou
+    pkg.criterion.hungarian = hungarian
     return saved
 
 

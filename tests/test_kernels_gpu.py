@@ -184,3 +184,46 @@ def test_nms_boxes_from_corners(cuda):
     c64 = corners.double()
     exp = torch.cat([c64.min(2).values, c64.max(2).values, obj.double()[..., None], cls.double()[..., None]], -1)
     assert torch.equal(t, exp)
+
+
+# ------------------------------------------------------------------ Hungarian
+@pytest.mark.parametrize("case", ["real", "ties", "const", "wide", "wide_ties", "scannet"])
+def test_hungarian_matches_scipy_golden(cuda, case):
+    from ov3d_amd.assignment import hungarian
+    fx = fixture("lsap.npz")
+    cost = torch.from_numpy(fx[f"{case}_cost"]).to(cuda)
+    nact = torch.from_numpy(fx[f"{case}_nact"]).to(cuda)
+    inds, mask, status = hungarian(cost, nact)
+    assert int(status.abs().sum()) == 0
+    np.testing.assert_array_equal(mask.cpu().numpy(), fx[f"{case}_mask"])
+    np.testing.assert_array_equal(inds.cpu().numpy(), fx[f"{case}_inds"])
+
+
+def test_hungarian_vs_oracle_random_ties(cuda):
+    from ov3d_amd.assignment import hungarian
+    rng = np.random.default_rng(11)
+    P, Q, G = 96, 128, 64
+    cost = rng.integers(0, 4, (P, Q, G)).astype(np.float32) * 0.5
+    cost[: P // 2] = rng.standard_normal((P // 2, Q, G)).astype(np.float32)
+    nact = rng.integers(0, G + 1, P).astype(np.int32)
+    inds, mask, _ = hungarian(torch.from_numpy(cost).to(cuda), torch.from_numpy(nact).to(cuda))
+    for p in range(P):
+        exp = np.full(Q, -1)
+        if nact[p]:
+            exp = O.lsap(cost[p, :, :nact[p]])
+        m = mask[p].cpu().numpy()
+        np.testing.assert_array_equal(m, (exp >= 0).astype(np.float32))
+        np.testing.assert_array_equal(inds[p].cpu().numpy(), np.where(exp >= 0, exp, 0))
+
+
+def test_hungarian_invalid_cost_status(cuda):
+    from ov3d_amd.assignment import check_status, hungarian
+    cost = torch.zeros(3, 16, 8, device=cuda)
+    cost[1, 3, 2] = float("nan")
+    cost[2, 0, 7] = float("nan")          # outside nactual: ignored, as in the reference slice
+    nact = torch.tensor([4, 4, 4], device=cuda, dtype=torch.int32)
+    inds, mask, status = hungarian(cost, nact)
+    assert status.tolist() == [0, -1, 0]
+    assert mask[1].sum().item() == 0 and mask[0].sum().item() == 4
+    with pytest.raises(ValueError, match="invalid numeric"):
+        check_status(status)

@@ -105,3 +105,56 @@ def test_graphed_step_equals_eager(cuda):
     for n, p in twin.named_parameters():
         if p.grad is not None:
             torch.testing.assert_close(p.grad, ge[n].grad, rtol=1e-4, atol=1e-6)
+
+
+def test_step_has_no_host_sync_and_matcher_equals_scipy(cuda):
+    """Full-size forward + criterion + backward run without a single device->host
+    synchronisation (torch sync-debug mode "error"), and the device Hungarian
+    assignments equal scipy.optimize.linear_sum_assignment (criterion.py:79) on the
+    same cost matrices."""
+    import ov3d_amd
+    from ov3d_amd import synthetic
+    from ov3d_amd.dataset_config import SunrgbdDatasetConfig
+    from bench import default_args
+    from scipy.optimize import linear_sum_assignment
+    args = default_args()
+    cfg = SunrgbdDatasetConfig()
+    torch.manual_seed(0)
+    model, _ = ov3d_amd.build_model(args, cfg, text_embedding=synthetic.text_embedding())
+    model = model.to(cuda).train()
+    crit = ov3d_amd.build_criterion(args, cfg).to(cuda)
+    batch = synthetic.make_batch(8, seed=3, device=cuda)
+    inputs = {k: batch[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")}
+    seen = {}
+    solve = crit.matcher.forward
+
+    def spy(cost, nact):
+        seen["cost"], seen["nact"] = cost, nact
+        seen.update(solve(cost, nact))
+        return seen
+    crit.matcher.forward = spy
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model(inputs)
+        loss, _ = crit(out, batch)
+        loss.backward()
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    assert torch.isfinite(loss)
+    cost = seen["cost"].float().cpu().numpy()
+    nact = seen["nact"].cpu().numpy()
+    inds = seen["per_prop_gt_inds"].cpu().numpy()
+    mask = seen["proposal_matched_mask"].cpu().numpy()
+    assert int(seen["status"].abs().sum()) == 0
+    for p in range(cost.shape[0]):
+        exp_i = np.zeros(cost.shape[1], np.int64)
+        exp_m = np.zeros(cost.shape[1], np.float32)
+        if nact[p]:
+            r, c = linear_sum_assignment(cost[p, :, :nact[p]])
+            exp_i[r], exp_m[r] = c, 1
+        np.testing.assert_array_equal(mask[p], exp_m)
+        np.testing.assert_array_equal(inds[p], exp_i)
+    asg = seen["assignments"]
+    assert len(asg) == cost.shape[0] and len(asg[0]) in (0, 2)

@@ -188,3 +188,47 @@ def test_group_gathers_columns():
 
 def test_math_constants():
     assert math.isclose(float(np.float32(0.2) * np.float32(0.2)), 0.04000000357627869, rel_tol=1e-7)
+
+
+# ------------------------------------------------------------------ Hungarian
+LSAP_CASES = ["real", "ties", "const", "wide", "wide_ties", "scannet"]
+
+
+def _lsap_batch(cost, nact):
+    P, Q, _ = cost.shape
+    inds = np.zeros((P, Q), np.int64)
+    mask = np.zeros((P, Q), np.float32)
+    for p in range(P):
+        if nact[p] > 0:
+            g = O.lsap(cost[p, :, :nact[p]])
+            inds[p, g >= 0] = g[g >= 0]
+            mask[p, g >= 0] = 1
+    return inds, mask
+
+
+@pytest.mark.parametrize("case", LSAP_CASES)
+def test_lsap_matches_scipy_golden(case):
+    """oracle LSAP == scipy.optimize.linear_sum_assignment (criterion.py:79) incl. ties."""
+    fx = fixture("lsap.npz")
+    inds, mask = _lsap_batch(fx[f"{case}_cost"], fx[f"{case}_nact"])
+    np.testing.assert_array_equal(mask, fx[f"{case}_mask"])
+    np.testing.assert_array_equal(inds, fx[f"{case}_inds"])
+
+
+def test_lsap_matches_scipy_random_shapes():
+    scipy_opt = pytest.importorskip("scipy.optimize")
+    rng = np.random.default_rng(5)
+    for it in range(600):
+        nq, ng = int(rng.integers(1, 60)), int(rng.integers(1, 60))
+        c = (rng.integers(0, 3, (nq, ng)) if it % 2 else rng.standard_normal((nq, ng))).astype(np.float32)
+        r, col = scipy_opt.linear_sum_assignment(c)
+        ref = np.full(nq, -1)
+        ref[r] = col
+        np.testing.assert_array_equal(O.lsap(c), ref)
+
+
+def test_lsap_rejects_invalid_entries():
+    c = np.zeros((3, 2), np.float32)
+    c[1, 1] = np.nan
+    with pytest.raises(ValueError):
+        O.lsap(c)

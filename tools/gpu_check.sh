@@ -25,4 +25,13 @@ if [ "${PROFILE:-1}" = "1" ]; then
   rc=$?; tail -3 $OUT/prof.err; [ $rc -eq 0 ] || stop rocprof $rc
   find $OUT/prof -name '*stats*' | head
 fi
+if [ "${PMC:-1}" = "1" ]; then
+  # HBM traffic of the FPS kernel: FETCH_SIZE and WRITE_SIZE need separate passes on gfx950
+  for c in FETCH_SIZE WRITE_SIZE; do
+    echo "== rocprofv3 --pmc $c"
+    timeout -k 10 600 rocprofv3 --pmc $c --kernel-include-regex fps -d $OUT/pmc_$c -o run --output-format csv -- \
+        python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-graph > $OUT/pmc_$c.json 2> $OUT/pmc_$c.err
+    rc=$?; tail -2 $OUT/pmc_$c.err; [ $rc -eq 0 ] || stop pmc_$c $rc
+  done
+fi
 echo "== done"
