@@ -112,6 +112,66 @@ int ov3d_giou3d_bwd_aligned(const float* corners1, const float* corners2, const 
 int ov3d_hungarian(const float* cost, const int32_t* nactual, int P, int Q, int G, int64_t* gt_inds,
                    float* matched, int32_t* status, void* stream);
 
+/* ---- Fused set-abstraction MLP (training, bf16 activations, fp32 accumulate) ----
+ * Replaces pointnet2 SharedMLP([3, C1, C2, C3], bn=True) + F.max_pool2d([1, nsample])
+ * inside PointnetSAModuleVotes (model_3detr.py:353-362) for training under bf16
+ * autocast.  Rows are channels-last (R = B*npoint*nsample, C); bf16 buffers are
+ * passed as void*.  BN statistics: each kernel writes fp64 partials (nparts, 2, C)
+ * (sum, sum of squares), ov3d_reduce_partials sums them (an all-reduce may follow
+ * for SyncBatchNorm), ov3d_bn_finalize folds them into scale/shift.  See
+ * DESIGN.md "Fused SA MLP" for the algebra. */
+/* layer 1: x0 (R,3) f32, W1 (C1,3) f32 -> y1 (R,C1) bf16, partials (nparts,2,C1) */
+int ov3d_sa_l1_fwd(const float* x0, const float* W1, int R, int C1, void* y1, double* partials,
+                   int nparts, void* stream);
+/* 1 if the MFMA layer kernel is built for (K, N) */
+int ov3d_sa_layer_supported(int K, int N);
+/* layer k: z = relu(scale*yprev + shift) (bf16, optionally stored to zout) ->
+ * y = z W^T (W (N,K) bf16) -> yout (R,N) bf16 + partials (nparts,2,N).  R % 64 == 0. */
+int ov3d_sa_layer_fwd(const void* yprev, const float* scale, const float* shift, const void* W,
+                      int R, int K, int N, void* zout, void* yout, double* partials, int nparts,
+                      void* stream);
+/* last layer + pool: as ov3d_sa_layer_fwd but y is not stored; per centroid (S rows,
+ * S in {32,64}) and channel: max/min of y (bf16 values) and their rows. */
+int ov3d_sa_layer_pool_fwd(const void* yprev, const float* scale, const float* shift,
+                           const void* W, int R, int K, int N, int S, void* zout, float* pmax,
+                           float* pmin, uint8_t* imax, uint8_t* imin, double* partials,
+                           int nparts, void* stream);
+/* backward of the last layer: recompute y, dy = cA*g + cB*y + cC with g = gsel at
+ * row isel of each centroid (0 elsewhere) -> dyout (R,N) bf16. */
+int ov3d_sa_layer_dy(const void* yprev, const float* scale, const float* shift, const void* W,
+                     int R, int K, int N, int S, const float* gsel, const uint8_t* isel,
+                     const float* cA, const float* cB, const float* cC, void* dyout, int nparts,
+                     void* stream);
+/* (nparts, width) fp64 -> (width) sums */
+int ov3d_reduce_partials(const double* partials, int nparts, int width, double* totals,
+                         void* stream);
+/* training BN: totals (2,C) over `count` rows -> mean, invstd, scale = gamma*invstd,
+ * shift = beta - mean*scale; running stats updated (momentum, unbiased var) if non-NULL */
+int ov3d_bn_finalize(const double* totals, double count, int C, const float* gamma,
+                     const float* beta, float eps, float momentum, float* running_mean,
+                     float* running_var, float* mean_out, float* invstd_out, float* scale_out,
+                     float* shift_out, void* stream);
+/* pooled output (P,N) f32 = relu(scale*(scale >= 0 ? pmax : pmin) + shift), plus the
+ * selected value / row for the backward */
+int ov3d_sa_pool_fwd(const float* pmax, const float* pmin, const uint8_t* imax,
+                     const uint8_t* imin, const float* scale, const float* shift, int P, int N,
+                     float* out, float* ysel, uint8_t* isel, void* stream);
+/* pooled-gradient ReLU mask + BN-backward partials (sum g, sum g*xhat) */
+int ov3d_sa_pool_bwd(const float* dout, const float* ysel, const float* scale, const float* shift,
+                     const float* mean, const float* invstd, int P, int N, float* gsel,
+                     double* partials, int nparts, void* stream);
+/* BN backward coefficients: dx = cA*g + cB*y + cC; dgamma, dbeta (may be NULL) */
+int ov3d_bn_bwd_finalize(const double* totals, double count, int C, const float* gamma,
+                         const float* mean, const float* invstd, float* cA, float* cB, float* cC,
+                         float* dgamma, float* dbeta, void* stream);
+/* ReLU + BN backward over (R,C) bf16 rows (dz = grad of the ReLU output, y = BN input):
+ * pass 0: partials (nparts,2,C) of dt and dt*xhat;  pass 1: dyout = cA*dt + cB*y + cC;
+ * pass 2: dW1 partials (nparts,C,3) = sum_r dy[r,c] * x0[r,k] (first layer, dy not stored) */
+int ov3d_bn_relu_bwd(int pass, const void* dz, const void* y, const float* scale,
+                     const float* shift, const float* mean, const float* invstd, const float* cA,
+                     const float* cB, const float* cC, const float* x0, int R, int C,
+                     double* partials, void* dyout, int nparts, void* stream);
+
 /* Greedy 3D NMS, batched over scenes.  Replaces utils/nms.py:79-162
  * (nms_3d_faster / nms_3d_faster_samecls) as called per scene by
  * utils/ap_calculator.py:153-190.

@@ -29,11 +29,21 @@ _SIGS = {
     "ov3d_gather_bwd": "ppiiiipp",
     "ov3d_giou3d": "pppiiiiipipp",
     "ov3d_giou3d_bwd_aligned": "pppiiippp",
-    "ov3d_hungarian": "ppiiippp",
+    "ov3d_hungarian": "ppiiipppp",
+    "ov3d_sa_l1_fwd": "ppiippip",
+    "ov3d_sa_layer_fwd": "ppppiiipppip",
+    "ov3d_sa_layer_pool_fwd": "ppppiiiippppppip",
+    "ov3d_sa_layer_dy": "ppppiiiippppppip",
+    "ov3d_reduce_partials": "piipp",
+    "ov3d_bn_finalize": "pdippffppppppp",
+    "ov3d_sa_pool_fwd": "ppppppiipppp",
+    "ov3d_sa_pool_bwd": "ppppppiippip",
+    "ov3d_bn_bwd_finalize": "pdippppppppp",
+    "ov3d_bn_relu_bwd": "ippppppppppiippip",
     "ov3d_nms3d": "ppiiidiipp",
     "ov3d_nms_boxes_from_corners": "pppiipp",
 }
-EXPORTS = tuple(_SIGS) + ("ov3d_version",)
+EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported")
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_longlong, "f": ctypes.c_float,
        "d": ctypes.c_double}
@@ -56,6 +66,8 @@ def load():
             fn = getattr(lib, name)
             fn.argtypes = [_CT[c] for c in sig]
             fn.restype = ctypes.c_int
+        lib.ov3d_sa_layer_supported.argtypes = [ctypes.c_int, ctypes.c_int]
+        lib.ov3d_sa_layer_supported.restype = ctypes.c_int
         lib.ov3d_version.argtypes = []
         lib.ov3d_version.restype = ctypes.c_char_p
         _lib = lib

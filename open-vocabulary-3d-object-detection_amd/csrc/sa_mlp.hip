@@ -1,0 +1,640 @@
+// Set-abstraction MLP of PointnetSAModuleVotes (model_3detr.py:353-362, the
+// pre-encoder) fused for training on MFMA: 1x1 conv (no bias) -> BatchNorm
+// (batch statistics) -> ReLU, three times, then max over the nsample rows of
+// each centroid (pointnet2 SharedMLP + F.max_pool2d [1, nsample]).
+//
+// Layout: channels-last rows (R = B*M*S, C), one row per (centroid, neighbour);
+// the S rows of a centroid are consecutive, a 64-row tile holds one centroid
+// (S = 64) or two (S = 32).  Activations are bf16 in HBM, accumulation fp32.
+//
+// Forward, per layer k >= 2, ONE pass over the rows (sa_layer_kernel):
+//   load y_{k-1} tile (bf16) -> z = relu(a*y + b) with the previous layer's BN
+//   folded into (a, b) -> LDS -> MFMA 32x32x16 with W_k held in VGPRs for the
+//   whole (persistent) workgroup -> epilogue:
+//     MODE_STORE: y_k (bf16) + per-channel sum / sum of squares partials;
+//     MODE_POOL : nothing per row: per centroid and channel the max and min of
+//                 y_k and their rows (first occurrence) + the BN partials.
+//     Because relu(a*y + b) is monotone in y (non-decreasing for a >= 0,
+//     non-increasing for a < 0, also after rounding), max_s relu(a*y_s + b) ==
+//     relu(a * (a >= 0 ? max_s y : min_s y) + b): the last layer's activations
+//     are never written (2^20 x 256 values per step).
+//     MODE_DY   : backward recompute of y_k fused with the BN backward:
+//                 dy = cA*g + cB*y + cC, g = pooled gradient at the arg row.
+// BN statistics are reduced per workgroup (fp32 per lane over its rows, fp64
+// across lanes / workgroups) and finalised on the device.
+#include "common.h"
+
+namespace {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kTile = 64;      // rows per tile
+constexpr int kThreads = 256;  // 4 waves
+enum { MODE_STORE = 0, MODE_POOL = 1, MODE_DY = 2 };
+
+__device__ __forceinline__ float relu_bn(float a, float y, float b) { return fmaxf(fmaf(a, y, b), 0.f); }
+
+struct LayerArgs {
+    const bf16* yprev;     // (R, K)
+    const float* scale;    // (K) previous layer's folded BN: a
+    const float* shift;    // (K) b
+    const bf16* W;         // (N, K)
+    int R, S;
+    bf16* zout;            // (R, K) optional: relu(a*yprev+b) as used by the MFMA
+    bf16* yout;            // MODE_STORE: (R, N)
+    double* partials;      // (gridDim.x, 2, N): sum, sum of squares
+    float* pmax;           // MODE_POOL: (P, N) per centroid max / min of y, rows
+    float* pmin;
+    uint8_t* imax;
+    uint8_t* imin;
+    const float* gsel;     // MODE_DY: (P, N) pooled gradient after the ReLU mask
+    const uint8_t* isel;   // (P, N) row of the pooled value within its centroid
+    const float* cA;       // (N) dy = cA*g + cB*y + cC
+    const float* cB;
+    const float* cC;
+    bf16* dyout;           // (R, N)
+};
+
+template <int K, int N, int MODE>
+__global__ __launch_bounds__(kThreads) void sa_layer_kernel(LayerArgs p) {
+    constexpr int LDK = K + 8;          // padded LDS row (bf16): spreads rows over banks
+    constexpr int NB = N / 128;         // 32-column blocks per wave
+    constexpr int KS = K / 16;          // MFMA k-steps
+    __shared__ __attribute__((aligned(16))) bf16 As[kTile * LDK];
+    __shared__ float sc[K], sh[K];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r32 = lane & 31, h = lane >> 5;
+
+    for (int k = tid; k < K; k += kThreads) {
+        sc[k] = p.scale[k];
+        sh[k] = p.shift[k];
+    }
+    bf16x8 bfrag[NB][KS];
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb) {
+        const int n = wave * (N / 4) + cb * 32 + r32;
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            bfrag[cb][s] = *reinterpret_cast<const bf16x8*>(p.W + (size_t)n * K + 16 * s + 8 * h);
+    }
+    float ssum[NB], ssq[NB];
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb) ssum[cb] = ssq[cb] = 0.f;
+    float cA[NB], cB[NB], cC[NB];
+    if constexpr (MODE == MODE_DY) {
+#pragma unroll
+        for (int cb = 0; cb < NB; ++cb) {
+            const int n = wave * (N / 4) + cb * 32 + r32;
+            cA[cb] = p.cA[n];
+            cB[cb] = p.cB[n];
+            cC[cb] = p.cC[n];
+        }
+    }
+    __syncthreads();
+
+    const int ntiles = p.R / kTile;
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const size_t row0 = (size_t)tile * kTile;
+        // prologue: previous layer's BN + ReLU, to bf16, into LDS (and optionally HBM)
+        for (int ch = tid; ch < kTile * K / 8; ch += kThreads) {
+            const int row = ch / (K / 8), kc = (ch % (K / 8)) * 8;
+            const bf16x8 v = *reinterpret_cast<const bf16x8*>(p.yprev + (row0 + row) * K + kc);
+            bf16x8 z;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) z[j] = (bf16)relu_bn(sc[kc + j], (float)v[j], sh[kc + j]);
+            *reinterpret_cast<bf16x8*>(&As[row * LDK + kc]) = z;
+            if (p.zout) *reinterpret_cast<bf16x8*>(p.zout + (row0 + row) * K + kc) = z;
+        }
+        __syncthreads();
+        f32x16 acc[2][NB];
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int cb = 0; cb < NB; ++cb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[rb][cb][i] = 0.f;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb) {
+                const bf16x8 a = *reinterpret_cast<const bf16x8*>(&As[(rb * 32 + r32) * LDK + 16 * s + 8 * h]);
+#pragma unroll
+                for (int cb = 0; cb < NB; ++cb)
+                    acc[rb][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfrag[cb][s], acc[rb][cb], 0, 0, 0);
+            }
+        }
+        __syncthreads();   // As is rewritten by the next tile's prologue
+
+        // epilogue: element (rb, cb, i) is row rb*32 + (i&3) + 8*(i>>2) + 4h, column n
+#pragma unroll
+        for (int cb = 0; cb < NB; ++cb) {
+            const int n = wave * (N / 4) + cb * 32 + r32;
+            if constexpr (MODE == MODE_STORE) {
+#pragma unroll
+                for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int row = rb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                        const bf16 yb = (bf16)acc[rb][cb][i];
+                        p.yout[(row0 + row) * N + n] = yb;
+                        const float f = (float)yb;
+                        ssum[cb] += f;
+                        ssq[cb] = fmaf(f, f, ssq[cb]);
+                    }
+            } else if constexpr (MODE == MODE_POOL) {
+                float mx[2], mn[2];
+                int imx[2], imn[2];
+#pragma unroll
+                for (int rb = 0; rb < 2; ++rb) {
+                    mx[rb] = -__builtin_huge_valf();
+                    mn[rb] = __builtin_huge_valf();
+                    imx[rb] = imn[rb] = 0;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {       // rows increase with i (fixed h)
+                        const int row = rb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                        const float f = (float)(bf16)acc[rb][cb][i];
+                        ssum[cb] += f;
+                        ssq[cb] = fmaf(f, f, ssq[cb]);
+                        if (f > mx[rb]) { mx[rb] = f; imx[rb] = row; }
+                        if (f < mn[rb]) { mn[rb] = f; imn[rb] = row; }
+                    }
+                    // combine the two lane halves (rows 4h..): value, then lower row
+                    const float omx = __shfl_xor(mx[rb], 32), omn = __shfl_xor(mn[rb], 32);
+                    const int oimx = __shfl_xor(imx[rb], 32), oimn = __shfl_xor(imn[rb], 32);
+                    if (omx > mx[rb] || (omx == mx[rb] && oimx < imx[rb])) { mx[rb] = omx; imx[rb] = oimx; }
+                    if (omn < mn[rb] || (omn == mn[rb] && oimn < imn[rb])) { mn[rb] = omn; imn[rb] = oimn; }
+                }
+                if (h == 0) {
+                    if (p.S == 64) {
+                        const int c0 = mx[1] > mx[0] ? 1 : 0, c1 = mn[1] < mn[0] ? 1 : 0;
+                        const size_t o = (size_t)tile * N + n;
+                        p.pmax[o] = mx[c0];
+                        p.imax[o] = (uint8_t)imx[c0];
+                        p.pmin[o] = mn[c1];
+                        p.imin[o] = (uint8_t)imn[c1];
+                    } else {   // S == 32: one centroid per row block
+#pragma unroll
+                        for (int rb = 0; rb < 2; ++rb) {
+                            const size_t o = ((size_t)tile * 2 + rb) * N + n;
+                            p.pmax[o] = mx[rb];
+                            p.imax[o] = (uint8_t)(imx[rb] - 32 * rb);
+                            p.pmin[o] = mn[rb];
+                            p.imin[o] = (uint8_t)(imn[rb] - 32 * rb);
+                        }
+                    }
+                }
+            } else {   // MODE_DY
+#pragma unroll
+                for (int rb = 0; rb < 2; ++rb) {
+                    const size_t pc = (p.S == 64 ? (size_t)tile : (size_t)tile * 2 + rb) * N + n;
+                    const int sel = p.isel[pc] + (p.S == 64 ? 0 : 32 * rb);
+                    const float g = p.gsel[pc];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int row = rb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                        const float y = (float)(bf16)acc[rb][cb][i];
+                        const float gi = row == sel ? g : 0.f;
+                        const float dy = fmaf(cA[cb], gi, fmaf(cB[cb], y, cC[cb]));
+                        p.dyout[(row0 + row) * N + n] = (bf16)dy;
+                    }
+                }
+            }
+        }
+    }
+
+    if constexpr (MODE != MODE_DY) {
+        // per-column totals of this workgroup: both lane halves hold the same column
+#pragma unroll
+        for (int cb = 0; cb < NB; ++cb) {
+            const double s = (double)ssum[cb] + (double)__shfl_xor(ssum[cb], 32);
+            const double q = (double)ssq[cb] + (double)__shfl_xor(ssq[cb], 32);
+            if (h == 0) {
+                const int n = wave * (N / 4) + cb * 32 + r32;
+                p.partials[(size_t)blockIdx.x * 2 * N + n] = s;
+                p.partials[(size_t)blockIdx.x * 2 * N + N + n] = q;
+            }
+        }
+    }
+}
+
+// First layer: Cin = 3 fp32 (grouped, normalised xyz) -> C1 channels.
+// Thread t: channel t % C1, row phase t / C1.
+__global__ __launch_bounds__(kThreads) void sa_l1_kernel(const float* __restrict__ x0,
+                                                         const float* __restrict__ W1, int R, int C1,
+                                                         bf16* __restrict__ y1,
+                                                         double* __restrict__ partials) {
+    __shared__ double red[2][kThreads];
+    const int tid = threadIdx.x;
+    const int c = tid % C1, ph = tid / C1, nph = kThreads / C1;
+    const float w0 = W1[c * 3], w1 = W1[c * 3 + 1], w2 = W1[c * 3 + 2];
+    float s = 0.f, q = 0.f;
+    for (long long r = (long long)blockIdx.x * nph + ph; r < R; r += (long long)gridDim.x * nph) {
+        const float* x = x0 + r * 3;
+        const float y = fmaf(w2, x[2], fmaf(w1, x[1], w0 * x[0]));
+        const bf16 yb = (bf16)y;
+        y1[r * C1 + c] = yb;
+        const float f = (float)yb;
+        s += f;
+        q = fmaf(f, f, q);
+    }
+    red[0][tid] = s;
+    red[1][tid] = q;
+    __syncthreads();
+    if (tid < C1) {
+        double ts = 0, tq = 0;
+        for (int k = 0; k < nph; ++k) {
+            ts += red[0][k * C1 + tid];
+            tq += red[1][k * C1 + tid];
+        }
+        partials[(size_t)blockIdx.x * 2 * C1 + tid] = ts;
+        partials[(size_t)blockIdx.x * 2 * C1 + C1 + tid] = tq;
+    }
+}
+
+// (nparts, 2, C) fp64 partials -> (2, C) totals; one thread per (k, c).
+__global__ void reduce_partials_kernel(const double* __restrict__ partials, int nparts, int C2,
+                                       double* __restrict__ totals) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= C2) return;
+    double s = 0;
+    for (int w = 0; w < nparts; ++w) s += partials[(size_t)w * C2 + i];
+    totals[i] = s;
+}
+
+// Training BatchNorm from totals (sum, sum of squares) over `count` rows:
+// mean, biased var -> invstd, folded scale/shift; running stats with momentum
+// and the unbiased variance (torch.nn.functional.batch_norm semantics).
+__global__ void bn_finalize_kernel(const double* __restrict__ totals, double count, int C,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float eps, float momentum, float* running_mean, float* running_var,
+                                   float* __restrict__ mean_out, float* __restrict__ invstd_out,
+                                   float* __restrict__ scale_out, float* __restrict__ shift_out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const double mean = totals[c] / count;
+    double var = totals[C + c] / count - mean * mean;
+    var = var < 0 ? 0 : var;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+    mean_out[c] = (float)mean;
+    invstd_out[c] = invstd;
+    const float a = g * invstd;
+    scale_out[c] = a;
+    shift_out[c] = b - (float)mean * a;
+    if (running_mean) {
+        const double unb = count > 1 ? var * count / (count - 1) : var;
+        running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+        running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
+    }
+}
+
+// Pool: out = relu(a * (a >= 0 ? max : min) + b); remembers the value and row used.
+__global__ void sa_pool_fwd_kernel(const float* __restrict__ pmax, const float* __restrict__ pmin,
+                                   const uint8_t* __restrict__ imax, const uint8_t* __restrict__ imin,
+                                   const float* __restrict__ scale, const float* __restrict__ shift,
+                                   long long PN, int N, float* __restrict__ out,
+                                   float* __restrict__ ysel, uint8_t* __restrict__ isel) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= PN) return;
+    const int n = (int)(i % N);
+    const float a = scale[n];
+    const bool up = a >= 0.f;
+    const float y = up ? pmax[i] : pmin[i];
+    out[i] = relu_bn(a, y, shift[n]);
+    ysel[i] = y;
+    isel[i] = up ? imax[i] : imin[i];
+}
+
+// Pool backward: g = dout masked by the ReLU at the pooled row; partial sums of
+// g and g * xhat per channel (the BN backward reductions; zero rows add nothing).
+__global__ __launch_bounds__(kThreads) void sa_pool_bwd_kernel(
+    const float* __restrict__ dout, const float* __restrict__ ysel, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ mean, const float* __restrict__ invstd,
+    int P, int N, float* __restrict__ gsel, double* __restrict__ partials) {
+    // thread: channel tid % N (N <= 256, 256 % N == 0), centroid phase tid / N
+    __shared__ double red[2][kThreads];
+    const int tid = threadIdx.x, n = tid % N, ph = tid / N, nph = kThreads / N;
+    const float a = scale[n], b = shift[n], mu = mean[n], is = invstd[n];
+    float s = 0.f, q = 0.f;
+    for (long long pi = (long long)blockIdx.x * nph + ph; pi < P; pi += (long long)gridDim.x * nph) {
+        const long long i = pi * N + n;
+        const float y = ysel[i];
+        const float g = fmaf(a, y, b) > 0.f ? dout[i] : 0.f;
+        gsel[i] = g;
+        s += g;
+        q = fmaf(g, (y - mu) * is, q);
+    }
+    red[0][tid] = s;
+    red[1][tid] = q;
+    __syncthreads();
+    if (tid < N) {
+        double ts = 0, tq = 0;
+        for (int k = 0; k < nph; ++k) {
+            ts += red[0][k * N + tid];
+            tq += red[1][k * N + tid];
+        }
+        partials[(size_t)blockIdx.x * 2 * N + tid] = ts;
+        partials[(size_t)blockIdx.x * 2 * N + N + tid] = tq;
+    }
+}
+
+// BN backward coefficients from totals (sum g, sum g*xhat) over `count` rows:
+//   dx = gamma*invstd * (g - mean(g) - xhat * mean(g*xhat))  ==  cA*g + cB*y + cC
+// (PyTorch batch_norm_backward, training), plus dgamma / dbeta.
+__global__ void bn_bwd_finalize_kernel(const double* __restrict__ totals, double count, int C,
+                                       const float* __restrict__ gamma, const float* __restrict__ mean,
+                                       const float* __restrict__ invstd, float* __restrict__ cA,
+                                       float* __restrict__ cB, float* __restrict__ cC,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const double m1 = totals[c] / count, m2 = totals[C + c] / count;
+    const double is = invstd[c], g = gamma ? gamma[c] : 1.0, mu = mean[c];
+    const double a = g * is;
+    cA[c] = (float)a;
+    cB[c] = (float)(-a * is * m2);
+    cC[c] = (float)(-a * m1 + a * is * m2 * mu);
+    if (dgamma) dgamma[c] = (float)totals[C + c];
+    if (dbeta) dbeta[c] = (float)totals[c];
+}
+
+// ReLU + BN backward over rows, C = 8 * (threads per row):
+// pass 0 (stats): partial sums of dt and dt*xhat, dt = relu'(a*y+b) * dz;
+// pass 1 (apply): dy = cA*dt + cB*y + cC stored as bf16;
+// pass 2 (weight): dy of a first layer with Cin = 3 is reduced against x0 into
+//                  dW1 partials (nparts, C, 3) and never stored.
+template <int PASS>
+__global__ __launch_bounds__(kThreads) void bn_relu_bwd_kernel(
+    const bf16* __restrict__ dz, const bf16* __restrict__ y, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ cA, const float* __restrict__ cB, const float* __restrict__ cC,
+    const float* __restrict__ x0, long long R, int C, double* __restrict__ partials,
+    bf16* __restrict__ dyout) {
+    const int tid = threadIdx.x;
+    const int tpr = C / 8;                          // threads per row
+    const int kc = (tid % tpr) * 8, ph = tid / tpr, nph = kThreads / tpr;
+    float pa[8], pb[8], p0[8], p1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        pa[j] = scale[kc + j];
+        pb[j] = shift[kc + j];
+        if (PASS == 0) {
+            p0[j] = mean[kc + j];
+            p1[j] = invstd[kc + j];
+        } else {
+            p0[j] = cA[kc + j];
+            p1[j] = cB[kc + j];
+        }
+    }
+    float c2[8];
+    if (PASS != 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) c2[j] = cC[kc + j];
+    }
+    float acc0[8], acc1[8], acc2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc0[j] = acc1[j] = acc2[j] = 0.f;
+    for (long long r = (long long)blockIdx.x * nph + ph; r < R; r += (long long)gridDim.x * nph) {
+        const bf16x8 vz = *reinterpret_cast<const bf16x8*>(dz + r * C + kc);
+        const bf16x8 vy = *reinterpret_cast<const bf16x8*>(y + r * C + kc);
+        float xr[3];
+        if (PASS == 2) {
+            xr[0] = x0[r * 3];
+            xr[1] = x0[r * 3 + 1];
+            xr[2] = x0[r * 3 + 2];
+        }
+        bf16x8 out;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float yy = (float)vy[j];
+            const float dt = fmaf(pa[j], yy, pb[j]) > 0.f ? (float)vz[j] : 0.f;
+            if (PASS == 0) {
+                acc0[j] += dt;
+                acc1[j] = fmaf(dt, (yy - p0[j]) * p1[j], acc1[j]);
+            } else {
+                const float d = fmaf(p0[j], dt, fmaf(p1[j], yy, c2[j]));
+                if (PASS == 1) {
+                    out[j] = (bf16)d;
+                } else {
+                    acc0[j] = fmaf(d, xr[0], acc0[j]);
+                    acc1[j] = fmaf(d, xr[1], acc1[j]);
+                    acc2[j] = fmaf(d, xr[2], acc2[j]);
+                }
+            }
+        }
+        if (PASS == 1) *reinterpret_cast<bf16x8*>(dyout + r * C + kc) = out;
+    }
+    if (PASS == 1) return;
+    // reduce over the row phases: LDS [value][phase * C + channel] (nph * C == 8 * kThreads)
+    __shared__ double sred[PASS == 0 ? 2 : 3][8 * kThreads];
+    const int nv = PASS == 0 ? 2 : 3;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        sred[0][ph * C + kc + j] = acc0[j];
+        sred[1][ph * C + kc + j] = acc1[j];
+        if constexpr (PASS == 2) sred[2][ph * C + kc + j] = acc2[j];
+    }
+    __syncthreads();
+    for (int i = tid; i < nv * C; i += kThreads) {
+        const int v = i / C, c = i % C;
+        double t = 0;
+        for (int k = 0; k < nph; ++k) t += sred[v][k * C + c];
+        if (PASS == 0)
+            partials[(size_t)blockIdx.x * 2 * C + v * C + c] = t;
+        else
+            partials[(size_t)blockIdx.x * 3 * C + c * 3 + v] = t;   // (C, 3) = dW1[c][k]
+    }
+}
+
+int grid_for(long long work, int cap) {
+    long long g = work < cap ? work : cap;
+    return g < 1 ? 1 : (int)g;
+}
+
+}  // namespace
+
+extern "C" int ov3d_sa_l1_fwd(const float* x0, const float* W1, int R, int C1, void* y1,
+                              double* partials, int nparts, void* stream) {
+    if (R < 0 || C1 <= 0 || C1 > kThreads || kThreads % C1 || nparts <= 0) return OV3D_EINVAL;
+    if (!x0 || !W1 || !y1 || !partials) return OV3D_EINVAL;
+    hipLaunchKernelGGL(sa_l1_kernel, dim3(nparts), dim3(kThreads), 0, ov3d_stream(stream), x0, W1, R,
+                       C1, reinterpret_cast<bf16*>(y1), partials);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+template <int MODE>
+static int launch_layer(const LayerArgs& a, int K, int N, int nparts, hipStream_t s) {
+#define OV3D_SA_CASE(KK, NN)                                                                     \
+    if (K == KK && N == NN) {                                                                    \
+        hipLaunchKernelGGL((sa_layer_kernel<KK, NN, MODE>), dim3(nparts), dim3(kThreads), 0, s, a); \
+        OV3D_LAUNCH_CHECK();                                                                     \
+        return OV3D_OK;                                                                          \
+    }
+    OV3D_SA_CASE(64, 128)
+    OV3D_SA_CASE(128, 256)
+    OV3D_SA_CASE(128, 128)
+#undef OV3D_SA_CASE
+    return OV3D_EINVAL;
+}
+
+extern "C" int ov3d_sa_layer_supported(int K, int N) {
+    return (K == 64 && N == 128) || (K == 128 && N == 256) || (K == 128 && N == 128);
+}
+
+extern "C" int ov3d_sa_layer_fwd(const void* yprev, const float* scale, const float* shift,
+                                 const void* W, int R, int K, int N, void* zout, void* yout,
+                                 double* partials, int nparts, void* stream) {
+    if (R < 0 || R % kTile || !yprev || !scale || !shift || !W || !yout || !partials || nparts <= 0)
+        return OV3D_EINVAL;
+    LayerArgs a = {};
+    a.yprev = reinterpret_cast<const bf16*>(yprev);
+    a.scale = scale;
+    a.shift = shift;
+    a.W = reinterpret_cast<const bf16*>(W);
+    a.R = R;
+    a.S = kTile;
+    a.zout = reinterpret_cast<bf16*>(zout);
+    a.yout = reinterpret_cast<bf16*>(yout);
+    a.partials = partials;
+    return launch_layer<MODE_STORE>(a, K, N, nparts, ov3d_stream(stream));
+}
+
+extern "C" int ov3d_sa_layer_pool_fwd(const void* yprev, const float* scale, const float* shift,
+                                      const void* W, int R, int K, int N, int S, void* zout,
+                                      float* pmax, float* pmin, uint8_t* imax, uint8_t* imin,
+                                      double* partials, int nparts, void* stream) {
+    if (R < 0 || R % kTile || (S != 32 && S != 64) || !yprev || !scale || !shift || !W || !pmax ||
+        !pmin || !imax || !imin || !partials || nparts <= 0)
+        return OV3D_EINVAL;
+    LayerArgs a = {};
+    a.yprev = reinterpret_cast<const bf16*>(yprev);
+    a.scale = scale;
+    a.shift = shift;
+    a.W = reinterpret_cast<const bf16*>(W);
+    a.R = R;
+    a.S = S;
+    a.zout = reinterpret_cast<bf16*>(zout);
+    a.partials = partials;
+    a.pmax = pmax;
+    a.pmin = pmin;
+    a.imax = imax;
+    a.imin = imin;
+    return launch_layer<MODE_POOL>(a, K, N, nparts, ov3d_stream(stream));
+}
+
+extern "C" int ov3d_sa_layer_dy(const void* yprev, const float* scale, const float* shift,
+                                const void* W, int R, int K, int N, int S, const float* gsel,
+                                const uint8_t* isel, const float* cA, const float* cB,
+                                const float* cC, void* dyout, int nparts, void* stream) {
+    if (R < 0 || R % kTile || (S != 32 && S != 64) || !yprev || !scale || !shift || !W || !gsel ||
+        !isel || !cA || !cB || !cC || !dyout || nparts <= 0)
+        return OV3D_EINVAL;
+    LayerArgs a = {};
+    a.yprev = reinterpret_cast<const bf16*>(yprev);
+    a.scale = scale;
+    a.shift = shift;
+    a.W = reinterpret_cast<const bf16*>(W);
+    a.R = R;
+    a.S = S;
+    a.gsel = gsel;
+    a.isel = isel;
+    a.cA = cA;
+    a.cB = cB;
+    a.cC = cC;
+    a.dyout = reinterpret_cast<bf16*>(dyout);
+    return launch_layer<MODE_DY>(a, K, N, nparts, ov3d_stream(stream));
+}
+
+extern "C" int ov3d_reduce_partials(const double* partials, int nparts, int width, double* totals,
+                                    void* stream) {
+    if (nparts <= 0 || width <= 0 || !partials || !totals) return OV3D_EINVAL;
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3(ov3d_cdiv(width, 256)), dim3(256), 0,
+                       ov3d_stream(stream), partials, nparts, width, totals);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_bn_finalize(const double* totals, double count, int C, const float* gamma,
+                                const float* beta, float eps, float momentum, float* running_mean,
+                                float* running_var, float* mean_out, float* invstd_out,
+                                float* scale_out, float* shift_out, void* stream) {
+    if (C <= 0 || count <= 0 || !totals || !mean_out || !invstd_out || !scale_out || !shift_out)
+        return OV3D_EINVAL;
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(ov3d_cdiv(C, 256)), dim3(256), 0, ov3d_stream(stream),
+                       totals, count, C, gamma, beta, eps, momentum, running_mean, running_var,
+                       mean_out, invstd_out, scale_out, shift_out);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_sa_pool_fwd(const float* pmax, const float* pmin, const uint8_t* imax,
+                                const uint8_t* imin, const float* scale, const float* shift, int P,
+                                int N, float* out, float* ysel, uint8_t* isel, void* stream) {
+    if (P < 0 || N <= 0 || !pmax || !pmin || !imax || !imin || !scale || !shift || !out || !ysel ||
+        !isel)
+        return OV3D_EINVAL;
+    const long long PN = (long long)P * N;
+    if (PN == 0) return OV3D_OK;
+    hipLaunchKernelGGL(sa_pool_fwd_kernel, dim3(ov3d_cdiv(PN, 256)), dim3(256), 0, ov3d_stream(stream),
+                       pmax, pmin, imax, imin, scale, shift, PN, N, out, ysel, isel);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_sa_pool_bwd(const float* dout, const float* ysel, const float* scale,
+                                const float* shift, const float* mean, const float* invstd, int P,
+                                int N, float* gsel, double* partials, int nparts, void* stream) {
+    if (P < 0 || N <= 0 || N > kThreads || kThreads % N || nparts <= 0 || !dout || !ysel || !scale ||
+        !shift || !mean || !invstd || !gsel || !partials)
+        return OV3D_EINVAL;
+    hipLaunchKernelGGL(sa_pool_bwd_kernel, dim3(nparts), dim3(kThreads), 0, ov3d_stream(stream), dout,
+                       ysel, scale, shift, mean, invstd, P, N, gsel, partials);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_bn_bwd_finalize(const double* totals, double count, int C, const float* gamma,
+                                    const float* mean, const float* invstd, float* cA, float* cB,
+                                    float* cC, float* dgamma, float* dbeta, void* stream) {
+    if (C <= 0 || count <= 0 || !totals || !mean || !invstd || !cA || !cB || !cC) return OV3D_EINVAL;
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ov3d_cdiv(C, 256)), dim3(256), 0,
+                       ov3d_stream(stream), totals, count, C, gamma, mean, invstd, cA, cB, cC, dgamma,
+                       dbeta);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_bn_relu_bwd(int pass, const void* dz, const void* y, const float* scale,
+                                const float* shift, const float* mean, const float* invstd,
+                                const float* cA, const float* cB, const float* cC, const float* x0,
+                                int R, int C, double* partials, void* dyout, int nparts,
+                                void* stream) {
+    if (R < 0 || C <= 0 || C % 8 || C / 8 > kThreads || kThreads % (C / 8) || C > 256 ||
+        nparts <= 0 || !dz || !y || !scale || !shift)
+        return OV3D_EINVAL;
+    const bf16* dzb = reinterpret_cast<const bf16*>(dz);
+    const bf16* yb = reinterpret_cast<const bf16*>(y);
+    hipStream_t s = ov3d_stream(stream);
+    if (pass == 0) {
+        if (!mean || !invstd || !partials) return OV3D_EINVAL;
+        hipLaunchKernelGGL(bn_relu_bwd_kernel<0>, dim3(nparts), dim3(kThreads), 0, s, dzb, yb, scale,
+                           shift, mean, invstd, cA, cB, cC, x0, (long long)R, C, partials,
+                           (bf16*)nullptr);
+    } else if (pass == 1) {
+        if (!cA || !cB || !cC || !dyout) return OV3D_EINVAL;
+        hipLaunchKernelGGL(bn_relu_bwd_kernel<1>, dim3(nparts), dim3(kThreads), 0, s, dzb, yb, scale,
+                           shift, mean, invstd, cA, cB, cC, x0, (long long)R, C, partials,
+                           reinterpret_cast<bf16*>(dyout));
+    } else if (pass == 2) {
+        if (!cA || !cB || !cC || !x0 || !partials) return OV3D_EINVAL;
+        hipLaunchKernelGGL(bn_relu_bwd_kernel<2>, dim3(nparts), dim3(kThreads), 0, s, dzb, yb, scale,
+                           shift, mean, invstd, cA, cB, cC, x0, (long long)R, C, partials,
+                           (bf16*)nullptr);
+    } else {
+        return OV3D_EINVAL;
+    }
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}

@@ -23,14 +23,30 @@ def _chunks(R, cout, cin):
     return nc
 
 
+_F32_OUT = None   # does this build's bmm take out_dtype=float32 for bf16 inputs (hipBLASLt)?
+
+
+def _bmm_f32(a, b):
+    """bf16 x bf16 -> fp32 batched GEMM without rounding the per-chunk partials to bf16."""
+    global _F32_OUT
+    if a.dtype in (torch.bfloat16, torch.float16) and a.is_cuda and _F32_OUT is not False:
+        try:
+            out = torch.bmm(a, b, out_dtype=torch.float32)
+            _F32_OUT = True
+            return out
+        except (RuntimeError, TypeError):
+            _F32_OUT = False
+    return torch.bmm(a, b)
+
+
 def weight_grad(dy, x):
     """dy (R, Cout), x (R, Cin) -> dy^T x (Cout, Cin) in fp32, split-K over R."""
     R, cout = dy.shape
     cin = x.shape[1]
     nc = _chunks(R, cout, cin)
     if nc == 1:
-        return (dy.t() @ x).float()
-    part = torch.bmm(dy.view(nc, R // nc, cout).transpose(1, 2), x.view(nc, R // nc, cin))
+        return _bmm_f32(dy.t()[None], x[None])[0].float()
+    part = _bmm_f32(dy.view(nc, R // nc, cout).transpose(1, 2), x.view(nc, R // nc, cin))
     return torch.sum(part, dim=0, dtype=torch.float32)
 
 

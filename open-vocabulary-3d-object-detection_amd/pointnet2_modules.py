@@ -12,6 +12,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import pointnet2_utils as pu
+from . import sa_fused
 from .gemm import rows_linear
 
 
@@ -110,7 +111,11 @@ class PointnetSAModuleVotes(nn.Module):
         """grouped rows -> SharedMLP -> max over nsample: (B, npoint, Cout)."""
         g = self.grouper.rows(xyz, new_xyz, features)          # (B, M, S, 3+C) fp32
         B, M, S, C = g.shape
-        y = self.mlp_module.rows(g.view(B * M * S, C))
+        rows = g.view(B * M * S, C)
+        if self.training and sa_fused.supported(self.mlp_module, rows, S):
+            # training under bf16 autocast: fused MFMA kernels (sa_fused.py)
+            return sa_fused.sa_mlp_pool(self.mlp_module, rows, S).view(B, M, -1)
+        y = self.mlp_module.rows(rows)
         # == F.max_pool2d(kernel [1, nsample]) of the reference
         return y.view(B, M, S, -1).max(dim=2).values
 

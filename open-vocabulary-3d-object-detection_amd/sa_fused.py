@@ -1,0 +1,196 @@
+"""Fused training path of the set-abstraction MLP + max-pool (ov3d_sa_* kernels).
+
+Replaces, for training under bf16 autocast, the SharedMLP([3, C1, C2, C3]) +
+F.max_pool2d([1, nsample]) of PointnetSAModuleVotes (reference
+models/model_3detr.py:353-362; pointnet2 pytorch_utils.SharedMLP: 1x1 conv
+without bias -> BatchNorm (batch statistics) -> ReLU per layer).
+
+Forward (csrc/sa_mlp.hip):
+  layer 1  ov3d_sa_l1_fwd      x0 (R,3) f32 -> y1 bf16 + BN partials
+  layer 2  ov3d_sa_layer_fwd   relu(bn1(y1)) -> MFMA W2 -> y2 bf16 + partials (z1 kept)
+  layer 3  ov3d_sa_layer_pool_fwd  relu(bn2(y2)) -> MFMA W3 -> per-centroid max/min of
+           y3 (never stored) + partials (z2 kept);  ov3d_sa_pool_fwd applies bn3 + ReLU
+           to the max (or min when gamma*invstd < 0: relu(a*y+b) is monotone in y).
+Backward: the pooled gradient only reaches one row per (centroid, channel); the BN
+backward reductions over all R rows therefore come from P*C3 values
+(ov3d_sa_pool_bwd), and dy3 = cA*g + cB*y3 + cC is produced while recomputing y3
+(ov3d_sa_layer_dy).  dz2 = dy3 W3 and the weight gradients are hipBLASLt GEMMs;
+the layer-2/1 ReLU + BN backward are two row passes each (ov3d_bn_relu_bwd), the
+layer-1 weight gradient is reduced against x0 inside the last pass.
+
+BatchNorm semantics are torch's training batch_norm: biased variance to normalise,
+unbiased for running_var, momentum update, num_batches_tracked += 1; SyncBatchNorm
+all-reduces the per-channel sums (one all-reduce per layer, forward and backward).
+"""
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+from torch.autograd import Function
+
+from . import _native as nat
+from .gemm import weight_grad
+
+NPARTS_LAYER = 512     # persistent MFMA workgroups (2 per CU)
+NPARTS_ROWS = 1024     # row-pass workgroups
+NPARTS_POOL = 256
+
+
+def _bn(layer):
+    return layer.bn.bn
+
+
+def _sync_group(bn):
+    if isinstance(bn, nn.SyncBatchNorm) and dist.is_available() and dist.is_initialized() \
+            and dist.get_world_size(bn.process_group) > 1:
+        return bn.process_group if bn.process_group is not None else dist.group.WORLD
+    return None
+
+
+def supported(mlp, x0, S):
+    """True when the fused path applies (else the caller runs the unfused rows path)."""
+    if not (x0.is_cuda and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        return False
+    layers = list(mlp)
+    if len(layers) != 3 or x0.requires_grad or x0.dim() != 2 or x0.shape[1] != 3:
+        return False
+    if S not in (32, 64) or x0.shape[0] % 64:
+        return False
+    dims = [3]
+    for l in layers:
+        if not hasattr(l, "bn") or l.conv.bias is not None:
+            return False
+        bn = _bn(l)
+        if not bn.training or not bn.track_running_stats or bn.momentum is None or not bn.affine:
+            return False
+        dims.append(l.conv.weight.shape[0])
+    c1, c2, c3 = dims[1:]
+    lib = nat.load()
+    return (256 % c1 == 0 and 256 % c3 == 0 and lib.ov3d_sa_layer_supported(c1, c2) == 1
+            and lib.ov3d_sa_layer_supported(c2, c3) == 1
+            and all(c % 8 == 0 and 256 % (c // 8) == 0 for c in (c1, c2)))
+
+
+def _totals(partials, nparts, width, group):
+    tot = torch.empty(width, dtype=torch.float64, device=partials.device)
+    nat.call("ov3d_reduce_partials", partials, nparts, width, tot, like=partials)
+    if group is not None:
+        dist.all_reduce(tot, group=group)
+    return tot
+
+
+def _finalize(tot, count, bn, C):
+    dev = tot.device
+    mean, invstd, scale, shift = (torch.empty(C, dtype=torch.float32, device=dev) for _ in range(4))
+    bn.num_batches_tracked.add_(1)
+    nat.call("ov3d_bn_finalize", tot, float(count), C, bn.weight, bn.bias, float(bn.eps),
+             float(bn.momentum), bn.running_mean, bn.running_var, mean, invstd, scale, shift, like=tot)
+    return mean, invstd, scale, shift
+
+
+def _bwd_coefs(tot, count, gamma, mean, invstd, C):
+    dev = tot.device
+    cA, cB, cC, dg, db = (torch.empty(C, dtype=torch.float32, device=dev) for _ in range(5))
+    nat.call("ov3d_bn_bwd_finalize", tot, float(count), C, gamma, mean, invstd, cA, cB, cC, dg, db,
+             like=tot)
+    return cA, cB, cC, dg, db
+
+
+class _SAMLPPool(Function):
+    @staticmethod
+    def forward(ctx, x0, w1, w2, w3, g1, b1, g2, b2, g3, b3, bns, S):
+        dev = x0.device
+        R = x0.shape[0]
+        P = R // S
+        c1, c2, c3 = w1.shape[0], w2.shape[0], w3.shape[0]
+        groups = [_sync_group(bn) for bn in bns]
+        world = [dist.get_world_size(g) if g is not None else 1 for g in groups]
+        x0 = x0.contiguous()
+        bf = torch.bfloat16
+        # layer 1
+        y1 = torch.empty((R, c1), dtype=bf, device=dev)
+        parts = torch.empty((NPARTS_ROWS, 2, c1), dtype=torch.float64, device=dev)
+        nat.call("ov3d_sa_l1_fwd", x0, w1.float().contiguous(), R, c1, y1, parts, NPARTS_ROWS, like=x0)
+        st1 = _finalize(_totals(parts, NPARTS_ROWS, 2 * c1, groups[0]), R * world[0], bns[0], c1)
+        # layer 2
+        w2b = w2.to(bf).contiguous()
+        z1 = torch.empty((R, c1), dtype=bf, device=dev)
+        y2 = torch.empty((R, c2), dtype=bf, device=dev)
+        parts = torch.empty((NPARTS_LAYER, 2, c2), dtype=torch.float64, device=dev)
+        nat.call("ov3d_sa_layer_fwd", y1, st1[2], st1[3], w2b, R, c1, c2, z1, y2, parts, NPARTS_LAYER,
+                 like=x0)
+        st2 = _finalize(_totals(parts, NPARTS_LAYER, 2 * c2, groups[1]), R * world[1], bns[1], c2)
+        # layer 3 + pool
+        w3b = w3.to(bf).contiguous()
+        z2 = torch.empty((R, c2), dtype=bf, device=dev)
+        pmax, pmin = (torch.empty((P, c3), dtype=torch.float32, device=dev) for _ in range(2))
+        imax, imin = (torch.empty((P, c3), dtype=torch.uint8, device=dev) for _ in range(2))
+        parts = torch.empty((NPARTS_LAYER, 2, c3), dtype=torch.float64, device=dev)
+        nat.call("ov3d_sa_layer_pool_fwd", y2, st2[2], st2[3], w3b, R, c2, c3, S, z2, pmax, pmin,
+                 imax, imin, parts, NPARTS_LAYER, like=x0)
+        st3 = _finalize(_totals(parts, NPARTS_LAYER, 2 * c3, groups[2]), R * world[2], bns[2], c3)
+        out = torch.empty((P, c3), dtype=torch.float32, device=dev)
+        ysel = torch.empty((P, c3), dtype=torch.float32, device=dev)
+        isel = torch.empty((P, c3), dtype=torch.uint8, device=dev)
+        nat.call("ov3d_sa_pool_fwd", pmax, pmin, imax, imin, st3[2], st3[3], P, c3, out, ysel, isel,
+                 like=x0)
+        ctx.save_for_backward(x0, y1, z1, y2, z2, w2b, w3b, g1, g2, g3, ysel, isel, *st1, *st2, *st3)
+        ctx.meta = (R, S, P, c1, c2, c3, groups, world, tuple(w1.shape))
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (x0, y1, z1, y2, z2, w2b, w3b, g1, g2, g3, ysel, isel,
+         m1, i1, a1, s1, m2, i2, a2, s2, m3, i3, a3, s3) = ctx.saved_tensors
+        R, S, P, c1, c2, c3, groups, world, w1shape = ctx.meta
+        dev = x0.device
+        bf = torch.bfloat16
+        dout = dout.float().contiguous()
+        # layer 3: pooled gradient -> BN backward coefficients -> dy3 (recomputed y3)
+        gsel = torch.empty((P, c3), dtype=torch.float32, device=dev)
+        parts = torch.empty((NPARTS_POOL, 2, c3), dtype=torch.float64, device=dev)
+        nat.call("ov3d_sa_pool_bwd", dout, ysel, a3, s3, m3, i3, P, c3, gsel, parts, NPARTS_POOL,
+                 like=dout)
+        cA, cB, cC, dg3, db3 = _bwd_coefs(_totals(parts, NPARTS_POOL, 2 * c3, groups[2]),
+                                          R * world[2], g3, m3, i3, c3)
+        dy3 = torch.empty((R, c3), dtype=bf, device=dev)
+        nat.call("ov3d_sa_layer_dy", y2, a2, s2, w3b, R, c2, c3, S, gsel, isel, cA, cB, cC, dy3,
+                 NPARTS_LAYER, like=dout)
+        dw3 = weight_grad(dy3, z2)
+        dz2 = torch.mm(dy3, w3b)
+        del dy3
+        # layer 2: ReLU + BN backward (two row passes), dz1 and dW2
+        parts = torch.empty((NPARTS_ROWS, 2, c2), dtype=torch.float64, device=dev)
+        nat.call("ov3d_bn_relu_bwd", 0, dz2, y2, a2, s2, m2, i2, None, None, None, None, R, c2, parts,
+                 None, NPARTS_ROWS, like=dout)
+        cA, cB, cC, dg2, db2 = _bwd_coefs(_totals(parts, NPARTS_ROWS, 2 * c2, groups[1]),
+                                          R * world[1], g2, m2, i2, c2)
+        dy2 = torch.empty((R, c2), dtype=bf, device=dev)
+        nat.call("ov3d_bn_relu_bwd", 1, dz2, y2, a2, s2, None, None, cA, cB, cC, None, R, c2, None,
+                 dy2, NPARTS_ROWS, like=dout)
+        del dz2
+        dw2 = weight_grad(dy2, z1)
+        dz1 = torch.mm(dy2, w2b)
+        del dy2
+        # layer 1: ReLU + BN backward, dW1 reduced against x0 (dy1 never stored)
+        parts = torch.empty((NPARTS_ROWS, 2, c1), dtype=torch.float64, device=dev)
+        nat.call("ov3d_bn_relu_bwd", 0, dz1, y1, a1, s1, m1, i1, None, None, None, None, R, c1, parts,
+                 None, NPARTS_ROWS, like=dout)
+        cA, cB, cC, dg1, db1 = _bwd_coefs(_totals(parts, NPARTS_ROWS, 2 * c1, groups[0]),
+                                          R * world[0], g1, m1, i1, c1)
+        parts = torch.empty((NPARTS_ROWS, c1, 3), dtype=torch.float64, device=dev)
+        nat.call("ov3d_bn_relu_bwd", 2, dz1, y1, a1, s1, None, None, cA, cB, cC, x0, R, c1, parts,
+                 None, NPARTS_ROWS, like=dout)
+        dw1 = _totals(parts, NPARTS_ROWS, 3 * c1, None).view(c1, 3).float().view(w1shape)
+        return (None, dw1, dw2.view(c2, c1), dw3.view(c3, c2), dg1, db1, dg2, db2, dg3, db3, None,
+                None)
+
+
+def sa_mlp_pool(mlp, x0, S):
+    """(R, 3) grouped xyz rows -> (R / S, C3) pooled features (fp32), fused training path."""
+    layers = list(mlp)
+    ws = [l.conv.weight for l in layers]
+    ws = [w.view(w.shape[0], w.shape[1]) for w in ws]
+    bns = tuple(_bn(l) for l in layers)
+    return _SAMLPPool.apply(x0, ws[0], ws[1], ws[2], bns[0].weight, bns[0].bias, bns[1].weight,
+                            bns[1].bias, bns[2].weight, bns[2].bias, bns, S)

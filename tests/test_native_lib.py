@@ -25,6 +25,27 @@ def test_library_exports_every_header_symbol():
     assert set(syms) == set(_native.EXPORTS)
 
 
+def test_ctypes_signatures_match_header_arity():
+    """_native._SIGS (argument kinds incl. the trailing stream) vs the header prototypes."""
+    from ov3d_amd import _native
+    src = open(os.path.join(ROOT, "include", "ov3d.h")).read()
+    protos = dict(re.findall(r"^int\s+(ov3d_\w+)\(([^)]*)\);", src, flags=re.M))
+    for name, sig in _native._SIGS.items():
+        params = [a.strip() for a in protos[name].split(",")]
+        assert len(params) == len(sig), (name, len(params), len(sig))
+        for a, k in zip(params, sig):
+            if "*" in a:
+                assert k == "p", (name, a)
+            elif a.startswith("double"):
+                assert k == "d", (name, a)
+            elif a.startswith("float"):
+                assert k == "f", (name, a)
+            elif a.startswith("long long"):
+                assert k == "l", (name, a)
+            else:
+                assert k == "i", (name, a)
+
+
 def test_version_string():
     from ov3d_amd import _native
     assert "gfx950" in _native.version()

@@ -1,0 +1,152 @@
+"""Fused SA MLP (csrc/sa_mlp.hip via sa_fused.py) on the GPU.
+
+Floating-point kernels: checked against plain PyTorch fp32 computations.
+  * kernel level, on identical bf16 inputs: each layer's GEMM + folded BN + ReLU, the
+    BN statistics, the pooled max / arg rows (tolerance: one bf16 ulp of the output,
+    accumulation order differs);
+  * module level: PointnetSAModuleVotes training step under bf16 autocast (fused) vs
+    the same module in fp32 (unfused rows path = reference semantics): outputs,
+    running statistics and every parameter gradient within bf16 tolerances.
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import ov3d
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a = a.double()
+    b = b.double()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-12))
+
+
+def test_layer_kernel_matches_torch(cuda):
+    from ov3d_amd import _native as nat
+    g = torch.Generator(device="cpu").manual_seed(0)
+    R, K, N = 64 * 300, 64, 128
+    y = (torch.randn(R, K, generator=g) * 2).to(torch.bfloat16).to(cuda)
+    sc = (torch.randn(K, generator=g)).to(cuda)
+    sh = (torch.randn(K, generator=g) * 0.5).to(cuda)
+    W = (torch.randn(N, K, generator=g) * 0.2).to(torch.bfloat16).to(cuda)
+    z = torch.empty(R, K, dtype=torch.bfloat16, device=cuda)
+    out = torch.empty(R, N, dtype=torch.bfloat16, device=cuda)
+    parts = torch.empty(64, 2, N, dtype=torch.float64, device=cuda)
+    nat.call("ov3d_sa_layer_fwd", y, sc, sh, W, R, K, N, z, out, parts, 64, like=y)
+    zr = torch.relu(torch.addcmul(sh, sc, y.float())).to(torch.bfloat16)
+    zr2 = torch.relu(sc * y.float() + sh).to(torch.bfloat16)
+    # fmaf vs mul+add may differ by an ulp before rounding: accept either
+    assert ((z == zr) | (z == zr2)).float().mean().item() > 0.999
+    ref = z.float() @ W.float().t()
+    assert _rel(out.float(), ref) < 8e-3
+    tot = parts.sum(0)
+    o = out.double()
+    torch.testing.assert_close(tot[0], o.sum(0), rtol=1e-5, atol=1e-2)   # fp32 per-lane sums
+    torch.testing.assert_close(tot[1], (o * o).sum(0), rtol=1e-5, atol=1e-2)
+
+
+@pytest.mark.parametrize("S", [64, 32])
+def test_pool_kernel_max_min_rows(cuda, S):
+    from ov3d_amd import _native as nat
+    g = torch.Generator(device="cpu").manual_seed(1)
+    R, K, N = 64 * 128, 128, 256
+    y = torch.randn(R, K, generator=g).to(torch.bfloat16).to(cuda)
+    sc = torch.rand(K, generator=g).to(cuda) + 0.5
+    sh = torch.randn(K, generator=g).to(cuda) * 0.1
+    W = (torch.randn(N, K, generator=g) * 0.1).to(torch.bfloat16).to(cuda)
+    P = R // S
+    pmax, pmin = (torch.empty(P, N, device=cuda) for _ in range(2))
+    imax, imin = (torch.empty(P, N, dtype=torch.uint8, device=cuda) for _ in range(2))
+    parts = torch.empty(32, 2, N, dtype=torch.float64, device=cuda)
+    z = torch.empty(R, K, dtype=torch.bfloat16, device=cuda)
+    nat.call("ov3d_sa_layer_pool_fwd", y, sc, sh, W, R, K, N, S, z, pmax, pmin, imax, imin, parts,
+             32, like=y)
+    yf = (z.float() @ W.float().t()).to(torch.bfloat16).float().view(P, S, N)
+    assert _rel(pmax, yf.max(1).values) < 8e-3
+    assert _rel(pmin, yf.min(1).values) < 8e-3
+    # the recorded rows hold the recorded extremes (up to accumulation-order ulps)
+    at_max = torch.gather(yf, 1, imax.long()[:, None, :])[:, 0]
+    at_min = torch.gather(yf, 1, imin.long()[:, None, :])[:, 0]
+    assert (at_max - pmax).abs().max().item() <= 0.02 * pmax.abs().max().item()
+    assert (at_min - pmin).abs().max().item() <= 0.02 * pmin.abs().max().item()
+    assert int(imax.max()) < S and int(imin.max()) < S
+
+
+def _sa_copies(cuda, n, seed=0):
+    from ov3d_amd.pointnet2_modules import PointnetSAModuleVotes
+    torch.manual_seed(seed)
+    sa = PointnetSAModuleVotes(radius=0.2, nsample=64, npoint=2048, mlp=[0, 64, 128, 256],
+                               normalize_xyz=True).to(cuda).train()
+    with torch.no_grad():   # non-trivial BN affine, some negative gammas (min-pool branch)
+        for layer in sa.mlp_module:
+            bn = layer.bn.bn
+            bn.weight.copy_(torch.randn_like(bn.weight) * 0.5 + 0.6)
+            bn.bias.copy_(torch.randn_like(bn.bias) * 0.2)
+    return [copy.deepcopy(sa) for _ in range(n)]
+
+
+def _run(sa, xyz, gw, amp, fused, monkeypatch):
+    from ov3d_amd import sa_fused
+    if not fused:
+        monkeypatch.setattr(sa_fused, "supported", lambda *a: False)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+        _, f, inds = sa(xyz)
+    monkeypatch.undo()
+    (f.float() * gw).sum().backward()
+    return f.detach().float(), inds, {n: p.grad for n, p in sa.named_parameters()}
+
+
+def test_sa_module_fused_vs_fp32_reference(cuda, monkeypatch):
+    """fused bf16 vs fp32 reference: outputs / running stats within bf16 tolerance, and every
+    gradient no further from fp32 than PyTorch's own bf16-autocast path (+ slack)."""
+    from ov3d_amd import synthetic
+    ref, unf, fus = _sa_copies(cuda, 3)
+    xyz = synthetic.make_batch(4, seed=5, device=cuda)["point_clouds"]
+    gw = torch.randn(4, 256, 2048, device=cuda)
+    f_ref, i_ref, g_ref = _run(ref, xyz, gw, False, False, monkeypatch)
+    f_unf, _, g_unf = _run(unf, xyz, gw, True, False, monkeypatch)
+    f_fus, i_fus, g_fus = _run(fus, xyz, gw, True, True, monkeypatch)
+    assert torch.equal(i_fus, i_ref)
+    assert f_fus.shape == f_ref.shape == (4, 256, 2048)
+    e_out, e_out_unf = _rel(f_fus, f_ref), _rel(f_unf, f_ref)
+    assert e_out < 3e-2, (e_out, e_out_unf)
+    for lf, lr in zip(fus.mlp_module, ref.mlp_module):
+        bf, br = lf.bn.bn, lr.bn.bn
+        assert int(bf.num_batches_tracked) == int(br.num_batches_tracked) == 1
+        assert _rel(bf.running_mean, br.running_mean) < 2e-2
+        assert _rel(bf.running_var, br.running_var) < 2e-2
+    report = {n: (round(_rel(g_fus[n], g_ref[n]), 4), round(_rel(g_unf[n], g_ref[n]), 4))
+              for n in g_ref}
+    print("grad rel err (fused, torch-bf16):", report)
+    for n, (ef, eu) in report.items():
+        assert ef <= max(2.0 * eu, 3e-2), (n, ef, eu)
+
+
+def test_model_step_uses_fused_sa_and_trains(cuda):
+    """Full-size bf16 step: the pre-encoder SA runs the fused kernels, loss finite."""
+    import ov3d_amd
+    from ov3d_amd import _native, synthetic
+    from ov3d_amd.dataset_config import SunrgbdDatasetConfig
+    from bench import default_args
+    args = default_args()
+    cfg = SunrgbdDatasetConfig()
+    torch.manual_seed(0)
+    model, _ = ov3d_amd.build_model(args, cfg, text_embedding=synthetic.text_embedding())
+    model = model.to(cuda).train()
+    crit = ov3d_amd.build_criterion(args, cfg).to(cuda)
+    batch = synthetic.make_batch(8, seed=2, device=cuda)
+    _native.timing_enable(["ov3d_sa_layer_pool_fwd", "ov3d_sa_layer_dy"])
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = model({k: batch[k] for k in ("point_clouds", "point_cloud_dims_min",
+                                           "point_cloud_dims_max")})
+    loss, _ = crit(out, batch)
+    loss.backward()
+    t = _native.timing_collect()
+    assert len(t["ov3d_sa_layer_pool_fwd"]) == 1 and len(t["ov3d_sa_layer_dy"]) == 1
+    assert torch.isfinite(loss)
+    w = model.pre_encoder.mlp_module.layer0.conv.weight
+    assert w.grad is not None and torch.isfinite(w.grad).all() and w.grad.abs().sum() > 0
