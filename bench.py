@@ -12,7 +12,7 @@ metric: scenes/sec (train step); weak scaling (8 scenes per GPU), DDP over RCCL.
 
 Rank 0 prints ONE JSON line.  It carries a `roofline` object for the dominant
 hand-written kernel (ov3d_fps, timed with HIP events on its launch stream; inside
-the timed region in eager mode, right after it when the step replays hipGraphs) and a `cpu_baseline` (the CPU port of the same step: the
+the timed region in eager mode, right after it when the step replays a hipGraph) and a `cpu_baseline` (the CPU port of the same step: the
 oracle's C restatement for the index kernels + PyTorch-CPU dense layers, a
 bounded sample, rank 0 only, N=1 only).
 """
@@ -52,7 +52,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build(args, device, ddp=False):
+def build(args, device, ddp=False, capturable=False):
     ov3d = ov3d_import.load()
     from ov3d_amd import synthetic
     from ov3d_amd.dataset_config import SunrgbdDatasetConfig
@@ -67,20 +67,19 @@ def build(args, device, ddp=False):
     crit = ov3d.build_criterion(args, cfg).to(device)
     params = [p for p in model.parameters() if p.requires_grad]
     try:
-        opt = torch.optim.AdamW(params, lr=args.base_lr, weight_decay=args.weight_decay, fused=True)
+        opt = torch.optim.AdamW(params, lr=args.base_lr, weight_decay=args.weight_decay, fused=True,
+                                capturable=capturable)
     except Exception:  # fused AdamW unavailable -> multi-tensor
-        opt = torch.optim.AdamW(params, lr=args.base_lr, weight_decay=args.weight_decay)
+        opt = torch.optim.AdamW(params, lr=args.base_lr, weight_decay=args.weight_decay,
+                                capturable=capturable)
     return model, crit, opt
 
 
-def train_step(model, crit, opt, batch, args, amp_dtype, graphed=None):
+def train_step(model, crit, opt, batch, args, amp_dtype):
     opt.zero_grad(set_to_none=True)
     inputs = {k: batch[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")}
-    if graphed is not None:
-        out = graphed(inputs)          # replays the captured forward (and, in backward, backward)
-    else:
-        with torch.autocast("cuda", dtype=amp_dtype, enabled=amp_dtype is not None):
-            out = model(inputs)
+    with torch.autocast("cuda", dtype=amp_dtype, enabled=amp_dtype is not None):
+        out = model(inputs)
     loss, _ = crit(out, batch)
     loss.backward()
     torch.nn.utils.clip_grad_norm_(model.parameters(), args.clip_gradient)
@@ -144,14 +143,16 @@ def cpu_baseline(args, batch_size=1, steps=2):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=30)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=50)      # >= 50 timed steps
+    p.add_argument("--warmup", type=int, default=10)     # after 10 warm-up steps
     p.add_argument("--batch", type=int, default=8)
     p.add_argument("--points", type=int, default=20000)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled")
-    p.add_argument("--no-graph", action="store_true", help="eager forward/backward (no hipGraph)")
+    p.add_argument("--eager", "--no-graph", dest="eager", action="store_true",
+                   help="launch the step eagerly (default at N>1); at N=1 the whole step is "
+                        "captured once and replayed as one hipGraph (graphs.StepGraph)")
     cli = p.parse_args()
 
     ov3d = ov3d_import.load()
@@ -161,16 +162,23 @@ def main():
     torch.cuda.set_device(device)
     args = default_args()
     amp = torch.bfloat16 if cli.dtype == "bf16" else None
-    model, crit, opt = build(args, device, ddp=world > 1)
+    use_graph = world == 1 and not cli.eager
+    model, crit, opt = build(args, device, ddp=world > 1, capturable=use_graph)
     pool = [synthetic.make_batch(cli.batch, seed=1000 * rank + i, num_points=cli.points, device=device)
             for i in range(cli.pool)]
 
     graphed = None
-    if world == 1 and not cli.no_graph:
-        from ov3d_amd.graphs import GraphedModel
-        graphed = GraphedModel(model, pool[0], amp_dtype=amp)
+    if use_graph:
+        from ov3d_amd.graphs import StepGraph
+        graphed = StepGraph(model, crit, opt, pool[0], amp_dtype=amp, clip=args.clip_gradient)
+
+    def step(i):
+        if graphed is not None:
+            return graphed.step(pool[i % cli.pool])
+        return train_step(model, crit, opt, pool[i % cli.pool], args, amp)
+
     for i in range(cli.warmup):
-        train_step(model, crit, opt, pool[i % cli.pool], args, amp, graphed)
+        step(i)
     torch.cuda.synchronize()
     dist.barrier()
 
@@ -180,7 +188,7 @@ def main():
     dist.barrier()
     t0 = time.perf_counter()
     for i in range(cli.steps):
-        loss = train_step(model, crit, opt, pool[i % cli.pool], args, amp, graphed)
+        loss = step(i)
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0

@@ -252,14 +252,24 @@ __global__ __launch_bounds__(kThreads) void sa_l1_kernel(const float* __restrict
     }
 }
 
-// (nparts, 2, C) fp64 partials -> (2, C) totals; one thread per (k, c).
-__global__ void reduce_partials_kernel(const double* __restrict__ partials, int nparts, int C2,
-                                       double* __restrict__ totals) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= C2) return;
+// (nparts, width) fp64 partials -> (width) totals.  Block: 64 columns x 16 partial
+// lanes (coalesced 512-B rows), fixed summation order (deterministic).
+__global__ __launch_bounds__(1024) void reduce_partials_kernel(const double* __restrict__ partials,
+                                                               int nparts, int width,
+                                                               double* __restrict__ totals) {
+    __shared__ double red[16][64];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63), pl = threadIdx.x >> 6;
     double s = 0;
-    for (int w = 0; w < nparts; ++w) s += partials[(size_t)w * C2 + i];
-    totals[i] = s;
+    if (c < width)
+        for (int w = pl; w < nparts; w += 16) s += partials[(size_t)w * width + c];
+    red[pl][threadIdx.x & 63] = s;
+    __syncthreads();
+    if (pl == 0 && c < width) {
+        double t = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) t += red[k][threadIdx.x];
+        totals[c] = t;
+    }
 }
 
 // Training BatchNorm from totals (sum, sum of squares) over `count` rows:
@@ -550,7 +560,7 @@ extern "C" int ov3d_sa_layer_dy(const void* yprev, const float* scale, const flo
 extern "C" int ov3d_reduce_partials(const double* partials, int nparts, int width, double* totals,
                                     void* stream) {
     if (nparts <= 0 || width <= 0 || !partials || !totals) return OV3D_EINVAL;
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3(ov3d_cdiv(width, 256)), dim3(256), 0,
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3(ov3d_cdiv(width, 64)), dim3(1024), 0,
                        ov3d_stream(stream), partials, nparts, width, totals);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;

@@ -8,6 +8,8 @@ BLAS as one GEMM it runs on 7-21 workgroups of the 256 CUs (1.4-2.1 ms per SA la
 measured: profiles/r01_kernel_stats_v2.csv).  Here the reduction is split into
 row chunks computed as one batched GEMM (>= ~256 workgroups) and summed in fp32.
 """
+import weakref
+
 import torch
 from torch.autograd import Function
 
@@ -50,16 +52,57 @@ def weight_grad(dy, x):
     return torch.sum(part, dim=0, dtype=torch.float32)
 
 
+# bf16 copies of the fp32 parameters used under autocast.  Casting per call costs a kernel
+# per weight and bias per step (~300 launches); instead every stale copy is refreshed with
+# ONE multi-tensor copy the first time a parameter changed by the optimizer (its version
+# counter moved) is used.  Disabled while a hipGraph is captured (graphs.py), where a host
+# side version check would not be replayed.
+SHADOW_CACHE = True
+_SHADOWS = {}   # id(base parameter) -> [weakref(base), bf16 copy, version copied]
+
+
+def refresh_shadows(force=False):
+    """Re-copy every stale (or, with force, every) registered parameter in one multi-tensor
+    copy.  A captured step graph calls this with force=True at its start."""
+    dead = [k for k, e in _SHADOWS.items() if e[0]() is None]
+    for k in dead:
+        del _SHADOWS[k]
+    stale = [e for e in _SHADOWS.values() if force or e[2] != e[0]()._version]
+    if stale:
+        with torch.no_grad():
+            torch._foreach_copy_([e[1] for e in stale], [e[0]() for e in stale])
+        for e in stale:
+            e[2] = e[0]()._version
+
+
+def cast_param(w, dt):
+    """w (a parameter or a view of one) as `dt`, from the shared refreshed copies."""
+    if w is None or w.dtype == dt:
+        return w
+    base = w if w._base is None else w._base
+    if not (SHADOW_CACHE and w.is_cuda and base.is_leaf and base.requires_grad
+            and base.dtype == torch.float32 and dt == torch.bfloat16):
+        return w.to(dt)
+    e = _SHADOWS.get(id(base))
+    if e is None or e[0]() is not base:
+        e = [weakref.ref(base), torch.empty_like(base, dtype=dt), -1]
+        _SHADOWS[id(base)] = e
+    if e[2] != base._version and not torch.cuda.is_current_stream_capturing():
+        refresh_shadows()
+    sh = e[1]
+    if w is base:
+        return sh
+    return sh.as_strided(w.size(), w.stride(), w.storage_offset() - base.storage_offset())
+
+
 class _RowsLinear(Function):
     @staticmethod
     def forward(ctx, x, w, b):
         dt = torch.get_autocast_dtype("cuda") if (x.is_cuda and torch.is_autocast_enabled("cuda")) \
             else x.dtype
-        xc, wc = x.to(dt), w.to(dt)
+        xc, wc = x.to(dt), cast_param(w, dt)
         with torch.autocast("cuda", enabled=False):
-            y = xc @ wc.t()
-            if b is not None:
-                y = y + b.to(dt)
+            y = torch.nn.functional.linear(xc, wc, cast_param(b, dt))   # bias in the GEMM epilogue
         ctx.save_for_backward(xc, wc)
         ctx.meta = (x.dtype, w.dtype, b is not None)
         return y

@@ -28,7 +28,7 @@ import torch.nn as nn
 from torch.autograd import Function
 
 from . import _native as nat
-from .gemm import weight_grad
+from .gemm import cast_param, weight_grad
 
 NPARTS_LAYER = 512     # persistent MFMA workgroups (2 per CU)
 NPARTS_ROWS = 1024     # row-pass workgroups
@@ -113,7 +113,7 @@ class _SAMLPPool(Function):
         nat.call("ov3d_sa_l1_fwd", x0, w1.float().contiguous(), R, c1, y1, parts, NPARTS_ROWS, like=x0)
         st1 = _finalize(_totals(parts, NPARTS_ROWS, 2 * c1, groups[0]), R * world[0], bns[0], c1)
         # layer 2
-        w2b = w2.to(bf).contiguous()
+        w2b = cast_param(w2, bf).contiguous()
         z1 = torch.empty((R, c1), dtype=bf, device=dev)
         y2 = torch.empty((R, c2), dtype=bf, device=dev)
         parts = torch.empty((NPARTS_LAYER, 2, c2), dtype=torch.float64, device=dev)
@@ -121,7 +121,7 @@ class _SAMLPPool(Function):
                  like=x0)
         st2 = _finalize(_totals(parts, NPARTS_LAYER, 2 * c2, groups[1]), R * world[1], bns[1], c2)
         # layer 3 + pool
-        w3b = w3.to(bf).contiguous()
+        w3b = cast_param(w3, bf).contiguous()
         z2 = torch.empty((R, c2), dtype=bf, device=dev)
         pmax, pmin = (torch.empty((P, c3), dtype=torch.float32, device=dev) for _ in range(2))
         imax, imin = (torch.empty((P, c3), dtype=torch.uint8, device=dev) for _ in range(2))
