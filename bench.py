@@ -150,6 +150,8 @@ def main():
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled")
+    p.add_argument("--no-prefetch", action="store_true",
+                   help="do not overlap the next batch's pre-encoder FPS with this step")
     p.add_argument("--eager", "--no-graph", dest="eager", action="store_true",
                    help="launch the step eagerly (default at N>1); at N=1 the whole step is "
                         "captured once and replayed as one hipGraph (graphs.StepGraph)")
@@ -170,11 +172,12 @@ def main():
     graphed = None
     if use_graph:
         from ov3d_amd.graphs import StepGraph
-        graphed = StepGraph(model, crit, opt, pool[0], amp_dtype=amp, clip=args.clip_gradient)
+        graphed = StepGraph(model, crit, opt, pool[0], amp_dtype=amp, clip=args.clip_gradient,
+                            prefetch_fps=not cli.no_prefetch)
 
     def step(i):
         if graphed is not None:
-            return graphed.step(pool[i % cli.pool])
+            return graphed.step(pool[i % cli.pool], pool[(i + 1) % cli.pool])
         return train_step(model, crit, opt, pool[i % cli.pool], args, amp)
 
     for i in range(cli.warmup):

@@ -22,8 +22,14 @@ solver) and the optimizer stay eager between the two replays.  Results are the
 eager results (same kernels, same order); dropout draws from the graph-safe
 Philox generator.
 """
+import os
+
 import torch
 import torch.nn as nn
+
+# measurement-only switch (tools/, never in bench numbers): drop the prefetched FPS from the
+# graph to see the step's critical path without it
+_EXP_NO_FPS = os.environ.get("OV3D_EXP_NO_FPS") == "1"
 
 OUT_KEYS = ("visual_embeds", "sem_cls_logits", "center_normalized", "center_unnormalized",
             "size_normalized", "size_unnormalized", "angle_logits", "angle_residual",
@@ -70,29 +76,61 @@ class StepGraph:
     """Replays forward + criterion + backward + clip_grad_norm_ + optimizer.step.
 
     model, crit: as for an eager step; opt must be built with capturable=True.
-    sample: a batch dict (device tensors) fixing the static shapes."""
+    sample: a batch dict (device tensors) fixing the static shapes.
+
+    Sampling prefetch (prefetch_fps=True): the pre-encoder's furthest-point
+    sampling depends on the input points only, and runs on 8 of the 256 CUs for
+    ~3 ms.  Inside the graph it is computed for the NEXT batch on a side stream,
+    concurrently with this batch's forward/backward, and handed to the next
+    replay (Model3DETR.run_encoder(pre_enc_inds=...)).  Each step still samples
+    exactly one batch; results are identical.  step(batch, next_batch) keeps the
+    pipeline primed; a batch that was not announced as `next_batch` is sampled
+    eagerly first."""
 
     def __init__(self, model, crit, opt, sample, amp_dtype=torch.bfloat16, clip=0.1,
-                 warmup_iters=3):
+                 warmup_iters=3, prefetch_fps=True):
         from . import gemm
+        from . import pointnet2_utils as pu
         self.model, self.crit, self.opt = model, crit, opt
         self.amp_dtype, self.clip = amp_dtype, clip
         self.static = {k: v.clone() for k, v in sample.items()}
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
+        self.prefetch = prefetch_fps and hasattr(model, "pre_encoder")
+        self._pu = pu
+        self._expected = None
+        if self.prefetch:
+            self.npoint = model.pre_encoder.npoint
+            self.next_pc = self.static["point_clouds"].clone()
+            self.inds_cur = self._sample(self.static["point_clouds"])
+            self.inds_next = torch.empty_like(self.inds_cur)
+        self.side = torch.cuda.Stream()
+        self.side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.side):
             for _ in range(warmup_iters):
                 self._body(gemm)
-        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.current_stream().wait_stream(self.side)
+        if self.prefetch:
+            self.inds_cur.copy_(self._sample(self.static["point_clouds"]))
         self.graph = torch.cuda.CUDAGraph()
         self.opt.zero_grad(set_to_none=True)
         with torch.cuda.graph(self.graph):
             self.loss = self._body(gemm)
 
+    def _sample(self, pc):
+        return self._pu.furthest_point_sample(pc[..., 0:3].contiguous(), self.npoint)
+
     def _body(self, gemm):
+        cur = torch.cuda.current_stream()
+        if self.prefetch and not _EXP_NO_FPS:   # next batch's pre-encoder FPS, concurrent
+            fps_stream = torch.cuda.Stream() if not hasattr(self, "_fps_stream") else self._fps_stream
+            self._fps_stream = fps_stream
+            fps_stream.wait_stream(cur)
+            with torch.cuda.stream(fps_stream):
+                self.inds_next.copy_(self._sample(self.next_pc))
         gemm.refresh_shadows(force=True)   # captured: bf16 weight copies follow every update
         self.opt.zero_grad(set_to_none=True)
         inputs = {k: self.static[k] for k in IN_KEYS}
+        if self.prefetch:
+            inputs["pre_enc_inds"] = self.inds_cur
         with torch.autocast("cuda", dtype=self.amp_dtype or torch.float32,
                             enabled=self.amp_dtype is not None):
             out = self.model(inputs)
@@ -100,10 +138,19 @@ class StepGraph:
         loss.backward()
         torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.clip)
         self.opt.step()
+        if self.prefetch and not _EXP_NO_FPS:
+            cur.wait_stream(self._fps_stream)
+            self.inds_cur.copy_(self.inds_next)
         return loss.detach()
 
-    def step(self, batch):
+    def step(self, batch, next_batch=None):
         for k, v in self.static.items():
             v.copy_(batch[k], non_blocking=True)
+        if self.prefetch:
+            if self._expected is None or batch["point_clouds"] is not self._expected:
+                self.inds_cur.copy_(self._sample(self.static["point_clouds"]))
+            nb = next_batch if next_batch is not None else batch
+            self.next_pc.copy_(nb["point_clouds"], non_blocking=True)
+            self._expected = nb["point_clouds"]
         self.graph.replay()
         return self.loss

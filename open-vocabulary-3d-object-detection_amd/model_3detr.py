@@ -125,9 +125,12 @@ class Model3DETR(nn.Module):
         feats = pc[..., 3:].transpose(1, 2).contiguous() if pc.size(-1) > 3 else None
         return xyz, feats
 
-    def run_encoder(self, point_clouds):
+    def run_encoder(self, point_clouds, pre_enc_inds=None):
+        """pre_enc_inds: optional furthest-point-sample indices of the pre-encoder computed
+        ahead of time (they depend on the input points only; graphs.StepGraph computes the
+        next batch's on a side stream while this one trains).  Identical results."""
         xyz, feats = self._break_up_pc(point_clouds)
-        pre_xyz, pre_feats, pre_inds = self.pre_encoder(xyz, feats)
+        pre_xyz, pre_feats, pre_inds = self.pre_encoder(xyz, feats, inds=pre_enc_inds)
         # (B, C, M) view of channels-last rows -> seq-first (M, B, C)
         enc_xyz, enc_feats, enc_inds = self.encoder(pre_feats.permute(2, 0, 1).contiguous(), xyz=pre_xyz)
         if enc_inds is None:
@@ -198,7 +201,7 @@ class Model3DETR(nn.Module):
 
     def forward(self, inputs, encoder_only=False):
         pc = inputs["point_clouds"]
-        enc_xyz, enc_feats, _ = self.run_encoder(pc)                        # (N', B, C)
+        enc_xyz, enc_feats, _ = self.run_encoder(pc, inputs.get("pre_enc_inds"))   # (N', B, C)
         Np, B, C = enc_feats.shape
         enc_feats = self.encoder_to_decoder_projection.rows(enc_feats.reshape(Np * B, C)).view(Np, B, -1)
         if encoder_only:

@@ -186,7 +186,10 @@ def test_step_graph_equals_eager_step(cuda):
     b2 = synthetic.make_batch(2, seed=5, num_points=4096, device=cuda)
     amp = torch.bfloat16
     sg = StepGraph(twin, crit, opt_g, b1, amp_dtype=amp, clip=args.clip_gradient, warmup_iters=1)
-    train_step(model, crit, opt_e, b1, args, amp)          # the warm-up step the graph took
+    # start the eager side from the graph side's state (parameters, BN buffers, AdamW state):
+    # one step then differs only by run-to-run noise of atomics-based kernels
+    model.load_state_dict(twin.state_dict())
+    opt_e.load_state_dict(opt_g.state_dict())
     loss_e = train_step(model, crit, opt_e, b2, args, amp)
     loss_g = sg.step(b2)
     torch.cuda.synchronize()
