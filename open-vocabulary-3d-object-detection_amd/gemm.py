@@ -41,15 +41,17 @@ def _bmm_f32(a, b):
     return torch.bmm(a, b)
 
 
-def weight_grad(dy, x):
-    """dy (R, Cout), x (R, Cin) -> dy^T x (Cout, Cin) in fp32, split-K over R."""
+def weight_grad(dy, x, out=None):
+    """dy (R, Cout), x (R, Cin) -> dy^T x (Cout, Cin) in fp32, split-K over R
+    (written into `out`, a contiguous fp32 (Cout, Cin) tensor, when given)."""
     R, cout = dy.shape
     cin = x.shape[1]
     nc = _chunks(R, cout, cin)
     if nc == 1:
-        return _bmm_f32(dy.t()[None], x[None])[0].float()
+        g = _bmm_f32(dy.t()[None], x[None])[0].float()
+        return g if out is None else out.copy_(g)
     part = _bmm_f32(dy.view(nc, R // nc, cout).transpose(1, 2), x.view(nc, R // nc, cin))
-    return torch.sum(part, dim=0, dtype=torch.float32)
+    return torch.sum(part, dim=0, dtype=torch.float32, out=out)
 
 
 # bf16 copies of the fp32 parameters used under autocast.  Casting per call costs a kernel
@@ -127,3 +129,60 @@ def rows_linear(x, w, b=None):
     shape = x.shape
     y = _RowsLinear.apply(x.reshape(-1, shape[-1]), w, b)
     return y.view(*shape[:-1], w.shape[0])
+
+
+class _InProj(Function):
+    """Row blocks of one (3E, E) projection applied to different inputs:
+    y_g = x_g W[r0:r1]^T + b[r0:r1] (nn.MultiheadAttention's in_proj for self / cross
+    attention).  The backward writes each block's weight / bias gradient straight into
+    ONE (3E, E) / (3E,) gradient, instead of autograd's slice-backward (zero-fill the
+    full-size gradient, copy the block in, accumulate the three) per block."""
+
+    @staticmethod
+    def forward(ctx, w, b, spec, *xs):
+        dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else xs[0].dtype
+        wc, bc = cast_param(w, dt), cast_param(b, dt)
+        outs, saved = [], []
+        with torch.autocast("cuda", enabled=False):
+            for x, (r0, r1) in zip(xs, spec):
+                xc = x.reshape(-1, x.shape[-1]).to(dt)
+                y = torch.nn.functional.linear(xc, wc[r0:r1], bc[r0:r1] if bc is not None else None)
+                outs.append(y.view(*x.shape[:-1], r1 - r0))
+                saved.append(xc)
+        ctx.save_for_backward(wc, *saved)
+        ctx.meta = (spec, w.dtype, b is not None, tuple(x.dtype for x in xs),
+                    tuple(x.shape for x in xs))
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        wc, *xcs = ctx.saved_tensors
+        spec, wdt, has_b, xdts, xshapes = ctx.meta
+        dw = torch.empty(wc.shape, dtype=torch.float32, device=wc.device) \
+            if ctx.needs_input_grad[0] else None
+        db = torch.empty(wc.shape[0], dtype=torch.float32, device=wc.device) \
+            if has_b and ctx.needs_input_grad[1] else None
+        dxs = []
+        with torch.autocast("cuda", enabled=False):
+            for i, (dy, xc, (r0, r1)) in enumerate(zip(dys, xcs, spec)):
+                if dy is None:
+                    dy = torch.zeros(xc.shape[0], r1 - r0, dtype=xc.dtype, device=xc.device)
+                dy = dy.reshape(-1, r1 - r0).to(xc.dtype).contiguous()
+                dxs.append((dy @ wc[r0:r1]).to(xdts[i]).view(xshapes[i])
+                           if ctx.needs_input_grad[3 + i] else None)
+                if dw is not None:
+                    weight_grad(dy, xc, out=dw[r0:r1])
+                if db is not None:
+                    torch.sum(dy, dim=0, dtype=torch.float32, out=db[r0:r1])
+        return (dw.to(wdt) if dw is not None else None,
+                db.to(wdt) if db is not None else None, None, *dxs)
+
+
+def in_projection(w, b, groups):
+    """groups: sequence of (x, r0, r1) -> tuple of x W[r0:r1]^T + b[r0:r1]."""
+    xs = [g[0] for g in groups]
+    if not xs[0].is_cuda:
+        return tuple(torch.nn.functional.linear(x, w[r0:r1], b[r0:r1] if b is not None else None)
+                     for x, r0, r1 in groups)
+    spec = tuple((r0, r1) for _, r0, r1 in groups)
+    return _InProj.apply(w, b, spec, *xs)

@@ -22,14 +22,9 @@ solver) and the optimizer stay eager between the two replays.  Results are the
 eager results (same kernels, same order); dropout draws from the graph-safe
 Philox generator.
 """
-import os
-
 import torch
 import torch.nn as nn
 
-# measurement-only switch (tools/, never in bench numbers): drop the prefetched FPS from the
-# graph to see the step's critical path without it
-_EXP_NO_FPS = os.environ.get("OV3D_EXP_NO_FPS") == "1"
 
 OUT_KEYS = ("visual_embeds", "sem_cls_logits", "center_normalized", "center_unnormalized",
             "size_normalized", "size_unnormalized", "angle_logits", "angle_residual",
@@ -80,9 +75,9 @@ class StepGraph:
 
     Sampling prefetch (prefetch_fps=True): the pre-encoder's furthest-point
     sampling depends on the input points only, and runs on 8 of the 256 CUs for
-    ~3 ms.  Inside the graph it is computed for the NEXT batch on a side stream,
-    concurrently with this batch's forward/backward, and handed to the next
-    replay (Model3DETR.run_encoder(pre_enc_inds=...)).  Each step still samples
+    ~3 ms.  It is computed for the NEXT batch on its own stream, concurrently
+    with this batch's graph replay, and handed to the next replay
+    (Model3DETR.run_encoder(pre_enc_inds=...)).  Each step still samples
     exactly one batch; results are identical.  step(batch, next_batch) keeps the
     pipeline primed; a batch that was not announced as `next_batch` is sampled
     eagerly first."""
@@ -101,7 +96,7 @@ class StepGraph:
             self.npoint = model.pre_encoder.npoint
             self.next_pc = self.static["point_clouds"].clone()
             self.inds_cur = self._sample(self.static["point_clouds"])
-            self.inds_next = torch.empty_like(self.inds_cur)
+        self.fps_stream = torch.cuda.Stream()
         self.side = torch.cuda.Stream()
         self.side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.side):
@@ -119,13 +114,6 @@ class StepGraph:
         return self._pu.furthest_point_sample(pc[..., 0:3].contiguous(), self.npoint)
 
     def _body(self, gemm):
-        cur = torch.cuda.current_stream()
-        if self.prefetch and not _EXP_NO_FPS:   # next batch's pre-encoder FPS, concurrent
-            fps_stream = torch.cuda.Stream() if not hasattr(self, "_fps_stream") else self._fps_stream
-            self._fps_stream = fps_stream
-            fps_stream.wait_stream(cur)
-            with torch.cuda.stream(fps_stream):
-                self.inds_next.copy_(self._sample(self.next_pc))
         gemm.refresh_shadows(force=True)   # captured: bf16 weight copies follow every update
         self.opt.zero_grad(set_to_none=True)
         inputs = {k: self.static[k] for k in IN_KEYS}
@@ -138,19 +126,27 @@ class StepGraph:
         loss.backward()
         torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.clip)
         self.opt.step()
-        if self.prefetch and not _EXP_NO_FPS:
-            cur.wait_stream(self._fps_stream)
-            self.inds_cur.copy_(self.inds_next)
         return loss.detach()
 
     def step(self, batch, next_batch=None):
+        cur = torch.cuda.current_stream()
         for k, v in self.static.items():
             v.copy_(batch[k], non_blocking=True)
-        if self.prefetch:
-            if self._expected is None or batch["point_clouds"] is not self._expected:
-                self.inds_cur.copy_(self._sample(self.static["point_clouds"]))
-            nb = next_batch if next_batch is not None else batch
-            self.next_pc.copy_(nb["point_clouds"], non_blocking=True)
-            self._expected = nb["point_clouds"]
+        if not self.prefetch:
+            self.graph.replay()
+            return self.loss
+        if self._expected is None or batch["point_clouds"] is not self._expected:
+            self.inds_cur.copy_(self._sample(self.static["point_clouds"]))
+        nb = next_batch if next_batch is not None else batch
+        self.next_pc.copy_(nb["point_clouds"], non_blocking=True)
+        self._expected = nb["point_clouds"]
+        # the next batch's FPS runs on its own stream (own hardware queue), concurrently with
+        # this step's graph; the graph reads inds_cur only
+        self.fps_stream.wait_stream(cur)
+        with torch.cuda.stream(self.fps_stream):
+            nxt = self._sample(self.next_pc)
         self.graph.replay()
+        cur.wait_stream(self.fps_stream)
+        nxt.record_stream(cur)
+        self.inds_cur.copy_(nxt)
         return self.loss

@@ -16,7 +16,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
-from .gemm import rows_linear
+from .gemm import in_projection, rows_linear
 from .helpers import ACTIVATION_DICT, NORM_DICT, get_clones
 
 
@@ -45,12 +45,10 @@ class MultiheadAttention(nn.Module):
         if query is key and key is value:
             q, k, v = rows_linear(query, w, bias).chunk(3, dim=-1)
         elif query is key:
-            q, k = rows_linear(query, w[: 2 * E], bias[: 2 * E]).chunk(2, dim=-1)
-            v = rows_linear(value, w[2 * E:], bias[2 * E:])
+            qk, v = in_projection(w, bias, ((query, 0, 2 * E), (value, 2 * E, 3 * E)))
+            q, k = qk.chunk(2, dim=-1)
         else:
-            q = rows_linear(query, w[:E], bias[:E])
-            k = rows_linear(key, w[E: 2 * E], bias[E: 2 * E])
-            v = rows_linear(value, w[2 * E:], bias[2 * E:])
+            q, k, v = in_projection(w, bias, ((query, 0, E), (key, E, 2 * E), (value, 2 * E, 3 * E)))
         q, k, v = self._heads(q, L, B), self._heads(k, S, B), self._heads(v, S, B)
         mask = None
         if attn_mask is not None:
