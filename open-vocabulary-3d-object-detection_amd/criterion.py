@@ -89,8 +89,29 @@ class SetCriterion(nn.Module):
         return wk not in self.loss_weight_dict or self.loss_weight_dict[wk] > 0
 
     def forward(self, outputs, targets, clip=None):
-        layers = [outputs["outputs"]] + list(outputs.get("aux_outputs", []))
-        L = len(layers)
+        stacked = outputs.get("_layers_stacked")
+        if stacked is not None:
+            # (L, B, ...) tensors in decoder order: computation index l, final layer = L-1
+            L = stacked["box_corners"].shape[0]
+            final, aux = L - 1, list(range(L - 1))
+
+            def cat(key):
+                t = stacked[key]
+                return t.reshape(t.shape[0] * t.shape[1], *t.shape[2:])    # (L*B, ...)
+
+            def layer(l):
+                return {k: v[l] for k, v in stacked.items()}
+        else:
+            # reference outputs: [final] + aux, concatenated once per key
+            layers = [outputs["outputs"]] + list(outputs.get("aux_outputs", []))
+            L = len(layers)
+            final, aux = 0, list(range(1, L))
+
+            def cat(key):
+                return torch.cat([o[key] for o in layers], dim=0)    # (L*B, ...)
+
+            def layer(l):
+                return layers[l]
         present = targets["gt_box_present"]
         nactual_gt = present.sum(axis=1).long()
         # No host synchronisation in the step: num_boxes stays a device scalar, the
@@ -101,9 +122,6 @@ class SetCriterion(nn.Module):
         targets["nactual_gt"] = nactual_gt
         targets["num_boxes"] = num_boxes
         targets["num_boxes_replica"] = nactual_gt.sum()
-
-        def cat(key):
-            return torch.cat([o[key] for o in layers], dim=0)    # (L*B, ...)
 
         B = present.shape[0]
 
@@ -121,8 +139,17 @@ class SetCriterion(nn.Module):
         gt_labels = rep(targets["gt_box_sem_cls_label"])
         cost = self.matcher.cost(cat("sem_cls_prob").float(), cat("objectness_prob").float(),
                                  center_dist, gious, gt_labels)
-        asg = self.matcher(cost, rep(nactual_gt))
-        inds, mask = asg["per_prop_gt_inds"], asg["proposal_matched_mask"]
+        if final == 0:
+            asg = self.matcher(cost, rep(nactual_gt))
+            inds, mask = asg["per_prop_gt_inds"], asg["proposal_matched_mask"]
+        else:
+            # the matcher sees its L*B problems in the reference order (final layer first,
+            # criterion.py:431-444): a rotation by one layer (torch.roll: no host index)
+            Q, G = cost.shape[1], cost.shape[2]
+            asg = self.matcher(torch.roll(cost.view(L, B, Q, G), 1, 0).reshape(L * B, Q, G),
+                               rep(nactual_gt))
+            inds = torch.roll(asg["per_prop_gt_inds"].view(L, B, Q), -1, 0).reshape(L * B, Q)
+            mask = torch.roll(asg["proposal_matched_mask"].view(L, B, Q), -1, 0).reshape(L * B, Q)
 
         per = {}  # key -> (L,) tensor of unweighted per-layer losses
         if self._computed("loss_sem_cls"):
@@ -161,7 +188,7 @@ class SetCriterion(nn.Module):
         if self._computed("loss_2dalignment"):
             if clip is None:
                 raise ValueError("loss_2dalignment_weight > 0 needs a RegionCLIP model (clip=...)")
-            per["loss_2dalignment"] = self._alignment(layers, targets, clip)
+            per["loss_2dalignment"] = self._alignment([layer(l) for l in range(L)], targets, clip)
         with torch.no_grad():
             lg = cat("sem_cls_logits")
             pred_obj = (lg.argmax(-1) != lg.shape[-1] - 1).sum(1).float().view(L, B)
@@ -170,8 +197,9 @@ class SetCriterion(nn.Module):
         loss_dict = {}
         total = None
         weighted = [k[: -len("_weight")] for k, w in self.loss_weight_dict.items() if w > 0]
-        for l in range(L):
-            suffix = "" if l == 0 else f"_{l - 1}"
+        # dict keys and total in the reference order: final layer first, then aux 0..L-2
+        for i, l in enumerate([final] + aux):
+            suffix = "" if i == 0 else f"_{i - 1}"
             vals = {k: per[k][l] * (self._w(k) if self._w(k) > 0 else 1) for k in LOSS_KEYS if k in per}
             for k in LOSS_KEYS:
                 if k in vals:

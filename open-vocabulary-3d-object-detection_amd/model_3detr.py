@@ -182,22 +182,20 @@ class Model3DETR(nn.Module):
         size_u = size_u.view(L, B, Q, 3)
         angle = angle.view(L, B, Q)
         corners = corners.view(L, B, Q, 8, 3)
-        outs = [{
-            "visual_embeds": visual[l],
-            "sem_cls_logits": logits[l],
-            "center_normalized": center_n[l],
-            "center_unnormalized": center_u[l],
-            "size_normalized": size_norm[l],
-            "size_unnormalized": size_u[l],
-            "angle_logits": angle_logits[l],
-            "angle_residual": angle_res[l],
-            "angle_residual_normalized": angle_res_norm[l],
-            "angle_continuous": angle[l],
-            "objectness_prob": obj_prob[l],
-            "sem_cls_prob": sem_prob[l],
-            "box_corners": corners[l],
-        } for l in range(L)]
-        return {"outputs": outs[-1], "aux_outputs": outs[:-1]}
+        stacked = {
+            "visual_embeds": visual, "sem_cls_logits": logits, "center_normalized": center_n,
+            "center_unnormalized": center_u, "size_normalized": size_norm, "size_unnormalized": size_u,
+            "angle_logits": angle_logits, "angle_residual": angle_res,
+            "angle_residual_normalized": angle_res_norm, "angle_continuous": angle,
+            "objectness_prob": obj_prob, "sem_cls_prob": sem_prob, "box_corners": corners,
+        }
+        # per-layer dicts as views (unbind: ONE stack in backward per key, not L selects that
+        # each zero-fill a full-size gradient)
+        per_key = {k: v.unbind(0) for k, v in stacked.items()}
+        outs = [{k: per_key[k][l] for k in stacked} for l in range(L)]
+        # "_layers_stacked": the same tensors stacked over decoder layers (natural order, last =
+        # final); the set criterion consumes them directly instead of re-concatenating
+        return {"outputs": outs[-1], "aux_outputs": outs[:-1], "_layers_stacked": stacked}
 
     def forward(self, inputs, encoder_only=False):
         pc = inputs["point_clouds"]
