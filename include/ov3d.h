@@ -187,6 +187,41 @@ int ov3d_nms3d(const double* boxes, const uint8_t* valid, int B, int K, int stri
 int ov3d_nms_boxes_from_corners(const float* corners, const float* obj, const int64_t* cls, int B,
                                 int K, double* boxes_out, void* stream);
 
+/* ---- RegionCLIP ROI-feature path (CLIPFastRCNN.inference, criterion.py:397) ---- */
+
+/* CLIPFastRCNN.preprocess_image + ImageList.from_tensors [upstream RegionCLIP]
+ * fed with the per-scene image views of criterion.py:371-375,394:
+ *   images (B, img_stride) f32: scene b's (H_b, W_b, 3) image in its first H_b*W_b*3
+ *   values; heights/widths (B,) int32 on the device
+ *   -> out (B, Hp, Wp, 3) NHWC, ((v / div) - mean[c]) / std[c], 0 outside (H_b, W_b);
+ *   out_bf16 selects bf16 (1) or f32 (0) output. */
+int ov3d_clip_preprocess(const float* images, long long img_stride, const int32_t* heights,
+                         const int32_t* widths, int B, int Hp, int Wp, float div, float m0,
+                         float m1, float m2, float s0, float s1, float s2, int out_bf16, void* out,
+                         void* stream);
+
+/* ROIAlign forward on channels-last features.  Replaces the ROIAlignV2 pooler of
+ * CLIPRes5ROIHeads (detectron2 ROIPooler -> torchvision roi_align, aligned=True)
+ * [upstream RegionCLIP] used by clip.inference at criterion.py:397.
+ *   feat (N, H, W, C) f32 (is_bf16 = 0, C % 4 == 0) or bf16 (is_bf16 = 1, C % 8 == 0)
+ *   boxes (R, 4) f32 [x1, y1, x2, y2] in image pixels; roi r samples image
+ *   (r / per_image) % nimages  (rows ordered (layer, scene, query))
+ *   -> out (R, pooled, pooled, C), same dtype; sampling_ratio <= 0 = adaptive
+ *   (ceil(roi_size / pooled)).  fp32 arithmetic in torchvision's order. */
+int ov3d_roi_align_fwd(const void* feat, int is_bf16, int N, int H, int W, int C,
+                       const float* boxes, int R, int per_image, int nimages, float spatial_scale,
+                       int pooled, int sampling_ratio, int aligned, void* out, void* stream);
+
+/* NHWC im2col for a 3x3 convolution (pad 1, stride 1|2) of the RegionCLIP
+ * ModifiedResNet [upstream CLIP/RegionCLIP; the convolutions of clip.inference,
+ * criterion.py:397], so that the convolution is one GEMM against the
+ * channels-last weight viewed as (Cout, 9*C):
+ *   in (N, H, W, C), elem_bytes 2 (bf16) or 4 (f32)
+ *   -> out (N*Ho*Wo, Kpad), column k = (ky*3 + kx)*C + c, zeros outside the image
+ *      and for 9*C <= k < Kpad;  Ho = (H-1)/stride + 1, Wo likewise. */
+int ov3d_im2col3x3(const void* in, int elem_bytes, int N, int H, int W, int C, int stride,
+                   int Kpad, void* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -42,6 +42,9 @@ _SIGS = {
     "ov3d_bn_relu_bwd": "ippppppppppiippip",
     "ov3d_nms3d": "ppiiidiipp",
     "ov3d_nms_boxes_from_corners": "pppiipp",
+    "ov3d_clip_preprocess": "plppiiifffffffipp",
+    "ov3d_roi_align_fwd": "piiiiipiiifiiipp",
+    "ov3d_im2col3x3": "piiiiiiipp",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported")
 

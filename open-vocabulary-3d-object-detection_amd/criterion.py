@@ -188,7 +188,10 @@ class SetCriterion(nn.Module):
         if self._computed("loss_2dalignment"):
             if clip is None:
                 raise ValueError("loss_2dalignment_weight > 0 needs a RegionCLIP model (clip=...)")
-            per["loss_2dalignment"] = self._alignment([layer(l) for l in range(L)], targets, clip)
+            if hasattr(clip, "region_features"):
+                per["loss_2dalignment"] = self._alignment_batched(cat, L, B, targets, clip)
+            else:
+                per["loss_2dalignment"] = self._alignment([layer(l) for l in range(L)], targets, clip)
         with torch.no_grad():
             lg = cat("sem_cls_logits")
             pred_obj = (lg.argmax(-1) != lg.shape[-1] - 1).sum(1).float().view(L, B)
@@ -218,6 +221,26 @@ class SetCriterion(nn.Module):
                                  targets["calib_K"], targets["image_height"], targets["image_width"])
         return clip.inference(clip_batch(targets["image"], targets["image_height"],
                                          targets["image_width"], boxes), do_postprocess=False)
+
+    def _alignment_batched(self, cat, L, B, targets, clip):
+        """All L decoder layers at once: one projection over (L*B, Q) boxes, one backbone
+        pass and one ROI batch in ``clip.region_features`` (ov3d_amd.regionclip).  Equal to
+        the per-layer loop below (criterion.py:379-398 once per layer, 432-442)."""
+        def rep(t):
+            return t.repeat((L,) + (1,) * (t.dim() - 1))
+
+        with torch.no_grad():
+            boxes = project_boxes_2d(cat("center_unnormalized").float(), cat("size_unnormalized").float(),
+                                     cat("angle_continuous").float(), rep(targets["calib_Rtilt"]),
+                                     rep(targets["calib_K"]), rep(targets["image_height"]),
+                                     rep(targets["image_width"]))
+            Q = boxes.shape[1]
+            feats = clip.region_features(targets["image"], targets["image_height"],
+                                         targets["image_width"], boxes.view(L, B, Q, 4))
+        v = cat("visual_embeds").float()                                    # (L*B, Q, C)
+        C = v.shape[-1]
+        cos = F.cosine_similarity(v, feats.reshape(L * B, Q, C).float(), dim=-1)
+        return (1 - cos).view(L, -1).sum(1)
 
     def _alignment(self, layers, targets, clip):
         vals = []

@@ -40,8 +40,9 @@ def lib():
         L.ov3d_giou3d_cpu.argtypes = [P, P, P, i, i, i, i, i, i, P]
         L.ov3d_nms3d_cpu.argtypes = [P, i, i, ctypes.c_double, i, i, P, P]
         L.ov3d_lsap_cpu.argtypes = [P, i, i, i, P]
+        L.ov3d_roi_align_cpu.argtypes = [P, i, i, i, i, P, i, i, i, ctypes.c_float, i, i, i, P]
         for f in (L.ov3d_lsap_cpu, L.ov3d_fps_cpu, L.ov3d_ball_query_cpu, L.ov3d_group_cpu,
-                  L.ov3d_giou3d_cpu, L.ov3d_nms3d_cpu):
+                  L.ov3d_giou3d_cpu, L.ov3d_nms3d_cpu, L.ov3d_roi_align_cpu):
             f.restype = ctypes.c_int
         _LIB = L
     return _LIB
@@ -127,4 +128,20 @@ def lsap(cost):
         raise ValueError("matrix contains invalid numeric entries")
     if rc:
         raise ValueError("cost matrix is infeasible")
+    return out
+
+
+def roi_align(feat_nhwc, boxes, per_image, nimages, spatial_scale=1.0 / 16, pooled=18,
+              sampling_ratio=0, aligned=True):
+    """ROIAlignV2 of RegionCLIP's ROI heads [upstream detectron2/torchvision roi_align,
+    reached from criterion.py:397]: feat (N,H,W,C) f32, boxes (R,4) -> (R,P,P,C) f32."""
+    f = np.ascontiguousarray(feat_nhwc, dtype=np.float32)
+    b = np.ascontiguousarray(boxes, dtype=np.float32).reshape(-1, 4)
+    N, H, W, C = f.shape
+    R = b.shape[0]
+    out = np.zeros((R, pooled, pooled, C), dtype=np.float32)
+    rc = lib().ov3d_roi_align_cpu(_p(f), N, H, W, C, _p(b), R, per_image, nimages,
+                                  float(spatial_scale), pooled, sampling_ratio, int(bool(aligned)),
+                                  _p(out))
+    assert rc == 0, rc
     return out

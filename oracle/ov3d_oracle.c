@@ -506,3 +506,63 @@ int ov3d_lsap_cpu(const float* cost, int nq, int ng, int ld, int32_t* gt_of_q) {
     free(u); free(v); free(spc); free(path); free(col4row); free(row4col); free(SR); free(SC); free(rem);
     return rc;
 }
+
+/* ------------------------------------------------------------- ROIAlign */
+/* ROIAlignV2 of the RegionCLIP ROI heads [upstream: detectron2 ROIPooler ->
+ * torchvision roi_align_forward_kernel_impl, aligned=True], reached from
+ * clip.inference at criterion.py:397.  PARITY UNPINNED by the reference
+ * (RegionCLIP / detectron2 / torchvision are not vendored); this restates the
+ * published kernel operation by operation in float:
+ *   start = box * scale - 0.5; size = end - start; bin = size / P;
+ *   grid = sampling_ratio > 0 ? sampling_ratio : ceil(size / P);
+ *   y = start_h + ph*bin_h + (iy + .5) * bin_h / grid_h  (x likewise)
+ *   bilinear: zero outside [-1, H] x [-1, W], clamp to 0, edge rows/cols
+ *   collapse; val = w1*v1 + w2*v2 + w3*v3 + w4*v4; out = sum / max(gh*gw, 1).
+ * Layout: feat (N,H,W,C) channels-last, boxes (R,4), roi r reads image
+ * (r / per_image) % nimages, out (R,P,P,C). */
+static float roi_bilinear(const float* f, int H, int W, int C, float y, float x) {
+    if (y < -1.0f || y > (float)H || x < -1.0f || x > (float)W) return 0.f;
+    if (y <= 0) y = 0;
+    if (x <= 0) x = 0;
+    int yl = (int)y, xl = (int)x, yh, xh;
+    if (yl >= H - 1) { yh = yl = H - 1; y = (float)yl; } else yh = yl + 1;
+    if (xl >= W - 1) { xh = xl = W - 1; x = (float)xl; } else xh = xl + 1;
+    float ly = y - (float)yl, lx = x - (float)xl, hy = 1.f - ly, hx = 1.f - lx;
+    float w1 = hy * hx, w2 = hy * lx, w3 = ly * hx, w4 = ly * lx;
+    float v1 = f[((size_t)yl * W + xl) * C], v2 = f[((size_t)yl * W + xh) * C];
+    float v3 = f[((size_t)yh * W + xl) * C], v4 = f[((size_t)yh * W + xh) * C];
+    return w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4;
+}
+
+int ov3d_roi_align_cpu(const float* feat, int N, int H, int W, int C, const float* boxes, int R,
+                       int per_image, int nimages, float scale, int P, int sampling_ratio,
+                       int aligned, float* out) {
+    if (per_image <= 0 || nimages <= 0 || nimages > N) return -1;
+    const float off = aligned ? 0.5f : 0.f;
+    for (int r = 0; r < R; r++) {
+        const float* bx = boxes + 4 * (size_t)r;
+        const float* f = feat + (size_t)((r / per_image) % nimages) * H * W * C;
+        float sw = bx[0] * scale - off, sh = bx[1] * scale - off;
+        float ew = bx[2] * scale - off, eh = bx[3] * scale - off;
+        float rw = ew - sw, rh = eh - sh;
+        if (!aligned) { rw = rw > 1.f ? rw : 1.f; rh = rh > 1.f ? rh : 1.f; }
+        float bh = rh / (float)P, bw = rw / (float)P;
+        int gh = sampling_ratio > 0 ? sampling_ratio : (int)ceilf(rh / (float)P);
+        int gw = sampling_ratio > 0 ? sampling_ratio : (int)ceilf(rw / (float)P);
+        float count = (float)(gh * gw > 1 ? gh * gw : 1);
+        for (int ph = 0; ph < P; ph++)
+            for (int pw = 0; pw < P; pw++)
+                for (int c = 0; c < C; c++) {
+                    float acc = 0.f;
+                    for (int iy = 0; iy < gh; iy++) {
+                        float y = sh + (float)ph * bh + (float)(iy + .5f) * bh / (float)gh;
+                        for (int ix = 0; ix < gw; ix++) {
+                            float x = sw + (float)pw * bw + (float)(ix + .5f) * bw / (float)gw;
+                            acc += roi_bilinear(f + c, H, W, C, y, x);
+                        }
+                    }
+                    out[(((size_t)r * P + ph) * P + pw) * C + c] = acc / count;
+                }
+    }
+    return 0;
+}
