@@ -52,6 +52,31 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# C5 (BASELINE.json configs[4]): --use_image RegionCLIP RN50x4 ROI path + 2D
+# alignment loss, bs=4/GPU (README.md:13-36: loss_2dalignment_weight 2e-4)
+WORKLOADS = {
+    "sun": dict(batch=8, use_image=False, args={}),
+    "sun_image": dict(batch=4, use_image=True, args=dict(loss_2dalignment_weight=2e-4)),
+}
+
+
+def build_regionclip(device):
+    """RegionCLIP RN50x4 ROI-feature extractor (seed 11, no checkpoint offline), bf16."""
+    from ov3d_amd import regionclip as rc
+    clip, _ = rc.build_regionclip(compute_dtype=torch.bfloat16)
+    clip = clip.to(device)
+    clip.static_image_size = (530, 730)   # synthetic SUN images are all 530x730
+    return clip
+
+
+def regionclip_gflop_per_scene(batch, nqueries=128, layers=8):
+    """algorithmic GFLOP/scene of the product's RegionCLIP pass (backbone once per image,
+    res5 per ROI, reassociated pool) — tools/bench_regionclip.py counts the same terms."""
+    backbone = 136.7                      # RN50x4 stem..res4 at 530x730 (conv FLOPs, per image)
+    res5, pool = 9356.0e-3, 76.2e-3       # per 18x18 ROI
+    return backbone + nqueries * layers * (res5 + pool)
+
+
 def build(args, device, ddp=False, capturable=False):
     ov3d = ov3d_import.load()
     from ov3d_amd import synthetic
@@ -75,12 +100,12 @@ def build(args, device, ddp=False, capturable=False):
     return model, crit, opt
 
 
-def train_step(model, crit, opt, batch, args, amp_dtype):
+def train_step(model, crit, opt, batch, args, amp_dtype, clip=None):
     opt.zero_grad(set_to_none=True)
     inputs = {k: batch[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")}
     with torch.autocast("cuda", dtype=amp_dtype, enabled=amp_dtype is not None):
         out = model(inputs)
-    loss, _ = crit(out, batch)
+    loss, _ = crit(out, batch, clip=clip)
     loss.backward()
     torch.nn.utils.clip_grad_norm_(model.parameters(), args.clip_gradient)
     opt.step()
@@ -145,7 +170,9 @@ def main():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)      # >= 50 timed steps
     p.add_argument("--warmup", type=int, default=10)     # after 10 warm-up steps
-    p.add_argument("--batch", type=int, default=8)
+    p.add_argument("--workload", default="sun", choices=sorted(WORKLOADS),
+                   help="sun = BASELINE metric config (C2/C3); sun_image = C5 (RegionCLIP ROI path)")
+    p.add_argument("--batch", type=int, default=None, help="scenes per GPU (default: workload's)")
     p.add_argument("--points", type=int, default=20000)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -156,29 +183,34 @@ def main():
                    help="launch the step eagerly (default at N>1); at N=1 the whole step is "
                         "captured once and replayed as one hipGraph (graphs.StepGraph)")
     cli = p.parse_args()
+    wl = WORKLOADS[cli.workload]
+    if cli.batch is None:
+        cli.batch = wl["batch"]
 
     ov3d = ov3d_import.load()
     from ov3d_amd import _native, dist, synthetic
     rank, world, local = dist.init_from_env()
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
-    args = default_args()
+    args = default_args(**wl["args"])
     amp = torch.bfloat16 if cli.dtype == "bf16" else None
     use_graph = world == 1 and not cli.eager
     model, crit, opt = build(args, device, ddp=world > 1, capturable=use_graph)
-    pool = [synthetic.make_batch(cli.batch, seed=1000 * rank + i, num_points=cli.points, device=device)
+    clip = build_regionclip(device) if wl["use_image"] else None
+    pool = [synthetic.make_batch(cli.batch, seed=1000 * rank + i, num_points=cli.points, device=device,
+                                 use_image=wl["use_image"])
             for i in range(cli.pool)]
 
     graphed = None
     if use_graph:
         from ov3d_amd.graphs import StepGraph
         graphed = StepGraph(model, crit, opt, pool[0], amp_dtype=amp, clip=args.clip_gradient,
-                            prefetch_fps=not cli.no_prefetch)
+                            prefetch_fps=not cli.no_prefetch, regionclip=clip)
 
     def step(i):
         if graphed is not None:
             return graphed.step(pool[i % cli.pool], pool[(i + 1) % cli.pool])
-        return train_step(model, crit, opt, pool[i % cli.pool], args, amp)
+        return train_step(model, crit, opt, pool[i % cli.pool], args, amp, clip=clip)
 
     for i in range(cli.warmup):
         step(i)
@@ -225,21 +257,31 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
                 "kernel": "ov3d_fps (pre-encoder, B=%d N=%d M=%d)" % (B, N, M),
                 "avg_launch_ms": round(avg_ms, 4), "launches": len(pre)}
-    step_tflops = STEP_GFLOP_PER_SCENE * value / 1e3
+    gflop_scene = STEP_GFLOP_PER_SCENE
+    metric = "scenes/sec (train step) SUN RGB-D 20k pts nqueries=128"
+    workload = (f"SUN RGB-D train step, bs={cli.batch}/GPU, {cli.points} pts, nqueries=128, "
+                "3DETR 256-d enc3/dec8, text-emb 640, AdamW + clip 0.1")
+    if wl["use_image"]:
+        gflop_scene += regionclip_gflop_per_scene(cli.batch)
+        metric += " +RegionCLIP RN50x4 2D alignment (C5)"
+        workload += ", --use_image: RegionCLIP RN50x4 ROI features (8 layers x 128 boxes) + 2D alignment loss 2e-4"
+    step_tflops = gflop_scene * value / 1e3
     res = {
-        "metric": "scenes/sec (train step) SUN RGB-D 20k pts nqueries=128",
+        "metric": metric,
         "value": round(value, 3), "unit": "scenes/s", "n_gpus": world, "steps": cli.steps,
         "warmup": cli.warmup, "ms_per_step": round(elapsed / cli.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": cli.dtype,
         "data": "synthetic SUN RGB-D-like scenes (numpy PCG64), random-init weights",
-        "config": {"workload": f"SUN RGB-D train step, bs={cli.batch}/GPU, {cli.points} pts, nqueries=128, "
-                               "3DETR 256-d enc3/dec8, text-emb 640, AdamW + clip 0.1",
+        "config": {"workload": workload,
                    "global_batch": cli.batch * world, "points": cli.points, "parallelism": f"dp{world}"},
         "roofline": roof,
         "step_mfma": {"achieved_tflops": round(step_tflops, 2), "peak_tflops": BF16_DENSE_PEAK_TFLOPS,
                       "frac": round(step_tflops / (world * BF16_DENSE_PEAK_TFLOPS), 5)},
     }
-    if world == 1 and not cli.no_cpu_baseline:
+    if wl["use_image"]:
+        res["cpu_baseline"] = {"value": None, "note": "not run for C5: the RN50x4 ROI path is "
+                               f"{regionclip_gflop_per_scene(cli.batch) / 1e3:.1f} TFLOP/scene"}
+    elif world == 1 and not cli.no_cpu_baseline:
         try:
             res["cpu_baseline"] = cpu_baseline(default_args())
         except Exception as e:  # report, never fake

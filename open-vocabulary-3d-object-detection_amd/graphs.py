@@ -83,10 +83,11 @@ class StepGraph:
     eagerly first."""
 
     def __init__(self, model, crit, opt, sample, amp_dtype=torch.bfloat16, clip=0.1,
-                 warmup_iters=3, prefetch_fps=True):
+                 warmup_iters=3, prefetch_fps=True, regionclip=None):
         from . import gemm
         from . import pointnet2_utils as pu
         self.model, self.crit, self.opt = model, crit, opt
+        self.regionclip = regionclip   # clip= of SetCriterion.forward (needs static_image_size)
         self.amp_dtype, self.clip = amp_dtype, clip
         self.static = {k: v.clone() for k, v in sample.items()}
         self.prefetch = prefetch_fps and hasattr(model, "pre_encoder")
@@ -122,7 +123,7 @@ class StepGraph:
         with torch.autocast("cuda", dtype=self.amp_dtype or torch.float32,
                             enabled=self.amp_dtype is not None):
             out = self.model(inputs)
-        loss, _ = self.crit(out, dict(self.static))
+        loss, _ = self.crit(out, dict(self.static), clip=self.regionclip)
         loss.backward()
         torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.clip)
         self.opt.step()

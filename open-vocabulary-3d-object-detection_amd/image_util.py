@@ -34,14 +34,24 @@ def _structures():
         return Boxes, Instances
 
 
+_SIGNS = {}
+
+
+def _corner_signs(dtype, device):
+    """(3, 8) corner sign table, built once per (dtype, device) outside any graph capture."""
+    key = (dtype, device)
+    if key not in _SIGNS:
+        _SIGNS[key] = torch.tensor([[-1, 1, 1, -1, -1, 1, 1, -1], [1, 1, -1, -1, 1, 1, -1, -1],
+                                    [1, 1, 1, 1, -1, -1, -1, -1]], dtype=dtype, device=device)
+    return _SIGNS[key]
+
+
 def project_boxes_2d(center, size, heading, Rtilt, K, img_h, img_w):
     """center/size (B,Q,3), heading (B,Q), Rtilt/K (B,3,3), img_h/img_w (B,) -> (B,Q,4)."""
     c = torch.cos(-heading)[..., None]
     s = torch.sin(-heading)[..., None]
     l, w, h = size[..., 0:1], size[..., 1:2], size[..., 2:3]
-    sx = torch.tensor([-1, 1, 1, -1, -1, 1, 1, -1], dtype=size.dtype, device=size.device)
-    sy = torch.tensor([1, 1, -1, -1, 1, 1, -1, -1], dtype=size.dtype, device=size.device)
-    sz = torch.tensor([1, 1, 1, 1, -1, -1, -1, -1], dtype=size.dtype, device=size.device)
+    sx, sy, sz = _corner_signs(size.dtype, size.device)
     xc, yc, zc = l * sx, w * sy, h * sz                               # (B,Q,8)
     X = c * xc - s * yc + center[..., 0:1]                            # rotz(-heading) @ corners
     Y = s * xc + c * yc + center[..., 1:2]

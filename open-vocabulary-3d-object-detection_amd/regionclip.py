@@ -306,14 +306,20 @@ class RegionCLIP(nn.Module):
         lay, wid = CLIP_RESNETS[depth] if layers is None else (layers, width)
         heads = heads if heads is not None else wid * 32 // 64
         self.backbone = ModifiedResNet(lay, output_dim, heads, pooler_resolution * 16, wid)
-        self.register_buffer("pixel_mean", torch.tensor(pixel_mean).view(-1, 1, 1))
-        self.register_buffer("pixel_std", torch.tensor(pixel_std).view(-1, 1, 1))
+        self.register_buffer("pixel_mean", torch.tensor(pixel_mean).view(-1, 1, 1), persistent=False)
+        self.register_buffer("pixel_std", torch.tensor(pixel_std).view(-1, 1, 1), persistent=False)
+        self._norm = (tuple(float(v) for v in pixel_mean), tuple(float(v) for v in pixel_std))
         self.div_pixel = div_pixel
         self.pooler_resolution = pooler_resolution
         self.spatial_scale = 1.0 / 16
         self.sampling_ratio = 0
         self.compute_dtype = compute_dtype
         self.max_rois_per_chunk = max_rois_per_chunk
+        # Optional (H, W) promise that every batch's largest image has exactly this size
+        # (e.g. SUN RGB-D batches holding a 530x730 image): the padded batch shape is then
+        # known without reading image_height / image_width back to the host, which keeps
+        # the step free of host syncs (hipGraph capture).  None = read them (reference).
+        self.static_image_size = None
         self._folded = None
         self.eval()
 
@@ -327,7 +333,7 @@ class RegionCLIP(nn.Module):
         return super()._apply(fn, *a, **k)
 
     def folded(self):
-        if self._folded is None or self._folded.pos.device != self.pixel_mean.device:
+        if self._folded is None or self._folded.pos.device != self.backbone.conv1.weight.device:
             self._folded = _Folded(self.backbone, self.compute_dtype)
         return self._folded
 
@@ -355,9 +361,12 @@ class RegionCLIP(nn.Module):
         ImageList.from_tensors makes it), boxes (L, B, Q, 4) image-pixel boxes
         -> (L, B, Q, output_dim) f32 == stacking clip.inference over the L layers."""
         L, B, Q, _ = boxes.shape
-        hs = heights.tolist() if torch.is_tensor(heights) else list(heights)
-        ws = widths.tolist() if torch.is_tensor(widths) else list(widths)
-        x = self._preprocess_1d(images_1d, heights, widths, max(hs), max(ws))
+        if self.static_image_size is not None:
+            hmax, wmax = self.static_image_size
+        else:
+            hmax = max(heights.tolist() if torch.is_tensor(heights) else list(heights))
+            wmax = max(widths.tolist() if torch.is_tensor(widths) else list(widths))
+        x = self._preprocess_1d(images_1d, heights, widths, hmax, wmax)
         feats = self._features(x)
         out = self._roi_features(feats, boxes.reshape(-1, 4).float().contiguous(), per_image=Q,
                                  nimages=B)
@@ -378,7 +387,7 @@ class RegionCLIP(nn.Module):
         wts = torch.as_tensor(widths, dtype=torch.int32, device=dev).contiguous()
         images_1d = _native.check(images_1d.float().contiguous(), "images", ndim=2)
         out = torch.empty((B, Hp, Wp, 3), dtype=self.compute_dtype, device=dev)
-        m, s = self.pixel_mean.view(-1).tolist(), self.pixel_std.view(-1).tolist()
+        m, s = self._norm      # host constants: no device read in the (capturable) step
         _native.call("ov3d_clip_preprocess", images_1d, images_1d.stride(0), hts, wts, B, Hp, Wp,
                      255.0 if self.div_pixel else 1.0, *m, *s,
                      int(self.compute_dtype == torch.bfloat16), out, like=images_1d)
