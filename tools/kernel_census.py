@@ -12,6 +12,7 @@ def main():
     ap.add_argument("--marker", default="fps_cull_kernel<2>")
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--top", type=int, default=45)
+    ap.add_argument("--by-time", action="store_true")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
@@ -27,7 +28,8 @@ def main():
         tm[key] += e - s
     print(f"kernels/step {sum(cnt.values()) / a.steps:.0f}, kernel time/step "
           f"{sum(tm.values()) / a.steps / 1e6:.2f} ms")
-    for k in sorted(cnt, key=lambda k: -cnt[k])[: a.top]:
+    order = (lambda k: -tm[k]) if a.by_time else (lambda k: -cnt[k])
+    for k in sorted(cnt, key=order)[: a.top]:
         print(f"{cnt[k] / a.steps:7.1f}/step {tm[k] / a.steps / 1e3:8.1f} us/step  {k}")
 
 
