@@ -222,6 +222,30 @@ int ov3d_roi_align_fwd(const void* feat, int is_bf16, int N, int H, int W, int C
 int ov3d_im2col3x3(const void* in, int elem_bytes, int N, int H, int W, int C, int stride,
                    int Kpad, void* out, void* stream);
 
+/* ---- Flash attention (head_dim 64, bf16, no mask) ----
+ * Replaces the nn.MultiheadAttention core of models/transformer.py:223,271 (encoder
+ * self-attention) and :307-308,365-372 (decoder self / cross attention): per head
+ * O = dropout(softmax(scale Q K^T)) V.  Q/K/V/O rows in the reference's seq-first
+ * layout: element (l, b, h, d) at ptr[(l*B + b)*stride + h*64 + d] (strides in
+ * elements), so projection outputs are read in place.  Lq % 32 == 0.
+ * Dropout: keep(q, k) from a counter-based hash of (*seed, site, b*H + h, q, k>>1)
+ * (16-bit half per key, keep iff half >= round(p * 65536)), regenerated in the
+ * backward.  lse (B*H, Lq) f32 = log2-domain logsumexp saved for the backward.
+ * nsplit > 1 splits the keys over workgroups (decoder: 128 queries) and needs
+ * ov3d_attn_fwd_workspace() floats of workspace. */
+int ov3d_attn_fwd(const void* q, const void* k, const void* v, long long sq, long long sk,
+                  long long sv, int B, int H, int Lq, int Lk, float scale, float dropout_p,
+                  const int64_t* seed, int site, void* o, long long so, float* lse,
+                  float* workspace, int nsplit, void* stream);
+long long ov3d_attn_fwd_workspace(int B, int H, int Lq, int Lk, int nsplit);
+/* Backward: dq/dk/dv rows (same layout, bf16) from o, dout (stride sdo), lse;
+ * dvec (B*H, Lq) f32 scratch receives D = rowsum(dout * o). */
+int ov3d_attn_bwd(const void* q, const void* k, const void* v, long long sq, long long sk,
+                  long long sv, const void* o, long long so, const void* dout, long long sdo,
+                  const float* lse, int B, int H, int Lq, int Lk, float scale, float dropout_p,
+                  const int64_t* seed, int site, float* dvec, void* dq, long long sdq, void* dk,
+                  long long sdk, void* dv, long long sdv, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -45,8 +45,10 @@ _SIGS = {
     "ov3d_clip_preprocess": "plppiiifffffffipp",
     "ov3d_roi_align_fwd": "piiiiipiiifiiipp",
     "ov3d_im2col3x3": "piiiiiiipp",
+    "ov3d_attn_fwd": "pppllliiiiffpiplppip",
+    "ov3d_attn_bwd": "ppplllplplpiiiiffpipplplplp",
 }
-EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported")
+EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace")
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_longlong, "f": ctypes.c_float,
        "d": ctypes.c_double}
@@ -71,6 +73,8 @@ def load():
             fn.restype = ctypes.c_int
         lib.ov3d_sa_layer_supported.argtypes = [ctypes.c_int, ctypes.c_int]
         lib.ov3d_sa_layer_supported.restype = ctypes.c_int
+        lib.ov3d_attn_fwd_workspace.argtypes = [ctypes.c_int] * 5
+        lib.ov3d_attn_fwd_workspace.restype = ctypes.c_longlong
         lib.ov3d_version.argtypes = []
         lib.ov3d_version.restype = ctypes.c_char_p
         _lib = lib

@@ -1,0 +1,146 @@
+"""Flash attention on the HIP kernels of csrc/attn.hip (``ov3d_attn_fwd/bwd``).
+
+Used by transformer.MultiheadAttention for the reference's nn.MultiheadAttention
+core (models/transformer.py:223,271,307-308,365-372): head_dim 64, no mask, bf16
+operands (autocast), fp32 softmax statistics, dropout on the attention
+probabilities as nn.MultiheadAttention(dropout=...) applies it in training.
+
+Q, K and V are passed as column ranges of their projection outputs, which keep the
+reference's seq-first row layout (L, B, n*E): the kernels read (l, b, head, d) at
+row l*B + b, column off + head*64 + d, so the heads are never permuted or copied;
+the gradients are written into one buffer per source tensor the same way.
+
+Dropout randomness: keep(q, k) is a counter-based hash of (step seed, call site,
+b*H + h, q, k), regenerated in the backward instead of stored.  The step seed is a
+device int64 advanced once per training step (``next_step``, captured by a hipGraph
+like any other kernel), the call site is fixed per module.
+"""
+import itertools
+
+import torch
+
+from . import _native
+
+HEAD_DIM = 64
+_SITES = itertools.count(1)
+_SEEDS = {}
+
+
+def new_site():
+    return next(_SITES)
+
+
+def _seed(device):
+    t = _SEEDS.get(device)
+    if t is None:
+        t = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).to(device)
+        _SEEDS[device] = t
+    return t
+
+
+def next_step(device):
+    """Advance the dropout seed of `device` (one tiny kernel; call once per step)."""
+    _seed(device).add_(1)
+
+
+def supported(q_src, k_src, num_heads, attn_mask):
+    """the HIP kernels: head_dim 64, no mask, query length a multiple of 32"""
+    return (q_src.is_cuda and attn_mask is None and q_src.shape[-1] % (num_heads * HEAD_DIM) == 0
+            and q_src.shape[0] % 32 == 0)
+
+
+def _split(Lq, Lk, BH):
+    """key splits so that the grid has >= ~256 workgroups (decoder: 128 queries)."""
+    wgs = ((Lq + 127) // 128) * BH
+    n = 1
+    while wgs * n < 256 and Lk // (n * 2) >= 128:
+        n *= 2
+    return n
+
+
+def _rows(src, off, E):
+    """(contiguous source, column offset) -> (data pointer, row stride) for the kernel."""
+    return src.data_ptr() + off * src.element_size(), src.shape[-1]
+
+
+class _Attention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, spec, dims, H, dropout_p, site, *srcs):
+        (qi, qo), (ki, ko), (vi, vo) = spec
+        q, k, v = srcs[qi], srcs[ki], srcs[vi]
+        Lq, Lk, B = dims
+        E = H * HEAD_DIM
+        dev = q.device
+        o = torch.empty((Lq, B, E), dtype=torch.bfloat16, device=dev)
+        lse = torch.empty((B * H, Lq), dtype=torch.float32, device=dev)
+        nsplit = _split(Lq, Lk, B * H)
+        ws_n = _native.load().ov3d_attn_fwd_workspace(B, H, Lq, Lk, nsplit)
+        ws = torch.empty((max(ws_n, 1),), dtype=torch.float32, device=dev)
+        seed = _seed(dev)
+        qp, sq = _rows(q, qo, E)
+        kp, sk = _rows(k, ko, E)
+        vp, sv = _rows(v, vo, E)
+        fn = _native.load().ov3d_attn_fwd
+        rc = fn(qp, kp, vp, sq, sk, sv, B, H, Lq, Lk, HEAD_DIM ** -0.5, float(dropout_p),
+                _native._ptr(seed), site, _native._ptr(o), E, _native._ptr(lse), _native._ptr(ws),
+                nsplit, _native._stream(q))
+        if rc:
+            raise _native.NativeError(f"ov3d_attn_fwd failed with status {rc}")
+        ctx.save_for_backward(*srcs, o, lse)
+        ctx.meta = (spec, dims, H, float(dropout_p), site, len(srcs))
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        spec, (Lq, Lk, B), H, p, site, n = ctx.meta
+        saved = ctx.saved_tensors
+        srcs, o, lse = saved[:n], saved[n], saved[n + 1]
+        (qi, qo), (ki, ko), (vi, vo) = spec
+        q, k, v = srcs[qi], srcs[ki], srcs[vi]
+        E = H * HEAD_DIM
+        do = do.to(torch.bfloat16).contiguous()
+        grads = [torch.empty_like(s) for s in srcs]   # every column is written below
+        dvec = torch.empty((B * H, Lq), dtype=torch.float32, device=q.device)
+        qp, sq = _rows(q, qo, E)
+        kp, sk = _rows(k, ko, E)
+        vp, sv = _rows(v, vo, E)
+        dqp, sdq = _rows(grads[qi], qo, E)
+        dkp, sdk = _rows(grads[ki], ko, E)
+        dvp, sdv = _rows(grads[vi], vo, E)
+        rc = _native.load().ov3d_attn_bwd(
+            qp, kp, vp, sq, sk, sv, _native._ptr(o), E, _native._ptr(do), E, _native._ptr(lse),
+            B, H, Lq, Lk, HEAD_DIM ** -0.5, p, _native._ptr(_seed(q.device)), site,
+            _native._ptr(dvec), dqp, sdq, dkp, sdk, dvp, sdv, _native._stream(q))
+        if rc:
+            raise _native.NativeError(f"ov3d_attn_bwd failed with status {rc}")
+        return (None, None, None, None, None, *grads)
+
+
+def attention_packed(srcs, spec, Lq, Lk, num_heads, dropout_p=0.0, site=0):
+    """Attention over column ranges of projection outputs.
+
+    srcs: contiguous (L, B, n*E) tensors (their rows l*B + b), spec: ((src index, column
+    offset) for q, for k, for v).  Every column of every source must belong to one of
+    q / k / v (their gradients are written column range by column range, not zeroed).
+    -> (Lq, B, E) bf16."""
+    E = num_heads * HEAD_DIM
+    B = srcs[spec[0][0]].shape[1]
+    for i, s in enumerate(srcs):
+        cols = sorted(off for j, off in spec if j == i)
+        if not s.is_contiguous() or s.dim() != 3 or s.shape[1] != B or \
+                cols != list(range(0, s.shape[-1], E)):
+            raise ValueError("attention_packed: sources must be contiguous (L, B, n*E) tensors "
+                             "fully covered by the q / k / v column ranges")
+        _native.check_device(s, "attention input")
+    srcs = [s if s.dtype == torch.bfloat16 else s.to(torch.bfloat16) for s in srcs]
+    return _Attention.apply(tuple(spec), (Lq, Lk, B), num_heads, dropout_p, site, *srcs)
+
+
+def attention(q, k, v, num_heads, dropout_p=0.0, site=0):
+    """q (Lq, B, E), k / v (Lk, B, E) -> (Lq, B, E) bf16 = softmax(q k^T / 8) v per head,
+    dropout on the probabilities (separate, contiguous copies of q, k, v)."""
+    if k.shape[1] != q.shape[1] or v.shape[:2] != k.shape[:2]:
+        raise ValueError("attention: q, k, v batch / key lengths disagree")
+    srcs = [t.contiguous() for t in (q, k, v)]
+    return attention_packed(srcs, ((0, 0), (1, 0), (2, 0)), q.shape[0], k.shape[0], num_heads,
+                            dropout_p, site)

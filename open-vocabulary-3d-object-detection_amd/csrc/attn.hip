@@ -1,0 +1,684 @@
+// Flash attention for the 3DETR transformer, head_dim 64,
+// bf16 operands, fp32 accumulation, attention-probability dropout, on MFMA 32x32x16.
+//
+// Replaces nn.MultiheadAttention's core in models/transformer.py:223,271 (encoder
+// self-attention, L = 2048) and :307-308,365-372 (decoder self / cross attention,
+// 128 queries over 128 / 2048 keys).  Q, K, V are read straight from the
+// projection rows: element (l, b, h, d) lives at ptr[(l*B + b)*stride + h*64 + d]
+// (the seq-first (L, B, E) layout of the reference, so no head permute copies), and
+// O is written in the same row layout for the output projection.
+//
+// Layout on the matrix cores ("swapped" QK^T): per wave 32 queries; the score tile
+// is S^T = K Q^T (32 keys x 32 queries), so each lane owns ONE query and 16 of its
+// keys: the softmax statistics are per lane (plus one lane^32 exchange), and
+// O^T = V^T P^T keeps the query on the lane as well, so the online-softmax rescale
+// is a per-lane scalar.  P^T feeds the PV MFMA straight from the accumulator
+// registers (its k order is the MFMA's row order); V^T's operand is read with
+// ds_read_b64_tr_b16 from the row-major V tile in LDS.
+//
+// Dropout: keep(q, k) = hash32(seed, site, b*H+h, q, k) >= p * 2^32, a counter-based
+// hash, so forward and backward regenerate the same mask without storing it.
+// Split-K (grid.z) serves the 128-query decoder attention: partial (O, m, l) per
+// key split, merged by attn_combine_kernel.
+#include <math.h>
+
+#include "common.h"
+
+namespace {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int D = 64;     // head dim
+constexpr int KB = 64;    // keys per LDS tile
+constexpr int QW = 32;    // queries per wave
+constexpr int LDK = 72;   // padded LDS row, bf16 elements (144 B)
+
+struct AttnArgs {
+    const bf16* q;
+    const bf16* k;
+    const bf16* v;
+    long long sq, sk, sv;  // row strides (elements)
+    int B, H, Lq, Lk;
+    float scale2;          // softmax scale * log2(e)
+    uint32_t thresh;       // dropout: drop when the 16-bit hash half < thresh (0 = off)
+    float keep_scale;      // 1 / (1 - p)
+    const int64_t* seed;   // device counter (advanced once per step by the host code)
+    uint32_t site;         // call-site id
+    bf16* o;
+    long long so;
+    float* lse;            // (B*H, Lq), log2 domain: m*scale2 + log2(l)
+    float* part_o;         // split-K partials (nsplit, B*H, Lq, 64) unnormalised
+    float* part_ml;        // (nsplit, B*H, Lq, 2): m*scale2, l
+    int nsplit, keys_per_split;
+};
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+// per (seed, site, b*H+h) scalar mix; per query base; per (query, key) hash
+__device__ __forceinline__ uint32_t drop_head_mix(const int64_t* seed, uint32_t site, uint32_t bh) {
+    const uint64_t s = (uint64_t)*seed;
+    return mix32((uint32_t)s ^ mix32((uint32_t)(s >> 32) + site * 0x9E3779B9u) ^ (bh * 0x85EBCA6Bu));
+}
+__device__ __forceinline__ uint32_t drop_query_base(uint32_t hm, uint32_t q) {
+    return mix32(hm ^ (q * 0xC2B2AE35u));
+}
+// one 32-bit hash per (query, key pair k>>1): its low half decides the even key, the
+// high half the odd key (keep iff half >= thresh, thresh = round(p * 2^16))
+__device__ __forceinline__ uint32_t drop_pair(uint32_t qbase, uint32_t kpair) {
+    return mix32(qbase + kpair * 0x27D4EB2Fu);
+}
+__device__ __forceinline__ bool drop_keep(uint32_t qbase, uint32_t k, uint32_t thresh) {
+    const uint32_t hsh = drop_pair(qbase, k >> 1);
+    return ((k & 1u) ? (hsh >> 16) : (hsh & 0xffffu)) >= thresh;
+}
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// online-softmax rescale only when a query's running max grows by more than this
+// (log2 units): P stays <= 2^8 between rescales (cdna_hip_programming.md T13)
+constexpr float RESCALE_THR = 8.f;
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x4 tr16(const bf16* p) {
+    s16x4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(p));
+    return __builtin_bit_cast(bf16x4, r);
+}
+
+// A operand of O^T += V^T P^T for d-tile dt and key k-step (t, s): lane (r = d, h)
+// element j = V[32t + 16s + 8(j>>2) + 4h + (j&3)][32dt + r]  (see header)
+__device__ __forceinline__ bf16x8 v_operand(const bf16* Vs, int lane, int dt, int t, int s) {
+    const int g = lane >> 4, i = lane & 15;
+    const int d0 = 32 * dt + 16 * (g & 1) + 4 * (i & 3);
+    const int k0 = 32 * t + 16 * s + 4 * (g >> 1) + (i >> 2);
+    const bf16x4 lo = tr16(Vs + k0 * LDK + d0);
+    const bf16x4 hi = tr16(Vs + (k0 + 8) * LDK + d0);
+    bf16x8 a;
+    a[0] = lo[0]; a[1] = lo[1]; a[2] = lo[2]; a[3] = lo[3];
+    a[4] = hi[0]; a[5] = hi[1]; a[6] = hi[2]; a[7] = hi[3];
+    return a;
+}
+
+template <bool DROP>
+__global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
+    __shared__ __attribute__((aligned(16))) bf16 Ks[2][KB * LDK];
+    __shared__ __attribute__((aligned(16))) bf16 Vs[2][KB * LDK];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int bh = blockIdx.y, b = bh / a.H, hh = bh - b * a.H;
+    const int q0 = blockIdx.x * (4 * QW) + wave * QW;
+    const bool active = q0 < a.Lq;
+    const int kbeg = blockIdx.z * a.keys_per_split;
+    const int kend = min(a.Lk, kbeg + a.keys_per_split);
+
+    bf16x8 qf[4];
+    {
+        const int qi = active ? q0 + r : 0;
+        const bf16* qrow = a.q + ((size_t)qi * a.B + b) * a.sq + hh * D;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qrow + 16 * s + 8 * h);
+    }
+    uint32_t qbase = 0;
+    if (DROP) qbase = drop_query_base(drop_head_mix(a.seed, a.site, bh), active ? q0 + r : 0);
+
+    // cooperative tile load: 64 keys x 8 chunks of 8 bf16 = 512 chunks, 2 per thread
+    bf16x8 kr[2], vr[2];
+    auto load = [&](int kb) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int idx = tid + 256 * c, key = kb + (idx >> 3), ch = idx & 7;
+            const int kk = key < a.Lk ? key : a.Lk - 1;
+            kr[c] = *reinterpret_cast<const bf16x8*>(a.k + ((size_t)kk * a.B + b) * a.sk + hh * D + 8 * ch);
+            vr[c] = *reinterpret_cast<const bf16x8*>(a.v + ((size_t)kk * a.B + b) * a.sv + hh * D + 8 * ch);
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int idx = tid + 256 * c, key = idx >> 3, ch = idx & 7;
+            *reinterpret_cast<bf16x8*>(&Ks[buf][key * LDK + 8 * ch]) = kr[c];
+            *reinterpret_cast<bf16x8*>(&Vs[buf][key * LDK + 8 * ch]) = vr[c];
+        }
+    };
+
+    f32x16 o[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[0][i] = o[1][i] = 0.f;
+    float m = -INFINITY, l = 0.f;
+
+    if (kbeg < kend) {
+        load(kbeg);
+        store(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int kb = kbeg; kb < kend; kb += KB, buf ^= 1) {
+        const bool more = kb + KB < kend;
+        if (more) load(kb + KB);
+        if (active) {
+            const bf16* K = Ks[buf];
+            const bf16* V = Vs[buf];
+            f32x16 st[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) st[t][i] = 0.f;
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const bf16x8 ka = *reinterpret_cast<const bf16x8*>(K + (32 * t + r) * LDK + 16 * s + 8 * h);
+                    st[t] = mfma(ka, qf[s], st[t]);
+                }
+            }
+            // keys past Lk (last partial tile) do not take part
+            const int nvalid = kend - kb;
+            if (nvalid < KB) {
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        if (32 * t + (i & 3) + 8 * (i >> 2) + 4 * h >= nvalid) st[t][i] = -INFINITY;
+            }
+            float mx = -INFINITY;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) mx = fmaxf(mx, st[t][i]);
+            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            // deferred rescale (T13): keep the stale max unless some query's max grew a lot
+            if (__any((mx - m) * a.scale2 > RESCALE_THR)) {
+                const float mnew = fmaxf(m, mx);
+                const float alpha = fast_exp2((m - mnew) * a.scale2);
+                m = mnew;
+                l *= alpha;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    o[0][i] *= alpha;
+                    o[1][i] *= alpha;
+                }
+            }
+            const float mb = m * a.scale2;
+            float rs = 0.f;
+            bf16x8 pf[2][2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int i = 0; i < 16; i += 2) {
+                    float p0 = fast_exp2(fmaf(st[t][i], a.scale2, -mb));
+                    float p1 = fast_exp2(fmaf(st[t][i + 1], a.scale2, -mb));
+                    rs += p0 + p1;
+                    if (DROP) {
+                        const int kk = kb + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;   // even
+                        const uint32_t hsh = drop_pair(qbase, (uint32_t)kk >> 1);
+                        p0 = (hsh & 0xffffu) >= a.thresh ? p0 * a.keep_scale : 0.f;
+                        p1 = (hsh >> 16) >= a.thresh ? p1 * a.keep_scale : 0.f;
+                    }
+                    pf[t][i >> 3][i & 7] = (bf16)p0;
+                    pf[t][i >> 3][(i & 7) + 1] = (bf16)p1;
+                }
+            l += rs;
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) o[dt] = mfma(v_operand(V, lane, dt, t, s), pf[t][s], o[dt]);
+        }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+    }
+    if (!active) return;
+    const float ltot = l + __shfl_xor(l, 32);
+    const int q = q0 + r;
+    if (a.nsplit == 1) {
+        const float inv = ltot > 0.f ? 1.f / ltot : 0.f;
+        bf16* orow = a.o + ((size_t)q * a.B + b) * a.so + hh * D;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                bf16x4 w;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) w[j] = (bf16)(o[dt][4 * g + j] * inv);
+                *reinterpret_cast<bf16x4*>(orow + 32 * dt + 8 * g + 4 * h) = w;
+            }
+        if (h == 0) a.lse[(size_t)bh * a.Lq + q] = m * a.scale2 + log2f(ltot);
+    } else {
+        const size_t row = ((size_t)blockIdx.z * gridDim.y + bh) * a.Lq + q;
+        float* po = a.part_o + row * D;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                float4 w = make_float4(o[dt][4 * g], o[dt][4 * g + 1], o[dt][4 * g + 2], o[dt][4 * g + 3]);
+                *reinterpret_cast<float4*>(po + 32 * dt + 8 * g + 4 * h) = w;
+            }
+        if (h == 0) {
+            a.part_ml[2 * row] = m == -INFINITY ? -INFINITY : m * a.scale2;
+            a.part_ml[2 * row + 1] = ltot;
+        }
+    }
+}
+
+// merge split-K partials: one 64-lane wave per (b*H+h, query); lane = d
+__global__ void __launch_bounds__(256) attn_combine_kernel(AttnArgs a) {
+    const int w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, d = threadIdx.x & 63;
+    const int BH = a.B * a.H;
+    if (w >= BH * a.Lq) return;
+    const int bh = w / a.Lq, q = w - bh * a.Lq;
+    const int b = bh / a.H, hh = bh - b * a.H;
+    float M = -INFINITY;
+    for (int s = 0; s < a.nsplit; ++s) M = fmaxf(M, a.part_ml[2 * (((size_t)s * BH + bh) * a.Lq + q)]);
+    float L = 0.f, acc = 0.f;
+    for (int s = 0; s < a.nsplit; ++s) {
+        const size_t row = ((size_t)s * BH + bh) * a.Lq + q;
+        const float ms = a.part_ml[2 * row];
+        if (ms == -INFINITY) continue;
+        const float wgt = exp2f(ms - M);
+        L = fmaf(a.part_ml[2 * row + 1], wgt, L);
+        acc = fmaf(a.part_o[row * D + d], wgt, acc);
+    }
+    a.o[((size_t)q * a.B + b) * a.so + hh * D + d] = (bf16)(L > 0.f ? acc / L : 0.f);
+    if (d == 0) a.lse[(size_t)bh * a.Lq + q] = M + log2f(L);
+}
+
+
+// ---------------------------------------------------------------- backward
+// Gradients of O = dropout(softmax(scale Q K^T)) V with the saved lse (log2 domain):
+//   P = exp2(scale2 S - lse2), P~ = P Z/(1-p), dP~ = dO V^T, dS = P (dP~ Z/(1-p) - D),
+//   D = rowsum(dO o O), dQ = scale dS K, dK = scale dS^T Q, dV = P~^T dO.
+// attn_bwd_dq_kernel (swapped layout as the forward, a lane owns a query) computes D,
+// stores it, and dQ; attn_bwd_dkdv_kernel (a lane owns a key) computes dK and dV.
+
+struct AttnBwdArgs {
+    AttnArgs f;
+    const bf16* o;        // forward output rows (stride f.so)
+    const bf16* dout;     // grad rows (stride sdo)
+    long long sdo;
+    float* dvec;          // (B*H, Lq) D
+    bf16* dq;
+    bf16* dk;
+    bf16* dv;
+    long long sdq, sdk, sdv;
+    float scale;
+};
+
+__global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnBwdArgs A) {
+    const AttnArgs& a = A.f;
+    __shared__ __attribute__((aligned(16))) bf16 Ks[2][KB * LDK];
+    __shared__ __attribute__((aligned(16))) bf16 Vs[2][KB * LDK];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int bh = blockIdx.y, b = bh / a.H, hh = bh - b * a.H;
+    const int q0 = blockIdx.x * (4 * QW) + wave * QW;
+    const bool active = q0 < a.Lq;
+    const int qi = active ? q0 + r : 0;
+    const bool drop = a.thresh != 0;
+
+    bf16x8 qf[4], df[4];
+    float dsum = 0.f;
+    {
+        const bf16* qrow = a.q + ((size_t)qi * a.B + b) * a.sq + hh * D;
+        const bf16* drow = A.dout + ((size_t)qi * a.B + b) * A.sdo + hh * D;
+        const bf16* orow = A.o + ((size_t)qi * a.B + b) * a.so + hh * D;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            qf[s] = *reinterpret_cast<const bf16x8*>(qrow + 16 * s + 8 * h);
+            df[s] = *reinterpret_cast<const bf16x8*>(drow + 16 * s + 8 * h);
+            const bf16x8 ov = *reinterpret_cast<const bf16x8*>(orow + 16 * s + 8 * h);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dsum = fmaf((float)df[s][j], (float)ov[j], dsum);
+        }
+    }
+    dsum += __shfl_xor(dsum, 32);
+    const float lse2 = active ? a.lse[(size_t)bh * a.Lq + qi] : 0.f;
+    if (active && h == 0) A.dvec[(size_t)bh * a.Lq + qi] = dsum;
+    uint32_t qbase = 0;
+    if (drop) qbase = drop_query_base(drop_head_mix(a.seed, a.site, bh), qi);
+
+    bf16x8 kr[2], vr[2];
+    auto load = [&](int kb) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int idx = tid + 256 * c, key = kb + (idx >> 3), ch = idx & 7;
+            const int kk = key < a.Lk ? key : a.Lk - 1;
+            kr[c] = *reinterpret_cast<const bf16x8*>(a.k + ((size_t)kk * a.B + b) * a.sk + hh * D + 8 * ch);
+            vr[c] = *reinterpret_cast<const bf16x8*>(a.v + ((size_t)kk * a.B + b) * a.sv + hh * D + 8 * ch);
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int idx = tid + 256 * c, key = idx >> 3, ch = idx & 7;
+            *reinterpret_cast<bf16x8*>(&Ks[buf][key * LDK + 8 * ch]) = kr[c];
+            *reinterpret_cast<bf16x8*>(&Vs[buf][key * LDK + 8 * ch]) = vr[c];
+        }
+    };
+    f32x16 dqt[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dqt[0][i] = dqt[1][i] = 0.f;
+    load(0);
+    store(0);
+    __syncthreads();
+    int buf = 0;
+    for (int kb = 0; kb < a.Lk; kb += KB, buf ^= 1) {
+        const bool more = kb + KB < a.Lk;
+        if (more) load(kb + KB);
+        if (active) {
+            const bf16* K = Ks[buf];
+            const bf16* V = Vs[buf];
+            const int nvalid = a.Lk - kb;
+            bf16x8 dsf[2][2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                f32x16 st, dpt;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) st[i] = dpt[i] = 0.f;
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const bf16x8 ka = *reinterpret_cast<const bf16x8*>(K + (32 * t + r) * LDK + 16 * s + 8 * h);
+                    const bf16x8 va = *reinterpret_cast<const bf16x8*>(V + (32 * t + r) * LDK + 16 * s + 8 * h);
+                    st = mfma(ka, qf[s], st);
+                    dpt = mfma(va, df[s], dpt);
+                }
+#pragma unroll
+                for (int i = 0; i < 16; i += 2) {
+                    const int kr0 = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;   // even
+                    float p0 = kr0 < nvalid ? fast_exp2(fmaf(st[i], a.scale2, -lse2)) : 0.f;
+                    float p1 = kr0 + 1 < nvalid ? fast_exp2(fmaf(st[i + 1], a.scale2, -lse2)) : 0.f;
+                    float dp0 = dpt[i], dp1 = dpt[i + 1];
+                    if (drop) {
+                        const uint32_t hsh = drop_pair(qbase, (uint32_t)(kb + kr0) >> 1);
+                        dp0 = (hsh & 0xffffu) >= a.thresh ? dp0 * a.keep_scale : 0.f;
+                        dp1 = (hsh >> 16) >= a.thresh ? dp1 * a.keep_scale : 0.f;
+                    }
+                    dsf[t][i >> 3][i & 7] = (bf16)(p0 * (dp0 - dsum));
+                    dsf[t][i >> 3][(i & 7) + 1] = (bf16)(p1 * (dp1 - dsum));
+                }
+            }
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) dqt[dt] = mfma(v_operand(K, lane, dt, t, s), dsf[t][s], dqt[dt]);
+        }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+    }
+    if (!active) return;
+    bf16* row = A.dq + ((size_t)qi * a.B + b) * A.sdq + hh * D;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            bf16x4 w;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w[j] = (bf16)(dqt[dt][4 * g + j] * A.scale);
+            *reinterpret_cast<bf16x4*>(row + 32 * dt + 8 * g + 4 * h) = w;
+        }
+}
+
+// a lane owns a key: S = Q K^T tiles (32 queries x 32 keys) with the query on the registers
+__global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
+    const AttnArgs& a = A.f;
+    constexpr int QB = 64;   // queries per LDS tile
+    __shared__ __attribute__((aligned(16))) bf16 Qs[2][QB * LDK];
+    __shared__ __attribute__((aligned(16))) bf16 Ds[2][QB * LDK];
+    __shared__ __attribute__((aligned(16))) float Ls[2][QB];
+    __shared__ __attribute__((aligned(16))) float Dv[2][QB];
+    __shared__ __attribute__((aligned(16))) uint32_t Zb[2][QB];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int bh = blockIdx.y, b = bh / a.H, hh = bh - b * a.H;
+    const int k0 = blockIdx.x * (4 * 32) + wave * 32;
+    const bool active = k0 < a.Lk;
+    const int ki = active ? min(k0 + r, a.Lk - 1) : 0;
+    const bool drop = a.thresh != 0;
+    const uint32_t hmix = drop ? drop_head_mix(a.seed, a.site, bh) : 0u;
+
+    bf16x8 kf[4], vf[4];
+    {
+        const bf16* krow = a.k + ((size_t)ki * a.B + b) * a.sk + hh * D;
+        const bf16* vrow = a.v + ((size_t)ki * a.B + b) * a.sv + hh * D;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            kf[s] = *reinterpret_cast<const bf16x8*>(krow + 16 * s + 8 * h);
+            vf[s] = *reinterpret_cast<const bf16x8*>(vrow + 16 * s + 8 * h);
+        }
+    }
+    bf16x8 qr[2], dr[2];
+    float lr = 0.f, dvr = 0.f;
+    uint32_t zr = 0u;
+    auto load = [&](int qb) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int idx = tid + 256 * c, qq = qb + (idx >> 3), ch = idx & 7;
+            const int qc = qq < a.Lq ? qq : a.Lq - 1;
+            qr[c] = *reinterpret_cast<const bf16x8*>(a.q + ((size_t)qc * a.B + b) * a.sq + hh * D + 8 * ch);
+            dr[c] = *reinterpret_cast<const bf16x8*>(A.dout + ((size_t)qc * a.B + b) * A.sdo + hh * D + 8 * ch);
+        }
+        if (tid < QB) {
+            const int qq = qb + tid;
+            const int qc = qq < a.Lq ? qq : a.Lq - 1;
+            // queries past Lq: lse = +inf -> P = 0
+            lr = qq < a.Lq ? a.lse[(size_t)bh * a.Lq + qc] : INFINITY;
+            dvr = A.dvec[(size_t)bh * a.Lq + qc];
+            if (drop) zr = drop_query_base(hmix, (uint32_t)qq);
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int idx = tid + 256 * c, qq = idx >> 3, ch = idx & 7;
+            *reinterpret_cast<bf16x8*>(&Qs[buf][qq * LDK + 8 * ch]) = qr[c];
+            *reinterpret_cast<bf16x8*>(&Ds[buf][qq * LDK + 8 * ch]) = dr[c];
+        }
+        if (tid < QB) {
+            Ls[buf][tid] = lr;
+            Dv[buf][tid] = dvr;
+            Zb[buf][tid] = zr;
+        }
+    };
+    f32x16 dkt[2], dvt[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dkt[0][i] = dkt[1][i] = dvt[0][i] = dvt[1][i] = 0.f;
+    const bool kvalid = active && (k0 + r) < a.Lk;
+    load(0);
+    store(0);
+    __syncthreads();
+    int buf = 0;
+    for (int qb = 0; qb < a.Lq; qb += QB, buf ^= 1) {
+        const bool more = qb + QB < a.Lq;
+        if (more) load(qb + QB);
+        if (active) {
+            const bf16* Q = Qs[buf];
+            const bf16* DO = Ds[buf];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                f32x16 st, dpt;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) st[i] = dpt[i] = 0.f;
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Q + (32 * u + r) * LDK + 16 * s + 8 * h);
+                    const bf16x8 da = *reinterpret_cast<const bf16x8*>(DO + (32 * u + r) * LDK + 16 * s + 8 * h);
+                    st = mfma(qa, kf[s], st);
+                    dpt = mfma(da, vf[s], dpt);
+                }
+                bf16x8 pf[2], dsf[2];
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int qrow = 32 * u + 8 * g + 4 * h;      // rows 4g..4g+3 of the tile
+                    const float4 l4 = *reinterpret_cast<const float4*>(&Ls[buf][qrow]);
+                    const float4 d4 = *reinterpret_cast<const float4*>(&Dv[buf][qrow]);
+                    const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int i = 4 * g + j;
+                        float p = kvalid ? fast_exp2(fmaf(st[i], a.scale2, -lv[j])) : 0.f;
+                        float pd = p, dp = dpt[i];
+                        if (drop) {
+                            const bool kp = drop_keep(Zb[buf][qrow + j], (uint32_t)(k0 + r), a.thresh);
+                            pd = kp ? p * a.keep_scale : 0.f;
+                            dp = kp ? dp * a.keep_scale : 0.f;
+                        }
+                        pf[i >> 3][i & 7] = (bf16)pd;
+                        dsf[i >> 3][i & 7] = (bf16)(p * (dp - dv4[j]));
+                    }
+                }
+#pragma unroll
+                for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        const int tt = u;   // query sub-tile = k-step block of 32 rows
+                        dvt[dt] = mfma(v_operand(DO, lane, dt, tt, s), pf[s], dvt[dt]);
+                        dkt[dt] = mfma(v_operand(Q, lane, dt, tt, s), dsf[s], dkt[dt]);
+                    }
+            }
+        }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+    }
+    if (!kvalid) return;
+    const int kk = k0 + r;
+    bf16* krow = A.dk + ((size_t)kk * a.B + b) * A.sdk + hh * D;
+    bf16* vrow = A.dv + ((size_t)kk * a.B + b) * A.sdv + hh * D;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            bf16x4 wk, wv;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                wk[j] = (bf16)(dkt[dt][4 * g + j] * A.scale);
+                wv[j] = (bf16)dvt[dt][4 * g + j];
+            }
+            *reinterpret_cast<bf16x4*>(krow + 32 * dt + 8 * g + 4 * h) = wk;
+            *reinterpret_cast<bf16x4*>(vrow + 32 * dt + 8 * g + 4 * h) = wv;
+        }
+}
+
+}  // namespace
+
+extern "C" int ov3d_attn_fwd(const void* q, const void* k, const void* v, long long sq,
+                             long long sk, long long sv, int B, int H, int Lq, int Lk, float scale,
+                             float dropout_p, const int64_t* seed, int site, void* o, long long so,
+                             float* lse, float* workspace, int nsplit, void* stream) {
+    if (!q || !k || !v || !o || !lse || B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || (Lq % QW) ||
+        nsplit <= 0 || dropout_p < 0.f || dropout_p >= 1.f || (dropout_p > 0.f && !seed) ||
+        (nsplit > 1 && !workspace))
+        return OV3D_EINVAL;
+    AttnArgs a;
+    a.q = (const bf16*)q;
+    a.k = (const bf16*)k;
+    a.v = (const bf16*)v;
+    a.sq = sq;
+    a.sk = sk;
+    a.sv = sv;
+    a.B = B;
+    a.H = H;
+    a.Lq = Lq;
+    a.Lk = Lk;
+    a.scale2 = scale * 1.4426950408889634f;
+    a.thresh = dropout_p > 0.f ? (uint32_t)fminf(rintf(dropout_p * 65536.0f), 65535.0f) : 0u;
+    a.keep_scale = 1.f / (1.f - dropout_p);
+    a.seed = seed;
+    a.site = (uint32_t)site;
+    a.o = (bf16*)o;
+    a.so = so;
+    a.lse = lse;
+    // keys per split: a multiple of the tile
+    int kps = (Lk + nsplit - 1) / nsplit;
+    kps = (kps + KB - 1) / KB * KB;
+    nsplit = (Lk + kps - 1) / kps;
+    a.keys_per_split = kps;
+    a.nsplit = nsplit;
+    a.part_o = workspace;
+    a.part_ml = workspace ? workspace + (size_t)nsplit * B * H * Lq * D : nullptr;
+    hipStream_t st = ov3d_stream(stream);
+    dim3 grid((Lq + 4 * QW - 1) / (4 * QW), B * H, nsplit);
+    if (a.thresh)
+        attn_fwd_kernel<true><<<grid, 256, 0, st>>>(a);
+    else
+        attn_fwd_kernel<false><<<grid, 256, 0, st>>>(a);
+    OV3D_LAUNCH_CHECK();
+    if (nsplit > 1) {
+        const long long waves = (long long)B * H * Lq;
+        attn_combine_kernel<<<ov3d_cdiv(waves * 64, 256), 256, 0, st>>>(a);
+        OV3D_LAUNCH_CHECK();
+    }
+    return OV3D_OK;
+}
+
+/* workspace floats needed by ov3d_attn_fwd for a given split count */
+extern "C" long long ov3d_attn_fwd_workspace(int B, int H, int Lq, int Lk, int nsplit) {
+    if (nsplit <= 1) return 0;
+    int kps = (Lk + nsplit - 1) / nsplit;
+    kps = (kps + KB - 1) / KB * KB;
+    nsplit = (Lk + kps - 1) / kps;
+    if (nsplit <= 1) return 0;
+    return (long long)nsplit * B * H * Lq * (D + 2);
+}
+
+extern "C" int ov3d_attn_bwd(const void* q, const void* k, const void* v, long long sq,
+                             long long sk, long long sv, const void* o, long long so,
+                             const void* dout, long long sdo, const float* lse, int B, int H,
+                             int Lq, int Lk, float scale, float dropout_p, const int64_t* seed,
+                             int site, float* dvec, void* dq, long long sdq, void* dk,
+                             long long sdk, void* dv, long long sdv, void* stream) {
+    if (!q || !k || !v || !o || !dout || !lse || !dvec || !dq || !dk || !dv || B <= 0 || H <= 0 ||
+        Lq <= 0 || Lk <= 0 || (Lq % QW) || dropout_p < 0.f || dropout_p >= 1.f ||
+        (dropout_p > 0.f && !seed))
+        return OV3D_EINVAL;
+    AttnBwdArgs A;
+    AttnArgs& a = A.f;
+    a.q = (const bf16*)q;
+    a.k = (const bf16*)k;
+    a.v = (const bf16*)v;
+    a.sq = sq;
+    a.sk = sk;
+    a.sv = sv;
+    a.B = B;
+    a.H = H;
+    a.Lq = Lq;
+    a.Lk = Lk;
+    a.scale2 = scale * 1.4426950408889634f;
+    a.thresh = dropout_p > 0.f ? (uint32_t)fminf(rintf(dropout_p * 65536.0f), 65535.0f) : 0u;
+    a.keep_scale = 1.f / (1.f - dropout_p);
+    a.seed = seed;
+    a.site = (uint32_t)site;
+    a.so = so;
+    a.lse = (float*)lse;
+    a.o = nullptr;
+    A.o = (const bf16*)o;
+    A.dout = (const bf16*)dout;
+    A.sdo = sdo;
+    A.dvec = dvec;
+    A.dq = (bf16*)dq;
+    A.dk = (bf16*)dk;
+    A.dv = (bf16*)dv;
+    A.sdq = sdq;
+    A.sdk = sdk;
+    A.sdv = sdv;
+    A.scale = scale;
+    hipStream_t st = ov3d_stream(stream);
+    attn_bwd_dq_kernel<<<dim3((Lq + 4 * QW - 1) / (4 * QW), B * H), 256, 0, st>>>(A);
+    OV3D_LAUNCH_CHECK();
+    attn_bwd_dkdv_kernel<<<dim3((Lk + 127) / 128, B * H), 256, 0, st>>>(A);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}

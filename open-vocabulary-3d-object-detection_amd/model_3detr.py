@@ -22,6 +22,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+from . import attention as flash
 from . import pointnet2_utils as pu
 from .helpers import GenericMLP
 from .pc_util import scale_points, shift_scale_points
@@ -199,6 +200,8 @@ class Model3DETR(nn.Module):
 
     def forward(self, inputs, encoder_only=False):
         pc = inputs["point_clouds"]
+        if self.training and pc.is_cuda:
+            flash.next_step(pc.device)   # fresh attention-dropout stream for this step
         enc_xyz, enc_feats, _ = self.run_encoder(pc, inputs.get("pre_enc_inds"))   # (N', B, C)
         Np, B, C = enc_feats.shape
         enc_feats = self.encoder_to_decoder_projection.rows(enc_feats.reshape(Np * B, C)).view(Np, B, -1)

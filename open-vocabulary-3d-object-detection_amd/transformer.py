@@ -4,10 +4,11 @@ Layout: sequence-first (L, B, C) tensors exactly as the reference, and the
 attention modules keep ``nn.MultiheadAttention``'s parameter names
 (``in_proj_weight``, ``in_proj_bias``, ``out_proj.{weight,bias}``) so reference
 checkpoints load.  Differences that do not change results:
-  * attention runs through fused scaled-dot-product attention and never
-    materialises the head-averaged weights that ``nn.MultiheadAttention``
-    computes and the reference discards (need_weights=True by default,
-    transformer.py:271-272, 365-372);
+  * attention runs through the HIP flash-attention kernels (attention.py,
+    csrc/attn.hip; bf16, no mask) or fused scaled-dot-product attention (fp32,
+    masked encoder) and never materialises the head-averaged weights that
+    ``nn.MultiheadAttention`` computes and the reference discards
+    (need_weights=True by default, transformer.py:271-272, 365-372);
   * ``memory + pos`` is formed once and shared by the 8 decoder layers.
 """
 from typing import Optional
@@ -16,6 +17,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
+from . import attention as flash
 from .gemm import in_projection, rows_linear
 from .helpers import ACTIVATION_DICT, NORM_DICT, get_clones
 
@@ -34,6 +36,7 @@ class MultiheadAttention(nn.Module):
         self.out_proj = nn.Linear(embed_dim, embed_dim)
         nn.init.xavier_uniform_(self.in_proj_weight)
         nn.init.zeros_(self.out_proj.bias)
+        self.site = flash.new_site()   # dropout hash stream of this module (attention.py)
 
     def _heads(self, x, L, B):
         return x.view(L, B, self.num_heads, self.head_dim).permute(1, 2, 0, 3)
@@ -43,12 +46,22 @@ class MultiheadAttention(nn.Module):
         S = key.shape[0]
         w, bias = self.in_proj_weight, self.in_proj_bias
         if query is key and key is value:
-            q, k, v = rows_linear(query, w, bias).chunk(3, dim=-1)
+            srcs = [rows_linear(query, w, bias)]
+            spec = ((0, 0), (0, E), (0, 2 * E))
         elif query is key:
-            qk, v = in_projection(w, bias, ((query, 0, 2 * E), (value, 2 * E, 3 * E)))
-            q, k = qk.chunk(2, dim=-1)
+            srcs = list(in_projection(w, bias, ((query, 0, 2 * E), (value, 2 * E, 3 * E))))
+            spec = ((0, 0), (0, E), (1, 0))
         else:
-            q, k, v = in_projection(w, bias, ((query, 0, E), (key, E, 2 * E), (value, 2 * E, 3 * E)))
+            srcs = list(in_projection(w, bias, ((query, 0, E), (key, E, 2 * E), (value, 2 * E, 3 * E))))
+            spec = ((0, 0), (1, 0), (2, 0))
+        if srcs[0].dtype == torch.bfloat16 and flash.supported(srcs[0], srcs[spec[1][0]],
+                                                               self.num_heads, attn_mask):
+            # HIP flash attention straight on the projection rows (csrc/attn.hip)
+            out = flash.attention_packed(srcs, spec, L, S, self.num_heads,
+                                         dropout_p=self.dropout if self.training else 0.0,
+                                         site=self.site)
+            return rows_linear(out, self.out_proj.weight, self.out_proj.bias)
+        q, k, v = (srcs[i][..., off:off + E] for i, off in spec)
         q, k, v = self._heads(q, L, B), self._heads(k, S, B), self._heads(v, S, B)
         mask = None
         if attn_mask is not None:

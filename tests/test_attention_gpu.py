@@ -1,0 +1,123 @@
+"""Flash attention kernels (csrc/attn.hip) against a plain PyTorch fp32 reference of the
+same op on the same bf16 inputs: softmax(q k^T / 8) [dropout] v per head, forward and
+all three gradients.  Tolerances: bf16 rounding of P / dS inside the kernel (relative
+Frobenius error <= 1e-2).  With dropout the reference rebuilds the kernel's keep mask
+from the documented hash, so the comparison is exact in the mask."""
+import numpy as np
+import pytest
+import torch
+
+from helpers import ov3d  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+M32 = 0xFFFFFFFF
+
+
+def _mix32(x):
+    x = x & M32
+    x = x ^ (x >> 16)
+    x = (x * 0x7feb352d) & M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846ca68b) & M32
+    x = x ^ (x >> 16)
+    return x
+
+
+def keep_mask(seed, site, B, H, Lq, Lk, p, device):
+    """attn.hip drop_head_mix / drop_query_base / drop_pair (16-bit half per key), in int64
+    torch arithmetic."""
+    s = int(seed)
+    lo, hi = s & M32, (s >> 32) & M32
+    bh = torch.arange(B * H, dtype=torch.int64, device=device)
+    inner = _mix32(torch.tensor(hi + site * 0x9E3779B9, dtype=torch.int64, device=device))
+    hm = _mix32(lo ^ inner ^ ((bh * 0x85EBCA6B) & M32))                       # (BH,)
+    q = torch.arange(Lq, dtype=torch.int64, device=device)
+    qb = _mix32(hm[:, None] ^ ((q[None] * 0xC2B2AE35) & M32))                  # (BH, Lq)
+    k = torch.arange(Lk, dtype=torch.int64, device=device)
+    hsh = _mix32(qb[:, :, None] + (((k[None, None] >> 1) * 0x27D4EB2F) & M32))   # (BH, Lq, Lk)
+    half = torch.where((k & 1).bool()[None, None], hsh >> 16, hsh & 0xFFFF)
+    thresh = min(int(np.rint(np.float32(p) * np.float32(65536.0))), 65535) if p > 0 else 0
+    return (half >= thresh).view(B, H, Lq, Lk)
+
+
+def reference(q, k, v, H, p=0.0, mask=None):
+    """q (Lq,B,E), k/v (Lk,B,E) fp32 -> (Lq,B,E)"""
+    Lq, B, E = q.shape
+    Lk = k.shape[0]
+    d = E // H
+    qh = q.reshape(Lq, B, H, d).permute(1, 2, 0, 3)
+    kh = k.reshape(Lk, B, H, d).permute(1, 2, 0, 3)
+    vh = v.reshape(Lk, B, H, d).permute(1, 2, 0, 3)
+    pr = torch.softmax(qh @ kh.transpose(-1, -2) / d ** 0.5, dim=-1)
+    if mask is not None:
+        pr = pr * mask / (1 - p)
+    return (pr @ vh).permute(2, 0, 1, 3).reshape(Lq, B, E)
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+
+@pytest.mark.parametrize("Lq,Lk,B,H,packed", [(2048, 2048, 2, 4, "qkv"), (128, 2048, 8, 4, "cross"),
+                                              (128, 128, 8, 4, "qk"), (96, 200, 3, 2, "cross"),
+                                              (64, 64, 1, 1, "qkv")])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_matches_reference(cuda, Lq, Lk, B, H, packed, p):
+    from ov3d_amd import attention as A
+    torch.manual_seed(Lq + Lk + B)
+    E = H * 64
+    if packed == "qkv" and Lq == Lk:
+        base = (torch.randn(Lq, B, 3 * E, device=cuda) * 1.5).to(torch.bfloat16).requires_grad_()
+        q, k, v = base.chunk(3, dim=-1)
+        leaves = [base]
+    elif packed == "qk" and Lq == Lk:
+        qk = (torch.randn(Lq, B, 2 * E, device=cuda) * 1.5).to(torch.bfloat16).requires_grad_()
+        v0 = torch.randn(Lk, B, E, device=cuda).to(torch.bfloat16).requires_grad_()
+        q, k = qk.chunk(2, dim=-1)
+        v = v0
+        leaves = [qk, v0]
+    else:
+        q0 = (torch.randn(Lq, B, E, device=cuda) * 1.5).to(torch.bfloat16).requires_grad_()
+        k0 = (torch.randn(Lk, B, E, device=cuda) * 1.5).to(torch.bfloat16).requires_grad_()
+        v0 = torch.randn(Lk, B, E, device=cuda).to(torch.bfloat16).requires_grad_()
+        q, k, v = q0, k0, v0
+        leaves = [q0, k0, v0]
+    site = 7
+    seed = int(A._seed(q.device).item())
+    out = A.attention(q, k, v, H, dropout_p=p, site=site)
+    g = torch.randn_like(out.float())
+    out.float().backward(g)
+    got_grads = [t.grad.float().clone() for t in leaves]
+
+    mask = keep_mask(seed, site, B, H, Lq, Lk, p, cuda) if p > 0 else None
+    if mask is not None:
+        keep = mask.float().mean().item()
+        assert abs(keep - (1 - p)) < 5 * (p * (1 - p) / mask.numel()) ** 0.5 + 1e-3, keep
+    leaves_r = [t.detach().float().requires_grad_() for t in leaves]
+    if packed == "qkv" and Lq == Lk:
+        qr, kr, vr = leaves_r[0].chunk(3, dim=-1)
+    elif packed == "qk" and Lq == Lk:
+        qr, kr = leaves_r[0].chunk(2, dim=-1)
+        vr = leaves_r[1]
+    else:
+        qr, kr, vr = leaves_r
+    ref = reference(qr, kr, vr, H, p, mask)
+    ref.backward(g)
+    assert _rel(out, ref) < 1e-2, _rel(out, ref)
+    for gg, lr in zip(got_grads, leaves_r):
+        assert _rel(gg, lr.grad) < 2e-2, _rel(gg, lr.grad)
+
+
+def test_attention_seed_advances_and_is_reproducible(cuda):
+    from ov3d_amd import attention as A
+    torch.manual_seed(0)
+    x = torch.randn(128, 2, 3 * 128, device=cuda).to(torch.bfloat16)
+    q, k, v = x.chunk(3, dim=-1)
+    a1 = A.attention(q, k, v, 2, dropout_p=0.1, site=3)
+    a2 = A.attention(q, k, v, 2, dropout_p=0.1, site=3)
+    assert torch.equal(a1, a2)                    # same step, same site: same mask
+    a3 = A.attention(q, k, v, 2, dropout_p=0.1, site=4)
+    A.next_step(cuda)
+    a4 = A.attention(q, k, v, 2, dropout_p=0.1, site=3)
+    assert not torch.equal(a1, a3) and not torch.equal(a1, a4)

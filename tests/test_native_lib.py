@@ -12,7 +12,7 @@ from helpers import ROOT, ov3d
 
 def header_symbols():
     src = open(os.path.join(ROOT, "include", "ov3d.h")).read()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(ov3d_\w+)\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|long long|const char\*)\s+(ov3d_\w+)\(", src, flags=re.M)))
 
 
 def test_library_exports_every_header_symbol():

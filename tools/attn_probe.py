@@ -29,7 +29,44 @@ def bench(B, H, Lq, Lk, d=64, drop=0.1, iters=20):
     return tf / iters * 1e3, tb / iters * 1e3
 
 
-for lib in ("aotriton", "ck"):
+def bench_ov3d(B, H, Lq, Lk, d=64, drop=0.1, iters=20):
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import ov3d_import
+    ov3d_import.load()
+    from ov3d_amd import attention as A
+    dev = "cuda"
+    E = H * d
+    q = torch.randn(Lq, B, E, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(Lk, B, E, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(Lk, B, E, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    g = torch.randn(Lq, B, E, device=dev, dtype=torch.bfloat16)
+    for _ in range(3):
+        A.attention(q, k, v, H, drop, site=1).backward(g)
+    torch.cuda.synchronize()
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    tf = tb = 0.0
+    for _ in range(iters):
+        e[0].record()
+        o = A.attention(q, k, v, H, drop, site=1)
+        e[1].record()
+        o.backward(g)
+        e[2].record()
+        torch.cuda.synchronize()
+        tf += e[0].elapsed_time(e[1])
+        tb += e[1].elapsed_time(e[2])
+    return tf / iters * 1e3, tb / iters * 1e3
+
+
+for shp in [(8, 4, 2048, 2048), (8, 4, 128, 2048), (8, 4, 128, 128)]:
+    for drop in (0.0, 0.1):
+        f, b = bench_ov3d(*shp, drop=drop)
+        fl = 4.0 * shp[0] * shp[1] * shp[2] * shp[3] * 64
+        print(f"ov3d      {shp} drop={drop}: fwd {f:7.1f} us ({fl / f / 1e6:6.1f} TF/s)  "
+              f"bwd {b:7.1f} us ({2.5 * fl / b / 1e6:6.1f} TF/s)", flush=True)
+
+for lib in ("aotriton",):
     try:
         torch.backends.cuda.preferred_rocm_fa_library(lib)
     except Exception as ex:
