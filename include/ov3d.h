@@ -239,12 +239,15 @@ int ov3d_attn_fwd(const void* q, const void* k, const void* v, long long sq, lon
                   float* workspace, int nsplit, void* stream);
 long long ov3d_attn_fwd_workspace(int B, int H, int Lq, int Lk, int nsplit);
 /* Backward: dq/dk/dv rows (same layout, bf16) from o, dout (stride sdo), lse;
- * dvec (B*H, Lq) f32 scratch receives D = rowsum(dout * o). */
+ * dvec (B*H, Lq) f32 scratch receives D = rowsum(dout * o).  nsplit > 1 splits the
+ * dQ key loop over workgroups (fp32 partials in `workspace`, sized as for the forward
+ * by ov3d_attn_fwd_workspace). */
 int ov3d_attn_bwd(const void* q, const void* k, const void* v, long long sq, long long sk,
                   long long sv, const void* o, long long so, const void* dout, long long sdo,
                   const float* lse, int B, int H, int Lq, int Lk, float scale, float dropout_p,
                   const int64_t* seed, int site, float* dvec, void* dq, long long sdq, void* dk,
-                  long long sdk, void* dv, long long sdv, void* stream);
+                  long long sdk, void* dv, long long sdv, float* workspace, int nsplit,
+                  void* stream);
 
 #ifdef __cplusplus
 }

@@ -46,7 +46,7 @@ _SIGS = {
     "ov3d_roi_align_fwd": "piiiiipiiifiiipp",
     "ov3d_im2col3x3": "piiiiiiipp",
     "ov3d_attn_fwd": "pppllliiiiffpiplppip",
-    "ov3d_attn_bwd": "ppplllplplpiiiiffpipplplplp",
+    "ov3d_attn_bwd": "ppplllplplpiiiiffpipplplplpip",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace")
 

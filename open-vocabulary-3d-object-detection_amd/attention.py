@@ -101,6 +101,9 @@ class _Attention(torch.autograd.Function):
         do = do.to(torch.bfloat16).contiguous()
         grads = [torch.empty_like(s) for s in srcs]   # every column is written below
         dvec = torch.empty((B * H, Lq), dtype=torch.float32, device=q.device)
+        nsplit = _split(Lq, Lk, B * H)
+        ws_n = _native.load().ov3d_attn_fwd_workspace(B, H, Lq, Lk, nsplit)
+        ws = torch.empty((max(ws_n, 1),), dtype=torch.float32, device=q.device)
         qp, sq = _rows(q, qo, E)
         kp, sk = _rows(k, ko, E)
         vp, sv = _rows(v, vo, E)
@@ -110,7 +113,8 @@ class _Attention(torch.autograd.Function):
         rc = _native.load().ov3d_attn_bwd(
             qp, kp, vp, sq, sk, sv, _native._ptr(o), E, _native._ptr(do), E, _native._ptr(lse),
             B, H, Lq, Lk, HEAD_DIM ** -0.5, p, _native._ptr(_seed(q.device)), site,
-            _native._ptr(dvec), dqp, sdq, dkp, sdk, dvp, sdv, _native._stream(q))
+            _native._ptr(dvec), dqp, sdq, dkp, sdk, dvp, sdv, _native._ptr(ws), nsplit,
+            _native._stream(q))
         if rc:
             raise _native.NativeError(f"ov3d_attn_bwd failed with status {rc}")
         return (None, None, None, None, None, *grads)

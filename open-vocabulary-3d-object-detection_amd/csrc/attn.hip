@@ -316,7 +316,7 @@ struct AttnBwdArgs {
     float scale;
 };
 
-__global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnBwdArgs A) {
+__global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
     const AttnArgs& a = A.f;
     __shared__ __attribute__((aligned(16))) bf16 Ks[2][KB * LDK];
     __shared__ __attribute__((aligned(16))) bf16 Vs[2][KB * LDK];
@@ -345,7 +345,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnBwdArgs A) {
     }
     dsum += __shfl_xor(dsum, 32);
     const float lse2 = active ? a.lse[(size_t)bh * a.Lq + qi] : 0.f;
-    if (active && h == 0) A.dvec[(size_t)bh * a.Lq + qi] = dsum;
+    if (active && h == 0 && blockIdx.z == 0) A.dvec[(size_t)bh * a.Lq + qi] = dsum;
     uint32_t qbase = 0;
     if (drop) qbase = drop_query_base(drop_head_mix(a.seed, a.site, bh), qi);
 
@@ -370,17 +370,21 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnBwdArgs A) {
     f32x16 dqt[2];
 #pragma unroll
     for (int i = 0; i < 16; ++i) dqt[0][i] = dqt[1][i] = 0.f;
-    load(0);
-    store(0);
+    const int kbeg = blockIdx.z * a.keys_per_split;
+    const int kend = min(a.Lk, kbeg + a.keys_per_split);
+    if (kbeg < kend) {
+        load(kbeg);
+        store(0);
+    }
     __syncthreads();
     int buf = 0;
-    for (int kb = 0; kb < a.Lk; kb += KB, buf ^= 1) {
-        const bool more = kb + KB < a.Lk;
+    for (int kb = kbeg; kb < kend; kb += KB, buf ^= 1) {
+        const bool more = kb + KB < kend;
         if (more) load(kb + KB);
         if (active) {
             const bf16* K = Ks[buf];
             const bf16* V = Vs[buf];
-            const int nvalid = a.Lk - kb;
+            const int nvalid = kend - kb;
             bf16x8 dsf[2][2];
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
@@ -420,6 +424,16 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnBwdArgs A) {
         __syncthreads();
     }
     if (!active) return;
+    if (a.nsplit > 1) {   // fp32 partial per key split, summed by attn_dq_combine_kernel
+        float* po = a.part_o + (((size_t)blockIdx.z * gridDim.y + bh) * a.Lq + qi) * D;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                *reinterpret_cast<float4*>(po + 32 * dt + 8 * g + 4 * h) =
+                    make_float4(dqt[dt][4 * g], dqt[dt][4 * g + 1], dqt[dt][4 * g + 2], dqt[dt][4 * g + 3]);
+        return;
+    }
     bf16* row = A.dq + ((size_t)qi * a.B + b) * A.sdq + hh * D;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
@@ -432,8 +446,35 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnBwdArgs A) {
         }
 }
 
+// dq = scale * sum over key splits; one thread per (b*H+h, query, 4 dims)
+__global__ void __launch_bounds__(256) attn_dq_combine_kernel(AttnBwdArgs A) {
+    const AttnArgs& a = A.f;
+    const int BH = a.B * a.H;
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long long)BH * a.Lq * (D / 4)) return;
+    const int d4 = (int)(t % (D / 4));
+    const long long w = t / (D / 4);
+    const int bh = (int)(w / a.Lq), q = (int)(w - (long long)bh * a.Lq);
+    const int b = bh / a.H, hh = bh - b * a.H;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int sp = 0; sp < a.nsplit; ++sp) {
+        const float4 v = *reinterpret_cast<const float4*>(
+            a.part_o + (((size_t)sp * BH + bh) * a.Lq + q) * D + 4 * d4);
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+    }
+    bf16x4 o;
+    o[0] = (bf16)(acc.x * A.scale);
+    o[1] = (bf16)(acc.y * A.scale);
+    o[2] = (bf16)(acc.z * A.scale);
+    o[3] = (bf16)(acc.w * A.scale);
+    *reinterpret_cast<bf16x4*>(A.dq + ((size_t)q * a.B + b) * A.sdq + hh * D + 4 * d4) = o;
+}
+
 // a lane owns a key: S = Q K^T tiles (32 queries x 32 keys) with the query on the registers
-__global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
+__global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
     const AttnArgs& a = A.f;
     constexpr int QB = 64;   // queries per LDS tile
     __shared__ __attribute__((aligned(16))) bf16 Qs[2][QB * LDK];
@@ -639,7 +680,8 @@ extern "C" int ov3d_attn_bwd(const void* q, const void* k, const void* v, long l
                              const void* dout, long long sdo, const float* lse, int B, int H,
                              int Lq, int Lk, float scale, float dropout_p, const int64_t* seed,
                              int site, float* dvec, void* dq, long long sdq, void* dk,
-                             long long sdk, void* dv, long long sdv, void* stream) {
+                             long long sdk, void* dv, long long sdv, float* workspace,
+                             int nsplit, void* stream) {
     if (!q || !k || !v || !o || !dout || !lse || !dvec || !dq || !dk || !dv || B <= 0 || H <= 0 ||
         Lq <= 0 || Lk <= 0 || (Lq % QW) || dropout_p < 0.f || dropout_p >= 1.f ||
         (dropout_p > 0.f && !seed))
@@ -675,9 +717,20 @@ extern "C" int ov3d_attn_bwd(const void* q, const void* k, const void* v, long l
     A.sdk = sdk;
     A.sdv = sdv;
     A.scale = scale;
+    int kps = (Lk + (nsplit > 0 ? nsplit : 1) - 1) / (nsplit > 0 ? nsplit : 1);
+    kps = (kps + KB - 1) / KB * KB;
+    nsplit = (Lk + kps - 1) / kps;
+    if (nsplit > 1 && !workspace) return OV3D_EINVAL;
+    a.keys_per_split = kps;
+    a.nsplit = nsplit;
+    a.part_o = workspace;
     hipStream_t st = ov3d_stream(stream);
-    attn_bwd_dq_kernel<<<dim3((Lq + 4 * QW - 1) / (4 * QW), B * H), 256, 0, st>>>(A);
+    attn_bwd_dq_kernel<<<dim3((Lq + 4 * QW - 1) / (4 * QW), B * H, nsplit), 256, 0, st>>>(A);
     OV3D_LAUNCH_CHECK();
+    if (nsplit > 1) {
+        attn_dq_combine_kernel<<<ov3d_cdiv((long long)B * H * Lq * (D / 4), 256), 256, 0, st>>>(A);
+        OV3D_LAUNCH_CHECK();
+    }
     attn_bwd_dkdv_kernel<<<dim3((Lk + 127) / 128, B * H), 256, 0, st>>>(A);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
