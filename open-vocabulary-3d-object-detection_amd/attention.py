@@ -33,7 +33,12 @@ def new_site():
 def _seed(device):
     t = _SEEDS.get(device)
     if t is None:
-        t = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).to(device)
+        # drawn from torch's generator (seeded per rank by the caller, main.py:415-418), and
+        # offset by the rank so data-parallel replicas never share dropout masks
+        rank = torch.distributed.get_rank() if (torch.distributed.is_available()
+                                                and torch.distributed.is_initialized()) else 0
+        v = int(torch.randint(0, 2 ** 40, (1,), dtype=torch.int64)) + (rank << 48)
+        t = torch.tensor([v], dtype=torch.int64).to(device)
         _SEEDS[device] = t
     return t
 

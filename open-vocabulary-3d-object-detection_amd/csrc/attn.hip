@@ -168,21 +168,39 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
     int buf = 0;
     for (int kb = kbeg; kb < kend; kb += KB, buf ^= 1) {
         const bool more = kb + KB < kend;
-        if (more) load(kb + KB);
+        if (!active && more) load(kb + KB);
         if (active) {
             const bf16* K = Ks[buf];
             const bf16* V = Vs[buf];
+            // all LDS operand reads of the tile are issued ahead of their MFMAs, so their
+            // latency overlaps the matrix / softmax work instead of stalling each MFMA
+            bf16x8 ka[2][4];
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+                    ka[t][s] = *reinterpret_cast<const bf16x8*>(K + (32 * t + r) * LDK + 16 * s + 8 * h);
             f32x16 st[2];
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
 #pragma unroll
                 for (int i = 0; i < 16; ++i) st[t][i] = 0.f;
-#pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    const bf16x8 ka = *reinterpret_cast<const bf16x8*>(K + (32 * t + r) * LDK + 16 * s + 8 * h);
-                    st[t] = mfma(ka, qf[s], st[t]);
-                }
             }
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int t = 0; t < 2; ++t) st[t] = mfma(ka[t][s], qf[s], st[t]);
+            bf16x8 va[2][2][2];
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) va[dt][t][s] = v_operand(V, lane, dt, t, s);
+            // next tile's global loads go out after this tile's LDS operand reads: issued
+            // earlier, their address registers collide with the operand registers and the
+            // compiler waits for the loads inside the score MFMAs
+            if (more) load(kb + KB);
             // keys past Lk (last partial tile) do not take part
             const int nvalid = kend - kb;
             if (nvalid < KB) {
@@ -231,11 +249,11 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
                 }
             l += rs;
 #pragma unroll
-            for (int dt = 0; dt < 2; ++dt)
+            for (int t = 0; t < 2; ++t)
 #pragma unroll
-                for (int t = 0; t < 2; ++t)
+                for (int s = 0; s < 2; ++s)
 #pragma unroll
-                    for (int s = 0; s < 2; ++s) o[dt] = mfma(v_operand(V, lane, dt, t, s), pf[t][s], o[dt]);
+                    for (int dt = 0; dt < 2; ++dt) o[dt] = mfma(va[dt][t][s], pf[t][s], o[dt]);
         }
         if (more) store(buf ^ 1);
         __syncthreads();
