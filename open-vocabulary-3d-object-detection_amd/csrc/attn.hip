@@ -73,10 +73,22 @@ __device__ __forceinline__ uint32_t drop_head_mix(const int64_t* seed, uint32_t 
 __device__ __forceinline__ uint32_t drop_query_base(uint32_t hm, uint32_t q) {
     return mix32(hm ^ (q * 0xC2B2AE35u));
 }
+// Per-element finaliser of the dropout hash: xor-shifts and 24-bit multiplies only
+// (v_mul_u32_u24 issues at the full VALU rate; the 32-bit v_mul_lo_u32 of mix32 is a
+// quarter-rate instruction and dominated the softmax).
+__device__ __forceinline__ uint32_t mix24(uint32_t x) {
+    x ^= x >> 16;
+    x = __umul24(x, 0x7feb35u) ^ (x >> 24);
+    x ^= x >> 15;
+    x = __umul24(x, 0x846ca7u) ^ (x >> 24);
+    x ^= x >> 16;
+    return x;
+}
+
 // one 32-bit hash per (query, key pair k>>1): its low half decides the even key, the
 // high half the odd key (keep iff half >= thresh, thresh = round(p * 2^16))
 __device__ __forceinline__ uint32_t drop_pair(uint32_t qbase, uint32_t kpair) {
-    return mix32(qbase + kpair * 0x27D4EB2Fu);
+    return mix24(qbase + kpair * 0x27D4EB2Fu);
 }
 __device__ __forceinline__ bool drop_keep(uint32_t qbase, uint32_t k, uint32_t thresh) {
     const uint32_t hsh = drop_pair(qbase, k >> 1);

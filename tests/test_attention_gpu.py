@@ -24,9 +24,23 @@ def _mix32(x):
     return x
 
 
+def _umul24(x, c):
+    return ((x & 0xFFFFFF) * (c & 0xFFFFFF)) & M32
+
+
+def _mix24(x):
+    x = x & M32
+    x = x ^ (x >> 16)
+    x = _umul24(x, 0x7feb35) ^ (x >> 24)
+    x = x ^ (x >> 15)
+    x = _umul24(x, 0x846ca7) ^ (x >> 24)
+    x = x ^ (x >> 16)
+    return x
+
+
 def keep_mask(seed, site, B, H, Lq, Lk, p, device):
-    """attn.hip drop_head_mix / drop_query_base / drop_pair (16-bit half per key), in int64
-    torch arithmetic."""
+    """attn.hip drop_head_mix / drop_query_base / drop_pair (mix24, 16-bit half per key), in
+    int64 torch arithmetic."""
     s = int(seed)
     lo, hi = s & M32, (s >> 32) & M32
     bh = torch.arange(B * H, dtype=torch.int64, device=device)
@@ -35,7 +49,7 @@ def keep_mask(seed, site, B, H, Lq, Lk, p, device):
     q = torch.arange(Lq, dtype=torch.int64, device=device)
     qb = _mix32(hm[:, None] ^ ((q[None] * 0xC2B2AE35) & M32))                  # (BH, Lq)
     k = torch.arange(Lk, dtype=torch.int64, device=device)
-    hsh = _mix32(qb[:, :, None] + (((k[None, None] >> 1) * 0x27D4EB2F) & M32))   # (BH, Lq, Lk)
+    hsh = _mix24(qb[:, :, None] + (((k[None, None] >> 1) * 0x27D4EB2F) & M32))   # (BH, Lq, Lk)
     half = torch.where((k & 1).bool()[None, None], hsh >> 16, hsh & 0xFFFF)
     thresh = min(int(np.rint(np.float32(p) * np.float32(65536.0))), 65535) if p > 0 else 0
     return (half >= thresh).view(B, H, Lq, Lk)
@@ -121,3 +135,17 @@ def test_attention_seed_advances_and_is_reproducible(cuda):
     A.next_step(cuda)
     a4 = A.attention(q, k, v, 2, dropout_p=0.1, site=3)
     assert not torch.equal(a1, a3) and not torch.equal(a1, a4)
+
+
+def test_dropout_hash_statistics(cuda):
+    """The keep mask behaves like i.i.d. Bernoulli(1 - p): overall rate within 5 sigma and
+    no correlation between neighbouring keys (same hash word), queries or heads."""
+    p = 0.1
+    m = keep_mask(123456789, 5, 2, 4, 512, 1024, p, cuda).float()     # 4.2M draws
+    n = m.numel()
+    assert abs(m.mean().item() - (1 - p)) < 5 * (p * (1 - p) / n) ** 0.5
+    z = (m - m.mean()) / m.std()
+    for a, b in [(z[..., 0::2], z[..., 1::2]), (z[..., :-1, :], z[..., 1:, :]),
+                 (z[:, :-1], z[:, 1:]), (z[:-1], z[1:])]:
+        corr = (a * b).mean().item()
+        assert abs(corr) < 5e-3, corr
