@@ -249,6 +249,20 @@ int ov3d_attn_bwd(const void* q, const void* k, const void* v, long long sq, lon
                   long long sdk, void* dv, long long sdv, float* workspace, int nsplit,
                   void* stream);
 
+/* ---- Linear-layer weight / bias gradient ----
+ * For every row-major dense layer y = x W^T + b of the step (transformer projections
+ * and FFNs, GenericMLP heads / projections; models/transformer.py, models/helpers.py):
+ *   dW (N, K) f32 (leading dim ldw) = dy^T x,  db (N) f32 = column sums of dy (db may be NULL)
+ *   dy (R, N) bf16 (row stride ldy), x (R, K) bf16 (row stride ldx).
+ * MFMA over row chunks; nsplit > 1 partials are summed in a fixed order by a second
+ * launch (deterministic).  workspace: ov3d_wgrad_workspace() floats; counters: unused
+ * (reserved, may be NULL). */
+int ov3d_wgrad(const void* dy, long long ldy, const void* x, long long ldx, int R, int N, int K,
+               float* dW, long long ldw, float* db, float* workspace, int* counters, int nsplit,
+               void* stream);
+long long ov3d_wgrad_workspace(int R, int N, int K, int nsplit);
+int ov3d_wgrad_tiles(int N, int K);
+
 #ifdef __cplusplus
 }
 #endif

@@ -47,8 +47,10 @@ _SIGS = {
     "ov3d_im2col3x3": "piiiiiiipp",
     "ov3d_attn_fwd": "pppllliiiiffpiplppip",
     "ov3d_attn_bwd": "ppplllplplpiiiiffpipplplplpip",
+    "ov3d_wgrad": "plpliiiplpppip",
 }
-EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace")
+EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
+                          "ov3d_wgrad_workspace", "ov3d_wgrad_tiles")
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_longlong, "f": ctypes.c_float,
        "d": ctypes.c_double}
@@ -75,6 +77,10 @@ def load():
         lib.ov3d_sa_layer_supported.restype = ctypes.c_int
         lib.ov3d_attn_fwd_workspace.argtypes = [ctypes.c_int] * 5
         lib.ov3d_attn_fwd_workspace.restype = ctypes.c_longlong
+        lib.ov3d_wgrad_workspace.argtypes = [ctypes.c_int] * 4
+        lib.ov3d_wgrad_workspace.restype = ctypes.c_longlong
+        lib.ov3d_wgrad_tiles.argtypes = [ctypes.c_int] * 2
+        lib.ov3d_wgrad_tiles.restype = ctypes.c_int
         lib.ov3d_version.argtypes = []
         lib.ov3d_version.restype = ctypes.c_char_p
         _lib = lib

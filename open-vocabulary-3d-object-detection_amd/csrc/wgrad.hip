@@ -1,0 +1,286 @@
+// Weight + bias gradient of a row-major linear layer (y = x W^T + b over R rows):
+//   dW (N, K) = dy^T x,   db (N) = sum_r dy[r, :]
+// for every dense layer of the 3DETR step (encoder / decoder projections and FFNs,
+// encoder->decoder projection, query projection, heads: models/transformer.py,
+// models/helpers.py GenericMLP), where R (points, memory tokens, query slots: 1024 ..
+// 16384) is long and N, K <= 768 are small.  Replaces a split-K batched GEMM + an fp32
+// sum over the splits + a separate bias reduction (three launches, gemm.py) by one
+// kernel:
+//   * split-K over row chunks (grid.z), 128 x 128 output tile per workgroup (grid.x, .y),
+//     4 waves of 64 x 64 (2 x 2 MFMA 32x32x16 tiles);
+//   * both operands are column reads of row-major tiles (dy^T and x): staged in LDS
+//     as loaded (coalesced 16-byte row segments) and read with ds_read_b64_tr_b16;
+//   * db rides on the same A fragments: one extra MFMA against a ones operand in the
+//     workgroups of output column tile 0;
+//   * split partials (fp32, a few MB, L2/MALL-resident) are summed in split order by a
+//     second, chip-wide launch (deterministic); R <= one chunk needs no second launch.
+#include "common.h"
+
+namespace {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int TN = 128, TK = 128;  // output tile (rows of dW = N, cols = K)
+constexpr int RS = 32;             // rows of dy / x per LDS stage
+constexpr int LDT = TN + 32;       // padded LDS row (bf16): conflict-free tr16 reads
+
+struct WgradArgs {
+    const bf16* dy;
+    const bf16* x;
+    long long ldy, ldx;
+    int R, N, K;
+    float* dW;        // (N, K), leading dimension ldw
+    long long ldw;
+    float* db;        // (N) or null
+    float* part;      // (nsplit, N, K) + (nsplit, N) split partials
+    int nsplit, rows_per_split;
+    int vec_dy, vec_x;  // 16-byte row segments are aligned (row strides % 8 == 0)
+};
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x4 tr16(const bf16* p) {
+    s16x4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+    return __builtin_bit_cast(bf16x4, r);
+}
+
+// operand fragment of a 32-column slice c0 of a [RS][LDT] tile for k-step ks (16 rows):
+// lane (col = c0 + (lane & 31), half h) gets rows 16ks + 8h + j, j = 0..7
+__device__ __forceinline__ bf16x8 col_frag(const bf16* T, int lane, int c0, int ks) {
+    const int g = lane >> 4, i = lane & 15;
+    const int col = c0 + 16 * (g & 1) + 4 * (i & 3);
+    const int row = 16 * ks + 8 * (g >> 1) + (i >> 2);
+    const bf16x4 lo = tr16(T + row * LDT + col);
+    const bf16x4 hi = tr16(T + (row + 4) * LDT + col);
+    bf16x8 a;
+    a[0] = lo[0]; a[1] = lo[1]; a[2] = lo[2]; a[3] = lo[3];
+    a[4] = hi[0]; a[5] = hi[1]; a[6] = hi[2]; a[7] = hi[3];
+    return a;
+}
+
+__global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradArgs a) {
+    __shared__ __attribute__((aligned(16))) bf16 Ds[2][RS * LDT];
+    __shared__ __attribute__((aligned(16))) bf16 Xs[2][RS * LDT];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wn = wave >> 1, wk = wave & 1;
+    const int n0 = blockIdx.x * TN, k0 = blockIdx.y * TK;
+    const int split = blockIdx.z;
+    const int rbeg = split * a.rows_per_split;
+    const int rend = min(a.R, rbeg + a.rows_per_split);
+    const bool do_bias = a.db != nullptr && blockIdx.y == 0 && wk == 0;
+
+    // stage loader: RS rows x 16 chunks (16 B) per operand = 512 chunks, 2 per thread
+    bf16x8 dr[2], xr[2];
+    auto load = [&](int r0) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int idx = tid + 256 * c, row = r0 + (idx >> 4), ch = idx & 15;
+            const int n = n0 + 8 * ch, k = k0 + 8 * ch;
+            bf16x8 zd, zx;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) zd[j] = zx[j] = (bf16)0.f;
+            if (row < rend) {
+                const bf16* pd = a.dy + (size_t)row * a.ldy + n;
+                const bf16* px = a.x + (size_t)row * a.ldx + k;
+                if (a.vec_dy && n + 8 <= a.N) zd = *reinterpret_cast<const bf16x8*>(pd);
+                else
+                    for (int j = 0; j < 8; ++j) zd[j] = n + j < a.N ? pd[j] : (bf16)0.f;
+                if (a.vec_x && k + 8 <= a.K) zx = *reinterpret_cast<const bf16x8*>(px);
+                else
+                    for (int j = 0; j < 8; ++j) zx[j] = k + j < a.K ? px[j] : (bf16)0.f;
+            }
+            dr[c] = zd;
+            xr[c] = zx;
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int idx = tid + 256 * c, row = idx >> 4, ch = idx & 15;
+            *reinterpret_cast<bf16x8*>(&Ds[buf][row * LDT + 8 * ch]) = dr[c];
+            *reinterpret_cast<bf16x8*>(&Xs[buf][row * LDT + 8 * ch]) = xr[c];
+        }
+    };
+
+    f32x16 acc[2][2], bacc[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        acc[0][0][i] = acc[0][1][i] = acc[1][0][i] = acc[1][1][i] = 0.f;
+        bacc[0][i] = bacc[1][i] = 0.f;
+    }
+    bf16x8 ones;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.f;
+
+    if (rbeg < rend) {
+        load(rbeg);
+        store(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int r0 = rbeg; r0 < rend; r0 += RS, buf ^= 1) {
+        const bool more = r0 + RS < rend;
+        if (more) load(r0 + RS);
+#pragma unroll
+        for (int ks = 0; ks < RS / 16; ++ks) {
+            bf16x8 af[2], bfr[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                af[t] = col_frag(Ds[buf], lane, 64 * wn + 32 * t, ks);
+                bfr[t] = col_frag(Xs[buf], lane, 64 * wk + 32 * t, ks);
+            }
+#pragma unroll
+            for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+                for (int tk = 0; tk < 2; ++tk) acc[tn][tk] = mfma(af[tn], bfr[tk], acc[tn][tk]);
+            if (do_bias) {
+                bacc[0] = mfma(af[0], ones, bacc[0]);
+                bacc[1] = mfma(af[1], ones, bacc[1]);
+            }
+        }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+    }
+
+    // accumulator element i of lane: row (n) = (i&3) + 8(i>>2) + 4h, col (k) = lane & 31
+    const int h = lane >> 5, cl = lane & 31;
+    const size_t NK = (size_t)a.N * a.K;
+    if (a.nsplit == 1) {
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+            for (int tk = 0; tk < 2; ++tk) {
+                const int k = k0 + 64 * wk + 32 * tk + cl;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int n = n0 + 64 * wn + 32 * tn + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    if (n < a.N && k < a.K) a.dW[(size_t)n * a.ldw + k] = acc[tn][tk][i];
+                }
+            }
+        if (do_bias && cl == 0) {
+#pragma unroll
+            for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int n = n0 + 64 * wn + 32 * tn + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    if (n < a.N) a.db[n] = bacc[tn][i];
+                }
+        }
+        return;
+    }
+    // split partials
+    float* pw = a.part + (size_t)split * NK;
+    float* pb = a.part + (size_t)a.nsplit * NK + (size_t)split * a.N;
+#pragma unroll
+    for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+        for (int tk = 0; tk < 2; ++tk) {
+            const int k = k0 + 64 * wk + 32 * tk + cl;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int n = n0 + 64 * wn + 32 * tn + (i & 3) + 8 * (i >> 2) + 4 * h;
+                if (n < a.N && k < a.K) pw[(size_t)n * a.K + k] = acc[tn][tk][i];
+            }
+        }
+    if (do_bias && cl == 0) {
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int n = n0 + 64 * wn + 32 * tn + (i & 3) + 8 * (i >> 2) + 4 * h;
+                if (n < a.N) pb[n] = bacc[tn][i];
+            }
+    }
+}
+
+// dW / db = sum of the split partials in split order (deterministic); one thread per 4
+// outputs, the nsplit loads of a thread issued together
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(WgradArgs a) {
+    const size_t NK = (size_t)a.N * a.K;
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long nk4 = (long long)a.N * ((a.K + 3) / 4);
+    if (t < nk4) {
+        const int n = (int)(t / ((a.K + 3) / 4)), k = 4 * (int)(t % ((a.K + 3) / 4));
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        const float* p = a.part + (size_t)n * a.K + k;
+        const int kk = min(4, a.K - k);
+        int sp = 0;
+        for (; sp + 4 <= a.nsplit; sp += 4) {
+            float v[4][4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[u][j] = j < kk ? p[(size_t)(sp + u) * NK + j] : 0.f;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] += v[u][j];
+        }
+        for (; sp < a.nsplit; ++sp)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[j] += j < kk ? p[(size_t)sp * NK + j] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (j < kk) a.dW[(size_t)n * a.ldw + k + j] = acc[j];
+    } else if (a.db != nullptr && t < nk4 + a.N) {
+        const int n = (int)(t - nk4);
+        const float* p = a.part + (size_t)a.nsplit * NK + n;
+        float acc = 0.f;
+        for (int sp = 0; sp < a.nsplit; ++sp) acc += p[(size_t)sp * a.N];
+        a.db[n] = acc;
+    }
+}
+
+}  // namespace
+
+extern "C" long long ov3d_wgrad_workspace(int R, int N, int K, int nsplit) {
+    if (nsplit <= 1) return 0;
+    return (long long)nsplit * ((long long)N * K + N);
+}
+
+extern "C" int ov3d_wgrad_tiles(int N, int K) { return ((N + TN - 1) / TN) * ((K + TK - 1) / TK); }
+
+extern "C" int ov3d_wgrad(const void* dy, long long ldy, const void* x, long long ldx, int R, int N,
+                          int K, float* dW, long long ldw, float* db, float* workspace,
+                          int* counters, int nsplit, void* stream) {
+    if (!dy || !x || !dW || R <= 0 || N <= 0 || K <= 0 || ldy < N || ldx < K || ldw < K ||
+        nsplit <= 0)
+        return OV3D_EINVAL;
+    int rps = (R + nsplit - 1) / nsplit;
+    rps = (rps + RS - 1) / RS * RS;
+    nsplit = (R + rps - 1) / rps;
+    if (nsplit > 1 && !workspace) return OV3D_EINVAL;
+    WgradArgs a;
+    a.dy = (const bf16*)dy;
+    a.x = (const bf16*)x;
+    a.ldy = ldy;
+    a.ldx = ldx;
+    a.R = R;
+    a.N = N;
+    a.K = K;
+    a.dW = dW;
+    a.ldw = ldw;
+    a.db = db;
+    a.part = workspace;
+    (void)counters;
+    a.nsplit = nsplit;
+    a.rows_per_split = rps;
+    a.vec_dy = (ldy % 8 == 0) && ((uintptr_t)dy % 16 == 0);
+    a.vec_x = (ldx % 8 == 0) && ((uintptr_t)x % 16 == 0);
+    dim3 grid((N + TN - 1) / TN, (K + TK - 1) / TK, nsplit);
+    hipStream_t st = ov3d_stream(stream);
+    wgrad_kernel<<<grid, 256, 0, st>>>(a);
+    OV3D_LAUNCH_CHECK();
+    if (nsplit > 1) {
+        const long long threads = (long long)N * ((K + 3) / 4) + (db ? N : 0);
+        wgrad_reduce_kernel<<<ov3d_cdiv(threads, 256), 256, 0, st>>>(a);
+        OV3D_LAUNCH_CHECK();
+    }
+    return OV3D_OK;
+}

@@ -41,6 +41,54 @@ def _bmm_f32(a, b):
     return torch.bmm(a, b)
 
 
+_WG_COUNTERS = {}
+
+
+def _wg_counters(device):
+    c = _WG_COUNTERS.get(device)
+    if c is None:   # arrival counters of csrc/wgrad.hip: zero, and left zero by every launch
+        c = torch.zeros(4096, dtype=torch.int32, device=device)
+        _WG_COUNTERS[device] = c
+    return c
+
+
+def _wg_splits(R, N, K):
+    from . import _native
+    tiles = _native.load().ov3d_wgrad_tiles(N, K)
+    return max(1, min((R + 255) // 256, 512 // tiles))
+
+
+def _fused_ok(dy, x):
+    """the one-launch HIP weight/bias gradient applies to bf16 rows on the ROCm device"""
+    return (dy.is_cuda and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16
+            and dy.dim() == 2 and x.dim() == 2 and dy.stride(1) == 1 and x.stride(1) == 1)
+
+
+def fused_weight_grad(dy, x, bias=True, out_w=None, out_b=None):
+    """dW = dy^T x (fp32, (N, K)) and db = column sums of dy (fp32, (N,)) in ONE HIP launch
+    (csrc/wgrad.hip, ov3d_wgrad); dy (R, N), x (R, K) bf16 rows (row strides taken from the
+    tensors).  out_w / out_b: optional fp32 destinations (row slices of a larger gradient)."""
+    from . import _native
+    R, N = dy.shape
+    K = x.shape[1]
+    if dy.stride(1) != 1 or x.stride(1) != 1:
+        raise ValueError("fused_weight_grad: rows must be contiguous")
+    dev = dy.device
+    dw = out_w if out_w is not None else torch.empty((N, K), dtype=torch.float32, device=dev)
+    db = None
+    if bias:
+        db = out_b if out_b is not None else torch.empty((N,), dtype=torch.float32, device=dev)
+    nsplit = _wg_splits(R, N, K)
+    lib = _native.load()
+    if lib.ov3d_wgrad_tiles(N, K) > 4096:
+        raise ValueError("fused_weight_grad: too many output tiles")
+    ws_n = lib.ov3d_wgrad_workspace(R, N, K, nsplit)
+    ws = torch.empty((max(ws_n, 1),), dtype=torch.float32, device=dev)
+    _native.call("ov3d_wgrad", dy, dy.stride(0), x, x.stride(0), R, N, K, dw, dw.stride(0), db, ws,
+                 _wg_counters(dev), nsplit, like=dy)
+    return dw, db
+
+
 def weight_grad(dy, x, out=None):
     """dy (R, Cout), x (R, Cin) -> dy^T x (Cout, Cin) in fp32, split-K over R
     (written into `out`, a contiguous fp32 (Cout, Cin) tensor, when given)."""
@@ -116,9 +164,14 @@ class _RowsLinear(Function):
         dy = dy.to(xc.dtype).contiguous()
         with torch.autocast("cuda", enabled=False):
             dx = (dy @ wc).to(xdt) if ctx.needs_input_grad[0] else None
-            dw = weight_grad(dy, xc).to(wdt) if ctx.needs_input_grad[1] else None
-            db = torch.sum(dy, dim=0, dtype=torch.float32).to(wdt) \
-                if has_b and ctx.needs_input_grad[2] else None
+            want_b = has_b and ctx.needs_input_grad[2]
+            if ctx.needs_input_grad[1] and _fused_ok(dy, xc):
+                dw, db = fused_weight_grad(dy, xc, bias=want_b)
+                dw = dw.to(wdt)
+                db = db.to(wdt) if want_b else None
+            else:
+                dw = weight_grad(dy, xc).to(wdt) if ctx.needs_input_grad[1] else None
+                db = torch.sum(dy, dim=0, dtype=torch.float32).to(wdt) if want_b else None
         return dx, dw, db
 
 
@@ -170,6 +223,10 @@ class _InProj(Function):
                 dy = dy.reshape(-1, r1 - r0).to(xc.dtype).contiguous()
                 dxs.append((dy @ wc[r0:r1]).to(xdts[i]).view(xshapes[i])
                            if ctx.needs_input_grad[3 + i] else None)
+                if dw is not None and _fused_ok(dy, xc):
+                    fused_weight_grad(dy, xc, bias=db is not None, out_w=dw[r0:r1],
+                                      out_b=db[r0:r1] if db is not None else None)
+                    continue
                 if dw is not None:
                     weight_grad(dy, xc, out=dw[r0:r1])
                 if db is not None:
