@@ -10,8 +10,7 @@
 //     4 waves of 64 x 64 (2 x 2 MFMA 32x32x16 tiles);
 //   * both operands are column reads of row-major tiles (dy^T and x): staged in LDS
 //     as loaded (coalesced 16-byte row segments) and read with ds_read_b64_tr_b16;
-//   * db rides on the same A fragments: one extra MFMA against a ones operand in the
-//     workgroups of output column tile 0;
+//   * db: the workgroups of output column tile 0 also sum the staged dy rows on the VALU;
 //   * split partials (fp32, a few MB, L2/MALL-resident) are summed in split order by a
 //     second, chip-wide launch (deterministic); R <= one chunk needs no second launch.
 #include "common.h"
@@ -73,7 +72,9 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradArgs a) {
     const int split = blockIdx.z;
     const int rbeg = split * a.rows_per_split;
     const int rend = min(a.R, rbeg + a.rows_per_split);
-    const bool do_bias = a.db != nullptr && blockIdx.y == 0 && wk == 0;
+    // db: the workgroups of output column tile 0 also sum their dy stage tile over its
+    // rows on the VALU (thread: 8 adjacent columns x 2 rows per stage)
+    const bool do_bias = a.db != nullptr && blockIdx.y == 0;
 
     // stage loader: RS rows x 16 chunks (16 B) per operand = 512 chunks, 2 per thread
     bf16x8 dr[2], xr[2];
@@ -108,15 +109,12 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradArgs a) {
         }
     };
 
-    f32x16 acc[2][2], bacc[2];
+    f32x16 acc[2][2];
+    float bsum[8];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        acc[0][0][i] = acc[0][1][i] = acc[1][0][i] = acc[1][1][i] = 0.f;
-        bacc[0][i] = bacc[1][i] = 0.f;
-    }
-    bf16x8 ones;
+    for (int i = 0; i < 16; ++i) acc[0][0][i] = acc[0][1][i] = acc[1][0][i] = acc[1][1][i] = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.f;
+    for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
 
     if (rbeg < rend) {
         load(rbeg);
@@ -139,15 +137,32 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradArgs a) {
             for (int tn = 0; tn < 2; ++tn)
 #pragma unroll
                 for (int tk = 0; tk < 2; ++tk) acc[tn][tk] = mfma(af[tn], bfr[tk], acc[tn][tk]);
-            if (do_bias) {
-                bacc[0] = mfma(af[0], ones, bacc[0]);
-                bacc[1] = mfma(af[1], ones, bacc[1]);
+        }
+        if (do_bias) {
+#pragma unroll
+            for (int rr = 0; rr < RS / 16; ++rr) {
+                const bf16x8 v = *reinterpret_cast<const bf16x8*>(
+                    &Ds[buf][((tid >> 4) + 16 * rr) * LDT + 8 * (tid & 15)]);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) bsum[j] += (float)v[j];
             }
         }
         if (more) store(buf ^ 1);
         __syncthreads();
     }
 
+    // column sums of this split: 16 row-threads per 8-column group -> LDS -> 128 values
+    float* bred = reinterpret_cast<float*>(&Xs[0][0]);   // 256 x 8 floats, free after the loop
+    if (do_bias) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bred[tid * 8 + j] = bsum[j];
+    }
+    __syncthreads();
+    float bcol = 0.f;   // thread t < 128: column n0 + t
+    if (do_bias && tid < TN) {
+        const int cg = tid >> 3, j = tid & 7;
+        for (int rt = 0; rt < 16; ++rt) bcol += bred[(rt * 16 + cg) * 8 + j];
+    }
     // accumulator element i of lane: row (n) = (i&3) + 8(i>>2) + 4h, col (k) = lane & 31
     const int h = lane >> 5, cl = lane & 31;
     const size_t NK = (size_t)a.N * a.K;
@@ -163,15 +178,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradArgs a) {
                     if (n < a.N && k < a.K) a.dW[(size_t)n * a.ldw + k] = acc[tn][tk][i];
                 }
             }
-        if (do_bias && cl == 0) {
-#pragma unroll
-            for (int tn = 0; tn < 2; ++tn)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int n = n0 + 64 * wn + 32 * tn + (i & 3) + 8 * (i >> 2) + 4 * h;
-                    if (n < a.N) a.db[n] = bacc[tn][i];
-                }
-        }
+        if (do_bias && tid < TN && n0 + tid < a.N) a.db[n0 + tid] = bcol;
         return;
     }
     // split partials
@@ -188,15 +195,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradArgs a) {
                 if (n < a.N && k < a.K) pw[(size_t)n * a.K + k] = acc[tn][tk][i];
             }
         }
-    if (do_bias && cl == 0) {
-#pragma unroll
-        for (int tn = 0; tn < 2; ++tn)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int n = n0 + 64 * wn + 32 * tn + (i & 3) + 8 * (i >> 2) + 4 * h;
-                if (n < a.N) pb[n] = bacc[tn][i];
-            }
-    }
+    if (do_bias && tid < TN && n0 + tid < a.N) pb[n0 + tid] = bcol;
 }
 
 // dW / db = sum of the split partials in split order (deterministic); one thread per 4
