@@ -76,9 +76,11 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradArgs a) {
     // rows on the VALU (thread: 8 adjacent columns x 2 rows per stage)
     const bool do_bias = a.db != nullptr && blockIdx.y == 0;
 
-    // stage loader: RS rows x 16 chunks (16 B) per operand = 512 chunks, 2 per thread
-    bf16x8 dr[2], xr[2];
-    auto load = [&](int r0) {
+    // stage loader: RS rows x 16 chunks (16 B) per operand = 512 chunks, 2 per thread.
+    // Two register sets: stage n+2 is in flight while stage n is computed and stage n+1
+    // waits in the other set (a stage is only 4-6 MFMAs per wave, too short to cover a
+    // global load).
+    auto load = [&](bf16x8 (&dr)[2], bf16x8 (&xr)[2], int r0) {
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             const int idx = tid + 256 * c, row = r0 + (idx >> 4), ch = idx & 15;
@@ -100,7 +102,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradArgs a) {
             xr[c] = zx;
         }
     };
-    auto store = [&](int buf) {
+    auto store = [&](const bf16x8 (&dr)[2], const bf16x8 (&xr)[2], int buf) {
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             const int idx = tid + 256 * c, row = idx >> 4, ch = idx & 15;
@@ -116,15 +118,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) bsum[j] = 0.f;
 
-    if (rbeg < rend) {
-        load(rbeg);
-        store(0);
-    }
-    __syncthreads();
-    int buf = 0;
-    for (int r0 = rbeg; r0 < rend; r0 += RS, buf ^= 1) {
-        const bool more = r0 + RS < rend;
-        if (more) load(r0 + RS);
+    auto compute = [&](int buf) {
 #pragma unroll
         for (int ks = 0; ks < RS / 16; ++ks) {
             bf16x8 af[2], bfr[2];
@@ -147,8 +141,29 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradArgs a) {
                 for (int j = 0; j < 8; ++j) bsum[j] += (float)v[j];
             }
         }
-        if (more) store(buf ^ 1);
+    };
+
+    bf16x8 dA[2], xA[2], dB[2], xB[2];
+    if (rbeg < rend) {
+        load(dA, xA, rbeg);
+        store(dA, xA, 0);
+        if (rbeg + RS < rend) load(dA, xA, rbeg + RS);
+    }
+    __syncthreads();
+    for (int r = rbeg; r < rend;) {
+        // LDS buffer 0 holds stage r, set A holds stage r + RS
+        if (r + 2 * RS < rend) load(dB, xB, r + 2 * RS);
+        compute(0);
+        if (r + RS < rend) store(dA, xA, 1);
         __syncthreads();
+        r += RS;
+        if (r >= rend) break;
+        // LDS buffer 1 holds stage r, set B holds stage r + RS
+        if (r + 2 * RS < rend) load(dA, xA, r + 2 * RS);
+        compute(1);
+        if (r + RS < rend) store(dB, xB, 0);
+        __syncthreads();
+        r += RS;
     }
 
     // column sums of this split: 16 row-threads per 8-column group -> LDS -> 128 values
