@@ -213,41 +213,37 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradArgs a) {
     if (do_bias && tid < TN && n0 + tid < a.N) pb[n0 + tid] = bcol;
 }
 
-// dW / db = sum of the split partials in split order (deterministic); one thread per 4
-// outputs, the nsplit loads of a thread issued together
+// dW / db = sum of the split partials in split order (deterministic).  One thread per
+// output element (coalesced across threads), 8 split loads in flight per thread.
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(WgradArgs a) {
     const size_t NK = (size_t)a.N * a.K;
     const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long long nk4 = (long long)a.N * ((a.K + 3) / 4);
-    if (t < nk4) {
-        const int n = (int)(t / ((a.K + 3) / 4)), k = 4 * (int)(t % ((a.K + 3) / 4));
-        float acc[4] = {0.f, 0.f, 0.f, 0.f};
-        const float* p = a.part + (size_t)n * a.K + k;
-        const int kk = min(4, a.K - k);
-        int sp = 0;
-        for (; sp + 4 <= a.nsplit; sp += 4) {
-            float v[4][4];
+    const float* p;
+    size_t stride;
+    if (t < (long long)NK) {
+        p = a.part + t;
+        stride = NK;
+    } else if (a.db != nullptr && t < (long long)NK + a.N) {
+        p = a.part + (size_t)a.nsplit * NK + (t - NK);
+        stride = a.N;
+    } else {
+        return;
+    }
+    float acc = 0.f;
+    int sp = 0;
+    for (; sp + 8 <= a.nsplit; sp += 8) {
+        float v[8];
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < 8; ++u) v[u] = p[(size_t)(sp + u) * stride];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) v[u][j] = j < kk ? p[(size_t)(sp + u) * NK + j] : 0.f;
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[j] += v[u][j];
-        }
-        for (; sp < a.nsplit; ++sp)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[j] += j < kk ? p[(size_t)sp * NK + j] : 0.f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if (j < kk) a.dW[(size_t)n * a.ldw + k + j] = acc[j];
-    } else if (a.db != nullptr && t < nk4 + a.N) {
-        const int n = (int)(t - nk4);
-        const float* p = a.part + (size_t)a.nsplit * NK + n;
-        float acc = 0.f;
-        for (int sp = 0; sp < a.nsplit; ++sp) acc += p[(size_t)sp * a.N];
-        a.db[n] = acc;
+        for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; sp < a.nsplit; ++sp) acc += p[(size_t)sp * stride];
+    if (t < (long long)NK) {
+        const int n = (int)(t / a.K), k = (int)(t - (long long)n * a.K);
+        a.dW[(size_t)n * a.ldw + k] = acc;
+    } else {
+        a.db[t - NK] = acc;
     }
 }
 
@@ -292,7 +288,7 @@ extern "C" int ov3d_wgrad(const void* dy, long long ldy, const void* x, long lon
     wgrad_kernel<<<grid, 256, 0, st>>>(a);
     OV3D_LAUNCH_CHECK();
     if (nsplit > 1) {
-        const long long threads = (long long)N * ((K + 3) / 4) + (db ? N : 0);
+        const long long threads = (long long)N * K + (db ? N : 0);
         wgrad_reduce_kernel<<<ov3d_cdiv(threads, 256), 256, 0, st>>>(a);
         OV3D_LAUNCH_CHECK();
     }

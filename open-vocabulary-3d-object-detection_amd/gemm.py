@@ -55,7 +55,8 @@ def _wg_counters(device):
 def _wg_splits(R, N, K):
     from . import _native
     tiles = _native.load().ov3d_wgrad_tiles(N, K)
-    return max(1, min((R + 255) // 256, 512 // tiles))
+    rows = 256 if R <= 4096 else 512   # short R: parallelism; long R: fewer partials to sum
+    return max(1, min((R + rows - 1) // rows, 512 // tiles))
 
 
 def _fused_ok(dy, x):
