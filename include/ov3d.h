@@ -263,6 +263,32 @@ int ov3d_wgrad(const void* dy, long long ldy, const void* x, long long ldx, int 
 long long ov3d_wgrad_workspace(int R, int N, int K, int nsplit);
 int ov3d_wgrad_tiles(int N, int K);
 
+/* ---- Training BatchNorm1d + ReLU + Dropout over channels-last rows ----
+ * The GenericMLP prediction heads (models/helpers.py:45-112, built by
+ * models/model_3detr.py _build_heads) evaluated as one MLP over 5*256 channels.
+ * Every operand's channel c of row r lives at base + (c/cb)*bstride + r*ld + (c%cb)
+ * (row-major: cb = C, bstride = 0; per-head blocks of a batched GEMM: cb = 256,
+ * ld = 256, bstride = R*256).  C % 8 == 0.  Dropout: hash of (*seed, site, r, c).
+ * stats: partials (nparts, 2, C) f64 of sum x, sum x^2 (then ov3d_reduce_partials,
+ *        ov3d_bn_finalize) */
+int ov3d_rows_bn_stats(const void* x, int is_bf16, long long ld, long long bstride, int cb,
+                       long long R, int C, double* partials, int nparts, void* stream);
+/* apply: out (bf16) = dropout(relu(x*scale + shift)) */
+int ov3d_rows_bn_apply(const void* x, int is_bf16, long long ld, long long bstride, int cb,
+                       long long R, int C, const float* scale, const float* shift,
+                       float dropout_p, const int64_t* seed, int site, void* out, long long ldo,
+                       long long bstride_o, int cbo, void* stream);
+/* backward, dt = dz * keep/(1-p) * [x*scale+shift > 0]:
+ * pass 0: partials (nparts, 2, C) of sum dt, sum dt*(x-mean)*invstd (then
+ *         ov3d_reduce_partials, ov3d_bn_bwd_finalize -> cA, cB, cC, dgamma, dbeta);
+ * pass 1: dx (bf16) = cA*dt + cB*x + cC */
+int ov3d_rows_bn_bwd(int pass, const void* dz, long long ldz, long long bstride_z, int cbz,
+                     const void* x, int x_bf16, long long ldx, long long bstride_x, int cbx,
+                     long long R, int C, const float* scale, const float* shift, const float* mean,
+                     const float* invstd, const float* cA, const float* cB, const float* cC,
+                     float dropout_p, const int64_t* seed, int site, double* partials, int nparts,
+                     void* dx, long long ldd, long long bstride_d, int cbd, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -48,6 +48,9 @@ _SIGS = {
     "ov3d_attn_fwd": "pppllliiiiffpiplppip",
     "ov3d_attn_bwd": "ppplllplplpiiiiffpipplplplpip",
     "ov3d_wgrad": "plpliiiplpppip",
+    "ov3d_rows_bn_stats": "pillilipip",
+    "ov3d_rows_bn_apply": "pillilippfpipllip",
+    "ov3d_rows_bn_bwd": "ipllipillilipppppppfpipipllip",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
                           "ov3d_wgrad_workspace", "ov3d_wgrad_tiles")

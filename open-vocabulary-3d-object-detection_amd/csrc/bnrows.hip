@@ -1,0 +1,320 @@
+// Training BatchNorm1d + ReLU + Dropout over channels-last rows, for the GenericMLP
+// prediction heads of 3DETR (models/helpers.py:45-112 as built by
+// models/model_3detr.py:_build_heads: Conv1d -> BatchNorm1d -> ReLU -> Dropout(0.3), x2)
+// with the five heads evaluated side by side as one (R, 5*256) channel set.
+//
+// Tensor addressing (every operand): channel c of row r lives at
+//   base + (c / cb) * bstride + r * ld + (c % cb)
+// so one kernel reads a row-major (R, C) tensor (cb = C, bstride = 0) or the per-head
+// blocks of a batched GEMM output (cb = 256, ld = 256, bstride = R*256).  A thread owns
+// 8 adjacent channels (one 16-byte bf16 run) of a row.
+//
+//   ov3d_rows_bn_stats  : fp64 partials (nparts, 2, C) of sum x and sum x^2
+//   (ov3d_reduce_partials + ov3d_bn_finalize of sa_mlp.hip turn them into scale/shift)
+//   ov3d_rows_bn_apply  : z = dropout(relu(x*scale + shift)) -> bf16
+//   ov3d_rows_bn_bwd    : dt = dz * keep/(1-p) * [x*scale+shift > 0];
+//                         pass 0: partials of sum dt and sum dt*xhat; pass 1: dx = cA dt + cB x + cC
+// Dropout keep(r, c) is a counter-based hash of (seed, site, r, c): the backward
+// regenerates the mask instead of storing it.
+#include "common.h"
+
+namespace {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+struct RowsLayout {
+    long long ld, bstride;
+    int cb;
+};
+
+__device__ __forceinline__ long long addr(const RowsLayout& L, long long r, int c) {
+    return (long long)(c / L.cb) * L.bstride + r * L.ld + (c % L.cb);
+}
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+__device__ __forceinline__ uint32_t mix24(uint32_t x) {
+    x ^= x >> 16;
+    x = __umul24(x, 0x7feb35u) ^ (x >> 24);
+    x ^= x >> 15;
+    x = __umul24(x, 0x846ca7u) ^ (x >> 24);
+    x ^= x >> 16;
+    return x;
+}
+__device__ __forceinline__ uint32_t row_base(uint32_t seedmix, long long r) {
+    return mix32(seedmix ^ ((uint32_t)r * 0xC2B2AE35u));
+}
+// keep decisions of channels c..c+7 of row r: 4 hashes, two 16-bit halves each
+__device__ __forceinline__ void keep8(uint32_t rowbase, int c, uint32_t thresh, bool* keep) {
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+        const uint32_t h = mix24(rowbase + (uint32_t)((c + j) >> 1) * 0x27D4EB2Fu);
+        keep[j] = (h & 0xffffu) >= thresh;
+        keep[j + 1] = (h >> 16) >= thresh;
+    }
+}
+
+// rows-per-thread phase layout: TP threads per row (one per 8-channel run), RP rows at once
+struct Phase {
+    int tp, rp, ph, c;
+    bool active;
+};
+__device__ __forceinline__ Phase phase(int C) {
+    Phase p;
+    const int runs = C / 8;
+    p.tp = runs < 256 ? runs : 256;
+    p.rp = 256 / p.tp;
+    p.ph = threadIdx.x / p.tp;
+    p.c = (threadIdx.x % p.tp) * 8;
+    p.active = p.ph < p.rp;
+    return p;
+}
+
+template <typename T>
+__device__ __forceinline__ void load8(const T* base, const RowsLayout& L, long long r, int c, float* v);
+template <>
+__device__ __forceinline__ void load8<bf16>(const bf16* base, const RowsLayout& L, long long r, int c,
+                                            float* v) {
+    const bf16x8 x = *reinterpret_cast<const bf16x8*>(base + addr(L, r, c));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)x[j];
+}
+template <>
+__device__ __forceinline__ void load8<float>(const float* base, const RowsLayout& L, long long r,
+                                             int c, float* v) {
+    const float4 a = *reinterpret_cast<const float4*>(base + addr(L, r, c));
+    const float4 b = *reinterpret_cast<const float4*>(base + addr(L, r, c) + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// reduce the two per-thread accumulators over the RP row phases of the block and write
+// the block's fp64 partials (sum over its rows) for channels cbase .. cbase + 8*TP
+__device__ void block_partials(const Phase& p, int C, int cbase, float (*acc)[8],
+                               double* partials) {
+    __shared__ float red[2][2048];
+    const int W = p.tp * 8;
+    __syncthreads();
+    if (p.active)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            red[0][p.ph * W + p.c + j] = acc[0][j];
+            red[1][p.ph * W + p.c + j] = acc[1][j];
+        }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * W; i += blockDim.x) {
+        const int v = i / W, cc = i - v * W;
+        if (cbase + cc < C) {
+            double t = 0.0;
+            for (int k = 0; k < p.rp; ++k) t += (double)red[v][k * W + cc];
+            partials[((size_t)blockIdx.x * 2 + v) * C + cbase + cc] = t;
+        }
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) rows_bn_stats_kernel(const T* __restrict__ x, RowsLayout L,
+                                                            long long R, int C,
+                                                            double* __restrict__ partials) {
+    const Phase p = phase(C);
+    for (int cbase = 0; cbase < C; cbase += p.tp * 8) {
+        const int c = cbase + p.c;
+        float acc[2][8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[0][j] = acc[1][j] = 0.f;
+        if (p.active && c < C)
+            for (long long r = (long long)blockIdx.x * p.rp + p.ph; r < R; r += (long long)gridDim.x * p.rp) {
+                float v[8];
+                load8<T>(x, L, r, c, v);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    acc[0][j] += v[j];
+                    acc[1][j] = fmaf(v[j], v[j], acc[1][j]);
+                }
+            }
+        block_partials(p, C, cbase, acc, partials);
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) rows_bn_apply_kernel(
+    const T* __restrict__ x, RowsLayout L, long long R, int C, const float* __restrict__ scale,
+    const float* __restrict__ shift, uint32_t thresh, float keep_scale, const int64_t* seed,
+    uint32_t site, bf16* __restrict__ out, RowsLayout LO) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int runs = C / 8;
+    if (t >= R * runs) return;
+    const long long r = t / runs;
+    const int c = (int)(t - r * runs) * 8;
+    float v[8];
+    load8<T>(x, L, r, c, v);
+    bool keep[8];
+    if (thresh) {
+        const uint64_t s = (uint64_t)*seed;
+        const uint32_t sm = mix32((uint32_t)s ^ mix32((uint32_t)(s >> 32) + site * 0x9E3779B9u));
+        keep8(row_base(sm, r), c, thresh, keep);
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        float z = fmaxf(fmaf(v[j], scale[c + j], shift[c + j]), 0.f);
+        if (thresh) z = keep[j] ? z * keep_scale : 0.f;
+        o[j] = (bf16)z;
+    }
+    *reinterpret_cast<bf16x8*>(out + addr(LO, r, c)) = o;
+}
+
+template <int PASS, typename T>
+__global__ void __launch_bounds__(256) rows_bn_bwd_kernel(
+    const bf16* __restrict__ dz, RowsLayout LZ, const T* __restrict__ x, RowsLayout LX, long long R,
+    int C, const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ cA,
+    const float* __restrict__ cB, const float* __restrict__ cC, uint32_t thresh, float keep_scale,
+    const int64_t* seed, uint32_t site, double* __restrict__ partials, bf16* __restrict__ dx,
+    RowsLayout LD) {
+    uint32_t sm = 0;
+    if (thresh) {
+        const uint64_t s = (uint64_t)*seed;
+        sm = mix32((uint32_t)s ^ mix32((uint32_t)(s >> 32) + site * 0x9E3779B9u));
+    }
+    if (PASS == 1) {
+        const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+        const int runs = C / 8;
+        if (t >= R * runs) return;
+        const long long r = t / runs;
+        const int c = (int)(t - r * runs) * 8;
+        float xv[8], zv[8];
+        load8<T>(x, LX, r, c, xv);
+        load8<bf16>(dz, LZ, r, c, zv);
+        bool keep[8];
+        if (thresh) keep8(row_base(sm, r), c, thresh, keep);
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float dt = fmaf(xv[j], scale[c + j], shift[c + j]) > 0.f ? zv[j] : 0.f;
+            if (thresh) dt = keep[j] ? dt * keep_scale : 0.f;
+            o[j] = (bf16)fmaf(cA[c + j], dt, fmaf(cB[c + j], xv[j], cC[c + j]));
+        }
+        *reinterpret_cast<bf16x8*>(dx + addr(LD, r, c)) = o;
+        return;
+    }
+    const Phase p = phase(C);
+    for (int cbase = 0; cbase < C; cbase += p.tp * 8) {
+        const int c = cbase + p.c;
+        float acc[2][8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[0][j] = acc[1][j] = 0.f;
+        if (p.active && c < C)
+            for (long long r = (long long)blockIdx.x * p.rp + p.ph; r < R; r += (long long)gridDim.x * p.rp) {
+                float xv[8], zv[8];
+                load8<T>(x, LX, r, c, xv);
+                load8<bf16>(dz, LZ, r, c, zv);
+                bool keep[8];
+                if (thresh) keep8(row_base(sm, r), c, thresh, keep);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    float dt = fmaf(xv[j], scale[c + j], shift[c + j]) > 0.f ? zv[j] : 0.f;
+                    if (thresh) dt = keep[j] ? dt * keep_scale : 0.f;
+                    acc[0][j] += dt;
+                    acc[1][j] = fmaf(dt, (xv[j] - mean[c + j]) * invstd[c + j], acc[1][j]);
+                }
+            }
+        block_partials(p, C, cbase, acc, partials);
+    }
+}
+
+uint32_t drop_thresh(float p) {
+    return p > 0.f ? (uint32_t)fminf(rintf(p * 65536.0f), 65535.0f) : 0u;
+}
+
+bool layout_ok(const RowsLayout& L, int C) {
+    return L.cb > 0 && L.cb % 8 == 0 && C % L.cb == 0 && L.ld >= L.cb && L.ld % 8 == 0 &&
+           L.bstride % 8 == 0;
+}
+
+}  // namespace
+
+extern "C" int ov3d_rows_bn_stats(const void* x, int is_bf16, long long ld, long long bstride,
+                                  int cb, long long R, int C, double* partials, int nparts,
+                                  void* stream) {
+    RowsLayout L{ld, bstride, cb};
+    if (!x || !partials || R <= 0 || C <= 0 || C % 8 || nparts <= 0 || !layout_ok(L, C))
+        return OV3D_EINVAL;
+    hipStream_t s = ov3d_stream(stream);
+    if (is_bf16)
+        rows_bn_stats_kernel<bf16><<<nparts, 256, 0, s>>>((const bf16*)x, L, R, C, partials);
+    else
+        rows_bn_stats_kernel<float><<<nparts, 256, 0, s>>>((const float*)x, L, R, C, partials);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_rows_bn_apply(const void* x, int is_bf16, long long ld, long long bstride, int cb,
+                                  long long R, int C, const float* scale, const float* shift,
+                                  float dropout_p, const int64_t* seed, int site, void* out,
+                                  long long ldo, long long bstride_o, int cbo, void* stream) {
+    RowsLayout L{ld, bstride, cb}, LO{ldo, bstride_o, cbo};
+    if (!x || !scale || !shift || !out || R <= 0 || C <= 0 || C % 8 || !layout_ok(L, C) ||
+        !layout_ok(LO, C) || dropout_p < 0.f || dropout_p >= 1.f || (dropout_p > 0.f && !seed))
+        return OV3D_EINVAL;
+    const long long n = R * (C / 8);
+    hipStream_t s = ov3d_stream(stream);
+    const uint32_t th = drop_thresh(dropout_p);
+    const float ks = 1.f / (1.f - dropout_p);
+    if (is_bf16)
+        rows_bn_apply_kernel<bf16><<<ov3d_cdiv(n, 256), 256, 0, s>>>(
+            (const bf16*)x, L, R, C, scale, shift, th, ks, seed, (uint32_t)site, (bf16*)out, LO);
+    else
+        rows_bn_apply_kernel<float><<<ov3d_cdiv(n, 256), 256, 0, s>>>(
+            (const float*)x, L, R, C, scale, shift, th, ks, seed, (uint32_t)site, (bf16*)out, LO);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_rows_bn_bwd(int pass, const void* dz, long long ldz, long long bstride_z, int cbz,
+                                const void* x, int x_bf16, long long ldx, long long bstride_x,
+                                int cbx, long long R, int C, const float* scale, const float* shift,
+                                const float* mean, const float* invstd, const float* cA,
+                                const float* cB, const float* cC, float dropout_p,
+                                const int64_t* seed, int site, double* partials, int nparts,
+                                void* dx, long long ldd, long long bstride_d, int cbd,
+                                void* stream) {
+    RowsLayout LZ{ldz, bstride_z, cbz}, LX{ldx, bstride_x, cbx}, LD{ldd, bstride_d, cbd};
+    if (!dz || !x || R <= 0 || C <= 0 || C % 8 || !layout_ok(LZ, C) || !layout_ok(LX, C) ||
+        dropout_p < 0.f || dropout_p >= 1.f || (dropout_p > 0.f && !seed) || (pass != 0 && pass != 1))
+        return OV3D_EINVAL;
+    if (pass == 0 && (!partials || nparts <= 0 || !mean || !invstd)) return OV3D_EINVAL;
+    if (pass == 1 && (!dx || !cA || !cB || !cC || !layout_ok(LD, C))) return OV3D_EINVAL;
+    hipStream_t s = ov3d_stream(stream);
+    const uint32_t th = drop_thresh(dropout_p);
+    const float ks = 1.f / (1.f - dropout_p);
+    if (pass == 0) {
+        if (x_bf16)
+            rows_bn_bwd_kernel<0, bf16><<<nparts, 256, 0, s>>>(
+                (const bf16*)dz, LZ, (const bf16*)x, LX, R, C, scale, shift, mean, invstd, cA, cB,
+                cC, th, ks, seed, (uint32_t)site, partials, (bf16*)dx, LD);
+        else
+            rows_bn_bwd_kernel<0, float><<<nparts, 256, 0, s>>>(
+                (const bf16*)dz, LZ, (const float*)x, LX, R, C, scale, shift, mean, invstd, cA, cB,
+                cC, th, ks, seed, (uint32_t)site, partials, (bf16*)dx, LD);
+    } else {
+        const long long n = R * (C / 8);
+        if (x_bf16)
+            rows_bn_bwd_kernel<1, bf16><<<ov3d_cdiv(n, 256), 256, 0, s>>>(
+                (const bf16*)dz, LZ, (const bf16*)x, LX, R, C, scale, shift, mean, invstd, cA, cB,
+                cC, th, ks, seed, (uint32_t)site, partials, (bf16*)dx, LD);
+        else
+            rows_bn_bwd_kernel<1, float><<<ov3d_cdiv(n, 256), 256, 0, s>>>(
+                (const bf16*)dz, LZ, (const float*)x, LX, R, C, scale, shift, mean, invstd, cA, cB,
+                cC, th, ks, seed, (uint32_t)site, partials, (bf16*)dx, LD);
+    }
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}

@@ -1,0 +1,261 @@
+"""The five 3DETR prediction heads side by side (training, bf16 autocast, one process).
+
+Reference: models/model_3detr.py:_build_heads / get_box_predictions — five GenericMLPs
+(models/helpers.py:45-112), each Conv1d(256,256) -> BatchNorm1d -> ReLU -> Dropout(0.3)
+-> Conv1d(256,256) -> BatchNorm1d -> ReLU -> Dropout(0.3) -> Conv1d(256, out), all on
+the same (L*B*Q, 256) decoder-feature rows.  BatchNorm is per channel, so the five
+heads are exactly one MLP over 5 x 256 channels with block-diagonal later layers:
+
+  layer 1  ONE GEMM            x (R,256) @ W1cat^T (1280,256)          -> h1 (R,1280)
+  BN+ReLU+Dropout              csrc/bnrows.hip over 1280 channels       -> z1
+  layer 2  ONE batched GEMM    per head z1[:, 256i:256i+256] @ W2_i^T   -> h2 (5,R,256)
+  BN+ReLU+Dropout              (head-major addressing)                  -> z2 (R,1280)
+  layer 3  visual: z2[:, :256] @ W3v^T;  box heads: z2[:, 256:] @ blockdiag(W3_1..4)^T
+
+Backward mirrors it; weight / bias gradients use the one-launch ov3d_wgrad kernel.
+The heads' parameters and BN buffers are re-pointed at shared storages (the module
+objects, their names and state-dict keys do not change), so the concatenated weights
+exist without a per-step concatenation.  Dropout masks come from a counter-based hash
+(bnrows.hip), regenerated in the backward.  Results equal the per-head evaluation up
+to bf16 rounding (tests/test_heads_gpu.py).
+"""
+import torch
+import torch.nn as nn
+
+from . import _native as nat
+from . import attention as flash
+from .gemm import fused_weight_grad
+from .sa_fused import _bwd_coefs, _finalize
+
+HEAD_ORDER = ("visual_embed_head", "center_head", "size_head", "angle_cls_head",
+              "angle_residual_head")
+NPARTS = 256
+
+
+def _structure(mlp):
+    """-> (conv1, bn1, drop1, conv2, bn2, drop2, conv3) of a reference head, or None."""
+    m = list(mlp.layers)
+    if len(m) != 9:
+        return None
+    c1, b1, r1, d1, c2, b2, r2, d2, c3 = m
+    ok = (isinstance(c1, nn.Conv1d) and isinstance(c2, nn.Conv1d) and isinstance(c3, nn.Conv1d)
+          and type(b1) is nn.BatchNorm1d and type(b2) is nn.BatchNorm1d
+          and isinstance(r1, nn.ReLU) and isinstance(r2, nn.ReLU)
+          and isinstance(d1, nn.Dropout) and isinstance(d2, nn.Dropout)
+          and c1.bias is None and c2.bias is None and c3.bias is not None)
+    return (c1, b1, d1, c2, b2, d2, c3) if ok else None
+
+
+class HeadPack:
+    """Shared storages for the five heads' hidden layers (built lazily on the device)."""
+
+    def __init__(self, heads):
+        self.parts = [_structure(heads[n]) for n in HEAD_ORDER]
+        self.ok = all(p is not None for p in self.parts)
+        if self.ok:
+            c1 = self.parts[0][0]
+            self.C = c1.in_channels
+            self.H = c1.out_channels
+            self.ok = all(p[0].in_channels == self.C and p[0].out_channels == self.H and
+                          p[3].in_channels == self.H and p[3].out_channels == self.H and
+                          p[6].in_channels == self.H for p in self.parts) and self.H % 64 == 0
+        self.store = None
+        self.sites = (flash.new_site(), flash.new_site())
+
+    def _tensors(self):
+        P = self.parts
+        return {"w1": [p[0].weight for p in P], "w2": [p[3].weight for p in P],
+                "g1": [p[1].weight for p in P], "b1": [p[1].bias for p in P],
+                "g2": [p[4].weight for p in P], "b2": [p[4].bias for p in P],
+                "rm1": [p[1].running_mean for p in P], "rv1": [p[1].running_var for p in P],
+                "rm2": [p[4].running_mean for p in P], "rv2": [p[4].running_var for p in P]}
+
+    def _shared(self):
+        if self.store is None:
+            return False
+        for key, ts in self._tensors().items():
+            base = self.store[key]
+            step = ts[0].numel()
+            for i, t in enumerate(ts):
+                if t.data_ptr() != base.data_ptr() + i * step * base.element_size() or \
+                        t.device != base.device:
+                    return False
+        return True
+
+    def ensure(self):
+        """(Re-)point parameters / buffers at the shared storages when needed (e.g. after
+        .to(device) or load_state_dict with assign=True)."""
+        if self._shared():
+            return
+        store = {}
+        with torch.no_grad():
+            for key, ts in self._tensors().items():
+                base = torch.cat([t.detach().reshape(-1) for t in ts])
+                store[key] = base
+                step = ts[0].numel()
+                for i, t in enumerate(ts):
+                    view = base[i * step:(i + 1) * step].view(t.shape)
+                    if isinstance(t, nn.Parameter):
+                        t.data = view
+                    else:
+                        for p in self.parts:
+                            for bn in (p[1], p[4]):
+                                for name in ("running_mean", "running_var"):
+                                    if bn._buffers[name] is t:
+                                        bn._buffers[name] = view
+        self.store = store
+
+    def bns(self):
+        return [p[1] for p in self.parts], [p[4] for p in self.parts]
+
+
+def supported(pack, rows):
+    if not (pack.ok and rows.is_cuda and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        return False
+    if torch.distributed.is_available() and torch.distributed.is_initialized() and \
+            torch.distributed.get_world_size() > 1:
+        return False   # DDP + SyncBatchNorm: the per-head modules (reference semantics)
+    drops = set()
+    for p in pack.parts:
+        for bn in (p[1], p[4]):
+            if not bn.training or not bn.track_running_stats or bn.momentum is None:
+                return False
+        drops.add((p[2].p if p[2].training else 0.0, p[5].p if p[5].training else 0.0))
+    return len(drops) == 1
+
+
+def _stats_finalize(x, layout, R, C, gamma, beta, bns, rm, rv):
+    """train-mode batch statistics of BN over R rows -> (mean, invstd, scale, shift);
+    running stats of the concatenated storages updated (momentum, unbiased var)."""
+    dev = x.device
+    parts = torch.empty((NPARTS, 2, C), dtype=torch.float64, device=dev)
+    nat.call("ov3d_rows_bn_stats", x, int(x.dtype == torch.bfloat16), *layout, R, C, parts, NPARTS,
+             like=x)
+    tot = torch.empty(2 * C, dtype=torch.float64, device=dev)
+    nat.call("ov3d_reduce_partials", parts, NPARTS, 2 * C, tot, like=x)
+    mean, invstd, scale, shift = (torch.empty(C, dtype=torch.float32, device=dev) for _ in range(4))
+    bn0 = bns[0]
+    nat.call("ov3d_bn_finalize", tot, float(R), C, gamma, beta, float(bn0.eps), float(bn0.momentum),
+             rm, rv, mean, invstd, scale, shift, like=x)
+    return mean, invstd, scale, shift
+
+
+class _Heads(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, pack, p1, p2, w3v, b3v, w3s, b3s, *params):
+        # params: the shared-storage views (grads are returned for them); the kernels use the
+        # storages directly
+        st = pack.store
+        R = x.shape[0]
+        H5 = 5 * pack.H
+        H = pack.H
+        bf = torch.bfloat16
+        dev = x.device
+        seed = flash._seed(dev)
+        xb = x.to(bf).contiguous()
+        w1 = st["w1"].view(H5, pack.C).to(bf)
+        w2 = st["w2"].view(5, H, H).to(bf)
+        bn1, bn2 = pack.bns()
+        torch._foreach_add_([b.num_batches_tracked for b in bn1 + bn2], 1)
+        h1 = xb @ w1.t()                                                         # (R, 5H)
+        rowmajor = (H5, 0, H5)
+        m1, i1, a1, s1 = _stats_finalize(h1, rowmajor, R, H5, st["g1"], st["b1"], bn1, st["rm1"],
+                                         st["rv1"])
+        z1 = torch.empty((R, H5), dtype=bf, device=dev)
+        nat.call("ov3d_rows_bn_apply", h1, 1, *rowmajor, R, H5, a1, s1, float(p1), seed,
+                 pack.sites[0], z1, *rowmajor, like=x)
+        h2 = torch.bmm(z1.view(R, 5, H).transpose(0, 1), w2.transpose(1, 2))  # (5, R, H)
+        headmajor = (H, R * H, H)
+        m2, i2, a2, s2 = _stats_finalize(h2, headmajor, R, H5, st["g2"], st["b2"], bn2, st["rm2"],
+                                         st["rv2"])
+        z2 = torch.empty((R, H5), dtype=bf, device=dev)
+        nat.call("ov3d_rows_bn_apply", h2, 1, *headmajor, R, H5, a2, s2, float(p2), seed,
+                 pack.sites[1], z2, *rowmajor, like=x)
+        w3vb, w3sb = w3v.to(bf), w3s.to(bf)
+        out_v = torch.addmm(b3v.to(bf), z2[:, :H], w3vb.t())
+        out_s = torch.addmm(b3s.to(bf), z2[:, H:], w3sb.t())
+        ctx.save_for_backward(xb, h1, h2, z1, z2, w1, w2, w3vb, w3sb, m1, i1, a1, s1, m2, i2, a2, s2)
+        ctx.meta = (pack, float(p1), float(p2), R, x.dtype, w3s.shape)
+        return out_v.float(), out_s.float()
+
+    @staticmethod
+    def backward(ctx, gv, gs):
+        (xb, h1, h2, z1, z2, w1, w2, w3vb, w3sb, m1, i1, a1, s1, m2, i2, a2, s2) = ctx.saved_tensors
+        pack, p1, p2, R, xdt, w3s_shape = ctx.meta
+        st = pack.store
+        H = pack.H
+        H5 = 5 * H
+        bf = torch.bfloat16
+        dev = xb.device
+        seed = flash._seed(dev)
+        gv = gv.to(bf).contiguous()
+        gs = gs.to(bf).contiguous()
+        dw3v, db3v = fused_weight_grad(gv, z2[:, :H], bias=True)
+        dw3s, db3s = fused_weight_grad(gs, z2[:, H:], bias=True)
+        dz2 = torch.empty((R, H5), dtype=bf, device=dev)
+        torch.mm(gv, w3vb, out=dz2[:, :H])
+        torch.mm(gs, w3sb, out=dz2[:, H:])
+        rowmajor = (H5, 0, H5)
+        headmajor = (H, R * H, H)
+        # BN2 (input h2 head-major, grad dz2 row-major) -> dh2 head-major
+        dh2 = torch.empty((5, R, H), dtype=bf, device=dev)
+        dg2, dbe2 = _bn_backward(dz2, rowmajor, h2, headmajor, R, H5, st["g2"], m2, i2, a2, s2, p2,
+                                 seed, pack.sites[1], dh2, headmajor)
+        dw2 = torch.empty((5, H, H), dtype=torch.float32, device=dev)
+        for i in range(5):
+            fused_weight_grad(dh2[i], z1[:, i * H:(i + 1) * H], bias=False, out_w=dw2[i])
+        dz1 = torch.bmm(dh2, w2)                                                 # (5, R, H)
+        dh1 = torch.empty((R, H5), dtype=bf, device=dev)
+        dg1, dbe1 = _bn_backward(dz1, headmajor, h1, rowmajor, R, H5, st["g1"], m1, i1, a1, s1, p1,
+                                 seed, pack.sites[0], dh1, rowmajor)
+        dw1, _ = fused_weight_grad(dh1, xb, bias=False)
+        dx = (dh1 @ w1).to(xdt)
+        grads = {"w1": dw1.view(-1), "w2": dw2.view(-1), "g1": dg1, "b1": dbe1, "g2": dg2,
+                 "b2": dbe2}
+        out = []
+        for key in ("w1", "w2", "g1", "b1", "g2", "b2"):
+            g = grads[key]
+            step = g.numel() // 5
+            shape = pack._tensors()[key][0].shape
+            out += [g[i * step:(i + 1) * step].view(shape) for i in range(5)]
+        return (dx, None, None, None, dw3v, db3v, dw3s.view(w3s_shape), db3s, *out)
+
+
+def _bn_backward(dz, lz, x, lx, R, C, gamma, mean, invstd, scale, shift, p, seed, site, dx, ld):
+    dev = x.device
+    parts = torch.empty((NPARTS, 2, C), dtype=torch.float64, device=dev)
+    nat.call("ov3d_rows_bn_bwd", 0, dz, *lz, x, 1, *lx, R, C, scale, shift, mean, invstd, None, None,
+             None, float(p), seed, site, parts, NPARTS, None, 0, 0, 8, like=x)
+    tot = torch.empty(2 * C, dtype=torch.float64, device=dev)
+    nat.call("ov3d_reduce_partials", parts, NPARTS, 2 * C, tot, like=x)
+    cA, cB, cC, dg, db = _bwd_coefs(tot, R, gamma, mean, invstd, C)
+    nat.call("ov3d_rows_bn_bwd", 1, dz, *lz, x, 1, *lx, R, C, scale, shift, mean, invstd, cA, cB, cC,
+             float(p), seed, site, None, 0, dx, *ld, like=x)
+    return dg, db
+
+
+def fused_heads(pack, rows):
+    """rows (R, 256) -> {head name: (R, out) fp32} for the five MLP heads (training)."""
+    pack.ensure()
+    P = pack.parts
+    p1 = P[0][2].p if P[0][2].training else 0.0
+    p2 = P[0][5].p if P[0][5].training else 0.0
+    w3v, b3v = P[0][6].weight, P[0][6].bias
+    small = P[1:]
+    outs = [p[6].weight.shape[0] for p in small]
+    w3s = torch.block_diag(*[p[6].weight.view(p[6].weight.shape[0], -1) for p in small])
+    b3s = torch.cat([p[6].bias for p in small])
+    params = []
+    for key, ts in pack._tensors().items():
+        if key in ("rm1", "rv1", "rm2", "rv2"):
+            continue
+        params += ts
+    out_v, out_s = _Heads.apply(rows, pack, p1, p2, w3v.view(w3v.shape[0], -1), b3v, w3s, b3s,
+                                *params)
+    res = {HEAD_ORDER[0]: out_v}
+    o = 0
+    for name, n in zip(HEAD_ORDER[1:], outs):
+        res[name] = out_s[:, o:o + n]
+        o += n
+    return res

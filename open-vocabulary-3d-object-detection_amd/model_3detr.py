@@ -23,6 +23,7 @@ import torch
 import torch.nn as nn
 
 from . import attention as flash
+from . import heads as heads_mod
 from . import pointnet2_utils as pu
 from .helpers import GenericMLP
 from .pc_util import scale_points, shift_scale_points
@@ -91,6 +92,7 @@ class Model3DETR(nn.Module):
         if cls_logits_layout not in ("reference", "fixed"):
             raise ValueError(cls_logits_layout)
         self.cls_logits_layout = cls_logits_layout
+        self.fuse_heads = True   # heads.py under bf16 autocast training (False: per-head MLPs)
 
     def _build_heads(self, cfg, dim, dropout, text_embedding):
         mlp = partial(GenericMLP, norm_fn_name="bn1d", activation="relu", use_conv=True,
@@ -143,18 +145,30 @@ class Model3DETR(nn.Module):
     # -------------------------------------------------------------------- heads
     def get_box_predictions(self, query_xyz, point_cloud_dims, box_features):
         """Heads for all L decoder layers at once (the reference loops over layers,
-        model_3detr.py:264-306); evaluated in fp32 like the reference, even under autocast."""
-        with torch.autocast(device_type=box_features.device.type, enabled=False):
-            return self._box_predictions(query_xyz.float(), point_cloud_dims, box_features.float())
-
-    def _box_predictions(self, query_xyz, point_cloud_dims, box_features):
+        model_3detr.py:264-306).  Training under bf16 autocast: the five MLP heads run as
+        one fused MLP (heads.py); the box parametrisation is evaluated in fp32 like the
+        reference, even under autocast."""
         L, Q, B, C = box_features.shape
         # heads on channels-last rows ordered (l, b, q): BatchNorm1d statistics are over all
         # L*B*Q positions exactly as on the reference's (L*B, C, Q) conv input
         rows = box_features.permute(0, 2, 1, 3).reshape(L * B * Q, C)
+        pre = None
+        if self.fuse_heads:
+            if getattr(self, "_head_pack", None) is None:
+                self._head_pack = heads_mod.HeadPack(self.mlp_heads)
+            if heads_mod.supported(self._head_pack, rows):
+                pre = heads_mod.fused_heads(self._head_pack, rows)
+        with torch.autocast(device_type=box_features.device.type, enabled=False):
+            return self._box_predictions(query_xyz.float(), point_cloud_dims, rows.float(),
+                                         (L, Q, B), pre)
+
+    def _box_predictions(self, query_xyz, point_cloud_dims, rows, dims_lqb, pre=None):
+        L, Q, B = dims_lqb
         heads = self.mlp_heads
 
         def head(name):
+            if pre is not None:
+                return pre[name].view(L, B, Q, -1)
             return heads[name].rows(rows).view(L, B, Q, -1)
 
         visual = head("visual_embed_head")                                  # (L, B, Q, 640)

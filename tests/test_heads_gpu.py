@@ -1,0 +1,100 @@
+"""Fused prediction heads (heads.py + csrc/bnrows.hip + ov3d_wgrad) against the five
+per-head GenericMLPs evaluated in fp32 PyTorch on the same rows: outputs, BatchNorm
+running statistics and every parameter gradient.  bf16 operands inside the fused path:
+outputs within 3e-2 relative (Frobenius), and running statistics and every
+gradient no further from fp32 than PyTorch's own bf16-autocast evaluation of the same
+heads (x1.5, or 3e-2): the two BatchNorm backward passes amplify bf16 rounding."""
+import copy
+
+import pytest
+import torch
+
+from helpers import ov3d  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(cuda):
+    from bench import default_args
+    from ov3d_amd import synthetic
+    from ov3d_amd.dataset_config import SunrgbdDatasetConfig
+    import ov3d_amd
+    torch.manual_seed(0)
+    model, _ = ov3d_amd.build_model(default_args(), SunrgbdDatasetConfig(),
+                                    text_embedding=synthetic.text_embedding())
+    return model.to(cuda).train()
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
+
+
+def test_fused_heads_match_per_head_fp32(cuda):
+    from ov3d_amd import heads as H
+    model = _model(cuda)
+    ref_heads = copy.deepcopy(model.mlp_heads)
+    fus_heads = model.mlp_heads
+    for hs in (ref_heads, fus_heads):
+        for m in hs.modules():
+            if isinstance(m, torch.nn.Dropout):
+                m.p = 0.0
+    torch.manual_seed(1)
+    rows = torch.randn(8192, 256, device=cuda)
+    g = {n: torch.randn(8192, fus_heads[n].layers[-1].out_channels, device=cuda) for n in H.HEAD_ORDER}
+
+    out_r = {n: ref_heads[n].rows(rows) for n in H.HEAD_ORDER}
+    sum(((out_r[n] * g[n]).sum() for n in H.HEAD_ORDER)).backward()
+    # PyTorch's own bf16 autocast evaluation of the per-head MLPs: the error budget
+    bf_heads = copy.deepcopy(ref_heads)
+    for p_ in bf_heads.parameters():
+        p_.grad = None
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out_b = {n: bf_heads[n].rows(rows) for n in H.HEAD_ORDER}
+    sum(((out_b[n].float() * g[n]).sum() for n in H.HEAD_ORDER)).backward()
+
+    pack = H.HeadPack(fus_heads)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        assert H.supported(pack, rows)
+        out_f = H.fused_heads(pack, rows)
+    sum(((out_f[n] * g[n]).sum() for n in H.HEAD_ORDER)).backward()
+
+    for n in H.HEAD_ORDER:
+        assert out_f[n].shape == out_r[n].shape
+        assert _rel(out_f[n], out_r[n]) < 3e-2, (n, _rel(out_f[n], out_r[n]))
+        for (name, pr), pf, pb in zip(ref_heads[n].named_parameters(), fus_heads[n].parameters(),
+                                      bf_heads[n].parameters()):
+            assert pf.grad is not None, (n, name)
+            ef, eb = _rel(pf.grad, pr.grad), _rel(pb.grad, pr.grad)
+            # no further from fp32 than PyTorch's bf16 autocast path (or within 3e-2)
+            assert ef <= max(1.5 * eb, 3e-2), (n, name, ef, eb)
+        for (name, br), bf, bb in zip(ref_heads[n].named_buffers(), fus_heads[n].buffers(),
+                                      bf_heads[n].buffers()):
+            if br.dtype.is_floating_point:
+                ef, eb = _rel(bf, br), _rel(bb, br)
+                assert ef <= max(1.5 * eb, 5e-3), (n, name, ef, eb)
+            else:
+                assert torch.equal(bf, br), (n, name)
+    # the state dict keeps the reference keys and shapes
+    assert set(model.state_dict()) == set(_model(cuda).state_dict())
+
+
+def test_fused_heads_dropout_and_step(cuda):
+    """Model-level: a bf16 training step takes the fused heads (dropout 0.3 active) and
+    produces finite losses and gradients for every head parameter."""
+    from bench import default_args
+    from ov3d_amd import synthetic
+    from ov3d_amd.dataset_config import SunrgbdDatasetConfig
+    import ov3d_amd
+    model = _model(cuda)
+    crit = ov3d_amd.build_criterion(default_args(), SunrgbdDatasetConfig()).to(cuda)
+    batch = synthetic.make_batch(4, seed=3, device=cuda)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = model({k: batch[k] for k in ("point_clouds", "point_cloud_dims_min",
+                                           "point_cloud_dims_max")})
+    assert model._head_pack is not None and model._head_pack.store is not None
+    loss, _ = crit(out, batch)
+    loss.backward()
+    assert torch.isfinite(loss)
+    for n, p in model.mlp_heads.named_parameters():
+        if p.requires_grad:
+            assert p.grad is not None and torch.isfinite(p.grad).all(), n
