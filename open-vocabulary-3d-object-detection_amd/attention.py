@@ -48,9 +48,9 @@ def next_step(device):
     _seed(device).add_(1)
 
 
-def supported(q_src, k_src, num_heads, attn_mask):
+def supported(q_src, embed_dim, num_heads, attn_mask):
     """the HIP kernels: head_dim 64, no mask, query length a multiple of 32"""
-    return (q_src.is_cuda and attn_mask is None and q_src.shape[-1] % (num_heads * HEAD_DIM) == 0
+    return (q_src.is_cuda and attn_mask is None and embed_dim == num_heads * HEAD_DIM
             and q_src.shape[0] % 32 == 0)
 
 

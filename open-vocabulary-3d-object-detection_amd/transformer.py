@@ -54,8 +54,8 @@ class MultiheadAttention(nn.Module):
         else:
             srcs = list(in_projection(w, bias, ((query, 0, E), (key, E, 2 * E), (value, 2 * E, 3 * E))))
             spec = ((0, 0), (1, 0), (2, 0))
-        if srcs[0].dtype == torch.bfloat16 and flash.supported(srcs[0], srcs[spec[1][0]],
-                                                               self.num_heads, attn_mask):
+        if srcs[0].dtype == torch.bfloat16 and flash.supported(srcs[0], E, self.num_heads,
+                                                               attn_mask):
             # HIP flash attention straight on the projection rows (csrc/attn.hip)
             out = flash.attention_packed(srcs, spec, L, S, self.num_heads,
                                          dropout_p=self.dropout if self.training else 0.0,

@@ -149,3 +149,21 @@ def test_dropout_hash_statistics(cuda):
                  (z[:, :-1], z[:, 1:]), (z[:-1], z[1:])]:
         corr = (a * b).mean().item()
         assert abs(corr) < 5e-3, corr
+
+
+@pytest.mark.parametrize("E,H", [(128, 4), (256, 2)])
+def test_module_head_dim_not_64_uses_sdpa(cuda, E, H):
+    """head_dim != 64 (e.g. dec_dim 128 / 4 heads) is not a flash-kernel shape: the module
+    must route it to scaled-dot-product attention, for self (q is k) and cross attention."""
+    from ov3d_amd.transformer import MultiheadAttention
+    torch.manual_seed(0)
+    m = MultiheadAttention(E, H).to(cuda).eval()
+    x = torch.randn(64, 2, E, device=cuda)
+    mem = torch.randn(256, 2, E, device=cuda)
+    x2 = x + 1
+    for q, k, v in ((x, x, x), (x, x, x2), (x, mem, mem)):
+        with torch.no_grad():
+            ref = m(q, k, v).float()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                out = m(q, k, v).float()
+        assert _rel(out, ref) < 2e-2
