@@ -289,6 +289,57 @@ int ov3d_rows_bn_bwd(int pass, const void* dz, long long ldz, long long bstride_
                      float dropout_p, const int64_t* seed, int site, double* partials, int nparts,
                      void* dx, long long ldd, long long bstride_d, int cbd, void* stream);
 
+
+/* ---- Set-criterion losses (criterion.py SetCriterion.forward, all decoder layers) ----
+ * Replaces criterion.py:143-337 (loss_sem_cls, loss_angle, loss_center, loss_size,
+ * loss_giou), 121-130 (loss_cardinality) and the weighting / layer sum of 402-442.
+ * Proposal (l, b, q) is row (l*B + b)*Q + q of every (L*B*Q, n) operand (row stride ld_*).
+ * Dict columns: OV3D_LOSS_COL_* ; dict row i = layer final, aux 0, aux 1, ... */
+#define OV3D_LOSS_SEM 1
+#define OV3D_LOSS_CENTER 2
+#define OV3D_LOSS_SIZE 4
+#define OV3D_LOSS_GIOU 8
+#define OV3D_LOSS_ALIGN 16
+#define OV3D_LOSS_NCOLS 8   /* sem, angle_cls, angle_reg, center, size, giou, 2dalignment, cardinality */
+#define OV3D_LOSS_MAX_B 256
+typedef struct {
+    int L, B, Q, G, T, NB;
+    int flags;             /* OV3D_LOSS_* terms computed (angle cls / reg always) */
+    int final_last;        /* 1: computation layer L-1 is the final layer; 0: layer 0 is */
+    const float* logits;        long long ld_logits;        /* (L*B*Q, T) */
+    const float* angle_logits;  long long ld_angle_logits;  /* (L*B*Q, NB) */
+    const float* angle_res;     long long ld_angle_res;     /* (L*B*Q, NB), normalised */
+    const float* center;        long long ld_center;        /* (L*B*Q, 3) normalised */
+    const float* size;          long long ld_size;          /* (L*B*Q, 3) normalised */
+    const float* gious;         /* (L*B, Q, G) or NULL */
+    const int64_t* inds;        /* (L*B, Q) matched GT slot */
+    const float* matched;       /* (L*B, Q) 0/1 */
+    const int64_t* gt_sem;      /* (B, G) */
+    const int64_t* gt_angle_cls;  /* (B, G) */
+    const float* gt_angle_res;  /* (B, G) radians */
+    const float* gt_center;     /* (B, G, 3) normalised */
+    const float* gt_size;       /* (B, G, 3) normalised */
+    const int64_t* nactual;     /* (B,) */
+    const float* cls_weights;   /* (T,) */
+    const float* num_boxes;     /* device scalar */
+    const float* align;         /* (L,) per-layer 2D alignment sums or NULL */
+    float dict_w[OV3D_LOSS_NCOLS];   /* dict value = per-layer term * dict_w */
+    float total_w[OV3D_LOSS_NCOLS];  /* d total / d term (0 = not in the total) */
+    int total_order[OV3D_LOSS_NCOLS]; int n_total;   /* summation order of the total */
+    float res_scale;            /* 1 / (float)(pi / NB) */
+} ov3d_set_loss_desc;
+/* raw: (L, 9) f32 workspace (kept for the backward); ticket: one int, zero before the first
+ * call (the kernel resets it); dict_out (L, 8); total: scalar */
+long long ov3d_set_loss_desc_size(void);   /* sizeof(ov3d_set_loss_desc), for FFI layout checks */
+int ov3d_set_loss_fwd(const ov3d_set_loss_desc* desc, float* raw, int* ticket, float* dict_out,
+                      float* total, void* stream);
+/* d_dict (L, 8) or NULL, d_total scalar (device) or NULL; every non-NULL gradient is written
+ * in full (contiguous (L*B*Q, n), g_gious (L*B, Q, G), g_align (L,)) */
+int ov3d_set_loss_bwd(const ov3d_set_loss_desc* desc, const float* raw, const float* d_dict,
+                      const float* d_total, float* g_logits, float* g_angle_logits,
+                      float* g_angle_res, float* g_center, float* g_size, float* g_gious,
+                      float* g_align, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

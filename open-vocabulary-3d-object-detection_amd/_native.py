@@ -51,9 +51,11 @@ _SIGS = {
     "ov3d_rows_bn_stats": "pillilipip",
     "ov3d_rows_bn_apply": "pillilippfpipllip",
     "ov3d_rows_bn_bwd": "ipllipillilipppppppfpipipllip",
+    "ov3d_set_loss_fwd": "pppppp",
+    "ov3d_set_loss_bwd": "pppppppppppp",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
-                          "ov3d_wgrad_workspace", "ov3d_wgrad_tiles")
+                          "ov3d_wgrad_workspace", "ov3d_wgrad_tiles", "ov3d_set_loss_desc_size")
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_longlong, "f": ctypes.c_float,
        "d": ctypes.c_double}
@@ -84,6 +86,8 @@ def load():
         lib.ov3d_wgrad_workspace.restype = ctypes.c_longlong
         lib.ov3d_wgrad_tiles.argtypes = [ctypes.c_int] * 2
         lib.ov3d_wgrad_tiles.restype = ctypes.c_int
+        lib.ov3d_set_loss_desc_size.argtypes = []
+        lib.ov3d_set_loss_desc_size.restype = ctypes.c_longlong
         lib.ov3d_version.argtypes = []
         lib.ov3d_version.restype = ctypes.c_char_p
         _lib = lib

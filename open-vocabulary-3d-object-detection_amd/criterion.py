@@ -26,6 +26,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .assignment import Assignments, hungarian
+from . import setloss
 from .box_util import generalized_box3d_iou
 from .dist import all_reduce_average
 from .image_util import clip_batch, project_boxes_2d
@@ -80,6 +81,7 @@ class SetCriterion(nn.Module):
         self.register_buffer("semcls_percls_weights", cls_w)
         self.loss_weight_dict = w
         self.giou_k2_bug = giou_k2_bug
+        self.fused_losses = True   # HIP loss kernels on the device (setloss.py); False: torch
 
     def _w(self, key):
         return self.loss_weight_dict.get(key + "_weight", 0)
@@ -151,6 +153,59 @@ class SetCriterion(nn.Module):
             inds = torch.roll(asg["per_prop_gt_inds"].view(L, B, Q), -1, 0).reshape(L * B, Q)
             mask = torch.roll(asg["proposal_matched_mask"].view(L, B, Q), -1, 0).reshape(L * B, Q)
 
+        align = None
+        if self._computed("loss_2dalignment"):
+            if clip is None:
+                raise ValueError("loss_2dalignment_weight > 0 needs a RegionCLIP model (clip=...)")
+            if hasattr(clip, "region_features"):
+                align = self._alignment_batched(cat, L, B, targets, clip)
+            else:
+                align = self._alignment([layer(l) for l in range(L)], targets, clip)
+        if self.fused_losses and setloss.supported(cat("sem_cls_logits")):
+            return self._losses_fused(cat, L, B, final, gious, inds, mask, targets, num_boxes, align)
+        return self._losses_torch(cat, L, B, final, aux, gious, center_dist, gt_labels, inds, mask,
+                                  targets, num_boxes, nactual_gt, align)
+
+    def _dict_keys(self):
+        """LOSS_KEYS present in the dict: computed terms (angle cls / reg always)"""
+        return [k for k in LOSS_KEYS if k in ("loss_angle_cls", "loss_angle_reg") or self._computed(k)]
+
+    def _losses_fused(self, cat, L, B, final, gious, inds, mask, targets, num_boxes, align):
+        """all terms, the dict table and the total in one HIP launch (setloss.py)."""
+        keys = self._dict_keys()
+        cols = {k: setloss.COLUMNS.index(k) for k in keys}
+        dict_w = [1.0] * 8
+        total_w = [0.0] * 8
+        for k in keys:
+            w = self._w(k)
+            dict_w[cols[k]] = float(w) if w > 0 else 1.0
+        weighted = [k[: -len("_weight")] for k, w in self.loss_weight_dict.items() if w > 0]
+        for k in weighted:
+            total_w[cols[k]] = float(self._w(k))
+        Q = inds.shape[1]
+        table, total = setloss.set_losses(
+            L, B, Q, final != 0, cat("sem_cls_logits"), cat("angle_logits"),
+            cat("angle_residual_normalized"),
+            cat("center_normalized") if "loss_center" in keys else None,
+            cat("size_normalized") if "loss_size" in keys else None,
+            gious if "loss_giou" in keys else None, align, inds, mask, targets,
+            self.semcls_percls_weights if "loss_sem_cls" in keys else None, num_boxes,
+            dict_w, total_w, [cols[k] for k in weighted])
+        loss_dict = {}
+        for i in range(L):
+            suffix = "" if i == 0 else f"_{i - 1}"
+            for k in keys:
+                loss_dict[k + suffix] = table[i, cols[k]]
+            loss_dict["loss_cardinality" + suffix] = table[i, 7].detach()
+        return total, loss_dict
+
+    def _losses_torch(self, cat, L, B, final, aux, gious, center_dist, gt_labels, inds, mask,
+                      targets, num_boxes, nactual_gt, align):
+        """the same terms as torch expressions (CPU, and the restatement the HIP loss
+        kernels are tested against)."""
+        def rep(t):
+            return t.repeat((L,) + (1,) * (t.dim() - 1))
+
         per = {}  # key -> (L,) tensor of unweighted per-layer losses
         if self._computed("loss_sem_cls"):
             logits = cat("sem_cls_logits").float()                    # (LB,Q,T)
@@ -185,13 +240,8 @@ class SetCriterion(nn.Module):
         if self._computed("loss_giou"):
             gl = torch.gather(1 - gious, 2, inds.unsqueeze(-1)).squeeze(-1)
             per["loss_giou"] = (gl * mask).view(L, -1).sum(1) / num_boxes
-        if self._computed("loss_2dalignment"):
-            if clip is None:
-                raise ValueError("loss_2dalignment_weight > 0 needs a RegionCLIP model (clip=...)")
-            if hasattr(clip, "region_features"):
-                per["loss_2dalignment"] = self._alignment_batched(cat, L, B, targets, clip)
-            else:
-                per["loss_2dalignment"] = self._alignment([layer(l) for l in range(L)], targets, clip)
+        if align is not None:
+            per["loss_2dalignment"] = align
         with torch.no_grad():
             lg = cat("sem_cls_logits")
             pred_obj = (lg.argmax(-1) != lg.shape[-1] - 1).sum(1).float().view(L, B)

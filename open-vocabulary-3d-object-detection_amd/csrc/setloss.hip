@@ -1,0 +1,295 @@
+// 3DETR set-criterion losses for every decoder layer: one launch forward, one backward.
+//
+// Reference: criterion.py SetCriterion — loss_sem_cls (143-178: weighted cross-entropy,
+// unmatched proposals labelled background), loss_angle (180-246: cross-entropy on the
+// matched GT bin + Huber(delta 1) on the residual of that bin, normalised by pi/nbins),
+// loss_center (248-272: L1 of the matched centre, the gathered cdist(p=1)), loss_size
+// (298-337: L1 over the 3 normalised sizes), loss_giou (274-296: 1 - GIoU of the match),
+// loss_cardinality (121-130, logged), the weighting of 402-419 and the layer sum of
+// 425-442 (final layer first, then the auxiliary layers).
+//
+// Rows: proposal (l, b, q) is row (l*B + b)*Q + q of every (L*B*Q, n) operand, read
+// through a row stride so column slices of a wider head output need no copy.
+//
+// Forward: one workgroup per decoder layer accumulates that layer's sums in fp64 and
+// writes the unweighted per-layer terms; the last workgroup to finish (ticket counter,
+// reset by that workgroup) forms the (L, 8) table of weighted dict values in the
+// reference's key order and the total in the reference's summation order
+// (criterion.py:415-419: per layer 0 + w_k0*l_k0 + w_k1*l_k1 ...; layers summed
+// final, aux 0, aux 1, ...), in fp32 like the torch expression.
+// Backward: one thread per proposal writes its rows of every gradient.
+#include "common.h"
+
+#include <math.h>
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kCols = OV3D_LOSS_NCOLS;   // sem, angle_cls, angle_reg, center, size, giou, 2d, card
+constexpr int kRaw = kCols + 1;          // + the layer's sum of class weights (sem denominator)
+
+__device__ __forceinline__ int clampi(long long v, int hi) {
+    return v < 0 ? 0 : (v > hi ? hi : (int)v);
+}
+
+__device__ __forceinline__ float huber(float e) {
+    // reference utils/misc.py:25-36 with delta = 1: 0.5*q^2 + (a - q), q = min(a, 1)
+    const float a = fabsf(e);
+    const float q = fminf(a, 1.f);
+    return 0.5f * (q * q) + (a - q);
+}
+
+__device__ __forceinline__ float sgnf(float x) { return (float)((x > 0.f) - (x < 0.f)); }
+
+// position of computation layer l in the reference's (final, aux 0, aux 1, ...) order
+__device__ __forceinline__ int dict_pos(const ov3d_set_loss_desc& d, int l) {
+    return d.final_last ? (l == d.L - 1 ? 0 : l + 1) : l;
+}
+__device__ __forceinline__ int layer_at(const ov3d_set_loss_desc& d, int i) {
+    return d.final_last ? (i == 0 ? d.L - 1 : i - 1) : i;
+}
+
+// max, index of the first maximum and sum of exp(x - max) over n values
+__device__ __forceinline__ void softmax_stats(const float* x, int n, float& mx, int& am, float& s) {
+    mx = x[0];
+    am = 0;
+    for (int t = 1; t < n; ++t)
+        if (x[t] > mx) { mx = x[t]; am = t; }
+    s = 0.f;
+    for (int t = 0; t < n; ++t) s += expf(x[t] - mx);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__global__ void __launch_bounds__(kThreads) set_loss_fwd_kernel(ov3d_set_loss_desc d, float* raw,
+                                                                 int* ticket, float* dict_out,
+                                                                 float* total) {
+    const int l = blockIdx.x;
+    const int P = d.B * d.Q;
+    __shared__ int cnt[OV3D_LOSS_MAX_B];
+    __shared__ double red[kThreads / 64][7];
+    __shared__ int is_last;
+    for (int b = threadIdx.x; b < d.B; b += kThreads) cnt[b] = 0;
+    __syncthreads();
+
+    double acc[7] = {0, 0, 0, 0, 0, 0, 0};   // sem num, sem den, acls, areg, center, size, giou
+    for (int p = threadIdx.x; p < P; p += kThreads) {
+        const int b = p / d.Q;
+        const long long row = (long long)l * P + p;
+        const float m = d.matched[row];
+        const int g = clampi(d.inds[row], d.G - 1);
+        const long long bg = (long long)b * d.G + g;
+
+        const float* x = d.logits + row * d.ld_logits;
+        float mx, s;
+        int am;
+        softmax_stats(x, d.T, mx, am, s);
+        if (am != d.T - 1) atomicAdd(&cnt[b], 1);
+        if (d.flags & OV3D_LOSS_SEM) {
+            const int lab = (m == 0.f) ? d.T - 1 : clampi(d.gt_sem[bg], d.T - 1);
+            const float nll = logf(s) - (x[lab] - mx);
+            const float wt = d.cls_weights[lab];
+            acc[0] += (double)(nll * wt);
+            acc[1] += (double)wt;
+        }
+        {
+            const float* a = d.angle_logits + row * d.ld_angle_logits;
+            float ma, sa;
+            int ia;
+            softmax_stats(a, d.NB, ma, ia, sa);
+            const int gl = clampi(d.gt_angle_cls[bg], d.NB - 1);
+            acc[2] += (double)((logf(sa) - (a[gl] - ma)) * m);
+            const float gr = d.gt_angle_res[bg] * d.res_scale;
+            const float e = d.angle_res[row * d.ld_angle_res + gl] - gr;
+            acc[3] += (double)(huber(e) * m);
+        }
+        if (d.flags & OV3D_LOSS_CENTER) {
+            const float* c = d.center + row * d.ld_center;
+            const float* gc = d.gt_center + bg * 3;
+            const float cl = (fabsf(c[0] - gc[0]) + fabsf(c[1] - gc[1])) + fabsf(c[2] - gc[2]);
+            acc[4] += (double)(cl * m);
+        }
+        if (d.flags & OV3D_LOSS_SIZE) {
+            const float* z = d.size + row * d.ld_size;
+            const float* gz = d.gt_size + bg * 3;
+            const float sl = (fabsf(z[0] - gz[0]) + fabsf(z[1] - gz[1])) + fabsf(z[2] - gz[2]);
+            acc[5] += (double)(sl * m);
+        }
+        if (d.flags & OV3D_LOSS_GIOU) {
+            acc[6] += (double)((1.f - d.gious[row * d.G + g]) * m);
+        }
+    }
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        const double v = wave_sum(acc[k]);
+        if (lane == 0) red[w][k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t[7];
+        for (int k = 0; k < 7; ++k) {
+            t[k] = 0;
+            for (int j = 0; j < kThreads / 64; ++j) t[k] += red[j][k];
+        }
+        const float nb = *d.num_boxes;
+        float* r = raw + (long long)l * kRaw;
+        r[0] = (d.flags & OV3D_LOSS_SEM) ? (float)t[0] / (float)t[1] : 0.f;
+        r[1] = (float)t[2] / nb;
+        r[2] = (float)t[3] / nb;
+        r[3] = (d.flags & OV3D_LOSS_CENTER) ? (float)t[4] / nb : 0.f;
+        r[4] = (d.flags & OV3D_LOSS_SIZE) ? (float)t[5] / nb : 0.f;
+        r[5] = (d.flags & OV3D_LOSS_GIOU) ? (float)t[6] / nb : 0.f;
+        r[6] = (d.flags & OV3D_LOSS_ALIGN) ? d.align[l] : 0.f;
+        float card = 0.f;
+        for (int b = 0; b < d.B; ++b) card += fabsf((float)cnt[b] - (float)d.nactual[b]);
+        r[7] = card / (float)d.B;
+        r[8] = (float)t[1];
+        __threadfence();
+        is_last = (atomicAdd(ticket, 1) == d.L - 1);
+    }
+    __syncthreads();
+    if (!is_last || threadIdx.x != 0) return;
+    __threadfence();
+    float tot = 0.f;
+    for (int i = 0; i < d.L; ++i) {
+        const float* r = raw + (long long)layer_at(d, i) * kRaw;
+        for (int k = 0; k < kCols; ++k) dict_out[i * kCols + k] = r[k] * d.dict_w[k];
+        float ll = 0.f;
+        for (int j = 0; j < d.n_total; ++j) {
+            const int k = d.total_order[j];
+            ll = (j == 0) ? r[k] * d.dict_w[k] : ll + r[k] * d.dict_w[k];
+        }
+        tot = (i == 0) ? ll : tot + ll;
+    }
+    *total = tot;
+    *ticket = 0;
+}
+
+__global__ void __launch_bounds__(kThreads) set_loss_bwd_kernel(
+    ov3d_set_loss_desc d, const float* raw, const float* d_dict, const float* d_total,
+    float* g_logits, float* g_alog, float* g_ares, float* g_center, float* g_size, float* g_gious,
+    float* g_align) {
+    const int P = d.B * d.Q;
+    const long long row = (long long)blockIdx.x * kThreads + threadIdx.x;
+    const float dt = d_total ? *d_total : 0.f;
+    if (blockIdx.x == 0 && threadIdx.x < d.L && g_align) {
+        const int l = threadIdx.x;
+        const float dd = d_dict ? d_dict[dict_pos(d, l) * kCols + 6] : 0.f;
+        g_align[l] = d.dict_w[6] * dd + d.total_w[6] * dt;
+    }
+    if (row >= (long long)d.L * P) return;
+    const int l = (int)(row / P);
+    const int b = (int)((row % P) / d.Q);
+    const int i = dict_pos(d, l);
+    float c[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        c[k] = d.dict_w[k] * (d_dict ? d_dict[i * kCols + k] : 0.f) + d.total_w[k] * dt;
+    const float nb = *d.num_boxes;
+    const float m = d.matched[row];
+    const int g = clampi(d.inds[row], d.G - 1);
+    const long long bg = (long long)b * d.G + g;
+
+    if (g_logits) {
+        const float* x = d.logits + row * d.ld_logits;
+        float* gx = g_logits + row * d.T;
+        float mx, s;
+        int am;
+        softmax_stats(x, d.T, mx, am, s);
+        const int lab = (m == 0.f) ? d.T - 1 : clampi(d.gt_sem[bg], d.T - 1);
+        const float den = raw[(long long)l * kRaw + 8];
+        const float gn = (c[0] / den) * d.cls_weights[lab];
+        const float inv = 1.f / s;
+        for (int t = 0; t < d.T; ++t)
+            gx[t] = gn * (expf(x[t] - mx) * inv - (t == lab ? 1.f : 0.f));
+    }
+    const float* a = d.angle_logits + row * d.ld_angle_logits;
+    const int gl = clampi(d.gt_angle_cls[bg], d.NB - 1);
+    if (g_alog) {
+        float ma, sa;
+        int ia;
+        softmax_stats(a, d.NB, ma, ia, sa);
+        const float gce = (c[1] / nb) * m;
+        const float inv = 1.f / sa;
+        float* ga = g_alog + row * d.NB;
+        for (int t = 0; t < d.NB; ++t) ga[t] = gce * (expf(a[t] - ma) * inv - (t == gl ? 1.f : 0.f));
+    }
+    if (g_ares) {
+        const float gr = d.gt_angle_res[bg] * d.res_scale;
+        const float e = d.angle_res[row * d.ld_angle_res + gl] - gr;
+        const float gh = (c[2] / nb) * m * (sgnf(e) * fminf(fabsf(e), 1.f));
+        float* ga = g_ares + row * d.NB;
+        for (int t = 0; t < d.NB; ++t) ga[t] = (t == gl) ? gh : 0.f;
+    }
+    if (g_center) {
+        const float* cc = d.center + row * d.ld_center;
+        const float* gc = d.gt_center + bg * 3;
+        const float gk = (c[3] / nb) * m;
+        for (int j = 0; j < 3; ++j) g_center[row * 3 + j] = gk * sgnf(cc[j] - gc[j]);
+    }
+    if (g_size) {
+        const float* z = d.size + row * d.ld_size;
+        const float* gz = d.gt_size + bg * 3;
+        const float gk = (c[4] / nb) * m;
+        for (int j = 0; j < 3; ++j) g_size[row * 3 + j] = gk * sgnf(z[j] - gz[j]);
+    }
+    if (g_gious) {
+        const float gk = -(c[5] / nb) * m;
+        float* gg = g_gious + row * d.G;
+        for (int j = 0; j < d.G; ++j) gg[j] = (j == g) ? gk : 0.f;
+    }
+}
+
+int check_desc(const ov3d_set_loss_desc* d) {
+    if (!d || d->L <= 0 || d->B <= 0 || d->Q <= 0 || d->G <= 0 || d->T < 1 || d->NB < 1 ||
+        d->B > OV3D_LOSS_MAX_B || !d->logits || !d->angle_logits || !d->angle_res || !d->inds ||
+        !d->matched || !d->gt_angle_cls || !d->gt_angle_res || !d->nactual || !d->num_boxes ||
+        d->ld_logits < d->T || d->ld_angle_logits < d->NB || d->ld_angle_res < d->NB ||
+        d->n_total < 0 || d->n_total > kCols)
+        return OV3D_EINVAL;
+    if ((d->flags & OV3D_LOSS_SEM) && (!d->gt_sem || !d->cls_weights)) return OV3D_EINVAL;
+    if ((d->flags & OV3D_LOSS_CENTER) && (!d->center || !d->gt_center || d->ld_center < 3))
+        return OV3D_EINVAL;
+    if ((d->flags & OV3D_LOSS_SIZE) && (!d->size || !d->gt_size || d->ld_size < 3))
+        return OV3D_EINVAL;
+    if ((d->flags & OV3D_LOSS_GIOU) && !d->gious) return OV3D_EINVAL;
+    if ((d->flags & OV3D_LOSS_ALIGN) && !d->align) return OV3D_EINVAL;
+    for (int j = 0; j < d->n_total; ++j)
+        if (d->total_order[j] < 0 || d->total_order[j] >= kCols - 1) return OV3D_EINVAL;
+    return OV3D_OK;
+}
+
+}  // namespace
+
+extern "C" long long ov3d_set_loss_desc_size(void) { return (long long)sizeof(ov3d_set_loss_desc); }
+
+extern "C" int ov3d_set_loss_fwd(const ov3d_set_loss_desc* desc, float* raw, int* ticket,
+                                 float* dict_out, float* total, void* stream) {
+    if (check_desc(desc) != OV3D_OK || !raw || !ticket || !dict_out || !total) return OV3D_EINVAL;
+    set_loss_fwd_kernel<<<desc->L, kThreads, 0, ov3d_stream(stream)>>>(*desc, raw, ticket, dict_out,
+                                                                       total);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_set_loss_bwd(const ov3d_set_loss_desc* desc, const float* raw,
+                                 const float* d_dict, const float* d_total, float* g_logits,
+                                 float* g_angle_logits, float* g_angle_res, float* g_center,
+                                 float* g_size, float* g_gious, float* g_align, void* stream) {
+    if (check_desc(desc) != OV3D_OK || !raw || desc->L > kThreads) return OV3D_EINVAL;
+    const ov3d_set_loss_desc& d = *desc;
+    if ((g_logits && !(d.flags & OV3D_LOSS_SEM)) || (g_center && !(d.flags & OV3D_LOSS_CENTER)) ||
+        (g_size && !(d.flags & OV3D_LOSS_SIZE)) || (g_gious && !(d.flags & OV3D_LOSS_GIOU)) ||
+        (g_align && !(d.flags & OV3D_LOSS_ALIGN)))
+        return OV3D_EINVAL;
+    const long long rows = (long long)d.L * d.B * d.Q;
+    set_loss_bwd_kernel<<<ov3d_cdiv(rows, kThreads), kThreads, 0, ov3d_stream(stream)>>>(
+        d, raw, d_dict, d_total, g_logits, g_angle_logits, g_angle_res, g_center, g_size, g_gious,
+        g_align);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
