@@ -340,6 +340,30 @@ int ov3d_set_loss_bwd(const ov3d_set_loss_desc* desc, const float* raw, const fl
                       float* g_angle_res, float* g_center, float* g_size, float* g_gious,
                       float* g_align, void* stream);
 
+
+/* ---- Residual add + dropout + LayerNorm (pre-norm transformer layers) ----
+ * Replaces models/transformer.py:262-280 / 355-379 `x = x + dropout(branch)` followed by the
+ * next sub-layer's `norm(x)` (+ pos), and the decoder's per-layer final norm (124-133).
+ * Contiguous (R, C) rows, C/8 a power of two <= 64.  Dropout: hash of (*seed, site, r, c).
+ *   s = src + dropout(y) (fp32); xa = bf16(LN_a(s)); xap = bf16(LN_a(s) + pos); xb = LN_b(s) (fp32)
+ * src / y / pos may be NULL (zero / absent); outputs NULL = not wanted. */
+int ov3d_resnorm_supported(int C);
+int ov3d_resnorm_fwd(long long R, int C, const void* src, int src_bf16, const void* y, int y_bf16,
+                     float dropout_p, const int64_t* seed, int site, const float* ga,
+                     const float* ba, const void* pos, int pos_bf16, const float* gb,
+                     const float* bb, float eps, float* s, float* mean, float* rstd, void* xa,
+                     void* xap, float* xb, void* stream);
+/* backward: ds (fp32, grad of s from its other consumers) or NULL, dxa / dxap (bf16),
+ * dxb (fp32) or NULL -> dsrc (fp32), dy (bf16 | fp32), dpos (= dxap), dga/dba/dgb/dbb.
+ * partials: (nparts, 4, C) f32 workspace with nparts = ov3d_resnorm_bwd_parts(R, C). */
+int ov3d_resnorm_bwd_parts(long long R, int C);
+int ov3d_resnorm_bwd(long long R, int C, const float* s, const float* mean, const float* rstd,
+                     const float* ds, const void* dxa, const void* dxap, const float* dxb,
+                     const float* ga, const float* gb, float dropout_p, const int64_t* seed,
+                     int site, float* dsrc, void* dy, int dy_bf16, void* dpos, int dpos_bf16,
+                     float* partials, int nparts, float* dga, float* dba, float* dgb, float* dbb,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

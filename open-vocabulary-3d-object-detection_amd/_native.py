@@ -53,9 +53,12 @@ _SIGS = {
     "ov3d_rows_bn_bwd": "ipllipillilipppppppfpipipllip",
     "ov3d_set_loss_fwd": "pppppp",
     "ov3d_set_loss_bwd": "pppppppppppp",
+    "ov3d_resnorm_fwd": "lipipifpipppippfppppppp",
+    "ov3d_resnorm_bwd": "lipppppppppfpippipipippppp",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
-                          "ov3d_wgrad_workspace", "ov3d_wgrad_tiles", "ov3d_set_loss_desc_size")
+                          "ov3d_wgrad_workspace", "ov3d_wgrad_tiles", "ov3d_set_loss_desc_size",
+                          "ov3d_resnorm_supported", "ov3d_resnorm_bwd_parts")
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_longlong, "f": ctypes.c_float,
        "d": ctypes.c_double}
@@ -88,6 +91,10 @@ def load():
         lib.ov3d_wgrad_tiles.restype = ctypes.c_int
         lib.ov3d_set_loss_desc_size.argtypes = []
         lib.ov3d_set_loss_desc_size.restype = ctypes.c_longlong
+        lib.ov3d_resnorm_supported.argtypes = [ctypes.c_int]
+        lib.ov3d_resnorm_supported.restype = ctypes.c_int
+        lib.ov3d_resnorm_bwd_parts.argtypes = [ctypes.c_longlong, ctypes.c_int]
+        lib.ov3d_resnorm_bwd_parts.restype = ctypes.c_int
         lib.ov3d_version.argtypes = []
         lib.ov3d_version.restype = ctypes.c_char_p
         _lib = lib

@@ -17,6 +17,7 @@
 // Dropout keep(r, c) is a counter-based hash of (seed, site, r, c): the backward
 // regenerates the mask instead of storing it.
 #include "common.h"
+#include "rowdrop.h"
 
 namespace {
 
@@ -32,34 +33,9 @@ __device__ __forceinline__ long long addr(const RowsLayout& L, long long r, int 
     return (long long)(c / L.cb) * L.bstride + r * L.ld + (c % L.cb);
 }
 
-__device__ __forceinline__ uint32_t mix32(uint32_t x) {
-    x ^= x >> 16;
-    x *= 0x7feb352du;
-    x ^= x >> 15;
-    x *= 0x846ca68bu;
-    x ^= x >> 16;
-    return x;
-}
-__device__ __forceinline__ uint32_t mix24(uint32_t x) {
-    x ^= x >> 16;
-    x = __umul24(x, 0x7feb35u) ^ (x >> 24);
-    x ^= x >> 15;
-    x = __umul24(x, 0x846ca7u) ^ (x >> 24);
-    x ^= x >> 16;
-    return x;
-}
-__device__ __forceinline__ uint32_t row_base(uint32_t seedmix, long long r) {
-    return mix32(seedmix ^ ((uint32_t)r * 0xC2B2AE35u));
-}
-// keep decisions of channels c..c+7 of row r: 4 hashes, two 16-bit halves each
-__device__ __forceinline__ void keep8(uint32_t rowbase, int c, uint32_t thresh, bool* keep) {
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-        const uint32_t h = mix24(rowbase + (uint32_t)((c + j) >> 1) * 0x27D4EB2Fu);
-        keep[j] = (h & 0xffffu) >= thresh;
-        keep[j + 1] = (h >> 16) >= thresh;
-    }
-}
+using rowdrop::keep8;
+using rowdrop::mix32;
+using rowdrop::row_base;
 
 // rows-per-thread phase layout: TP threads per row (one per 8-channel run), RP rows at once
 struct Phase {
@@ -230,9 +206,7 @@ __global__ void __launch_bounds__(256) rows_bn_bwd_kernel(
     }
 }
 
-uint32_t drop_thresh(float p) {
-    return p > 0.f ? (uint32_t)fminf(rintf(p * 65536.0f), 65535.0f) : 0u;
-}
+uint32_t drop_thresh(float p) { return rowdrop::thresh(p); }
 
 bool layout_ok(const RowsLayout& L, int C) {
     return L.cb > 0 && L.cb % 8 == 0 && C % L.cb == 0 && L.ld >= L.cb && L.ld % 8 == 0 &&

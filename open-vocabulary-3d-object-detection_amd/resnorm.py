@@ -1,0 +1,164 @@
+"""Residual add + dropout + LayerNorm of the pre-norm transformer layers as one HIP
+launch each way (csrc/resnorm.hip, ``ov3d_resnorm_fwd`` / ``ov3d_resnorm_bwd``).
+
+Reference: models/transformer.py — every pre-norm sub-layer ends with
+``x = x + dropout(branch)`` (forward_pre, 262-280 / 355-379), the next starts with
+``norm(x)`` (+ ``pos`` / ``query_pos`` for the attention inputs), and the decoder applies
+its final norm to every layer output (return_intermediate, 124-133).  A ``Pending``
+residual (stream value, branch output not yet added, its dropout) is carried from one
+sub-layer to the next and resolved inside the next norm's launch:
+
+    s, xa, xap, xb = resnorm(Pending(src, y, p, site), norm_a, pos, norm_b)
+    s   = src + dropout_p(y)           (fp32)
+    xa  = bf16(norm_a(s)),  xap = bf16(norm_a(s) + pos),  xb = norm_b(s) (fp32)
+
+Dropout keep masks are the counter hash of csrc/rowdrop.h (seed of attention.py, one
+site per call site), regenerated in the backward.  Under bf16 autocast only: the fp32
+path keeps the plain module code, which is what the parity tests compare against.
+"""
+from collections import namedtuple
+
+import torch
+from torch import nn
+
+from . import _native
+from . import attention as flash
+
+Pending = namedtuple("Pending", "src y p site")
+
+enabled = True   # False: the plain module code under autocast as well (tests compare the two)
+
+
+def supported(x, *norms):
+    C = x.shape[-1]
+    if not (enabled and x.is_cuda and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        return False
+    if not _native.load().ov3d_resnorm_supported(C):
+        return False
+    eps = None
+    for n in norms:
+        if n is None:
+            continue
+        if type(n) is not nn.LayerNorm or not n.elementwise_affine or n.bias is None or \
+                tuple(n.normalized_shape) != (C,):
+            return False
+        if eps is not None and n.eps != eps:
+            return False
+        eps = n.eps
+    return True
+
+
+def _dt_flag(t):
+    if t is None:
+        return 0
+    if t.dtype == torch.bfloat16:
+        return 1
+    if t.dtype == torch.float32:
+        return 0
+    raise TypeError(f"resnorm: unsupported dtype {t.dtype}")
+
+
+def _rows(t, C):
+    if t is None:
+        return None
+    if t.dtype not in (torch.float32, torch.bfloat16):
+        t = t.float()
+    return t.reshape(-1, C).contiguous()
+
+
+class _ResNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, meta, src, y, pos, ga, ba, gb, bb):
+        p, site, want_a, want_ap, want_b, eps, shape = meta
+        C = shape[-1]
+        srcr, yr, posr = _rows(src, C), _rows(y, C), _rows(pos, C)
+        R = 1
+        for d in shape[:-1]:
+            R *= d
+        dev = next(t.device for t in (srcr, yr, ga, gb) if t is not None)
+        s = torch.empty((R, C), dtype=torch.float32, device=dev)
+        norm = want_a or want_ap or want_b
+        mean = torch.empty(R, dtype=torch.float32, device=dev) if norm else None
+        rstd = torch.empty(R, dtype=torch.float32, device=dev) if norm else None
+        xa = torch.empty((R, C), dtype=torch.bfloat16, device=dev) if want_a else None
+        xap = torch.empty((R, C), dtype=torch.bfloat16, device=dev) if want_ap else None
+        xb = torch.empty((R, C), dtype=torch.float32, device=dev) if want_b else None
+        seed = flash._seed(dev) if p > 0 else None
+        _native.call("ov3d_resnorm_fwd", R, C, srcr, _dt_flag(srcr), yr, _dt_flag(yr), float(p),
+                     seed, site, ga, ba, posr, _dt_flag(posr), gb, bb, float(eps), s, mean, rstd,
+                     xa, xap, xb, like=s)
+        ctx.save_for_backward(s, mean, rstd, ga, gb)
+        ctx.meta = (p, site, R, C, shape, src.dtype if src is not None else None,
+                    y.dtype if y is not None else None, pos.dtype if pos is not None else None)
+        v = lambda t: t.view(shape) if t is not None else None   # noqa: E731
+        return v(s), v(xa), v(xap), v(xb)
+
+    @staticmethod
+    def backward(ctx, ds, dxa, dxap, dxb):
+        p, site, R, C, shape, src_dt, y_dt, pos_dt = ctx.meta
+        s, mean, rstd, ga, gb = ctx.saved_tensors
+        need = ctx.needs_input_grad   # meta, src, y, pos, ga, ba, gb, bb
+        dev = s.device
+
+        def g(t, dt):
+            return t.reshape(R, C).to(dt).contiguous() if t is not None else None
+
+        ds, dxa, dxap, dxb = (g(ds, torch.float32), g(dxa, torch.bfloat16),
+                              g(dxap, torch.bfloat16), g(dxb, torch.float32))
+        if ga is None:
+            dxa = dxap = None
+        if gb is None:
+            dxb = None
+        dsrc = torch.empty((R, C), dtype=torch.float32, device=dev) if need[1] else None
+        dy = torch.empty((R, C), dtype=y_dt, device=dev) if need[2] else None
+        dpos = torch.empty((R, C), dtype=pos_dt, device=dev) if (need[3] and dxap is not None) else None
+        has_a = dxa is not None or dxap is not None
+        has_b = dxb is not None
+        dga = torch.empty(C, dtype=torch.float32, device=dev) if (need[4] and has_a) else None
+        dba = torch.empty(C, dtype=torch.float32, device=dev) if (need[5] and has_a) else None
+        dgb = torch.empty(C, dtype=torch.float32, device=dev) if (need[6] and has_b) else None
+        dbb = torch.empty(C, dtype=torch.float32, device=dev) if (need[7] and has_b) else None
+        lib = _native.load()
+        nparts = lib.ov3d_resnorm_bwd_parts(R, C)
+        partials = torch.empty((nparts, 4, C), dtype=torch.float32, device=dev) \
+            if (has_a or has_b) else None
+        seed = flash._seed(dev) if (p > 0 and dy is not None) else None
+        if dsrc is not None or dy is not None or dpos is not None or has_a or has_b:
+            _native.call("ov3d_resnorm_bwd", R, C, s, mean, rstd, ds, dxa, dxap, dxb, ga, gb,
+                         float(p) if dy is not None else 0.0, seed, site, dsrc, dy, _dt_flag(dy),
+                         dpos, _dt_flag(dpos), partials, nparts, dga, dba,
+                         dgb, dbb, like=s)
+        v = lambda t: t.view(shape) if t is not None else None   # noqa: E731
+        if dsrc is not None and src_dt != torch.float32:
+            dsrc = dsrc.to(src_dt)
+        return None, v(dsrc), v(dy), v(dpos), dga, dba, dgb, dbb
+
+
+def resnorm(pend, norm_a=None, pos=None, want_a=True, want_ap=False, norm_b=None):
+    """-> (s, xa, xap, xb) for Pending(src, y, p, site); unwanted outputs are None."""
+    src, y, p, psite = pend
+    ref = y if y is not None else src
+    shape = tuple(ref.shape)
+    if norm_a is None:
+        want_a = want_ap = False
+    if want_ap and pos is None:
+        raise ValueError("resnorm: xap needs pos")
+    eps = (norm_a.eps if norm_a is not None else (norm_b.eps if norm_b is not None else 1e-5))
+    meta = (float(p) if y is not None else 0.0, int(psite), bool(want_a), bool(want_ap),
+            norm_b is not None, eps, shape)
+    ga = norm_a.weight if norm_a is not None else None
+    ba = norm_a.bias if norm_a is not None else None
+    gb = norm_b.weight if norm_b is not None else None
+    bb = norm_b.bias if norm_b is not None else None
+    with torch.autocast("cuda", enabled=False):
+        return _ResNorm.apply(meta, src, y, pos if want_ap else None, ga, ba, gb, bb)
+
+
+def sites(module, n):
+    """n dropout hash sites owned by `module` (allocated once)"""
+    s = getattr(module, "_resnorm_sites", None)
+    if s is None:
+        s = tuple(flash.new_site() for _ in range(n))
+        module._resnorm_sites = s
+    return s

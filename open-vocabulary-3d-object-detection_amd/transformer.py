@@ -18,6 +18,7 @@ import torch.nn.functional as F
 from torch import Tensor, nn
 
 from . import attention as flash
+from . import resnorm as rn
 from .gemm import in_projection, rows_linear
 from .helpers import ACTIVATION_DICT, NORM_DICT, get_clones
 
@@ -108,6 +109,22 @@ class TransformerEncoderLayer(nn.Module):
             src = src + self.dropout2(rows_linear(h, self.linear2.weight, self.linear2.bias))
         return src
 
+    def forward_fused(self, pend, src_mask=None, pos=None):
+        """bf16 training / eval step on a Pending residual (resnorm.py); -> Pending."""
+        p1, p2 = (self.dropout1.p, self.dropout2.p) if self.training else (0.0, 0.0)
+        site1, site2 = rn.sites(self, 2)
+        s, x, xp, _ = rn.resnorm(pend, self.norm1, pos=pos, want_a=True, want_ap=pos is not None)
+        qk = xp if pos is not None else x
+        y = self.self_attn(qk, qk, x, attn_mask=src_mask)
+        if not self.use_ffn:
+            return rn.Pending(s, y, p1, site1)
+        s, x, _, _ = rn.resnorm(rn.Pending(s, y, p1, site1), self.norm2)
+        h = self.dropout(self.activation(rows_linear(x, self.linear1.weight, self.linear1.bias)))
+        return rn.Pending(s, rows_linear(h, self.linear2.weight, self.linear2.bias), p2, site2)
+
+    def fused_ok(self, x):
+        return rn.supported(x, self.norm1, self.norm2 if self.use_ffn else None)
+
 
 class TransformerDecoderLayer(nn.Module):
     def __init__(self, d_model, nhead=4, dim_feedforward=256, dropout=0.1, dropout_attn=None,
@@ -147,6 +164,26 @@ class TransformerDecoderLayer(nn.Module):
         tgt = tgt + self.dropout3(rows_linear(h, self.linear2.weight, self.linear2.bias))
         return tgt, None
 
+    def forward_fused(self, s, x, xp, memory, memory_pos, query_pos=None, tgt_mask=None,
+                      memory_mask=None):
+        """bf16 step from norm1's outputs (x = norm1(tgt), xp = x + query_pos) -> Pending of
+        the layer output (resnorm.py)."""
+        p1, p2, p3 = ((self.dropout1.p, self.dropout2.p, self.dropout3.p) if self.training
+                      else (0.0, 0.0, 0.0))
+        site1, site2, site3 = rn.sites(self, 3)
+        qk = xp if query_pos is not None else x
+        y = self.self_attn(qk, qk, x, attn_mask=tgt_mask)
+        s, x2, q, _ = rn.resnorm(rn.Pending(s, y, p1, site1), self.norm2, pos=query_pos,
+                                 want_a=query_pos is None, want_ap=query_pos is not None)
+        y = self.multihead_attn(q if query_pos is not None else x2, memory_pos, memory,
+                                attn_mask=memory_mask)
+        s, x3, _, _ = rn.resnorm(rn.Pending(s, y, p2, site2), self.norm3)
+        h = self.dropout(self.activation(rows_linear(x3, self.linear1.weight, self.linear1.bias)))
+        return rn.Pending(s, rows_linear(h, self.linear2.weight, self.linear2.bias), p3, site3)
+
+    def fused_ok(self, x):
+        return rn.supported(x, self.norm1, self.norm2, self.norm3)
+
 
 class TransformerEncoder(nn.Module):
     def __init__(self, encoder_layer, num_layers, norm=None, weight_init_name="xavier_uniform"):
@@ -163,15 +200,35 @@ class TransformerEncoder(nn.Module):
         if transpose_swap:
             raise NotImplementedError
         masks = mask if isinstance(mask, list) else [mask] * len(self.layers)
+        masks = [self._head_mask(m, layer) for layer, m in zip(self.layers, masks)]
+        if self._fused_ok(src):
+            pend = rn.Pending(src, None, 0.0, 0)
+            for layer, m in zip(self.layers, masks):
+                pend = layer.forward_fused(pend, src_mask=m, pos=pos)
+            return xyz, self._finish_fused(pend), None
         out = src
         for layer, m in zip(self.layers, masks):
-            if m is not None:
-                bsz, n, _ = m.shape
-                m = m.unsqueeze(1).expand(bsz, layer.nhead, n, n).reshape(bsz * layer.nhead, n, n)
             out = layer(out, src_mask=m, pos=pos)
         if self.norm is not None:
             out = self.norm(out)
         return xyz, out, None
+
+    @staticmethod
+    def _head_mask(m, layer):
+        if m is None:
+            return None
+        bsz, n, _ = m.shape
+        return m.unsqueeze(1).expand(bsz, layer.nhead, n, n).reshape(bsz * layer.nhead, n, n)
+
+    def _fused_ok(self, x):
+        """HIP residual + LayerNorm launches (resnorm.py) under bf16 autocast"""
+        return (all(hasattr(l, "fused_ok") and l.fused_ok(x) for l in self.layers)
+                and (self.norm is None or rn.supported(x, self.norm)))
+
+    def _finish_fused(self, pend):
+        """the encoder output (fp32): last residual add (+ the encoder norm)"""
+        s, _, _, xb = rn.resnorm(pend, norm_b=self.norm)
+        return xb if self.norm is not None else s
 
 
 class MaskedTransformerEncoder(TransformerEncoder):
@@ -197,16 +254,25 @@ class MaskedTransformerEncoder(TransformerEncoder):
         out = src
         xyz_dist = None
         xyz_inds = None
+        fused = self._fused_ok(src)
+        pend = rn.Pending(src, None, 0.0, 0)
         for idx, layer in enumerate(self.layers):
             m = None
             if self.masking_radius[idx] > 0:
                 m, xyz_dist = self.compute_mask(xyz, self.masking_radius[idx], xyz_dist)
-                bsz, n, _ = m.shape
-                m = m.unsqueeze(1).expand(bsz, layer.nhead, n, n).reshape(bsz * layer.nhead, n, n)
-            out = layer(out, src_mask=m, pos=pos)
+                m = self._head_mask(m, layer)
+            if fused:
+                pend = layer.forward_fused(pend, src_mask=m, pos=pos)
+            else:
+                out = layer(out, src_mask=m, pos=pos)
             if idx == 0 and self.interim_downsampling:
+                if fused:
+                    out = rn.resnorm(pend)[0]
                 xyz, feats, xyz_inds = self.interim_downsampling(xyz, out.permute(1, 2, 0))
                 out = feats.permute(2, 0, 1)
+                pend = rn.Pending(out, None, 0.0, 0)
+        if fused:
+            return xyz, self._finish_fused(pend), xyz_inds
         if self.norm is not None:
             out = self.norm(out)
         return xyz, out, xyz_inds
@@ -231,6 +297,9 @@ class TransformerDecoder(nn.Module):
         if transpose_swap or return_attn_weights:
             raise NotImplementedError
         memory_pos = memory if pos is None else memory + pos
+        if all(hasattr(l, "fused_ok") and l.fused_ok(tgt) for l in self.layers) and \
+                (self.norm is None or rn.supported(tgt, self.norm)):
+            return self._forward_fused(tgt, memory, memory_pos, query_pos, tgt_mask, memory_mask)
         out = tgt
         inter = []
         for layer in self.layers:
@@ -243,5 +312,31 @@ class TransformerDecoder(nn.Module):
             if self.return_intermediate:
                 inter[-1] = out
         if self.return_intermediate:
+            return torch.stack(inter), []
+        return out, []
+
+    def _forward_fused(self, tgt, memory, memory_pos, query_pos, tgt_mask, memory_mask):
+        """bf16: one resnorm launch per sub-layer boundary; the decoder norm of layer i's
+        output shares the launch with layer i+1's norm1 (same row statistics)."""
+        # K / V projection inputs are cast to bf16 once for the 8 layers
+        memory = memory.to(torch.bfloat16)
+        memory_pos = memory_pos.to(torch.bfloat16)
+        pend = rn.Pending(tgt, None, 0.0, 0)
+        inter = []
+        dec_norm = self.norm if self.return_intermediate else None
+        for i, layer in enumerate(self.layers):
+            s, x, xp, xd = rn.resnorm(pend, layer.norm1, pos=query_pos, want_a=True,
+                                      want_ap=query_pos is not None,
+                                      norm_b=dec_norm if i > 0 else None)
+            if i > 0 and dec_norm is not None:
+                inter.append(xd)
+            pend = layer.forward_fused(s, x, xp, memory, memory_pos, query_pos, tgt_mask,
+                                       memory_mask)
+        s, _, _, xd = rn.resnorm(pend, norm_b=self.norm)
+        out = xd if self.norm is not None else s
+        if self.return_intermediate:
+            if self.norm is None:
+                raise NotImplementedError("return_intermediate without a decoder norm")
+            inter.append(out)
             return torch.stack(inter), []
         return out, []

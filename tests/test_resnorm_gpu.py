@@ -1,0 +1,149 @@
+"""Residual + dropout + LayerNorm launches (csrc/resnorm.hip, resnorm.py) against a plain
+PyTorch fp32 restatement with the same keep mask (rebuilt from the documented row hash,
+csrc/rowdrop.h): outputs and every gradient.  Then the bf16 encoder / decoder with the
+fused launches against the same modules on the plain torch code (dropout 0)."""
+import numpy as np
+import pytest
+import torch
+
+from helpers import ov3d  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+M32 = 0xFFFFFFFF
+
+
+def _mix32(x):
+    x = x & M32
+    x = x ^ (x >> 16)
+    x = (x * 0x7feb352d) & M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846ca68b) & M32
+    x = x ^ (x >> 16)
+    return x
+
+
+def _umul24(x, c):
+    return ((x & 0xFFFFFF) * (c & 0xFFFFFF)) & M32
+
+
+def _mix24(x):
+    x = x & M32
+    x = x ^ (x >> 16)
+    x = _umul24(x, 0x7feb35) ^ (x >> 24)
+    x = x ^ (x >> 15)
+    x = _umul24(x, 0x846ca7) ^ (x >> 24)
+    x = x ^ (x >> 16)
+    return x
+
+
+def row_keep(seed, site, R, C, p, device):
+    """rowdrop.h keep(r, c) in int64 torch arithmetic"""
+    s = int(seed)
+    lo, hi = s & M32, (s >> 32) & M32
+    sm = _mix32(torch.tensor(lo, dtype=torch.int64, device=device)
+                ^ _mix32(torch.tensor((hi + site * 0x9E3779B9) & M32, dtype=torch.int64, device=device)))
+    r = torch.arange(R, dtype=torch.int64, device=device)
+    rb = _mix32(sm ^ ((r * 0xC2B2AE35) & M32))                                   # (R,)
+    c = torch.arange(C, dtype=torch.int64, device=device)
+    h = _mix24(rb[:, None] + (((c[None] >> 1) * 0x27D4EB2F) & M32))
+    half = torch.where((c & 1).bool()[None], h >> 16, h & 0xFFFF)
+    th = min(int(np.rint(np.float32(p) * np.float32(65536.0))), 65535) if p > 0 else 0
+    return half >= th
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("R,C,p,src_bf16", [(1024, 256, 0.1, False), (16384, 256, 0.0, False),
+                                            (3000, 128, 0.3, True), (64, 512, 0.1, False)])
+def test_resnorm_matches_torch(cuda, R, C, p, src_bf16):
+    from ov3d_amd import attention as flash
+    from ov3d_amd import resnorm as rn
+    torch.manual_seed(0)
+    na = torch.nn.LayerNorm(C).to(cuda)
+    nb = torch.nn.LayerNorm(C).to(cuda)
+    with torch.no_grad():
+        for n in (na, nb):
+            n.weight.copy_(1 + 0.1 * torch.randn(C))
+            n.bias.copy_(0.1 * torch.randn(C))
+    src = torch.randn(R, 1, C, device=cuda)
+    if src_bf16:
+        src = src.bfloat16()
+    src.requires_grad_()
+    y = torch.randn(R, 1, C, device=cuda).bfloat16().requires_grad_()
+    pos = torch.randn(R, 1, C, device=cuda).requires_grad_()
+    site = flash.new_site()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        s, xa, xap, xb = rn.resnorm(rn.Pending(src, y, p, site), na, pos=pos, want_a=True,
+                                    want_ap=True, norm_b=nb)
+    g = [torch.randn_like(t) for t in (s, xa, xap, xb)]
+    torch.autograd.backward((s, xa, xap, xb), g)
+    fused = [t.grad.clone() for t in (src, y, pos)] + [na.weight.grad.clone(), na.bias.grad.clone(),
+                                                       nb.weight.grad.clone(), nb.bias.grad.clone()]
+    for t in (src, y, pos, na.weight, na.bias, nb.weight, nb.bias):
+        t.grad = None
+    # fp32 restatement with the same mask and torch's bf16 dropout rounding
+    keep = row_keep(flash._seed(cuda).item(), site, R, C, p, cuda).view(R, 1, C)
+    d = (y.float() * (1 / (1 - p))).bfloat16().float() if p > 0 else y.float()
+    s_ref = src.float() + torch.where(keep, d, torch.zeros_like(d)) if p > 0 else src.float() + d
+    ln_a = torch.nn.functional.layer_norm(s_ref, (C,), na.weight, na.bias, na.eps)
+    xa_ref = ln_a.bfloat16()
+    xap_ref = (ln_a + pos).bfloat16()
+    xb_ref = torch.nn.functional.layer_norm(s_ref, (C,), nb.weight, nb.bias, nb.eps)
+    assert _rel(s, s_ref) < 1e-6
+    assert _rel(xa, xa_ref) < 8e-3 and _rel(xap, xap_ref) < 8e-3
+    assert _rel(xb, xb_ref) < 1e-5
+    torch.autograd.backward((s_ref, xa_ref, xap_ref, xb_ref), g)
+    ref = [t.grad for t in (src, y, pos, na.weight, na.bias, nb.weight, nb.bias)]
+    names = ("src", "y", "pos", "ga", "ba", "gb", "bb")
+    for n, a, b in zip(names, fused, ref):
+        tol = 1e-2 if n in ("src", "y") and (src_bf16 or n == "y") else 1e-4
+        assert _rel(a, b) < tol, (n, _rel(a, b))
+
+
+def _layers(cuda, enc_layers=2, dec_layers=3):
+    from ov3d_amd.transformer import (TransformerDecoder, TransformerDecoderLayer,
+                                      TransformerEncoder, TransformerEncoderLayer)
+    torch.manual_seed(1)
+    enc = TransformerEncoder(TransformerEncoderLayer(256, 4, 128, dropout=0.0), enc_layers)
+    dec = TransformerDecoder(TransformerDecoderLayer(256, 4, 256, dropout=0.0), dec_layers,
+                             return_intermediate=True)
+    with torch.no_grad():
+        for m in list(enc.modules()) + list(dec.modules()):
+            if isinstance(m, torch.nn.LayerNorm):
+                m.weight.normal_(1, 0.1)
+                m.bias.normal_(0, 0.1)
+    return enc.to(cuda).train(), dec.to(cuda).train()
+
+
+def test_encoder_decoder_fused_vs_plain_bf16(cuda):
+    """the fused bf16 path is as close to the fp32 modules as the plain bf16 path is"""
+    from ov3d_amd import resnorm as rn
+    enc, dec = _layers(cuda)
+    src = torch.randn(256, 2, 256, device=cuda)
+    tgt = torch.zeros(64, 2, 256, device=cuda)
+    qpos = torch.randn(64, 2, 256, device=cuda)
+    mpos = torch.randn(256, 2, 256, device=cuda)
+    g = torch.randn((3, 64, 2, 256), device=cuda, generator=torch.Generator(device=cuda).manual_seed(2))
+    res = {}
+    for mode in ("fp32", "plain", "fused"):
+        rn.enabled = mode == "fused"
+        try:
+            for prm in list(enc.parameters()) + list(dec.parameters()):
+                prm.grad = None
+            s = src.clone().requires_grad_()
+            q = qpos.clone().requires_grad_()
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=mode != "fp32"):
+                _, mem, _ = enc(s)
+                out, _ = dec(tgt, mem, query_pos=q, pos=mpos)
+            (out.float() * g).sum().backward()
+            res[mode] = [out.float().detach(), s.grad.clone(), q.grad.clone()] + \
+                [p.grad.clone() for p in list(enc.parameters()) + list(dec.parameters())]
+        finally:
+            rn.enabled = True
+    for i, ref in enumerate(res["fp32"]):
+        e_plain = _rel(res["plain"][i], ref)
+        e_fused = _rel(res["fused"][i], ref)
+        assert e_fused <= 1.5 * e_plain + 5e-3, (i, e_fused, e_plain)
+        assert e_fused < 0.1, (i, e_fused)
