@@ -91,6 +91,12 @@ def build(args, device, ddp=False, capturable=False):
             model, device_ids=[device.index], bucket_cap_mb=32, gradient_as_bucket_view=True)
     crit = ov3d.build_criterion(args, cfg).to(device)
     params = [p for p in model.parameters() if p.requires_grad]
+    if getattr(args, "optim", "fused") == "fused":
+        # clip_grad_norm_(clip_gradient) + AdamW in three HIP launches (ov3d_amd/optim.py)
+        from ov3d_amd.optim import FusedAdamW
+        opt = FusedAdamW(params, lr=args.base_lr, weight_decay=args.weight_decay,
+                         max_grad_norm=args.clip_gradient)
+        return model, crit, opt
     try:
         opt = torch.optim.AdamW(params, lr=args.base_lr, weight_decay=args.weight_decay, fused=True,
                                 capturable=capturable)
@@ -107,7 +113,8 @@ def train_step(model, crit, opt, batch, args, amp_dtype, clip=None):
         out = model(inputs)
     loss, _ = crit(out, batch, clip=clip)
     loss.backward()
-    torch.nn.utils.clip_grad_norm_(model.parameters(), args.clip_gradient)
+    if not getattr(opt, "clips_grads", False):
+        torch.nn.utils.clip_grad_norm_(model.parameters(), args.clip_gradient)
     opt.step()
     return loss
 
@@ -182,6 +189,9 @@ def main():
     p.add_argument("--eager", "--no-graph", dest="eager", action="store_true",
                    help="launch the step eagerly (default at N>1); at N=1 the whole step is "
                         "captured once and replayed as one hipGraph (graphs.StepGraph)")
+    p.add_argument("--optim", default="fused", choices=["fused", "torch"],
+                   help="fused: clip + AdamW in three HIP launches (ov3d_amd.optim.FusedAdamW); "
+                        "torch: clip_grad_norm_ + torch.optim.AdamW(fused=True)")
     cli = p.parse_args()
     wl = WORKLOADS[cli.workload]
     if cli.batch is None:
@@ -193,6 +203,7 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     args = default_args(**wl["args"])
+    args.optim = cli.optim
     amp = torch.bfloat16 if cli.dtype == "bf16" else None
     use_graph = world == 1 and not cli.eager
     model, crit, opt = build(args, device, ddp=world > 1, capturable=use_graph)

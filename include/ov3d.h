@@ -364,6 +364,28 @@ int ov3d_resnorm_bwd(long long R, int C, const float* s, const float* mean, cons
                      float* partials, int nparts, float* dga, float* dba, float* dgb, float* dbb,
                      void* stream);
 
+
+/* ---- Gradient clipping + AdamW over all parameter tensors (3 launches) ----
+ * Replaces engine.py:104-112 torch.nn.utils.clip_grad_norm_(params, max_norm) +
+ * torch.optim.AdamW.step() (main.py optimizer), torch's fused ADAMW arithmetic.
+ * table[i]: one parameter tensor (fp32 param / grad / exp_avg / exp_avg_sq, optional bf16
+ * shadow); workgroup b updates elements [blk_c[b]*chunk, +chunk) of tensor blk_t[b]
+ * (chunk = ov3d_adamw_chunk()).  partials: (nblocks) f64 workspace; step: device scalar
+ * (incremented); coefs (4) f64 out: clip multiplier, 1-b1^t, sqrt(1-b2^t), grad norm.
+ * max_norm <= 0: no clipping.  write_grad: store the clipped gradient back. */
+typedef struct {
+    float* param; float* grad; float* exp_avg; float* exp_avg_sq;
+    void* shadow;            /* bf16 copy of param or NULL */
+    long long numel;
+    float lr, weight_decay;
+} ov3d_adamw_tensor;
+int ov3d_adamw_chunk(void);
+/* table[i].grad = grads[i] (host array of device pointers) by kernel arguments: graph-safe */
+int ov3d_adamw_set_grads(ov3d_adamw_tensor* table, int ntensors, float* const* grads, void* stream);
+int ov3d_adamw_step(const ov3d_adamw_tensor* table, const int* blk_t, const int* blk_c, int nblocks,
+                    double* partials, float max_norm, float* step, double beta1, double beta2,
+                    float eps, double* coefs, int write_grad, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

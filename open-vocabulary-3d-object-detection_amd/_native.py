@@ -53,12 +53,15 @@ _SIGS = {
     "ov3d_rows_bn_bwd": "ipllipillilipppppppfpipipllip",
     "ov3d_set_loss_fwd": "pppppp",
     "ov3d_set_loss_bwd": "pppppppppppp",
+    "ov3d_adamw_step": "pppipfpddfpip",
+    "ov3d_adamw_set_grads": "pipp",
     "ov3d_resnorm_fwd": "lipipifpipppippfppppppp",
     "ov3d_resnorm_bwd": "lipppppppppfpippipipippppp",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
                           "ov3d_wgrad_workspace", "ov3d_wgrad_tiles", "ov3d_set_loss_desc_size",
-                          "ov3d_resnorm_supported", "ov3d_resnorm_bwd_parts")
+                          "ov3d_resnorm_supported", "ov3d_resnorm_bwd_parts",
+                          "ov3d_adamw_chunk")
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_longlong, "f": ctypes.c_float,
        "d": ctypes.c_double}
@@ -95,6 +98,8 @@ def load():
         lib.ov3d_resnorm_supported.restype = ctypes.c_int
         lib.ov3d_resnorm_bwd_parts.argtypes = [ctypes.c_longlong, ctypes.c_int]
         lib.ov3d_resnorm_bwd_parts.restype = ctypes.c_int
+        lib.ov3d_adamw_chunk.argtypes = []
+        lib.ov3d_adamw_chunk.restype = ctypes.c_int
         lib.ov3d_version.argtypes = []
         lib.ov3d_version.restype = ctypes.c_char_p
         _lib = lib

@@ -1,0 +1,159 @@
+// Gradient-norm clipping + AdamW over every parameter tensor of the model in three launches.
+//
+// Reference: main.py builds torch.optim.AdamW(lr, weight_decay) and engine.py:104-112 runs
+// torch.nn.utils.clip_grad_norm_(model.parameters(), clip_gradient) then optimizer.step()
+// per iteration.  Here the ~200 parameter tensors are one launch space: a device table
+// lists (param, grad, exp_avg, exp_avg_sq, bf16 shadow, numel, lr, weight decay) per
+// tensor and every workgroup owns a 4096-element chunk of one tensor.
+//
+//   1. adamw_norm_kernel     : per-chunk sum of grad^2 (fp64 partials, fixed order)
+//   2. adamw_finalize_kernel : total norm, clip coefficient min(1, max_norm/(norm+1e-6))
+//                              (clip_grad_norm_), step += 1, bias corrections
+//   3. adamw_update_kernel   : g *= clip (written back, as clip_grad_norm_ does), then the
+//                              AdamW update of torch.optim.AdamW (decoupled decay):
+//        p -= lr*wd*p;  m = lerp(m, g, 1-b1);  v = b2*v + (1-b2)*g*g
+//        p -= (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
+//      and refreshes the parameter's bf16 copy used by the autocast GEMMs (gemm.py).
+// Coalesced fp32 element streams; HBM-bound (28 B per parameter, + 2 B with a shadow).
+#include "common.h"
+
+namespace {
+
+typedef __bf16 bf16;
+constexpr int kThreads = 256;
+constexpr int kPer = 16;                 // elements per thread
+constexpr int kChunk = kThreads * kPer;  // elements per workgroup
+
+__global__ void __launch_bounds__(kThreads) adamw_norm_kernel(const ov3d_adamw_tensor* __restrict__ T,
+                                                              const int* __restrict__ blk_t,
+                                                              const int* __restrict__ blk_c,
+                                                              double* __restrict__ partials) {
+    const ov3d_adamw_tensor t = T[blk_t[blockIdx.x]];
+    const long long base = (long long)blk_c[blockIdx.x] * kChunk;
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const long long e = base + j * kThreads + threadIdx.x;
+        if (e < t.numel) {
+            const float g = t.grad[e];
+            s = fmaf(g, g, s);
+        }
+    }
+    double d = (double)s;
+    for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+    __shared__ double red[kThreads / 64];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = d;
+    __syncthreads();
+    if (threadIdx.x == 0) partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// coefs: [0] clip multiplier, [1] 1 - b1^t, [2] sqrt(1 - b2^t), [3] total grad norm
+// (fp64 like the Python-float bias corrections of torch.optim.AdamW)
+__global__ void __launch_bounds__(kThreads) adamw_finalize_kernel(const double* __restrict__ partials,
+                                                                  int nblocks, float max_norm,
+                                                                  float* step, double beta1,
+                                                                  double beta2, double* coefs) {
+    double s = 0.0;
+    for (int i = threadIdx.x; i < nblocks; i += kThreads) s += partials[i];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    __shared__ double red[kThreads / 64];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const float norm = (float)sqrt((red[0] + red[1]) + (red[2] + red[3]));
+    float clip = 1.f;
+    if (max_norm > 0.f) clip = fminf(max_norm / (norm + 1e-6f), 1.f);
+    const float t = *step + 1.f;
+    *step = t;
+    coefs[0] = clip;
+    coefs[1] = 1.0 - pow(beta1, (double)t);
+    coefs[2] = sqrt(1.0 - pow(beta2, (double)t));
+    coefs[3] = norm;
+}
+
+__global__ void __launch_bounds__(kThreads) adamw_update_kernel(const ov3d_adamw_tensor* __restrict__ T,
+                                                                const int* __restrict__ blk_t,
+                                                                const int* __restrict__ blk_c,
+                                                                const double* __restrict__ coefs,
+                                                                float beta2, float omb1, float omb2,
+                                                                float eps, int write_grad) {
+    const ov3d_adamw_tensor t = T[blk_t[blockIdx.x]];
+    const long long base = (long long)blk_c[blockIdx.x] * kChunk;
+    const float clip = (float)coefs[0];
+    const float step_size = (float)((double)t.lr / coefs[1]);
+    const float inv_bc2s = 1.f / (float)coefs[2];   // tensor / python float: * fp32 reciprocal
+    const float decay = (float)(1.0 - (double)t.lr * (double)t.weight_decay);
+#pragma unroll 4
+    for (int j = 0; j < kPer; ++j) {
+        const long long e = base + j * kThreads + threadIdx.x;
+        if (e >= t.numel) break;
+        float g = t.grad[e];
+        if (clip != 1.f) {
+            g *= clip;
+            if (write_grad) t.grad[e] = g;
+        }
+        // torch.optim.AdamW's single-tensor / foreach arithmetic, operation for operation:
+        // p.mul_(1 - lr*wd); m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
+        // p.addcdiv_(m, v.sqrt() / sqrt(bc2) + eps, -lr/bc1)
+        float p = t.param[e] * decay;
+        const float m0 = t.exp_avg[e];
+        // (single-kernel torch ops contract to FMA: lerp, addcmul, addcdiv)
+        const float m = omb1 < 0.5f ? fmaf(omb1, g - m0, m0) : fmaf(-(g - m0), 1.f - omb1, g);
+        const float v = fmaf(omb2, g * g, beta2 * t.exp_avg_sq[e]);
+        const float denom = sqrtf(v) * inv_bc2s + eps;
+        p = fmaf(-step_size, m / denom, p);
+        t.param[e] = p;
+        t.exp_avg[e] = m;
+        t.exp_avg_sq[e] = v;
+        if (t.shadow) reinterpret_cast<bf16*>(t.shadow)[e] = (bf16)p;
+    }
+}
+
+constexpr int kGradsPerLaunch = 256;
+struct GradPtrs {
+    float* g[kGradsPerLaunch];
+};
+// table[first + i].grad = p.g[i]: the gradient pointers travel as kernel arguments, so a
+// captured step graph carries its own (graph-pool) gradient addresses
+__global__ void adamw_set_grads_kernel(ov3d_adamw_tensor* table, int first, int count, GradPtrs p) {
+    const int i = threadIdx.x;
+    if (i < count) table[first + i].grad = p.g[i];
+}
+
+}  // namespace
+
+extern "C" int ov3d_adamw_chunk(void) { return kChunk; }
+
+extern "C" int ov3d_adamw_set_grads(ov3d_adamw_tensor* table, int ntensors, float* const* grads,
+                                    void* stream) {
+    if (!table || ntensors <= 0 || !grads) return OV3D_EINVAL;
+    for (int first = 0; first < ntensors; first += kGradsPerLaunch) {
+        const int count = ntensors - first < kGradsPerLaunch ? ntensors - first : kGradsPerLaunch;
+        GradPtrs p;
+        for (int i = 0; i < kGradsPerLaunch; ++i) p.g[i] = i < count ? grads[first + i] : nullptr;
+        adamw_set_grads_kernel<<<1, kGradsPerLaunch, 0, ov3d_stream(stream)>>>(table, first, count, p);
+        OV3D_LAUNCH_CHECK();
+    }
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_adamw_step(const ov3d_adamw_tensor* table, const int* blk_t, const int* blk_c,
+                               int nblocks, double* partials, float max_norm, float* step,
+                               double beta1, double beta2, float eps, double* coefs, int write_grad,
+                               void* stream) {
+    if (!table || !blk_t || !blk_c || nblocks <= 0 || !partials || !step || !coefs ||
+        beta1 < 0.0 || beta1 >= 1.0 || beta2 < 0.0 || beta2 >= 1.0 || eps < 0.f)
+        return OV3D_EINVAL;
+    hipStream_t s = ov3d_stream(stream);
+    adamw_norm_kernel<<<nblocks, kThreads, 0, s>>>(table, blk_t, blk_c, partials);
+    OV3D_LAUNCH_CHECK();
+    adamw_finalize_kernel<<<1, kThreads, 0, s>>>(partials, nblocks, max_norm, step, beta1, beta2,
+                                                 coefs);
+    OV3D_LAUNCH_CHECK();
+    // 1 - beta in fp64 first (Python floats in torch), then fp32
+    adamw_update_kernel<<<nblocks, kThreads, 0, s>>>(table, blk_t, blk_c, coefs, (float)beta2,
+                                                     (float)(1.0 - beta1), (float)(1.0 - beta2), eps,
+                                                     write_grad);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}

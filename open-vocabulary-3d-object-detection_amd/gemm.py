@@ -55,7 +55,8 @@ def _wg_counters(device):
 def _wg_splits(R, N, K):
     from . import _native
     tiles = _native.load().ov3d_wgrad_tiles(N, K)
-    rows = 256 if R <= 4096 else 512   # short R: parallelism; long R: fewer partials to sum
+    # short R: parallelism; long R: fewer partials to sum (tools/wgrad_split_probe.py sweep)
+    rows = 128 if R <= 2048 else (256 if R <= 4096 else 512)
     return max(1, min((R + rows - 1) // rows, 512 // tiles))
 
 
@@ -124,6 +125,19 @@ def refresh_shadows(force=False):
             torch._foreach_copy_([e[1] for e in stale], [e[0]() for e in stale])
         for e in stale:
             e[2] = e[0]()._version
+
+
+def shadow_of(p):
+    """the registered bf16 copy of parameter p (or None)"""
+    e = _SHADOWS.get(id(p))
+    return e[1] if e is not None and e[0]() is p else None
+
+
+def mark_shadow_fresh(p):
+    """p's bf16 copy was rewritten together with p (optim.FusedAdamW)"""
+    e = _SHADOWS.get(id(p))
+    if e is not None and e[0]() is p:
+        e[2] = p._version
 
 
 def cast_param(w, dt):

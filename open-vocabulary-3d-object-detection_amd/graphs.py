@@ -70,7 +70,8 @@ class GraphedModel:
 class StepGraph:
     """Replays forward + criterion + backward + clip_grad_norm_ + optimizer.step.
 
-    model, crit: as for an eager step; opt must be built with capturable=True.
+    model, crit: as for an eager step; opt: torch AdamW built with capturable=True, or
+    optim.FusedAdamW (its step clips the gradients and rewrites the bf16 weight copies).
     sample: a batch dict (device tensors) fixing the static shapes.
 
     Sampling prefetch (prefetch_fps=True): the pre-encoder's furthest-point
@@ -115,7 +116,8 @@ class StepGraph:
         return self._pu.furthest_point_sample(pc[..., 0:3].contiguous(), self.npoint)
 
     def _body(self, gemm):
-        gemm.refresh_shadows(force=True)   # captured: bf16 weight copies follow every update
+        if not getattr(self.opt, "writes_shadows", False):
+            gemm.refresh_shadows(force=True)   # captured: bf16 weight copies follow every update
         self.opt.zero_grad(set_to_none=True)
         inputs = {k: self.static[k] for k in IN_KEYS}
         if self.prefetch:
@@ -125,7 +127,8 @@ class StepGraph:
             out = self.model(inputs)
         loss, _ = self.crit(out, dict(self.static), clip=self.regionclip)
         loss.backward()
-        torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.clip)
+        if not getattr(self.opt, "clips_grads", False):
+            torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.clip)
         self.opt.step()
         return loss.detach()
 

@@ -1,0 +1,146 @@
+"""AdamW with the gradient-norm clipping fused in: three HIP launches per step over all
+parameter tensors (csrc/adamw.hip, ``ov3d_adamw_step``).
+
+Reference: main.py builds ``torch.optim.AdamW(params, lr=base_lr,
+weight_decay=weight_decay)``; engine.py:104-112 calls
+``torch.nn.utils.clip_grad_norm_(model.parameters(), clip_gradient)`` (when > 0) and then
+``optimizer.step()``.  ``FusedAdamW(params, lr, weight_decay=..., max_grad_norm=clip)``
+does both in ``step()``: the clipped gradients are written back to ``p.grad`` as
+clip_grad_norm_ does, ``last_grad_norm`` holds the total norm (device scalar) it returns,
+and the state keeps torch's keys (``step``, ``exp_avg``, ``exp_avg_sq``).  Built with
+``max_grad_norm=None`` it is a drop-in for AdamW after a separate clip_grad_norm_ call.
+
+The bf16 copies of the parameters used by the autocast GEMMs (gemm.cast_param) are
+rewritten by the same update launch, so no separate refresh copy runs.  Capturable: the
+step counter and bias corrections live on the device, the per-tensor table (parameter,
+moments, shadow, size, lr, weight decay) is built by one eager step, and the gradient
+addresses travel as kernel arguments of ov3d_adamw_set_grads, so a step graph carries its
+own.  Learning-rate changes rebuild the table eagerly (a captured graph keeps its lr).
+"""
+import ctypes
+
+import torch
+
+from . import _native
+from . import gemm
+
+
+class _Entry(ctypes.Structure):
+    """mirror of ov3d_adamw_tensor (include/ov3d.h)"""
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p),
+                ("exp_avg", ctypes.c_void_p), ("exp_avg_sq", ctypes.c_void_p),
+                ("shadow", ctypes.c_void_p), ("numel", ctypes.c_longlong),
+                ("lr", ctypes.c_float), ("weight_decay", ctypes.c_float)]
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    clips_grads = True        # step() includes clip_grad_norm_ (when max_grad_norm is set)
+    writes_shadows = True     # step() refreshes gemm.py's bf16 parameter copies
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2,
+                 max_grad_norm=None):
+        if lr < 0 or eps < 0 or weight_decay < 0 or not (0 <= betas[0] < 1 and 0 <= betas[1] < 1):
+            raise ValueError("FusedAdamW: invalid hyper-parameters")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self.max_grad_norm = max_grad_norm
+        self.last_grad_norm = None
+        self._key = None
+        self._dev = None
+
+    def _params(self):
+        out = []
+        b = e = None
+        for g in self.param_groups:
+            if b is None:
+                b, e = tuple(g["betas"]), g["eps"]
+            elif tuple(g["betas"]) != b or g["eps"] != e:
+                raise ValueError("FusedAdamW: betas / eps must be equal across param groups")
+            for p in g["params"]:
+                if p.grad is not None:
+                    out.append((p, g))
+        return out, b, e
+
+    def _state(self, p, dev):
+        st = self.state[p]
+        if not st:
+            if self._step_t is None:
+                self._step_t = torch.zeros((), dtype=torch.float32, device=dev)
+            st["step"] = self._step_t
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        return st
+
+    _step_t = None
+
+    def _table(self, items, dev):
+        """entries without the gradient pointers (set per step by ov3d_adamw_set_grads)"""
+        chunk = _native.load().ov3d_adamw_chunk()
+        ents, blk_t, blk_c, key = [], [], [], []
+        for i, (p, g) in enumerate(items):
+            if not (p.is_cuda and p.dtype == torch.float32 and p.grad.dtype == torch.float32
+                    and p.is_contiguous() and p.grad.is_contiguous()
+                    and p.grad.shape == p.shape):
+                raise ValueError("FusedAdamW: fp32 contiguous device parameters and gradients only")
+            st = self._state(p, dev)
+            sh = gemm.shadow_of(p)
+            n = p.numel()
+            ents.append(_Entry(p.data_ptr(), 0, st["exp_avg"].data_ptr(),
+                               st["exp_avg_sq"].data_ptr(), sh.data_ptr() if sh is not None else 0,
+                               n, float(g["lr"]), float(g["weight_decay"])))
+            nb = (n + chunk - 1) // chunk
+            blk_t += [i] * nb
+            blk_c += list(range(nb))
+            key.append((p.data_ptr(), ents[-1].shadow, n, float(g["lr"]), float(g["weight_decay"])))
+        return tuple(key), ents, blk_t, blk_c
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        steps = [st["step"] for st in self.state.values() if "step" in st]
+        if steps:
+            dev = next(iter(self.state.values()))["exp_avg"].device
+            self._step_t = torch.as_tensor(steps[0], dtype=torch.float32).to(dev).reshape(())
+            for st in self.state.values():
+                st["step"] = self._step_t
+        self._key = None
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        items, (b1, b2), eps = self._params()
+        if not items:
+            return loss
+        dev = items[0][0].device
+        _native.check_device(items[0][0], "FusedAdamW parameters")
+        key, ents, blk_t, blk_c = self._table(items, dev)
+        if key != self._key or dev != self._dev:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("FusedAdamW: run one eager step before capturing a graph "
+                                   "(the parameter table is built outside capture)")
+            raw = (_Entry * len(ents))(*ents)
+            nbytes = ctypes.sizeof(raw)
+            host = torch.empty(nbytes + 8 * len(blk_t), dtype=torch.uint8)
+            ctypes.memmove(host.data_ptr(), ctypes.addressof(raw), nbytes)
+            host[nbytes:].view(torch.int32).copy_(torch.tensor(blk_t + blk_c, dtype=torch.int32))
+            self._buf = host.to(dev)
+            self._nbytes, self._nblocks, self._ntensors = nbytes, len(blk_t), len(ents)
+            self._partials = torch.empty(len(blk_t), dtype=torch.float64, device=dev)
+            self._coefs = torch.empty(4, dtype=torch.float64, device=dev)
+            self._key, self._dev = key, dev
+        grads = (ctypes.c_void_p * len(items))(*[p.grad.data_ptr() for p, _ in items])
+        _native.call("ov3d_adamw_set_grads", self._buf, len(items), ctypes.addressof(grads),
+                     like=self._buf)
+        idx = self._buf[self._nbytes:].view(torch.int32)
+        clip = float(self.max_grad_norm) if self.max_grad_norm and self.max_grad_norm > 0 else 0.0
+        _native.call("ov3d_adamw_step", self._buf, idx, idx[self._nblocks:], self._nblocks,
+                     self._partials, clip, self._step_t, float(b1), float(b2), float(eps),
+                     self._coefs, 1, like=self._buf)
+        self.last_grad_norm = self._coefs[3]   # fp64 view (no launch)
+        for p, _ in items:
+            torch.autograd.graph.increment_version(p)
+            if clip:
+                torch.autograd.graph.increment_version(p.grad)
+            gemm.mark_shadow_fresh(p)
+        return loss
