@@ -94,19 +94,37 @@ __global__ __launch_bounds__(kThreads) void sa_layer_kernel(LayerArgs p) {
     __syncthreads();
 
     const int ntiles = p.R / kTile;
+    // software pipeline: the next tile's rows are loaded into registers while this tile's
+    // MFMA phase and epilogue run (CH 16-byte chunks per thread)
+    constexpr int CH = kTile * K / 8 / kThreads;
+    static_assert(CH * kThreads * 8 == kTile * K, "tile chunks");
+    bf16x8 pre[CH];
+    auto fetch = [&](int tile) {
+        const size_t row0 = (size_t)tile * kTile;
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const int ch = tid + c * kThreads;
+            const int row = ch / (K / 8), kc = (ch % (K / 8)) * 8;
+            pre[c] = *reinterpret_cast<const bf16x8*>(p.yprev + (row0 + row) * K + kc);
+        }
+    };
+    if (blockIdx.x < ntiles) fetch(blockIdx.x);
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const size_t row0 = (size_t)tile * kTile;
-        // prologue: previous layer's BN + ReLU, to bf16, into LDS (and optionally HBM)
-        for (int ch = tid; ch < kTile * K / 8; ch += kThreads) {
+        // prologue: previous layer's BN + ReLU of the prefetched rows, to bf16, into LDS
+        // (and optionally HBM)
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const int ch = tid + c * kThreads;
             const int row = ch / (K / 8), kc = (ch % (K / 8)) * 8;
-            const bf16x8 v = *reinterpret_cast<const bf16x8*>(p.yprev + (row0 + row) * K + kc);
             bf16x8 z;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) z[j] = (bf16)relu_bn(sc[kc + j], (float)v[j], sh[kc + j]);
+            for (int j = 0; j < 8; ++j) z[j] = (bf16)relu_bn(sc[kc + j], (float)pre[c][j], sh[kc + j]);
             *reinterpret_cast<bf16x8*>(&As[row * LDK + kc]) = z;
             if (p.zout) *reinterpret_cast<bf16x8*>(p.zout + (row0 + row) * K + kc) = z;
         }
         __syncthreads();
+        if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);   // in flight during the MFMAs
         f32x16 acc[2][NB];
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb)

@@ -30,7 +30,8 @@ from torch.autograd import Function
 from . import _native as nat
 from .gemm import cast_param, weight_grad
 
-NPARTS_LAYER = 512     # persistent MFMA workgroups (2 per CU)
+NPARTS_LAYER = 1024    # MFMA workgroups over 64-row tiles (more than resident: no tail when
+                       # the side-stream FPS holds a few CUs; tools/sa_layer_probe.py)
 NPARTS_ROWS = 1024     # row-pass workgroups
 NPARTS_POOL = 256
 
