@@ -189,6 +189,9 @@ def main():
     p.add_argument("--eager", "--no-graph", dest="eager", action="store_true",
                    help="launch the step eagerly (default at N>1); at N=1 the whole step is "
                         "captured once and replayed as one hipGraph (graphs.StepGraph)")
+    p.add_argument("--no-defer-wgrad", action="store_true",
+                   help="compute each linear layer's dW / db inside its backward instead of one "
+                        "grouped launch at the end of the backward pass (gemm.DEFER_WGRAD)")
     p.add_argument("--optim", default="fused", choices=["fused", "torch"],
                    help="fused: clip + AdamW in three HIP launches (ov3d_amd.optim.FusedAdamW); "
                         "torch: clip_grad_norm_ + torch.optim.AdamW(fused=True)")
@@ -207,6 +210,9 @@ def main():
     amp = torch.bfloat16 if cli.dtype == "bf16" else None
     use_graph = world == 1 and not cli.eager
     model, crit, opt = build(args, device, ddp=world > 1, capturable=use_graph)
+    if world == 1 and not cli.no_defer_wgrad:
+        from ov3d_amd import gemm
+        gemm.DEFER_WGRAD = True   # one grouped weight-gradient launch per backward (not under DDP)
     clip = build_regionclip(device) if wl["use_image"] else None
     pool = [synthetic.make_batch(cli.batch, seed=1000 * rank + i, num_points=cli.points, device=device,
                                  use_image=wl["use_image"])

@@ -261,6 +261,16 @@ int ov3d_wgrad(const void* dy, long long ldy, const void* x, long long ldx, int 
                float* dW, long long ldw, float* db, float* workspace, int* counters, int nsplit,
                void* stream);
 long long ov3d_wgrad_workspace(int R, int N, int K, int nsplit);
+/* several independent weight gradients in one launch (+ one split reduction launch) per
+ * 28 problems: the deferred dW / db of a backward pass (gemm.py).  workspace:
+ * ov3d_wgrad_group_workspace() floats. */
+typedef struct {
+    const void* dy; long long ldy; const void* x; long long ldx;
+    int R, N, K, nsplit;
+    float* dW; long long ldw; float* db;
+} ov3d_wgrad_problem;
+long long ov3d_wgrad_group_workspace(const ov3d_wgrad_problem* probs, int n);
+int ov3d_wgrad_group(const ov3d_wgrad_problem* probs, int n, float* workspace, void* stream);
 int ov3d_wgrad_tiles(int N, int K);
 
 /* ---- Training BatchNorm1d + ReLU + Dropout over channels-last rows ----

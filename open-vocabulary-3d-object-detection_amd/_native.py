@@ -48,6 +48,7 @@ _SIGS = {
     "ov3d_attn_fwd": "pppllliiiiffpiplppip",
     "ov3d_attn_bwd": "ppplllplplpiiiiffpipplplplpip",
     "ov3d_wgrad": "plpliiiplpppip",
+    "ov3d_wgrad_group": "pipp",
     "ov3d_rows_bn_stats": "pillilipip",
     "ov3d_rows_bn_apply": "pillilippfpipllip",
     "ov3d_rows_bn_bwd": "ipllipillilipppppppfpipipllip",
@@ -61,7 +62,7 @@ _SIGS = {
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
                           "ov3d_wgrad_workspace", "ov3d_wgrad_tiles", "ov3d_set_loss_desc_size",
                           "ov3d_resnorm_supported", "ov3d_resnorm_bwd_parts",
-                          "ov3d_adamw_chunk")
+                          "ov3d_adamw_chunk", "ov3d_wgrad_group_workspace")
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_longlong, "f": ctypes.c_float,
        "d": ctypes.c_double}
@@ -100,6 +101,8 @@ def load():
         lib.ov3d_resnorm_bwd_parts.restype = ctypes.c_int
         lib.ov3d_adamw_chunk.argtypes = []
         lib.ov3d_adamw_chunk.restype = ctypes.c_int
+        lib.ov3d_wgrad_group_workspace.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        lib.ov3d_wgrad_group_workspace.restype = ctypes.c_longlong
         lib.ov3d_version.argtypes = []
         lib.ov3d_version.restype = ctypes.c_char_p
         _lib = lib

@@ -63,18 +63,18 @@ __device__ __forceinline__ bf16x8 col_frag(const bf16* T, int lane, int c0, int 
     return a;
 }
 
-__global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradArgs a) {
+// one 128 x 128 output tile (bx, by) of one row split
+__device__ __forceinline__ void wgrad_body(const WgradArgs& a, int bx, int by, int split) {
     __shared__ __attribute__((aligned(16))) bf16 Ds[2][RS * LDT];
     __shared__ __attribute__((aligned(16))) bf16 Xs[2][RS * LDT];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wn = wave >> 1, wk = wave & 1;
-    const int n0 = blockIdx.x * TN, k0 = blockIdx.y * TK;
-    const int split = blockIdx.z;
+    const int n0 = bx * TN, k0 = by * TK;
     const int rbeg = split * a.rows_per_split;
     const int rend = min(a.R, rbeg + a.rows_per_split);
     // db: the workgroups of output column tile 0 also sum their dy stage tile over its
     // rows on the VALU (thread: 8 adjacent columns x 2 rows per stage)
-    const bool do_bias = a.db != nullptr && blockIdx.y == 0;
+    const bool do_bias = a.db != nullptr && by == 0;
 
     // stage loader: RS rows x 16 chunks (16 B) per operand = 512 chunks, 2 per thread.
     // Two register sets: stage n+2 is in flight while stage n is computed and stage n+1
@@ -215,9 +215,8 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradArgs a) {
 
 // dW / db = sum of the split partials in split order (deterministic).  One thread per
 // output element (coalesced across threads), 8 split loads in flight per thread.
-__global__ void __launch_bounds__(256) wgrad_reduce_kernel(WgradArgs a) {
+__device__ __forceinline__ void wgrad_reduce_body(const WgradArgs& a, long long t) {
     const size_t NK = (size_t)a.N * a.K;
-    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const float* p;
     size_t stride;
     if (t < (long long)NK) {
@@ -247,6 +246,43 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(WgradArgs a) {
     }
 }
 
+__global__ void __launch_bounds__(256, 2) wgrad_kernel(WgradArgs a) {
+    wgrad_body(a, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(WgradArgs a) {
+    wgrad_reduce_body(a, (long long)blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// Several independent weight gradients in one launch (the deferred dW / db of a whole
+// backward pass, gemm.py): problem i owns workgroups [blk[i], blk[i+1]).
+constexpr int kGroupMax = 28;
+struct WgradGroup {
+    WgradArgs p[kGroupMax];
+    int blk[kGroupMax + 1];
+    int red[kGroupMax + 1];   // reduce: workgroups [red[i], red[i+1]) of problem i
+    int n;
+};
+static_assert(sizeof(WgradGroup) <= 4000, "kernel argument space");
+
+__global__ void __launch_bounds__(256, 2) wgrad_group_kernel(WgradGroup g) {
+    const int b = blockIdx.x;
+    int i = 0;
+    while (i + 1 < g.n && b >= g.blk[i + 1]) ++i;
+    const WgradArgs& a = g.p[i];
+    const int tn = (a.N + TN - 1) / TN, tk = (a.K + TK - 1) / TK;
+    const int local = b - g.blk[i];
+    wgrad_body(a, local % tn, (local / tn) % tk, local / (tn * tk));
+}
+
+__global__ void __launch_bounds__(256) wgrad_group_reduce_kernel(WgradGroup g) {
+    const int b = blockIdx.x;
+    int i = 0;
+    while (i + 1 < g.n && b >= g.red[i + 1]) ++i;
+    if (b >= g.red[i + 1] || b < g.red[i]) return;
+    wgrad_reduce_body(g.p[i], (long long)(b - g.red[i]) * blockDim.x + threadIdx.x);
+}
+
 }  // namespace
 
 extern "C" long long ov3d_wgrad_workspace(int R, int N, int K, int nsplit) {
@@ -256,9 +292,9 @@ extern "C" long long ov3d_wgrad_workspace(int R, int N, int K, int nsplit) {
 
 extern "C" int ov3d_wgrad_tiles(int N, int K) { return ((N + TN - 1) / TN) * ((K + TK - 1) / TK); }
 
-extern "C" int ov3d_wgrad(const void* dy, long long ldy, const void* x, long long ldx, int R, int N,
-                          int K, float* dW, long long ldw, float* db, float* workspace,
-                          int* counters, int nsplit, void* stream) {
+static int make_args(WgradArgs& a, const void* dy, long long ldy, const void* x, long long ldx,
+                     int R, int N, int K, float* dW, long long ldw, float* db, float* workspace,
+                     int nsplit) {
     if (!dy || !x || !dW || R <= 0 || N <= 0 || K <= 0 || ldy < N || ldx < K || ldw < K ||
         nsplit <= 0)
         return OV3D_EINVAL;
@@ -266,7 +302,6 @@ extern "C" int ov3d_wgrad(const void* dy, long long ldy, const void* x, long lon
     rps = (rps + RS - 1) / RS * RS;
     nsplit = (R + rps - 1) / rps;
     if (nsplit > 1 && !workspace) return OV3D_EINVAL;
-    WgradArgs a;
     a.dy = (const bf16*)dy;
     a.x = (const bf16*)x;
     a.ldy = ldy;
@@ -278,11 +313,21 @@ extern "C" int ov3d_wgrad(const void* dy, long long ldy, const void* x, long lon
     a.ldw = ldw;
     a.db = db;
     a.part = workspace;
-    (void)counters;
     a.nsplit = nsplit;
     a.rows_per_split = rps;
     a.vec_dy = (ldy % 8 == 0) && ((uintptr_t)dy % 16 == 0);
     a.vec_x = (ldx % 8 == 0) && ((uintptr_t)x % 16 == 0);
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_wgrad(const void* dy, long long ldy, const void* x, long long ldx, int R, int N,
+                          int K, float* dW, long long ldw, float* db, float* workspace,
+                          int* counters, int nsplit, void* stream) {
+    (void)counters;
+    WgradArgs a;
+    const int rc = make_args(a, dy, ldy, x, ldx, R, N, K, dW, ldw, db, workspace, nsplit);
+    if (rc != OV3D_OK) return rc;
+    nsplit = a.nsplit;
     dim3 grid((N + TN - 1) / TN, (K + TK - 1) / TK, nsplit);
     hipStream_t st = ov3d_stream(stream);
     wgrad_kernel<<<grid, 256, 0, st>>>(a);
@@ -291,6 +336,47 @@ extern "C" int ov3d_wgrad(const void* dy, long long ldy, const void* x, long lon
         const long long threads = (long long)N * K + (db ? N : 0);
         wgrad_reduce_kernel<<<ov3d_cdiv(threads, 256), 256, 0, st>>>(a);
         OV3D_LAUNCH_CHECK();
+    }
+    return OV3D_OK;
+}
+
+extern "C" long long ov3d_wgrad_group_workspace(const ov3d_wgrad_problem* probs, int n) {
+    long long w = 0;
+    for (int i = 0; i < n; ++i) w += ov3d_wgrad_workspace(probs[i].R, probs[i].N, probs[i].K, probs[i].nsplit);
+    return w;
+}
+
+extern "C" int ov3d_wgrad_group(const ov3d_wgrad_problem* probs, int n, float* workspace,
+                                void* stream) {
+    if (!probs || n <= 0) return OV3D_EINVAL;
+    hipStream_t st = ov3d_stream(stream);
+    long long woff = 0;
+    for (int first = 0; first < n; first += kGroupMax) {
+        WgradGroup g;
+        g.n = n - first < kGroupMax ? n - first : kGroupMax;
+        int blk = 0, red = 0;
+        for (int j = 0; j < g.n; ++j) {
+            const ov3d_wgrad_problem& q = probs[first + j];
+            const long long ws = ov3d_wgrad_workspace(q.R, q.N, q.K, q.nsplit);
+            const int rc = make_args(g.p[j], q.dy, q.ldy, q.x, q.ldx, q.R, q.N, q.K, q.dW, q.ldw,
+                                     q.db, ws > 0 && workspace ? workspace + woff : nullptr,
+                                     q.nsplit);
+            if (rc != OV3D_OK) return rc;
+            woff += ws;
+            g.blk[j] = blk;
+            g.red[j] = red;
+            blk += ((q.N + TN - 1) / TN) * ((q.K + TK - 1) / TK) * g.p[j].nsplit;
+            if (g.p[j].nsplit > 1)
+                red += ov3d_cdiv((long long)q.N * q.K + (q.db ? q.N : 0), 256);
+        }
+        g.blk[g.n] = blk;
+        g.red[g.n] = red;
+        wgrad_group_kernel<<<blk, 256, 0, st>>>(g);
+        OV3D_LAUNCH_CHECK();
+        if (red > 0) {
+            wgrad_group_reduce_kernel<<<red, 256, 0, st>>>(g);
+            OV3D_LAUNCH_CHECK();
+        }
     }
     return OV3D_OK;
 }

@@ -8,6 +8,7 @@ BLAS as one GEMM it runs on 7-21 workgroups of the 256 CUs (1.4-2.1 ms per SA la
 measured: profiles/r01_kernel_stats_v2.csv).  Here the reduction is split into
 row chunks computed as one batched GEMM (>= ~256 workgroups) and summed in fp32.
 """
+import ctypes
 import weakref
 
 import torch
@@ -91,6 +92,105 @@ def fused_weight_grad(dy, x, bias=True, out_w=None, out_b=None):
     return dw, db
 
 
+# ---------------------------------------------------------------- deferred weight grads
+# dW / db of a linear layer are not needed by anything else in the backward pass, so they
+# can run after it: every deferred (dy, x) pair of one backward pass goes into ONE grouped
+# launch (csrc/wgrad.hip ov3d_wgrad_group) queued to run when the autograd engine finishes
+# (queue_callback), instead of ~100 latency-bound launches interleaved with the dgrad
+# chain.  The layers' backward returns None for the weight / bias and the flush assigns
+# (or adds into) ``param.grad`` itself, so hooks on those parameters do not fire:
+# enabled only by the single-process training step (bench.py / graphs.StepGraph), never
+# under DDP (its reducer needs the per-parameter gradient hooks).
+DEFER_WGRAD = False
+_PENDING = []
+
+
+class _WgProblem(ctypes.Structure):
+    """mirror of ov3d_wgrad_problem (include/ov3d.h)"""
+    _fields_ = [("dy", ctypes.c_void_p), ("ldy", ctypes.c_longlong), ("x", ctypes.c_void_p),
+                ("ldx", ctypes.c_longlong), ("R", ctypes.c_int), ("N", ctypes.c_int),
+                ("K", ctypes.c_int), ("nsplit", ctypes.c_int), ("dW", ctypes.c_void_p),
+                ("ldw", ctypes.c_longlong), ("db", ctypes.c_void_p)]
+
+
+def _leaf_param(w):
+    """the fp32 leaf parameter w is (or fully aliases as a contiguous view), else None"""
+    if w is None:
+        return None
+    base = w if w._base is None else w._base
+    if not (base.is_leaf and base.requires_grad and base.dtype == torch.float32 and base.is_cuda):
+        return None
+    if w is not base and not (w.is_contiguous() and w.numel() == base.numel()
+                              and w.data_ptr() == base.data_ptr()):
+        return None
+    return base
+
+
+def can_defer(x, w, b=None):
+    """x: the saved bf16 input rows (dy is cast to x's dtype and made row-contiguous)"""
+    return (DEFER_WGRAD and not torch.is_grad_enabled() and x.is_cuda
+            and x.dtype == torch.bfloat16 and x.dim() == 2 and x.stride(1) == 1
+            and _leaf_param(w) is not None and (b is None or _leaf_param(b) is not None))
+
+
+def defer_weight_grad(dy, x, w, b=None, rows=None):
+    """queue dW = dy^T x (+ db = sum dy) for parameter w (and bias b); rows=(r0, r1): the
+    block of w's rows this pair produces (nn.MultiheadAttention in_proj)."""
+    if not _PENDING:
+        torch.autograd.Variable._execution_engine.queue_callback(flush_weight_grads)
+    _PENDING.append((dy, x, _leaf_param(w), w.shape, _leaf_param(b) if b is not None else None,
+                     rows))
+
+
+def flush_weight_grads():
+    """run every queued weight gradient in one grouped launch and store them as .grad"""
+    from . import _native
+    items = list(_PENDING)
+    _PENDING.clear()
+    if not items:
+        return
+    bufs = {}      # id(param) -> [param, fp32 buffer, covered rows]
+    probs = []
+
+    def buf(param):
+        e = bufs.get(id(param))
+        if e is None:
+            e = [param, None, 0]
+            bufs[id(param)] = e
+        return e
+
+    for dy, x, wp, wshape, bp, rows in items:
+        r0, r1 = rows if rows is not None else (0, wshape[0])
+        buf(wp)[2] += r1 - r0
+        if bp is not None:
+            buf(bp)[2] += r1 - r0
+    for e in bufs.values():
+        full = e[2] == e[0].shape[0]
+        e[1] = (torch.empty if full else torch.zeros)(e[0].shape, dtype=torch.float32,
+                                                       device=e[0].device)
+    for dy, x, wp, wshape, bp, rows in items:
+        R, N = dy.shape
+        K = x.shape[1]
+        r0, r1 = rows if rows is not None else (0, wshape[0])
+        dw = bufs[id(wp)][1].view(wshape)[r0:r1].reshape(r1 - r0, K)
+        db = bufs[id(bp)][1][r0:r1] if bp is not None else None
+        probs.append(_WgProblem(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), R, N, K,
+                                _wg_splits(R, N, K), dw.data_ptr(), dw.stride(0),
+                                db.data_ptr() if db is not None else None))
+    arr = (_WgProblem * len(probs))(*probs)
+    lib = _native.load()
+    ws_n = lib.ov3d_wgrad_group_workspace(ctypes.addressof(arr), len(probs))
+    dev = items[0][0].device
+    ws = torch.empty((max(ws_n, 1),), dtype=torch.float32, device=dev)
+    _native.call("ov3d_wgrad_group", ctypes.addressof(arr), len(probs), ws, like=ws)
+    with torch.no_grad():
+        for param, g, _ in bufs.values():
+            if param.grad is None:
+                param.grad = g
+            else:
+                param.grad.add_(g)
+
+
 def weight_grad(dy, x, out=None):
     """dy (R, Cout), x (R, Cin) -> dy^T x (Cout, Cin) in fp32, split-K over R
     (written into `out`, a contiguous fp32 (Cout, Cin) tensor, when given)."""
@@ -170,6 +270,7 @@ class _RowsLinear(Function):
             y = torch.nn.functional.linear(xc, wc, cast_param(b, dt))   # bias in the GEMM epilogue
         ctx.save_for_backward(xc, wc)
         ctx.meta = (x.dtype, w.dtype, b is not None)
+        ctx.params = (w, b)
         return y
 
     @staticmethod
@@ -180,6 +281,10 @@ class _RowsLinear(Function):
         with torch.autocast("cuda", enabled=False):
             dx = (dy @ wc).to(xdt) if ctx.needs_input_grad[0] else None
             want_b = has_b and ctx.needs_input_grad[2]
+            w, b = ctx.params
+            if ctx.needs_input_grad[1] and can_defer(xc, w, b if want_b else None):
+                defer_weight_grad(dy, xc, w, b if want_b else None)
+                return dx, None, None
             if ctx.needs_input_grad[1] and _fused_ok(dy, xc):
                 dw, db = fused_weight_grad(dy, xc, bias=want_b)
                 dw = dw.to(wdt)
@@ -220,16 +325,21 @@ class _InProj(Function):
         ctx.save_for_backward(wc, *saved)
         ctx.meta = (spec, w.dtype, b is not None, tuple(x.dtype for x in xs),
                     tuple(x.shape for x in xs))
+        ctx.params = (w, b)
         return tuple(outs)
 
     @staticmethod
     def backward(ctx, *dys):
         wc, *xcs = ctx.saved_tensors
         spec, wdt, has_b, xdts, xshapes = ctx.meta
+        wp, bp = ctx.params
+        want_b = has_b and ctx.needs_input_grad[1]
+        defer = ctx.needs_input_grad[0] and all(can_defer(xc, wp, bp if want_b else None)
+                                                for xc in xcs)
         dw = torch.empty(wc.shape, dtype=torch.float32, device=wc.device) \
-            if ctx.needs_input_grad[0] else None
+            if ctx.needs_input_grad[0] and not defer else None
         db = torch.empty(wc.shape[0], dtype=torch.float32, device=wc.device) \
-            if has_b and ctx.needs_input_grad[1] else None
+            if want_b and not defer else None
         dxs = []
         with torch.autocast("cuda", enabled=False):
             for i, (dy, xc, (r0, r1)) in enumerate(zip(dys, xcs, spec)):
@@ -238,6 +348,9 @@ class _InProj(Function):
                 dy = dy.reshape(-1, r1 - r0).to(xc.dtype).contiguous()
                 dxs.append((dy @ wc[r0:r1]).to(xdts[i]).view(xshapes[i])
                            if ctx.needs_input_grad[3 + i] else None)
+                if defer:
+                    defer_weight_grad(dy, xc, wp, bp if want_b else None, rows=(r0, r1))
+                    continue
                 if dw is not None and _fused_ok(dy, xc):
                     fused_weight_grad(dy, xc, bias=db is not None, out_w=dw[r0:r1],
                                       out_b=db[r0:r1] if db is not None else None)
