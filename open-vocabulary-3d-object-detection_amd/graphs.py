@@ -56,9 +56,14 @@ class GraphedModel:
         self.flat = _Flat(model, amp_dtype)
         args = tuple(sample_inputs[k] for k in IN_KEYS)
         from . import gemm
-        gemm.SHADOW_CACHE = False      # per-call casts inside the graph (see gemm.cast_param)
-        self.graphed = torch.cuda.make_graphed_callables(self.flat, args,
-                                                         num_warmup_iters=warmup_iters)
+        # per-call casts inside the captured graph (see gemm.cast_param); the process-wide
+        # cache is restored afterwards (the replays do not run the Python cast path)
+        saved, gemm.SHADOW_CACHE = gemm.SHADOW_CACHE, False
+        try:
+            self.graphed = torch.cuda.make_graphed_callables(self.flat, args,
+                                                             num_warmup_iters=warmup_iters)
+        finally:
+            gemm.SHADOW_CACHE = saved
 
     def __call__(self, inputs):
         flat = self.graphed(*(inputs[k] for k in IN_KEYS))
