@@ -72,14 +72,28 @@ class GenericMLP(nn.Module):
 
     def rows(self, x):
         """Channels-last evaluation on (R, Cin) rows -> (R, Cout): each 1x1 conv is one
-        GEMM, BatchNorm1d statistics over the R rows (== over (B, N) positions)."""
-        for m in self.layers:
+        GEMM, BatchNorm1d statistics over the R rows (== over (B, N) positions).  Training
+        under bf16 autocast: BatchNorm + ReLU (+ Dropout) run as one HIP row pass each way
+        (heads.bn_relu_rows)."""
+        from . import heads
+        mods = list(self.layers)
+        i = 0
+        while i < len(mods):
+            m = mods[i]
             if isinstance(m, nn.Conv1d):
                 x = rows_linear(x, m.weight.view(m.weight.shape[0], m.weight.shape[1]), m.bias)
             elif isinstance(m, nn.GroupNorm):
                 raise NotImplementedError("GroupNorm MLPs are not on the reference path")
+            elif isinstance(m, nn.BatchNorm1d) and i + 1 < len(mods):
+                drop = mods[i + 2] if i + 2 < len(mods) and isinstance(mods[i + 2], nn.Dropout) else None
+                if heads.bn_relu_rows_ok(x, m, mods[i + 1], drop):
+                    x = heads.bn_relu_rows(x, m, drop)
+                    i += 3 if drop is not None else 2
+                    continue
+                x = m(x)
             else:
                 x = m(x)
+            i += 1
         return x
 
 

@@ -98,3 +98,42 @@ def test_fused_heads_dropout_and_step(cuda):
     for n, p in model.mlp_heads.named_parameters():
         if p.requires_grad:
             assert p.grad is not None and torch.isfinite(p.grad).all(), n
+
+
+def test_bn_relu_rows_projection_matches_torch(cuda):
+    """encoder -> decoder projection GenericMLP (model_3detr.py:106-120) in training under
+    bf16 autocast: the fused BN + ReLU row launches (heads.bn_relu_rows) against PyTorch's
+    BatchNorm1d + ReLU on the same module: outputs, running statistics and gradients."""
+    import copy
+    from ov3d_amd.helpers import GenericMLP
+    torch.manual_seed(0)
+    m0 = GenericMLP(input_dim=256, hidden_dims=[256, 256], output_dim=256, norm_fn_name="bn1d",
+                    activation="relu", use_conv=True, output_use_activation=True,
+                    output_use_norm=True, output_use_bias=False).to(cuda).train()
+    m1 = copy.deepcopy(m0)
+    x = torch.randn(16384, 256, device=cuda)
+    outs, grads = [], []
+    for m, fused in ((m0, False), (m1, True)):
+        xi = x.clone().requires_grad_()
+        if fused:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = m.rows(xi)
+        else:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = xi
+                for layer in m.layers:   # plain module chain (reference semantics)
+                    if isinstance(layer, torch.nn.Conv1d):
+                        y = y @ layer.weight.view(layer.weight.shape[0], -1).t().to(y.dtype)
+                    else:
+                        y = layer(y)
+        (y.float() * torch.linspace(-1, 1, 256, device=cuda)).sum().backward()
+        outs.append(y.float().detach())
+        grads.append([xi.grad] + [p.grad for p in m.parameters()])
+    assert _rel(outs[1], outs[0]) < 2e-2
+    for bn0, bn1 in zip([l for l in m0.layers if isinstance(l, torch.nn.BatchNorm1d)],
+                        [l for l in m1.layers if isinstance(l, torch.nn.BatchNorm1d)]):
+        assert _rel(bn1.running_mean, bn0.running_mean) < 1e-2
+        assert _rel(bn1.running_var, bn0.running_var) < 1e-2
+        assert int(bn1.num_batches_tracked) == int(bn0.num_batches_tracked) == 1
+    for a, b in zip(grads[1], grads[0]):
+        assert _rel(a, b) < 3e-2
