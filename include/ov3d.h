@@ -367,6 +367,12 @@ int ov3d_resnorm_fwd(long long R, int C, const void* src, int src_bf16, const vo
  * dxb (fp32) or NULL -> dsrc (fp32), dy (bf16 | fp32), dpos (= dxap), dga/dba/dgb/dbb.
  * partials: (nparts, 4, C) f32 workspace with nparts = ov3d_resnorm_bwd_parts(R, C). */
 int ov3d_resnorm_bwd_parts(long long R, int C);
+/* FFN activation h = dropout(relu(y)) over contiguous bf16 (R, C) rows (transformer.py
+ * FFN), dropout keep = hash of (*seed, site, r, c); backward dy = dh / (1-p) where h > 0 */
+int ov3d_relu_dropout_fwd(const void* y, long long R, int C, float dropout_p, const int64_t* seed,
+                          int site, void* h, void* stream);
+int ov3d_relu_dropout_bwd(const void* h, const void* dh, long long n, float dropout_p, void* dy,
+                          void* stream);
 int ov3d_resnorm_bwd(long long R, int C, const float* s, const float* mean, const float* rstd,
                      const float* ds, const void* dxa, const void* dxap, const float* dxb,
                      const float* ga, const float* gb, float dropout_p, const int64_t* seed,

@@ -56,6 +56,8 @@ _SIGS = {
     "ov3d_set_loss_bwd": "pppppppppppp",
     "ov3d_adamw_step": "pppipfpddfpip",
     "ov3d_adamw_set_grads": "pipp",
+    "ov3d_relu_dropout_fwd": "plifpipp",
+    "ov3d_relu_dropout_bwd": "pplfpp",
     "ov3d_resnorm_fwd": "lipipifpipppippfppppppp",
     "ov3d_resnorm_bwd": "lipppppppppfpippipipippppp",
 }

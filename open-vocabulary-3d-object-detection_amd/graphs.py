@@ -139,8 +139,9 @@ class StepGraph:
 
     def step(self, batch, next_batch=None):
         cur = torch.cuda.current_stream()
-        for k, v in self.static.items():
-            v.copy_(batch[k], non_blocking=True)
+        keys = list(self.static)
+        torch._foreach_copy_([self.static[k] for k in keys], [batch[k] for k in keys],
+                             non_blocking=True)   # one multi-tensor launch per dtype
         if not self.prefetch:
             self.graph.replay()
             return self.loss

@@ -157,8 +157,41 @@ def resnorm(pend, norm_a=None, pos=None, want_a=True, want_ap=False, norm_b=None
 
 def sites(module, n):
     """n dropout hash sites owned by `module` (allocated once)"""
-    s = getattr(module, "_resnorm_sites", None)
-    if s is None:
-        s = tuple(flash.new_site() for _ in range(n))
+    s = getattr(module, "_resnorm_sites", ())
+    if len(s) < n:
+        s = tuple(s) + tuple(flash.new_site() for _ in range(n - len(s)))
         module._resnorm_sites = s
-    return s
+    return s[:n]
+
+
+class _ReluDropout(torch.autograd.Function):
+    """h = dropout_p(relu(y)) on bf16 rows in one launch each way (csrc/resnorm.hip)."""
+
+    @staticmethod
+    def forward(ctx, y, p, site):
+        C = y.shape[-1]
+        yr = y.reshape(-1, C).contiguous()
+        h = torch.empty_like(yr)
+        seed = flash._seed(y.device) if p > 0 else None
+        _native.call("ov3d_relu_dropout_fwd", yr, yr.shape[0], C, float(p), seed, site, h, like=yr)
+        ctx.save_for_backward(h)
+        ctx.p = float(p)
+        ctx.yshape = y.shape
+        return h.view(y.shape)
+
+    @staticmethod
+    def backward(ctx, dh):
+        (h,) = ctx.saved_tensors
+        dh = dh.to(h.dtype).reshape(h.shape).contiguous()
+        dy = torch.empty_like(h)
+        _native.call("ov3d_relu_dropout_bwd", h, dh, h.numel(), ctx.p, dy, like=h)
+        return dy.view(ctx.yshape), None, None
+
+
+def ffn_act(y, activation, dropout, site):
+    """dropout(activation(y)) of a transformer FFN: one HIP launch for bf16 ReLU rows."""
+    if (isinstance(activation, nn.ReLU) and y.is_cuda and y.dtype == torch.bfloat16
+            and y.shape[-1] % 8 == 0):
+        p = dropout.p if dropout.training else 0.0
+        return _ReluDropout.apply(y, p, site)
+    return dropout(activation(y))

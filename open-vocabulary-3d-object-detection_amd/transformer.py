@@ -112,14 +112,15 @@ class TransformerEncoderLayer(nn.Module):
     def forward_fused(self, pend, src_mask=None, pos=None):
         """bf16 training / eval step on a Pending residual (resnorm.py); -> Pending."""
         p1, p2 = (self.dropout1.p, self.dropout2.p) if self.training else (0.0, 0.0)
-        site1, site2 = rn.sites(self, 2)
+        site1, site2, site_ffn = rn.sites(self, 3)
         s, x, xp, _ = rn.resnorm(pend, self.norm1, pos=pos, want_a=True, want_ap=pos is not None)
         qk = xp if pos is not None else x
         y = self.self_attn(qk, qk, x, attn_mask=src_mask)
         if not self.use_ffn:
             return rn.Pending(s, y, p1, site1)
         s, x, _, _ = rn.resnorm(rn.Pending(s, y, p1, site1), self.norm2)
-        h = self.dropout(self.activation(rows_linear(x, self.linear1.weight, self.linear1.bias)))
+        h = rn.ffn_act(rows_linear(x, self.linear1.weight, self.linear1.bias), self.activation,
+                       self.dropout, site_ffn)
         return rn.Pending(s, rows_linear(h, self.linear2.weight, self.linear2.bias), p2, site2)
 
     def fused_ok(self, x):
@@ -170,7 +171,7 @@ class TransformerDecoderLayer(nn.Module):
         the layer output (resnorm.py)."""
         p1, p2, p3 = ((self.dropout1.p, self.dropout2.p, self.dropout3.p) if self.training
                       else (0.0, 0.0, 0.0))
-        site1, site2, site3 = rn.sites(self, 3)
+        site1, site2, site3, site_ffn = rn.sites(self, 4)
         qk = xp if query_pos is not None else x
         y = self.self_attn(qk, qk, x, attn_mask=tgt_mask)
         s, x2, q, _ = rn.resnorm(rn.Pending(s, y, p1, site1), self.norm2, pos=query_pos,
@@ -178,7 +179,8 @@ class TransformerDecoderLayer(nn.Module):
         y = self.multihead_attn(q if query_pos is not None else x2, memory_pos, memory,
                                 attn_mask=memory_mask)
         s, x3, _, _ = rn.resnorm(rn.Pending(s, y, p2, site2), self.norm3)
-        h = self.dropout(self.activation(rows_linear(x3, self.linear1.weight, self.linear1.bias)))
+        h = rn.ffn_act(rows_linear(x3, self.linear1.weight, self.linear1.bias), self.activation,
+                       self.dropout, site_ffn)
         return rn.Pending(s, rows_linear(h, self.linear2.weight, self.linear2.bias), p3, site3)
 
     def fused_ok(self, x):

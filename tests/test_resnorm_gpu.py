@@ -147,3 +147,23 @@ def test_encoder_decoder_fused_vs_plain_bf16(cuda):
         e_fused = _rel(res["fused"][i], ref)
         assert e_fused <= 1.5 * e_plain + 5e-3, (i, e_fused, e_plain)
         assert e_fused < 0.1, (i, e_fused)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_relu_dropout_matches_torch(cuda, p):
+    from ov3d_amd import attention as flash
+    from ov3d_amd import resnorm as rn
+    R, C = 4096, 128
+    y = torch.randn(R, C, device=cuda).bfloat16().requires_grad_()
+    site = flash.new_site()
+    drop = torch.nn.Dropout(p).train()
+    h = rn.ffn_act(y, torch.nn.ReLU(), drop, site)
+    g = torch.randn(R, C, device=cuda).bfloat16()
+    h.backward(g)
+    keep = row_keep(flash._seed(cuda).item(), site, R, C, p, cuda)
+    a = torch.relu(y.detach().float())
+    ref = torch.where(keep, (a * (1 / (1 - p))).bfloat16().float(), torch.zeros_like(a)) if p > 0 \
+        else a.bfloat16().float()
+    assert torch.equal(h.float(), ref)
+    gref = torch.where((ref > 0), g.float() * (1 / (1 - p)), torch.zeros_like(a)).bfloat16()
+    assert torch.equal(y.grad, gref)
