@@ -70,7 +70,7 @@ def _rows(src, off, E):
 
 class _Attention(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, spec, dims, H, dropout_p, site, *srcs):
+    def forward(ctx, spec, dims, H, dropout_p, site, ext, token, *srcs):
         (qi, qo), (ki, ko), (vi, vo) = spec
         q, k, v = srcs[qi], srcs[ki], srcs[vi]
         Lq, Lk, B = dims
@@ -93,6 +93,7 @@ class _Attention(torch.autograd.Function):
             raise _native.NativeError(f"ov3d_attn_fwd failed with status {rc}")
         ctx.save_for_backward(*srcs, o, lse)
         ctx.meta = (spec, dims, H, float(dropout_p), site, len(srcs))
+        ctx.ext = ext
         return o
 
     @staticmethod
@@ -104,7 +105,11 @@ class _Attention(torch.autograd.Function):
         q, k, v = srcs[qi], srcs[ki], srcs[vi]
         E = H * HEAD_DIM
         do = do.to(torch.bfloat16).contiguous()
-        grads = [torch.empty_like(s) for s in srcs]   # every column is written below
+        ext, tok_grad = ctx.ext if ctx.ext is not None else ((None,) * n, None)
+        # every column of an own source is written below; external sources (shared K / V
+        # of the decoder layers, transformer.MemoryKV) get their column block written into
+        # the caller's gradient buffer
+        grads = [e if e is not None else torch.empty_like(s) for s, e in zip(srcs, ext)]
         dvec = torch.empty((B * H, Lq), dtype=torch.float32, device=q.device)
         nsplit = _split(Lq, Lk, B * H)
         ws_n = _native.load().ov3d_attn_fwd_workspace(B, H, Lq, Lk, nsplit)
@@ -122,27 +127,39 @@ class _Attention(torch.autograd.Function):
             _native._stream(q))
         if rc:
             raise _native.NativeError(f"ov3d_attn_bwd failed with status {rc}")
-        return (None, None, None, None, None, *grads)
+        grads = [None if e is not None else g for g, e in zip(grads, ext)]
+        return (None, None, None, None, None, None, tok_grad, *grads)
 
 
-def attention_packed(srcs, spec, Lq, Lk, num_heads, dropout_p=0.0, site=0):
+def attention_packed(srcs, spec, Lq, Lk, num_heads, dropout_p=0.0, site=0, ext=None):
     """Attention over column ranges of projection outputs.
 
     srcs: contiguous (L, B, n*E) tensors (their rows l*B + b), spec: ((src index, column
     offset) for q, for k, for v).  Every column of every source must belong to one of
     q / k / v (their gradients are written column range by column range, not zeroed).
-    -> (Lq, B, E) bf16."""
+    ext: optional (grad buffers per source or None, token, token gradient): a source with
+    a buffer is shared with other calls (it may have more columns than this call reads);
+    its gradient columns go into the buffer and ``token`` (an output of the producer of
+    the shared sources) carries the dependency instead.  -> (Lq, B, E) bf16."""
     E = num_heads * HEAD_DIM
     B = srcs[spec[0][0]].shape[1]
+    bufs = ext[0] if ext is not None else (None,) * len(srcs)
     for i, s in enumerate(srcs):
         cols = sorted(off for j, off in spec if j == i)
+        shared = bufs[i] is not None
         if not s.is_contiguous() or s.dim() != 3 or s.shape[1] != B or \
-                cols != list(range(0, s.shape[-1], E)):
+                (not shared and cols != list(range(0, s.shape[-1], E))) or \
+                (shared and (bufs[i].shape != s.shape or any(c + E > s.shape[-1] for c in cols))):
             raise ValueError("attention_packed: sources must be contiguous (L, B, n*E) tensors "
                              "fully covered by the q / k / v column ranges")
         _native.check_device(s, "attention input")
     srcs = [s if s.dtype == torch.bfloat16 else s.to(torch.bfloat16) for s in srcs]
-    return _Attention.apply(tuple(spec), (Lq, Lk, B), num_heads, dropout_p, site, *srcs)
+    if ext is None:
+        return _Attention.apply(tuple(spec), (Lq, Lk, B), num_heads, dropout_p, site, None, None,
+                                *srcs)
+    bufs, token, tok_grad = ext
+    return _Attention.apply(tuple(spec), (Lq, Lk, B), num_heads, dropout_p, site,
+                            (tuple(bufs), tok_grad), token, *srcs)
 
 
 def attention(q, k, v, num_heads, dropout_p=0.0, site=0):

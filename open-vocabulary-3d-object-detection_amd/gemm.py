@@ -336,9 +336,11 @@ class _InProj(Function):
         want_b = has_b and ctx.needs_input_grad[1]
         defer = ctx.needs_input_grad[0] and all(can_defer(xc, wp, bp if want_b else None)
                                                 for xc in xcs)
-        dw = torch.empty(wc.shape, dtype=torch.float32, device=wc.device) \
+        full = sum(r1 - r0 for r0, r1 in spec) == wc.shape[0]   # else zero the other rows
+        alloc = torch.empty if full else torch.zeros
+        dw = alloc(wc.shape, dtype=torch.float32, device=wc.device) \
             if ctx.needs_input_grad[0] and not defer else None
-        db = torch.empty(wc.shape[0], dtype=torch.float32, device=wc.device) \
+        db = alloc(wc.shape[0], dtype=torch.float32, device=wc.device) \
             if want_b and not defer else None
         dxs = []
         with torch.autocast("cuda", enabled=False):

@@ -19,7 +19,8 @@ from torch import Tensor, nn
 
 from . import attention as flash
 from . import resnorm as rn
-from .gemm import in_projection, rows_linear
+from . import gemm
+from .gemm import cast_param, in_projection, rows_linear
 from .helpers import ACTIVATION_DICT, NORM_DICT, get_clones
 
 
@@ -72,6 +73,97 @@ class MultiheadAttention(nn.Module):
                                              dropout_p=self.dropout if self.training else 0.0)
         out = out.permute(2, 0, 1, 3).reshape(L, B, E)
         return rows_linear(out, self.out_proj.weight, self.out_proj.bias)
+
+
+    def forward_kv(self, query, kv, idx):
+        """Cross attention whose K / V projections of the memory were computed for all decoder
+        layers at once (MemoryKV): kv = (K_all, V_all, dK_all, dV_all, token, token_grad),
+        this layer's block = columns idx*E .. (idx+1)*E."""
+        L, B, E = query.shape
+        K_all, V_all, dK, dV, token, tok_grad = kv
+        S = K_all.shape[0]
+        q = in_projection(self.in_proj_weight, self.in_proj_bias, ((query, 0, E),))[0]
+        out = flash.attention_packed(
+            [q, K_all, V_all], ((0, 0), (1, idx * E), (2, idx * E)), L, S, self.num_heads,
+            dropout_p=self.dropout if self.training else 0.0, site=self.site,
+            ext=((None, dK, dV), token, tok_grad))
+        return rows_linear(out, self.out_proj.weight, self.out_proj.bias)
+
+
+class _MemoryKV(torch.autograd.Function):
+    """K and V of the decoder's cross attention for all L layers in two GEMMs:
+    K_all = (memory + pos) [Wk_0 .. Wk_{L-1}]^T + bk, V_all = memory [Wv_0 ..]^T + bv, each
+    (S, B, L*E) bf16 (reference transformer.py:365-372 projects the same memory once per
+    layer).  The layers' attention backward writes dK / dV column blocks into the shared
+    buffers; the ``token`` output carries the dependency so this backward runs after all of
+    them: d memory = dV_all Wv_all + dK_all Wk_all (one GEMM + one accumulating GEMM), and
+    the K / V rows of every in_proj weight gradient (deferred with the others when
+    gemm.DEFER_WGRAD, else returned)."""
+
+    @staticmethod
+    def forward(ctx, memory, pos, E, *params):
+        ws, bs = params[0::2], params[1::2]
+        S, B, C = memory.shape
+        bf = torch.bfloat16
+        mem = memory.reshape(S * B, C).to(bf).contiguous()
+        mpos = (memory + pos).reshape(S * B, C).to(bf).contiguous() if pos is not None else mem
+        Wk = torch.cat([cast_param(w, bf)[E:2 * E] for w in ws])
+        Wv = torch.cat([cast_param(w, bf)[2 * E:] for w in ws])
+        bk = torch.cat([cast_param(b, bf)[E:2 * E] for b in bs])
+        bv = torch.cat([cast_param(b, bf)[2 * E:] for b in bs])
+        n = len(ws) * E
+        K_all = torch.addmm(bk, mpos, Wk.t()).view(S, B, n)
+        V_all = torch.addmm(bv, mem, Wv.t()).view(S, B, n)
+        dK, dV = torch.empty_like(K_all), torch.empty_like(V_all)
+        token = torch.empty((), dtype=torch.float32, device=memory.device)
+        tok_grad = torch.zeros((), dtype=torch.float32, device=memory.device)
+        ctx.save_for_backward(mem, mpos, Wk, Wv)
+        ctx.meta = (E, memory.dtype, pos is not None and pos.requires_grad, len(ws), S * B, C)
+        ctx.bufs = (dK, dV)
+        ctx.params = params
+        ctx.mark_non_differentiable(K_all, V_all, dK, dV, tok_grad)
+        return K_all, V_all, dK, dV, token, tok_grad
+
+    @staticmethod
+    def backward(ctx, _k, _v, _dk, _dv, _tok, _tg):
+        mem, mpos, Wk, Wv = ctx.saved_tensors
+        E, mdt, pos_grad, L, R, C = ctx.meta
+        dK, dV = (t.view(R, L * E) for t in ctx.bufs)
+        params = ctx.params
+        with torch.autocast("cuda", enabled=False):
+            dmk = dK @ Wk
+            dmem = torch.addmm(dmk, dV, Wv) if not pos_grad else dV @ Wv + dmk
+            grads = [None] * len(params)
+            for l in range(L):
+                w, b = params[2 * l], params[2 * l + 1]
+                for blk, (dy, x) in enumerate(((dK, mpos), (dV, mem))):
+                    r0 = (1 + blk) * E
+                    dyl = dy[:, l * E:(l + 1) * E]
+                    if gemm.can_defer(x, w, b):
+                        gemm.defer_weight_grad(dyl, x, w, b, rows=(r0, r0 + E))
+                        continue
+                    if grads[2 * l] is None:
+                        grads[2 * l] = torch.zeros(w.shape, dtype=torch.float32, device=w.device)
+                        grads[2 * l + 1] = torch.zeros(b.shape, dtype=torch.float32, device=b.device)
+                    gemm.fused_weight_grad(dyl, x, bias=True, out_w=grads[2 * l][r0:r0 + E],
+                                           out_b=grads[2 * l + 1][r0:r0 + E])
+        shape = ctx.bufs[0].shape[:2] + (C,)
+        dpos = dmk.view(shape).to(mdt) if pos_grad else None
+        return (dmem.view(shape).to(mdt), dpos, None, *grads)
+
+
+def memory_kv_ok(layers, memory):
+    """the batched K / V path: bf16 autocast on the device, every cross attention a flash
+    shape (head_dim 64, no mask) with its own in_proj weight / bias"""
+    if not (memory.is_cuda and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        return False
+    for l in layers:
+        a = getattr(l, "multihead_attn", None)
+        if not isinstance(a, MultiheadAttention) or a.embed_dim != a.num_heads * flash.HEAD_DIM \
+                or a.in_proj_bias is None:
+            return False
+    return True
 
 
 class TransformerEncoderLayer(nn.Module):
@@ -166,7 +258,7 @@ class TransformerDecoderLayer(nn.Module):
         return tgt, None
 
     def forward_fused(self, s, x, xp, memory, memory_pos, query_pos=None, tgt_mask=None,
-                      memory_mask=None):
+                      memory_mask=None, kv=None, idx=0):
         """bf16 step from norm1's outputs (x = norm1(tgt), xp = x + query_pos) -> Pending of
         the layer output (resnorm.py)."""
         p1, p2, p3 = ((self.dropout1.p, self.dropout2.p, self.dropout3.p) if self.training
@@ -176,8 +268,11 @@ class TransformerDecoderLayer(nn.Module):
         y = self.self_attn(qk, qk, x, attn_mask=tgt_mask)
         s, x2, q, _ = rn.resnorm(rn.Pending(s, y, p1, site1), self.norm2, pos=query_pos,
                                  want_a=query_pos is None, want_ap=query_pos is not None)
-        y = self.multihead_attn(q if query_pos is not None else x2, memory_pos, memory,
-                                attn_mask=memory_mask)
+        qx = q if query_pos is not None else x2
+        if kv is not None and memory_mask is None:
+            y = self.multihead_attn.forward_kv(qx, kv, idx)
+        else:
+            y = self.multihead_attn(qx, memory_pos, memory, attn_mask=memory_mask)
         s, x3, _, _ = rn.resnorm(rn.Pending(s, y, p2, site2), self.norm3)
         h = rn.ffn_act(rows_linear(x3, self.linear1.weight, self.linear1.bias), self.activation,
                        self.dropout, site_ffn)
@@ -298,10 +393,10 @@ class TransformerDecoder(nn.Module):
                 return_attn_weights=False):
         if transpose_swap or return_attn_weights:
             raise NotImplementedError
-        memory_pos = memory if pos is None else memory + pos
         if all(hasattr(l, "fused_ok") and l.fused_ok(tgt) for l in self.layers) and \
                 (self.norm is None or rn.supported(tgt, self.norm)):
-            return self._forward_fused(tgt, memory, memory_pos, query_pos, tgt_mask, memory_mask)
+            return self._forward_fused(tgt, memory, pos, query_pos, tgt_mask, memory_mask)
+        memory_pos = memory if pos is None else memory + pos
         out = tgt
         inter = []
         for layer in self.layers:
@@ -317,12 +412,22 @@ class TransformerDecoder(nn.Module):
             return torch.stack(inter), []
         return out, []
 
-    def _forward_fused(self, tgt, memory, memory_pos, query_pos, tgt_mask, memory_mask):
+    def _forward_fused(self, tgt, memory, pos, query_pos, tgt_mask, memory_mask):
         """bf16: one resnorm launch per sub-layer boundary; the decoder norm of layer i's
         output shares the launch with layer i+1's norm1 (same row statistics)."""
-        # K / V projection inputs are cast to bf16 once for the 8 layers
-        memory = memory.to(torch.bfloat16)
-        memory_pos = memory_pos.to(torch.bfloat16)
+        kv = None
+        memory_pos = None
+        if memory_mask is None and memory_kv_ok(self.layers, memory):
+            # K / V of all layers' cross attention: two GEMMs over the memory (_MemoryKV)
+            params = []
+            for l in self.layers:
+                params += [l.multihead_attn.in_proj_weight, l.multihead_attn.in_proj_bias]
+            kv = _MemoryKV.apply(memory, pos, self.layers[0].multihead_attn.embed_dim, *params)
+        else:
+            memory_pos = memory if pos is None else memory + pos
+            # K / V projection inputs are cast to bf16 once for the 8 layers
+            memory = memory.to(torch.bfloat16)
+            memory_pos = memory_pos.to(torch.bfloat16)
         pend = rn.Pending(tgt, None, 0.0, 0)
         inter = []
         dec_norm = self.norm if self.return_intermediate else None
@@ -332,8 +437,11 @@ class TransformerDecoder(nn.Module):
                                       norm_b=dec_norm if i > 0 else None)
             if i > 0 and dec_norm is not None:
                 inter.append(xd)
+            kvi = None
+            if kv is not None:   # the token gradient is returned once (by layer 0)
+                kvi = kv[:5] + ((kv[5] if i == 0 else None),)
             pend = layer.forward_fused(s, x, xp, memory, memory_pos, query_pos, tgt_mask,
-                                       memory_mask)
+                                       memory_mask, kv=kvi, idx=i)
         s, _, _, xd = rn.resnorm(pend, norm_b=self.norm)
         out = xd if self.norm is not None else s
         if self.return_intermediate:
