@@ -396,6 +396,10 @@ typedef struct {
     float lr, weight_decay;
 } ov3d_adamw_tensor;
 int ov3d_adamw_chunk(void);
+/* n device-to-device copies (bytes[i] from srcs[i] to dsts[i], host arrays) in one launch
+ * per 32 (the step graph's static input batch) */
+int ov3d_multi_copy(int n, const void* const* srcs, void* const* dsts, const long long* bytes,
+                    void* stream);
 /* table[i].grad = grads[i] (host array of device pointers) by kernel arguments: graph-safe */
 int ov3d_adamw_set_grads(ov3d_adamw_tensor* table, int ntensors, float* const* grads, void* stream);
 int ov3d_adamw_step(const ov3d_adamw_tensor* table, const int* blk_t, const int* blk_c, int nblocks,

@@ -56,6 +56,7 @@ _SIGS = {
     "ov3d_set_loss_bwd": "pppppppppppp",
     "ov3d_adamw_step": "pppipfpddfpip",
     "ov3d_adamw_set_grads": "pipp",
+    "ov3d_multi_copy": "ipppp",
     "ov3d_relu_dropout_fwd": "plifpipp",
     "ov3d_relu_dropout_bwd": "pplfpp",
     "ov3d_resnorm_fwd": "lipipifpipppippfppppppp",
@@ -188,3 +189,20 @@ def call(name, *args, like):
         rec.append((ev0, ev1, tuple(a for a in args if isinstance(a, int))[:3]))
     if rc != 0:
         raise NativeError(f"{name} failed with status {rc}")
+
+
+def multi_copy(dsts, srcs):
+    """copy every src tensor into the same-size dst tensor (contiguous, device) in one launch"""
+    n = len(dsts)
+    if n == 0:
+        return
+    for d, s in zip(dsts, srcs):
+        if d.nbytes != s.nbytes or not (d.is_contiguous() and s.is_contiguous()) or d.dtype != s.dtype:
+            raise ValueError("multi_copy: contiguous same-dtype, same-size tensors only")
+        check_device(d, "multi_copy dst")
+        check_device(s, "multi_copy src")
+    sp = (ctypes.c_void_p * n)(*[s.data_ptr() for s in srcs])
+    dp = (ctypes.c_void_p * n)(*[d.data_ptr() for d in dsts])
+    nb = (ctypes.c_longlong * n)(*[d.nbytes for d in dsts])
+    call("ov3d_multi_copy", n, ctypes.addressof(sp), ctypes.addressof(dp), ctypes.addressof(nb),
+         like=dsts[0])

@@ -157,3 +157,57 @@ extern "C" int ov3d_adamw_step(const ov3d_adamw_tensor* table, const int* blk_t,
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }
+
+// ---- several device buffers copied by ONE launch (graphs.StepGraph's static batch) ----
+namespace {
+constexpr int kCopyMax = 32;
+struct CopyList {
+    const void* src[kCopyMax];
+    void* dst[kCopyMax];
+    long long bytes[kCopyMax];
+    long long blk[kCopyMax + 1];   // workgroup offsets, 16 B x 256 threads x 4 per workgroup
+    int n;
+};
+__global__ void __launch_bounds__(256) multi_copy_kernel(CopyList c) {
+    const long long b = blockIdx.x;
+    int i = 0;
+    while (i + 1 < c.n && b >= c.blk[i + 1]) ++i;
+    const long long base = (b - c.blk[i]) * 256 * 4 * 16;
+    const char* s = (const char*)c.src[i];
+    char* d = (char*)c.dst[i];
+    const long long nb = c.bytes[i];
+    const bool vec = ((uintptr_t)s % 16 == 0) && ((uintptr_t)d % 16 == 0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const long long o = base + ((long long)u * 256 + threadIdx.x) * 16;
+        if (o + 16 <= nb && vec) {
+            *reinterpret_cast<uint4*>(d + o) = *reinterpret_cast<const uint4*>(s + o);
+        } else {
+            for (long long k = o; k < o + 16 && k < nb; ++k) d[k] = s[k];
+        }
+    }
+}
+}  // namespace
+
+extern "C" int ov3d_multi_copy(int n, const void* const* srcs, void* const* dsts,
+                               const long long* bytes, void* stream) {
+    if (n < 0 || (n > 0 && (!srcs || !dsts || !bytes))) return OV3D_EINVAL;
+    for (int first = 0; first < n; first += kCopyMax) {
+        CopyList c;
+        c.n = n - first < kCopyMax ? n - first : kCopyMax;
+        long long blk = 0;
+        for (int j = 0; j < c.n; ++j) {
+            c.src[j] = srcs[first + j];
+            c.dst[j] = dsts[first + j];
+            c.bytes[j] = bytes[first + j];
+            if (c.bytes[j] < 0 || (c.bytes[j] > 0 && (!c.src[j] || !c.dst[j]))) return OV3D_EINVAL;
+            c.blk[j] = blk;
+            blk += (c.bytes[j] + 256 * 4 * 16 - 1) / (256 * 4 * 16);
+        }
+        c.blk[c.n] = blk;
+        if (blk == 0) continue;
+        multi_copy_kernel<<<(unsigned)blk, 256, 0, ov3d_stream(stream)>>>(c);
+        OV3D_LAUNCH_CHECK();
+    }
+    return OV3D_OK;
+}

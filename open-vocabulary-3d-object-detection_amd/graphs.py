@@ -140,8 +140,14 @@ class StepGraph:
     def step(self, batch, next_batch=None):
         cur = torch.cuda.current_stream()
         keys = list(self.static)
-        torch._foreach_copy_([self.static[k] for k in keys], [batch[k] for k in keys],
-                             non_blocking=True)   # one multi-tensor launch per dtype
+        srcs = [batch[k] for k in keys]
+        if all(s.is_cuda and s.is_contiguous() and s.dtype == self.static[k].dtype
+               for k, s in zip(keys, srcs)):
+            from . import _native
+            _native.multi_copy([self.static[k] for k in keys], srcs)   # one launch
+        else:
+            for k, s in zip(keys, srcs):
+                self.static[k].copy_(s, non_blocking=True)
         if not self.prefetch:
             self.graph.replay()
             return self.loss

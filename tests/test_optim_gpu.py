@@ -98,3 +98,20 @@ def test_fused_adamw_graph_replay_equals_eager(cuda):
     torch.cuda.synchronize()
     for a, b in zip(pa, pb):
         assert torch.allclose(a, b, rtol=1e-6, atol=1e-8)
+
+
+def test_multi_copy_ragged(cuda):
+    """ov3d_multi_copy (graphs.StepGraph's batch copy): ragged sizes, odd byte counts, mixed
+    dtypes, more than one launch's worth of tensors"""
+    from ov3d_amd import _native
+    g = torch.Generator().manual_seed(0)
+    srcs, dsts = [], []
+    for i in range(40):
+        n = int(torch.randint(1, 70000, (1,), generator=g))
+        dt = (torch.float32, torch.int64, torch.uint8, torch.bfloat16)[i % 4]
+        s = (torch.rand(n, generator=g) * 100).to(dt).to(cuda)
+        srcs.append(s)
+        dsts.append(torch.empty_like(s))
+    _native.multi_copy(dsts, srcs)
+    for d, s in zip(dsts, srcs):
+        assert torch.equal(d, s)
