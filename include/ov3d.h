@@ -406,6 +406,25 @@ int ov3d_adamw_step(const ov3d_adamw_tensor* table, const int* blk_t, const int*
                     double* partials, float max_norm, float* step, double beta1, double beta2,
                     float eps, double* coefs, int write_grad, void* stream);
 
+
+/* ---- Box parametrisation of the heads (model_3detr.py BoxProcessor + corners) ----
+ * raw: (R, ld) rows [center 3 | size 3 | angle logits NB | angle residual NB], R = L*B*Q
+ * rows (l, b, q); qxyz (B, Q, 3), dmin / dmax (B, 3); logits (R, T) or NULL (no probs).
+ * Outputs (R, ...) contiguous fp32: center_n / center_u / size_n / size_u (3), angle
+ * logits / residual_normalized / residual (NB), angle (1), corners (8, 3), sem_prob (T-1),
+ * objectness (1).  Backward: any gradient may be NULL; writes draw (R, ldd) columns 0..6+2NB. */
+int ov3d_box_param_fwd(long long R, int B, int Q, int NB, int T, const float* raw, long long ld,
+                       const float* qxyz, const float* dmin, const float* dmax,
+                       const float* logits, float* center_n, float* center_u, float* size_n,
+                       float* size_u, float* alog, float* ares_n, float* ares, float* angle,
+                       float* corners, float* sem_prob, float* obj_prob, void* stream);
+int ov3d_box_param_bwd(long long R, int B, int Q, int NB, const float* raw, long long ld,
+                       const float* qxyz, const float* dmin, const float* dmax,
+                       const float* g_center_n, const float* g_center_u, const float* g_size_n,
+                       const float* g_size_u, const float* g_alog, const float* g_ares_n,
+                       const float* g_ares, const float* g_angle, const float* g_corners,
+                       float* draw, long long ldd, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

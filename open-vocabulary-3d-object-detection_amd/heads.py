@@ -253,7 +253,7 @@ def fused_heads(pack, rows):
         params += ts
     out_v, out_s = _Heads.apply(rows, pack, p1, p2, w3v.view(w3v.shape[0], -1), b3v, w3s, b3s,
                                 *params)
-    res = {HEAD_ORDER[0]: out_v}
+    res = {HEAD_ORDER[0]: out_v, "_raw": out_s}   # _raw: [center | size | angle cls | angle res]
     o = 0
     for name, n in zip(HEAD_ORDER[1:], outs):
         res[name] = out_s[:, o:o + n]

@@ -22,6 +22,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+from . import _native
 from . import attention as flash
 from . import heads as heads_mod
 from . import pointnet2_utils as pu
@@ -65,6 +66,44 @@ class BoxProcessor:
     def box_parametrization_to_corners(self, box_center_unnorm, box_size_unnorm, box_angle):
         return self.dataset_config.box_parametrization_to_corners(box_center_unnorm, box_size_unnorm,
                                                                   box_angle)
+
+
+class _BoxParam(torch.autograd.Function):
+    """BoxProcessor (model_3detr.py:19-69) + corners for all L*B*Q proposals in one HIP launch
+    each way (csrc/boxparam.hip) from the fused heads' raw rows
+    [center 3 | size 3 | angle logits NB | angle residual NB]."""
+
+    @staticmethod
+    def forward(ctx, raw, qxyz, dmin, dmax, logits, B, Q, NB):
+        R = raw.shape[0]
+        dev = raw.device
+        T = logits.shape[-1]
+        f = dict(dtype=torch.float32, device=dev)
+        outs = [torch.empty((R, 3), **f) for _ in range(4)] + \
+            [torch.empty((R, NB), **f) for _ in range(3)] + \
+            [torch.empty((R,), **f), torch.empty((R, 8, 3), **f),
+             torch.empty((R, T - 1), **f), torch.empty((R,), **f)]
+        qxyz, dmin, dmax = (t.float().contiguous() for t in (qxyz, dmin, dmax))
+        lg = logits.detach().float().reshape(R, T).contiguous()
+        _native.call("ov3d_box_param_fwd", R, B, Q, NB, T, raw, raw.stride(0), qxyz, dmin, dmax,
+                     lg, *outs, like=raw)
+        ctx.save_for_backward(raw, qxyz, dmin, dmax)
+        ctx.meta = (B, Q, NB)
+        ctx.mark_non_differentiable(outs[9], outs[10])
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        raw, qxyz, dmin, dmax = ctx.saved_tensors
+        B, Q, NB = ctx.meta
+        R = raw.shape[0]
+        g = [t.float().contiguous() if t is not None else None for t in grads[:9]]
+        draw = torch.empty_like(raw)
+        if draw.shape[1] > 6 + 2 * NB:
+            draw.zero_()
+        _native.call("ov3d_box_param_bwd", R, B, Q, NB, raw, raw.stride(0), qxyz, dmin, dmax, *g,
+                     draw, draw.stride(0), like=raw)
+        return draw, None, None, None, None, None, None, None
 
 
 class Model3DETR(nn.Module):
@@ -165,6 +204,9 @@ class Model3DETR(nn.Module):
     def _box_predictions(self, query_xyz, point_cloud_dims, rows, dims_lqb, pre=None):
         L, Q, B = dims_lqb
         heads = self.mlp_heads
+        if pre is not None and "_raw" in pre and pre["_raw"].is_cuda and \
+                pre["_raw"].dtype == torch.float32 and pre["_raw"].stride(1) == 1:
+            return self._box_predictions_fused(query_xyz, point_cloud_dims, pre, L, Q, B)
 
         def head(name):
             if pre is not None:
@@ -210,6 +252,29 @@ class Model3DETR(nn.Module):
         outs = [{k: per_key[k][l] for k in stacked} for l in range(L)]
         # "_layers_stacked": the same tensors stacked over decoder layers (natural order, last =
         # final); the set criterion consumes them directly instead of re-concatenating
+        return {"outputs": outs[-1], "aux_outputs": outs[:-1], "_layers_stacked": stacked}
+
+    def _box_predictions_fused(self, query_xyz, point_cloud_dims, pre, L, Q, B):
+        """same outputs as _box_predictions, the parametrisation in one HIP launch each way"""
+        visual = pre["visual_embed_head"].view(L, B, Q, -1)
+        logits = self.mlp_heads["sem_cls_head"](visual)                     # (L, B, Q, T)
+        if self.cls_logits_layout == "reference":
+            logits = logits.reshape(L * B, Q, -1).transpose(1, 2).reshape(L, B, Q, -1)   # Q8
+        NB = self.box_processor.dataset_config.num_angle_bin
+        (center_n, center_u, size_n, size_u, angle_logits, angle_res_norm, angle_res, angle,
+         corners, sem_prob, obj_prob) = _BoxParam.apply(pre["_raw"], query_xyz, point_cloud_dims[0],
+                                                       point_cloud_dims[1], logits, B, Q, NB)
+        v = lambda t, *tail: t.view(L, B, Q, *tail)   # noqa: E731
+        stacked = {
+            "visual_embeds": visual, "sem_cls_logits": logits, "center_normalized": v(center_n, 3),
+            "center_unnormalized": v(center_u, 3), "size_normalized": v(size_n, 3),
+            "size_unnormalized": v(size_u, 3), "angle_logits": v(angle_logits, NB),
+            "angle_residual": v(angle_res, NB), "angle_residual_normalized": v(angle_res_norm, NB),
+            "angle_continuous": v(angle), "objectness_prob": v(obj_prob),
+            "sem_cls_prob": v(sem_prob, -1), "box_corners": v(corners, 8, 3),
+        }
+        per_key = {k: t.unbind(0) for k, t in stacked.items()}
+        outs = [{k: per_key[k][l] for k in stacked} for l in range(L)]
         return {"outputs": outs[-1], "aux_outputs": outs[:-1], "_layers_stacked": stacked}
 
     def forward(self, inputs, encoder_only=False):

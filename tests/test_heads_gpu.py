@@ -137,3 +137,53 @@ def test_bn_relu_rows_projection_matches_torch(cuda):
         assert int(bn1.num_batches_tracked) == int(bn0.num_batches_tracked) == 1
     for a, b in zip(grads[1], grads[0]):
         assert _rel(a, b) < 3e-2
+
+
+@pytest.mark.parametrize("ds", ["sunrgbd", "scannet"])
+def test_box_param_fused_matches_torch(cuda, ds):
+    """csrc/boxparam.hip (model_3detr._BoxParam) against the torch BoxProcessor expressions on
+    the same raw head rows: all 13 outputs and the raw-row gradient, corners included."""
+    import numpy as np
+    from ov3d_amd import synthetic
+    from ov3d_amd.dataset_config import CONFIGS
+    model = _model(cuda)
+    cfg = CONFIGS[ds]()
+    model.box_processor.dataset_config = cfg
+    L, B, Q, NB = 8, 4, 128, cfg.num_angle_bin
+    R = L * B * Q
+    g = torch.Generator().manual_seed(1)
+    raw = (torch.randn(R, 6 + 2 * NB, generator=g) * 2).to(cuda)
+    vis = torch.randn(R, 640, generator=g).to(cuda)
+    if ds == "scannet":
+        sem = torch.nn.Linear(640, 19, bias=False).to(cuda)
+        model.mlp_heads["sem_cls_head"] = sem
+    batch = synthetic.make_batch(B, seed=4, num_points=2048, device=cuda)
+    dims = [batch["point_cloud_dims_min"].float(), batch["point_cloud_dims_max"].float()]
+    qxyz = batch["point_clouds"][:, :Q, :3].contiguous()
+    res = {}
+    for fused in (False, True):
+        r = raw.clone().requires_grad_()
+        names = ("center_head", "size_head", "angle_cls_head", "angle_residual_head")
+        widths = (3, 3, NB, NB)
+        pre = {"visual_embed_head": vis}
+        o = 0
+        for n, w in zip(names, widths):
+            pre[n] = r[:, o:o + w]
+            o += w
+        if fused:
+            pre["_raw"] = r
+        out = model._box_predictions(qxyz, dims, None, (L, Q, B), pre)["_layers_stacked"]
+        gen = torch.Generator(device=cuda).manual_seed(7)
+        loss = 0
+        for k in ("center_normalized", "center_unnormalized", "size_normalized",
+                  "size_unnormalized", "angle_logits", "angle_residual",
+                  "angle_residual_normalized", "angle_continuous", "box_corners"):
+            loss = loss + (out[k] * torch.randn(out[k].shape, device=cuda, generator=gen)).sum()
+        loss.backward()
+        res[fused] = ({k: v.detach() for k, v in out.items()}, r.grad)
+    (a, ga), (b, gb) = res[True], res[False]
+    for k in b:
+        assert a[k].shape == b[k].shape, k
+        assert torch.allclose(a[k], b[k], rtol=1e-5, atol=1e-5), (k, (a[k] - b[k]).abs().max())
+    assert torch.allclose(ga, gb, rtol=1e-4, atol=1e-5), (ga - gb).abs().max()
+    assert np.isfinite(ga.cpu().numpy()).all()
