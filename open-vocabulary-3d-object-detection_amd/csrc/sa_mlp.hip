@@ -270,22 +270,27 @@ __global__ __launch_bounds__(kThreads) void sa_l1_kernel(const float* __restrict
     }
 }
 
-// (nparts, width) fp64 partials -> (width) totals.  Block: 64 columns x 16 partial
-// lanes (coalesced 512-B rows), fixed summation order (deterministic).
+// (nparts, width) fp64 partials -> (width) totals, fixed summation order (deterministic).
 __global__ __launch_bounds__(1024) void reduce_partials_kernel(const double* __restrict__ partials,
                                                                int nparts, int width,
                                                                double* __restrict__ totals) {
-    __shared__ double red[16][64];
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63), pl = threadIdx.x >> 6;
-    double s = 0;
-    if (c < width)
-        for (int w = pl; w < nparts; w += 16) s += partials[(size_t)w * width + c];
-    red[pl][threadIdx.x & 63] = s;
+    // 32 columns x 32 partial lanes per block, 8 loads in flight per thread (fixed order)
+    __shared__ double red[32][33];
+    const int c = blockIdx.x * 32 + (threadIdx.x & 31), pl = threadIdx.x >> 5;
+    double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (c < width) {
+        int w = pl;
+        for (; w + 7 * 32 < nparts; w += 8 * 32)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s[u] += partials[(size_t)(w + u * 32) * width + c];
+        for (; w < nparts; w += 32) s[0] += partials[(size_t)w * width + c];
+    }
+    red[pl][threadIdx.x & 31] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
     __syncthreads();
     if (pl == 0 && c < width) {
         double t = 0;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) t += red[k][threadIdx.x];
+        for (int k = 0; k < 32; ++k) t += red[k][threadIdx.x];
         totals[c] = t;
     }
 }
@@ -578,7 +583,7 @@ extern "C" int ov3d_sa_layer_dy(const void* yprev, const float* scale, const flo
 extern "C" int ov3d_reduce_partials(const double* partials, int nparts, int width, double* totals,
                                     void* stream) {
     if (nparts <= 0 || width <= 0 || !partials || !totals) return OV3D_EINVAL;
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3(ov3d_cdiv(width, 64)), dim3(1024), 0,
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3(ov3d_cdiv(width, 32)), dim3(1024), 0,
                        ov3d_stream(stream), partials, nparts, width, totals);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
