@@ -77,7 +77,11 @@ def regionclip_gflop_per_scene(batch, nqueries=128, layers=8):
     return backbone + nqueries * layers * (res5 + pool)
 
 
-def build(args, device, ddp=False, capturable=False):
+def build(args, device, ddp=False, capturable=False, sync_bn=False, allreduce=False):
+    """ddp: the reference's DistributedDataParallel + SyncBatchNorm (eager); sync_bn +
+    allreduce: the same semantics for the captured step (SyncBatchNorm statistics
+    all-reduced inside the fused BN kernels' launches, the gradient mean by ONE collective
+    in FusedAdamW)."""
     ov3d = ov3d_import.load()
     from ov3d_amd import synthetic
     from ov3d_amd.dataset_config import SunrgbdDatasetConfig
@@ -85,8 +89,9 @@ def build(args, device, ddp=False, capturable=False):
     torch.manual_seed(0)
     model, _ = ov3d.build_model(args, cfg, text_embedding=synthetic.text_embedding(cfg.num_semcls + 1))
     model = model.to(device).train()
-    if ddp:
+    if ddp or sync_bn:
         model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
+    if ddp:
         model = torch.nn.parallel.DistributedDataParallel(
             model, device_ids=[device.index], bucket_cap_mb=32, gradient_as_bucket_view=True)
     crit = ov3d.build_criterion(args, cfg).to(device)
@@ -94,8 +99,12 @@ def build(args, device, ddp=False, capturable=False):
     if getattr(args, "optim", "fused") == "fused":
         # clip_grad_norm_(clip_gradient) + AdamW in three HIP launches (ov3d_amd/optim.py)
         from ov3d_amd.optim import FusedAdamW
+        group = None
+        if allreduce:
+            import torch.distributed as tdist
+            group = tdist.group.WORLD
         opt = FusedAdamW(params, lr=args.base_lr, weight_decay=args.weight_decay,
-                         max_grad_norm=args.clip_gradient)
+                         max_grad_norm=args.clip_gradient, allreduce_group=group)
         return model, crit, opt
     try:
         opt = torch.optim.AdamW(params, lr=args.base_lr, weight_decay=args.weight_decay, fused=True,
@@ -187,8 +196,12 @@ def main():
     p.add_argument("--no-prefetch", action="store_true",
                    help="do not overlap the next batch's pre-encoder FPS with this step")
     p.add_argument("--eager", "--no-graph", dest="eager", action="store_true",
-                   help="launch the step eagerly (default at N>1); at N=1 the whole step is "
-                        "captured once and replayed as one hipGraph (graphs.StepGraph)")
+                   help="launch the step eagerly (DDP at N>1); by default the whole step is "
+                        "captured once and replayed as one hipGraph (graphs.StepGraph), "
+                        "with the RCCL collectives inside it at N>1")
+    p.add_argument("--dp-collectives", action="store_true",
+                   help="run the data-parallel collectives (SyncBN statistics, gradient all-reduce) "
+                        "even at world size 1 (tests the captured collectives on one GPU)")
     p.add_argument("--no-defer-wgrad", action="store_true",
                    help="compute each linear layer's dW / db inside its backward instead of one "
                         "grouped launch at the end of the backward pass (gemm.DEFER_WGRAD)")
@@ -196,21 +209,43 @@ def main():
                    help="fused: clip + AdamW in three HIP launches (ov3d_amd.optim.FusedAdamW); "
                         "torch: clip_grad_norm_ + torch.optim.AdamW(fused=True)")
     cli = p.parse_args()
+    # stdout carries exactly ONE JSON line: native libraries' banners (RCCL's version block at
+    # communicator init) are sent to stderr by pointing fd 1 there; the result line is written
+    # to the saved descriptor
+    sys.stdout.flush()
+    result_fd = os.dup(1)
+    os.dup2(2, 1)
     wl = WORKLOADS[cli.workload]
     if cli.batch is None:
         cli.batch = wl["batch"]
 
     ov3d = ov3d_import.load()
     from ov3d_amd import _native, dist, synthetic
+    if cli.dp_collectives and "WORLD_SIZE" not in os.environ:
+        # a one-rank RCCL group so the captured step holds real collectives (single-GPU test)
+        os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=os.environ.get("MASTER_PORT", "29517"))
+        torch.cuda.set_device(0)
+        torch.distributed.init_process_group(backend="nccl", init_method="env://", world_size=1,
+                                             rank=0)
     rank, world, local = dist.init_from_env()
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     args = default_args(**wl["args"])
     args.optim = cli.optim
     amp = torch.bfloat16 if cli.dtype == "bf16" else None
-    use_graph = world == 1 and not cli.eager
-    model, crit, opt = build(args, device, ddp=world > 1, capturable=use_graph)
-    if world == 1 and not cli.no_defer_wgrad:
+    # N >= 1: the whole step is one captured hipGraph; at N > 1 it holds the SyncBN and the
+    # gradient collectives (RCCL), no DDP wrapper.  --eager: the DDP path.
+    use_graph = not cli.eager
+    dp = (world > 1 or cli.dp_collectives) and use_graph
+    if dp and cli.dp_collectives:
+        from ov3d_amd import sa_fused
+        sa_fused.FORCE_SYNC = True   # collectives even at world 1 (capture test)
+    if cli.optim != "fused" and dp:
+        raise SystemExit("the captured data-parallel step needs --optim fused")
+    model, crit, opt = build(args, device, ddp=world > 1 and not use_graph, capturable=use_graph,
+                             sync_bn=dp, allreduce=dp)
+    if use_graph and not cli.no_defer_wgrad:
         from ov3d_amd import gemm
         gemm.DEFER_WGRAD = True   # one grouped weight-gradient launch per backward (not under DDP)
     clip = build_regionclip(device) if wl["use_image"] else None
@@ -303,7 +338,7 @@ def main():
             res["cpu_baseline"] = cpu_baseline(default_args())
         except Exception as e:  # report, never fake
             res["cpu_baseline"] = {"value": None, "error": repr(e)}
-    print(json.dumps(res), flush=True)
+    os.write(result_fd, (json.dumps(res) + "\n").encode())
 
 
 if __name__ == "__main__":

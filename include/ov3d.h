@@ -388,7 +388,8 @@ int ov3d_resnorm_bwd(long long R, int C, const float* s, const float* mean, cons
  * shadow); workgroup b updates elements [blk_c[b]*chunk, +chunk) of tensor blk_t[b]
  * (chunk = ov3d_adamw_chunk()).  partials: (nblocks) f64 workspace; step: device scalar
  * (incremented); coefs (4) f64 out: clip multiplier, 1-b1^t, sqrt(1-b2^t), grad norm.
- * max_norm <= 0: no clipping.  write_grad: store the clipped gradient back. */
+ * max_norm <= 0: no clipping.  write_grad: store the clipped gradient back.  grad_scale:
+ * gradients are multiplied by it first (1/world after an all-reduce sum: DDP's mean). */
 typedef struct {
     float* param; float* grad; float* exp_avg; float* exp_avg_sq;
     void* shadow;            /* bf16 copy of param or NULL */
@@ -397,14 +398,14 @@ typedef struct {
 } ov3d_adamw_tensor;
 int ov3d_adamw_chunk(void);
 /* n device-to-device copies (bytes[i] from srcs[i] to dsts[i], host arrays) in one launch
- * per 32 (the step graph's static input batch) */
+ * per 120 (the step graph's static input batch, the flat gradient buffer) */
 int ov3d_multi_copy(int n, const void* const* srcs, void* const* dsts, const long long* bytes,
                     void* stream);
 /* table[i].grad = grads[i] (host array of device pointers) by kernel arguments: graph-safe */
 int ov3d_adamw_set_grads(ov3d_adamw_tensor* table, int ntensors, float* const* grads, void* stream);
 int ov3d_adamw_step(const ov3d_adamw_tensor* table, const int* blk_t, const int* blk_c, int nblocks,
                     double* partials, float max_norm, float* step, double beta1, double beta2,
-                    float eps, double* coefs, int write_grad, void* stream);
+                    float eps, double* coefs, int write_grad, float grad_scale, void* stream);
 
 
 /* ---- Box parametrisation of the heads (model_3detr.py BoxProcessor + corners) ----

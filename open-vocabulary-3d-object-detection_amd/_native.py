@@ -54,7 +54,7 @@ _SIGS = {
     "ov3d_rows_bn_bwd": "ipllipillilipppppppfpipipllip",
     "ov3d_set_loss_fwd": "pppppp",
     "ov3d_set_loss_bwd": "pppppppppppp",
-    "ov3d_adamw_step": "pppipfpddfpip",
+    "ov3d_adamw_step": "pppipfpddfpifp",
     "ov3d_adamw_set_grads": "pipp",
     "ov3d_multi_copy": "ipppp",
     "ov3d_box_param_fwd": "liiiiplpppppppppppppppp",

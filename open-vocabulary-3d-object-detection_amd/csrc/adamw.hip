@@ -27,7 +27,8 @@ constexpr int kChunk = kThreads * kPer;  // elements per workgroup
 __global__ void __launch_bounds__(kThreads) adamw_norm_kernel(const ov3d_adamw_tensor* __restrict__ T,
                                                               const int* __restrict__ blk_t,
                                                               const int* __restrict__ blk_c,
-                                                              double* __restrict__ partials) {
+                                                              double* __restrict__ partials,
+                                                              float grad_scale) {
     const ov3d_adamw_tensor t = T[blk_t[blockIdx.x]];
     const long long base = (long long)blk_c[blockIdx.x] * kChunk;
     float s = 0.f;
@@ -35,7 +36,7 @@ __global__ void __launch_bounds__(kThreads) adamw_norm_kernel(const ov3d_adamw_t
     for (int j = 0; j < kPer; ++j) {
         const long long e = base + j * kThreads + threadIdx.x;
         if (e < t.numel) {
-            const float g = t.grad[e];
+            const float g = t.grad[e] * grad_scale;
             s = fmaf(g, g, s);
         }
     }
@@ -76,7 +77,8 @@ __global__ void __launch_bounds__(kThreads) adamw_update_kernel(const ov3d_adamw
                                                                 const int* __restrict__ blk_c,
                                                                 const double* __restrict__ coefs,
                                                                 float beta2, float omb1, float omb2,
-                                                                float eps, int write_grad) {
+                                                                float eps, int write_grad,
+                                                                float grad_scale) {
     const ov3d_adamw_tensor t = T[blk_t[blockIdx.x]];
     const long long base = (long long)blk_c[blockIdx.x] * kChunk;
     const float clip = (float)coefs[0];
@@ -87,11 +89,9 @@ __global__ void __launch_bounds__(kThreads) adamw_update_kernel(const ov3d_adamw
     for (int j = 0; j < kPer; ++j) {
         const long long e = base + j * kThreads + threadIdx.x;
         if (e >= t.numel) break;
-        float g = t.grad[e];
-        if (clip != 1.f) {
-            g *= clip;
-            if (write_grad) t.grad[e] = g;
-        }
+        float g = t.grad[e] * grad_scale;   // 1/world: the all-reduced sum -> mean (DDP)
+        if (clip != 1.f) g *= clip;
+        if (write_grad && (clip != 1.f || grad_scale != 1.f)) t.grad[e] = g;
         // torch.optim.AdamW's single-tensor / foreach arithmetic, operation for operation:
         // p.mul_(1 - lr*wd); m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
         // p.addcdiv_(m, v.sqrt() / sqrt(bc2) + eps, -lr/bc1)
@@ -140,12 +140,12 @@ extern "C" int ov3d_adamw_set_grads(ov3d_adamw_tensor* table, int ntensors, floa
 extern "C" int ov3d_adamw_step(const ov3d_adamw_tensor* table, const int* blk_t, const int* blk_c,
                                int nblocks, double* partials, float max_norm, float* step,
                                double beta1, double beta2, float eps, double* coefs, int write_grad,
-                               void* stream) {
+                               float grad_scale, void* stream) {
     if (!table || !blk_t || !blk_c || nblocks <= 0 || !partials || !step || !coefs ||
         beta1 < 0.0 || beta1 >= 1.0 || beta2 < 0.0 || beta2 >= 1.0 || eps < 0.f)
         return OV3D_EINVAL;
     hipStream_t s = ov3d_stream(stream);
-    adamw_norm_kernel<<<nblocks, kThreads, 0, s>>>(table, blk_t, blk_c, partials);
+    adamw_norm_kernel<<<nblocks, kThreads, 0, s>>>(table, blk_t, blk_c, partials, grad_scale);
     OV3D_LAUNCH_CHECK();
     adamw_finalize_kernel<<<1, kThreads, 0, s>>>(partials, nblocks, max_norm, step, beta1, beta2,
                                                  coefs);
@@ -153,21 +153,22 @@ extern "C" int ov3d_adamw_step(const ov3d_adamw_tensor* table, const int* blk_t,
     // 1 - beta in fp64 first (Python floats in torch), then fp32
     adamw_update_kernel<<<nblocks, kThreads, 0, s>>>(table, blk_t, blk_c, coefs, (float)beta2,
                                                      (float)(1.0 - beta1), (float)(1.0 - beta2), eps,
-                                                     write_grad);
+                                                     write_grad, grad_scale);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }
 
 // ---- several device buffers copied by ONE launch (graphs.StepGraph's static batch) ----
 namespace {
-constexpr int kCopyMax = 32;
-struct CopyList {
+constexpr int kCopyMax = 120;   // kernel-argument space (< 4 KB)
+struct CopyList {   // static_assert below
     const void* src[kCopyMax];
     void* dst[kCopyMax];
     long long bytes[kCopyMax];
     long long blk[kCopyMax + 1];   // workgroup offsets, 16 B x 256 threads x 4 per workgroup
     int n;
 };
+static_assert(sizeof(CopyList) <= 4000, "kernel argument space");
 __global__ void __launch_bounds__(256) multi_copy_kernel(CopyList c) {
     const long long b = blockIdx.x;
     int i = 0;

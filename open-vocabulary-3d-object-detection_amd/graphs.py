@@ -114,7 +114,11 @@ class StepGraph:
             self.inds_cur.copy_(self._sample(self.static["point_clouds"]))
         self.graph = torch.cuda.CUDAGraph()
         self.opt.zero_grad(set_to_none=True)
-        with torch.cuda.graph(self.graph):
+        # with a process group the RCCL collectives are captured too; the watchdog thread of
+        # the process group must not invalidate the capture ("thread_local" capture mode)
+        mode = "thread_local" if (torch.distributed.is_available()
+                                  and torch.distributed.is_initialized()) else "global"
+        with torch.cuda.graph(self.graph, capture_error_mode=mode):
             self.loss = self._body(gemm)
 
     def _sample(self, pc):

@@ -25,7 +25,11 @@ import torch.nn as nn
 from . import _native as nat
 from . import attention as flash
 from .gemm import fused_weight_grad
-from .sa_fused import _bwd_coefs, _finalize
+from .sa_fused import _bwd_coefs, _finalize, _sync_group
+
+# BatchNorm1d, or its SyncBatchNorm conversion (DDP, main.py:427-431): the statistics
+# totals are then all-reduced over the BN's process group (exact SyncBN semantics)
+_BN_TYPES = (nn.BatchNorm1d, nn.SyncBatchNorm)
 
 HEAD_ORDER = ("visual_embed_head", "center_head", "size_head", "angle_cls_head",
               "angle_residual_head")
@@ -39,7 +43,7 @@ def _structure(mlp):
         return None
     c1, b1, r1, d1, c2, b2, r2, d2, c3 = m
     ok = (isinstance(c1, nn.Conv1d) and isinstance(c2, nn.Conv1d) and isinstance(c3, nn.Conv1d)
-          and type(b1) is nn.BatchNorm1d and type(b2) is nn.BatchNorm1d
+          and type(b1) in _BN_TYPES and type(b2) in _BN_TYPES
           and isinstance(r1, nn.ReLU) and isinstance(r2, nn.ReLU)
           and isinstance(d1, nn.Dropout) and isinstance(d2, nn.Dropout)
           and c1.bias is None and c2.bias is None and c3.bias is not None)
@@ -113,31 +117,39 @@ def supported(pack, rows):
     if not (pack.ok and rows.is_cuda and torch.is_autocast_enabled("cuda")
             and torch.get_autocast_dtype("cuda") == torch.bfloat16):
         return False
-    if torch.distributed.is_available() and torch.distributed.is_initialized() and \
-            torch.distributed.get_world_size() > 1:
-        return False   # DDP + SyncBatchNorm: the per-head modules (reference semantics)
     drops = set()
+    groups = set()
     for p in pack.parts:
         for bn in (p[1], p[4]):
             if not bn.training or not bn.track_running_stats or bn.momentum is None:
                 return False
+            groups.add(id(_sync_group(bn)))
         drops.add((p[2].p if p[2].training else 0.0, p[5].p if p[5].training else 0.0))
-    return len(drops) == 1
+    return len(drops) == 1 and len(groups) == 1
+
+
+def _group_world(bn):
+    g = _sync_group(bn)
+    return g, (torch.distributed.get_world_size(g) if g is not None else 1)
 
 
 def _stats_finalize(x, layout, R, C, gamma, beta, bns, rm, rv):
-    """train-mode batch statistics of BN over R rows -> (mean, invstd, scale, shift);
-    running stats of the concatenated storages updated (momentum, unbiased var)."""
+    """train-mode batch statistics of BN over R rows (x all ranks of a SyncBatchNorm group)
+    -> (mean, invstd, scale, shift); running stats of the concatenated storages updated
+    (momentum, unbiased var)."""
     dev = x.device
     parts = torch.empty((NPARTS, 2, C), dtype=torch.float64, device=dev)
     nat.call("ov3d_rows_bn_stats", x, int(x.dtype == torch.bfloat16), *layout, R, C, parts, NPARTS,
              like=x)
     tot = torch.empty(2 * C, dtype=torch.float64, device=dev)
     nat.call("ov3d_reduce_partials", parts, NPARTS, 2 * C, tot, like=x)
-    mean, invstd, scale, shift = (torch.empty(C, dtype=torch.float32, device=dev) for _ in range(4))
     bn0 = bns[0]
-    nat.call("ov3d_bn_finalize", tot, float(R), C, gamma, beta, float(bn0.eps), float(bn0.momentum),
-             rm, rv, mean, invstd, scale, shift, like=x)
+    group, world = _group_world(bn0)
+    if group is not None:
+        torch.distributed.all_reduce(tot, group=group)
+    mean, invstd, scale, shift = (torch.empty(C, dtype=torch.float32, device=dev) for _ in range(4))
+    nat.call("ov3d_bn_finalize", tot, float(R * world), C, gamma, beta, float(bn0.eps),
+             float(bn0.momentum), rm, rv, mean, invstd, scale, shift, like=x)
     return mean, invstd, scale, shift
 
 
@@ -201,14 +213,14 @@ class _Heads(torch.autograd.Function):
         # BN2 (input h2 head-major, grad dz2 row-major) -> dh2 head-major
         dh2 = torch.empty((5, R, H), dtype=bf, device=dev)
         dg2, dbe2 = _bn_backward(dz2, rowmajor, h2, headmajor, R, H5, st["g2"], m2, i2, a2, s2, p2,
-                                 seed, pack.sites[1], dh2, headmajor)
+                                 seed, pack.sites[1], dh2, headmajor, bn=pack.bns()[1][0])
         dw2 = torch.empty((5, H, H), dtype=torch.float32, device=dev)
         for i in range(5):
             fused_weight_grad(dh2[i], z1[:, i * H:(i + 1) * H], bias=False, out_w=dw2[i])
         dz1 = torch.bmm(dh2, w2)                                                 # (5, R, H)
         dh1 = torch.empty((R, H5), dtype=bf, device=dev)
         dg1, dbe1 = _bn_backward(dz1, headmajor, h1, rowmajor, R, H5, st["g1"], m1, i1, a1, s1, p1,
-                                 seed, pack.sites[0], dh1, rowmajor)
+                                 seed, pack.sites[0], dh1, rowmajor, bn=pack.bns()[0][0])
         dw1, _ = fused_weight_grad(dh1, xb, bias=False)
         dx = (dh1 @ w1).to(xdt)
         grads = {"w1": dw1.view(-1), "w2": dw2.view(-1), "g1": dg1, "b1": dbe1, "g2": dg2,
@@ -222,14 +234,18 @@ class _Heads(torch.autograd.Function):
         return (dx, None, None, None, dw3v, db3v, dw3s.view(w3s_shape), db3s, *out)
 
 
-def _bn_backward(dz, lz, x, lx, R, C, gamma, mean, invstd, scale, shift, p, seed, site, dx, ld):
+def _bn_backward(dz, lz, x, lx, R, C, gamma, mean, invstd, scale, shift, p, seed, site, dx, ld,
+                 bn=None):
     dev = x.device
     parts = torch.empty((NPARTS, 2, C), dtype=torch.float64, device=dev)
     nat.call("ov3d_rows_bn_bwd", 0, dz, *lz, x, 1, *lx, R, C, scale, shift, mean, invstd, None, None,
              None, float(p), seed, site, parts, NPARTS, None, 0, 0, 8, like=x)
     tot = torch.empty(2 * C, dtype=torch.float64, device=dev)
     nat.call("ov3d_reduce_partials", parts, NPARTS, 2 * C, tot, like=x)
-    cA, cB, cC, dg, db = _bwd_coefs(tot, R, gamma, mean, invstd, C)
+    group, world = _group_world(bn) if bn is not None else (None, 1)
+    if group is not None:
+        torch.distributed.all_reduce(tot, group=group)
+    cA, cB, cC, dg, db = _bwd_coefs(tot, R * world, gamma, mean, invstd, C)
     nat.call("ov3d_rows_bn_bwd", 1, dz, *lz, x, 1, *lx, R, C, scale, shift, mean, invstd, cA, cB, cC,
              float(p), seed, site, None, 0, dx, *ld, like=x)
     return dg, db
@@ -282,6 +298,7 @@ class _BnReluRows(torch.autograd.Function):
                  shift, float(p), seed if p > 0 else None, site, z, *rowmajor, like=h)
         ctx.save_for_backward(h, gamma, mean, invstd, scale, shift)
         ctx.meta = (float(p), site)
+        ctx.bn = bn
         return z
 
     @staticmethod
@@ -300,7 +317,10 @@ class _BnReluRows(torch.autograd.Function):
                  like=h)
         tot = torch.empty(2 * C, dtype=torch.float64, device=dev)
         nat.call("ov3d_reduce_partials", parts, NPARTS, 2 * C, tot, like=h)
-        cA, cB, cC, dg, db = _bwd_coefs(tot, R, gamma, mean, invstd, C)
+        group, world = _group_world(ctx.bn)
+        if group is not None:
+            torch.distributed.all_reduce(tot, group=group)
+        cA, cB, cC, dg, db = _bwd_coefs(tot, R * world, gamma, mean, invstd, C)
         dh = torch.empty((R, C), dtype=torch.bfloat16, device=dev)
         nat.call("ov3d_rows_bn_bwd", 1, dz, *rowmajor, h, hf, *rowmajor, R, C, scale, shift, mean,
                  invstd, cA, cB, cC, float(p), seed, site, None, 0, dh, *rowmajor, like=h)
@@ -308,14 +328,11 @@ class _BnReluRows(torch.autograd.Function):
 
 
 def bn_relu_rows_ok(h, bn, relu, drop):
-    """the fused rows path applies: single process, training BN with running stats, ReLU"""
+    """the fused rows path applies: training BN (or SyncBN) with running stats, then ReLU"""
     if not (h.is_cuda and h.dim() == 2 and h.shape[1] % 8 == 0 and torch.is_autocast_enabled("cuda")
             and torch.get_autocast_dtype("cuda") == torch.bfloat16):
         return False
-    if torch.distributed.is_available() and torch.distributed.is_initialized() and \
-            torch.distributed.get_world_size() > 1:
-        return False   # DDP + SyncBatchNorm: the reference module
-    return (type(bn) is nn.BatchNorm1d and bn.training and bn.track_running_stats
+    return (type(bn) in _BN_TYPES and bn.training and bn.track_running_stats
             and bn.momentum is not None and bn.affine and isinstance(relu, nn.ReLU)
             and (drop is None or isinstance(drop, nn.Dropout)))
 

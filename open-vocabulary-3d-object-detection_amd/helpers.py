@@ -84,7 +84,7 @@ class GenericMLP(nn.Module):
                 x = rows_linear(x, m.weight.view(m.weight.shape[0], m.weight.shape[1]), m.bias)
             elif isinstance(m, nn.GroupNorm):
                 raise NotImplementedError("GroupNorm MLPs are not on the reference path")
-            elif isinstance(m, nn.BatchNorm1d) and i + 1 < len(mods):
+            elif isinstance(m, (nn.BatchNorm1d, nn.SyncBatchNorm)) and i + 1 < len(mods):
                 drop = mods[i + 2] if i + 2 < len(mods) and isinstance(mods[i + 2], nn.Dropout) else None
                 if heads.bn_relu_rows_ok(x, m, mods[i + 1], drop):
                     x = heads.bn_relu_rows(x, m, drop)

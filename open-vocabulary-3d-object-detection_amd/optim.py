@@ -9,6 +9,8 @@ does both in ``step()``: the clipped gradients are written back to ``p.grad`` as
 clip_grad_norm_ does, ``last_grad_norm`` holds the total norm (device scalar) it returns,
 and the state keeps torch's keys (``step``, ``exp_avg``, ``exp_avg_sq``).  Built with
 ``max_grad_norm=None`` it is a drop-in for AdamW after a separate clip_grad_norm_ call.
+With ``allreduce_group`` (data parallel without DDP) the averaged, clipped gradients live
+in the optimizer's flat buffer (``flat_grads()``) instead of ``p.grad``.
 
 The bf16 copies of the parameters used by the autocast GEMMs (gemm.cast_param) are
 rewritten by the same update launch, so no separate refresh copy runs.  Capturable: the
@@ -38,11 +40,15 @@ class FusedAdamW(torch.optim.Optimizer):
     writes_shadows = True     # step() refreshes gemm.py's bf16 parameter copies
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2,
-                 max_grad_norm=None):
+                 max_grad_norm=None, allreduce_group=None):
         if lr < 0 or eps < 0 or weight_decay < 0 or not (0 <= betas[0] < 1 and 0 <= betas[1] < 1):
             raise ValueError("FusedAdamW: invalid hyper-parameters")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self.max_grad_norm = max_grad_norm
+        # data parallel without DDP (graphs.StepGraph at N > 1): the gradients are copied into
+        # one flat buffer (one launch), all-reduced by ONE collective (sum) and averaged by
+        # the update kernels (grad_scale = 1/world): DDP's gradient mean, main.py:427-431
+        self.allreduce_group = allreduce_group
         self.last_grad_norm = None
         self._key = None
         self._dev = None
@@ -129,18 +135,42 @@ class FusedAdamW(torch.optim.Optimizer):
             self._partials = torch.empty(len(blk_t), dtype=torch.float64, device=dev)
             self._coefs = torch.empty(4, dtype=torch.float64, device=dev)
             self._key, self._dev = key, dev
-        grads = (ctypes.c_void_p * len(items))(*[p.grad.data_ptr() for p, _ in items])
+        scale = 1.0
+        if self.allreduce_group is not None:
+            import torch.distributed as dist
+            if getattr(self, "_flat", None) is None or self._flat_key != key:
+                if torch.cuda.is_current_stream_capturing():
+                    raise RuntimeError("FusedAdamW: run one eager step before capturing a graph")
+                self._flat = torch.empty(sum(p.numel() for p, _ in items), dtype=torch.float32,
+                                         device=dev)
+                self._flat_key = key
+                views, o = [], 0
+                for p, _ in items:
+                    views.append(self._flat[o:o + p.numel()].view(p.shape))
+                    o += p.numel()
+                self._flat_views = views
+            _native.multi_copy(self._flat_views, [p.grad for p, _ in items])
+            dist.all_reduce(self._flat, group=self.allreduce_group)
+            grad_src = self._flat_views
+            scale = 1.0 / dist.get_world_size(self.allreduce_group)
+        else:
+            grad_src = [p.grad for p, _ in items]
+        grads = (ctypes.c_void_p * len(items))(*[g.data_ptr() for g in grad_src])
         _native.call("ov3d_adamw_set_grads", self._buf, len(items), ctypes.addressof(grads),
                      like=self._buf)
         idx = self._buf[self._nbytes:].view(torch.int32)
         clip = float(self.max_grad_norm) if self.max_grad_norm and self.max_grad_norm > 0 else 0.0
         _native.call("ov3d_adamw_step", self._buf, idx, idx[self._nblocks:], self._nblocks,
                      self._partials, clip, self._step_t, float(b1), float(b2), float(eps),
-                     self._coefs, 1, like=self._buf)
+                     self._coefs, 1, float(scale), like=self._buf)
         self.last_grad_norm = self._coefs[3]   # fp64 view (no launch)
         for p, _ in items:
             torch.autograd.graph.increment_version(p)
-            if clip:
+            if clip and self.allreduce_group is None:
                 torch.autograd.graph.increment_version(p.grad)
             gemm.mark_shadow_fresh(p)
         return loss
+
+    def flat_grads(self):
+        """the averaged, clipped gradients of the last all-reduced step, one view per parameter"""
+        return getattr(self, "_flat_views", None)

@@ -22,6 +22,8 @@ BatchNorm semantics are torch's training batch_norm: biased variance to normalis
 unbiased for running_var, momentum update, num_batches_tracked += 1; SyncBatchNorm
 all-reduces the per-channel sums (one all-reduce per layer, forward and backward).
 """
+import os
+
 import torch
 import torch.distributed as dist
 import torch.nn as nn
@@ -40,9 +42,13 @@ def _bn(layer):
     return layer.bn.bn
 
 
+FORCE_SYNC = os.environ.get("OV3D_FORCE_SYNC_BN", "0") == "1"   # test hook: sync even at world 1
+
+
 def _sync_group(bn):
+    """the process group a SyncBatchNorm's statistics are all-reduced over (None: local)"""
     if isinstance(bn, nn.SyncBatchNorm) and dist.is_available() and dist.is_initialized() \
-            and dist.get_world_size(bn.process_group) > 1:
+            and (FORCE_SYNC or dist.get_world_size(bn.process_group) > 1):
         return bn.process_group if bn.process_group is not None else dist.group.WORLD
     return None
 

@@ -1,0 +1,33 @@
+"""The captured data-parallel step (graphs.StepGraph with SyncBatchNorm statistics and the
+gradient all-reduce as RCCL collectives inside the graph, no DDP) on a one-rank group equals
+the single-process step (tools/dp_graph_check.py, run in its own process because it
+initialises a process group), and bench.py keeps exactly one JSON line on stdout with the
+RCCL communicator up."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from helpers import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def test_dp_graph_step_equals_single_process():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "dp_graph_check.py")],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "OK dp-graph" in r.stdout
+
+
+def test_bench_dp_collectives_one_json_line():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dp-collectives",
+                        "--steps", "3", "--warmup", "2", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["value"] > 0 and res["n_gpus"] == 1
