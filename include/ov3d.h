@@ -414,6 +414,11 @@ int ov3d_adamw_step(const ov3d_adamw_tensor* table, const int* blk_t, const int*
  * Outputs (R, ...) contiguous fp32: center_n / center_u / size_n / size_u (3), angle
  * logits / residual_normalized / residual (NB), angle (1), corners (8, 3), sem_prob (T-1),
  * objectness (1).  Backward: any gradient may be NULL; writes draw (R, ldd) columns 0..6+2NB. */
+/* Fourier position embedding (position_embedding.py:89-118): xyz (B, N, 3), optional scene
+ * range dmin / dmax (B, 3) (both or neither), gauss_B (3, ldb) first d columns ->
+ * out (B, N, 2d) = [sin | cos] of (normalised xyz * 2 pi) @ gauss_B */
+int ov3d_fourier_pe(const float* xyz, int B, int N, const float* dmin, const float* dmax,
+                    const float* gauss_b, int ldb, int d, float* out, void* stream);
 int ov3d_box_param_fwd(long long R, int B, int Q, int NB, int T, const float* raw, long long ld,
                        const float* qxyz, const float* dmin, const float* dmax,
                        const float* logits, float* center_n, float* center_u, float* size_n,

@@ -57,6 +57,7 @@ _SIGS = {
     "ov3d_adamw_step": "pppipfpddfpifp",
     "ov3d_adamw_set_grads": "pipp",
     "ov3d_multi_copy": "ipppp",
+    "ov3d_fourier_pe": "piipppiipp",
     "ov3d_box_param_fwd": "liiiiplpppppppppppppppp",
     "ov3d_box_param_bwd": "liiiplppppppppppppplp",
     "ov3d_relu_dropout_fwd": "plifpipp",

@@ -36,6 +36,16 @@ class PositionEmbeddingCoordsSine(nn.Module):
         if d_out > max_d_out or d_in != xyz.shape[-1]:
             raise ValueError("bad fourier embedding size")
         B, N = xyz.shape[:2]
+        if xyz.is_cuda:
+            # one HIP launch (csrc/boxparam.hip ov3d_fourier_pe) instead of ~12 torch kernels
+            from . import _native
+            x = xyz.float().contiguous()
+            rng = [t.float().contiguous() for t in input_range] if self.normalize else [None, None]
+            gb = self.gauss_B.float().contiguous()
+            out = torch.empty((B, N, 2 * d_out), dtype=torch.float32, device=xyz.device)
+            _native.call("ov3d_fourier_pe", x, B, N, rng[0], rng[1], gb, gb.shape[1], d_out, out,
+                         like=x)
+            return out
         x = xyz.float()
         if self.normalize:
             x = shift_scale_points(x, src_range=input_range)

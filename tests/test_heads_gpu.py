@@ -187,3 +187,16 @@ def test_box_param_fused_matches_torch(cuda, ds):
         assert torch.allclose(a[k], b[k], rtol=1e-5, atol=1e-5), (k, (a[k] - b[k]).abs().max())
     assert torch.allclose(ga, gb, rtol=1e-4, atol=1e-5), (ga - gb).abs().max()
     assert np.isfinite(ga.cpu().numpy()).all()
+
+
+def test_fourier_pe_kernel_matches_torch(cuda):
+    """ov3d_fourier_pe against the module's torch expression (run on the CPU, fp32)"""
+    from ov3d_amd.position_embedding import PositionEmbeddingCoordsSine
+    torch.manual_seed(3)
+    pe = PositionEmbeddingCoordsSine(d_pos=256, pos_type="fourier", normalize=True)
+    xyz = torch.rand(4, 2048, 3) * 6 - 3
+    rng = [xyz.min(1).values - 0.1, xyz.max(1).values + 0.1]
+    ref = pe.rows(xyz, input_range=rng)
+    out = pe.to(cuda).rows(xyz.to(cuda), input_range=[r.to(cuda) for r in rng]).cpu()
+    assert out.shape == ref.shape
+    assert (out - ref).abs().max().item() < 2e-5
