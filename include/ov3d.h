@@ -316,6 +316,7 @@ typedef struct {
     int L, B, Q, G, T, NB;
     int flags;             /* OV3D_LOSS_* terms computed (angle cls / reg always) */
     int final_last;        /* 1: computation layer L-1 is the final layer; 0: layer 0 is */
+    int match_ref_order;   /* inds / matched rows in the reference's problem order (final first) */
     const float* logits;        long long ld_logits;        /* (L*B*Q, T) */
     const float* angle_logits;  long long ld_angle_logits;  /* (L*B*Q, NB) */
     const float* angle_res;     long long ld_angle_res;     /* (L*B*Q, NB), normalised */
@@ -340,6 +341,22 @@ typedef struct {
 } ov3d_set_loss_desc;
 /* raw: (L, 9) f32 workspace (kept for the backward); ticket: one int, zero before the first
  * call (the kernel resets it); dict_out (L, 8); total: scalar */
+/* Hungarian matcher cost (criterion.py:33-92 Matcher.cost with the center cdist(p=1) of
+ * 357-360) for P = L*B problems: prob (P, Q, C) row stride ldp, obj (P, Q), center (P, Q, 3),
+ * gious (P, Q, G), gt_center (B, G, 3), gt_label (B, G) -> cost (P, Q, G), written in the
+ * reference's problem order (final layer first) when final_last (layer l of the inputs is
+ * the computation order with the final layer last) */
+int ov3d_matcher_cost(int P, int B, int Q, int G, int C, int final_last, const float* prob,
+                      long long ldp,
+                      const float* obj, const float* center, const float* gious,
+                      const float* gt_center, const int64_t* gt_label, float w_cls, float w_obj,
+                      float w_center, float w_giou, float* cost, void* stream);
+/* target counts (criterion.py:346-352, 425): nactual per scene (int64, and int32 repeated for
+ * the L layers), the replica's total, num_boxes = max(total, 1) (single process; NULL to
+ * skip) and the rotated flag (any GT angle > 0) */
+int ov3d_targets_prep(int B, int G, int L, const float* present, const float* angles,
+                      int64_t* nact64, int32_t* nact32_rep, int64_t* total, float* num_boxes,
+                      int32_t* rotated, void* stream);
 long long ov3d_set_loss_desc_size(void);   /* sizeof(ov3d_set_loss_desc), for FFI layout checks */
 int ov3d_set_loss_fwd(const ov3d_set_loss_desc* desc, float* raw, int* ticket, float* dict_out,
                       float* total, void* stream);

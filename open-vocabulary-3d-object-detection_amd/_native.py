@@ -53,6 +53,8 @@ _SIGS = {
     "ov3d_rows_bn_apply": "pillilippfpipllip",
     "ov3d_rows_bn_bwd": "ipllipillilipppppppfpipipllip",
     "ov3d_set_loss_fwd": "pppppp",
+    "ov3d_matcher_cost": "iiiiiiplpppppffffpp",
+    "ov3d_targets_prep": "iiipppppppp",
     "ov3d_set_loss_bwd": "pppppppppppp",
     "ov3d_adamw_step": "pppipfpddfpifp",
     "ov3d_adamw_set_grads": "pipp",

@@ -115,43 +115,64 @@ class SetCriterion(nn.Module):
             def layer(l):
                 return layers[l]
         present = targets["gt_box_present"]
-        nactual_gt = present.sum(axis=1).long()
-        # No host synchronisation in the step: num_boxes stays a device scalar, the
-        # rotated switch (criterion.py:317-330, Q2) is a device flag read by the GIoU
-        # kernel, and the matcher runs on the device.
-        num_boxes = torch.clamp(all_reduce_average(nactual_gt.sum()), min=1)
-        rotated = (targets["gt_box_angles"] > 0).any().to(torch.int32)
-        targets["nactual_gt"] = nactual_gt
-        targets["num_boxes"] = num_boxes
-        targets["num_boxes_replica"] = nactual_gt.sum()
-
         B = present.shape[0]
 
         def rep(t):
             return t.repeat((L,) + (1,) * (t.dim() - 1))
 
         needs_grad = self._w("loss_giou") > 0
-        gious = generalized_box3d_iou(cat("box_corners"), rep(targets["gt_box_corners"]),
-                                      rep(nactual_gt), rotated_boxes=rotated, needs_grad=needs_grad,
-                                      k2_bug=self.giou_k2_bug)
-        center_norm = cat("center_normalized").float()
-        gt_centers = rep(targets["gt_box_centers_normalized"]).float()
-        # == torch.cdist(p=1) (criterion.py:357-360) as one broadcast kernel chain
-        center_dist = (center_norm[:, :, None, :] - gt_centers[:, None, :, :]).abs().sum(-1)
-        gt_labels = rep(targets["gt_box_sem_cls_label"])
-        cost = self.matcher.cost(cat("sem_cls_prob").float(), cat("objectness_prob").float(),
-                                 center_dist, gious, gt_labels)
-        if final == 0:
-            asg = self.matcher(cost, rep(nactual_gt))
+        fused = self.fused_losses and setloss.supported(present)
+        if fused:
+            # counts / flags in one launch, the matcher cost in one launch written in the
+            # reference's problem order (final layer first, criterion.py:431-444) for the
+            # matcher; the loss kernels read its assignments in that order
+            nactual_gt, nact_rep, num_boxes, rotated, replica = setloss.target_counts(present,
+                                                                                       targets, L)
+            gious = generalized_box3d_iou(cat("box_corners"), rep(targets["gt_box_corners"]),
+                                          nact_rep, rotated_boxes=rotated, needs_grad=needs_grad,
+                                          k2_bug=self.giou_k2_bug)
+            m = self.matcher
+            cost = setloss.matcher_cost(cat("sem_cls_prob"), cat("objectness_prob"),
+                                        cat("center_normalized"), gious, targets, B,
+                                        (m.cost_class, m.cost_objectness, m.cost_center,
+                                         m.cost_giou), final_last=final != 0)
+            asg = m(cost, nact_rep)
             inds, mask = asg["per_prop_gt_inds"], asg["proposal_matched_mask"]
+            targets["nactual_gt"] = nactual_gt
+            targets["num_boxes"] = num_boxes
+            targets["num_boxes_replica"] = replica
+            center_dist = gt_labels = None
         else:
-            # the matcher sees its L*B problems in the reference order (final layer first,
-            # criterion.py:431-444): a rotation by one layer (torch.roll: no host index)
-            Q, G = cost.shape[1], cost.shape[2]
-            asg = self.matcher(torch.roll(cost.view(L, B, Q, G), 1, 0).reshape(L * B, Q, G),
-                               rep(nactual_gt))
-            inds = torch.roll(asg["per_prop_gt_inds"].view(L, B, Q), -1, 0).reshape(L * B, Q)
-            mask = torch.roll(asg["proposal_matched_mask"].view(L, B, Q), -1, 0).reshape(L * B, Q)
+            nactual_gt = present.sum(axis=1).long()
+            # No host synchronisation in the step: num_boxes stays a device scalar, the
+            # rotated switch (criterion.py:317-330, Q2) is a device flag read by the GIoU
+            # kernel, and the matcher runs on the device.
+            num_boxes = torch.clamp(all_reduce_average(nactual_gt.sum()), min=1)
+            rotated = (targets["gt_box_angles"] > 0).any().to(torch.int32)
+            targets["nactual_gt"] = nactual_gt
+            targets["num_boxes"] = num_boxes
+            targets["num_boxes_replica"] = nactual_gt.sum()
+            gious = generalized_box3d_iou(cat("box_corners"), rep(targets["gt_box_corners"]),
+                                          rep(nactual_gt), rotated_boxes=rotated,
+                                          needs_grad=needs_grad, k2_bug=self.giou_k2_bug)
+            center_norm = cat("center_normalized").float()
+            gt_centers = rep(targets["gt_box_centers_normalized"]).float()
+            # == torch.cdist(p=1) (criterion.py:357-360) as one broadcast kernel chain
+            center_dist = (center_norm[:, :, None, :] - gt_centers[:, None, :, :]).abs().sum(-1)
+            gt_labels = rep(targets["gt_box_sem_cls_label"])
+            cost = self.matcher.cost(cat("sem_cls_prob").float(), cat("objectness_prob").float(),
+                                     center_dist, gious, gt_labels)
+            if final == 0:
+                asg = self.matcher(cost, rep(nactual_gt))
+                inds, mask = asg["per_prop_gt_inds"], asg["proposal_matched_mask"]
+            else:
+                # the matcher sees its L*B problems in the reference order (final layer first,
+                # criterion.py:431-444): a rotation by one layer (torch.roll: no host index)
+                Q, G = cost.shape[1], cost.shape[2]
+                asg = self.matcher(torch.roll(cost.view(L, B, Q, G), 1, 0).reshape(L * B, Q, G),
+                                   rep(nactual_gt))
+                inds = torch.roll(asg["per_prop_gt_inds"].view(L, B, Q), -1, 0).reshape(L * B, Q)
+                mask = torch.roll(asg["proposal_matched_mask"].view(L, B, Q), -1, 0).reshape(L * B, Q)
 
         align = None
         if self._computed("loss_2dalignment"):
@@ -161,8 +182,9 @@ class SetCriterion(nn.Module):
                 align = self._alignment_batched(cat, L, B, targets, clip)
             else:
                 align = self._alignment([layer(l) for l in range(L)], targets, clip)
-        if self.fused_losses and setloss.supported(cat("sem_cls_logits")):
-            return self._losses_fused(cat, L, B, final, gious, inds, mask, targets, num_boxes, align)
+        if fused:
+            return self._losses_fused(cat, L, B, final, gious, inds, mask, targets, num_boxes, align,
+                                      match_ref_order=final != 0)
         return self._losses_torch(cat, L, B, final, aux, gious, center_dist, gt_labels, inds, mask,
                                   targets, num_boxes, nactual_gt, align)
 
@@ -170,7 +192,8 @@ class SetCriterion(nn.Module):
         """LOSS_KEYS present in the dict: computed terms (angle cls / reg always)"""
         return [k for k in LOSS_KEYS if k in ("loss_angle_cls", "loss_angle_reg") or self._computed(k)]
 
-    def _losses_fused(self, cat, L, B, final, gious, inds, mask, targets, num_boxes, align):
+    def _losses_fused(self, cat, L, B, final, gious, inds, mask, targets, num_boxes, align,
+                      match_ref_order=False):
         """all terms, the dict table and the total in one HIP launch (setloss.py)."""
         keys = self._dict_keys()
         cols = {k: setloss.COLUMNS.index(k) for k in keys}
@@ -190,7 +213,7 @@ class SetCriterion(nn.Module):
             cat("size_normalized") if "loss_size" in keys else None,
             gious if "loss_giou" in keys else None, align, inds, mask, targets,
             self.semcls_percls_weights if "loss_sem_cls" in keys else None, num_boxes,
-            dict_w, total_w, [cols[k] for k in weighted])
+            dict_w, total_w, [cols[k] for k in weighted], match_ref_order=match_ref_order)
         loss_dict = {}
         for i in range(L):
             suffix = "" if i == 0 else f"_{i - 1}"

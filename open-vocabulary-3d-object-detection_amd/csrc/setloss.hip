@@ -48,6 +48,12 @@ __device__ __forceinline__ int dict_pos(const ov3d_set_loss_desc& d, int l) {
 __device__ __forceinline__ int layer_at(const ov3d_set_loss_desc& d, int i) {
     return d.final_last ? (i == 0 ? d.L - 1 : i - 1) : i;
 }
+// row of (layer l, proposal p of the layer) in the matcher's outputs: computation order, or
+// the reference's problem order (final layer first) when match_ref_order
+__device__ __forceinline__ long long match_row(const ov3d_set_loss_desc& d, int l, int p) {
+    const int lm = d.match_ref_order ? dict_pos(d, l) : l;
+    return (long long)lm * d.B * d.Q + p;
+}
 
 // max, index of the first maximum and sum of exp(x - max) over n values
 __device__ __forceinline__ void softmax_stats(const float* x, int n, float& mx, int& am, float& s) {
@@ -79,8 +85,9 @@ __global__ void __launch_bounds__(kThreads) set_loss_fwd_kernel(ov3d_set_loss_de
     for (int p = threadIdx.x; p < P; p += kThreads) {
         const int b = p / d.Q;
         const long long row = (long long)l * P + p;
-        const float m = d.matched[row];
-        const int g = clampi(d.inds[row], d.G - 1);
+        const long long mrow = match_row(d, l, p);
+        const float m = d.matched[mrow];
+        const int g = clampi(d.inds[mrow], d.G - 1);
         const long long bg = (long long)b * d.G + g;
 
         const float* x = d.logits + row * d.ld_logits;
@@ -190,8 +197,9 @@ __global__ void __launch_bounds__(kThreads) set_loss_bwd_kernel(
     for (int k = 0; k < 6; ++k)
         c[k] = d.dict_w[k] * (d_dict ? d_dict[i * kCols + k] : 0.f) + d.total_w[k] * dt;
     const float nb = *d.num_boxes;
-    const float m = d.matched[row];
-    const int g = clampi(d.inds[row], d.G - 1);
+    const long long mrow = match_row(d, l, (int)(row % P));
+    const float m = d.matched[mrow];
+    const int g = clampi(d.inds[mrow], d.G - 1);
     const long long bg = (long long)b * d.G + g;
 
     if (g_logits) {
@@ -290,6 +298,108 @@ extern "C" int ov3d_set_loss_bwd(const ov3d_set_loss_desc* desc, const float* ra
     set_loss_bwd_kernel<<<ov3d_cdiv(rows, kThreads), kThreads, 0, ov3d_stream(stream)>>>(
         d, raw, d_dict, d_total, g_logits, g_angle_logits, g_angle_res, g_center, g_size, g_gious,
         g_align);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+// ---- Hungarian matcher cost and target counts (criterion.py:33-92, 346-360, 425) ----
+namespace {
+
+// cost[p, q, g] = w_cls * (-prob[p, q, label[b, g]]) + w_obj * (-obj[p, q])
+//               + w_center * |center[p, q] - gt_center[b, g]|_1 + w_giou * (-giou[p, q, g]),
+// b = p % B (the L*B problems stack the B scenes L times); one thread per (p, q, g)
+__global__ void __launch_bounds__(256) matcher_cost_kernel(
+    long long total, int B, int Q, int G, int C, int L, int final_last,
+    const float* __restrict__ prob, long long ldp,
+    const float* __restrict__ obj, const float* __restrict__ center, const float* __restrict__ gious,
+    const float* __restrict__ gt_center, const int64_t* __restrict__ gt_label, float w_cls,
+    float w_obj, float w_center, float w_giou, float* __restrict__ cost) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= total) return;
+    const int g = (int)(t % G);
+    const long long pq = t / G;
+    const long long p = pq / Q;
+    const int b = (int)(p % B);
+    const int lab = clampi(gt_label[(long long)b * G + g], C - 1);
+    const float* c = center + pq * 3;
+    const float* gc = gt_center + ((long long)b * G + g) * 3;
+    const float dist = (fabsf(c[0] - gc[0]) + fabsf(c[1] - gc[1])) + fabsf(c[2] - gc[2]);
+    const float v = ((w_cls * (-prob[pq * ldp + lab]) + w_obj * (-obj[pq])) + w_center * dist) +
+                    w_giou * (-gious[t]);
+    // problem p = l*B + b goes to the reference's problem order (final layer first:
+    // criterion.py:431-444) when final_last, i.e. layer l -> position (l + 1) % L
+    const long long l = p / B;
+    const long long lo = final_last ? (l + 1) % L : l;
+    cost[((lo * B + b) * Q + (pq % Q)) * G + g] = v;
+}
+
+// per scene: nactual = (int64)(sum present), int32 copies repeated L times, the replica's
+// box count, the clamped num_boxes (single process) and the rotated flag (any angle > 0)
+__global__ void __launch_bounds__(256) targets_prep_kernel(int B, int G, int L,
+                                                          const float* __restrict__ present,
+                                                          const float* __restrict__ angles,
+                                                          int64_t* nact64, int32_t* nact32_rep,
+                                                          int64_t* total, float* num_boxes,
+                                                          int32_t* rotated) {
+    __shared__ long long cnt[256];
+    __shared__ int rot[256];
+    long long my = 0;
+    int r = 0;
+    for (int b = threadIdx.x; b < B; b += blockDim.x) {
+        float s = 0.f;
+        for (int g = 0; g < G; ++g) {
+            s += present[(long long)b * G + g];
+            r |= angles[(long long)b * G + g] > 0.f;
+        }
+        const long long n = (long long)s;
+        nact64[b] = n;
+        for (int l = 0; l < L; ++l) nact32_rep[(long long)l * B + b] = (int32_t)n;
+        my += n;
+    }
+    cnt[threadIdx.x] = my;
+    rot[threadIdx.x] = r;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        long long t = 0;
+        int rr = 0;
+        for (int i = 0; i < (int)blockDim.x; ++i) {
+            t += cnt[i];
+            rr |= rot[i];
+        }
+        *total = t;
+        if (num_boxes) *num_boxes = fmaxf((float)t, 1.f);
+        *rotated = rr;
+    }
+}
+
+}  // namespace
+
+extern "C" int ov3d_matcher_cost(int P, int B, int Q, int G, int C, int final_last,
+                                 const float* prob, long long ldp, const float* obj,
+                                 const float* center,
+                                 const float* gious, const float* gt_center,
+                                 const int64_t* gt_label, float w_cls, float w_obj, float w_center,
+                                 float w_giou, float* cost, void* stream) {
+    if (P <= 0 || B <= 0 || P % B || Q <= 0 || G <= 0 || C <= 0 || ldp < C || !prob || !obj ||
+        !center || !gious || !gt_center || !gt_label || !cost)
+        return OV3D_EINVAL;
+    const long long total = (long long)P * Q * G;
+    matcher_cost_kernel<<<ov3d_cdiv(total, 256), 256, 0, ov3d_stream(stream)>>>(
+        total, B, Q, G, C, P / B, final_last, prob, ldp, obj, center, gious, gt_center, gt_label,
+        w_cls, w_obj,
+        w_center, w_giou, cost);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_targets_prep(int B, int G, int L, const float* present, const float* angles,
+                                 int64_t* nact64, int32_t* nact32_rep, int64_t* total,
+                                 float* num_boxes, int32_t* rotated, void* stream) {
+    if (B <= 0 || G <= 0 || L <= 0 || !present || !angles || !nact64 || !nact32_rep || !total ||
+        !rotated)
+        return OV3D_EINVAL;
+    targets_prep_kernel<<<1, 256, 0, ov3d_stream(stream)>>>(B, G, L, present, angles, nact64,
+                                                            nact32_rep, total, num_boxes, rotated);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

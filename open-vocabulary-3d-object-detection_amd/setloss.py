@@ -32,7 +32,7 @@ class Desc(ctypes.Structure):
     """mirror of ov3d_set_loss_desc (include/ov3d.h)"""
     _fields_ = [("L", ctypes.c_int), ("B", ctypes.c_int), ("Q", ctypes.c_int), ("G", ctypes.c_int),
                 ("T", ctypes.c_int), ("NB", ctypes.c_int), ("flags", ctypes.c_int),
-                ("final_last", ctypes.c_int),
+                ("final_last", ctypes.c_int), ("match_ref_order", ctypes.c_int),
                 ("logits", _P), ("ld_logits", _L), ("angle_logits", _P), ("ld_angle_logits", _L),
                 ("angle_res", _P), ("ld_angle_res", _L), ("center", _P), ("ld_center", _L),
                 ("size", _P), ("ld_size", _L), ("gious", _P), ("inds", _P), ("matched", _P),
@@ -134,7 +134,8 @@ class _SetLoss(torch.autograd.Function):
 
 
 def set_losses(L, B, Q, final_last, logits, angle_logits, angle_res, center, size, gious, align,
-               inds, matched, targets, cls_weights, num_boxes, dict_w, total_w, total_order):
+               inds, matched, targets, cls_weights, num_boxes, dict_w, total_w, total_order,
+               match_ref_order=False):
     """-> table (L, 8) of weighted values (rows in dict order), total (0-d).
 
     logits (L*B, Q, T) ..., gious (L*B, Q, G) or None, align (L,) or None, inds / matched
@@ -167,6 +168,7 @@ def set_losses(L, B, Q, final_last, logits, angle_logits, angle_res, center, siz
                | (SIZE if size is not None else 0) | (GIOU if gious is not None else 0)
                | (ALIGN if align is not None else 0))
     d.final_last = int(final_last)
+    d.match_ref_order = int(match_ref_order)
     d.logits, d.ld_logits = lg.data_ptr(), ld_lg
     d.angle_logits, d.ld_angle_logits = al.data_ptr(), ld_al
     d.angle_res, d.ld_angle_res = ar.data_ptr(), ld_ar
@@ -193,3 +195,44 @@ def set_losses(L, B, Q, final_last, logits, angle_logits, angle_res, center, siz
     d.res_scale = _res_scale(NB)
     return _SetLoss.apply((d, keep), logits, angle_logits, angle_res, center, size, gious, align,
                           None)
+
+
+def target_counts(present, targets, L):
+    """-> nactual (B,) int64, nactual repeated for the L layers (L*B,) int32, num_boxes (device
+    scalar: max(total, 1), all-reduce-averaged across ranks), rotated flag (int32), the
+    replica's total (int64) — criterion.py:346-352, 425 in ONE launch (ov3d_targets_prep)."""
+    from .dist import all_reduce_average, get_world_size
+    B, G = present.shape
+    dev = present.device
+    nact = torch.empty(B, dtype=torch.int64, device=dev)
+    nrep = torch.empty(L * B, dtype=torch.int32, device=dev)
+    total = torch.empty((), dtype=torch.int64, device=dev)
+    rotated = torch.empty((), dtype=torch.int32, device=dev)
+    single = get_world_size() == 1
+    nb = torch.empty((), dtype=torch.float32, device=dev) if single else None
+    _native.call("ov3d_targets_prep", B, G, L, present.float().contiguous(),
+                 targets["gt_box_angles"].float().contiguous(), nact, nrep, total, nb, rotated,
+                 like=present)
+    if not single:
+        nb = torch.clamp(all_reduce_average(total), min=1)
+    return nact, nrep, nb, rotated, total
+
+
+def matcher_cost(prob, obj, center, gious, targets, B, weights, final_last=False):
+    """Matcher.cost (criterion.py:54-62) with the center cdist(p=1) of 357-360 for the L*B
+    problems in one launch (ov3d_matcher_cost) -> (L*B, Q, G), in the reference's problem
+    order (final layer first) when final_last."""
+    pr, ldp = rows(prob)
+    ob = obj.float().contiguous()
+    ce = center.float().contiguous()
+    gi = gious.detach().float().contiguous()
+    gc = targets["gt_box_centers_normalized"].float().contiguous()
+    gl = targets["gt_box_sem_cls_label"].to(torch.int64).contiguous()
+    P, Q, G = gi.shape
+    C = prob.shape[-1]
+    cost = torch.empty((P, Q, G), dtype=torch.float32, device=prob.device)
+    w_cls, w_obj, w_center, w_giou = (float(w) for w in weights)
+    _native.call("ov3d_matcher_cost", P, B, Q, G, C, int(final_last), pr, ldp, ob, ce, gi, gc, gl,
+                 w_cls, w_obj,
+                 w_center, w_giou, cost, like=gi)
+    return cost

@@ -125,3 +125,35 @@ def test_fused_losses_inside_graph_replay(cuda):
     crit = _criterion(cuda, 0.0, 0.0)
     vals = [_run(crit, st, batch, True, True, None)[0].item() for _ in range(5)]
     assert len(set(vals)) == 1, vals
+
+
+def test_matcher_cost_and_counts_match_torch(cuda):
+    """ov3d_matcher_cost / ov3d_targets_prep against Matcher.cost + the torch counts"""
+    from ov3d_amd import setloss, synthetic
+    from ov3d_amd.box_util import generalized_box3d_iou
+    B, Q, L, T, NB = 8, 128, 8, 21, 12
+    st = _outputs(cuda, B, Q, L, T, NB, seed=9)
+    batch = synthetic.make_batch(B, seed=10, num_points=2048, device=cuda)
+    crit = _criterion(cuda, 0.0, 0.0)
+    nact, nrep, nb, rot, total = setloss.target_counts(batch["gt_box_present"], batch, L)
+    ref_n = batch["gt_box_present"].sum(1).long()
+    assert torch.equal(nact, ref_n) and torch.equal(nrep, ref_n.repeat(L).int())
+    assert int(total) == int(ref_n.sum()) and float(nb) == max(float(ref_n.sum()), 1.0)
+    assert int(rot) == int((batch["gt_box_angles"] > 0).any())
+
+    def cat(k):
+        t = st[k]
+        return t.reshape(L * B, *t.shape[2:])
+
+    gious = generalized_box3d_iou(cat("box_corners").detach(), batch["gt_box_corners"].repeat(L, 1, 1, 1),
+                                  nrep, rotated_boxes=rot)
+    m = crit.matcher
+    cost = setloss.matcher_cost(cat("sem_cls_prob"), cat("objectness_prob"),
+                                cat("center_normalized").detach(), gious, batch, B,
+                                (m.cost_class, m.cost_objectness, m.cost_center, m.cost_giou))
+    cn = cat("center_normalized").detach()
+    gc = batch["gt_box_centers_normalized"].repeat(L, 1, 1)
+    dist = (cn[:, :, None, :] - gc[:, None, :, :]).abs().sum(-1)
+    ref = m.cost(cat("sem_cls_prob"), cat("objectness_prob"), dist, gious,
+                 batch["gt_box_sem_cls_label"].repeat(L, 1))
+    assert torch.allclose(cost, ref, rtol=1e-6, atol=1e-6), (cost - ref).abs().max()
