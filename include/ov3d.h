@@ -146,11 +146,12 @@ int ov3d_sa_layer_dy(const void* yprev, const float* scale, const float* shift, 
 int ov3d_reduce_partials(const double* partials, int nparts, int width, double* totals,
                          void* stream);
 /* training BN: totals (2,C) over `count` rows -> mean, invstd, scale = gamma*invstd,
- * shift = beta - mean*scale; running stats updated (momentum, unbiased var) if non-NULL */
+ * shift = beta - mean*scale; running stats updated (momentum, unbiased var) if non-NULL;
+ * num_batches_tracked (int64) += 1 if non-NULL (nn.BatchNorm1d's counter) */
 int ov3d_bn_finalize(const double* totals, double count, int C, const float* gamma,
                      const float* beta, float eps, float momentum, float* running_mean,
                      float* running_var, float* mean_out, float* invstd_out, float* scale_out,
-                     float* shift_out, void* stream);
+                     float* shift_out, long long* num_batches_tracked, void* stream);
 /* pooled output (P,N) f32 = relu(scale*(scale >= 0 ? pmax : pmin) + shift), plus the
  * selected value / row for the backward */
 int ov3d_sa_pool_fwd(const float* pmax, const float* pmin, const uint8_t* imax,
@@ -382,6 +383,13 @@ int ov3d_resnorm_fwd(long long R, int C, const void* src, int src_bf16, const vo
                      void* xap, float* xb, void* stream);
 /* backward: ds (fp32, grad of s from its other consumers) or NULL, dxa / dxap (bf16),
  * dxb (fp32) or NULL -> dsrc (fp32), dy (bf16 | fp32), dpos (= dxap), dga/dba/dgb/dbb.
+ * dxb_inner > 0: dxb row r lives at (r / dxb_inner) * dxb_s0 + (r % dxb_inner) * dxb_s1
+ * (a strided (L, B, C) view, e.g. one layer of the stacked decoder outputs' gradient);
+ * dxb_inner = 0: contiguous rows.
+ * accumulate (bit mask): 1 dpos, 2 dga/dba, 4 dgb/dbb are added to (old + new) instead of
+ * written — one gradient buffer shared by the calls that use the same pos / norm (the
+ * decoder: query_pos in 16 calls, the decoder norm in 8), summed in backward order as
+ * autograd's fan-in would.
  * partials: (nparts, 4, C) f32 workspace with nparts = ov3d_resnorm_bwd_parts(R, C). */
 int ov3d_resnorm_bwd_parts(long long R, int C);
 /* FFN activation h = dropout(relu(y)) over contiguous bf16 (R, C) rows (transformer.py
@@ -392,10 +400,11 @@ int ov3d_relu_dropout_bwd(const void* h, const void* dh, long long n, float drop
                           void* stream);
 int ov3d_resnorm_bwd(long long R, int C, const float* s, const float* mean, const float* rstd,
                      const float* ds, const void* dxa, const void* dxap, const float* dxb,
+                     long long dxb_inner, long long dxb_s0, long long dxb_s1,
                      const float* ga, const float* gb, float dropout_p, const int64_t* seed,
                      int site, float* dsrc, void* dy, int dy_bf16, void* dpos, int dpos_bf16,
                      float* partials, int nparts, float* dga, float* dba, float* dgb, float* dbb,
-                     void* stream);
+                     int accumulate, void* stream);
 
 
 /* ---- Gradient clipping + AdamW over all parameter tensors (3 launches) ----

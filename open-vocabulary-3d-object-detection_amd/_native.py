@@ -35,7 +35,7 @@ _SIGS = {
     "ov3d_sa_layer_pool_fwd": "ppppiiiippppppip",
     "ov3d_sa_layer_dy": "ppppiiiippppppip",
     "ov3d_reduce_partials": "piipp",
-    "ov3d_bn_finalize": "pdippffppppppp",
+    "ov3d_bn_finalize": "pdippffpppppppp",
     "ov3d_sa_pool_fwd": "ppppppiipppp",
     "ov3d_sa_pool_bwd": "ppppppiippip",
     "ov3d_bn_bwd_finalize": "pdippppppppp",
@@ -65,7 +65,7 @@ _SIGS = {
     "ov3d_relu_dropout_fwd": "plifpipp",
     "ov3d_relu_dropout_bwd": "pplfpp",
     "ov3d_resnorm_fwd": "lipipifpipppippfppppppp",
-    "ov3d_resnorm_bwd": "lipppppppppfpippipipippppp",
+    "ov3d_resnorm_bwd": "lippppppplllppfpippipipippppip",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
                           "ov3d_wgrad_workspace", "ov3d_wgrad_tiles", "ov3d_set_loss_desc_size",

@@ -302,8 +302,10 @@ __global__ void bn_finalize_kernel(const double* __restrict__ totals, double cou
                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                    float eps, float momentum, float* running_mean, float* running_var,
                                    float* __restrict__ mean_out, float* __restrict__ invstd_out,
-                                   float* __restrict__ scale_out, float* __restrict__ shift_out) {
+                                   float* __restrict__ scale_out, float* __restrict__ shift_out,
+                                   long long* num_batches_tracked) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c == 0 && num_batches_tracked) *num_batches_tracked += 1;
     if (c >= C) return;
     const double mean = totals[c] / count;
     double var = totals[C + c] / count - mean * mean;
@@ -592,12 +594,13 @@ extern "C" int ov3d_reduce_partials(const double* partials, int nparts, int widt
 extern "C" int ov3d_bn_finalize(const double* totals, double count, int C, const float* gamma,
                                 const float* beta, float eps, float momentum, float* running_mean,
                                 float* running_var, float* mean_out, float* invstd_out,
-                                float* scale_out, float* shift_out, void* stream) {
+                                float* scale_out, float* shift_out, long long* num_batches_tracked,
+                                void* stream) {
     if (C <= 0 || count <= 0 || !totals || !mean_out || !invstd_out || !scale_out || !shift_out)
         return OV3D_EINVAL;
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(ov3d_cdiv(C, 256)), dim3(256), 0, ov3d_stream(stream),
                        totals, count, C, gamma, beta, eps, momentum, running_mean, running_var,
-                       mean_out, invstd_out, scale_out, shift_out);
+                       mean_out, invstd_out, scale_out, shift_out, num_batches_tracked);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

@@ -133,7 +133,7 @@ def _group_world(bn):
     return g, (torch.distributed.get_world_size(g) if g is not None else 1)
 
 
-def _stats_finalize(x, layout, R, C, gamma, beta, bns, rm, rv):
+def _stats_finalize(x, layout, R, C, gamma, beta, bns, rm, rv, nbt=None):
     """train-mode batch statistics of BN over R rows (x all ranks of a SyncBatchNorm group)
     -> (mean, invstd, scale, shift); running stats of the concatenated storages updated
     (momentum, unbiased var)."""
@@ -149,7 +149,7 @@ def _stats_finalize(x, layout, R, C, gamma, beta, bns, rm, rv):
         torch.distributed.all_reduce(tot, group=group)
     mean, invstd, scale, shift = (torch.empty(C, dtype=torch.float32, device=dev) for _ in range(4))
     nat.call("ov3d_bn_finalize", tot, float(R * world), C, gamma, beta, float(bn0.eps),
-             float(bn0.momentum), rm, rv, mean, invstd, scale, shift, like=x)
+             float(bn0.momentum), rm, rv, mean, invstd, scale, shift, nbt, like=x)
     return mean, invstd, scale, shift
 
 
@@ -288,10 +288,11 @@ class _BnReluRows(torch.autograd.Function):
     def forward(ctx, h, gamma, beta, bn, p, site):
         R, C = h.shape
         dev = h.device
-        bn.num_batches_tracked.add_(1)
+        nbt = bn.num_batches_tracked if (bn.track_running_stats and
+                                         bn.num_batches_tracked is not None) else None
         rowmajor = (C, 0, C)
         mean, invstd, scale, shift = _stats_finalize(h, rowmajor, R, C, gamma, beta, [bn],
-                                                     bn.running_mean, bn.running_var)
+                                                     bn.running_mean, bn.running_var, nbt)
         z = torch.empty((R, C), dtype=torch.bfloat16, device=dev)
         seed = flash._seed(dev)
         nat.call("ov3d_rows_bn_apply", h, int(h.dtype == torch.bfloat16), *rowmajor, R, C, scale,

@@ -90,6 +90,7 @@ class _BoxParam(torch.autograd.Function):
         ctx.save_for_backward(raw, qxyz, dmin, dmax)
         ctx.meta = (B, Q, NB)
         ctx.mark_non_differentiable(outs[9], outs[10])
+        ctx.set_materialize_grads(False)   # unused outputs: no zero-filled gradients
         return tuple(outs)
 
     @staticmethod
@@ -289,7 +290,8 @@ class Model3DETR(nn.Module):
         dims = [inputs["point_cloud_dims_min"].float(), inputs["point_cloud_dims_max"].float()]
         query_xyz, query_embed = self._query_rows(enc_xyz, dims)            # (B, Q, C)
         enc_pos = self.pos_embedding.rows(enc_xyz, input_range=dims).transpose(0, 1)
-        query_embed = query_embed.transpose(0, 1)                           # (Q, B, C)
+        # (Q, B, C) rows, made contiguous once: every decoder layer reads it twice
+        query_embed = query_embed.transpose(0, 1).contiguous()
         tgt = torch.zeros_like(query_embed)
         box_features = self.decoder(tgt, enc_feats, query_pos=query_embed, pos=enc_pos)[0]
         return self.get_box_predictions(query_xyz, dims, box_features)

@@ -26,7 +26,32 @@ from . import attention as flash
 
 Pending = namedtuple("Pending", "src y p site")
 
+
+class FanIn:
+    """Gradient fan-in of one tensor over the resnorm calls that read it (the decoder's
+    query_pos in 16 calls, its final norm's weight / bias in 8).  Autograd would return a
+    gradient from every call and add them (15 + 14 small add launches per step); here the
+    backward of the call that runs first writes the shared buffer, the others add to it
+    inside their launch (``accumulate``), and the call that runs last returns the sum — the
+    others return None.  The calls are chained through the residual stream, so their
+    backward order is fixed and the sum is the one autograd forms, in the same order."""
+
+    def __init__(self):
+        self.n = 0       # calls registered in the forward
+        self.seen = 0    # backward calls so far
+        self.bufs = None
+
+    def take(self):
+        """-> (first, last) for the next backward call"""
+        k = self.seen
+        self.seen += 1
+        last = self.seen == self.n
+        if last:
+            self.seen = 0
+        return k == 0, last
+
 enabled = True   # False: the plain module code under autocast as well (tests compare the two)
+fan_in = True    # False: every call returns its own pos / norm_b gradient (autograd sums them)
 
 
 def supported(x, *norms):
@@ -70,7 +95,7 @@ def _rows(t, C):
 class _ResNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, meta, src, y, pos, ga, ba, gb, bb):
-        p, site, want_a, want_ap, want_b, eps, shape = meta
+        p, site, want_a, want_ap, want_b, eps, shape, fans = meta
         C = shape[-1]
         srcr, yr, posr = _rows(src, C), _rows(y, C), _rows(pos, C)
         R = 1
@@ -89,8 +114,10 @@ class _ResNorm(torch.autograd.Function):
                      seed, site, ga, ba, posr, _dt_flag(posr), gb, bb, float(eps), s, mean, rstd,
                      xa, xap, xb, like=s)
         ctx.save_for_backward(s, mean, rstd, ga, gb)
+        ctx.set_materialize_grads(False)   # unused outputs: no zero-filled gradients
         ctx.meta = (p, site, R, C, shape, src.dtype if src is not None else None,
                     y.dtype if y is not None else None, pos.dtype if pos is not None else None)
+        ctx.fans = fans
         v = lambda t: t.view(shape) if t is not None else None   # noqa: E731
         return v(s), v(xa), v(xap), v(xb)
 
@@ -104,8 +131,16 @@ class _ResNorm(torch.autograd.Function):
         def g(t, dt):
             return t.reshape(R, C).to(dt).contiguous() if t is not None else None
 
-        ds, dxa, dxap, dxb = (g(ds, torch.float32), g(dxa, torch.bfloat16),
-                              g(dxap, torch.bfloat16), g(dxb, torch.float32))
+        # the decoder's layer outputs reach here as strided (L, B, C) views of the stacked
+        # outputs' gradient: read in place (row r at (r // B) * s0 + (r % B) * s1)
+        xb_map = (0, 0, 0)
+        if dxb is not None and dxb.dtype == torch.float32 and dxb.dim() == 3 and \
+                dxb.stride(2) == 1 and not dxb.is_contiguous() and len(shape) == 3 and \
+                tuple(dxb.shape) == tuple(shape) and dxb.stride(0) >= C and dxb.stride(1) >= C:
+            xb_map = (shape[1], dxb.stride(0), dxb.stride(1))
+        ds, dxa, dxap = g(ds, torch.float32), g(dxa, torch.bfloat16), g(dxap, torch.bfloat16)
+        if not xb_map[0]:
+            dxb = g(dxb, torch.float32)
         if ga is None:
             dxa = dxap = None
         if gb is None:
@@ -119,24 +154,53 @@ class _ResNorm(torch.autograd.Function):
         dba = torch.empty(C, dtype=torch.float32, device=dev) if (need[5] and has_a) else None
         dgb = torch.empty(C, dtype=torch.float32, device=dev) if (need[6] and has_b) else None
         dbb = torch.empty(C, dtype=torch.float32, device=dev) if (need[7] and has_b) else None
+        acc = 0
+        pos_fan, nb_fan = ctx.fans
+        ret_pos = ret_nb = True
+        if pos_fan is not None and need[3]:
+            first, ret_pos = pos_fan.take()
+            if first:   # this call's gradient (or zeros) starts the sum
+                pos_fan.bufs = dpos if dpos is not None else \
+                    torch.zeros((R, C), dtype=pos_dt, device=dev)
+            elif dpos is not None:
+                dpos, acc = pos_fan.bufs, acc | 1
+            if ret_pos:
+                dpos_ret, pos_fan.bufs = pos_fan.bufs, None
+        if nb_fan is not None and (need[6] or need[7]):
+            first, ret_nb = nb_fan.take()
+            if first:
+                z = lambda t, n: t if t is not None or not n else \
+                    torch.zeros(C, dtype=torch.float32, device=dev)   # noqa: E731
+                nb_fan.bufs = (z(dgb, need[6]), z(dbb, need[7]))
+            elif has_b:
+                dgb, dbb = nb_fan.bufs
+                acc |= 4
+            if ret_nb:
+                nb_ret, nb_fan.bufs = nb_fan.bufs, None
         lib = _native.load()
         nparts = lib.ov3d_resnorm_bwd_parts(R, C)
         partials = torch.empty((nparts, 4, C), dtype=torch.float32, device=dev) \
             if (has_a or has_b) else None
         seed = flash._seed(dev) if (p > 0 and dy is not None) else None
         if dsrc is not None or dy is not None or dpos is not None or has_a or has_b:
-            _native.call("ov3d_resnorm_bwd", R, C, s, mean, rstd, ds, dxa, dxap, dxb, ga, gb,
+            _native.call("ov3d_resnorm_bwd", R, C, s, mean, rstd, ds, dxa, dxap, dxb, *xb_map, ga, gb,
                          float(p) if dy is not None else 0.0, seed, site, dsrc, dy, _dt_flag(dy),
                          dpos, _dt_flag(dpos), partials, nparts, dga, dba,
-                         dgb, dbb, like=s)
+                         dgb, dbb, acc, like=s)
         v = lambda t: t.view(shape) if t is not None else None   # noqa: E731
         if dsrc is not None and src_dt != torch.float32:
             dsrc = dsrc.to(src_dt)
+        if pos_fan is not None and need[3]:
+            dpos = dpos_ret if ret_pos else None
+        if nb_fan is not None and (need[6] or need[7]):
+            dgb, dbb = nb_ret if ret_nb else (None, None)
         return None, v(dsrc), v(dy), v(dpos), dga, dba, dgb, dbb
 
 
-def resnorm(pend, norm_a=None, pos=None, want_a=True, want_ap=False, norm_b=None):
-    """-> (s, xa, xap, xb) for Pending(src, y, p, site); unwanted outputs are None."""
+def resnorm(pend, norm_a=None, pos=None, want_a=True, want_ap=False, norm_b=None, pos_fan=None,
+            norm_b_fan=None):
+    """-> (s, xa, xap, xb) for Pending(src, y, p, site); unwanted outputs are None.
+    pos_fan / norm_b_fan: FanIn shared by the calls that read the same pos / norm_b."""
     src, y, p, psite = pend
     ref = y if y is not None else src
     shape = tuple(ref.shape)
@@ -145,8 +209,15 @@ def resnorm(pend, norm_a=None, pos=None, want_a=True, want_ap=False, norm_b=None
     if want_ap and pos is None:
         raise ValueError("resnorm: xap needs pos")
     eps = (norm_a.eps if norm_a is not None else (norm_b.eps if norm_b is not None else 1e-5))
+    if not (fan_in and want_ap and pos is not None and pos.requires_grad):
+        pos_fan = None
+    if norm_b is None or not fan_in:
+        norm_b_fan = None
+    for fan in (pos_fan, norm_b_fan):
+        if fan is not None:
+            fan.n += 1
     meta = (float(p) if y is not None else 0.0, int(psite), bool(want_a), bool(want_ap),
-            norm_b is not None, eps, shape)
+            norm_b is not None, eps, shape, (pos_fan, norm_b_fan))
     ga = norm_a.weight if norm_a is not None else None
     ba = norm_a.bias if norm_a is not None else None
     gb = norm_b.weight if norm_b is not None else None

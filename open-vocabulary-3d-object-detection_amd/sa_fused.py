@@ -89,9 +89,11 @@ def _totals(partials, nparts, width, group):
 def _finalize(tot, count, bn, C):
     dev = tot.device
     mean, invstd, scale, shift = (torch.empty(C, dtype=torch.float32, device=dev) for _ in range(4))
-    bn.num_batches_tracked.add_(1)
+    nbt = bn.num_batches_tracked if (bn.track_running_stats and
+                                     bn.num_batches_tracked is not None) else None
     nat.call("ov3d_bn_finalize", tot, float(count), C, bn.weight, bn.bias, float(bn.eps),
-             float(bn.momentum), bn.running_mean, bn.running_var, mean, invstd, scale, shift, like=tot)
+             float(bn.momentum), bn.running_mean, bn.running_var, mean, invstd, scale, shift, nbt,
+             like=tot)
     return mean, invstd, scale, shift
 
 

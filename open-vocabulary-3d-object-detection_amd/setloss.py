@@ -108,6 +108,7 @@ class _SetLoss(torch.autograd.Function):
         ctx.shapes = tuple(t.shape if t is not None else None
                            for t in (logits, angle_logits, angle_res, center, size, gious, align))
         ctx.save_for_backward(raw)
+        ctx.set_materialize_grads(False)
         return table, total
 
     @staticmethod

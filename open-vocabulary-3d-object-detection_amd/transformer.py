@@ -122,6 +122,7 @@ class _MemoryKV(torch.autograd.Function):
         ctx.bufs = (dK, dV)
         ctx.params = params
         ctx.mark_non_differentiable(K_all, V_all, dK, dV, tok_grad)
+        ctx.set_materialize_grads(False)
         return K_all, V_all, dK, dV, token, tok_grad
 
     @staticmethod
@@ -258,7 +259,7 @@ class TransformerDecoderLayer(nn.Module):
         return tgt, None
 
     def forward_fused(self, s, x, xp, memory, memory_pos, query_pos=None, tgt_mask=None,
-                      memory_mask=None, kv=None, idx=0):
+                      memory_mask=None, kv=None, idx=0, pos_fan=None):
         """bf16 step from norm1's outputs (x = norm1(tgt), xp = x + query_pos) -> Pending of
         the layer output (resnorm.py)."""
         p1, p2, p3 = ((self.dropout1.p, self.dropout2.p, self.dropout3.p) if self.training
@@ -267,7 +268,8 @@ class TransformerDecoderLayer(nn.Module):
         qk = xp if query_pos is not None else x
         y = self.self_attn(qk, qk, x, attn_mask=tgt_mask)
         s, x2, q, _ = rn.resnorm(rn.Pending(s, y, p1, site1), self.norm2, pos=query_pos,
-                                 want_a=query_pos is None, want_ap=query_pos is not None)
+                                 want_a=query_pos is None, want_ap=query_pos is not None,
+                                 pos_fan=pos_fan)
         qx = q if query_pos is not None else x2
         if kv is not None and memory_mask is None:
             y = self.multihead_attn.forward_kv(qx, kv, idx)
@@ -431,18 +433,21 @@ class TransformerDecoder(nn.Module):
         pend = rn.Pending(tgt, None, 0.0, 0)
         inter = []
         dec_norm = self.norm if self.return_intermediate else None
+        # query_pos and the decoder norm are read by many launches: one gradient buffer each
+        pos_fan, nb_fan = rn.FanIn(), rn.FanIn()
         for i, layer in enumerate(self.layers):
             s, x, xp, xd = rn.resnorm(pend, layer.norm1, pos=query_pos, want_a=True,
                                       want_ap=query_pos is not None,
-                                      norm_b=dec_norm if i > 0 else None)
+                                      norm_b=dec_norm if i > 0 else None, pos_fan=pos_fan,
+                                      norm_b_fan=nb_fan)
             if i > 0 and dec_norm is not None:
                 inter.append(xd)
             kvi = None
             if kv is not None:   # the token gradient is returned once (by layer 0)
                 kvi = kv[:5] + ((kv[5] if i == 0 else None),)
             pend = layer.forward_fused(s, x, xp, memory, memory_pos, query_pos, tgt_mask,
-                                       memory_mask, kv=kvi, idx=i)
-        s, _, _, xd = rn.resnorm(pend, norm_b=self.norm)
+                                       memory_mask, kv=kvi, idx=i, pos_fan=pos_fan)
+        s, _, _, xd = rn.resnorm(pend, norm_b=self.norm, norm_b_fan=nb_fan)
         out = xd if self.norm is not None else s
         if self.return_intermediate:
             if self.norm is None:

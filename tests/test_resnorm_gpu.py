@@ -149,6 +149,50 @@ def test_encoder_decoder_fused_vs_plain_bf16(cuda):
         assert e_fused < 0.1, (i, e_fused)
 
 
+@pytest.mark.parametrize("pos_bf16", [False, True])
+def test_decoder_fan_in_and_strided_grads_bitwise(cuda, pos_bf16):
+    """the shared query_pos / decoder-norm gradient buffers (resnorm.FanIn, accumulate
+    launches) give autograd's per-call sums bit for bit, and the decoder outputs' gradient
+    read in place as a strided (L, B, Q, C) view equals the contiguous one"""
+    from ov3d_amd import attention as flash
+    from ov3d_amd import resnorm as rn
+    from ov3d_amd.transformer import TransformerDecoder, TransformerDecoderLayer
+    torch.manual_seed(3)
+    dec = TransformerDecoder(TransformerDecoderLayer(256, 4, 256, dropout=0.1), 4,
+                             return_intermediate=True)
+    with torch.no_grad():
+        for m in dec.modules():
+            if isinstance(m, torch.nn.LayerNorm):
+                m.weight.normal_(1, 0.1)
+                m.bias.normal_(0, 0.1)
+    dec = dec.to(cuda).train()
+    flash.next_step(cuda)
+    tgt = torch.zeros(64, 2, 256, device=cuda)
+    mem = torch.randn(256, 2, 256, device=cuda)
+    qpos = torch.randn(64, 2, 256, device=cuda).to(torch.bfloat16 if pos_bf16 else torch.float32)
+    mpos = torch.randn(256, 2, 256, device=cuda)
+    g = torch.randn((4, 2, 64, 256), device=cuda)
+    res = {}
+    for mode in ("autograd", "fan", "fan_strided"):
+        rn.fan_in = mode != "autograd"
+        try:
+            dec.zero_grad(set_to_none=True)
+            q = qpos.clone().requires_grad_()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                out, _ = dec(tgt, mem, query_pos=q, pos=mpos)        # (L, Q, B, C)
+            if mode == "fan_strided":   # as model_3detr: (L, B, Q, C) rows of the stack
+                (out.permute(0, 2, 1, 3).reshape(-1, 256) * g.reshape(-1, 256)).sum().backward()
+            else:
+                (out * g.permute(0, 2, 1, 3).contiguous()).sum().backward()
+            res[mode] = [out.detach().clone(), q.grad.clone()] + \
+                [p.grad.clone() for p in dec.parameters()]
+        finally:
+            rn.fan_in = True
+    for mode in ("fan", "fan_strided"):
+        for i, (a, b) in enumerate(zip(res[mode], res["autograd"])):
+            assert torch.equal(a, b), (mode, i, (a.float() - b.float()).abs().max().item())
+
+
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_relu_dropout_matches_torch(cuda, p):
     from ov3d_amd import attention as flash

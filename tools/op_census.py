@@ -39,6 +39,8 @@ def main():
     ov3d_import.load()
     from ov3d_amd import synthetic
     from bench import build, default_args, train_step
+    from ov3d_amd import gemm
+    gemm.DEFER_WGRAD = True   # as bench.py's captured step
     args = default_args()
     dev = torch.device("cuda")
     model, crit, opt = build(args, dev)
