@@ -81,10 +81,10 @@ class StepGraph:
 
     Sampling prefetch (prefetch_fps=True): the pre-encoder's furthest-point
     sampling depends on the input points only, and runs on 8 of the 256 CUs for
-    ~3 ms.  It is computed for the NEXT batch on its own stream, concurrently
-    with this batch's graph replay, and handed to the next replay
-    (Model3DETR.run_encoder(pre_enc_inds=...)).  Each step still samples
-    exactly one batch; results are identical.  step(batch, next_batch) keeps the
+    ~3 ms; so do its ball query and the query FPS (Model3DETR.sampling_plan).  The
+    plan is computed for the NEXT batch on its own stream, concurrently with this
+    batch's graph replay, and handed to the next replay (as extra model inputs).  Each
+    step still samples exactly one batch; results are identical.  step(batch, next_batch) keeps the
     pipeline primed; a batch that was not announced as `next_batch` is sampled
     eagerly first."""
 
@@ -102,7 +102,7 @@ class StepGraph:
         if self.prefetch:
             self.npoint = model.pre_encoder.npoint
             self.next_pc = self.static["point_clouds"].clone()
-            self.inds_cur = self._sample(self.static["point_clouds"])
+            self.plan_cur = self._sample(self.static["point_clouds"])
         self.fps_stream = torch.cuda.Stream()
         self.side = torch.cuda.Stream()
         self.side.wait_stream(torch.cuda.current_stream())
@@ -111,7 +111,7 @@ class StepGraph:
                 self._body(gemm)
         torch.cuda.current_stream().wait_stream(self.side)
         if self.prefetch:
-            self.inds_cur.copy_(self._sample(self.static["point_clouds"]))
+            self._set_plan(self._sample(self.static["point_clouds"]))
         self.graph = torch.cuda.CUDAGraph()
         self.opt.zero_grad(set_to_none=True)
         # with a process group the RCCL collectives are captured too; the watchdog thread of
@@ -122,7 +122,16 @@ class StepGraph:
             self.loss = self._body(gemm)
 
     def _sample(self, pc):
-        return self._pu.furthest_point_sample(pc[..., 0:3].contiguous(), self.npoint)
+        """-> dict of the step's point-only index work (extra model inputs)"""
+        if hasattr(self.model, "sampling_plan"):
+            return self.model.sampling_plan(pc)
+        return {"pre_enc_inds": self._pu.furthest_point_sample(pc[..., 0:3].contiguous(),
+                                                               self.npoint)}
+
+    def _set_plan(self, plan):
+        from . import _native
+        keys = list(self.plan_cur)
+        _native.multi_copy([self.plan_cur[k] for k in keys], [plan[k] for k in keys])
 
     def _body(self, gemm):
         if not getattr(self.opt, "writes_shadows", False):
@@ -130,7 +139,7 @@ class StepGraph:
         self.opt.zero_grad(set_to_none=True)
         inputs = {k: self.static[k] for k in IN_KEYS}
         if self.prefetch:
-            inputs["pre_enc_inds"] = self.inds_cur
+            inputs.update(self.plan_cur)
         with torch.autocast("cuda", dtype=self.amp_dtype or torch.float32,
                             enabled=self.amp_dtype is not None):
             out = self.model(inputs)
@@ -156,17 +165,18 @@ class StepGraph:
             self.graph.replay()
             return self.loss
         if self._expected is None or batch["point_clouds"] is not self._expected:
-            self.inds_cur.copy_(self._sample(self.static["point_clouds"]))
+            self._set_plan(self._sample(self.static["point_clouds"]))
         nb = next_batch if next_batch is not None else batch
         self.next_pc.copy_(nb["point_clouds"], non_blocking=True)
         self._expected = nb["point_clouds"]
-        # the next batch's FPS runs on its own stream (own hardware queue), concurrently with
-        # this step's graph; the graph reads inds_cur only
+        # the next batch's sampling plan runs on its own stream (own hardware queue),
+        # concurrently with this step's graph; the graph reads plan_cur only
         self.fps_stream.wait_stream(cur)
         with torch.cuda.stream(self.fps_stream):
             nxt = self._sample(self.next_pc)
         self.graph.replay()
         cur.wait_stream(self.fps_stream)
-        nxt.record_stream(cur)
-        self.inds_cur.copy_(nxt)
+        for t in nxt.values():
+            t.record_stream(cur)
+        self._set_plan(nxt)
         return self.loss

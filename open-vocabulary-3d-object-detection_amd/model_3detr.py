@@ -156,8 +156,9 @@ class Model3DETR(nn.Module):
         query_xyz, rows = self._query_rows(encoder_xyz, point_cloud_dims)
         return query_xyz, rows.permute(0, 2, 1)
 
-    def _query_rows(self, encoder_xyz, point_cloud_dims):
-        _, query_xyz = pu.furthest_point_sample_gather(encoder_xyz, self.num_queries)
+    def _query_rows(self, encoder_xyz, point_cloud_dims, query_xyz=None):
+        if query_xyz is None:
+            _, query_xyz = pu.furthest_point_sample_gather(encoder_xyz, self.num_queries)
         pe = self.pos_embedding.rows(query_xyz, input_range=point_cloud_dims)      # (B, Q, C)
         B, Q, C = pe.shape
         return query_xyz, self.query_projection.rows(pe.reshape(B * Q, C)).view(B, Q, -1)
@@ -168,12 +169,39 @@ class Model3DETR(nn.Module):
         feats = pc[..., 3:].transpose(1, 2).contiguous() if pc.size(-1) > 3 else None
         return xyz, feats
 
-    def run_encoder(self, point_clouds, pre_enc_inds=None):
-        """pre_enc_inds: optional furthest-point-sample indices of the pre-encoder computed
-        ahead of time (they depend on the input points only; graphs.StepGraph computes the
-        next batch's on a side stream while this one trains).  Identical results."""
+    # index work that depends on the input points only (sampling_plan)
+    PLAN_KEYS = ("pre_enc_inds", "pre_enc_xyz", "pre_enc_ball", "query_xyz")
+
+    def _encoder_keeps_xyz(self):
+        from .transformer import MaskedTransformerEncoder
+        return not isinstance(self.encoder, MaskedTransformerEncoder)
+
+    @torch.no_grad()
+    def sampling_plan(self, point_clouds):
+        """The step's sampling and neighbourhood indices, which depend on the input points
+        only: pre-encoder FPS (indices + points), its ball query, and (when the encoder keeps
+        its input points) the query FPS.  graphs.StepGraph computes the next batch's plan on
+        a side stream while this batch trains; forward(inputs | plan) gives results
+        identical to forward(inputs)."""
+        xyz = point_clouds[..., 0:3].contiguous()
+        pe = self.pre_encoder
+        inds, pre_xyz = pu.furthest_point_sample_gather(xyz, pe.npoint)
+        plan = {"pre_enc_inds": inds, "pre_enc_xyz": pre_xyz,
+                "pre_enc_ball": pu.ball_query(pe.grouper.radius, pe.grouper.nsample, xyz, pre_xyz)}
+        if self._encoder_keeps_xyz():
+            plan["query_xyz"] = pu.furthest_point_sample_gather(pre_xyz, self.num_queries)[1]
+        return plan
+
+    def run_encoder(self, point_clouds, pre_enc_inds=None, plan=None):
+        """pre_enc_inds / plan: the pre-encoder's sampling computed ahead of time (they
+        depend on the input points only; see sampling_plan).  Identical results."""
+        plan = plan or {}
+        pre_enc_inds = plan.get("pre_enc_inds", pre_enc_inds)
         xyz, feats = self._break_up_pc(point_clouds)
-        pre_xyz, pre_feats, pre_inds = self.pre_encoder(xyz, feats, inds=pre_enc_inds)
+        pre_xyz, pre_feats, pre_inds = self.pre_encoder(
+            xyz, feats, inds=pre_enc_inds,
+            new_xyz=plan.get("pre_enc_xyz") if pre_enc_inds is not None else None,
+            ball=plan.get("pre_enc_ball") if pre_enc_inds is not None else None)
         # (B, C, M) view of channels-last rows -> seq-first (M, B, C)
         enc_xyz, enc_feats, enc_inds = self.encoder(pre_feats.permute(2, 0, 1).contiguous(), xyz=pre_xyz)
         if enc_inds is None:
@@ -282,13 +310,14 @@ class Model3DETR(nn.Module):
         pc = inputs["point_clouds"]
         if self.training and pc.is_cuda:
             flash.next_step(pc.device)   # fresh attention-dropout stream for this step
-        enc_xyz, enc_feats, _ = self.run_encoder(pc, inputs.get("pre_enc_inds"))   # (N', B, C)
+        plan = {k: inputs[k] for k in self.PLAN_KEYS if k in inputs}
+        enc_xyz, enc_feats, _ = self.run_encoder(pc, plan=plan)   # (N', B, C)
         Np, B, C = enc_feats.shape
         enc_feats = self.encoder_to_decoder_projection.rows(enc_feats.reshape(Np * B, C)).view(Np, B, -1)
         if encoder_only:
             return enc_xyz, enc_feats.transpose(0, 1)
         dims = [inputs["point_cloud_dims_min"].float(), inputs["point_cloud_dims_max"].float()]
-        query_xyz, query_embed = self._query_rows(enc_xyz, dims)            # (B, Q, C)
+        query_xyz, query_embed = self._query_rows(enc_xyz, dims, plan.get("query_xyz"))   # (B, Q, C)
         enc_pos = self.pos_embedding.rows(enc_xyz, input_range=dims).transpose(0, 1)
         # (Q, B, C) rows, made contiguous once: every decoder layer reads it twice
         query_embed = query_embed.transpose(0, 1).contiguous()

@@ -164,11 +164,16 @@ class QueryAndGroup(nn.Module):
         self.radius, self.nsample = radius, nsample
         self.use_xyz, self.ret_grouped_xyz, self.normalize_xyz = use_xyz, ret_grouped_xyz, normalize_xyz
 
-    def rows(self, xyz, new_xyz, features=None):
-        """Grouped features as channels-last rows (B, npoint, nsample, 3+C)."""
+    def rows(self, xyz, new_xyz, features=None, idx=None):
+        """Grouped features as channels-last rows (B, npoint, nsample, 3+C).  idx: the
+        ball-query indices of (xyz, new_xyz) when computed ahead of time."""
         if xyz.requires_grad or new_xyz.requires_grad:
             raise NotImplementedError("gradients w.r.t. point coordinates are not on the path")
-        idx = ball_query(self.radius, self.nsample, xyz, new_xyz)
+        if idx is None:
+            idx = ball_query(self.radius, self.nsample, xyz, new_xyz)
+        elif idx.dtype != torch.int32 or tuple(idx.shape) != (xyz.shape[0], new_xyz.shape[1],
+                                                              self.nsample):
+            raise ValueError("idx must be int32 (B, npoint, nsample)")
         xyz = _f32(xyz, "xyz", 3)
         new_xyz = _f32(new_xyz, "new_xyz", 3)
         if features is not None:

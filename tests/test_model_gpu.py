@@ -208,3 +208,29 @@ def test_step_graph_equals_eager_step(cuda):
             torch.testing.assert_close(bg[k], v, rtol=1e-3, atol=1e-5, msg=k)
         else:
             assert torch.equal(bg[k], v), k
+
+
+def test_sampling_plan_inputs_give_identical_forward(cuda):
+    """Model3DETR.sampling_plan (pre-encoder FPS + points, its ball query, the query FPS:
+    computed ahead of time by graphs.StepGraph on a side stream) fed back as inputs gives
+    the forward without it, bit for bit"""
+    import ov3d_amd
+    from ov3d_amd import synthetic
+    from ov3d_amd.dataset_config import SunrgbdDatasetConfig
+    from bench import default_args
+    args = default_args(enc_dropout=0.0, dec_dropout=0.0, mlp_dropout=0.0, preenc_npoints=512,
+                        nqueries=64)
+    cfg = SunrgbdDatasetConfig()
+    torch.manual_seed(0)
+    model, _ = ov3d_amd.build_model(args, cfg, text_embedding=synthetic.text_embedding())
+    model = model.to(cuda).train()
+    b = synthetic.make_batch(2, seed=6, num_points=4096, device=cuda)
+    inputs = {k: b[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")}
+    plan = model.sampling_plan(b["point_clouds"])
+    assert set(plan) == set(model.PLAN_KEYS)
+    outs = []
+    for extra in ({}, plan):
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            outs.append(model({**inputs, **extra}))
+    for k in ("sem_cls_logits", "center_unnormalized", "size_unnormalized", "angle_continuous"):
+        assert torch.equal(outs[0]["outputs"][k], outs[1]["outputs"][k]), k
