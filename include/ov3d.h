@@ -457,6 +457,18 @@ int ov3d_box_param_bwd(long long R, int B, int Q, int NB, const float* raw, long
                        const float* g_ares, const float* g_angle, const float* g_corners,
                        float* draw, long long ldd, void* stream);
 
+/* ---- short row-block GEMMs (csrc/rowsgemm.hip): the decoder's nn.Linear layers ----
+ * Replaces the library GEMMs under F.linear / the input-gradient matmul of
+ * models/transformer.py:355-379 (M = nqueries * batch rows).  bf16 in / out, fp32 sums:
+ *   trans_b = 1: C (M x N) = A (M x K) W^T + bias   W (N x K) row-major (nn.Linear weight)
+ *   trans_b = 0: C (M x N) = A (M x K) W             W (K x N) row-major (bias must be NULL)
+ * N % 32 == 0, K % 64 == 0, K <= 1024; 16-byte aligned A / W, lda / ldw % 8 == 0,
+ * ldc % 4 == 0; bias (N) bf16 or NULL. */
+int ov3d_rows_gemm_supported(int M, int N, int K);
+int ov3d_rows_gemm(int M, int N, int K, const void* A, long long lda, const void* W,
+                   long long ldw, int trans_b, const void* bias, void* C, long long ldc,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

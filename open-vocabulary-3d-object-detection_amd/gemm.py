@@ -28,6 +28,54 @@ def _chunks(R, cout, cin):
 
 _F32_OUT = None   # does this build's bmm take out_dtype=float32 for bf16 inputs (hipBLASLt)?
 
+# Short row blocks (the decoder: nqueries * batch = 1024 rows) run on csrc/rowsgemm.hip: one
+# memory round trip per launch instead of a library GEMM's K pipeline.  Longer row blocks
+# stay on hipBLASLt, whose large tiles reuse operands across rows.
+ROWS_GEMM = True
+ROWS_GEMM_MAX_M = 2048
+
+
+def _rows_gemm_ok(a, w, trans_b):
+    if not (ROWS_GEMM and a.is_cuda and a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and a.dim() == 2 and w.dim() == 2 and a.stride(1) == 1 and w.stride(1) == 1):
+        return False
+    M, K = a.shape
+    N = w.shape[0] if trans_b else w.shape[1]
+    if M > ROWS_GEMM_MAX_M or (w.shape[1] if trans_b else w.shape[0]) != K:
+        return False
+    if a.data_ptr() % 16 or w.data_ptr() % 16 or a.stride(0) % 8 or w.stride(0) % 8:
+        return False
+    from . import _native
+    return bool(_native.load().ov3d_rows_gemm_supported(M, N, K))
+
+
+def rows_gemm(a, w, bias=None, trans_b=True):
+    """a (M, K) bf16 rows; w bf16 (N, K) when trans_b (y = a w^T + bias, nn.Linear) else
+    (K, N) (y = a w) -> (M, N) bf16 (csrc/rowsgemm.hip; check _rows_gemm_ok first)"""
+    from . import _native
+    M, K = a.shape
+    N = w.shape[0] if trans_b else w.shape[1]
+    out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    if bias is not None and (bias.dtype != torch.bfloat16 or not bias.is_contiguous()):
+        bias = bias.to(torch.bfloat16).contiguous()
+    _native.call("ov3d_rows_gemm", M, N, K, a, a.stride(0), w, w.stride(0), int(trans_b), bias,
+                 out, N, like=a)
+    return out
+
+
+def _linear(x, w, b):
+    """F.linear on bf16 rows (bias in the epilogue), short row blocks on rowsgemm"""
+    if _rows_gemm_ok(x, w, True):
+        return rows_gemm(x, w, b, trans_b=True)
+    return torch.nn.functional.linear(x, w, b)
+
+
+def _dgrad(dy, w):
+    """dy (M, N) @ w (N, K) for the input gradient of a linear layer"""
+    if _rows_gemm_ok(dy, w, False):
+        return rows_gemm(dy, w, trans_b=False)
+    return dy @ w
+
 
 def _bmm_f32(a, b):
     """bf16 x bf16 -> fp32 batched GEMM without rounding the per-chunk partials to bf16."""
@@ -267,7 +315,7 @@ class _RowsLinear(Function):
             else x.dtype
         xc, wc = x.to(dt), cast_param(w, dt)
         with torch.autocast("cuda", enabled=False):
-            y = torch.nn.functional.linear(xc, wc, cast_param(b, dt))   # bias in the GEMM epilogue
+            y = _linear(xc, wc, cast_param(b, dt))   # bias in the GEMM epilogue
         ctx.save_for_backward(xc, wc)
         ctx.meta = (x.dtype, w.dtype, b is not None)
         ctx.params = (w, b)
@@ -279,7 +327,7 @@ class _RowsLinear(Function):
         xdt, wdt, has_b = ctx.meta
         dy = dy.to(xc.dtype).contiguous()
         with torch.autocast("cuda", enabled=False):
-            dx = (dy @ wc).to(xdt) if ctx.needs_input_grad[0] else None
+            dx = _dgrad(dy, wc).to(xdt) if ctx.needs_input_grad[0] else None
             want_b = has_b and ctx.needs_input_grad[2]
             w, b = ctx.params
             if ctx.needs_input_grad[1] and can_defer(xc, w, b if want_b else None):
@@ -319,7 +367,7 @@ class _InProj(Function):
         with torch.autocast("cuda", enabled=False):
             for x, (r0, r1) in zip(xs, spec):
                 xc = x.reshape(-1, x.shape[-1]).to(dt)
-                y = torch.nn.functional.linear(xc, wc[r0:r1], bc[r0:r1] if bc is not None else None)
+                y = _linear(xc, wc[r0:r1], bc[r0:r1] if bc is not None else None)
                 outs.append(y.view(*x.shape[:-1], r1 - r0))
                 saved.append(xc)
         ctx.save_for_backward(wc, *saved)
@@ -348,7 +396,7 @@ class _InProj(Function):
                 if dy is None:
                     dy = torch.zeros(xc.shape[0], r1 - r0, dtype=xc.dtype, device=xc.device)
                 dy = dy.reshape(-1, r1 - r0).to(xc.dtype).contiguous()
-                dxs.append((dy @ wc[r0:r1]).to(xdts[i]).view(xshapes[i])
+                dxs.append(_dgrad(dy, wc[r0:r1]).to(xdts[i]).view(xshapes[i])
                            if ctx.needs_input_grad[3 + i] else None)
                 if defer:
                     defer_weight_grad(dy, xc, wp, bp if want_b else None, rows=(r0, r1))
