@@ -468,6 +468,16 @@ int ov3d_rows_gemm_supported(int M, int N, int K);
 int ov3d_rows_gemm(int M, int N, int K, const void* A, long long lda, const void* W,
                    long long ldw, int trans_b, const void* bias, void* C, long long ldc,
                    void* stream);
+/* the same with the transformer FFN activation fused into the epilogue:
+ *   epilogue 1: C = dropout_p(relu(bf16(A W^T + bias)))  (keep = hash of (*seed, site, row,
+ *               column) as ov3d_relu_dropout_fwd — identical output)
+ *   epilogue 2: C = H > 0 ? bf16(bf16(A W) / (1 - dropout_p)) : 0  (H: the activation
+ *               output, (M x N) bf16 rows of ldh; as ov3d_relu_dropout_bwd)
+ *   epilogue 0: ov3d_rows_gemm. */
+int ov3d_rows_gemm_act(int M, int N, int K, const void* A, long long lda, const void* W,
+                       long long ldw, int trans_b, const void* bias, int epilogue,
+                       float dropout_p, const int64_t* seed, int site, const void* H,
+                       long long ldh, void* C, long long ldc, void* stream);
 
 #ifdef __cplusplus
 }

@@ -67,6 +67,7 @@ _SIGS = {
     "ov3d_resnorm_fwd": "lipipifpipppippfppppppp",
     "ov3d_resnorm_bwd": "lippppppplllppfpippipipippppip",
     "ov3d_rows_gemm": "iiiplplipplp",
+    "ov3d_rows_gemm_act": "iiiplplipifpiplplp",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
                           "ov3d_wgrad_workspace", "ov3d_wgrad_tiles", "ov3d_set_loss_desc_size",

@@ -15,7 +15,14 @@
 //   trans_b = 0: the W tile (k rows x 32 columns) goes through LDS and is read transposed
 //                with ds_read_b64_tr_b16 (k order 8(j>>2) + 4h + (j&3) inside a 16-k step;
 //                A's fragment is loaded in the same k order).
+// Epilogues (ov3d_rows_gemm_act) fuse the FFN activation of the transformer layers
+// (models/transformer.py:276-278, 375-377: linear1 -> ReLU -> dropout):
+//   EPI_RELU_DROP: out = dropout(relu(bf16(acc + bias)))   (the rowdrop.h keep hash, as
+//                  ov3d_relu_dropout_fwd: identical output)
+//   EPI_MASK:      out = h > 0 ? bf16(bf16(acc) / (1 - p)) : 0   (the input gradient of
+//                  linear2 through that activation, as ov3d_relu_dropout_bwd)
 #include "common.h"
+#include "rowdrop.h"
 
 namespace {
 
@@ -29,6 +36,7 @@ constexpr int kWaves = 4;
 constexpr int kTile = 32;
 constexpr int kMaxSteps = 16;   // 16-k MFMA steps per wave: K <= 4 * 16 * 16 = 1024
 constexpr int LDW = 40;         // LDS row of the (k, 32 columns) W tile, bf16 elements (80 B)
+enum { EPI_NONE = 0, EPI_RELU_DROP = 1, EPI_MASK = 2 };
 
 struct GemmArgs {
     const bf16* A; long long lda;
@@ -36,6 +44,8 @@ struct GemmArgs {
     const bf16* bias;
     bf16* C; long long ldc;
     int M, N, K;
+    int epi; uint32_t thresh; float keep_scale; const int64_t* seed; uint32_t site;
+    const bf16* H; long long ldh;   // EPI_MASK: the activation output
 };
 
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
@@ -109,16 +119,38 @@ __global__ void __launch_bounds__(256) rows_gemm_kernel(GemmArgs a) {
     for (int v = 0; v < 16; ++v) red[w][(v & 3) + 8 * (v >> 2) + 4 * h][r] = acc[v];
     __syncthreads();
     const int orow = threadIdx.x >> 3, oc = (threadIdx.x & 7) * 4;
-    if (m0 + orow >= a.M) return;
+    const int gr = m0 + orow, gc = n0 + oc;
+    if (gr >= a.M) return;
+    bool keep[4] = {true, true, true, true};
+    if (a.epi == EPI_RELU_DROP && a.thresh) {
+        // rowdrop.h: one hash per channel pair of row gr
+        const uint32_t rb = rowdrop::row_base(rowdrop::seed_mix(a.seed, a.site), gr);
+#pragma unroll
+        for (int j = 0; j < 4; j += 2) {
+            const uint32_t hs = rowdrop::mix24(rb + (uint32_t)((gc + j) >> 1) * 0x27D4EB2Fu);
+            keep[j] = (hs & 0xffffu) >= a.thresh;
+            keep[j + 1] = (hs >> 16) >= a.thresh;
+        }
+    }
+    bf16x4 hv;
+    if (a.epi == EPI_MASK) hv = *reinterpret_cast<const bf16x4*>(a.H + (size_t)gr * a.ldh + gc);
     bf16x4 o;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         float t = (red[0][orow][oc + q] + red[1][orow][oc + q]) +
                   (red[2][orow][oc + q] + red[3][orow][oc + q]);
-        if (a.bias) t += (float)a.bias[n0 + oc + q];
-        o[q] = (bf16)t;
+        if (a.bias) t += (float)a.bias[gc + q];
+        const bf16 y = (bf16)t;
+        if (a.epi == EPI_RELU_DROP) {
+            const float r = fmaxf((float)y, 0.f);
+            o[q] = a.thresh ? (keep[q] ? (bf16)(r * a.keep_scale) : (bf16)0.f) : (bf16)r;
+        } else if (a.epi == EPI_MASK) {
+            o[q] = (float)hv[q] > 0.f ? (bf16)((float)y * a.keep_scale) : (bf16)0.f;
+        } else {
+            o[q] = y;
+        }
     }
-    *reinterpret_cast<bf16x4*>(a.C + (size_t)(m0 + orow) * a.ldc + n0 + oc) = o;
+    *reinterpret_cast<bf16x4*>(a.C + (size_t)gr * a.ldc + gc) = o;
 }
 
 template <int TB>
@@ -144,15 +176,29 @@ extern "C" int ov3d_rows_gemm_supported(int M, int N, int K) {
            K / (16 * kWaves) <= kMaxSteps;
 }
 
-extern "C" int ov3d_rows_gemm(int M, int N, int K, const void* A, long long lda, const void* W,
-                              long long ldw, int trans_b, const void* bias, void* C, long long ldc,
-                              void* stream) {
+extern "C" int ov3d_rows_gemm_act(int M, int N, int K, const void* A, long long lda, const void* W,
+                                  long long ldw, int trans_b, const void* bias, int epilogue,
+                                  float dropout_p, const int64_t* seed, int site, const void* H,
+                                  long long ldh, void* C, long long ldc, void* stream) {
     if (!ov3d_rows_gemm_supported(M, N, K) || !A || !W || !C) return OV3D_EINVAL;
     // 16-byte operand loads, 8-byte output stores
     if (((uintptr_t)A | (uintptr_t)W) % 16 || (uintptr_t)C % 8 || (bias && (uintptr_t)bias % 2) ||
         lda % 8 || ldw % 8 || ldc % 4 || lda < K || ldc < N || ldw < (trans_b ? K : N))
         return OV3D_EINVAL;
-    GemmArgs a{(const bf16*)A, lda, (const bf16*)W, ldw, (const bf16*)bias, (bf16*)C, ldc, M, N, K};
+    if (epilogue < EPI_NONE || epilogue > EPI_MASK || dropout_p < 0.f || dropout_p >= 1.f)
+        return OV3D_EINVAL;
+    if (epilogue == EPI_RELU_DROP && dropout_p > 0.f && !seed) return OV3D_EINVAL;
+    if (epilogue == EPI_MASK && (!H || (uintptr_t)H % 8 || ldh % 4 || ldh < N)) return OV3D_EINVAL;
+    GemmArgs a{(const bf16*)A, lda, (const bf16*)W, ldw, (const bf16*)bias, (bf16*)C, ldc, M, N, K,
+               epilogue, epilogue == EPI_RELU_DROP ? rowdrop::thresh(dropout_p) : 0u,
+               1.f / (1.f - dropout_p), seed, (uint32_t)site, (const bf16*)H, ldh};
     hipStream_t s = ov3d_stream(stream);
     return trans_b ? launch<1>(a, s) : launch<0>(a, s);
+}
+
+extern "C" int ov3d_rows_gemm(int M, int N, int K, const void* A, long long lda, const void* W,
+                              long long ldw, int trans_b, const void* bias, void* C, long long ldc,
+                              void* stream) {
+    return ov3d_rows_gemm_act(M, N, K, A, lda, W, ldw, trans_b, bias, EPI_NONE, 0.f, nullptr, 0,
+                              nullptr, 0, C, ldc, stream);
 }

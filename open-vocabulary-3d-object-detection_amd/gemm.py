@@ -70,6 +70,21 @@ def _linear(x, w, b):
     return torch.nn.functional.linear(x, w, b)
 
 
+def linear_weight_grads(dy, xc, w, b, need_w, need_b):
+    """(dW, db) of y = xc w^T + b for the gradient dy (bf16 rows like xc), or (None, None)
+    when they were queued for the grouped launch at the end of the backward (DEFER_WGRAD)"""
+    want_b = b is not None and need_b
+    if need_w and can_defer(xc, w, b if want_b else None):
+        defer_weight_grad(dy, xc, w, b if want_b else None)
+        return None, None
+    if need_w and _fused_ok(dy, xc):
+        dw, db = fused_weight_grad(dy, xc, bias=want_b)
+        return dw.to(w.dtype), (db.to(b.dtype) if want_b else None)
+    dw = weight_grad(dy, xc).to(w.dtype) if need_w else None
+    db = torch.sum(dy, dim=0, dtype=torch.float32).to(b.dtype) if want_b else None
+    return dw, db
+
+
 def _dgrad(dy, w):
     """dy (M, N) @ w (N, K) for the input gradient of a linear layer"""
     if _rows_gemm_ok(dy, w, False):

@@ -16,6 +16,7 @@ Dropout keep masks are the counter hash of csrc/rowdrop.h (seed of attention.py,
 site per call site), regenerated in the backward.  Under bf16 autocast only: the fp32
 path keeps the plain module code, which is what the parity tests compare against.
 """
+import os
 from collections import namedtuple
 
 import torch
@@ -23,6 +24,7 @@ from torch import nn
 
 from . import _native
 from . import attention as flash
+from . import gemm
 
 Pending = namedtuple("Pending", "src y p site")
 
@@ -52,6 +54,7 @@ class FanIn:
 
 enabled = True   # False: the plain module code under autocast as well (tests compare the two)
 fan_in = True    # False: every call returns its own pos / norm_b gradient (autograd sums them)
+fused_ffn = os.environ.get("OV3D_FUSED_FFN", "1") != "0"   # _FFN on short row blocks
 
 
 def supported(x, *norms):
@@ -257,6 +260,79 @@ class _ReluDropout(torch.autograd.Function):
         dy = torch.empty_like(h)
         _native.call("ov3d_relu_dropout_bwd", h, dh, h.numel(), ctx.p, dy, like=h)
         return dy.view(ctx.yshape), None, None
+
+
+class _FFN(torch.autograd.Function):
+    """linear2(dropout(relu(linear1(x)))) on short bf16 row blocks (the decoder's FFN,
+    models/transformer.py:375-377): the activation is the epilogue of linear1's rowsgemm
+    launch forward, and of linear2's input-gradient launch backward (ov3d_rows_gemm_act),
+    so the FFN is two launches each way (+ its weight gradients, deferred with the others)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, p, site):
+        bf = torch.bfloat16
+        C = x.shape[-1]
+        xc = x.reshape(-1, C)
+        w1c, b1c = gemm.cast_param(w1, bf), gemm.cast_param(b1, bf)
+        w2c, b2c = gemm.cast_param(w2, bf), gemm.cast_param(b2, bf)
+        M, F, N = xc.shape[0], w1c.shape[0], w2c.shape[0]
+        h = torch.empty((M, F), dtype=bf, device=x.device)
+        seed = flash._seed(x.device) if p > 0 else None
+        _native.call("ov3d_rows_gemm_act", M, F, C, xc, xc.stride(0), w1c, w1c.stride(0), 1,
+                     _bias(b1c), 1, float(p), seed, site, None, 0, h, F, like=xc)
+        y = gemm.rows_gemm(h, w2c, _bias(b2c), trans_b=True)
+        ctx.save_for_backward(xc, h, w1c, w2c)
+        ctx.params = (w1, b1, w2, b2)
+        ctx.meta = (float(p), x.shape, x.dtype)
+        return y.view(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, h, w1c, w2c = ctx.saved_tensors
+        w1, b1, w2, b2 = ctx.params
+        p, xshape, xdt = ctx.meta
+        need = ctx.needs_input_grad
+        M, F, N = h.shape[0], h.shape[1], w2c.shape[0]
+        dy = dy.reshape(-1, N).to(torch.bfloat16).contiguous()
+        dy1 = torch.empty((M, F), dtype=torch.bfloat16, device=dy.device)
+        _native.call("ov3d_rows_gemm_act", M, F, N, dy, N, w2c, w2c.stride(0), 0, None, 2, float(p),
+                     None, 0, h, F, dy1, F, like=dy)
+        dw2, db2 = gemm.linear_weight_grads(dy, h, w2, b2, need[3], need[4])
+        dw1, db1 = gemm.linear_weight_grads(dy1, xc, w1, b1, need[1], need[2])
+        dx = gemm.rows_gemm(dy1, w1c, trans_b=False).to(xdt).view(xshape) if need[0] else None
+        return dx, dw1, db1, dw2, db2, None, None
+
+
+def _bias(b):
+    return b.contiguous() if b is not None else None
+
+
+def _ffn_ok(x, linear1, linear2, activation):
+    if not (fused_ffn and isinstance(activation, nn.ReLU) and x.is_cuda and x.dtype == torch.bfloat16
+            and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16 and x.stride(-1) == 1):
+        return False
+    xr = x.reshape(-1, x.shape[-1])
+    bf = torch.bfloat16
+    w1c, w2c = gemm.cast_param(linear1.weight, bf), gemm.cast_param(linear2.weight, bf)
+    if not (gemm._rows_gemm_ok(xr, w1c, True) and w2c.stride(1) == 1 and w2c.stride(0) % 8 == 0
+            and w2c.data_ptr() % 16 == 0 and w2c.shape[1] == w1c.shape[0]):
+        return False
+    # the launches on the fresh (contiguous) h / dy / dy1 rows: linear2, its input gradient
+    # (output F columns over N), linear1's input gradient (C columns over F)
+    M, C, F, N = xr.shape[0], xr.shape[1], w1c.shape[0], w2c.shape[0]
+    ok = _native.load().ov3d_rows_gemm_supported
+    return bool(ok(M, N, F) and ok(M, F, N) and ok(M, C, F))
+
+
+def ffn(x, linear1, linear2, activation, dropout, site):
+    """linear2(dropout(activation(linear1(x)))) of a transformer layer (bf16 rows)."""
+    if _ffn_ok(x, linear1, linear2, activation):
+        p = dropout.p if dropout.training else 0.0
+        with torch.autocast("cuda", enabled=False):
+            return _FFN.apply(x, linear1.weight, linear1.bias, linear2.weight, linear2.bias, p, site)
+    h = ffn_act(gemm.rows_linear(x, linear1.weight, linear1.bias), activation, dropout, site)
+    return gemm.rows_linear(h, linear2.weight, linear2.bias)
 
 
 def ffn_act(y, activation, dropout, site):

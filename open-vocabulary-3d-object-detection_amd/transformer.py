@@ -212,9 +212,8 @@ class TransformerEncoderLayer(nn.Module):
         if not self.use_ffn:
             return rn.Pending(s, y, p1, site1)
         s, x, _, _ = rn.resnorm(rn.Pending(s, y, p1, site1), self.norm2)
-        h = rn.ffn_act(rows_linear(x, self.linear1.weight, self.linear1.bias), self.activation,
-                       self.dropout, site_ffn)
-        return rn.Pending(s, rows_linear(h, self.linear2.weight, self.linear2.bias), p2, site2)
+        y = rn.ffn(x, self.linear1, self.linear2, self.activation, self.dropout, site_ffn)
+        return rn.Pending(s, y, p2, site2)
 
     def fused_ok(self, x):
         return rn.supported(x, self.norm1, self.norm2 if self.use_ffn else None)
@@ -276,9 +275,8 @@ class TransformerDecoderLayer(nn.Module):
         else:
             y = self.multihead_attn(qx, memory_pos, memory, attn_mask=memory_mask)
         s, x3, _, _ = rn.resnorm(rn.Pending(s, y, p2, site2), self.norm3)
-        h = rn.ffn_act(rows_linear(x3, self.linear1.weight, self.linear1.bias), self.activation,
-                       self.dropout, site_ffn)
-        return rn.Pending(s, rows_linear(h, self.linear2.weight, self.linear2.bias), p3, site3)
+        y = rn.ffn(x3, self.linear1, self.linear2, self.activation, self.dropout, site_ffn)
+        return rn.Pending(s, y, p3, site3)
 
     def fused_ok(self, x):
         return rn.supported(x, self.norm1, self.norm2, self.norm3)

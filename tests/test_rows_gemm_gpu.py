@@ -70,3 +70,33 @@ def test_rows_linear_uses_rows_gemm_and_matches_library(cuda):
     assert res[True][4] == 2 and res[False][4] == 0     # forward + input gradient
     for a, b in zip(res[True][:4], res[False][:4]):
         assert ((a - b).norm() / b.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_fused_ffn_equals_unfused_bitwise(cuda, p, monkeypatch):
+    """resnorm.ffn (ReLU + dropout in the epilogues of linear1 forward and of linear2's input
+    gradient, ov3d_rows_gemm_act) gives the unfused linear -> ov3d_relu_dropout -> linear
+    chain's output and every gradient bit for bit"""
+    from ov3d_amd import attention as flash
+    from ov3d_amd import resnorm as rn
+    torch.manual_seed(2)
+    l1 = torch.nn.Linear(256, 256).to(cuda)
+    l2 = torch.nn.Linear(256, 256).to(cuda)
+    drop = torch.nn.Dropout(p).train()
+    act = torch.nn.ReLU()
+    flash.next_step(cuda)
+    x0 = torch.randn(1024, 256, device=cuda).to(torch.bfloat16)
+    g = torch.randn(1024, 256, device=cuda)
+    res = {}
+    for fused in (True, False):
+        if not fused:
+            monkeypatch.setattr(rn, "_ffn_ok", lambda *a: False)
+        for m in (l1, l2):
+            m.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = rn.ffn(x, l1, l2, act, drop, site=77)
+        (y.float() * g).sum().backward()
+        res[fused] = [y, x.grad, l1.weight.grad, l1.bias.grad, l2.weight.grad, l2.bias.grad]
+    for i, (a, b) in enumerate(zip(res[True], res[False])):
+        assert torch.equal(a, b), (i, (a.float() - b.float()).abs().max().item())
