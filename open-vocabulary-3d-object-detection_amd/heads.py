@@ -24,6 +24,7 @@ import torch.nn as nn
 
 from . import _native as nat
 from . import attention as flash
+from . import gemm
 from .gemm import fused_weight_grad
 from .sa_fused import _bwd_coefs, _finalize, _sync_group
 
@@ -203,8 +204,23 @@ class _Heads(torch.autograd.Function):
         seed = flash._seed(dev)
         gv = gv.to(bf).contiguous()
         gs = gs.to(bf).contiguous()
-        dw3v, db3v = fused_weight_grad(gv, z2[:, :H], bias=True)
-        dw3s, db3s = fused_weight_grad(gs, z2[:, H:], bias=True)
+        # weight gradients: queued for the grouped launch at the end of the backward
+        # (gemm.DEFER_WGRAD) as one problem per head parameter, else computed here
+        P = pack.parts
+        defer = gemm.DEFER_WGRAD and all(
+            gemm.can_defer(xb, m.weight, m.bias) for p in P for m in (p[0], p[3], p[6]))
+        if defer:
+            gemm.defer_weight_grad(gv, z2[:, :H], P[0][6].weight, P[0][6].bias)
+            o = 0
+            for i, p in enumerate(P[1:], start=1):
+                n = p[6].weight.shape[0]
+                gemm.defer_weight_grad(gs[:, o:o + n], z2[:, i * H:(i + 1) * H], p[6].weight,
+                                       p[6].bias)
+                o += n
+            dw3v = db3v = dw3s = db3s = None
+        else:
+            dw3v, db3v = fused_weight_grad(gv, z2[:, :H], bias=True)
+            dw3s, db3s = fused_weight_grad(gs, z2[:, H:], bias=True)
         dz2 = torch.empty((R, H5), dtype=bf, device=dev)
         torch.mm(gv, w3vb, out=dz2[:, :H])
         torch.mm(gs, w3sb, out=dz2[:, H:])
@@ -214,24 +230,37 @@ class _Heads(torch.autograd.Function):
         dh2 = torch.empty((5, R, H), dtype=bf, device=dev)
         dg2, dbe2 = _bn_backward(dz2, rowmajor, h2, headmajor, R, H5, st["g2"], m2, i2, a2, s2, p2,
                                  seed, pack.sites[1], dh2, headmajor, bn=pack.bns()[1][0])
-        dw2 = torch.empty((5, H, H), dtype=torch.float32, device=dev)
-        for i in range(5):
-            fused_weight_grad(dh2[i], z1[:, i * H:(i + 1) * H], bias=False, out_w=dw2[i])
+        if defer:
+            for i in range(5):
+                gemm.defer_weight_grad(dh2[i], z1[:, i * H:(i + 1) * H], P[i][3].weight)
+        else:
+            dw2 = torch.empty((5, H, H), dtype=torch.float32, device=dev)
+            for i in range(5):
+                fused_weight_grad(dh2[i], z1[:, i * H:(i + 1) * H], bias=False, out_w=dw2[i])
         dz1 = torch.bmm(dh2, w2)                                                 # (5, R, H)
         dh1 = torch.empty((R, H5), dtype=bf, device=dev)
         dg1, dbe1 = _bn_backward(dz1, headmajor, h1, rowmajor, R, H5, st["g1"], m1, i1, a1, s1, p1,
                                  seed, pack.sites[0], dh1, rowmajor, bn=pack.bns()[0][0])
-        dw1, _ = fused_weight_grad(dh1, xb, bias=False)
+        if defer:
+            for i in range(5):
+                gemm.defer_weight_grad(dh1[:, i * H:(i + 1) * H], xb, P[i][0].weight)
+        else:
+            dw1, _ = fused_weight_grad(dh1, xb, bias=False)
         dx = (dh1 @ w1).to(xdt)
-        grads = {"w1": dw1.view(-1), "w2": dw2.view(-1), "g1": dg1, "b1": dbe1, "g2": dg2,
-                 "b2": dbe2}
+        grads = {"g1": dg1, "b1": dbe1, "g2": dg2, "b2": dbe2}
+        if not defer:
+            grads.update({"w1": dw1.view(-1), "w2": dw2.view(-1)})
         out = []
         for key in ("w1", "w2", "g1", "b1", "g2", "b2"):
+            if key not in grads:
+                out += [None] * 5
+                continue
             g = grads[key]
             step = g.numel() // 5
             shape = pack._tensors()[key][0].shape
             out += [g[i * step:(i + 1) * step].view(shape) for i in range(5)]
-        return (dx, None, None, None, dw3v, db3v, dw3s.view(w3s_shape), db3s, *out)
+        return (dx, None, None, None, dw3v, db3v,
+                dw3s.view(w3s_shape) if dw3s is not None else None, db3s, *out)
 
 
 def _bn_backward(dz, lz, x, lx, R, C, gamma, mean, invstd, scale, shift, p, seed, site, dx, ld,
