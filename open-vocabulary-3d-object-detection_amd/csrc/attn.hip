@@ -97,6 +97,11 @@ __device__ __forceinline__ bool drop_keep(uint32_t qbase, uint32_t k, uint32_t t
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// value of lane ^ 1 (DPP quad_perm [1,0,3,2]: one VALU move, no LDS crossbar)
+__device__ __forceinline__ uint32_t lane_xor1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);
+}
+
 // online-softmax rescale only when a query's running max grows by more than this
 // (log2 units): P stays <= 2^8 between rescales (cdna_hip_programming.md T13)
 constexpr float RESCALE_THR = 8.f;
@@ -597,13 +602,27 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
                     const float4 l4 = *reinterpret_cast<const float4*>(&Ls[buf][qrow]);
                     const float4 d4 = *reinterpret_cast<const float4*>(&Dv[buf][qrow]);
                     const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+                    // keys k0+r and k0+(r^1) share one pair hash per query: this lane hashes
+                    // rows j = (r&1), (r&1)+2 and takes the other two from its neighbour
+                    uint32_t hsh[4] = {0u, 0u, 0u, 0u};
+                    if (drop) {
+                        const int j0 = r & 1;
+                        const uint32_t kp2 = (uint32_t)(k0 + r) >> 1;
+                        const uint32_t ha = drop_pair(Zb[buf][qrow + j0], kp2);
+                        const uint32_t hb = drop_pair(Zb[buf][qrow + j0 + 2], kp2);
+                        const uint32_t oa = lane_xor1(ha), ob = lane_xor1(hb);
+                        hsh[0] = j0 ? oa : ha;
+                        hsh[1] = j0 ? ha : oa;
+                        hsh[2] = j0 ? ob : hb;
+                        hsh[3] = j0 ? hb : ob;
+                    }
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int i = 4 * g + j;
                         float p = kvalid ? fast_exp2(fmaf(st[i], a.scale2, -lv[j])) : 0.f;
                         float pd = p, dp = dpt[i];
                         if (drop) {
-                            const bool kp = drop_keep(Zb[buf][qrow + j], (uint32_t)(k0 + r), a.thresh);
+                            const bool kp = ((r & 1) ? (hsh[j] >> 16) : (hsh[j] & 0xffffu)) >= a.thresh;
                             pd = kp ? p * a.keep_scale : 0.f;
                             dp = kp ? dp * a.keep_scale : 0.f;
                         }
