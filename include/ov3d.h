@@ -152,6 +152,18 @@ int ov3d_bn_finalize(const double* totals, double count, int C, const float* gam
                      const float* beta, float eps, float momentum, float* running_mean,
                      float* running_var, float* mean_out, float* invstd_out, float* scale_out,
                      float* shift_out, long long* num_batches_tracked, void* stream);
+/* ov3d_reduce_partials(2C) + ov3d_bn_finalize in one launch (single-replica BatchNorm):
+ * partials (nparts, 2C) of (sum, sum of squares); bit-identical to the two launches */
+int ov3d_bn_stats_finalize(const double* partials, int nparts, int C, double count,
+                           const float* gamma, const float* beta, float eps, float momentum,
+                           float* running_mean, float* running_var, float* mean_out,
+                           float* invstd_out, float* scale_out, float* shift_out,
+                           long long* num_batches_tracked, void* stream);
+/* ov3d_reduce_partials(2C) + ov3d_bn_bwd_finalize in one launch (single replica) */
+int ov3d_bn_bwd_stats_finalize(const double* partials, int nparts, int C, double count,
+                               const float* gamma, const float* mean, const float* invstd,
+                               float* cA, float* cB, float* cC, float* dgamma, float* dbeta,
+                               void* stream);
 /* pooled output (P,N) f32 = relu(scale*(scale >= 0 ? pmax : pmin) + shift), plus the
  * selected value / row for the backward */
 int ov3d_sa_pool_fwd(const float* pmax, const float* pmin, const uint8_t* imax,

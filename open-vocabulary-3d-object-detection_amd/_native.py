@@ -67,6 +67,8 @@ _SIGS = {
     "ov3d_resnorm_fwd": "lipipifpipppippfppppppp",
     "ov3d_resnorm_bwd": "lippppppplllppfpippipipippppip",
     "ov3d_rows_gemm": "iiiplplipplp",
+    "ov3d_bn_stats_finalize": "piidppffpppppppp",
+    "ov3d_bn_bwd_stats_finalize": "piidppppppppp",
     "ov3d_rows_gemm_act": "iiiplplipifpiplplp",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",

@@ -271,12 +271,11 @@ __global__ __launch_bounds__(kThreads) void sa_l1_kernel(const float* __restrict
 }
 
 // (nparts, width) fp64 partials -> (width) totals, fixed summation order (deterministic).
-__global__ __launch_bounds__(1024) void reduce_partials_kernel(const double* __restrict__ partials,
-                                                               int nparts, int width,
-                                                               double* __restrict__ totals) {
-    // 32 columns x 32 partial lanes per block, 8 loads in flight per thread (fixed order)
-    __shared__ double red[32][33];
-    const int c = blockIdx.x * 32 + (threadIdx.x & 31), pl = threadIdx.x >> 5;
+// Sum over the nparts rows of column c of (nparts, width) fp64 partials, by a 1024-thread
+// block of 32 columns x 32 partial lanes (pl), 8 loads in flight per thread, fixed order.
+// The result is valid in the pl == 0 lanes.
+__device__ __forceinline__ double column_total(const double* __restrict__ partials, int nparts,
+                                               int width, int c, int pl, double (*red)[33]) {
     double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (c < width) {
         int w = pl;
@@ -285,13 +284,48 @@ __global__ __launch_bounds__(1024) void reduce_partials_kernel(const double* __r
             for (int u = 0; u < 8; ++u) s[u] += partials[(size_t)(w + u * 32) * width + c];
         for (; w < nparts; w += 32) s[0] += partials[(size_t)w * width + c];
     }
+    __syncthreads();   // red may still be read by a previous round
     red[pl][threadIdx.x & 31] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
     __syncthreads();
-    if (pl == 0 && c < width) {
-        double t = 0;
+    double t = 0;
+    if (pl == 0) {
 #pragma unroll
         for (int k = 0; k < 32; ++k) t += red[k][threadIdx.x];
-        totals[c] = t;
+    }
+    return t;
+}
+
+__global__ __launch_bounds__(1024) void reduce_partials_kernel(const double* __restrict__ partials,
+                                                               int nparts, int width,
+                                                               double* __restrict__ totals) {
+    __shared__ double red[32][33];
+    const int c = blockIdx.x * 32 + (threadIdx.x & 31), pl = threadIdx.x >> 5;
+    const double t = column_total(partials, nparts, width, c, pl, red);
+    if (pl == 0 && c < width) totals[c] = t;
+}
+
+// sum / sum of squares of channel c over `count` rows -> mean, invstd, scale, shift (and the
+// running statistics)
+__device__ __forceinline__ void bn_finalize_one(int c, double tsum, double tsq, double count,
+                                                const float* gamma, const float* beta, float eps,
+                                                float momentum, float* running_mean,
+                                                float* running_var, float* mean_out,
+                                                float* invstd_out, float* scale_out,
+                                                float* shift_out) {
+    const double mean = tsum / count;
+    double var = tsq / count - mean * mean;
+    var = var < 0 ? 0 : var;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+    mean_out[c] = (float)mean;
+    invstd_out[c] = invstd;
+    const float a = g * invstd;
+    scale_out[c] = a;
+    shift_out[c] = b - (float)mean * a;
+    if (running_mean) {
+        const double unb = count > 1 ? var * count / (count - 1) : var;
+        running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+        running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
     }
 }
 
@@ -307,22 +341,10 @@ __global__ void bn_finalize_kernel(const double* __restrict__ totals, double cou
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c == 0 && num_batches_tracked) *num_batches_tracked += 1;
     if (c >= C) return;
-    const double mean = totals[c] / count;
-    double var = totals[C + c] / count - mean * mean;
-    var = var < 0 ? 0 : var;
-    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
-    mean_out[c] = (float)mean;
-    invstd_out[c] = invstd;
-    const float a = g * invstd;
-    scale_out[c] = a;
-    shift_out[c] = b - (float)mean * a;
-    if (running_mean) {
-        const double unb = count > 1 ? var * count / (count - 1) : var;
-        running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
-        running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
-    }
+    bn_finalize_one(c, totals[c], totals[C + c], count, gamma, beta, eps, momentum, running_mean,
+                    running_var, mean_out, invstd_out, scale_out, shift_out);
 }
+
 
 // Pool: out = relu(a * (a >= 0 ? max : min) + b); remembers the value and row used.
 __global__ void sa_pool_fwd_kernel(const float* __restrict__ pmax, const float* __restrict__ pmin,
@@ -377,6 +399,20 @@ __global__ __launch_bounds__(kThreads) void sa_pool_bwd_kernel(
 // BN backward coefficients from totals (sum g, sum g*xhat) over `count` rows:
 //   dx = gamma*invstd * (g - mean(g) - xhat * mean(g*xhat))  ==  cA*g + cB*y + cC
 // (PyTorch batch_norm_backward, training), plus dgamma / dbeta.
+__device__ __forceinline__ void bn_bwd_finalize_one(int c, double t1, double t2, double count,
+                                                    const float* gamma, const float* mean,
+                                                    const float* invstd, float* cA, float* cB,
+                                                    float* cC, float* dgamma, float* dbeta) {
+    const double m1 = t1 / count, m2 = t2 / count;
+    const double is = invstd[c], g = gamma ? gamma[c] : 1.0, mu = mean[c];
+    const double a = g * is;
+    cA[c] = (float)a;
+    cB[c] = (float)(-a * is * m2);
+    cC[c] = (float)(-a * m1 + a * is * m2 * mu);
+    if (dgamma) dgamma[c] = (float)t2;
+    if (dbeta) dbeta[c] = (float)t1;
+}
+
 __global__ void bn_bwd_finalize_kernel(const double* __restrict__ totals, double count, int C,
                                        const float* __restrict__ gamma, const float* __restrict__ mean,
                                        const float* __restrict__ invstd, float* __restrict__ cA,
@@ -384,14 +420,38 @@ __global__ void bn_bwd_finalize_kernel(const double* __restrict__ totals, double
                                        float* __restrict__ dgamma, float* __restrict__ dbeta) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
-    const double m1 = totals[c] / count, m2 = totals[C + c] / count;
-    const double is = invstd[c], g = gamma ? gamma[c] : 1.0, mu = mean[c];
-    const double a = g * is;
-    cA[c] = (float)a;
-    cB[c] = (float)(-a * is * m2);
-    cC[c] = (float)(-a * m1 + a * is * m2 * mu);
-    if (dgamma) dgamma[c] = (float)totals[C + c];
-    if (dbeta) dbeta[c] = (float)totals[c];
+    bn_bwd_finalize_one(c, totals[c], totals[C + c], count, gamma, mean, invstd, cA, cB, cC, dgamma,
+                        dbeta);
+}
+
+// Both reductions in one launch: column totals of the (nparts, 2C) partials for 32 channels
+// per block (the reduce_partials_kernel order, so the totals are bit-identical), then the
+// finalize of those channels.  Single-replica BatchNorm (no all-reduce in between).
+__global__ __launch_bounds__(1024) void bn_stats_finalize_kernel(
+    const double* __restrict__ partials, int nparts, int C, double count, const float* gamma,
+    const float* beta, float eps, float momentum, float* running_mean, float* running_var,
+    float* mean_out, float* invstd_out, float* scale_out, float* shift_out,
+    long long* num_batches_tracked) {
+    __shared__ double red[32][33];
+    const int c = blockIdx.x * 32 + (threadIdx.x & 31), pl = threadIdx.x >> 5;
+    const double tsum = column_total(partials, nparts, 2 * C, c, pl, red);
+    const double tsq = column_total(partials, nparts, 2 * C, C + c, pl, red);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && num_batches_tracked) *num_batches_tracked += 1;
+    if (pl == 0 && c < C)
+        bn_finalize_one(c, tsum, tsq, count, gamma, beta, eps, momentum, running_mean, running_var,
+                        mean_out, invstd_out, scale_out, shift_out);
+}
+
+__global__ __launch_bounds__(1024) void bn_bwd_stats_finalize_kernel(
+    const double* __restrict__ partials, int nparts, int C, double count, const float* gamma,
+    const float* mean, const float* invstd, float* cA, float* cB, float* cC, float* dgamma,
+    float* dbeta) {
+    __shared__ double red[32][33];
+    const int c = blockIdx.x * 32 + (threadIdx.x & 31), pl = threadIdx.x >> 5;
+    const double t1 = column_total(partials, nparts, 2 * C, c, pl, red);
+    const double t2 = column_total(partials, nparts, 2 * C, C + c, pl, red);
+    if (pl == 0 && c < C)
+        bn_bwd_finalize_one(c, t1, t2, count, gamma, mean, invstd, cA, cB, cC, dgamma, dbeta);
 }
 
 // ReLU + BN backward over rows, C = 8 * (threads per row):
@@ -601,6 +661,36 @@ extern "C" int ov3d_bn_finalize(const double* totals, double count, int C, const
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(ov3d_cdiv(C, 256)), dim3(256), 0, ov3d_stream(stream),
                        totals, count, C, gamma, beta, eps, momentum, running_mean, running_var,
                        mean_out, invstd_out, scale_out, shift_out, num_batches_tracked);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_bn_stats_finalize(const double* partials, int nparts, int C, double count,
+                                      const float* gamma, const float* beta, float eps,
+                                      float momentum, float* running_mean, float* running_var,
+                                      float* mean_out, float* invstd_out, float* scale_out,
+                                      float* shift_out, long long* num_batches_tracked,
+                                      void* stream) {
+    if (C <= 0 || nparts <= 0 || count <= 0 || !partials || !mean_out || !invstd_out ||
+        !scale_out || !shift_out)
+        return OV3D_EINVAL;
+    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(ov3d_cdiv(C, 32)), dim3(1024), 0,
+                       ov3d_stream(stream), partials, nparts, C, count, gamma, beta, eps, momentum,
+                       running_mean, running_var, mean_out, invstd_out, scale_out, shift_out,
+                       num_batches_tracked);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_bn_bwd_stats_finalize(const double* partials, int nparts, int C, double count,
+                                          const float* gamma, const float* mean,
+                                          const float* invstd, float* cA, float* cB, float* cC,
+                                          float* dgamma, float* dbeta, void* stream) {
+    if (C <= 0 || nparts <= 0 || count <= 0 || !partials || !mean || !invstd || !cA || !cB || !cC)
+        return OV3D_EINVAL;
+    hipLaunchKernelGGL(bn_bwd_stats_finalize_kernel, dim3(ov3d_cdiv(C, 32)), dim3(1024), 0,
+                       ov3d_stream(stream), partials, nparts, C, count, gamma, mean, invstd, cA, cB,
+                       cC, dgamma, dbeta);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

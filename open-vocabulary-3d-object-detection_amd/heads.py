@@ -26,7 +26,7 @@ from . import _native as nat
 from . import attention as flash
 from . import gemm
 from .gemm import fused_weight_grad
-from .sa_fused import _bwd_coefs, _finalize, _sync_group
+from .sa_fused import _sync_group, bn_affine, bn_bwd_affine
 
 # BatchNorm1d, or its SyncBatchNorm conversion (DDP, main.py:427-431): the statistics
 # totals are then all-reduced over the BN's process group (exact SyncBN semantics)
@@ -142,16 +142,10 @@ def _stats_finalize(x, layout, R, C, gamma, beta, bns, rm, rv, nbt=None):
     parts = torch.empty((NPARTS, 2, C), dtype=torch.float64, device=dev)
     nat.call("ov3d_rows_bn_stats", x, int(x.dtype == torch.bfloat16), *layout, R, C, parts, NPARTS,
              like=x)
-    tot = torch.empty(2 * C, dtype=torch.float64, device=dev)
-    nat.call("ov3d_reduce_partials", parts, NPARTS, 2 * C, tot, like=x)
     bn0 = bns[0]
     group, world = _group_world(bn0)
-    if group is not None:
-        torch.distributed.all_reduce(tot, group=group)
-    mean, invstd, scale, shift = (torch.empty(C, dtype=torch.float32, device=dev) for _ in range(4))
-    nat.call("ov3d_bn_finalize", tot, float(R * world), C, gamma, beta, float(bn0.eps),
-             float(bn0.momentum), rm, rv, mean, invstd, scale, shift, nbt, like=x)
-    return mean, invstd, scale, shift
+    return bn_affine(parts, NPARTS, C, group, R * world, gamma, beta, bn0.eps, bn0.momentum, rm, rv,
+                     nbt)
 
 
 class _Heads(torch.autograd.Function):
@@ -269,12 +263,8 @@ def _bn_backward(dz, lz, x, lx, R, C, gamma, mean, invstd, scale, shift, p, seed
     parts = torch.empty((NPARTS, 2, C), dtype=torch.float64, device=dev)
     nat.call("ov3d_rows_bn_bwd", 0, dz, *lz, x, 1, *lx, R, C, scale, shift, mean, invstd, None, None,
              None, float(p), seed, site, parts, NPARTS, None, 0, 0, 8, like=x)
-    tot = torch.empty(2 * C, dtype=torch.float64, device=dev)
-    nat.call("ov3d_reduce_partials", parts, NPARTS, 2 * C, tot, like=x)
     group, world = _group_world(bn) if bn is not None else (None, 1)
-    if group is not None:
-        torch.distributed.all_reduce(tot, group=group)
-    cA, cB, cC, dg, db = _bwd_coefs(tot, R * world, gamma, mean, invstd, C)
+    cA, cB, cC, dg, db = bn_bwd_affine(parts, NPARTS, C, group, R * world, gamma, mean, invstd)
     nat.call("ov3d_rows_bn_bwd", 1, dz, *lz, x, 1, *lx, R, C, scale, shift, mean, invstd, cA, cB, cC,
              float(p), seed, site, None, 0, dx, *ld, like=x)
     return dg, db
@@ -345,12 +335,8 @@ class _BnReluRows(torch.autograd.Function):
         nat.call("ov3d_rows_bn_bwd", 0, dz, *rowmajor, h, hf, *rowmajor, R, C, scale, shift, mean,
                  invstd, None, None, None, float(p), seed, site, parts, NPARTS, None, 0, 0, 8,
                  like=h)
-        tot = torch.empty(2 * C, dtype=torch.float64, device=dev)
-        nat.call("ov3d_reduce_partials", parts, NPARTS, 2 * C, tot, like=h)
         group, world = _group_world(ctx.bn)
-        if group is not None:
-            torch.distributed.all_reduce(tot, group=group)
-        cA, cB, cC, dg, db = _bwd_coefs(tot, R * world, gamma, mean, invstd, C)
+        cA, cB, cC, dg, db = bn_bwd_affine(parts, NPARTS, C, group, R * world, gamma, mean, invstd)
         dh = torch.empty((R, C), dtype=torch.bfloat16, device=dev)
         nat.call("ov3d_rows_bn_bwd", 1, dz, *rowmajor, h, hf, *rowmajor, R, C, scale, shift, mean,
                  invstd, cA, cB, cC, float(p), seed, site, None, 0, dh, *rowmajor, like=h)

@@ -97,6 +97,41 @@ def _finalize(tot, count, bn, C):
     return mean, invstd, scale, shift
 
 
+def bn_affine(parts, nparts, C, group, count, gamma, beta, eps, momentum, rm, rv, nbt):
+    """(nparts, 2C) partial (sum, sum of squares) -> mean, invstd, scale, shift (+ running
+    statistics, num_batches_tracked): one launch for a single replica, else the totals are
+    all-reduced over the SyncBatchNorm group between the reduction and the finalize."""
+    dev = parts.device
+    mean, invstd, scale, shift = (torch.empty(C, dtype=torch.float32, device=dev) for _ in range(4))
+    if group is None:
+        nat.call("ov3d_bn_stats_finalize", parts, nparts, C, float(count), gamma, beta, float(eps),
+                 float(momentum), rm, rv, mean, invstd, scale, shift, nbt, like=parts)
+    else:
+        tot = _totals(parts, nparts, 2 * C, group)
+        nat.call("ov3d_bn_finalize", tot, float(count), C, gamma, beta, float(eps),
+                 float(momentum), rm, rv, mean, invstd, scale, shift, nbt, like=tot)
+    return mean, invstd, scale, shift
+
+
+def bn_bwd_affine(parts, nparts, C, group, count, gamma, mean, invstd):
+    """(nparts, 2C) partial (sum dt, sum dt*xhat) -> cA, cB, cC, dgamma, dbeta (one launch
+    for a single replica)"""
+    if group is not None:
+        return _bwd_coefs(_totals(parts, nparts, 2 * C, group), count, gamma, mean, invstd, C)
+    dev = parts.device
+    cA, cB, cC, dg, db = (torch.empty(C, dtype=torch.float32, device=dev) for _ in range(5))
+    nat.call("ov3d_bn_bwd_stats_finalize", parts, nparts, C, float(count), gamma, mean, invstd,
+             cA, cB, cC, dg, db, like=parts)
+    return cA, cB, cC, dg, db
+
+
+def _bn_stats(parts, nparts, C, group, count, bn):
+    nbt = bn.num_batches_tracked if (bn.track_running_stats and
+                                     bn.num_batches_tracked is not None) else None
+    return bn_affine(parts, nparts, C, group, count, bn.weight, bn.bias, bn.eps, bn.momentum,
+                     bn.running_mean, bn.running_var, nbt)
+
+
 def _bwd_coefs(tot, count, gamma, mean, invstd, C):
     dev = tot.device
     cA, cB, cC, dg, db = (torch.empty(C, dtype=torch.float32, device=dev) for _ in range(5))
@@ -120,7 +155,7 @@ class _SAMLPPool(Function):
         y1 = torch.empty((R, c1), dtype=bf, device=dev)
         parts = torch.empty((NPARTS_ROWS, 2, c1), dtype=torch.float64, device=dev)
         nat.call("ov3d_sa_l1_fwd", x0, w1.float().contiguous(), R, c1, y1, parts, NPARTS_ROWS, like=x0)
-        st1 = _finalize(_totals(parts, NPARTS_ROWS, 2 * c1, groups[0]), R * world[0], bns[0], c1)
+        st1 = _bn_stats(parts, NPARTS_ROWS, c1, groups[0], R * world[0], bns[0])
         # layer 2
         w2b = cast_param(w2, bf).contiguous()
         z1 = torch.empty((R, c1), dtype=bf, device=dev)
@@ -128,7 +163,7 @@ class _SAMLPPool(Function):
         parts = torch.empty((NPARTS_LAYER, 2, c2), dtype=torch.float64, device=dev)
         nat.call("ov3d_sa_layer_fwd", y1, st1[2], st1[3], w2b, R, c1, c2, z1, y2, parts, NPARTS_LAYER,
                  like=x0)
-        st2 = _finalize(_totals(parts, NPARTS_LAYER, 2 * c2, groups[1]), R * world[1], bns[1], c2)
+        st2 = _bn_stats(parts, NPARTS_LAYER, c2, groups[1], R * world[1], bns[1])
         # layer 3 + pool
         w3b = cast_param(w3, bf).contiguous()
         z2 = torch.empty((R, c2), dtype=bf, device=dev)
@@ -137,7 +172,7 @@ class _SAMLPPool(Function):
         parts = torch.empty((NPARTS_LAYER, 2, c3), dtype=torch.float64, device=dev)
         nat.call("ov3d_sa_layer_pool_fwd", y2, st2[2], st2[3], w3b, R, c2, c3, S, z2, pmax, pmin,
                  imax, imin, parts, NPARTS_LAYER, like=x0)
-        st3 = _finalize(_totals(parts, NPARTS_LAYER, 2 * c3, groups[2]), R * world[2], bns[2], c3)
+        st3 = _bn_stats(parts, NPARTS_LAYER, c3, groups[2], R * world[2], bns[2])
         out = torch.empty((P, c3), dtype=torch.float32, device=dev)
         ysel = torch.empty((P, c3), dtype=torch.float32, device=dev)
         isel = torch.empty((P, c3), dtype=torch.uint8, device=dev)
@@ -160,8 +195,8 @@ class _SAMLPPool(Function):
         parts = torch.empty((NPARTS_POOL, 2, c3), dtype=torch.float64, device=dev)
         nat.call("ov3d_sa_pool_bwd", dout, ysel, a3, s3, m3, i3, P, c3, gsel, parts, NPARTS_POOL,
                  like=dout)
-        cA, cB, cC, dg3, db3 = _bwd_coefs(_totals(parts, NPARTS_POOL, 2 * c3, groups[2]),
-                                          R * world[2], g3, m3, i3, c3)
+        cA, cB, cC, dg3, db3 = bn_bwd_affine(parts, NPARTS_POOL, c3, groups[2], R * world[2], g3,
+                                             m3, i3)
         dy3 = torch.empty((R, c3), dtype=bf, device=dev)
         nat.call("ov3d_sa_layer_dy", y2, a2, s2, w3b, R, c2, c3, S, gsel, isel, cA, cB, cC, dy3,
                  NPARTS_LAYER, like=dout)
@@ -172,8 +207,8 @@ class _SAMLPPool(Function):
         parts = torch.empty((NPARTS_ROWS, 2, c2), dtype=torch.float64, device=dev)
         nat.call("ov3d_bn_relu_bwd", 0, dz2, y2, a2, s2, m2, i2, None, None, None, None, R, c2, parts,
                  None, NPARTS_ROWS, like=dout)
-        cA, cB, cC, dg2, db2 = _bwd_coefs(_totals(parts, NPARTS_ROWS, 2 * c2, groups[1]),
-                                          R * world[1], g2, m2, i2, c2)
+        cA, cB, cC, dg2, db2 = bn_bwd_affine(parts, NPARTS_ROWS, c2, groups[1], R * world[1], g2,
+                                             m2, i2)
         dy2 = torch.empty((R, c2), dtype=bf, device=dev)
         nat.call("ov3d_bn_relu_bwd", 1, dz2, y2, a2, s2, None, None, cA, cB, cC, None, R, c2, None,
                  dy2, NPARTS_ROWS, like=dout)
@@ -185,8 +220,8 @@ class _SAMLPPool(Function):
         parts = torch.empty((NPARTS_ROWS, 2, c1), dtype=torch.float64, device=dev)
         nat.call("ov3d_bn_relu_bwd", 0, dz1, y1, a1, s1, m1, i1, None, None, None, None, R, c1, parts,
                  None, NPARTS_ROWS, like=dout)
-        cA, cB, cC, dg1, db1 = _bwd_coefs(_totals(parts, NPARTS_ROWS, 2 * c1, groups[0]),
-                                          R * world[0], g1, m1, i1, c1)
+        cA, cB, cC, dg1, db1 = bn_bwd_affine(parts, NPARTS_ROWS, c1, groups[0], R * world[0], g1,
+                                             m1, i1)
         parts = torch.empty((NPARTS_ROWS, c1, 3), dtype=torch.float64, device=dev)
         nat.call("ov3d_bn_relu_bwd", 2, dz1, y1, a1, s1, None, None, cA, cB, cC, x0, R, c1, parts,
                  None, NPARTS_ROWS, like=dout)

@@ -200,3 +200,37 @@ def test_fourier_pe_kernel_matches_torch(cuda):
     out = pe.to(cuda).rows(xyz.to(cuda), input_range=[r.to(cuda) for r in rng]).cpu()
     assert out.shape == ref.shape
     assert (out - ref).abs().max().item() < 2e-5
+
+
+@pytest.mark.parametrize("C,nparts", [(256, 1024), (1280, 1024), (64, 37)])
+def test_bn_stats_finalize_one_launch_bitwise(cuda, C, nparts):
+    """ov3d_bn_stats_finalize / ov3d_bn_bwd_stats_finalize (column totals + finalize in one
+    launch) equal ov3d_reduce_partials followed by ov3d_bn_finalize / ov3d_bn_bwd_finalize"""
+    from ov3d_amd import _native as nat
+    g = torch.Generator(device=cuda).manual_seed(C)
+    parts = torch.rand((nparts, 2 * C), dtype=torch.float64, device=cuda, generator=g)
+    parts[:, C:] += parts[:, :C] ** 2   # sum of squares >= square of sum / n
+    gamma = torch.randn(C, device=cuda, generator=g)
+    beta = torch.randn(C, device=cuda, generator=g)
+    count = float(nparts * 3)
+    outs = []
+    for fused in (True, False):
+        rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+        nbt = torch.zeros((), dtype=torch.int64, device=cuda)
+        st = [torch.empty(C, device=cuda) for _ in range(4)]
+        bw = [torch.empty(C, device=cuda) for _ in range(5)]
+        if fused:
+            nat.call("ov3d_bn_stats_finalize", parts, nparts, C, count, gamma, beta, 1e-5, 0.1, rm,
+                     rv, *st, nbt, like=parts)
+            nat.call("ov3d_bn_bwd_stats_finalize", parts, nparts, C, count, gamma, st[0], st[1],
+                     *bw, like=parts)
+        else:
+            tot = torch.empty(2 * C, dtype=torch.float64, device=cuda)
+            nat.call("ov3d_reduce_partials", parts, nparts, 2 * C, tot, like=parts)
+            nat.call("ov3d_bn_finalize", tot, count, C, gamma, beta, 1e-5, 0.1, rm, rv, *st, nbt,
+                     like=parts)
+            nat.call("ov3d_bn_bwd_finalize", tot, count, C, gamma, st[0], st[1], *bw, like=parts)
+        outs.append(st + bw + [rm, rv, nbt])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert int(outs[0][-1]) == 1
