@@ -404,6 +404,23 @@ int ov3d_resnorm_fwd(long long R, int C, const void* src, int src_bf16, const vo
  * autograd's fan-in would.
  * partials: (nparts, 4, C) f32 workspace with nparts = ov3d_resnorm_bwd_parts(R, C). */
 int ov3d_resnorm_bwd_parts(long long R, int C);
+/* The LayerNorm weight / bias gradients of a backward pass in one launch: the resnorm
+ * backward calls leave their (nparts, 4, C) partials (column blocks k = 0 dga, 1 dba,
+ * 2 dgb, 3 dbb) and ov3d_colsum_group writes every output = the ordered sum over its
+ * segments of each segment's column total (the ov3d_resnorm_bwd colsum, then the
+ * accumulate adds: bit-identical). */
+typedef struct {
+    const float* partials;
+    int nparts;
+    int k;
+} ov3d_colsum_seg;
+typedef struct {
+    float* dst;      /* (C) */
+    int first_seg;   /* segments [first_seg, first_seg + nseg) of segs */
+    int nseg;
+} ov3d_colsum_out;
+int ov3d_colsum_group(const ov3d_colsum_seg* segs, int nseg, const ov3d_colsum_out* outs, int nout,
+                      int C, void* stream);
 /* FFN activation h = dropout(relu(y)) over contiguous bf16 (R, C) rows (transformer.py
  * FFN), dropout keep = hash of (*seed, site, r, c); backward dy = dh / (1-p) where h > 0 */
 int ov3d_relu_dropout_fwd(const void* y, long long R, int C, float dropout_p, const int64_t* seed,

@@ -166,6 +166,64 @@ def fused_weight_grad(dy, x, bias=True, out_w=None, out_b=None):
 # under DDP (its reducer needs the per-parameter gradient hooks).
 DEFER_WGRAD = False
 _PENDING = []
+_PENDING_COLS = []   # deferred LayerNorm weight / bias gradients (resnorm.py)
+_QUEUED = [False]
+
+
+def _ensure_flush():
+    if not _QUEUED[0]:
+        torch.autograd.Variable._execution_engine.queue_callback(flush_weight_grads)
+        _QUEUED[0] = True
+
+
+class _ColSeg(ctypes.Structure):
+    """mirror of ov3d_colsum_seg"""
+    _fields_ = [("partials", ctypes.c_void_p), ("nparts", ctypes.c_int), ("k", ctypes.c_int)]
+
+
+class _ColOut(ctypes.Structure):
+    """mirror of ov3d_colsum_out"""
+    _fields_ = [("dst", ctypes.c_void_p), ("first_seg", ctypes.c_int), ("nseg", ctypes.c_int)]
+
+
+def defer_norm_grads(partials, nparts, C, slots):
+    """queue LayerNorm parameter gradients: slots [(k, param)], column block k of the
+    (nparts, 4, C) resnorm backward partials is param's gradient (summed with the blocks of
+    the other calls that use the same param, in backward order)."""
+    _ensure_flush()
+    _PENDING_COLS.append((partials, nparts, C, [(k, p) for k, p in slots]))
+
+
+def _flush_norm_grads():
+    from . import _native
+    cols = list(_PENDING_COLS)
+    _PENDING_COLS.clear()
+    if not cols:
+        return
+    by_c = {}
+    for partials, nparts, C, slots in cols:
+        outs = by_c.setdefault(C, {})
+        for k, p in slots:
+            outs.setdefault(id(p), [p, []])[1].append((partials, nparts, k))
+    for C, outs in by_c.items():
+        entries = list(outs.values())
+        dev = entries[0][0].device
+        flat = torch.empty(len(entries) * C, dtype=torch.float32, device=dev)
+        segs, outa = [], []
+        for i, (p, sl) in enumerate(entries):
+            outa.append(_ColOut(flat[i * C:].data_ptr(), len(segs), len(sl)))
+            segs += [_ColSeg(t.data_ptr(), n, k) for t, n, k in sl]
+        sa = (_ColSeg * len(segs))(*segs)
+        oa = (_ColOut * len(outa))(*outa)
+        _native.call("ov3d_colsum_group", ctypes.addressof(sa), len(segs), ctypes.addressof(oa),
+                     len(outa), C, like=flat)
+        with torch.no_grad():
+            for i, (p, _) in enumerate(entries):
+                g = flat[i * C:(i + 1) * C].view(p.shape)
+                if p.grad is None:
+                    p.grad = g
+                else:
+                    p.grad.add_(g)
 
 
 class _WgProblem(ctypes.Structure):
@@ -199,8 +257,7 @@ def can_defer(x, w, b=None):
 def defer_weight_grad(dy, x, w, b=None, rows=None):
     """queue dW = dy^T x (+ db = sum dy) for parameter w (and bias b); rows=(r0, r1): the
     block of w's rows this pair produces (nn.MultiheadAttention in_proj)."""
-    if not _PENDING:
-        torch.autograd.Variable._execution_engine.queue_callback(flush_weight_grads)
+    _ensure_flush()
     _PENDING.append((dy, x, _leaf_param(w), w.shape, _leaf_param(b) if b is not None else None,
                      rows))
 
@@ -208,6 +265,8 @@ def defer_weight_grad(dy, x, w, b=None, rows=None):
 def flush_weight_grads():
     """run every queued weight gradient in one grouped launch and store them as .grad"""
     from . import _native
+    _QUEUED[0] = False
+    _flush_norm_grads()
     items = list(_PENDING)
     _PENDING.clear()
     if not items:

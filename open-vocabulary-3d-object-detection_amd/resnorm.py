@@ -117,6 +117,7 @@ class _ResNorm(torch.autograd.Function):
                      seed, site, ga, ba, posr, _dt_flag(posr), gb, bb, float(eps), s, mean, rstd,
                      xa, xap, xb, like=s)
         ctx.save_for_backward(s, mean, rstd, ga, gb)
+        ctx.params = (ga, ba, gb, bb)
         ctx.set_materialize_grads(False)   # unused outputs: no zero-filled gradients
         ctx.meta = (p, site, R, C, shape, src.dtype if src is not None else None,
                     y.dtype if y is not None else None, pos.dtype if pos is not None else None)
@@ -159,6 +160,19 @@ class _ResNorm(torch.autograd.Function):
         dbb = torch.empty(C, dtype=torch.float32, device=dev) if (need[7] and has_b) else None
         acc = 0
         pos_fan, nb_fan = ctx.fans
+        # LayerNorm weight / bias gradients: deferred to one grouped launch at the end of the
+        # backward (with the weight gradients, gemm.DEFER_WGRAD) from this call's partials
+        params = ctx.params
+        defer_norm = gemm.DEFER_WGRAD and not torch.is_grad_enabled() and (has_a or has_b) and all(
+            t is None or gemm._leaf_param(t) is t for t in params)
+        slots = []
+        if defer_norm:
+            for k, (nd, have) in enumerate(((need[4], has_a), (need[5], has_a),
+                                            (need[6], has_b), (need[7], has_b))):
+                if nd and have:
+                    slots.append((k, params[k]))
+            dga = dba = dgb = dbb = None
+            nb_fan = None
         ret_pos = ret_nb = True
         if pos_fan is not None and need[3]:
             first, ret_pos = pos_fan.take()
@@ -190,6 +204,8 @@ class _ResNorm(torch.autograd.Function):
                          float(p) if dy is not None else 0.0, seed, site, dsrc, dy, _dt_flag(dy),
                          dpos, _dt_flag(dpos), partials, nparts, dga, dba,
                          dgb, dbb, acc, like=s)
+        if slots:
+            gemm.defer_norm_grads(partials, nparts, C, slots)
         v = lambda t: t.view(shape) if t is not None else None   # noqa: E731
         if dsrc is not None and src_dt != torch.float32:
             dsrc = dsrc.to(src_dt)
@@ -197,6 +213,8 @@ class _ResNorm(torch.autograd.Function):
             dpos = dpos_ret if ret_pos else None
         if nb_fan is not None and (need[6] or need[7]):
             dgb, dbb = nb_ret if ret_nb else (None, None)
+        if defer_norm:
+            dga = dba = dgb = dbb = None
         return None, v(dsrc), v(dy), v(dpos), dga, dba, dgb, dbb
 
 
