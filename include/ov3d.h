@@ -503,6 +503,17 @@ int ov3d_rows_gemm(int M, int N, int K, const void* A, long long lda, const void
  *   epilogue 2: C = H > 0 ? bf16(bf16(A W) / (1 - dropout_p)) : 0  (H: the activation
  *               output, (M x N) bf16 rows of ldh; as ov3d_relu_dropout_bwd)
  *   epilogue 0: ov3d_rows_gemm. */
+/* up to 4 problems over the same M rows in one launch (the in-projection blocks of one
+ * attention); each as ov3d_rows_gemm with the common trans_b */
+typedef struct {
+    const void* A; long long lda;
+    const void* W; long long ldw;
+    const void* bias;   /* bf16 (N) or NULL */
+    void* C; long long ldc;
+    int N, K;
+} ov3d_rows_gemm_problem;
+int ov3d_rows_gemm_group(int M, int n, const ov3d_rows_gemm_problem* probs, int trans_b,
+                         void* stream);
 int ov3d_rows_gemm_act(int M, int N, int K, const void* A, long long lda, const void* W,
                        long long ldw, int trans_b, const void* bias, int epilogue,
                        float dropout_p, const int64_t* seed, int site, const void* H,

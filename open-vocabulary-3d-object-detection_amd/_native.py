@@ -71,6 +71,7 @@ _SIGS = {
     "ov3d_colsum_group": "pipiip",
     "ov3d_bn_bwd_stats_finalize": "piidppppppppp",
     "ov3d_rows_gemm_act": "iiiplplipifpiplplp",
+    "ov3d_rows_gemm_group": "iipip",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
                           "ov3d_wgrad_workspace", "ov3d_wgrad_tiles", "ov3d_set_loss_desc_size",

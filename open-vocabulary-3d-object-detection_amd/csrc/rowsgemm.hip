@@ -58,14 +58,13 @@ __device__ __forceinline__ bf16x4 tr16(const bf16* p) {
     return __builtin_bit_cast(bf16x4, r);
 }
 
+// One 32 x 32 output tile (m0, n0) of problem a; K = 4 waves x 16 x `steps` (<= STEPS).
 template <int TB, int STEPS>
-__global__ void __launch_bounds__(256) rows_gemm_kernel(GemmArgs a) {
-    constexpr int KW = 16 * STEPS;   // k per wave
-    __shared__ float red[kWaves][kTile][kTile + 1];
-    __shared__ __attribute__((aligned(16))) bf16 Ws[TB ? 1 : kWaves * KW * LDW];
+__device__ __forceinline__ void gemm_tile(const GemmArgs& a, int m0, int n0, int steps,
+                                          float (*red)[kTile][kTile + 1], bf16* Ws) {
+    const int KW = 16 * steps;   // k per wave
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int m0 = blockIdx.x * kTile, n0 = blockIdx.y * kTile;
     const int kq = w * KW;
     const int row = min(m0 + r, a.M - 1);
     const bf16* ap = a.A + (size_t)row * a.lda + kq;
@@ -74,39 +73,47 @@ __global__ void __launch_bounds__(256) rows_gemm_kernel(GemmArgs a) {
         const bf16* wp = a.W + (size_t)(n0 + r) * a.ldw + kq + 8 * h;
 #pragma unroll
         for (int s = 0; s < STEPS; ++s) {
-            av[s] = *reinterpret_cast<const bf16x8*>(ap + 16 * s + 8 * h);
-            bv[s] = *reinterpret_cast<const bf16x8*>(wp + 16 * s);
+            if (s < steps) {
+                av[s] = *reinterpret_cast<const bf16x8*>(ap + 16 * s + 8 * h);
+                bv[s] = *reinterpret_cast<const bf16x8*>(wp + 16 * s);
+            }
         }
         // every load in flight before the first MFMA (the scheduler would otherwise pair
         // each load with its MFMA and serialise the memory latency)
         __builtin_amdgcn_sched_barrier(0);
     } else {
         // W rows kq .. kq+KW-1, columns n0 .. n0+31: 4 lanes x 16 B per row, 16 rows a pass
-        bf16* ws = Ws + w * KW * LDW;
+        bf16* ws = Ws + w * 16 * STEPS * LDW;
         bf16x8 wr[STEPS];
 #pragma unroll
         for (int s = 0; s < STEPS; ++s)
-            wr[s] = *reinterpret_cast<const bf16x8*>(a.W + (size_t)(kq + 16 * s + (lane >> 2)) * a.ldw +
-                                                     n0 + 8 * (lane & 3));
+            if (s < steps)
+                wr[s] = *reinterpret_cast<const bf16x8*>(a.W + (size_t)(kq + 16 * s + (lane >> 2)) * a.ldw +
+                                                         n0 + 8 * (lane & 3));
 #pragma unroll
         for (int s = 0; s < STEPS; ++s) {
-            const bf16x4 lo = *reinterpret_cast<const bf16x4*>(ap + 16 * s + 4 * h);
-            const bf16x4 hi = *reinterpret_cast<const bf16x4*>(ap + 16 * s + 8 + 4 * h);
-            av[s] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            if (s < steps) {
+                const bf16x4 lo = *reinterpret_cast<const bf16x4*>(ap + 16 * s + 4 * h);
+                const bf16x4 hi = *reinterpret_cast<const bf16x4*>(ap + 16 * s + 8 + 4 * h);
+                av[s] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int s = 0; s < STEPS; ++s)
-            *reinterpret_cast<bf16x8*>(ws + (16 * s + (lane >> 2)) * LDW + 8 * (lane & 3)) = wr[s];
+            if (s < steps)
+                *reinterpret_cast<bf16x8*>(ws + (16 * s + (lane >> 2)) * LDW + 8 * (lane & 3)) = wr[s];
         __syncthreads();
         const int g = lane >> 4, i = lane & 15;
         const int d0 = 16 * (g & 1) + 4 * (i & 3);
 #pragma unroll
         for (int s = 0; s < STEPS; ++s) {
-            const int k0 = 16 * s + 4 * (g >> 1) + (i >> 2);
-            const bf16x4 lo = tr16(ws + k0 * LDW + d0);
-            const bf16x4 hi = tr16(ws + (k0 + 8) * LDW + d0);
-            bv[s] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            if (s < steps) {
+                const int k0 = 16 * s + 4 * (g >> 1) + (i >> 2);
+                const bf16x4 lo = tr16(ws + k0 * LDW + d0);
+                const bf16x4 hi = tr16(ws + (k0 + 8) * LDW + d0);
+                bv[s] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            }
         }
     }
     // S^T-style product: acc lane (col = r, rows (v&3) + 8(v>>2) + 4h) = C[m0 + row][n0 + r]
@@ -114,7 +121,8 @@ __global__ void __launch_bounds__(256) rows_gemm_kernel(GemmArgs a) {
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[v] = 0.f;
 #pragma unroll
-    for (int s = 0; s < STEPS; ++s) acc = mfma(av[s], bv[s], acc);
+    for (int s = 0; s < STEPS; ++s)
+        if (s < steps) acc = mfma(av[s], bv[s], acc);
 #pragma unroll
     for (int v = 0; v < 16; ++v) red[w][(v & 3) + 8 * (v >> 2) + 4 * h][r] = acc[v];
     __syncthreads();
@@ -142,8 +150,8 @@ __global__ void __launch_bounds__(256) rows_gemm_kernel(GemmArgs a) {
         if (a.bias) t += (float)a.bias[gc + q];
         const bf16 y = (bf16)t;
         if (a.epi == EPI_RELU_DROP) {
-            const float r = fmaxf((float)y, 0.f);
-            o[q] = a.thresh ? (keep[q] ? (bf16)(r * a.keep_scale) : (bf16)0.f) : (bf16)r;
+            const float rr = fmaxf((float)y, 0.f);
+            o[q] = a.thresh ? (keep[q] ? (bf16)(rr * a.keep_scale) : (bf16)0.f) : (bf16)rr;
         } else if (a.epi == EPI_MASK) {
             o[q] = (float)hv[q] > 0.f ? (bf16)((float)y * a.keep_scale) : (bf16)0.f;
         } else {
@@ -151,6 +159,34 @@ __global__ void __launch_bounds__(256) rows_gemm_kernel(GemmArgs a) {
         }
     }
     *reinterpret_cast<bf16x4*>(a.C + (size_t)gr * a.ldc + gc) = o;
+}
+
+template <int TB, int STEPS>
+__global__ void __launch_bounds__(256) rows_gemm_kernel(GemmArgs a) {
+    __shared__ float red[kWaves][kTile][kTile + 1];
+    __shared__ __attribute__((aligned(16))) bf16 Ws[TB ? 1 : kWaves * 16 * STEPS * LDW];
+    gemm_tile<TB, STEPS>(a, blockIdx.x * kTile, blockIdx.y * kTile, STEPS, red, Ws);
+}
+
+// Several problems over the same rows in one launch (the in-projection blocks of one
+// attention, gemm._InProj): blockIdx.y enumerates the 32-column tiles of all problems.
+constexpr int kGroupProbs = 4;
+struct GemmGroup {
+    GemmArgs p[kGroupProbs];
+    int tiles[kGroupProbs + 1];
+    int n;
+};
+
+template <int TB, int STEPS>
+__global__ void __launch_bounds__(256) rows_gemm_group_kernel(GemmGroup g) {
+    __shared__ float red[kWaves][kTile][kTile + 1];
+    __shared__ __attribute__((aligned(16))) bf16 Ws[TB ? 1 : kWaves * 16 * STEPS * LDW];
+    const int t = blockIdx.y;
+    int i = 0;
+    while (i + 1 < g.n && t >= g.tiles[i + 1]) ++i;
+    const GemmArgs& a = g.p[i];
+    gemm_tile<TB, STEPS>(a, blockIdx.x * kTile, (t - g.tiles[i]) * kTile, a.K / (16 * kWaves), red,
+                         Ws);
 }
 
 template <int TB>
@@ -201,4 +237,43 @@ extern "C" int ov3d_rows_gemm(int M, int N, int K, const void* A, long long lda,
                               void* stream) {
     return ov3d_rows_gemm_act(M, N, K, A, lda, W, ldw, trans_b, bias, EPI_NONE, 0.f, nullptr, 0,
                               nullptr, 0, C, ldc, stream);
+}
+
+namespace {
+template <int TB>
+int launch_group(const GemmGroup& g, int M, int steps, hipStream_t s) {
+    const dim3 grid(ov3d_cdiv(M, kTile), g.tiles[g.n]);
+    switch (steps <= 4 ? 4 : steps <= 8 ? 8 : steps <= 12 ? 12 : 16) {
+        case 4: rows_gemm_group_kernel<TB, 4><<<grid, 256, 0, s>>>(g); break;
+        case 8: rows_gemm_group_kernel<TB, 8><<<grid, 256, 0, s>>>(g); break;
+        case 12: rows_gemm_group_kernel<TB, 12><<<grid, 256, 0, s>>>(g); break;
+        default: rows_gemm_group_kernel<TB, 16><<<grid, 256, 0, s>>>(g); break;
+    }
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+}  // namespace
+
+extern "C" int ov3d_rows_gemm_group(int M, int n, const ov3d_rows_gemm_problem* probs, int trans_b,
+                                    void* stream) {
+    if (M <= 0 || n <= 0 || n > kGroupProbs || !probs) return OV3D_EINVAL;
+    GemmGroup g;
+    g.n = n;
+    g.tiles[0] = 0;
+    int steps = 1;
+    for (int i = 0; i < n; ++i) {
+        const ov3d_rows_gemm_problem& q = probs[i];
+        if (!ov3d_rows_gemm_supported(M, q.N, q.K) || !q.A || !q.W || !q.C) return OV3D_EINVAL;
+        if (((uintptr_t)q.A | (uintptr_t)q.W) % 16 || (uintptr_t)q.C % 8 ||
+            (q.bias && (uintptr_t)q.bias % 2) || q.lda % 8 || q.ldw % 8 || q.ldc % 4 ||
+            q.lda < q.K || q.ldc < q.N || q.ldw < (trans_b ? q.K : q.N))
+            return OV3D_EINVAL;
+        g.p[i] = GemmArgs{(const bf16*)q.A, q.lda, (const bf16*)q.W, q.ldw, (const bf16*)q.bias,
+                          (bf16*)q.C, q.ldc, M, q.N, q.K, EPI_NONE, 0u, 1.f, nullptr, 0u,
+                          nullptr, 0};
+        g.tiles[i + 1] = g.tiles[i] + q.N / kTile;
+        steps = max(steps, q.K / (16 * kWaves));
+    }
+    hipStream_t s = ov3d_stream(stream);
+    return trans_b ? launch_group<1>(g, M, steps, s) : launch_group<0>(g, M, steps, s);
 }

@@ -9,6 +9,7 @@ measured: profiles/r01_kernel_stats_v2.csv).  Here the reduction is split into
 row chunks computed as one batched GEMM (>= ~256 workgroups) and summed in fp32.
 """
 import ctypes
+import os
 import weakref
 
 import torch
@@ -61,6 +62,43 @@ def rows_gemm(a, w, bias=None, trans_b=True):
     _native.call("ov3d_rows_gemm", M, N, K, a, a.stride(0), w, w.stride(0), int(trans_b), bias,
                  out, N, like=a)
     return out
+
+
+class _RgProblem(ctypes.Structure):
+    """mirror of ov3d_rows_gemm_problem (include/ov3d.h)"""
+    _fields_ = [("A", ctypes.c_void_p), ("lda", ctypes.c_longlong), ("W", ctypes.c_void_p),
+                ("ldw", ctypes.c_longlong), ("bias", ctypes.c_void_p), ("C", ctypes.c_void_p),
+                ("ldc", ctypes.c_longlong), ("N", ctypes.c_int), ("K", ctypes.c_int)]
+
+
+def rows_gemm_group(problems, trans_b=True):
+    """[(a, w, bias)] over the same rows -> [outputs], one launch (every pair must pass
+    _rows_gemm_ok; at most 4)"""
+    from . import _native
+    M = problems[0][0].shape[0]
+    outs, keep, probs = [], [], []
+    for a, w, b in problems:
+        N = w.shape[0] if trans_b else w.shape[1]
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+        if b is not None and (b.dtype != torch.bfloat16 or not b.is_contiguous()):
+            b = b.to(torch.bfloat16).contiguous()
+        keep.append(b)
+        outs.append(out)
+        probs.append(_RgProblem(a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0),
+                                b.data_ptr() if b is not None else None, out.data_ptr(), N, N,
+                                a.shape[1]))
+    arr = (_RgProblem * len(probs))(*probs)
+    _native.call("ov3d_rows_gemm_group", M, len(probs), ctypes.addressof(arr), int(trans_b),
+                 like=problems[0][0])
+    return outs
+
+
+ROWS_GEMM_GROUP = os.environ.get("OV3D_ROWS_GEMM_GROUP", "1") != "0"
+
+
+def _group_ok(pairs, trans_b):
+    return (ROWS_GEMM_GROUP and 1 < len(pairs) <= 4 and len({a.shape[0] for a, _ in pairs}) == 1
+            and all(_rows_gemm_ok(a, w, trans_b) for a, w in pairs))
 
 
 def _linear(x, w, b):
@@ -439,9 +477,14 @@ class _InProj(Function):
         wc, bc = cast_param(w, dt), cast_param(b, dt)
         outs, saved = [], []
         with torch.autocast("cuda", enabled=False):
-            for x, (r0, r1) in zip(xs, spec):
-                xc = x.reshape(-1, x.shape[-1]).to(dt)
-                y = _linear(xc, wc[r0:r1], bc[r0:r1] if bc is not None else None)
+            xcs = [x.reshape(-1, x.shape[-1]).to(dt) for x in xs]
+            if _group_ok([(xc, wc[r0:r1]) for xc, (r0, r1) in zip(xcs, spec)], True):
+                ys = rows_gemm_group([(xc, wc[r0:r1], bc[r0:r1] if bc is not None else None)
+                                      for xc, (r0, r1) in zip(xcs, spec)], trans_b=True)
+            else:
+                ys = [_linear(xc, wc[r0:r1], bc[r0:r1] if bc is not None else None)
+                      for xc, (r0, r1) in zip(xcs, spec)]
+            for x, xc, y, (r0, r1) in zip(xs, xcs, ys, spec):
                 outs.append(y.view(*x.shape[:-1], r1 - r0))
                 saved.append(xc)
         ctx.save_for_backward(wc, *saved)
@@ -466,12 +509,22 @@ class _InProj(Function):
             if want_b and not defer else None
         dxs = []
         with torch.autocast("cuda", enabled=False):
+            dys = [(torch.zeros(xc.shape[0], r1 - r0, dtype=xc.dtype, device=xc.device)
+                    if dy is None else dy.reshape(-1, r1 - r0).to(xc.dtype).contiguous())
+                   for dy, xc, (r0, r1) in zip(dys, xcs, spec)]
+            want = [i for i in range(len(dys)) if ctx.needs_input_grad[3 + i]]
+            pairs = [(dys[i], wc[spec[i][0]:spec[i][1]]) for i in want]
+            dx_all = [None] * len(dys)
+            if _group_ok(pairs, False):   # the input gradients in one launch
+                for i, d in zip(want, rows_gemm_group([(a, w, None) for a, w in pairs],
+                                                      trans_b=False)):
+                    dx_all[i] = d
             for i, (dy, xc, (r0, r1)) in enumerate(zip(dys, xcs, spec)):
-                if dy is None:
-                    dy = torch.zeros(xc.shape[0], r1 - r0, dtype=xc.dtype, device=xc.device)
-                dy = dy.reshape(-1, r1 - r0).to(xc.dtype).contiguous()
-                dxs.append(_dgrad(dy, wc[r0:r1]).to(xdts[i]).view(xshapes[i])
-                           if ctx.needs_input_grad[3 + i] else None)
+                if ctx.needs_input_grad[3 + i]:
+                    d = dx_all[i] if dx_all[i] is not None else _dgrad(dy, wc[r0:r1])
+                    dxs.append(d.to(xdts[i]).view(xshapes[i]))
+                else:
+                    dxs.append(None)
                 if defer:
                     defer_weight_grad(dy, xc, wp, bp if want_b else None, rows=(r0, r1))
                     continue

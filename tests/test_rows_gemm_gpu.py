@@ -100,3 +100,24 @@ def test_fused_ffn_equals_unfused_bitwise(cuda, p, monkeypatch):
         res[fused] = [y, x.grad, l1.weight.grad, l1.bias.grad, l2.weight.grad, l2.bias.grad]
     for i, (a, b) in enumerate(zip(res[True], res[False])):
         assert torch.equal(a, b), (i, (a.float() - b.float()).abs().max().item())
+
+
+@pytest.mark.parametrize("trans_b", [True, False])
+def test_rows_gemm_group_equals_single_launches(cuda, trans_b):
+    """ov3d_rows_gemm_group (problems of different N / K over the same rows: an attention's
+    in-projection blocks) equals one ov3d_rows_gemm per problem, bit for bit"""
+    from ov3d_amd import gemm
+    g = torch.Generator(device=cuda).manual_seed(11)
+    M = 1024
+    shapes = [(512, 256), (256, 256), (256, 512)]   # (N, K)
+    probs = []
+    for N, K in shapes:
+        a = torch.randn(M, K, device=cuda, generator=g).to(torch.bfloat16)
+        w = (torch.randn(*((N, K) if trans_b else (K, N)), device=cuda, generator=g) / K ** 0.5
+             ).to(torch.bfloat16)
+        b = torch.randn(N, device=cuda, generator=g).to(torch.bfloat16) if trans_b else None
+        probs.append((a, w, b))
+    assert gemm._group_ok([(a, w) for a, w, _ in probs], trans_b)
+    outs = gemm.rows_gemm_group(probs, trans_b=trans_b)
+    for (a, w, b), o in zip(probs, outs):
+        assert torch.equal(o, gemm.rows_gemm(a, w, b, trans_b=trans_b))
