@@ -1,0 +1,258 @@
+// Backward of the last SA MLP layer (the pooled one, model_3detr.py:353-362 pre-encoder
+// SharedMLP layer 3: 1x1 conv 128 -> 256, BN, ReLU, max over nsample) in ONE pass over the
+// R = B*M*S rows, replacing the dy recompute kernel + a dW GEMM + a dgrad GEMM that each
+// streamed the (R, 256) bf16 dy3 through HBM (sa_dy_fused_kernel):
+//
+//   per 64-row tile (persistent workgroups, W3 fragments in VGPRs for the whole launch):
+//     z   = relu(a2*y2 + b2)            (layer 2's folded BN, bf16)   -> LDS
+//     y3  = z W3^T                      (MFMA 32x32x16, recomputed)
+//     dy3 = cA*g + cB*y3 + cC           (BN backward of the pooled layer; g = the pooled
+//                                        gradient at its arg row)     -> LDS (bf16)
+//     dz  = dy3 W3                      (MFMA, W3^T fragments)         -> HBM (R, 128) bf16
+//     dW3 += dy3^T z                    (MFMA on ds_read_b64_tr_b16 reads of both LDS tiles,
+//                                        accumulated over the workgroup's tiles)
+//   dW3 partials per workgroup (fixed order), summed by the caller.
+// dy3 and z are never stored: the forward no longer writes z (2^20 x 128 bf16) either.
+#include "common.h"
+
+namespace {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kTile = 64;      // rows per tile (one centroid at S = 64, two at S = 32)
+constexpr int kThreads = 256;  // 4 waves
+
+struct DyFusedArgs {
+    const bf16* yprev;     // (R, K) layer-2 output y2
+    const float* scale;    // (K) layer-2 folded BN a2
+    const float* shift;    // (K) b2
+    const bf16* W;         // (N, K) W3
+    int R, S;
+    const float* gsel;     // (P, N) pooled gradient after the ReLU mask
+    const uint8_t* isel;   // (P, N) row of the pooled value within its centroid
+    const float* cA;       // (N) dy3 = cA*g + cB*y3 + cC
+    const float* cB;
+    const float* cC;
+    bf16* dz;              // (R, K) gradient of z (layer-2 activation output)
+    float* dwpart;         // (gridDim.x, N, K) dW3 partial per workgroup
+};
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x4 tr16(const bf16* p) {
+    s16x4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(p));
+    return __builtin_bit_cast(bf16x4, r);
+}
+
+// MFMA operand whose lane index runs over the columns c0 .. c0+31 of a row-major LDS tile
+// and whose 8 elements are rows 16s + 8(j>>2) + 4h + (j&3) (ds_read_b64_tr_b16; the two
+// operands of one product use the same row order)
+__device__ __forceinline__ bf16x8 col_operand(const bf16* T, int ld, int lane, int c0, int s) {
+    const int g = lane >> 4, i = lane & 15;
+    const int d0 = c0 + 16 * (g & 1) + 4 * (i & 3);
+    const int k0 = 16 * s + 4 * (g >> 1) + (i >> 2);
+    const bf16x4 lo = tr16(T + k0 * ld + d0);
+    const bf16x4 hi = tr16(T + (k0 + 8) * ld + d0);
+    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int K, int N>
+__global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p) {
+    constexpr int LDK = K + 8;        // padded LDS rows (bf16)
+    constexpr int LDN = N + 8;
+    constexpr int NB = N / 128;       // y3: 32-column blocks per wave (a wave owns N/4 columns)
+    constexpr int KS = K / 16;        // y3: k-steps
+    constexpr int KB = K / 128;       // dz: 32-column blocks per wave (a wave owns K/4 columns)
+    constexpr int NS = N / 16;        // dz: k-steps
+    constexpr int WN = N / 128;       // dW: 32-row blocks per wave (a wave owns N/4 rows)
+    constexpr int WK = K / 32;        // dW: 32-column blocks (all K)
+    static_assert(N % 128 == 0 && K % 128 == 0, "tile shape");
+    __shared__ __attribute__((aligned(16))) bf16 As[kTile * LDK];
+    __shared__ __attribute__((aligned(16))) bf16 Ds[kTile * LDN];
+    __shared__ float sc[K], sh[K];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r32 = lane & 31, h = lane >> 5;
+
+    for (int k = tid; k < K; k += kThreads) {
+        sc[k] = p.scale[k];
+        sh[k] = p.shift[k];
+    }
+    // W3 fragments for y3 = z W3^T: lane row n, 8 consecutive k
+    bf16x8 bfrag[NB][KS];
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb) {
+        const int n = wave * (N / 4) + cb * 32 + r32;
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+            bfrag[cb][s] = *reinterpret_cast<const bf16x8*>(p.W + (size_t)n * K + 16 * s + 8 * h);
+    }
+    // W3^T fragments for dz = dy3 W3: lane column k, 8 consecutive n (gathered once)
+    bf16x8 wt[KB][NS];
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+        const int k = wave * (K / 4) + kb * 32 + r32;
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) wt[kb][s][j] = p.W[(size_t)(16 * s + 8 * h + j) * K + k];
+    }
+    float cA[NB], cB[NB], cC[NB];
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb) {
+        const int n = wave * (N / 4) + cb * 32 + r32;
+        cA[cb] = p.cA[n];
+        cB[cb] = p.cB[n];
+        cC[cb] = p.cC[n];
+    }
+    f32x16 dw[WN][WK];
+#pragma unroll
+    for (int a = 0; a < WN; ++a)
+#pragma unroll
+        for (int b = 0; b < WK; ++b)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) dw[a][b][i] = 0.f;
+    __syncthreads();
+
+    const int ntiles = p.R / kTile;
+    constexpr int CH = kTile * K / 8 / kThreads;
+    static_assert(CH * kThreads * 8 == kTile * K, "tile chunks");
+    bf16x8 pre[CH];
+    auto fetch = [&](int tile) {
+        const size_t row0 = (size_t)tile * kTile;
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const int ch = tid + c * kThreads;
+            const int row = ch / (K / 8), kc = (ch % (K / 8)) * 8;
+            pre[c] = *reinterpret_cast<const bf16x8*>(p.yprev + (row0 + row) * K + kc);
+        }
+    };
+    if (blockIdx.x < ntiles) fetch(blockIdx.x);
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const size_t row0 = (size_t)tile * kTile;
+        // z = relu(a2*y2 + b2) of the prefetched rows -> LDS
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const int ch = tid + c * kThreads;
+            const int row = ch / (K / 8), kc = (ch % (K / 8)) * 8;
+            bf16x8 z;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                z[j] = (bf16)fmaxf(fmaf(sc[kc + j], (float)pre[c][j], sh[kc + j]), 0.f);
+            *reinterpret_cast<bf16x8*>(&As[row * LDK + kc]) = z;
+        }
+        __syncthreads();
+        if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);   // in flight below
+
+        // y3 = z W3^T, then dy3 -> LDS
+        {
+            f32x16 acc[2][NB];
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+                for (int cb = 0; cb < NB; ++cb)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) acc[rb][cb][i] = 0.f;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+#pragma unroll
+                for (int rb = 0; rb < 2; ++rb) {
+                    const bf16x8 a = *reinterpret_cast<const bf16x8*>(&As[(rb * 32 + r32) * LDK + 16 * s + 8 * h]);
+#pragma unroll
+                    for (int cb = 0; cb < NB; ++cb) acc[rb][cb] = mfma(a, bfrag[cb][s], acc[rb][cb]);
+                }
+            }
+#pragma unroll
+            for (int cb = 0; cb < NB; ++cb) {
+                const int n = wave * (N / 4) + cb * 32 + r32;
+#pragma unroll
+                for (int rb = 0; rb < 2; ++rb) {
+                    const size_t pc = (p.S == 64 ? (size_t)tile : (size_t)tile * 2 + rb) * N + n;
+                    const int sel = p.isel[pc] + (p.S == 64 ? 0 : 32 * rb);
+                    const float g = p.gsel[pc];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int row = rb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                        const float y = (float)(bf16)acc[rb][cb][i];
+                        const float gi = row == sel ? g : 0.f;
+                        Ds[row * LDN + n] = (bf16)fmaf(cA[cb], gi, fmaf(cB[cb], y, cC[cb]));
+                    }
+                }
+            }
+        }
+        __syncthreads();
+
+        // dz = dy3 W3 -> HBM
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+            const int k = wave * (K / 4) + kb * 32 + r32;
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb) {
+                f32x16 acc;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+                for (int s = 0; s < NS; ++s) {
+                    const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Ds[(rb * 32 + r32) * LDN + 16 * s + 8 * h]);
+                    acc = mfma(a, wt[kb][s], acc);
+                }
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int row = rb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    p.dz[(row0 + row) * K + k] = (bf16)acc[i];
+                }
+            }
+        }
+        // dW3 += dy3^T z over this tile's rows
+#pragma unroll
+        for (int s = 0; s < kTile / 16; ++s) {
+            bf16x8 bz[WK];
+#pragma unroll
+            for (int b = 0; b < WK; ++b) bz[b] = col_operand(As, LDK, lane, 32 * b, s);
+#pragma unroll
+            for (int a = 0; a < WN; ++a) {
+                const bf16x8 ad = col_operand(Ds, LDN, lane, wave * (N / 4) + 32 * a, s);
+#pragma unroll
+                for (int b = 0; b < WK; ++b) dw[a][b] = mfma(ad, bz[b], dw[a][b]);
+            }
+        }
+        __syncthreads();   // As / Ds are rewritten by the next tile
+    }
+    // this workgroup's dW3 partial: element (a, b, i) = dW[n][k],
+    // n = wave*(N/4) + 32a + (i&3) + 8(i>>2) + 4h, k = 32b + r32
+    float* out = p.dwpart + (size_t)blockIdx.x * N * K;
+#pragma unroll
+    for (int a = 0; a < WN; ++a)
+#pragma unroll
+        for (int b = 0; b < WK; ++b)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int n = wave * (N / 4) + 32 * a + (i & 3) + 8 * (i >> 2) + 4 * h;
+                out[(size_t)n * K + 32 * b + r32] = dw[a][b][i];
+            }
+}
+
+}  // namespace
+
+extern "C" int ov3d_sa_dy_fused_supported(int K, int N) { return K == 128 && N == 256; }
+
+extern "C" int ov3d_sa_dy_fused(const void* yprev, const float* scale, const float* shift,
+                                const void* W, int R, int K, int N, int S, const float* gsel,
+                                const uint8_t* isel, const float* cA, const float* cB,
+                                const float* cC, void* dz, float* dwpart, int nwg, void* stream) {
+    if (!ov3d_sa_dy_fused_supported(K, N) || R <= 0 || R % kTile || (S != 32 && S != 64) ||
+        !yprev || !scale || !shift || !W || !gsel || !isel || !cA || !cB || !cC || !dz ||
+        !dwpart || nwg <= 0)
+        return OV3D_EINVAL;
+    DyFusedArgs a{(const bf16*)yprev, scale, shift, (const bf16*)W, R, S, gsel, isel, cA, cB, cC,
+                  (bf16*)dz, dwpart};
+    hipLaunchKernelGGL((sa_dy_fused_kernel<128, 256>), dim3(nwg), dim3(kThreads), 0,
+                       ov3d_stream(stream), a);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}

@@ -36,6 +36,9 @@ NPARTS_LAYER = 1024    # MFMA workgroups over 64-row tiles (more than resident: 
                        # the side-stream FPS holds a few CUs; tools/sa_layer_probe.py)
 NPARTS_ROWS = 1024     # row-pass workgroups
 NPARTS_POOL = 256
+# last layer's backward in one pass (csrc/sa_bwd.hip): one persistent workgroup per CU
+FUSED_BWD = os.environ.get("OV3D_SA_FUSED_BWD", "1") != "0"
+NWG_DY_FUSED = 256
 
 
 def _bn(layer):
@@ -164,9 +167,10 @@ class _SAMLPPool(Function):
         nat.call("ov3d_sa_layer_fwd", y1, st1[2], st1[3], w2b, R, c1, c2, z1, y2, parts, NPARTS_LAYER,
                  like=x0)
         st2 = _bn_stats(parts, NPARTS_LAYER, c2, groups[1], R * world[1], bns[1])
-        # layer 3 + pool
+        # layer 3 + pool (z2 is kept for the backward only when it is not recomputed there)
         w3b = cast_param(w3, bf).contiguous()
-        z2 = torch.empty((R, c2), dtype=bf, device=dev)
+        fused_bwd = FUSED_BWD and bool(nat.load().ov3d_sa_dy_fused_supported(c2, c3))
+        z2 = None if fused_bwd else torch.empty((R, c2), dtype=bf, device=dev)
         pmax, pmin = (torch.empty((P, c3), dtype=torch.float32, device=dev) for _ in range(2))
         imax, imin = (torch.empty((P, c3), dtype=torch.uint8, device=dev) for _ in range(2))
         parts = torch.empty((NPARTS_LAYER, 2, c3), dtype=torch.float64, device=dev)
@@ -179,14 +183,14 @@ class _SAMLPPool(Function):
         nat.call("ov3d_sa_pool_fwd", pmax, pmin, imax, imin, st3[2], st3[3], P, c3, out, ysel, isel,
                  like=x0)
         ctx.save_for_backward(x0, y1, z1, y2, z2, w2b, w3b, g1, g2, g3, ysel, isel, *st1, *st2, *st3)
-        ctx.meta = (R, S, P, c1, c2, c3, groups, world, tuple(w1.shape))
+        ctx.meta = (R, S, P, c1, c2, c3, groups, world, tuple(w1.shape), fused_bwd)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         (x0, y1, z1, y2, z2, w2b, w3b, g1, g2, g3, ysel, isel,
          m1, i1, a1, s1, m2, i2, a2, s2, m3, i3, a3, s3) = ctx.saved_tensors
-        R, S, P, c1, c2, c3, groups, world, w1shape = ctx.meta
+        R, S, P, c1, c2, c3, groups, world, w1shape, fused_bwd = ctx.meta
         dev = x0.device
         bf = torch.bfloat16
         dout = dout.float().contiguous()
@@ -197,12 +201,21 @@ class _SAMLPPool(Function):
                  like=dout)
         cA, cB, cC, dg3, db3 = bn_bwd_affine(parts, NPARTS_POOL, c3, groups[2], R * world[2], g3,
                                              m3, i3)
-        dy3 = torch.empty((R, c3), dtype=bf, device=dev)
-        nat.call("ov3d_sa_layer_dy", y2, a2, s2, w3b, R, c2, c3, S, gsel, isel, cA, cB, cC, dy3,
-                 NPARTS_LAYER, like=dout)
-        dw3 = weight_grad(dy3, z2)
-        dz2 = torch.mm(dy3, w3b)
-        del dy3
+        if fused_bwd:   # dy3 -> dz2 and dW3 inside one pass (csrc/sa_bwd.hip)
+            nwg = min(NWG_DY_FUSED, R // 64)
+            dz2 = torch.empty((R, c2), dtype=bf, device=dev)
+            part = torch.empty((nwg, c3, c2), dtype=torch.float32, device=dev)
+            nat.call("ov3d_sa_dy_fused", y2, a2, s2, w3b, R, c2, c3, S, gsel, isel, cA, cB, cC, dz2,
+                     part, nwg, like=dout)
+            dw3 = part.sum(0)
+            del part
+        else:
+            dy3 = torch.empty((R, c3), dtype=bf, device=dev)
+            nat.call("ov3d_sa_layer_dy", y2, a2, s2, w3b, R, c2, c3, S, gsel, isel, cA, cB, cC, dy3,
+                     NPARTS_LAYER, like=dout)
+            dw3 = weight_grad(dy3, z2)
+            dz2 = torch.mm(dy3, w3b)
+            del dy3
         # layer 2: ReLU + BN backward (two row passes), dz1 and dW2
         parts = torch.empty((NPARTS_ROWS, 2, c2), dtype=torch.float64, device=dev)
         nat.call("ov3d_bn_relu_bwd", 0, dz2, y2, a2, s2, m2, i2, None, None, None, None, R, c2, parts,

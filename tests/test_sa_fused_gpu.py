@@ -139,14 +139,44 @@ def test_model_step_uses_fused_sa_and_trains(cuda):
     model = model.to(cuda).train()
     crit = ov3d_amd.build_criterion(args, cfg).to(cuda)
     batch = synthetic.make_batch(8, seed=2, device=cuda)
-    _native.timing_enable(["ov3d_sa_layer_pool_fwd", "ov3d_sa_layer_dy"])
+    _native.timing_enable(["ov3d_sa_layer_pool_fwd", "ov3d_sa_layer_dy", "ov3d_sa_dy_fused"])
     with torch.autocast("cuda", dtype=torch.bfloat16):
         out = model({k: batch[k] for k in ("point_clouds", "point_cloud_dims_min",
                                            "point_cloud_dims_max")})
     loss, _ = crit(out, batch)
     loss.backward()
     t = _native.timing_collect()
-    assert len(t["ov3d_sa_layer_pool_fwd"]) == 1 and len(t["ov3d_sa_layer_dy"]) == 1
+    assert len(t["ov3d_sa_layer_pool_fwd"]) == 1
+    assert len(t["ov3d_sa_dy_fused"]) == 1 and len(t["ov3d_sa_layer_dy"]) == 0   # one-pass bwd
     assert torch.isfinite(loss)
     w = model.pre_encoder.mlp_module.layer0.conv.weight
     assert w.grad is not None and torch.isfinite(w.grad).all() and w.grad.abs().sum() > 0
+
+
+@pytest.mark.parametrize("nsample", [64, 32])
+def test_last_layer_backward_one_pass_equals_three_passes(cuda, monkeypatch, nsample):
+    """csrc/sa_bwd.hip (dy3 -> dz2 and dW3 in one pass, dy3 / z2 never stored) against the dy
+    recompute kernel + dW GEMM + dgrad GEMM: same gradients up to fp32 summation order"""
+    from ov3d_amd import sa_fused, synthetic
+    from ov3d_amd.pointnet2_modules import PointnetSAModuleVotes
+    torch.manual_seed(3)
+    sa = PointnetSAModuleVotes(radius=0.2, nsample=nsample, npoint=2048, mlp=[0, 64, 128, 256],
+                               normalize_xyz=True).to(cuda).train()
+    with torch.no_grad():
+        for layer in sa.mlp_module:
+            bn = layer.bn.bn
+            bn.weight.copy_(torch.randn_like(bn.weight) * 0.5 + 0.6)
+            bn.bias.copy_(torch.randn_like(bn.bias) * 0.2)
+    xyz = synthetic.make_batch(2, seed=9, device=cuda)["point_clouds"]
+    gw = torch.randn(2, 256, 2048, device=cuda)
+    res = {}
+    for fused in (True, False):
+        monkeypatch.setattr(sa_fused, "FUSED_BWD", fused)
+        twin = copy.deepcopy(sa)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            _, f, _ = twin(xyz[..., :3].contiguous())
+        (f.float() * gw).sum().backward()
+        res[fused] = {n: p.grad.clone() for n, p in twin.named_parameters()}
+    for n in res[False]:
+        e = _rel(res[True][n], res[False][n])
+        assert e < 2e-3, (n, e)
