@@ -145,12 +145,15 @@ int ov3d_sa_layer_dy(const void* yprev, const float* scale, const float* shift, 
 /* Backward of the pooled last layer in one pass (csrc/sa_bwd.hip): recomputes
  * z = relu(scale*yprev + shift) and y = z W^T, dy = cA*g + cB*y + cC (g = gsel at the isel
  * row), and writes dz = dy W (R, K) bf16 and the per-workgroup dW = dy^T z partials
- * dwpart (nwg, N, K) fp32 (sum them over nwg); dy and z never reach HBM.  K = 128, N = 256. */
+ * dwpart (nwg, N, K) fp32 (sum them over nwg); dy and z never reach HBM.  K = 128, N = 256.
+ * stats (nwg, 2, K) fp64 or NULL: the previous layer's ReLU + BN backward partials (sum dt,
+ * sum dt * (yprev - mean) * invstd with dt = (scale*yprev + shift > 0) * dz), the pass 0
+ * of ov3d_bn_relu_bwd on the dz written. */
 int ov3d_sa_dy_fused_supported(int K, int N);
 int ov3d_sa_dy_fused(const void* yprev, const float* scale, const float* shift, const void* W,
                      int R, int K, int N, int S, const float* gsel, const uint8_t* isel,
                      const float* cA, const float* cB, const float* cC, void* dz, float* dwpart,
-                     int nwg, void* stream);
+                     const float* mean, const float* invstd, double* stats, int nwg, void* stream);
 /* (nparts, width) fp64 -> (width) sums */
 int ov3d_reduce_partials(const double* partials, int nparts, int width, double* totals,
                          void* stream);

@@ -12,6 +12,9 @@
 //     dW3 += dy3^T z                    (MFMA on ds_read_b64_tr_b16 reads of both LDS tiles,
 //                                        accumulated over the workgroup's tiles)
 //   dW3 partials per workgroup (fixed order), summed by the caller.
+//   With `stats`: also the previous layer's ReLU + BN backward partial sums over the rows,
+//   sum dt and sum dt * xhat2 per channel, dt = (a2*y2 + b2 > 0) * bf16(dz) (the pass 0 of
+//   bn_relu_bwd_kernel, whose read of dz and y2 it replaces).
 // dy3 and z are never stored: the forward no longer writes z (2^20 x 128 bf16) either.
 #include "common.h"
 
@@ -39,6 +42,9 @@ struct DyFusedArgs {
     const float* cC;
     bf16* dz;              // (R, K) gradient of z (layer-2 activation output)
     float* dwpart;         // (gridDim.x, N, K) dW3 partial per workgroup
+    const float* mean;     // (K) layer-2 batch mean / invstd (with stats)
+    const float* invstd;
+    double* stats;         // (gridDim.x, 2, K) or null
 };
 
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
@@ -76,6 +82,7 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
     static_assert(N % 128 == 0 && K % 128 == 0, "tile shape");
     __shared__ __attribute__((aligned(16))) bf16 As[kTile * LDK];
     __shared__ __attribute__((aligned(16))) bf16 Ds[kTile * LDN];
+    __shared__ __attribute__((aligned(16))) bf16 Ys[kTile * LDK];   // raw y2 (stats only)
     __shared__ float sc[K], sh[K];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r32 = lane & 31, h = lane >> 5;
 
@@ -109,6 +116,15 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
         cA[cb] = p.cA[n];
         cB[cb] = p.cB[n];
         cC[cb] = p.cC[n];
+    }
+    const bool stats = p.stats != nullptr;
+    float mu[KB], istd[KB], st1[KB], st2[KB];
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+        const int k = wave * (K / 4) + kb * 32 + r32;
+        mu[kb] = stats ? p.mean[k] : 0.f;
+        istd[kb] = stats ? p.invstd[k] : 0.f;
+        st1[kb] = st2[kb] = 0.f;
     }
     f32x16 dw[WN][WK];
 #pragma unroll
@@ -145,6 +161,7 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
             for (int j = 0; j < 8; ++j)
                 z[j] = (bf16)fmaxf(fmaf(sc[kc + j], (float)pre[c][j], sh[kc + j]), 0.f);
             *reinterpret_cast<bf16x8*>(&As[row * LDK + kc]) = z;
+            if (stats) *reinterpret_cast<bf16x8*>(&Ys[row * LDK + kc]) = pre[c];
         }
         __syncthreads();
         if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);   // in flight below
@@ -204,7 +221,14 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     const int row = rb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                    p.dz[(row0 + row) * K + k] = (bf16)acc[i];
+                    const bf16 dzb = (bf16)acc[i];
+                    p.dz[(row0 + row) * K + k] = dzb;
+                    if (stats) {   // bn_relu_bwd pass 0 on the stored values
+                        const float yy = (float)Ys[row * LDK + k];
+                        const float dt = fmaf(sc[k], yy, sh[k]) > 0.f ? (float)dzb : 0.f;
+                        st1[kb] += dt;
+                        st2[kb] = fmaf(dt, (yy - mu[kb]) * istd[kb], st2[kb]);
+                    }
                 }
             }
         }
@@ -222,6 +246,18 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
             }
         }
         __syncthreads();   // As / Ds are rewritten by the next tile
+    }
+    if (stats) {   // both lane halves hold the same channel
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+            const double s1 = (double)st1[kb] + (double)__shfl_xor(st1[kb], 32);
+            const double s2 = (double)st2[kb] + (double)__shfl_xor(st2[kb], 32);
+            if (h == 0) {
+                const int k = wave * (K / 4) + kb * 32 + r32;
+                p.stats[(size_t)blockIdx.x * 2 * K + k] = s1;
+                p.stats[(size_t)blockIdx.x * 2 * K + K + k] = s2;
+            }
+        }
     }
     // this workgroup's dW3 partial: element (a, b, i) = dW[n][k],
     // n = wave*(N/4) + 32a + (i&3) + 8(i>>2) + 4h, k = 32b + r32
@@ -244,13 +280,14 @@ extern "C" int ov3d_sa_dy_fused_supported(int K, int N) { return K == 128 && N =
 extern "C" int ov3d_sa_dy_fused(const void* yprev, const float* scale, const float* shift,
                                 const void* W, int R, int K, int N, int S, const float* gsel,
                                 const uint8_t* isel, const float* cA, const float* cB,
-                                const float* cC, void* dz, float* dwpart, int nwg, void* stream) {
+                                const float* cC, void* dz, float* dwpart, const float* mean,
+                                const float* invstd, double* stats, int nwg, void* stream) {
     if (!ov3d_sa_dy_fused_supported(K, N) || R <= 0 || R % kTile || (S != 32 && S != 64) ||
         !yprev || !scale || !shift || !W || !gsel || !isel || !cA || !cB || !cC || !dz ||
-        !dwpart || nwg <= 0)
+        !dwpart || nwg <= 0 || (stats && (!mean || !invstd)))
         return OV3D_EINVAL;
     DyFusedArgs a{(const bf16*)yprev, scale, shift, (const bf16*)W, R, S, gsel, isel, cA, cB, cC,
-                  (bf16*)dz, dwpart};
+                  (bf16*)dz, dwpart, mean, invstd, stats};
     hipLaunchKernelGGL((sa_dy_fused_kernel<128, 256>), dim3(nwg), dim3(kThreads), 0,
                        ov3d_stream(stream), a);
     OV3D_LAUNCH_CHECK();

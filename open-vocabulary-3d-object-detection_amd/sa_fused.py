@@ -205,8 +205,10 @@ class _SAMLPPool(Function):
             nwg = min(NWG_DY_FUSED, R // 64)
             dz2 = torch.empty((R, c2), dtype=bf, device=dev)
             part = torch.empty((nwg, c3, c2), dtype=torch.float32, device=dev)
+            # + layer 2's ReLU + BN backward partials (the stats pass over dz2 and y2)
+            parts2 = torch.empty((nwg, 2, c2), dtype=torch.float64, device=dev)
             nat.call("ov3d_sa_dy_fused", y2, a2, s2, w3b, R, c2, c3, S, gsel, isel, cA, cB, cC, dz2,
-                     part, nwg, like=dout)
+                     part, m2, i2, parts2, nwg, like=dout)
             dw3 = part.sum(0)
             del part
         else:
@@ -216,12 +218,16 @@ class _SAMLPPool(Function):
             dw3 = weight_grad(dy3, z2)
             dz2 = torch.mm(dy3, w3b)
             del dy3
-        # layer 2: ReLU + BN backward (two row passes), dz1 and dW2
-        parts = torch.empty((NPARTS_ROWS, 2, c2), dtype=torch.float64, device=dev)
-        nat.call("ov3d_bn_relu_bwd", 0, dz2, y2, a2, s2, m2, i2, None, None, None, None, R, c2, parts,
-                 None, NPARTS_ROWS, like=dout)
-        cA, cB, cC, dg2, db2 = bn_bwd_affine(parts, NPARTS_ROWS, c2, groups[1], R * world[1], g2,
-                                             m2, i2)
+        # layer 2: ReLU + BN backward (stats pass, unless done by the fused kernel; apply
+        # pass), dz1 and dW2
+        if fused_bwd:
+            parts, nparts = parts2, nwg
+        else:
+            parts, nparts = torch.empty((NPARTS_ROWS, 2, c2), dtype=torch.float64, device=dev), \
+                NPARTS_ROWS
+            nat.call("ov3d_bn_relu_bwd", 0, dz2, y2, a2, s2, m2, i2, None, None, None, None, R, c2,
+                     parts, None, NPARTS_ROWS, like=dout)
+        cA, cB, cC, dg2, db2 = bn_bwd_affine(parts, nparts, c2, groups[1], R * world[1], g2, m2, i2)
         dy2 = torch.empty((R, c2), dtype=bf, device=dev)
         nat.call("ov3d_bn_relu_bwd", 1, dz2, y2, a2, s2, None, None, cA, cB, cC, None, R, c2, None,
                  dy2, NPARTS_ROWS, like=dout)
