@@ -7,8 +7,10 @@
 //     z   = relu(a2*y2 + b2)            (layer 2's folded BN, bf16)   -> LDS
 //     y3  = z W3^T                      (MFMA 32x32x16, recomputed)
 //     dy3 = cA*g + cB*y3 + cC           (BN backward of the pooled layer; g = the pooled
-//                                        gradient at its arg row)     -> LDS (bf16)
-//     dz  = dy3 W3                      (MFMA, W3^T fragments)         -> HBM (R, 128) bf16
+//                                        gradient at its arg row)     -> LDS (bf16), stored
+//                                        transposed [n][row] (8-byte LDS stores)
+//     dz^T = W3^T dy3^T                 (MFMA, W3^T fragments: a lane holds 4 consecutive
+//                                        channels of a row -> 8-byte stores) -> HBM (R, 128)
 //     dW3 += dy3^T z                    (MFMA on ds_read_b64_tr_b16 reads of both LDS tiles,
 //                                        accumulated over the workgroup's tiles)
 //   dW3 partials per workgroup (fixed order), summed by the caller.
@@ -69,10 +71,10 @@ __device__ __forceinline__ bf16x8 col_operand(const bf16* T, int ld, int lane, i
     return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-template <int K, int N>
+template <int K, int N, bool STATS>
 __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p) {
     constexpr int LDK = K + 8;        // padded LDS rows (bf16)
-    constexpr int LDN = N + 8;
+    constexpr int LDR = kTile + 8;    // DsT row: one channel n, the tile's 64 rows
     constexpr int NB = N / 128;       // y3: 32-column blocks per wave (a wave owns N/4 columns)
     constexpr int KS = K / 16;        // y3: k-steps
     constexpr int KB = K / 128;       // dz: 32-column blocks per wave (a wave owns K/4 columns)
@@ -81,14 +83,17 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
     constexpr int WK = K / 32;        // dW: 32-column blocks (all K)
     static_assert(N % 128 == 0 && K % 128 == 0, "tile shape");
     __shared__ __attribute__((aligned(16))) bf16 As[kTile * LDK];
-    __shared__ __attribute__((aligned(16))) bf16 Ds[kTile * LDN];
-    __shared__ __attribute__((aligned(16))) bf16 Ys[kTile * LDK];   // raw y2 (stats only)
-    __shared__ float sc[K], sh[K];
+    __shared__ __attribute__((aligned(16))) bf16 DsT[N * LDR];        // dy3 transposed
+    __shared__ __attribute__((aligned(16))) bf16 Ys[STATS ? kTile * LDK : 8];   // raw y2 (stats)
+    __shared__ float sc[K], sh[K], smu[K], sis[K];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r32 = lane & 31, h = lane >> 5;
 
+    constexpr bool stats = STATS;
     for (int k = tid; k < K; k += kThreads) {
         sc[k] = p.scale[k];
         sh[k] = p.shift[k];
+        smu[k] = stats ? p.mean[k] : 0.f;
+        sis[k] = stats ? p.invstd[k] : 0.f;
     }
     // W3 fragments for y3 = z W3^T: lane row n, 8 consecutive k
     bf16x8 bfrag[NB][KS];
@@ -99,7 +104,8 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
         for (int s = 0; s < KS; ++s)
             bfrag[cb][s] = *reinterpret_cast<const bf16x8*>(p.W + (size_t)n * K + 16 * s + 8 * h);
     }
-    // W3^T fragments for dz = dy3 W3: lane column k, 8 consecutive n (gathered once)
+    // W3^T fragments for dz^T = W3^T dy3^T: lane row k, 8 channels n in the row order of
+    // col_operand (16s + 8(j>>2) + 4h + (j&3)); gathered once
     bf16x8 wt[KB][NS];
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
@@ -107,7 +113,8 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
 #pragma unroll
         for (int s = 0; s < NS; ++s)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) wt[kb][s][j] = p.W[(size_t)(16 * s + 8 * h + j) * K + k];
+            for (int j = 0; j < 8; ++j)
+                wt[kb][s][j] = p.W[(size_t)(16 * s + 8 * (j >> 2) + 4 * h + (j & 3)) * K + k];
     }
     float cA[NB], cB[NB], cC[NB];
 #pragma unroll
@@ -117,15 +124,12 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
         cB[cb] = p.cB[n];
         cC[cb] = p.cC[n];
     }
-    const bool stats = p.stats != nullptr;
-    float mu[KB], istd[KB], st1[KB], st2[KB];
+    // stats: a lane's 16 channels kb*32 + 8g + 4h + j (g, j < 4), summed over its rows
+    float st1[KB][STATS ? 16 : 1], st2[KB][STATS ? 16 : 1];
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb) {
-        const int k = wave * (K / 4) + kb * 32 + r32;
-        mu[kb] = stats ? p.mean[k] : 0.f;
-        istd[kb] = stats ? p.invstd[k] : 0.f;
-        st1[kb] = st2[kb] = 0.f;
-    }
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int i = 0; i < (STATS ? 16 : 1); ++i) st1[kb][i] = st2[kb][i] = 0.f;
     f32x16 dw[WN][WK];
 #pragma unroll
     for (int a = 0; a < WN; ++a)
@@ -161,7 +165,7 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
             for (int j = 0; j < 8; ++j)
                 z[j] = (bf16)fmaxf(fmaf(sc[kc + j], (float)pre[c][j], sh[kc + j]), 0.f);
             *reinterpret_cast<bf16x8*>(&As[row * LDK + kc]) = z;
-            if (stats) *reinterpret_cast<bf16x8*>(&Ys[row * LDK + kc]) = pre[c];
+            if constexpr (STATS) *reinterpret_cast<bf16x8*>(&Ys[row * LDK + kc]) = pre[c];
         }
         __syncthreads();
         if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);   // in flight below
@@ -193,41 +197,52 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
                     const int sel = p.isel[pc] + (p.S == 64 ? 0 : 32 * rb);
                     const float g = p.gsel[pc];
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const int row = rb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                        const float y = (float)(bf16)acc[rb][cb][i];
-                        const float gi = row == sel ? g : 0.f;
-                        Ds[row * LDN + n] = (bf16)fmaf(cA[cb], gi, fmaf(cB[cb], y, cC[cb]));
+                    for (int q = 0; q < 4; ++q) {   // rows rb*32 + 8q + 4h + (0..3)
+                        bf16x4 d4;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int row = rb * 32 + 8 * q + 4 * h + j;
+                            const float y = (float)(bf16)acc[rb][cb][4 * q + j];
+                            const float gi = row == sel ? g : 0.f;
+                            d4[j] = (bf16)fmaf(cA[cb], gi, fmaf(cB[cb], y, cC[cb]));
+                        }
+                        *reinterpret_cast<bf16x4*>(&DsT[n * LDR + rb * 32 + 8 * q + 4 * h]) = d4;
                     }
                 }
             }
         }
         __syncthreads();
 
-        // dz = dy3 W3 -> HBM
+        // dz^T = W3^T dy3^T -> HBM: lane = row rb*32 + r32, channels kbase + 8g + 4h + (0..3)
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {
-            const int k = wave * (K / 4) + kb * 32 + r32;
+            const int kbase = wave * (K / 4) + kb * 32;
 #pragma unroll
             for (int rb = 0; rb < 2; ++rb) {
                 f32x16 acc;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) acc[i] = 0.f;
 #pragma unroll
-                for (int s = 0; s < NS; ++s) {
-                    const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Ds[(rb * 32 + r32) * LDN + 16 * s + 8 * h]);
-                    acc = mfma(a, wt[kb][s], acc);
-                }
+                for (int s = 0; s < NS; ++s)
+                    acc = mfma(wt[kb][s], col_operand(DsT, LDR, lane, rb * 32, s), acc);
+                const int row = rb * 32 + r32;
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int row = rb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                    const bf16 dzb = (bf16)acc[i];
-                    p.dz[(row0 + row) * K + k] = dzb;
-                    if (stats) {   // bn_relu_bwd pass 0 on the stored values
-                        const float yy = (float)Ys[row * LDK + k];
-                        const float dt = fmaf(sc[k], yy, sh[k]) > 0.f ? (float)dzb : 0.f;
-                        st1[kb] += dt;
-                        st2[kb] = fmaf(dt, (yy - mu[kb]) * istd[kb], st2[kb]);
+                for (int g = 0; g < 4; ++g) {
+                    const int k = kbase + 8 * g + 4 * h;
+                    bf16x4 o;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) o[j] = (bf16)acc[4 * g + j];
+                    *reinterpret_cast<bf16x4*>(p.dz + (row0 + row) * K + k) = o;
+                    if constexpr (STATS) {   // bn_relu_bwd pass 0 on the stored values
+                        const bf16x4 y4 = *reinterpret_cast<const bf16x4*>(&Ys[row * LDK + k]);
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const float yy = (float)y4[j];
+                            const float dt = fmaf(sc[k + j], yy, sh[k + j]) > 0.f ? (float)o[j] : 0.f;
+                            st1[kb][4 * g + j] += dt;
+                            st2[kb][4 * g + j] = fmaf(dt, (yy - smu[k + j]) * sis[k + j],
+                                                      st2[kb][4 * g + j]);
+                        }
                     }
                 }
             }
@@ -240,24 +255,34 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
             for (int b = 0; b < WK; ++b) bz[b] = col_operand(As, LDK, lane, 32 * b, s);
 #pragma unroll
             for (int a = 0; a < WN; ++a) {
-                const bf16x8 ad = col_operand(Ds, LDN, lane, wave * (N / 4) + 32 * a, s);
+                // dy3^T rows of channel n, rows in col_operand's order
+                const bf16* dn = DsT + (wave * (N / 4) + 32 * a + r32) * LDR + 16 * s + 4 * h;
+                const bf16x4 lo = *reinterpret_cast<const bf16x4*>(dn);
+                const bf16x4 hi = *reinterpret_cast<const bf16x4*>(dn + 8);
+                const bf16x8 ad = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
                 for (int b = 0; b < WK; ++b) dw[a][b] = mfma(ad, bz[b], dw[a][b]);
             }
         }
         __syncthreads();   // As / Ds are rewritten by the next tile
     }
-    if (stats) {   // both lane halves hold the same channel
+    if constexpr (STATS) {   // sum each channel over the 32 lanes (rows) of its lane half
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
-            const double s1 = (double)st1[kb] + (double)__shfl_xor(st1[kb], 32);
-            const double s2 = (double)st2[kb] + (double)__shfl_xor(st2[kb], 32);
-            if (h == 0) {
-                const int k = wave * (K / 4) + kb * 32 + r32;
-                p.stats[(size_t)blockIdx.x * 2 * K + k] = s1;
-                p.stats[(size_t)blockIdx.x * 2 * K + K + k] = s2;
+        for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                double s1 = (double)st1[kb][i], s2 = (double)st2[kb][i];
+#pragma unroll
+                for (int o = 16; o > 0; o >>= 1) {
+                    s1 += __shfl_xor(s1, o, 64);
+                    s2 += __shfl_xor(s2, o, 64);
+                }
+                if (r32 == 0) {
+                    const int k = wave * (K / 4) + kb * 32 + 8 * (i >> 2) + 4 * h + (i & 3);
+                    p.stats[(size_t)blockIdx.x * 2 * K + k] = s1;
+                    p.stats[(size_t)blockIdx.x * 2 * K + K + k] = s2;
+                }
             }
-        }
     }
     // this workgroup's dW3 partial: element (a, b, i) = dW[n][k],
     // n = wave*(N/4) + 32a + (i&3) + 8(i>>2) + 4h, k = 32b + r32
@@ -288,8 +313,12 @@ extern "C" int ov3d_sa_dy_fused(const void* yprev, const float* scale, const flo
         return OV3D_EINVAL;
     DyFusedArgs a{(const bf16*)yprev, scale, shift, (const bf16*)W, R, S, gsel, isel, cA, cB, cC,
                   (bf16*)dz, dwpart, mean, invstd, stats};
-    hipLaunchKernelGGL((sa_dy_fused_kernel<128, 256>), dim3(nwg), dim3(kThreads), 0,
-                       ov3d_stream(stream), a);
+    if (stats)
+        hipLaunchKernelGGL((sa_dy_fused_kernel<128, 256, true>), dim3(nwg), dim3(kThreads), 0,
+                           ov3d_stream(stream), a);
+    else
+        hipLaunchKernelGGL((sa_dy_fused_kernel<128, 256, false>), dim3(nwg), dim3(kThreads), 0,
+                           ov3d_stream(stream), a);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

@@ -39,6 +39,7 @@ NPARTS_POOL = 256
 # last layer's backward in one pass (csrc/sa_bwd.hip): one persistent workgroup per CU
 FUSED_BWD = os.environ.get("OV3D_SA_FUSED_BWD", "1") != "0"
 NWG_DY_FUSED = 256
+FUSED_STATS = os.environ.get("OV3D_SA_FUSED_STATS", "1") != "0"   # + layer 2's BN-bwd stats
 
 
 def _bn(layer):
@@ -201,12 +202,14 @@ class _SAMLPPool(Function):
                  like=dout)
         cA, cB, cC, dg3, db3 = bn_bwd_affine(parts, NPARTS_POOL, c3, groups[2], R * world[2], g3,
                                              m3, i3)
+        parts2 = None
         if fused_bwd:   # dy3 -> dz2 and dW3 inside one pass (csrc/sa_bwd.hip)
             nwg = min(NWG_DY_FUSED, R // 64)
             dz2 = torch.empty((R, c2), dtype=bf, device=dev)
             part = torch.empty((nwg, c3, c2), dtype=torch.float32, device=dev)
             # + layer 2's ReLU + BN backward partials (the stats pass over dz2 and y2)
-            parts2 = torch.empty((nwg, 2, c2), dtype=torch.float64, device=dev)
+            parts2 = torch.empty((nwg, 2, c2), dtype=torch.float64, device=dev) \
+                if FUSED_STATS else None
             nat.call("ov3d_sa_dy_fused", y2, a2, s2, w3b, R, c2, c3, S, gsel, isel, cA, cB, cC, dz2,
                      part, m2, i2, parts2, nwg, like=dout)
             dw3 = part.sum(0)
@@ -220,7 +223,7 @@ class _SAMLPPool(Function):
             del dy3
         # layer 2: ReLU + BN backward (stats pass, unless done by the fused kernel; apply
         # pass), dz1 and dW2
-        if fused_bwd:
+        if fused_bwd and parts2 is not None:
             parts, nparts = parts2, nwg
         else:
             parts, nparts = torch.empty((NPARTS_ROWS, 2, c2), dtype=torch.float64, device=dev), \
