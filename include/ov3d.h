@@ -150,6 +150,16 @@ int ov3d_sa_layer_dy(const void* yprev, const float* scale, const float* shift, 
  * sum dt * (yprev - mean) * invstd with dt = (scale*yprev + shift > 0) * dz), the pass 0
  * of ov3d_bn_relu_bwd on the dz written. */
 int ov3d_sa_dy_fused_supported(int K, int N);
+/* The middle layer's backward in one pass (csrc/sa_bwd.hip): from dz2 and the layer-2 BN
+ * backward coefficients: dy2 = cA*dt + cB*y2 + cC (dt = (a2*y2 + b2 > 0) * dz2), z1 =
+ * relu(a1*y1 + b1) recomputed; writes dz1 = dy2 W2 (R, K) bf16, dW2 = dy2^T z1 partials
+ * dwpart (nwg, N, K) and layer 1's ReLU + BN backward partials stats (2*nwg, 2, K) (sum dt1,
+ * sum dt1 * (y1 - mean1) * invstd1 on the stored dz1).  K = 64, N = 128. */
+int ov3d_sa_dy2_fused(const void* y1, const float* a1, const float* b1, const void* y2,
+                      const float* a2, const float* b2, const void* dz2, const float* cA,
+                      const float* cB, const float* cC, const void* W, const float* mean1,
+                      const float* invstd1, int R, int K, int N, void* dz1, float* dwpart,
+                      double* stats, int nwg, void* stream);
 int ov3d_sa_dy_fused(const void* yprev, const float* scale, const float* shift, const void* W,
                      int R, int K, int N, int S, const float* gsel, const uint8_t* isel,
                      const float* cA, const float* cB, const float* cC, void* dz, float* dwpart,

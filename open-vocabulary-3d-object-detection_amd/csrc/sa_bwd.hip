@@ -298,6 +298,176 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
             }
 }
 
+// The middle layer's backward in one pass (sa_dy2_fused_kernel), after the pooled layer's
+// (which produced dz2 and this layer's BN-backward coefficients cA2 / cB2 / cC2):
+//   per 64-row tile:  z1 = relu(a1*y1 + b1) -> LDS (and raw y1 for the statistics)
+//                     dy2 = cA2*dt + cB2*y2 + cC2, dt = (a2*y2 + b2 > 0) * dz2 -> LDS
+//                     dz1^T = W2^T dy2^T (MFMA) -> HBM (R, K) bf16, 8-byte stores
+//                     layer 1's ReLU + BN backward partials on the stored dz1
+//                     dW2 += dy2^T z1 (MFMA on transposed LDS reads), per workgroup
+// replacing the ReLU+BN apply pass (dy2 stored), a dW2 GEMM, a dgrad GEMM and the layer-1
+// statistics pass.  K = 64 (layer-1 channels), N = 128 (layer-2 channels).
+struct Dy2Args {
+    const bf16* y1; const float* a1; const float* b1;    // (R, K), layer-1 folded BN
+    const bf16* y2; const float* a2; const float* b2;    // (R, N), layer-2 folded BN
+    const bf16* dz2;                                     // (R, N)
+    const float* cA; const float* cB; const float* cC;   // (N) layer-2 BN backward
+    const bf16* W;                                       // (N, K) W2
+    const float* mean1; const float* invstd1;            // (K)
+    int R;
+    bf16* dz1;          // (R, K)
+    float* dwpart;      // (gridDim.x, N, K)
+    double* stats;      // (gridDim.x, 2, K)
+};
+
+template <int K, int N>
+__global__ __launch_bounds__(kThreads, 1) void sa_dy2_fused_kernel(Dy2Args p) {
+    static_assert(K == 64 && N == 128, "4 waves = 2 x 2 dz tiles, 32 dW rows each");
+    constexpr int LDK = K + 8, LDN = N + 8;
+    __shared__ __attribute__((aligned(16))) bf16 As[kTile * LDK];   // z1
+    __shared__ __attribute__((aligned(16))) bf16 Ys[kTile * LDK];   // raw y1
+    __shared__ __attribute__((aligned(16))) bf16 Ds[kTile * LDN];   // dy2, row-major
+    __shared__ float a1s[K], b1s[K], mus[K], iss[K], a2s[N], b2s[N], cAs[N], cBs[N], cCs[N];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r32 = lane & 31, h = lane >> 5;
+    for (int k = tid; k < K; k += kThreads) {
+        a1s[k] = p.a1[k];
+        b1s[k] = p.b1[k];
+        mus[k] = p.mean1[k];
+        iss[k] = p.invstd1[k];
+    }
+    for (int n = tid; n < N; n += kThreads) {
+        a2s[n] = p.a2[n];
+        b2s[n] = p.b2[n];
+        cAs[n] = p.cA[n];
+        cBs[n] = p.cB[n];
+        cCs[n] = p.cC[n];
+    }
+    // dz1^T tile of this wave: channels kbase .. +31, rows rb*32 .. +31
+    const int kbase = (wave & 1) * 32, rb = wave >> 1;
+    constexpr int NS = N / 16;
+    bf16x8 wt[NS];   // W2^T: lane row k = kbase + r32, channels 16s + 8h + j
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) wt[s][j] = p.W[(size_t)(16 * s + 8 * h + j) * K + kbase + r32];
+    f32x16 dw[2];    // dW2 rows wave*32 .. +31, columns 0..31 / 32..63
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dw[b][i] = 0.f;
+    float st1[16], st2[16];   // channels kbase + 8g + 4h + j of this lane's rows
+#pragma unroll
+    for (int i = 0; i < 16; ++i) st1[i] = st2[i] = 0.f;
+    __syncthreads();
+
+    const int ntiles = p.R / kTile;
+    constexpr int C1 = kTile * K / 8 / kThreads;   // 16-byte chunks per thread: y1
+    constexpr int C2 = kTile * N / 8 / kThreads;   // y2, dz2
+    bf16x8 py1[C1], py2[C2], pdz[C2];
+    auto fetch = [&](int tile) {
+        const size_t row0 = (size_t)tile * kTile;
+#pragma unroll
+        for (int c = 0; c < C1; ++c) {
+            const int ch = tid + c * kThreads, row = ch / (K / 8), kc = (ch % (K / 8)) * 8;
+            py1[c] = *reinterpret_cast<const bf16x8*>(p.y1 + (row0 + row) * K + kc);
+        }
+#pragma unroll
+        for (int c = 0; c < C2; ++c) {
+            const int ch = tid + c * kThreads, row = ch / (N / 8), nc = (ch % (N / 8)) * 8;
+            py2[c] = *reinterpret_cast<const bf16x8*>(p.y2 + (row0 + row) * N + nc);
+            pdz[c] = *reinterpret_cast<const bf16x8*>(p.dz2 + (row0 + row) * N + nc);
+        }
+    };
+    if (blockIdx.x < ntiles) fetch(blockIdx.x);
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const size_t row0 = (size_t)tile * kTile;
+#pragma unroll
+        for (int c = 0; c < C1; ++c) {
+            const int ch = tid + c * kThreads, row = ch / (K / 8), kc = (ch % (K / 8)) * 8;
+            bf16x8 z;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                z[j] = (bf16)fmaxf(fmaf(a1s[kc + j], (float)py1[c][j], b1s[kc + j]), 0.f);
+            *reinterpret_cast<bf16x8*>(&As[row * LDK + kc]) = z;
+            *reinterpret_cast<bf16x8*>(&Ys[row * LDK + kc]) = py1[c];
+        }
+#pragma unroll
+        for (int c = 0; c < C2; ++c) {   // bn_relu_bwd_kernel pass 1 arithmetic
+            const int ch = tid + c * kThreads, row = ch / (N / 8), nc = (ch % (N / 8)) * 8;
+            bf16x8 d;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float yy = (float)py2[c][j];
+                const float dt = fmaf(a2s[nc + j], yy, b2s[nc + j]) > 0.f ? (float)pdz[c][j] : 0.f;
+                d[j] = (bf16)fmaf(cAs[nc + j], dt, fmaf(cBs[nc + j], yy, cCs[nc + j]));
+            }
+            *reinterpret_cast<bf16x8*>(&Ds[row * LDN + nc]) = d;
+        }
+        __syncthreads();
+        if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);   // in flight below
+
+        // dz1^T = W2^T dy2^T: lane = row rb*32 + r32, channels kbase + 8g + 4h + (0..3)
+        {
+            f32x16 acc;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                const bf16x8 b = *reinterpret_cast<const bf16x8*>(&Ds[(rb * 32 + r32) * LDN + 16 * s + 8 * h]);
+                acc = mfma(wt[s], b, acc);
+            }
+            const int row = rb * 32 + r32;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int k = kbase + 8 * g + 4 * h;
+                bf16x4 o;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) o[j] = (bf16)acc[4 * g + j];
+                *reinterpret_cast<bf16x4*>(p.dz1 + (row0 + row) * K + k) = o;
+                const bf16x4 y4 = *reinterpret_cast<const bf16x4*>(&Ys[row * LDK + k]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {   // bn_relu_bwd pass 0 of layer 1
+                    const float yy = (float)y4[j];
+                    const float dt = fmaf(a1s[k + j], yy, b1s[k + j]) > 0.f ? (float)o[j] : 0.f;
+                    st1[4 * g + j] += dt;
+                    st2[4 * g + j] = fmaf(dt, (yy - mus[k + j]) * iss[k + j], st2[4 * g + j]);
+                }
+            }
+        }
+        // dW2 += dy2^T z1 over the tile's rows
+#pragma unroll
+        for (int s = 0; s < kTile / 16; ++s) {
+            const bf16x8 ad = col_operand(Ds, LDN, lane, wave * 32, s);
+#pragma unroll
+            for (int b = 0; b < 2; ++b) dw[b] = mfma(ad, col_operand(As, LDK, lane, 32 * b, s), dw[b]);
+        }
+        __syncthreads();   // As / Ys / Ds are rewritten by the next tile
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        double s1 = (double)st1[i], s2 = (double)st2[i];
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) {
+            s1 += __shfl_xor(s1, o, 64);
+            s2 += __shfl_xor(s2, o, 64);
+        }
+        if (r32 == 0) {
+            const int k = kbase + 8 * (i >> 2) + 4 * h + (i & 3);
+            // rows rb*32..: two waves (rb = 0, 1) per channel -> separate slots, summed below
+            p.stats[((size_t)blockIdx.x * 2 + rb) * 2 * K + k] = s1;
+            p.stats[((size_t)blockIdx.x * 2 + rb) * 2 * K + K + k] = s2;
+        }
+    }
+    float* out = p.dwpart + (size_t)blockIdx.x * N * K;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int n = wave * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+            out[(size_t)n * K + 32 * b + r32] = dw[b][i];
+        }
+}
+
 }  // namespace
 
 extern "C" int ov3d_sa_dy_fused_supported(int K, int N) { return K == 128 && N == 256; }
@@ -319,6 +489,23 @@ extern "C" int ov3d_sa_dy_fused(const void* yprev, const float* scale, const flo
     else
         hipLaunchKernelGGL((sa_dy_fused_kernel<128, 256, false>), dim3(nwg), dim3(kThreads), 0,
                            ov3d_stream(stream), a);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_sa_dy2_fused(const void* y1, const float* a1, const float* b1, const void* y2,
+                                 const float* a2, const float* b2, const void* dz2, const float* cA,
+                                 const float* cB, const float* cC, const void* W,
+                                 const float* mean1, const float* invstd1, int R, int K, int N,
+                                 void* dz1, float* dwpart, double* stats, int nwg, void* stream) {
+    if (K != 64 || N != 128 || R <= 0 || R % kTile || !y1 || !a1 || !b1 || !y2 || !a2 || !b2 ||
+        !dz2 || !cA || !cB || !cC || !W || !mean1 || !invstd1 || !dz1 || !dwpart || !stats ||
+        nwg <= 0)
+        return OV3D_EINVAL;
+    Dy2Args a{(const bf16*)y1, a1, b1, (const bf16*)y2, a2, b2, (const bf16*)dz2, cA, cB, cC,
+              (const bf16*)W, mean1, invstd1, R, (bf16*)dz1, dwpart, stats};
+    hipLaunchKernelGGL((sa_dy2_fused_kernel<64, 128>), dim3(nwg), dim3(kThreads), 0,
+                       ov3d_stream(stream), a);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

@@ -162,7 +162,10 @@ class _SAMLPPool(Function):
         st1 = _bn_stats(parts, NPARTS_ROWS, c1, groups[0], R * world[0], bns[0])
         # layer 2
         w2b = cast_param(w2, bf).contiguous()
-        z1 = torch.empty((R, c1), dtype=bf, device=dev)
+        # z1 is kept for the backward only when that does not recompute it (sa_dy2_fused)
+        fused_bwd2 = FUSED_BWD and c1 == 64 and c2 == 128 and \
+            bool(nat.load().ov3d_sa_dy_fused_supported(c2, w3.shape[0]))
+        z1 = None if fused_bwd2 else torch.empty((R, c1), dtype=bf, device=dev)
         y2 = torch.empty((R, c2), dtype=bf, device=dev)
         parts = torch.empty((NPARTS_LAYER, 2, c2), dtype=torch.float64, device=dev)
         nat.call("ov3d_sa_layer_fwd", y1, st1[2], st1[3], w2b, R, c1, c2, z1, y2, parts, NPARTS_LAYER,
@@ -184,14 +187,14 @@ class _SAMLPPool(Function):
         nat.call("ov3d_sa_pool_fwd", pmax, pmin, imax, imin, st3[2], st3[3], P, c3, out, ysel, isel,
                  like=x0)
         ctx.save_for_backward(x0, y1, z1, y2, z2, w2b, w3b, g1, g2, g3, ysel, isel, *st1, *st2, *st3)
-        ctx.meta = (R, S, P, c1, c2, c3, groups, world, tuple(w1.shape), fused_bwd)
+        ctx.meta = (R, S, P, c1, c2, c3, groups, world, tuple(w1.shape), fused_bwd, fused_bwd2)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         (x0, y1, z1, y2, z2, w2b, w3b, g1, g2, g3, ysel, isel,
          m1, i1, a1, s1, m2, i2, a2, s2, m3, i3, a3, s3) = ctx.saved_tensors
-        R, S, P, c1, c2, c3, groups, world, w1shape, fused_bwd = ctx.meta
+        R, S, P, c1, c2, c3, groups, world, w1shape, fused_bwd, fused_bwd2 = ctx.meta
         dev = x0.device
         bf = torch.bfloat16
         dout = dout.float().contiguous()
@@ -231,19 +234,30 @@ class _SAMLPPool(Function):
             nat.call("ov3d_bn_relu_bwd", 0, dz2, y2, a2, s2, m2, i2, None, None, None, None, R, c2,
                      parts, None, NPARTS_ROWS, like=dout)
         cA, cB, cC, dg2, db2 = bn_bwd_affine(parts, nparts, c2, groups[1], R * world[1], g2, m2, i2)
-        dy2 = torch.empty((R, c2), dtype=bf, device=dev)
-        nat.call("ov3d_bn_relu_bwd", 1, dz2, y2, a2, s2, None, None, cA, cB, cC, None, R, c2, None,
-                 dy2, NPARTS_ROWS, like=dout)
-        del dz2
-        dw2 = weight_grad(dy2, z1)
-        dz1 = torch.mm(dy2, w2b)
-        del dy2
+        if fused_bwd2:   # dy2 -> dz1, dW2 and layer 1's statistics in one pass
+            nwg2 = min(NWG_DY_FUSED, R // 64)
+            dz1 = torch.empty((R, c1), dtype=bf, device=dev)
+            part = torch.empty((nwg2, c2, c1), dtype=torch.float32, device=dev)
+            parts, nparts = torch.empty((2 * nwg2, 2, c1), dtype=torch.float64, device=dev), \
+                2 * nwg2
+            nat.call("ov3d_sa_dy2_fused", y1, a1, s1, y2, a2, s2, dz2, cA, cB, cC, w2b, m1, i1, R, c1,
+                     c2, dz1, part, parts, nwg2, like=dout)
+            dw2 = part.sum(0)
+            del dz2, part
+        else:
+            dy2 = torch.empty((R, c2), dtype=bf, device=dev)
+            nat.call("ov3d_bn_relu_bwd", 1, dz2, y2, a2, s2, None, None, cA, cB, cC, None, R, c2,
+                     None, dy2, NPARTS_ROWS, like=dout)
+            del dz2
+            dw2 = weight_grad(dy2, z1)
+            dz1 = torch.mm(dy2, w2b)
+            del dy2
+            parts, nparts = torch.empty((NPARTS_ROWS, 2, c1), dtype=torch.float64, device=dev), \
+                NPARTS_ROWS
+            nat.call("ov3d_bn_relu_bwd", 0, dz1, y1, a1, s1, m1, i1, None, None, None, None, R, c1,
+                     parts, None, NPARTS_ROWS, like=dout)
         # layer 1: ReLU + BN backward, dW1 reduced against x0 (dy1 never stored)
-        parts = torch.empty((NPARTS_ROWS, 2, c1), dtype=torch.float64, device=dev)
-        nat.call("ov3d_bn_relu_bwd", 0, dz1, y1, a1, s1, m1, i1, None, None, None, None, R, c1, parts,
-                 None, NPARTS_ROWS, like=dout)
-        cA, cB, cC, dg1, db1 = bn_bwd_affine(parts, NPARTS_ROWS, c1, groups[0], R * world[0], g1,
-                                             m1, i1)
+        cA, cB, cC, dg1, db1 = bn_bwd_affine(parts, nparts, c1, groups[0], R * world[0], g1, m1, i1)
         parts = torch.empty((NPARTS_ROWS, c1, 3), dtype=torch.float64, device=dev)
         nat.call("ov3d_bn_relu_bwd", 2, dz1, y1, a1, s1, None, None, cA, cB, cC, x0, R, c1, parts,
                  None, NPARTS_ROWS, like=dout)
