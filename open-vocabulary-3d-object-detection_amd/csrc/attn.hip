@@ -106,6 +106,9 @@ __device__ __forceinline__ uint32_t lane_xor1(uint32_t v) {
 // (log2 units): P stays <= 2^8 between rescales (cdna_hip_programming.md T13)
 constexpr float RESCALE_THR = 8.f;
 
+// split-K merges with at most this many key splits load every partial up front
+constexpr int kMaxCombine = 16;
+
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -316,8 +319,36 @@ __global__ void __launch_bounds__(256) attn_combine_kernel(AttnArgs a) {
     const int bh = w / a.Lq, q = w - bh * a.Lq;
     const int b = bh / a.H, hh = bh - b * a.H;
     float M = -INFINITY;
-    for (int s = 0; s < a.nsplit; ++s) M = fmaxf(M, a.part_ml[2 * (((size_t)s * BH + bh) * a.Lq + q)]);
     float L = 0.f, acc = 0.f;
+    if (a.nsplit <= kMaxCombine) {
+        // every split's (m, l, o) is loaded up front: the generic loops below are 2·nsplit
+        // dependent global round trips
+        float ms[kMaxCombine], ls[kMaxCombine], os[kMaxCombine];
+#pragma unroll
+        for (int s = 0; s < kMaxCombine; ++s) {   // unpredicated loads (split clamped)
+            const int sc = s < a.nsplit ? s : a.nsplit - 1;
+            const size_t row = ((size_t)sc * BH + bh) * a.Lq + q;
+            ms[s] = a.part_ml[2 * row];
+            ls[s] = a.part_ml[2 * row + 1];
+            os[s] = a.part_o[row * D + d];
+        }
+#pragma unroll
+        for (int s = 0; s < kMaxCombine; ++s)
+            if (s >= a.nsplit) ms[s] = -INFINITY;
+#pragma unroll
+        for (int s = 0; s < kMaxCombine; ++s) M = fmaxf(M, ms[s]);
+#pragma unroll
+        for (int s = 0; s < kMaxCombine; ++s) {
+            if (ms[s] == -INFINITY) continue;
+            const float wgt = exp2f(ms[s] - M);
+            L = fmaf(ls[s], wgt, L);
+            acc = fmaf(os[s], wgt, acc);
+        }
+        a.o[((size_t)q * a.B + b) * a.so + hh * D + d] = (bf16)(L > 0.f ? acc / L : 0.f);
+        if (d == 0) a.lse[(size_t)bh * a.Lq + q] = M + log2f(L);
+        return;
+    }
+    for (int s = 0; s < a.nsplit; ++s) M = fmaxf(M, a.part_ml[2 * (((size_t)s * BH + bh) * a.Lq + q)]);
     for (int s = 0; s < a.nsplit; ++s) {
         const size_t row = ((size_t)s * BH + bh) * a.Lq + q;
         const float ms = a.part_ml[2 * row];
