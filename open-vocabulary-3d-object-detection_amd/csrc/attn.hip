@@ -134,7 +134,7 @@ __device__ __forceinline__ bf16x8 v_operand(const bf16* Vs, int lane, int dt, in
 }
 
 template <bool DROP>
-__global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
+__global__ void __launch_bounds__(256, 3) attn_fwd_kernel(AttnArgs a) {
     __shared__ __attribute__((aligned(16))) bf16 Ks[2][KB * LDK];
     __shared__ __attribute__((aligned(16))) bf16 Vs[2][KB * LDK];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -261,8 +261,9 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
                     if (DROP) {
                         const int kk = kb + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;   // even
                         const uint32_t hsh = drop_pair(qbase, (uint32_t)kk >> 1);
-                        p0 = (hsh & 0xffffu) >= a.thresh ? p0 * a.keep_scale : 0.f;
-                        p1 = (hsh >> 16) >= a.thresh ? p1 * a.keep_scale : 0.f;
+                        // 1/(1-p) is applied once to the output (keep_scale below)
+                        p0 = (hsh & 0xffffu) >= a.thresh ? p0 : 0.f;
+                        p1 = (hsh >> 16) >= a.thresh ? p1 : 0.f;
                     }
                     pf[t][i >> 3][i & 7] = (bf16)p0;
                     pf[t][i >> 3][(i & 7) + 1] = (bf16)p1;
@@ -282,7 +283,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
     const float ltot = l + __shfl_xor(l, 32);
     const int q = q0 + r;
     if (a.nsplit == 1) {
-        const float inv = ltot > 0.f ? 1.f / ltot : 0.f;
+        const float inv = ltot > 0.f ? a.keep_scale / ltot : 0.f;
         bf16* orow = a.o + ((size_t)q * a.B + b) * a.so + hh * D;
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt)
@@ -301,7 +302,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
         for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                float4 w = make_float4(o[dt][4 * g], o[dt][4 * g + 1], o[dt][4 * g + 2], o[dt][4 * g + 3]);
+                float4 w = make_float4(o[dt][4 * g] * a.keep_scale, o[dt][4 * g + 1] * a.keep_scale,
+                                       o[dt][4 * g + 2] * a.keep_scale, o[dt][4 * g + 3] * a.keep_scale);
                 *reinterpret_cast<float4*>(po + 32 * dt + 8 * g + 4 * h) = w;
             }
         if (h == 0) {
@@ -416,13 +418,23 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
     if (drop) qbase = drop_query_base(drop_head_mix(a.seed, a.site, bh), qi);
 
     bf16x8 kr[2], vr[2];
+    // row (key) r of the tile starts at r * B * s: the per-thread offsets of key tid>>3 are
+    // formed once and a tile adds kb * B * s (wave-uniform, scalar unit), so the loads carry
+    // no per-tile 64-bit vector multiplies
+    const size_t rowk = (size_t)a.B * a.sk, rowv = (size_t)a.B * a.sv;
+    const size_t k0off = (size_t)b * a.sk + hh * D + 8 * (tid & 7) + (size_t)(tid >> 3) * rowk;
+    const size_t v0off = (size_t)b * a.sv + hh * D + 8 * (tid & 7) + (size_t)(tid >> 3) * rowv;
     auto load = [&](int kb) {
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-            const int idx = tid + 256 * c, key = kb + (idx >> 3), ch = idx & 7;
-            const int kk = key < a.Lk ? key : a.Lk - 1;
-            kr[c] = *reinterpret_cast<const bf16x8*>(a.k + ((size_t)kk * a.B + b) * a.sk + hh * D + 8 * ch);
-            vr[c] = *reinterpret_cast<const bf16x8*>(a.v + ((size_t)kk * a.B + b) * a.sv + hh * D + 8 * ch);
+            const int key = kb + (tid >> 3) + 32 * c;
+            size_t ko = k0off + (size_t)(kb + 32 * c) * rowk, vo = v0off + (size_t)(kb + 32 * c) * rowv;
+            if (key >= a.Lk) {   // past the last key (partial tile): repeat the last row
+                ko -= (size_t)(key - (a.Lk - 1)) * rowk;
+                vo -= (size_t)(key - (a.Lk - 1)) * rowv;
+            }
+            kr[c] = *reinterpret_cast<const bf16x8*>(a.k + ko);
+            vr[c] = *reinterpret_cast<const bf16x8*>(a.v + vo);
         }
     };
     auto store = [&](int buf) {
@@ -472,11 +484,12 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
                     float dp0 = dpt[i], dp1 = dpt[i + 1];
                     if (drop) {
                         const uint32_t hsh = drop_pair(qbase, (uint32_t)(kb + kr0) >> 1);
-                        dp0 = (hsh & 0xffffu) >= a.thresh ? dp0 * a.keep_scale : 0.f;
-                        dp1 = (hsh >> 16) >= a.thresh ? dp1 * a.keep_scale : 0.f;
+                        dp0 = (hsh & 0xffffu) >= a.thresh ? dp0 : 0.f;
+                        dp1 = (hsh >> 16) >= a.thresh ? dp1 : 0.f;
                     }
-                    dsf[t][i >> 3][i & 7] = (bf16)(p0 * (dp0 - dsum));
-                    dsf[t][i >> 3][(i & 7) + 1] = (bf16)(p1 * (dp1 - dsum));
+                    // P (Z dP~ / (1-p) - D): the scale rides in the fma (exact for p = 0)
+                    dsf[t][i >> 3][i & 7] = (bf16)(p0 * fmaf(dp0, a.keep_scale, -dsum));
+                    dsf[t][i >> 3][(i & 7) + 1] = (bf16)(p1 * fmaf(dp1, a.keep_scale, -dsum));
                 }
             }
 #pragma unroll
@@ -654,11 +667,11 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
                         float pd = p, dp = dpt[i];
                         if (drop) {
                             const bool kp = ((r & 1) ? (hsh[j] >> 16) : (hsh[j] & 0xffffu)) >= a.thresh;
-                            pd = kp ? p * a.keep_scale : 0.f;
-                            dp = kp ? dp * a.keep_scale : 0.f;
+                            pd = kp ? p : 0.f;   // 1/(1-p) applied to dV once at the end
+                            dp = kp ? dp : 0.f;
                         }
                         pf[i >> 3][i & 7] = (bf16)pd;
-                        dsf[i >> 3][i & 7] = (bf16)(p * (dp - dv4[j]));
+                        dsf[i >> 3][i & 7] = (bf16)(p * fmaf(dp, a.keep_scale, -dv4[j]));
                     }
                 }
 #pragma unroll
@@ -686,7 +699,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 wk[j] = (bf16)(dkt[dt][4 * g + j] * A.scale);
-                wv[j] = (bf16)dvt[dt][4 * g + j];
+                wv[j] = (bf16)(dvt[dt][4 * g + j] * a.keep_scale);
             }
             *reinterpret_cast<bf16x4*>(krow + 32 * dt + 8 * g + 4 * h) = wk;
             *reinterpret_cast<bf16x4*>(vrow + 32 * dt + 8 * g + 4 * h) = wv;
