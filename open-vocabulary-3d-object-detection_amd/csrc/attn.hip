@@ -583,13 +583,21 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
     bf16x8 qr[2], dr[2];
     float lr = 0.f, dvr = 0.f;
     uint32_t zr = 0u;
+    // per-thread offsets of query row tid>>3, advanced per tile by qb * B * s (scalar unit)
+    const size_t rowq = (size_t)a.B * a.sq, rowd = (size_t)a.B * A.sdo;
+    const size_t q0off = (size_t)b * a.sq + hh * D + 8 * (tid & 7) + (size_t)(tid >> 3) * rowq;
+    const size_t d0off = (size_t)b * A.sdo + hh * D + 8 * (tid & 7) + (size_t)(tid >> 3) * rowd;
     auto load = [&](int qb) {
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-            const int idx = tid + 256 * c, qq = qb + (idx >> 3), ch = idx & 7;
-            const int qc = qq < a.Lq ? qq : a.Lq - 1;
-            qr[c] = *reinterpret_cast<const bf16x8*>(a.q + ((size_t)qc * a.B + b) * a.sq + hh * D + 8 * ch);
-            dr[c] = *reinterpret_cast<const bf16x8*>(A.dout + ((size_t)qc * a.B + b) * A.sdo + hh * D + 8 * ch);
+            const int qq = qb + (tid >> 3) + 32 * c;
+            size_t qo = q0off + (size_t)(qb + 32 * c) * rowq, dof = d0off + (size_t)(qb + 32 * c) * rowd;
+            if (qq >= a.Lq) {   // past the last query (partial tile): repeat the last row
+                qo -= (size_t)(qq - (a.Lq - 1)) * rowq;
+                dof -= (size_t)(qq - (a.Lq - 1)) * rowd;
+            }
+            qr[c] = *reinterpret_cast<const bf16x8*>(a.q + qo);
+            dr[c] = *reinterpret_cast<const bf16x8*>(A.dout + dof);
         }
         if (tid < QB) {
             const int qq = qb + tid;

@@ -33,7 +33,7 @@ _F32_OUT = None   # does this build's bmm take out_dtype=float32 for bf16 inputs
 # memory round trip per launch instead of a library GEMM's K pipeline.  Longer row blocks
 # stay on hipBLASLt, whose large tiles reuse operands across rows.
 ROWS_GEMM = True
-ROWS_GEMM_MAX_M = 2048
+ROWS_GEMM_MAX_M = int(os.environ.get("OV3D_ROWS_GEMM_MAX_M", "2048"))
 
 
 def _rows_gemm_ok(a, w, trans_b):
