@@ -541,6 +541,17 @@ int ov3d_rows_gemm_act(int M, int N, int K, const void* A, long long lda, const 
                        float dropout_p, const int64_t* seed, int site, const void* H,
                        long long ldh, void* C, long long ldc, void* stream);
 
+/* ---- long row-block GEMMs (csrc/tilegemm.hip): the encoder's nn.Linear layers ----
+ * Replaces the library GEMMs under F.linear / the input-gradient matmul of
+ * models/transformer.py:262-278 (M = batch * 2048 points).  Same contract as
+ * ov3d_rows_gemm (trans_b = 1: C = A W^T + bias; trans_b = 0: C = A W, bias NULL), with a
+ * 128 x 128 output tile per workgroup: N % 128 == 0, K % 64 == 0; 16-byte aligned A / W,
+ * lda / ldw % 8 == 0; bias (N) bf16 or NULL. */
+int ov3d_tile_gemm_supported(int M, int N, int K);
+int ov3d_tile_gemm(int M, int N, int K, const void* A, long long lda, const void* W,
+                   long long ldw, int trans_b, const void* bias, void* C, long long ldc,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -74,12 +74,14 @@ _SIGS = {
     "ov3d_bn_bwd_stats_finalize": "piidppppppppp",
     "ov3d_rows_gemm_act": "iiiplplipifpiplplp",
     "ov3d_rows_gemm_group": "iipip",
+    "ov3d_tile_gemm": "iiiplplipplp",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
                           "ov3d_wgrad_workspace", "ov3d_wgrad_tiles", "ov3d_set_loss_desc_size",
                           "ov3d_resnorm_supported", "ov3d_resnorm_bwd_parts",
                           "ov3d_adamw_chunk", "ov3d_wgrad_group_workspace",
-                          "ov3d_rows_gemm_supported", "ov3d_sa_dy_fused_supported")
+                          "ov3d_rows_gemm_supported", "ov3d_sa_dy_fused_supported",
+                          "ov3d_tile_gemm_supported")
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_longlong, "f": ctypes.c_float,
        "d": ctypes.c_double}
@@ -124,6 +126,8 @@ def load():
         lib.ov3d_sa_dy_fused_supported.restype = ctypes.c_int
         lib.ov3d_rows_gemm_supported.argtypes = [ctypes.c_int] * 3
         lib.ov3d_rows_gemm_supported.restype = ctypes.c_int
+        lib.ov3d_tile_gemm_supported.argtypes = [ctypes.c_int] * 3
+        lib.ov3d_tile_gemm_supported.restype = ctypes.c_int
         lib.ov3d_version.argtypes = []
         lib.ov3d_version.restype = ctypes.c_char_p
         _lib = lib

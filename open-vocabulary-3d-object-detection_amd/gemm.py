@@ -101,10 +101,46 @@ def _group_ok(pairs, trans_b):
             and all(_rows_gemm_ok(a, w, trans_b) for a, w in pairs))
 
 
+# Long row blocks (the encoder: batch * 2048 rows) can run on csrc/tilegemm.hip (128 x 128
+# output tiles, the W chunk staged once per workgroup).  Off by default: measured 0.4 %
+# slower per step than hipBLASLt (measured dead ends); OV3D_TILE_GEMM=1 enables it.
+TILE_GEMM = os.environ.get("OV3D_TILE_GEMM", "0") == "1"
+
+
+def _tile_gemm_ok(a, w, trans_b):
+    if not (TILE_GEMM and a.is_cuda and a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and a.dim() == 2 and w.dim() == 2 and a.stride(1) == 1 and w.stride(1) == 1):
+        return False
+    M, K = a.shape
+    N = w.shape[0] if trans_b else w.shape[1]
+    if M <= ROWS_GEMM_MAX_M or (w.shape[1] if trans_b else w.shape[0]) != K:
+        return False
+    if a.data_ptr() % 16 or w.data_ptr() % 16 or a.stride(0) % 8 or w.stride(0) % 8:
+        return False
+    from . import _native
+    return bool(_native.load().ov3d_tile_gemm_supported(M, N, K))
+
+
+def tile_gemm(a, w, bias=None, trans_b=True):
+    """as rows_gemm, on the 128 x 128-tile kernel (check _tile_gemm_ok first)"""
+    from . import _native
+    M, K = a.shape
+    N = w.shape[0] if trans_b else w.shape[1]
+    out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    if bias is not None and (bias.dtype != torch.bfloat16 or not bias.is_contiguous()):
+        bias = bias.to(torch.bfloat16).contiguous()
+    _native.call("ov3d_tile_gemm", M, N, K, a, a.stride(0), w, w.stride(0), int(trans_b), bias,
+                 out, N, like=a)
+    return out
+
+
 def _linear(x, w, b):
-    """F.linear on bf16 rows (bias in the epilogue), short row blocks on rowsgemm"""
+    """F.linear on bf16 rows (bias in the epilogue): short row blocks on rowsgemm, long ones
+    on tilegemm"""
     if _rows_gemm_ok(x, w, True):
         return rows_gemm(x, w, b, trans_b=True)
+    if _tile_gemm_ok(x, w, True):
+        return tile_gemm(x, w, b, trans_b=True)
     return torch.nn.functional.linear(x, w, b)
 
 
@@ -127,6 +163,8 @@ def _dgrad(dy, w):
     """dy (M, N) @ w (N, K) for the input gradient of a linear layer"""
     if _rows_gemm_ok(dy, w, False):
         return rows_gemm(dy, w, trans_b=False)
+    if _tile_gemm_ok(dy, w, False):
+        return tile_gemm(dy, w, trans_b=False)
     return dy @ w
 
 
