@@ -373,6 +373,10 @@ typedef struct {
     float total_w[OV3D_LOSS_NCOLS];  /* d total / d term (0 = not in the total) */
     int total_order[OV3D_LOSS_NCOLS]; int n_total;   /* summation order of the total */
     float res_scale;            /* 1 / (float)(pi / NB) */
+    const int* match_status;    /* (n_status,) ov3d_hungarian status or NULL: any nonzero
+                                 * (NaN / infeasible cost, where scipy raises) -> total = NaN,
+                                 * so engine.py's non-finite-loss exit fires */
+    int n_status;
 } ov3d_set_loss_desc;
 /* raw: (L, 9) f32 workspace (kept for the backward); ticket: one int, zero before the first
  * call (the kernel resets it); dict_out (L, 8); total: scalar */
@@ -471,7 +475,8 @@ typedef struct {
     float* param; float* grad; float* exp_avg; float* exp_avg_sq;
     void* shadow;            /* bf16 copy of param or NULL */
     long long numel;
-    float lr, weight_decay;
+    int group;               /* parameter group: row of the hyper table */
+    int reserved;
 } ov3d_adamw_tensor;
 int ov3d_adamw_chunk(void);
 /* n device-to-device copies (bytes[i] from srcs[i] to dsts[i], host arrays) in one launch
@@ -480,9 +485,13 @@ int ov3d_multi_copy(int n, const void* const* srcs, void* const* dsts, const lon
                     void* stream);
 /* table[i].grad = grads[i] (host array of device pointers) by kernel arguments: graph-safe */
 int ov3d_adamw_set_grads(ov3d_adamw_tensor* table, int ntensors, float* const* grads, void* stream);
+/* hyper: DEVICE (ngroups, 2) f64 table {lr, weight_decay} per parameter group, read by the
+ * update launch (a captured step graph follows lr schedules: the caller rewrites the table
+ * before each replay, engine.py:79 adjust_learning_rate) */
 int ov3d_adamw_step(const ov3d_adamw_tensor* table, const int* blk_t, const int* blk_c, int nblocks,
                     double* partials, float max_norm, float* step, double beta1, double beta2,
-                    float eps, double* coefs, int write_grad, float grad_scale, void* stream);
+                    float eps, double* coefs, int write_grad, float grad_scale,
+                    const double* hyper, void* stream);
 
 
 /* ---- Box parametrisation of the heads (model_3detr.py BoxProcessor + corners) ----

@@ -56,7 +56,7 @@ _SIGS = {
     "ov3d_matcher_cost": "iiiiiiplpppppffffpp",
     "ov3d_targets_prep": "iiipppppppp",
     "ov3d_set_loss_bwd": "pppppppppppp",
-    "ov3d_adamw_step": "pppipfpddfpifp",
+    "ov3d_adamw_step": "pppipfpddfpifpp",
     "ov3d_adamw_set_grads": "pipp",
     "ov3d_multi_copy": "ipppp",
     "ov3d_fourier_pe": "piipppiipp",

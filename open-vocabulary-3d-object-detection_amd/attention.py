@@ -12,8 +12,10 @@ the gradients are written into one buffer per source tensor the same way.
 
 Dropout randomness: keep(q, k) is a counter-based hash of (step seed, call site,
 b*H + h, q, k), regenerated in the backward instead of stored.  The step seed is a
-device int64 advanced once per training step (``next_step``, captured by a hipGraph
-like any other kernel), the call site is fixed per module.
+device int64 advanced once per training forward (``next_step``, captured by a hipGraph
+like any other kernel) and snapshotted for that forward; each op keeps the snapshot it
+used on its ctx, so its backward is right whatever forwards ran in between.  The call
+site is fixed per module.
 """
 import itertools
 
@@ -23,14 +25,15 @@ from . import _native
 
 HEAD_DIM = 64
 _SITES = itertools.count(1)
-_SEEDS = {}
+_SEEDS = {}     # live per-device step counter (advanced in place: graph-replay safe)
+_SNAPS = {}     # per device: the snapshot the current forward's dropout masks use
 
 
 def new_site():
     return next(_SITES)
 
 
-def _seed(device):
+def _live(device):
     t = _SEEDS.get(device)
     if t is None:
         # drawn from torch's generator (seeded per rank by the caller, main.py:415-418), and
@@ -43,9 +46,24 @@ def _seed(device):
     return t
 
 
+def _seed(device):
+    """The seed tensor of the CURRENT forward.  Every dropout site saves the object it got
+    here on its autograd ctx and its backward regenerates the masks from that object, never
+    from this function: a later forward (an EMA-teacher pass, forward-forward-backward)
+    takes a new snapshot and leaves the saved one untouched."""
+    s = _SNAPS.get(device)
+    if s is None:
+        s = _live(device).clone()
+        _SNAPS[device] = s
+    return s
+
+
 def next_step(device):
-    """Advance the dropout seed of `device` (one tiny kernel; call once per step)."""
-    _seed(device).add_(1)
+    """Advance the dropout seed of `device` and snapshot it for this forward (two tiny
+    kernels, captured by a hipGraph like any other; call once per training forward)."""
+    live = _live(device)
+    live.add_(1)
+    _SNAPS[device] = live.clone()
 
 
 def supported(q_src, embed_dim, num_heads, attn_mask):
@@ -92,6 +110,7 @@ class _Attention(torch.autograd.Function):
         if rc:
             raise _native.NativeError(f"ov3d_attn_fwd failed with status {rc}")
         ctx.save_for_backward(*srcs, o, lse)
+        ctx.seed = seed   # this forward's snapshot: the backward regenerates the same masks
         ctx.meta = (spec, dims, H, float(dropout_p), site, len(srcs))
         ctx.ext = ext
         return o
@@ -122,7 +141,7 @@ class _Attention(torch.autograd.Function):
         dvp, sdv = _rows(grads[vi], vo, E)
         rc = _native.load().ov3d_attn_bwd(
             qp, kp, vp, sq, sk, sv, _native._ptr(o), E, _native._ptr(do), E, _native._ptr(lse),
-            B, H, Lq, Lk, HEAD_DIM ** -0.5, p, _native._ptr(_seed(q.device)), site,
+            B, H, Lq, Lk, HEAD_DIM ** -0.5, p, _native._ptr(ctx.seed), site,
             _native._ptr(dvec), dqp, sdq, dkp, sdk, dvp, sdv, _native._ptr(ws), nsplit,
             _native._stream(q))
         if rc:

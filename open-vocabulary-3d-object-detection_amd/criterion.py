@@ -182,18 +182,24 @@ class SetCriterion(nn.Module):
                 align = self._alignment_batched(cat, L, B, targets, clip)
             else:
                 align = self._alignment([layer(l) for l in range(L)], targets, clip)
+        status = asg.get("status") if isinstance(asg, dict) else None
         if fused:
             return self._losses_fused(cat, L, B, final, gious, inds, mask, targets, num_boxes, align,
-                                      match_ref_order=final != 0)
-        return self._losses_torch(cat, L, B, final, aux, gious, center_dist, gt_labels, inds, mask,
-                                  targets, num_boxes, nactual_gt, align)
+                                      match_ref_order=final != 0, status=status)
+        total, loss_dict = self._losses_torch(cat, L, B, final, aux, gious, center_dist, gt_labels,
+                                              inds, mask, targets, num_boxes, nactual_gt, align)
+        if status is not None:
+            # a cost matrix scipy's linear_sum_assignment refuses (criterion.py:79 raises on
+            # NaN / -inf): the total becomes NaN so engine.py's isfinite exit fires
+            total = torch.where(status.ne(0).any(), torch.full_like(total, float("nan")), total)
+        return total, loss_dict
 
     def _dict_keys(self):
         """LOSS_KEYS present in the dict: computed terms (angle cls / reg always)"""
         return [k for k in LOSS_KEYS if k in ("loss_angle_cls", "loss_angle_reg") or self._computed(k)]
 
     def _losses_fused(self, cat, L, B, final, gious, inds, mask, targets, num_boxes, align,
-                      match_ref_order=False):
+                      match_ref_order=False, status=None):
         """all terms, the dict table and the total in one HIP launch (setloss.py)."""
         keys = self._dict_keys()
         cols = {k: setloss.COLUMNS.index(k) for k in keys}
@@ -213,7 +219,8 @@ class SetCriterion(nn.Module):
             cat("size_normalized") if "loss_size" in keys else None,
             gious if "loss_giou" in keys else None, align, inds, mask, targets,
             self.semcls_percls_weights if "loss_sem_cls" in keys else None, num_boxes,
-            dict_w, total_w, [cols[k] for k in weighted], match_ref_order=match_ref_order)
+            dict_w, total_w, [cols[k] for k in weighted], match_ref_order=match_ref_order,
+            match_status=status)
         loss_dict = {}
         for i in range(L):
             suffix = "" if i == 0 else f"_{i - 1}"

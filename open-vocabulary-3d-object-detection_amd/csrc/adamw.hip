@@ -78,13 +78,16 @@ __global__ void __launch_bounds__(kThreads) adamw_update_kernel(const ov3d_adamw
                                                                 const double* __restrict__ coefs,
                                                                 float beta2, float omb1, float omb2,
                                                                 float eps, int write_grad,
-                                                                float grad_scale) {
+                                                                float grad_scale,
+                                                                const double* __restrict__ hyper) {
     const ov3d_adamw_tensor t = T[blk_t[blockIdx.x]];
     const long long base = (long long)blk_c[blockIdx.x] * kChunk;
     const float clip = (float)coefs[0];
-    const float step_size = (float)((double)t.lr / coefs[1]);
+    // lr / weight decay of the tensor's group: Python floats (f64) in torch's AdamW
+    const double lr = hyper[2 * t.group], wd = hyper[2 * t.group + 1];
+    const float step_size = (float)(lr / coefs[1]);
     const float inv_bc2s = 1.f / (float)coefs[2];   // tensor / python float: * fp32 reciprocal
-    const float decay = (float)(1.0 - (double)t.lr * (double)t.weight_decay);
+    const float decay = (float)(1.0 - lr * wd);
 #pragma unroll 4
     for (int j = 0; j < kPer; ++j) {
         const long long e = base + j * kThreads + threadIdx.x;
@@ -140,8 +143,8 @@ extern "C" int ov3d_adamw_set_grads(ov3d_adamw_tensor* table, int ntensors, floa
 extern "C" int ov3d_adamw_step(const ov3d_adamw_tensor* table, const int* blk_t, const int* blk_c,
                                int nblocks, double* partials, float max_norm, float* step,
                                double beta1, double beta2, float eps, double* coefs, int write_grad,
-                               float grad_scale, void* stream) {
-    if (!table || !blk_t || !blk_c || nblocks <= 0 || !partials || !step || !coefs ||
+                               float grad_scale, const double* hyper, void* stream) {
+    if (!table || !blk_t || !blk_c || nblocks <= 0 || !partials || !step || !coefs || !hyper ||
         beta1 < 0.0 || beta1 >= 1.0 || beta2 < 0.0 || beta2 >= 1.0 || eps < 0.f)
         return OV3D_EINVAL;
     hipStream_t s = ov3d_stream(stream);
@@ -153,7 +156,7 @@ extern "C" int ov3d_adamw_step(const ov3d_adamw_tensor* table, const int* blk_t,
     // 1 - beta in fp64 first (Python floats in torch), then fp32
     adamw_update_kernel<<<nblocks, kThreads, 0, s>>>(table, blk_t, blk_c, coefs, (float)beta2,
                                                      (float)(1.0 - beta1), (float)(1.0 - beta2), eps,
-                                                     write_grad, grad_scale);
+                                                     write_grad, grad_scale, hyper);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

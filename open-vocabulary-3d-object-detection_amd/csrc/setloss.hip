@@ -172,6 +172,11 @@ __global__ void __launch_bounds__(kThreads) set_loss_fwd_kernel(ov3d_set_loss_de
         }
         tot = (i == 0) ? ll : tot + ll;
     }
+    if (d.match_status) {   // a matching that scipy would have refused poisons the total
+        int bad = 0;
+        for (int p = 0; p < d.n_status; ++p) bad |= d.match_status[p];
+        if (bad) tot = __int_as_float(0x7fc00000);
+    }
     *total = tot;
     *ticket = 0;
 }

@@ -85,8 +85,10 @@ class StepGraph:
     plan is computed for the NEXT batch on its own stream, concurrently with this
     batch's graph replay, and handed to the next replay (as extra model inputs).  Each
     step still samples exactly one batch; results are identical.  step(batch, next_batch) keeps the
-    pipeline primed; a batch that was not announced as `next_batch` is sampled
-    eagerly first."""
+    pipeline primed; a batch that was not announced as `next_batch` (or whose point tensor
+    was written in place after it was announced) is sampled eagerly first.  With an
+    FusedAdamW optimizer each step first writes the groups' current lr / weight decay into
+    the table the captured update reads (FusedAdamW.sync_hyper)."""
 
     def __init__(self, model, crit, opt, sample, amp_dtype=torch.bfloat16, clip=0.1,
                  warmup_iters=3, prefetch_fps=True, regionclip=None):
@@ -152,6 +154,8 @@ class StepGraph:
 
     def step(self, batch, next_batch=None):
         cur = torch.cuda.current_stream()
+        if hasattr(self.opt, "sync_hyper"):
+            self.opt.sync_hyper()   # this iteration's lr (engine.py:79) into the graph's table
         keys = list(self.static)
         srcs = [batch[k] for k in keys]
         if all(s.is_cuda and s.is_contiguous() and s.dtype == self.static[k].dtype
@@ -164,11 +168,16 @@ class StepGraph:
         if not self.prefetch:
             self.graph.replay()
             return self.loss
-        if self._expected is None or batch["point_clouds"] is not self._expected:
+        # the prefetched plan is this batch's only if the announced tensor is the same object
+        # AND was not written in place since (a loader refilling one device buffer bumps its
+        # version counter): otherwise sample it now
+        pc = batch["point_clouds"]
+        if self._expected is None or pc is not self._expected[0] or \
+                pc._version != self._expected[1]:
             self._set_plan(self._sample(self.static["point_clouds"]))
         nb = next_batch if next_batch is not None else batch
         self.next_pc.copy_(nb["point_clouds"], non_blocking=True)
-        self._expected = nb["point_clouds"]
+        self._expected = (nb["point_clouds"], nb["point_clouds"]._version)
         # the next batch's sampling plan runs on its own stream (own hardware queue),
         # concurrently with this step's graph; the graph reads plan_cur only
         self.fps_stream.wait_stream(cur)

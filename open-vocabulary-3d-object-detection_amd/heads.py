@@ -183,6 +183,7 @@ class _Heads(torch.autograd.Function):
         out_v = torch.addmm(b3v.to(bf), z2[:, :H], w3vb.t())
         out_s = torch.addmm(b3s.to(bf), z2[:, H:], w3sb.t())
         ctx.save_for_backward(xb, h1, h2, z1, z2, w1, w2, w3vb, w3sb, m1, i1, a1, s1, m2, i2, a2, s2)
+        ctx.seed = seed   # the forward's dropout snapshot (attention._seed)
         ctx.meta = (pack, float(p1), float(p2), R, x.dtype, w3s.shape)
         return out_v.float(), out_s.float()
 
@@ -195,7 +196,7 @@ class _Heads(torch.autograd.Function):
         H5 = 5 * H
         bf = torch.bfloat16
         dev = xb.device
-        seed = flash._seed(dev)
+        seed = ctx.seed
         gv = gv.to(bf).contiguous()
         gs = gs.to(bf).contiguous()
         # weight gradients: queued for the grouped launch at the end of the backward
@@ -318,6 +319,7 @@ class _BnReluRows(torch.autograd.Function):
                  shift, float(p), seed if p > 0 else None, site, z, *rowmajor, like=h)
         ctx.save_for_backward(h, gamma, mean, invstd, scale, shift)
         ctx.meta = (float(p), site)
+        ctx.seed = seed if p > 0 else None
         ctx.bn = bn
         return z
 
@@ -330,7 +332,7 @@ class _BnReluRows(torch.autograd.Function):
         dz = dz.to(torch.bfloat16).contiguous()
         rowmajor = (C, 0, C)
         hf = int(h.dtype == torch.bfloat16)
-        seed = flash._seed(dev) if p > 0 else None
+        seed = ctx.seed
         parts = torch.empty((NPARTS, 2, C), dtype=torch.float64, device=dev)
         nat.call("ov3d_rows_bn_bwd", 0, dz, *rowmajor, h, hf, *rowmajor, R, C, scale, shift, mean,
                  invstd, None, None, None, float(p), seed, site, parts, NPARTS, None, 0, 0, 8,

@@ -15,9 +15,15 @@ in the optimizer's flat buffer (``flat_grads()``) instead of ``p.grad``.
 The bf16 copies of the parameters used by the autocast GEMMs (gemm.cast_param) are
 rewritten by the same update launch, so no separate refresh copy runs.  Capturable: the
 step counter and bias corrections live on the device, the per-tensor table (parameter,
-moments, shadow, size, lr, weight decay) is built by one eager step, and the gradient
+moments, shadow, size, parameter group) is built by one eager step, and the gradient
 addresses travel as kernel arguments of ov3d_adamw_set_grads, so a step graph carries its
-own.  Learning-rate changes rebuild the table eagerly (a captured graph keeps its lr).
+own.  Each group's lr and weight decay live in a small device table (f64, as torch's
+Python floats) that the update launch reads: ``sync_hyper()`` rewrites it from
+``param_groups`` (step() does so itself when it runs eagerly; graphs.StepGraph calls it
+before every replay), so the reference's per-iteration lr schedule (engine.py:79,
+adjust_learning_rate: warmup then cosine) reaches a captured step.  Once a step has been
+captured, the table and buffers are never reallocated (a change of the parameter set
+raises instead of freeing memory the graph still uses).
 """
 import ctypes
 
@@ -32,7 +38,7 @@ class _Entry(ctypes.Structure):
     _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p),
                 ("exp_avg", ctypes.c_void_p), ("exp_avg_sq", ctypes.c_void_p),
                 ("shadow", ctypes.c_void_p), ("numel", ctypes.c_longlong),
-                ("lr", ctypes.c_float), ("weight_decay", ctypes.c_float)]
+                ("group", ctypes.c_int), ("reserved", ctypes.c_int)]
 
 
 class FusedAdamW(torch.optim.Optimizer):
@@ -52,6 +58,9 @@ class FusedAdamW(torch.optim.Optimizer):
         self.last_grad_norm = None
         self._key = None
         self._dev = None
+        self._captured = False   # a graph holds the table / buffers: never reallocate them
+        self._hyper = None       # device (ngroups, 2) f64 {lr, weight_decay}
+        self._hyper_host = None
 
     def _params(self):
         out = []
@@ -82,6 +91,7 @@ class FusedAdamW(torch.optim.Optimizer):
         """entries without the gradient pointers (set per step by ov3d_adamw_set_grads)"""
         chunk = _native.load().ov3d_adamw_chunk()
         ents, blk_t, blk_c, key = [], [], [], []
+        gid = {id(g): i for i, g in enumerate(self.param_groups)}
         for i, (p, g) in enumerate(items):
             if not (p.is_cuda and p.dtype == torch.float32 and p.grad.dtype == torch.float32
                     and p.is_contiguous() and p.grad.is_contiguous()
@@ -92,12 +102,30 @@ class FusedAdamW(torch.optim.Optimizer):
             n = p.numel()
             ents.append(_Entry(p.data_ptr(), 0, st["exp_avg"].data_ptr(),
                                st["exp_avg_sq"].data_ptr(), sh.data_ptr() if sh is not None else 0,
-                               n, float(g["lr"]), float(g["weight_decay"])))
+                               n, gid[id(g)], 0))
             nb = (n + chunk - 1) // chunk
             blk_t += [i] * nb
             blk_c += list(range(nb))
-            key.append((p.data_ptr(), ents[-1].shadow, n, float(g["lr"]), float(g["weight_decay"])))
+            key.append((p.data_ptr(), ents[-1].shadow, n, gid[id(g)]))
         return tuple(key), ents, blk_t, blk_c
+
+    def sync_hyper(self):
+        """Write every group's current lr / weight decay into the device table the update
+        launch reads (stream-ordered, no host sync; only when a value changed).  Not during
+        capture: call it before each replay of a captured step."""
+        vals = [float(v) for g in self.param_groups for v in (g["lr"], g["weight_decay"])]
+        if self._hyper is None or self._hyper.numel() != len(vals):
+            if self._captured:
+                raise RuntimeError("FusedAdamW: param groups changed after a step was captured")
+            dev = self._dev or next(p.device for g in self.param_groups for p in g["params"])
+            self._hyper = torch.empty(len(vals), dtype=torch.float64, device=dev)
+            self._hyper_host = None
+        if vals != self._hyper_host:
+            src = torch.tensor(vals, dtype=torch.float64)
+            if self._hyper.is_cuda:
+                src = src.pin_memory()
+            self._hyper.copy_(src, non_blocking=True)
+            self._hyper_host = vals
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
@@ -121,10 +149,14 @@ class FusedAdamW(torch.optim.Optimizer):
         dev = items[0][0].device
         _native.check_device(items[0][0], "FusedAdamW parameters")
         key, ents, blk_t, blk_c = self._table(items, dev)
+        capturing = torch.cuda.is_current_stream_capturing()
         if key != self._key or dev != self._dev:
-            if torch.cuda.is_current_stream_capturing():
+            if capturing:
                 raise RuntimeError("FusedAdamW: run one eager step before capturing a graph "
                                    "(the parameter table is built outside capture)")
+            if self._captured:
+                raise RuntimeError("FusedAdamW: the parameter set changed after a step was "
+                                   "captured (the graph still uses the old table)")
             raw = (_Entry * len(ents))(*ents)
             nbytes = ctypes.sizeof(raw)
             host = torch.empty(nbytes + 8 * len(blk_t), dtype=torch.uint8)
@@ -139,8 +171,9 @@ class FusedAdamW(torch.optim.Optimizer):
         if self.allreduce_group is not None:
             import torch.distributed as dist
             if getattr(self, "_flat", None) is None or self._flat_key != key:
-                if torch.cuda.is_current_stream_capturing():
-                    raise RuntimeError("FusedAdamW: run one eager step before capturing a graph")
+                if capturing or self._captured:
+                    raise RuntimeError("FusedAdamW: run one eager step before capturing a graph "
+                                       "(and never change the parameter set after it)")
                 self._flat = torch.empty(sum(p.numel() for p, _ in items), dtype=torch.float32,
                                          device=dev)
                 self._flat_key = key
@@ -155,6 +188,12 @@ class FusedAdamW(torch.optim.Optimizer):
             scale = 1.0 / dist.get_world_size(self.allreduce_group)
         else:
             grad_src = [p.grad for p, _ in items]
+        if capturing:
+            self._captured = True
+            if self._hyper is None:
+                raise RuntimeError("FusedAdamW: run one eager step before capturing a graph")
+        else:
+            self.sync_hyper()
         grads = (ctypes.c_void_p * len(items))(*[g.data_ptr() for g in grad_src])
         _native.call("ov3d_adamw_set_grads", self._buf, len(items), ctypes.addressof(grads),
                      like=self._buf)
@@ -162,7 +201,7 @@ class FusedAdamW(torch.optim.Optimizer):
         clip = float(self.max_grad_norm) if self.max_grad_norm and self.max_grad_norm > 0 else 0.0
         _native.call("ov3d_adamw_step", self._buf, idx, idx[self._nblocks:], self._nblocks,
                      self._partials, clip, self._step_t, float(b1), float(b2), float(eps),
-                     self._coefs, 1, float(scale), like=self._buf)
+                     self._coefs, 1, float(scale), self._hyper, like=self._buf)
         self.last_grad_norm = self._coefs[3]   # fp64 view (no launch)
         for p, _ in items:
             torch.autograd.graph.increment_version(p)

@@ -117,6 +117,7 @@ class _ResNorm(torch.autograd.Function):
                      seed, site, ga, ba, posr, _dt_flag(posr), gb, bb, float(eps), s, mean, rstd,
                      xa, xap, xb, like=s)
         ctx.save_for_backward(s, mean, rstd, ga, gb)
+        ctx.seed = seed   # the forward's dropout snapshot (attention._seed)
         ctx.params = (ga, ba, gb, bb)
         ctx.set_materialize_grads(False)   # unused outputs: no zero-filled gradients
         ctx.meta = (p, site, R, C, shape, src.dtype if src is not None else None,
@@ -198,7 +199,7 @@ class _ResNorm(torch.autograd.Function):
         nparts = lib.ov3d_resnorm_bwd_parts(R, C)
         partials = torch.empty((nparts, 4, C), dtype=torch.float32, device=dev) \
             if (has_a or has_b) else None
-        seed = flash._seed(dev) if (p > 0 and dy is not None) else None
+        seed = ctx.seed if (p > 0 and dy is not None) else None
         if dsrc is not None or dy is not None or dpos is not None or has_a or has_b:
             _native.call("ov3d_resnorm_bwd", R, C, s, mean, rstd, ds, dxa, dxap, dxb, *xb_map, ga, gb,
                          float(p) if dy is not None else 0.0, seed, site, dsrc, dy, _dt_flag(dy),

@@ -40,7 +40,7 @@ class Desc(ctypes.Structure):
                 ("gt_size", _P), ("nactual", _P), ("cls_weights", _P), ("num_boxes", _P),
                 ("align", _P), ("dict_w", ctypes.c_float * 8), ("total_w", ctypes.c_float * 8),
                 ("total_order", ctypes.c_int * 8), ("n_total", ctypes.c_int),
-                ("res_scale", ctypes.c_float)]
+                ("res_scale", ctypes.c_float), ("match_status", _P), ("n_status", ctypes.c_int)]
 
 
 _checked = False
@@ -136,8 +136,9 @@ class _SetLoss(torch.autograd.Function):
 
 def set_losses(L, B, Q, final_last, logits, angle_logits, angle_res, center, size, gious, align,
                inds, matched, targets, cls_weights, num_boxes, dict_w, total_w, total_order,
-               match_ref_order=False):
+               match_ref_order=False, match_status=None):
     """-> table (L, 8) of weighted values (rows in dict order), total (0-d).
+    match_status: the matcher's per-problem status (device): any nonzero -> total NaN.
 
     logits (L*B, Q, T) ..., gious (L*B, Q, G) or None, align (L,) or None, inds / matched
     (L*B, Q), dict_w / total_w: 8 floats per COLUMNS entry, total_order: column indices."""
@@ -194,6 +195,9 @@ def set_losses(L, B, Q, final_last, logits, angle_logits, angle_res, center, siz
         d.total_order[j] = k
     d.n_total = len(total_order)
     d.res_scale = _res_scale(NB)
+    if match_status is not None:
+        st = dev_t(match_status, torch.int32)
+        d.match_status, d.n_status = st.data_ptr(), st.numel()
     return _SetLoss.apply((d, keep), logits, angle_logits, angle_res, center, size, gious, align,
                           None)
 

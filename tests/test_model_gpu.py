@@ -234,3 +234,47 @@ def test_sampling_plan_inputs_give_identical_forward(cuda):
             outs.append(model({**inputs, **extra}))
     for k in ("sem_cls_logits", "center_unnormalized", "size_unnormalized", "angle_continuous"):
         assert torch.equal(outs[0]["outputs"][k], outs[1]["outputs"][k]), k
+
+
+def test_second_forward_does_not_change_first_backward(cuda):
+    """Dropout masks are regenerated in the backward from the seed SNAPSHOT the forward used
+    (attention._seed, saved on every op's ctx).  The reference's --use_pseudo_labels loop
+    runs a second train-mode forward (EMA teacher) between a forward and its backward
+    (engine.py): the first forward's gradients must equal a plain forward + backward."""
+    import ov3d_amd
+    from ov3d_amd import attention as flash
+    from ov3d_amd import synthetic
+    from ov3d_amd.dataset_config import SunrgbdDatasetConfig
+    from bench import default_args
+    args = default_args(preenc_npoints=512, nqueries=64)   # dropout ON (0.1 / 0.3)
+    cfg = SunrgbdDatasetConfig()
+    torch.manual_seed(0)
+    model, _ = ov3d_amd.build_model(args, cfg, text_embedding=synthetic.text_embedding())
+    model = model.to(cuda).train()
+    crit = ov3d_amd.build_criterion(args, cfg).to(cuda)
+    batch = synthetic.make_batch(2, seed=8, num_points=4096, device=cuda)
+    inputs = {k: batch[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")}
+    live0 = flash._live(cuda).clone()
+
+    def run(second):
+        flash._live(cuda).copy_(live0)
+        model.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model(inputs)
+            if second:   # teacher-style pass: train mode, new masks, its own graph
+                out2 = model(inputs)
+        loss, _ = crit(out, dict(batch))
+        loss.backward()
+        if second:
+            assert not torch.equal(out2["outputs"]["center_normalized"],
+                                   out["outputs"]["center_normalized"])
+        return loss.item(), {n: p.grad.float().clone() for n, p in model.named_parameters()
+                             if p.grad is not None}
+
+    l1, g1 = run(False)
+    l2, g2 = run(True)
+    assert l1 == l2
+    assert g1.keys() == g2.keys()
+    for n in g1:
+        d = (g1[n] - g2[n]).norm() / g1[n].norm().clamp_min(1e-12)
+        assert d.item() < 1e-3, (n, d.item())

@@ -115,3 +115,60 @@ def test_multi_copy_ragged(cuda):
     _native.multi_copy(dsts, srcs)
     for d, s in zip(dsts, srcs):
         assert torch.equal(d, s)
+
+
+def test_fused_adamw_graph_follows_lr_schedule(cuda):
+    """The reference changes lr every iteration (engine.py:79, warmup then cosine).  A
+    captured FusedAdamW step reads each group's lr / weight decay from a device table that
+    sync_hyper() rewrites before the replay: replays with a schedule over two parameter
+    groups equal torch.optim.AdamW stepping eagerly with the same schedule."""
+    from ov3d_amd.optim import FusedAdamW
+    pa, pb = _params(cuda, 2), _params(cuda, 2)
+    oa = FusedAdamW([{"params": pa[:4]}, {"params": pa[4:], "weight_decay": 0.0}],
+                    lr=1e-3, weight_decay=0.1, max_grad_norm=None)
+    ob = torch.optim.AdamW([{"params": pb[:4]}, {"params": pb[4:], "weight_decay": 0.0}],
+                           lr=1e-3, weight_decay=0.1, foreach=False)
+    src = [torch.zeros_like(p) for p in pa]
+
+    def body(ps, opt):
+        opt.zero_grad(set_to_none=True)
+        sum((p * s).sum() for p, s in zip(ps, src)).backward()
+        opt.step()
+
+    def set_lr(opt, lr):
+        for i, g in enumerate(opt.param_groups):
+            g["lr"] = lr * (1.0 if i == 0 else 0.5)
+
+    schedule = [1e-3, 3e-3, 7e-4, 2e-4, 5e-5]
+    for s, g in zip(src, _grads(pa, 0)):
+        s.copy_(g)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    set_lr(oa, schedule[0])
+    with torch.cuda.stream(side):
+        body(pa, oa)            # eager step builds the table
+    torch.cuda.current_stream().wait_stream(side)
+    set_lr(ob, schedule[0])
+    body(pb, ob)
+    graph = torch.cuda.CUDAGraph()
+    oa.zero_grad(set_to_none=True)
+    with torch.cuda.graph(graph):
+        body(pa, oa)
+    for k, lr in enumerate(schedule[1:], start=1):
+        for s, g in zip(src, _grads(pa, k)):
+            s.copy_(g)
+        set_lr(oa, lr)
+        oa.sync_hyper()
+        graph.replay()
+        set_lr(ob, lr)
+        body(pb, ob)
+    torch.cuda.synchronize()
+    for a, b in zip(pa, pb):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6 * b.abs().max().item()), \
+            (a - b).abs().max().item()
+    # the captured table must never be rebuilt: a new parameter set raises
+    extra = torch.nn.Parameter(torch.ones(4, device=cuda))
+    oa.add_param_group({"params": [extra]})
+    extra.grad = torch.ones_like(extra)
+    with pytest.raises(RuntimeError):
+        oa.step()

@@ -157,3 +157,23 @@ def test_matcher_cost_and_counts_match_torch(cuda):
     ref = m.cost(cat("sem_cls_prob"), cat("objectness_prob"), dist, gious,
                  batch["gt_box_sem_cls_label"].repeat(L, 1))
     assert torch.allclose(cost, ref, rtol=1e-6, atol=1e-6), (cost - ref).abs().max()
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_invalid_matching_cost_poisons_total(cuda, fused):
+    """A NaN matcher cost (scipy's linear_sum_assignment raises ValueError there,
+    criterion.py:79) must not train on silently: the device matcher reports status -1 and
+    the criterion's total becomes NaN, so engine.py's non-finite-loss exit fires.  The
+    objectness probability enters the matching cost only, so the loss terms stay finite."""
+    from ov3d_amd import synthetic
+    B, Q, L, T, NB = 2, 64, 3, 21, 12
+    st = _outputs(cuda, B, Q, L, T, NB, seed=11)
+    batch = synthetic.make_batch(B, seed=12, num_points=1024, device=cuda)
+    crit = _criterion(cuda, 0.0, 0.0)
+    ok, _, _ = _run(crit, st, batch, fused, True, None)
+    assert torch.isfinite(ok)
+    st["objectness_prob"] = st["objectness_prob"].clone()
+    st["objectness_prob"][1, 0, 5] = float("nan")
+    bad, ld, _ = _run(crit, st, batch, fused, True, None)
+    assert torch.isnan(bad)
+    assert all(torch.isfinite(v) for v in ld.values())

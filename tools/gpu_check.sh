@@ -12,7 +12,7 @@ fatal() { case "$1" in 0|1) return 1;; *) return 0;; esac; }
 echo "== smoke"; timeout -k 10 400 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
 rc=$?; tail -3 $OUT/smoke.log; [ $rc -eq 0 ] || stop smoke $rc
 
-echo "== pytest -m gpu"; timeout -k 10 1000 python -m pytest tests -m gpu -q -x > $OUT/pytest_gpu.log 2>&1
+echo "== pytest -m gpu"; timeout -k 10 1000 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 rc=$?; tail -15 $OUT/pytest_gpu.log; if fatal $rc; then stop pytest $rc; fi
 
 echo "== bench"; timeout -k 10 600 python bench.py --steps ${STEPS:-20} --warmup 5 > $OUT/bench.json 2> $OUT/bench.err
