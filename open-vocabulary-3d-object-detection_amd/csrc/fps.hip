@@ -161,39 +161,41 @@ __global__ __launch_bounds__(kThreads) void fps_global_kernel(const float* __res
 // Reductions: DPP row reductions + readlane, 32-bit keys (distance bits, then
 // min rank only when distances tie).
 template <int CTRL, int ROWS = 0xf>
-__device__ __forceinline__ int dpp_mov(int v) {
-    return __builtin_amdgcn_update_dpp(v, v, CTRL, ROWS, 0xf, false);
+__device__ __forceinline__ int dpp_mov(int v, int identity) {
+    // lanes outside the row mask read `identity`: lets the compiler fold the move into
+    // the consuming v_max/v_min (one v_max_i32_dpp per step instead of mov + max)
+    return __builtin_amdgcn_update_dpp(identity, v, CTRL, ROWS, 0xf, false);
 }
 
 // every lane of each 16-lane row gets the row's max / min
 __device__ __forceinline__ int row_max_i32(int v) {
-    v = max(v, dpp_mov<0xb1>(v));   // quad_perm(1,0,3,2)
-    v = max(v, dpp_mov<0x4e>(v));   // quad_perm(2,3,0,1)
-    v = max(v, dpp_mov<0x141>(v));  // row_half_mirror
-    v = max(v, dpp_mov<0x140>(v));  // row_mirror
+    v = max(v, dpp_mov<0xb1>(v, INT_MIN));   // quad_perm(1,0,3,2)
+    v = max(v, dpp_mov<0x4e>(v, INT_MIN));   // quad_perm(2,3,0,1)
+    v = max(v, dpp_mov<0x141>(v, INT_MIN));  // row_half_mirror
+    v = max(v, dpp_mov<0x140>(v, INT_MIN));  // row_mirror
     return v;
 }
 
 __device__ __forceinline__ uint32_t row_min_u32(uint32_t v) {
-    v = min(v, (uint32_t)dpp_mov<0xb1>((int)v));
-    v = min(v, (uint32_t)dpp_mov<0x4e>((int)v));
-    v = min(v, (uint32_t)dpp_mov<0x141>((int)v));
-    v = min(v, (uint32_t)dpp_mov<0x140>((int)v));
+    v = min(v, (uint32_t)dpp_mov<0xb1>((int)v, -1));
+    v = min(v, (uint32_t)dpp_mov<0x4e>((int)v, -1));
+    v = min(v, (uint32_t)dpp_mov<0x141>((int)v, -1));
+    v = min(v, (uint32_t)dpp_mov<0x140>((int)v, -1));
     return v;
 }
 
 // wave64 reductions: rows, then row_bcast15 / row_bcast31 fold rows into lane 63
 __device__ __forceinline__ int wave_max_i32(int v) {
     v = row_max_i32(v);
-    v = max(v, dpp_mov<0x142, 0xa>(v));  // row_bcast:15 into rows 1, 3
-    v = max(v, dpp_mov<0x143, 0xc>(v));  // row_bcast:31 into rows 2, 3
+    v = max(v, dpp_mov<0x142, 0xa>(v, INT_MIN));  // row_bcast:15 into rows 1, 3
+    v = max(v, dpp_mov<0x143, 0xc>(v, INT_MIN));  // row_bcast:31 into rows 2, 3
     return __builtin_amdgcn_readlane(v, 63);
 }
 
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     v = row_min_u32(v);
-    v = min(v, (uint32_t)dpp_mov<0x142, 0xa>((int)v));
-    v = min(v, (uint32_t)dpp_mov<0x143, 0xc>((int)v));
+    v = min(v, (uint32_t)dpp_mov<0x142, 0xa>((int)v, -1));
+    v = min(v, (uint32_t)dpp_mov<0x143, 0xc>((int)v, -1));
     return __builtin_amdgcn_readlane(v, 63);
 }
 
@@ -222,7 +224,11 @@ template <int PPT>
 __global__ __launch_bounds__(kThreads) void fps_cull_kernel(const float* __restrict__ xyz, int N,
                                                             int M, int L,
                                                             int32_t* __restrict__ idx,
-                                                            float* __restrict__ new_xyz) {
+                                                            float* __restrict__ new_xyz
+#ifdef OV3D_FPS_PROBE
+                                                            , unsigned long long* __restrict__ dbg
+#endif
+                                                            ) {
     constexpr int PW = PPT * 64;
     __shared__ uint32_t s_hist[kCells];
     __shared__ uint16_t s_perm[kThreads * PPT];
@@ -361,25 +367,43 @@ __global__ __launch_bounds__(kThreads) void fps_cull_kernel(const float* __restr
     int wpos = 0;
     float wx = 0.f, wy = 0.f, wz = 0.f;
 
+#ifdef OV3D_FPS_PROBE
+    // diagnostic build only (tools/fps_probe.py): per-wave phase cycle totals
+    unsigned long long pr_loop = 0, pr_upd = 0, pr_nupd = 0, pr_cupd = 0, pr_cnupd = 0, pr_bar = 0, pr_post = 0;
+    const unsigned long long pr_rt0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long pr_c0 = __builtin_amdgcn_s_memtime();
+#endif
     for (int j = 1; j < M; ++j) {
+#ifdef OV3D_FPS_PROBE
+        const unsigned long long pt0 = __builtin_amdgcn_s_memtime();
+        bool pr_did = false;
+#endif
         const int buf = j & 1;
         const float gx = fmaxf(fmaxf(wlo[0] - x1, x1 - whi[0]), 0.f);
         const float gy = fmaxf(fmaxf(wlo[1] - y1, y1 - whi[1]), 0.f);
         const float gz = fmaxf(fmaxf(wlo[2] - z1, z1 - whi[2]), 0.f);
         const float lb = fmaf(gz, gz, fmaf(gy, gy, gx * gx));
         if (lb < wtmax) {  // wave-uniform
+#ifdef OV3D_FPS_PROBE
+            pr_did = true;
+#endif
             float best = -1.f;
             int bi = 0;
+            float sx = 0.f, sy = 0.f, sz = 0.f;  // this lane's best point, carried along
 #pragma unroll
             for (int i = 0; i < PPT; ++i) {
                 const float dx = px[i] - x1, dy = py[i] - y1, dz = pz[i] - z1;
                 const float d = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                const float d2 = fminf(d, td[i]);
+                const float d2 = fminf(d, td[i]);  // no NaN canonicalisation: built non-IEEE (Makefile)
                 td[i] = d2;
                 const bool gt = d2 > best;
                 best = gt ? d2 : best;
                 bi = gt ? i : bi;
+                sx = gt ? px[i] : sx; sy = gt ? py[i] : sy; sz = gt ? pz[i] : sz;
             }
+#ifdef OV3D_FPS_PROBE
+            pr_loop += __builtin_amdgcn_s_memtime() - pt0;
+#endif
             const int bb = __float_as_int(best);
             const int wm = wave_max_i32(bb);
             wdist = wm;
@@ -395,17 +419,16 @@ __global__ __launch_bounds__(kThreads) void fps_cull_kernel(const float* __restr
                     const uint32_t mr = wave_min_u32(my);
                     wl = __ffsll((long long)__ballot(my == mr)) - 1;
                 }
-                const int bis = __builtin_amdgcn_readlane(bi, wl);
-                float sx = 0.f, sy = 0.f, sz = 0.f;
-#pragma unroll
-                for (int i = 0; i < PPT; ++i)
-                    if (i == bis) { sx = px[i]; sy = py[i]; sz = pz[i]; }
                 wx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sx), wl));
                 wy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sy), wl));
                 wz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sz), wl));
-                wpos = w * PW + bis * 64 + wl;
+                wpos = w * PW + __builtin_amdgcn_readlane(bi, wl) * 64 + wl;
             }
         }
+#ifdef OV3D_FPS_PROBE
+        const unsigned long long pt1 = __builtin_amdgcn_s_memtime();
+        if (pr_did) { pr_upd++; pr_cupd += pt1 - pt0; } else { pr_nupd++; pr_cnupd += pt1 - pt0; }
+#endif
         if (lane == 0) {
             s_pub[buf][w] = make_float4(wx, wy, wz, __int_as_float(wdist));
             s_pos[buf][w] = wpos;
@@ -413,23 +436,29 @@ __global__ __launch_bounds__(kThreads) void fps_cull_kernel(const float* __restr
         // only LDS is shared inside the loop: wait for LDS, not for global memory
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        const float4 v = lane < kWaves ? s_pub[buf][lane] : make_float4(0.f, 0.f, 0.f, __int_as_float(INT_MIN));
-        const int vp = lane < kWaves ? s_pos[buf][lane] : 0;
+#ifdef OV3D_FPS_PROBE
+        const unsigned long long pt2 = __builtin_amdgcn_s_memtime();
+        pr_bar += pt2 - pt1;
+#endif
+        // every row of the wave reads the 16 wave slots (lane & 15): the row reduction
+        // leaves the maximum in every lane, no lane masking
+        const float4 v = s_pub[buf][lane & (kWaves - 1)];
+        const int vp = s_pos[buf][lane & (kWaves - 1)];
         const int dv = __float_as_int(v.w);
-        const int dm = __builtin_amdgcn_readlane(row_max_i32(dv), 0);
+        const int dm = __builtin_amdgcn_readfirstlane(row_max_i32(dv));
         int pj;
         if (dm < 0) {  // no candidate anywhere: upstream keeps thread 0's besti = 0
             pj = 0xffff;
             x1 = x0; y1 = y0; z1 = z0;
         } else {
-            const unsigned long long cand = __ballot(lane < kWaves && dv == dm);
+            const unsigned long long cand = __ballot(dv == dm) & 0xffffull;
             int ws;
             if (__popcll(cand) == 1) {
                 ws = __ffsll((long long)cand) - 1;
             } else {  // distance tie across waves: smallest rank wins
-                const uint32_t r = (lane < kWaves && dv == dm) ? fps_rank(s_perm[vp], L) : 0xffffffffu;
-                const uint32_t rm = __builtin_amdgcn_readlane(row_min_u32(r), 0);
-                ws = __ffsll((long long)__ballot(r == rm && lane < kWaves)) - 1;
+                const uint32_t r = dv == dm ? fps_rank(s_perm[vp], L) : 0xffffffffu;
+                const uint32_t rm = __builtin_amdgcn_readfirstlane(row_min_u32(r));
+                ws = __ffsll((long long)(__ballot(r == rm) & 0xffffull)) - 1;
             }
             x1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.x), ws));
             y1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.y), ws));
@@ -437,7 +466,21 @@ __global__ __launch_bounds__(kThreads) void fps_cull_kernel(const float* __restr
             pj = __builtin_amdgcn_readlane(vp, ws);
         }
         if (tid == 0) s_out[j] = (uint16_t)pj;
+#ifdef OV3D_FPS_PROBE
+        pr_post += __builtin_amdgcn_s_memtime() - pt2;
+#endif
     }
+#ifdef OV3D_FPS_PROBE
+    {
+        const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+        const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            unsigned long long* o = dbg + ((size_t)b * kWaves + w) * 9;
+            o[0] = pr_upd; o[1] = pr_cupd; o[2] = pr_nupd; o[3] = pr_cnupd;
+            o[4] = pr_bar; o[5] = pr_post; o[6] = c1 - pr_c0; o[7] = rt1 - pr_rt0; o[8] = pr_loop;
+        }
+    }
+#endif
     __syncthreads();
     // ---- deferred outputs: indices + gathered coordinates, coalesced
     for (int j = tid; j < M; j += kThreads) {
@@ -452,10 +495,18 @@ __global__ __launch_bounds__(kThreads) void fps_cull_kernel(const float* __restr
     }
 }
 
+#ifdef OV3D_FPS_PROBE
+unsigned long long* g_probe_dbg = nullptr;
+#define OV3D_FPS_PROBE_ARG , g_probe_dbg
+#else
+#define OV3D_FPS_PROBE_ARG
+#endif
+
 template <int PPT>
 void launch_cull(const float* xyz, int B, int N, int M, int L, int32_t* idx, float* nx,
                  hipStream_t s) {
-    hipLaunchKernelGGL(fps_cull_kernel<PPT>, dim3(B), dim3(kThreads), 0, s, xyz, N, M, L, idx, nx);
+    hipLaunchKernelGGL(fps_cull_kernel<PPT>, dim3(B), dim3(kThreads), 0, s, xyz, N, M, L, idx, nx
+                       OV3D_FPS_PROBE_ARG);
 }
 
 }  // namespace
@@ -485,5 +536,10 @@ extern "C" int ov3d_fps(const float* xyz, int B, int N, int M, int32_t* idx_out,
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }
+
+#ifdef OV3D_FPS_PROBE
+// diagnostic entry (probe build only): dbg = B*16*9 u64 phase counters
+extern "C" void ov3d_fps_probe_set(unsigned long long* dbg) { g_probe_dbg = dbg; }
+#endif
 
 extern "C" const char* ov3d_version(void) { return "ov3d-hip 0.1 gfx950"; }
