@@ -561,6 +561,68 @@ int ov3d_tile_gemm(int M, int N, int K, const void* A, long long lda, const void
                    long long ldw, int trans_b, const void* bias, void* C, long long ldc,
                    void* stream);
 
+/* ---- SUN RGB-D training-data pipeline on the device (csrc/sunaug.hip) ----
+ * Replaces SunrgbdDetectionDataset.__getitem__ (datasets/sunrgbd.py:256-462, use_color /
+ * use_height off) for a batch of scenes resident in HBM: raw points (S, raw_stride, raw_c)
+ * of float32 (pc_f64 = 0) or float64, raw boxes (S, k_stride, 8) float64; scene_idx (B)
+ * selects the batch.  The random draws are the reference's numpy draws, made on the host
+ * (sunaug.py) and passed in:
+ *   params   (B, 8) f64: flip flag, rot_angle, cos(rot_angle), sin(rot_angle), scale_ratio
+ *   attempts (B, A, 4) f64: RandomCuboid crop_range xyz + centre index (< 0: the attempt
+ *            failed check_aspect), random_cuboid.py:45-53
+ *   choices  (B, num_points) int64: np.random.choice of random_sampling (pc_util.py:28)
+ * Entry points, in stream order:
+ *   ov3d_sun_aug_points : flip / rotz / scale of the points (sunrgbd.py:309-344) ->
+ *                         out (B, n_max, 3) T and range_part (B, ov3d_sun_range_parts(n_max), 6)
+ *   ov3d_sun_aug_boxes  : support-class filter (train, sunrgbd.py:268-270; n_support = 0 for
+ *                         val) + the same transforms of the boxes -> out (B, k_max, 8), out_n
+ *   ov3d_sun_cuboid_eval: all A attempts of RandomCuboid (min_points, box filter "center"),
+ *                         counts / accept (B, A), crop_mm (B, A, 6) T, and
+ *                         sel (B, 2) int32 = [first accepted attempt or -1, points to sample]
+ *   ov3d_sun_crop_sample: order-preserving crop (crop_idx (B, n_max)) + random_sampling gather
+ *                         -> points (B, num_points, 3) f32, dims_part (B, range_parts(num_points), 6)
+ *   ov3d_sun_labels     : box filter of the selected crop + every label tensor of the
+ *                         reference's ret_dict (sunrgbd.py:356-460). */
+int ov3d_sun_range_parts(int n);
+int ov3d_sun_aug_points(const void* raw, int pc_f64, long long raw_stride, int raw_c,
+                        const int32_t* scene_idx, const int32_t* npts, int B, int n_max,
+                        const double* params, int augment, void* out, void* range_part,
+                        void* stream);
+int ov3d_sun_aug_boxes(const double* raw, long long k_stride, const int32_t* scene_idx,
+                       const int32_t* nbox, int B, int k_max, const double* params, int augment,
+                       const double* support, int n_support, double* out, int32_t* out_n,
+                       void* stream);
+int ov3d_sun_cuboid_eval(const void* pts, int pc_f64, int n_max, const int32_t* npts,
+                         const void* range_part, const double* attempts, int B, int A,
+                         int min_points, const double* boxes, const int32_t* nbox, int k_max,
+                         int32_t* counts, void* crop_mm, int32_t* accept, int32_t* sel,
+                         void* stream);
+int ov3d_sun_crop_sample(const void* pts, int pc_f64, int n_max, const int32_t* npts,
+                         const void* range_part, const double* attempts, int B, int A,
+                         const int32_t* sel, const int64_t* choices, int num_points,
+                         int32_t* crop_idx, float* out, void* dims_part, void* stream);
+typedef struct {
+    int B, max_num_obj, k_max, num_angle_bin, num_attempts, n_dims_part;
+    const double* boxes;      /* (B, k_max, 8) augmented boxes */
+    const int32_t* nbox;      /* (B) */
+    const int32_t* sel;       /* (B, 2) of ov3d_sun_cuboid_eval, or NULL (no RandomCuboid) */
+    const void* crop_mm;      /* (B, num_attempts, 6) T */
+    const void* dims_part;    /* (B, n_dims_part, 6) T */
+    void* dims_min;           /* (B, 3) T: point_cloud_dims_min */
+    void* dims_max;           /* (B, 3) T */
+    float* corners;           /* (B, G, 8, 3) gt_box_corners */
+    float* centers;           /* (B, G, 3) gt_box_centers */
+    float* centers_normalized;/* (B, G, 3) */
+    int64_t* sem_cls;         /* (B, G) gt_box_sem_cls_label */
+    float* present;           /* (B, G) gt_box_present */
+    float* sizes;             /* (B, G, 3) gt_box_sizes */
+    float* sizes_normalized;  /* (B, G, 3) */
+    float* angles;            /* (B, G) gt_box_angles */
+    int64_t* angle_cls;       /* (B, G) gt_angle_class_label */
+    float* angle_res;         /* (B, G) gt_angle_residual_label */
+} ov3d_sun_labels_args;
+int ov3d_sun_labels(const ov3d_sun_labels_args* args, int pc_f64, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

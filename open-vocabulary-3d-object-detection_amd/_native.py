@@ -75,13 +75,18 @@ _SIGS = {
     "ov3d_rows_gemm_act": "iiiplplipifpiplplp",
     "ov3d_rows_gemm_group": "iipip",
     "ov3d_tile_gemm": "iiiplplipplp",
+    "ov3d_sun_aug_points": "pilippiipippp",
+    "ov3d_sun_aug_boxes": "plppiipipippp",
+    "ov3d_sun_cuboid_eval": "piipppiiippippppp",
+    "ov3d_sun_crop_sample": "piipppiippipppp",
+    "ov3d_sun_labels": "pip",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
                           "ov3d_wgrad_workspace", "ov3d_wgrad_tiles", "ov3d_set_loss_desc_size",
                           "ov3d_resnorm_supported", "ov3d_resnorm_bwd_parts",
                           "ov3d_adamw_chunk", "ov3d_wgrad_group_workspace",
                           "ov3d_rows_gemm_supported", "ov3d_sa_dy_fused_supported",
-                          "ov3d_tile_gemm_supported")
+                          "ov3d_tile_gemm_supported", "ov3d_sun_range_parts")
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_longlong, "f": ctypes.c_float,
        "d": ctypes.c_double}
@@ -128,6 +133,8 @@ def load():
         lib.ov3d_rows_gemm_supported.restype = ctypes.c_int
         lib.ov3d_tile_gemm_supported.argtypes = [ctypes.c_int] * 3
         lib.ov3d_tile_gemm_supported.restype = ctypes.c_int
+        lib.ov3d_sun_range_parts.argtypes = [ctypes.c_int]
+        lib.ov3d_sun_range_parts.restype = ctypes.c_int
         lib.ov3d_version.argtypes = []
         lib.ov3d_version.restype = ctypes.c_char_p
         _lib = lib
@@ -211,6 +218,22 @@ def call(name, *args, like):
         rec.append((ev0, ev1, tuple(a for a in args if isinstance(a, int))[:3]))
     if rc != 0:
         raise NativeError(f"{name} failed with status {rc}")
+
+
+class SunLabelsArgs(ctypes.Structure):
+    """ov3d_sun_labels_args (include/ov3d.h)"""
+    _fields_ = [(n, ctypes.c_int) for n in ("B", "max_num_obj", "k_max", "num_angle_bin",
+                                             "num_attempts", "n_dims_part")] + \
+               [(n, ctypes.c_void_p) for n in ("boxes", "nbox", "sel", "crop_mm", "dims_part",
+                                                "dims_min", "dims_max", "corners", "centers",
+                                                "centers_normalized", "sem_cls", "present", "sizes",
+                                                "sizes_normalized", "angles", "angle_cls",
+                                                "angle_res")]
+
+
+def byref(struct):
+    """address of a ctypes structure, for a "p" argument (the caller keeps it alive)"""
+    return ctypes.c_void_p(ctypes.addressof(struct))
 
 
 def multi_copy(dsts, srcs):

@@ -126,3 +126,28 @@ def text_embedding(num_classes=21, dim=640, seed=7):
     g = torch.Generator().manual_seed(seed)
     t = torch.randn(num_classes, dim, generator=g)
     return t / t.norm(dim=1, keepdim=True)
+
+
+def make_raw_scene(rng, num_points=50000, nobj=None, num_classes=20, dtype=np.float32):
+    """A raw SUN RGB-D v1 scan as the reference loader reads it (sunrgbd.py:260-262):
+    pc (N, 3) upright-depth points (the `_pc.npz` "pc" array, colour dropped) and bboxes
+    (K, 8) float64 [cx, cy, cz, l/2, w/2, h/2, heading, class] (the `_bbox.npy` array)."""
+    if nobj is None:
+        nobj = int(rng.integers(0, 16))
+    half = rng.uniform(0.15, 1.0, size=(nobj, 3))
+    heading = rng.uniform(-np.pi, np.pi, size=nobj)
+    centers = np.stack([rng.uniform(-2.4, 2.4, nobj), rng.uniform(1.0, 6.0, nobj), half[:, 2]], 1)
+    surf = [36.0, 18.0, 18.0] + [8 * (a * b + b * c + a * c) for a, b, c in half]
+    counts = rng.multinomial(num_points, np.array(surf) / np.sum(surf))
+    parts = [
+        np.stack([rng.uniform(-3, 3, counts[0]), rng.uniform(0.5, 6.5, counts[0]), np.zeros(counts[0])], 1),
+        np.stack([rng.uniform(-3, 3, counts[1]), np.full(counts[1], 6.5), rng.uniform(0, 3, counts[1])], 1),
+        np.stack([np.full(counts[2], -3.0), rng.uniform(0.5, 6.5, counts[2]), rng.uniform(0, 3, counts[2])], 1),
+    ]
+    for i in range(nobj):
+        parts.append(_box_surface(rng, counts[3 + i], half[i], heading[i], centers[i]))
+    pts = np.concatenate(parts, 0) + rng.normal(0, 0.01, size=(num_points, 3))
+    pc = pts[rng.permutation(num_points)].astype(dtype)
+    cls = rng.integers(0, num_classes, nobj).astype(np.float64)
+    bboxes = np.concatenate([centers, half, heading[:, None], cls[:, None]], 1)
+    return pc, bboxes
