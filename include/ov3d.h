@@ -623,6 +623,33 @@ typedef struct {
 } ov3d_sun_labels_args;
 int ov3d_sun_labels(const ov3d_sun_labels_args* args, int pc_f64, void* stream);
 
+/* ---- detection evaluation on the device (csrc/evaldet.hip) ----
+ * Replaces the CPU evaluation of utils/ap_calculator.py + utils/eval_det.py.
+ *   ov3d_box_points_count: remove_empty_box (ap_calculator.py:70-84): for every predicted box
+ *     (corners (B,K,8,3) f32, upright camera, flipped to depth as flip_axis_to_depth), the
+ *     number of scene points inside its convex hull (in_hull, box_util.py:22-31);
+ *     point (b, n) xyz at pts[b*pt_sb + n*pt_sn + 0..2] -> counts (B,K) int32
+ *   ov3d_box3d_iou_eval: box3d_iou (box_util.py:116-141) of every (prediction, GT) pair of a
+ *     scene: pred (S,K,8,3) f32 with pvalid (S,K) u8, gt (S,G,8,3) f32 with gvalid (S,G) u8
+ *     -> iou (S,K,G) f64 (0 where either is invalid)
+ *   ov3d_ap_match: eval_det_cls's TP/FP walk (eval_det.py:104-131) per (scene, class):
+ *     scores (S,K,C) f32 (-inf: not a detection of that class), gt_cls (S,G) int64 ->
+ *     tp (S,K,C) u8 (1 TP, 0 FP) for every detection; K <= 256, G <= 64
+ *   ov3d_ap_curve: voc_ap (eval_det.py:20-52, 133-146) per class from the detections' TP flags
+ *     in global descending-confidence order, tp_sorted (C, M) u8 with nvalid (C) leading
+ *     entries valid, npos (C) GT counts; tp_pos (C, tp_cap) int32 workspace
+ *     -> ap (C) f64, rec_last (C) f64 (the recall at the last detection) */
+int ov3d_box_points_count(const float* pts, long long pt_sb, long long pt_sn, int N,
+                          const float* corners, int B, int K, int32_t* counts, void* stream);
+int ov3d_box3d_iou_eval(const float* pred, const uint8_t* pvalid, const float* gt,
+                        const uint8_t* gvalid, int S, int K, int G, double* iou, void* stream);
+int ov3d_ap_match(const double* iou, const float* scores, const int64_t* gt_cls,
+                  const uint8_t* gvalid, int S, int K, int G, int C, double thresh, uint8_t* tp,
+                  void* stream);
+int ov3d_ap_curve(const uint8_t* tp_sorted, long long M, const int32_t* nvalid,
+                  const int32_t* npos, int C, int32_t* tp_pos, long long tp_cap, double* ap,
+                  double* rec_last, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

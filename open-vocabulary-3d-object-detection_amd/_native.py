@@ -80,6 +80,10 @@ _SIGS = {
     "ov3d_sun_cuboid_eval": "piipppiiippippppp",
     "ov3d_sun_crop_sample": "piipppiippipppp",
     "ov3d_sun_labels": "pip",
+    "ov3d_box_points_count": "pllipiipp",
+    "ov3d_box3d_iou_eval": "ppppiiipp",
+    "ov3d_ap_match": "ppppiiiidpp",
+    "ov3d_ap_curve": "plppiplppp",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
                           "ov3d_wgrad_workspace", "ov3d_wgrad_tiles", "ov3d_set_loss_desc_size",
