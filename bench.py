@@ -301,10 +301,10 @@ def main():
         algo_bytes = B * M * N * 16.0      # per scene M*N*(12 B coords + 4 B running min)
         achieved = algo_bytes / (avg_ms * 1e-3) / 1e9
         traffic, tsrc = None, None
-        pmc = os.path.join(ROOT, "profiles", "r01_fps_pmc.json")
+        pmc = os.path.join(ROOT, "profiles", "r02_fps_pmc.json")
         if os.path.exists(pmc) and (B, N, M) == (8, 20000, 2048):
             traffic = json.load(open(pmc))["traffic_bytes_per_launch"]
-            tsrc = "profiles/r01_fps_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, gfx950-corrected)"
+            tsrc = "profiles/r02_fps_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, gfx950-corrected)"
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
                 "kernel": "ov3d_fps (pre-encoder, B=%d N=%d M=%d)" % (B, N, M),
