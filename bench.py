@@ -32,6 +32,7 @@ import ov3d_import  # noqa: E402
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 BF16_DENSE_PEAK_TFLOPS = 2500.0
 STEP_GFLOP_PER_SCENE = 113.64  # SURVEY §8d, fwd+bwd matmul/conv FLOPs, SUN config
+SCANNET_GFLOP_PER_SCENE = 130.78
 
 
 def default_args(**kw):
@@ -57,6 +58,13 @@ def log(*a):
 WORKLOADS = {
     "sun": dict(batch=8, use_image=False, args={}),
     "sun_image": dict(batch=4, use_image=True, args=dict(loss_2dalignment_weight=2e-4)),
+    # C4 (BASELINE.json configs[3]): scripts/scannet_masked_ep1080.sh, ScanNet 40000 pts + colour
+    # (scannet.py:181), masked encoder, 256 queries, differentiable GIoU loss
+    "scannet": dict(batch=8, use_image=False, dataset="scannet", points=40000, queries=256,
+                    args=dict(enc_type="masked", enc_dropout=0.3, nqueries=256, use_color=True,
+                              base_lr=5e-4, matcher_giou_cost=2.0, matcher_cls_cost=1.0,
+                              matcher_center_cost=0.0, matcher_objectness_cost=0.0,
+                              loss_giou_weight=1.0, loss_no_object_weight=0.25)),
 }
 
 
@@ -77,15 +85,16 @@ def regionclip_gflop_per_scene(batch, nqueries=128, layers=8):
     return backbone + nqueries * layers * (res5 + pool)
 
 
-def build(args, device, ddp=False, capturable=False, sync_bn=False, allreduce=False):
+def build(args, device, ddp=False, capturable=False, sync_bn=False, allreduce=False,
+          dataset="sunrgbd"):
     """ddp: the reference's DistributedDataParallel + SyncBatchNorm (eager); sync_bn +
     allreduce: the same semantics for the captured step (SyncBatchNorm statistics
     all-reduced inside the fused BN kernels' launches, the gradient mean by ONE collective
     in FusedAdamW)."""
     ov3d = ov3d_import.load()
     from ov3d_amd import synthetic
-    from ov3d_amd.dataset_config import SunrgbdDatasetConfig
-    cfg = SunrgbdDatasetConfig()
+    from ov3d_amd.dataset_config import CONFIGS
+    cfg = CONFIGS[dataset]()
     torch.manual_seed(0)
     model, _ = ov3d.build_model(args, cfg, text_embedding=synthetic.text_embedding(cfg.num_semcls + 1))
     model = model.to(device).train()
@@ -134,7 +143,7 @@ def fps_launch_timings(pool, cli, reps=5):
     from ov3d_amd import _native, pointnet2_utils as pu
     _native.timing_enable(["ov3d_fps"])
     for i in range(reps):
-        pu.furthest_point_sample_gather(pool[i % len(pool)]["point_clouds"], 2048)
+        pu.furthest_point_sample_gather(pool[i % len(pool)]["point_clouds"][..., 0:3].contiguous(), 2048)
     return _native.timing_collect()
 
 
@@ -189,7 +198,7 @@ def main():
     p.add_argument("--workload", default="sun", choices=sorted(WORKLOADS),
                    help="sun = BASELINE metric config (C2/C3); sun_image = C5 (RegionCLIP ROI path)")
     p.add_argument("--batch", type=int, default=None, help="scenes per GPU (default: workload's)")
-    p.add_argument("--points", type=int, default=20000)
+    p.add_argument("--points", type=int, default=None, help="points per scene (default: workload's)")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled")
@@ -218,6 +227,9 @@ def main():
     wl = WORKLOADS[cli.workload]
     if cli.batch is None:
         cli.batch = wl["batch"]
+    if cli.points is None:
+        cli.points = wl.get("points", 20000)
+    dataset = wl.get("dataset", "sunrgbd")
 
     ov3d = ov3d_import.load()
     from ov3d_amd import _native, dist, synthetic
@@ -244,13 +256,14 @@ def main():
     if cli.optim != "fused" and dp:
         raise SystemExit("the captured data-parallel step needs --optim fused")
     model, crit, opt = build(args, device, ddp=world > 1 and not use_graph, capturable=use_graph,
-                             sync_bn=dp, allreduce=dp)
+                             sync_bn=dp, allreduce=dp, dataset=dataset)
     if use_graph and not cli.no_defer_wgrad:
         from ov3d_amd import gemm
         gemm.DEFER_WGRAD = True   # one grouped weight-gradient launch per backward (not under DDP)
     clip = build_regionclip(device) if wl["use_image"] else None
     pool = [synthetic.make_batch(cli.batch, seed=1000 * rank + i, num_points=cli.points, device=device,
-                                 use_image=wl["use_image"])
+                                 use_image=wl["use_image"], dataset=dataset,
+                                 use_color=bool(args.use_color))
             for i in range(cli.pool)]
 
     graphed = None
@@ -313,6 +326,11 @@ def main():
     metric = "scenes/sec (train step) SUN RGB-D 20k pts nqueries=128"
     workload = (f"SUN RGB-D train step, bs={cli.batch}/GPU, {cli.points} pts, nqueries=128, "
                 "3DETR 256-d enc3/dec8, text-emb 640, AdamW + clip 0.1")
+    if dataset == "scannet":
+        gflop_scene = SCANNET_GFLOP_PER_SCENE
+        metric = "scenes/sec (train step) ScanNet 40k pts + colour nqueries=256 masked encoder (C4)"
+        workload = (f"ScanNet train step (scannet_masked_ep1080.sh), bs={cli.batch}/GPU, {cli.points} "
+                    "pts + colour, nqueries=256, masked encoder, GIoU loss, AdamW + clip 0.1")
     if wl["use_image"]:
         gflop_scene += regionclip_gflop_per_scene(cli.batch)
         metric += " +RegionCLIP RN50x4 2D alignment (C5)"
@@ -330,10 +348,12 @@ def main():
         "step_mfma": {"achieved_tflops": round(step_tflops, 2), "peak_tflops": BF16_DENSE_PEAK_TFLOPS,
                       "frac": round(step_tflops / (world * BF16_DENSE_PEAK_TFLOPS), 5)},
     }
+    if dataset == "scannet":
+        res["data"] = "synthetic ScanNet-like scenes (numpy PCG64, axis-aligned boxes), random-init weights"
     if wl["use_image"]:
         res["cpu_baseline"] = {"value": None, "note": "not run for C5: the RN50x4 ROI path is "
                                f"{regionclip_gflop_per_scene(cli.batch) / 1e3:.1f} TFLOP/scene"}
-    elif world == 1 and not cli.no_cpu_baseline:
+    elif world == 1 and not cli.no_cpu_baseline and dataset == "sunrgbd":
         try:
             res["cpu_baseline"] = cpu_baseline(default_args())
         except Exception as e:  # report, never fake

@@ -19,6 +19,8 @@ site is fixed per module.
 """
 import itertools
 
+import os
+
 import torch
 
 from . import _native
@@ -74,6 +76,9 @@ def supported(q_src, embed_dim, num_heads, attn_mask):
 
 def _split(Lq, Lk, BH):
     """key splits so that the grid has >= ~256 workgroups (decoder: 128 queries)."""
+    force = os.environ.get("OV3D_ATTN_SPLIT")    # measurement knob (tools/attn_time.py)
+    if force:
+        return max(1, min(int(force), Lk // 64))
     wgs = ((Lq + 127) // 128) * BH
     n = 1
     while wgs * n < 256 and Lk // (n * 2) >= 128:

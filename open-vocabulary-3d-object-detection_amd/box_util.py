@@ -117,22 +117,33 @@ def giou3d_raw(corners1, corners2, nums_k2, mode, rotated, k2_bug=True):
 
 
 class _GIoUAligned(Function):
+    """differentiable GIoU (box_util.py:517-621, all K2).  `rotated` is False or the
+    criterion's device flag (any(gt_box_angles > 0)): the forward then follows it on the
+    device, and since only the axis-aligned gradient is implemented, a rotated batch gets
+    NaN gradients (the loss is finite, the step's non-finite check fires) instead of a
+    host sync that a captured step cannot make."""
+
     @staticmethod
-    def forward(ctx, corners1, corners2, nums_k2):
+    def forward(ctx, corners1, corners2, nums_k2, rotated):
         c1, c2, nums = _prep(corners1, corners2, nums_k2)
-        ctx.save_for_backward(c1, c2, nums if nums is not None else torch.empty(0))
+        flag = rotated if isinstance(rotated, torch.Tensor) else None
+        ctx.save_for_backward(c1, c2, nums if nums is not None else torch.empty(0),
+                              flag if flag is not None else torch.empty(0))
         ctx.has_nums = nums is not None
-        return giou3d_raw(c1, c2, nums, nat.OV3D_GIOU_TENSOR, False)
+        ctx.has_flag = flag is not None
+        return giou3d_raw(c1, c2, nums, nat.OV3D_GIOU_TENSOR, flag if flag is not None else False)
 
     @staticmethod
     def backward(ctx, g):
-        c1, c2, nums = ctx.saved_tensors
+        c1, c2, nums, flag = ctx.saved_tensors
         nums = nums if ctx.has_nums else None
         g = nat.check(g.float().contiguous(), "grad", torch.float32, 3)
         B, K1, K2 = g.shape
         gc1 = torch.empty_like(c1)
         nat.call("ov3d_giou3d_bwd_aligned", c1, c2, nums, B, K1, K2, g, gc1, like=g)
-        return gc1, None, None
+        if ctx.has_flag:
+            gc1 = torch.where(flag.reshape(()).bool(), torch.full_like(gc1, float("nan")), gc1)
+        return gc1, None, None, None
 
 
 def generalized_box3d_iou(corners1, corners2, nums_k2, rotated_boxes=True,
@@ -143,12 +154,11 @@ def generalized_box3d_iou(corners1, corners2, nums_k2, rotated_boxes=True,
     if return_inter_vols_only:
         raise NotImplementedError("return_inter_vols_only is not on the training path")
     if needs_grad:
-        if isinstance(rotated_boxes, torch.Tensor):
-            rotated_boxes = bool(rotated_boxes.item())    # host sync: ScanNet-style GIoU loss only
-        if rotated_boxes:
+        if not isinstance(rotated_boxes, torch.Tensor) and rotated_boxes:
             raise NotImplementedError(
                 "differentiable rotated GIoU (loss_giou_weight > 0 with rotated GT) is not "
                 "implemented yet; the reference evaluates it with a Python triple loop")
-        return _GIoUAligned.apply(corners1, corners2, nums_k2)
+        return _GIoUAligned.apply(corners1, corners2, nums_k2,
+                                  rotated_boxes if isinstance(rotated_boxes, torch.Tensor) else False)
     with torch.no_grad():
         return giou3d_raw(corners1, corners2, nums_k2, nat.OV3D_GIOU_CYTHON, rotated_boxes, k2_bug)

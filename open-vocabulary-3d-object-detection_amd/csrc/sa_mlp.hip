@@ -58,7 +58,7 @@ struct LayerArgs {
 };
 
 template <int K, int N, int MODE>
-__global__ __launch_bounds__(kThreads) void sa_layer_kernel(LayerArgs p) {
+__global__ __launch_bounds__(kThreads, 2) void sa_layer_kernel(LayerArgs p) {
     constexpr int LDK = K + 8;          // padded LDS row (bf16): spreads rows over banks
     constexpr int NB = N / 128;         // 32-column blocks per wave
     constexpr int KS = K / 16;          // MFMA k-steps

@@ -31,12 +31,17 @@ def _box_surface(rng, n, half, heading, center):
 
 def make_scene(rng, num_points=20000, cfg=None, nobj=None, use_color=False, use_image=False,
                max_num_obj=64, uniform_volume=False):
+    """cfg = ScannetDatasetConfig: axis-aligned boxes (heading 0, angle labels 0, as
+    datasets/scannet.py:329-378), classes 0..17"""
     cfg = cfg or SunrgbdDatasetConfig()
+    aligned = cfg.num_angle_bin == 1
     if nobj is None:
         nobj = int(rng.integers(1, 11))
     half = rng.uniform(0.15, 1.0, size=(nobj, 3))
     heading = rng.uniform(-np.pi, np.pi, size=nobj)
     heading[0] = abs(heading[0]) + 1e-3  # at least one positive angle -> rotated GIoU path
+    if aligned:
+        heading[:] = 0.0
     centers = np.stack([rng.uniform(-2.4, 2.4, nobj), rng.uniform(1.0, 6.0, nobj), half[:, 2]], 1)
     if uniform_volume:
         pts = np.stack([rng.uniform(-3, 3, num_points), rng.uniform(0.5, 6.5, num_points),
@@ -68,7 +73,7 @@ def make_scene(rng, num_points=20000, cfg=None, nobj=None, use_color=False, use_
     sem[:nobj] = rng.integers(0, cfg.num_semcls, nobj)
     for i in range(nobj):
         raw_sizes[i] = half[i] * 2
-        c, r = cfg.angle2class(heading[i])
+        c, r = (0, 0.0) if aligned else cfg.angle2class(heading[i])
         ang_cls[i], ang_res[i] = c, r
         local = np.array([[sx * half[i, 0], sy * half[i, 1], sz * half[i, 2]]
                           for sx, sy, sz in [(-1, 1, 1), (1, 1, 1), (1, -1, 1), (-1, -1, 1),
@@ -83,7 +88,8 @@ def make_scene(rng, num_points=20000, cfg=None, nobj=None, use_color=False, use_
     box_centers = target[:, 0:3].astype(np.float32)
     centers_n = ((box_centers - dmin[None]) / mult[None]) * present[:, None]
     ang_cls_i = ang_cls.astype(np.int64)
-    raw_angles = cfg.class2angle_batch(ang_cls_i, ang_res.astype(np.float32))
+    raw_angles = (np.zeros(G, np.float32) if aligned else
+                  cfg.class2angle_batch(ang_cls_i, ang_res.astype(np.float32)))
     corners = cfg.box_parametrization_to_corners_np(box_centers[None], raw_sizes[None],
                                                    raw_angles.astype(np.float32)[None])[0]
     d = {
@@ -111,8 +117,11 @@ def make_scene(rng, num_points=20000, cfg=None, nobj=None, use_color=False, use_
     return d
 
 
-def make_batch(batch_size, seed=0, device="cpu", **kw):
+def make_batch(batch_size, seed=0, device="cpu", dataset="sunrgbd", **kw):
     """Collate `batch_size` scenes (seeds seed*1000 + i) into tensors on `device`."""
+    if dataset == "scannet":
+        from .dataset_config import ScannetDatasetConfig
+        kw.setdefault("cfg", ScannetDatasetConfig())
     scenes = [make_scene(np.random.Generator(np.random.PCG64(seed * 1000 + i)), **kw)
               for i in range(batch_size)]
     out = {}
