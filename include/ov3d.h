@@ -123,6 +123,7 @@ int ov3d_hungarian(const float* cost, const int32_t* nactual, int P, int Q, int 
 /* layer 1: x0 (R,3) f32, W1 (C1,3) f32 -> y1 (R,C1) bf16, partials (nparts,2,C1) */
 int ov3d_sa_l1_fwd(const float* x0, const float* W1, int R, int C1, void* y1, double* partials,
                    int nparts, void* stream);
+/* (y1 may be NULL: statistics only, for consumers that recompute the layer from x0) */
 /* 1 if the MFMA layer kernel is built for (K, N) */
 int ov3d_sa_layer_supported(int K, int N);
 /* layer k: z = relu(scale*yprev + shift) (bf16, optionally stored to zout) ->
@@ -130,6 +131,12 @@ int ov3d_sa_layer_supported(int K, int N);
 int ov3d_sa_layer_fwd(const void* yprev, const float* scale, const float* shift, const void* W,
                       int R, int K, int N, void* zout, void* yout, double* partials, int nparts,
                       void* stream);
+/* layer 2 with its input recomputed: yprev = bf16(x0 W1^T) per row (ov3d_sa_l1_fwd's value,
+ * bit for bit) instead of read, so the first layer's (R, 64) output is never stored:
+ * x0 (R, 3) f32, W1 (K, 3) f32; K = 64, N = 128. */
+int ov3d_sa_layer_fwd_x0(const float* x0, const float* W1, const float* scale, const float* shift,
+                         const void* W, int R, int K, int N, void* yout, double* partials,
+                         int nparts, void* stream);
 /* last layer + pool: as ov3d_sa_layer_fwd but y is not stored; per centroid (S rows,
  * S in {32,64}) and channel: max/min of y (bf16 values) and their rows. */
 int ov3d_sa_layer_pool_fwd(const void* yprev, const float* scale, const float* shift,
@@ -155,11 +162,12 @@ int ov3d_sa_dy_fused_supported(int K, int N);
  * relu(a1*y1 + b1) recomputed; writes dz1 = dy2 W2 (R, K) bf16, dW2 = dy2^T z1 partials
  * dwpart (nwg, N, K) and layer 1's ReLU + BN backward partials stats (2*nwg, 2, K) (sum dt1,
  * sum dt1 * (y1 - mean1) * invstd1 on the stored dz1).  K = 64, N = 128. */
-int ov3d_sa_dy2_fused(const void* y1, const float* a1, const float* b1, const void* y2,
-                      const float* a2, const float* b2, const void* dz2, const float* cA,
-                      const float* cB, const float* cC, const void* W, const float* mean1,
-                      const float* invstd1, int R, int K, int N, void* dz1, float* dwpart,
-                      double* stats, int nwg, void* stream);
+/* (y1 == NULL: y1 recomputed from x0 (R, 3) and W1 (K, 3) as ov3d_sa_layer_fwd_x0) */
+int ov3d_sa_dy2_fused(const void* y1, const float* x0, const float* W1, const float* a1,
+                      const float* b1, const void* y2, const float* a2, const float* b2,
+                      const void* dz2, const float* cA, const float* cB, const float* cC,
+                      const void* W, const float* mean1, const float* invstd1, int R, int K, int N,
+                      void* dz1, float* dwpart, double* stats, int nwg, void* stream);
 int ov3d_sa_dy_fused(const void* yprev, const float* scale, const float* shift, const void* W,
                      int R, int K, int N, int S, const float* gsel, const uint8_t* isel,
                      const float* cA, const float* cB, const float* cC, void* dz, float* dwpart,
@@ -202,10 +210,11 @@ int ov3d_bn_bwd_finalize(const double* totals, double count, int C, const float*
 /* ReLU + BN backward over (R,C) bf16 rows (dz = grad of the ReLU output, y = BN input):
  * pass 0: partials (nparts,2,C) of dt and dt*xhat;  pass 1: dyout = cA*dt + cB*y + cC;
  * pass 2: dW1 partials (nparts,C,3) = sum_r dy[r,c] * x0[r,k] (first layer, dy not stored) */
+/* (pass 2 with y == NULL: the first layer's y recomputed from x0 and W1 (C, 3)) */
 int ov3d_bn_relu_bwd(int pass, const void* dz, const void* y, const float* scale,
                      const float* shift, const float* mean, const float* invstd, const float* cA,
                      const float* cB, const float* cC, const float* x0, int R, int C,
-                     double* partials, void* dyout, int nparts, void* stream);
+                     double* partials, void* dyout, int nparts, const float* W1, void* stream);
 
 /* Greedy 3D NMS, batched over scenes.  Replaces utils/nms.py:79-162
  * (nms_3d_faster / nms_3d_faster_samecls) as called per scene by

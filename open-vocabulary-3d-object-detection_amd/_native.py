@@ -32,6 +32,7 @@ _SIGS = {
     "ov3d_hungarian": "ppiiipppp",
     "ov3d_sa_l1_fwd": "ppiippip",
     "ov3d_sa_layer_fwd": "ppppiiipppip",
+    "ov3d_sa_layer_fwd_x0": "pppppiiippip",
     "ov3d_sa_layer_pool_fwd": "ppppiiiippppppip",
     "ov3d_sa_layer_dy": "ppppiiiippppppip",
     "ov3d_reduce_partials": "piipp",
@@ -39,7 +40,7 @@ _SIGS = {
     "ov3d_sa_pool_fwd": "ppppppiipppp",
     "ov3d_sa_pool_bwd": "ppppppiippip",
     "ov3d_bn_bwd_finalize": "pdippppppppp",
-    "ov3d_bn_relu_bwd": "ippppppppppiippip",
+    "ov3d_bn_relu_bwd": "ippppppppppiippipp",
     "ov3d_nms3d": "ppiiidiipp",
     "ov3d_nms_boxes_from_corners": "pppiipp",
     "ov3d_clip_preprocess": "plppiiifffffffipp",
@@ -70,7 +71,7 @@ _SIGS = {
     "ov3d_bn_stats_finalize": "piidppffpppppppp",
     "ov3d_colsum_group": "pipiip",
     "ov3d_sa_dy_fused": "ppppiiiippppppppppip",
-    "ov3d_sa_dy2_fused": "pppppppppppppiiipppip",
+    "ov3d_sa_dy2_fused": "pppppppppppppppiiipppip",
     "ov3d_bn_bwd_stats_finalize": "piidppppppppp",
     "ov3d_rows_gemm_act": "iiiplplipifpiplplp",
     "ov3d_rows_gemm_group": "iipip",

@@ -49,6 +49,20 @@ struct DyFusedArgs {
     double* stats;         // (gridDim.x, 2, K) or null
 };
 
+#ifdef OV3D_SA_PROBE
+// diagnostic build only (tools/sa_probe.py): per-wave s_memtime totals of the tile phases
+__device__ unsigned long long* g_sa_probe;
+#define PROBE_DECL unsigned long long pr_t = __builtin_amdgcn_s_memtime(), pr_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PROBE(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); pr_acc[i] += t_ - pr_t; pr_t = t_; } while (0)
+#define PROBE_END do { if ((threadIdx.x & 63) == 0 && g_sa_probe) { \
+    unsigned long long* o_ = g_sa_probe + ((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8; \
+    for (int i_ = 0; i_ < 8; ++i_) o_[i_] = pr_acc[i_]; } } while (0)
+#else
+#define PROBE_DECL
+#define PROBE(i) do { } while (0)
+#define PROBE_END do { } while (0)
+#endif
+
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -153,8 +167,10 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
         }
     };
     if (blockIdx.x < ntiles) fetch(blockIdx.x);
+    PROBE_DECL
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const size_t row0 = (size_t)tile * kTile;
+        PROBE(0);
         // z = relu(a2*y2 + b2) of the prefetched rows -> LDS
 #pragma unroll
         for (int c = 0; c < CH; ++c) {
@@ -167,7 +183,9 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
             *reinterpret_cast<bf16x8*>(&As[row * LDK + kc]) = z;
             if constexpr (STATS) *reinterpret_cast<bf16x8*>(&Ys[row * LDK + kc]) = pre[c];
         }
+        PROBE(1);
         __syncthreads();
+        PROBE(2);
         if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);   // in flight below
 
         // y3 = z W3^T, then dy3 -> LDS
@@ -211,7 +229,9 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
                 }
             }
         }
+        PROBE(3);
         __syncthreads();
+        PROBE(4);
 
         // dz^T = W3^T dy3^T -> HBM: lane = row rb*32 + r32, channels kbase + 8g + 4h + (0..3)
 #pragma unroll
@@ -247,6 +267,7 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
                 }
             }
         }
+        PROBE(5);
         // dW3 += dy3^T z over this tile's rows
 #pragma unroll
         for (int s = 0; s < kTile / 16; ++s) {
@@ -264,8 +285,11 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
                 for (int b = 0; b < WK; ++b) dw[a][b] = mfma(ad, bz[b], dw[a][b]);
             }
         }
+        PROBE(6);
         __syncthreads();   // As / Ds are rewritten by the next tile
+        PROBE(7);
     }
+    PROBE_END;
     if constexpr (STATS) {   // sum each channel over the 32 lanes (rows) of its lane half
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb)
@@ -318,9 +342,11 @@ struct Dy2Args {
     bf16* dz1;          // (R, K)
     float* dwpart;      // (gridDim.x, N, K)
     double* stats;      // (gridDim.x, 2, K)
+    const float* x0;    // X0 variant (y1 == NULL): y1 = bf16(x0 W1^T) recomputed, (R, 3)
+    const float* W1;    // (K, 3)
 };
 
-template <int K, int N>
+template <int K, int N, bool X0>
 __global__ __launch_bounds__(kThreads, 1) void sa_dy2_fused_kernel(Dy2Args p) {
     static_assert(K == 64 && N == 128, "4 waves = 2 x 2 dz tiles, 32 dW rows each");
     constexpr int LDK = K + 8, LDN = N + 8;
@@ -328,6 +354,8 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy2_fused_kernel(Dy2Args p) {
     __shared__ __attribute__((aligned(16))) bf16 Ys[kTile * LDK];   // raw y1
     __shared__ __attribute__((aligned(16))) bf16 Ds[kTile * LDN];   // dy2, row-major
     __shared__ float a1s[K], b1s[K], mus[K], iss[K], a2s[N], b2s[N], cAs[N], cBs[N], cCs[N];
+    __shared__ float w1s[X0 ? 3 * K : 1];
+    __shared__ __attribute__((aligned(16))) float x0s[X0 ? 3 * kTile : 4];   // the tile's x0 rows
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r32 = lane & 31, h = lane >> 5;
     for (int k = tid; k < K; k += kThreads) {
         a1s[k] = p.a1[k];
@@ -335,6 +363,8 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy2_fused_kernel(Dy2Args p) {
         mus[k] = p.mean1[k];
         iss[k] = p.invstd1[k];
     }
+    if constexpr (X0)
+        for (int k = tid; k < 3 * K; k += kThreads) w1s[k] = p.W1[k];
     for (int n = tid; n < N; n += kThreads) {
         a2s[n] = p.a2[n];
         b2s[n] = p.b2[n];
@@ -363,13 +393,18 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy2_fused_kernel(Dy2Args p) {
     const int ntiles = p.R / kTile;
     constexpr int C1 = kTile * K / 8 / kThreads;   // 16-byte chunks per thread: y1
     constexpr int C2 = kTile * N / 8 / kThreads;   // y2, dz2
-    bf16x8 py1[C1], py2[C2], pdz[C2];
+    bf16x8 py1[X0 ? 1 : C1], py2[C2], pdz[C2];
+    float4 px0 = make_float4(0.f, 0.f, 0.f, 0.f);   // X0: 16 bytes of the tile's 768 B of x0
     auto fetch = [&](int tile) {
         const size_t row0 = (size_t)tile * kTile;
+        if constexpr (X0) {
+            if (tid < 3 * kTile / 4) px0 = reinterpret_cast<const float4*>(p.x0 + row0 * 3)[tid];
+        } else {
 #pragma unroll
-        for (int c = 0; c < C1; ++c) {
-            const int ch = tid + c * kThreads, row = ch / (K / 8), kc = (ch % (K / 8)) * 8;
-            py1[c] = *reinterpret_cast<const bf16x8*>(p.y1 + (row0 + row) * K + kc);
+            for (int c = 0; c < C1; ++c) {
+                const int ch = tid + c * kThreads, row = ch / (K / 8), kc = (ch % (K / 8)) * 8;
+                py1[c] = *reinterpret_cast<const bf16x8*>(p.y1 + (row0 + row) * K + kc);
+            }
         }
 #pragma unroll
         for (int c = 0; c < C2; ++c) {
@@ -379,17 +414,32 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy2_fused_kernel(Dy2Args p) {
         }
     };
     if (blockIdx.x < ntiles) fetch(blockIdx.x);
+    if constexpr (X0) {   // x0 of the first tile -> LDS (read in the first prologue)
+        if (tid < 3 * kTile / 4) reinterpret_cast<float4*>(x0s)[tid] = px0;
+        __syncthreads();
+    }
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const size_t row0 = (size_t)tile * kTile;
 #pragma unroll
         for (int c = 0; c < C1; ++c) {
             const int ch = tid + c * kThreads, row = ch / (K / 8), kc = (ch % (K / 8)) * 8;
+            bf16x8 y1v;
+            if constexpr (X0) {
+                const float* xr = &x0s[3 * row];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {   // sa_l1_kernel's value, bit for bit
+                    const float* w = &w1s[3 * (kc + j)];
+                    y1v[j] = (bf16)fmaf(w[2], xr[2], fmaf(w[1], xr[1], w[0] * xr[0]));
+                }
+            } else {
+                y1v = py1[c];
+            }
             bf16x8 z;
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-                z[j] = (bf16)fmaxf(fmaf(a1s[kc + j], (float)py1[c][j], b1s[kc + j]), 0.f);
+                z[j] = (bf16)fmaxf(fmaf(a1s[kc + j], (float)y1v[j], b1s[kc + j]), 0.f);
             *reinterpret_cast<bf16x8*>(&As[row * LDK + kc]) = z;
-            *reinterpret_cast<bf16x8*>(&Ys[row * LDK + kc]) = py1[c];
+            *reinterpret_cast<bf16x8*>(&Ys[row * LDK + kc]) = y1v;
         }
 #pragma unroll
         for (int c = 0; c < C2; ++c) {   // bn_relu_bwd_kernel pass 1 arithmetic
@@ -441,7 +491,11 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy2_fused_kernel(Dy2Args p) {
 #pragma unroll
             for (int b = 0; b < 2; ++b) dw[b] = mfma(ad, col_operand(As, LDK, lane, 32 * b, s), dw[b]);
         }
-        __syncthreads();   // As / Ys / Ds are rewritten by the next tile
+        if constexpr (X0) {   // the next tile's x0 (its prologue reads it after the barrier)
+            if (tid < 3 * kTile / 4 && tile + (int)gridDim.x < ntiles)
+                reinterpret_cast<float4*>(x0s)[tid] = px0;
+        }
+        __syncthreads();   // As / Ys / Ds (and x0s) are rewritten by the next tile
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -472,6 +526,12 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy2_fused_kernel(Dy2Args p) {
 
 extern "C" int ov3d_sa_dy_fused_supported(int K, int N) { return K == 128 && N == 256; }
 
+#ifdef OV3D_SA_PROBE
+extern "C" void ov3d_sa_probe_set(unsigned long long* dbg) {
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sa_probe), &dbg, sizeof(dbg));
+}
+#endif
+
 extern "C" int ov3d_sa_dy_fused(const void* yprev, const float* scale, const float* shift,
                                 const void* W, int R, int K, int N, int S, const float* gsel,
                                 const uint8_t* isel, const float* cA, const float* cB,
@@ -493,19 +553,24 @@ extern "C" int ov3d_sa_dy_fused(const void* yprev, const float* scale, const flo
     return OV3D_OK;
 }
 
-extern "C" int ov3d_sa_dy2_fused(const void* y1, const float* a1, const float* b1, const void* y2,
-                                 const float* a2, const float* b2, const void* dz2, const float* cA,
-                                 const float* cB, const float* cC, const void* W,
-                                 const float* mean1, const float* invstd1, int R, int K, int N,
-                                 void* dz1, float* dwpart, double* stats, int nwg, void* stream) {
-    if (K != 64 || N != 128 || R <= 0 || R % kTile || !y1 || !a1 || !b1 || !y2 || !a2 || !b2 ||
-        !dz2 || !cA || !cB || !cC || !W || !mean1 || !invstd1 || !dz1 || !dwpart || !stats ||
-        nwg <= 0)
+extern "C" int ov3d_sa_dy2_fused(const void* y1, const float* x0, const float* W1, const float* a1,
+                                 const float* b1, const void* y2, const float* a2, const float* b2,
+                                 const void* dz2, const float* cA, const float* cB, const float* cC,
+                                 const void* W, const float* mean1, const float* invstd1, int R,
+                                 int K, int N, void* dz1, float* dwpart, double* stats, int nwg,
+                                 void* stream) {
+    if (K != 64 || N != 128 || R <= 0 || R % kTile || (!y1 && !(x0 && W1)) || !a1 || !b1 || !y2 ||
+        !a2 || !b2 || !dz2 || !cA || !cB || !cC || !W || !mean1 || !invstd1 || !dz1 || !dwpart ||
+        !stats || nwg <= 0)
         return OV3D_EINVAL;
     Dy2Args a{(const bf16*)y1, a1, b1, (const bf16*)y2, a2, b2, (const bf16*)dz2, cA, cB, cC,
-              (const bf16*)W, mean1, invstd1, R, (bf16*)dz1, dwpart, stats};
-    hipLaunchKernelGGL((sa_dy2_fused_kernel<64, 128>), dim3(nwg), dim3(kThreads), 0,
-                       ov3d_stream(stream), a);
+              (const bf16*)W, mean1, invstd1, R, (bf16*)dz1, dwpart, stats, x0, W1};
+    if (y1)
+        hipLaunchKernelGGL((sa_dy2_fused_kernel<64, 128, false>), dim3(nwg), dim3(kThreads), 0,
+                           ov3d_stream(stream), a);
+    else
+        hipLaunchKernelGGL((sa_dy2_fused_kernel<64, 128, true>), dim3(nwg), dim3(kThreads), 0,
+                           ov3d_stream(stream), a);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

@@ -55,21 +55,33 @@ struct LayerArgs {
     const float* cB;
     const float* cC;
     bf16* dyout;           // (R, N)
+    const float* x0;       // X0 variant: (R, 3) first-layer input, yprev = bf16(x0 W1^T)
+    const float* W1;       // (K, 3) fp32 first-layer weight
 };
 
-template <int K, int N, int MODE>
+// the first SA layer's output row element, recomputed instead of stored (sa_l1_kernel's
+// formula: bit-identical values)
+__device__ __forceinline__ float l1_value(const float* w, const float* x) {
+    return (float)(bf16)fmaf(w[2], x[2], fmaf(w[1], x[1], w[0] * x[0]));
+}
+
+template <int K, int N, int MODE, bool X0 = false>
 __global__ __launch_bounds__(kThreads, 2) void sa_layer_kernel(LayerArgs p) {
     constexpr int LDK = K + 8;          // padded LDS row (bf16): spreads rows over banks
     constexpr int NB = N / 128;         // 32-column blocks per wave
     constexpr int KS = K / 16;          // MFMA k-steps
     __shared__ __attribute__((aligned(16))) bf16 As[kTile * LDK];
     __shared__ float sc[K], sh[K];
+    __shared__ float w1s[X0 ? 3 * K : 1];
+    __shared__ __attribute__((aligned(16))) float x0s[X0 ? 3 * kTile : 4];   // the tile's x0 rows
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r32 = lane & 31, h = lane >> 5;
 
     for (int k = tid; k < K; k += kThreads) {
         sc[k] = p.scale[k];
         sh[k] = p.shift[k];
     }
+    if constexpr (X0)
+        for (int k = tid; k < 3 * K; k += kThreads) w1s[k] = p.W1[k];
     bf16x8 bfrag[NB][KS];
 #pragma unroll
     for (int cb = 0; cb < NB; ++cb) {
@@ -98,17 +110,26 @@ __global__ __launch_bounds__(kThreads, 2) void sa_layer_kernel(LayerArgs p) {
     // MFMA phase and epilogue run (CH 16-byte chunks per thread)
     constexpr int CH = kTile * K / 8 / kThreads;
     static_assert(CH * kThreads * 8 == kTile * K, "tile chunks");
-    bf16x8 pre[CH];
+    bf16x8 pre[X0 ? 1 : CH];
+    float4 prex = make_float4(0.f, 0.f, 0.f, 0.f);   // X0: 16 bytes of the tile's 768 B of x0
     auto fetch = [&](int tile) {
         const size_t row0 = (size_t)tile * kTile;
+        if constexpr (X0) {
+            if (tid < 3 * kTile / 4) prex = reinterpret_cast<const float4*>(p.x0 + row0 * 3)[tid];
+        } else {
 #pragma unroll
-        for (int c = 0; c < CH; ++c) {
-            const int ch = tid + c * kThreads;
-            const int row = ch / (K / 8), kc = (ch % (K / 8)) * 8;
-            pre[c] = *reinterpret_cast<const bf16x8*>(p.yprev + (row0 + row) * K + kc);
+            for (int c = 0; c < CH; ++c) {
+                const int ch = tid + c * kThreads;
+                const int row = ch / (K / 8), kc = (ch % (K / 8)) * 8;
+                pre[c] = *reinterpret_cast<const bf16x8*>(p.yprev + (row0 + row) * K + kc);
+            }
         }
     };
     if (blockIdx.x < ntiles) fetch(blockIdx.x);
+    if constexpr (X0) {   // x0 of the first tile -> LDS (read in the first prologue)
+        if (tid < 3 * kTile / 4) reinterpret_cast<float4*>(x0s)[tid] = prex;
+        __syncthreads();
+    }
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const size_t row0 = (size_t)tile * kTile;
         // prologue: previous layer's BN + ReLU of the prefetched rows, to bf16, into LDS
@@ -119,7 +140,12 @@ __global__ __launch_bounds__(kThreads, 2) void sa_layer_kernel(LayerArgs p) {
             const int row = ch / (K / 8), kc = (ch % (K / 8)) * 8;
             bf16x8 z;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) z[j] = (bf16)relu_bn(sc[kc + j], (float)pre[c][j], sh[kc + j]);
+            for (int j = 0; j < 8; ++j) {
+                float yv;
+                if constexpr (X0) yv = l1_value(&w1s[3 * (kc + j)], &x0s[3 * row]);
+                else yv = (float)pre[c][j];
+                z[j] = (bf16)relu_bn(sc[kc + j], yv, sh[kc + j]);
+            }
             *reinterpret_cast<bf16x8*>(&As[row * LDK + kc]) = z;
             if (p.zout) *reinterpret_cast<bf16x8*>(p.zout + (row0 + row) * K + kc) = z;
         }
@@ -142,7 +168,11 @@ __global__ __launch_bounds__(kThreads, 2) void sa_layer_kernel(LayerArgs p) {
                     acc[rb][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfrag[cb][s], acc[rb][cb], 0, 0, 0);
             }
         }
-        __syncthreads();   // As is rewritten by the next tile's prologue
+        if constexpr (X0) {   // the next tile's x0 (its prologue reads it after the barrier)
+            if (tid < 3 * kTile / 4 && tile + (int)gridDim.x < ntiles)
+                reinterpret_cast<float4*>(x0s)[tid] = prex;
+        }
+        __syncthreads();   // As (and x0s) are rewritten by the next tile's prologue
 
         // epilogue: element (rb, cb, i) is row rb*32 + (i&3) + 8*(i>>2) + 4h, column n
 #pragma unroll
@@ -237,24 +267,35 @@ __global__ __launch_bounds__(kThreads, 2) void sa_layer_kernel(LayerArgs p) {
 }
 
 // First layer: Cin = 3 fp32 (grouped, normalised xyz) -> C1 channels.
-// Thread t: channel t % C1, row phase t / C1.
+// Chunks of 256 rows: their inputs staged through LDS by coalesced loads, then thread t
+// computes channel t % C1 of the rows t / C1, t / C1 + kThreads / C1, ...
+// y1 == NULL: BN statistics only.
 __global__ __launch_bounds__(kThreads) void sa_l1_kernel(const float* __restrict__ x0,
                                                          const float* __restrict__ W1, int R, int C1,
                                                          bf16* __restrict__ y1,
                                                          double* __restrict__ partials) {
     __shared__ double red[2][kThreads];
+    __shared__ float xs[kThreads * 3];
     const int tid = threadIdx.x;
     const int c = tid % C1, ph = tid / C1, nph = kThreads / C1;
     const float w0 = W1[c * 3], w1 = W1[c * 3 + 1], w2 = W1[c * 3 + 2];
     float s = 0.f, q = 0.f;
-    for (long long r = (long long)blockIdx.x * nph + ph; r < R; r += (long long)gridDim.x * nph) {
-        const float* x = x0 + r * 3;
-        const float y = fmaf(w2, x[2], fmaf(w1, x[1], w0 * x[0]));
-        const bf16 yb = (bf16)y;
-        y1[r * C1 + c] = yb;
-        const float f = (float)yb;
-        s += f;
-        q = fmaf(f, f, q);
+    const long long nchunk = ((long long)R + kThreads - 1) / kThreads;
+    for (long long ck = blockIdx.x; ck < nchunk; ck += gridDim.x) {
+        const long long r0 = ck * kThreads;
+        const int nr = (int)min((long long)kThreads, (long long)R - r0);
+        for (int i = tid; i < 3 * nr; i += kThreads) xs[i] = x0[r0 * 3 + i];
+        __syncthreads();
+        for (int rr = ph; rr < nr; rr += nph) {
+            const float* x = xs + rr * 3;
+            const float y = fmaf(w2, x[2], fmaf(w1, x[1], w0 * x[0]));
+            const bf16 yb = (bf16)y;
+            if (y1) y1[(r0 + rr) * C1 + c] = yb;
+            const float f = (float)yb;
+            s += f;
+            q = fmaf(f, f, q);
+        }
+        __syncthreads();
     }
     red[0][tid] = s;
     red[1][tid] = q;
@@ -465,10 +506,17 @@ __global__ __launch_bounds__(kThreads) void bn_relu_bwd_kernel(
     const float* __restrict__ shift, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ cA, const float* __restrict__ cB, const float* __restrict__ cC,
     const float* __restrict__ x0, long long R, int C, double* __restrict__ partials,
-    bf16* __restrict__ dyout) {
+    bf16* __restrict__ dyout, const float* __restrict__ W1) {
     const int tid = threadIdx.x;
     const int tpr = C / 8;                          // threads per row
     const int kc = (tid % tpr) * 8, ph = tid / tpr, nph = kThreads / tpr;
+    // y == NULL (PASS 2): the first layer's y recomputed from x0 and W1 (l1_value)
+    float w1r[PASS == 2 ? 24 : 1];
+    if constexpr (PASS == 2) {
+        if (!y)
+#pragma unroll
+            for (int q = 0; q < 24; ++q) w1r[q] = W1[kc * 3 + q];
+    }
     float pa[8], pb[8], p0[8], p1[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -492,12 +540,18 @@ __global__ __launch_bounds__(kThreads) void bn_relu_bwd_kernel(
     for (int j = 0; j < 8; ++j) acc0[j] = acc1[j] = acc2[j] = 0.f;
     for (long long r = (long long)blockIdx.x * nph + ph; r < R; r += (long long)gridDim.x * nph) {
         const bf16x8 vz = *reinterpret_cast<const bf16x8*>(dz + r * C + kc);
-        const bf16x8 vy = *reinterpret_cast<const bf16x8*>(y + r * C + kc);
         float xr[3];
         if (PASS == 2) {
             xr[0] = x0[r * 3];
             xr[1] = x0[r * 3 + 1];
             xr[2] = x0[r * 3 + 2];
+        }
+        bf16x8 vy;
+        if (PASS != 2 || y) {
+            vy = *reinterpret_cast<const bf16x8*>(y + r * C + kc);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) vy[j] = (bf16)l1_value(&w1r[PASS == 2 ? 3 * j : 0], xr);
         }
         bf16x8 out;
 #pragma unroll
@@ -552,7 +606,7 @@ int grid_for(long long work, int cap) {
 extern "C" int ov3d_sa_l1_fwd(const float* x0, const float* W1, int R, int C1, void* y1,
                               double* partials, int nparts, void* stream) {
     if (R < 0 || C1 <= 0 || C1 > kThreads || kThreads % C1 || nparts <= 0) return OV3D_EINVAL;
-    if (!x0 || !W1 || !y1 || !partials) return OV3D_EINVAL;
+    if (!x0 || !W1 || !partials) return OV3D_EINVAL;
     hipLaunchKernelGGL(sa_l1_kernel, dim3(nparts), dim3(kThreads), 0, ov3d_stream(stream), x0, W1, R,
                        C1, reinterpret_cast<bf16*>(y1), partials);
     OV3D_LAUNCH_CHECK();
@@ -594,6 +648,28 @@ extern "C" int ov3d_sa_layer_fwd(const void* yprev, const float* scale, const fl
     a.yout = reinterpret_cast<bf16*>(yout);
     a.partials = partials;
     return launch_layer<MODE_STORE>(a, K, N, nparts, ov3d_stream(stream));
+}
+
+extern "C" int ov3d_sa_layer_fwd_x0(const float* x0, const float* W1, const float* scale,
+                                    const float* shift, const void* W, int R, int K, int N,
+                                    void* yout, double* partials, int nparts, void* stream) {
+    if (R < 0 || R % kTile || !x0 || !W1 || !scale || !shift || !W || !yout || !partials ||
+        nparts <= 0 || K != 64 || N != 128)
+        return OV3D_EINVAL;
+    LayerArgs a = {};
+    a.x0 = x0;
+    a.W1 = W1;
+    a.scale = scale;
+    a.shift = shift;
+    a.W = reinterpret_cast<const bf16*>(W);
+    a.R = R;
+    a.S = kTile;
+    a.yout = reinterpret_cast<bf16*>(yout);
+    a.partials = partials;
+    hipLaunchKernelGGL((sa_layer_kernel<64, 128, MODE_STORE, true>), dim3(nparts), dim3(kThreads), 0,
+                       ov3d_stream(stream), a);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
 }
 
 extern "C" int ov3d_sa_layer_pool_fwd(const void* yprev, const float* scale, const float* shift,
@@ -736,9 +812,9 @@ extern "C" int ov3d_bn_relu_bwd(int pass, const void* dz, const void* y, const f
                                 const float* shift, const float* mean, const float* invstd,
                                 const float* cA, const float* cB, const float* cC, const float* x0,
                                 int R, int C, double* partials, void* dyout, int nparts,
-                                void* stream) {
+                                const float* W1, void* stream) {
     if (R < 0 || C <= 0 || C % 8 || C / 8 > kThreads || kThreads % (C / 8) || C > 256 ||
-        nparts <= 0 || !dz || !y || !scale || !shift)
+        nparts <= 0 || !dz || !scale || !shift || (!y && !(pass == 2 && x0 && W1)))
         return OV3D_EINVAL;
     const bf16* dzb = reinterpret_cast<const bf16*>(dz);
     const bf16* yb = reinterpret_cast<const bf16*>(y);
@@ -747,17 +823,17 @@ extern "C" int ov3d_bn_relu_bwd(int pass, const void* dz, const void* y, const f
         if (!mean || !invstd || !partials) return OV3D_EINVAL;
         hipLaunchKernelGGL(bn_relu_bwd_kernel<0>, dim3(nparts), dim3(kThreads), 0, s, dzb, yb, scale,
                            shift, mean, invstd, cA, cB, cC, x0, (long long)R, C, partials,
-                           (bf16*)nullptr);
+                           (bf16*)nullptr, W1);
     } else if (pass == 1) {
         if (!cA || !cB || !cC || !dyout) return OV3D_EINVAL;
         hipLaunchKernelGGL(bn_relu_bwd_kernel<1>, dim3(nparts), dim3(kThreads), 0, s, dzb, yb, scale,
                            shift, mean, invstd, cA, cB, cC, x0, (long long)R, C, partials,
-                           reinterpret_cast<bf16*>(dyout));
+                           reinterpret_cast<bf16*>(dyout), W1);
     } else if (pass == 2) {
         if (!cA || !cB || !cC || !x0 || !partials) return OV3D_EINVAL;
         hipLaunchKernelGGL(bn_relu_bwd_kernel<2>, dim3(nparts), dim3(kThreads), 0, s, dzb, yb, scale,
                            shift, mean, invstd, cA, cB, cC, x0, (long long)R, C, partials,
-                           (bf16*)nullptr);
+                           (bf16*)nullptr, W1);
     } else {
         return OV3D_EINVAL;
     }

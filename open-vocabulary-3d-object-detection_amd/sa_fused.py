@@ -6,8 +6,11 @@ models/model_3detr.py:353-362; pointnet2 pytorch_utils.SharedMLP: 1x1 conv
 without bias -> BatchNorm (batch statistics) -> ReLU per layer).
 
 Forward (csrc/sa_mlp.hip):
-  layer 1  ov3d_sa_l1_fwd      x0 (R,3) f32 -> y1 bf16 + BN partials
-  layer 2  ov3d_sa_layer_fwd   relu(bn1(y1)) -> MFMA W2 -> y2 bf16 + partials (z1 kept)
+  layer 1  ov3d_sa_l1_fwd      x0 (R,3) f32 -> BN partials (y1 = bf16(x0 W1^T) is recomputed
+                               by its consumers from x0, never stored, when the fused backward
+                               runs; otherwise stored)
+  layer 2  ov3d_sa_layer_fwd   relu(bn1(y1)) -> MFMA W2 -> y2 bf16 + partials (z1 kept);
+           ov3d_sa_layer_fwd_x0 the same with y1 recomputed from x0 in the prologue
   layer 3  ov3d_sa_layer_pool_fwd  relu(bn2(y2)) -> MFMA W3 -> per-centroid max/min of
            y3 (never stored) + partials (z2 kept);  ov3d_sa_pool_fwd applies bn3 + ReLU
            to the max (or min when gamma*invstd < 0: relu(a*y+b) is monotone in y).
@@ -155,21 +158,28 @@ class _SAMLPPool(Function):
         world = [dist.get_world_size(g) if g is not None else 1 for g in groups]
         x0 = x0.contiguous()
         bf = torch.bfloat16
-        # layer 1
-        y1 = torch.empty((R, c1), dtype=bf, device=dev)
+        # z1 is kept for the backward only when that does not recompute it (sa_dy2_fused), and
+        # then y1 is not stored either: every consumer recomputes it from x0 (12 B per row
+        # instead of 128 B: the (R, 64) first-layer output never reaches HBM)
+        fused_bwd2 = FUSED_BWD and c1 == 64 and c2 == 128 and \
+            bool(nat.load().ov3d_sa_dy_fused_supported(c2, w3.shape[0]))
+        w1f = w1.float().contiguous()
+        # layer 1 (statistics only when y1 is recomputed)
+        y1 = None if fused_bwd2 else torch.empty((R, c1), dtype=bf, device=dev)
         parts = torch.empty((NPARTS_ROWS, 2, c1), dtype=torch.float64, device=dev)
-        nat.call("ov3d_sa_l1_fwd", x0, w1.float().contiguous(), R, c1, y1, parts, NPARTS_ROWS, like=x0)
+        nat.call("ov3d_sa_l1_fwd", x0, w1f, R, c1, y1, parts, NPARTS_ROWS, like=x0)
         st1 = _bn_stats(parts, NPARTS_ROWS, c1, groups[0], R * world[0], bns[0])
         # layer 2
         w2b = cast_param(w2, bf).contiguous()
-        # z1 is kept for the backward only when that does not recompute it (sa_dy2_fused)
-        fused_bwd2 = FUSED_BWD and c1 == 64 and c2 == 128 and \
-            bool(nat.load().ov3d_sa_dy_fused_supported(c2, w3.shape[0]))
         z1 = None if fused_bwd2 else torch.empty((R, c1), dtype=bf, device=dev)
         y2 = torch.empty((R, c2), dtype=bf, device=dev)
         parts = torch.empty((NPARTS_LAYER, 2, c2), dtype=torch.float64, device=dev)
-        nat.call("ov3d_sa_layer_fwd", y1, st1[2], st1[3], w2b, R, c1, c2, z1, y2, parts, NPARTS_LAYER,
-                 like=x0)
+        if fused_bwd2:
+            nat.call("ov3d_sa_layer_fwd_x0", x0, w1f, st1[2], st1[3], w2b, R, c1, c2, y2, parts,
+                     NPARTS_LAYER, like=x0)
+        else:
+            nat.call("ov3d_sa_layer_fwd", y1, st1[2], st1[3], w2b, R, c1, c2, z1, y2, parts,
+                     NPARTS_LAYER, like=x0)
         st2 = _bn_stats(parts, NPARTS_LAYER, c2, groups[1], R * world[1], bns[1])
         # layer 3 + pool (z2 is kept for the backward only when it is not recomputed there)
         w3b = cast_param(w3, bf).contiguous()
@@ -186,13 +196,14 @@ class _SAMLPPool(Function):
         isel = torch.empty((P, c3), dtype=torch.uint8, device=dev)
         nat.call("ov3d_sa_pool_fwd", pmax, pmin, imax, imin, st3[2], st3[3], P, c3, out, ysel, isel,
                  like=x0)
-        ctx.save_for_backward(x0, y1, z1, y2, z2, w2b, w3b, g1, g2, g3, ysel, isel, *st1, *st2, *st3)
+        ctx.save_for_backward(x0, y1, z1, y2, z2, w2b, w3b, g1, g2, g3, ysel, isel, w1f, *st1, *st2,
+                              *st3)
         ctx.meta = (R, S, P, c1, c2, c3, groups, world, tuple(w1.shape), fused_bwd, fused_bwd2)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        (x0, y1, z1, y2, z2, w2b, w3b, g1, g2, g3, ysel, isel,
+        (x0, y1, z1, y2, z2, w2b, w3b, g1, g2, g3, ysel, isel, w1f,
          m1, i1, a1, s1, m2, i2, a2, s2, m3, i3, a3, s3) = ctx.saved_tensors
         R, S, P, c1, c2, c3, groups, world, w1shape, fused_bwd, fused_bwd2 = ctx.meta
         dev = x0.device
@@ -232,7 +243,7 @@ class _SAMLPPool(Function):
             parts, nparts = torch.empty((NPARTS_ROWS, 2, c2), dtype=torch.float64, device=dev), \
                 NPARTS_ROWS
             nat.call("ov3d_bn_relu_bwd", 0, dz2, y2, a2, s2, m2, i2, None, None, None, None, R, c2,
-                     parts, None, NPARTS_ROWS, like=dout)
+                     parts, None, NPARTS_ROWS, None, like=dout)
         cA, cB, cC, dg2, db2 = bn_bwd_affine(parts, nparts, c2, groups[1], R * world[1], g2, m2, i2)
         if fused_bwd2:   # dy2 -> dz1, dW2 and layer 1's statistics in one pass
             nwg2 = min(NWG_DY_FUSED, R // 64)
@@ -240,14 +251,14 @@ class _SAMLPPool(Function):
             part = torch.empty((nwg2, c2, c1), dtype=torch.float32, device=dev)
             parts, nparts = torch.empty((2 * nwg2, 2, c1), dtype=torch.float64, device=dev), \
                 2 * nwg2
-            nat.call("ov3d_sa_dy2_fused", y1, a1, s1, y2, a2, s2, dz2, cA, cB, cC, w2b, m1, i1, R, c1,
-                     c2, dz1, part, parts, nwg2, like=dout)
+            nat.call("ov3d_sa_dy2_fused", y1, x0, w1f, a1, s1, y2, a2, s2, dz2, cA, cB, cC, w2b, m1,
+                     i1, R, c1, c2, dz1, part, parts, nwg2, like=dout)
             dw2 = part.sum(0)
             del dz2, part
         else:
             dy2 = torch.empty((R, c2), dtype=bf, device=dev)
             nat.call("ov3d_bn_relu_bwd", 1, dz2, y2, a2, s2, None, None, cA, cB, cC, None, R, c2,
-                     None, dy2, NPARTS_ROWS, like=dout)
+                     None, dy2, NPARTS_ROWS, None, like=dout)
             del dz2
             dw2 = weight_grad(dy2, z1)
             dz1 = torch.mm(dy2, w2b)
@@ -255,12 +266,12 @@ class _SAMLPPool(Function):
             parts, nparts = torch.empty((NPARTS_ROWS, 2, c1), dtype=torch.float64, device=dev), \
                 NPARTS_ROWS
             nat.call("ov3d_bn_relu_bwd", 0, dz1, y1, a1, s1, m1, i1, None, None, None, None, R, c1,
-                     parts, None, NPARTS_ROWS, like=dout)
+                     parts, None, NPARTS_ROWS, None, like=dout)
         # layer 1: ReLU + BN backward, dW1 reduced against x0 (dy1 never stored)
         cA, cB, cC, dg1, db1 = bn_bwd_affine(parts, nparts, c1, groups[0], R * world[0], g1, m1, i1)
         parts = torch.empty((NPARTS_ROWS, c1, 3), dtype=torch.float64, device=dev)
         nat.call("ov3d_bn_relu_bwd", 2, dz1, y1, a1, s1, None, None, cA, cB, cC, x0, R, c1, parts,
-                 None, NPARTS_ROWS, like=dout)
+                 None, NPARTS_ROWS, w1f, like=dout)
         dw1 = _totals(parts, NPARTS_ROWS, 3 * c1, None).view(c1, 3).float().view(w1shape)
         return (None, dw1, dw2.view(c2, c1), dw3.view(c3, c2), dg1, db1, dg2, db2, dg3, db3, None,
                 None)
