@@ -18,6 +18,8 @@
 //   sum dt and sum dt * xhat2 per channel, dt = (a2*y2 + b2 > 0) * bf16(dz) (the pass 0 of
 //   bn_relu_bwd_kernel, whose read of dz and y2 it replaces).
 // dy3 and z are never stored: the forward no longer writes z (2^20 x 128 bf16) either.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -322,6 +324,214 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
             }
 }
 
+// The same pass with 8 waves (512 threads, two waves per SIMD): each wave owns half the
+// columns of each product, so its accumulators and operand registers halve (dW3 64 instead of
+// 128 VGPRs) and the kernel fits 256 registers: the matrix work of one wave overlaps the
+// VALU epilogue / LDS work of its SIMD partner, which the 4-wave kernel (512 registers, one
+// wave per SIMD) serialises.  Roles per tile:
+//   y3 + dy3 : wave w, columns n = 32w .. 32w+31, both 32-row blocks; W3 rows read from an
+//              LDS image of W3 (ds_read_b128)
+//   dz       : wave w, channels k = 32(w&3) .. +31, rows 32(w>>2) .. +31; W3^T fragments in
+//              VGPRs
+//   dW3      : wave w, rows n = 32w .. +31 of dW3, all K
+// Stats (layer 2's ReLU + BN backward partials): the two row halves' lanes meet in LDS after
+// the loop.  Output layouts are the 4-wave kernel's (dwpart (nwg, N, K), stats (nwg, 2, K)).
+template <int K, int N, bool STATS>
+__global__ __launch_bounds__(512, 1) void sa_dy8_kernel(DyFusedArgs p) {
+    constexpr int T8 = 512;
+    constexpr int LDK = K + 8;        // padded LDS rows (bf16)
+    constexpr int LDR = kTile + 8;    // DsT row: one channel n, the tile's 64 rows
+    constexpr int LDW = K + 8;        // W3 image row n
+    constexpr int KS = K / 16;
+    constexpr int NS = N / 16;
+    static_assert(K == 128 && N == 256, "8 waves: 32 y3 columns, 32 dz channels x 32 rows, 32 dW rows");
+    __shared__ __attribute__((aligned(16))) bf16 As[kTile * LDK];
+    __shared__ __attribute__((aligned(16))) bf16 DsT[N * LDR];
+    __shared__ __attribute__((aligned(16))) bf16 Ys[STATS ? kTile * LDK : 8];
+    __shared__ __attribute__((aligned(16))) bf16 W3s[N * LDW];
+    __shared__ float sc[K], sh[K], smu[K], sis[K];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r32 = lane & 31, h = lane >> 5;
+
+    for (int k = tid; k < K; k += T8) {
+        sc[k] = p.scale[k];
+        sh[k] = p.shift[k];
+        smu[k] = STATS ? p.mean[k] : 0.f;
+        sis[k] = STATS ? p.invstd[k] : 0.f;
+    }
+    for (int i = tid; i < N * K / 8; i += T8) {   // W3 (N, K) -> padded LDS rows
+        const int n = i / (K / 8), kc = (i % (K / 8)) * 8;
+        *reinterpret_cast<bf16x8*>(&W3s[n * LDW + kc]) = *reinterpret_cast<const bf16x8*>(p.W + (size_t)n * K + kc);
+    }
+    const int kbz = (wave & 3) * 32, rbz = wave >> 2;   // dz: channel block, row block
+    bf16x8 wt[NS];   // W3^T fragments: lane row k = kbz + r32, channels in col_operand's order
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            wt[s][j] = p.W[(size_t)(16 * s + 8 * (j >> 2) + 4 * h + (j & 3)) * K + kbz + r32];
+    const int ny = wave * 32 + r32;   // y3 column / dW3 row of this lane
+    const float cA = p.cA[ny], cB = p.cB[ny], cC = p.cC[ny];
+    float st1[STATS ? 16 : 1], st2[STATS ? 16 : 1];
+#pragma unroll
+    for (int i = 0; i < (STATS ? 16 : 1); ++i) st1[i] = st2[i] = 0.f;
+    f32x16 dw[K / 32];
+#pragma unroll
+    for (int b = 0; b < K / 32; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dw[b][i] = 0.f;
+
+    const int ntiles = p.R / kTile;
+    constexpr int CH = kTile * K / 8 / T8;
+    static_assert(CH * T8 * 8 == kTile * K, "tile chunks");
+    bf16x8 pre[CH];
+    auto fetch = [&](int tile) {
+        const size_t row0 = (size_t)tile * kTile;
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const int ch = tid + c * T8;
+            const int row = ch / (K / 8), kc = (ch % (K / 8)) * 8;
+            pre[c] = *reinterpret_cast<const bf16x8*>(p.yprev + (row0 + row) * K + kc);
+        }
+    };
+    if (blockIdx.x < ntiles) fetch(blockIdx.x);
+    __syncthreads();
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const size_t row0 = (size_t)tile * kTile;
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const int ch = tid + c * T8;
+            const int row = ch / (K / 8), kc = (ch % (K / 8)) * 8;
+            bf16x8 z;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                z[j] = (bf16)fmaxf(fmaf(sc[kc + j], (float)pre[c][j], sh[kc + j]), 0.f);
+            *reinterpret_cast<bf16x8*>(&As[row * LDK + kc]) = z;
+            if constexpr (STATS) *reinterpret_cast<bf16x8*>(&Ys[row * LDK + kc]) = pre[c];
+        }
+        // the pooled gradient of this lane's column (issued before the barrier)
+        float gv[2];
+        int sv[2];
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+            const size_t pc = (p.S == 64 ? (size_t)tile : (size_t)tile * 2 + rb) * N + ny;
+            sv[rb] = p.isel[pc] + (p.S == 64 ? 0 : 32 * rb);
+            gv[rb] = p.gsel[pc];
+        }
+        __syncthreads();
+        if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);   // in flight below
+
+        // y3 = z W3^T for columns 32w.., then dy3 -> DsT
+        {
+            f32x16 acc[2];
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[rb][i] = 0.f;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const bf16x8 b = *reinterpret_cast<const bf16x8*>(&W3s[ny * LDW + 16 * s + 8 * h]);
+#pragma unroll
+                for (int rb = 0; rb < 2; ++rb) {
+                    const bf16x8 a = *reinterpret_cast<const bf16x8*>(&As[(rb * 32 + r32) * LDK + 16 * s + 8 * h]);
+                    acc[rb] = mfma(a, b, acc[rb]);
+                }
+            }
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {   // rows rb*32 + 8q + 4h + (0..3)
+                    bf16x4 d4;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int row = rb * 32 + 8 * q + 4 * h + j;
+                        const float y = (float)(bf16)acc[rb][4 * q + j];
+                        const float gi = row == sv[rb] ? gv[rb] : 0.f;
+                        d4[j] = (bf16)fmaf(cA, gi, fmaf(cB, y, cC));
+                    }
+                    *reinterpret_cast<bf16x4*>(&DsT[ny * LDR + rb * 32 + 8 * q + 4 * h]) = d4;
+                }
+            }
+        }
+        __syncthreads();
+
+        // dz^T = W3^T dy3^T for channels kbz.., rows rbz*32.. -> HBM
+        {
+            f32x16 acc;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) acc = mfma(wt[s], col_operand(DsT, LDR, lane, rbz * 32, s), acc);
+            const int row = rbz * 32 + r32;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int k = kbz + 8 * g + 4 * h;
+                bf16x4 o;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) o[j] = (bf16)acc[4 * g + j];
+                *reinterpret_cast<bf16x4*>(p.dz + (row0 + row) * K + k) = o;
+                if constexpr (STATS) {   // bn_relu_bwd pass 0 on the stored values
+                    const bf16x4 y4 = *reinterpret_cast<const bf16x4*>(&Ys[row * LDK + k]);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const float yy = (float)y4[j];
+                        const float dt = fmaf(sc[k + j], yy, sh[k + j]) > 0.f ? (float)o[j] : 0.f;
+                        st1[4 * g + j] += dt;
+                        st2[4 * g + j] = fmaf(dt, (yy - smu[k + j]) * sis[k + j], st2[4 * g + j]);
+                    }
+                }
+            }
+        }
+        // dW3 rows 32w.. += dy3^T z over this tile's rows
+#pragma unroll
+        for (int s = 0; s < kTile / 16; ++s) {
+            const bf16* dn = DsT + ny * LDR + 16 * s + 4 * h;
+            const bf16x4 lo = *reinterpret_cast<const bf16x4*>(dn);
+            const bf16x4 hi = *reinterpret_cast<const bf16x4*>(dn + 8);
+            const bf16x8 ad = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+            for (int b = 0; b < K / 32; ++b) dw[b] = mfma(ad, col_operand(As, LDK, lane, 32 * b, s), dw[b]);
+        }
+        __syncthreads();   // As / DsT / Ys are rewritten by the next tile
+    }
+    if constexpr (STATS) {
+        // the row-block-1 waves hand their partials to the row-block-0 waves of the same channels
+        float* xs = reinterpret_cast<float*>(As);   // (4 channel blocks, 64 lanes, 32) floats
+        if (rbz == 1)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                xs[((wave & 3) * 64 + lane) * 32 + i] = st1[i];
+                xs[((wave & 3) * 64 + lane) * 32 + 16 + i] = st2[i];
+            }
+        __syncthreads();
+        if (rbz == 0) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                double s1 = (double)st1[i] + (double)xs[(wave * 64 + lane) * 32 + i];
+                double s2 = (double)st2[i] + (double)xs[(wave * 64 + lane) * 32 + 16 + i];
+#pragma unroll
+                for (int o = 16; o > 0; o >>= 1) {
+                    s1 += __shfl_xor(s1, o, 64);
+                    s2 += __shfl_xor(s2, o, 64);
+                }
+                if (r32 == 0) {
+                    const int k = kbz + 8 * (i >> 2) + 4 * h + (i & 3);
+                    p.stats[(size_t)blockIdx.x * 2 * K + k] = s1;
+                    p.stats[(size_t)blockIdx.x * 2 * K + K + k] = s2;
+                }
+            }
+        }
+    }
+    // dW3 partial: element (b, i) = dW[n][k], n = 32w + (i&3) + 8(i>>2) + 4h, k = 32b + r32
+    float* out = p.dwpart + (size_t)blockIdx.x * N * K;
+#pragma unroll
+    for (int b = 0; b < K / 32; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int n = wave * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+            out[(size_t)n * K + 32 * b + r32] = dw[b][i];
+        }
+}
+
 // The middle layer's backward in one pass (sa_dy2_fused_kernel), after the pooled layer's
 // (which produced dz2 and this layer's BN-backward coefficients cA2 / cB2 / cC2):
 //   per 64-row tile:  z1 = relu(a1*y1 + b1) -> LDS (and raw y1 for the statistics)
@@ -543,12 +753,21 @@ extern "C" int ov3d_sa_dy_fused(const void* yprev, const float* scale, const flo
         return OV3D_EINVAL;
     DyFusedArgs a{(const bf16*)yprev, scale, shift, (const bf16*)W, R, S, gsel, isel, cA, cB, cC,
                   (bf16*)dz, dwpart, mean, invstd, stats};
-    if (stats)
-        hipLaunchKernelGGL((sa_dy_fused_kernel<128, 256, true>), dim3(nwg), dim3(kThreads), 0,
+    static const bool four = getenv("OV3D_SA_DY4") != nullptr;   // A/B: the 4-wave kernel
+    if (four) {
+        if (stats)
+            hipLaunchKernelGGL((sa_dy_fused_kernel<128, 256, true>), dim3(nwg), dim3(kThreads), 0,
+                               ov3d_stream(stream), a);
+        else
+            hipLaunchKernelGGL((sa_dy_fused_kernel<128, 256, false>), dim3(nwg), dim3(kThreads), 0,
+                               ov3d_stream(stream), a);
+    } else if (stats) {
+        hipLaunchKernelGGL((sa_dy8_kernel<128, 256, true>), dim3(nwg), dim3(512), 0,
                            ov3d_stream(stream), a);
-    else
-        hipLaunchKernelGGL((sa_dy_fused_kernel<128, 256, false>), dim3(nwg), dim3(kThreads), 0,
+    } else {
+        hipLaunchKernelGGL((sa_dy8_kernel<128, 256, false>), dim3(nwg), dim3(512), 0,
                            ov3d_stream(stream), a);
+    }
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }
