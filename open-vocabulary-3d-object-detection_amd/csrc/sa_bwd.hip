@@ -395,8 +395,10 @@ __global__ __launch_bounds__(512, 1) void sa_dy8_kernel(DyFusedArgs p) {
     };
     if (blockIdx.x < ntiles) fetch(blockIdx.x);
     __syncthreads();
+    PROBE_DECL
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const size_t row0 = (size_t)tile * kTile;
+        PROBE(0);
 #pragma unroll
         for (int c = 0; c < CH; ++c) {
             const int ch = tid + c * T8;
@@ -417,7 +419,9 @@ __global__ __launch_bounds__(512, 1) void sa_dy8_kernel(DyFusedArgs p) {
             sv[rb] = p.isel[pc] + (p.S == 64 ? 0 : 32 * rb);
             gv[rb] = p.gsel[pc];
         }
+        PROBE(1);
         __syncthreads();
+        PROBE(2);
         if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);   // in flight below
 
         // y3 = z W3^T for columns 32w.., then dy3 -> DsT
@@ -452,7 +456,9 @@ __global__ __launch_bounds__(512, 1) void sa_dy8_kernel(DyFusedArgs p) {
                 }
             }
         }
+        PROBE(3);
         __syncthreads();
+        PROBE(4);
 
         // dz^T = W3^T dy3^T for channels kbz.., rows rbz*32.. -> HBM
         {
@@ -481,6 +487,7 @@ __global__ __launch_bounds__(512, 1) void sa_dy8_kernel(DyFusedArgs p) {
                 }
             }
         }
+        PROBE(5);
         // dW3 rows 32w.. += dy3^T z over this tile's rows
 #pragma unroll
         for (int s = 0; s < kTile / 16; ++s) {
@@ -491,8 +498,11 @@ __global__ __launch_bounds__(512, 1) void sa_dy8_kernel(DyFusedArgs p) {
 #pragma unroll
             for (int b = 0; b < K / 32; ++b) dw[b] = mfma(ad, col_operand(As, LDK, lane, 32 * b, s), dw[b]);
         }
+        PROBE(6);
         __syncthreads();   // As / DsT / Ys are rewritten by the next tile
+        PROBE(7);
     }
+    PROBE_END;
     if constexpr (STATS) {
         // the row-block-1 waves hand their partials to the row-block-0 waves of the same channels
         float* xs = reinterpret_cast<float*>(As);   // (4 channel blocks, 64 lanes, 32) floats

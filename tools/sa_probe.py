@@ -1,4 +1,5 @@
-"""Phase stamps of the SA layer-3 backward kernel (sa_dy_fused_kernel) on the GPU.
+"""Phase stamps of the SA layer-3 backward kernel (sa_dy8_kernel; OV3D_SA_DY4=1: the 4-wave
+sa_dy_fused_kernel) on the GPU.
 
     python tools/sa_probe.py build     # (CPU) tools/probe/libov3d_saprobe.so, sa_bwd.hip with -DOV3D_SA_PROBE
     python tools/sa_probe.py run       # (GPU) one eager SUN training step, per-phase cycles per tile
@@ -50,13 +51,14 @@ def run():
         bench.train_step(model, crit, opt, batch, args, torch.bfloat16)
     torch.cuda.synchronize()
     nwg = sa_fused.NWG_DY_FUSED
-    dbg = torch.zeros(nwg * 4 * 8, dtype=torch.int64, device=dev)
+    waves = 4 if os.environ.get("OV3D_SA_DY4") else 8
+    dbg = torch.zeros(nwg * waves * 8, dtype=torch.int64, device=dev)
     lib.ov3d_sa_probe_set.argtypes = [ctypes.c_void_p]
     lib.ov3d_sa_probe_set(dbg.data_ptr())
     bench.train_step(model, crit, opt, batch, args, torch.bfloat16)
     torch.cuda.synchronize()
     lib.ov3d_sa_probe_set(None)
-    d = dbg.view(nwg, 4, 8).double().cpu()
+    d = dbg.view(nwg, waves, 8).double().cpu()
     tiles = (8 * 2048 * 64 // 64) / nwg
     per = (d.mean((0, 1)) / tiles).tolist()
     res = {"tiles_per_wg": tiles, "cycles_per_tile_by_phase": dict(zip(PHASES, [round(x) for x in per])),
