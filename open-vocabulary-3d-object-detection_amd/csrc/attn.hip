@@ -31,6 +31,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int D = 64;     // head dim
 constexpr int KB = 64;    // keys per LDS tile
@@ -87,8 +90,14 @@ __device__ __forceinline__ uint32_t mix24(uint32_t x) {
 
 // one 32-bit hash per (query, key pair k>>1): its low half decides the even key, the
 // high half the odd key (keep iff half >= thresh, thresh = round(p * 2^16))
+constexpr uint32_t kPairMul = 0x27D4EB2Fu;
 __device__ __forceinline__ uint32_t drop_pair(uint32_t qbase, uint32_t kpair) {
-    return mix24(qbase + kpair * 0x27D4EB2Fu);
+    return mix24(qbase + kpair * kPairMul);
+}
+
+// two fp32 -> two bf16 in one dword (one v_cvt_pk_bf16_f32), the even key in the low half
+__device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
 }
 __device__ __forceinline__ bool drop_keep(uint32_t qbase, uint32_t k, uint32_t thresh) {
     const uint32_t hsh = drop_pair(qbase, k >> 1);
@@ -108,6 +117,21 @@ constexpr float RESCALE_THR = 8.f;
 
 // split-K merges with at most this many key splits load every partial up front
 constexpr int kMaxCombine = 16;
+
+#ifdef OV3D_ATTN_PROBE
+// diagnostic build only (tools/attn_probe_phases.py): per-wave s_memtime totals of the tile
+// phases of attn_fwd_kernel
+__device__ unsigned long long* g_attn_probe;
+#define PROBE_DECL unsigned long long pr_t = __builtin_amdgcn_s_memtime(), pr_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PROBE(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); pr_acc[i] += t_ - pr_t; pr_t = t_; } while (0)
+#define PROBE_END do { if ((threadIdx.x & 63) == 0 && g_attn_probe) { \
+    unsigned long long* o_ = g_attn_probe + (((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 32 + (threadIdx.x >> 6) * 8; \
+    for (int i_ = 0; i_ < 8; ++i_) o_[i_] = pr_acc[i_]; } } while (0)
+#else
+#define PROBE_DECL
+#define PROBE(i) do { } while (0)
+#define PROBE_END do { } while (0)
+#endif
 
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -152,18 +176,29 @@ __global__ void __launch_bounds__(256, 3) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qrow + 16 * s + 8 * h);
     }
-    uint32_t qbase = 0;
-    if (DROP) qbase = drop_query_base(drop_head_mix(a.seed, a.site, bh), active ? q0 + r : 0);
+    // dropout hash input of key pair (kb >> 1) + 2h + c: qh + (kb >> 1) * kPairMul (wave-
+    // uniform, once per tile) + c * kPairMul (a constant per unrolled pair)
+    uint32_t qh = 0;
+    if (DROP) qh = drop_query_base(drop_head_mix(a.seed, a.site, bh), active ? q0 + r : 0) +
+                   (uint32_t)(2 * h) * kPairMul;
 
-    // cooperative tile load: 64 keys x 8 chunks of 8 bf16 = 512 chunks, 2 per thread
+    // cooperative tile load: 64 keys x 8 chunks of 8 bf16 = 512 chunks, 2 per thread; the
+    // per-thread offsets of key tid>>3 are formed once, a tile adds kb * B * s (scalar unit)
     bf16x8 kr[2], vr[2];
+    const size_t rowk = (size_t)a.B * a.sk, rowv = (size_t)a.B * a.sv;
+    const size_t k0off = (size_t)b * a.sk + hh * D + 8 * (tid & 7) + (size_t)(tid >> 3) * rowk;
+    const size_t v0off = (size_t)b * a.sv + hh * D + 8 * (tid & 7) + (size_t)(tid >> 3) * rowv;
     auto load = [&](int kb) {
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-            const int idx = tid + 256 * c, key = kb + (idx >> 3), ch = idx & 7;
-            const int kk = key < a.Lk ? key : a.Lk - 1;
-            kr[c] = *reinterpret_cast<const bf16x8*>(a.k + ((size_t)kk * a.B + b) * a.sk + hh * D + 8 * ch);
-            vr[c] = *reinterpret_cast<const bf16x8*>(a.v + ((size_t)kk * a.B + b) * a.sv + hh * D + 8 * ch);
+            const int key = kb + (tid >> 3) + 32 * c;
+            size_t ko = k0off + (size_t)(kb + 32 * c) * rowk, vo = v0off + (size_t)(kb + 32 * c) * rowv;
+            if (key >= a.Lk) {   // past the last key (partial tile): repeat the last row
+                ko -= (size_t)(key - (a.Lk - 1)) * rowk;
+                vo -= (size_t)(key - (a.Lk - 1)) * rowv;
+            }
+            kr[c] = *reinterpret_cast<const bf16x8*>(a.k + ko);
+            vr[c] = *reinterpret_cast<const bf16x8*>(a.v + vo);
         }
     };
     auto store = [&](int buf) {
@@ -185,10 +220,12 @@ __global__ void __launch_bounds__(256, 3) attn_fwd_kernel(AttnArgs a) {
         store(0);
     }
     __syncthreads();
+    PROBE_DECL
     int buf = 0;
     for (int kb = kbeg; kb < kend; kb += KB, buf ^= 1) {
         const bool more = kb + KB < kend;
         if (!active && more) load(kb + KB);
+        PROBE(0);
         if (active) {
             const bf16* K = Ks[buf];
             const bf16* V = Vs[buf];
@@ -221,6 +258,7 @@ __global__ void __launch_bounds__(256, 3) attn_fwd_kernel(AttnArgs a) {
             // earlier, their address registers collide with the operand registers and the
             // compiler waits for the loads inside the score MFMAs
             if (more) load(kb + KB);
+            PROBE(1);
             // keys past Lk (last partial tile) do not take part
             const int nvalid = kend - kb;
             if (nvalid < KB) {
@@ -236,6 +274,7 @@ __global__ void __launch_bounds__(256, 3) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
                 for (int i = 0; i < 16; ++i) mx = fmaxf(mx, st[t][i]);
             mx = fmaxf(mx, __shfl_xor(mx, 32));
+            PROBE(2);
             // deferred rescale (T13): keep the stale max unless some query's max grew a lot
             if (__any((mx - m) * a.scale2 > RESCALE_THR)) {
                 const float mnew = fmaxf(m, mx);
@@ -248,37 +287,50 @@ __global__ void __launch_bounds__(256, 3) attn_fwd_kernel(AttnArgs a) {
                     o[1][i] *= alpha;
                 }
             }
+            // p = exp2(s * scale2 - m * scale2), one bf16 pack per key pair; dropout zeroes p
+            // after the row sum.  Scalar f32 ops on purpose: packed v_pk_fma / v_pk_add issue
+            // slower than two scalar ops beside the MFMAs (MI355X_MICROARCH.md cycle table;
+            // the file is built with -fno-slp-vectorize)
             const float mb = m * a.scale2;
-            float rs = 0.f;
-            bf16x8 pf[2][2];
+            const uint32_t hb = qh + (uint32_t)(kb >> 1) * kPairMul;
+            float rs0 = 0.f, rs1 = 0.f;
+            u32x4 pw[2][2];
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int i = 0; i < 16; i += 2) {
                     float p0 = fast_exp2(fmaf(st[t][i], a.scale2, -mb));
                     float p1 = fast_exp2(fmaf(st[t][i + 1], a.scale2, -mb));
-                    rs += p0 + p1;
+                    rs0 += p0;
+                    rs1 += p1;
                     if (DROP) {
-                        const int kk = kb + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;   // even
-                        const uint32_t hsh = drop_pair(qbase, (uint32_t)kk >> 1);
+                        // key 32t + (i&3) + 8(i>>2) + 4h (even): pair 16t + (i&3)/2 + 4(i>>2) + 2h
+                        const uint32_t c = 16 * t + ((i & 3) >> 1) + 4 * (i >> 2);
+                        const uint32_t hsh = mix24(hb + c * kPairMul);
                         // 1/(1-p) is applied once to the output (keep_scale below)
                         p0 = (hsh & 0xffffu) >= a.thresh ? p0 : 0.f;
                         p1 = (hsh >> 16) >= a.thresh ? p1 : 0.f;
                     }
-                    pf[t][i >> 3][i & 7] = (bf16)p0;
-                    pf[t][i >> 3][(i & 7) + 1] = (bf16)p1;
+                    pw[t][i >> 3][(i & 7) >> 1] = pack_bf16(p0, p1);
                 }
-            l += rs;
+            l += rs0 + rs1;
+            PROBE(3);
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
-                for (int s = 0; s < 2; ++s)
+                for (int s = 0; s < 2; ++s) {
+                    const bf16x8 pf = __builtin_bit_cast(bf16x8, pw[t][s]);
 #pragma unroll
-                    for (int dt = 0; dt < 2; ++dt) o[dt] = mfma(va[dt][t][s], pf[t][s], o[dt]);
+                    for (int dt = 0; dt < 2; ++dt) o[dt] = mfma(va[dt][t][s], pf, o[dt]);
+                }
         }
+        PROBE(4);
         if (more) store(buf ^ 1);
+        PROBE(5);
         __syncthreads();
+        PROBE(6);
     }
+    PROBE_END;
     if (!active) return;
     const float ltot = l + __shfl_xor(l, 32);
     const int q = q0 + r;
@@ -384,6 +436,7 @@ struct AttnBwdArgs {
     float scale;
 };
 
+template <bool DROP>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
     const AttnArgs& a = A.f;
     __shared__ __attribute__((aligned(16))) bf16 Ks[2][KB * LDK];
@@ -394,7 +447,6 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
     const int q0 = blockIdx.x * (4 * QW) + wave * QW;
     const bool active = q0 < a.Lq;
     const int qi = active ? q0 + r : 0;
-    const bool drop = a.thresh != 0;
 
     bf16x8 qf[4], df[4];
     float dsum = 0.f;
@@ -414,8 +466,9 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
     dsum += __shfl_xor(dsum, 32);
     const float lse2 = active ? a.lse[(size_t)bh * a.Lq + qi] : 0.f;
     if (active && h == 0 && blockIdx.z == 0) A.dvec[(size_t)bh * a.Lq + qi] = dsum;
-    uint32_t qbase = 0;
-    if (drop) qbase = drop_query_base(drop_head_mix(a.seed, a.site, bh), qi);
+    // dropout hash input of key pair (kb >> 1) + 2h + c (see attn_fwd_kernel)
+    uint32_t qh = 0;
+    if (DROP) qh = drop_query_base(drop_head_mix(a.seed, a.site, bh), qi) + (uint32_t)(2 * h) * kPairMul;
 
     bf16x8 kr[2], vr[2];
     // row (key) r of the tile starts at r * B * s: the per-thread offsets of key tid>>3 are
@@ -463,7 +516,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
             const bf16* K = Ks[buf];
             const bf16* V = Vs[buf];
             const int nvalid = kend - kb;
-            bf16x8 dsf[2][2];
+            const uint32_t hb = qh + (uint32_t)(kb >> 1) * kPairMul;
+            u32x4 dsw[2][2];
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
                 f32x16 st, dpt;
@@ -476,20 +530,26 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
                     st = mfma(ka, qf[s], st);
                     dpt = mfma(va, df[s], dpt);
                 }
+                // keys past Lk (last partial tile, wave-uniform branch): score -inf -> P = 0
+                if (nvalid < KB) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        if (32 * t + (i & 3) + 8 * (i >> 2) + 4 * h >= nvalid) st[i] = -INFINITY;
+                }
 #pragma unroll
                 for (int i = 0; i < 16; i += 2) {
-                    const int kr0 = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;   // even
-                    float p0 = kr0 < nvalid ? fast_exp2(fmaf(st[i], a.scale2, -lse2)) : 0.f;
-                    float p1 = kr0 + 1 < nvalid ? fast_exp2(fmaf(st[i + 1], a.scale2, -lse2)) : 0.f;
+                    const float p0 = fast_exp2(fmaf(st[i], a.scale2, -lse2));
+                    const float p1 = fast_exp2(fmaf(st[i + 1], a.scale2, -lse2));
                     float dp0 = dpt[i], dp1 = dpt[i + 1];
-                    if (drop) {
-                        const uint32_t hsh = drop_pair(qbase, (uint32_t)(kb + kr0) >> 1);
+                    if (DROP) {
+                        const uint32_t c = 16 * t + ((i & 3) >> 1) + 4 * (i >> 2);
+                        const uint32_t hsh = mix24(hb + c * kPairMul);
                         dp0 = (hsh & 0xffffu) >= a.thresh ? dp0 : 0.f;
                         dp1 = (hsh >> 16) >= a.thresh ? dp1 : 0.f;
                     }
                     // P (Z dP~ / (1-p) - D): the scale rides in the fma (exact for p = 0)
-                    dsf[t][i >> 3][i & 7] = (bf16)(p0 * fmaf(dp0, a.keep_scale, -dsum));
-                    dsf[t][i >> 3][(i & 7) + 1] = (bf16)(p1 * fmaf(dp1, a.keep_scale, -dsum));
+                    dsw[t][i >> 3][(i & 7) >> 1] = pack_bf16(p0 * fmaf(dp0, a.keep_scale, -dsum),
+                                                             p1 * fmaf(dp1, a.keep_scale, -dsum));
                 }
             }
 #pragma unroll
@@ -497,7 +557,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
 #pragma unroll
                 for (int t = 0; t < 2; ++t)
 #pragma unroll
-                    for (int s = 0; s < 2; ++s) dqt[dt] = mfma(v_operand(K, lane, dt, t, s), dsf[t][s], dqt[dt]);
+                    for (int s = 0; s < 2; ++s)
+                        dqt[dt] = mfma(v_operand(K, lane, dt, t, s), __builtin_bit_cast(bf16x8, dsw[t][s]), dqt[dt]);
         }
         if (more) store(buf ^ 1);
         __syncthreads();
@@ -553,6 +614,7 @@ __global__ void __launch_bounds__(256) attn_dq_combine_kernel(AttnBwdArgs A) {
 }
 
 // a lane owns a key: S = Q K^T tiles (32 queries x 32 keys) with the query on the registers
+template <bool DROP>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
     const AttnArgs& a = A.f;
     constexpr int QB = 64;   // queries per LDS tile
@@ -567,8 +629,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
     const int k0 = blockIdx.x * (4 * 32) + wave * 32;
     const bool active = k0 < a.Lk;
     const int ki = active ? min(k0 + r, a.Lk - 1) : 0;
-    const bool drop = a.thresh != 0;
-    const uint32_t hmix = drop ? drop_head_mix(a.seed, a.site, bh) : 0u;
+    const uint32_t hmix = DROP ? drop_head_mix(a.seed, a.site, bh) : 0u;
 
     bf16x8 kf[4], vf[4];
     {
@@ -605,7 +666,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
             // queries past Lq: lse = +inf -> P = 0
             lr = qq < a.Lq ? a.lse[(size_t)bh * a.Lq + qc] : INFINITY;
             dvr = A.dvec[(size_t)bh * a.Lq + qc];
-            if (drop) zr = drop_query_base(hmix, (uint32_t)qq);
+            if (DROP) zr = drop_query_base(hmix, (uint32_t)qq);
         }
     };
     auto store = [&](int buf) {
@@ -625,6 +686,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) dkt[0][i] = dkt[1][i] = dvt[0][i] = dvt[1][i] = 0.f;
     const bool kvalid = active && (k0 + r) < a.Lk;
+    const float s0 = kvalid ? 0.f : -INFINITY;
     load(0);
     store(0);
     __syncthreads();
@@ -637,9 +699,14 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
             const bf16* DO = Ds[buf];
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
+                // a lane past the last key (its K row is a copy of the last one) starts its
+                // scores at -inf: P = exp2(-inf) = 0 without a per-element select
                 f32x16 st, dpt;
 #pragma unroll
-                for (int i = 0; i < 16; ++i) st[i] = dpt[i] = 0.f;
+                for (int i = 0; i < 16; ++i) {
+                    st[i] = s0;
+                    dpt[i] = 0.f;
+                }
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
                     const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Q + (32 * u + r) * LDK + 16 * s + 8 * h);
@@ -657,7 +724,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
                     // keys k0+r and k0+(r^1) share one pair hash per query: this lane hashes
                     // rows j = (r&1), (r&1)+2 and takes the other two from its neighbour
                     uint32_t hsh[4] = {0u, 0u, 0u, 0u};
-                    if (drop) {
+                    if (DROP) {
                         const int j0 = r & 1;
                         const uint32_t kp2 = (uint32_t)(k0 + r) >> 1;
                         const uint32_t ha = drop_pair(Zb[buf][qrow + j0], kp2);
@@ -671,9 +738,9 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int i = 4 * g + j;
-                        float p = kvalid ? fast_exp2(fmaf(st[i], a.scale2, -lv[j])) : 0.f;
+                        const float p = fast_exp2(fmaf(st[i], a.scale2, -lv[j]));
                         float pd = p, dp = dpt[i];
-                        if (drop) {
+                        if (DROP) {
                             const bool kp = ((r & 1) ? (hsh[j] >> 16) : (hsh[j] & 0xffffu)) >= a.thresh;
                             pd = kp ? p : 0.f;   // 1/(1-p) applied to dV once at the end
                             dp = kp ? dp : 0.f;
@@ -766,6 +833,12 @@ extern "C" int ov3d_attn_fwd(const void* q, const void* k, const void* v, long l
     return OV3D_OK;
 }
 
+#ifdef OV3D_ATTN_PROBE
+extern "C" int ov3d_attn_probe_set(unsigned long long* p) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_attn_probe), &p, sizeof(p)) == hipSuccess ? 0 : 1;
+}
+#endif
+
 /* workspace floats needed by ov3d_attn_fwd for a given split count */
 extern "C" long long ov3d_attn_fwd_workspace(int B, int H, int Lq, int Lk, int nsplit) {
     if (nsplit <= 1) return 0;
@@ -826,13 +899,21 @@ extern "C" int ov3d_attn_bwd(const void* q, const void* k, const void* v, long l
     a.nsplit = nsplit;
     a.part_o = workspace;
     hipStream_t st = ov3d_stream(stream);
-    attn_bwd_dq_kernel<<<dim3((Lq + 4 * QW - 1) / (4 * QW), B * H, nsplit), 256, 0, st>>>(A);
+    const dim3 gq((Lq + 4 * QW - 1) / (4 * QW), B * H, nsplit);
+    if (a.thresh)
+        attn_bwd_dq_kernel<true><<<gq, 256, 0, st>>>(A);
+    else
+        attn_bwd_dq_kernel<false><<<gq, 256, 0, st>>>(A);
     OV3D_LAUNCH_CHECK();
     if (nsplit > 1) {
         attn_dq_combine_kernel<<<ov3d_cdiv((long long)B * H * Lq * (D / 4), 256), 256, 0, st>>>(A);
         OV3D_LAUNCH_CHECK();
     }
-    attn_bwd_dkdv_kernel<<<dim3((Lk + 127) / 128, B * H), 256, 0, st>>>(A);
+    const dim3 gk((Lk + 127) / 128, B * H);
+    if (a.thresh)
+        attn_bwd_dkdv_kernel<true><<<gk, 256, 0, st>>>(A);
+    else
+        attn_bwd_dkdv_kernel<false><<<gk, 256, 0, st>>>(A);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }
