@@ -273,23 +273,27 @@ int ov3d_im2col3x3(const void* in, int elem_bytes, int N, int H, int W, int C, i
  * layout: element (l, b, h, d) at ptr[(l*B + b)*stride + h*64 + d] (strides in
  * elements), so projection outputs are read in place.  Lq % 32 == 0.
  * Dropout: keep(q, k) from a counter-based hash of (*seed, site, b*H + h, q, k>>1)
- * (16-bit half per key, keep iff half >= round(p * 65536)), regenerated in the
- * backward.  lse (B*H, Lq) f32 = log2-domain logsumexp saved for the backward.
- * nsplit > 1 splits the keys over workgroups (decoder: 128 queries) and needs
- * ov3d_attn_fwd_workspace() floats of workspace. */
+ * (signed 16-bit half per key, keep iff (half ^ 0x8000) >= round(p * 65536)).  The
+ * forward stores the drop bits (dropbits, ov3d_attn_dropbits_words() uint32 words, needed
+ * when p > 0) and the backward reads them.  lse (B*H, Lq) f32 = log2-domain logsumexp
+ * saved for the backward.  nsplit > 1 splits the keys over workgroups (decoder: 128
+ * queries) and needs ov3d_attn_fwd_workspace() floats of workspace. */
 int ov3d_attn_fwd(const void* q, const void* k, const void* v, long long sq, long long sk,
                   long long sv, int B, int H, int Lq, int Lk, float scale, float dropout_p,
                   const int64_t* seed, int site, void* o, long long so, float* lse,
-                  float* workspace, int nsplit, void* stream);
+                  uint32_t* dropbits, float* workspace, int nsplit, void* stream);
 long long ov3d_attn_fwd_workspace(int B, int H, int Lq, int Lk, int nsplit);
-/* Backward: dq/dk/dv rows (same layout, bf16) from o, dout (stride sdo), lse;
- * dvec (B*H, Lq) f32 scratch receives D = rowsum(dout * o).  nsplit > 1 splits the
- * dQ key loop over workgroups (fp32 partials in `workspace`, sized as for the forward
- * by ov3d_attn_fwd_workspace). */
+/* uint32 words of the drop bits: query-major [nkt][B*H][Lq][2] then key-major
+ * [Lq/32][B*H][nkt*64], nkt = ceil(Lk / 64); 0 for invalid shapes. */
+long long ov3d_attn_dropbits_words(int B, int H, int Lq, int Lk);
+/* Backward: dq/dk/dv rows (same layout, bf16) from o, dout (stride sdo), lse and the
+ * forward's drop bits; dvec (B*H, Lq) f32 scratch receives D = rowsum(dout * o).
+ * nsplit > 1 splits the dQ key loop over workgroups (fp32 partials in `workspace`, sized
+ * as for the forward by ov3d_attn_fwd_workspace). */
 int ov3d_attn_bwd(const void* q, const void* k, const void* v, long long sq, long long sk,
                   long long sv, const void* o, long long so, const void* dout, long long sdo,
                   const float* lse, int B, int H, int Lq, int Lk, float scale, float dropout_p,
-                  const int64_t* seed, int site, float* dvec, void* dq, long long sdq, void* dk,
+                  const uint32_t* dropbits, float* dvec, void* dq, long long sdq, void* dk,
                   long long sdk, void* dv, long long sdv, float* workspace, int nsplit,
                   void* stream);
 

@@ -46,8 +46,8 @@ _SIGS = {
     "ov3d_clip_preprocess": "plppiiifffffffipp",
     "ov3d_roi_align_fwd": "piiiiipiiifiiipp",
     "ov3d_im2col3x3": "piiiiiiipp",
-    "ov3d_attn_fwd": "pppllliiiiffpiplppip",
-    "ov3d_attn_bwd": "ppplllplplpiiiiffpipplplplpip",
+    "ov3d_attn_fwd": "pppllliiiiffpiplpppip",
+    "ov3d_attn_bwd": "ppplllplplpiiiiffppplplplpip",
     "ov3d_wgrad": "plpliiiplpppip",
     "ov3d_wgrad_group": "pipp",
     "ov3d_rows_bn_stats": "pillilipip",
@@ -87,6 +87,7 @@ _SIGS = {
     "ov3d_ap_curve": "plppiplppp",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
+                          "ov3d_attn_dropbits_words",
                           "ov3d_wgrad_workspace", "ov3d_wgrad_tiles", "ov3d_set_loss_desc_size",
                           "ov3d_resnorm_supported", "ov3d_resnorm_bwd_parts",
                           "ov3d_adamw_chunk", "ov3d_wgrad_group_workspace",
@@ -118,6 +119,8 @@ def load():
         lib.ov3d_sa_layer_supported.restype = ctypes.c_int
         lib.ov3d_attn_fwd_workspace.argtypes = [ctypes.c_int] * 5
         lib.ov3d_attn_fwd_workspace.restype = ctypes.c_longlong
+        lib.ov3d_attn_dropbits_words.argtypes = [ctypes.c_int] * 4
+        lib.ov3d_attn_dropbits_words.restype = ctypes.c_longlong
         lib.ov3d_wgrad_workspace.argtypes = [ctypes.c_int] * 4
         lib.ov3d_wgrad_workspace.restype = ctypes.c_longlong
         lib.ov3d_wgrad_tiles.argtypes = [ctypes.c_int] * 2

@@ -11,11 +11,12 @@ row l*B + b, column off + head*64 + d, so the heads are never permuted or copied
 the gradients are written into one buffer per source tensor the same way.
 
 Dropout randomness: keep(q, k) is a counter-based hash of (step seed, call site,
-b*H + h, q, k), regenerated in the backward instead of stored.  The step seed is a
-device int64 advanced once per training forward (``next_step``, captured by a hipGraph
-like any other kernel) and snapshotted for that forward; each op keeps the snapshot it
-used on its ctx, so its backward is right whatever forwards ran in between.  The call
-site is fixed per module.
+b*H + h, q, k).  The forward hashes once and stores the drop bits (two 1-bit-per-pair
+layouts, query-major for the dQ kernel and key-major for the dK/dV kernel: 16 + 16 MB per
+encoder layer), saved on the ctx like the logsumexp; the backward reads them.  The step
+seed is a device int64 advanced once per training forward (``next_step``, captured by a
+hipGraph like any other kernel) and snapshotted for that forward.  The call site is fixed
+per module.
 """
 import itertools
 
@@ -49,10 +50,10 @@ def _live(device):
 
 
 def _seed(device):
-    """The seed tensor of the CURRENT forward.  Every dropout site saves the object it got
-    here on its autograd ctx and its backward regenerates the masks from that object, never
-    from this function: a later forward (an EMA-teacher pass, forward-forward-backward)
-    takes a new snapshot and leaves the saved one untouched."""
+    """The seed tensor of the CURRENT forward.  Attention saves the drop bits it drew from it
+    on its autograd ctx (resnorm / FFN dropout save the seed object itself), so a backward
+    never reads this function: a later forward (an EMA-teacher pass,
+    forward-forward-backward) takes a new snapshot and leaves the saved masks untouched."""
     s = _SNAPS.get(device)
     if s is None:
         s = _live(device).clone()
@@ -105,17 +106,18 @@ class _Attention(torch.autograd.Function):
         ws_n = _native.load().ov3d_attn_fwd_workspace(B, H, Lq, Lk, nsplit)
         ws = torch.empty((max(ws_n, 1),), dtype=torch.float32, device=dev)
         seed = _seed(dev)
+        nbits = _native.load().ov3d_attn_dropbits_words(B, H, Lq, Lk) if dropout_p > 0 else 0
+        bits = torch.empty((max(nbits, 1),), dtype=torch.int32, device=dev)
         qp, sq = _rows(q, qo, E)
         kp, sk = _rows(k, ko, E)
         vp, sv = _rows(v, vo, E)
         fn = _native.load().ov3d_attn_fwd
         rc = fn(qp, kp, vp, sq, sk, sv, B, H, Lq, Lk, HEAD_DIM ** -0.5, float(dropout_p),
-                _native._ptr(seed), site, _native._ptr(o), E, _native._ptr(lse), _native._ptr(ws),
-                nsplit, _native._stream(q))
+                _native._ptr(seed), site, _native._ptr(o), E, _native._ptr(lse), _native._ptr(bits),
+                _native._ptr(ws), nsplit, _native._stream(q))
         if rc:
             raise _native.NativeError(f"ov3d_attn_fwd failed with status {rc}")
-        ctx.save_for_backward(*srcs, o, lse)
-        ctx.seed = seed   # this forward's snapshot: the backward regenerates the same masks
+        ctx.save_for_backward(*srcs, o, lse, bits)
         ctx.meta = (spec, dims, H, float(dropout_p), site, len(srcs))
         ctx.ext = ext
         return o
@@ -124,7 +126,7 @@ class _Attention(torch.autograd.Function):
     def backward(ctx, do):
         spec, (Lq, Lk, B), H, p, site, n = ctx.meta
         saved = ctx.saved_tensors
-        srcs, o, lse = saved[:n], saved[n], saved[n + 1]
+        srcs, o, lse, bits = saved[:n], saved[n], saved[n + 1], saved[n + 2]
         (qi, qo), (ki, ko), (vi, vo) = spec
         q, k, v = srcs[qi], srcs[ki], srcs[vi]
         E = H * HEAD_DIM
@@ -146,7 +148,7 @@ class _Attention(torch.autograd.Function):
         dvp, sdv = _rows(grads[vi], vo, E)
         rc = _native.load().ov3d_attn_bwd(
             qp, kp, vp, sq, sk, sv, _native._ptr(o), E, _native._ptr(do), E, _native._ptr(lse),
-            B, H, Lq, Lk, HEAD_DIM ** -0.5, p, _native._ptr(ctx.seed), site,
+            B, H, Lq, Lk, HEAD_DIM ** -0.5, p, _native._ptr(bits),
             _native._ptr(dvec), dqp, sdq, dkp, sdk, dvp, sdv, _native._ptr(ws), nsplit,
             _native._stream(q))
         if rc:

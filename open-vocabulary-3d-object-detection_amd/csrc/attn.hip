@@ -16,8 +16,13 @@
 // registers (its k order is the MFMA's row order); V^T's operand is read with
 // ds_read_b64_tr_b16 from the row-major V tile in LDS.
 //
-// Dropout: keep(q, k) = hash32(seed, site, b*H+h, q, k) >= p * 2^32, a counter-based
-// hash, so forward and backward regenerate the same mask without storing it.
+// Dropout: keep(q, k) from a counter-based hash of (seed, site, b*H+h, q, k>>1) (one 32-bit
+// hash per key pair, a signed 16-bit half per key).  The forward computes it once and stores
+// the DROP bits twice, 16 + 16 MB per encoder layer: query-major words (one per lane and
+// 64-key tile, the layout of attn_bwd_dq_kernel's lanes) and, after a 32 x 32 bit transpose
+// across the lanes, key-major words (32 queries of one key, the layout of
+// attn_bwd_dkdv_kernel's lanes); the backward reads bits instead of re-hashing (the hash was
+// half of each kernel's VALU issue).
 // Split-K (grid.z) serves the 128-query decoder attention: partial (O, m, l) per
 // key split, merged by attn_combine_kernel.
 #include <math.h>
@@ -34,6 +39,7 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int D = 64;     // head dim
 constexpr int KB = 64;    // keys per LDS tile
@@ -57,6 +63,9 @@ struct AttnArgs {
     float* part_o;         // split-K partials (nsplit, B*H, Lq, 64) unnormalised
     float* part_ml;        // (nsplit, B*H, Lq, 2): m*scale2, l
     int nsplit, keys_per_split;
+    uint32_t* wq;          // drop bits, query-major: [nkt][B*H][Lq][2] (see drop_word)
+    uint32_t* wk;          // drop bits, key-major:   [Lq/32][B*H][nkt*64]
+    int nkt;               // 64-key tiles = ceil(Lk / 64)
 };
 
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
@@ -89,27 +98,63 @@ __device__ __forceinline__ uint32_t mix24(uint32_t x) {
 }
 
 // one 32-bit hash per (query, key pair k>>1): its low half decides the even key, the
-// high half the odd key (keep iff half >= thresh, thresh = round(p * 2^16))
+// high half the odd key; keep iff int16(half) >= thresh - 32768 (thresh = round(p * 2^16)),
+// i.e. (half ^ 0x8000) >= thresh unsigned
 constexpr uint32_t kPairMul = 0x27D4EB2Fu;
-__device__ __forceinline__ uint32_t drop_pair(uint32_t qbase, uint32_t kpair) {
-    return mix24(qbase + kpair * kPairMul);
-}
 
 // two fp32 -> two bf16 in one dword (one v_cvt_pk_bf16_f32), the even key in the low half
 __device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
 }
-__device__ __forceinline__ bool drop_keep(uint32_t qbase, uint32_t k, uint32_t thresh) {
-    const uint32_t hsh = drop_pair(qbase, k >> 1);
-    return ((k & 1u) ? (hsh >> 16) : (hsh & 0xffffu)) >= thresh;
+
+// 0xFFFF in each 16-bit half of the pair hash whose key is DROPPED: a saturating packed
+// subtract of the signed threshold leaves the sign of (half - tsig), an arithmetic shift
+// spreads it (v_pk_sub_i16 clamp + v_pk_ashrrev_i16)
+__device__ __forceinline__ uint32_t drop_halves(uint32_t hsh, s16x2 tsig) {
+    const s16x2 d = __builtin_elementwise_sub_sat(__builtin_bit_cast(s16x2, hsh), tsig);
+    return __builtin_bit_cast(uint32_t, (s16x2)(d >> (s16x2){15, 15}));
 }
+
+// Drop words.  A lane (query q, half h) of a 64-key tile owns the 32 keys
+// kb + 32t + 2(m&1) + 8(m>>1) + 4h + e  (t, e in {0,1}, m in 0..7); bit 8t + m of its word is
+// the even key (e = 0), bit 16 + 8t + m the odd key.  drop_key(b, h) = that key's offset.
+__device__ __forceinline__ int drop_key(int b, int h) {
+    const int e = b >> 4, j = b & 15, t = j >> 3, m = j & 7;
+    return 32 * t + 2 * (m & 1) + 8 * (m >> 1) + 4 * h + e;
+}
+
+// value of lane ^ J within 32 lanes: DPP quad_perm for 1 and 2, ds_swizzle in bit-mask mode
+// (offset = xor_mask << 10 | or_mask << 5 | and_mask) above
+template <int J>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
+    if constexpr (J == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);
+    else if constexpr (J == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true);
+    else return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (J << 10) | 0x1F);
+}
+
+// one butterfly stage of a 32 x 32 bit-matrix transpose across lanes r = lane & 31 (rows)
+// and bits (columns): swap row-index bit J with column-index bit J
+template <int J, uint32_t MLOW>
+__device__ __forceinline__ uint32_t transpose_stage(uint32_t a, int r) {
+    const uint32_t p = lane_xor<J>(a);
+    const bool low = (r & J) == 0;
+    // low rows take the partner's bits c - J into columns with bit J set (rotl J), high
+    // rows its bits c + J into columns with bit J clear (rotr J)
+    const uint32_t rot = __builtin_amdgcn_alignbit(p, p, low ? 32 - J : J);
+    const uint32_t keep = low ? MLOW : ~MLOW;
+    return (a & keep) | (rot & ~keep);
+}
+
+__device__ __forceinline__ uint32_t transpose32(uint32_t a, int r) {
+    a = transpose_stage<16, 0x0000FFFFu>(a, r);
+    a = transpose_stage<8, 0x00FF00FFu>(a, r);
+    a = transpose_stage<4, 0x0F0F0F0Fu>(a, r);
+    a = transpose_stage<2, 0x33333333u>(a, r);
+    return transpose_stage<1, 0x55555555u>(a, r);
+}
+
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
-
-// value of lane ^ 1 (DPP quad_perm [1,0,3,2]: one VALU move, no LDS crossbar)
-__device__ __forceinline__ uint32_t lane_xor1(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);
-}
 
 // online-softmax rescale only when a query's running max grows by more than this
 // (log2 units): P stays <= 2^8 between rescales (cdna_hip_programming.md T13)
@@ -158,7 +203,7 @@ __device__ __forceinline__ bf16x8 v_operand(const bf16* Vs, int lane, int dt, in
 }
 
 template <bool DROP>
-__global__ void __launch_bounds__(256, 3) attn_fwd_kernel(AttnArgs a) {
+__global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     __shared__ __attribute__((aligned(16))) bf16 Ks[2][KB * LDK];
     __shared__ __attribute__((aligned(16))) bf16 Vs[2][KB * LDK];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -181,6 +226,16 @@ __global__ void __launch_bounds__(256, 3) attn_fwd_kernel(AttnArgs a) {
     uint32_t qh = 0;
     if (DROP) qh = drop_query_base(drop_head_mix(a.seed, a.site, bh), active ? q0 + r : 0) +
                    (uint32_t)(2 * h) * kPairMul;
+    // drop-word destinations: query-major word (kt, bh, q, h), key-major word (q0/32, bh, key)
+    uint32_t* const wq_lane = DROP ? a.wq + ((size_t)bh * a.Lq + q0 + r) * 2 + h : nullptr;
+    const size_t wq_tile = (size_t)gridDim.y * a.Lq * 2;
+    uint32_t* const wk_lane = DROP ? a.wk + ((size_t)(q0 >> 5) * gridDim.y + bh) * ((size_t)a.nkt * 64) +
+                                         drop_key(r, h) : nullptr;
+    uint32_t dw_prev = 0;   // drop word of the tile before this one
+    auto store_drop = [&](int kbp) {
+        wq_lane[(size_t)(kbp >> 6) * wq_tile] = dw_prev;
+        wk_lane[kbp] = transpose32(dw_prev, r);   // lane r: key drop_key(r, h), bit n = query q0 + n
+    };
 
     // cooperative tile load: 64 keys x 8 chunks of 8 bf16 = 512 chunks, 2 per thread; the
     // per-thread offsets of key tid>>3 are formed once, a tile adds kb * B * s (scalar unit)
@@ -258,6 +313,9 @@ __global__ void __launch_bounds__(256, 3) attn_fwd_kernel(AttnArgs a) {
             // earlier, their address registers collide with the operand registers and the
             // compiler waits for the loads inside the score MFMAs
             if (more) load(kb + KB);
+            // the previous tile's drop word goes out while the score MFMAs run: the lane
+            // transpose's swizzle round trips would otherwise sit on this tile's critical path
+            if (DROP && kb > kbeg) store_drop(kb - KB);
             PROBE(1);
             // keys past Lk (last partial tile) do not take part
             const int nvalid = kend - kb;
@@ -293,7 +351,10 @@ __global__ void __launch_bounds__(256, 3) attn_fwd_kernel(AttnArgs a) {
             // the file is built with -fno-slp-vectorize)
             const float mb = m * a.scale2;
             const uint32_t hb = qh + (uint32_t)(kb >> 1) * kPairMul;
+            const short ts = (short)((int)a.thresh - 32768);
+            const s16x2 tsig = {ts, ts};
             float rs0 = 0.f, rs1 = 0.f;
+            uint32_t dw = 0;   // this lane's drop word of the tile
             u32x4 pw[2][2];
 #pragma unroll
             for (int t = 0; t < 2; ++t)
@@ -303,17 +364,20 @@ __global__ void __launch_bounds__(256, 3) attn_fwd_kernel(AttnArgs a) {
                     float p1 = fast_exp2(fmaf(st[t][i + 1], a.scale2, -mb));
                     rs0 += p0;
                     rs1 += p1;
+                    uint32_t pk = pack_bf16(p0, p1);
                     if (DROP) {
                         // key 32t + (i&3) + 8(i>>2) + 4h (even): pair 16t + (i&3)/2 + 4(i>>2) + 2h
                         const uint32_t c = 16 * t + ((i & 3) >> 1) + 4 * (i >> 2);
-                        const uint32_t hsh = mix24(hb + c * kPairMul);
+                        const uint32_t dm = drop_halves(mix24(hb + c * kPairMul), tsig);
                         // 1/(1-p) is applied once to the output (keep_scale below)
-                        p0 = (hsh & 0xffffu) >= a.thresh ? p0 : 0.f;
-                        p1 = (hsh >> 16) >= a.thresh ? p1 : 0.f;
+                        pk &= ~dm;
+                        const int jb = 8 * t + (i >> 1);
+                        dw |= dm & ((1u << jb) | (1u << (16 + jb)));
                     }
-                    pw[t][i >> 3][(i & 7) >> 1] = pack_bf16(p0, p1);
+                    pw[t][i >> 3][(i & 7) >> 1] = pk;
                 }
             l += rs0 + rs1;
+            if (DROP) dw_prev = dw;
             PROBE(3);
 #pragma unroll
             for (int t = 0; t < 2; ++t)
@@ -332,6 +396,7 @@ __global__ void __launch_bounds__(256, 3) attn_fwd_kernel(AttnArgs a) {
     }
     PROBE_END;
     if (!active) return;
+    if (DROP && kend > kbeg) store_drop((kend - 1) & ~(KB - 1));
     const float ltot = l + __shfl_xor(l, 32);
     const int q = q0 + r;
     if (a.nsplit == 1) {
@@ -466,9 +531,11 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
     dsum += __shfl_xor(dsum, 32);
     const float lse2 = active ? a.lse[(size_t)bh * a.Lq + qi] : 0.f;
     if (active && h == 0 && blockIdx.z == 0) A.dvec[(size_t)bh * a.Lq + qi] = dsum;
-    // dropout hash input of key pair (kb >> 1) + 2h + c (see attn_fwd_kernel)
-    uint32_t qh = 0;
-    if (DROP) qh = drop_query_base(drop_head_mix(a.seed, a.site, bh), qi) + (uint32_t)(2 * h) * kPairMul;
+    // the forward's query-major drop words of this lane, one per 64-key tile (prefetched a
+    // tile ahead with the K / V rows)
+    const uint32_t* wrow = DROP ? a.wq + ((size_t)bh * a.Lq + qi) * 2 + h : nullptr;
+    const size_t wstride = (size_t)gridDim.y * a.Lq * 2;
+    uint32_t wcur = 0, wnext = 0;
 
     bf16x8 kr[2], vr[2];
     // row (key) r of the tile starts at r * B * s: the per-thread offsets of key tid>>3 are
@@ -506,17 +573,18 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
     if (kbeg < kend) {
         load(kbeg);
         store(0);
+        if (DROP && active) wcur = wrow[(size_t)(kbeg >> 6) * wstride];
     }
     __syncthreads();
     int buf = 0;
     for (int kb = kbeg; kb < kend; kb += KB, buf ^= 1) {
         const bool more = kb + KB < kend;
         if (more) load(kb + KB);
+        if (DROP && active && more) wnext = wrow[(size_t)((kb >> 6) + 1) * wstride];
         if (active) {
             const bf16* K = Ks[buf];
             const bf16* V = Vs[buf];
             const int nvalid = kend - kb;
-            const uint32_t hb = qh + (uint32_t)(kb >> 1) * kPairMul;
             u32x4 dsw[2][2];
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
@@ -541,11 +609,12 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
                     const float p0 = fast_exp2(fmaf(st[i], a.scale2, -lse2));
                     const float p1 = fast_exp2(fmaf(st[i + 1], a.scale2, -lse2));
                     float dp0 = dpt[i], dp1 = dpt[i + 1];
-                    if (DROP) {
-                        const uint32_t c = 16 * t + ((i & 3) >> 1) + 4 * (i >> 2);
-                        const uint32_t hsh = mix24(hb + c * kPairMul);
-                        dp0 = (hsh & 0xffffu) >= a.thresh ? dp0 : 0.f;
-                        dp1 = (hsh >> 16) >= a.thresh ? dp1 : 0.f;
+                    if (DROP) {   // bits 8t + (i>>1) (even key) and 16 + 8t + (i>>1) (odd key)
+                        const int jb = 8 * t + (i >> 1);
+                        const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)wcur, jb, 1);
+                        const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)wcur, 16 + jb, 1);
+                        dp0 = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, dp0) & ~m0);
+                        dp1 = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, dp1) & ~m1);
                     }
                     // P (Z dP~ / (1-p) - D): the scale rides in the fma (exact for p = 0)
                     dsw[t][i >> 3][(i & 7) >> 1] = pack_bf16(p0 * fmaf(dp0, a.keep_scale, -dsum),
@@ -561,6 +630,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
                         dqt[dt] = mfma(v_operand(K, lane, dt, t, s), __builtin_bit_cast(bf16x8, dsw[t][s]), dqt[dt]);
         }
         if (more) store(buf ^ 1);
+        wcur = wnext;
         __syncthreads();
     }
     if (!active) return;
@@ -622,14 +692,17 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
     __shared__ __attribute__((aligned(16))) bf16 Ds[2][QB * LDK];
     __shared__ __attribute__((aligned(16))) float Ls[2][QB];
     __shared__ __attribute__((aligned(16))) float Dv[2][QB];
-    __shared__ __attribute__((aligned(16))) uint32_t Zb[2][QB];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int bh = blockIdx.y, b = bh / a.H, hh = bh - b * a.H;
     const int k0 = blockIdx.x * (4 * 32) + wave * 32;
     const bool active = k0 < a.Lk;
     const int ki = active ? min(k0 + r, a.Lk - 1) : 0;
-    const uint32_t hmix = DROP ? drop_head_mix(a.seed, a.site, bh) : 0u;
+    // the forward's key-major drop words of this lane's key: bit n of word (qblk, key) is
+    // query 32 qblk + n (two 32-query blocks per tile, prefetched a tile ahead)
+    const uint32_t* wcol = DROP ? a.wk + (size_t)bh * ((size_t)a.nkt * 64) + ki : nullptr;
+    const size_t wstride = (size_t)gridDim.y * a.nkt * 64;
+    uint32_t wn[2] = {0u, 0u};
 
     bf16x8 kf[4], vf[4];
     {
@@ -643,7 +716,6 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
     }
     bf16x8 qr[2], dr[2];
     float lr = 0.f, dvr = 0.f;
-    uint32_t zr = 0u;
     // per-thread offsets of query row tid>>3, advanced per tile by qb * B * s (scalar unit)
     const size_t rowq = (size_t)a.B * a.sq, rowd = (size_t)a.B * A.sdo;
     const size_t q0off = (size_t)b * a.sq + hh * D + 8 * (tid & 7) + (size_t)(tid >> 3) * rowq;
@@ -666,7 +738,11 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
             // queries past Lq: lse = +inf -> P = 0
             lr = qq < a.Lq ? a.lse[(size_t)bh * a.Lq + qc] : INFINITY;
             dvr = A.dvec[(size_t)bh * a.Lq + qc];
-            if (DROP) zr = drop_query_base(hmix, (uint32_t)qq);
+        }
+        if (DROP && active) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                wn[u] = qb + 32 * u < a.Lq ? wcol[(size_t)((qb >> 5) + u) * wstride] : 0u;
         }
     };
     auto store = [&](int buf) {
@@ -679,7 +755,6 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
         if (tid < QB) {
             Ls[buf][tid] = lr;
             Dv[buf][tid] = dvr;
-            Zb[buf][tid] = zr;
         }
     };
     f32x16 dkt[2], dvt[2];
@@ -689,6 +764,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
     const float s0 = kvalid ? 0.f : -INFINITY;
     load(0);
     store(0);
+    uint32_t wc[2] = {wn[0], wn[1]};
     __syncthreads();
     int buf = 0;
     for (int qb = 0; qb < a.Lq; qb += QB, buf ^= 1) {
@@ -714,52 +790,47 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
                     st = mfma(qa, kf[s], st);
                     dpt = mfma(da, vf[s], dpt);
                 }
-                bf16x8 pf[2], dsf[2];
+                // drop bit of row 8g + 4h + j of this 32-query block: bit 8g + j of w >> 4h
+                const uint32_t wsh = DROP ? wc[u] >> (4 * h) : 0u;
+                u32x4 pw[2], dsw[2];
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     const int qrow = 32 * u + 8 * g + 4 * h;      // rows 4g..4g+3 of the tile
                     const float4 l4 = *reinterpret_cast<const float4*>(&Ls[buf][qrow]);
                     const float4 d4 = *reinterpret_cast<const float4*>(&Dv[buf][qrow]);
                     const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
-                    // keys k0+r and k0+(r^1) share one pair hash per query: this lane hashes
-                    // rows j = (r&1), (r&1)+2 and takes the other two from its neighbour
-                    uint32_t hsh[4] = {0u, 0u, 0u, 0u};
-                    if (DROP) {
-                        const int j0 = r & 1;
-                        const uint32_t kp2 = (uint32_t)(k0 + r) >> 1;
-                        const uint32_t ha = drop_pair(Zb[buf][qrow + j0], kp2);
-                        const uint32_t hb = drop_pair(Zb[buf][qrow + j0 + 2], kp2);
-                        const uint32_t oa = lane_xor1(ha), ob = lane_xor1(hb);
-                        hsh[0] = j0 ? oa : ha;
-                        hsh[1] = j0 ? ha : oa;
-                        hsh[2] = j0 ? ob : hb;
-                        hsh[3] = j0 ? hb : ob;
-                    }
+                    float pd[4], ds[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int i = 4 * g + j;
                         const float p = fast_exp2(fmaf(st[i], a.scale2, -lv[j]));
-                        float pd = p, dp = dpt[i];
-                        if (DROP) {
-                            const bool kp = ((r & 1) ? (hsh[j] >> 16) : (hsh[j] & 0xffffu)) >= a.thresh;
-                            pd = kp ? p : 0.f;   // 1/(1-p) applied to dV once at the end
-                            dp = kp ? dp : 0.f;
+                        float pk = p, dp = dpt[i];
+                        if (DROP) {   // 1/(1-p) applied to dV once at the end
+                            const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)wsh, 8 * g + j, 1);
+                            pk = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, p) & ~m);
+                            dp = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, dp) & ~m);
                         }
-                        pf[i >> 3][i & 7] = (bf16)pd;
-                        dsf[i >> 3][i & 7] = (bf16)(p * fmaf(dp, a.keep_scale, -dv4[j]));
+                        pd[j] = pk;
+                        ds[j] = p * fmaf(dp, a.keep_scale, -dv4[j]);
                     }
+                    pw[g >> 1][2 * (g & 1)] = pack_bf16(pd[0], pd[1]);
+                    pw[g >> 1][2 * (g & 1) + 1] = pack_bf16(pd[2], pd[3]);
+                    dsw[g >> 1][2 * (g & 1)] = pack_bf16(ds[0], ds[1]);
+                    dsw[g >> 1][2 * (g & 1) + 1] = pack_bf16(ds[2], ds[3]);
                 }
 #pragma unroll
                 for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
                         const int tt = u;   // query sub-tile = k-step block of 32 rows
-                        dvt[dt] = mfma(v_operand(DO, lane, dt, tt, s), pf[s], dvt[dt]);
-                        dkt[dt] = mfma(v_operand(Q, lane, dt, tt, s), dsf[s], dkt[dt]);
+                        dvt[dt] = mfma(v_operand(DO, lane, dt, tt, s), __builtin_bit_cast(bf16x8, pw[s]), dvt[dt]);
+                        dkt[dt] = mfma(v_operand(Q, lane, dt, tt, s), __builtin_bit_cast(bf16x8, dsw[s]), dkt[dt]);
                     }
             }
         }
         if (more) store(buf ^ 1);
+        wc[0] = wn[0];
+        wc[1] = wn[1];
         __syncthreads();
     }
     if (!kvalid) return;
@@ -783,13 +854,27 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
 
 }  // namespace
 
+/* uint32 words of the drop bits ov3d_attn_fwd writes and ov3d_attn_bwd reads (p > 0):
+ * query-major [nkt][B*H][Lq][2] followed by key-major [Lq/32][B*H][nkt*64], nkt = ceil(Lk/64) */
+extern "C" long long ov3d_attn_dropbits_words(int B, int H, int Lq, int Lk) {
+    if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || (Lq % QW)) return 0;
+    return 4LL * ((Lk + KB - 1) / KB) * B * H * Lq;
+}
+
+static void set_dropbits(AttnArgs& a, uint32_t* bits) {
+    a.nkt = (a.Lk + KB - 1) / KB;
+    a.wq = bits;
+    a.wk = bits ? bits + 2 * (size_t)a.nkt * a.B * a.H * a.Lq : nullptr;
+}
+
 extern "C" int ov3d_attn_fwd(const void* q, const void* k, const void* v, long long sq,
                              long long sk, long long sv, int B, int H, int Lq, int Lk, float scale,
                              float dropout_p, const int64_t* seed, int site, void* o, long long so,
-                             float* lse, float* workspace, int nsplit, void* stream) {
+                             float* lse, uint32_t* dropbits, float* workspace, int nsplit,
+                             void* stream) {
     if (!q || !k || !v || !o || !lse || B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || (Lq % QW) ||
-        nsplit <= 0 || dropout_p < 0.f || dropout_p >= 1.f || (dropout_p > 0.f && !seed) ||
-        (nsplit > 1 && !workspace))
+        nsplit <= 0 || dropout_p < 0.f || dropout_p >= 1.f ||
+        (dropout_p > 0.f && (!seed || !dropbits)) || (nsplit > 1 && !workspace))
         return OV3D_EINVAL;
     AttnArgs a;
     a.q = (const bf16*)q;
@@ -818,6 +903,7 @@ extern "C" int ov3d_attn_fwd(const void* q, const void* k, const void* v, long l
     a.nsplit = nsplit;
     a.part_o = workspace;
     a.part_ml = workspace ? workspace + (size_t)nsplit * B * H * Lq * D : nullptr;
+    set_dropbits(a, dropbits);
     hipStream_t st = ov3d_stream(stream);
     dim3 grid((Lq + 4 * QW - 1) / (4 * QW), B * H, nsplit);
     if (a.thresh)
@@ -852,13 +938,12 @@ extern "C" long long ov3d_attn_fwd_workspace(int B, int H, int Lq, int Lk, int n
 extern "C" int ov3d_attn_bwd(const void* q, const void* k, const void* v, long long sq,
                              long long sk, long long sv, const void* o, long long so,
                              const void* dout, long long sdo, const float* lse, int B, int H,
-                             int Lq, int Lk, float scale, float dropout_p, const int64_t* seed,
-                             int site, float* dvec, void* dq, long long sdq, void* dk,
-                             long long sdk, void* dv, long long sdv, float* workspace,
-                             int nsplit, void* stream) {
+                             int Lq, int Lk, float scale, float dropout_p, const uint32_t* dropbits,
+                             float* dvec, void* dq, long long sdq, void* dk, long long sdk,
+                             void* dv, long long sdv, float* workspace, int nsplit, void* stream) {
     if (!q || !k || !v || !o || !dout || !lse || !dvec || !dq || !dk || !dv || B <= 0 || H <= 0 ||
         Lq <= 0 || Lk <= 0 || (Lq % QW) || dropout_p < 0.f || dropout_p >= 1.f ||
-        (dropout_p > 0.f && !seed))
+        (dropout_p > 0.f && !dropbits))
         return OV3D_EINVAL;
     AttnBwdArgs A;
     AttnArgs& a = A.f;
@@ -875,8 +960,8 @@ extern "C" int ov3d_attn_bwd(const void* q, const void* k, const void* v, long l
     a.scale2 = scale * 1.4426950408889634f;
     a.thresh = dropout_p > 0.f ? (uint32_t)fminf(rintf(dropout_p * 65536.0f), 65535.0f) : 0u;
     a.keep_scale = 1.f / (1.f - dropout_p);
-    a.seed = seed;
-    a.site = (uint32_t)site;
+    a.seed = nullptr;
+    a.site = 0;
     a.so = so;
     a.lse = (float*)lse;
     a.o = nullptr;
@@ -898,6 +983,7 @@ extern "C" int ov3d_attn_bwd(const void* q, const void* k, const void* v, long l
     a.keys_per_split = kps;
     a.nsplit = nsplit;
     a.part_o = workspace;
+    set_dropbits(a, (uint32_t*)dropbits);
     hipStream_t st = ov3d_stream(stream);
     const dim3 gq((Lq + 4 * QW - 1) / (4 * QW), B * H, nsplit);
     if (a.thresh)

@@ -52,7 +52,7 @@ def keep_mask(seed, site, B, H, Lq, Lk, p, device):
     hsh = _mix24(qb[:, :, None] + (((k[None, None] >> 1) * 0x27D4EB2F) & M32))   # (BH, Lq, Lk)
     half = torch.where((k & 1).bool()[None, None], hsh >> 16, hsh & 0xFFFF)
     thresh = min(int(np.rint(np.float32(p) * np.float32(65536.0))), 65535) if p > 0 else 0
-    return (half >= thresh).view(B, H, Lq, Lk)
+    return ((half ^ 0x8000) >= thresh).view(B, H, Lq, Lk)     # int16(half) >= thresh - 32768
 
 
 def reference(q, k, v, H, p=0.0, mask=None):
@@ -121,6 +121,59 @@ def test_attention_matches_reference(cuda, Lq, Lk, B, H, packed, p):
     assert _rel(out, ref) < 1e-2, _rel(out, ref)
     for gg, lr in zip(got_grads, leaves_r):
         assert _rel(gg, lr.grad) < 2e-2, _rel(gg, lr.grad)
+
+
+def _drop_key(b, h):
+    """attn.hip drop_key: key offset in its 64-key tile of bit b of a (query, h) word"""
+    e, j = b >> 4, b & 15
+    t, m = j >> 3, j & 7
+    return 32 * t + 2 * (m & 1) + 8 * (m >> 1) + 4 * h + e
+
+
+@pytest.mark.parametrize("Lq,Lk,B,H,nsplit", [(128, 200, 2, 2, 1), (256, 256, 1, 3, 1),
+                                              (128, 2048, 2, 2, 8), (96, 64, 2, 1, 1)])
+def test_attention_drop_bits_layouts(cuda, Lq, Lk, B, H, nsplit):
+    """The forward's stored drop bits, both layouts, decoded bit by bit against the hash."""
+    from ov3d_amd import _native, attention as A
+    lib = _native.load()
+    torch.manual_seed(1)
+    E = H * 64
+    q = torch.randn(Lq, B, E, device=cuda).to(torch.bfloat16)
+    k = torch.randn(Lk, B, E, device=cuda).to(torch.bfloat16)
+    v = torch.randn(Lk, B, E, device=cuda).to(torch.bfloat16)
+    p, site = 0.3, 11
+    seed_t = A._seed(cuda)
+    o = torch.empty(Lq, B, E, device=cuda, dtype=torch.bfloat16)
+    lse = torch.empty(B * H, Lq, device=cuda)
+    nw = lib.ov3d_attn_dropbits_words(B, H, Lq, Lk)
+    nkt = (Lk + 63) // 64
+    assert nw == 4 * nkt * B * H * Lq
+    bits = torch.zeros(nw, dtype=torch.int32, device=cuda)
+    ws = torch.empty(max(lib.ov3d_attn_fwd_workspace(B, H, Lq, Lk, nsplit), 1), device=cuda)
+    rc = lib.ov3d_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), E, E, E, B, H, Lq, Lk, 0.125, p,
+                           seed_t.data_ptr(), site, o.data_ptr(), E, lse.data_ptr(), bits.data_ptr(),
+                           ws.data_ptr(), nsplit, _native._stream(q))
+    assert rc == 0
+    torch.cuda.synchronize()
+    keep = keep_mask(int(seed_t.item()), site, B, H, Lq, Lk, p, cuda).view(B * H, Lq, Lk)
+    w = bits.to(torch.int64) & M32
+    half = 2 * nkt * B * H * Lq
+    wq = w[:half].view(nkt, B * H, Lq, 2)
+    wk = w[half:].view(Lq // 32, B * H, nkt * 64)
+    bidx = torch.arange(32, device=cuda)
+    # query-major: word (kt, bh, q, h) bit b -> key 64 kt + drop_key(b, h)
+    drop_q = ((wq[..., None] >> bidx) & 1).bool()                        # (nkt, BH, Lq, 2, 32)
+    keys = torch.tensor([[_drop_key(b, h) for b in range(32)] for h in range(2)], device=cuda)
+    kabs = 64 * torch.arange(nkt, device=cuda)[:, None, None] + keys[None]   # (nkt, 2, 32)
+    got = torch.zeros(B * H, Lq, nkt * 64, dtype=torch.bool, device=cuda)
+    for kt in range(nkt):
+        for h in range(2):
+            got[:, :, kabs[kt, h]] = drop_q[kt, :, :, h, :]
+    assert torch.equal(got[:, :, :Lk], ~keep)
+    # key-major: word (qblk, bh, key) bit n -> query 32 qblk + n
+    drop_k = ((wk[..., None] >> bidx) & 1).bool()                        # (Lq/32, BH, nkt*64, 32)
+    got_k = drop_k.permute(1, 0, 3, 2).reshape(B * H, Lq, nkt * 64)
+    assert torch.equal(got_k[:, :, :Lk], ~keep)
 
 
 def test_attention_seed_advances_and_is_reproducible(cuda):
