@@ -310,8 +310,9 @@ int ov3d_wgrad(const void* dy, long long ldy, const void* x, long long ldx, int 
                void* stream);
 long long ov3d_wgrad_workspace(int R, int N, int K, int nsplit);
 /* several independent weight gradients in one launch (+ one split reduction launch) per
- * 28 problems: the deferred dW / db of a backward pass (gemm.py).  workspace:
- * ov3d_wgrad_group_workspace() floats. */
+ * 28 problems: the deferred dW / db of a backward pass (gemm.py).  256 x 256 tiles,
+ * stream-K over (problem, tile, 32-row stage) units with one workgroup per CU; `nsplit`
+ * is not used.  workspace: ov3d_wgrad_group_workspace() floats. */
 typedef struct {
     const void* dy; long long ldy; const void* x; long long ldx;
     int R, N, K, nsplit;
@@ -320,6 +321,8 @@ typedef struct {
 long long ov3d_wgrad_group_workspace(const ov3d_wgrad_problem* probs, int n);
 int ov3d_wgrad_group(const ov3d_wgrad_problem* probs, int n, float* workspace, void* stream);
 int ov3d_wgrad_tiles(int N, int K);
+/* output tiles of one problem in ov3d_wgrad_group (256 x 256 tiles, 512-thread workgroups) */
+int ov3d_wgrad_group_tiles(int N, int K);
 
 /* ---- Training BatchNorm1d + ReLU + Dropout over channels-last rows ----
  * The GenericMLP prediction heads (models/helpers.py:45-112, built by

@@ -88,7 +88,8 @@ _SIGS = {
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
                           "ov3d_attn_dropbits_words",
-                          "ov3d_wgrad_workspace", "ov3d_wgrad_tiles", "ov3d_set_loss_desc_size",
+                          "ov3d_wgrad_workspace", "ov3d_wgrad_tiles", "ov3d_wgrad_group_tiles",
+                          "ov3d_set_loss_desc_size",
                           "ov3d_resnorm_supported", "ov3d_resnorm_bwd_parts",
                           "ov3d_adamw_chunk", "ov3d_wgrad_group_workspace",
                           "ov3d_rows_gemm_supported", "ov3d_sa_dy_fused_supported",
@@ -125,6 +126,8 @@ def load():
         lib.ov3d_wgrad_workspace.restype = ctypes.c_longlong
         lib.ov3d_wgrad_tiles.argtypes = [ctypes.c_int] * 2
         lib.ov3d_wgrad_tiles.restype = ctypes.c_int
+        lib.ov3d_wgrad_group_tiles.argtypes = [ctypes.c_int] * 2
+        lib.ov3d_wgrad_group_tiles.restype = ctypes.c_int
         lib.ov3d_set_loss_desc_size.argtypes = []
         lib.ov3d_set_loss_desc_size.restype = ctypes.c_longlong
         lib.ov3d_resnorm_supported.argtypes = [ctypes.c_int]

@@ -200,6 +200,13 @@ def _wg_splits(R, N, K):
     return max(1, min((R + rows - 1) // rows, 512 // tiles))
 
 
+def _wg_group_splits(R):
+    """row splits of one problem in the grouped launch (256 x 256 tiles, csrc/wgrad.hip):
+    1024-row chunks (32 stages of 32 rows) keep the split partials to 256 KB per tile and
+    chunk, and give a few workgroups per CU over the step's ~100 problems"""
+    return max(1, (R + 1023) // 1024)
+
+
 def _fused_ok(dy, x):
     """the one-launch HIP weight/bias gradient applies to bf16 rows on the ROCm device"""
     return (dy.is_cuda and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16
@@ -373,7 +380,7 @@ def flush_weight_grads():
         dw = bufs[id(wp)][1].view(wshape)[r0:r1].reshape(r1 - r0, K)
         db = bufs[id(bp)][1][r0:r1] if bp is not None else None
         probs.append(_WgProblem(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), R, N, K,
-                                _wg_splits(R, N, K), dw.data_ptr(), dw.stride(0),
+                                _wg_group_splits(R), dw.data_ptr(), dw.stride(0),
                                 db.data_ptr() if db is not None else None))
     arr = (_WgProblem * len(probs))(*probs)
     lib = _native.load()

@@ -1,6 +1,9 @@
 """Deferred, grouped weight gradients (gemm.DEFER_WGRAD, csrc/wgrad.hip ov3d_wgrad_group):
-the full BASELINE-size training step gives bit-identical parameter gradients with the
-deferral on and off (same kernels, same split order), including the in_proj row blocks."""
+the full BASELINE-size training step gives the same parameter gradients with the deferral
+on and off, including the in_proj row blocks.  The grouped launch uses 256 x 256 tiles and
+1024-row splits, the immediate one 128 x 128 tiles and its own split count: every row chunk
+is accumulated in the same order, only the fp32 sum of the split partials is grouped
+differently (relative error <= 1e-4: the bias column sums over 16384 rows cancel)."""
 import pytest
 import torch
 
@@ -39,4 +42,6 @@ def test_deferred_weight_grads_equal_immediate(cuda):
             gemm.DEFER_WGRAD = False
     assert set(grads[True]) == set(grads[False])
     for n in grads[False]:
-        assert torch.equal(grads[True][n], grads[False][n]), n
+        a, b = grads[True][n], grads[False][n]
+        err = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+        assert err <= 1e-4, (n, err)
