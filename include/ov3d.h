@@ -288,6 +288,7 @@ long long ov3d_attn_fwd_workspace(int B, int H, int Lq, int Lk, int nsplit);
 long long ov3d_attn_dropbits_words(int B, int H, int Lq, int Lk);
 /* Backward: dq/dk/dv rows (same layout, bf16) from o, dout (stride sdo), lse and the
  * forward's drop bits; dvec (B*H, Lq) f32 scratch receives D = rowsum(dout * o).
+ * dk = dv = NULL computes dQ and D only (dK / dV later by ov3d_attn_bwd_dkdv_batch).
  * nsplit > 1 splits the dQ key loop over workgroups (fp32 partials in `workspace`, sized
  * as for the forward by ov3d_attn_fwd_workspace). */
 int ov3d_attn_bwd(const void* q, const void* k, const void* v, long long sq, long long sk,
@@ -296,6 +297,18 @@ int ov3d_attn_bwd(const void* q, const void* k, const void* v, long long sq, lon
                   const uint32_t* dropbits, float* dvec, void* dq, long long sdq, void* dk,
                   long long sdk, void* dv, long long sdv, float* workspace, int nsplit,
                   void* stream);
+
+/* dK / dV of several ov3d_attn_bwd calls of one shape in one launch (the decoder's cross
+ * attentions, deferred to the end of the decoder backward): each job is what
+ * ov3d_attn_bwd would have read for it, with dvec already written by an ov3d_attn_bwd call
+ * with dk = dv = NULL (dQ and D only). */
+typedef struct {
+    const void* q; long long sq; const void* k; long long sk; const void* v; long long sv;
+    const void* dout; long long sdo; const float* lse; const float* dvec;
+    const uint32_t* dropbits; void* dk; long long sdk; void* dv; long long sdv;
+} ov3d_attn_dkdv_job;
+int ov3d_attn_bwd_dkdv_batch(const ov3d_attn_dkdv_job* jobs, int njobs, int B, int H, int Lq,
+                             int Lk, float scale, float dropout_p, void* stream);
 
 /* ---- Linear-layer weight / bias gradient ----
  * For every row-major dense layer y = x W^T + b of the step (transformer projections

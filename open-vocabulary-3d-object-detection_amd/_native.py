@@ -48,6 +48,7 @@ _SIGS = {
     "ov3d_im2col3x3": "piiiiiiipp",
     "ov3d_attn_fwd": "pppllliiiiffpiplpppip",
     "ov3d_attn_bwd": "ppplllplplpiiiiffppplplplpip",
+    "ov3d_attn_bwd_dkdv_batch": "piiiiiffp",
     "ov3d_wgrad": "plpliiiplpppip",
     "ov3d_wgrad_group": "pipp",
     "ov3d_rows_bn_stats": "pillilipip",

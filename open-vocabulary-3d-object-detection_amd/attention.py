@@ -18,8 +18,8 @@ seed is a device int64 advanced once per training forward (``next_step``, captur
 hipGraph like any other kernel) and snapshotted for that forward.  The call site is fixed
 per module.
 """
+import ctypes
 import itertools
-
 import os
 
 import torch
@@ -30,6 +30,49 @@ HEAD_DIM = 64
 _SITES = itertools.count(1)
 _SEEDS = {}     # live per-device step counter (advanced in place: graph-replay safe)
 _SNAPS = {}     # per device: the snapshot the current forward's dropout masks use
+
+
+# Deferred dK / dV (the decoder's cross attentions): the K / V of all layers are column blocks
+# of two shared buffers whose gradient only feeds transformer._MemoryKV's backward, which
+# runs after every layer's attention backward.  A layer's backward computes dQ (and D) at
+# once and queues its dK / dV job here; _MemoryKV.backward launches all of them in one
+# ov3d_attn_bwd_dkdv_batch call before it reads the buffers.
+_KV_JOBS = {}   # id(dK buffer) -> [((B, H, Lq, Lk, p), job struct, tensors kept alive), ...]
+DEFER_KV = True   # off: every call computes its dK / dV at once (tests compare the two)
+
+
+class _DkdvJob(ctypes.Structure):
+    """mirror of ov3d_attn_dkdv_job (include/ov3d.h)"""
+    _fields_ = [("q", ctypes.c_void_p), ("sq", ctypes.c_longlong), ("k", ctypes.c_void_p),
+                ("sk", ctypes.c_longlong), ("v", ctypes.c_void_p), ("sv", ctypes.c_longlong),
+                ("dout", ctypes.c_void_p), ("sdo", ctypes.c_longlong), ("lse", ctypes.c_void_p),
+                ("dvec", ctypes.c_void_p), ("dropbits", ctypes.c_void_p), ("dk", ctypes.c_void_p),
+                ("sdk", ctypes.c_longlong), ("dv", ctypes.c_void_p), ("sdv", ctypes.c_longlong)]
+
+
+def defer_kv_grads(dk_buf):
+    """attention calls whose K gradient goes to `dk_buf` queue their dK / dV (see _KV_JOBS)"""
+    if len(_KV_JOBS) > 16:   # forwards without a backward (eval) leave empty entries
+        for key in [k for k, v in _KV_JOBS.items() if not v]:
+            del _KV_JOBS[key]
+    _KV_JOBS[id(dk_buf)] = []
+
+
+def flush_kv_grads(dk_buf):
+    """launch the queued dK / dV of the calls writing `dk_buf` (one launch per shape)"""
+    jobs = _KV_JOBS.pop(id(dk_buf), None)
+    if not jobs:
+        return
+    lib = _native.load()
+    by_shape = {}
+    for dims, job, keep in jobs:
+        by_shape.setdefault(dims, []).append((job, keep))
+    for (B, H, Lq, Lk, p), lst in by_shape.items():
+        arr = (_DkdvJob * len(lst))(*[j for j, _ in lst])
+        rc = lib.ov3d_attn_bwd_dkdv_batch(ctypes.addressof(arr), len(lst), B, H, Lq, Lk,
+                                          HEAD_DIM ** -0.5, p, _native._stream(lst[0][1][0]))
+        if rc:
+            raise _native.NativeError(f"ov3d_attn_bwd_dkdv_batch failed with status {rc}")
 
 
 def new_site():
@@ -146,13 +189,23 @@ class _Attention(torch.autograd.Function):
         dqp, sdq = _rows(grads[qi], qo, E)
         dkp, sdk = _rows(grads[ki], ko, E)
         dvp, sdv = _rows(grads[vi], vo, E)
+        # K and V gradients into shared buffers registered for deferral: dQ now, dK / dV
+        # queued for the batched launch (flush_kv_grads)
+        defer = (DEFER_KV and ext[ki] is not None and ext[vi] is not None and ki != qi
+                 and vi != qi and id(ext[ki]) in _KV_JOBS)
         rc = _native.load().ov3d_attn_bwd(
             qp, kp, vp, sq, sk, sv, _native._ptr(o), E, _native._ptr(do), E, _native._ptr(lse),
             B, H, Lq, Lk, HEAD_DIM ** -0.5, p, _native._ptr(bits),
-            _native._ptr(dvec), dqp, sdq, dkp, sdk, dvp, sdv, _native._ptr(ws), nsplit,
-            _native._stream(q))
+            _native._ptr(dvec), dqp, sdq, 0 if defer else dkp, sdk, 0 if defer else dvp, sdv,
+            _native._ptr(ws), nsplit, _native._stream(q))
         if rc:
             raise _native.NativeError(f"ov3d_attn_bwd failed with status {rc}")
+        if defer:
+            job = _DkdvJob(qp, sq, kp, sk, vp, sv, _native._ptr(do), E, _native._ptr(lse),
+                           _native._ptr(dvec), _native._ptr(bits) if p > 0 else 0,
+                           dkp, sdk, dvp, sdv)
+            _KV_JOBS[id(ext[ki])].append(((B, H, Lq, Lk, p), job,
+                                          (q, k, v, do, lse, dvec, bits, ext[ki], ext[vi])))
         grads = [None if e is not None else g for g, e in zip(grads, ext)]
         return (None, None, None, None, None, None, tok_grad, *grads)
 

@@ -685,7 +685,7 @@ __global__ void __launch_bounds__(256) attn_dq_combine_kernel(AttnBwdArgs A) {
 
 // a lane owns a key: S = Q K^T tiles (32 queries x 32 keys) with the query on the registers
 template <bool DROP>
-__global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
+__device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
     const AttnArgs& a = A.f;
     constexpr int QB = 64;   // queries per LDS tile
     __shared__ __attribute__((aligned(16))) bf16 Qs[2][QB * LDK];
@@ -852,6 +852,25 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
         }
 }
 
+template <bool DROP>
+__global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
+    attn_bwd_dkdv_body<DROP>(A);
+}
+
+// dK / dV of several attention calls with the same shape in one launch (blockIdx.z = call):
+// the decoder's 8 cross attentions, deferred to the end of the decoder backward because
+// their K / V gradients only feed the shared memory-K/V projection (transformer._MemoryKV)
+constexpr int kDkdvBatchMax = 8;
+struct AttnBwdBatch {
+    AttnBwdArgs a[kDkdvBatchMax];
+};
+static_assert(sizeof(AttnBwdBatch) <= 4000, "kernel argument space");
+
+template <bool DROP>
+__global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_batch_kernel(AttnBwdBatch g) {
+    attn_bwd_dkdv_body<DROP>(g.a[blockIdx.z]);
+}
+
 }  // namespace
 
 /* uint32 words of the drop bits ov3d_attn_fwd writes and ov3d_attn_bwd reads (p > 0):
@@ -941,7 +960,7 @@ extern "C" int ov3d_attn_bwd(const void* q, const void* k, const void* v, long l
                              int Lq, int Lk, float scale, float dropout_p, const uint32_t* dropbits,
                              float* dvec, void* dq, long long sdq, void* dk, long long sdk,
                              void* dv, long long sdv, float* workspace, int nsplit, void* stream) {
-    if (!q || !k || !v || !o || !dout || !lse || !dvec || !dq || !dk || !dv || B <= 0 || H <= 0 ||
+    if (!q || !k || !v || !o || !dout || !lse || !dvec || !dq || (!dk != !dv) || B <= 0 || H <= 0 ||
         Lq <= 0 || Lk <= 0 || (Lq % QW) || dropout_p < 0.f || dropout_p >= 1.f ||
         (dropout_p > 0.f && !dropbits))
         return OV3D_EINVAL;
@@ -995,11 +1014,73 @@ extern "C" int ov3d_attn_bwd(const void* q, const void* k, const void* v, long l
         attn_dq_combine_kernel<<<ov3d_cdiv((long long)B * H * Lq * (D / 4), 256), 256, 0, st>>>(A);
         OV3D_LAUNCH_CHECK();
     }
+    if (!dk) return OV3D_OK;   // dQ (and D) only: dK / dV follow in ov3d_attn_bwd_dkdv_batch
     const dim3 gk((Lk + 127) / 128, B * H);
     if (a.thresh)
         attn_bwd_dkdv_kernel<true><<<gk, 256, 0, st>>>(A);
     else
         attn_bwd_dkdv_kernel<false><<<gk, 256, 0, st>>>(A);
     OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_attn_bwd_dkdv_batch(const ov3d_attn_dkdv_job* jobs, int njobs, int B, int H,
+                                        int Lq, int Lk, float scale, float dropout_p, void* stream) {
+    if (!jobs || njobs <= 0 || B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || (Lq % QW) ||
+        dropout_p < 0.f || dropout_p >= 1.f)
+        return OV3D_EINVAL;
+    hipStream_t st = ov3d_stream(stream);
+    for (int first = 0; first < njobs; first += kDkdvBatchMax) {
+        const int n = njobs - first < kDkdvBatchMax ? njobs - first : kDkdvBatchMax;
+        AttnBwdBatch g;
+        for (int j = 0; j < n; ++j) {
+            const ov3d_attn_dkdv_job& J = jobs[first + j];
+            if (!J.q || !J.k || !J.v || !J.dout || !J.lse || !J.dvec || !J.dk || !J.dv ||
+                (dropout_p > 0.f && !J.dropbits))
+                return OV3D_EINVAL;
+            AttnBwdArgs& A = g.a[j];
+            AttnArgs& a = A.f;
+            a.q = (const bf16*)J.q;
+            a.k = (const bf16*)J.k;
+            a.v = (const bf16*)J.v;
+            a.sq = J.sq;
+            a.sk = J.sk;
+            a.sv = J.sv;
+            a.B = B;
+            a.H = H;
+            a.Lq = Lq;
+            a.Lk = Lk;
+            a.scale2 = scale * 1.4426950408889634f;
+            a.thresh = dropout_p > 0.f ? (uint32_t)fminf(rintf(dropout_p * 65536.0f), 65535.0f) : 0u;
+            a.keep_scale = 1.f / (1.f - dropout_p);
+            a.seed = nullptr;
+            a.site = 0;
+            a.o = nullptr;
+            a.so = 0;
+            a.lse = (float*)J.lse;
+            a.part_o = nullptr;
+            a.part_ml = nullptr;
+            a.nsplit = 1;
+            a.keys_per_split = Lk;
+            set_dropbits(a, (uint32_t*)J.dropbits);
+            A.o = nullptr;
+            A.dout = (const bf16*)J.dout;
+            A.sdo = J.sdo;
+            A.dvec = (float*)J.dvec;
+            A.dq = nullptr;
+            A.dk = (bf16*)J.dk;
+            A.dv = (bf16*)J.dv;
+            A.sdq = 0;
+            A.sdk = J.sdk;
+            A.sdv = J.sdv;
+            A.scale = scale;
+        }
+        const dim3 gk((Lk + 127) / 128, B * H, n);
+        if (dropout_p > 0.f)
+            attn_bwd_dkdv_batch_kernel<true><<<gk, 256, 0, st>>>(g);
+        else
+            attn_bwd_dkdv_batch_kernel<false><<<gk, 256, 0, st>>>(g);
+        OV3D_LAUNCH_CHECK();
+    }
     return OV3D_OK;
 }

@@ -115,6 +115,7 @@ class _MemoryKV(torch.autograd.Function):
         K_all = torch.addmm(bk, mpos, Wk.t()).view(S, B, n)
         V_all = torch.addmm(bv, mem, Wv.t()).view(S, B, n)
         dK, dV = torch.empty_like(K_all), torch.empty_like(V_all)
+        flash.defer_kv_grads(dK)   # the layers' dK / dV run batched in this op's backward
         token = torch.empty((), dtype=torch.float32, device=memory.device)
         tok_grad = torch.zeros((), dtype=torch.float32, device=memory.device)
         ctx.save_for_backward(mem, mpos, Wk, Wv)
@@ -129,6 +130,7 @@ class _MemoryKV(torch.autograd.Function):
     def backward(ctx, _k, _v, _dk, _dv, _tok, _tg):
         mem, mpos, Wk, Wv = ctx.saved_tensors
         E, mdt, pos_grad, L, R, C = ctx.meta
+        flash.flush_kv_grads(ctx.bufs[0])   # the deferred dK / dV of every layer, one launch
         dK, dV = (t.view(R, L * E) for t in ctx.bufs)
         params = ctx.params
         with torch.autocast("cuda", enabled=False):
