@@ -310,6 +310,31 @@ typedef struct {
 int ov3d_attn_bwd_dkdv_batch(const ov3d_attn_dkdv_job* jobs, int njobs, int B, int H, int Lq,
                              int Lk, float scale, float dropout_p, void* stream);
 
+/* ---- Masked attention (the masked encoder) ----
+ * Replaces the (B*H, L, L) boolean attn_mask of MaskedTransformerEncoder
+ * (models/transformer.py:152-190: mask = cdist(xyz, xyz) >= radius, tiled to the heads,
+ * True = not attended) given to nn.MultiheadAttention.  ov3d_attn_mask_pack packs a
+ * (B, Lq, Lk) row-major source, shared by the heads, into ov3d_attn_maskbits_words() uint32
+ * words (query-major [nkt][B][Lq][2] then key-major [Lq/32][B][nkt*64]): kind 0 = uint8
+ * mask (nonzero = not attended), kind 1 = fp32 distances (not attended iff d >= thr).
+ * The _masked entry points take the words (NULL = no mask) and are otherwise
+ * ov3d_attn_fwd / ov3d_attn_bwd.  A query with no attended key gets O = 0 and zero
+ * gradients (the reference's softmax would give NaN). */
+long long ov3d_attn_maskbits_words(int B, int Lq, int Lk);
+int ov3d_attn_mask_pack(const void* src, int kind, float thr, int B, int Lq, int Lk,
+                        uint32_t* words, void* stream);
+int ov3d_attn_fwd_masked(const void* q, const void* k, const void* v, long long sq, long long sk,
+                         long long sv, int B, int H, int Lq, int Lk, float scale, float dropout_p,
+                         const int64_t* seed, int site, void* o, long long so, float* lse,
+                         uint32_t* dropbits, float* workspace, int nsplit,
+                         const uint32_t* maskbits, void* stream);
+int ov3d_attn_bwd_masked(const void* q, const void* k, const void* v, long long sq, long long sk,
+                         long long sv, const void* o, long long so, const void* dout, long long sdo,
+                         const float* lse, int B, int H, int Lq, int Lk, float scale,
+                         float dropout_p, const uint32_t* dropbits, float* dvec, void* dq,
+                         long long sdq, void* dk, long long sdk, void* dv, long long sdv,
+                         float* workspace, int nsplit, const uint32_t* maskbits, void* stream);
+
 /* ---- Linear-layer weight / bias gradient ----
  * For every row-major dense layer y = x W^T + b of the step (transformer projections
  * and FFNs, GenericMLP heads / projections; models/transformer.py, models/helpers.py):

@@ -17,6 +17,12 @@ encoder layer), saved on the ctx like the logsumexp; the backward reads them.  T
 seed is a device int64 advanced once per training forward (``next_step``, captured by a
 hipGraph like any other kernel) and snapshotted for that forward.  The call site is fixed
 per module.
+
+Masked encoder (reference models/transformer.py:152-190): the boolean mask
+``cdist(xyz, xyz) >= radius`` (True = not attended), the same for every head, reaches the
+kernels as a ``PackedMask`` of 1-bit words (``pack_mask``: one launch from the distances,
+no (B*H, L, L) tensor); masked keys get a -inf score in the forward and both backward
+kernels.
 """
 import ctypes
 import itertools
@@ -112,10 +118,41 @@ def next_step(device):
     _SNAPS[device] = live.clone()
 
 
+class PackedMask:
+    """An attention mask shared by the heads, packed for the kernels (ov3d_attn_mask_pack):
+    ``words`` int32 (ov3d_attn_maskbits_words(B, Lq, Lk),), bit set = not attended."""
+
+    def __init__(self, words, B, Lq, Lk):
+        self.words, self.B, self.Lq, self.Lk = words, B, Lq, Lk
+
+
+def pack_mask(src, thr=None):
+    """(B, Lq, Lk) bool mask (True = not attended), or fp32 distances with ``thr`` (not
+    attended iff d >= thr: MaskedTransformerEncoder.compute_mask) -> PackedMask."""
+    B, Lq, Lk = src.shape
+    _native.check_device(src, "attention mask")
+    lib = _native.load()
+    n = lib.ov3d_attn_maskbits_words(B, Lq, Lk)
+    if n <= 0:
+        raise ValueError("pack_mask: query length must be a multiple of 32")
+    src = src.contiguous()
+    if thr is None:
+        if src.dtype != torch.bool:
+            raise ValueError("pack_mask: a bool mask, or distances with a threshold")
+        kind, thr = 0, 0.0
+    else:
+        if src.dtype != torch.float32:
+            raise ValueError("pack_mask: distances must be float32")
+        kind = 1
+    words = torch.empty((n,), dtype=torch.int32, device=src.device)
+    _native.call("ov3d_attn_mask_pack", src, kind, float(thr), B, Lq, Lk, words, like=src)
+    return PackedMask(words, B, Lq, Lk)
+
+
 def supported(q_src, embed_dim, num_heads, attn_mask):
-    """the HIP kernels: head_dim 64, no mask, query length a multiple of 32"""
-    return (q_src.is_cuda and attn_mask is None and embed_dim == num_heads * HEAD_DIM
-            and q_src.shape[0] % 32 == 0)
+    """the HIP kernels: head_dim 64, no mask or a PackedMask, query length a multiple of 32"""
+    return (q_src.is_cuda and (attn_mask is None or isinstance(attn_mask, PackedMask))
+            and embed_dim == num_heads * HEAD_DIM and q_src.shape[0] % 32 == 0)
 
 
 def _split(Lq, Lk, BH):
@@ -137,7 +174,7 @@ def _rows(src, off, E):
 
 class _Attention(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, spec, dims, H, dropout_p, site, ext, token, *srcs):
+    def forward(ctx, spec, dims, H, dropout_p, site, ext, mask, token, *srcs):
         (qi, qo), (ki, ko), (vi, vo) = spec
         q, k, v = srcs[qi], srcs[ki], srcs[vi]
         Lq, Lk, B = dims
@@ -154,13 +191,15 @@ class _Attention(torch.autograd.Function):
         qp, sq = _rows(q, qo, E)
         kp, sk = _rows(k, ko, E)
         vp, sv = _rows(v, vo, E)
-        fn = _native.load().ov3d_attn_fwd
+        mw = mask.words if mask is not None else None
+        fn = _native.load().ov3d_attn_fwd_masked
         rc = fn(qp, kp, vp, sq, sk, sv, B, H, Lq, Lk, HEAD_DIM ** -0.5, float(dropout_p),
                 _native._ptr(seed), site, _native._ptr(o), E, _native._ptr(lse), _native._ptr(bits),
-                _native._ptr(ws), nsplit, _native._stream(q))
+                _native._ptr(ws), nsplit, _native._ptr(mw) if mw is not None else 0,
+                _native._stream(q))
         if rc:
             raise _native.NativeError(f"ov3d_attn_fwd failed with status {rc}")
-        ctx.save_for_backward(*srcs, o, lse, bits)
+        ctx.save_for_backward(*srcs, o, lse, bits, mw)
         ctx.meta = (spec, dims, H, float(dropout_p), site, len(srcs))
         ctx.ext = ext
         return o
@@ -169,7 +208,7 @@ class _Attention(torch.autograd.Function):
     def backward(ctx, do):
         spec, (Lq, Lk, B), H, p, site, n = ctx.meta
         saved = ctx.saved_tensors
-        srcs, o, lse, bits = saved[:n], saved[n], saved[n + 1], saved[n + 2]
+        srcs, o, lse, bits, mw = saved[:n], saved[n], saved[n + 1], saved[n + 2], saved[n + 3]
         (qi, qo), (ki, ko), (vi, vo) = spec
         q, k, v = srcs[qi], srcs[ki], srcs[vi]
         E = H * HEAD_DIM
@@ -191,13 +230,14 @@ class _Attention(torch.autograd.Function):
         dvp, sdv = _rows(grads[vi], vo, E)
         # K and V gradients into shared buffers registered for deferral: dQ now, dK / dV
         # queued for the batched launch (flush_kv_grads)
-        defer = (DEFER_KV and ext[ki] is not None and ext[vi] is not None and ki != qi
-                 and vi != qi and id(ext[ki]) in _KV_JOBS)
-        rc = _native.load().ov3d_attn_bwd(
+        defer = (DEFER_KV and mw is None and ext[ki] is not None and ext[vi] is not None
+                 and ki != qi and vi != qi and id(ext[ki]) in _KV_JOBS)
+        rc = _native.load().ov3d_attn_bwd_masked(
             qp, kp, vp, sq, sk, sv, _native._ptr(o), E, _native._ptr(do), E, _native._ptr(lse),
             B, H, Lq, Lk, HEAD_DIM ** -0.5, p, _native._ptr(bits),
             _native._ptr(dvec), dqp, sdq, 0 if defer else dkp, sdk, 0 if defer else dvp, sdv,
-            _native._ptr(ws), nsplit, _native._stream(q))
+            _native._ptr(ws), nsplit, _native._ptr(mw) if mw is not None else 0,
+            _native._stream(q))
         if rc:
             raise _native.NativeError(f"ov3d_attn_bwd failed with status {rc}")
         if defer:
@@ -207,10 +247,10 @@ class _Attention(torch.autograd.Function):
             _KV_JOBS[id(ext[ki])].append(((B, H, Lq, Lk, p), job,
                                           (q, k, v, do, lse, dvec, bits, ext[ki], ext[vi])))
         grads = [None if e is not None else g for g, e in zip(grads, ext)]
-        return (None, None, None, None, None, None, tok_grad, *grads)
+        return (None, None, None, None, None, None, None, tok_grad, *grads)
 
 
-def attention_packed(srcs, spec, Lq, Lk, num_heads, dropout_p=0.0, site=0, ext=None):
+def attention_packed(srcs, spec, Lq, Lk, num_heads, dropout_p=0.0, site=0, ext=None, mask=None):
     """Attention over column ranges of projection outputs.
 
     srcs: contiguous (L, B, n*E) tensors (their rows l*B + b), spec: ((src index, column
@@ -219,7 +259,8 @@ def attention_packed(srcs, spec, Lq, Lk, num_heads, dropout_p=0.0, site=0, ext=N
     ext: optional (grad buffers per source or None, token, token gradient): a source with
     a buffer is shared with other calls (it may have more columns than this call reads);
     its gradient columns go into the buffer and ``token`` (an output of the producer of
-    the shared sources) carries the dependency instead.  -> (Lq, B, E) bf16."""
+    the shared sources) carries the dependency instead.  mask: optional PackedMask of shape
+    (B, Lq, Lk).  -> (Lq, B, E) bf16."""
     E = num_heads * HEAD_DIM
     B = srcs[spec[0][0]].shape[1]
     bufs = ext[0] if ext is not None else (None,) * len(srcs)
@@ -232,20 +273,23 @@ def attention_packed(srcs, spec, Lq, Lk, num_heads, dropout_p=0.0, site=0, ext=N
             raise ValueError("attention_packed: sources must be contiguous (L, B, n*E) tensors "
                              "fully covered by the q / k / v column ranges")
         _native.check_device(s, "attention input")
+    if mask is not None and (mask.B, mask.Lq, mask.Lk) != (B, Lq, Lk):
+        raise ValueError("attention_packed: mask shape does not match (B, Lq, Lk)")
     srcs = [s if s.dtype == torch.bfloat16 else s.to(torch.bfloat16) for s in srcs]
     if ext is None:
-        return _Attention.apply(tuple(spec), (Lq, Lk, B), num_heads, dropout_p, site, None, None,
-                                *srcs)
+        return _Attention.apply(tuple(spec), (Lq, Lk, B), num_heads, dropout_p, site, None, mask,
+                                None, *srcs)
     bufs, token, tok_grad = ext
     return _Attention.apply(tuple(spec), (Lq, Lk, B), num_heads, dropout_p, site,
-                            (tuple(bufs), tok_grad), token, *srcs)
+                            (tuple(bufs), tok_grad), mask, token, *srcs)
 
 
-def attention(q, k, v, num_heads, dropout_p=0.0, site=0):
+def attention(q, k, v, num_heads, dropout_p=0.0, site=0, mask=None):
     """q (Lq, B, E), k / v (Lk, B, E) -> (Lq, B, E) bf16 = softmax(q k^T / 8) v per head,
-    dropout on the probabilities (separate, contiguous copies of q, k, v)."""
+    dropout on the probabilities (separate, contiguous copies of q, k, v); mask: optional
+    PackedMask (B, Lq, Lk)."""
     if k.shape[1] != q.shape[1] or v.shape[:2] != k.shape[:2]:
         raise ValueError("attention: q, k, v batch / key lengths disagree")
     srcs = [t.contiguous() for t in (q, k, v)]
     return attention_packed(srcs, ((0, 0), (1, 0), (2, 0)), q.shape[0], k.shape[0], num_heads,
-                            dropout_p, site)
+                            dropout_p, site, mask=mask)

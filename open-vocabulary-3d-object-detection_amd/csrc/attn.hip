@@ -23,6 +23,10 @@
 // across the lanes, key-major words (32 queries of one key, the layout of
 // attn_bwd_dkdv_kernel's lanes); the backward reads bits instead of re-hashing (the hash was
 // half of each kernel's VALU issue).
+// Masked encoder (MaskedTransformerEncoder, transformer.py:152-190: mask = cdist(xyz) >= r^2,
+// the same for every head): ov3d_attn_mask_pack packs the (B, Lq, Lk) mask into 1-bit words
+// in the two drop-word layouts (per batch row instead of per head, 2 + 2 MB per 2048-point
+// layer); masked keys get a -inf score before the softmax in every kernel (MASK template).
 // Split-K (grid.z) serves the 128-query decoder attention: partial (O, m, l) per
 // key split, merged by attn_combine_kernel.
 #include <math.h>
@@ -66,6 +70,8 @@ struct AttnArgs {
     uint32_t* wq;          // drop bits, query-major: [nkt][B*H][Lq][2] (see drop_word)
     uint32_t* wk;          // drop bits, key-major:   [Lq/32][B*H][nkt*64]
     int nkt;               // 64-key tiles = ceil(Lk / 64)
+    const uint32_t* mq;    // mask bits (1 = not attended), query-major: [nkt][B][Lq][2]
+    const uint32_t* mk;    // mask bits, key-major: [Lq/32][B][nkt*64]
 };
 
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
@@ -202,7 +208,10 @@ __device__ __forceinline__ bf16x8 v_operand(const bf16* Vs, int lane, int dt, in
     return a;
 }
 
-template <bool DROP>
+// score bit of element i of score tile t in a query-major (drop / mask) word
+__device__ __forceinline__ constexpr int score_bit(int t, int i) { return ((i & 1) << 4) + 8 * t + (i >> 1); }
+
+template <bool DROP, bool MASK>
 __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     __shared__ __attribute__((aligned(16))) bf16 Ks[2][KB * LDK];
     __shared__ __attribute__((aligned(16))) bf16 Vs[2][KB * LDK];
@@ -232,6 +241,9 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     uint32_t* const wk_lane = DROP ? a.wk + ((size_t)(q0 >> 5) * gridDim.y + bh) * ((size_t)a.nkt * 64) +
                                          drop_key(r, h) : nullptr;
     uint32_t dw_prev = 0;   // drop word of the tile before this one
+    // mask words of this lane (query q0 + r, half h), one per 64-key tile
+    const uint32_t* const mrow = MASK ? a.mq + ((size_t)b * a.Lq + (active ? q0 + r : 0)) * 2 + h : nullptr;
+    const size_t mtile = (size_t)a.B * a.Lq * 2;
     auto store_drop = [&](int kbp) {
         wq_lane[(size_t)(kbp >> 6) * wq_tile] = dw_prev;
         wk_lane[kbp] = transpose32(dw_prev, r);   // lane r: key drop_key(r, h), bit n = query q0 + n
@@ -284,6 +296,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
         if (active) {
             const bf16* K = Ks[buf];
             const bf16* V = Vs[buf];
+            const uint32_t mw = MASK ? mrow[(size_t)(kb >> 6) * mtile] : 0u;
             // all LDS operand reads of the tile are issued ahead of their MFMAs, so their
             // latency overlaps the matrix / softmax work instead of stalling each MFMA
             bf16x8 ka[2][4];
@@ -326,6 +339,13 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
                     for (int i = 0; i < 16; ++i)
                         if (32 * t + (i & 3) + 8 * (i >> 2) + 4 * h >= nvalid) st[t][i] = -INFINITY;
             }
+            if (MASK) {   // masked keys: -inf scores (p = 0, not in the row sum)
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        if ((mw >> score_bit(t, i)) & 1u) st[t][i] = -INFINITY;
+            }
             float mx = -INFINITY;
 #pragma unroll
             for (int t = 0; t < 2; ++t)
@@ -336,7 +356,8 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
             // deferred rescale (T13): keep the stale max unless some query's max grew a lot
             if (__any((mx - m) * a.scale2 > RESCALE_THR)) {
                 const float mnew = fmaxf(m, mx);
-                const float alpha = fast_exp2((m - mnew) * a.scale2);
+                // (masked: a query with no attended key yet keeps m = -inf and alpha = 1)
+                const float alpha = (MASK && mnew == -INFINITY) ? 1.f : fast_exp2((m - mnew) * a.scale2);
                 m = mnew;
                 l *= alpha;
 #pragma unroll
@@ -349,7 +370,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
             // after the row sum.  Scalar f32 ops on purpose: packed v_pk_fma / v_pk_add issue
             // slower than two scalar ops beside the MFMAs (MI355X_MICROARCH.md cycle table;
             // the file is built with -fno-slp-vectorize)
-            const float mb = m * a.scale2;
+            const float mb = (MASK && m == -INFINITY) ? 0.f : m * a.scale2;
             const uint32_t hb = qh + (uint32_t)(kb >> 1) * kPairMul;
             const short ts = (short)((int)a.thresh - 32768);
             const s16x2 tsig = {ts, ts};
@@ -501,7 +522,7 @@ struct AttnBwdArgs {
     float scale;
 };
 
-template <bool DROP>
+template <bool DROP, bool MASK>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
     const AttnArgs& a = A.f;
     __shared__ __attribute__((aligned(16))) bf16 Ks[2][KB * LDK];
@@ -529,13 +550,17 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
         }
     }
     dsum += __shfl_xor(dsum, 32);
-    const float lse2 = active ? a.lse[(size_t)bh * a.Lq + qi] : 0.f;
+    float lse2 = active ? a.lse[(size_t)bh * a.Lq + qi] : 0.f;
+    if (MASK && lse2 == -INFINITY) lse2 = INFINITY;   // no attended key: P = 0
     if (active && h == 0 && blockIdx.z == 0) A.dvec[(size_t)bh * a.Lq + qi] = dsum;
     // the forward's query-major drop words of this lane, one per 64-key tile (prefetched a
     // tile ahead with the K / V rows)
     const uint32_t* wrow = DROP ? a.wq + ((size_t)bh * a.Lq + qi) * 2 + h : nullptr;
     const size_t wstride = (size_t)gridDim.y * a.Lq * 2;
     uint32_t wcur = 0, wnext = 0;
+    const uint32_t* mrow = MASK ? a.mq + ((size_t)b * a.Lq + qi) * 2 + h : nullptr;
+    const size_t mtile = (size_t)a.B * a.Lq * 2;
+    uint32_t mcur = 0, mnext = 0;
 
     bf16x8 kr[2], vr[2];
     // row (key) r of the tile starts at r * B * s: the per-thread offsets of key tid>>3 are
@@ -574,6 +599,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
         load(kbeg);
         store(0);
         if (DROP && active) wcur = wrow[(size_t)(kbeg >> 6) * wstride];
+        if (MASK && active) mcur = mrow[(size_t)(kbeg >> 6) * mtile];
     }
     __syncthreads();
     int buf = 0;
@@ -581,6 +607,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
         const bool more = kb + KB < kend;
         if (more) load(kb + KB);
         if (DROP && active && more) wnext = wrow[(size_t)((kb >> 6) + 1) * wstride];
+        if (MASK && active && more) mnext = mrow[(size_t)((kb >> 6) + 1) * mtile];
         if (active) {
             const bf16* K = Ks[buf];
             const bf16* V = Vs[buf];
@@ -603,6 +630,11 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
 #pragma unroll
                     for (int i = 0; i < 16; ++i)
                         if (32 * t + (i & 3) + 8 * (i >> 2) + 4 * h >= nvalid) st[i] = -INFINITY;
+                }
+                if (MASK) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        if ((mcur >> score_bit(t, i)) & 1u) st[i] = -INFINITY;
                 }
 #pragma unroll
                 for (int i = 0; i < 16; i += 2) {
@@ -631,6 +663,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
         }
         if (more) store(buf ^ 1);
         wcur = wnext;
+        mcur = mnext;
         __syncthreads();
     }
     if (!active) return;
@@ -684,7 +717,7 @@ __global__ void __launch_bounds__(256) attn_dq_combine_kernel(AttnBwdArgs A) {
 }
 
 // a lane owns a key: S = Q K^T tiles (32 queries x 32 keys) with the query on the registers
-template <bool DROP>
+template <bool DROP, bool MASK>
 __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
     const AttnArgs& a = A.f;
     constexpr int QB = 64;   // queries per LDS tile
@@ -703,6 +736,10 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
     const uint32_t* wcol = DROP ? a.wk + (size_t)bh * ((size_t)a.nkt * 64) + ki : nullptr;
     const size_t wstride = (size_t)gridDim.y * a.nkt * 64;
     uint32_t wn[2] = {0u, 0u};
+    // mask words of this lane's key (batch row b), same key-major layout
+    const uint32_t* mcol = MASK ? a.mk + (size_t)b * ((size_t)a.nkt * 64) + ki : nullptr;
+    const size_t mstride = (size_t)a.B * a.nkt * 64;
+    uint32_t mn[2] = {0u, 0u};
 
     bf16x8 kf[4], vf[4];
     {
@@ -737,12 +774,18 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
             const int qc = qq < a.Lq ? qq : a.Lq - 1;
             // queries past Lq: lse = +inf -> P = 0
             lr = qq < a.Lq ? a.lse[(size_t)bh * a.Lq + qc] : INFINITY;
+            if (MASK && lr == -INFINITY) lr = INFINITY;   // query with no attended key
             dvr = A.dvec[(size_t)bh * a.Lq + qc];
         }
         if (DROP && active) {
 #pragma unroll
             for (int u = 0; u < 2; ++u)
                 wn[u] = qb + 32 * u < a.Lq ? wcol[(size_t)((qb >> 5) + u) * wstride] : 0u;
+        }
+        if (MASK && active) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                mn[u] = qb + 32 * u < a.Lq ? mcol[(size_t)((qb >> 5) + u) * mstride] : 0u;
         }
     };
     auto store = [&](int buf) {
@@ -765,6 +808,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
     load(0);
     store(0);
     uint32_t wc[2] = {wn[0], wn[1]};
+    uint32_t mc[2] = {mn[0], mn[1]};
     __syncthreads();
     int buf = 0;
     for (int qb = 0; qb < a.Lq; qb += QB, buf ^= 1) {
@@ -792,6 +836,12 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
                 }
                 // drop bit of row 8g + 4h + j of this 32-query block: bit 8g + j of w >> 4h
                 const uint32_t wsh = DROP ? wc[u] >> (4 * h) : 0u;
+                if (MASK) {   // masked (query, key): -inf score
+                    const uint32_t msh = mc[u] >> (4 * h);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        if ((msh >> (8 * (i >> 2) + (i & 3))) & 1u) st[i] = -INFINITY;
+                }
                 u32x4 pw[2], dsw[2];
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
@@ -831,6 +881,8 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
         if (more) store(buf ^ 1);
         wc[0] = wn[0];
         wc[1] = wn[1];
+        mc[0] = mn[0];
+        mc[1] = mn[1];
         __syncthreads();
     }
     if (!kvalid) return;
@@ -852,9 +904,9 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
         }
 }
 
-template <bool DROP>
+template <bool DROP, bool MASK>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
-    attn_bwd_dkdv_body<DROP>(A);
+    attn_bwd_dkdv_body<DROP, MASK>(A);
 }
 
 // dK / dV of several attention calls with the same shape in one launch (blockIdx.z = call):
@@ -868,7 +920,49 @@ static_assert(sizeof(AttnBwdBatch) <= 4000, "kernel argument space");
 
 template <bool DROP>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_batch_kernel(AttnBwdBatch g) {
-    attn_bwd_dkdv_body<DROP>(g.a[blockIdx.z]);
+    attn_bwd_dkdv_body<DROP, false>(g.a[blockIdx.z]);
+}
+
+// mask (B, Lq, Lk) -> 1-bit words, thread per word: words [0, W) query-major
+// [nkt][B][Lq][2] (bit n of lane (q, h) = key 64 kt + drop_key(n, h)), words [W, 2W) key-major
+// [Lq/32][B][nkt*64] (bit n = query 32 qb + n).  KIND 0: uint8 mask, nonzero = not attended;
+// KIND 1: fp32 distances, not attended iff d >= thr (MaskedTransformerEncoder.compute_mask)
+template <int KIND>
+__global__ void __launch_bounds__(256) attn_mask_pack_kernel(const void* __restrict__ src, float thr,
+                                                             int B, int Lq, int Lk, int nkt,
+                                                             uint32_t* __restrict__ words) {
+    const long long W = (long long)nkt * B * Lq * 2;
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 2 * W) return;
+    auto masked = [&](int b, int q, int k) -> bool {
+        const size_t e = ((size_t)b * Lq + q) * Lk + k;
+        if (KIND == 0) return ((const uint8_t*)src)[e] != 0;
+        return ((const float*)src)[e] >= thr;
+    };
+    uint32_t w = 0;
+    if (t < W) {
+        const int h = (int)(t & 1);
+        const long long r = t >> 1;
+        const int q = (int)(r % Lq);
+        const long long kb = r / Lq;
+        const int b = (int)(kb % B), kt = (int)(kb / B);
+#pragma unroll 4
+        for (int n = 0; n < 32; ++n) {
+            const int k = 64 * kt + drop_key(n, h);
+            if (k < Lk && masked(b, q, k)) w |= 1u << n;
+        }
+    } else {
+        const long long u = t - W;
+        const int k = (int)(u % ((long long)nkt * 64));
+        const long long qb = u / ((long long)nkt * 64);
+        const int b = (int)(qb % B), q0 = 32 * (int)(qb / B);
+        if (k < Lk) {
+#pragma unroll 4
+            for (int n = 0; n < 32; ++n)
+                if (q0 + n < Lq && masked(b, q0 + n, k)) w |= 1u << n;
+        }
+    }
+    words[t] = w;
 }
 
 }  // namespace
@@ -886,11 +980,39 @@ static void set_dropbits(AttnArgs& a, uint32_t* bits) {
     a.wk = bits ? bits + 2 * (size_t)a.nkt * a.B * a.H * a.Lq : nullptr;
 }
 
-extern "C" int ov3d_attn_fwd(const void* q, const void* k, const void* v, long long sq,
-                             long long sk, long long sv, int B, int H, int Lq, int Lk, float scale,
-                             float dropout_p, const int64_t* seed, int site, void* o, long long so,
-                             float* lse, uint32_t* dropbits, float* workspace, int nsplit,
-                             void* stream) {
+static void set_maskbits(AttnArgs& a, const uint32_t* bits) {
+    a.mq = bits;
+    a.mk = bits ? bits + 2 * (size_t)a.nkt * a.B * a.Lq : nullptr;
+}
+
+/* uint32 words of a packed attention mask (ov3d_attn_mask_pack): query-major
+ * [nkt][B][Lq][2] followed by key-major [Lq/32][B][nkt*64], nkt = ceil(Lk/64) */
+extern "C" long long ov3d_attn_maskbits_words(int B, int Lq, int Lk) {
+    if (B <= 0 || Lq <= 0 || Lk <= 0 || (Lq % QW)) return 0;
+    return 4LL * ((Lk + KB - 1) / KB) * B * Lq;
+}
+
+extern "C" int ov3d_attn_mask_pack(const void* src, int kind, float thr, int B, int Lq, int Lk,
+                                   uint32_t* words, void* stream) {
+    if (!src || !words || (kind != 0 && kind != 1) || B <= 0 || Lq <= 0 || Lk <= 0 || (Lq % QW))
+        return OV3D_EINVAL;
+    const int nkt = (Lk + KB - 1) / KB;
+    const long long n = ov3d_attn_maskbits_words(B, Lq, Lk);
+    hipStream_t st = ov3d_stream(stream);
+    if (kind == 0)
+        attn_mask_pack_kernel<0><<<ov3d_cdiv(n, 256), 256, 0, st>>>(src, thr, B, Lq, Lk, nkt, words);
+    else
+        attn_mask_pack_kernel<1><<<ov3d_cdiv(n, 256), 256, 0, st>>>(src, thr, B, Lq, Lk, nkt, words);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_attn_fwd_masked(const void* q, const void* k, const void* v, long long sq,
+                                    long long sk, long long sv, int B, int H, int Lq, int Lk,
+                                    float scale, float dropout_p, const int64_t* seed, int site,
+                                    void* o, long long so, float* lse, uint32_t* dropbits,
+                                    float* workspace, int nsplit, const uint32_t* maskbits,
+                                    void* stream) {
     if (!q || !k || !v || !o || !lse || B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || (Lq % QW) ||
         nsplit <= 0 || dropout_p < 0.f || dropout_p >= 1.f ||
         (dropout_p > 0.f && (!seed || !dropbits)) || (nsplit > 1 && !workspace))
@@ -923,12 +1045,19 @@ extern "C" int ov3d_attn_fwd(const void* q, const void* k, const void* v, long l
     a.part_o = workspace;
     a.part_ml = workspace ? workspace + (size_t)nsplit * B * H * Lq * D : nullptr;
     set_dropbits(a, dropbits);
+    set_maskbits(a, maskbits);
     hipStream_t st = ov3d_stream(stream);
     dim3 grid((Lq + 4 * QW - 1) / (4 * QW), B * H, nsplit);
-    if (a.thresh)
-        attn_fwd_kernel<true><<<grid, 256, 0, st>>>(a);
-    else
-        attn_fwd_kernel<false><<<grid, 256, 0, st>>>(a);
+    if (maskbits) {
+        if (a.thresh)
+            attn_fwd_kernel<true, true><<<grid, 256, 0, st>>>(a);
+        else
+            attn_fwd_kernel<false, true><<<grid, 256, 0, st>>>(a);
+    } else if (a.thresh) {
+        attn_fwd_kernel<true, false><<<grid, 256, 0, st>>>(a);
+    } else {
+        attn_fwd_kernel<false, false><<<grid, 256, 0, st>>>(a);
+    }
     OV3D_LAUNCH_CHECK();
     if (nsplit > 1) {
         const long long waves = (long long)B * H * Lq;
@@ -936,6 +1065,15 @@ extern "C" int ov3d_attn_fwd(const void* q, const void* k, const void* v, long l
         OV3D_LAUNCH_CHECK();
     }
     return OV3D_OK;
+}
+
+extern "C" int ov3d_attn_fwd(const void* q, const void* k, const void* v, long long sq,
+                             long long sk, long long sv, int B, int H, int Lq, int Lk, float scale,
+                             float dropout_p, const int64_t* seed, int site, void* o, long long so,
+                             float* lse, uint32_t* dropbits, float* workspace, int nsplit,
+                             void* stream) {
+    return ov3d_attn_fwd_masked(q, k, v, sq, sk, sv, B, H, Lq, Lk, scale, dropout_p, seed, site, o,
+                                so, lse, dropbits, workspace, nsplit, nullptr, stream);
 }
 
 #ifdef OV3D_ATTN_PROBE
@@ -954,12 +1092,14 @@ extern "C" long long ov3d_attn_fwd_workspace(int B, int H, int Lq, int Lk, int n
     return (long long)nsplit * B * H * Lq * (D + 2);
 }
 
-extern "C" int ov3d_attn_bwd(const void* q, const void* k, const void* v, long long sq,
-                             long long sk, long long sv, const void* o, long long so,
-                             const void* dout, long long sdo, const float* lse, int B, int H,
-                             int Lq, int Lk, float scale, float dropout_p, const uint32_t* dropbits,
-                             float* dvec, void* dq, long long sdq, void* dk, long long sdk,
-                             void* dv, long long sdv, float* workspace, int nsplit, void* stream) {
+extern "C" int ov3d_attn_bwd_masked(const void* q, const void* k, const void* v, long long sq,
+                                    long long sk, long long sv, const void* o, long long so,
+                                    const void* dout, long long sdo, const float* lse, int B, int H,
+                                    int Lq, int Lk, float scale, float dropout_p,
+                                    const uint32_t* dropbits, float* dvec, void* dq, long long sdq,
+                                    void* dk, long long sdk, void* dv, long long sdv,
+                                    float* workspace, int nsplit, const uint32_t* maskbits,
+                                    void* stream) {
     if (!q || !k || !v || !o || !dout || !lse || !dvec || !dq || (!dk != !dv) || B <= 0 || H <= 0 ||
         Lq <= 0 || Lk <= 0 || (Lq % QW) || dropout_p < 0.f || dropout_p >= 1.f ||
         (dropout_p > 0.f && !dropbits))
@@ -1003,12 +1143,19 @@ extern "C" int ov3d_attn_bwd(const void* q, const void* k, const void* v, long l
     a.nsplit = nsplit;
     a.part_o = workspace;
     set_dropbits(a, (uint32_t*)dropbits);
+    set_maskbits(a, maskbits);
     hipStream_t st = ov3d_stream(stream);
     const dim3 gq((Lq + 4 * QW - 1) / (4 * QW), B * H, nsplit);
-    if (a.thresh)
-        attn_bwd_dq_kernel<true><<<gq, 256, 0, st>>>(A);
-    else
-        attn_bwd_dq_kernel<false><<<gq, 256, 0, st>>>(A);
+    if (maskbits) {
+        if (a.thresh)
+            attn_bwd_dq_kernel<true, true><<<gq, 256, 0, st>>>(A);
+        else
+            attn_bwd_dq_kernel<false, true><<<gq, 256, 0, st>>>(A);
+    } else if (a.thresh) {
+        attn_bwd_dq_kernel<true, false><<<gq, 256, 0, st>>>(A);
+    } else {
+        attn_bwd_dq_kernel<false, false><<<gq, 256, 0, st>>>(A);
+    }
     OV3D_LAUNCH_CHECK();
     if (nsplit > 1) {
         attn_dq_combine_kernel<<<ov3d_cdiv((long long)B * H * Lq * (D / 4), 256), 256, 0, st>>>(A);
@@ -1016,12 +1163,29 @@ extern "C" int ov3d_attn_bwd(const void* q, const void* k, const void* v, long l
     }
     if (!dk) return OV3D_OK;   // dQ (and D) only: dK / dV follow in ov3d_attn_bwd_dkdv_batch
     const dim3 gk((Lk + 127) / 128, B * H);
-    if (a.thresh)
-        attn_bwd_dkdv_kernel<true><<<gk, 256, 0, st>>>(A);
-    else
-        attn_bwd_dkdv_kernel<false><<<gk, 256, 0, st>>>(A);
+    if (maskbits) {
+        if (a.thresh)
+            attn_bwd_dkdv_kernel<true, true><<<gk, 256, 0, st>>>(A);
+        else
+            attn_bwd_dkdv_kernel<false, true><<<gk, 256, 0, st>>>(A);
+    } else if (a.thresh) {
+        attn_bwd_dkdv_kernel<true, false><<<gk, 256, 0, st>>>(A);
+    } else {
+        attn_bwd_dkdv_kernel<false, false><<<gk, 256, 0, st>>>(A);
+    }
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
+}
+
+extern "C" int ov3d_attn_bwd(const void* q, const void* k, const void* v, long long sq,
+                             long long sk, long long sv, const void* o, long long so,
+                             const void* dout, long long sdo, const float* lse, int B, int H,
+                             int Lq, int Lk, float scale, float dropout_p, const uint32_t* dropbits,
+                             float* dvec, void* dq, long long sdq, void* dk, long long sdk,
+                             void* dv, long long sdv, float* workspace, int nsplit, void* stream) {
+    return ov3d_attn_bwd_masked(q, k, v, sq, sk, sv, o, so, dout, sdo, lse, B, H, Lq, Lk, scale,
+                                dropout_p, dropbits, dvec, dq, sdq, dk, sdk, dv, sdv, workspace,
+                                nsplit, nullptr, stream);
 }
 
 extern "C" int ov3d_attn_bwd_dkdv_batch(const ov3d_attn_dkdv_job* jobs, int njobs, int B, int H,
@@ -1063,6 +1227,7 @@ extern "C" int ov3d_attn_bwd_dkdv_batch(const ov3d_attn_dkdv_job* jobs, int njob
             a.nsplit = 1;
             a.keys_per_split = Lk;
             set_dropbits(a, (uint32_t*)J.dropbits);
+            set_maskbits(a, nullptr);
             A.o = nullptr;
             A.dout = (const bf16*)J.dout;
             A.sdo = J.sdo;

@@ -31,6 +31,9 @@ from .sa_fused import _sync_group, bn_affine, bn_bwd_affine
 # BatchNorm1d, or its SyncBatchNorm conversion (DDP, main.py:427-431): the statistics
 # totals are then all-reduced over the BN's process group (exact SyncBN semantics)
 _BN_TYPES = (nn.BatchNorm1d, nn.SyncBatchNorm)
+# BatchNorm2d over channels-last rows == BatchNorm1d over the same rows (per-channel statistics
+# over every position): the SharedMLP layers of the set-abstraction modules
+_BN_ROW_TYPES = _BN_TYPES + (nn.BatchNorm2d,)
 
 HEAD_ORDER = ("visual_embed_head", "center_head", "size_head", "angle_cls_head",
               "angle_residual_head")
@@ -350,7 +353,7 @@ def bn_relu_rows_ok(h, bn, relu, drop):
     if not (h.is_cuda and h.dim() == 2 and h.shape[1] % 8 == 0 and torch.is_autocast_enabled("cuda")
             and torch.get_autocast_dtype("cuda") == torch.bfloat16):
         return False
-    return (type(bn) in _BN_TYPES and bn.training and bn.track_running_stats
+    return (type(bn) in _BN_ROW_TYPES and bn.training and bn.track_running_stats
             and bn.momentum is not None and bn.affine and isinstance(relu, nn.ReLU)
             and (drop is None or isinstance(drop, nn.Dropout)))
 

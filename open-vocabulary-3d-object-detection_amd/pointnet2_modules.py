@@ -66,12 +66,20 @@ class SharedMLP(nn.Sequential):
 
     def rows(self, x):
         """The 1x1-conv stack on channels-last rows (R, Cin) -> (R, Cout): each layer is one
-        GEMM (hipBLASLt) + BN over rows + ReLU; no NCHW<->NHWC transposes."""
+        GEMM (hipBLASLt) + BN over rows + ReLU; no NCHW<->NHWC transposes.  Training under
+        bf16 autocast: BN + ReLU as one HIP row pass each way (heads.bn_relu_rows; the
+        ScanNet SA with colour and the masked encoder's interim SA, which the fused
+        3-channel kernels of sa_fused.py do not take)."""
+        from . import heads
         for layer in self:
             w = layer.conv.weight
             x = rows_linear(x, w.view(w.shape[0], w.shape[1]), layer.conv.bias)
             if hasattr(layer, "bn"):
-                x = batch_norm_rows(layer.bn.bn, x)
+                bn = layer.bn.bn
+                if heads.bn_relu_rows_ok(x, bn, layer.activation, None):
+                    x = heads.bn_relu_rows(x, bn)
+                    continue
+                x = batch_norm_rows(bn, x)
             x = torch.relu(x)
         return x
 

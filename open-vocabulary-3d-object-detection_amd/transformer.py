@@ -56,13 +56,16 @@ class MultiheadAttention(nn.Module):
         else:
             srcs = list(in_projection(w, bias, ((query, 0, E), (key, E, 2 * E), (value, 2 * E, 3 * E))))
             spec = ((0, 0), (1, 0), (2, 0))
+        packed = isinstance(attn_mask, flash.PackedMask)
         if srcs[0].dtype == torch.bfloat16 and flash.supported(srcs[0], E, self.num_heads,
                                                                attn_mask):
             # HIP flash attention straight on the projection rows (csrc/attn.hip)
             out = flash.attention_packed(srcs, spec, L, S, self.num_heads,
                                          dropout_p=self.dropout if self.training else 0.0,
-                                         site=self.site)
+                                         site=self.site, mask=attn_mask if packed else None)
             return rows_linear(out, self.out_proj.weight, self.out_proj.bias)
+        if packed:
+            raise ValueError("a PackedMask needs the HIP attention path (bf16, head_dim 64)")
         q, k, v = (srcs[i][..., off:off + E] for i, off in spec)
         q, k, v = self._heads(q, L, B), self._heads(k, S, B), self._heads(v, S, B)
         mask = None
@@ -348,6 +351,20 @@ class MaskedTransformerEncoder(TransformerEncoder):
             dist = torch.cdist(xyz.float(), xyz.float(), p=2)
         return dist >= radius, dist
 
+    @torch.no_grad()
+    def _packed_mask(self, xyz, radius, dist=None):
+        """the same mask as compute_mask, packed for the HIP attention kernels straight from
+        the distances (no (B*H, L, L) bool tensor)"""
+        if dist is None or dist.shape[1] != xyz.shape[1]:
+            dist = torch.cdist(xyz.float(), xyz.float(), p=2)
+        return flash.pack_mask(dist, float(radius)), dist
+
+    @staticmethod
+    def _packed_ok(layer, src):
+        a = getattr(layer, "self_attn", None)
+        return (isinstance(a, MultiheadAttention) and src.is_cuda and src.shape[0] % 32 == 0
+                and a.embed_dim == a.num_heads * flash.HEAD_DIM and layer.nhead == a.num_heads)
+
     def forward(self, src, mask=None, src_key_padding_mask=None, pos=None, xyz=None,
                 transpose_swap=False):
         out = src
@@ -358,8 +375,11 @@ class MaskedTransformerEncoder(TransformerEncoder):
         for idx, layer in enumerate(self.layers):
             m = None
             if self.masking_radius[idx] > 0:
-                m, xyz_dist = self.compute_mask(xyz, self.masking_radius[idx], xyz_dist)
-                m = self._head_mask(m, layer)
+                if fused and self._packed_ok(layer, out if idx else src):
+                    m, xyz_dist = self._packed_mask(xyz, self.masking_radius[idx], xyz_dist)
+                else:
+                    m, xyz_dist = self.compute_mask(xyz, self.masking_radius[idx], xyz_dist)
+                    m = self._head_mask(m, layer)
             if fused:
                 pend = layer.forward_fused(pend, src_mask=m, pos=pos)
             else:

@@ -268,3 +268,135 @@ def test_deferred_cross_attention_kv_grads_equal_immediate(cuda):
     assert set(grads[True]) == set(grads[False])
     for k in grads[False]:
         assert torch.equal(grads[True][k], grads[False][k]), k
+
+
+def _ref_masked(q, k, v, H, am, p=0.0, keep=None):
+    """fp32 reference with a (B, Lq, Lk) bool mask (True = not attended, shared by the heads,
+    models/transformer.py:183-190) and an optional keep mask"""
+    Lq, B, E = q.shape
+    Lk = k.shape[0]
+    d = E // H
+    qh = q.reshape(Lq, B, H, d).permute(1, 2, 0, 3)
+    kh = k.reshape(Lk, B, H, d).permute(1, 2, 0, 3)
+    vh = v.reshape(Lk, B, H, d).permute(1, 2, 0, 3)
+    sc = (qh @ kh.transpose(-1, -2) / d ** 0.5).masked_fill(am[:, None], float("-inf"))
+    pr = torch.softmax(sc, dim=-1)
+    if keep is not None:
+        pr = pr * keep / (1 - p)
+    return (pr @ vh).permute(2, 0, 1, 3).reshape(Lq, B, E)
+
+
+def _radius_mask(B, L, r2, cuda, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    xyz = (torch.rand(B, L, 3, generator=g) * torch.tensor([4.0, 4.0, 2.0])).to(cuda)
+    dist = torch.cdist(xyz, xyz, p=2)
+    return dist, r2
+
+
+@pytest.mark.parametrize("Lq,Lk,B,H,kind", [(2048, 2048, 2, 4, "radius"), (1024, 1024, 2, 4, "radius"),
+                                            (128, 2048, 2, 4, "random"), (96, 200, 3, 2, "random")])
+@pytest.mark.parametrize("p", [0.0, 0.3])
+def test_masked_attention_matches_reference(cuda, Lq, Lk, B, H, kind, p):
+    """HIP masked attention (PackedMask) vs fp32 softmax with the boolean mask; radius masks
+    packed from the distances (kind 1), random masks from a bool tensor (kind 0)."""
+    from ov3d_amd import attention as A
+    torch.manual_seed(Lq + Lk)
+    E = H * 64
+    if kind == "radius":
+        dist, r2 = _radius_mask(B, Lq, 0.64, cuda)
+        am = dist >= r2
+        pm = A.pack_mask(dist, r2)
+    else:
+        am = torch.rand(B, Lq, Lk, device=cuda) < 0.7
+        am[:, :, 0] = False   # every query attends to something
+        pm = A.pack_mask(am)
+    assert 0.05 < am.float().mean().item() < 0.995
+    q0 = (torch.randn(Lq, B, E, device=cuda) * 1.5).to(torch.bfloat16).requires_grad_()
+    k0 = (torch.randn(Lk, B, E, device=cuda) * 1.5).to(torch.bfloat16).requires_grad_()
+    v0 = torch.randn(Lk, B, E, device=cuda).to(torch.bfloat16).requires_grad_()
+    site = 11
+    seed = int(A._seed(q0.device).item())
+    out = A.attention(q0, k0, v0, H, dropout_p=p, site=site, mask=pm)
+    g = torch.randn_like(out.float())
+    out.float().backward(g)
+    keep = keep_mask(seed, site, B, H, Lq, Lk, p, cuda) if p > 0 else None
+    lr = [t.detach().float().requires_grad_() for t in (q0, k0, v0)]
+    ref = _ref_masked(*lr, H, am, p, keep)
+    ref.backward(g)
+    assert _rel(out, ref) < 1e-2, _rel(out, ref)
+    for t, r in zip((q0, k0, v0), lr):
+        assert _rel(t.grad, r.grad) < 2e-2, _rel(t.grad, r.grad)
+
+
+def test_mask_pack_layouts(cuda):
+    """ov3d_attn_mask_pack: both word layouts decode to the mask bit for bit, and the
+    distance form (kind 1) equals the bool form of dist >= thr (kind 0)"""
+    from ov3d_amd import attention as A
+    B, Lq, Lk = 2, 96, 200
+    am = torch.rand(B, Lq, Lk, device=cuda) < 0.4
+    w = A.pack_mask(am).words.cpu().numpy().view(np.uint32)
+    nkt = (Lk + 63) // 64
+    W = nkt * B * Lq * 2
+    wq = w[:W].reshape(nkt, B, Lq, 2)
+    wk = w[W:].reshape(Lq // 32, B, nkt * 64)
+    m = am.cpu().numpy()
+    dec_q = np.zeros((B, Lq, nkt * 64), bool)
+    for n in range(32):
+        for h in range(2):
+            kk = np.arange(nkt) * 64 + _drop_key(n, h)
+            dec_q[:, :, kk] = ((wq[:, :, :, h] >> n) & 1).transpose(1, 2, 0).astype(bool)
+    assert np.array_equal(dec_q[:, :, :Lk], m) and not dec_q[:, :, Lk:].any()
+    dec_k = np.zeros((B, Lq, nkt * 64), bool)
+    for n in range(32):
+        dec_k[:, n::32, :] = ((wk >> n) & 1).transpose(1, 0, 2).astype(bool)
+    assert np.array_equal(dec_k[:, :, :Lk], m) and not dec_k[:, :, Lk:].any()
+    dist = torch.rand(B, Lq, Lk, device=cuda) * 2
+    thr = 0.64
+    a = A.pack_mask(dist, thr).words
+    b = A.pack_mask(dist >= thr).words
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("with_interim", [False, True])
+def test_masked_encoder_packed_equals_bool_mask_path(cuda, monkeypatch, with_interim):
+    """MaskedTransformerEncoder (bf16 fused layers): PackedMask through the HIP kernels vs
+    the (B*H, L, L) bool mask through PyTorch's fused SDPA, dropout off: same encoder
+    output and gradients within bf16 tolerance"""
+    import copy
+    from ov3d_amd import transformer as T
+    from ov3d_amd.pointnet2_modules import PointnetSAModuleVotes
+    torch.manual_seed(5)
+    layer = T.TransformerEncoderLayer(256, 4, 128, dropout=0.0)
+    # the interim SA's max-pool picks its rows from bf16 values, so tiny differences re-route
+    # its gradient: compared here with and without it (outputs / indices only with it)
+    interim = PointnetSAModuleVotes(radius=0.4, nsample=32, npoint=512, mlp=[256, 256, 256, 256],
+                                    normalize_xyz=True) if with_interim else None
+    enc = T.MaskedTransformerEncoder(layer, 3, [0.16, 0.64, 1.44], interim).to(cuda).train()
+    B, L = 2, 1024
+    xyz = torch.rand(B, L, 3, device=cuda) * torch.tensor([4.0, 4.0, 2.0], device=cuda)
+    src0 = torch.randn(L, B, 256, device=cuda)
+    res = {}
+    for packed in (True, False):
+        twin = copy.deepcopy(enc)
+        if not packed:
+            monkeypatch.setattr(T.MaskedTransformerEncoder, "_packed_ok", staticmethod(lambda *a: False))
+        calls = []
+        real = T.flash.pack_mask
+        monkeypatch.setattr(T.flash, "pack_mask", lambda *a: calls.append(1) or real(*a))
+        src = src0.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            _, out, inds = twin(src, xyz=xyz)
+        monkeypatch.undo()
+        assert len(calls) == (3 if packed else 0)
+        gw = torch.randn(out.shape, device=cuda, generator=torch.Generator(device=cuda).manual_seed(1))
+        (out.float() * gw).sum().backward()
+        res[packed] = (out.detach().float(), src.grad.clone(), inds,
+                       {n: p.grad.clone() for n, p in twin.named_parameters() if p.grad is not None})
+    if with_interim:
+        assert torch.equal(res[True][2], res[False][2])
+    assert _rel(res[True][0], res[False][0]) < 2e-2
+    if with_interim:
+        return
+    assert _rel(res[True][1], res[False][1]) < 3e-2
+    for n, g in res[False][3].items():
+        assert _rel(res[True][3][n], g) < 5e-2, n

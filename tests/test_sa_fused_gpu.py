@@ -180,3 +180,61 @@ def test_last_layer_backward_one_pass_equals_three_passes(cuda, monkeypatch, nsa
     for n in res[False]:
         e = _rel(res[True][n], res[False][n])
         assert e < 2e-3, (n, e)
+
+
+@pytest.mark.parametrize("kind", ["scannet_colour", "interim"])
+def test_sa_rows_bn_relu_path_vs_fp32(cuda, monkeypatch, kind):
+    """SA modules the 3-channel fused kernels do not take (ScanNet pre-encoder with colour:
+    6 input channels; the masked encoder's interim SA: 256 features + xyz, gradient to the
+    features) run BN + ReLU on the HIP row kernels (heads.bn_relu_rows) under bf16
+    autocast.  Against the fp32 module: outputs, running statistics and gradients no further
+    from fp32 than PyTorch's own bf16 batch_norm path (+ slack)."""
+    from ov3d_amd import heads, synthetic
+    from ov3d_amd.pointnet2_modules import PointnetSAModuleVotes
+    torch.manual_seed(4)
+    if kind == "scannet_colour":
+        sa = PointnetSAModuleVotes(radius=0.2, nsample=64, npoint=512, mlp=[3, 64, 128, 256],
+                                   normalize_xyz=True)
+        B, N, C = 2, 4096, 3
+    else:
+        sa = PointnetSAModuleVotes(radius=0.4, nsample=32, npoint=256, mlp=[256, 256, 256, 256])
+        B, N, C = 2, 1024, 256
+    sa = sa.to(cuda).train()
+    with torch.no_grad():
+        for layer in sa.mlp_module:
+            bn = layer.bn.bn
+            bn.weight.copy_(torch.randn_like(bn.weight) * 0.5 + 0.6)
+            bn.bias.copy_(torch.randn_like(bn.bias) * 0.2)
+    xyz = synthetic.make_batch(B, seed=6, device=cuda)["point_clouds"][:, :N, :3].contiguous()
+    feats0 = torch.randn(B, C, N, device=cuda)
+    gw = None
+    res = {}
+    for name, amp, rows in (("ref", False, True), ("torch", True, False), ("hip", True, True)):
+        twin = copy.deepcopy(sa)
+        feats = feats0.clone().requires_grad_(kind == "interim")
+        if not rows:
+            monkeypatch.setattr(heads, "bn_relu_rows_ok", lambda *a: False)
+        calls = []
+        real = heads.bn_relu_rows
+        monkeypatch.setattr(heads, "bn_relu_rows", lambda *a, **k: calls.append(1) or real(*a, **k))
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            _, f, _ = twin(xyz, feats)
+        monkeypatch.undo()
+        if gw is None:
+            gw = torch.randn(f.shape, device=cuda)
+        (f.float() * gw).sum().backward()
+        assert len(calls) == (3 if name == "hip" else 0), (name, len(calls))
+        g = {n: p.grad.clone() for n, p in twin.named_parameters()}
+        if feats.requires_grad:
+            g["features"] = feats.grad.clone()
+        res[name] = (f.detach().float(), g, twin)
+    f_ref, g_ref, m_ref = res["ref"]
+    assert _rel(res["hip"][0], f_ref) < max(2.0 * _rel(res["torch"][0], f_ref), 3e-2)
+    for lh, lr in zip(res["hip"][2].mlp_module, m_ref.mlp_module):
+        bh, br = lh.bn.bn, lr.bn.bn
+        assert int(bh.num_batches_tracked) == int(br.num_batches_tracked) == 1
+        assert _rel(bh.running_mean, br.running_mean) < 2e-2
+        assert _rel(bh.running_var, br.running_var) < 2e-2
+    for n in g_ref:
+        eh, et = _rel(res["hip"][1][n], g_ref[n]), _rel(res["torch"][1][n], g_ref[n])
+        assert eh <= max(2.0 * et, 3e-2), (n, eh, et)
