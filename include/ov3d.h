@@ -36,10 +36,13 @@ const char* ov3d_version(void);
  * models/model_3detr.py:355-361, 385-391).
  *   xyz      (B,N,3) f32      idx_out (B,M) int32, idx_out[:,0] = 0
  *   new_xyz_out (B,M,3) f32 or NULL: fused gather_operation of the samples
- *   workspace: B*N floats (only used when N > 20480), may be NULL otherwise.
+ *   workspace: ov3d_fps_workspace(B, N) floats, 16-byte aligned (N > 20480: up to 40960
+ *   points a two-cluster kernel keeps half of each wave's points in this L2-resident
+ *   scratch; beyond, the running distances), may be NULL when that is 0.
  * Tie rule = the upstream 512-thread tree reduction. */
 int ov3d_fps(const float* xyz, int B, int N, int M, int32_t* idx_out, float* new_xyz_out,
              float* workspace, void* stream);
+long long ov3d_fps_workspace(int B, int N);
 
 /* Ball query: first S point indices (ascending) with |p - c|^2 < radius^2,
  * padded with the first hit, zeros if none.

@@ -495,6 +495,336 @@ __global__ __launch_bounds__(kThreads) void fps_cull_kernel(const float* __restr
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Culled FPS for kThreads*kMaxPPT < N <= kThreads*(kPR+kPS) (ScanNet: 40000 points).
+// A CU cannot hold 40000 points (16 B each: 640 KB > 512 KB of VGPRs + 160 KB of LDS), so
+// each wave owns TWO spatial clusters of the Morton order: cluster A (kPR slots per lane,
+// coordinates + running distance in VGPRs, exactly as fps_cull_kernel) and cluster B
+// (kPS slots per lane as float4 (x, y, z, running distance) in a global workspace that stays
+// in L2: 384 KB per scene).  Each cluster has its own bounding box, max running distance and
+// cached best, and is skipped by the same exact test; only B's updates touch memory (one
+// 16-byte load + one 4-byte store per slot, read back only by the lane that wrote it).
+// The wave publishes the better of its two candidates (distance, then smaller rank).
+constexpr int kPR = 16, kPS = 24;
+
+__device__ __forceinline__ float sgpr_f(float v) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+__global__ __launch_bounds__(kThreads) void fps_stream_kernel(const float* __restrict__ xyz, int N,
+                                                              int M, int L,
+                                                              float4* __restrict__ ws,
+                                                              int32_t* __restrict__ idx,
+                                                              float* __restrict__ new_xyz) {
+    constexpr int PA = kPR * 64, PB = kPS * 64;   // positions per wave: cluster A, cluster B
+    constexpr int NA = kWaves * PA;               // cluster B positions start here
+    constexpr int NS = kPR + kPS;                 // slots per thread in the setup
+    __shared__ uint32_t s_hist[kCells];
+    __shared__ uint16_t s_perm[kThreads * NS];
+    __shared__ uint16_t s_out[kMaxOutLDS];
+    __shared__ float s_red[6][kWaves];
+    __shared__ uint32_t s_scan[kWaves];
+    __shared__ float4 s_pub[2][kWaves];
+    __shared__ int s_pos[2][kWaves];
+
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar addressing)
+    const float* __restrict__ p = xyz + (size_t)b * N * 3;
+    idx += (size_t)b * M;
+    if (new_xyz) new_xyz += (size_t)b * M * 3;
+    // slot i of this lane at wsw[64 i + lane]: scalar base + 32-bit lane offset per access
+    float4* __restrict__ wsw = ws + ((size_t)b * kWaves + w) * kPS * 64;
+
+    // ---- (a) scene bbox, (b) Morton cell codes + LDS counting sort (as fps_cull_kernel)
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int k = tid; k < N; k += kThreads)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float v = p[3 * k + a];
+            lo[a] = fminf(lo[a], v);
+            hi[a] = fmaxf(hi[a], v);
+        }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = wave_fmin(lo[a]);
+        hi[a] = wave_fmax(hi[a]);
+    }
+    if (lane == 0)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) { s_red[a][w] = lo[a]; s_red[3 + a][w] = hi[a]; }
+    for (int i = tid; i < kCells; i += kThreads) s_hist[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        float l = s_red[a][0], h = s_red[3 + a][0];
+        for (int q = 1; q < kWaves; ++q) { l = fminf(l, s_red[a][q]); h = fmaxf(h, s_red[3 + a][q]); }
+        lo[a] = l;
+        hi[a] = 16.f / fmaxf(h - l, 1e-6f);
+    }
+    uint32_t cp[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        const int k = tid + i * kThreads;
+        cp[i] = 0xffffffffu;
+        if (k < N) {
+            uint32_t q[3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const int c = (int)((p[3 * k + a] - lo[a]) * hi[a]);
+                q[a] = (uint32_t)min(max(c, 0), 15);
+            }
+            const uint32_t code = spread3(q[0]) | (spread3(q[1]) << 1) | (spread3(q[2]) << 2);
+            const uint32_t old = atomicAdd(&s_hist[code], 1u);
+            cp[i] = (code << 16) | old;
+        }
+    }
+    __syncthreads();
+    {
+        uint32_t v[4], sum = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { v[q] = s_hist[4 * tid + q]; sum += v[q]; }
+        uint32_t inc = sum;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t o = __shfl_up(inc, off);
+            if (lane >= off) inc += o;
+        }
+        if (lane == 63) s_scan[w] = inc;
+        __syncthreads();
+        uint32_t base = 0;
+        for (int q = 0; q < w; ++q) base += s_scan[q];
+        uint32_t run = base + inc - sum;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { s_hist[4 * tid + q] = run; run += v[q]; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NS; ++i)
+        if (cp[i] != 0xffffffffu)
+            s_perm[s_hist[cp[i] >> 16] + (cp[i] & 0xffffu)] = (uint16_t)(tid + i * kThreads);
+    __syncthreads();
+
+    // ---- (c) cluster B slots (first: their ranks are dead before cluster A fills its registers): positions NA + w*PB + i*64 + lane, sorted by rank, to the workspace
+    float bLo[3] = {INFINITY, INFINITY, INFINITY}, bHi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    {
+        uint32_t rk[kPS];
+#pragma unroll
+        for (int i = 0; i < kPS; ++i) {
+            const int pos = NA + w * PB + i * 64 + lane;
+            rk[i] = pos < N ? fps_rank(s_perm[pos], L) : 0xffffffffu;
+        }
+#pragma unroll
+        for (int pass = 0; pass < kPS; ++pass)
+#pragma unroll
+            for (int i = pass & 1; i + 1 < kPS; i += 2) {
+                const uint32_t a = rk[i], c = rk[i + 1];
+                rk[i] = min(a, c);
+                rk[i + 1] = max(a, c);
+            }
+#pragma unroll
+        for (int i = 0; i < kPS; ++i) {
+            const int pos = NA + w * PB + i * 64 + lane;
+            float4 e = make_float4(0.f, 0.f, 0.f, -1.f);
+            if (rk[i] != 0xffffffffu) {
+                const int k = fps_unrank(rk[i], L);
+                s_perm[pos] = (uint16_t)k;
+                const float x = p[3 * k], y = p[3 * k + 1], z = p[3 * k + 2];
+                const bool skip = (double)fmaf(z, z, fmaf(y, y, x * x)) <= 1e-3;
+                e = make_float4(x, y, z, skip ? -1.f : 1e10f);
+                if (!skip) {
+                    bLo[0] = fminf(bLo[0], x); bLo[1] = fminf(bLo[1], y); bLo[2] = fminf(bLo[2], z);
+                    bHi[0] = fmaxf(bHi[0], x); bHi[1] = fmaxf(bHi[1], y); bHi[2] = fmaxf(bHi[2], z);
+                }
+            }
+            wsw[64 * i + lane] = e;
+        }
+    }
+    // ---- cluster A slots: positions w*PA + i*64 + lane, sorted by rank, in registers
+    float px[kPR], py[kPR], pz[kPR], td[kPR];
+    float aLo[3] = {INFINITY, INFINITY, INFINITY}, aHi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    {
+        uint32_t rk[kPR];
+#pragma unroll
+        for (int i = 0; i < kPR; ++i) {
+            const int pos = w * PA + i * 64 + lane;
+            rk[i] = pos < N ? fps_rank(s_perm[pos], L) : 0xffffffffu;
+        }
+#pragma unroll
+        for (int pass = 0; pass < kPR; ++pass)
+#pragma unroll
+            for (int i = pass & 1; i + 1 < kPR; i += 2) {
+                const uint32_t a = rk[i], c = rk[i + 1];
+                rk[i] = min(a, c);
+                rk[i + 1] = max(a, c);
+            }
+#pragma unroll
+        for (int i = 0; i < kPR; ++i) {
+            const int pos = w * PA + i * 64 + lane;
+            px[i] = 0.f; py[i] = 0.f; pz[i] = 0.f; td[i] = -1.f;
+            if (rk[i] != 0xffffffffu) {
+                const int k = fps_unrank(rk[i], L);
+                s_perm[pos] = (uint16_t)k;
+                const float x = p[3 * k], y = p[3 * k + 1], z = p[3 * k + 2];
+                const bool skip = (double)fmaf(z, z, fmaf(y, y, x * x)) <= 1e-3;
+                px[i] = x; py[i] = y; pz[i] = z;
+                td[i] = skip ? -1.f : 1e10f;
+                if (!skip) {
+                    aLo[0] = fminf(aLo[0], x); aLo[1] = fminf(aLo[1], y); aLo[2] = fminf(aLo[2], z);
+                    aHi[0] = fmaxf(aHi[0], x); aHi[1] = fmaxf(aHi[1], y); aHi[2] = fmaxf(aHi[2], z);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {   // wave-uniform: scalar registers
+        aLo[a] = sgpr_f(wave_fmin(aLo[a]));
+        aHi[a] = sgpr_f(wave_fmax(aHi[a]));
+        bLo[a] = sgpr_f(wave_fmin(bLo[a]));
+        bHi[a] = sgpr_f(wave_fmax(bHi[a]));
+    }
+    __syncthreads();   // s_perm complete before any tie lookup
+    // this wave's cluster-B slots through a buffer descriptor: scalar base + lane offset +
+    // a constant slot offset per access (64-bit per-slot addresses would take 48 VGPRs)
+    const uint64_t wsa = reinterpret_cast<uint64_t>(wsw);
+    float4* const wsu = reinterpret_cast<float4*>(
+        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(wsa >> 32)) << 32) |
+        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wsa));
+    const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc(wsu, 0, kPS * 64 * 16, 0x00020000);
+    const float x0 = p[0], y0 = p[1], z0 = p[2];
+    float x1 = x0, y1 = y0, z1 = z0;
+    // per-cluster cache: max running distance, best distance bits, position, coordinates
+    float aT = INFINITY, bT = INFINITY;
+    int aD = __float_as_int(-1.f), bD = __float_as_int(-1.f), aP = 0, bP = 0;
+    float aX = 0.f, aY = 0.f, aZ = 0.f, bX = 0.f, bY = 0.f, bZ = 0.f;
+
+    // wave argmax of (dist bits bb, slot bi, coords) over the lanes -> cache (T, D, P, X, Y, Z)
+    auto wave_pick = [&](float best, int bi, float sx, float sy, float sz, int pbase,
+                         float& T, int& Dd, int& P, float& X, float& Y, float& Z)
+        __attribute__((always_inline)) {
+        const int bb = __float_as_int(best);
+        const int wm = wave_max_i32(bb);
+        Dd = wm;
+        T = __int_as_float(wm);
+        if (wm >= 0) {
+            const unsigned long long cand = __ballot(bb == wm);
+            int wl;
+            if (__popcll(cand) == 1) {
+                wl = __ffsll((long long)cand) - 1;
+            } else {   // distance tie inside the cluster: smallest rank wins
+                uint32_t my = 0xffffffffu;
+                if (bb == wm) my = fps_rank(s_perm[pbase + bi * 64 + lane], L);
+                const uint32_t mr = wave_min_u32(my);
+                wl = __ffsll((long long)__ballot(my == mr)) - 1;
+            }
+            X = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sx), wl));
+            Y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sy), wl));
+            Z = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sz), wl));
+            P = pbase + __builtin_amdgcn_readlane(bi, wl) * 64 + wl;
+        }
+    };
+
+    for (int j = 1; j < M; ++j) {
+        const int buf = j & 1;
+        {   // cluster A (registers)
+            const float gx = fmaxf(fmaxf(aLo[0] - x1, x1 - aHi[0]), 0.f);
+            const float gy = fmaxf(fmaxf(aLo[1] - y1, y1 - aHi[1]), 0.f);
+            const float gz = fmaxf(fmaxf(aLo[2] - z1, z1 - aHi[2]), 0.f);
+            if (fmaf(gz, gz, fmaf(gy, gy, gx * gx)) < aT) {
+                float best = -1.f, sx = 0.f, sy = 0.f, sz = 0.f;
+                int bi = 0;
+#pragma unroll
+                for (int i = 0; i < kPR; ++i) {
+                    const float dx = px[i] - x1, dy = py[i] - y1, dz = pz[i] - z1;
+                    const float d2 = fminf(fmaf(dz, dz, fmaf(dy, dy, dx * dx)), td[i]);
+                    td[i] = d2;
+                    const bool gt = d2 > best;
+                    best = gt ? d2 : best;
+                    bi = gt ? i : bi;
+                    sx = gt ? px[i] : sx; sy = gt ? py[i] : sy; sz = gt ? pz[i] : sz;
+                }
+                wave_pick(best, bi, sx, sy, sz, w * PA, aT, aD, aP, aX, aY, aZ);
+            }
+        }
+        {   // cluster B (workspace, L2-resident)
+            const float gx = fmaxf(fmaxf(bLo[0] - x1, x1 - bHi[0]), 0.f);
+            const float gy = fmaxf(fmaxf(bLo[1] - y1, y1 - bHi[1]), 0.f);
+            const float gz = fmaxf(fmaxf(bLo[2] - z1, z1 - bHi[2]), 0.f);
+            if (fmaf(gz, gz, fmaf(gy, gy, gx * gx)) < bT) {
+                float best = -1.f, sx = 0.f, sy = 0.f, sz = 0.f;
+                int bi = 0;
+#pragma unroll
+                for (int c = 0; c < kPS; c += 4) {
+                    float4 e[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        e[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                   wsr, lane * 16, 1024 * (c + u), 0));
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const float dx = e[u].x - x1, dy = e[u].y - y1, dz = e[u].z - z1;
+                        const float d2 = fminf(fmaf(dz, dz, fmaf(dy, dy, dx * dx)), e[u].w);
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(d2), wsr, lane * 16 + 12,
+                                                              1024 * (c + u), 0);
+                        const bool gt = d2 > best;
+                        best = gt ? d2 : best;
+                        bi = gt ? c + u : bi;
+                        sx = gt ? e[u].x : sx; sy = gt ? e[u].y : sy; sz = gt ? e[u].z : sz;
+                    }
+                }
+                wave_pick(best, bi, sx, sy, sz, NA + w * PB, bT, bD, bP, bX, bY, bZ);
+            }
+        }
+        // the wave's candidate: larger distance, equal distances -> smaller rank
+        bool useB = bD > aD;
+        if (bD == aD && aD >= 0)
+            useB = fps_rank(s_perm[bP], L) < fps_rank(s_perm[aP], L);
+        if (lane == 0) {
+            s_pub[buf][w] = useB ? make_float4(bX, bY, bZ, __int_as_float(bD))
+                                 : make_float4(aX, aY, aZ, __int_as_float(aD));
+            s_pos[buf][w] = useB ? bP : aP;
+        }
+        __syncthreads();
+        const float4 v = s_pub[buf][lane & (kWaves - 1)];
+        const int vp = s_pos[buf][lane & (kWaves - 1)];
+        const int dv = __float_as_int(v.w);
+        const int dm = __builtin_amdgcn_readfirstlane(row_max_i32(dv));
+        int pj;
+        if (dm < 0) {
+            pj = 0xffff;
+            x1 = x0; y1 = y0; z1 = z0;
+        } else {
+            const unsigned long long cand = __ballot(dv == dm) & 0xffffull;
+            int wsel;
+            if (__popcll(cand) == 1) {
+                wsel = __ffsll((long long)cand) - 1;
+            } else {
+                const uint32_t r = dv == dm ? fps_rank(s_perm[vp], L) : 0xffffffffu;
+                const uint32_t rm = __builtin_amdgcn_readfirstlane(row_min_u32(r));
+                wsel = __ffsll((long long)(__ballot(r == rm) & 0xffffull)) - 1;
+            }
+            x1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.x), wsel));
+            y1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.y), wsel));
+            z1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.z), wsel));
+            pj = __builtin_amdgcn_readlane(vp, wsel);
+        }
+        if (tid == 0) s_out[j] = (uint16_t)pj;
+    }
+    __syncthreads();
+    for (int j = tid; j < M; j += kThreads) {
+        int k = 0;
+        if (j > 0 && s_out[j] != 0xffff) k = s_perm[s_out[j]];
+        idx[j] = k;
+        if (new_xyz) {
+            new_xyz[3 * j] = p[3 * k];
+            new_xyz[3 * j + 1] = p[3 * k + 1];
+            new_xyz[3 * j + 2] = p[3 * k + 2];
+        }
+    }
+}
+
 #ifdef OV3D_FPS_PROBE
 unsigned long long* g_probe_dbg = nullptr;
 #define OV3D_FPS_PROBE_ARG , g_probe_dbg
@@ -528,6 +858,10 @@ extern "C" int ov3d_fps(const float* xyz, int B, int N, int M, int32_t* idx_out,
         else if (ppt <= 12) launch_cull<12>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
         else if (ppt <= 16) launch_cull<16>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
         else launch_cull<20>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
+    } else if (N <= kThreads * (kPR + kPS) && M <= kMaxOutLDS) {
+        if (!workspace) return OV3D_EINVAL;
+        hipLaunchKernelGGL(fps_stream_kernel, dim3(B), dim3(kThreads), 0, s, xyz, N, M, L,
+                           reinterpret_cast<float4*>(workspace), idx_out, new_xyz_out);
     } else {
         if (!workspace) return OV3D_EINVAL;
         hipLaunchKernelGGL(fps_global_kernel, dim3(B), dim3(kThreads), 0, s, xyz, N, M, L, workspace,
@@ -541,5 +875,12 @@ extern "C" int ov3d_fps(const float* xyz, int B, int N, int M, int32_t* idx_out,
 // diagnostic entry (probe build only): dbg = B*16*9 u64 phase counters
 extern "C" void ov3d_fps_probe_set(unsigned long long* dbg) { g_probe_dbg = dbg; }
 #endif
+
+/* workspace floats ov3d_fps needs for (B, N) (16-byte aligned) */
+extern "C" long long ov3d_fps_workspace(int B, int N) {
+    if (B <= 0 || N <= kThreads * kMaxPPT) return 0;
+    if (N <= kThreads * (kPR + kPS)) return (long long)B * kWaves * kPS * 64 * 4;
+    return (long long)B * N;
+}
 
 extern "C" const char* ov3d_version(void) { return "ov3d-hip 0.1 gfx950"; }

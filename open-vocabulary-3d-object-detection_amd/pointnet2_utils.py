@@ -23,13 +23,19 @@ def _i32(t, name, ndim):
     return nat.check(t.to(torch.int32).contiguous(), name, torch.int32, ndim)
 
 
+def _fps_workspace(B, N, device):
+    """scratch of ov3d_fps for N > 20480 points (ov3d_fps_workspace floats), else None"""
+    n = nat.load().ov3d_fps_workspace(B, N)
+    return torch.empty((n,), dtype=torch.float32, device=device) if n > 0 else None
+
+
 class FurthestPointSampling(Function):
     @staticmethod
     def forward(ctx, xyz, npoint):
         xyz = _f32(xyz, "xyz", 3)
         B, N, _ = xyz.shape
         idx = torch.empty((B, npoint), dtype=torch.int32, device=xyz.device)
-        ws = torch.empty((B, N), dtype=torch.float32, device=xyz.device) if N > 20480 else None
+        ws = _fps_workspace(B, N, xyz.device)
         nat.call("ov3d_fps", xyz, B, N, int(npoint), idx, None, ws, like=xyz)
         ctx.mark_non_differentiable(idx)
         return idx
@@ -51,7 +57,7 @@ def furthest_point_sample_gather(xyz, npoint):
         B, N, _ = xyz.shape
         idx = torch.empty((B, npoint), dtype=torch.int32, device=xyz.device)
         new_xyz = torch.empty((B, npoint, 3), dtype=torch.float32, device=xyz.device)
-        ws = torch.empty((B, N), dtype=torch.float32, device=xyz.device) if N > 20480 else None
+        ws = _fps_workspace(B, N, xyz.device)
         nat.call("ov3d_fps", xyz, B, N, int(npoint), idx, new_xyz, ws, like=xyz)
     return idx, new_xyz
 

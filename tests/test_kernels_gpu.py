@@ -19,7 +19,8 @@ def scene_batch(B, N, seed, uniform=False):
 # ------------------------------------------------------------------- FPS
 @pytest.mark.parametrize("B,N,M", [(8, 20000, 2048), (8, 2048, 128), (2, 40000, 1024),
                                    (3, 2048, 1024), (2, 1000, 64), (4, 300, 17), (2, 37, 37),
-                                   (1, 1, 4), (2, 20480, 8), (2, 20481, 8)])
+                                   (1, 1, 4), (2, 20480, 8), (2, 20481, 8), (1, 40960, 512),
+                                   (1, 40961, 64), (8, 40000, 2048)])
 def test_fps_bit_exact(cuda, B, N, M):
     from ov3d_amd import pointnet2_utils as pu
     xyz = scene_batch(B, N, seed=N + M) if N >= 64 else torch.rand(B, N, 3)
@@ -33,7 +34,7 @@ def test_fps_bit_exact(cuda, B, N, M):
                                   np.take_along_axis(xyz.numpy(), ref[..., None].astype(np.int64), 1))
 
 
-@pytest.mark.parametrize("N", [700, 5000])
+@pytest.mark.parametrize("N", [700, 5000, 30000])
 def test_fps_ties_and_skipped_points(cuda, N):
     """integer grid -> exact distance ties; origin points -> the |p|^2 <= 1e-3 skip."""
     from ov3d_amd import pointnet2_utils as pu
