@@ -126,6 +126,9 @@ int ov3d_hungarian(const float* cost, const int32_t* nactual, int P, int Q, int 
 /* layer 1: x0 (R,3) f32, W1 (C1,3) f32 -> y1 (R,C1) bf16, partials (nparts,2,C1) */
 int ov3d_sa_l1_fwd(const float* x0, const float* W1, int R, int C1, void* y1, double* partials,
                    int nparts, void* stream);
+/* the same for x0 (R, cin) with cin = 3 or 6 (xyz + colour, ScanNet --use_color), W1 (C1, cin) */
+int ov3d_sa_l1_fwd_cin(const float* x0, int cin, const float* W1, int R, int C1, void* y1,
+                       double* partials, int nparts, void* stream);
 /* (y1 may be NULL: statistics only, for consumers that recompute the layer from x0) */
 /* 1 if the MFMA layer kernel is built for (K, N) */
 int ov3d_sa_layer_supported(int K, int N);
@@ -218,6 +221,13 @@ int ov3d_bn_relu_bwd(int pass, const void* dz, const void* y, const float* scale
                      const float* shift, const float* mean, const float* invstd, const float* cA,
                      const float* cB, const float* cC, const float* x0, int R, int C,
                      double* partials, void* dyout, int nparts, const float* W1, void* stream);
+/* the same with x0 (R, cin), cin = 3 or 6: pass 2 writes dW1 partials (nparts, C, cin)
+ * (y == NULL recompute only for cin = 3) */
+int ov3d_bn_relu_bwd_cin(int pass, const void* dz, const void* y, const float* scale,
+                         const float* shift, const float* mean, const float* invstd,
+                         const float* cA, const float* cB, const float* cC, const float* x0, int cin,
+                         int R, int C, double* partials, void* dyout, int nparts, const float* W1,
+                         void* stream);
 
 /* Greedy 3D NMS, batched over scenes.  Replaces utils/nms.py:79-162
  * (nms_3d_faster / nms_3d_faster_samecls) as called per scene by

@@ -31,6 +31,7 @@ _SIGS = {
     "ov3d_giou3d_bwd_aligned": "pppiiippp",
     "ov3d_hungarian": "ppiiipppp",
     "ov3d_sa_l1_fwd": "ppiippip",
+    "ov3d_sa_l1_fwd_cin": "pipiippip",
     "ov3d_sa_layer_fwd": "ppppiiipppip",
     "ov3d_sa_layer_fwd_x0": "pppppiiippip",
     "ov3d_sa_layer_pool_fwd": "ppppiiiippppppip",
@@ -41,6 +42,7 @@ _SIGS = {
     "ov3d_sa_pool_bwd": "ppppppiippip",
     "ov3d_bn_bwd_finalize": "pdippppppppp",
     "ov3d_bn_relu_bwd": "ippppppppppiippipp",
+    "ov3d_bn_relu_bwd_cin": "ippppppppppiiippipp",
     "ov3d_nms3d": "ppiiidiipp",
     "ov3d_nms_boxes_from_corners": "pppiipp",
     "ov3d_clip_preprocess": "plppiiifffffffipp",

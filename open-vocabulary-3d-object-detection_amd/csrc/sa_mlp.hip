@@ -266,29 +266,41 @@ __global__ __launch_bounds__(kThreads, 2) void sa_layer_kernel(LayerArgs p) {
     }
 }
 
-// First layer: Cin = 3 fp32 (grouped, normalised xyz) -> C1 channels.
+// First layer: Cin = CIN fp32 (grouped, normalised xyz; + 3 colour features for ScanNet
+// with --use_color) -> C1 channels.
 // Chunks of 256 rows: their inputs staged through LDS by coalesced loads, then thread t
 // computes channel t % C1 of the rows t / C1, t / C1 + kThreads / C1, ...
 // y1 == NULL: BN statistics only.
+// y = x[0] w[0] + x[1] w[1] + ... in fmaf order: the Conv2d(1x1) of the first SA layer
+template <int CIN>
+__device__ __forceinline__ float l1_dot(const float* w, const float* x) {
+    float y = w[0] * x[0];
+#pragma unroll
+    for (int k = 1; k < CIN; ++k) y = fmaf(w[k], x[k], y);
+    return y;
+}
+
+template <int CIN>
 __global__ __launch_bounds__(kThreads) void sa_l1_kernel(const float* __restrict__ x0,
                                                          const float* __restrict__ W1, int R, int C1,
                                                          bf16* __restrict__ y1,
                                                          double* __restrict__ partials) {
     __shared__ double red[2][kThreads];
-    __shared__ float xs[kThreads * 3];
+    __shared__ float xs[kThreads * CIN];
     const int tid = threadIdx.x;
     const int c = tid % C1, ph = tid / C1, nph = kThreads / C1;
-    const float w0 = W1[c * 3], w1 = W1[c * 3 + 1], w2 = W1[c * 3 + 2];
+    float wr[CIN];
+#pragma unroll
+    for (int k = 0; k < CIN; ++k) wr[k] = W1[c * CIN + k];
     float s = 0.f, q = 0.f;
     const long long nchunk = ((long long)R + kThreads - 1) / kThreads;
     for (long long ck = blockIdx.x; ck < nchunk; ck += gridDim.x) {
         const long long r0 = ck * kThreads;
         const int nr = (int)min((long long)kThreads, (long long)R - r0);
-        for (int i = tid; i < 3 * nr; i += kThreads) xs[i] = x0[r0 * 3 + i];
+        for (int i = tid; i < CIN * nr; i += kThreads) xs[i] = x0[r0 * CIN + i];
         __syncthreads();
         for (int rr = ph; rr < nr; rr += nph) {
-            const float* x = xs + rr * 3;
-            const float y = fmaf(w2, x[2], fmaf(w1, x[1], w0 * x[0]));
+            const float y = l1_dot<CIN>(wr, xs + rr * CIN);
             const bf16 yb = (bf16)y;
             if (y1) y1[(r0 + rr) * C1 + c] = yb;
             const float f = (float)yb;
@@ -498,9 +510,9 @@ __global__ __launch_bounds__(1024) void bn_bwd_stats_finalize_kernel(
 // ReLU + BN backward over rows, C = 8 * (threads per row):
 // pass 0 (stats): partial sums of dt and dt*xhat, dt = relu'(a*y+b) * dz;
 // pass 1 (apply): dy = cA*dt + cB*y + cC stored as bf16;
-// pass 2 (weight): dy of a first layer with Cin = 3 is reduced against x0 into
-//                  dW1 partials (nparts, C, 3) and never stored.
-template <int PASS>
+// pass 2 (weight): dy of a first layer with Cin = CIN (3, or 6 with colour) is reduced
+//                  against x0 into dW1 partials (nparts, C, CIN) and never stored.
+template <int PASS, int CIN = 3>
 __global__ __launch_bounds__(kThreads) void bn_relu_bwd_kernel(
     const bf16* __restrict__ dz, const bf16* __restrict__ y, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -536,15 +548,19 @@ __global__ __launch_bounds__(kThreads) void bn_relu_bwd_kernel(
         for (int j = 0; j < 8; ++j) c2[j] = cC[kc + j];
     }
     float acc0[8], acc1[8], acc2[8];
+    float accx[PASS == 2 && CIN > 3 ? CIN - 3 : 1][8];   // dW1 columns 3.. (colour)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc0[j] = acc1[j] = acc2[j] = 0.f;
+    for (int j = 0; j < 8; ++j) {
+        acc0[j] = acc1[j] = acc2[j] = 0.f;
+#pragma unroll
+        for (int k = 0; k < (PASS == 2 && CIN > 3 ? CIN - 3 : 1); ++k) accx[k][j] = 0.f;
+    }
     for (long long r = (long long)blockIdx.x * nph + ph; r < R; r += (long long)gridDim.x * nph) {
         const bf16x8 vz = *reinterpret_cast<const bf16x8*>(dz + r * C + kc);
-        float xr[3];
+        float xr[PASS == 2 ? CIN : 3];
         if (PASS == 2) {
-            xr[0] = x0[r * 3];
-            xr[1] = x0[r * 3 + 1];
-            xr[2] = x0[r * 3 + 2];
+#pragma unroll
+            for (int k = 0; k < CIN; ++k) xr[k] = x0[r * CIN + k];
         }
         bf16x8 vy;
         if (PASS != 2 || y) {
@@ -569,6 +585,10 @@ __global__ __launch_bounds__(kThreads) void bn_relu_bwd_kernel(
                     acc0[j] = fmaf(d, xr[0], acc0[j]);
                     acc1[j] = fmaf(d, xr[1], acc1[j]);
                     acc2[j] = fmaf(d, xr[2], acc2[j]);
+                    if constexpr (PASS == 2 && CIN > 3) {
+#pragma unroll
+                        for (int k = 3; k < CIN; ++k) accx[k - 3][j] = fmaf(d, xr[k], accx[k - 3][j]);
+                    }
                 }
             }
         }
@@ -576,23 +596,36 @@ __global__ __launch_bounds__(kThreads) void bn_relu_bwd_kernel(
     }
     if (PASS == 1) return;
     // reduce over the row phases: LDS [value][phase * C + channel] (nph * C == 8 * kThreads)
+    // (CIN > 3: the 3 + CIN - 3 values go through the LDS in rounds of at most 3)
     __shared__ double sred[PASS == 0 ? 2 : 3][8 * kThreads];
-    const int nv = PASS == 0 ? 2 : 3;
+    constexpr int NV = PASS == 0 ? 2 : CIN;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        sred[0][ph * C + kc + j] = acc0[j];
-        sred[1][ph * C + kc + j] = acc1[j];
-        if constexpr (PASS == 2) sred[2][ph * C + kc + j] = acc2[j];
-    }
-    __syncthreads();
-    for (int i = tid; i < nv * C; i += kThreads) {
-        const int v = i / C, c = i % C;
-        double t = 0;
-        for (int k = 0; k < nph; ++k) t += sred[v][k * C + c];
-        if (PASS == 0)
-            partials[(size_t)blockIdx.x * 2 * C + v * C + c] = t;
-        else
-            partials[(size_t)blockIdx.x * 3 * C + c * 3 + v] = t;   // (C, 3) = dW1[c][k]
+    for (int v0 = 0; v0 < NV; v0 += 3) {
+        if (v0) __syncthreads();   // the previous round's reads are done
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+#pragma unroll
+            for (int u = 0; u < 3 && v0 + u < NV; ++u) {
+                const int v = v0 + u;
+                float a;
+                if (v == 0) a = acc0[j];
+                else if (v == 1) a = acc1[j];
+                else if (v == 2) a = acc2[j];
+                else a = accx[(v >= 3 ? v - 3 : 0) % (PASS == 2 && CIN > 3 ? CIN - 3 : 1)][j];
+                sred[u][ph * C + kc + j] = a;
+            }
+        }
+        __syncthreads();
+        const int nv = NV - v0 < 3 ? NV - v0 : 3;
+        for (int i = tid; i < nv * C; i += kThreads) {
+            const int u = i / C, c = i % C;
+            double t = 0;
+            for (int k = 0; k < nph; ++k) t += sred[u][k * C + c];
+            if (PASS == 0)
+                partials[(size_t)blockIdx.x * 2 * C + u * C + c] = t;
+            else   // (C, CIN) = dW1[c][k]
+                partials[(size_t)blockIdx.x * CIN * C + c * CIN + v0 + u] = t;
+        }
     }
 }
 
@@ -603,14 +636,23 @@ int grid_for(long long work, int cap) {
 
 }  // namespace
 
-extern "C" int ov3d_sa_l1_fwd(const float* x0, const float* W1, int R, int C1, void* y1,
-                              double* partials, int nparts, void* stream) {
+extern "C" int ov3d_sa_l1_fwd_cin(const float* x0, int cin, const float* W1, int R, int C1,
+                                  void* y1, double* partials, int nparts, void* stream) {
     if (R < 0 || C1 <= 0 || C1 > kThreads || kThreads % C1 || nparts <= 0) return OV3D_EINVAL;
-    if (!x0 || !W1 || !partials) return OV3D_EINVAL;
-    hipLaunchKernelGGL(sa_l1_kernel, dim3(nparts), dim3(kThreads), 0, ov3d_stream(stream), x0, W1, R,
-                       C1, reinterpret_cast<bf16*>(y1), partials);
+    if (!x0 || !W1 || !partials || (cin != 3 && cin != 6)) return OV3D_EINVAL;
+    if (cin == 3)
+        hipLaunchKernelGGL(sa_l1_kernel<3>, dim3(nparts), dim3(kThreads), 0, ov3d_stream(stream), x0,
+                           W1, R, C1, reinterpret_cast<bf16*>(y1), partials);
+    else
+        hipLaunchKernelGGL(sa_l1_kernel<6>, dim3(nparts), dim3(kThreads), 0, ov3d_stream(stream), x0,
+                           W1, R, C1, reinterpret_cast<bf16*>(y1), partials);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
+}
+
+extern "C" int ov3d_sa_l1_fwd(const float* x0, const float* W1, int R, int C1, void* y1,
+                              double* partials, int nparts, void* stream) {
+    return ov3d_sa_l1_fwd_cin(x0, 3, W1, R, C1, y1, partials, nparts, stream);
 }
 
 template <int MODE>
@@ -808,13 +850,14 @@ extern "C" int ov3d_bn_bwd_finalize(const double* totals, double count, int C, c
     return OV3D_OK;
 }
 
-extern "C" int ov3d_bn_relu_bwd(int pass, const void* dz, const void* y, const float* scale,
-                                const float* shift, const float* mean, const float* invstd,
-                                const float* cA, const float* cB, const float* cC, const float* x0,
-                                int R, int C, double* partials, void* dyout, int nparts,
-                                const float* W1, void* stream) {
+extern "C" int ov3d_bn_relu_bwd_cin(int pass, const void* dz, const void* y, const float* scale,
+                                    const float* shift, const float* mean, const float* invstd,
+                                    const float* cA, const float* cB, const float* cC,
+                                    const float* x0, int cin, int R, int C, double* partials,
+                                    void* dyout, int nparts, const float* W1, void* stream) {
     if (R < 0 || C <= 0 || C % 8 || C / 8 > kThreads || kThreads % (C / 8) || C > 256 ||
-        nparts <= 0 || !dz || !scale || !shift || (!y && !(pass == 2 && x0 && W1)))
+        nparts <= 0 || !dz || !scale || !shift || (!y && !(pass == 2 && x0 && W1 && cin == 3)) ||
+        (cin != 3 && cin != 6))
         return OV3D_EINVAL;
     const bf16* dzb = reinterpret_cast<const bf16*>(dz);
     const bf16* yb = reinterpret_cast<const bf16*>(y);
@@ -831,12 +874,26 @@ extern "C" int ov3d_bn_relu_bwd(int pass, const void* dz, const void* y, const f
                            reinterpret_cast<bf16*>(dyout), W1);
     } else if (pass == 2) {
         if (!cA || !cB || !cC || !x0 || !partials) return OV3D_EINVAL;
-        hipLaunchKernelGGL(bn_relu_bwd_kernel<2>, dim3(nparts), dim3(kThreads), 0, s, dzb, yb, scale,
-                           shift, mean, invstd, cA, cB, cC, x0, (long long)R, C, partials,
-                           (bf16*)nullptr, W1);
+        if (cin == 3)
+            hipLaunchKernelGGL(bn_relu_bwd_kernel<2>, dim3(nparts), dim3(kThreads), 0, s, dzb, yb,
+                               scale, shift, mean, invstd, cA, cB, cC, x0, (long long)R, C, partials,
+                               (bf16*)nullptr, W1);
+        else
+            hipLaunchKernelGGL((bn_relu_bwd_kernel<2, 6>), dim3(nparts), dim3(kThreads), 0, s, dzb,
+                               yb, scale, shift, mean, invstd, cA, cB, cC, x0, (long long)R, C,
+                               partials, (bf16*)nullptr, W1);
     } else {
         return OV3D_EINVAL;
     }
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
+}
+
+extern "C" int ov3d_bn_relu_bwd(int pass, const void* dz, const void* y, const float* scale,
+                                const float* shift, const float* mean, const float* invstd,
+                                const float* cA, const float* cB, const float* cC, const float* x0,
+                                int R, int C, double* partials, void* dyout, int nparts,
+                                const float* W1, void* stream) {
+    return ov3d_bn_relu_bwd_cin(pass, dz, y, scale, shift, mean, invstd, cA, cB, cC, x0, 3, R, C,
+                                partials, dyout, nparts, W1, stream);
 }

@@ -66,11 +66,12 @@ def supported(mlp, x0, S):
             and torch.get_autocast_dtype("cuda") == torch.bfloat16):
         return False
     layers = list(mlp)
-    if len(layers) != 3 or x0.requires_grad or x0.dim() != 2 or x0.shape[1] != 3:
+    # first-layer input: grouped xyz (3), or xyz + colour (6: ScanNet --use_color)
+    if len(layers) != 3 or x0.requires_grad or x0.dim() != 2 or x0.shape[1] not in (3, 6):
         return False
     if S not in (32, 64) or x0.shape[0] % 64:
         return False
-    dims = [3]
+    dims = [x0.shape[1]]
     for l in layers:
         if not hasattr(l, "bn") or l.conv.bias is not None:
             return False
@@ -151,7 +152,7 @@ class _SAMLPPool(Function):
     @staticmethod
     def forward(ctx, x0, w1, w2, w3, g1, b1, g2, b2, g3, b3, bns, S):
         dev = x0.device
-        R = x0.shape[0]
+        R, cin = x0.shape
         P = R // S
         c1, c2, c3 = w1.shape[0], w2.shape[0], w3.shape[0]
         groups = [_sync_group(bn) for bn in bns]
@@ -161,13 +162,13 @@ class _SAMLPPool(Function):
         # z1 is kept for the backward only when that does not recompute it (sa_dy2_fused), and
         # then y1 is not stored either: every consumer recomputes it from x0 (12 B per row
         # instead of 128 B: the (R, 64) first-layer output never reaches HBM)
-        fused_bwd2 = FUSED_BWD and c1 == 64 and c2 == 128 and \
+        fused_bwd2 = FUSED_BWD and cin == 3 and c1 == 64 and c2 == 128 and \
             bool(nat.load().ov3d_sa_dy_fused_supported(c2, w3.shape[0]))
         w1f = w1.float().contiguous()
         # layer 1 (statistics only when y1 is recomputed)
         y1 = None if fused_bwd2 else torch.empty((R, c1), dtype=bf, device=dev)
         parts = torch.empty((NPARTS_ROWS, 2, c1), dtype=torch.float64, device=dev)
-        nat.call("ov3d_sa_l1_fwd", x0, w1f, R, c1, y1, parts, NPARTS_ROWS, like=x0)
+        nat.call("ov3d_sa_l1_fwd_cin", x0, cin, w1f, R, c1, y1, parts, NPARTS_ROWS, like=x0)
         st1 = _bn_stats(parts, NPARTS_ROWS, c1, groups[0], R * world[0], bns[0])
         # layer 2
         w2b = cast_param(w2, bf).contiguous()
@@ -269,16 +270,18 @@ class _SAMLPPool(Function):
                      parts, None, NPARTS_ROWS, None, like=dout)
         # layer 1: ReLU + BN backward, dW1 reduced against x0 (dy1 never stored)
         cA, cB, cC, dg1, db1 = bn_bwd_affine(parts, nparts, c1, groups[0], R * world[0], g1, m1, i1)
-        parts = torch.empty((NPARTS_ROWS, c1, 3), dtype=torch.float64, device=dev)
-        nat.call("ov3d_bn_relu_bwd", 2, dz1, y1, a1, s1, None, None, cA, cB, cC, x0, R, c1, parts,
-                 None, NPARTS_ROWS, w1f, like=dout)
-        dw1 = _totals(parts, NPARTS_ROWS, 3 * c1, None).view(c1, 3).float().view(w1shape)
+        cin = x0.shape[1]
+        parts = torch.empty((NPARTS_ROWS, c1, cin), dtype=torch.float64, device=dev)
+        nat.call("ov3d_bn_relu_bwd_cin", 2, dz1, y1, a1, s1, None, None, cA, cB, cC, x0, cin, R, c1,
+                 parts, None, NPARTS_ROWS, w1f, like=dout)
+        dw1 = _totals(parts, NPARTS_ROWS, cin * c1, None).view(c1, cin).float().view(w1shape)
         return (None, dw1, dw2.view(c2, c1), dw3.view(c3, c2), dg1, db1, dg2, db2, dg3, db3, None,
                 None)
 
 
 def sa_mlp_pool(mlp, x0, S):
-    """(R, 3) grouped xyz rows -> (R / S, C3) pooled features (fp32), fused training path."""
+    """(R, 3) grouped xyz rows (or (R, 6) xyz + colour) -> (R / S, C3) pooled features
+    (fp32), fused training path."""
     layers = list(mlp)
     ws = [l.conv.weight for l in layers]
     ws = [w.view(w.shape[0], w.shape[1]) for w in ws]

@@ -182,17 +182,18 @@ def test_last_layer_backward_one_pass_equals_three_passes(cuda, monkeypatch, nsa
         assert e < 2e-3, (n, e)
 
 
-@pytest.mark.parametrize("kind", ["scannet_colour", "interim"])
+@pytest.mark.parametrize("kind", ["scannet_colour", "scannet_colour_rows", "interim"])
 def test_sa_rows_bn_relu_path_vs_fp32(cuda, monkeypatch, kind):
-    """SA modules the 3-channel fused kernels do not take (ScanNet pre-encoder with colour:
-    6 input channels; the masked encoder's interim SA: 256 features + xyz, gradient to the
-    features) run BN + ReLU on the HIP row kernels (heads.bn_relu_rows) under bf16
-    autocast.  Against the fp32 module: outputs, running statistics and gradients no further
-    from fp32 than PyTorch's own bf16 batch_norm path (+ slack)."""
-    from ov3d_amd import heads, synthetic
+    """ScanNet pre-encoder SA with colour (6 input channels): the fused MFMA kernels
+    (sa_fused, first layer on 6 channels) — and, forced off, the rows path; the masked
+    encoder's interim SA (256 features + xyz, gradient to the features): BN + ReLU on the
+    HIP row kernels (heads.bn_relu_rows).  Under bf16 autocast, against the fp32 module:
+    outputs, running statistics and gradients no further from fp32 than PyTorch's own bf16
+    batch_norm path (+ slack)."""
+    from ov3d_amd import heads, sa_fused, synthetic
     from ov3d_amd.pointnet2_modules import PointnetSAModuleVotes
     torch.manual_seed(4)
-    if kind == "scannet_colour":
+    if kind.startswith("scannet_colour"):
         sa = PointnetSAModuleVotes(radius=0.2, nsample=64, npoint=512, mlp=[3, 64, 128, 256],
                                    normalize_xyz=True)
         B, N, C = 2, 4096, 3
@@ -214,16 +215,21 @@ def test_sa_rows_bn_relu_path_vs_fp32(cuda, monkeypatch, kind):
         feats = feats0.clone().requires_grad_(kind == "interim")
         if not rows:
             monkeypatch.setattr(heads, "bn_relu_rows_ok", lambda *a: False)
-        calls = []
-        real = heads.bn_relu_rows
+        if not rows or kind != "scannet_colour":
+            monkeypatch.setattr(sa_fused, "supported", lambda *a: False)
+        calls, fcalls = [], []
+        real, freal = heads.bn_relu_rows, sa_fused.sa_mlp_pool
         monkeypatch.setattr(heads, "bn_relu_rows", lambda *a, **k: calls.append(1) or real(*a, **k))
+        monkeypatch.setattr(sa_fused, "sa_mlp_pool", lambda *a: fcalls.append(1) or freal(*a))
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
             _, f, _ = twin(xyz, feats)
         monkeypatch.undo()
         if gw is None:
             gw = torch.randn(f.shape, device=cuda)
         (f.float() * gw).sum().backward()
-        assert len(calls) == (3 if name == "hip" else 0), (name, len(calls))
+        fused = name == "hip" and kind == "scannet_colour"
+        assert len(fcalls) == (1 if fused else 0), (name, len(fcalls))
+        assert len(calls) == (3 if name == "hip" and not fused else 0), (name, len(calls))
         g = {n: p.grad.clone() for n, p in twin.named_parameters()}
         if feats.requires_grad:
             g["features"] = feats.grad.clone()

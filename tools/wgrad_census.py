@@ -1,5 +1,5 @@
 """List the deferred weight-gradient problems of one bench training step (R, N, K, nsplit,
-GFLOP) in launch order.  python tools/wgrad_census.py   (GPU)"""
+GFLOP) in launch order.  python tools/wgrad_census.py [sun|scannet]   (GPU)"""
 import json
 import os
 import sys
@@ -15,10 +15,14 @@ def main():
     import bench
     from ov3d_amd import _native, gemm, synthetic
     dev = torch.device("cuda", 0)
-    args = bench.default_args()
-    model, crit, opt = bench.build(args, dev)
+    wl = bench.WORKLOADS[sys.argv[1] if len(sys.argv) > 1 else "sun"]
+    args = bench.default_args(**wl["args"])
+    ds = wl.get("dataset", "sunrgbd")
+    model, crit, opt = bench.build(args, dev, dataset=ds)
     gemm.DEFER_WGRAD = True
-    batch = synthetic.make_batch(8, seed=1, device=dev)
+    kw = {"num_points": wl["points"]} if "points" in wl else {}
+    kw["use_color"] = bool(getattr(args, "use_color", False))
+    batch = synthetic.make_batch(wl["batch"], seed=1, device=dev, dataset=ds, **kw)
     seen = []
     orig = _native.call
 
