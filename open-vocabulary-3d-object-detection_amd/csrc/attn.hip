@@ -923,46 +923,71 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_batch_kernel(AttnBwdBatc
     attn_bwd_dkdv_body<DROP, false>(g.a[blockIdx.z]);
 }
 
-// mask (B, Lq, Lk) -> 1-bit words, thread per word: words [0, W) query-major
-// [nkt][B][Lq][2] (bit n of lane (q, h) = key 64 kt + drop_key(n, h)), words [W, 2W) key-major
-// [Lq/32][B][nkt*64] (bit n = query 32 qb + n).  KIND 0: uint8 mask, nonzero = not attended;
-// KIND 1: fp32 distances, not attended iff d >= thr (MaskedTransformerEncoder.compute_mask)
+// mask (B, Lq, Lk) -> 1-bit words: words [0, W) query-major [nkt][B][Lq][2] (bit n of lane
+// (q, h) = key 64 kt + drop_key(n, h)), words [W, 2W) key-major [Lq/32][B][nkt*64] (bit n =
+// query 32 qb + n).  KIND 0: uint8 mask, nonzero = not attended; KIND 1: fp32 distances, not
+// attended iff d >= thr (MaskedTransformerEncoder.compute_mask).
+// Query-major: a thread per (b, q, 64-key tile) reads the tile's 64 contiguous values and
+// writes both halves' words; key-major: a thread per (32-query block, b, key) reads one
+// column (consecutive threads = consecutive keys: coalesced).
+template <int KIND>
+__device__ __forceinline__ bool mask_at(const void* src, size_t e, float thr) {
+    if (KIND == 0) return ((const uint8_t*)src)[e] != 0;
+    return ((const float*)src)[e] >= thr;
+}
+
 template <int KIND>
 __global__ void __launch_bounds__(256) attn_mask_pack_kernel(const void* __restrict__ src, float thr,
                                                              int B, int Lq, int Lk, int nkt,
                                                              uint32_t* __restrict__ words) {
     const long long W = (long long)nkt * B * Lq * 2;
+    const long long nq = (long long)B * Lq * nkt;   // query-major threads
     const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= 2 * W) return;
-    auto masked = [&](int b, int q, int k) -> bool {
-        const size_t e = ((size_t)b * Lq + q) * Lk + k;
-        if (KIND == 0) return ((const uint8_t*)src)[e] != 0;
-        return ((const float*)src)[e] >= thr;
-    };
-    uint32_t w = 0;
-    if (t < W) {
-        const int h = (int)(t & 1);
-        const long long r = t >> 1;
-        const int q = (int)(r % Lq);
-        const long long kb = r / Lq;
-        const int b = (int)(kb % B), kt = (int)(kb / B);
-#pragma unroll 4
-        for (int n = 0; n < 32; ++n) {
-            const int k = 64 * kt + drop_key(n, h);
-            if (k < Lk && masked(b, q, k)) w |= 1u << n;
+    if (t < nq) {
+        const int kt = (int)(t % nkt);
+        const long long bq = t / nkt;
+        const int q = (int)(bq % Lq), b = (int)(bq / Lq);
+        const size_t row = ((size_t)b * Lq + q) * Lk + 64 * kt;
+        uint32_t w0 = 0, w1 = 0;
+        const bool full = 64 * kt + 64 <= Lk;
+        if (KIND == 1 && full && (row & 3) == 0) {
+#pragma unroll
+            for (int c = 0; c < 16; ++c) {
+                const float4 v = *reinterpret_cast<const float4*>((const float*)src + row + 4 * c);
+                const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int kk = 4 * c + u;   // key offset in the tile -> (half, bit)
+                    const int rem = kk & 31;
+                    const int bit = (kk & 1) * 16 + (kk >> 5) * 8 + (rem >> 3) * 2 + ((rem >> 1) & 1);
+                    const uint32_t m = vv[u] >= thr ? 1u << bit : 0u;
+                    if ((rem >> 2) & 1) w1 |= m; else w0 |= m;
+                }
+            }
+        } else {
+            for (int kk = 0; kk < 64 && 64 * kt + kk < Lk; ++kk) {
+                const int rem = kk & 31;
+                const int bit = (kk & 1) * 16 + (kk >> 5) * 8 + (rem >> 3) * 2 + ((rem >> 1) & 1);
+                const uint32_t m = mask_at<KIND>(src, row + kk, thr) ? 1u << bit : 0u;
+                if ((rem >> 2) & 1) w1 |= m; else w0 |= m;
+            }
         }
-    } else {
-        const long long u = t - W;
-        const int k = (int)(u % ((long long)nkt * 64));
-        const long long qb = u / ((long long)nkt * 64);
-        const int b = (int)(qb % B), q0 = 32 * (int)(qb / B);
-        if (k < Lk) {
-#pragma unroll 4
-            for (int n = 0; n < 32; ++n)
-                if (q0 + n < Lq && masked(b, q0 + n, k)) w |= 1u << n;
-        }
+        uint32_t* o = words + (((size_t)kt * B + b) * Lq + q) * 2;
+        *reinterpret_cast<uint2*>(o) = make_uint2(w0, w1);
+        return;
     }
-    words[t] = w;
+    const long long u = t - nq;
+    if (u >= W) return;
+    const int k = (int)(u % ((long long)nkt * 64));
+    const long long qb = u / ((long long)nkt * 64);
+    const int b = (int)(qb % B), q0 = 32 * (int)(qb / B);
+    uint32_t w = 0;
+    if (k < Lk) {
+#pragma unroll 8
+        for (int n = 0; n < 32; ++n)
+            if (q0 + n < Lq && mask_at<KIND>(src, ((size_t)b * Lq + q0 + n) * Lk + k, thr)) w |= 1u << n;
+    }
+    words[W + u] = w;
 }
 
 }  // namespace
@@ -997,7 +1022,8 @@ extern "C" int ov3d_attn_mask_pack(const void* src, int kind, float thr, int B, 
     if (!src || !words || (kind != 0 && kind != 1) || B <= 0 || Lq <= 0 || Lk <= 0 || (Lq % QW))
         return OV3D_EINVAL;
     const int nkt = (Lk + KB - 1) / KB;
-    const long long n = ov3d_attn_maskbits_words(B, Lq, Lk);
+    // threads: B*Lq*nkt query-major (two words each) + W key-major
+    const long long n = (long long)B * Lq * nkt + ov3d_attn_maskbits_words(B, Lq, Lk) / 2;
     hipStream_t st = ov3d_stream(stream);
     if (kind == 0)
         attn_mask_pack_kernel<0><<<ov3d_cdiv(n, 256), 256, 0, st>>>(src, thr, B, Lq, Lk, nkt, words);

@@ -248,6 +248,7 @@ def fused_weight_grad(dy, x, bias=True, out_w=None, out_b=None):
 # enabled only by the single-process training step (bench.py / graphs.StepGraph), never
 # under DDP (its reducer needs the per-parameter gradient hooks).
 DEFER_WGRAD = False
+WGRAD_SINGLE_MIN_R = int(os.environ.get("OV3D_WGRAD_SINGLE_MIN_R", str(1 << 17)))
 _PENDING = []
 _PENDING_COLS = []   # deferred LayerNorm weight / bias gradients (resnorm.py)
 _QUEUED = [False]
@@ -379,15 +380,28 @@ def flush_weight_grads():
         r0, r1 = rows if rows is not None else (0, wshape[0])
         dw = bufs[id(wp)][1].view(wshape)[r0:r1].reshape(r1 - r0, K)
         db = bufs[id(bp)][1][r0:r1] if bp is not None else None
+        if R >= WGRAD_SINGLE_MIN_R:
+            # long problems (the masked encoder's interim SA, R = 2^18) run on their own
+            # launch: the grouped stream-K split gives them hundreds of partial slots
+            # (tools/wgrad_big.py: 104 vs 140 us at R = 2^18, N = K = 256)
+            fused_weight_grad(dy, x, bias=db is not None, out_w=dw, out_b=db)
+            continue
         probs.append(_WgProblem(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), R, N, K,
                                 _wg_group_splits(R), dw.data_ptr(), dw.stride(0),
                                 db.data_ptr() if db is not None else None))
+    if not probs:
+        _assign_grads(bufs)
+        return
     arr = (_WgProblem * len(probs))(*probs)
     lib = _native.load()
     ws_n = lib.ov3d_wgrad_group_workspace(ctypes.addressof(arr), len(probs))
     dev = items[0][0].device
     ws = torch.empty((max(ws_n, 1),), dtype=torch.float32, device=dev)
     _native.call("ov3d_wgrad_group", ctypes.addressof(arr), len(probs), ws, like=ws)
+    _assign_grads(bufs)
+
+
+def _assign_grads(bufs):
     with torch.no_grad():
         for param, g, _ in bufs.values():
             if param.grad is None:

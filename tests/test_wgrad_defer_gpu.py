@@ -12,11 +12,15 @@ from helpers import ov3d  # noqa: F401
 pytestmark = pytest.mark.gpu
 
 
-def test_deferred_weight_grads_equal_immediate(cuda):
+@pytest.mark.parametrize("single_min_r", [1 << 17, 1 << 13])
+def test_deferred_weight_grads_equal_immediate(cuda, monkeypatch, single_min_r):
+    """single_min_r = 2^13: the R = 16384 problems leave the grouped launch for their own
+    ov3d_wgrad launches (gemm.WGRAD_SINGLE_MIN_R, the path of the long SA problems)"""
     import ov3d_amd
     from bench import default_args
     from ov3d_amd import gemm, synthetic
     from ov3d_amd.dataset_config import SunrgbdDatasetConfig
+    monkeypatch.setattr(gemm, "WGRAD_SINGLE_MIN_R", single_min_r)
     args = default_args(enc_dropout=0.0, dec_dropout=0.0, mlp_dropout=0.0)
     cfg = SunrgbdDatasetConfig()
     torch.manual_seed(0)
