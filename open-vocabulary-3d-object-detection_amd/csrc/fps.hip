@@ -22,6 +22,8 @@
 // (bit-reversed thread id, then k).  Within one of our threads the slots are
 // visited in increasing rank order (1024 is a multiple of the upstream block
 // size), so strict '>' there and the u64 key across threads reproduce it.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -512,6 +514,8 @@ __device__ __forceinline__ float sgpr_f(float v) {
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
 }
 
+// kCS: slots per cluster-B chunk (kNCB = kPS / kCS chunks, <= 16)
+template <int kCS>
 __global__ __launch_bounds__(kThreads) void fps_stream_kernel(const float* __restrict__ xyz, int N,
                                                               int M, int L,
                                                               float4* __restrict__ ws,
@@ -520,6 +524,8 @@ __global__ __launch_bounds__(kThreads) void fps_stream_kernel(const float* __res
     constexpr int PA = kPR * 64, PB = kPS * 64;   // positions per wave: cluster A, cluster B
     constexpr int NA = kWaves * PA;               // cluster B positions start here
     constexpr int NS = kPR + kPS;                 // slots per thread in the setup
+    constexpr int kNCB = kPS / kCS;
+    static_assert(kPS % kCS == 0 && kNCB <= 16, "cluster B chunking");
     __shared__ uint32_t s_hist[kCells];
     __shared__ uint16_t s_perm[kThreads * NS];
     __shared__ uint16_t s_out[kMaxOutLDS];
@@ -607,9 +613,17 @@ __global__ __launch_bounds__(kThreads) void fps_stream_kernel(const float* __res
             s_perm[s_hist[cp[i] >> 16] + (cp[i] & 0xffffu)] = (uint16_t)(tid + i * kThreads);
     __syncthreads();
 
-    // ---- (c) cluster B slots (first: their ranks are dead before cluster A fills its registers): positions NA + w*PB + i*64 + lane, sorted by rank, to the workspace
-    float bLo[3] = {INFINITY, INFINITY, INFINITY}, bHi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    // ---- (c) cluster B slots (first: their ranks are dead before cluster A fills its
+    //      registers): positions NA + w*PB + i*64 + lane, sorted by rank, to the workspace.
+    //      Cluster B is culled per chunk of 4 slots (256 consecutive Morton positions):
+    //      chunk c's bounding box and cached best live in lane c (lane-distributed).
+    float qLo[3] = {INFINITY, INFINITY, INFINITY}, qHi[3] = {-INFINITY, -INFINITY, -INFINITY};
     {
+        float cLo[kNCB][3], cHi[kNCB][3];
+#pragma unroll
+        for (int c = 0; c < kNCB; ++c)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) { cLo[c][a] = INFINITY; cHi[c][a] = -INFINITY; }
         uint32_t rk[kPS];
 #pragma unroll
         for (int i = 0; i < kPS; ++i) {
@@ -635,12 +649,21 @@ __global__ __launch_bounds__(kThreads) void fps_stream_kernel(const float* __res
                 const bool skip = (double)fmaf(z, z, fmaf(y, y, x * x)) <= 1e-3;
                 e = make_float4(x, y, z, skip ? -1.f : 1e10f);
                 if (!skip) {
-                    bLo[0] = fminf(bLo[0], x); bLo[1] = fminf(bLo[1], y); bLo[2] = fminf(bLo[2], z);
-                    bHi[0] = fmaxf(bHi[0], x); bHi[1] = fmaxf(bHi[1], y); bHi[2] = fmaxf(bHi[2], z);
+                    float* lo = cLo[i / kCS];
+                    float* hi = cHi[i / kCS];
+                    lo[0] = fminf(lo[0], x); lo[1] = fminf(lo[1], y); lo[2] = fminf(lo[2], z);
+                    hi[0] = fmaxf(hi[0], x); hi[1] = fmaxf(hi[1], y); hi[2] = fmaxf(hi[2], z);
                 }
             }
             wsw[64 * i + lane] = e;
         }
+#pragma unroll
+        for (int c = 0; c < kNCB; ++c)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const float lo = wave_fmin(cLo[c][a]), hi = wave_fmax(cHi[c][a]);
+                if (lane == c) { qLo[a] = lo; qHi[a] = hi; }
+            }
     }
     // ---- cluster A slots: positions w*PA + i*64 + lane, sorted by rank, in registers
     float px[kPR], py[kPR], pz[kPR], td[kPR];
@@ -682,8 +705,6 @@ __global__ __launch_bounds__(kThreads) void fps_stream_kernel(const float* __res
     for (int a = 0; a < 3; ++a) {   // wave-uniform: scalar registers
         aLo[a] = sgpr_f(wave_fmin(aLo[a]));
         aHi[a] = sgpr_f(wave_fmax(aHi[a]));
-        bLo[a] = sgpr_f(wave_fmin(bLo[a]));
-        bHi[a] = sgpr_f(wave_fmax(bHi[a]));
     }
     __syncthreads();   // s_perm complete before any tie lookup
     // this wave's cluster-B slots through a buffer descriptor: scalar base + lane offset +
@@ -696,9 +717,13 @@ __global__ __launch_bounds__(kThreads) void fps_stream_kernel(const float* __res
     const float x0 = p[0], y0 = p[1], z0 = p[2];
     float x1 = x0, y1 = y0, z1 = z0;
     // per-cluster cache: max running distance, best distance bits, position, coordinates
-    float aT = INFINITY, bT = INFINITY;
-    int aD = __float_as_int(-1.f), bD = __float_as_int(-1.f), aP = 0, bP = 0;
-    float aX = 0.f, aY = 0.f, aZ = 0.f, bX = 0.f, bY = 0.f, bZ = 0.f;
+    float aT = INFINITY;
+    int aD = __float_as_int(-1.f), aP = 0;
+    float aX = 0.f, aY = 0.f, aZ = 0.f;
+    // cluster B chunk caches, chunk c in lane c (lanes >= kNCB: never updated)
+    float qT = lane < kNCB ? INFINITY : -INFINITY;
+    int qD = __float_as_int(-1.f), qP = 0;
+    float qX = 0.f, qY = 0.f, qZ = 0.f;
 
     // wave argmax of (dist bits bb, slot bi, coords) over the lanes -> cache (T, D, P, X, Y, Z)
     auto wave_pick = [&](float best, int bi, float sx, float sy, float sz, int pbase,
@@ -748,34 +773,59 @@ __global__ __launch_bounds__(kThreads) void fps_stream_kernel(const float* __res
                 wave_pick(best, bi, sx, sy, sz, w * PA, aT, aD, aP, aX, aY, aZ);
             }
         }
-        {   // cluster B (workspace, L2-resident)
-            const float gx = fmaxf(fmaxf(bLo[0] - x1, x1 - bHi[0]), 0.f);
-            const float gy = fmaxf(fmaxf(bLo[1] - y1, y1 - bHi[1]), 0.f);
-            const float gz = fmaxf(fmaxf(bLo[2] - z1, z1 - bHi[2]), 0.f);
-            if (fmaf(gz, gz, fmaf(gy, gy, gx * gx)) < bT) {
+        {   // cluster B (workspace, L2-resident): only the chunks that can change are loaded
+            const float gx = fmaxf(fmaxf(qLo[0] - x1, x1 - qHi[0]), 0.f);
+            const float gy = fmaxf(fmaxf(qLo[1] - y1, y1 - qHi[1]), 0.f);
+            const float gz = fmaxf(fmaxf(qLo[2] - z1, z1 - qHi[2]), 0.f);
+            unsigned long long need = __ballot(fmaf(gz, gz, fmaf(gy, gy, gx * gx)) < qT);
+            while (need) {
+                const int c = __builtin_amdgcn_readfirstlane(__ffsll((long long)need) - 1);
+                need &= need - 1;
                 float best = -1.f, sx = 0.f, sy = 0.f, sz = 0.f;
                 int bi = 0;
+                float4 e[kCS];
 #pragma unroll
-                for (int c = 0; c < kPS; c += 4) {
-                    float4 e[4];
+                for (int u = 0; u < kCS; ++u)
+                    e[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                               wsr, lane * 16, 1024 * (kCS * c + u), 0));
 #pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        e[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                   wsr, lane * 16, 1024 * (c + u), 0));
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const float dx = e[u].x - x1, dy = e[u].y - y1, dz = e[u].z - z1;
-                        const float d2 = fminf(fmaf(dz, dz, fmaf(dy, dy, dx * dx)), e[u].w);
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(d2), wsr, lane * 16 + 12,
-                                                              1024 * (c + u), 0);
-                        const bool gt = d2 > best;
-                        best = gt ? d2 : best;
-                        bi = gt ? c + u : bi;
-                        sx = gt ? e[u].x : sx; sy = gt ? e[u].y : sy; sz = gt ? e[u].z : sz;
-                    }
+                for (int u = 0; u < kCS; ++u) {
+                    const float dx = e[u].x - x1, dy = e[u].y - y1, dz = e[u].z - z1;
+                    const float d2 = fminf(fmaf(dz, dz, fmaf(dy, dy, dx * dx)), e[u].w);
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(d2), wsr, lane * 16 + 12,
+                                                          1024 * (kCS * c + u), 0);
+                    const bool gt = d2 > best;
+                    best = gt ? d2 : best;
+                    bi = gt ? kCS * c + u : bi;
+                    sx = gt ? e[u].x : sx; sy = gt ? e[u].y : sy; sz = gt ? e[u].z : sz;
                 }
-                wave_pick(best, bi, sx, sy, sz, NA + w * PB, bT, bD, bP, bX, bY, bZ);
+                float T, X = 0.f, Y = 0.f, Z = 0.f;
+                int Dd, P = 0;
+                wave_pick(best, bi, sx, sy, sz, NA + w * PB, T, Dd, P, X, Y, Z);
+                if (lane == c) { qT = T; qD = Dd; qP = P; qX = X; qY = Y; qZ = Z; }
             }
+        }
+        // cluster B's candidate: the best chunk cache (ties: smallest rank)
+        int bD, bP;
+        float bX, bY, bZ;
+        {
+            const int dq = lane < kNCB ? qD : INT_MIN;
+            bD = __builtin_amdgcn_readlane(row_max_i32(dq), 0);
+            int lc = 0;
+            if (bD >= 0) {
+                const unsigned long long cand = __ballot(lane < kNCB && qD == bD);
+                if (__popcll(cand) == 1) {
+                    lc = __ffsll((long long)cand) - 1;
+                } else {
+                    const uint32_t r = (lane < kNCB && qD == bD) ? fps_rank(s_perm[qP], L) : 0xffffffffu;
+                    const uint32_t rm = __builtin_amdgcn_readlane(row_min_u32(r), 0);
+                    lc = __ffsll((long long)(__ballot(r == rm) & cand)) - 1;
+                }
+            }
+            bP = __builtin_amdgcn_readlane(qP, lc);
+            bX = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qX), lc));
+            bY = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qY), lc));
+            bZ = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qZ), lc));
         }
         // the wave's candidate: larger distance, equal distances -> smaller rank
         bool useB = bD > aD;
@@ -860,8 +910,21 @@ extern "C" int ov3d_fps(const float* xyz, int B, int N, int M, int32_t* idx_out,
         else launch_cull<20>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
     } else if (N <= kThreads * (kPR + kPS) && M <= kMaxOutLDS) {
         if (!workspace) return OV3D_EINVAL;
-        hipLaunchKernelGGL(fps_stream_kernel, dim3(B), dim3(kThreads), 0, s, xyz, N, M, L,
-                           reinterpret_cast<float4*>(workspace), idx_out, new_xyz_out);
+        // chunk size of the workspace cluster's culling (OV3D_FPS_CHUNK: measurement knob)
+        static const int cs = [] {
+            const char* e = getenv("OV3D_FPS_CHUNK");
+            return e ? atoi(e) : 4;
+        }();
+        float4* ws4 = reinterpret_cast<float4*>(workspace);
+        if (cs == 2)
+            hipLaunchKernelGGL(fps_stream_kernel<2>, dim3(B), dim3(kThreads), 0, s, xyz, N, M, L, ws4,
+                               idx_out, new_xyz_out);
+        else if (cs == 3)
+            hipLaunchKernelGGL(fps_stream_kernel<3>, dim3(B), dim3(kThreads), 0, s, xyz, N, M, L, ws4,
+                               idx_out, new_xyz_out);
+        else
+            hipLaunchKernelGGL(fps_stream_kernel<4>, dim3(B), dim3(kThreads), 0, s, xyz, N, M, L, ws4,
+                               idx_out, new_xyz_out);
     } else {
         if (!workspace) return OV3D_EINVAL;
         hipLaunchKernelGGL(fps_global_kernel, dim3(B), dim3(kThreads), 0, s, xyz, N, M, L, workspace,
