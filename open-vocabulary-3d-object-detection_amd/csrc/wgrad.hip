@@ -24,6 +24,8 @@
 #include <type_traits>
 #include <vector>
 
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -684,6 +686,12 @@ static int cu_count() {
             cus = n;
         else
             cus = 256;
+        // OV3D_WGRAD_WGS: workgroups of the stream-K launch (measurement knob; default one
+        // per CU)
+        if (const char* e = getenv("OV3D_WGRAD_WGS")) {
+            const int v = atoi(e);
+            if (v > 0) cus = v;
+        }
     }
     return cus;
 }

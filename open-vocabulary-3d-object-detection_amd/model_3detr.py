@@ -170,11 +170,17 @@ class Model3DETR(nn.Module):
         return xyz, feats
 
     # index work that depends on the input points only (sampling_plan)
-    PLAN_KEYS = ("pre_enc_inds", "pre_enc_xyz", "pre_enc_ball", "query_xyz")
+    PLAN_KEYS = ("pre_enc_inds", "pre_enc_xyz", "pre_enc_ball", "query_xyz", "interim_inds",
+                 "interim_xyz", "interim_ball")
 
     def _encoder_keeps_xyz(self):
         from .transformer import MaskedTransformerEncoder
         return not isinstance(self.encoder, MaskedTransformerEncoder)
+
+    def _interim_sa(self):
+        """the masked encoder's interim downsampling SA (None for the vanilla encoder)"""
+        return None if self._encoder_keeps_xyz() else getattr(self.encoder, "interim_downsampling",
+                                                               None)
 
     @torch.no_grad()
     def sampling_plan(self, point_clouds):
@@ -190,6 +196,16 @@ class Model3DETR(nn.Module):
                 "pre_enc_ball": pu.ball_query(pe.grouper.radius, pe.grouper.nsample, xyz, pre_xyz)}
         if self._encoder_keeps_xyz():
             plan["query_xyz"] = pu.furthest_point_sample_gather(pre_xyz, self.num_queries)[1]
+        elif self._interim_sa() is not None:
+            # masked encoder (transformer.py:192-197): its interim SA samples the pre-encoder
+            # points, so its FPS / ball query and the query FPS on its output points are also
+            # functions of the input points
+            ids = self._interim_sa()
+            i_inds, i_xyz = pu.furthest_point_sample_gather(pre_xyz, ids.npoint)
+            plan.update(interim_inds=i_inds, interim_xyz=i_xyz,
+                        interim_ball=pu.ball_query(ids.grouper.radius, ids.grouper.nsample,
+                                                   pre_xyz, i_xyz),
+                        query_xyz=pu.furthest_point_sample_gather(i_xyz, self.num_queries)[1])
         return plan
 
     def run_encoder(self, point_clouds, pre_enc_inds=None, plan=None):
@@ -203,7 +219,13 @@ class Model3DETR(nn.Module):
             new_xyz=plan.get("pre_enc_xyz") if pre_enc_inds is not None else None,
             ball=plan.get("pre_enc_ball") if pre_enc_inds is not None else None)
         # (B, C, M) view of channels-last rows -> seq-first (M, B, C)
-        enc_xyz, enc_feats, enc_inds = self.encoder(pre_feats.permute(2, 0, 1).contiguous(), xyz=pre_xyz)
+        src = pre_feats.permute(2, 0, 1).contiguous()
+        if "interim_inds" in plan:
+            enc_xyz, enc_feats, enc_inds = self.encoder(
+                src, xyz=pre_xyz, interim_plan=(plan["interim_inds"], plan["interim_xyz"],
+                                                plan["interim_ball"]))
+        else:
+            enc_xyz, enc_feats, enc_inds = self.encoder(src, xyz=pre_xyz)
         if enc_inds is None:
             enc_inds = pre_inds
         else:

@@ -41,7 +41,7 @@ NPARTS_ROWS = 1024     # row-pass workgroups
 NPARTS_POOL = 256
 # last layer's backward in one pass (csrc/sa_bwd.hip): one persistent workgroup per CU
 FUSED_BWD = os.environ.get("OV3D_SA_FUSED_BWD", "1") != "0"
-NWG_DY_FUSED = 256
+NWG_DY_FUSED = int(os.environ.get("OV3D_SA_DY_NWG", "256"))
 FUSED_STATS = os.environ.get("OV3D_SA_FUSED_STATS", "1") != "0"   # + layer 2's BN-bwd stats
 
 

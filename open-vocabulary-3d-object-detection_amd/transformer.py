@@ -366,7 +366,9 @@ class MaskedTransformerEncoder(TransformerEncoder):
                 and a.embed_dim == a.num_heads * flash.HEAD_DIM and layer.nhead == a.num_heads)
 
     def forward(self, src, mask=None, src_key_padding_mask=None, pos=None, xyz=None,
-                transpose_swap=False):
+                transpose_swap=False, interim_plan=None):
+        """interim_plan: (inds, new_xyz, ball) of the interim SA computed ahead of time from
+        the same points (Model3DETR.sampling_plan); identical results."""
         out = src
         xyz_dist = None
         xyz_inds = None
@@ -387,7 +389,12 @@ class MaskedTransformerEncoder(TransformerEncoder):
             if idx == 0 and self.interim_downsampling:
                 if fused:
                     out = rn.resnorm(pend)[0]
-                xyz, feats, xyz_inds = self.interim_downsampling(xyz, out.permute(1, 2, 0))
+                if interim_plan is not None:
+                    inds, nxyz, ball = interim_plan
+                    xyz, feats, xyz_inds = self.interim_downsampling(
+                        xyz, out.permute(1, 2, 0), inds=inds, new_xyz=nxyz, ball=ball)
+                else:
+                    xyz, feats, xyz_inds = self.interim_downsampling(xyz, out.permute(1, 2, 0))
                 out = feats.permute(2, 0, 1)
                 pend = rn.Pending(out, None, 0.0, 0)
         if fused:

@@ -210,24 +210,30 @@ def test_step_graph_equals_eager_step(cuda):
             assert torch.equal(bg[k], v), k
 
 
-def test_sampling_plan_inputs_give_identical_forward(cuda):
-    """Model3DETR.sampling_plan (pre-encoder FPS + points, its ball query, the query FPS:
-    computed ahead of time by graphs.StepGraph on a side stream) fed back as inputs gives
-    the forward without it, bit for bit"""
+@pytest.mark.parametrize("masked", [False, True])
+def test_sampling_plan_inputs_give_identical_forward(cuda, masked):
+    """Model3DETR.sampling_plan (pre-encoder FPS + points, its ball query, the query FPS;
+    masked encoder: also the interim SA's FPS + points and ball query: computed ahead of
+    time by graphs.StepGraph on a side stream) fed back as inputs gives the forward
+    without it, bit for bit"""
     import ov3d_amd
     from ov3d_amd import synthetic
-    from ov3d_amd.dataset_config import SunrgbdDatasetConfig
+    from ov3d_amd.dataset_config import ScannetDatasetConfig, SunrgbdDatasetConfig
     from bench import default_args
+    extra_args = dict(enc_type="masked", use_color=True) if masked else {}
     args = default_args(enc_dropout=0.0, dec_dropout=0.0, mlp_dropout=0.0, preenc_npoints=512,
-                        nqueries=64)
-    cfg = SunrgbdDatasetConfig()
+                        nqueries=64, **extra_args)
+    cfg = ScannetDatasetConfig() if masked else SunrgbdDatasetConfig()
     torch.manual_seed(0)
-    model, _ = ov3d_amd.build_model(args, cfg, text_embedding=synthetic.text_embedding())
+    model, _ = ov3d_amd.build_model(args, cfg, text_embedding=synthetic.text_embedding(
+        cfg.num_semcls + 1))
     model = model.to(cuda).train()
-    b = synthetic.make_batch(2, seed=6, num_points=4096, device=cuda)
+    b = synthetic.make_batch(2, seed=6, num_points=4096, device=cuda,
+                             dataset="scannet" if masked else "sunrgbd", use_color=masked)
     inputs = {k: b[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")}
     plan = model.sampling_plan(b["point_clouds"])
-    assert set(plan) == set(model.PLAN_KEYS)
+    interim = {"interim_inds", "interim_xyz", "interim_ball"}
+    assert set(plan) == (set(model.PLAN_KEYS) if masked else set(model.PLAN_KEYS) - interim)
     outs = []
     for extra in ({}, plan):
         with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
