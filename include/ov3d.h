@@ -44,6 +44,16 @@ int ov3d_fps(const float* xyz, int B, int N, int M, int32_t* idx_out, float* new
              float* workspace, void* stream);
 long long ov3d_fps_workspace(int B, int N);
 
+/* Max over the S neighbour rows of each centroid (F.max_pool2d(kernel [1, nsample]) in
+ * PointnetSAModuleVotes, models/model_3detr.py:353-362, 385-391) on channels-last bf16 rows:
+ *   y (P*S, C) -> out (P, C), arg (P, C) uint8 = the first row (0..S-1) holding the max;
+ *   backward: g (P, C) -> dy (P*S, C) bf16, g on the arg rows, zero elsewhere.  C % 8 == 0,
+ *   S <= 256. */
+int ov3d_nbr_max_fwd(const void* y, long long P, int S, int C, void* out, uint8_t* arg,
+                     void* stream);
+int ov3d_nbr_max_bwd(const void* g, const uint8_t* arg, long long P, int S, int C, void* dy,
+                     void* stream);
+
 /* Ball query: first S point indices (ascending) with |p - c|^2 < radius^2,
  * padded with the first hit, zeros if none.
  * Replaces pointnet2_utils.ball_query (QueryAndGroup, model_3detr.py:355-361).

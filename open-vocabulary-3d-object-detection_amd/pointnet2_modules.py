@@ -11,6 +11,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import _native as nat
 from . import pointnet2_utils as pu
 from . import sa_fused
 from .gemm import rows_linear
@@ -84,6 +85,39 @@ class SharedMLP(nn.Sequential):
         return x
 
 
+def _nbr_max_ok(y, S):
+    return (y.is_cuda and y.dtype == torch.bfloat16 and y.dim() == 2 and y.shape[1] % 8 == 0
+            and 0 < S <= 256 and y.shape[0] % S == 0)
+
+
+class _NbrMax(torch.autograd.Function):
+    """max over the S neighbour rows of each centroid (bf16 (P*S, C) -> (P, C)) on
+    csrc/pool.hip: the arg row is the first maximum (max_pool2d's window order) and the
+    backward writes the dense row gradient in one pass (no scatter, no zero fill)."""
+
+    @staticmethod
+    def forward(ctx, y, S):
+        y = y.contiguous()
+        R, C = y.shape
+        P = R // S
+        out = torch.empty((P, C), dtype=y.dtype, device=y.device)
+        arg = torch.empty((P, C), dtype=torch.uint8, device=y.device)
+        nat.call("ov3d_nbr_max_fwd", y, P, S, C, out, arg, like=y)
+        ctx.save_for_backward(arg)
+        ctx.S = S
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (arg,) = ctx.saved_tensors
+        P, C = arg.shape
+        S = ctx.S
+        g = g.to(torch.bfloat16).contiguous()
+        dy = torch.empty((P * S, C), dtype=torch.bfloat16, device=g.device)
+        nat.call("ov3d_nbr_max_bwd", g, arg, P, S, C, dy, like=g)
+        return dy, None
+
+
 class PointnetSAModuleVotes(nn.Module):
     """Set abstraction: FPS -> ball query -> group (+xyz, /radius) -> SharedMLP -> max over nsample."""
 
@@ -130,6 +164,8 @@ class PointnetSAModuleVotes(nn.Module):
             return sa_fused.sa_mlp_pool(self.mlp_module, rows, S).view(B, M, -1)
         y = self.mlp_module.rows(rows)
         # == F.max_pool2d(kernel [1, nsample]) of the reference
+        if _nbr_max_ok(y, S):
+            return _NbrMax.apply(y, S).view(B, M, -1)
         return y.view(B, M, S, -1).max(dim=2).values
 
 

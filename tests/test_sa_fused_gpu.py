@@ -244,3 +244,24 @@ def test_sa_rows_bn_relu_path_vs_fp32(cuda, monkeypatch, kind):
     for n in g_ref:
         eh, et = _rel(res["hip"][1][n], g_ref[n]), _rel(res["torch"][1][n], g_ref[n])
         assert eh <= max(2.0 * et, 3e-2), (n, eh, et)
+
+
+@pytest.mark.parametrize("S,C", [(32, 256), (64, 128), (5, 24)])
+def test_neighbour_max_pool_kernel(cuda, S, C):
+    """csrc/pool.hip: pooled values bit-exact vs torch max; the arg row is the first
+    maximum of the window (max_pool2d order; bf16 rows have many ties); the backward routes
+    each pooled gradient to that row and writes zeros elsewhere"""
+    from ov3d_amd.pointnet2_modules import _NbrMax
+    g = torch.Generator(device="cpu").manual_seed(S + C)
+    P = 300
+    y = (torch.randn(P * S, C, generator=g) * 3).round().to(torch.bfloat16).to(cuda)  # ties
+    y.requires_grad_()
+    out = _NbrMax.apply(y, S)
+    ref = y.detach().view(P, S, C).max(dim=1).values
+    assert torch.equal(out, ref)
+    first = np.argmax(y.detach().float().view(P, S, C).cpu().numpy(), axis=1)   # first max
+    gout = torch.randn(P, C, generator=g).to(torch.bfloat16).to(cuda)
+    out.backward(gout)
+    exp = torch.zeros(P, S, C, dtype=torch.bfloat16)
+    exp.scatter_(1, torch.from_numpy(first).long()[:, None, :], gout.cpu()[:, None, :])
+    assert torch.equal(y.grad.cpu(), exp.view(P * S, C))
