@@ -80,6 +80,17 @@ int ov3d_group_bwd(const float* grad_out, const int32_t* idx, int B, int C, int 
                    long long feat_sb, long long feat_sn, long long feat_sc, float* grad_features,
                    void* stream);
 
+/* Inverse of a ball-query index, for a gather-form grouping backward (no float atomics):
+ *   idx (B,M,S) -> offsets (B*N+1) and rows (B*M*S): the rows r = (b*M + m)*S + s with
+ *   idx[r] = n are rows[offsets[b*N+n] .. offsets[b*N+n+1]) (in no particular order).
+ *   cnt, cursor: B*N int32 scratch.  (B*N up to ~10^6: the scan is one workgroup.) */
+int ov3d_group_inverse(const int32_t* idx, int B, int N, int M, int S, int32_t* cnt,
+                       int32_t* offsets, int32_t* cursor, int32_t* rows, void* stream);
+/* ov3d_group_bwd through the inverse: every grad_features element written (no zero fill). */
+int ov3d_group_bwd_csr(const float* grad_out, const int32_t* offsets, const int32_t* rows, int B,
+                       int C, int N, long long feat_sb, long long feat_sn, long long feat_sc,
+                       float* grad_features, void* stream);
+
 /* gather_operation (pointnet2_utils): features (B,C,N), idx (B,M) -> out (B,C,M) */
 int ov3d_gather_fwd(const float* features, const int32_t* idx, int B, int C, int N, int M,
                     float* out, void* stream);

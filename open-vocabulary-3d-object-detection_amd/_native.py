@@ -55,6 +55,8 @@ _SIGS = {
     "ov3d_attn_bwd_masked": "ppplllplplpiiiiffppplplplpipp",
     "ov3d_attn_mask_pack": "pifiiipp",
     "ov3d_nbr_max_fwd": "pliippp",
+    "ov3d_group_inverse": "piiiippppp",
+    "ov3d_group_bwd_csr": "pppiiilllpp",
     "ov3d_nbr_max_bwd": "ppliipp",
     "ov3d_wgrad": "plpliiiplpppip",
     "ov3d_wgrad_group": "pipp",

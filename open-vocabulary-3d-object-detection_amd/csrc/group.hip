@@ -157,7 +157,131 @@ __global__ __launch_bounds__(256) void gather_bwd_kernel(const float* __restrict
     atomicAdd(gf + bc * N + idx[(size_t)b * M + m], g[t]);
 }
 
+// ---- inverse of the ball-query index (CSR per source point), for a gather-form backward
+// count: rows per (b, n) into cnt[b*N + n] (zeroed by the caller's launch below)
+__global__ __launch_bounds__(256) void inv_count_kernel(const int32_t* __restrict__ idx, int N,
+                                                        long long MS, long long total,
+                                                        int32_t* __restrict__ cnt) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= total) return;
+    const int b = (int)(t / MS);
+    atomicAdd(cnt + (size_t)b * N + idx[t], 1);
+}
+
+// exclusive scan of n counts -> off[0..n] (one 1024-thread workgroup, sequential per thread);
+// cur = off[0..n-1] (fill cursors)
+__global__ __launch_bounds__(1024) void inv_scan_kernel(const int32_t* __restrict__ cnt, int n,
+                                                        int32_t* __restrict__ off,
+                                                        int32_t* __restrict__ cur) {
+    __shared__ int32_t part[1024];
+    const int tid = threadIdx.x;
+    const int per = (n + 1023) / 1024;
+    const int b0 = tid * per, b1 = min(n, b0 + per);
+    int sum = 0;
+    for (int i = b0; i < b1; ++i) sum += cnt[i];
+    part[tid] = sum;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {   // Hillis-Steele inclusive scan of the parts
+        const int v = tid >= o ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int run = part[tid] - sum;
+    for (int i = b0; i < b1; ++i) {
+        off[i] = run;
+        cur[i] = run;
+        run += cnt[i];
+    }
+    if (tid == 1023) off[n] = part[1023];
+}
+
+__global__ __launch_bounds__(256) void inv_fill_kernel(const int32_t* __restrict__ idx, int N,
+                                                       long long MS, long long total,
+                                                       int32_t* __restrict__ cur,
+                                                       int32_t* __restrict__ rows) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= total) return;
+    const int b = (int)(t / MS);
+    const int pos = atomicAdd(cur + (size_t)b * N + idx[t], 1);
+    rows[pos] = (int32_t)t;
+}
+
+// gather-form grouping backward: thread per (b, n, c), c fastest (a wave reads 64 channels of
+// one grad row per list entry); every (b, n, c) written (0 when no row refers to n)
+__global__ __launch_bounds__(256) void group_bwd_csr_kernel(const float* __restrict__ gout,
+                                                            const int32_t* __restrict__ off,
+                                                            const int32_t* __restrict__ rows, int B,
+                                                            int C, int N, long long sb,
+                                                            long long sn, long long sc,
+                                                            float* __restrict__ gfeat) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long long)B * N * C) return;
+    const int c = (int)(t % C);
+    const long long bn = t / C;
+    const int b = (int)(bn / N), n = (int)(bn - (long long)b * N);
+    const int e0 = off[bn], e1 = off[bn + 1];
+    float acc = 0.f;
+    // 8 entries per round: their row ids, then their values, are independent loads (one
+    // memory round trip each instead of two per entry)
+    int e = e0;
+    for (; e + 8 <= e1; e += 8) {
+        int r[8];
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) r[u] = rows[e + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = gout[(size_t)r[u] * (3 + C) + 3 + c];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    if (e < e1) {
+        int r[8];
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) r[u] = e + u < e1 ? rows[e + u] : -1;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = r[u] >= 0 ? gout[(size_t)r[u] * (3 + C) + 3 + c] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    gfeat[b * sb + n * sn + c * sc] = acc;
+}
+
 }  // namespace
+
+extern "C" int ov3d_group_inverse(const int32_t* idx, int B, int N, int M, int S, int32_t* cnt,
+                                  int32_t* offsets, int32_t* cursor, int32_t* rows, void* stream) {
+    if (!idx || !cnt || !offsets || !cursor || !rows || B <= 0 || N <= 0 || M < 0 || S <= 0)
+        return OV3D_EINVAL;
+    hipStream_t s = ov3d_stream(stream);
+    const long long total = (long long)B * M * S, n = (long long)B * N;
+    if (hipMemsetAsync(cnt, 0, n * sizeof(int32_t), s) != hipSuccess) return OV3D_ELAUNCH;
+    if (total > 0)
+        hipLaunchKernelGGL(inv_count_kernel, dim3(ov3d_cdiv(total, 256)), dim3(256), 0, s, idx, N,
+                           (long long)M * S, total, cnt);
+    hipLaunchKernelGGL(inv_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, (int)n, offsets, cursor);
+    if (total > 0)
+        hipLaunchKernelGGL(inv_fill_kernel, dim3(ov3d_cdiv(total, 256)), dim3(256), 0, s, idx, N,
+                           (long long)M * S, total, cursor, rows);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_group_bwd_csr(const float* grad_out, const int32_t* offsets,
+                                  const int32_t* rows, int B, int C, int N, long long feat_sb,
+                                  long long feat_sn, long long feat_sc, float* grad_features,
+                                  void* stream) {
+    if (!grad_out || !offsets || !rows || !grad_features || B < 0 || C < 0 || N <= 0)
+        return OV3D_EINVAL;
+    const long long total = (long long)B * N * C;
+    if (total == 0) return OV3D_OK;
+    hipLaunchKernelGGL(group_bwd_csr_kernel, dim3(ov3d_cdiv(total, 256)), dim3(256), 0,
+                       ov3d_stream(stream), grad_out, offsets, rows, B, C, N, feat_sb, feat_sn,
+                       feat_sc, grad_features);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
 
 extern "C" int ov3d_ball_query(const float* xyz, const float* new_xyz, int B, int N, int M,
                                float radius, int S, int32_t* idx_out, void* stream) {

@@ -171,7 +171,7 @@ class Model3DETR(nn.Module):
 
     # index work that depends on the input points only (sampling_plan)
     PLAN_KEYS = ("pre_enc_inds", "pre_enc_xyz", "pre_enc_ball", "query_xyz", "interim_inds",
-                 "interim_xyz", "interim_ball")
+                 "interim_xyz", "interim_ball", "interim_inv_off", "interim_inv_rows")
 
     def _encoder_keeps_xyz(self):
         from .transformer import MaskedTransformerEncoder
@@ -202,9 +202,11 @@ class Model3DETR(nn.Module):
             # functions of the input points
             ids = self._interim_sa()
             i_inds, i_xyz = pu.furthest_point_sample_gather(pre_xyz, ids.npoint)
-            plan.update(interim_inds=i_inds, interim_xyz=i_xyz,
-                        interim_ball=pu.ball_query(ids.grouper.radius, ids.grouper.nsample,
-                                                   pre_xyz, i_xyz),
+            ball = pu.ball_query(ids.grouper.radius, ids.grouper.nsample, pre_xyz, i_xyz)
+            # the ball's inverse (rows per point) for the gather-form grouping backward
+            inv_off, inv_rows = pu.group_inverse(ball, pre_xyz.shape[1])
+            plan.update(interim_inds=i_inds, interim_xyz=i_xyz, interim_ball=ball,
+                        interim_inv_off=inv_off, interim_inv_rows=inv_rows,
                         query_xyz=pu.furthest_point_sample_gather(i_xyz, self.num_queries)[1])
         return plan
 
@@ -223,7 +225,8 @@ class Model3DETR(nn.Module):
         if "interim_inds" in plan:
             enc_xyz, enc_feats, enc_inds = self.encoder(
                 src, xyz=pre_xyz, interim_plan=(plan["interim_inds"], plan["interim_xyz"],
-                                                plan["interim_ball"]))
+                                                plan["interim_ball"],
+                                                (plan["interim_inv_off"], plan["interim_inv_rows"])))
         else:
             enc_xyz, enc_feats, enc_inds = self.encoder(src, xyz=pre_xyz)
         if enc_inds is None:

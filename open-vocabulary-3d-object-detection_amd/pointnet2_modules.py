@@ -138,7 +138,7 @@ class PointnetSAModuleVotes(nn.Module):
             mlp_spec[0] += 3  # upstream mutates the caller's list (reference relies on it)
         self.mlp_module = SharedMLP(mlp_spec, bn=bn)
 
-    def forward(self, xyz, features=None, inds=None, new_xyz=None, ball=None):
+    def forward(self, xyz, features=None, inds=None, new_xyz=None, ball=None, inverse=None):
         """inds / new_xyz / ball: the FPS indices, sampled points and ball-query indices
         computed ahead of time from the same points (Model3DETR.sampling_plan); identical
         results."""
@@ -151,12 +151,12 @@ class PointnetSAModuleVotes(nn.Module):
             if new_xyz is None:
                 new_xyz = pu.gather_operation(xyz.transpose(1, 2).contiguous(), inds).transpose(1, 2)
                 new_xyz = new_xyz.contiguous()
-        return new_xyz, self._mlp_pool(xyz, new_xyz, features, ball).transpose(1, 2), inds
+        return new_xyz, self._mlp_pool(xyz, new_xyz, features, ball, inverse).transpose(1, 2), inds
 
-    def _mlp_pool(self, xyz, new_xyz, features, ball=None):
+    def _mlp_pool(self, xyz, new_xyz, features, ball=None, inverse=None):
         """grouped rows -> SharedMLP -> max over nsample: (B, npoint, Cout)."""
         g = self.grouper.rows(xyz, new_xyz, features) if ball is None else \
-            self.grouper.rows(xyz, new_xyz, features, idx=ball)      # (B, M, S, 3+C) fp32
+            self.grouper.rows(xyz, new_xyz, features, idx=ball, inverse=inverse)   # (B,M,S,3+C)
         B, M, S, C = g.shape
         rows = g.view(B * M * S, C)
         if self.training and sa_fused.supported(self.mlp_module, rows, S):

@@ -117,7 +117,7 @@ class _Group(Function):
     (xyz[idx]-new_xyz)[/r] ++ features[idx]; features may be any dense (B,C,N) view."""
 
     @staticmethod
-    def forward(ctx, xyz, new_xyz, features, idx, radius, normalize):
+    def forward(ctx, xyz, new_xyz, features, idx, radius, normalize, inverse=None):
         B, N, _ = xyz.shape
         _, M, S = idx.shape
         C = 0 if features is None else features.shape[1]
@@ -133,6 +133,7 @@ class _Group(Function):
         ctx.save_for_backward(idx)
         ctx.meta = (B, C, N, M, S, strides, tuple(features.shape) if C else None,
                     tuple(features.stride()) if C else None)
+        ctx.inverse = inverse
         return out
 
     @staticmethod
@@ -140,11 +141,27 @@ class _Group(Function):
         (idx,) = ctx.saved_tensors
         B, C, N, M, S, strides, shape, stride = ctx.meta
         if C == 0 or not ctx.needs_input_grad[2]:
-            return None, None, None, None, None, None
+            return None, None, None, None, None, None, None
         g = nat.check(g.float().contiguous(), "grad", torch.float32, 4)
         gf = torch.empty_strided(shape, stride, dtype=torch.float32, device=g.device)
-        nat.call("ov3d_group_bwd", g, idx, B, C, N, M, S, *strides, gf, like=g)
-        return None, None, gf, None, None, None
+        if ctx.inverse is not None:   # gather form: one pass, no atomics, no zero fill
+            off, rows = ctx.inverse
+            nat.call("ov3d_group_bwd_csr", g, off, rows, B, C, N, *strides, gf, like=g)
+        else:
+            nat.call("ov3d_group_bwd", g, idx, B, C, N, M, S, *strides, gf, like=g)
+        return None, None, gf, None, None, None, None
+
+
+def group_inverse(idx, N):
+    """(B, M, S) int32 ball-query indices over N points -> (offsets (B*N+1), rows (B*M*S)):
+    the rows that read each point (ov3d_group_inverse), for the gather-form backward."""
+    B, M, S = idx.shape
+    dev = idx.device
+    cnt, cur = (torch.empty((B * N,), dtype=torch.int32, device=dev) for _ in range(2))
+    off = torch.empty((B * N + 1,), dtype=torch.int32, device=dev)
+    rows = torch.empty((B * M * S,), dtype=torch.int32, device=dev)
+    nat.call("ov3d_group_inverse", idx, B, N, M, S, cnt, off, cur, rows, like=idx)
+    return off, rows
 
 
 def grouping_operation(features, idx):
@@ -156,6 +173,11 @@ def grouping_operation(features, idx):
     z = torch.zeros((B, N, 3), dtype=torch.float32, device=features.device)
     zc = torch.zeros((B, idx.shape[1], 3), dtype=torch.float32, device=features.device)
     return _Group.apply(z, zc, features, idx, 1.0, False)[..., 3:].permute(0, 3, 1, 2)
+
+
+# feature gradients of the grouping through the inverse index (ov3d_group_bwd_csr) instead of
+# float atomics (ov3d_group_bwd): the masked encoder's interim SA
+GATHER_BWD = True
 
 
 class QueryAndGroup(nn.Module):
@@ -170,9 +192,10 @@ class QueryAndGroup(nn.Module):
         self.radius, self.nsample = radius, nsample
         self.use_xyz, self.ret_grouped_xyz, self.normalize_xyz = use_xyz, ret_grouped_xyz, normalize_xyz
 
-    def rows(self, xyz, new_xyz, features=None, idx=None):
+    def rows(self, xyz, new_xyz, features=None, idx=None, inverse=None):
         """Grouped features as channels-last rows (B, npoint, nsample, 3+C).  idx: the
-        ball-query indices of (xyz, new_xyz) when computed ahead of time."""
+        ball-query indices of (xyz, new_xyz) when computed ahead of time; inverse: its
+        group_inverse (offsets, rows), likewise."""
         if xyz.requires_grad or new_xyz.requires_grad:
             raise NotImplementedError("gradients w.r.t. point coordinates are not on the path")
         if idx is None:
@@ -187,7 +210,11 @@ class QueryAndGroup(nn.Module):
                 raise ValueError("features must be (B, C, N)")
             features = features if features.dtype == torch.float32 else features.float()
             nat.check_device(features, "features")
-        return _Group.apply(xyz, new_xyz, features, idx, self.radius, self.normalize_xyz)
+        inv = None
+        if features is not None and features.requires_grad and torch.is_grad_enabled() and \
+                GATHER_BWD:
+            inv = inverse if inverse is not None else group_inverse(idx.contiguous(), xyz.shape[1])
+        return _Group.apply(xyz, new_xyz, features, idx, self.radius, self.normalize_xyz, inv)
 
     def forward(self, xyz, new_xyz, features=None):
         """Reference layout: (B, 3+C, npoint, nsample) (a view of the channels-last rows)."""

@@ -367,8 +367,9 @@ class MaskedTransformerEncoder(TransformerEncoder):
 
     def forward(self, src, mask=None, src_key_padding_mask=None, pos=None, xyz=None,
                 transpose_swap=False, interim_plan=None):
-        """interim_plan: (inds, new_xyz, ball) of the interim SA computed ahead of time from
-        the same points (Model3DETR.sampling_plan); identical results."""
+        """interim_plan: (inds, new_xyz, ball, (inverse offsets, rows)) of the interim SA
+        computed ahead of time from the same points (Model3DETR.sampling_plan); identical
+        results."""
         out = src
         xyz_dist = None
         xyz_inds = None
@@ -390,9 +391,9 @@ class MaskedTransformerEncoder(TransformerEncoder):
                 if fused:
                     out = rn.resnorm(pend)[0]
                 if interim_plan is not None:
-                    inds, nxyz, ball = interim_plan
+                    inds, nxyz, ball, inv = interim_plan
                     xyz, feats, xyz_inds = self.interim_downsampling(
-                        xyz, out.permute(1, 2, 0), inds=inds, new_xyz=nxyz, ball=ball)
+                        xyz, out.permute(1, 2, 0), inds=inds, new_xyz=nxyz, ball=ball, inverse=inv)
                 else:
                     xyz, feats, xyz_inds = self.interim_downsampling(xyz, out.permute(1, 2, 0))
                 out = feats.permute(2, 0, 1)

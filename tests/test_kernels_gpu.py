@@ -67,8 +67,10 @@ def test_ball_query_bit_exact(cuda, B, N, M, r, S, uniform):
 
 # -------------------------------------------------------------- grouping
 @pytest.mark.parametrize("C", [0, 3, 256])
-def test_group_fwd_bwd(cuda, C):
+@pytest.mark.parametrize("gather_bwd", [True, False])
+def test_group_fwd_bwd(cuda, C, gather_bwd, monkeypatch):
     from ov3d_amd import pointnet2_utils as pu
+    monkeypatch.setattr(pu, "GATHER_BWD", gather_bwd)   # inverse-index backward vs atomics
     B, N, M, S, r = 2, 2048, 256, 32, 0.4
     xyz = scene_batch(B, N, seed=11)
     new_xyz = xyz[:, :M].clone()
@@ -87,6 +89,21 @@ def test_group_fwd_bwd(cuda, C):
         gi = torch.from_numpy(idx).long().view(B, 1, M * S).expand(B, C, M * S)
         ref.scatter_add_(2, gi, g[:, 3:].double().cpu().reshape(B, C, M * S))
         np.testing.assert_allclose(fg.grad.cpu().numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
+
+
+def test_group_inverse_index(cuda):
+    """ov3d_group_inverse: every row appears exactly once, in the list of the point it reads"""
+    from ov3d_amd import pointnet2_utils as pu
+    B, N, M, S = 3, 500, 64, 16
+    idx = torch.randint(0, N, (B, M, S), device=cuda, dtype=torch.int32)
+    idx[1] = 7   # one point read by every row of a scene
+    off, rows = pu.group_inverse(idx, N)
+    off, rows, idx = off.cpu().numpy(), rows.cpu().numpy(), idx.cpu().numpy().reshape(-1)
+    assert off[0] == 0 and off[-1] == B * M * S and np.all(np.diff(off) >= 0)
+    assert np.array_equal(np.sort(rows), np.arange(B * M * S))
+    for bn in range(B * N):
+        r = rows[off[bn]:off[bn + 1]]
+        assert np.all(idx[r] == bn % N) and np.all(r // (M * S) == bn // N)
 
 
 def test_gather_fwd_bwd(cuda):

@@ -232,7 +232,7 @@ def test_sampling_plan_inputs_give_identical_forward(cuda, masked):
                              dataset="scannet" if masked else "sunrgbd", use_color=masked)
     inputs = {k: b[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")}
     plan = model.sampling_plan(b["point_clouds"])
-    interim = {"interim_inds", "interim_xyz", "interim_ball"}
+    interim = {k for k in model.PLAN_KEYS if k.startswith("interim")}
     assert set(plan) == (set(model.PLAN_KEYS) if masked else set(model.PLAN_KEYS) - interim)
     outs = []
     for extra in ({}, plan):
