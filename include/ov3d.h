@@ -344,6 +344,12 @@ typedef struct {
 int ov3d_attn_bwd_dkdv_batch(const ov3d_attn_dkdv_job* jobs, int njobs, int B, int H, int Lq,
                              int Lk, float scale, float dropout_p, void* stream);
 
+/* Short attentions (Lq, Lk <= 128, one key split, no mask: the decoder self attention) run
+ * their whole ov3d_attn_bwd in one launch (dQ, then dK / dV in the same workgroup).
+ * on = 0 / 1 selects the two-launch / one-launch form, -1 only queries; returns the
+ * previous setting (host-only). */
+int ov3d_attn_small_bwd(int on);
+
 /* ---- Masked attention (the masked encoder) ----
  * Replaces the (B*H, L, L) boolean attn_mask of MaskedTransformerEncoder
  * (models/transformer.py:152-190: mask = cdist(xyz, xyz) >= radius, tiled to the heads,

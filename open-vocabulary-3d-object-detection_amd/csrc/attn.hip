@@ -30,6 +30,7 @@
 // Split-K (grid.z) serves the 128-query decoder attention: partial (O, m, l) per
 // key split, merged by attn_combine_kernel.
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.h"
 
@@ -523,7 +524,7 @@ struct AttnBwdArgs {
 };
 
 template <bool DROP, bool MASK>
-__global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
+__device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
     const AttnArgs& a = A.f;
     __shared__ __attribute__((aligned(16))) bf16 Ks[2][KB * LDK];
     __shared__ __attribute__((aligned(16))) bf16 Vs[2][KB * LDK];
@@ -687,6 +688,11 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
             for (int j = 0; j < 4; ++j) w[j] = (bf16)(dqt[dt][4 * g + j] * A.scale);
             *reinterpret_cast<bf16x4*>(row + 32 * dt + 8 * g + 4 * h) = w;
         }
+}
+
+template <bool DROP, bool MASK>
+__global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
+    attn_bwd_dq_body<DROP, MASK>(A);
 }
 
 // dq = scale * sum over key splits; one thread per (b*H+h, query, 4 dims)
@@ -909,6 +915,17 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
     attn_bwd_dkdv_body<DROP, MASK>(A);
 }
 
+// The whole backward of a short attention (Lq, Lk <= 128, one key split: the decoder's
+// 128 x 128 self attention) in ONE launch: a workgroup per (b, h) runs the dQ pass over its
+// queries (which also writes D), then, after the barrier that publishes D to the
+// workgroup, the dK / dV pass over its keys.  Same arithmetic as the two kernels.
+template <bool DROP>
+__global__ void __launch_bounds__(256, 2) attn_bwd_small_kernel(AttnBwdArgs A) {
+    attn_bwd_dq_body<DROP, false>(A);
+    __syncthreads();
+    attn_bwd_dkdv_body<DROP, false>(A);
+}
+
 // dK / dV of several attention calls with the same shape in one launch (blockIdx.z = call):
 // the decoder's 8 cross attentions, deferred to the end of the decoder backward because
 // their K / V gradients only feed the shared memory-K/V projection (transformer._MemoryKV)
@@ -1003,6 +1020,23 @@ static void set_dropbits(AttnArgs& a, uint32_t* bits) {
     a.nkt = (a.Lk + KB - 1) / KB;
     a.wq = bits;
     a.wk = bits ? bits + 2 * (size_t)a.nkt * a.B * a.H * a.Lq : nullptr;
+}
+
+// one-launch backward of short attentions (attn_bwd_small_kernel); OV3D_ATTN_SMALL_BWD=0 or
+// ov3d_attn_small_bwd(0) restores the two launches (A/B measurement, tests)
+static int g_small_bwd = -1;
+static bool fuse_small_bwd() {
+    if (g_small_bwd < 0) {
+        const char* e = getenv("OV3D_ATTN_SMALL_BWD");
+        g_small_bwd = (e && e[0] == '0') ? 0 : 1;
+    }
+    return g_small_bwd != 0;
+}
+
+extern "C" int ov3d_attn_small_bwd(int on) {
+    const int prev = fuse_small_bwd() ? 1 : 0;
+    if (on >= 0) g_small_bwd = on ? 1 : 0;
+    return prev;
 }
 
 static void set_maskbits(AttnArgs& a, const uint32_t* bits) {
@@ -1171,6 +1205,14 @@ extern "C" int ov3d_attn_bwd_masked(const void* q, const void* k, const void* v,
     set_dropbits(a, (uint32_t*)dropbits);
     set_maskbits(a, maskbits);
     hipStream_t st = ov3d_stream(stream);
+    if (dk && !maskbits && nsplit == 1 && Lq <= 4 * QW && Lk <= 128 && fuse_small_bwd()) {
+        if (a.thresh)
+            attn_bwd_small_kernel<true><<<dim3(1, B * H), 256, 0, st>>>(A);
+        else
+            attn_bwd_small_kernel<false><<<dim3(1, B * H), 256, 0, st>>>(A);
+        OV3D_LAUNCH_CHECK();
+        return OV3D_OK;
+    }
     const dim3 gq((Lq + 4 * QW - 1) / (4 * QW), B * H, nsplit);
     if (maskbits) {
         if (a.thresh)

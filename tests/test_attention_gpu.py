@@ -400,3 +400,29 @@ def test_masked_encoder_packed_equals_bool_mask_path(cuda, monkeypatch, with_int
     assert _rel(res[True][1], res[False][1]) < 3e-2
     for n, g in res[False][3].items():
         assert _rel(res[True][3][n], g) < 5e-2, n
+
+
+@pytest.mark.parametrize("L,B,p", [(128, 8, 0.1), (96, 3, 0.0), (64, 2, 0.3)])
+def test_short_attention_one_launch_backward_equals_two(cuda, L, B, p):
+    """attn_bwd_small_kernel (dQ then dK / dV in one workgroup per (b, h)) gives exactly the
+    gradients of the dQ + dK/dV launches"""
+    from ov3d_amd import _native, attention as A
+    lib = _native.load()
+    torch.manual_seed(L + B)
+    H = 4
+    base = (torch.randn(L, B, 3 * H * 64, device=cuda) * 1.5).to(torch.bfloat16)
+    seed = A._seed(cuda).clone()
+    grads = []
+    prev = lib.ov3d_attn_small_bwd(-1)
+    try:
+        for fused in (1, 0):
+            lib.ov3d_attn_small_bwd(fused)
+            A._SNAPS[cuda] = seed.clone()
+            x = base.clone().requires_grad_()
+            q, k, v = x.chunk(3, dim=-1)
+            out = A.attention(q, k, v, H, dropout_p=p, site=3)
+            out.float().backward(torch.ones_like(out, dtype=torch.float32))
+            grads.append(x.grad.clone())
+    finally:
+        lib.ov3d_attn_small_bwd(prev)
+    assert torch.equal(grads[0], grads[1])
