@@ -22,6 +22,8 @@ solver) and the optimizer stay eager between the two replays.  Results are the
 eager results (same kernels, same order); dropout draws from the graph-safe
 Philox generator.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -72,6 +74,9 @@ class GraphedModel:
         return {"outputs": layers[0], "aux_outputs": layers[1:]}
 
 
+MID_START = os.environ.get("OV3D_PLAN_MID_START", "1") != "0"
+
+
 class StepGraph:
     """Replays forward + criterion + backward + clip_grad_norm_ + optimizer.step.
 
@@ -106,6 +111,15 @@ class StepGraph:
             self.next_pc = self.static["point_clouds"].clone()
             self.plan_cur = self._sample(self.static["point_clouds"])
         self.fps_stream = torch.cuda.Stream()
+        # the next batch's sampling starts when this step's encoder forward is done: the
+        # step is captured as TWO graphs split at Model3DETR.after_encoder (one memory pool),
+        # and an event between their replays releases the side stream (ROCm PyTorch has no
+        # external events inside a graph).  The FPS holds 8 CUs for ~2.5 ms; beside the
+        # encoder's full-grid kernels it costs them a tail round (tools/contention.py:
+        # attention forward 89 -> 127 us), beside the decoder's short launches ~nothing.
+        self.split = bool(self.prefetch and MID_START and hasattr(model, "run_encoder"))
+        self.mid_event = torch.cuda.Event() if self.split else None
+        self.graph2 = None
         self.side = torch.cuda.Stream()
         self.side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.side):
@@ -120,8 +134,42 @@ class StepGraph:
         # the process group must not invalidate the capture ("thread_local" capture mode)
         mode = "thread_local" if (torch.distributed.is_available()
                                   and torch.distributed.is_initialized()) else "global"
-        with torch.cuda.graph(self.graph, capture_error_mode=mode):
-            self.loss = self._body(gemm)
+        if not self.split:
+            with torch.cuda.graph(self.graph, capture_error_mode=mode):
+                self.loss = self._body(gemm)
+            return
+        # split capture (the torch.cuda.graph context's steps, done by hand so the capture
+        # can switch graphs in the middle of the forward)
+        self.graph2 = torch.cuda.CUDAGraph()
+        cap = torch.cuda.Stream()
+        torch.cuda.synchronize()
+        cap.wait_stream(torch.cuda.current_stream())
+        switched = []
+
+        def switch():
+            self.graph.capture_end()
+            self.graph2.capture_begin(pool=self.graph.pool(), capture_error_mode=mode)
+            switched.append(1)
+
+        self.model.after_encoder = switch
+        try:
+            with torch.cuda.stream(cap):
+                self.graph.capture_begin(capture_error_mode=mode)
+                try:
+                    self.loss = self._body(gemm)
+                finally:
+                    (self.graph2 if switched else self.graph).capture_end()
+        finally:
+            self.model.after_encoder = None
+        torch.cuda.current_stream().wait_stream(cap)
+        if len(switched) != 1:
+            raise RuntimeError("StepGraph: the forward did not pass Model3DETR.after_encoder once")
+
+    def _replay(self):
+        self.graph.replay()
+        if self.graph2 is not None:
+            self.mid_event.record()
+            self.graph2.replay()
 
     def _sample(self, pc):
         """-> dict of the step's point-only index work (extra model inputs)"""
@@ -180,10 +228,16 @@ class StepGraph:
         self._expected = (nb["point_clouds"], nb["point_clouds"]._version)
         # the next batch's sampling plan runs on its own stream (own hardware queue),
         # concurrently with this step's graph; the graph reads plan_cur only
-        self.fps_stream.wait_stream(cur)
-        with torch.cuda.stream(self.fps_stream):
-            nxt = self._sample(self.next_pc)
-        self.graph.replay()
+        if self.split:
+            self._replay()
+            self.fps_stream.wait_event(self.mid_event)   # after next_pc's copy, too
+            with torch.cuda.stream(self.fps_stream):
+                nxt = self._sample(self.next_pc)
+        else:
+            self.fps_stream.wait_stream(cur)
+            with torch.cuda.stream(self.fps_stream):
+                nxt = self._sample(self.next_pc)
+            self.graph.replay()
         cur.wait_stream(self.fps_stream)
         for t in nxt.values():
             t.record_stream(cur)

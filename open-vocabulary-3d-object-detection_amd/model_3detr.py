@@ -233,6 +233,9 @@ class Model3DETR(nn.Module):
             enc_inds = pre_inds
         else:
             enc_inds = torch.gather(pre_inds.long(), 1, enc_inds.long())
+        hook = getattr(self, "after_encoder", None)
+        if hook is not None:   # graphs.StepGraph: the point in the step the side stream waits for
+            hook()
         return enc_xyz, enc_feats, enc_inds
 
     # -------------------------------------------------------------------- heads
