@@ -74,7 +74,11 @@ class GraphedModel:
         return {"outputs": layers[0], "aux_outputs": layers[1:]}
 
 
-MID_START = os.environ.get("OV3D_PLAN_MID_START", "1") != "0"
+# "auto": split when the plan is short against the step (the register-resident FPS, N <= 20480
+# points: SUN); ScanNet's 40000-point plan (~8.7 ms) must start with the step or it becomes
+# the bound (C4: 10.5 ms at the start vs 11.9 ms after the encoder)
+MID_START = os.environ.get("OV3D_PLAN_MID_START", "auto")
+MID_START_MAX_POINTS = 20480
 
 
 class StepGraph:
@@ -117,7 +121,9 @@ class StepGraph:
         # external events inside a graph).  The FPS holds 8 CUs for ~2.5 ms; beside the
         # encoder's full-grid kernels it costs them a tail round (tools/contention.py:
         # attention forward 89 -> 127 us), beside the decoder's short launches ~nothing.
-        self.split = bool(self.prefetch and MID_START and hasattr(model, "run_encoder"))
+        npts = self.static["point_clouds"].shape[1]
+        want = MID_START == "1" or (MID_START == "auto" and npts <= MID_START_MAX_POINTS)
+        self.split = bool(self.prefetch and want and hasattr(model, "run_encoder"))
         self.mid_event = torch.cuda.Event() if self.split else None
         self.graph2 = None
         self.side = torch.cuda.Stream()
