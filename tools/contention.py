@@ -30,19 +30,27 @@ def main():
     q, k, v = (t.contiguous() for t in qkv.chunk(3, dim=-1))
     x = torch.randn(16384, 256, device=dev).to(torch.bfloat16)
     w = torch.randn(768, 256, device=dev).to(torch.bfloat16)
+    from ov3d_amd.gemm import rows_linear
+    qd = (torch.randn(128, 8, 256, device=dev)).to(torch.bfloat16)
+    xr = torch.randn(1024, 256, device=dev).to(torch.bfloat16)
+    wr = torch.randn(256, 256, device=dev)
+    br = torch.randn(256, device=dev)
     kern = {"attn_fwd_L2048": lambda: A.attention(q, k, v, 4, dropout_p=0.1, site=1),
-            "gemm_16384x256x768": lambda: torch.mm(x, w.t())}
+            "gemm_16384x256x768": lambda: torch.mm(x, w.t()),
+            "dec_cross_attn_128x2048": lambda: A.attention(qd, k, v, 4, dropout_p=0.1, site=2),
+            "dec_self_attn_128": lambda: A.attention(qd, qd, qd, 4, dropout_p=0.1, site=3),
+            "rows_linear_1024x256": lambda: rows_linear(xr, wr, br)}
     side = torch.cuda.Stream()
     res = {}
     for name, fn in kern.items():
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
-        alone = timed(fn, 10)
+        alone = timed(fn, 20)
         torch.cuda.synchronize()
         with torch.cuda.stream(side):
             pu.furthest_point_sample_gather(xyz, 2048)   # ~2.5 ms on 8 CUs
-        with_fps = timed(fn, 10)
+        with_fps = timed(fn, 20)
         torch.cuda.synchronize()
         res[name] = {"alone_us": round(alone, 1), "beside_fps_us": round(with_fps, 1)}
     print(json.dumps(res))
