@@ -235,10 +235,15 @@ class StepGraph:
         # the next batch's sampling plan runs on its own stream (own hardware queue),
         # concurrently with this step's graph; the graph reads plan_cur only
         if self.split:
-            self._replay()
+            # the side-stream work is enqueued BEFORE the second graph: launching a graph of
+            # ~1000 nodes takes the host milliseconds, and the FPS must be in its queue when
+            # the first graph's last kernel retires
+            self.graph.replay()
+            self.mid_event.record()
             self.fps_stream.wait_event(self.mid_event)   # after next_pc's copy, too
             with torch.cuda.stream(self.fps_stream):
                 nxt = self._sample(self.next_pc)
+            self.graph2.replay()
         else:
             self.fps_stream.wait_stream(cur)
             with torch.cuda.stream(self.fps_stream):
