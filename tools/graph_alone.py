@@ -42,5 +42,40 @@ def main():
     print(json.dumps(res))
 
 
+
+
+def host_launch_cost():
+    """host time of graph.replay() (the launch call only) vs the GPU time of the step"""
+    ov3d_import.load()
+    import bench
+    from ov3d_amd import gemm, synthetic
+    from ov3d_amd.graphs import StepGraph
+    dev = torch.device("cuda", 0)
+    args = bench.default_args()
+    model, crit, opt = bench.build(args, dev)
+    gemm.DEFER_WGRAD = True
+    pool = [synthetic.make_batch(8, seed=i, device=dev) for i in range(2)]
+    g = StepGraph(model, crit, opt, pool[0], amp_dtype=torch.bfloat16, clip=args.clip_gradient)
+    for i in range(3):
+        g.step(pool[i % 2], pool[(i + 1) % 2])
+    torch.cuda.synchronize()
+    out = {}
+    for name, gr in (("graph_A", g.graph), ("graph_B", g.graph2)):
+        if gr is None:
+            continue
+        ts = []
+        for _ in range(5):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            gr.replay()
+            ts.append((time.perf_counter() - t0) * 1e3)
+        torch.cuda.synchronize()
+        out[name + "_host_ms"] = round(sorted(ts)[2], 3)
+    print(json.dumps(out))
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "host":
+        host_launch_cost()
+    else:
+        main()
