@@ -458,6 +458,9 @@ class TransformerDecoder(nn.Module):
             # K / V projection inputs are cast to bf16 once for the 8 layers
             memory = memory.to(torch.bfloat16)
             memory_pos = memory_pos.to(torch.bfloat16)
+        hook = getattr(self, "after_memory_kv", None)
+        if hook is not None:   # graphs.StepGraph: where the step's graph is split
+            hook()
         pend = rn.Pending(tgt, None, 0.0, 0)
         inter = []
         dec_norm = self.norm if self.return_intermediate else None
