@@ -105,8 +105,24 @@ __global__ void __launch_bounds__(256) rows_bn_stats_kernel(const T* __restrict_
         float acc[2][8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[0][j] = acc[1][j] = 0.f;
-        if (p.active && c < C)
-            for (long long r = (long long)blockIdx.x * p.rp + p.ph; r < R; r += (long long)gridDim.x * p.rp) {
+        if (p.active && c < C) {
+            // 4 rows' loads in flight per round (the loop is latency-bound otherwise: 32 rows
+            // per block at 8192 rows); the per-lane summation order is the row order, as before
+            const long long step = (long long)gridDim.x * p.rp;
+            long long r = (long long)blockIdx.x * p.rp + p.ph;
+            for (; r + 3 * step < R; r += 4 * step) {
+                float v[4][8];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) load8<T>(x, L, r + u * step, c, v[u]);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        acc[0][j] += v[u][j];
+                        acc[1][j] = fmaf(v[u][j], v[u][j], acc[1][j]);
+                    }
+            }
+            for (; r < R; r += step) {
                 float v[8];
                 load8<T>(x, L, r, c, v);
 #pragma unroll
@@ -115,6 +131,7 @@ __global__ void __launch_bounds__(256) rows_bn_stats_kernel(const T* __restrict_
                     acc[1][j] = fmaf(v[j], v[j], acc[1][j]);
                 }
             }
+        }
         block_partials(p, C, cbase, acc, partials);
     }
 }
@@ -187,21 +204,43 @@ __global__ void __launch_bounds__(256) rows_bn_bwd_kernel(
         float acc[2][8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[0][j] = acc[1][j] = 0.f;
-        if (p.active && c < C)
-            for (long long r = (long long)blockIdx.x * p.rp + p.ph; r < R; r += (long long)gridDim.x * p.rp) {
-                float xv[8], zv[8];
-                load8<T>(x, LX, r, c, xv);
-                load8<bf16>(dz, LZ, r, c, zv);
+        if (p.active && c < C) {
+            float sc[8], sh[8], mu[8], is[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                sc[j] = scale[c + j]; sh[j] = shift[c + j]; mu[j] = mean[c + j]; is[j] = invstd[c + j];
+            }
+            auto row = [&](long long r, const float* xv, const float* zv) {
                 bool keep[8];
                 if (thresh) keep8(row_base(sm, r), c, thresh, keep);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    float dt = fmaf(xv[j], scale[c + j], shift[c + j]) > 0.f ? zv[j] : 0.f;
+                    float dt = fmaf(xv[j], sc[j], sh[j]) > 0.f ? zv[j] : 0.f;
                     if (thresh) dt = keep[j] ? dt * keep_scale : 0.f;
                     acc[0][j] += dt;
-                    acc[1][j] = fmaf(dt, (xv[j] - mean[c + j]) * invstd[c + j], acc[1][j]);
+                    acc[1][j] = fmaf(dt, (xv[j] - mu[j]) * is[j], acc[1][j]);
                 }
+            };
+            // 2 rows' loads in flight per round (latency-bound loop otherwise); row order kept
+            const long long step = (long long)gridDim.x * p.rp;
+            long long r = (long long)blockIdx.x * p.rp + p.ph;
+            for (; r + step < R; r += 2 * step) {
+                float xv[2][8], zv[2][8];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    load8<T>(x, LX, r + u * step, c, xv[u]);
+                    load8<bf16>(dz, LZ, r + u * step, c, zv[u]);
+                }
+                row(r, xv[0], zv[0]);
+                row(r + step, xv[1], zv[1]);
             }
+            for (; r < R; r += step) {
+                float xv[8], zv[8];
+                load8<T>(x, LX, r, c, xv);
+                load8<bf16>(dz, LZ, r, c, zv);
+                row(r, xv, zv);
+            }
+        }
         block_partials(p, C, cbase, acc, partials);
     }
 }
