@@ -427,6 +427,7 @@ __global__ __launch_bounds__(kThreads) void sa_pool_bwd_kernel(
     const int tid = threadIdx.x, n = tid % N, ph = tid / N, nph = kThreads / N;
     const float a = scale[n], b = shift[n], mu = mean[n], is = invstd[n];
     float s = 0.f, q = 0.f;
+#pragma unroll 4
     for (long long pi = (long long)blockIdx.x * nph + ph; pi < P; pi += (long long)gridDim.x * nph) {
         const long long i = pi * N + n;
         const float y = ysel[i];

@@ -38,7 +38,7 @@ from .gemm import cast_param, weight_grad
 NPARTS_LAYER = 1024    # MFMA workgroups over 64-row tiles (more than resident: no tail when
                        # the side-stream FPS holds a few CUs; tools/sa_layer_probe.py)
 NPARTS_ROWS = 1024     # row-pass workgroups
-NPARTS_POOL = 256
+NPARTS_POOL = 1024    # pooled-gradient pass: 16 centroids per thread at P = 16384 (was 64: latency-bound)
 # last layer's backward in one pass (csrc/sa_bwd.hip): one persistent workgroup per CU
 FUSED_BWD = os.environ.get("OV3D_SA_FUSED_BWD", "1") != "0"
 NWG_DY_FUSED = int(os.environ.get("OV3D_SA_DY_NWG", "256"))
