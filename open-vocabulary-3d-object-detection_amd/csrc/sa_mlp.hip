@@ -324,36 +324,66 @@ __global__ __launch_bounds__(kThreads) void sa_l1_kernel(const float* __restrict
 }
 
 // (nparts, width) fp64 partials -> (width) totals, fixed summation order (deterministic).
-// Sum over the nparts rows of column c of (nparts, width) fp64 partials, by a 1024-thread
-// block of 32 columns x 32 partial lanes (pl), 8 loads in flight per thread, fixed order.
-// The result is valid in the pl == 0 lanes.
-__device__ __forceinline__ double column_total(const double* __restrict__ partials, int nparts,
-                                               int width, int c, int pl, double (*red)[33]) {
-    double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (c < width) {
-        int w = pl;
-        for (; w + 7 * 32 < nparts; w += 8 * 32)
+// A 1024-thread block covers 8 columns x 128 partial lanes (pl): a lane sums rows pl,
+// pl + 128, ... of up to two columns (ca, cb < 0: none) with 8 loads of each in flight, then
+// a fixed two-level LDS reduction (16 lanes x 8, then 16).  (Was 32 columns x 32 lanes: one
+// block per 32 columns left the C <= 256 BatchNorms latency-bound on 2-8 CUs.)  The results
+// are valid in the pl == 0 lanes.
+constexpr int kColW = 8, kColPL = 1024 / kColW;
+__device__ __forceinline__ void column_totals2(const double* __restrict__ partials, int nparts,
+                                               int width, int ca, int cb, int pl,
+                                               double (*red)[2][kColW + 1], double& ta,
+                                               double& tb) {
+    double a[8] = {0, 0, 0, 0, 0, 0, 0, 0}, b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const bool va = ca >= 0 && ca < width, vb = cb >= 0 && cb < width;
+    int w = pl;
+    for (; w + 7 * kColPL < nparts; w += 8 * kColPL) {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) s[u] += partials[(size_t)(w + u * 32) * width + c];
-        for (; w < nparts; w += 32) s[0] += partials[(size_t)w * width + c];
+        for (int u = 0; u < 8; ++u) {
+            if (va) a[u] += partials[(size_t)(w + u * kColPL) * width + ca];
+            if (vb) b[u] += partials[(size_t)(w + u * kColPL) * width + cb];
+        }
     }
+    for (; w < nparts; w += kColPL) {
+        if (va) a[0] += partials[(size_t)w * width + ca];
+        if (vb) b[0] += partials[(size_t)w * width + cb];
+    }
+    const int col = threadIdx.x % kColW;
     __syncthreads();   // red may still be read by a previous round
-    red[pl][threadIdx.x & 31] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+    red[pl][0][col] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    red[pl][1][col] = ((b[0] + b[1]) + (b[2] + b[3])) + ((b[4] + b[5]) + (b[6] + b[7]));
     __syncthreads();
-    double t = 0;
+    double ra = 0, rb = 0;
+    if (pl < 16) {
+#pragma unroll
+        for (int k = 0; k < kColPL / 16; ++k) {
+            ra += red[pl + 16 * k][0][col];
+            rb += red[pl + 16 * k][1][col];
+        }
+    }
+    __syncthreads();
+    if (pl < 16) {
+        red[pl][0][col] = ra;
+        red[pl][1][col] = rb;
+    }
+    __syncthreads();
+    ta = tb = 0;
     if (pl == 0) {
 #pragma unroll
-        for (int k = 0; k < 32; ++k) t += red[k][threadIdx.x];
+        for (int k = 0; k < 16; ++k) {
+            ta += red[k][0][col];
+            tb += red[k][1][col];
+        }
     }
-    return t;
 }
 
 __global__ __launch_bounds__(1024) void reduce_partials_kernel(const double* __restrict__ partials,
                                                                int nparts, int width,
                                                                double* __restrict__ totals) {
-    __shared__ double red[32][33];
-    const int c = blockIdx.x * 32 + (threadIdx.x & 31), pl = threadIdx.x >> 5;
-    const double t = column_total(partials, nparts, width, c, pl, red);
+    __shared__ double red[kColPL][2][kColW + 1];
+    const int c = blockIdx.x * kColW + (threadIdx.x % kColW), pl = threadIdx.x / kColW;
+    double t, unused;
+    column_totals2(partials, nparts, width, c, -1, pl, red, t, unused);
     if (pl == 0 && c < width) totals[c] = t;
 }
 
@@ -486,10 +516,10 @@ __global__ __launch_bounds__(1024) void bn_stats_finalize_kernel(
     const float* beta, float eps, float momentum, float* running_mean, float* running_var,
     float* mean_out, float* invstd_out, float* scale_out, float* shift_out,
     long long* num_batches_tracked) {
-    __shared__ double red[32][33];
-    const int c = blockIdx.x * 32 + (threadIdx.x & 31), pl = threadIdx.x >> 5;
-    const double tsum = column_total(partials, nparts, 2 * C, c, pl, red);
-    const double tsq = column_total(partials, nparts, 2 * C, C + c, pl, red);
+    __shared__ double red[kColPL][2][kColW + 1];
+    const int c = blockIdx.x * kColW + (threadIdx.x % kColW), pl = threadIdx.x / kColW;
+    double tsum, tsq;
+    column_totals2(partials, nparts, 2 * C, c < C ? c : -1, c < C ? C + c : -1, pl, red, tsum, tsq);
     if (blockIdx.x == 0 && threadIdx.x == 0 && num_batches_tracked) *num_batches_tracked += 1;
     if (pl == 0 && c < C)
         bn_finalize_one(c, tsum, tsq, count, gamma, beta, eps, momentum, running_mean, running_var,
@@ -500,10 +530,10 @@ __global__ __launch_bounds__(1024) void bn_bwd_stats_finalize_kernel(
     const double* __restrict__ partials, int nparts, int C, double count, const float* gamma,
     const float* mean, const float* invstd, float* cA, float* cB, float* cC, float* dgamma,
     float* dbeta) {
-    __shared__ double red[32][33];
-    const int c = blockIdx.x * 32 + (threadIdx.x & 31), pl = threadIdx.x >> 5;
-    const double t1 = column_total(partials, nparts, 2 * C, c, pl, red);
-    const double t2 = column_total(partials, nparts, 2 * C, C + c, pl, red);
+    __shared__ double red[kColPL][2][kColW + 1];
+    const int c = blockIdx.x * kColW + (threadIdx.x % kColW), pl = threadIdx.x / kColW;
+    double t1, t2;
+    column_totals2(partials, nparts, 2 * C, c < C ? c : -1, c < C ? C + c : -1, pl, red, t1, t2);
     if (pl == 0 && c < C)
         bn_bwd_finalize_one(c, t1, t2, count, gamma, mean, invstd, cA, cB, cC, dgamma, dbeta);
 }
@@ -764,7 +794,7 @@ extern "C" int ov3d_sa_layer_dy(const void* yprev, const float* scale, const flo
 extern "C" int ov3d_reduce_partials(const double* partials, int nparts, int width, double* totals,
                                     void* stream) {
     if (nparts <= 0 || width <= 0 || !partials || !totals) return OV3D_EINVAL;
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3(ov3d_cdiv(width, 32)), dim3(1024), 0,
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3(ov3d_cdiv(width, kColW)), dim3(1024), 0,
                        ov3d_stream(stream), partials, nparts, width, totals);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
@@ -793,7 +823,7 @@ extern "C" int ov3d_bn_stats_finalize(const double* partials, int nparts, int C,
     if (C <= 0 || nparts <= 0 || count <= 0 || !partials || !mean_out || !invstd_out ||
         !scale_out || !shift_out)
         return OV3D_EINVAL;
-    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(ov3d_cdiv(C, 32)), dim3(1024), 0,
+    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(ov3d_cdiv(C, kColW)), dim3(1024), 0,
                        ov3d_stream(stream), partials, nparts, C, count, gamma, beta, eps, momentum,
                        running_mean, running_var, mean_out, invstd_out, scale_out, shift_out,
                        num_batches_tracked);
@@ -807,7 +837,7 @@ extern "C" int ov3d_bn_bwd_stats_finalize(const double* partials, int nparts, in
                                           float* dgamma, float* dbeta, void* stream) {
     if (C <= 0 || nparts <= 0 || count <= 0 || !partials || !mean || !invstd || !cA || !cB || !cC)
         return OV3D_EINVAL;
-    hipLaunchKernelGGL(bn_bwd_stats_finalize_kernel, dim3(ov3d_cdiv(C, 32)), dim3(1024), 0,
+    hipLaunchKernelGGL(bn_bwd_stats_finalize_kernel, dim3(ov3d_cdiv(C, kColW)), dim3(1024), 0,
                        ov3d_stream(stream), partials, nparts, C, count, gamma, mean, invstd, cA, cB,
                        cC, dgamma, dbeta);
     OV3D_LAUNCH_CHECK();
