@@ -493,6 +493,12 @@ int ov3d_targets_prep(int B, int G, int L, const float* present, const float* an
 long long ov3d_set_loss_desc_size(void);   /* sizeof(ov3d_set_loss_desc), for FFI layout checks */
 int ov3d_set_loss_fwd(const ov3d_set_loss_desc* desc, float* raw, int* ticket, float* dict_out,
                       float* total, void* stream);
+/* The same with a workgroup per (256 proposals, layer) (the per-layer launch is
+ * latency-bound); parts: ov3d_set_loss_fwd_parts(L, B, Q) doubles of scratch.  The chunk sums
+ * are added in chunk order: deterministic, equal to the per-layer form up to fp64 rounding. */
+long long ov3d_set_loss_fwd_parts(int L, int B, int Q);
+int ov3d_set_loss_fwd_split(const ov3d_set_loss_desc* desc, float* raw, int* ticket,
+                            float* dict_out, float* total, double* parts, void* stream);
 /* d_dict (L, 8) or NULL, d_total scalar (device) or NULL; every non-NULL gradient is written
  * in full (contiguous (L*B*Q, n), g_gious (L*B, Q, G), g_align (L,)) */
 int ov3d_set_loss_bwd(const ov3d_set_loss_desc* desc, const float* raw, const float* d_dict,

@@ -55,6 +55,7 @@ _SIGS = {
     "ov3d_attn_bwd_masked": "ppplllplplpiiiiffppplplplpipp",
     "ov3d_attn_mask_pack": "pifiiipp",
     "ov3d_nbr_max_fwd": "pliippp",
+    "ov3d_set_loss_fwd_split": "ppppppp",
     "ov3d_group_inverse": "piiiippppp",
     "ov3d_group_bwd_csr": "pppiiilllpp",
     "ov3d_nbr_max_bwd": "ppliipp",
@@ -97,7 +98,7 @@ _SIGS = {
     "ov3d_ap_curve": "plppiplppp",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
-                          "ov3d_attn_dropbits_words", "ov3d_attn_maskbits_words", "ov3d_fps_workspace", "ov3d_attn_small_bwd",
+                          "ov3d_attn_dropbits_words", "ov3d_attn_maskbits_words", "ov3d_fps_workspace", "ov3d_attn_small_bwd", "ov3d_set_loss_fwd_parts",
                           "ov3d_wgrad_workspace", "ov3d_wgrad_tiles", "ov3d_wgrad_group_tiles",
                           "ov3d_set_loss_desc_size",
                           "ov3d_resnorm_supported", "ov3d_resnorm_bwd_parts",
@@ -132,6 +133,8 @@ def load():
         lib.ov3d_attn_fwd_workspace.restype = ctypes.c_longlong
         lib.ov3d_attn_dropbits_words.argtypes = [ctypes.c_int] * 4
         lib.ov3d_attn_dropbits_words.restype = ctypes.c_longlong
+        lib.ov3d_set_loss_fwd_parts.argtypes = [ctypes.c_int] * 3
+        lib.ov3d_set_loss_fwd_parts.restype = ctypes.c_longlong
         lib.ov3d_fps_workspace.argtypes = [ctypes.c_int] * 2
         lib.ov3d_fps_workspace.restype = ctypes.c_longlong
         lib.ov3d_attn_small_bwd.argtypes = [ctypes.c_int]

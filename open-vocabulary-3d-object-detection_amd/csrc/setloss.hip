@@ -70,97 +70,76 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-__global__ void __launch_bounds__(kThreads) set_loss_fwd_kernel(ov3d_set_loss_desc d, float* raw,
-                                                                 int* ticket, float* dict_out,
-                                                                 float* total) {
-    const int l = blockIdx.x;
-    const int P = d.B * d.Q;
-    __shared__ int cnt[OV3D_LOSS_MAX_B];
-    __shared__ double red[kThreads / 64][7];
-    __shared__ int is_last;
-    for (int b = threadIdx.x; b < d.B; b += kThreads) cnt[b] = 0;
-    __syncthreads();
+// the loss terms of proposal p of computation layer l into acc (sem num, sem den, angle cls,
+// angle reg, center, size, giou) and the scene's count of non-background argmax (cnt, LDS)
+__device__ __forceinline__ void proposal_terms(const ov3d_set_loss_desc& d, int l, int p, int P,
+                                               double* acc, int* cnt) {
+    const int b = p / d.Q;
+    const long long row = (long long)l * P + p;
+    const long long mrow = match_row(d, l, p);
+    const float m = d.matched[mrow];
+    const int g = clampi(d.inds[mrow], d.G - 1);
+    const long long bg = (long long)b * d.G + g;
 
-    double acc[7] = {0, 0, 0, 0, 0, 0, 0};   // sem num, sem den, acls, areg, center, size, giou
-    for (int p = threadIdx.x; p < P; p += kThreads) {
-        const int b = p / d.Q;
-        const long long row = (long long)l * P + p;
-        const long long mrow = match_row(d, l, p);
-        const float m = d.matched[mrow];
-        const int g = clampi(d.inds[mrow], d.G - 1);
-        const long long bg = (long long)b * d.G + g;
+    const float* x = d.logits + row * d.ld_logits;
+    float mx, s;
+    int am;
+    softmax_stats(x, d.T, mx, am, s);
+    if (am != d.T - 1) atomicAdd(&cnt[b], 1);
+    if (d.flags & OV3D_LOSS_SEM) {
+        const int lab = (m == 0.f) ? d.T - 1 : clampi(d.gt_sem[bg], d.T - 1);
+        const float nll = logf(s) - (x[lab] - mx);
+        const float wt = d.cls_weights[lab];
+        acc[0] += (double)(nll * wt);
+        acc[1] += (double)wt;
+    }
+    {
+        const float* a = d.angle_logits + row * d.ld_angle_logits;
+        float ma, sa;
+        int ia;
+        softmax_stats(a, d.NB, ma, ia, sa);
+        const int gl = clampi(d.gt_angle_cls[bg], d.NB - 1);
+        acc[2] += (double)((logf(sa) - (a[gl] - ma)) * m);
+        const float gr = d.gt_angle_res[bg] * d.res_scale;
+        const float e = d.angle_res[row * d.ld_angle_res + gl] - gr;
+        acc[3] += (double)(huber(e) * m);
+    }
+    if (d.flags & OV3D_LOSS_CENTER) {
+        const float* c = d.center + row * d.ld_center;
+        const float* gc = d.gt_center + bg * 3;
+        const float cl = (fabsf(c[0] - gc[0]) + fabsf(c[1] - gc[1])) + fabsf(c[2] - gc[2]);
+        acc[4] += (double)(cl * m);
+    }
+    if (d.flags & OV3D_LOSS_SIZE) {
+        const float* z = d.size + row * d.ld_size;
+        const float* gz = d.gt_size + bg * 3;
+        const float sl = (fabsf(z[0] - gz[0]) + fabsf(z[1] - gz[1])) + fabsf(z[2] - gz[2]);
+        acc[5] += (double)(sl * m);
+    }
+    if (d.flags & OV3D_LOSS_GIOU) {
+        acc[6] += (double)((1.f - d.gious[row * d.G + g]) * m);
+    }
+}
 
-        const float* x = d.logits + row * d.ld_logits;
-        float mx, s;
-        int am;
-        softmax_stats(x, d.T, mx, am, s);
-        if (am != d.T - 1) atomicAdd(&cnt[b], 1);
-        if (d.flags & OV3D_LOSS_SEM) {
-            const int lab = (m == 0.f) ? d.T - 1 : clampi(d.gt_sem[bg], d.T - 1);
-            const float nll = logf(s) - (x[lab] - mx);
-            const float wt = d.cls_weights[lab];
-            acc[0] += (double)(nll * wt);
-            acc[1] += (double)wt;
-        }
-        {
-            const float* a = d.angle_logits + row * d.ld_angle_logits;
-            float ma, sa;
-            int ia;
-            softmax_stats(a, d.NB, ma, ia, sa);
-            const int gl = clampi(d.gt_angle_cls[bg], d.NB - 1);
-            acc[2] += (double)((logf(sa) - (a[gl] - ma)) * m);
-            const float gr = d.gt_angle_res[bg] * d.res_scale;
-            const float e = d.angle_res[row * d.ld_angle_res + gl] - gr;
-            acc[3] += (double)(huber(e) * m);
-        }
-        if (d.flags & OV3D_LOSS_CENTER) {
-            const float* c = d.center + row * d.ld_center;
-            const float* gc = d.gt_center + bg * 3;
-            const float cl = (fabsf(c[0] - gc[0]) + fabsf(c[1] - gc[1])) + fabsf(c[2] - gc[2]);
-            acc[4] += (double)(cl * m);
-        }
-        if (d.flags & OV3D_LOSS_SIZE) {
-            const float* z = d.size + row * d.ld_size;
-            const float* gz = d.gt_size + bg * 3;
-            const float sl = (fabsf(z[0] - gz[0]) + fabsf(z[1] - gz[1])) + fabsf(z[2] - gz[2]);
-            acc[5] += (double)(sl * m);
-        }
-        if (d.flags & OV3D_LOSS_GIOU) {
-            acc[6] += (double)((1.f - d.gious[row * d.G + g]) * m);
-        }
-    }
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-        const double v = wave_sum(acc[k]);
-        if (lane == 0) red[w][k] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double t[7];
-        for (int k = 0; k < 7; ++k) {
-            t[k] = 0;
-            for (int j = 0; j < kThreads / 64; ++j) t[k] += red[j][k];
-        }
-        const float nb = *d.num_boxes;
-        float* r = raw + (long long)l * kRaw;
-        r[0] = (d.flags & OV3D_LOSS_SEM) ? (float)t[0] / (float)t[1] : 0.f;
-        r[1] = (float)t[2] / nb;
-        r[2] = (float)t[3] / nb;
-        r[3] = (d.flags & OV3D_LOSS_CENTER) ? (float)t[4] / nb : 0.f;
-        r[4] = (d.flags & OV3D_LOSS_SIZE) ? (float)t[5] / nb : 0.f;
-        r[5] = (d.flags & OV3D_LOSS_GIOU) ? (float)t[6] / nb : 0.f;
-        r[6] = (d.flags & OV3D_LOSS_ALIGN) ? d.align[l] : 0.f;
-        float card = 0.f;
-        for (int b = 0; b < d.B; ++b) card += fabsf((float)cnt[b] - (float)d.nactual[b]);
-        r[7] = card / (float)d.B;
-        r[8] = (float)t[1];
-        __threadfence();
-        is_last = (atomicAdd(ticket, 1) == d.L - 1);
-    }
-    __syncthreads();
-    if (!is_last || threadIdx.x != 0) return;
-    __threadfence();
+// one layer's raw loss row (criterion.py:274-311 terms, normalised as the reference)
+__device__ __forceinline__ void layer_raw(const ov3d_set_loss_desc& d, int l, const double* t,
+                                          float card_sum, float* raw) {
+    const float nb = *d.num_boxes;
+    float* r = raw + (long long)l * kRaw;
+    r[0] = (d.flags & OV3D_LOSS_SEM) ? (float)t[0] / (float)t[1] : 0.f;
+    r[1] = (float)t[2] / nb;
+    r[2] = (float)t[3] / nb;
+    r[3] = (d.flags & OV3D_LOSS_CENTER) ? (float)t[4] / nb : 0.f;
+    r[4] = (d.flags & OV3D_LOSS_SIZE) ? (float)t[5] / nb : 0.f;
+    r[5] = (d.flags & OV3D_LOSS_GIOU) ? (float)t[6] / nb : 0.f;
+    r[6] = (d.flags & OV3D_LOSS_ALIGN) ? d.align[l] : 0.f;
+    r[7] = card_sum / (float)d.B;
+    r[8] = (float)t[1];
+}
+
+// the dict table and the total from every layer's raw row (one thread)
+__device__ __forceinline__ void finalize_total(const ov3d_set_loss_desc& d, const float* raw,
+                                               float* dict_out, float* total) {
     float tot = 0.f;
     for (int i = 0; i < d.L; ++i) {
         const float* r = raw + (long long)layer_at(d, i) * kRaw;
@@ -178,6 +157,102 @@ __global__ void __launch_bounds__(kThreads) set_loss_fwd_kernel(ov3d_set_loss_de
         if (bad) tot = __int_as_float(0x7fc00000);
     }
     *total = tot;
+}
+
+__global__ void __launch_bounds__(kThreads) set_loss_fwd_kernel(ov3d_set_loss_desc d, float* raw,
+                                                                 int* ticket, float* dict_out,
+                                                                 float* total) {
+    const int l = blockIdx.x;
+    const int P = d.B * d.Q;
+    __shared__ int cnt[OV3D_LOSS_MAX_B];
+    __shared__ double red[kThreads / 64][7];
+    __shared__ int is_last;
+    for (int b = threadIdx.x; b < d.B; b += kThreads) cnt[b] = 0;
+    __syncthreads();
+
+    double acc[7] = {0, 0, 0, 0, 0, 0, 0};   // sem num, sem den, acls, areg, center, size, giou
+    for (int p = threadIdx.x; p < P; p += kThreads) proposal_terms(d, l, p, P, acc, cnt);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        const double v = wave_sum(acc[k]);
+        if (lane == 0) red[w][k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t[7];
+        for (int k = 0; k < 7; ++k) {
+            t[k] = 0;
+            for (int j = 0; j < kThreads / 64; ++j) t[k] += red[j][k];
+        }
+        float card = 0.f;
+        for (int b = 0; b < d.B; ++b) card += fabsf((float)cnt[b] - (float)d.nactual[b]);
+        layer_raw(d, l, t, card, raw);
+        __threadfence();
+        is_last = (atomicAdd(ticket, 1) == d.L - 1);
+    }
+    __syncthreads();
+    if (!is_last || threadIdx.x != 0) return;
+    __threadfence();
+    finalize_total(d, raw, dict_out, total);
+    *ticket = 0;
+}
+
+// Split form (ov3d_set_loss_fwd_split): a workgroup per (chunk of kThreads proposals, layer),
+// one proposal per thread (the per-layer form runs 4 proposals per thread through two
+// softmaxes each on 8 workgroups: latency-bound).  Each workgroup writes its chunk's 7 sums
+// and per-scene argmax counts; the last one to finish adds each layer's chunks in chunk
+// order (deterministic) and finalises as the per-layer form.
+__global__ void __launch_bounds__(kThreads) set_loss_fwd_split_kernel(
+    ov3d_set_loss_desc d, float* raw, int* ticket, float* dict_out, float* total,
+    double* __restrict__ part) {
+    const int S = gridDim.x, sidx = blockIdx.x, l = blockIdx.y;
+    const int P = d.B * d.Q, W = 7 + d.B;
+    __shared__ int cnt[OV3D_LOSS_MAX_B];
+    __shared__ double red[kThreads / 64][7];
+    __shared__ int is_last;
+    for (int b = threadIdx.x; b < d.B; b += kThreads) cnt[b] = 0;
+    __syncthreads();
+    double acc[7] = {0, 0, 0, 0, 0, 0, 0};
+    const int p = sidx * kThreads + threadIdx.x;
+    if (p < P) proposal_terms(d, l, p, P, acc, cnt);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        const double v = wave_sum(acc[k]);
+        if (lane == 0) red[w][k] = v;
+    }
+    __syncthreads();
+    double* mine = part + ((size_t)l * S + sidx) * W;
+    if (threadIdx.x < 7) {
+        double t = 0;
+        for (int j = 0; j < kThreads / 64; ++j) t += red[j][threadIdx.x];
+        mine[threadIdx.x] = t;
+    }
+    for (int b = threadIdx.x; b < d.B; b += kThreads) mine[7 + b] = (double)cnt[b];
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) is_last = (atomicAdd(ticket, 1) == d.L * S - 1);
+    __syncthreads();
+    if (!is_last) return;
+    __threadfence();
+    for (int ll = threadIdx.x; ll < d.L; ll += kThreads) {
+        double t[7] = {0, 0, 0, 0, 0, 0, 0};
+        const double* pl = part + (size_t)ll * S * W;
+        for (int c = 0; c < S; ++c)
+            for (int k = 0; k < 7; ++k) t[k] += pl[(size_t)c * W + k];
+        float card = 0.f;
+        for (int b = 0; b < d.B; ++b) {
+            double n = 0;
+            for (int c = 0; c < S; ++c) n += pl[(size_t)c * W + 7 + b];
+            card += fabsf((float)n - (float)d.nactual[b]);
+        }
+        layer_raw(d, ll, t, card, raw);
+    }
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    finalize_total(d, raw, dict_out, total);
     *ticket = 0;
 }
 
@@ -285,6 +360,23 @@ extern "C" int ov3d_set_loss_fwd(const ov3d_set_loss_desc* desc, float* raw, int
     if (check_desc(desc) != OV3D_OK || !raw || !ticket || !dict_out || !total) return OV3D_EINVAL;
     set_loss_fwd_kernel<<<desc->L, kThreads, 0, ov3d_stream(stream)>>>(*desc, raw, ticket, dict_out,
                                                                        total);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+/* doubles of scratch ov3d_set_loss_fwd_split needs */
+extern "C" long long ov3d_set_loss_fwd_parts(int L, int B, int Q) {
+    if (L <= 0 || B <= 0 || Q <= 0) return 0;
+    return (long long)L * ((B * Q + kThreads - 1) / kThreads) * (7 + B);
+}
+
+extern "C" int ov3d_set_loss_fwd_split(const ov3d_set_loss_desc* desc, float* raw, int* ticket,
+                                       float* dict_out, float* total, double* parts, void* stream) {
+    if (check_desc(desc) != OV3D_OK || !raw || !ticket || !dict_out || !total || !parts)
+        return OV3D_EINVAL;
+    const int S = (desc->B * desc->Q + kThreads - 1) / kThreads;
+    set_loss_fwd_split_kernel<<<dim3(S, desc->L), kThreads, 0, ov3d_stream(stream)>>>(
+        *desc, raw, ticket, dict_out, total, parts);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

@@ -93,6 +93,9 @@ def _res_scale(nb):
     return float(torch.tensor(1.0, dtype=torch.float32) / torch.tensor(math.pi / nb, dtype=torch.float32))
 
 
+SPLIT_FWD = True   # ov3d_set_loss_fwd_split (tests compare it with the per-layer launch)
+
+
 class _SetLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, meta, logits, angle_logits, angle_res, center, size, gious, align, aux):
@@ -102,8 +105,14 @@ class _SetLoss(torch.autograd.Function):
         raw = torch.empty((L, 9), dtype=torch.float32, device=dev)
         table = torch.empty((L, 8), dtype=torch.float32, device=dev)
         total = torch.empty((), dtype=torch.float32, device=dev)
-        _native.call("ov3d_set_loss_fwd", ctypes.addressof(desc), raw, _ticket(dev), table, total,
-                     like=logits)
+        n = _native.load().ov3d_set_loss_fwd_parts(L, desc.B, desc.Q) if SPLIT_FWD else 0
+        if n > 0:   # a workgroup per (256 proposals, layer) instead of one per layer
+            parts = torch.empty((n,), dtype=torch.float64, device=dev)
+            _native.call("ov3d_set_loss_fwd_split", ctypes.addressof(desc), raw, _ticket(dev),
+                         table, total, parts, like=logits)
+        else:
+            _native.call("ov3d_set_loss_fwd", ctypes.addressof(desc), raw, _ticket(dev), table,
+                         total, like=logits)
         ctx.meta = meta
         ctx.shapes = tuple(t.shape if t is not None else None
                            for t in (logits, angle_logits, angle_res, center, size, gious, align))

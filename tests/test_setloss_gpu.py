@@ -177,3 +177,30 @@ def test_invalid_matching_cost_poisons_total(cuda, fused):
     bad, ld, _ = _run(crit, st, batch, fused, True, None)
     assert torch.isnan(bad)
     assert all(torch.isfinite(v) for v in ld.values())
+
+
+@pytest.mark.parametrize("giou_w,align_w", [(0.0, 0.0), (1.0, 2e-4)])
+def test_split_loss_forward_equals_per_layer(cuda, monkeypatch, giou_w, align_w):
+    """ov3d_set_loss_fwd_split (a workgroup per 256 proposals and layer, chunk sums added in
+    chunk order) vs the per-layer launch: the same loss dict and total up to fp64 rounding
+    of the sums (1e-6 relative), identical gradients (the backward reads the same raw rows
+    up to that rounding)"""
+    from ov3d_amd import setloss, synthetic
+    B, Q, L, T, NB = 8, 128, 8, 21, 12
+    st = _outputs(cuda, B, Q, L, T, NB, seed=4)
+    batch = synthetic.make_batch(B, seed=6, num_points=2048, device=cuda, use_image=align_w > 0)
+    if giou_w > 0:
+        batch["gt_box_angles"].zero_()
+    crit = _criterion(cuda, giou_w, align_w)
+    clip = FakeRegionCLIP() if align_w > 0 else None
+    res = {}
+    for split in (True, False):
+        monkeypatch.setattr(setloss, "SPLIT_FWD", split)
+        res[split] = _run(crit, st, batch, True, True, clip)
+    (ls, ds, gs), (lp, dp, gp) = res[True], res[False]
+    assert abs(ls.item() - lp.item()) <= 1e-6 * abs(lp.item())
+    for k in dp:
+        assert abs(ds[k].item() - dp[k].item()) <= 1e-6 * max(abs(dp[k].item()), 1e-6), k
+    for k in gp:
+        a, b = gs[k].cpu().numpy(), gp[k].cpu().numpy()
+        assert np.abs(a - b).max() <= 1e-6 * max(np.abs(b).max(), 1e-12), k
