@@ -66,11 +66,35 @@ __global__ void __launch_bounds__(kThreads) box_param_fwd_kernel(
     BoxArgs a, float* center_n, float* center_u, float* size_n, float* size_u, float* alog,
     float* ares_n, float* ares, float* angle_out, float* corners, float* sem_prob,
     float* obj_prob) {
+    // blockIdx.y = part: 0 centre / size / angle / corners, 1 angle logits and residuals,
+    // 2 class probabilities (a thread per proposal and part: the serial per-proposal chain
+    // on 32 workgroups was latency-bound)
     const long long row = (long long)blockIdx.x * kThreads + threadIdx.x;
     if (row >= a.R) return;
+    const int part = blockIdx.y;
     const long long bq = row % ((long long)a.B * a.Q);
     const int b = (int)(bq / a.Q);
     const float* r = a.raw + row * a.ld;
+    if (part == 2) {
+        if (!a.logits) return;
+        const float* x = a.logits + row * a.T;
+        float mx = x[0];
+        for (int t = 1; t < a.T; ++t) mx = fmaxf(mx, x[t]);
+        float sum = 0.f;
+        for (int t = 0; t < a.T; ++t) sum += expf(x[t] - mx);
+        for (int t = 0; t < a.T - 1; ++t) sem_prob[row * (a.T - 1) + t] = expf(x[t] - mx) / sum;
+        obj_prob[row] = 1.f - expf(x[a.T - 1] - mx) / sum;
+        return;
+    }
+    if (part == 1) {
+        for (int t = 0; t < a.NB; ++t) {
+            alog[row * a.NB + t] = r[6 + t];
+            const float rn = r[6 + a.NB + t];
+            ares_n[row * a.NB + t] = rn;
+            ares[row * a.NB + t] = rn * a.res_scale;
+        }
+        return;
+    }
     float cu[3], su[3];
     for (int j = 0; j < 3; ++j) {
         const float lo = a.dmin[b * 3 + j], hi = a.dmax[b * 3 + j];
@@ -82,12 +106,6 @@ __global__ void __launch_bounds__(kThreads) box_param_fwd_kernel(
         size_n[row * 3 + j] = sn;
         su[j] = sn * fmaxf(hi - lo, 0.1f);
         size_u[row * 3 + j] = su[j];
-    }
-    for (int t = 0; t < a.NB; ++t) {
-        alog[row * a.NB + t] = r[6 + t];
-        const float rn = r[6 + a.NB + t];
-        ares_n[row * a.NB + t] = rn;
-        ares[row * a.NB + t] = rn * a.res_scale;
     }
     float ang;
     angle_of(a, r, ang);
@@ -102,15 +120,6 @@ __global__ void __launch_bounds__(kThreads) box_param_fwd_kernel(
         o[0] = (lx * c + lz * s) + cx;
         o[1] = ly + cy;
         o[2] = (lz * c - lx * s) + cz;
-    }
-    if (a.logits) {
-        const float* x = a.logits + row * a.T;
-        float mx = x[0];
-        for (int t = 1; t < a.T; ++t) mx = fmaxf(mx, x[t]);
-        float sum = 0.f;
-        for (int t = 0; t < a.T; ++t) sum += expf(x[t] - mx);
-        for (int t = 0; t < a.T - 1; ++t) sem_prob[row * (a.T - 1) + t] = expf(x[t] - mx) / sum;
-        obj_prob[row] = 1.f - expf(x[a.T - 1] - mx) / sum;
     }
 }
 
@@ -219,7 +228,7 @@ extern "C" int ov3d_box_param_fwd(long long R, int B, int Q, int NB, int T, cons
         (logits && (T < 2 || !sem_prob || !obj_prob)))
         return OV3D_EINVAL;
     const BoxArgs a = make(R, B, Q, NB, T, raw, ld, qxyz, dmin, dmax, logits);
-    box_param_fwd_kernel<<<ov3d_cdiv(R, kThreads), kThreads, 0, ov3d_stream(stream)>>>(
+    box_param_fwd_kernel<<<dim3(ov3d_cdiv(R, kThreads), 3), kThreads, 0, ov3d_stream(stream)>>>(
         a, center_n, center_u, size_n, size_u, alog, ares_n, ares, angle, corners, sem_prob,
         obj_prob);
     OV3D_LAUNCH_CHECK();
