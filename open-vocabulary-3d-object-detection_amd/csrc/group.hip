@@ -4,7 +4,7 @@
 // PointnetSAModuleVotes / QueryAndGroup (models/model_3detr.py:355-361, 385-391):
 // ball_query, grouping_operation (+ backward), gather_operation (+ backward).
 //
-// Ball query = one wave64 per centroid.  Each lane owns 4 consecutive points of a
+// Ball query = one wave64 per 1-8 centroids.  Each lane owns 4 consecutive points of a
 // 256-point chunk (3 x 16-B loads per lane, one coalesced 3 KiB wave read), four
 // ballots give the in-radius masks, and popcounts of the masks below the lane give
 // every hit its slot -- so the output is the first S in-radius indices in
@@ -36,58 +36,123 @@ __device__ __forceinline__ void load4(const float* __restrict__ p, int k0, int N
     }
 }
 
-template <bool ALIGNED>
+// CPW consecutive centroids of one scene per wave (M % CPW == 0; CPW = 1 is one wave per
+// centroid): each 256-point chunk is loaded once and tested against all CPW centres.  The
+// scan is VALU-bound (with few in-radius points per centroid nearly every wave scans the
+// whole scene), so the distances run as packed-f32 pairs (v_pk_add / v_pk_mul / v_pk_fma:
+// two points per lane and instruction, the same IEEE operations per element as
+// fmaf(dz, dz, fmaf(dy, dy, dx * dx))), and points past N are padded far away
+// (d2 = inf) instead of being masked.  A centroid whose S slots are full skips the tests;
+// the wave stops when all CPW are full.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <bool ALIGNED, int CPW>
 __global__ __launch_bounds__(64 * kBQWavesPerBlock) void ball_query_kernel(
     const float* __restrict__ xyz, const float* __restrict__ new_xyz, int B, int N, int M, float r2,
     int S, int32_t* __restrict__ idx) {
-    const int gw = blockIdx.x * kBQWavesPerBlock + (threadIdx.x >> 6);
-    if (gw >= B * M) return;  // wave-uniform
+    const int c0 = (blockIdx.x * kBQWavesPerBlock + (threadIdx.x >> 6)) * CPW;
+    if (c0 >= B * M) return;  // wave-uniform
     const int lane = threadIdx.x & 63;
-    const int b = gw / M;
+    const int b = c0 / M;      // the CPW centroids share the scene
     const float* __restrict__ p = xyz + (size_t)b * N * 3;
-    const float cx = new_xyz[(size_t)gw * 3], cy = new_xyz[(size_t)gw * 3 + 1],
-                cz = new_xyz[(size_t)gw * 3 + 2];
-    int32_t* __restrict__ out = idx + (size_t)gw * S;
+    float cx[CPW], cy[CPW], cz[CPW];
+    int cnt[CPW], first[CPW];
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+        cx[c] = new_xyz[(size_t)(c0 + c) * 3];
+        cy[c] = new_xyz[(size_t)(c0 + c) * 3 + 1];
+        cz[c] = new_xyz[(size_t)(c0 + c) * 3 + 2];
+        cnt[c] = 0;
+        first[c] = 0;
+    }
     const unsigned long long below = lanemask_lt();
-    int cnt = 0;
-    int first = 0;
-    for (int base = 0; base < N && cnt < S; base += 256) {
+    bool open = true;
+    for (int base = 0; base < N && open; base += 256) {
         const int k0 = base + 4 * lane;
         float x[4], y[4], z[4];
         load4<ALIGNED>(p, k0, N, x, y, z);
-        bool hit[4];
-        unsigned long long m[4];
-        int tot = 0, pre = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float dx = cx - x[j], dy = cy - y[j], dz = cz - z[j];
-            const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-            hit[j] = (k0 + j < N) && (d2 < r2);
-            m[j] = __ballot(hit[j]);
-            tot += __popcll(m[j]);
-            pre += __popcll(m[j] & below);
-        }
-        if (tot == 0) continue;
-        if (cnt == 0) {
-            int f = 0x7fffffff;
+        if (k0 + 3 >= N) {
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                if (m[j]) { const int c = base + 4 * (__ffsll((long long)m[j]) - 1) + j; f = c < f ? c : f; }
-            first = f;
+                if (k0 + j >= N) { x[j] = 3.0e38f; y[j] = 3.0e38f; z[j] = 3.0e38f; }
         }
-        int pos = cnt + pre;
+        const f32x2 xa = {x[0], x[1]}, xb = {x[2], x[3]};
+        const f32x2 ya = {y[0], y[1]}, yb = {y[2], y[3]};
+        const f32x2 za = {z[0], z[1]}, zb = {z[2], z[3]};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (hit[j]) {
-                if (pos < S) out[pos] = k0 + j;
-                ++pos;
+        for (int c = 0; c < CPW; ++c) {
+            if (cnt[c] >= S) continue;   // wave-uniform
+            const f32x2 ccx = {cx[c], cx[c]}, ccy = {cy[c], cy[c]}, ccz = {cz[c], cz[c]};
+            const f32x2 dxa = ccx - xa, dya = ccy - ya, dza = ccz - za;
+            const f32x2 dxb = ccx - xb, dyb = ccy - yb, dzb = ccz - zb;
+            const f32x2 da = __builtin_elementwise_fma(
+                dza, dza, __builtin_elementwise_fma(dya, dya, dxa * dxa));
+            const f32x2 db = __builtin_elementwise_fma(
+                dzb, dzb, __builtin_elementwise_fma(dyb, dyb, dxb * dxb));
+            const bool hit[4] = {da.x < r2, da.y < r2, db.x < r2, db.y < r2};
+            if (__ballot(hit[0] | hit[1] | hit[2] | hit[3]) == 0) continue;
+            unsigned long long m[4];
+            int tot = 0, pre = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                m[j] = __ballot(hit[j]);
+                tot += __popcll(m[j]);
+                pre += __popcll(m[j] & below);
             }
+            if (cnt[c] == 0) {
+                int f = 0x7fffffff;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (m[j]) {
+                        const int q = base + 4 * (__ffsll((long long)m[j]) - 1) + j;
+                        f = q < f ? q : f;
+                    }
+                first[c] = f;
+            }
+            int32_t* __restrict__ out = idx + (size_t)(c0 + c) * S;
+            int pos = cnt[c] + pre;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (hit[j]) {
+                    if (pos < S) out[pos] = k0 + j;
+                    ++pos;
+                }
+            }
+            cnt[c] += tot;
         }
-        cnt += tot;
+        open = false;
+#pragma unroll
+        for (int c = 0; c < CPW; ++c) open |= cnt[c] < S;
     }
-    const int filled = cnt < S ? cnt : S;
-    const int fill = cnt > 0 ? first : 0;
-    for (int s = filled + lane; s < S; s += 64) out[s] = fill;
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+        int32_t* __restrict__ out = idx + (size_t)(c0 + c) * S;
+        const int filled = cnt[c] < S ? cnt[c] : S;
+        const int fill = cnt[c] > 0 ? first[c] : 0;
+        for (int s = filled + lane; s < S; s += 64) out[s] = fill;
+    }
+}
+
+// centroids per wave of the ball query (OV3D_BQ_CPW: 1, 2, 4, 8)
+int bq_cpw() {
+    static const int v = [] {
+        const char* e = getenv("OV3D_BQ_CPW");
+        const int c = e ? atoi(e) : 2;
+        return (c == 1 || c == 2 || c == 4 || c == 8) ? c : 2;
+    }();
+    return v;
+}
+
+template <int CPW>
+void launch_bq_multi(bool aligned, hipStream_t s, const float* xyz, const float* new_xyz, int B,
+                     int N, int M, float r2, int S, int32_t* idx) {
+    const int blocks = ov3d_cdiv((long long)B * M / CPW, kBQWavesPerBlock);
+    if (aligned)
+        hipLaunchKernelGGL((ball_query_kernel<true, CPW>), dim3(blocks),
+                           dim3(64 * kBQWavesPerBlock), 0, s, xyz, new_xyz, B, N, M, r2, S, idx);
+    else
+        hipLaunchKernelGGL((ball_query_kernel<false, CPW>), dim3(blocks),
+                           dim3(64 * kBQWavesPerBlock), 0, s, xyz, new_xyz, B, N, M, r2, S, idx);
 }
 
 // out (B,M,S,3+C) channels-last rows: thread per output element (row, channel);
@@ -288,15 +353,13 @@ extern "C" int ov3d_ball_query(const float* xyz, const float* new_xyz, int B, in
     if (B < 0 || N < 0 || M < 0 || S <= 0 || !xyz || !new_xyz || !idx_out) return OV3D_EINVAL;
     if ((long long)B * M == 0) return OV3D_OK;
     const float r2 = radius * radius;
-    const int blocks = ov3d_cdiv((long long)B * M, kBQWavesPerBlock);
     hipStream_t s = ov3d_stream(stream);
     const bool aligned = (reinterpret_cast<uintptr_t>(xyz) % 16 == 0) && (N % 4 == 0);
-    if (aligned)
-        hipLaunchKernelGGL(ball_query_kernel<true>, dim3(blocks), dim3(64 * kBQWavesPerBlock), 0, s,
-                           xyz, new_xyz, B, N, M, r2, S, idx_out);
-    else
-        hipLaunchKernelGGL(ball_query_kernel<false>, dim3(blocks), dim3(64 * kBQWavesPerBlock), 0, s,
-                           xyz, new_xyz, B, N, M, r2, S, idx_out);
+    const int cpw = M % bq_cpw() == 0 ? bq_cpw() : 1;
+    if (cpw == 2) launch_bq_multi<2>(aligned, s, xyz, new_xyz, B, N, M, r2, S, idx_out);
+    else if (cpw == 4) launch_bq_multi<4>(aligned, s, xyz, new_xyz, B, N, M, r2, S, idx_out);
+    else if (cpw == 8) launch_bq_multi<8>(aligned, s, xyz, new_xyz, B, N, M, r2, S, idx_out);
+    else launch_bq_multi<1>(aligned, s, xyz, new_xyz, B, N, M, r2, S, idx_out);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

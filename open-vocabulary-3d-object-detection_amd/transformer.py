@@ -109,7 +109,10 @@ class _MemoryKV(torch.autograd.Function):
         S, B, C = memory.shape
         bf = torch.bfloat16
         mem = memory.reshape(S * B, C).to(bf).contiguous()
-        mpos = (memory + pos).reshape(S * B, C).to(bf).contiguous() if pos is not None else mem
+        mpos = mem
+        if pos is not None:   # the sum in the inputs' common type, rounded once on the store
+            mpos = torch.empty((S * B, C), dtype=bf, device=memory.device)
+            torch.add(memory, pos, out=mpos.view(S, B, C))
         Wk = torch.cat([cast_param(w, bf)[E:2 * E] for w in ws])
         Wv = torch.cat([cast_param(w, bf)[2 * E:] for w in ws])
         bk = torch.cat([cast_param(b, bf)[E:2 * E] for b in bs])

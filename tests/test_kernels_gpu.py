@@ -53,6 +53,8 @@ def test_fps_ties_and_skipped_points(cuda, N):
                                                (8, 20000, 2048, 0.2, 64, True),
                                                (4, 2048, 1024, 0.4, 32, False),
                                                (2, 1001, 100, 0.3, 16, False),
+                                               (3, 1000, 99, 0.3, 16, False),   # one per wave
+                                               (8, 40000, 1024, 0.4, 32, True),
                                                (2, 500, 64, 0.05, 8, True)])
 def test_ball_query_bit_exact(cuda, B, N, M, r, S, uniform):
     from ov3d_amd import pointnet2_utils as pu
