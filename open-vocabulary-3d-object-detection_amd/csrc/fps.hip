@@ -222,30 +222,6 @@ __device__ __forceinline__ uint32_t spread3(uint32_t x) {  // 4 bits -> every 3r
 constexpr int kCells = 4096;
 constexpr int kMaxOutLDS = 8192;  // deferred outputs: M <= 8192 on the culled path
 
-// d[i] = fmaf(dz, dz, fmaf(dy, dy, dx * dx)) with (dx, dy, dz) = p[i] - c, for a lane's
-// PPT register slots: point pairs as packed f32 (v_pk_add / v_pk_mul / v_pk_fma, two
-// points per instruction; per element the same IEEE operations as the scalar form).
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-template <int PPT>
-__device__ __forceinline__ void point_dists(const float (&px)[PPT], const float (&py)[PPT],
-                                            const float (&pz)[PPT], float cx, float cy, float cz,
-                                            float (&d)[PPT]) {
-    const f32x2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
-#pragma unroll
-    for (int i = 0; i + 1 < PPT; i += 2) {
-        const f32x2 dx = f32x2{px[i], px[i + 1]} - c2x;
-        const f32x2 dy = f32x2{py[i], py[i + 1]} - c2y;
-        const f32x2 dz = f32x2{pz[i], pz[i + 1]} - c2z;
-        const f32x2 v = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
-        d[i] = v.x;
-        d[i + 1] = v.y;
-    }
-    if (PPT & 1) {
-        const float dx = px[PPT - 1] - cx, dy = py[PPT - 1] - cy, dz = pz[PPT - 1] - cz;
-        d[PPT - 1] = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-    }
-}
-
 template <int PPT>
 __global__ __launch_bounds__(kThreads) void fps_cull_kernel(const float* __restrict__ xyz, int N,
                                                             int M, int L,
@@ -416,11 +392,11 @@ __global__ __launch_bounds__(kThreads) void fps_cull_kernel(const float* __restr
             float best = -1.f;
             int bi = 0;
             float sx = 0.f, sy = 0.f, sz = 0.f;  // this lane's best point, carried along
-            float dd[PPT];
-            point_dists<PPT>(px, py, pz, x1, y1, z1, dd);
 #pragma unroll
             for (int i = 0; i < PPT; ++i) {
-                const float d2 = fminf(dd[i], td[i]);  // no NaN canonicalisation: built non-IEEE (Makefile)
+                const float dx = px[i] - x1, dy = py[i] - y1, dz = pz[i] - z1;
+                const float d = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                const float d2 = fminf(d, td[i]);  // no NaN canonicalisation: built non-IEEE (Makefile)
                 td[i] = d2;
                 const bool gt = d2 > best;
                 best = gt ? d2 : best;
