@@ -222,13 +222,15 @@ int ov3d_bn_bwd_stats_finalize(const double* partials, int nparts, int C, double
                                float* cA, float* cB, float* cC, float* dgamma, float* dbeta,
                                void* stream);
 /* pooled output (P,N) f32 = relu(scale*(scale >= 0 ? pmax : pmin) + shift), plus the
- * selected value / row for the backward */
+ * selected value / row for the backward.  seq_m = 0: out row p = b*M + m; seq_m = M > 0:
+ * out row m*B + b (sequence-first, the encoder's input layout; P % M == 0) */
 int ov3d_sa_pool_fwd(const float* pmax, const float* pmin, const uint8_t* imax,
                      const uint8_t* imin, const float* scale, const float* shift, int P, int N,
-                     float* out, float* ysel, uint8_t* isel, void* stream);
-/* pooled-gradient ReLU mask + BN-backward partials (sum g, sum g*xhat) */
+                     int seq_m, float* out, float* ysel, uint8_t* isel, void* stream);
+/* pooled-gradient ReLU mask + BN-backward partials (sum g, sum g*xhat); dout in the
+ * forward's output row order (seq_m) */
 int ov3d_sa_pool_bwd(const float* dout, const float* ysel, const float* scale, const float* shift,
-                     const float* mean, const float* invstd, int P, int N, float* gsel,
+                     const float* mean, const float* invstd, int P, int N, int seq_m, float* gsel,
                      double* partials, int nparts, void* stream);
 /* BN backward coefficients: dx = cA*g + cB*y + cC; dgamma, dbeta (may be NULL) */
 int ov3d_bn_bwd_finalize(const double* totals, double count, int C, const float* gamma,

@@ -38,8 +38,8 @@ _SIGS = {
     "ov3d_sa_layer_dy": "ppppiiiippppppip",
     "ov3d_reduce_partials": "piipp",
     "ov3d_bn_finalize": "pdippffpppppppp",
-    "ov3d_sa_pool_fwd": "ppppppiipppp",
-    "ov3d_sa_pool_bwd": "ppppppiippip",
+    "ov3d_sa_pool_fwd": "ppppppiiipppp",
+    "ov3d_sa_pool_bwd": "ppppppiiippip",
     "ov3d_bn_bwd_finalize": "pdippppppppp",
     "ov3d_bn_relu_bwd": "ippppppppppiippipp",
     "ov3d_bn_relu_bwd_cin": "ippppppppppiiippipp",

@@ -429,19 +429,26 @@ __global__ void bn_finalize_kernel(const double* __restrict__ totals, double cou
 }
 
 
+// pooled row p = b*M + m -> its output row: p itself, or m*B + b when the output is written
+// sequence-first (seq_m = M > 0: the encoder's (M, B, C) input layout, no transpose pass)
+__device__ __forceinline__ long long pool_out_row(long long p, int seq_m, long long nb) {
+    return seq_m > 0 ? (p % seq_m) * nb + p / seq_m : p;
+}
+
 // Pool: out = relu(a * (a >= 0 ? max : min) + b); remembers the value and row used.
 __global__ void sa_pool_fwd_kernel(const float* __restrict__ pmax, const float* __restrict__ pmin,
                                    const uint8_t* __restrict__ imax, const uint8_t* __restrict__ imin,
                                    const float* __restrict__ scale, const float* __restrict__ shift,
-                                   long long PN, int N, float* __restrict__ out,
-                                   float* __restrict__ ysel, uint8_t* __restrict__ isel) {
+                                   long long PN, int N, int seq_m, long long nb,
+                                   float* __restrict__ out, float* __restrict__ ysel,
+                                   uint8_t* __restrict__ isel) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= PN) return;
     const int n = (int)(i % N);
     const float a = scale[n];
     const bool up = a >= 0.f;
     const float y = up ? pmax[i] : pmin[i];
-    out[i] = relu_bn(a, y, shift[n]);
+    out[pool_out_row(i / N, seq_m, nb) * N + n] = relu_bn(a, y, shift[n]);
     ysel[i] = y;
     isel[i] = up ? imax[i] : imin[i];
 }
@@ -451,7 +458,7 @@ __global__ void sa_pool_fwd_kernel(const float* __restrict__ pmax, const float* 
 __global__ __launch_bounds__(kThreads) void sa_pool_bwd_kernel(
     const float* __restrict__ dout, const float* __restrict__ ysel, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ mean, const float* __restrict__ invstd,
-    int P, int N, float* __restrict__ gsel, double* __restrict__ partials) {
+    int P, int N, int seq_m, float* __restrict__ gsel, double* __restrict__ partials) {
     // thread: channel tid % N (N <= 256, 256 % N == 0), centroid phase tid / N
     __shared__ double red[2][kThreads];
     const int tid = threadIdx.x, n = tid % N, ph = tid / N, nph = kThreads / N;
@@ -461,7 +468,9 @@ __global__ __launch_bounds__(kThreads) void sa_pool_bwd_kernel(
     for (long long pi = (long long)blockIdx.x * nph + ph; pi < P; pi += (long long)gridDim.x * nph) {
         const long long i = pi * N + n;
         const float y = ysel[i];
-        const float g = fmaf(a, y, b) > 0.f ? dout[i] : 0.f;
+        const float g = fmaf(a, y, b) > 0.f
+                            ? dout[pool_out_row(pi, seq_m, seq_m > 0 ? P / seq_m : 0) * N + n]
+                            : 0.f;
         gsel[i] = g;
         s += g;
         q = fmaf(g, (y - mu) * is, q);
@@ -846,26 +855,30 @@ extern "C" int ov3d_bn_bwd_stats_finalize(const double* partials, int nparts, in
 
 extern "C" int ov3d_sa_pool_fwd(const float* pmax, const float* pmin, const uint8_t* imax,
                                 const uint8_t* imin, const float* scale, const float* shift, int P,
-                                int N, float* out, float* ysel, uint8_t* isel, void* stream) {
-    if (P < 0 || N <= 0 || !pmax || !pmin || !imax || !imin || !scale || !shift || !out || !ysel ||
-        !isel)
+                                int N, int seq_m, float* out, float* ysel, uint8_t* isel,
+                                void* stream) {
+    if (P < 0 || N <= 0 || seq_m < 0 || (seq_m > 0 && P % seq_m) || !pmax || !pmin || !imax ||
+        !imin || !scale || !shift || !out || !ysel || !isel)
         return OV3D_EINVAL;
     const long long PN = (long long)P * N;
     if (PN == 0) return OV3D_OK;
     hipLaunchKernelGGL(sa_pool_fwd_kernel, dim3(ov3d_cdiv(PN, 256)), dim3(256), 0, ov3d_stream(stream),
-                       pmax, pmin, imax, imin, scale, shift, PN, N, out, ysel, isel);
+                       pmax, pmin, imax, imin, scale, shift, PN, N, seq_m,
+                       seq_m > 0 ? (long long)(P / seq_m) : 0LL, out, ysel, isel);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }
 
 extern "C" int ov3d_sa_pool_bwd(const float* dout, const float* ysel, const float* scale,
                                 const float* shift, const float* mean, const float* invstd, int P,
-                                int N, float* gsel, double* partials, int nparts, void* stream) {
-    if (P < 0 || N <= 0 || N > kThreads || kThreads % N || nparts <= 0 || !dout || !ysel || !scale ||
-        !shift || !mean || !invstd || !gsel || !partials)
+                                int N, int seq_m, float* gsel, double* partials, int nparts,
+                                void* stream) {
+    if (P < 0 || N <= 0 || N > kThreads || kThreads % N || nparts <= 0 || seq_m < 0 ||
+        (seq_m > 0 && P % seq_m) || !dout || !ysel || !scale || !shift || !mean || !invstd ||
+        !gsel || !partials)
         return OV3D_EINVAL;
     hipLaunchKernelGGL(sa_pool_bwd_kernel, dim3(nparts), dim3(kThreads), 0, ov3d_stream(stream), dout,
-                       ysel, scale, shift, mean, invstd, P, N, gsel, partials);
+                       ysel, scale, shift, mean, invstd, P, N, seq_m, gsel, partials);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

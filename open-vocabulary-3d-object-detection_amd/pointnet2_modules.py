@@ -118,6 +118,10 @@ class _NbrMax(torch.autograd.Function):
         return dy, None
 
 
+# fused SA output stored sequence-first (the pool kernel's seq_m); False: (B, M, C) rows
+SEQ_FIRST_OUT = True
+
+
 class PointnetSAModuleVotes(nn.Module):
     """Set abstraction: FPS -> ball query -> group (+xyz, /radius) -> SharedMLP -> max over nsample."""
 
@@ -160,7 +164,12 @@ class PointnetSAModuleVotes(nn.Module):
         B, M, S, C = g.shape
         rows = g.view(B * M * S, C)
         if self.training and sa_fused.supported(self.mlp_module, rows, S):
-            # training under bf16 autocast: fused MFMA kernels (sa_fused.py)
+            # training under bf16 autocast: fused MFMA kernels (sa_fused.py); the pool kernel
+            # writes the rows sequence-first (M, B, C), the encoder's input layout, and this
+            # returns the (B, M, C) view of them (same values, no transpose pass either way)
+            if SEQ_FIRST_OUT:
+                return sa_fused.sa_mlp_pool(self.mlp_module, rows, S, seq_m=M).view(
+                    M, B, -1).transpose(0, 1)
             return sa_fused.sa_mlp_pool(self.mlp_module, rows, S).view(B, M, -1)
         y = self.mlp_module.rows(rows)
         # == F.max_pool2d(kernel [1, nsample]) of the reference

@@ -150,7 +150,7 @@ def _bwd_coefs(tot, count, gamma, mean, invstd, C):
 
 class _SAMLPPool(Function):
     @staticmethod
-    def forward(ctx, x0, w1, w2, w3, g1, b1, g2, b2, g3, b3, bns, S):
+    def forward(ctx, x0, w1, w2, w3, g1, b1, g2, b2, g3, b3, bns, S, seq_m=0):
         dev = x0.device
         R, cin = x0.shape
         P = R // S
@@ -195,25 +195,26 @@ class _SAMLPPool(Function):
         out = torch.empty((P, c3), dtype=torch.float32, device=dev)
         ysel = torch.empty((P, c3), dtype=torch.float32, device=dev)
         isel = torch.empty((P, c3), dtype=torch.uint8, device=dev)
-        nat.call("ov3d_sa_pool_fwd", pmax, pmin, imax, imin, st3[2], st3[3], P, c3, out, ysel, isel,
-                 like=x0)
+        nat.call("ov3d_sa_pool_fwd", pmax, pmin, imax, imin, st3[2], st3[3], P, c3, seq_m, out, ysel,
+                 isel, like=x0)
         ctx.save_for_backward(x0, y1, z1, y2, z2, w2b, w3b, g1, g2, g3, ysel, isel, w1f, *st1, *st2,
                               *st3)
-        ctx.meta = (R, S, P, c1, c2, c3, groups, world, tuple(w1.shape), fused_bwd, fused_bwd2)
+        ctx.meta = (R, S, P, c1, c2, c3, groups, world, tuple(w1.shape), fused_bwd, fused_bwd2,
+                    seq_m)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         (x0, y1, z1, y2, z2, w2b, w3b, g1, g2, g3, ysel, isel, w1f,
          m1, i1, a1, s1, m2, i2, a2, s2, m3, i3, a3, s3) = ctx.saved_tensors
-        R, S, P, c1, c2, c3, groups, world, w1shape, fused_bwd, fused_bwd2 = ctx.meta
+        R, S, P, c1, c2, c3, groups, world, w1shape, fused_bwd, fused_bwd2, seq_m = ctx.meta
         dev = x0.device
         bf = torch.bfloat16
         dout = dout.float().contiguous()
         # layer 3: pooled gradient -> BN backward coefficients -> dy3 (recomputed y3)
         gsel = torch.empty((P, c3), dtype=torch.float32, device=dev)
         parts = torch.empty((NPARTS_POOL, 2, c3), dtype=torch.float64, device=dev)
-        nat.call("ov3d_sa_pool_bwd", dout, ysel, a3, s3, m3, i3, P, c3, gsel, parts, NPARTS_POOL,
+        nat.call("ov3d_sa_pool_bwd", dout, ysel, a3, s3, m3, i3, P, c3, seq_m, gsel, parts, NPARTS_POOL,
                  like=dout)
         cA, cB, cC, dg3, db3 = bn_bwd_affine(parts, NPARTS_POOL, c3, groups[2], R * world[2], g3,
                                              m3, i3)
@@ -276,15 +277,16 @@ class _SAMLPPool(Function):
                  parts, None, NPARTS_ROWS, w1f, like=dout)
         dw1 = _totals(parts, NPARTS_ROWS, cin * c1, None).view(c1, cin).float().view(w1shape)
         return (None, dw1, dw2.view(c2, c1), dw3.view(c3, c2), dg1, db1, dg2, db2, dg3, db3, None,
-                None)
+                None, None)
 
 
-def sa_mlp_pool(mlp, x0, S):
+def sa_mlp_pool(mlp, x0, S, seq_m=0):
     """(R, 3) grouped xyz rows (or (R, 6) xyz + colour) -> (R / S, C3) pooled features
-    (fp32), fused training path."""
+    (fp32), fused training path.  seq_m = M (centroids per scene): rows in (m, b) order,
+    the encoder's sequence-first layout, written by the pool kernel directly."""
     layers = list(mlp)
     ws = [l.conv.weight for l in layers]
     ws = [w.view(w.shape[0], w.shape[1]) for w in ws]
     bns = tuple(_bn(l) for l in layers)
     return _SAMLPPool.apply(x0, ws[0], ws[1], ws[2], bns[0].weight, bns[0].bias, bns[1].weight,
-                            bns[1].bias, bns[2].weight, bns[2].bias, bns, S)
+                            bns[1].bias, bns[2].weight, bns[2].bias, bns, S, seq_m)

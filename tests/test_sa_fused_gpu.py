@@ -220,7 +220,7 @@ def test_sa_rows_bn_relu_path_vs_fp32(cuda, monkeypatch, kind):
         calls, fcalls = [], []
         real, freal = heads.bn_relu_rows, sa_fused.sa_mlp_pool
         monkeypatch.setattr(heads, "bn_relu_rows", lambda *a, **k: calls.append(1) or real(*a, **k))
-        monkeypatch.setattr(sa_fused, "sa_mlp_pool", lambda *a: fcalls.append(1) or freal(*a))
+        monkeypatch.setattr(sa_fused, "sa_mlp_pool", lambda *a, **k: fcalls.append(1) or freal(*a, **k))
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
             _, f, _ = twin(xyz, feats)
         monkeypatch.undo()
