@@ -221,6 +221,9 @@ int ov3d_bn_bwd_stats_finalize(const double* partials, int nparts, int C, double
                                const float* gamma, const float* mean, const float* invstd,
                                float* cA, float* cB, float* cC, float* dgamma, float* dbeta,
                                void* stream);
+/* out[c] = sum over the nparts rows of parts (nparts, width) f32, fixed order (the fused SA
+ * backward's per-workgroup dW partials; replaces torch's part.sum(0) in sa_fused.py) */
+int ov3d_colsum_f32(const float* parts, int nparts, int width, float* out, void* stream);
 /* pooled output (P,N) f32 = relu(scale*(scale >= 0 ? pmax : pmin) + shift), plus the
  * selected value / row for the backward.  seq_m = 0: out row p = b*M + m; seq_m = M > 0:
  * out row m*B + b (sequence-first, the encoder's input layout; P % M == 0) */

@@ -37,6 +37,7 @@ _SIGS = {
     "ov3d_sa_layer_pool_fwd": "ppppiiiippppppip",
     "ov3d_sa_layer_dy": "ppppiiiippppppip",
     "ov3d_reduce_partials": "piipp",
+    "ov3d_colsum_f32": "piipp",
     "ov3d_bn_finalize": "pdippffpppppppp",
     "ov3d_sa_pool_fwd": "ppppppiiipppp",
     "ov3d_sa_pool_bwd": "ppppppiiippip",

@@ -387,6 +387,38 @@ __global__ __launch_bounds__(1024) void reduce_partials_kernel(const double* __r
     if (pl == 0 && c < width) totals[c] = t;
 }
 
+// f32 column sums of (nparts, width) partials (the SA backward's per-workgroup dW partials):
+// 64 lanes x V columns per 512-thread block, the 8 waves take every 8th part with 8 loads in
+// flight, then the waves' sums are added in a fixed order (deterministic; replaces a torch
+// sum(0) whose few blocks each walked all parts)
+template <int V>
+__global__ __launch_bounds__(512) void colsum_f32_kernel(const float* __restrict__ parts,
+                                                         int nparts, int width,
+                                                         float* __restrict__ out) {
+    typedef float fv __attribute__((ext_vector_type(V)));
+    __shared__ fv red[8][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long long c0 = ((long long)blockIdx.x * 64 + lane) * V;
+    const bool ok = c0 < width;
+    fv a[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] = (fv)0.f;
+    int r = w;
+    if (ok) {
+        for (; r + 56 < nparts; r += 64) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                a[u] += *reinterpret_cast<const fv*>(parts + (size_t)(r + 8 * u) * width + c0);
+        }
+        for (; r < nparts; r += 8) a[0] += *reinterpret_cast<const fv*>(parts + (size_t)r * width + c0);
+    }
+    red[w][lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    __syncthreads();
+    if (w == 0 && ok)
+        *reinterpret_cast<fv*>(out + c0) = ((red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane])) +
+                                           ((red[4][lane] + red[5][lane]) + (red[6][lane] + red[7][lane]));
+}
+
 // sum / sum of squares of channel c over `count` rows -> mean, invstd, scale, shift (and the
 // running statistics)
 __device__ __forceinline__ void bn_finalize_one(int c, double tsum, double tsq, double count,
@@ -849,6 +881,25 @@ extern "C" int ov3d_bn_bwd_stats_finalize(const double* partials, int nparts, in
     hipLaunchKernelGGL(bn_bwd_stats_finalize_kernel, dim3(ov3d_cdiv(C, kColW)), dim3(1024), 0,
                        ov3d_stream(stream), partials, nparts, C, count, gamma, mean, invstd, cA, cB,
                        cC, dgamma, dbeta);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_colsum_f32(const float* parts, int nparts, int width, float* out,
+                               void* stream) {
+    if (nparts <= 0 || width <= 0 || !parts || !out) return OV3D_EINVAL;
+    const bool al16 = reinterpret_cast<uintptr_t>(parts) % 16 == 0 &&
+                      reinterpret_cast<uintptr_t>(out) % 16 == 0;
+    const bool al8 = reinterpret_cast<uintptr_t>(parts) % 8 == 0 &&
+                     reinterpret_cast<uintptr_t>(out) % 8 == 0;
+    // widest vector that still gives >= 256 blocks (one per CU), when the width allows it
+    const int v = (al16 && width % 4 == 0 && width >= 4 * 64 * 256) ? 4
+                : (al8 && width % 2 == 0 && width >= 2 * 64 * 256) ? 2 : 1;
+    hipStream_t s = ov3d_stream(stream);
+    const int blocks = ov3d_cdiv(width, 64 * v);
+    if (v == 4) hipLaunchKernelGGL(colsum_f32_kernel<4>, dim3(blocks), dim3(512), 0, s, parts, nparts, width, out);
+    else if (v == 2) hipLaunchKernelGGL(colsum_f32_kernel<2>, dim3(blocks), dim3(512), 0, s, parts, nparts, width, out);
+    else hipLaunchKernelGGL(colsum_f32_kernel<1>, dim3(blocks), dim3(512), 0, s, parts, nparts, width, out);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

@@ -86,6 +86,13 @@ def supported(mlp, x0, S):
             and all(c % 8 == 0 and 256 % (c // 8) == 0 for c in (c1, c2)))
 
 
+def _colsum(part):
+    """(nparts, ...) f32 partials -> their sum over dim 0 (ov3d_colsum_f32, fixed order)"""
+    out = torch.empty(part.shape[1:], dtype=torch.float32, device=part.device)
+    nat.call("ov3d_colsum_f32", part, part.shape[0], out.numel(), out, like=part)
+    return out
+
+
 def _totals(partials, nparts, width, group):
     tot = torch.empty(width, dtype=torch.float64, device=partials.device)
     nat.call("ov3d_reduce_partials", partials, nparts, width, tot, like=partials)
@@ -228,7 +235,7 @@ class _SAMLPPool(Function):
                 if FUSED_STATS else None
             nat.call("ov3d_sa_dy_fused", y2, a2, s2, w3b, R, c2, c3, S, gsel, isel, cA, cB, cC, dz2,
                      part, m2, i2, parts2, nwg, like=dout)
-            dw3 = part.sum(0)
+            dw3 = _colsum(part)
             del part
         else:
             dy3 = torch.empty((R, c3), dtype=bf, device=dev)
@@ -255,7 +262,7 @@ class _SAMLPPool(Function):
                 2 * nwg2
             nat.call("ov3d_sa_dy2_fused", y1, x0, w1f, a1, s1, y2, a2, s2, dz2, cA, cB, cC, w2b, m1,
                      i1, R, c1, c2, dz1, part, parts, nwg2, like=dout)
-            dw2 = part.sum(0)
+            dw2 = _colsum(part)
             del dz2, part
         else:
             dy2 = torch.empty((R, c2), dtype=bf, device=dev)

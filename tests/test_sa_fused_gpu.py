@@ -265,3 +265,18 @@ def test_neighbour_max_pool_kernel(cuda, S, C):
     exp = torch.zeros(P, S, C, dtype=torch.bfloat16)
     exp.scatter_(1, torch.from_numpy(first).long()[:, None, :], gout.cpu()[:, None, :])
     assert torch.equal(y.grad.cpu(), exp.view(P * S, C))
+
+
+@pytest.mark.parametrize("nparts,shape", [(256, (256, 128)), (256, (128, 64)), (37, (3, 5)),
+                                          (1, (1000,)), (200, (64, 1024))])
+def test_colsum_f32_equals_torch_sum(cuda, nparts, shape):
+    """ov3d_colsum_f32 (the fused SA backward's dW partial sums) == part.sum(0) up to the
+    summation order (f32); deterministic across calls."""
+    from ov3d_amd import sa_fused
+    g = torch.Generator(device="cpu").manual_seed(nparts)
+    part = torch.randn((nparts,) + shape, generator=g).to(cuda)
+    got = sa_fused._colsum(part)
+    ref = part.double().sum(0).float()
+    assert got.shape == ref.shape
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5 * nparts ** 0.5)
+    assert torch.equal(got, sa_fused._colsum(part))
