@@ -679,8 +679,10 @@ int ov3d_tile_gemm(int M, int N, int K, const void* A, long long lda, const void
  * Entry points, in stream order:
  *   ov3d_sun_aug_points : flip / rotz / scale of the points (sunrgbd.py:309-344) ->
  *                         out (B, n_max, 3) T and range_part (B, ov3d_sun_range_parts(n_max), 6)
- *   ov3d_sun_aug_boxes  : support-class filter (train, sunrgbd.py:268-270; n_support = 0 for
- *                         val) + the same transforms of the boxes -> out (B, k_max, 8), out_n
+ *   ov3d_sun_aug_boxes  : support-class filter (train, sunrgbd.py:266-268; n_support = 0 for
+ *                         val) of each scene's first ngt[b] boxes (ngt NULL: all of them; the
+ *                         rest are use_pbox pseudo boxes, appended unfiltered, :269-271) + the
+ *                         same transforms of the boxes -> out (B, k_max, 8), out_n
  *   ov3d_sun_cuboid_eval: all A attempts of RandomCuboid (min_points, box filter "center"),
  *                         counts / accept (B, A), crop_mm (B, A, 6) T, and
  *                         sel (B, 2) int32 = [first accepted attempt or -1, points to sample]
@@ -694,9 +696,9 @@ int ov3d_sun_aug_points(const void* raw, int pc_f64, long long raw_stride, int r
                         const double* params, int augment, void* out, void* range_part,
                         void* stream);
 int ov3d_sun_aug_boxes(const double* raw, long long k_stride, const int32_t* scene_idx,
-                       const int32_t* nbox, int B, int k_max, const double* params, int augment,
-                       const double* support, int n_support, double* out, int32_t* out_n,
-                       void* stream);
+                       const int32_t* nbox, const int32_t* ngt, int B, int k_max,
+                       const double* params, int augment, const double* support, int n_support,
+                       double* out, int32_t* out_n, void* stream);
 int ov3d_sun_cuboid_eval(const void* pts, int pc_f64, int n_max, const int32_t* npts,
                          const void* range_part, const double* attempts, int B, int A,
                          int min_points, const double* boxes, const int32_t* nbox, int k_max,

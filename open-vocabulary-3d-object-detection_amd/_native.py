@@ -89,7 +89,7 @@ _SIGS = {
     "ov3d_rows_gemm_group": "iipip",
     "ov3d_tile_gemm": "iiiplplipplp",
     "ov3d_sun_aug_points": "pilippiipippp",
-    "ov3d_sun_aug_boxes": "plppiipipippp",
+    "ov3d_sun_aug_boxes": "plpppiipipippp",
     "ov3d_sun_cuboid_eval": "piipppiiippippppp",
     "ov3d_sun_crop_sample": "piipppiippipppp",
     "ov3d_sun_labels": "pip",
@@ -228,9 +228,32 @@ def timing_collect():
     return out
 
 
+# Optional launch census (tests): the set of entry points called while enabled.
+_CALLED = None
+
+
+def census_start():
+    global _CALLED
+    _CALLED = {}
+
+
+def census_stop():
+    """-> {entry point: number of calls} since census_start()"""
+    global _CALLED
+    out, _CALLED = _CALLED or {}, None
+    return out
+
+
+def note(name):
+    """count a launch made without call() (census)"""
+    if _CALLED is not None:
+        _CALLED[name] = _CALLED.get(name, 0) + 1
+
+
 def call(name, *args, like):
     """Invoke `name` with args (+ the current stream of `like`); raise on nonzero status."""
     fn = getattr(load(), name)
+    note(name)
     conv = []
     for a in args:
         if isinstance(a, torch.Tensor) or a is None:

@@ -29,6 +29,11 @@ import torch
 from . import _native as nat
 from . import nms as _nms
 
+# ov3d_ap_match limits (csrc/evaldet.hip): proposals walked per (scene, class), and the
+# per-scene "detected" flags of the GT boxes in one 64-bit word
+AP_MAX_PROPOSALS = 256
+AP_MAX_GT = 64
+
 
 def get_ap_config_dict(remove_empty_box=True, use_3d_nms=True, nms_iou=0.25, use_old_type_nms=False,
                        cls_nms=True, per_class_proposal=True, use_cls_confidence_only=False,
@@ -128,6 +133,11 @@ def eval_det_device(scores, corners, gt_corners, gt_cls, gt_present, ovthresh_li
     threshold, {class: (ap, rec_last)} in the reference's gt.keys() order, plus the npos."""
     S, K, C = scores.shape
     G = gt_corners.shape[1]
+    if K > AP_MAX_PROPOSALS or G > AP_MAX_GT:
+        # ov3d_ap_match keeps one 64-bit "detected" word per GT block and walks <= 256
+        # proposals per (scene, class) thread
+        raise ValueError(f"device AP supports <= {AP_MAX_PROPOSALS} proposals and <= {AP_MAX_GT} "
+                         f"GT boxes per scene (got K={K}, G={G}); nqueries / max_num_obj too large")
     dev = scores.device
     det = torch.isfinite(scores)
     pvalid = det.any(-1).to(torch.uint8).contiguous()

@@ -79,6 +79,7 @@ def flush_kv_grads(dk_buf):
                                           HEAD_DIM ** -0.5, p, _native._stream(lst[0][1][0]))
         if rc:
             raise _native.NativeError(f"ov3d_attn_bwd_dkdv_batch failed with status {rc}")
+        _native.note("ov3d_attn_bwd_dkdv_batch")
 
 
 def new_site():
@@ -199,6 +200,7 @@ class _Attention(torch.autograd.Function):
                 _native._stream(q))
         if rc:
             raise _native.NativeError(f"ov3d_attn_fwd failed with status {rc}")
+        _native.note("ov3d_attn_fwd_masked")
         ctx.save_for_backward(*srcs, o, lse, bits, mw)
         ctx.meta = (spec, dims, H, float(dropout_p), site, len(srcs))
         ctx.ext = ext
@@ -240,6 +242,7 @@ class _Attention(torch.autograd.Function):
             _native._stream(q))
         if rc:
             raise _native.NativeError(f"ov3d_attn_bwd failed with status {rc}")
+        _native.note("ov3d_attn_bwd_masked")
         if defer:
             job = _DkdvJob(qp, sq, kp, sk, vp, sv, _native._ptr(do), E, _native._ptr(lse),
                            _native._ptr(dvec), _native._ptr(bits) if p > 0 else 0,

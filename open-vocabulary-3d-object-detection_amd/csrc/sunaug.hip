@@ -117,16 +117,19 @@ __device__ __forceinline__ void scene_range(const T* __restrict__ part, int b, i
 }
 
 // ---------------------------------------------------------------------------
-// (2) boxes: train-split support-class filter (sunrgbd.py:268-270, np.isin on the
-//     class column), then the same flip / rotation / scale (sunrgbd.py:311-343).
+// (2) boxes: train-split support-class filter (sunrgbd.py:266-268, np.isin on the
+//     class column) of the first ngt boxes -- the GT boxes; boxes past them are the
+//     use_pbox pseudo boxes, appended after the filter (sunrgbd.py:269-271) and never
+//     filtered -- then the same flip / rotation / scale (sunrgbd.py:302-343).
 //     One workgroup per scene; order-preserving compaction.
 __global__ __launch_bounds__(kAugThreads) void aug_boxes_kernel(
     const double* __restrict__ raw, long long k_stride, const int32_t* __restrict__ sidx,
-    const int32_t* __restrict__ nbox, int k_max, const double* __restrict__ params, int augment,
-    const double* __restrict__ support, int n_support, double* __restrict__ out,
-    int32_t* __restrict__ out_n) {
+    const int32_t* __restrict__ nbox, const int32_t* __restrict__ ngt, int k_max,
+    const double* __restrict__ params, int augment, const double* __restrict__ support,
+    int n_support, double* __restrict__ out, int32_t* __restrict__ out_n) {
     const int b = blockIdx.x;
     const int k = nbox[b];
+    const int kf = ngt ? ngt[b] : k;     // boxes the support filter applies to
     const double* src = raw + (long long)sidx[b] * k_stride * 8;
     double* dst = out + (long long)b * k_max * 8;
     const double* P = params + b * 8;
@@ -138,7 +141,7 @@ __global__ __launch_bounds__(kAugThreads) void aug_boxes_kernel(
     for (int c0 = 0; c0 < k; c0 += kAugThreads) {
         const int i = c0 + threadIdx.x;
         bool keep = i < k;
-        if (keep && n_support > 0) {
+        if (keep && n_support > 0 && i < kf) {
             const double cls = src[(long long)i * 8 + 7];
             bool hit = false;
             for (int q = 0; q < n_support; ++q) hit |= cls == support[q];
@@ -530,16 +533,16 @@ extern "C" int ov3d_sun_aug_points(const void* raw, int pc_f64, long long raw_st
 extern "C" int ov3d_sun_range_parts(int n) { return (n + kAugThreads - 1) / kAugThreads; }
 
 extern "C" int ov3d_sun_aug_boxes(const double* raw, long long k_stride, const int32_t* scene_idx,
-                                  const int32_t* nbox, int B, int k_max, const double* params,
-                                  int augment, const double* support, int n_support, double* out,
-                                  int32_t* out_n, void* stream) {
+                                  const int32_t* nbox, const int32_t* ngt, int B, int k_max,
+                                  const double* params, int augment, const double* support,
+                                  int n_support, double* out, int32_t* out_n, void* stream) {
     if (!raw || !scene_idx || !nbox || !params || !out || !out_n || B < 0 || k_max <= 0 ||
         k_stride <= 0 || n_support < 0 || (n_support > 0 && !support))
         return OV3D_EINVAL;
     if (B == 0) return OV3D_OK;
     hipLaunchKernelGGL(aug_boxes_kernel, dim3(B), dim3(kAugThreads), 0, ov3d_stream(stream), raw,
-                       k_stride, scene_idx, nbox, k_max, params, augment, support, n_support, out,
-                       out_n);
+                       k_stride, scene_idx, nbox, ngt, k_max, params, augment, support, n_support,
+                       out, out_n);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

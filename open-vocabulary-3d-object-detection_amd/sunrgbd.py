@@ -22,7 +22,11 @@ scene: per batch and chunk).
 
 Scope: use_color / use_height are rejected as in practice by the reference (use_color
 fails in scale_points' broadcast at sunrgbd.py:407-410; use_height is never passed by
-build_dataset).  use_image / use_pbox / use_2d_feature: the extra arrays pass through.
+build_dataset).  use_pbox: the pseudo boxes are appended after the support-class filter of the
+GT boxes, unfiltered (sunrgbd.py:266-271).  use_image: image (B, MAX_NUM_PIXEL*3) float32
+zero-padded, image_height / image_width, calib_Rtilt / calib_K (sunrgbd.py:275-285, 456-461);
+the images are kept resident as read (uint8 from a JPEG decoder).  use_2d_feature: feature_2d
+(sunrgbd.py:272-273, 454-455).
 """
 import os
 
@@ -32,14 +36,36 @@ import torch
 from . import _native as nat
 
 MAX_ATTEMPTS = 100   # random_cuboid.py:43
+MAX_NUM_PIXEL = 530 * 730   # sunrgbd.py:47
+RAW_DATA_PATH = "/share/suzhengyuan/code/ScanRefer-3DVG/votenet/sunrgbd/sunrgbd_trainval"  # :42
+
+
+def read_image_cv2(path):
+    """the reference's image read (sunrgbd.py:281: np.array(cv2.imread(path)), BGR uint8)"""
+    try:
+        import cv2
+    except ImportError as e:   # not in this image; pass image_reader= to the dataset
+        raise ImportError("use_image needs cv2 (absent here): pass image_reader=") from e
+    return np.array(cv2.imread(path))
+
+
+def read_calib(path):
+    """sunrgbd.py:277-279: two lines of 9 floats, column-major 3x3 (Rtilt, K)"""
+    with open(path) as f:
+        lines = f.readlines()
+    rt = np.reshape(np.array([float(x) for x in lines[0].rstrip().split(" ")]), (3, 3), "F")
+    k = np.reshape(np.array([float(x) for x in lines[1].rstrip().split(" ")]), (3, 3), "F")
+    return rt, k
 
 
 class SceneStore:
     """Raw scans resident in device memory: points (S, n_max, 3) of the scans' dtype and
     boxes (S, k_max, 8) float64, with per-scan counts."""
 
-    def __init__(self, scans, device):
-        pcs, boxes = zip(*scans)
+    def __init__(self, scans, device, extras=None):
+        pcs, boxes = [s[0] for s in scans], [s[1] for s in scans]
+        # boxes past the first ngt are use_pbox pseudo boxes (never support-filtered)
+        self.ngt = np.array([s[2] if len(s) > 2 else s[1].shape[0] for s in scans], np.int32)
         dt = pcs[0].dtype
         if any(p.dtype != dt for p in pcs) or dt not in (np.float32, np.float64):
             raise TypeError("scans must share one float32 / float64 point dtype")
@@ -51,7 +77,7 @@ class SceneStore:
         S = len(pcs)
         pts = np.zeros((S, self.n_max, 3), dt)
         bx = np.zeros((S, self.k_max, 8), np.float64)
-        for i, (p, b) in enumerate(scans):
+        for i, (p, b) in enumerate(zip(pcs, boxes)):
             pts[i, : p.shape[0]] = p[:, 0:3]
             bx[i, : b.shape[0]] = b
         self.device = torch.device(device)
@@ -59,6 +85,32 @@ class SceneStore:
         self.boxes = torch.as_tensor(bx).to(self.device)
         self.n_dev = torch.as_tensor(self.n).to(self.device)
         self.k_dev = torch.as_tensor(self.k).to(self.device)
+        self.ngt_dev = torch.as_tensor(self.ngt).to(self.device)
+        self.extras = {}
+        if extras:
+            self._stack_extras(extras)
+
+    def _stack_extras(self, extras):
+        """per-scan dicts of image (H, W, 3) / calib_Rtilt / calib_K / feature_2d ->
+        resident tensors: images flattened and zero-padded to MAX_NUM_PIXEL * 3 in their
+        read dtype (the float32 conversion happens per batch, exactly as full_img_1d's)"""
+        dev = self.device
+        if "image" in extras[0]:
+            imgs = [np.asarray(e["image"]) for e in extras]
+            dt = imgs[0].dtype if all(i.dtype == imgs[0].dtype for i in imgs) else np.float32
+            flat = np.zeros((len(imgs), MAX_NUM_PIXEL * 3), dt)
+            for i, im in enumerate(imgs):
+                if im.size > MAX_NUM_PIXEL * 3:
+                    raise ValueError("image larger than MAX_NUM_PIXEL (sunrgbd.py:284-285)")
+                flat[i, : im.size] = im.reshape(-1)
+            self.extras["image"] = torch.as_tensor(flat).to(dev)
+            self.extras["image_height"] = torch.as_tensor(np.array([i.shape[0] for i in imgs], np.int64)).to(dev)
+            self.extras["image_width"] = torch.as_tensor(np.array([i.shape[1] for i in imgs], np.int64)).to(dev)
+            for k in ("calib_Rtilt", "calib_K"):
+                self.extras[k] = torch.as_tensor(np.stack([np.asarray(e[k], np.float64)
+                                                           for e in extras])).to(dev)
+        if "feature_2d" in extras[0]:
+            self.extras["feature_2d"] = torch.as_tensor(np.stack([e["feature_2d"] for e in extras])).to(dev)
 
 
 class SunrgbdDetectionDataset:
@@ -71,7 +123,8 @@ class SunrgbdDetectionDataset:
                  pseudo_box_dir=None, feature_2d_dir=None, num_points=20000, use_color=False,
                  use_image=False, use_height=False, use_v1=True, augment=False,
                  use_random_cuboid=True, random_cuboid_min_points=30000, use_pbox=False,
-                 use_2d_feature=False, device="cuda", scans=None):
+                 use_2d_feature=False, device="cuda", scans=None, extras=None,
+                 raw_data_path=RAW_DATA_PATH, image_reader=read_image_cv2):
         assert num_points <= 50000
         assert split_set in ["train", "val", "trainval"]
         if use_color:
@@ -88,11 +141,17 @@ class SunrgbdDetectionDataset:
         self.aspect, self.min_crop, self.max_crop = 0.75, 0.75, 1.0   # sunrgbd.py:234-239
         self.max_num_obj = 64
         self.train = split_set == "train"
+        self.use_2d_feature = use_2d_feature
         if scans is None:
             scans, self.scan_names = self._read(root_dir, split_set, use_pbox, pseudo_box_dir)
+            if use_image or use_2d_feature:
+                extras = [self._read_extras(n, use_image, use_2d_feature, raw_data_path,
+                                            feature_2d_dir, image_reader) for n in self.scan_names]
         else:
             self.scan_names = [f"{i:06d}" for i in range(len(scans))]
-        self.store = SceneStore(scans, device)
+        if (use_image or use_2d_feature) and not extras:
+            raise ValueError("use_image / use_2d_feature: no images / features (extras=)")
+        self.store = SceneStore(scans, device, extras)
         sup = np.asarray(dataset_config.support_class, np.float64) if self.train else np.zeros(0)
         self._support = torch.as_tensor(sup).to(self.store.device)
 
@@ -110,11 +169,23 @@ class SunrgbdDetectionDataset:
         for p in paths:
             pc = np.load(p + "_pc.npz")["pc"]
             bb = np.load(p + "_bbox.npy")
+            ngt = bb.shape[0]
             if use_pbox:
                 bb = np.concatenate([bb, np.load(os.path.join(pseudo_box_dir, os.path.basename(p))
                                                  + "_bbox.npy")], 0)
-            scans.append((pc[:, 0:3], bb))
+            scans.append((pc[:, 0:3], bb, ngt))
         return scans, [os.path.basename(p) for p in paths]
+
+    @staticmethod
+    def _read_extras(name, use_image, use_2d_feature, raw_data_path, feature_2d_dir, reader):
+        """sunrgbd.py:272-285 for one scan"""
+        e = {}
+        if use_2d_feature:
+            e["feature_2d"] = np.load(os.path.join(feature_2d_dir, name) + ".npy")
+        if use_image:
+            e["calib_Rtilt"], e["calib_K"] = read_calib(os.path.join(raw_data_path, "calib", name + ".txt"))
+            e["image"] = reader(os.path.join(raw_data_path, "image", name + ".jpg"))
+        return e
 
     def __len__(self):
         return len(self.scan_names)
@@ -164,6 +235,7 @@ class SunrgbdDetectionDataset:
         idx = torch.as_tensor(np.asarray(indices, np.int32)).to(dev)
         npts = st.n_dev[idx.long()].contiguous()
         nbox = st.k_dev[idx.long()].contiguous()
+        ngt = st.ngt_dev[idx.long()].contiguous()
         n_host = st.n[np.asarray(indices)]
         T = torch.float64 if st.pc_f64 else torch.float32
         nparts = nat.load().ov3d_sun_range_parts(st.n_max)
@@ -186,9 +258,9 @@ class SunrgbdDetectionDataset:
             nat.call("ov3d_sun_aug_points", st.points, st.pc_f64, st.n_max, 3, idx[lo:hi],
                      npts[lo:hi], hi - lo, st.n_max, p, int(self.augment), pts[lo:hi],
                      rpart[lo:hi], like=pts)
-            nat.call("ov3d_sun_aug_boxes", st.boxes, st.k_max, idx[lo:hi], nbox[lo:hi], hi - lo,
-                     st.k_max, p, int(self.augment), self._support, int(self._support.numel()),
-                     boxes[lo:hi], nbox_aug[lo:hi], like=pts)
+            nat.call("ov3d_sun_aug_boxes", st.boxes, st.k_max, idx[lo:hi], nbox[lo:hi],
+                     ngt[lo:hi], hi - lo, st.k_max, p, int(self.augment), self._support,
+                     int(self._support.numel()), boxes[lo:hi], nbox_aug[lo:hi], like=pts)
             return p
 
         def launch_cuboid(lo, hi):
@@ -293,6 +365,9 @@ class SunrgbdDetectionDataset:
             angles=out["gt_box_angles"].data_ptr(), angle_cls=out["gt_angle_class_label"].data_ptr(),
             angle_res=out["gt_angle_residual_label"].data_ptr())
         nat.call("ov3d_sun_labels", nat.byref(args), st.pc_f64, like=pts)
+        li = idx.long()
+        for k, v in st.extras.items():
+            out[k] = v[li].float() if k == "image" else v[li]
         return out
 
     def __getitem__(self, idx):

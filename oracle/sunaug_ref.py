@@ -85,12 +85,15 @@ def _corners_camera(sizes, angles, centers):
 
 
 def sun_item(pc, boxes, rng, support_class=None, augment=True, use_cuboid=True,
-             min_points=30000, num_points=20000, nbin=12, G=64):
-    """one reference __getitem__ -> dict (numpy).  pc (N, 3) float32|float64, boxes (K, 8)."""
+             min_points=30000, num_points=20000, nbin=12, G=64, pseudo_boxes=None):
+    """one reference __getitem__ -> dict (numpy).  pc (N, 3) float32|float64, boxes (K, 8);
+    pseudo_boxes (use_pbox): appended after the support filter (sunrgbd.py:266-271)."""
     pc = pc[:, 0:3].copy()
     boxes = boxes.copy()
     if support_class is not None:
         boxes = boxes[np.isin(boxes[:, -1], support_class)]
+    if pseudo_boxes is not None:
+        boxes = np.concatenate([boxes, pseudo_boxes], axis=0)
     if augment:
         if rng.random() > 0.5:
             pc[:, 0] = -1 * pc[:, 0]

@@ -20,7 +20,7 @@ class FakeRegionCLIP:
         feats = []
         for d in batch:
             inst = d["instances"]
-            boxes = inst.gt_boxes.tensor.float()
+            boxes = inst.gt_boxes.tensor.to(torch.float32)   # float32 features in any run
             H, W = d["image"].shape[1], d["image"].shape[2]
             scale = torch.tensor([W, H, W, H], dtype=boxes.dtype, device=boxes.device)
             feats.append(torch.tanh((boxes / scale - 0.5) @ self.W.to(boxes.device)))

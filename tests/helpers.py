@@ -66,13 +66,23 @@ def pin_matcher(crit, fx, device):
     return crit
 
 
-# Gradient tolerance per parameter group.  The reference fixture model is random-init, so
-# many ReLU pre-activations sit at ~0; a 1e-5 relative change of the SA output (different
-# GEMM/BN accumulation order) flips a few ReLU masks in the encoder / projection and moves
-# those gradients by up to a few 1e-2 relative.  Parameters downstream of every ReLU
-# boundary that matters (last decoder layer, decoder norm, heads) are held to 1e-3; the
-# SA module's own backward is pinned separately on identical inputs
-# (test_sa_module_matches_reference_semantics).
+# Gradient bar of the REDUCED fixtures (model_sun.npz / model_scannet.npz: fp32 reference
+# vs fp32 product, 64-d random-init model).  Both sides are fp32, and the fp32 gradient of a
+# random-init model is not reproducible element-wise: ReLU masks / max-pool winners with
+# ~1e-7 margins flip between any two fp32 runs (the reference's own fp32 runs, jittered by
+# 2^-21, disagree by up to 1.2e-2; see test_parity_full).  These fixtures therefore check the
+# wiring with the relative L2 error (1e-3 past the last ReLU boundary: decoder tail, heads;
+# 2e-2 before it).  The element-wise parity bar is carried by the float64 full-shape fixtures
+# (tests/test_parity_full.py): product float64 == reference float64 to 1e-6, product fp32
+# within max(1e-3, 3x the reference's own fp32 envelope) per entry.
 def grad_tol(name):
     strict = ("decoder.layers.7.", "decoder.norm.", "mlp_heads.")
-    return 1e-3 if name.startswith(strict) else 5e-2
+    return 1e-3 if name.startswith(strict) else 2e-2
+
+
+def grad_err(a, b):
+    """relative L2 error of gradient a against the fixture's b (0 when both are zero)"""
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    nb = np.linalg.norm(b)
+    return float(np.linalg.norm(a - b) / nb) if nb > 0 else float(np.abs(a).max())

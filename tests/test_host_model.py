@@ -8,7 +8,7 @@ import torch
 
 from fake_clip import FakeRegionCLIP
 from helpers import (batch_from_fixture, build_model_from_fixture, fixture, fixture_prefix, ov3d,
-                     grad_tol, pin_matcher, rel_err)
+                     grad_err, grad_tol, pin_matcher, rel_err)
 
 CASES = [("model_sun.npz", "sunrgbd"), ("model_scannet.npz", "scannet")]
 
@@ -79,7 +79,7 @@ def test_gradients_match_reference(shim, name, ds):
     grads = fixture_prefix(fx, "grad/")
     assert len(grads) >= 10
     for k, g in grads.items():
-        assert rel_err(named[k].grad.numpy(), g) < grad_tol(k), k
+        assert grad_err(named[k].grad.numpy(), g) < grad_tol(k), k
 
 
 def test_geometry_matches_reference():

@@ -7,7 +7,7 @@ import torch
 
 from fake_clip import FakeRegionCLIP
 from helpers import (batch_from_fixture, build_model_from_fixture, fixture, fixture_prefix,
-                     grad_tol, pin_matcher, rel_err)
+                     grad_err, grad_tol, pin_matcher, rel_err)
 
 pytestmark = pytest.mark.gpu
 
@@ -39,7 +39,7 @@ def test_model_matches_reference_on_gpu(cuda, name, ds):
     loss.backward()
     named = dict(model.named_parameters())
     for k, g in fixture_prefix(fx, "grad/").items():
-        assert rel_err(named[k].grad.cpu().numpy(), g) < grad_tol(k), k
+        assert grad_err(named[k].grad.cpu().numpy(), g) < grad_tol(k), k
 
 
 def test_full_size_train_step_properties(cuda):

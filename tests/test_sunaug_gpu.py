@@ -7,6 +7,7 @@ gt_box_corners, where the reference's float32 cos / sin come from numpy's SIMD r
 (get_3d_box_batch_np, box_util.py:265-285) and the device's from ocml: <= 4 float32 ulp
 of max(|value|, 1).
 """
+import hashlib
 import os
 import sys
 
@@ -17,7 +18,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "golden"))
 
-from sunaug_cases import CASES, raw_scans  # noqa: E402
+from sunaug_cases import CASES, OPTS, image_extras, pseudo_boxes, raw_scans  # noqa: E402
 from ov3d_amd import sunrgbd  # noqa: E402
 from ov3d_amd.dataset_config import SunrgbdDatasetConfig  # noqa: E402
 
@@ -35,23 +36,45 @@ def _ulp_close(a, b, ulps):
     return bool(np.all(d <= ulps * np.spacing(mag).astype(np.float64)))
 
 
-def _dataset(split, dt, nraw, npts, aug, cub, minp):
+def _dataset(split, dt, nraw, npts, aug, cub, minp, use_pbox=False, use_image=False,
+             use_2d_feature=False):
+    scans = raw_scans(dt, nraw)
+    if use_pbox:      # GT boxes, then the pseudo boxes (the count of GT boxes kept beside)
+        scans = [(pc, np.concatenate([bb, pseudo_boxes(i)], 0), bb.shape[0])
+                 for i, (pc, bb) in enumerate(scans)]
+    extras = None
+    if use_image or use_2d_feature:
+        extras = []
+        for i in range(len(scans)):
+            img, rt, kk, feat = image_extras(i)
+            e = {}
+            if use_image:
+                # the calib file round trip of the golden (repr -> float) is exact
+                e.update(image=img, calib_Rtilt=rt, calib_K=kk)
+            if use_2d_feature:
+                e["feature_2d"] = feat
+            extras.append(e)
     return sunrgbd.SunrgbdDetectionDataset(SunrgbdDatasetConfig(), split_set=split, num_points=npts,
                                            augment=aug, use_random_cuboid=cub,
                                            random_cuboid_min_points=minp, device="cuda",
-                                           scans=raw_scans(dt, nraw))
+                                           scans=scans, extras=extras, use_pbox=use_pbox,
+                                           use_image=use_image, use_2d_feature=use_2d_feature)
 
 
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_device_batch_equals_reference_loader(name):
     split, dt, nraw, npts, aug, cub, minp, seed, inds, per_scene = CASES[name]
-    ds = _dataset(split, dt, nraw, npts, aug, cub, minp)
+    ds = _dataset(split, dt, nraw, npts, aug, cub, minp, **OPTS.get(name, {}))
     if per_scene:
         out = ds.get_batch(inds, rngs=[np.random.RandomState(seed * 100 + j) for j in range(len(inds))])
     else:
         out = ds.get_batch(inds, rng=np.random.RandomState(seed))
     torch.cuda.synchronize()
     keys = [k.split("/", 1)[1] for k in GOLD.files if k.startswith(name + "/")]
+    if "image" in out:   # the golden keeps the (B, 530*730*3) float32 images as a sha256
+        digest = hashlib.sha256(out.pop("image").cpu().numpy().tobytes()).digest()
+        assert np.frombuffer(digest, np.uint8).tolist() == GOLD[f"{name}/image_sha256"].tolist()
+        keys.remove("image_sha256")
     assert set(keys) == set(out), sorted(set(keys) ^ set(out))
     for k in keys:
         ref = GOLD[f"{name}/{k}"]
