@@ -147,10 +147,68 @@ def fps_launch_timings(pool, cli, reps=5):
     return _native.timing_collect()
 
 
-def cpu_baseline(args, batch_size=1, steps=2):
+def _gpu_busy(ms=3.0):
+    """keep the stream busy (a spin kernel) while the host enqueues the timed launches, so
+    the HIP events bracket kernel time, not host launch gaps"""
+    try:
+        torch.cuda._sleep(int(ms * 2.4e6))
+    except Exception:
+        pass
+
+
+def attn_launch_timings(B, L, H=4, p=0.1, reps=5):
+    """The roofline kernel: the encoder self-attention (flash attention, csrc/attn.hip) at the
+    step's shape.  Inside graph replays it is not reachable by host events, so the same
+    launches (forward kernel; backward = dQ + dK/dV kernels) run right after the timed region
+    on the step's stream, bracketed by HIP events."""
+    from ov3d_amd import attention as A
+    E = H * A.HEAD_DIM
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.randn((L, B, 3 * E), device="cuda", dtype=torch.bfloat16, generator=g)
+    x.requires_grad_(True)
+    gout = torch.randn((L, B, E), device="cuda", dtype=torch.bfloat16, generator=g)
+    spec = ((0, 0), (0, E), (0, 2 * E))
+    st = torch.cuda.current_stream()
+    fwd, bwd = [], []
+    for i in range(reps + 1):          # the first pair warms the allocator
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        _gpu_busy()
+        ev[0].record(st)
+        o = A.attention_packed([x], spec, L, L, H, p, site=1)
+        ev[1].record(st)
+        o.backward(gout)
+        ev[2].record(st)
+        ev[2].synchronize()
+        x.grad = None
+        if i:
+            fwd.append(ev[0].elapsed_time(ev[1]))
+            bwd.append(ev[1].elapsed_time(ev[2]))
+    return float(np.mean(fwd)), float(np.mean(bwd))
+
+
+def fps_latency_floor(B, M, reps=3):
+    """FPS iteration cost with one point per thread (N = M): what the per-iteration barrier /
+    reduction / LDS chain costs with (almost) no distance work -- the kernel's latency floor"""
+    from ov3d_amd import pointnet2_utils as pu
+    xyz = torch.rand((B, M, 3), device="cuda") + 0.1
+    st = torch.cuda.current_stream()
+    ts = []
+    for i in range(reps + 1):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        pu.furthest_point_sample_gather(xyz, M)
+        e1.record(st)
+        e1.synchronize()
+        if i:
+            ts.append(e0.elapsed_time(e1))
+    return float(np.mean(ts))
+
+
+def cpu_baseline(args, samples=((1, 2), (8, 1))):
     """The reference step on the host cores: product host code on CPU with the
     C oracle for FPS / ball query / grouping / GIoU (test-infrastructure
-    injection, oracle/torch_shim.py), fp32, bounded sample."""
+    injection, oracle/torch_shim.py), fp32, bounded samples: (batch, steps) pairs, B=1
+    (config C1) and B=8 (the GPU workload's batch), after one B=1 warm-up step."""
     from oracle import torch_shim
     ov3d = ov3d_import.load()
     from ov3d_amd import synthetic
@@ -167,8 +225,6 @@ def cpu_baseline(args, batch_size=1, steps=2):
         crit = ov3d.build_criterion(args, cfg)
         opt = torch.optim.AdamW([p for p in model.parameters() if p.requires_grad], lr=args.base_lr,
                                 weight_decay=args.weight_decay)
-        batches = [synthetic.make_batch(batch_size, seed=100 + i) for i in range(steps + 1)]
-
         def step(b):
             opt.zero_grad(set_to_none=True)
             out = model({k: b[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")})
@@ -177,17 +233,22 @@ def cpu_baseline(args, batch_size=1, steps=2):
             torch.nn.utils.clip_grad_norm_(model.parameters(), args.clip_gradient)
             opt.step()
 
-        step(batches[0])  # warm-up
-        t0 = time.perf_counter()
-        for i in range(steps):
-            step(batches[i + 1])
-        dt = time.perf_counter() - t0
+        step(synthetic.make_batch(1, seed=99))  # warm-up
+        rates = {}
+        for bs, steps in samples:
+            batches = [synthetic.make_batch(bs, seed=100 + i) for i in range(steps)]
+            t0 = time.perf_counter()
+            for b in batches:
+                step(b)
+            rates[bs] = (bs * steps / (time.perf_counter() - t0), steps)
     finally:
         torch_shim.uninstall(saved)
-    return {"value": round(batch_size * steps / dt, 4), "unit": "scenes/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{steps} train steps x {batch_size} scene(s) of 20000 pts (B={batch_size}), fp32, "
-                      "oracle C for FPS/ball-query/grouping/GIoU + PyTorch-CPU dense layers"}
+    b0 = samples[0][0]
+    return {"value": round(rates[b0][0], 4), "unit": "scenes/s", "cores": threads, "kind": "port",
+            "by_batch": {f"B={b}": {"value": round(r, 4), "steps": n} for b, (r, n) in rates.items()},
+            "sample": "; ".join(f"{n} train step(s) x B={b}" for b, (_, n) in rates.items())
+                      + " of 20000-pt scenes, fp32, oracle C for FPS/ball-query/grouping/GIoU + "
+                        "PyTorch-CPU dense layers (value: B=%d)" % b0}
 
 
 def main():
@@ -286,13 +347,20 @@ def main():
         _native.timing_enable(["ov3d_fps"])
     torch.cuda.synchronize()
     dist.barrier()
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(cli.steps + 1)]
     t0 = time.perf_counter()
+    marks[0].record()
     for i in range(cli.steps):
         loss = step(i)
+        marks[i + 1].record()
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
     timings = _native.timing_collect() if graphed is None else fps_launch_timings(pool, cli)
+    att = None
+    if rank == 0 and dataset == "sunrgbd":
+        att = attn_launch_timings(cli.batch, args.preenc_npoints, args.enc_nhead, args.enc_dropout)
+        fps_floor_ms = fps_latency_floor(cli.batch, args.preenc_npoints)
     el = torch.tensor([elapsed], device=device, dtype=torch.float64)
     if world > 1:
         torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
@@ -304,24 +372,46 @@ def main():
         return
     scenes = cli.batch * world * cli.steps
     value = scenes / elapsed
-    # roofline of ov3d_fps: launches alternate pre-encoder (N=20000 -> 2048) and query (2048 -> 128)
+    # per-step times on this rank (HIP events between steps; SURVEY §8d asks for the median)
+    per_step = [marks[i].elapsed_time(marks[i + 1]) for i in range(cli.steps)]
+    # roofline: the encoder flash attention (the largest kernel family on the step's critical
+    # path; FPS runs on the side stream).  Algorithmic flops per launch: 4 * L^2 * d per
+    # (scene, head) forward (Q K^T and P V); the backward 10 * L^2 * d (dV, dP, dS->dQ, dK:
+    # 2.5x the forward, the usual flash-attention count; the S recompute is not counted)
+    roof, extra = None, {}
+    if att is not None:
+        L, H, d = args.preenc_npoints, args.enc_nhead, 64
+        fwd_ms, bwd_ms = att
+        fl_fwd = 4.0 * L * L * d * cli.batch * H
+        ach = fl_fwd / (fwd_ms * 1e-3) / 1e12
+        traffic, tsrc = None, None
+        pmc = os.path.join(ROOT, "profiles", "r03_attn_pmc.json")
+        if os.path.exists(pmc) and (cli.batch, L, H) == (8, 2048, 4):
+            traffic = json.load(open(pmc)).get("fwd_traffic_bytes_per_launch")
+            tsrc = "profiles/r03_attn_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)"
+        roof = {"bound": "mfma", "achieved": round(ach, 1), "peak": BF16_DENSE_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(ach / BF16_DENSE_PEAK_TFLOPS, 4),
+                "traffic": traffic, "traffic_source": tsrc,
+                "kernel": "attn_fwd_kernel (encoder self-attention, B=%d H=%d L=%d d=64, dropout %.1f)"
+                          % (cli.batch, H, L, args.enc_dropout),
+                "flop_per_launch": fl_fwd, "avg_launch_ms": round(fwd_ms, 4), "launches": 5}
+        fl_bwd = 2.5 * fl_fwd
+        extra["attn_bwd"] = {"kernels": "attn_bwd_dq_kernel + attn_bwd_dkdv_kernel",
+                             "avg_ms": round(bwd_ms, 4), "flop": fl_bwd,
+                             "achieved_tflops": round(fl_bwd / (bwd_ms * 1e-3) / 1e12, 1),
+                             "frac": round(fl_bwd / (bwd_ms * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS, 4)}
+    # FPS (side stream): a serial chain of M - 1 dependent iterations, reported per iteration
+    # against the same kernel's cost with one point per thread (its latency floor)
     fps = timings.get("ov3d_fps", [])
     pre = [t for t in fps if t["shape"][1] == cli.points]
-    roof = None
-    if pre:
+    if pre and att is not None:
         B, N, M = pre[0]["shape"]
         avg_ms = float(np.mean([t["ms"] for t in pre]))
-        algo_bytes = B * M * N * 16.0      # per scene M*N*(12 B coords + 4 B running min)
-        achieved = algo_bytes / (avg_ms * 1e-3) / 1e9
-        traffic, tsrc = None, None
-        pmc = os.path.join(ROOT, "profiles", "r02_fps_pmc.json")
-        if os.path.exists(pmc) and (B, N, M) == (8, 20000, 2048):
-            traffic = json.load(open(pmc))["traffic_bytes_per_launch"]
-            tsrc = "profiles/r02_fps_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, gfx950-corrected)"
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
-                "kernel": "ov3d_fps (pre-encoder, B=%d N=%d M=%d)" % (B, N, M),
-                "avg_launch_ms": round(avg_ms, 4), "launches": len(pre)}
+        extra["fps"] = {"kernel": "fps_cull_kernel (pre-encoder, B=%d N=%d M=%d, side stream)" % (B, N, M),
+                        "avg_launch_ms": round(avg_ms, 4),
+                        "us_per_iteration": round(avg_ms * 1e3 / (M - 1), 4),
+                        "floor_us_per_iteration": round(fps_floor_ms * 1e3 / (M - 1), 4),
+                        "floor": f"same kernel, N = M = {M} (one point per thread)"}
     gflop_scene = STEP_GFLOP_PER_SCENE
     metric = "scenes/sec (train step) SUN RGB-D 20k pts nqueries=128"
     workload = (f"SUN RGB-D train step, bs={cli.batch}/GPU, {cli.points} pts, nqueries=128, "
@@ -340,11 +430,13 @@ def main():
         "metric": metric,
         "value": round(value, 3), "unit": "scenes/s", "n_gpus": world, "steps": cli.steps,
         "warmup": cli.warmup, "ms_per_step": round(elapsed / cli.steps * 1e3, 3),
+        "ms_per_step_median": round(float(np.median(per_step)), 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": cli.dtype,
         "data": "synthetic SUN RGB-D-like scenes (numpy PCG64), random-init weights",
         "config": {"workload": workload,
                    "global_batch": cli.batch * world, "points": cli.points, "parallelism": f"dp{world}"},
         "roofline": roof,
+        **extra,
         "step_mfma": {"achieved_tflops": round(step_tflops, 2), "peak_tflops": BF16_DENSE_PEAK_TFLOPS,
                       "frac": round(step_tflops / (world * BF16_DENSE_PEAK_TFLOPS), 5)},
     }

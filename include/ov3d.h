@@ -118,8 +118,15 @@ int ov3d_giou3d(const float* corners1, const float* corners2, const int32_t* num
                 int K2, int mode, int rotated, const int32_t* rotated_dev, int k2_bug, float* out,
                 void* stream);
 
-/* Backward of the axis-aligned (rotated == 0) GIoU w.r.t. corners1:
- * grad_out (B,K1,K2) -> grad_corners1 (B,K1,8,3) (overwritten). */
+/* Backward of the differentiable GIoU (OV3D_GIOU_TENSOR semantics, box_util.py:517-618 under
+ * autograd) w.r.t. corners1: grad_out (B,K1,K2) -> grad_corners1 (B,K1,8,3) (overwritten).
+ * rotated / rotated_dev as ov3d_giou3d: the rotated intersection is differentiated through
+ * every Sutherland-Hodgman intersection vertex (box_util.py:387-440, 579-600). */
+int ov3d_giou3d_bwd(const float* corners1, const float* corners2, const int32_t* nums, int B,
+                    int K1, int K2, int rotated, const int32_t* rotated_dev, const float* grad_out,
+                    float* grad_corners1, void* stream);
+
+/* ov3d_giou3d_bwd with rotated = 0 (axis-aligned GIoU). */
 int ov3d_giou3d_bwd_aligned(const float* corners1, const float* corners2, const int32_t* nums,
                             int B, int K1, int K2, const float* grad_out, float* grad_corners1,
                             void* stream);
@@ -282,6 +289,17 @@ int ov3d_clip_preprocess(const float* images, long long img_stride, const int32_
                          const int32_t* widths, int B, int Hp, int Wp, float div, float m0,
                          float m1, float m2, float s0, float s1, float s2, int out_bf16, void* out,
                          void* stream);
+
+/* 3D box -> 2D image box of the RegionCLIP alignment branch.  Replaces
+ * utils/image_util.py:117-134 project_box_3d_cuda with SUNRGBD_Calibration_cuda
+ * (image_util.py:275-298) and the clamp of criterion.py:386-391 (quirk Q4: the full size
+ * as half-extent; [min v, min u, max v, max u]).
+ *   center / size (n, 3), heading (n) f32, rows ordered (.., scene, query): the scene of
+ *   row r is (r / Q) % B; Rtilt / K (B, 3, 3) f32 row-major; img_h / img_w (B) int64
+ *   -> out (n, 4) f32 clamped to [0, (w, h, w, h)].  float32 arithmetic as the reference. */
+int ov3d_project_box2d(const float* center, const float* size, const float* heading, long long n,
+                       int Q, int B, const float* Rtilt, const float* K, const int64_t* img_h,
+                       const int64_t* img_w, float* out, void* stream);
 
 /* ROIAlign forward on channels-last features.  Replaces the ROIAlignV2 pooler of
  * CLIPRes5ROIHeads (detectron2 ROIPooler -> torchvision roi_align, aligned=True)

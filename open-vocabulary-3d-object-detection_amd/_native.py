@@ -29,6 +29,7 @@ _SIGS = {
     "ov3d_gather_bwd": "ppiiiipp",
     "ov3d_giou3d": "pppiiiiipipp",
     "ov3d_giou3d_bwd_aligned": "pppiiippp",
+    "ov3d_giou3d_bwd": "pppiiiipppp",
     "ov3d_hungarian": "ppiiipppp",
     "ov3d_sa_l1_fwd": "ppiippip",
     "ov3d_sa_l1_fwd_cin": "pipiippip",
@@ -97,6 +98,7 @@ _SIGS = {
     "ov3d_box3d_iou_eval": "ppppiiipp",
     "ov3d_ap_match": "ppppiiiidpp",
     "ov3d_ap_curve": "plppiplppp",
+    "ov3d_project_box2d": "pppliipppppp",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
                           "ov3d_attn_dropbits_words", "ov3d_attn_maskbits_words", "ov3d_fps_workspace", "ov3d_attn_small_bwd", "ov3d_set_loss_fwd_parts",

@@ -5,7 +5,7 @@ parts of reference utils/box_util.py).
 and its dispatch: ``needs_grad=False`` -> the Cython semantics
 (box_util.py:624-714 + box_intersection.pyx, including the K2 bug, Q1, unless
 ``k2_bug=False``), ``needs_grad=True`` -> the TorchScript semantics
-(box_util.py:517-618) with an analytic HIP backward for the axis-aligned case.
+(box_util.py:517-618) with an analytic HIP backward, axis-aligned and rotated.
 Both run on the device (the reference copies rectangles to the host and loops
 in Cython, box_util.py:684-698).
 """
@@ -116,33 +116,36 @@ def giou3d_raw(corners1, corners2, nums_k2, mode, rotated, k2_bug=True):
     return out
 
 
-class _GIoUAligned(Function):
-    """differentiable GIoU (box_util.py:517-621, all K2).  `rotated` is False or the
-    criterion's device flag (any(gt_box_angles > 0)): the forward then follows it on the
-    device, and since only the axis-aligned gradient is implemented, a rotated batch gets
-    NaN gradients (the loss is finite, the step's non-finite check fires) instead of a
-    host sync that a captured step cannot make."""
+class _GIoUTensor(Function):
+    """differentiable GIoU (box_util.py:517-621, all K2) with the reference's autograd
+    gradient w.r.t. corners1: axis-aligned, or rotated -- through the Sutherland-Hodgman
+    clip's intersection vertices (box_util.py:387-440, 579-600).  `rotated` is a bool or the
+    criterion's device flag (any(gt_box_angles > 0), criterion.py:317-330): read on the
+    device, forward and backward, so a captured step needs no host sync."""
 
     @staticmethod
     def forward(ctx, corners1, corners2, nums_k2, rotated):
         c1, c2, nums = _prep(corners1, corners2, nums_k2)
         flag = rotated if isinstance(rotated, torch.Tensor) else None
+        if flag is not None:
+            flag = nat.check(flag.to(device=c1.device, dtype=torch.int32).reshape(1).contiguous(),
+                             "rotated", torch.int32, 1)
         ctx.save_for_backward(c1, c2, nums if nums is not None else torch.empty(0),
                               flag if flag is not None else torch.empty(0))
         ctx.has_nums = nums is not None
-        ctx.has_flag = flag is not None
-        return giou3d_raw(c1, c2, nums, nat.OV3D_GIOU_TENSOR, flag if flag is not None else False)
+        ctx.rot_host = bool(rotated) if flag is None else False
+        return giou3d_raw(c1, c2, nums, nat.OV3D_GIOU_TENSOR,
+                          flag if flag is not None else ctx.rot_host)
 
     @staticmethod
     def backward(ctx, g):
         c1, c2, nums, flag = ctx.saved_tensors
         nums = nums if ctx.has_nums else None
+        flag = flag if flag.numel() else None
         g = nat.check(g.float().contiguous(), "grad", torch.float32, 3)
         B, K1, K2 = g.shape
         gc1 = torch.empty_like(c1)
-        nat.call("ov3d_giou3d_bwd_aligned", c1, c2, nums, B, K1, K2, g, gc1, like=g)
-        if ctx.has_flag:
-            gc1 = torch.where(flag.reshape(()).bool(), torch.full_like(gc1, float("nan")), gc1)
+        nat.call("ov3d_giou3d_bwd", c1, c2, nums, B, K1, K2, int(ctx.rot_host), flag, g, gc1, like=g)
         return gc1, None, None, None
 
 
@@ -154,11 +157,6 @@ def generalized_box3d_iou(corners1, corners2, nums_k2, rotated_boxes=True,
     if return_inter_vols_only:
         raise NotImplementedError("return_inter_vols_only is not on the training path")
     if needs_grad:
-        if not isinstance(rotated_boxes, torch.Tensor) and rotated_boxes:
-            raise NotImplementedError(
-                "differentiable rotated GIoU (loss_giou_weight > 0 with rotated GT) is not "
-                "implemented yet; the reference evaluates it with a Python triple loop")
-        return _GIoUAligned.apply(corners1, corners2, nums_k2,
-                                  rotated_boxes if isinstance(rotated_boxes, torch.Tensor) else False)
+        return _GIoUTensor.apply(corners1, corners2, nums_k2, rotated_boxes)
     with torch.no_grad():
         return giou3d_raw(corners1, corners2, nums_k2, nat.OV3D_GIOU_CYTHON, rotated_boxes, k2_bug)

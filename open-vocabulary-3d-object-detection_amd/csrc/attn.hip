@@ -212,7 +212,45 @@ __device__ __forceinline__ bf16x8 v_operand(const bf16* Vs, int lane, int dt, in
 // score bit of element i of score tile t in a query-major (drop / mask) word
 __device__ __forceinline__ constexpr int score_bit(int t, int i) { return ((i & 1) << 4) + 8 * t + (i >> 1); }
 
-template <bool DROP, bool MASK>
+// Drop bits ahead of the forward (long attentions: the encoder's L = 2048): the query-major
+// and key-major words the forward would store, from the same hash, in a VALU-only pass; the
+// forward then reads one word per lane and tile (BITS) instead of hashing 16 key pairs on the
+// softmax's critical path (the hash was ~40 % of the forward's vector issue).  Same grid and
+// lane layout as attn_fwd_kernel (a wave = 32 queries, lane = (query r, half h)), every
+// 64-key tile of the key range.
+__global__ void __launch_bounds__(256) attn_dropgen_kernel(AttnArgs a) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int bh = blockIdx.y;
+    const int q0 = blockIdx.x * (4 * QW) + wave * QW;
+    if (q0 >= a.Lq) return;
+    const uint32_t qh = drop_query_base(drop_head_mix(a.seed, a.site, bh), q0 + r) +
+                        (uint32_t)(2 * h) * kPairMul;
+    uint32_t* const wq_lane = a.wq + ((size_t)bh * a.Lq + q0 + r) * 2 + h;
+    const size_t wq_tile = (size_t)gridDim.y * a.Lq * 2;
+    uint32_t* const wk_lane = a.wk + ((size_t)(q0 >> 5) * gridDim.y + bh) * ((size_t)a.nkt * 64) +
+                              drop_key(r, h);
+    const short ts = (short)((int)a.thresh - 32768);
+    const s16x2 tsig = {ts, ts};
+    for (int kt = 0; kt < a.nkt; ++kt) {
+        const uint32_t hb = qh + (uint32_t)(32 * kt) * kPairMul;
+        uint32_t dw = 0;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; i += 2) {
+                const uint32_t c = 16 * t + ((i & 3) >> 1) + 4 * (i >> 2);
+                const uint32_t dm = drop_halves(mix24(hb + c * kPairMul), tsig);
+                const int jb = 8 * t + (i >> 1);
+                dw |= dm & ((1u << jb) | (1u << (16 + jb)));
+            }
+        wq_lane[(size_t)kt * wq_tile] = dw;
+        wk_lane[64 * kt] = transpose32(dw, r);
+    }
+}
+
+// BITS: dropout from the words of attn_dropgen_kernel (read, not hashed, not stored)
+template <bool DROP, bool MASK, bool BITS>
 __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     __shared__ __attribute__((aligned(16))) bf16 Ks[2][KB * LDK];
     __shared__ __attribute__((aligned(16))) bf16 Vs[2][KB * LDK];
@@ -234,12 +272,13 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     // dropout hash input of key pair (kb >> 1) + 2h + c: qh + (kb >> 1) * kPairMul (wave-
     // uniform, once per tile) + c * kPairMul (a constant per unrolled pair)
     uint32_t qh = 0;
-    if (DROP) qh = drop_query_base(drop_head_mix(a.seed, a.site, bh), active ? q0 + r : 0) +
-                   (uint32_t)(2 * h) * kPairMul;
-    // drop-word destinations: query-major word (kt, bh, q, h), key-major word (q0/32, bh, key)
-    uint32_t* const wq_lane = DROP ? a.wq + ((size_t)bh * a.Lq + q0 + r) * 2 + h : nullptr;
+    if (DROP && !BITS) qh = drop_query_base(drop_head_mix(a.seed, a.site, bh), active ? q0 + r : 0) +
+                            (uint32_t)(2 * h) * kPairMul;
+    // drop-word destinations (BITS: sources): query-major word (kt, bh, q, h), key-major word
+    // (q0/32, bh, key)
+    uint32_t* const wq_lane = DROP ? a.wq + ((size_t)bh * a.Lq + (active ? q0 + r : 0)) * 2 + h : nullptr;
     const size_t wq_tile = (size_t)gridDim.y * a.Lq * 2;
-    uint32_t* const wk_lane = DROP ? a.wk + ((size_t)(q0 >> 5) * gridDim.y + bh) * ((size_t)a.nkt * 64) +
+    uint32_t* const wk_lane = (DROP && !BITS) ? a.wk + ((size_t)(q0 >> 5) * gridDim.y + bh) * ((size_t)a.nkt * 64) +
                                          drop_key(r, h) : nullptr;
     uint32_t dw_prev = 0;   // drop word of the tile before this one
     // mask words of this lane (query q0 + r, half h), one per 64-key tile
@@ -298,6 +337,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
             const bf16* K = Ks[buf];
             const bf16* V = Vs[buf];
             const uint32_t mw = MASK ? mrow[(size_t)(kb >> 6) * mtile] : 0u;
+            const uint32_t dwin = (DROP && BITS) ? wq_lane[(size_t)(kb >> 6) * wq_tile] : 0u;
             // all LDS operand reads of the tile are issued ahead of their MFMAs, so their
             // latency overlaps the matrix / softmax work instead of stalling each MFMA
             bf16x8 ka[2][4];
@@ -329,7 +369,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
             if (more) load(kb + KB);
             // the previous tile's drop word goes out while the score MFMAs run: the lane
             // transpose's swizzle round trips would otherwise sit on this tile's critical path
-            if (DROP && kb > kbeg) store_drop(kb - KB);
+            if (DROP && !BITS && kb > kbeg) store_drop(kb - KB);
             PROBE(1);
             // keys past Lk (last partial tile) do not take part
             const int nvalid = kend - kb;
@@ -387,7 +427,12 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
                     rs0 += p0;
                     rs1 += p1;
                     uint32_t pk = pack_bf16(p0, p1);
-                    if (DROP) {
+                    if (DROP && BITS) {   // bits 8t + (i>>1) (even key), 16 + 8t + (i>>1) (odd)
+                        const int jb = 8 * t + (i >> 1);
+                        const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)dwin, jb, 1);
+                        const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)dwin, 16 + jb, 1);
+                        pk &= ~((m0 & 0xFFFFu) | (m1 & 0xFFFF0000u));
+                    } else if (DROP) {
                         // key 32t + (i&3) + 8(i>>2) + 4h (even): pair 16t + (i&3)/2 + 4(i>>2) + 2h
                         const uint32_t c = 16 * t + ((i & 3) >> 1) + 4 * (i >> 2);
                         const uint32_t dm = drop_halves(mix24(hb + c * kPairMul), tsig);
@@ -399,7 +444,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
                     pw[t][i >> 3][(i & 7) >> 1] = pk;
                 }
             l += rs0 + rs1;
-            if (DROP) dw_prev = dw;
+            if (DROP && !BITS) dw_prev = dw;
             PROBE(3);
 #pragma unroll
             for (int t = 0; t < 2; ++t)
@@ -418,7 +463,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     }
     PROBE_END;
     if (!active) return;
-    if (DROP && kend > kbeg) store_drop((kend - 1) & ~(KB - 1));
+    if (DROP && !BITS && kend > kbeg) store_drop((kend - 1) & ~(KB - 1));
     const float ltot = l + __shfl_xor(l, 32);
     const int q = q0 + r;
     if (a.nsplit == 1) {
@@ -1039,6 +1084,14 @@ extern "C" int ov3d_attn_small_bwd(int on) {
     return prev;
 }
 
+// drop bits from attn_dropgen_kernel for attentions with at least this many (query, key)
+// pairs per head (OV3D_ATTN_DROPGEN_MIN overrides; 0 = always, -1 = never)
+static bool dropgen_ahead(int Lq, int Lk) {
+    const char* e = getenv("OV3D_ATTN_DROPGEN_MIN");   // read per call: tests flip it
+    const long long min_pairs = e ? atoll(e) : 512LL * 1024;
+    return min_pairs >= 0 && (long long)Lq * Lk >= min_pairs;
+}
+
 static void set_maskbits(AttnArgs& a, const uint32_t* bits) {
     a.mq = bits;
     a.mk = bits ? bits + 2 * (size_t)a.nkt * a.B * a.Lq : nullptr;
@@ -1108,15 +1161,26 @@ extern "C" int ov3d_attn_fwd_masked(const void* q, const void* k, const void* v,
     set_maskbits(a, maskbits);
     hipStream_t st = ov3d_stream(stream);
     dim3 grid((Lq + 4 * QW - 1) / (4 * QW), B * H, nsplit);
+    // long attentions take their drop bits from a separate VALU pass (attn_dropgen_kernel);
+    // short ones (the decoder) hash in the forward, where one more launch would cost more
+    const bool bits = a.thresh && dropgen_ahead(Lq, Lk);
+    if (bits) {
+        attn_dropgen_kernel<<<dim3(grid.x, grid.y), 256, 0, st>>>(a);
+        OV3D_LAUNCH_CHECK();
+    }
     if (maskbits) {
-        if (a.thresh)
-            attn_fwd_kernel<true, true><<<grid, 256, 0, st>>>(a);
+        if (bits)
+            attn_fwd_kernel<true, true, true><<<grid, 256, 0, st>>>(a);
+        else if (a.thresh)
+            attn_fwd_kernel<true, true, false><<<grid, 256, 0, st>>>(a);
         else
-            attn_fwd_kernel<false, true><<<grid, 256, 0, st>>>(a);
+            attn_fwd_kernel<false, true, false><<<grid, 256, 0, st>>>(a);
+    } else if (bits) {
+        attn_fwd_kernel<true, false, true><<<grid, 256, 0, st>>>(a);
     } else if (a.thresh) {
-        attn_fwd_kernel<true, false><<<grid, 256, 0, st>>>(a);
+        attn_fwd_kernel<true, false, false><<<grid, 256, 0, st>>>(a);
     } else {
-        attn_fwd_kernel<false, false><<<grid, 256, 0, st>>>(a);
+        attn_fwd_kernel<false, false, false><<<grid, 256, 0, st>>>(a);
     }
     OV3D_LAUNCH_CHECK();
     if (nsplit > 1) {

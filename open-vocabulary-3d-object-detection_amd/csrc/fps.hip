@@ -875,12 +875,327 @@ __global__ __launch_bounds__(kThreads) void fps_stream_kernel(const float* __res
     }
 }
 
+// ---------------------------------------------------------------------------
+// Two workgroups (two CUs) per scene for kThreads*kMaxPPT < N <= 2*kThreads*kMaxPPT (ScanNet:
+// 40000 points).  Both workgroups sort the whole scene by Morton cell (as fps_cull_kernel) and
+// each keeps one half of the sorted order -- a compact spatial half -- in VGPRs (<= 20 slots
+// per lane, the 20000-point register kernel's layout).  Per iteration each workgroup runs the
+// culled update and its block argmax, then the halves swap their candidates through L2:
+// five 64-bit words per (scene, half, iteration parity), each carrying the iteration number
+// as a tag (no fences: a word is valid when its tag matches), written by one lane, polled by
+// one lane per wave.  The winner is (larger distance, then smaller upstream rank), the same
+// rule inside and across the halves, so the indices equal the one-workgroup kernels'.
+// Scene b runs on workgroups b and b + B: with B a multiple of 8, the same XCD (one L2).
+// The exchange slots are zeroed by the host before each launch (tag 0 is never used).
+constexpr int kPairSpin = 1 << 26;   // polls before giving up (a hung partner: garbage, not a hang)
+
+__device__ __forceinline__ unsigned long long xword(uint32_t v, uint32_t tag) {
+    return ((unsigned long long)tag << 32) | v;
+}
+
+template <int PPT>
+__global__ __launch_bounds__(kThreads) void fps_pair_kernel(const float* __restrict__ xyz, int B,
+                                                            int N, int M, int L,
+                                                            unsigned long long* __restrict__ xch,
+                                                            int32_t* __restrict__ idx,
+                                                            float* __restrict__ new_xyz) {
+    constexpr int PW = PPT * 64;
+    constexpr int NSORT = 2 * PPT;   // setup slots per thread (the whole scene)
+    __shared__ uint32_t s_hist[kCells];
+    __shared__ uint16_t s_perm[kThreads * NSORT];
+    __shared__ uint16_t s_out[kMaxOutLDS];     // winning point index per iteration
+    __shared__ float s_red[6][kWaves];
+    __shared__ uint32_t s_scan[kWaves];
+    __shared__ float4 s_pub[2][kWaves];
+    __shared__ int s_pos[2][kWaves];
+
+    const int b = blockIdx.x % B;
+    const int half = blockIdx.x / B;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int w = tid >> 6;
+    const float* __restrict__ p = xyz + (size_t)b * N * 3;
+    const int NH = (N + 1) / 2;
+    const int base = half * NH;                 // this half's sorted positions [base, end)
+    const int end = half ? N : NH;
+    // exchange words: [b][half][parity][8] (5 used: distance, point index, x, y, z)
+    unsigned long long* const mine = xch + ((size_t)b * 2 + half) * 16;
+    const unsigned long long* const other = xch + ((size_t)b * 2 + (half ^ 1)) * 16;
+
+    // ---- (a) scene bbox, (b) Morton counting sort of all N points (as fps_cull_kernel)
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int k = tid; k < N; k += kThreads)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float v = p[3 * k + a];
+            lo[a] = fminf(lo[a], v);
+            hi[a] = fmaxf(hi[a], v);
+        }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = wave_fmin(lo[a]);
+        hi[a] = wave_fmax(hi[a]);
+    }
+    if (lane == 0)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) { s_red[a][w] = lo[a]; s_red[3 + a][w] = hi[a]; }
+    for (int i = tid; i < kCells; i += kThreads) s_hist[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        float l = s_red[a][0], h = s_red[3 + a][0];
+        for (int q = 1; q < kWaves; ++q) { l = fminf(l, s_red[a][q]); h = fmaxf(h, s_red[3 + a][q]); }
+        lo[a] = l;
+        hi[a] = 16.f / fmaxf(h - l, 1e-6f);
+    }
+    {
+        uint32_t cp[NSORT];
+#pragma unroll
+        for (int i = 0; i < NSORT; ++i) {
+            const int k = tid + i * kThreads;
+            cp[i] = 0xffffffffu;
+            if (k < N) {
+                uint32_t q[3];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    const int c = (int)((p[3 * k + a] - lo[a]) * hi[a]);
+                    q[a] = (uint32_t)min(max(c, 0), 15);
+                }
+                const uint32_t code = spread3(q[0]) | (spread3(q[1]) << 1) | (spread3(q[2]) << 2);
+                const uint32_t old = atomicAdd(&s_hist[code], 1u);
+                cp[i] = (code << 16) | old;
+            }
+        }
+        __syncthreads();
+        {
+            uint32_t v[4], sum = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { v[q] = s_hist[4 * tid + q]; sum += v[q]; }
+            uint32_t inc = sum;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t o = __shfl_up(inc, off);
+                if (lane >= off) inc += o;
+            }
+            if (lane == 63) s_scan[w] = inc;
+            __syncthreads();
+            uint32_t basew = 0;
+            for (int q = 0; q < w; ++q) basew += s_scan[q];
+            uint32_t run = basew + inc - sum;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { s_hist[4 * tid + q] = run; run += v[q]; }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < NSORT; ++i)
+            if (cp[i] != 0xffffffffu)
+                s_perm[s_hist[cp[i] >> 16] + (cp[i] & 0xffffu)] = (uint16_t)(tid + i * kThreads);
+    }
+    __syncthreads();
+
+    // ---- (c) this thread's slots: positions base + w*PW + i*64 + lane (< end), by rank
+    uint32_t rk[PPT];
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+        const int pos = base + w * PW + i * 64 + lane;
+        rk[i] = pos < end ? fps_rank(s_perm[pos], L) : 0xffffffffu;
+    }
+#pragma unroll
+    for (int pass = 0; pass < PPT; ++pass)
+#pragma unroll
+        for (int i = pass & 1; i + 1 < PPT; i += 2) {
+            const uint32_t a = rk[i], c = rk[i + 1];
+            rk[i] = min(a, c);
+            rk[i + 1] = max(a, c);
+        }
+    __syncthreads();   // every thread has read s_perm of its positions before the rewrite
+    float px[PPT], py[PPT], pz[PPT], td[PPT];
+    float wlo[3] = {INFINITY, INFINITY, INFINITY}, whi[3] = {-INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+        const int pos = base + w * PW + i * 64 + lane;
+        if (rk[i] != 0xffffffffu) {
+            const int k = fps_unrank(rk[i], L);
+            s_perm[pos] = (uint16_t)k;
+            const float x = p[3 * k], y = p[3 * k + 1], z = p[3 * k + 2];
+            const float mag = fmaf(z, z, fmaf(y, y, x * x));
+            px[i] = x; py[i] = y; pz[i] = z;
+            const bool skip = (double)mag <= 1e-3;
+            td[i] = skip ? -1.f : 1e10f;
+            if (!skip) {
+                wlo[0] = fminf(wlo[0], x); wlo[1] = fminf(wlo[1], y); wlo[2] = fminf(wlo[2], z);
+                whi[0] = fmaxf(whi[0], x); whi[1] = fmaxf(whi[1], y); whi[2] = fmaxf(whi[2], z);
+            }
+        } else {
+            px[i] = 0.f; py[i] = 0.f; pz[i] = 0.f; td[i] = -1.f;
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        wlo[a] = wave_fmin(wlo[a]);
+        whi[a] = wave_fmax(whi[a]);
+    }
+    __syncthreads();   // s_perm (this half's positions) complete before any tie lookup
+    const float x0 = p[0], y0 = p[1], z0 = p[2];
+    float x1 = x0, y1 = y0, z1 = z0;
+    float wtmax = INFINITY;
+    int wdist = __float_as_int(-1.f);
+    int wpos = 0;
+    float wx = 0.f, wy = 0.f, wz = 0.f;
+    bool lost = false;   // the partner never answered (spin limit): stop exchanging
+
+    for (int j = 1; j < M; ++j) {
+        const int buf = j & 1;
+        const float gx = fmaxf(fmaxf(wlo[0] - x1, x1 - whi[0]), 0.f);
+        const float gy = fmaxf(fmaxf(wlo[1] - y1, y1 - whi[1]), 0.f);
+        const float gz = fmaxf(fmaxf(wlo[2] - z1, z1 - whi[2]), 0.f);
+        const float lb = fmaf(gz, gz, fmaf(gy, gy, gx * gx));
+        if (lb < wtmax) {  // wave-uniform
+            float best = -1.f;
+            int bi = 0;
+            float sx = 0.f, sy = 0.f, sz = 0.f;
+#pragma unroll
+            for (int i = 0; i < PPT; ++i) {
+                const float dx = px[i] - x1, dy = py[i] - y1, dz = pz[i] - z1;
+                const float d = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                const float d2 = fminf(d, td[i]);
+                td[i] = d2;
+                const bool gt = d2 > best;
+                best = gt ? d2 : best;
+                bi = gt ? i : bi;
+                sx = gt ? px[i] : sx; sy = gt ? py[i] : sy; sz = gt ? pz[i] : sz;
+            }
+            const int bb = __float_as_int(best);
+            const int wm = wave_max_i32(bb);
+            wdist = wm;
+            wtmax = __int_as_float(wm);
+            if (wm >= 0) {
+                const unsigned long long cand = __ballot(bb == wm);
+                int wl;
+                if (__popcll(cand) == 1) {
+                    wl = __ffsll((long long)cand) - 1;
+                } else {
+                    uint32_t my = 0xffffffffu;
+                    if (bb == wm) my = fps_rank(s_perm[base + w * PW + bi * 64 + lane], L);
+                    const uint32_t mr = wave_min_u32(my);
+                    wl = __ffsll((long long)__ballot(my == mr)) - 1;
+                }
+                wx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sx), wl));
+                wy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sy), wl));
+                wz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sz), wl));
+                wpos = base + w * PW + __builtin_amdgcn_readlane(bi, wl) * 64 + wl;
+            }
+        }
+        if (lane == 0) {
+            s_pub[buf][w] = make_float4(wx, wy, wz, __int_as_float(wdist));
+            s_pos[buf][w] = wpos;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        // this half's winner (every wave reduces the 16 wave slots)
+        const float4 v = s_pub[buf][lane & (kWaves - 1)];
+        const int vp = s_pos[buf][lane & (kWaves - 1)];
+        const int dv = __float_as_int(v.w);
+        const int dm = __builtin_amdgcn_readfirstlane(row_max_i32(dv));
+        int hk = 0xffff;   // this half's winning point index (none: 0xffff)
+        float hx = x0, hy = y0, hz = z0;
+        uint32_t hr = 0xffffffffu;
+        if (dm >= 0) {
+            const unsigned long long cand = __ballot(dv == dm) & 0xffffull;
+            int ws;
+            if (__popcll(cand) == 1) {
+                ws = __ffsll((long long)cand) - 1;
+            } else {
+                const uint32_t r = dv == dm ? fps_rank(s_perm[vp], L) : 0xffffffffu;
+                const uint32_t rm = __builtin_amdgcn_readfirstlane(row_min_u32(r));
+                ws = __ffsll((long long)(__ballot(r == rm) & 0xffffull)) - 1;
+            }
+            hx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.x), ws));
+            hy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.y), ws));
+            hz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.z), ws));
+            hk = s_perm[__builtin_amdgcn_readlane(vp, ws)];
+            hr = fps_rank((uint32_t)hk, L);
+        }
+        // ---- swap candidates with the other half through L2: 5 tagged 64-bit words
+        //      (distance bits, point index, x, y, z) per (scene, half, iteration parity)
+        const uint32_t tag = (uint32_t)j;
+        if (tid == 0) {
+            unsigned long long* const slot = mine + 8 * buf;
+            const uint32_t val[5] = {(uint32_t)dm, (uint32_t)hk, __float_as_uint(hx),
+                                     __float_as_uint(hy), __float_as_uint(hz)};
+#pragma unroll
+            for (int q = 0; q < 5; ++q)
+                __hip_atomic_store(slot + q, xword(val[q], tag), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        uint32_t ov[5] = {0u, 0u, 0u, 0u, 0u};
+        uint32_t ot = 0u;
+        if (lane == 0 && !lost) {
+            const unsigned long long* const os = other + 8 * buf;
+            for (int spin = 0; spin < kPairSpin; ++spin) {
+                bool all = true;
+#pragma unroll
+                for (int q = 0; q < 5; ++q) {
+                    const unsigned long long x = __hip_atomic_load(os + q, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT);
+                    ov[q] = (uint32_t)x;
+                    all = all && (uint32_t)(x >> 32) == tag;
+                }
+                if (all) { ot = tag; break; }
+            }
+        }
+        // lane 0's words to the whole wave (scalar registers)
+        lost = lost || (uint32_t)__builtin_amdgcn_readfirstlane((int)ot) != tag;
+        const int odm = __builtin_amdgcn_readfirstlane((int)ov[0]);
+        const int ok = __builtin_amdgcn_readfirstlane((int)ov[1]);
+        const float ox = __int_as_float(__builtin_amdgcn_readfirstlane((int)ov[2]));
+        const float oy = __int_as_float(__builtin_amdgcn_readfirstlane((int)ov[3]));
+        const float oz = __int_as_float(__builtin_amdgcn_readfirstlane((int)ov[4]));
+        // the scene's winner: larger distance, equal distances -> smaller upstream rank
+        bool useO = !lost && odm > dm;
+        if (!lost && odm == dm && dm >= 0) useO = fps_rank((uint32_t)ok, L) < hr;
+        int pk;
+        if (useO) {
+            pk = ok;
+            x1 = ox; y1 = oy; z1 = oz;
+        } else if (dm >= 0) {
+            pk = hk;
+            x1 = hx; y1 = hy; z1 = hz;
+        } else {   // no candidate anywhere: upstream keeps thread 0's besti = 0
+            pk = 0xffff;
+            x1 = x0; y1 = y0; z1 = z0;
+        }
+        if (tid == 0) s_out[j] = (uint16_t)pk;
+    }
+    __syncthreads();
+    if (half) return;
+    idx += (size_t)b * M;
+    if (new_xyz) new_xyz += (size_t)b * M * 3;
+    for (int j = tid; j < M; j += kThreads) {
+        int k = 0;
+        if (j > 0 && s_out[j] != 0xffff) k = s_out[j];
+        idx[j] = k;
+        if (new_xyz) {
+            new_xyz[3 * j] = p[3 * k];
+            new_xyz[3 * j + 1] = p[3 * k + 1];
+            new_xyz[3 * j + 2] = p[3 * k + 2];
+        }
+    }
+}
+
 #ifdef OV3D_FPS_PROBE
 unsigned long long* g_probe_dbg = nullptr;
 #define OV3D_FPS_PROBE_ARG , g_probe_dbg
 #else
 #define OV3D_FPS_PROBE_ARG
 #endif
+
+// the two-workgroup kernel for 20480 < N <= 40960 (OV3D_FPS_PAIR=0: the one-workgroup
+// two-cluster kernel instead)
+bool fps_pair_enabled() {
+    const char* e = getenv("OV3D_FPS_PAIR");
+    return !(e && e[0] == '0');
+}
 
 template <int PPT>
 void launch_cull(const float* xyz, int B, int N, int M, int L, int32_t* idx, float* nx,
@@ -908,6 +1223,22 @@ extern "C" int ov3d_fps(const float* xyz, int B, int N, int M, int32_t* idx_out,
         else if (ppt <= 12) launch_cull<12>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
         else if (ppt <= 16) launch_cull<16>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
         else launch_cull<20>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
+    } else if (N <= 2 * kThreads * kMaxPPT && M <= kMaxOutLDS && fps_pair_enabled()) {
+        // two workgroups per scene, candidates swapped through L2 (fps_pair_kernel)
+        if (!workspace) return OV3D_EINVAL;
+        const size_t xbytes = (size_t)B * 2 * 16 * sizeof(unsigned long long);
+        if (hipMemsetAsync(workspace, 0, xbytes, s) != hipSuccess) return OV3D_ELAUNCH;
+        unsigned long long* xch = reinterpret_cast<unsigned long long*>(workspace);
+        const int half = (N + 1) / 2, ppt2 = (half + kThreads - 1) / kThreads;
+        if (ppt2 <= 12)
+            hipLaunchKernelGGL(fps_pair_kernel<12>, dim3(2 * B), dim3(kThreads), 0, s, xyz, B, N, M, L,
+                               xch, idx_out, new_xyz_out);
+        else if (ppt2 <= 16)
+            hipLaunchKernelGGL(fps_pair_kernel<16>, dim3(2 * B), dim3(kThreads), 0, s, xyz, B, N, M, L,
+                               xch, idx_out, new_xyz_out);
+        else
+            hipLaunchKernelGGL(fps_pair_kernel<20>, dim3(2 * B), dim3(kThreads), 0, s, xyz, B, N, M, L,
+                               xch, idx_out, new_xyz_out);
     } else if (N <= kThreads * (kPR + kPS) && M <= kMaxOutLDS) {
         if (!workspace) return OV3D_EINVAL;
         // chunk size of the workspace cluster's culling (OV3D_FPS_CHUNK: measurement knob)
@@ -942,6 +1273,8 @@ extern "C" void ov3d_fps_probe_set(unsigned long long* dbg) { g_probe_dbg = dbg;
 /* workspace floats ov3d_fps needs for (B, N) (16-byte aligned) */
 extern "C" long long ov3d_fps_workspace(int B, int N) {
     if (B <= 0 || N <= kThreads * kMaxPPT) return 0;
+    // (both kernels of 20480 < N <= 40960 may run: the pair kernel's exchange slots fit
+    // inside the two-cluster kernel's workspace)
     if (N <= kThreads * (kPR + kPS)) return (long long)B * kWaves * kPS * 64 * 4;
     return (long long)B * N;
 }

@@ -190,12 +190,135 @@ __device__ __forceinline__ void bin_max_grad(float a, float b, float g, float& g
 }
 __device__ __forceinline__ float sgn(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
 
-__global__ __launch_bounds__(128) void giou_bwd_aligned_kernel(
+// The rotated intersection area, differentiated: clip_poly<float> (the forward's arithmetic,
+// box_util.py:387-440 on float32 tensors) with each stage's vertices and their parents
+// recorded, the shoelace area (:591-596, |.| and the 0.5), then reverse mode back through the
+// stages: a vertex kept as is passes its gradient to its parent; an intersection point
+// q(cp1, cp2, s, e) (helper_computeIntersection, :387-396) sends J^T g to s and e (the clip
+// edge is the GT box: constant).  Stage 0 is rect1 = corners (3, 2, 1, 0) (x, z).
+struct ClipTrace {
+    P2<float> v[5][10];
+    int8_t pa[5][10], pb[5][10];   // stage s >= 1: parents in stage s - 1 (pb < 0: kept vertex)
+    int n[5];
+    int last;                      // final stage
+};
+
+__device__ __noinline__ float rot_area_grad(const float* c1, const float* c2, float g_area,
+                                            float* gc) {
+    ClipTrace T;
+    P2<float> clip[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        T.v[0][i].x = c1[(3 - i) * 3]; T.v[0][i].y = c1[(3 - i) * 3 + 2];
+        clip[i].x = c2[(3 - i) * 3]; clip[i].y = c2[(3 - i) * 3 + 2];
+    }
+    T.n[0] = 4;
+    T.last = 0;
+    P2<float> cp1 = clip[3];
+    for (int ci = 0; ci < 4; ++ci) {
+        const P2<float> cp2 = clip[ci];
+        const int nin = T.n[ci];
+        int nout = 0;
+        if (nin == 0) break;
+        int si = nin - 1;
+        for (int ii = 0; ii < nin; ++ii) {
+            const P2<float> s = T.v[ci][si], e = T.v[ci][ii];
+            const bool e_in = (cp2.x - cp1.x) * (e.y - cp1.y) > (cp2.y - cp1.y) * (e.x - cp1.x);
+            const bool s_in = (cp2.x - cp1.x) * (s.y - cp1.y) > (cp2.y - cp1.y) * (s.x - cp1.x);
+            if (e_in || s_in) {
+                if (e_in != s_in) {
+                    const float dc0 = cp1.x - cp2.x, dc1 = cp1.y - cp2.y;
+                    const float dp0 = s.x - e.x, dp1 = s.y - e.y;
+                    const float n1 = cp1.x * cp2.y - cp1.y * cp2.x;
+                    const float n2 = s.x * e.y - s.y * e.x;
+                    const float n3 = 1.f / (dc0 * dp1 - dc1 * dp0);
+                    if (nout < 10) {
+                        T.v[ci + 1][nout].x = (n1 * dp0 - n2 * dc0) * n3;
+                        T.v[ci + 1][nout].y = (n1 * dp1 - n2 * dc1) * n3;
+                        T.pa[ci + 1][nout] = (int8_t)si;
+                        T.pb[ci + 1][nout] = (int8_t)ii;
+                        ++nout;
+                    }
+                }
+                if (e_in && nout < 10) {
+                    T.v[ci + 1][nout] = e;
+                    T.pa[ci + 1][nout] = (int8_t)ii;
+                    T.pb[ci + 1][nout] = (int8_t)-1;
+                    ++nout;
+                }
+            }
+            si = ii;
+        }
+        T.n[ci + 1] = nout;
+        T.last = ci + 1;
+        cp1 = cp2;
+        if (nout == 0) break;
+    }
+    const int L = T.last, n = T.n[L];
+    if (n == 0) return 0.f;
+    float s1 = 0.f, s2 = 0.f;
+    for (int i = 0; i < n; ++i) {
+        const int im = (i == 0) ? n - 1 : i - 1;
+        s1 = s1 + T.v[L][i].x * T.v[L][im].y;
+        s2 = s2 + T.v[L][i].y * T.v[L][im].x;
+    }
+    const float S = s1 - s2;
+    const float area = 0.5f * fabsf(S);
+    if (g_area == 0.f) return area;
+    // d area / d S = 0.5 sign(S); dS/dx_k = y_{k-1} - y_{k+1}, dS/dy_k = x_{k+1} - x_{k-1}
+    const float gS = 0.5f * g_area * sgn(S);
+    P2<float> g[5][10];
+    for (int st = 0; st <= L; ++st)
+        for (int i = 0; i < 10; ++i) g[st][i].x = g[st][i].y = 0.f;
+    for (int k = 0; k < n; ++k) {
+        const int km = (k == 0) ? n - 1 : k - 1, kp = (k + 1 == n) ? 0 : k + 1;
+        g[L][k].x = gS * (T.v[L][km].y - T.v[L][kp].y);
+        g[L][k].y = gS * (T.v[L][kp].x - T.v[L][km].x);
+    }
+    for (int st = L; st >= 1; --st) {
+        const int ci = st - 1;
+        const P2<float> cp2 = clip[ci], cp1 = clip[(ci + 3) & 3];
+        const float dc0 = cp1.x - cp2.x, dc1 = cp1.y - cp2.y;
+        const float n1 = cp1.x * cp2.y - cp1.y * cp2.x;
+        for (int i = 0; i < T.n[st]; ++i) {
+            const P2<float> gq = g[st][i];
+            const int a = T.pa[st][i], bb = T.pb[st][i];
+            if (bb < 0) {
+                g[ci][a].x += gq.x;
+                g[ci][a].y += gq.y;
+                continue;
+            }
+            const P2<float> sv = T.v[ci][a], ev = T.v[ci][bb];
+            const float dp0 = sv.x - ev.x, dp1 = sv.y - ev.y;
+            const float n2 = sv.x * ev.y - sv.y * ev.x;
+            const float n3 = 1.f / (dc0 * dp1 - dc1 * dp0);
+            const float A = n1 * dp0 - n2 * dc0, Bq = n1 * dp1 - n2 * dc1;
+            const float gA = gq.x * n3, gB = gq.y * n3;
+            const float gden = -(n3 * n3) * (gq.x * A + gq.y * Bq);
+            const float gdp0 = gA * n1 - gden * dc1, gdp1 = gB * n1 + gden * dc0;
+            const float gn2 = -(gA * dc0 + gB * dc1);
+            g[ci][a].x += gdp0 + gn2 * ev.y;
+            g[ci][a].y += gdp1 - gn2 * ev.x;
+            g[ci][bb].x += -gdp0 - gn2 * sv.y;
+            g[ci][bb].y += -gdp1 + gn2 * sv.x;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        gc[(3 - i) * 3] += g[0][i].x;
+        gc[(3 - i) * 3 + 2] += g[0][i].y;
+    }
+    return area;
+}
+
+__global__ __launch_bounds__(128) void giou_bwd_kernel(
     const float* __restrict__ corners1, const float* __restrict__ corners2,
-    const int32_t* __restrict__ nums, int B, int K1, int K2, const float* __restrict__ gout,
+    const int32_t* __restrict__ nums, int B, int K1, int K2, int rotated_host,
+    const int32_t* __restrict__ rotated_dev, const float* __restrict__ gout,
     float* __restrict__ gc1_out) {
     const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (long long)B * K1) return;
+    const bool rotated = rotated_dev ? (*rotated_dev != 0) : (rotated_host != 0);
     const int b = (int)(t / K1);
     const int nk = nums ? nums[b] : K2;
     float c1[24], gc[24];
@@ -243,6 +366,10 @@ __global__ __launch_bounds__(128) void giou_bwd_aligned_kernel(
         const float wxr = rbx - ltx, wzr = rbz - ltz;
         const float wx = fmaxf(wxr, 0.f), wz = fmaxf(wzr, 0.f);
         const float non_rot = wx * wz;
+        // rotated: the clipped polygon's area where the axis-aligned overlap is nonzero
+        // (box_util.py:583-585), its gradient taken once gI is known (below)
+        float inter_area = non_rot;
+        if (rotated) inter_area = non_rot != 0.f ? rot_area_grad(c1, c2, 0.f, gc) : 0.f;
         float mn2[3], mx2[3];
         minmax_flip(c2, mn2, mx2);
         const float X = fmaxf(mx1[0], mx2[0]) - fminf(mn1[0], mn2[0]);
@@ -253,7 +380,7 @@ __global__ __launch_bounds__(128) void giou_bwd_aligned_kernel(
         const float sum_vols = v1 + v2;
         const bool good = (enc > 2e-8f && sum_vols > 4e-8f);
         if (!good) continue;  // g * 0: no gradient (NaN-free by construction of good)
-        const float I = non_rot * height;
+        const float I = inter_area * height;
         const float uraw = sum_vols - I;
         const float U = fmaxf(uraw, EPS);
         const float mU = (uraw >= EPS) ? 1.f : 0.f;
@@ -261,8 +388,8 @@ __global__ __launch_bounds__(128) void giou_bwd_aligned_kernel(
         const float gI = G * (1.f / U - mU * A);
         gv1 += G * mU * A;
         const float genc = G * (-U / (enc * enc));
-        // I = non_rot * height
-        const float gnon = gI * height, gh = gI * non_rot;
+        // I = inter_area * height
+        const float gnon = gI * height, gh = gI * inter_area;
         // height = clamp(ymax - ymin, 0)
         if (hraw >= 0.f) {
             bin_min_grad(c1[1], c2[1], gh, gc[1]);
@@ -270,15 +397,18 @@ __global__ __launch_bounds__(128) void giou_bwd_aligned_kernel(
             bin_max_grad(c1[13], c2[13], gh, tmp);
             gc[13] -= tmp;
         }
+        if (rotated) {   // through the clip (non_rot only selects the pairs)
+            if (non_rot != 0.f) rot_area_grad(c1, c2, gnon, gc);
+        }
         // non_rot = wx * wz
-        const float gwx = gnon * wz, gwz = gnon * wx;
-        if (wxr >= 0.f) {
+        const float gwx = rotated ? 0.f : gnon * wz, gwz = rotated ? 0.f : gnon * wx;
+        if (!rotated && wxr >= 0.f) {
             bin_min_grad(c1[0], c2[0], gwx, gc[0]);
             float tmp = 0.f;
             bin_max_grad(c1[6], c2[6], gwx, tmp);
             gc[6] -= tmp;
         }
-        if (wzr >= 0.f) {
+        if (!rotated && wzr >= 0.f) {
             bin_min_grad(c1[2], c2[2], gwz, gc[2]);
             float tmp = 0.f;
             bin_max_grad(c1[8], c2[8], gwz, tmp);
@@ -345,16 +475,23 @@ extern "C" int ov3d_giou3d(const float* corners1, const float* corners2, const i
     return OV3D_OK;
 }
 
-extern "C" int ov3d_giou3d_bwd_aligned(const float* corners1, const float* corners2,
-                                       const int32_t* nums, int B, int K1, int K2,
-                                       const float* grad_out, float* grad_corners1, void* stream) {
+extern "C" int ov3d_giou3d_bwd(const float* corners1, const float* corners2, const int32_t* nums,
+                               int B, int K1, int K2, int rotated, const int32_t* rotated_dev,
+                               const float* grad_out, float* grad_corners1, void* stream) {
     if (B < 0 || K1 < 0 || K2 < 0 || !corners1 || !corners2 || !grad_out || !grad_corners1)
         return OV3D_EINVAL;
     const long long total = (long long)B * K1;
     if (total == 0) return OV3D_OK;
-    hipLaunchKernelGGL(giou_bwd_aligned_kernel, dim3(ov3d_cdiv(total, 128)), dim3(128), 0,
-                       ov3d_stream(stream), corners1, corners2, nums, B, K1, K2, grad_out,
-                       grad_corners1);
+    hipLaunchKernelGGL(giou_bwd_kernel, dim3(ov3d_cdiv(total, 128)), dim3(128), 0,
+                       ov3d_stream(stream), corners1, corners2, nums, B, K1, K2, rotated,
+                       rotated_dev, grad_out, grad_corners1);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
+}
+
+extern "C" int ov3d_giou3d_bwd_aligned(const float* corners1, const float* corners2,
+                                       const int32_t* nums, int B, int K1, int K2,
+                                       const float* grad_out, float* grad_corners1, void* stream) {
+    return ov3d_giou3d_bwd(corners1, corners2, nums, B, K1, K2, 0, nullptr, grad_out,
+                           grad_corners1, stream);
 }

@@ -146,3 +146,58 @@ def all_gather_dict(data):
                 v = torch.cat(parts, dim=0)
             out[k] = v
     return out
+
+
+class _SyncBNRows(torch.autograd.Function):
+    """SyncBatchNorm over the rows of (R, C) on the host path (torch ops; the reference wraps
+    the model with convert_sync_batchnorm, main.py:427-431).  The same arithmetic as the
+    fused HIP BN launches (sa_fused.py / heads.py): float64 per-rank sums (Σx, Σx², R) and
+    backward sums (Σdy, Σdy·x̂), ONE all-reduce each way over `group`, statistics with the
+    global count; the weight / bias gradients stay rank-local (torch's SyncBatchNorm
+    semantics: DDP averages them with the other gradients).  torch's SyncBatchNorm runs on
+    GPU only; this keeps the CPU world>1 path (gloo tests) on the same semantics."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, group):
+        xd = x.double()
+        R, C = x.shape
+        tot = torch.cat([xd.sum(0), (xd * xd).sum(0), xd.new_tensor([float(R)])])
+        dist.all_reduce(tot, group=group)
+        n = tot[2 * C]
+        mean = tot[:C] / n
+        var = (tot[C: 2 * C] / n - mean * mean).clamp_min(0)
+        invstd = torch.rsqrt(var + eps)
+        if running_mean is not None:
+            with torch.no_grad():
+                running_mean.mul_(1 - momentum).add_(momentum * mean.to(running_mean.dtype))
+                running_var.mul_(1 - momentum).add_(
+                    momentum * (var * n / (n - 1)).to(running_var.dtype))
+        xhat = (xd - mean) * invstd
+        y = xhat * weight.double() + bias.double()
+        ctx.save_for_backward(xhat, weight, invstd, n)
+        ctx.group = group
+        return y.to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xhat, weight, invstd, n = ctx.saved_tensors
+        dyd = dy.double()
+        C = xhat.shape[1]
+        s_dy = dyd.sum(0)
+        s_dyx = (dyd * xhat).sum(0)
+        tot = torch.cat([s_dy, s_dyx])
+        dist.all_reduce(tot, group=ctx.group)
+        dx = (weight.double() * invstd) * (dyd - tot[:C] / n - xhat * (tot[C:] / n))
+        return dx.to(dy.dtype), s_dyx.to(weight.dtype), s_dy.to(weight.dtype), None, None, None, \
+            None, None
+
+
+def sync_batch_norm_rows(bn, x):
+    """train-mode SyncBatchNorm `bn` over rows x (R, C) across bn.process_group (host path)"""
+    group = bn.process_group if bn.process_group is not None else dist.group.WORLD
+    if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+    rm = bn.running_mean if bn.track_running_stats else None
+    rv = bn.running_var if bn.track_running_stats else None
+    return _SyncBNRows.apply(x, bn.weight, bn.bias, rm, rv,
+                             bn.momentum if bn.momentum is not None else 0.0, bn.eps, group)

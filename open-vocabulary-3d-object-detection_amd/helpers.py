@@ -90,7 +90,8 @@ class GenericMLP(nn.Module):
                     x = heads.bn_relu_rows(x, m, drop)
                     i += 3 if drop is not None else 2
                     continue
-                x = m(x)
+                from .pointnet2_modules import batch_norm_rows
+                x = batch_norm_rows(m, x) if isinstance(m, nn.SyncBatchNorm) else m(x)
             else:
                 x = m(x)
             i += 1

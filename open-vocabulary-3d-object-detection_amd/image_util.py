@@ -47,7 +47,11 @@ def _corner_signs(dtype, device):
 
 
 def project_boxes_2d(center, size, heading, Rtilt, K, img_h, img_w):
-    """center/size (B,Q,3), heading (B,Q), Rtilt/K (B,3,3), img_h/img_w (B,) -> (B,Q,4)."""
+    """center/size (B,Q,3), heading (B,Q), Rtilt/K (B,3,3), img_h/img_w (B,) -> (B,Q,4).
+    On the device: one HIP launch (csrc/project.hip, ov3d_project_box2d); the torch form
+    below is the host restatement (CPU parity runs)."""
+    if center.is_cuda:
+        return _project_device(center, size, heading, Rtilt, K, img_h, img_w)
     c = torch.cos(-heading)[..., None]
     s = torch.sin(-heading)[..., None]
     l, w, h = size[..., 0:1], size[..., 1:2], size[..., 2:3]
@@ -70,6 +74,26 @@ def project_boxes_2d(center, size, heading, Rtilt, K, img_h, img_w):
     hf = img_h.to(box.dtype)[:, None]
     lim = torch.stack([wf, hf, wf, hf], dim=-1)
     return torch.minimum(torch.clamp_min(box, 0), lim)
+
+
+def _project_device(center, size, heading, Rtilt, K, img_h, img_w):
+    from . import _native as nat
+    B, Q = heading.shape
+    f32 = dict(dtype=torch.float32)
+    c = nat.check(center.detach().to(**f32).contiguous(), "center", torch.float32, 3)
+    s = nat.check(size.detach().to(**f32).contiguous(), "size", torch.float32, 3)
+    h = nat.check(heading.detach().to(**f32).contiguous(), "heading", torch.float32, 2)
+    rt = Rtilt.detach().to(device=c.device, **f32).contiguous()     # .float() as image_util.py:276
+    kk = K.detach().to(device=c.device, **f32).contiguous()
+    ih = img_h.to(device=c.device, dtype=torch.int64).contiguous()
+    iw = img_w.to(device=c.device, dtype=torch.int64).contiguous()
+    if rt.shape != (B, 3, 3) or kk.shape != (B, 3, 3) or ih.shape != (B,) or iw.shape != (B,) \
+            or c.shape != (B, Q, 3) or s.shape != (B, Q, 3):
+        raise ValueError("project_boxes_2d: center/size (B,Q,3), heading (B,Q), Rtilt/K (B,3,3), "
+                         "img_h/img_w (B,)")
+    out = torch.empty((B, Q, 4), dtype=torch.float32, device=c.device)
+    nat.call("ov3d_project_box2d", c, s, h, B * Q, Q, B, rt, kk, ih, iw, out, like=c)
+    return out
 
 
 def clip_batch(images_1d, img_h, img_w, boxes):

@@ -22,6 +22,9 @@ def batch_norm_rows(bn, x):
     running statistics of `bn` (BatchNorm1d/2d or SyncBatchNorm): statistics over R,
     which are exactly the (N, H, W) positions of the channel-first module."""
     if isinstance(bn, nn.SyncBatchNorm):
+        from . import dist
+        if bn.training and not x.is_cuda and dist.is_distributed():
+            return dist.sync_batch_norm_rows(bn, x)   # torch's SyncBatchNorm is GPU-only
         return bn(x)
     training = bn.training or bn.running_mean is None
     if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:

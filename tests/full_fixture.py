@@ -59,7 +59,32 @@ def float64_host():
         torch.Tensor.float = orig
 
 
-def run(name, dataset, device, amp=None, f64=False):
+@contextlib.contextmanager
+def torch_bf16_path():
+    """The same model under bf16 autocast with every HIP dense / fused kernel switched off:
+    PyTorch's own autocast execution (hipBLASLt GEMMs, SDPA attention, torch BatchNorm /
+    LayerNorm / ReLU, torch weight gradients).  The precision baseline the HIP bf16 kernels
+    are measured against (they must be no less accurate against the float64 reference)."""
+    from ov3d_amd import attention, gemm, heads, resnorm, sa_fused, transformer
+    patches = [(sa_fused, "supported", lambda *a, **k: False),
+               (heads, "supported", lambda *a, **k: False),
+               (heads, "bn_relu_rows_ok", lambda *a, **k: False),
+               (resnorm, "supported", lambda *a, **k: False),
+               (attention, "supported", lambda *a, **k: False),
+               (transformer, "memory_kv_ok", lambda *a, **k: False),
+               (gemm, "_fused_ok", lambda *a, **k: False),
+               (gemm, "ROWS_GEMM_MAX_M", 0)]
+    saved = [(m, n, getattr(m, n)) for m, n, _ in patches]
+    for m, n, v in patches:
+        setattr(m, n, v)
+    try:
+        yield
+    finally:
+        for m, n, v in saved:
+            setattr(m, n, v)
+
+
+def run(name, dataset, device, amp=None, f64=False, grad_floor=None):
     """-> dict of error reports (max relative error per group, worst key)"""
     from ov3d_amd.criterion import build_criterion
     fx = fixture(name)
@@ -80,11 +105,14 @@ def run(name, dataset, device, amp=None, f64=False):
         crit = pin_matcher(build_criterion(args, cfg).to(device), fx, device)
         loss, ld = crit(out, dict(batch), clip=FakeRegionCLIP())
         loss.backward()
-    rep = {"out": [], "loss": [], "grad": [], "grad_norm": [], "grad_proj": []}
+    rep = {"out": [], "out_l2": [], "loss": [], "grad": [], "grad_norm": [], "grad_proj": []}
     layers = [out["outputs"]] + out["aux_outputs"]
     for li, lay in enumerate(layers):
         for k, ref in fixture_prefix(fx, f"out/{li}/").items():
-            rep["out"].append((rel(lay[k].detach().float().cpu().numpy(), ref), f"{li}/{k}"))
+            got = lay[k].detach().double().cpu().numpy()
+            rep["out"].append((rel(got, ref), f"{li}/{k}"))
+            rep["out_l2"].append((float(np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-30)),
+                                  f"{li}/{k}"))
     ref_ld = fixture_prefix(fx, "ld/")
     assert set(ld) == set(ref_ld), set(ld) ^ set(ref_ld)
     for k, v in ref_ld.items():
@@ -93,7 +121,7 @@ def run(name, dataset, device, amp=None, f64=False):
     named = dict(model.named_parameters())
     norms = fixture_prefix(fx, "gradnorm/")
     assert set(norms) == {n for n, p in named.items() if p.grad is not None}
-    floor = GRAD_FLOOR * float(fx["gradtotal"])
+    floor = (GRAD_FLOOR if grad_floor is None else grad_floor) * float(fx["gradtotal"])
     for n, gn in norms.items():
         g = named[n].grad.detach().double().cpu().numpy()
         den = max(gn, floor)
@@ -113,7 +141,7 @@ def worst(rep, k):
     return rep[k][0] if rep[k] else (0.0, None)
 
 
-REF32_KEY = {"out": "out/", "loss": "ld/", "grad": "grad/", "grad_norm": "gradnorm/",
+REF32_KEY = {"out": "out/", "out_l2": "out/", "loss": "ld/", "grad": "grad/", "grad_norm": "gradnorm/",
              "grad_proj": "gradproj/"}
 
 

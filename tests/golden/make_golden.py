@@ -77,6 +77,18 @@ def gen_giou(R):
     (g * G).sum().backward()
     out.update(grad_c1=c1.numpy(), grad_c2=c2.numpy(), grad_nums=nums.numpy().astype(np.int32),
                grad_G=G.numpy(), grad_giou=g.detach().numpy(), grad_dc1=c1g.grad.numpy())
+    # autograd of the differentiable ROTATED path (box_util.py:579-600: the Sutherland-Hodgman
+    # clip on tensors, differentiated through every intersection vertex)
+    _, _, _, c1 = rand_boxes(rs, cfg, 2, 12, True)
+    _, _, _, c2 = rand_boxes(rs, cfg, 2, 9, True)
+    c2[:, :8] = c1[:, :8] + torch.tensor(rs.uniform(-0.25, 0.25, (2, 8, 1, 3)), dtype=torch.float32)
+    nums = torch.tensor([9, 6])
+    G = torch.tensor(rs.randn(2, 12, 9), dtype=torch.float32)
+    c1g = c1.clone().requires_grad_(True)
+    g = bu.generalized_box3d_iou(c1g, c2, nums, rotated_boxes=True, needs_grad=True)
+    (g * G).sum().backward()
+    out.update(rgrad_c1=c1.numpy(), rgrad_c2=c2.numpy(), rgrad_nums=nums.numpy().astype(np.int32),
+               rgrad_G=G.numpy(), rgrad_giou=g.detach().numpy(), rgrad_dc1=c1g.grad.numpy())
     np.savez_compressed(os.path.join(HERE, "giou.npz"), **out)
 
 

@@ -131,7 +131,8 @@ def _drop_key(b, h):
 
 
 @pytest.mark.parametrize("Lq,Lk,B,H,nsplit", [(128, 200, 2, 2, 1), (256, 256, 1, 3, 1),
-                                              (128, 2048, 2, 2, 8), (96, 64, 2, 1, 1)])
+                                              (128, 2048, 2, 2, 8), (96, 64, 2, 1, 1),
+                                              (1024, 1024, 1, 2, 1), (1024, 800, 1, 1, 1)])
 def test_attention_drop_bits_layouts(cuda, Lq, Lk, B, H, nsplit):
     """The forward's stored drop bits, both layouts, decoded bit by bit against the hash."""
     from ov3d_amd import _native, attention as A
@@ -426,3 +427,34 @@ def test_short_attention_one_launch_backward_equals_two(cuda, L, B, p):
     finally:
         lib.ov3d_attn_small_bwd(prev)
     assert torch.equal(grads[0], grads[1])
+
+
+@pytest.mark.parametrize("Lq,Lk,B,H,masked", [(1024, 1024, 2, 4, False), (2048, 2048, 1, 2, False),
+                                              (1024, 1000, 2, 2, True)])
+def test_forward_with_drop_bits_ahead_equals_hashing_forward(cuda, monkeypatch, Lq, Lk, B, H, masked):
+    """Long attentions take their drop bits from attn_dropgen_kernel and the forward reads
+    them (BITS); the outputs, lse and both stored bit layouts equal the hashing forward's
+    bit for bit (OV3D_ATTN_DROPGEN_MIN: -1 = never ahead, 0 = always)."""
+    from ov3d_amd import _native, attention as A
+    lib = _native.load()
+    torch.manual_seed(Lq + H)
+    E = H * 64
+    q = torch.randn(Lq, B, E, device=cuda).to(torch.bfloat16)
+    k = torch.randn(Lk, B, E, device=cuda).to(torch.bfloat16)
+    v = torch.randn(Lk, B, E, device=cuda).to(torch.bfloat16)
+    mask = None
+    if masked:
+        mask = A.pack_mask(torch.rand(B, Lq, Lk, device=cuda) * 2.0, 1.0)
+    seed = torch.tensor([12345], dtype=torch.int64, device=cuda)
+    res = []
+    for mode in ("-1", "0"):
+        monkeypatch.setenv("OV3D_ATTN_DROPGEN_MIN", mode)
+        o = torch.empty(Lq, B, E, dtype=torch.bfloat16, device=cuda)
+        lse = torch.empty(B * H, Lq, device=cuda)
+        bits = torch.zeros(lib.ov3d_attn_dropbits_words(B, H, Lq, Lk), dtype=torch.int32, device=cuda)
+        _native.call("ov3d_attn_fwd_masked", q, k, v, E, E, E, B, H, Lq, Lk, 0.125, 0.1, seed, 3, o,
+                     E, lse, bits, None, 1, mask.words if mask is not None else None, like=q)
+        torch.cuda.synchronize()
+        res.append((o, lse, bits))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

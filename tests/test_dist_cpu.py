@@ -145,3 +145,101 @@ def test_ddp_gradients_equal_rank_average(shim, monkeypatch):
     assert checked > 50
     for r in range(WORLD):
         assert abs(res[r]["loss"].item() - losses[r]) <= 1e-5 * abs(losses[r])
+
+
+def _slice_outputs(out, r):
+    """scene r of the model outputs (every tensor is (B, Q, ...))"""
+    def one(d):
+        return {k: v[r: r + 1] for k, v in d.items()}
+    return {"outputs": one(out["outputs"]), "aux_outputs": [one(a) for a in out["aux_outputs"]]}
+
+
+def _train_rank(rank, port, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    torch.set_num_threads(2)
+    from oracle import torch_shim
+    from helpers import batch_from_fixture as bff, build_model_from_fixture as bmf, fixture as fxl, ov3d as pkg
+    _init(rank, port)
+    torch_shim.install(pkg)
+    from ov3d_amd.criterion import build_criterion
+    fx = fxl("model_sun.npz")
+    from full_fixture import float64_host
+    model, cfg, args = bmf(fx, "cpu", "sunrgbd")
+    args.loss_2dalignment_weight = 0.0
+    model = model.double().train()   # batch-statistics BN; the fixture's dropouts are all 0
+    # the reference's data-parallel semantics (main.py:427-431): SyncBatchNorm + the DDP
+    # gradient mean.  The product's step has no DDP wrapper (torch's refuses SyncBatchNorm on
+    # CPU modules anyway): ONE all-reduce of every gradient, averaged (FusedAdamW on the GPU,
+    # dist.all_reduce_coalesced here)
+    from ov3d_amd import dist as pdist
+    model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
+    crit = build_criterion(args, cfg)
+    batch = {k: (v.double() if v.is_floating_point() else v)[rank: rank + 1]
+             for k, v in bff(fx, "cpu").items()}
+    with float64_host():
+        loss = _step(model, crit, batch)
+    named = [(n, p) for n, p in model.named_parameters() if p.grad is not None]
+    avg = pdist.all_reduce_coalesced([p.grad for _, p in named], average=True)
+    grads = {n: g.clone() for (n, _), g in zip(named, avg)}
+    bufs = {n: b.clone() for n, b in model.named_buffers()}
+    torch.save({"loss": loss.detach(), "grads": grads, "bufs": bufs}, os.path.join(out_dir, f"tr{rank}.pt"))
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_ddp_syncbn_train_step_equals_global_batch(shim, monkeypatch):
+    """§8(e): 2 ranks x 1 scene (train mode: SyncBatchNorm batch statistics over both ranks,
+    the gradient mean by one all-reduce, num_boxes all-reduced) == 1 process x 2 scenes,
+    both in float64 (so ReLU / max-pool decisions cannot flip between the two orders of
+    summation and the comparison is of the semantics: 1e-6, the few float32 roundings left
+    on the host path -- the index ops' coordinates, the matcher cost -- turn 1e-16 summation-
+    order differences into single float32 ulps): the same B=2 forward (BatchNorm
+    over both scenes), each scene's loss with the global num_boxes, their mean backpropagated
+    (what DDP's gradient average of the per-rank losses is).  Gradients, losses and the BN
+    running statistics."""
+    from ov3d_amd import criterion as crit_mod
+    torch.set_num_threads(4)
+    from full_fixture import float64_host
+    fx = fixture("model_sun.npz")
+    full = {k: (v.double() if v.is_floating_point() else v)
+            for k, v in batch_from_fixture(fx, "cpu").items()}
+    nbox = full["gt_box_present"].sum(dim=1)
+    monkeypatch.setattr(crit_mod, "all_reduce_average", lambda t: nbox.sum() / WORLD)
+    model, cfg, args = build_model_from_fixture(fx, "cpu", "sunrgbd")
+    args.loss_2dalignment_weight = 0.0
+    model = model.double().train()
+    crit = crit_mod.build_criterion(args, cfg)
+    with float64_host():
+        out = model({k: full[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")})
+        losses = []
+        for r in range(WORLD):
+            loss_r, _ = crit(_slice_outputs(out, r), {k: v[r: r + 1] for k, v in full.items()})
+            losses.append(loss_r)
+        (sum(losses) / WORLD).backward()
+    ref = {n: p.grad for n, p in model.named_parameters() if p.grad is not None}
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_train_rank, args=(_free_port(), d), nprocs=WORLD, join=True)
+        res = [torch.load(os.path.join(d, f"tr{r}.pt"), weights_only=True) for r in range(WORLD)]
+    assert set(res[0]["grads"]) == set(ref)
+    checked = 0
+    for n, g in ref.items():
+        g0, g1 = res[0]["grads"][n], res[1]["grads"][n]
+        assert torch.equal(g0, g1), n
+        if g.abs().max() > 1e-8:
+            err = (g0.double() - g.double()).norm() / g.double().norm()
+            assert err < 1e-6, (n, err.item())
+            checked += 1
+    assert checked > 50
+    for r in range(WORLD):
+        assert abs(res[r]["loss"].item() - losses[r].item()) <= 1e-9 * abs(losses[r].item())
+    # SyncBN running statistics == plain BN's over the whole batch, identical on both ranks
+    nb = 0
+    for n, b in model.named_buffers():
+        if n.endswith(("running_mean", "running_var")):
+            torch.testing.assert_close(res[0]["bufs"][n], b, rtol=1e-7, atol=1e-12, msg=n)
+            assert torch.equal(res[0]["bufs"][n], res[1]["bufs"][n]), n
+            nb += 1
+    assert nb >= 16

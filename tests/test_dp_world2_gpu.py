@@ -1,0 +1,123 @@
+"""Data-parallel step at world size 2 on ONE GPU: two processes on cuda:0 over gloo (RCCL
+refuses two ranks on one device; gloo all-reduces device tensors through the host).  The
+bf16 product step as bench.py runs it eagerly -- fused SA MLP, heads and projection BN row
+kernels with SyncBatchNorm statistics all-reduced inside their launches (sa_fused.py,
+heads.py), num_boxes all-reduced by the criterion, the gradient mean by one all-reduce --
+against the single-process step on both scenes (BatchNorm over both, each scene's loss with
+the global num_boxes, their mean).  Reference semantics: main.py:427-431 (SyncBatchNorm +
+DDP), criterion.py:425."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from helpers import ROOT
+
+pytestmark = pytest.mark.gpu
+WORLD = 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _setup():
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ov3d_import
+    ov3d_import.load()
+    from bench import default_args
+    import ov3d_amd
+    from ov3d_amd import synthetic
+    from ov3d_amd.dataset_config import SunrgbdDatasetConfig
+    args = default_args(enc_dropout=0.0, dec_dropout=0.0, mlp_dropout=0.0, preenc_npoints=512,
+                        nqueries=64)
+    cfg = SunrgbdDatasetConfig()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model, _ = ov3d_amd.build_model(args, cfg, text_embedding=synthetic.text_embedding())
+    model = model.to(dev).train()
+    crit = ov3d_amd.build_criterion(args, cfg).to(dev)
+    batch = synthetic.make_batch(WORLD, seed=12, num_points=4096, device=dev)
+    return model, crit, batch, dev
+
+
+def _inputs(b):
+    return {k: b[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")}
+
+
+def _slice_outputs(out, r):
+    def one(d):
+        return {k: v[r: r + 1] for k, v in d.items()}
+    return {"outputs": one(out["outputs"]), "aux_outputs": [one(a) for a in out["aux_outputs"]]}
+
+
+def _rank(rank, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(WORLD), LOCAL_RANK="0")
+    torch.distributed.init_process_group("gloo", init_method="env://", world_size=WORLD, rank=rank)
+    model, crit, batch, dev = _setup()
+    from ov3d_amd import dist as pdist
+    model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
+    b = {k: v[rank: rank + 1] for k, v in batch.items()}
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = model(_inputs(b))
+    loss, _ = crit(out, b)
+    loss.backward()
+    named = [(n, p) for n, p in model.named_parameters() if p.grad is not None]
+    avg = pdist.all_reduce_coalesced([p.grad for _, p in named], average=True)
+    torch.save({"loss": loss.detach().cpu(),
+                "grads": {n: g.float().cpu() for (n, _), g in zip(named, avg)},
+                "bufs": {n: t.cpu() for n, t in model.named_buffers()}},
+               os.path.join(out_dir, f"r{rank}.pt"))
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_world2_step_equals_global_batch_step(cuda):
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_rank, args=(_free_port(), d), nprocs=WORLD, join=True)
+        res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(WORLD)]
+    from ov3d_amd import criterion as crit_mod
+    from ov3d_amd import dist as pdist
+    model, crit, batch, dev = _setup()
+    nbox = batch["gt_box_present"].sum(dim=1)
+    # each scene's loss with the GLOBAL num_boxes (criterion.py:425 all_reduce_average over 2
+    # ranks): the criterion's own call and the fused set-loss's target_counts read these
+    saved = (crit_mod.all_reduce_average, pdist.all_reduce_average, pdist.get_world_size)
+    crit_mod.all_reduce_average = pdist.all_reduce_average = lambda t: nbox.sum() / WORLD
+    pdist.get_world_size = lambda: WORLD
+    try:
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model(_inputs(batch))
+        losses = [crit(_slice_outputs(out, r), {k: v[r: r + 1] for k, v in batch.items()})[0]
+                  for r in range(WORLD)]
+        (sum(losses) / WORLD).backward()
+    finally:
+        crit_mod.all_reduce_average, pdist.all_reduce_average, pdist.get_world_size = saved
+    for r in range(WORLD):
+        assert abs(res[r]["loss"].item() - losses[r].item()) <= 5e-3 * abs(losses[r].item()), r
+    checked = 0
+    for n, p in model.named_parameters():
+        if p.grad is None:
+            continue
+        g = p.grad.float().cpu()
+        assert torch.equal(res[0]["grads"][n], res[1]["grads"][n]), n
+        if g.norm() > 1e-6:
+            err = ((res[0]["grads"][n] - g).norm() / g.norm()).item()
+            assert err < 3e-2, (n, err)
+            checked += 1
+    assert checked > 100
+    nb = 0
+    for n, t in model.named_buffers():
+        if n.endswith(("running_mean", "running_var")):
+            torch.testing.assert_close(res[0]["bufs"][n], t.cpu(), rtol=2e-2, atol=2e-3, msg=n)
+            torch.testing.assert_close(res[0]["bufs"][n], res[1]["bufs"][n], rtol=0, atol=0, msg=n)
+            nb += 1
+    assert nb >= 16

@@ -20,7 +20,8 @@ def scene_batch(B, N, seed, uniform=False):
 @pytest.mark.parametrize("B,N,M", [(8, 20000, 2048), (8, 2048, 128), (2, 40000, 1024),
                                    (3, 2048, 1024), (2, 1000, 64), (4, 300, 17), (2, 37, 37),
                                    (1, 1, 4), (2, 20480, 8), (2, 20481, 8), (1, 40960, 512),
-                                   (1, 40961, 64), (8, 40000, 2048)])
+                                   (1, 40961, 64), (8, 40000, 2048), (3, 30000, 700),
+                                   (2, 20482, 2048)])
 def test_fps_bit_exact(cuda, B, N, M):
     from ov3d_amd import pointnet2_utils as pu
     xyz = scene_batch(B, N, seed=N + M) if N >= 64 else torch.rand(B, N, 3)
@@ -55,6 +56,7 @@ def test_fps_ties_and_skipped_points(cuda, N):
                                                (2, 1001, 100, 0.3, 16, False),
                                                (3, 1000, 99, 0.3, 16, False),   # one per wave
                                                (8, 40000, 1024, 0.4, 32, True),
+                                               (8, 40000, 2048, 0.2, 64, False),  # C4 pre-encoder
                                                (2, 500, 64, 0.05, 8, True)])
 def test_ball_query_bit_exact(cuda, B, N, M, r, S, uniform):
     from ov3d_amd import pointnet2_utils as pu
@@ -164,6 +166,25 @@ def test_giou_backward_matches_reference_autograd(cuda):
     np.testing.assert_allclose(g.detach().cpu().numpy(), fx["grad_giou"], atol=2e-6)
     (g * torch.from_numpy(fx["grad_G"]).to(cuda)).sum().backward()
     np.testing.assert_allclose(c1.grad.cpu().numpy(), fx["grad_dc1"], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("flag", ["host", "device"])
+def test_rotated_giou_backward_matches_reference_autograd(cuda, flag):
+    """d(sum(G * giou))/dcorners1 through the rotated Sutherland-Hodgman clip (the reference's
+    TorchScript autograd, box_util.py:387-440, 579-600), rotated given on the host or as the
+    criterion's device flag"""
+    from ov3d_amd.box_util import generalized_box3d_iou
+    fx = fixture("giou.npz")
+    c1 = torch.from_numpy(fx["rgrad_c1"]).to(cuda).requires_grad_(True)
+    rot = True if flag == "host" else torch.ones((), dtype=torch.int32, device=cuda)
+    g = generalized_box3d_iou(c1, torch.from_numpy(fx["rgrad_c2"]).to(cuda),
+                              torch.from_numpy(fx["rgrad_nums"]).to(cuda), rotated_boxes=rot,
+                              needs_grad=True)
+    np.testing.assert_allclose(g.detach().cpu().numpy(), fx["rgrad_giou"], atol=2e-6)
+    (g * torch.from_numpy(fx["rgrad_G"]).to(cuda)).sum().backward()
+    ref = fx["rgrad_dc1"]
+    assert np.abs(ref).max() > 0.1             # the clip's gradient is exercised
+    np.testing.assert_allclose(c1.grad.cpu().numpy(), ref, rtol=1e-4, atol=2e-5)
 
 
 # ------------------------------------------------------------------- NMS

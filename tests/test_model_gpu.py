@@ -75,6 +75,50 @@ def test_full_size_train_step_properties(cuda):
     assert (bq[..., 1:] >= bq[..., :1]).all()   # padded with the first hit, ascending
 
 
+def test_full_size_c4_train_step_properties(cuda):
+    """BASELINE config C4 shapes (ScanNet: B=8, 40000 points + colour, masked encoder with
+    the interim SA, 256 queries, GIoU loss, enc_dropout 0.3), bf16: the HIP kernels of the
+    masked path run (packed mask, masked flash attention, interim SA row kernels, the
+    neighbour max-pool), the step is finite, and the sampling invariants hold at N=40000."""
+    import ov3d_amd
+    from ov3d_amd import _native, synthetic
+    from ov3d_amd.dataset_config import ScannetDatasetConfig
+    from bench import WORKLOADS, default_args
+    wl = WORKLOADS["scannet"]
+    args = default_args(**wl["args"])
+    cfg = ScannetDatasetConfig()
+    torch.manual_seed(0)
+    model, _ = ov3d_amd.build_model(args, cfg, text_embedding=synthetic.text_embedding(cfg.num_semcls + 1))
+    model = model.to(cuda).train()
+    crit = ov3d_amd.build_criterion(args, cfg).to(cuda)
+    batch = synthetic.make_batch(8, seed=2, num_points=wl["points"], device=cuda, dataset="scannet",
+                                 use_color=True)
+    inputs = {k: batch[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")}
+    _native.census_start()
+    try:
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model(inputs)
+        loss, ld = crit(out, batch)
+        loss.backward()
+        torch.cuda.synchronize()
+    finally:
+        called = _native.census_stop()
+    for k in ("ov3d_attn_mask_pack", "ov3d_attn_fwd_masked", "ov3d_attn_bwd_masked", "ov3d_nbr_max_fwd",
+              "ov3d_nbr_max_bwd", "ov3d_giou3d_bwd", "ov3d_sa_layer_pool_fwd", "ov3d_fps",
+              "ov3d_ball_query"):
+        assert called.get(k), (k, sorted(called))
+    assert called.get("ov3d_group_bwd_csr") or called.get("ov3d_group_bwd"), sorted(called)
+    assert torch.isfinite(loss) and len(ld) == 56
+    assert out["outputs"]["sem_cls_logits"].shape[:2] == (8, 256)
+    gn = torch.nn.utils.clip_grad_norm_(model.parameters(), 0.1)
+    assert torch.isfinite(gn) and gn > 0
+    from ov3d_amd import pointnet2_utils as pu
+    idx, nx = pu.furthest_point_sample_gather(batch["point_clouds"][..., :3].contiguous(), 2048)
+    assert (idx[:, 0] == 0).all()
+    for b in range(8):
+        assert torch.unique(idx[b]).numel() == 2048
+
+
 def test_graphed_step_equals_eager(cuda):
     """hipGraph replay of forward+backward gives the eager results (dropout off)."""
     import copy

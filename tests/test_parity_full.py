@@ -84,7 +84,7 @@ BF16_KERNELS = {
                 "ov3d_ball_query", "ov3d_hungarian"),
     "scannet": ("ov3d_sa_layer_pool_fwd", "ov3d_attn_fwd_masked", "ov3d_attn_bwd_masked",
                 "ov3d_attn_mask_pack", "ov3d_resnorm_fwd", "ov3d_rows_bn_apply", "ov3d_rows_gemm",
-                "ov3d_set_loss_bwd", "ov3d_giou3d_bwd_aligned", "ov3d_nbr_max_fwd", "ov3d_fps"),
+                "ov3d_set_loss_bwd", "ov3d_giou3d_bwd", "ov3d_nbr_max_fwd", "ov3d_fps"),
 }
 
 
