@@ -59,7 +59,8 @@ def test_disk_read_pbox_image_feature(tree):
         assert st.extras["image_width"][i] == img.shape[1]
 
 
-def test_image_without_reader_raises_clearly(tree):
+def test_image_without_reader_raises_clearly(tree, monkeypatch):
+    monkeypatch.setitem(sys.modules, "cv2", None)    # absent (other tests may stub it)
     with pytest.raises(ImportError, match="image_reader"):
         sunrgbd.SunrgbdDetectionDataset(SunrgbdDatasetConfig(), split_set="train",
                                         root_dir=tree["root"], use_image=True,
