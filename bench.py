@@ -318,7 +318,7 @@ def main():
         raise SystemExit("the captured data-parallel step needs --optim fused")
     model, crit, opt = build(args, device, ddp=world > 1 and not use_graph, capturable=use_graph,
                              sync_bn=dp, allreduce=dp, dataset=dataset)
-    if use_graph and not cli.no_defer_wgrad:
+    if not cli.no_defer_wgrad and not (world > 1 and not use_graph):
         from ov3d_amd import gemm
         gemm.DEFER_WGRAD = True   # one grouped weight-gradient launch per backward (not under DDP)
     clip = build_regionclip(device) if wl["use_image"] else None

@@ -301,6 +301,30 @@ int ov3d_project_box2d(const float* center, const float* size, const float* head
                        int Q, int B, const float* Rtilt, const float* K, const int64_t* img_h,
                        const int64_t* img_w, float* out, void* stream);
 
+/* Output layers of the five prediction heads + the query <-> text alignment, one launch.
+ * Replaces the last Conv1d of each GenericMLP head (models/model_3detr.py:_build_heads,
+ * models/helpers.py:45-112) and sem_cls_head = Linear(640, T, bias=False) over the visual
+ * embedding (model_3detr.py:152-154, 237-238).
+ *   z (R, ldz) bf16 hidden rows: visual head columns [0, 256), box head i at kcol[i]
+ *   wv (Nv, 256) bf16, bv (Nv) f32 -> out_v (R, Nv) f32 (Nv % 32 == 0)
+ *   text (T, Nv) f32 (T <= ov3d_heads_out_max_text(); null = no alignment) -> logits f32,
+ *     row-major (R, T) when lq == 0, else the reference's transposed layout of quirk Q8:
+ *     (lb, q, t) at lb*lq*T + t*lq + q
+ *   box head i (ns <= 4): ws[i] (n[i] <= 32, 256) bf16, bs[i] (n[i]) f32 ->
+ *     out_s[:, ocol[i] : ocol[i] + n[i]] of (R, Ns) f32 */
+int ov3d_heads_out_max_text(void);
+int ov3d_heads_out_fwd(const void* z, long long ldz, int R, const void* wv, const float* bv, int Nv,
+                       const float* text, int T, int lq, float* out_v, float* logits, int ns,
+                       const void* const* ws, const float* const* bs, const int* n,
+                       const int* kcol, const int* ocol, float* out_s, int Ns, void* stream);
+/* Its backward: gvb = bf16(gv + glog . text) (R, Nv); gsb = bf16(gs) (R, Ns); the box heads'
+ * input gradient dz[:, kcol[i] + c] = bf16(sum_j gsb[:, ocol[i] + j] ws[i][j, c]), c < 256
+ * (dz (R, lddz) bf16; its visual columns are left to the caller's dgrad GEMM on gvb). */
+int ov3d_heads_out_bwd(const float* gv, const float* glog, const float* text, int R, int Nv, int T,
+                       int lq, const float* gs, int Ns, int ns, const void* const* ws,
+                       const int* n, const int* kcol, const int* ocol, void* gvb, void* gsb,
+                       void* dz, long long lddz, void* stream);
+
 /* ROIAlign forward on channels-last features.  Replaces the ROIAlignV2 pooler of
  * CLIPRes5ROIHeads (detectron2 ROIPooler -> torchvision roi_align, aligned=True)
  * [upstream RegionCLIP] used by clip.inference at criterion.py:397.

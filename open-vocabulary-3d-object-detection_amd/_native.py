@@ -99,6 +99,8 @@ _SIGS = {
     "ov3d_ap_match": "ppppiiiidpp",
     "ov3d_ap_curve": "plppiplppp",
     "ov3d_project_box2d": "pppliipppppp",
+    "ov3d_heads_out_fwd": "plippipiippippppppip",
+    "ov3d_heads_out_bwd": "pppiiiipiippppppplp",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
                           "ov3d_attn_dropbits_words", "ov3d_attn_maskbits_words", "ov3d_fps_workspace", "ov3d_attn_small_bwd", "ov3d_set_loss_fwd_parts",
@@ -107,7 +109,7 @@ EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_
                           "ov3d_resnorm_supported", "ov3d_resnorm_bwd_parts",
                           "ov3d_adamw_chunk", "ov3d_wgrad_group_workspace",
                           "ov3d_rows_gemm_supported", "ov3d_sa_dy_fused_supported",
-                          "ov3d_tile_gemm_supported", "ov3d_sun_range_parts")
+                          "ov3d_tile_gemm_supported", "ov3d_sun_range_parts", "ov3d_heads_out_max_text")
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_longlong, "f": ctypes.c_float,
        "d": ctypes.c_double}
@@ -168,6 +170,8 @@ def load():
         lib.ov3d_tile_gemm_supported.restype = ctypes.c_int
         lib.ov3d_sun_range_parts.argtypes = [ctypes.c_int]
         lib.ov3d_sun_range_parts.restype = ctypes.c_int
+        lib.ov3d_heads_out_max_text.argtypes = []
+        lib.ov3d_heads_out_max_text.restype = ctypes.c_int
         lib.ov3d_version.argtypes = []
         lib.ov3d_version.restype = ctypes.c_char_p
         _lib = lib

@@ -30,6 +30,7 @@
 // Split-K (grid.z) serves the 128-query decoder attention: partial (O, m, l) per
 // key split, merged by attn_combine_kernel.
 #include <math.h>
+#include <type_traits>
 #include <stdlib.h>
 
 #include "common.h"
@@ -209,6 +210,25 @@ __device__ __forceinline__ bf16x8 v_operand(const bf16* Vs, int lane, int dt, in
     return a;
 }
 
+// 0xFFFFFFFF where bit b of w is set, else 0 (one v_bfe_i32; written as asm so that the
+// masking below stays bfe + bfi instead of the compiler's bit test + compare + select)
+__device__ __forceinline__ uint32_t bit_mask(uint32_t w, int b) {   // b: a constant after unrolling
+    uint32_t m;
+    asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(w), "s"(b));
+    return m;
+}
+
+// -inf where bit b of w is set (masked key), else x: v_bfe_i32 + v_bfi_b32 (asm: hipcc turns
+// the select into xor + bitop3).  Only for values that are NOT an MFMA's result: the
+// compiler's MFMA -> VALU hazard padding does not see inside inline asm, so the masks are
+// applied to the score accumulators' initial values (-inf + products = -inf).
+__device__ __forceinline__ float neg_inf_if(float x, uint32_t w, int b) {
+    const uint32_t m = bit_mask(w, b);
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "s"(0xFF800000u), "v"(__builtin_bit_cast(uint32_t, x)));
+    return __builtin_bit_cast(float, r);
+}
+
 // score bit of element i of score tile t in a query-major (drop / mask) word
 __device__ __forceinline__ constexpr int score_bit(int t, int i) { return ((i & 1) << 4) + 8 * t + (i >> 1); }
 
@@ -281,6 +301,9 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     uint32_t* const wk_lane = (DROP && !BITS) ? a.wk + ((size_t)(q0 >> 5) * gridDim.y + bh) * ((size_t)a.nkt * 64) +
                                          drop_key(r, h) : nullptr;
     uint32_t dw_prev = 0;   // drop word of the tile before this one
+    // BITS: this tile's drop word, loaded one tile ahead (its latency off the softmax)
+    uint32_t dw_cur = 0, dw_next = 0;
+    uint32_t mw_cur = 0, mw_next = 0;   // MASK: the same for the mask word
     // mask words of this lane (query q0 + r, half h), one per 64-key tile
     const uint32_t* const mrow = MASK ? a.mq + ((size_t)b * a.Lq + (active ? q0 + r : 0)) * 2 + h : nullptr;
     const size_t mtile = (size_t)a.B * a.Lq * 2;
@@ -296,6 +319,14 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     const size_t k0off = (size_t)b * a.sk + hh * D + 8 * (tid & 7) + (size_t)(tid >> 3) * rowk;
     const size_t v0off = (size_t)b * a.sv + hh * D + 8 * (tid & 7) + (size_t)(tid >> 3) * rowv;
     auto load = [&](int kb) {
+        if (kb + KB <= a.Lk) {   // whole tile (wave-uniform): scalar offsets, no clamps
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                kr[c] = *reinterpret_cast<const bf16x8*>(a.k + k0off + (size_t)(kb + 32 * c) * rowk);
+                vr[c] = *reinterpret_cast<const bf16x8*>(a.v + v0off + (size_t)(kb + 32 * c) * rowv);
+            }
+            return;
+        }
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             const int key = kb + (tid >> 3) + 32 * c;
@@ -325,6 +356,8 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     if (kbeg < kend) {
         load(kbeg);
         store(0);
+        if (DROP && BITS && active) dw_cur = wq_lane[(size_t)(kbeg >> 6) * wq_tile];
+        if (MASK && active) mw_cur = mrow[(size_t)(kbeg >> 6) * mtile];
     }
     __syncthreads();
     PROBE_DECL
@@ -336,8 +369,10 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
         if (active) {
             const bf16* K = Ks[buf];
             const bf16* V = Vs[buf];
-            const uint32_t mw = MASK ? mrow[(size_t)(kb >> 6) * mtile] : 0u;
-            const uint32_t dwin = (DROP && BITS) ? wq_lane[(size_t)(kb >> 6) * wq_tile] : 0u;
+            if (MASK && more) mw_next = mrow[(size_t)((kb >> 6) + 1) * mtile];
+            const uint32_t mw = mw_cur;
+            if (DROP && BITS && more) dw_next = wq_lane[(size_t)((kb >> 6) + 1) * wq_tile];
+            const uint32_t kwin = ~dw_cur;
             // all LDS operand reads of the tile are issued ahead of their MFMAs, so their
             // latency overlaps the matrix / softmax work instead of stalling each MFMA
             bf16x8 ka[2][4];
@@ -346,11 +381,13 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
                 for (int s = 0; s < 4; ++s)
                     ka[t][s] = *reinterpret_cast<const bf16x8*>(K + (32 * t + r) * LDK + 16 * s + 8 * h);
+            // masked keys (MASK): -inf initial scores, so the MFMA results carry the mask
             f32x16 st[2];
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
 #pragma unroll
-                for (int i = 0; i < 16; ++i) st[t][i] = 0.f;
+                for (int i = 0; i < 16; ++i)
+                    st[t][i] = MASK ? __builtin_bit_cast(float, bit_mask(mw, score_bit(t, i)) & 0xFF800000u) : 0.f;
             }
 #pragma unroll
             for (int s = 0; s < 4; ++s)
@@ -379,13 +416,6 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
                     for (int i = 0; i < 16; ++i)
                         if (32 * t + (i & 3) + 8 * (i >> 2) + 4 * h >= nvalid) st[t][i] = -INFINITY;
-            }
-            if (MASK) {   // masked keys: -inf scores (p = 0, not in the row sum)
-#pragma unroll
-                for (int t = 0; t < 2; ++t)
-#pragma unroll
-                    for (int i = 0; i < 16; ++i)
-                        if ((mw >> score_bit(t, i)) & 1u) st[t][i] = -INFINITY;
             }
             float mx = -INFINITY;
 #pragma unroll
@@ -427,11 +457,13 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
                     rs0 += p0;
                     rs1 += p1;
                     uint32_t pk = pack_bf16(p0, p1);
-                    if (DROP && BITS) {   // bits 8t + (i>>1) (even key), 16 + 8t + (i>>1) (odd)
+                    if (DROP && BITS) {
+                        // keep bits 8t + (i>>1) (even key) and 16 + 8t + (i>>1) (odd key) move
+                        // to bits 15 and 31; one packed arithmetic shift spreads each over its
+                        // bf16 half: shift, v_pk_ashrrev_i16, and
                         const int jb = 8 * t + (i >> 1);
-                        const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)dwin, jb, 1);
-                        const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)dwin, 16 + jb, 1);
-                        pk &= ~((m0 & 0xFFFFu) | (m1 & 0xFFFF0000u));
+                        const s16x2 kh = __builtin_bit_cast(s16x2, kwin << (15 - jb));
+                        pk &= __builtin_bit_cast(uint32_t, (s16x2)(kh >> (s16x2){15, 15}));
                     } else if (DROP) {
                         // key 32t + (i&3) + 8(i>>2) + 4h (even): pair 16t + (i&3)/2 + 4(i>>2) + 2h
                         const uint32_t c = 16 * t + ((i & 3) >> 1) + 4 * (i >> 2);
@@ -445,6 +477,8 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
                 }
             l += rs0 + rs1;
             if (DROP && !BITS) dw_prev = dw;
+            if (DROP && BITS) dw_cur = dw_next;
+            if (MASK) mw_cur = mw_next;
             PROBE(3);
 #pragma unroll
             for (int t = 0; t < 2; ++t)
@@ -568,7 +602,8 @@ struct AttnBwdArgs {
     float scale;
 };
 
-template <bool DROP, bool MASK>
+// RAGGED: Lk % 64 != 0 (the last key tile is partial); the key check exists only then
+template <bool DROP, bool MASK, bool RAGGED>
 __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
     const AttnArgs& a = A.f;
     __shared__ __attribute__((aligned(16))) bf16 Ks[2][KB * LDK];
@@ -598,6 +633,12 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
     dsum += __shfl_xor(dsum, 32);
     float lse2 = active ? a.lse[(size_t)bh * a.Lq + qi] : 0.f;
     if (MASK && lse2 == -INFINITY) lse2 = INFINITY;   // no attended key: P = 0
+    // row constants as the initial accumulators (the lane's query): S' = S + s_init gives
+    // p' = exp2(S' scale2) = P / (1 - p) directly, dP' = dP + d_init gives
+    // dS = p' (Z ? dP' : d_init) = P (Z dP / (1 - p) - D): no subtraction per element and the
+    // dropout select is one v_bfi_b32
+    const float s_init = (-lse2 + (DROP ? __log2f(a.keep_scale) : 0.f)) / a.scale2;
+    const float d_init = -dsum / a.keep_scale;
     if (active && h == 0 && blockIdx.z == 0) A.dvec[(size_t)bh * a.Lq + qi] = dsum;
     // the forward's query-major drop words of this lane, one per 64-key tile (prefetched a
     // tile ahead with the K / V rows)
@@ -616,6 +657,14 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
     const size_t k0off = (size_t)b * a.sk + hh * D + 8 * (tid & 7) + (size_t)(tid >> 3) * rowk;
     const size_t v0off = (size_t)b * a.sv + hh * D + 8 * (tid & 7) + (size_t)(tid >> 3) * rowv;
     auto load = [&](int kb) {
+        if (kb + KB <= a.Lk) {   // whole tile (wave-uniform): scalar offsets, no clamps
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                kr[c] = *reinterpret_cast<const bf16x8*>(a.k + k0off + (size_t)(kb + 32 * c) * rowk);
+                vr[c] = *reinterpret_cast<const bf16x8*>(a.v + v0off + (size_t)(kb + 32 * c) * rowv);
+            }
+            return;
+        }
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             const int key = kb + (tid >> 3) + 32 * c;
@@ -654,16 +703,24 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
         if (more) load(kb + KB);
         if (DROP && active && more) wnext = wrow[(size_t)((kb >> 6) + 1) * wstride];
         if (MASK && active && more) mnext = mrow[(size_t)((kb >> 6) + 1) * mtile];
-        if (active) {
+        // the tile body as a generic lambda, instantiated twice when RAGGED: the partial-tile key
+        // check exists only in the copy the last tile takes (inline, hipcc if-converts it into
+        // every tile)
+        auto tile = [&](auto partial) {
+            constexpr bool PARTIAL = decltype(partial)::value;
             const bf16* K = Ks[buf];
             const bf16* V = Vs[buf];
             const int nvalid = kend - kb;
+            const uint32_t kcur = ~wcur;   // keep bits
             u32x4 dsw[2][2];
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
                 f32x16 st, dpt;
 #pragma unroll
-                for (int i = 0; i < 16; ++i) st[i] = dpt[i] = 0.f;
+                for (int i = 0; i < 16; ++i) {   // masked keys: -inf initial scores
+                    st[i] = MASK ? neg_inf_if(s_init, mcur, score_bit(t, i)) : s_init;
+                    dpt[i] = d_init;
+                }
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
                     const bf16x8 ka = *reinterpret_cast<const bf16x8*>(K + (32 * t + r) * LDK + 16 * s + 8 * h);
@@ -672,31 +729,24 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
                     dpt = mfma(va, df[s], dpt);
                 }
                 // keys past Lk (last partial tile, wave-uniform branch): score -inf -> P = 0
-                if (nvalid < KB) {
+                if (PARTIAL) {
 #pragma unroll
                     for (int i = 0; i < 16; ++i)
                         if (32 * t + (i & 3) + 8 * (i >> 2) + 4 * h >= nvalid) st[i] = -INFINITY;
                 }
-                if (MASK) {
-#pragma unroll
-                    for (int i = 0; i < 16; ++i)
-                        if ((mcur >> score_bit(t, i)) & 1u) st[i] = -INFINITY;
-                }
 #pragma unroll
                 for (int i = 0; i < 16; i += 2) {
-                    const float p0 = fast_exp2(fmaf(st[i], a.scale2, -lse2));
-                    const float p1 = fast_exp2(fmaf(st[i + 1], a.scale2, -lse2));
+                    const float p0 = fast_exp2(st[i] * a.scale2);
+                    const float p1 = fast_exp2(st[i + 1] * a.scale2);
                     float dp0 = dpt[i], dp1 = dpt[i + 1];
-                    if (DROP) {   // bits 8t + (i>>1) (even key) and 16 + 8t + (i>>1) (odd key)
-                        const int jb = 8 * t + (i >> 1);
-                        const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)wcur, jb, 1);
-                        const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)wcur, 16 + jb, 1);
-                        dp0 = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, dp0) & ~m0);
-                        dp1 = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, dp1) & ~m1);
+                    if (DROP) {   // keep bits 8t + (i>>1) (even key), 16 + 8t + (i>>1) (odd key)
+                        const uint32_t k0 = bit_mask(kcur, 8 * t + (i >> 1));
+                        const uint32_t k1 = bit_mask(kcur, 16 + 8 * t + (i >> 1));
+                        const uint32_t di = __builtin_bit_cast(uint32_t, d_init);
+                        dp0 = __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, dp0) & k0) | (di & ~k0));
+                        dp1 = __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, dp1) & k1) | (di & ~k1));
                     }
-                    // P (Z dP~ / (1-p) - D): the scale rides in the fma (exact for p = 0)
-                    dsw[t][i >> 3][(i & 7) >> 1] = pack_bf16(p0 * fmaf(dp0, a.keep_scale, -dsum),
-                                                             p1 * fmaf(dp1, a.keep_scale, -dsum));
+                    dsw[t][i >> 3][(i & 7) >> 1] = pack_bf16(p0 * dp0, p1 * dp1);
                 }
             }
 #pragma unroll
@@ -706,6 +756,14 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
 #pragma unroll
                     for (int s = 0; s < 2; ++s)
                         dqt[dt] = mfma(v_operand(K, lane, dt, t, s), __builtin_bit_cast(bf16x8, dsw[t][s]), dqt[dt]);
+        };
+        if (active) {
+            if constexpr (RAGGED) {
+                if (kend - kb < KB) tile(std::true_type{});
+                else tile(std::false_type{});
+            } else {
+                tile(std::false_type{});
+            }
         }
         if (more) store(buf ^ 1);
         wcur = wnext;
@@ -735,9 +793,9 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
         }
 }
 
-template <bool DROP, bool MASK>
+template <bool DROP, bool MASK, bool RAGGED>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
-    attn_bwd_dq_body<DROP, MASK>(A);
+    attn_bwd_dq_body<DROP, MASK, RAGGED>(A);
 }
 
 // dq = scale * sum over key splits; one thread per (b*H+h, query, 4 dims)
@@ -768,7 +826,10 @@ __global__ void __launch_bounds__(256) attn_dq_combine_kernel(AttnBwdArgs A) {
 }
 
 // a lane owns a key: S = Q K^T tiles (32 queries x 32 keys) with the query on the registers
-template <bool DROP, bool MASK>
+// OWN_D: D = rowsum(dO . O) of each query tile computed here from the forward output (the
+// split small backward, whose dQ pass runs beside it in another workgroup) instead of read
+// from the dQ pass's dvec
+template <bool DROP, bool MASK, bool OWN_D = false>
 __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
     const AttnArgs& a = A.f;
     constexpr int QB = 64;   // queries per LDS tile
@@ -802,7 +863,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
             vf[s] = *reinterpret_cast<const bf16x8*>(vrow + 16 * s + 8 * h);
         }
     }
-    bf16x8 qr[2], dr[2];
+    bf16x8 qr[2], dr[2], orr[2];
     float lr = 0.f, dvr = 0.f;
     // per-thread offsets of query row tid>>3, advanced per tile by qb * B * s (scalar unit)
     const size_t rowq = (size_t)a.B * a.sq, rowd = (size_t)a.B * A.sdo;
@@ -812,13 +873,21 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             const int qq = qb + (tid >> 3) + 32 * c;
-            size_t qo = q0off + (size_t)(qb + 32 * c) * rowq, dof = d0off + (size_t)(qb + 32 * c) * rowd;
-            if (qq >= a.Lq) {   // past the last query (partial tile): repeat the last row
-                qo -= (size_t)(qq - (a.Lq - 1)) * rowq;
-                dof -= (size_t)(qq - (a.Lq - 1)) * rowd;
+            const int qc = qq < a.Lq ? qq : a.Lq - 1;   // past the last query: repeat the last row
+            if (qb + QB <= a.Lq) {   // whole tile (wave-uniform): scalar offsets, no clamps
+                qr[c] = *reinterpret_cast<const bf16x8*>(a.q + q0off + (size_t)(qb + 32 * c) * rowq);
+                dr[c] = *reinterpret_cast<const bf16x8*>(A.dout + d0off + (size_t)(qb + 32 * c) * rowd);
+            } else {
+                size_t qo = q0off + (size_t)(qb + 32 * c) * rowq, dof = d0off + (size_t)(qb + 32 * c) * rowd;
+                if (qq >= a.Lq) {
+                    qo -= (size_t)(qq - (a.Lq - 1)) * rowq;
+                    dof -= (size_t)(qq - (a.Lq - 1)) * rowd;
+                }
+                qr[c] = *reinterpret_cast<const bf16x8*>(a.q + qo);
+                dr[c] = *reinterpret_cast<const bf16x8*>(A.dout + dof);
             }
-            qr[c] = *reinterpret_cast<const bf16x8*>(a.q + qo);
-            dr[c] = *reinterpret_cast<const bf16x8*>(A.dout + dof);
+            if (OWN_D)
+                orr[c] = *reinterpret_cast<const bf16x8*>(A.o + ((size_t)qc * a.B + b) * a.so + hh * D + 8 * (tid & 7));
         }
         if (tid < QB) {
             const int qq = qb + tid;
@@ -826,7 +895,10 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
             // queries past Lq: lse = +inf -> P = 0
             lr = qq < a.Lq ? a.lse[(size_t)bh * a.Lq + qc] : INFINITY;
             if (MASK && lr == -INFINITY) lr = INFINITY;   // query with no attended key
-            dvr = A.dvec[(size_t)bh * a.Lq + qc];
+            if (!OWN_D) dvr = A.dvec[(size_t)bh * a.Lq + qc];
+            // the row constants as the S / dP accumulators' initial values (see the loop)
+            lr = -lr / a.scale2;
+            if (!OWN_D) dvr = -dvr / a.keep_scale;
         }
         if (DROP && active) {
 #pragma unroll
@@ -848,14 +920,26 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
         }
         if (tid < QB) {
             Ls[buf][tid] = lr;
-            Dv[buf][tid] = dvr;
+            if (!OWN_D) Dv[buf][tid] = dvr;
+        }
+        if (OWN_D) {   // 8 lanes per query row, 8 of its 64 dims each
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                float t = 0.f;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) t = fmaf((float)dr[c][j], (float)orr[c][j], t);
+                t += __shfl_xor(t, 1);
+                t += __shfl_xor(t, 2);
+                t += __shfl_xor(t, 4);
+                if ((tid & 7) == 0) Dv[buf][(tid >> 3) + 32 * c] = -t / a.keep_scale;
+            }
         }
     };
     f32x16 dkt[2], dvt[2];
 #pragma unroll
     for (int i = 0; i < 16; ++i) dkt[0][i] = dkt[1][i] = dvt[0][i] = dvt[1][i] = 0.f;
+    // a lane past the last key holds a copy of the last key's row: finite values, never stored
     const bool kvalid = active && (k0 + r) < a.Lk;
-    const float s0 = kvalid ? 0.f : -INFINITY;
     load(0);
     store(0);
     uint32_t wc[2] = {wn[0], wn[1]};
@@ -870,13 +954,26 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
             const bf16* DO = Ds[buf];
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
-                // a lane past the last key (its K row is a copy of the last one) starts its
-                // scores at -inf: P = exp2(-inf) = 0 without a per-element select
+                // row constants (per element = query row 8g + 4h + j) as the initial
+                // accumulators: S' = S - lse / scale2 gives P = exp2(S' scale2), dP' = dP - D (1-p)
+                // gives dS = P (Z dP / (1-p) - D) = P (Z ? dP' : -D (1-p)) / (1-p), the 1/(1-p)
+                // applied to dK once at the end as it is to dV
+                float lv[16], dv[16];
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int qrow = 32 * u + 8 * g + 4 * h;      // rows 4g..4g+3 of the tile
+                    const float4 l4 = *reinterpret_cast<const float4*>(&Ls[buf][qrow]);
+                    const float4 d4 = *reinterpret_cast<const float4*>(&Dv[buf][qrow]);
+                    lv[4 * g] = l4.x; lv[4 * g + 1] = l4.y; lv[4 * g + 2] = l4.z; lv[4 * g + 3] = l4.w;
+                    dv[4 * g] = d4.x; dv[4 * g + 1] = d4.y; dv[4 * g + 2] = d4.z; dv[4 * g + 3] = d4.w;
+                }
+                // masked (query, key): -inf initial score
+                const uint32_t msh = MASK ? mc[u] >> (4 * h) : 0u;
                 f32x16 st, dpt;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    st[i] = s0;
-                    dpt[i] = 0.f;
+                    st[i] = MASK ? neg_inf_if(lv[i], msh, 8 * (i >> 2) + (i & 3)) : lv[i];
+                    dpt[i] = dv[i];
                 }
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
@@ -885,34 +982,25 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
                     st = mfma(qa, kf[s], st);
                     dpt = mfma(da, vf[s], dpt);
                 }
-                // drop bit of row 8g + 4h + j of this 32-query block: bit 8g + j of w >> 4h
-                const uint32_t wsh = DROP ? wc[u] >> (4 * h) : 0u;
-                if (MASK) {   // masked (query, key): -inf score
-                    const uint32_t msh = mc[u] >> (4 * h);
-#pragma unroll
-                    for (int i = 0; i < 16; ++i)
-                        if ((msh >> (8 * (i >> 2) + (i & 3))) & 1u) st[i] = -INFINITY;
-                }
+                // keep bit of row 8g + 4h + j of this 32-query block: bit 8g + j of ~w >> 4h
+                const uint32_t ksh = DROP ? ~wc[u] >> (4 * h) : 0u;
                 u32x4 pw[2], dsw[2];
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    const int qrow = 32 * u + 8 * g + 4 * h;      // rows 4g..4g+3 of the tile
-                    const float4 l4 = *reinterpret_cast<const float4*>(&Ls[buf][qrow]);
-                    const float4 d4 = *reinterpret_cast<const float4*>(&Dv[buf][qrow]);
-                    const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
                     float pd[4], ds[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int i = 4 * g + j;
-                        const float p = fast_exp2(fmaf(st[i], a.scale2, -lv[j]));
+                        const float p = fast_exp2(st[i] * a.scale2);
                         float pk = p, dp = dpt[i];
                         if (DROP) {   // 1/(1-p) applied to dV once at the end
-                            const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)wsh, 8 * g + j, 1);
-                            pk = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, p) & ~m);
-                            dp = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, dp) & ~m);
+                            const uint32_t km = bit_mask(ksh, 8 * g + j);
+                            pk = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, p) & km);
+                            dp = __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, dp) & km) |
+                                                               (__builtin_bit_cast(uint32_t, dv[i]) & ~km));
                         }
                         pd[j] = pk;
-                        ds[j] = p * fmaf(dp, a.keep_scale, -dv4[j]);
+                        ds[j] = p * dp;
                     }
                     pw[g >> 1][2 * (g & 1)] = pack_bf16(pd[0], pd[1]);
                     pw[g >> 1][2 * (g & 1) + 1] = pack_bf16(pd[2], pd[3]);
@@ -947,7 +1035,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
             bf16x4 wk, wv;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                wk[j] = (bf16)(dkt[dt][4 * g + j] * A.scale);
+                wk[j] = (bf16)(dkt[dt][4 * g + j] * (A.scale * a.keep_scale));
                 wv[j] = (bf16)(dvt[dt][4 * g + j] * a.keep_scale);
             }
             *reinterpret_cast<bf16x4*>(krow + 32 * dt + 8 * g + 4 * h) = wk;
@@ -964,11 +1052,19 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
 // 128 x 128 self attention) in ONE launch: a workgroup per (b, h) runs the dQ pass over its
 // queries (which also writes D), then, after the barrier that publishes D to the
 // workgroup, the dK / dV pass over its keys.  Same arithmetic as the two kernels.
-template <bool DROP>
+template <bool DROP, bool RAGGED>
 __global__ void __launch_bounds__(256, 2) attn_bwd_small_kernel(AttnBwdArgs A) {
-    attn_bwd_dq_body<DROP, false>(A);
+    attn_bwd_dq_body<DROP, false, RAGGED>(A);
     __syncthreads();
     attn_bwd_dkdv_body<DROP, false>(A);
+}
+
+// The same backward as two workgroups per (b, h) that run side by side: blockIdx.z = 0 the dQ
+// pass, 1 the dK / dV pass with its own D (the two passes share no data)
+template <bool DROP, bool RAGGED>
+__global__ void __launch_bounds__(256, 2) attn_bwd_small2_kernel(AttnBwdArgs A) {
+    if (blockIdx.z == 0) attn_bwd_dq_body<DROP, false, RAGGED>(A);
+    else attn_bwd_dkdv_body<DROP, false, true>(A);
 }
 
 // dK / dV of several attention calls with the same shape in one launch (blockIdx.z = call):
@@ -1069,6 +1165,13 @@ static void set_dropbits(AttnArgs& a, uint32_t* bits) {
 
 // one-launch backward of short attentions (attn_bwd_small_kernel); OV3D_ATTN_SMALL_BWD=0 or
 // ov3d_attn_small_bwd(0) restores the two launches (A/B measurement, tests)
+// the short backward as two side-by-side workgroups per (b, h) (attn_bwd_small2_kernel);
+// OV3D_ATTN_SMALL_SPLIT=0: both passes in one workgroup (read per call: tests flip it)
+static bool small_bwd_split() {
+    const char* e = getenv("OV3D_ATTN_SMALL_SPLIT");
+    return !(e && e[0] == '0');
+}
+
 static int g_small_bwd = -1;
 static bool fuse_small_bwd() {
     if (g_small_bwd < 0) {
@@ -1086,9 +1189,13 @@ extern "C" int ov3d_attn_small_bwd(int on) {
 
 // drop bits from attn_dropgen_kernel for attentions with at least this many (query, key)
 // pairs per head (OV3D_ATTN_DROPGEN_MIN overrides; 0 = always, -1 = never)
+// Off by default: measured on the encoder (B 8, H 4, L 2048, p 0.1) the pre-pass costs 33.5 us
+// and saves the forward 21.6 us (82.4 -> 60.8 us, profiles/r03_dropgen_trace.json): hashing
+// beside the MFMAs is cheaper than hashing alone.  OV3D_ATTN_DROPGEN_MIN = the query x key
+// count from which the pre-pass runs (0 = always).
 static bool dropgen_ahead(int Lq, int Lk) {
     const char* e = getenv("OV3D_ATTN_DROPGEN_MIN");   // read per call: tests flip it
-    const long long min_pairs = e ? atoll(e) : 512LL * 1024;
+    const long long min_pairs = e ? atoll(e) : -1;
     return min_pairs >= 0 && (long long)Lq * Lk >= min_pairs;
 }
 
@@ -1270,23 +1377,34 @@ extern "C" int ov3d_attn_bwd_masked(const void* q, const void* k, const void* v,
     set_maskbits(a, maskbits);
     hipStream_t st = ov3d_stream(stream);
     if (dk && !maskbits && nsplit == 1 && Lq <= 4 * QW && Lk <= 128 && fuse_small_bwd()) {
-        if (a.thresh)
-            attn_bwd_small_kernel<true><<<dim3(1, B * H), 256, 0, st>>>(A);
+        if (small_bwd_split()) {
+            const dim3 g2(1, B * H, 2);
+            if (Lk % KB)
+                (a.thresh ? attn_bwd_small2_kernel<true, true> : attn_bwd_small2_kernel<false, true>)<<<g2, 256, 0, st>>>(A);
+            else
+                (a.thresh ? attn_bwd_small2_kernel<true, false> : attn_bwd_small2_kernel<false, false>)<<<g2, 256, 0, st>>>(A);
+            OV3D_LAUNCH_CHECK();
+            return OV3D_OK;
+        }
+        const dim3 g1(1, B * H);
+        if (Lk % KB)
+            (a.thresh ? attn_bwd_small_kernel<true, true> : attn_bwd_small_kernel<false, true>)<<<g1, 256, 0, st>>>(A);
         else
-            attn_bwd_small_kernel<false><<<dim3(1, B * H), 256, 0, st>>>(A);
+            (a.thresh ? attn_bwd_small_kernel<true, false> : attn_bwd_small_kernel<false, false>)<<<g1, 256, 0, st>>>(A);
         OV3D_LAUNCH_CHECK();
         return OV3D_OK;
     }
     const dim3 gq((Lq + 4 * QW - 1) / (4 * QW), B * H, nsplit);
+    const bool ragged = Lk % KB != 0;
     if (maskbits) {
         if (a.thresh)
-            attn_bwd_dq_kernel<true, true><<<gq, 256, 0, st>>>(A);
+            (ragged ? attn_bwd_dq_kernel<true, true, true> : attn_bwd_dq_kernel<true, true, false>)<<<gq, 256, 0, st>>>(A);
         else
-            attn_bwd_dq_kernel<false, true><<<gq, 256, 0, st>>>(A);
+            (ragged ? attn_bwd_dq_kernel<false, true, true> : attn_bwd_dq_kernel<false, true, false>)<<<gq, 256, 0, st>>>(A);
     } else if (a.thresh) {
-        attn_bwd_dq_kernel<true, false><<<gq, 256, 0, st>>>(A);
+        (ragged ? attn_bwd_dq_kernel<true, false, true> : attn_bwd_dq_kernel<true, false, false>)<<<gq, 256, 0, st>>>(A);
     } else {
-        attn_bwd_dq_kernel<false, false><<<gq, 256, 0, st>>>(A);
+        (ragged ? attn_bwd_dq_kernel<false, false, true> : attn_bwd_dq_kernel<false, false, false>)<<<gq, 256, 0, st>>>(A);
     }
     OV3D_LAUNCH_CHECK();
     if (nsplit > 1) {

@@ -1,0 +1,409 @@
+// Output layers of the five 3DETR prediction heads plus the query <-> text alignment, in one
+// launch each way.
+//
+// Reference: models/model_3detr.py:_build_heads / get_box_predictions -- each head's last
+// Conv1d(256, n_out) (visual_embed_head n_out = 640, center 3, size 3, angle_cls / angle_residual
+// num_angle_bin) on the decoder-feature rows, then sem_cls_head = Linear(640, T, bias=False)
+// holding the frozen text embedding (model_3detr.py:152-154, 237-238) on the visual embedding.
+// heads.py feeds the rows z2 (R, 5*256) bf16: columns [0, 256) are the visual head's hidden
+// features, [256 (1+i), 256 (2+i)) those of box head i.
+//
+// Forward (heads_out_fwd_kernel): a workgroup per 32 rows, 4 waves.  Each 32-channel output
+// tile is one MFMA 32x32x16 chain over K = 256 (A = weight rows, B = the 32 rows, so a lane
+// owns a row and 16 of the tile's channels): the visual head's 20 tiles (5 per wave) and one
+// tile per box head (n_out <= 32, rows past n_out read as zero).  The visual tiles' epilogue
+// writes the fp32 embedding and, with the text embedding staged in LDS, accumulates the fp32
+// logits of the lane's row over its channels (1/4 of the 640 per wave; reduced across the
+// two lane halves and the four waves in LDS) -- the alignment GEMM never re-reads the
+// embedding from HBM.  Logits are written in the caller's layout: row-major (R, T), or with
+// Q > 0 the reference's transposed layout (quirk Q8: element (lb, q, t) of the (L*B, Q, T)
+// result at lb*Q*T + t*Q + q).
+//
+// Backward (heads_out_bwd_kernel): a workgroup per 32 rows: the visual embedding's gradient
+// plus the alignment's contribution, g_v + g_logits . text, rounded once to bf16 (the operand
+// of the dgrad GEMM and the deferred weight gradient); the box heads' output gradients in
+// bf16; and the box heads' input gradient dz2[:, 256 (1+i) + c] = sum_j g_i[j] W_i[j, c]
+// (n_out <= 32 terms, fp32) into its columns of the caller's dz2.
+#include "common.h"
+
+namespace {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int RB = 32;          // rows per workgroup
+constexpr int KH = 256;         // hidden width of every head
+constexpr int MAXT = 32;        // text rows (classes) the fused alignment supports
+constexpr int MAXS = 4;         // box heads
+
+struct HeadsOutArgs {
+    const bf16* z;              // (R, ldz) bf16
+    long long ldz;
+    int R;
+    const bf16* wv;             // (Nv, 256) bf16 visual output weight
+    const float* bv;            // (Nv) fp32
+    int Nv;
+    const float* text;          // (T, Nv) fp32, or null (no alignment)
+    int T;
+    int lq;                     // logits layout: 0 row-major, else the Q of quirk Q8
+    float* out_v;               // (R, Nv) fp32
+    float* logits;              // (R, T) fp32
+    int ns;                     // box heads
+    const bf16* ws[MAXS];       // (n_i, 256) bf16
+    const float* bs[MAXS];      // (n_i) fp32
+    int n[MAXS];
+    int kcol[MAXS];             // input column of head i (256 (1+i))
+    int ocol[MAXS];             // output column of head i in out_s
+    float* out_s;               // (R, Ns) fp32
+    int Ns;
+};
+
+// copy n4 float4 from global to LDS with every thread's loads in flight together (a plain
+// load -> store loop waits out one global latency per iteration)
+__device__ __forceinline__ void stage_f4(float4* __restrict__ dst, const float4* __restrict__ src, int n4,
+                                         int tid) {
+    constexpr int U = 8;
+    for (int base = 0; base < n4; base += 256 * U) {
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = base + 256 * u + tid;
+            if (i < n4) v[u] = src[i];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = base + 256 * u + tid;
+            if (i < n4) dst[i] = v[u];
+        }
+    }
+}
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ long long logit_at(const HeadsOutArgs& a, int row, int t) {
+    if (a.lq <= 0) return (long long)row * a.T + t;
+    const int lb = row / a.lq, q = row - lb * a.lq;
+    return ((long long)lb * a.T + t) * a.lq + q;
+}
+
+// one 32-channel tile of rows z (this lane: row r, operand k-half h): acc[e] = channel
+// 8 (e / 4) + 4 h + e % 4 of the tile
+__device__ __forceinline__ f32x16 tile_gemm(const bf16* __restrict__ w, int nrows, const bf16x8* zf,
+                                            int r, int h) {
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    const bool live = r < nrows;
+    const bf16* wr = w + (size_t)(live ? r : 0) * KH + 8 * h;
+    bf16x8 wf[KH / 16];
+#pragma unroll
+    for (int s = 0; s < KH / 16; ++s) {
+        wf[s] = *reinterpret_cast<const bf16x8*>(wr + 16 * s);
+        if (!live) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) wf[s][j] = (bf16)0.f;
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < KH / 16; ++s) acc = mfma(wf[s], zf[s], acc);
+    return acc;
+}
+
+__global__ void __launch_bounds__(256) heads_out_fwd_kernel(HeadsOutArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* textS = smem;                         // (T, Nv)
+    float* red = smem + (size_t)a.T * a.Nv;      // (4 waves, 32 rows, T)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int row0 = blockIdx.x * RB;
+    const int row = row0 + r;
+    const int rowc = row < a.R ? row : a.R - 1;
+    const bool align = a.text != nullptr;
+    if (align) {
+        stage_f4(reinterpret_cast<float4*>(textS), reinterpret_cast<const float4*>(a.text),
+                 a.T * a.Nv / 4, tid);
+        __syncthreads();
+    }
+    // this lane's row, visual columns [0, 256)
+    bf16x8 zf[KH / 16];
+    {
+        const bf16* zr = a.z + (size_t)rowc * a.ldz + 8 * h;
+#pragma unroll
+        for (int s = 0; s < KH / 16; ++s) zf[s] = *reinterpret_cast<const bf16x8*>(zr + 16 * s);
+    }
+    float lg[MAXT];
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t) lg[t] = 0.f;
+    const int nvt = a.Nv / 32;
+    for (int ct = wave; ct < nvt; ct += 4) {
+        const f32x16 acc = tile_gemm(a.wv + (size_t)ct * 32 * KH, 32, zf, r, h);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int ch = 32 * ct + 8 * g + 4 * h;
+            const float4 b4 = *reinterpret_cast<const float4*>(a.bv + ch);
+            const float4 v = make_float4(acc[4 * g] + b4.x, acc[4 * g + 1] + b4.y,
+                                         acc[4 * g + 2] + b4.z, acc[4 * g + 3] + b4.w);
+            if (row < a.R) *reinterpret_cast<float4*>(a.out_v + (size_t)row * a.Nv + ch) = v;
+            if (align) {
+#pragma unroll
+                for (int t = 0; t < MAXT; ++t) {
+                    if (t < a.T) {
+                        const float4 tx = *reinterpret_cast<const float4*>(textS + (size_t)t * a.Nv + ch);
+                        lg[t] = fmaf(v.x, tx.x, fmaf(v.y, tx.y, fmaf(v.z, tx.z, fmaf(v.w, tx.w, lg[t]))));
+                    }
+                }
+            }
+        }
+    }
+    if (align) {
+#pragma unroll
+        for (int t = 0; t < MAXT; ++t)
+            if (t < a.T) lg[t] += __shfl_xor(lg[t], 32);
+        if (h == 0) {
+#pragma unroll
+            for (int t = 0; t < MAXT; ++t)
+                if (t < a.T) red[((size_t)wave * RB + r) * a.T + t] = lg[t];
+        }
+    }
+    // box head `wave`: its 256 input columns, one tile
+    if (wave < a.ns) {
+        const bf16* zr = a.z + (size_t)rowc * a.ldz + a.kcol[wave] + 8 * h;
+#pragma unroll
+        for (int s = 0; s < KH / 16; ++s) zf[s] = *reinterpret_cast<const bf16x8*>(zr + 16 * s);
+        const int n = a.n[wave];
+        const f32x16 acc = tile_gemm(a.ws[wave], n, zf, r, h);
+        if (row < a.R) {
+            float* o = a.out_s + (size_t)row * a.Ns + a.ocol[wave];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int c = 8 * (e >> 2) + 4 * h + (e & 3);
+                if (c < n) o[c] = acc[e] + a.bs[wave][c];
+            }
+        }
+    }
+    if (align) {
+        __syncthreads();
+        for (int i = tid; i < RB * a.T; i += 256) {
+            const int rr = i / a.T, t = i - rr * a.T;
+            if (row0 + rr >= a.R) continue;
+            const float s = red[(size_t)rr * a.T + t] + red[((size_t)RB + rr) * a.T + t] +
+                            red[((size_t)2 * RB + rr) * a.T + t] + red[((size_t)3 * RB + rr) * a.T + t];
+            a.logits[logit_at(a, row0 + rr, t)] = s;
+        }
+    }
+}
+
+struct HeadsOutBwdArgs {
+    const float* gv;            // (R, Nv) fp32 gradient of the visual embedding
+    const float* glog;          // logits gradient (layout of the forward) or null
+    const float* text;          // (T, Nv)
+    int R, Nv, T, lq;
+    const float* gs;            // (R, Ns) fp32 gradient of the box heads' outputs
+    int Ns, ns;
+    const bf16* ws[MAXS];
+    int n[MAXS];
+    int kcol[MAXS];
+    int ocol[MAXS];
+    bf16* gvb;                  // (R, Nv) bf16
+    bf16* gsb;                  // (R, Ns) bf16
+    bf16* dz;                   // (R, lddz) bf16: box head i's input gradient at column kcol[i]
+    long long lddz;
+};
+
+__global__ void __launch_bounds__(256) heads_out_bwd_kernel(HeadsOutBwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* textS = smem;                               // (T, Nv)
+    float* gl = smem + (size_t)a.T * a.Nv;             // (32 rows, MAXT)
+    float* gsS = gl + RB * MAXT;                       // (32 rows, Ns) bf16-rounded
+    bf16* wS = reinterpret_cast<bf16*>(gsS + RB * MAXS * 32);   // box heads' weights (Ns, 256)
+    const int tid = threadIdx.x;
+    const int row0 = blockIdx.x * RB;
+    const int nrows = min(RB, a.R - row0);
+    const bool align = a.glog != nullptr;
+    if (align)
+        stage_f4(reinterpret_cast<float4*>(textS), reinterpret_cast<const float4*>(a.text),
+                 a.T * a.Nv / 4, tid);
+    for (int hi = 0; hi < a.ns; ++hi)      // (n_i, 256) bf16 rows at row ocol[i]
+        stage_f4(reinterpret_cast<float4*>(wS + (size_t)a.ocol[hi] * KH),
+                 reinterpret_cast<const float4*>(a.ws[hi]), a.n[hi] * KH / 8, tid);
+    if (align) {
+        for (int i = tid; i < nrows * a.T; i += 256) {
+            const int rr = i / a.T, t = i - rr * a.T;
+            const int row = row0 + rr;
+            long long at;
+            if (a.lq <= 0) {
+                at = (long long)row * a.T + t;
+            } else {
+                const int lb = row / a.lq, q = row - lb * a.lq;
+                at = ((long long)lb * a.T + t) * a.lq + q;
+            }
+            gl[rr * MAXT + t] = a.glog[at];
+        }
+    }
+    for (int i = tid; i < nrows * a.Ns; i += 256) {
+        const int rr = i / a.Ns, j = i - rr * a.Ns;
+        const bf16 v = (bf16)a.gs[(size_t)(row0 + rr) * a.Ns + j];
+        a.gsb[(size_t)(row0 + rr) * a.Ns + j] = v;
+        gsS[rr * a.Ns + j] = (float)v;
+    }
+    __syncthreads();
+    // visual: 4 channels per item, U items' loads in flight per thread
+    constexpr int U = 4;
+    const int nv4 = a.Nv / 4;
+    const int nitems = nrows * nv4;
+    for (int base = tid; base < nitems; base += 256 * U) {
+        float4 g[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = base + 256 * u;
+            if (i < nitems) {
+                const int rr = i / nv4, c4 = i - rr * nv4;
+                g[u] = *reinterpret_cast<const float4*>(a.gv + (size_t)(row0 + rr) * a.Nv + 4 * c4);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = base + 256 * u;
+            if (i >= nitems) continue;
+            const int rr = i / nv4, c4 = i - rr * nv4;
+            float4 v = g[u];
+            if (align) {
+                for (int t = 0; t < a.T; ++t) {
+                    const float w = gl[rr * MAXT + t];
+                    const float4 tx = *reinterpret_cast<const float4*>(textS + (size_t)t * a.Nv + 4 * c4);
+                    v.x = fmaf(w, tx.x, v.x);
+                    v.y = fmaf(w, tx.y, v.y);
+                    v.z = fmaf(w, tx.z, v.z);
+                    v.w = fmaf(w, tx.w, v.w);
+                }
+            }
+            bf16x4 o;
+            o[0] = (bf16)v.x;
+            o[1] = (bf16)v.y;
+            o[2] = (bf16)v.z;
+            o[3] = (bf16)v.w;
+            *reinterpret_cast<bf16x4*>(a.gvb + (size_t)(row0 + rr) * a.Nv + 4 * c4) = o;
+        }
+    }
+    // box heads' input gradient: 4 columns per item, weights from LDS
+    for (int i = tid; i < nrows * a.ns * (KH / 4); i += 256) {
+        const int c4 = i % (KH / 4), hi = (i / (KH / 4)) % a.ns, rr = i / (KH / 4 * a.ns);
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        const bf16* w = wS + (size_t)a.ocol[hi] * KH + 4 * c4;
+        const float* gr = gsS + rr * a.Ns + a.ocol[hi];
+        for (int j = 0; j < a.n[hi]; ++j) {
+            const bf16x4 wv = *reinterpret_cast<const bf16x4*>(w + (size_t)j * KH);
+            const float gj = gr[j];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] = fmaf(gj, (float)wv[q], acc[q]);
+        }
+        bf16x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = (bf16)acc[q];
+        *reinterpret_cast<bf16x4*>(a.dz + (size_t)(row0 + rr) * a.lddz + a.kcol[hi] + 4 * c4) = o;
+    }
+}
+
+bool common_ok(int R, int Nv, int T, int ns, const int* n) {
+    if (R <= 0 || Nv <= 0 || Nv % 32 || T < 0 || T > MAXT || ns < 0 || ns > MAXS) return false;
+    for (int i = 0; i < ns; ++i)
+        if (n[i] <= 0 || n[i] > 32) return false;
+    return true;
+}
+
+}  // namespace
+
+extern "C" int ov3d_heads_out_max_text(void) { return MAXT; }
+
+extern "C" int ov3d_heads_out_fwd(const void* z, long long ldz, int R, const void* wv, const float* bv,
+                                  int Nv, const float* text, int T, int lq, float* out_v,
+                                  float* logits, int ns, const void* const* ws,
+                                  const float* const* bs, const int* n, const int* kcol,
+                                  const int* ocol, float* out_s, int Ns, void* stream) {
+    if (!z || !wv || !bv || !out_v || !common_ok(R, Nv, text ? T : 0, ns, n) ||
+        (text && (!logits || T <= 0)) || (ns > 0 && (!ws || !bs || !kcol || !ocol || !out_s)))
+        return OV3D_EINVAL;
+    HeadsOutArgs a = {};
+    a.z = static_cast<const bf16*>(z);
+    a.ldz = ldz;
+    a.R = R;
+    a.wv = static_cast<const bf16*>(wv);
+    a.bv = bv;
+    a.Nv = Nv;
+    a.text = text;
+    a.T = text ? T : 0;
+    a.lq = lq;
+    a.out_v = out_v;
+    a.logits = logits;
+    a.ns = ns;
+    for (int i = 0; i < ns; ++i) {
+        if (!ws[i] || !bs[i] || kcol[i] < 0 || kcol[i] + KH > ldz || ocol[i] < 0 || ocol[i] + n[i] > Ns)
+            return OV3D_EINVAL;
+        a.ws[i] = static_cast<const bf16*>(ws[i]);
+        a.bs[i] = bs[i];
+        a.n[i] = n[i];
+        a.kcol[i] = kcol[i];
+        a.ocol[i] = ocol[i];
+    }
+    if (KH > ldz) return OV3D_EINVAL;
+    a.out_s = out_s;
+    a.Ns = Ns;
+    const size_t lds = ((size_t)a.T * Nv + (a.T ? 4 * RB * a.T : 0)) * sizeof(float);
+    if (lds > 160 * 1024) return OV3D_EINVAL;
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute(reinterpret_cast<const void*>(heads_out_fwd_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return OV3D_ELAUNCH;
+    hipLaunchKernelGGL(heads_out_fwd_kernel, dim3((unsigned)((R + RB - 1) / RB)), dim3(256), lds,
+                       ov3d_stream(stream), a);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_heads_out_bwd(const float* gv, const float* glog, const float* text, int R, int Nv,
+                                  int T, int lq, const float* gs, int Ns, int ns,
+                                  const void* const* ws, const int* n, const int* kcol,
+                                  const int* ocol, void* gvb, void* gsb, void* dz, long long lddz,
+                                  void* stream) {
+    if (!gv || !gvb || !common_ok(R, Nv, glog ? T : 0, ns, n) || (glog && (!text || T <= 0)) ||
+        (ns > 0 && (!gs || !gsb || !dz || !ws || !kcol || !ocol)) || Ns > MAXS * 32)
+        return OV3D_EINVAL;
+    HeadsOutBwdArgs a = {};
+    a.gv = gv;
+    a.glog = glog;
+    a.text = text;
+    a.R = R;
+    a.Nv = Nv;
+    a.T = glog ? T : 0;
+    a.lq = lq;
+    a.gs = gs;
+    a.Ns = ns > 0 ? Ns : 0;
+    a.ns = ns;
+    for (int i = 0; i < ns; ++i) {
+        if (!ws[i] || kcol[i] < 0 || kcol[i] + KH > lddz || ocol[i] < 0 || ocol[i] + n[i] > Ns)
+            return OV3D_EINVAL;
+        a.ws[i] = static_cast<const bf16*>(ws[i]);
+        a.n[i] = n[i];
+        a.kcol[i] = kcol[i];
+        a.ocol[i] = ocol[i];
+    }
+    a.gvb = static_cast<bf16*>(gvb);
+    a.gsb = static_cast<bf16*>(gsb);
+    a.dz = static_cast<bf16*>(dz);
+    a.lddz = lddz;
+    const size_t lds = ((size_t)a.T * Nv + RB * MAXT + RB * MAXS * 32) * sizeof(float) +
+                       (size_t)a.Ns * KH * sizeof(bf16);
+    if (lds > 160 * 1024) return OV3D_EINVAL;
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute(reinterpret_cast<const void*>(heads_out_bwd_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return OV3D_ELAUNCH;
+    hipLaunchKernelGGL(heads_out_bwd_kernel, dim3((unsigned)((R + RB - 1) / RB)), dim3(256), lds,
+                       ov3d_stream(stream), a);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}

@@ -459,6 +459,26 @@ def mark_shadow_fresh(p):
         e[2] = p._version
 
 
+def register_shadow(p, view):
+    """make `view` (bf16, p's shape, e.g. a slice of a shared storage) p's refreshed bf16
+    copy: FusedAdamW rewrites it with p, refresh_shadows() re-copies it when stale"""
+    e = _SHADOWS.get(id(p))
+    if e is not None and e[0]() is p and e[1].data_ptr() == view.data_ptr():
+        return
+    _SHADOWS[id(p)] = [weakref.ref(p), view, -1]
+
+
+def ensure_fresh(params):
+    """re-copy the stale registered shadows if one of `params` changed (not during capture)"""
+    if torch.cuda.is_current_stream_capturing():
+        return
+    for p in params:
+        e = _SHADOWS.get(id(p))
+        if e is not None and e[0]() is p and e[2] != p._version:
+            refresh_shadows()
+            return
+
+
 def cast_param(w, dt):
     """w (a parameter or a view of one) as `dt`, from the shared refreshed copies."""
     if w is None or w.dtype == dt:

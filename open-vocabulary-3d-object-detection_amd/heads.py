@@ -19,6 +19,8 @@ exist without a per-step concatenation.  Dropout masks come from a counter-based
 (bnrows.hip), regenerated in the backward.  Results equal the per-head evaluation up
 to bf16 rounding (tests/test_heads_gpu.py).
 """
+import ctypes
+
 import torch
 import torch.nn as nn
 
@@ -94,6 +96,7 @@ class HeadPack:
         """(Re-)point parameters / buffers at the shared storages when needed (e.g. after
         .to(device) or load_state_dict with assign=True)."""
         if self._shared():
+            self._ensure_bf16()
             return
         store = {}
         with torch.no_grad():
@@ -112,6 +115,35 @@ class HeadPack:
                                     if bn._buffers[name] is t:
                                         bn._buffers[name] = view
         self.store = store
+        self._ensure_bf16()
+
+    def _ensure_bf16(self):
+        """bf16 storages of the hidden layers' weights, registered as the parameters' shadow
+        copies (gemm.register_shadow): the optimizer keeps them current, no per-step cast"""
+        st = self.store
+        for key in ("w1", "w2"):
+            bk = key + "_bf"
+            if bk not in st or st[bk].device != st[key].device:
+                st[bk] = st[key].to(torch.bfloat16)
+            ts = self._tensors()[key]
+            step = ts[0].numel()
+            for i, t in enumerate(ts):
+                gemm.register_shadow(t, st[bk][i * step:(i + 1) * step].view(t.shape))
+
+    def out_layout(self, w3):
+        """ctypes arrays of the box heads' output widths, input and output columns"""
+        n = tuple(int(w.shape[0]) for w in w3[1:])
+        lay = getattr(self, "_lay", None)
+        if lay is None or lay["key"] != n:
+            ocol, o = [], 0
+            for k in n:
+                ocol.append(o)
+                o += k
+            lay = {"key": n, "Ns": o, "n": (ctypes.c_int * 4)(*n),
+                   "kcol": (ctypes.c_int * 4)(*[self.H * (1 + i) for i in range(4)]),
+                   "ocol": (ctypes.c_int * 4)(*ocol)}
+            self._lay = lay
+        return lay
 
     def bns(self):
         return [p[1] for p in self.parts], [p[4] for p in self.parts]
@@ -153,9 +185,10 @@ def _stats_finalize(x, layout, R, C, gamma, beta, bns, rm, rv, nbt=None):
 
 class _Heads(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, pack, p1, p2, w3v, b3v, w3s, b3s, *params):
-        # params: the shared-storage views (grads are returned for them); the kernels use the
-        # storages directly
+    def forward(ctx, x, pack, p1, p2, text, lq, *params):
+        # params: the shared-storage views of w1 / w2 / g1 / b1 / g2 / b2 (5 each, the grads are
+        # returned for them; the kernels use the storages directly), then the output layers'
+        # weights (5) and biases (5) in HEAD_ORDER
         st = pack.store
         R = x.shape[0]
         H5 = 5 * pack.H
@@ -164,8 +197,9 @@ class _Heads(torch.autograd.Function):
         dev = x.device
         seed = flash._seed(dev)
         xb = x.to(bf).contiguous()
-        w1 = st["w1"].view(H5, pack.C).to(bf)
-        w2 = st["w2"].view(5, H, H).to(bf)
+        # bf16 copies kept current by the optimizer (HeadPack.ensure registers them)
+        w1 = st["w1_bf"].view(H5, pack.C)
+        w2 = st["w2_bf"].view(5, H, H)
         bn1, bn2 = pack.bns()
         torch._foreach_add_([b.num_batches_tracked for b in bn1 + bn2], 1)
         h1 = xb @ w1.t()                                                         # (R, 5H)
@@ -182,46 +216,73 @@ class _Heads(torch.autograd.Function):
         z2 = torch.empty((R, H5), dtype=bf, device=dev)
         nat.call("ov3d_rows_bn_apply", h2, 1, *headmajor, R, H5, a2, s2, float(p2), seed,
                  pack.sites[1], z2, *rowmajor, like=x)
-        w3vb, w3sb = w3v.to(bf), w3s.to(bf)
-        out_v = torch.addmm(b3v.to(bf), z2[:, :H], w3vb.t())
-        out_s = torch.addmm(b3s.to(bf), z2[:, H:], w3sb.t())
-        ctx.save_for_backward(xb, h1, h2, z1, z2, w1, w2, w3vb, w3sb, m1, i1, a1, s1, m2, i2, a2, s2)
+        # output layers + the text alignment: one launch (csrc/headsout.hip)
+        w3 = [gemm.cast_param(w.view(w.shape[0], -1), bf) for w in params[-10:-5]]
+        b3 = list(params[-5:])
+        lay = pack.out_layout(w3)
+        Nv, Ns = w3[0].shape[0], lay["Ns"]
+        out_v = torch.empty((R, Nv), dtype=torch.float32, device=dev)
+        out_s = torch.empty((R, Ns), dtype=torch.float32, device=dev)
+        T = text.shape[0] if text is not None else 0
+        logits = torch.empty((R, T), dtype=torch.float32, device=dev) if text is not None else None
+        ws = (ctypes.c_void_p * 4)(*[w.data_ptr() for w in w3[1:]])
+        bs = (ctypes.c_void_p * 4)(*[b.data_ptr() for b in b3[1:]])
+        nat.call("ov3d_heads_out_fwd", z2, H5, R, w3[0], b3[0], Nv, text, T, int(lq), out_v, logits,
+                 4, ctypes.addressof(ws), ctypes.addressof(bs), ctypes.addressof(lay["n"]),
+                 ctypes.addressof(lay["kcol"]), ctypes.addressof(lay["ocol"]), out_s, Ns, like=x)
+        ctx.save_for_backward(xb, h1, h2, z1, z2, w1, w2, *w3, m1, i1, a1, s1, m2, i2, a2, s2, text)
         ctx.seed = seed   # the forward's dropout snapshot (attention._seed)
-        ctx.meta = (pack, float(p1), float(p2), R, x.dtype, w3s.shape)
-        return out_v.float(), out_s.float()
+        ctx.meta = (pack, float(p1), float(p2), R, x.dtype, int(lq), [w.shape for w in params[-10:-5]])
+        if logits is None:
+            return out_v, out_s
+        return out_v, out_s, logits
 
     @staticmethod
-    def backward(ctx, gv, gs):
-        (xb, h1, h2, z1, z2, w1, w2, w3vb, w3sb, m1, i1, a1, s1, m2, i2, a2, s2) = ctx.saved_tensors
-        pack, p1, p2, R, xdt, w3s_shape = ctx.meta
+    def backward(ctx, gv, gs, glog=None):
+        (xb, h1, h2, z1, z2, w1, w2, w3v, w3a, w3b, w3c, w3d, m1, i1, a1, s1, m2, i2, a2, s2,
+         text) = ctx.saved_tensors
+        w3 = [w3v, w3a, w3b, w3c, w3d]
+        pack, p1, p2, R, xdt, lq, w3_shapes = ctx.meta
         st = pack.store
         H = pack.H
         H5 = 5 * H
         bf = torch.bfloat16
         dev = xb.device
         seed = ctx.seed
-        gv = gv.to(bf).contiguous()
-        gs = gs.to(bf).contiguous()
+        lay = pack.out_layout(w3)
+        Nv, Ns = w3v.shape[0], lay["Ns"]
+        T = text.shape[0] if text is not None else 0
+        # g_v + g_logits . text and the box heads' output gradients in bf16, the box heads'
+        # input gradient into dz2[:, H:]: one launch; the visual input gradient on the BLAS
+        gv = gv.contiguous()
+        gs = gs.contiguous()
+        if glog is not None:
+            glog = glog.contiguous()
+        gvb = torch.empty((R, Nv), dtype=bf, device=dev)
+        gsb = torch.empty((R, Ns), dtype=bf, device=dev)
+        dz2 = torch.empty((R, H5), dtype=bf, device=dev)
+        ws = (ctypes.c_void_p * 4)(*[w.data_ptr() for w in w3[1:]])
+        nat.call("ov3d_heads_out_bwd", gv, glog if text is not None else None, text, R, Nv, T, lq,
+                 gs, Ns, 4, ctypes.addressof(ws), ctypes.addressof(lay["n"]),
+                 ctypes.addressof(lay["kcol"]), ctypes.addressof(lay["ocol"]), gvb, gsb, dz2, H5,
+                 like=xb)
+        torch.mm(gvb, w3v, out=dz2[:, :H])
         # weight gradients: queued for the grouped launch at the end of the backward
         # (gemm.DEFER_WGRAD) as one problem per head parameter, else computed here
         P = pack.parts
         defer = gemm.DEFER_WGRAD and all(
             gemm.can_defer(xb, m.weight, m.bias) for p in P for m in (p[0], p[3], p[6]))
-        if defer:
-            gemm.defer_weight_grad(gv, z2[:, :H], P[0][6].weight, P[0][6].bias)
-            o = 0
-            for i, p in enumerate(P[1:], start=1):
-                n = p[6].weight.shape[0]
-                gemm.defer_weight_grad(gs[:, o:o + n], z2[:, i * H:(i + 1) * H], p[6].weight,
-                                       p[6].bias)
-                o += n
-            dw3v = db3v = dw3s = db3s = None
-        else:
-            dw3v, db3v = fused_weight_grad(gv, z2[:, :H], bias=True)
-            dw3s, db3s = fused_weight_grad(gs, z2[:, H:], bias=True)
-        dz2 = torch.empty((R, H5), dtype=bf, device=dev)
-        torch.mm(gv, w3vb, out=dz2[:, :H])
-        torch.mm(gs, w3sb, out=dz2[:, H:])
+        d3 = [None] * 10
+        gsl = [gvb]
+        for i in range(4):
+            o = lay["ocol"][i]
+            gsl.append(gsb[:, o:o + lay["n"][i]])
+        for i, p in enumerate(P):
+            if defer:
+                gemm.defer_weight_grad(gsl[i], z2[:, i * H:(i + 1) * H], p[6].weight, p[6].bias)
+            else:
+                dw, db = fused_weight_grad(gsl[i], z2[:, i * H:(i + 1) * H], bias=True)
+                d3[i], d3[5 + i] = dw.view(w3_shapes[i]), db
         rowmajor = (H5, 0, H5)
         headmajor = (H, R * H, H)
         # BN2 (input h2 head-major, grad dz2 row-major) -> dh2 head-major
@@ -257,8 +318,7 @@ class _Heads(torch.autograd.Function):
             step = g.numel() // 5
             shape = pack._tensors()[key][0].shape
             out += [g[i * step:(i + 1) * step].view(shape) for i in range(5)]
-        return (dx, None, None, None, dw3v, db3v,
-                dw3s.view(w3s_shape) if dw3s is not None else None, db3s, *out)
+        return (dx, None, None, None, None, None, *out, *d3)
 
 
 def _bn_backward(dz, lz, x, lx, R, C, gamma, mean, invstd, scale, shift, p, seed, site, dx, ld,
@@ -274,30 +334,43 @@ def _bn_backward(dz, lz, x, lx, R, C, gamma, mean, invstd, scale, shift, p, seed
     return dg, db
 
 
-def fused_heads(pack, rows):
-    """rows (R, 256) -> {head name: (R, out) fp32} for the five MLP heads (training)."""
+def fused_heads(pack, rows, sem=None, lq=0):
+    """rows (R, 256) -> {head name: (R, out) fp32} for the five MLP heads (training); with
+    `sem` (the sem_cls_head Linear: frozen text embedding, no bias, T <= 32) also
+    "sem_cls_logits" (R, T), in the reference's transposed layout (quirk Q8) when lq = Q > 0."""
     pack.ensure()
     P = pack.parts
     p1 = P[0][2].p if P[0][2].training else 0.0
     p2 = P[0][5].p if P[0][5].training else 0.0
-    w3v, b3v = P[0][6].weight, P[0][6].bias
-    small = P[1:]
-    outs = [p[6].weight.shape[0] for p in small]
-    w3s = torch.block_diag(*[p[6].weight.view(p[6].weight.shape[0], -1) for p in small])
-    b3s = torch.cat([p[6].bias for p in small])
+    text = None
+    if sem is not None and text_alignment_ok(sem, P[0][6].weight.shape[0]):
+        text = sem.weight
     params = []
     for key, ts in pack._tensors().items():
         if key in ("rm1", "rv1", "rm2", "rv2"):
             continue
         params += ts
-    out_v, out_s = _Heads.apply(rows, pack, p1, p2, w3v.view(w3v.shape[0], -1), b3v, w3s, b3s,
-                                *params)
+    gemm.ensure_fresh(params[:10])
+    params += [p[6].weight for p in P] + [p[6].bias for p in P]
+    res_t = _Heads.apply(rows, pack, p1, p2, text, lq if text is not None else 0, *params)
+    out_v, out_s = res_t[0], res_t[1]
     res = {HEAD_ORDER[0]: out_v, "_raw": out_s}   # _raw: [center | size | angle cls | angle res]
+    if text is not None:
+        res["sem_cls_logits"] = res_t[2]
     o = 0
-    for name, n in zip(HEAD_ORDER[1:], outs):
+    for name, p in zip(HEAD_ORDER[1:], P[1:]):
+        n = p[6].weight.shape[0]
         res[name] = out_s[:, o:o + n]
         o += n
     return res
+
+
+def text_alignment_ok(sem, nv):
+    """the alignment Linear folds into the output launch: frozen (T, nv) fp32 weight, no bias"""
+    w = sem.weight
+    return (isinstance(sem, nn.Linear) and sem.bias is None and not w.requires_grad and w.is_cuda
+            and w.dtype == torch.float32 and w.is_contiguous() and w.shape[1] == nv
+            and 0 < w.shape[0] <= nat.load().ov3d_heads_out_max_text())
 
 
 # ------------------------------------------------------------------------- BN + ReLU rows

@@ -253,7 +253,10 @@ class Model3DETR(nn.Module):
             if getattr(self, "_head_pack", None) is None:
                 self._head_pack = heads_mod.HeadPack(self.mlp_heads)
             if heads_mod.supported(self._head_pack, rows):
-                pre = heads_mod.fused_heads(self._head_pack, rows)
+                # the text alignment folds into the heads' output launch (Q8 layout written
+                # there when the reference layout is kept)
+                pre = heads_mod.fused_heads(self._head_pack, rows, sem=self.mlp_heads["sem_cls_head"],
+                                            lq=Q if self.cls_logits_layout == "reference" else 0)
         with torch.autocast(device_type=box_features.device.type, enabled=False):
             return self._box_predictions(query_xyz.float(), point_cloud_dims, rows.float(),
                                          (L, Q, B), pre)
@@ -271,9 +274,12 @@ class Model3DETR(nn.Module):
             return heads[name].rows(rows).view(L, B, Q, -1)
 
         visual = head("visual_embed_head")                                  # (L, B, Q, 640)
-        logits = heads["sem_cls_head"](visual)                              # (L, B, Q, T)
-        if self.cls_logits_layout == "reference":
-            logits = logits.reshape(L * B, Q, -1).transpose(1, 2).reshape(L, B, Q, -1)   # Q8
+        if pre is not None and "sem_cls_logits" in pre:   # the heads' launch, final layout
+            logits = pre["sem_cls_logits"].view(L, B, Q, -1)
+        else:
+            logits = heads["sem_cls_head"](visual)                          # (L, B, Q, T)
+            if self.cls_logits_layout == "reference":
+                logits = logits.reshape(L * B, Q, -1).transpose(1, 2).reshape(L, B, Q, -1)   # Q8
         center_offset = head("center_head").sigmoid() - 0.5
         size_norm = head("size_head").sigmoid()
         angle_logits = head("angle_cls_head")
@@ -314,9 +320,12 @@ class Model3DETR(nn.Module):
     def _box_predictions_fused(self, query_xyz, point_cloud_dims, pre, L, Q, B):
         """same outputs as _box_predictions, the parametrisation in one HIP launch each way"""
         visual = pre["visual_embed_head"].view(L, B, Q, -1)
-        logits = self.mlp_heads["sem_cls_head"](visual)                     # (L, B, Q, T)
-        if self.cls_logits_layout == "reference":
-            logits = logits.reshape(L * B, Q, -1).transpose(1, 2).reshape(L, B, Q, -1)   # Q8
+        if "sem_cls_logits" in pre:   # computed by the heads' output launch, final layout
+            logits = pre["sem_cls_logits"].view(L, B, Q, -1)
+        else:
+            logits = self.mlp_heads["sem_cls_head"](visual)                 # (L, B, Q, T)
+            if self.cls_logits_layout == "reference":
+                logits = logits.reshape(L * B, Q, -1).transpose(1, 2).reshape(L, B, Q, -1)   # Q8
         NB = self.box_processor.dataset_config.num_angle_bin
         (center_n, center_u, size_n, size_u, angle_logits, angle_res_norm, angle_res, angle,
          corners, sem_prob, obj_prob) = _BoxParam.apply(pre["_raw"], query_xyz, point_cloud_dims[0],

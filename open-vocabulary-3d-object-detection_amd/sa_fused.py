@@ -132,7 +132,14 @@ def bn_bwd_affine(parts, nparts, C, group, count, gamma, mean, invstd):
     """(nparts, 2C) partial (sum dt, sum dt*xhat) -> cA, cB, cC, dgamma, dbeta (one launch
     for a single replica)"""
     if group is not None:
-        return _bwd_coefs(_totals(parts, nparts, 2 * C, group), count, gamma, mean, invstd, C)
+        # SyncBatchNorm: the input-gradient coefficients from the totals over every rank, the
+        # weight / bias gradients from this rank's own rows (torch's SyncBatchNorm.backward
+        # returns the local sums; the data-parallel gradient mean averages them)
+        tot = _totals(parts, nparts, 2 * C, None)
+        db, dg = tot[:C].float(), tot[C:].float()
+        dist.all_reduce(tot, group=group)
+        cA, cB, cC, _, _ = _bwd_coefs(tot, count, gamma, mean, invstd, C, local=False)
+        return cA, cB, cC, dg, db
     dev = parts.device
     cA, cB, cC, dg, db = (torch.empty(C, dtype=torch.float32, device=dev) for _ in range(5))
     nat.call("ov3d_bn_bwd_stats_finalize", parts, nparts, C, float(count), gamma, mean, invstd,
@@ -147,9 +154,11 @@ def _bn_stats(parts, nparts, C, group, count, bn):
                      bn.running_mean, bn.running_var, nbt)
 
 
-def _bwd_coefs(tot, count, gamma, mean, invstd, C):
+def _bwd_coefs(tot, count, gamma, mean, invstd, C, local=True):
     dev = tot.device
-    cA, cB, cC, dg, db = (torch.empty(C, dtype=torch.float32, device=dev) for _ in range(5))
+    cA, cB, cC = (torch.empty(C, dtype=torch.float32, device=dev) for _ in range(3))
+    dg, db = ((torch.empty(C, dtype=torch.float32, device=dev) for _ in range(2)) if local
+              else (None, None))
     nat.call("ov3d_bn_bwd_finalize", tot, float(count), C, gamma, mean, invstd, cA, cB, cC, dg, db,
              like=tot)
     return cA, cB, cC, dg, db

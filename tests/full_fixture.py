@@ -24,6 +24,7 @@ GRAD_FLOOR = 1e-6        # as make_golden.py: below 1e-6 x the total norm a grad
 # bf16 autocast: GEMM / attention inputs rounded to 8 mantissa bits (2^-9 = 2e-3 relative per
 # element); through 3 encoder + 8 decoder layers the outputs move by a few 1e-2 of their max
 BF16_TOL = dict(out=5e-2, loss=3e-2, grad_norm=5e-2, grad=1e-1, grad_proj=1e-1)
+BF16_GRAD_FLOOR = 1e-3   # bf16: gradients below this fraction of the total norm count as zero
 
 
 def build(fx, device, dataset):

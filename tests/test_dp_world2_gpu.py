@@ -72,7 +72,7 @@ def _rank(rank, port, out_dir):
     loss.backward()
     named = [(n, p) for n, p in model.named_parameters() if p.grad is not None]
     avg = pdist.all_reduce_coalesced([p.grad for _, p in named], average=True)
-    torch.save({"loss": loss.detach().cpu(),
+    torch.save({"loss": loss.item(),
                 "grads": {n: g.float().cpu() for (n, _), g in zip(named, avg)},
                 "bufs": {n: t.cpu() for n, t in model.named_buffers()}},
                os.path.join(out_dir, f"r{rank}.pt"))
@@ -93,26 +93,50 @@ def test_world2_step_equals_global_batch_step(cuda):
     saved = (crit_mod.all_reduce_average, pdist.all_reduce_average, pdist.get_world_size)
     crit_mod.all_reduce_average = pdist.all_reduce_average = lambda t: nbox.sum() / WORLD
     pdist.get_world_size = lambda: WORLD
-    try:
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+
+    def global_step(amp):
+        model.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
             out = model(_inputs(batch))
         losses = [crit(_slice_outputs(out, r), {k: v[r: r + 1] for k, v in batch.items()})[0]
                   for r in range(WORLD)]
         (sum(losses) / WORLD).backward()
+        return [x.item() for x in losses], {n: p.grad.float().cpu().clone()
+                                            for n, p in model.named_parameters()
+                                            if p.grad is not None}
+    try:
+        # the float32 step first: the BN running statistics compared below are the bf16 step's
+        state = {k: v.clone() for k, v in model.state_dict().items()}
+        _, g32 = global_step(False)
+        model.load_state_dict(state)
+        losses, g16 = global_step(True)
     finally:
         crit_mod.all_reduce_average, pdist.all_reduce_average, pdist.get_world_size = saved
     for r in range(WORLD):
-        assert abs(res[r]["loss"].item() - losses[r].item()) <= 5e-3 * abs(losses[r].item()), r
-    checked = 0
-    for n, p in model.named_parameters():
-        if p.grad is None:
-            continue
-        g = p.grad.float().cpu()
+        assert abs(res[r]["loss"] - losses[r]) <= 5e-3 * abs(losses[r]), r
+    checked = noisy = 0
+    ratios = []
+    for n, g in g16.items():
         assert torch.equal(res[0]["grads"][n], res[1]["grads"][n]), n
         if g.norm() > 1e-6:
             err = ((res[0]["grads"][n] - g).norm() / g.norm()).item()
-            assert err < 3e-2, (n, err)
+            # bf16 rounding alone moves a gradient by |g_bf16 - g_fp32| (the deepest layers by
+            # several 1e-2); two such roundings (the two-rank and the one-process step, different
+            # GEMM shapes and summation orders) differ by a few times that.  Per entry within 4x
+            # that noise, and the median entry within 1.5x: a semantic error (e.g. SyncBatchNorm
+            # weight gradients summed over ranks before the mean: 2x) fails both.
+            noise = ((g - g32[n]).norm() / g32[n].norm().clamp_min(1e-12)).item()
+            bar = max(3e-2, 4.0 * noise)
+            noisy += bar > 3e-2
+            ratios.append((err / max(noise, 1e-3), n, err, noise, bar))
             checked += 1
+    worst = sorted(ratios, reverse=True)
+    print("largest err/noise:", [("%.1f" % r, n, "%.2e" % e, "%.2e" % z) for r, n, e, z, _ in worst[:12]])
+    bad = [(n, e, z) for r, n, e, z, b in worst if e >= b]
+    assert not bad, bad
+    med = sorted(r for r, *_ in ratios)[len(ratios) // 2]
+    print(f"{checked} gradients checked, {noisy} against their bf16 noise, median err/noise {med:.2f}")
+    assert med <= 1.5, med
     assert checked > 100
     nb = 0
     for n, t in model.named_buffers():

