@@ -306,7 +306,7 @@ int ov3d_project_box2d(const float* center, const float* size, const float* head
  * models/helpers.py:45-112) and sem_cls_head = Linear(640, T, bias=False) over the visual
  * embedding (model_3detr.py:152-154, 237-238).
  *   z (R, ldz) bf16 hidden rows: visual head columns [0, 256), box head i at kcol[i]
- *   wv (Nv, 256) bf16, bv (Nv) f32 -> out_v (R, Nv) f32 (Nv % 32 == 0)
+ *   wv (Nv, 256) bf16, bv (Nv) f32 -> out_v (R, Nv) f32 (Nv = 640, the CLIP embedding)
  *   text (T, Nv) f32 (T <= ov3d_heads_out_max_text(); null = no alignment) -> logits f32,
  *     row-major (R, T) when lq == 0, else the reference's transposed layout of quirk Q8:
  *     (lb, q, t) at lb*lq*T + t*lq + q

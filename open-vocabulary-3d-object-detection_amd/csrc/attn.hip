@@ -352,6 +352,16 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) o[0][i] = o[1][i] = 0.f;
     float m = -INFINITY, l = 0.f;
+    // row sums on the matrix cores: an all-ones A operand times the (undropped) P^T packs
+    // gives every accumulator row the column sums = each lane's query row sum over the 64 keys
+    // of the tile (both lane halves), 4 MFMAs per tile instead of 32 VALU adds (the loop is
+    // VALU-issue bound); element 0 carries the running sum (the rescale touches only it)
+    f32x16 lacc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) lacc[i] = 0.f;
+    bf16x8 ones;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.f;
 
     if (kbeg < kend) {
         load(kbeg);
@@ -431,6 +441,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
                 const float alpha = (MASK && mnew == -INFINITY) ? 1.f : fast_exp2((m - mnew) * a.scale2);
                 m = mnew;
                 l *= alpha;
+                lacc[0] *= alpha;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     o[0][i] *= alpha;
@@ -447,16 +458,19 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
             const s16x2 tsig = {ts, ts};
             float rs0 = 0.f, rs1 = 0.f;
             uint32_t dw = 0;   // this lane's drop word of the tile
-            u32x4 pw[2][2];
+            u32x4 pw[2][2], praw[2][2];
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int i = 0; i < 16; i += 2) {
                     float p0 = fast_exp2(fmaf(st[t][i], a.scale2, -mb));
                     float p1 = fast_exp2(fmaf(st[t][i + 1], a.scale2, -mb));
+#ifdef OV3D_ATTN_VALU_ROWSUM
                     rs0 += p0;
                     rs1 += p1;
+#endif
                     uint32_t pk = pack_bf16(p0, p1);
+                    praw[t][i >> 3][(i & 7) >> 1] = pk;
                     if (DROP && BITS) {
                         // keep bits 8t + (i>>1) (even key) and 16 + 8t + (i>>1) (odd key) move
                         // to bits 15 and 31; one packed arithmetic shift spreads each over its
@@ -487,6 +501,9 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
                     const bf16x8 pf = __builtin_bit_cast(bf16x8, pw[t][s]);
 #pragma unroll
                     for (int dt = 0; dt < 2; ++dt) o[dt] = mfma(va[dt][t][s], pf, o[dt]);
+#ifndef OV3D_ATTN_VALU_ROWSUM
+                    lacc = mfma(ones, __builtin_bit_cast(bf16x8, praw[t][s]), lacc);
+#endif
                 }
         }
         PROBE(4);
@@ -498,7 +515,11 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     PROBE_END;
     if (!active) return;
     if (DROP && !BITS && kend > kbeg) store_drop((kend - 1) & ~(KB - 1));
+#ifdef OV3D_ATTN_VALU_ROWSUM
     const float ltot = l + __shfl_xor(l, 32);
+#else
+    const float ltot = lacc[0];
+#endif
     const int q = q0 + r;
     if (a.nsplit == 1) {
         const float inv = ltot > 0.f ? a.keep_scale / ltot : 0.f;

@@ -37,6 +37,8 @@ constexpr int RB = 32;          // rows per workgroup
 constexpr int KH = 256;         // hidden width of every head
 constexpr int MAXT = 32;        // text rows (classes) the fused alignment supports
 constexpr int MAXS = 4;         // box heads
+constexpr int NV = 640;         // visual embedding width (clip_embed_length)
+constexpr int VT = NV / 32 / 4; // visual output tiles per wave
 
 struct HeadsOutArgs {
     const bf16* z;              // (R, ldz) bf16
@@ -60,6 +62,13 @@ struct HeadsOutArgs {
     int Ns;
 };
 
+// element i (0..3, wave-uniform) of a kernel-argument array without a dynamic index (which
+// would copy the argument struct into scratch)
+template <class T>
+__device__ __forceinline__ T pick4(const T (&v)[MAXS], int i) {
+    return i == 0 ? v[0] : i == 1 ? v[1] : i == 2 ? v[2] : v[3];
+}
+
 // copy n4 float4 from global to LDS with every thread's loads in flight together (a plain
 // load -> store loop waits out one global latency per iteration)
 __device__ __forceinline__ void stage_f4(float4* __restrict__ dst, const float4* __restrict__ src, int n4,
@@ -70,7 +79,7 @@ __device__ __forceinline__ void stage_f4(float4* __restrict__ dst, const float4*
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int i = base + 256 * u + tid;
-            if (i < n4) v[u] = src[i];
+            v[u] = src[i < n4 ? i : n4 - 1];   // clamped, unconditional (keeps v in registers)
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -113,10 +122,14 @@ __device__ __forceinline__ f32x16 tile_gemm(const bf16* __restrict__ w, int nrow
     return acc;
 }
 
-__global__ void __launch_bounds__(256) heads_out_fwd_kernel(HeadsOutArgs a) {
+// TMAX: the text rows rounded up (8, 16, 24 or 32); rows T..TMAX-1 of the LDS image are zero,
+// so the logit loops are branch-free and their LDS reads batch (a per-row `t < T` branch
+// waited out one LDS round trip per read)
+template <int TMAX>
+__global__ void __launch_bounds__(256, 1) heads_out_fwd_kernel(HeadsOutArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    float* textS = smem;                         // (T, Nv)
-    float* red = smem + (size_t)a.T * a.Nv;      // (4 waves, 32 rows, T)
+    float* textS = smem;                         // (TMAX, Nv), zero rows past T
+    float* red = smem + (size_t)TMAX * a.Nv;     // (4 waves, 32 rows, TMAX)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int row0 = blockIdx.x * RB;
@@ -126,6 +139,8 @@ __global__ void __launch_bounds__(256) heads_out_fwd_kernel(HeadsOutArgs a) {
     if (align) {
         stage_f4(reinterpret_cast<float4*>(textS), reinterpret_cast<const float4*>(a.text),
                  a.T * a.Nv / 4, tid);
+        for (int i = a.T * a.Nv / 4 + tid; i < TMAX * a.Nv / 4; i += 256)
+            reinterpret_cast<float4*>(textS)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         __syncthreads();
     }
     // this lane's row, visual columns [0, 256)
@@ -135,53 +150,56 @@ __global__ void __launch_bounds__(256) heads_out_fwd_kernel(HeadsOutArgs a) {
 #pragma unroll
         for (int s = 0; s < KH / 16; ++s) zf[s] = *reinterpret_cast<const bf16x8*>(zr + 16 * s);
     }
-    float lg[MAXT];
+    // the wave's VT visual tiles (channels 32 (wave + 4k) ..), kept for the logits
+    float v[VT][16];
 #pragma unroll
-    for (int t = 0; t < MAXT; ++t) lg[t] = 0.f;
-    const int nvt = a.Nv / 32;
-    for (int ct = wave; ct < nvt; ct += 4) {
+    for (int k = 0; k < VT; ++k) {
+        const int ct = wave + 4 * k;
         const f32x16 acc = tile_gemm(a.wv + (size_t)ct * 32 * KH, 32, zf, r, h);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int ch = 32 * ct + 8 * g + 4 * h;
             const float4 b4 = *reinterpret_cast<const float4*>(a.bv + ch);
-            const float4 v = make_float4(acc[4 * g] + b4.x, acc[4 * g + 1] + b4.y,
-                                         acc[4 * g + 2] + b4.z, acc[4 * g + 3] + b4.w);
-            if (row < a.R) *reinterpret_cast<float4*>(a.out_v + (size_t)row * a.Nv + ch) = v;
-            if (align) {
-#pragma unroll
-                for (int t = 0; t < MAXT; ++t) {
-                    if (t < a.T) {
-                        const float4 tx = *reinterpret_cast<const float4*>(textS + (size_t)t * a.Nv + ch);
-                        lg[t] = fmaf(v.x, tx.x, fmaf(v.y, tx.y, fmaf(v.z, tx.z, fmaf(v.w, tx.w, lg[t]))));
-                    }
-                }
-            }
+            v[k][4 * g] = acc[4 * g] + b4.x;
+            v[k][4 * g + 1] = acc[4 * g + 1] + b4.y;
+            v[k][4 * g + 2] = acc[4 * g + 2] + b4.z;
+            v[k][4 * g + 3] = acc[4 * g + 3] + b4.w;
+            if (row < a.R)
+                *reinterpret_cast<float4*>(a.out_v + (size_t)row * a.Nv + ch) =
+                    make_float4(v[k][4 * g], v[k][4 * g + 1], v[k][4 * g + 2], v[k][4 * g + 3]);
         }
     }
     if (align) {
 #pragma unroll
-        for (int t = 0; t < MAXT; ++t)
-            if (t < a.T) lg[t] += __shfl_xor(lg[t], 32);
-        if (h == 0) {
+        for (int t = 0; t < TMAX; ++t) {
+            float lg = 0.f;
 #pragma unroll
-            for (int t = 0; t < MAXT; ++t)
-                if (t < a.T) red[((size_t)wave * RB + r) * a.T + t] = lg[t];
+            for (int k = 0; k < VT; ++k)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int ch = 32 * (wave + 4 * k) + 8 * g + 4 * h;
+                    const float4 tx = *reinterpret_cast<const float4*>(textS + (size_t)t * a.Nv + ch);
+                    lg = fmaf(v[k][4 * g], tx.x, fmaf(v[k][4 * g + 1], tx.y,
+                         fmaf(v[k][4 * g + 2], tx.z, fmaf(v[k][4 * g + 3], tx.w, lg))));
+                }
+            lg += __shfl_xor(lg, 32);
+            if (h == 0) red[((size_t)wave * RB + r) * TMAX + t] = lg;
         }
     }
     // box head `wave`: its 256 input columns, one tile
     if (wave < a.ns) {
-        const bf16* zr = a.z + (size_t)rowc * a.ldz + a.kcol[wave] + 8 * h;
+        const bf16* zr = a.z + (size_t)rowc * a.ldz + pick4(a.kcol, wave) + 8 * h;
 #pragma unroll
         for (int s = 0; s < KH / 16; ++s) zf[s] = *reinterpret_cast<const bf16x8*>(zr + 16 * s);
-        const int n = a.n[wave];
-        const f32x16 acc = tile_gemm(a.ws[wave], n, zf, r, h);
+        const int n = pick4(a.n, wave);
+        const f32x16 acc = tile_gemm(pick4(a.ws, wave), n, zf, r, h);
         if (row < a.R) {
-            float* o = a.out_s + (size_t)row * a.Ns + a.ocol[wave];
+            float* o = a.out_s + (size_t)row * a.Ns + pick4(a.ocol, wave);
+            const float* bsw = pick4(a.bs, wave);
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
                 const int c = 8 * (e >> 2) + 4 * h + (e & 3);
-                if (c < n) o[c] = acc[e] + a.bs[wave][c];
+                if (c < n) o[c] = acc[e] + bsw[c];
             }
         }
     }
@@ -190,8 +208,8 @@ __global__ void __launch_bounds__(256) heads_out_fwd_kernel(HeadsOutArgs a) {
         for (int i = tid; i < RB * a.T; i += 256) {
             const int rr = i / a.T, t = i - rr * a.T;
             if (row0 + rr >= a.R) continue;
-            const float s = red[(size_t)rr * a.T + t] + red[((size_t)RB + rr) * a.T + t] +
-                            red[((size_t)2 * RB + rr) * a.T + t] + red[((size_t)3 * RB + rr) * a.T + t];
+            const float s = red[(size_t)rr * TMAX + t] + red[((size_t)RB + rr) * TMAX + t] +
+                            red[((size_t)2 * RB + rr) * TMAX + t] + red[((size_t)3 * RB + rr) * TMAX + t];
             a.logits[logit_at(a, row0 + rr, t)] = s;
         }
     }
@@ -214,26 +232,41 @@ struct HeadsOutBwdArgs {
     long long lddz;
 };
 
-__global__ void __launch_bounds__(256) heads_out_bwd_kernel(HeadsOutBwdArgs a) {
+// 320 threads: thread (c4 = tid % 160, half = tid / 160) owns 4 visual columns of 16 rows,
+// its text columns in registers (TMAX float4, zero past T), the rows' logit gradients read
+// from LDS four classes at a time (broadcast); the box heads' part on every thread
+constexpr int BT = 320;
+template <int TMAX>
+__global__ void __launch_bounds__(BT) heads_out_bwd_kernel(HeadsOutBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    float* textS = smem;                               // (T, Nv)
-    float* gl = smem + (size_t)a.T * a.Nv;             // (32 rows, MAXT)
-    float* gsS = gl + RB * MAXT;                       // (32 rows, Ns) bf16-rounded
+    float* gl = smem;                                  // (32 rows, TMAX), zero past T
+    float* gsS = gl + RB * TMAX;                       // (32 rows, MAXS * 32) bf16-rounded
     bf16* wS = reinterpret_cast<bf16*>(gsS + RB * MAXS * 32);   // box heads' weights (Ns, 256)
     const int tid = threadIdx.x;
     const int row0 = blockIdx.x * RB;
     const int nrows = min(RB, a.R - row0);
     const bool align = a.glog != nullptr;
-    if (align)
-        stage_f4(reinterpret_cast<float4*>(textS), reinterpret_cast<const float4*>(a.text),
-                 a.T * a.Nv / 4, tid);
-    for (int hi = 0; hi < a.ns; ++hi)      // (n_i, 256) bf16 rows at row ocol[i]
-        stage_f4(reinterpret_cast<float4*>(wS + (size_t)a.ocol[hi] * KH),
-                 reinterpret_cast<const float4*>(a.ws[hi]), a.n[hi] * KH / 8, tid);
-    if (align) {
-        for (int i = tid; i < nrows * a.T; i += 256) {
-            const int rr = i / a.T, t = i - rr * a.T;
-            const int row = row0 + rr;
+    const int c4 = tid % (NV / 4), half = tid / (NV / 4);
+    float4 tx[TMAX];
+#pragma unroll
+    for (int t = 0; t < TMAX; ++t) {
+        const int tc = t < a.T ? t : 0;
+        const float4 x = align ? *reinterpret_cast<const float4*>(a.text + (size_t)tc * NV + 4 * c4)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float z = t < a.T ? 1.f : 0.f;
+        tx[t] = make_float4(x.x * z, x.y * z, x.z * z, x.w * z);
+    }
+    for (int hi = 0; hi < a.ns; ++hi) {    // (n_i, 256) bf16 rows at row ocol[i]
+        const int n8 = pick4(a.n, hi) * KH / 8;
+        for (int i = tid; i < n8; i += BT)
+            reinterpret_cast<float4*>(wS + (size_t)pick4(a.ocol, hi) * KH)[i] =
+                reinterpret_cast<const float4*>(pick4(a.ws, hi))[i];
+    }
+    for (int i = tid; i < RB * TMAX; i += BT) {
+        const int rr = i / TMAX, t = i - rr * TMAX;
+        const int row = row0 + rr;
+        float g = 0.f;
+        if (align && rr < nrows && t < a.T) {
             long long at;
             if (a.lq <= 0) {
                 at = (long long)row * a.T + t;
@@ -241,61 +274,69 @@ __global__ void __launch_bounds__(256) heads_out_bwd_kernel(HeadsOutBwdArgs a) {
                 const int lb = row / a.lq, q = row - lb * a.lq;
                 at = ((long long)lb * a.T + t) * a.lq + q;
             }
-            gl[rr * MAXT + t] = a.glog[at];
+            g = a.glog[at];
         }
+        gl[i] = g;
     }
-    for (int i = tid; i < nrows * a.Ns; i += 256) {
+    for (int i = tid; i < nrows * a.Ns; i += BT) {
         const int rr = i / a.Ns, j = i - rr * a.Ns;
         const bf16 v = (bf16)a.gs[(size_t)(row0 + rr) * a.Ns + j];
         a.gsb[(size_t)(row0 + rr) * a.Ns + j] = v;
-        gsS[rr * a.Ns + j] = (float)v;
+        gsS[rr * (MAXS * 32) + j] = (float)v;
     }
     __syncthreads();
-    // visual: 4 channels per item, U items' loads in flight per thread
-    constexpr int U = 4;
-    const int nv4 = a.Nv / 4;
-    const int nitems = nrows * nv4;
-    for (int base = tid; base < nitems; base += 256 * U) {
-        float4 g[U];
+    // visual: g_v + g_logits . text for 16 rows x 4 columns
+    if (half < 2) {
+#pragma unroll 4
+        for (int k = 0; k < RB / 2; ++k) {
+            const int rr = half * (RB / 2) + k;
+            if (rr >= nrows) break;
+            const size_t off = (size_t)(row0 + rr) * NV + 4 * c4;
+            float4 g = *reinterpret_cast<const float4*>(a.gv + off);
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int i = base + 256 * u;
-            if (i < nitems) {
-                const int rr = i / nv4, c4 = i - rr * nv4;
-                g[u] = *reinterpret_cast<const float4*>(a.gv + (size_t)(row0 + rr) * a.Nv + 4 * c4);
-            }
-        }
+            for (int t4 = 0; t4 < TMAX / 4; ++t4) {
+                const float4 w = *reinterpret_cast<const float4*>(gl + rr * TMAX + 4 * t4);
+                const float wv[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int i = base + 256 * u;
-            if (i >= nitems) continue;
-            const int rr = i / nv4, c4 = i - rr * nv4;
-            float4 v = g[u];
-            if (align) {
-                for (int t = 0; t < a.T; ++t) {
-                    const float w = gl[rr * MAXT + t];
-                    const float4 tx = *reinterpret_cast<const float4*>(textS + (size_t)t * a.Nv + 4 * c4);
-                    v.x = fmaf(w, tx.x, v.x);
-                    v.y = fmaf(w, tx.y, v.y);
-                    v.z = fmaf(w, tx.z, v.z);
-                    v.w = fmaf(w, tx.w, v.w);
+                for (int u = 0; u < 4; ++u) {
+                    const float4 x = tx[4 * t4 + u];
+                    g.x = fmaf(wv[u], x.x, g.x);
+                    g.y = fmaf(wv[u], x.y, g.y);
+                    g.z = fmaf(wv[u], x.z, g.z);
+                    g.w = fmaf(wv[u], x.w, g.w);
                 }
             }
             bf16x4 o;
-            o[0] = (bf16)v.x;
-            o[1] = (bf16)v.y;
-            o[2] = (bf16)v.z;
-            o[3] = (bf16)v.w;
-            *reinterpret_cast<bf16x4*>(a.gvb + (size_t)(row0 + rr) * a.Nv + 4 * c4) = o;
+            o[0] = (bf16)g.x;
+            o[1] = (bf16)g.y;
+            o[2] = (bf16)g.z;
+            o[3] = (bf16)g.w;
+            *reinterpret_cast<bf16x4*>(a.gvb + off) = o;
         }
     }
     // box heads' input gradient: 4 columns per item, weights from LDS
-    for (int i = tid; i < nrows * a.ns * (KH / 4); i += 256) {
-        const int c4 = i % (KH / 4), hi = (i / (KH / 4)) % a.ns, rr = i / (KH / 4 * a.ns);
+    for (int i = tid; i < nrows * a.ns * (KH / 4); i += BT) {
+        const int cc = i % (KH / 4), hi = (i / (KH / 4)) % a.ns, rr = i / (KH / 4 * a.ns);
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
-        const bf16* w = wS + (size_t)a.ocol[hi] * KH + 4 * c4;
-        const float* gr = gsS + rr * a.Ns + a.ocol[hi];
-        for (int j = 0; j < a.n[hi]; ++j) {
+        const int oc = pick4(a.ocol, hi);
+        const bf16* w = wS + (size_t)oc * KH + 4 * cc;
+        const float* gr = gsS + rr * (MAXS * 32) + oc;
+        const int n = pick4(a.n, hi);
+        int j = 0;
+        for (; j + 4 <= n; j += 4) {
+            bf16x4 wv[4];
+            float gj[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                wv[u] = *reinterpret_cast<const bf16x4*>(w + (size_t)(j + u) * KH);
+                gj[u] = gr[j + u];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[q] = fmaf(gj[u], (float)wv[u][q], acc[q]);
+        }
+        for (; j < n; ++j) {
             const bf16x4 wv = *reinterpret_cast<const bf16x4*>(w + (size_t)j * KH);
             const float gj = gr[j];
 #pragma unroll
@@ -304,12 +345,14 @@ __global__ void __launch_bounds__(256) heads_out_bwd_kernel(HeadsOutBwdArgs a) {
         bf16x4 o;
 #pragma unroll
         for (int q = 0; q < 4; ++q) o[q] = (bf16)acc[q];
-        *reinterpret_cast<bf16x4*>(a.dz + (size_t)(row0 + rr) * a.lddz + a.kcol[hi] + 4 * c4) = o;
+        *reinterpret_cast<bf16x4*>(a.dz + (size_t)(row0 + rr) * a.lddz + pick4(a.kcol, hi) + 4 * cc) = o;
     }
 }
 
+int tmax_of(int T) { return T <= 8 ? 8 : T <= 16 ? 16 : T <= 24 ? 24 : 32; }
+
 bool common_ok(int R, int Nv, int T, int ns, const int* n) {
-    if (R <= 0 || Nv <= 0 || Nv % 32 || T < 0 || T > MAXT || ns < 0 || ns > MAXS) return false;
+    if (R <= 0 || Nv != NV || T < 0 || T > MAXT || ns < 0 || ns > MAXS) return false;
     for (int i = 0; i < ns; ++i)
         if (n[i] <= 0 || n[i] > 32) return false;
     return true;
@@ -352,14 +395,23 @@ extern "C" int ov3d_heads_out_fwd(const void* z, long long ldz, int R, const voi
     if (KH > ldz) return OV3D_EINVAL;
     a.out_s = out_s;
     a.Ns = Ns;
-    const size_t lds = ((size_t)a.T * Nv + (a.T ? 4 * RB * a.T : 0)) * sizeof(float);
-    if (lds > 160 * 1024) return OV3D_EINVAL;
+    const int tm = tmax_of(a.T);
+    const size_t lds = a.T ? ((size_t)tm * Nv + 4 * RB * tm) * sizeof(float) : 0;
+    const void* fn = tm == 8 ? reinterpret_cast<const void*>(heads_out_fwd_kernel<8>)
+                   : tm == 16 ? reinterpret_cast<const void*>(heads_out_fwd_kernel<16>)
+                   : tm == 24 ? reinterpret_cast<const void*>(heads_out_fwd_kernel<24>)
+                              : reinterpret_cast<const void*>(heads_out_fwd_kernel<32>);
     if (lds > 64 * 1024 &&
-        hipFuncSetAttribute(reinterpret_cast<const void*>(heads_out_fwd_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return OV3D_ELAUNCH;
-    hipLaunchKernelGGL(heads_out_fwd_kernel, dim3((unsigned)((R + RB - 1) / RB)), dim3(256), lds,
-                       ov3d_stream(stream), a);
+    const dim3 grid((unsigned)((R + RB - 1) / RB));
+    hipStream_t st = ov3d_stream(stream);
+    switch (tm) {
+        case 8: hipLaunchKernelGGL(heads_out_fwd_kernel<8>, grid, dim3(256), lds, st, a); break;
+        case 16: hipLaunchKernelGGL(heads_out_fwd_kernel<16>, grid, dim3(256), lds, st, a); break;
+        case 24: hipLaunchKernelGGL(heads_out_fwd_kernel<24>, grid, dim3(256), lds, st, a); break;
+        default: hipLaunchKernelGGL(heads_out_fwd_kernel<32>, grid, dim3(256), lds, st, a); break;
+    }
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }
@@ -395,15 +447,16 @@ extern "C" int ov3d_heads_out_bwd(const float* gv, const float* glog, const floa
     a.gsb = static_cast<bf16*>(gsb);
     a.dz = static_cast<bf16*>(dz);
     a.lddz = lddz;
-    const size_t lds = ((size_t)a.T * Nv + RB * MAXT + RB * MAXS * 32) * sizeof(float) +
-                       (size_t)a.Ns * KH * sizeof(bf16);
-    if (lds > 160 * 1024) return OV3D_EINVAL;
-    if (lds > 64 * 1024 &&
-        hipFuncSetAttribute(reinterpret_cast<const void*>(heads_out_bwd_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-        return OV3D_ELAUNCH;
-    hipLaunchKernelGGL(heads_out_bwd_kernel, dim3((unsigned)((R + RB - 1) / RB)), dim3(256), lds,
-                       ov3d_stream(stream), a);
+    const int tm = tmax_of(a.T);
+    const size_t lds = ((size_t)RB * tm + RB * MAXS * 32) * sizeof(float) + (size_t)a.Ns * KH * sizeof(bf16);
+    const dim3 grid((unsigned)((R + RB - 1) / RB));
+    hipStream_t st = ov3d_stream(stream);
+    switch (tm) {
+        case 8: hipLaunchKernelGGL(heads_out_bwd_kernel<8>, grid, dim3(BT), lds, st, a); break;
+        case 16: hipLaunchKernelGGL(heads_out_bwd_kernel<16>, grid, dim3(BT), lds, st, a); break;
+        case 24: hipLaunchKernelGGL(heads_out_bwd_kernel<24>, grid, dim3(BT), lds, st, a); break;
+        default: hipLaunchKernelGGL(heads_out_bwd_kernel<32>, grid, dim3(BT), lds, st, a); break;
+    }
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

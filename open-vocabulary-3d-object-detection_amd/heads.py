@@ -8,9 +8,10 @@ heads are exactly one MLP over 5 x 256 channels with block-diagonal later layers
 
   layer 1  ONE GEMM            x (R,256) @ W1cat^T (1280,256)          -> h1 (R,1280)
   BN+ReLU+Dropout              csrc/bnrows.hip over 1280 channels       -> z1
-  layer 2  ONE batched GEMM    per head z1[:, 256i:256i+256] @ W2_i^T   -> h2 (5,R,256)
+  layer 2  ONE batched GEMM    per head z1[i] @ W2_i^T (z1 head-major)  -> h2 (5,R,256)
   BN+ReLU+Dropout              (head-major addressing)                  -> z2 (R,1280)
-  layer 3  visual: z2[:, :256] @ W3v^T;  box heads: z2[:, 256:] @ blockdiag(W3_1..4)^T
+  layer 3  ONE launch (csrc/headsout.hip): the five output layers on z2 + the text
+           alignment of the visual embedding
 
 Backward mirrors it; weight / bias gradients use the one-launch ov3d_wgrad kernel.
 The heads' parameters and BN buffers are re-pointed at shared storages (the module
@@ -206,11 +207,14 @@ class _Heads(torch.autograd.Function):
         rowmajor = (H5, 0, H5)
         m1, i1, a1, s1 = _stats_finalize(h1, rowmajor, R, H5, st["g1"], st["b1"], bn1, st["rm1"],
                                          st["rv1"])
-        z1 = torch.empty((R, H5), dtype=bf, device=dev)
-        nat.call("ov3d_rows_bn_apply", h1, 1, *rowmajor, R, H5, a1, s1, float(p1), seed,
-                 pack.sites[0], z1, *rowmajor, like=x)
-        h2 = torch.bmm(z1.view(R, 5, H).transpose(0, 1), w2.transpose(1, 2))  # (5, R, H)
+        # z1 written head-major (5, R, H): the second layer is a packed batched GEMM (batch
+        # stride R*H; the row-major z1 viewed per head had batch stride H inside rows of 5H,
+        # the layout the TunableOp solution faulted on)
         headmajor = (H, R * H, H)
+        z1 = torch.empty((5, R, H), dtype=bf, device=dev)
+        nat.call("ov3d_rows_bn_apply", h1, 1, *rowmajor, R, H5, a1, s1, float(p1), seed,
+                 pack.sites[0], z1, *headmajor, like=x)
+        h2 = torch.bmm(z1, w2.transpose(1, 2))                                  # (5, R, H)
         m2, i2, a2, s2 = _stats_finalize(h2, headmajor, R, H5, st["g2"], st["b2"], bn2, st["rm2"],
                                          st["rv2"])
         z2 = torch.empty((R, H5), dtype=bf, device=dev)
@@ -291,11 +295,11 @@ class _Heads(torch.autograd.Function):
                                  seed, pack.sites[1], dh2, headmajor, bn=pack.bns()[1][0])
         if defer:
             for i in range(5):
-                gemm.defer_weight_grad(dh2[i], z1[:, i * H:(i + 1) * H], P[i][3].weight)
+                gemm.defer_weight_grad(dh2[i], z1[i], P[i][3].weight)
         else:
             dw2 = torch.empty((5, H, H), dtype=torch.float32, device=dev)
             for i in range(5):
-                fused_weight_grad(dh2[i], z1[:, i * H:(i + 1) * H], bias=False, out_w=dw2[i])
+                fused_weight_grad(dh2[i], z1[i], bias=False, out_w=dw2[i])
         dz1 = torch.bmm(dh2, w2)                                                 # (5, R, H)
         dh1 = torch.empty((R, H5), dtype=bf, device=dev)
         dg1, dbe1 = _bn_backward(dz1, headmajor, h1, rowmajor, R, H5, st["g1"], m1, i1, a1, s1, p1,

@@ -4,8 +4,10 @@ bf16 product step as bench.py runs it eagerly -- fused SA MLP, heads and project
 kernels with SyncBatchNorm statistics all-reduced inside their launches (sa_fused.py,
 heads.py), num_boxes all-reduced by the criterion, the gradient mean by one all-reduce --
 against the single-process step on both scenes (BatchNorm over both, each scene's loss with
-the global num_boxes, their mean).  Reference semantics: main.py:427-431 (SyncBatchNorm +
-DDP), criterion.py:425."""
+the global num_boxes, their mean).  The Hungarian assignment is pinned to the one-process
+float32 step's (a random-init model's matching costs have near ties that bf16 rounding flips
+between any two runs).  Reference semantics: main.py:427-431 (SyncBatchNorm + DDP),
+criterion.py:425."""
 import os
 import socket
 import tempfile
@@ -58,12 +60,38 @@ def _slice_outputs(out, r):
     return {"outputs": one(out["outputs"]), "aux_outputs": [one(a) for a in out["aux_outputs"]]}
 
 
+def _pin(crit, asg):
+    """the matcher returns a fixed assignment: a random-init model's matching costs have near
+    ties that bf16 rounding flips between any two runs (flips move whole queries' gradients)"""
+    inds, mask = asg
+    crit.matcher.forward = lambda cost, nact: {"assignments": [], "per_prop_gt_inds": inds,
+                                               "proposal_matched_mask": mask}
+
+
+def _recording(crit, rec):
+    """record the matcher's assignment of each scene's criterion call (calls alternate
+    scene 0, scene 1) on its first call, replay it afterwards"""
+    orig = crit.matcher.forward
+    calls = [0]
+
+    def fwd(cost, nact):
+        r = calls[0] % WORLD
+        calls[0] += 1
+        if r not in rec:
+            a = orig(cost, nact)
+            rec[r] = (a["per_prop_gt_inds"].clone(), a["proposal_matched_mask"].clone())
+        return {"assignments": [], "per_prop_gt_inds": rec[r][0], "proposal_matched_mask": rec[r][1]}
+    crit.matcher.forward = fwd
+
+
 def _rank(rank, port, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(WORLD), LOCAL_RANK="0")
     torch.distributed.init_process_group("gloo", init_method="env://", world_size=WORLD, rank=rank)
     model, crit, batch, dev = _setup()
     from ov3d_amd import dist as pdist
+    pinned = torch.load(os.path.join(out_dir, "match.pt"), weights_only=True)[rank]
+    _pin(crit, [t.to(dev) for t in pinned])
     model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
     b = {k: v[rank: rank + 1] for k, v in batch.items()}
     with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -81,12 +109,11 @@ def _rank(rank, port, out_dir):
 
 
 def test_world2_step_equals_global_batch_step(cuda):
-    with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_rank, args=(_free_port(), d), nprocs=WORLD, join=True)
-        res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(WORLD)]
     from ov3d_amd import criterion as crit_mod
     from ov3d_amd import dist as pdist
     model, crit, batch, dev = _setup()
+    rec = {}
+    _recording(crit, rec)
     nbox = batch["gt_box_present"].sum(dim=1)
     # each scene's loss with the GLOBAL num_boxes (criterion.py:425 all_reduce_average over 2
     # ranks): the criterion's own call and the fused set-loss's target_counts read these
@@ -105,13 +132,18 @@ def test_world2_step_equals_global_batch_step(cuda):
                                             for n, p in model.named_parameters()
                                             if p.grad is not None}
     try:
-        # the float32 step first: the BN running statistics compared below are the bf16 step's
+        # the float32 step first (its matching is pinned for every later run); the BN running
+        # statistics compared below are the bf16 step's
         state = {k: v.clone() for k, v in model.state_dict().items()}
         _, g32 = global_step(False)
         model.load_state_dict(state)
         losses, g16 = global_step(True)
     finally:
         crit_mod.all_reduce_average, pdist.all_reduce_average, pdist.get_world_size = saved
+    with tempfile.TemporaryDirectory() as d:
+        torch.save({r: [t.cpu() for t in rec[r]] for r in range(WORLD)}, os.path.join(d, "match.pt"))
+        mp.spawn(_rank, args=(_free_port(), d), nprocs=WORLD, join=True)
+        res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(WORLD)]
     for r in range(WORLD):
         assert abs(res[r]["loss"] - losses[r]) <= 5e-3 * abs(losses[r]), r
     checked = noisy = 0
