@@ -232,6 +232,25 @@ __device__ __forceinline__ float neg_inf_if(float x, uint32_t w, int b) {
 // score bit of element i of score tile t in a query-major (drop / mask) word
 __device__ __forceinline__ constexpr int score_bit(int t, int i) { return ((i & 1) << 4) + 8 * t + (i >> 1); }
 
+// XCD-aware workgroup order: workgroup L of a launch runs on XCD L % 8 (the dispatcher's
+// round robin; an assumption for speed only, any order is correct).  With the (block, b*H+h)
+// grid taken in launch order every XCD would get 2 of the 16 workgroups of each (b, h), so
+// each XCD's L2 fetched every head's K / V (Q / dO): 8x the HBM reads (rocprofv3 FETCH_SIZE,
+// profiles/r03_pmc_summary_v1.json).  Remapped, XCD x runs all workgroups of heads
+// [x * H/8, (x+1) * H/8): each K / V reaches one L2.  Single-split grids with gridDim.y % 8 == 0.
+__device__ __forceinline__ void xcd_block(int& bx, int& by) {
+    const int nx = gridDim.x, ny = gridDim.y;
+    if (gridDim.z != 1 || (ny & 7)) {
+        bx = blockIdx.x;
+        by = blockIdx.y;
+        return;
+    }
+    const int L = blockIdx.x + nx * blockIdx.y;
+    const int j = L >> 3;
+    by = (L & 7) * (ny >> 3) + j / nx;
+    bx = j - (j / nx) * nx;
+}
+
 // Drop bits ahead of the forward (long attentions: the encoder's L = 2048): the query-major
 // and key-major words the forward would store, from the same hash, in a VALU-only pass; the
 // forward then reads one word per lane and tile (BITS) instead of hashing 16 key pairs on the
@@ -241,8 +260,9 @@ __device__ __forceinline__ constexpr int score_bit(int t, int i) { return ((i & 
 __global__ void __launch_bounds__(256) attn_dropgen_kernel(AttnArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int bh = blockIdx.y;
-    const int q0 = blockIdx.x * (4 * QW) + wave * QW;
+    int bx, bh;
+    xcd_block(bx, bh);
+    const int q0 = bx * (4 * QW) + wave * QW;
     if (q0 >= a.Lq) return;
     const uint32_t qh = drop_query_base(drop_head_mix(a.seed, a.site, bh), q0 + r) +
                         (uint32_t)(2 * h) * kPairMul;
@@ -276,8 +296,10 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     __shared__ __attribute__((aligned(16))) bf16 Vs[2][KB * LDK];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int bh = blockIdx.y, b = bh / a.H, hh = bh - b * a.H;
-    const int q0 = blockIdx.x * (4 * QW) + wave * QW;
+    int bx, bh;
+    xcd_block(bx, bh);
+    const int b = bh / a.H, hh = bh - b * a.H;
+    const int q0 = bx * (4 * QW) + wave * QW;
     const bool active = q0 < a.Lq;
     const int kbeg = blockIdx.z * a.keys_per_split;
     const int kend = min(a.Lk, kbeg + a.keys_per_split);
@@ -631,8 +653,10 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
     __shared__ __attribute__((aligned(16))) bf16 Vs[2][KB * LDK];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int bh = blockIdx.y, b = bh / a.H, hh = bh - b * a.H;
-    const int q0 = blockIdx.x * (4 * QW) + wave * QW;
+    int bx, bh;
+    xcd_block(bx, bh);
+    const int b = bh / a.H, hh = bh - b * a.H;
+    const int q0 = bx * (4 * QW) + wave * QW;
     const bool active = q0 < a.Lq;
     const int qi = active ? q0 + r : 0;
 
@@ -860,8 +884,10 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
     __shared__ __attribute__((aligned(16))) float Dv[2][QB];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int bh = blockIdx.y, b = bh / a.H, hh = bh - b * a.H;
-    const int k0 = blockIdx.x * (4 * 32) + wave * 32;
+    int bx, bh;
+    xcd_block(bx, bh);
+    const int b = bh / a.H, hh = bh - b * a.H;
+    const int k0 = bx * (4 * 32) + wave * 32;
     const bool active = k0 < a.Lk;
     const int ki = active ? min(k0 + r, a.Lk - 1) : 0;
     // the forward's key-major drop words of this lane's key: bit n of word (qblk, key) is

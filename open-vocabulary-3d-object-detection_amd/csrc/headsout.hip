@@ -150,16 +150,34 @@ __global__ void __launch_bounds__(256, 1) heads_out_fwd_kernel(HeadsOutArgs a) {
 #pragma unroll
         for (int s = 0; s < KH / 16; ++s) zf[s] = *reinterpret_cast<const bf16x8*>(zr + 16 * s);
     }
-    // the wave's VT visual tiles (channels 32 (wave + 4k) ..), kept for the logits
+    // the wave's VT visual tiles (channels 32 (wave + 4k) ..), kept for the logits; the next
+    // tile's weight rows and biases are loaded while this tile's MFMAs run (one wave per SIMD:
+    // nothing else hides the L2 latency)
     float v[VT][16];
+    bf16x8 wf[2][KH / 16];
+    float4 bq[2][4];
+    auto load_tile = [&](int k, int slot) {
+        const int ct = wave + 4 * k;
+        const bf16* wr = a.wv + ((size_t)ct * 32 + r) * KH + 8 * h;
+#pragma unroll
+        for (int s = 0; s < KH / 16; ++s) wf[slot][s] = *reinterpret_cast<const bf16x8*>(wr + 16 * s);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) bq[slot][g] = *reinterpret_cast<const float4*>(a.bv + 32 * ct + 8 * g + 4 * h);
+    };
+    load_tile(0, 0);
 #pragma unroll
     for (int k = 0; k < VT; ++k) {
         const int ct = wave + 4 * k;
-        const f32x16 acc = tile_gemm(a.wv + (size_t)ct * 32 * KH, 32, zf, r, h);
+        if (k + 1 < VT) load_tile(k + 1, (k + 1) & 1);
+        f32x16 acc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+        for (int s = 0; s < KH / 16; ++s) acc = mfma(wf[k & 1][s], zf[s], acc);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int ch = 32 * ct + 8 * g + 4 * h;
-            const float4 b4 = *reinterpret_cast<const float4*>(a.bv + ch);
+            const float4 b4 = bq[k & 1][g];
             v[k][4 * g] = acc[4 * g] + b4.x;
             v[k][4 * g + 1] = acc[4 * g + 1] + b4.y;
             v[k][4 * g + 2] = acc[4 * g + 2] + b4.z;
@@ -287,12 +305,19 @@ __global__ void __launch_bounds__(BT) heads_out_bwd_kernel(HeadsOutBwdArgs a) {
     __syncthreads();
     // visual: g_v + g_logits . text for 16 rows x 4 columns
     if (half < 2) {
-#pragma unroll 4
+        // the 16 rows' gradients are loaded up front (clamped rows past R), then combined
+        float4 gvr[RB / 2];
+#pragma unroll
+        for (int k = 0; k < RB / 2; ++k) {
+            const int rr = min(half * (RB / 2) + k, nrows - 1);
+            gvr[k] = *reinterpret_cast<const float4*>(a.gv + (size_t)(row0 + rr) * NV + 4 * c4);
+        }
+#pragma unroll
         for (int k = 0; k < RB / 2; ++k) {
             const int rr = half * (RB / 2) + k;
             if (rr >= nrows) break;
             const size_t off = (size_t)(row0 + rr) * NV + 4 * c4;
-            float4 g = *reinterpret_cast<const float4*>(a.gv + off);
+            float4 g = gvr[k];
 #pragma unroll
             for (int t4 = 0; t4 < TMAX / 4; ++t4) {
                 const float4 w = *reinterpret_cast<const float4*>(gl + rr * TMAX + 4 * t4);

@@ -505,7 +505,8 @@ __global__ __launch_bounds__(512, 1) void sa_dy8_kernel(DyFusedArgs p) {
     PROBE_END;
     if constexpr (STATS) {
         // the row-block-1 waves hand their partials to the row-block-0 waves of the same channels
-        float* xs = reinterpret_cast<float*>(As);   // (4 channel blocks, 64 lanes, 32) floats
+        // (4 channel blocks, 64 lanes, 32) floats = 32 KB: DsT (36.9 KB) holds it, As (17 KB) does not
+        float* xs = reinterpret_cast<float*>(DsT);
         if (rbz == 1)
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
