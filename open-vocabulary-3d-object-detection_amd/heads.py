@@ -150,9 +150,18 @@ class HeadPack:
         return [p[1] for p in self.parts], [p[4] for p in self.parts]
 
 
+# shapes the output launch is compiled for (csrc/headsout.hip: KH, NV, MAXS, a box head's
+# outputs <= 32); other head shapes (e.g. the reduced smoke model) take the per-head rows path
+OUT_HIDDEN, OUT_VISUAL, OUT_BOX_HEADS, OUT_BOX_MAX = 256, 640, 4, 32
+
+
 def supported(pack, rows):
     if not (pack.ok and rows.is_cuda and torch.is_autocast_enabled("cuda")
             and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        return False
+    outs = [p[6].out_channels for p in pack.parts]
+    if pack.H != OUT_HIDDEN or outs[0] != OUT_VISUAL or len(outs) != 1 + OUT_BOX_HEADS \
+            or not all(0 < n <= OUT_BOX_MAX for n in outs[1:]):
         return False
     drops = set()
     groups = set()
