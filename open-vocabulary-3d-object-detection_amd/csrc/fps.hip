@@ -885,12 +885,43 @@ __global__ __launch_bounds__(kThreads) void fps_stream_kernel(const float* __res
 // as a tag (no fences: a word is valid when its tag matches), written by one lane, polled by
 // one lane per wave.  The winner is (larger distance, then smaller upstream rank), the same
 // rule inside and across the halves, so the indices equal the one-workgroup kernels'.
-// Scene b runs on workgroups b and b + B: with B a multiple of 8, the same XCD (one L2).
+// Scene b runs on workgroups b and b + B: with B a multiple of 8, the same XCD (one L2) under
+// the dispatcher's round robin -- for speed only: the halves first swap their XCC_ID through
+// memory (sc1 granules, correct at any placement).  Same XCD: candidates are stored plain (the
+// line stays in that XCD's L2) and polled with sc1 loads (L2-served, bypassing L1): one L2 round
+// trip per iteration.  Different XCDs: sc1 stores too (the line goes to memory), the guide's
+// tagged-granule hand-off.  A slot is four 8-byte {value, tag} granules (distance, x, y, z; tag =
+// iteration << 16 | point index) moved by two 16-byte accesses; each granule is read untorn and
+// checked against its tag, so no fences are needed.
 // The exchange slots are zeroed by the host before each launch (tag 0 is never used).
 constexpr int kPairSpin = 1 << 26;   // polls before giving up (a hung partner: garbage, not a hang)
 
 __device__ __forceinline__ unsigned long long xword(uint32_t v, uint32_t tag) {
     return ((unsigned long long)tag << 32) | v;
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte sc1 load (bypasses this CU's L1; served by the XCD's L2 when the line is there)
+__device__ __forceinline__ u32x4 load_sc1_x4(const void* p) {
+    u32x4 r;
+    asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(r) : "v"(p) : "memory");
+    return r;
+}
+// two 16-byte sc1 loads, both in flight before the wait
+struct u32x4x2 { u32x4 a, b; };
+__device__ __forceinline__ u32x4x2 load_sc1_x4x2(const void* p) {
+    u32x4x2 r;
+    asm volatile("global_load_dwordx4 %0, %2, off sc1\n\tglobal_load_dwordx4 %1, %2, off offset:16 sc1\n\t"
+                 "s_waitcnt vmcnt(0)" : "=&v"(r.a), "=&v"(r.b) : "v"(p) : "memory");
+    return r;
+}
+// 16-byte store: plain (the line stays in this XCD's L2) or sc1 (written through to memory)
+__device__ __forceinline__ void store_x4(void* p, u32x4 v, bool through) {
+    if (through)
+        asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
+    else
+        asm volatile("global_store_dwordx4 %0, %1, off" :: "v"(p), "v"(v) : "memory");
 }
 
 template <int PPT>
@@ -918,9 +949,27 @@ __global__ __launch_bounds__(kThreads) void fps_pair_kernel(const float* __restr
     const int NH = (N + 1) / 2;
     const int base = half * NH;                 // this half's sorted positions [base, end)
     const int end = half ? N : NH;
-    // exchange words: [b][half][parity][8] (5 used: distance, point index, x, y, z)
+    // exchange words: [b][half][parity][8] (4 granules: distance, x, y, z, each tagged with
+    // (iteration << 16) | point index);
+    // XCC_ID hand-shake words after them: [b][half][16] (one 128-byte line each)
     unsigned long long* const mine = xch + ((size_t)b * 2 + half) * 16;
     const unsigned long long* const other = xch + ((size_t)b * 2 + (half ^ 1)) * 16;
+    unsigned long long* const hs_mine = xch + (size_t)B * 32 + ((size_t)b * 2 + half) * 16;
+    const unsigned long long* const hs_other = xch + (size_t)B * 32 + ((size_t)b * 2 + (half ^ 1)) * 16;
+    __shared__ int s_through;
+    if (tid == 0) {
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        xcc &= 0xfu;
+        const u32x4 hv = {xcc, 1u, 0u, 1u};
+        store_x4(hs_mine, hv, true);
+        int through = 1;   // partner silent (spin limit): the memory path
+        for (int spin = 0; spin < kPairSpin; ++spin) {
+            const u32x4 o = load_sc1_x4(hs_other);
+            if (o[1] == 1u) { through = o[0] != xcc; break; }
+        }
+        s_through = through;
+    }
 
     // ---- (a) scene bbox, (b) Morton counting sort of all N points (as fps_cull_kernel)
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -1043,6 +1092,7 @@ __global__ __launch_bounds__(kThreads) void fps_pair_kernel(const float* __restr
     int wpos = 0;
     float wx = 0.f, wy = 0.f, wz = 0.f;
     bool lost = false;   // the partner never answered (spin limit): stop exchanging
+    const bool through = s_through != 0;   // written by tid 0 before the barriers above
 
     for (int j = 1; j < M; ++j) {
         const int buf = j & 1;
@@ -1119,29 +1169,25 @@ __global__ __launch_bounds__(kThreads) void fps_pair_kernel(const float* __restr
         // ---- swap candidates with the other half through L2: 5 tagged 64-bit words
         //      (distance bits, point index, x, y, z) per (scene, half, iteration parity)
         const uint32_t tag = (uint32_t)j;
+        // granule tags: (iteration << 16) | point index
+        const uint32_t tk = (tag << 16) | (uint32_t)hk;
         if (tid == 0) {
             unsigned long long* const slot = mine + 8 * buf;
-            const uint32_t val[5] = {(uint32_t)dm, (uint32_t)hk, __float_as_uint(hx),
-                                     __float_as_uint(hy), __float_as_uint(hz)};
-#pragma unroll
-            for (int q = 0; q < 5; ++q)
-                __hip_atomic_store(slot + q, xword(val[q], tag), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+            store_x4(slot, (u32x4){(uint32_t)dm, tk, __float_as_uint(hx), tk}, through);
+            store_x4(slot + 2, (u32x4){__float_as_uint(hy), tk, __float_as_uint(hz), tk}, through);
         }
         uint32_t ov[5] = {0u, 0u, 0u, 0u, 0u};
         uint32_t ot = 0u;
         if (lane == 0 && !lost) {
             const unsigned long long* const os = other + 8 * buf;
             for (int spin = 0; spin < kPairSpin; ++spin) {
-                bool all = true;
-#pragma unroll
-                for (int q = 0; q < 5; ++q) {
-                    const unsigned long long x = __hip_atomic_load(os + q, __ATOMIC_RELAXED,
-                                                                   __HIP_MEMORY_SCOPE_AGENT);
-                    ov[q] = (uint32_t)x;
-                    all = all && (uint32_t)(x >> 32) == tag;
+                const u32x4x2 g = load_sc1_x4x2(os);
+                const uint32_t t0 = g.a[1];
+                ov[0] = g.a[0]; ov[1] = t0 & 0xffffu; ov[2] = g.a[2]; ov[3] = g.b[0]; ov[4] = g.b[2];
+                if ((t0 >> 16) == tag && g.a[3] == t0 && g.b[1] == t0 && g.b[3] == t0) {
+                    ot = tag;
+                    break;
                 }
-                if (all) { ot = tag; break; }
             }
         }
         // lane 0's words to the whole wave (scalar registers)
@@ -1226,7 +1272,7 @@ extern "C" int ov3d_fps(const float* xyz, int B, int N, int M, int32_t* idx_out,
     } else if (N <= 2 * kThreads * kMaxPPT && M <= kMaxOutLDS && fps_pair_enabled()) {
         // two workgroups per scene, candidates swapped through L2 (fps_pair_kernel)
         if (!workspace) return OV3D_EINVAL;
-        const size_t xbytes = (size_t)B * 2 * 16 * sizeof(unsigned long long);
+        const size_t xbytes = (size_t)B * 2 * 2 * 16 * sizeof(unsigned long long);   // slots + XCC_IDs
         if (hipMemsetAsync(workspace, 0, xbytes, s) != hipSuccess) return OV3D_ELAUNCH;
         unsigned long long* xch = reinterpret_cast<unsigned long long*>(workspace);
         const int half = (N + 1) / 2, ppt2 = (half + kThreads - 1) / kThreads;
