@@ -209,6 +209,9 @@ int ov3d_sa_dy_fused(const void* yprev, const float* scale, const float* shift, 
 /* (nparts, width) fp64 -> (width) sums */
 int ov3d_reduce_partials(const double* partials, int nparts, int width, double* totals,
                          void* stream);
+/* the same sums rounded once to fp32 (the fused SA's first-layer weight gradient) */
+int ov3d_reduce_partials_f32(const double* partials, int nparts, int width, float* totals,
+                             void* stream);
 /* training BN: totals (2,C) over `count` rows -> mean, invstd, scale = gamma*invstd,
  * shift = beta - mean*scale; running stats updated (momentum, unbiased var) if non-NULL;
  * num_batches_tracked (int64) += 1 if non-NULL (nn.BatchNorm1d's counter) */
@@ -565,9 +568,14 @@ int ov3d_resnorm_fwd(long long R, int C, const void* src, int src_bf16, const vo
                      float dropout_p, const int64_t* seed, int site, const float* ga,
                      const float* ba, const void* pos, int pos_bf16, const float* gb,
                      const float* bb, float eps, float* s, float* mean, float* rstd, void* xa,
-                     void* xap, float* xb, void* stream);
-/* backward: ds (fp32, grad of s from its other consumers) or NULL, dxa / dxap (bf16),
- * dxb (fp32) or NULL -> dsrc (fp32), dy (bf16 | fp32), dpos (= dxap), dga/dba/dgb/dbb.
+                     void* xap, void* xb, int xb_bf16, long long xb_inner, long long xb_s0,
+                     long long xb_s1, void* stream);
+/* xb (fp32, or bf16 when xb_bf16) rows; xb_inner > 0: row r written at
+ * (r / xb_inner) * xb_s0 + (r % xb_inner) * xb_s1 (the decoder writes its layer outputs
+ * straight into the heads' (layer, scene, query) rows).
+ * backward: ds (fp32, grad of s from its other consumers) or NULL, dxa / dxap (bf16),
+ * dxb (fp32, or bf16 when dxb_bf16) or NULL -> dsrc (fp32), dy (bf16 | fp32), dpos (= dxap),
+ * dga/dba/dgb/dbb.
  * dxb_inner > 0: dxb row r lives at (r / dxb_inner) * dxb_s0 + (r % dxb_inner) * dxb_s1
  * (a strided (L, B, C) view, e.g. one layer of the stacked decoder outputs' gradient);
  * dxb_inner = 0: contiguous rows.
@@ -601,8 +609,8 @@ int ov3d_relu_dropout_fwd(const void* y, long long R, int C, float dropout_p, co
 int ov3d_relu_dropout_bwd(const void* h, const void* dh, long long n, float dropout_p, void* dy,
                           void* stream);
 int ov3d_resnorm_bwd(long long R, int C, const float* s, const float* mean, const float* rstd,
-                     const float* ds, const void* dxa, const void* dxap, const float* dxb,
-                     long long dxb_inner, long long dxb_s0, long long dxb_s1,
+                     const float* ds, const void* dxa, const void* dxap, const void* dxb,
+                     int dxb_bf16, long long dxb_inner, long long dxb_s0, long long dxb_s1,
                      const float* ga, const float* gb, float dropout_p, const int64_t* seed,
                      int site, float* dsrc, void* dy, int dy_bf16, void* dpos, int dpos_bf16,
                      float* partials, int nparts, float* dga, float* dba, float* dgb, float* dbb,
@@ -626,6 +634,9 @@ typedef struct {
     int reserved;
 } ov3d_adamw_tensor;
 int ov3d_adamw_chunk(void);
+/* the dropout seed of a training forward (attention.py next_step): *live += 1, *snap = *live
+ * (int64 device scalars), one launch */
+int ov3d_seed_next(long long* live, long long* snap, void* stream);
 /* n device-to-device copies (bytes[i] from srcs[i] to dsts[i], host arrays) in one launch
  * per 120 (the step graph's static input batch, the flat gradient buffer) */
 int ov3d_multi_copy(int n, const void* const* srcs, void* const* dsts, const long long* bytes,
@@ -649,9 +660,10 @@ int ov3d_adamw_step(const ov3d_adamw_tensor* table, const int* blk_t, const int*
  * objectness (1).  Backward: any gradient may be NULL; writes draw (R, ldd) columns 0..6+2NB. */
 /* Fourier position embedding (position_embedding.py:89-118): xyz (B, N, 3), optional scene
  * range dmin / dmax (B, 3) (both or neither), gauss_B (3, ldb) first d columns ->
- * out (B, N, 2d) = [sin | cos] of (normalised xyz * 2 pi) @ gauss_B */
+ * out (B, N, 2d) = [sin | cos] of (normalised xyz * 2 pi) @ gauss_B; seq_first != 0: out
+ * (N, B, 2d), the transformer's sequence-first rows */
 int ov3d_fourier_pe(const float* xyz, int B, int N, const float* dmin, const float* dmax,
-                    const float* gauss_b, int ldb, int d, float* out, void* stream);
+                    const float* gauss_b, int ldb, int d, int seq_first, float* out, void* stream);
 int ov3d_box_param_fwd(long long R, int B, int Q, int NB, int T, const float* raw, long long ld,
                        const float* qxyz, const float* dmin, const float* dmax,
                        const float* logits, float* center_n, float* center_u, float* size_n,

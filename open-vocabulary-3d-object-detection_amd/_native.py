@@ -38,6 +38,7 @@ _SIGS = {
     "ov3d_sa_layer_pool_fwd": "ppppiiiippppppip",
     "ov3d_sa_layer_dy": "ppppiiiippppppip",
     "ov3d_reduce_partials": "piipp",
+    "ov3d_reduce_partials_f32": "piipp",
     "ov3d_colsum_f32": "piipp",
     "ov3d_bn_finalize": "pdippffpppppppp",
     "ov3d_sa_pool_fwd": "ppppppiiipppp",
@@ -73,13 +74,14 @@ _SIGS = {
     "ov3d_adamw_step": "pppipfpddfpifpp",
     "ov3d_adamw_set_grads": "pipp",
     "ov3d_multi_copy": "ipppp",
-    "ov3d_fourier_pe": "piipppiipp",
+    "ov3d_seed_next": "ppp",
+    "ov3d_fourier_pe": "piipppiiipp",
     "ov3d_box_param_fwd": "liiiiplpppppppppppppppp",
     "ov3d_box_param_bwd": "liiiplppppppppppppplp",
     "ov3d_relu_dropout_fwd": "plifpipp",
     "ov3d_relu_dropout_bwd": "pplfpp",
-    "ov3d_resnorm_fwd": "lipipifpipppippfppppppp",
-    "ov3d_resnorm_bwd": "lippppppplllppfpippipipippppip",
+    "ov3d_resnorm_fwd": "lipipifpipppippfppppppilllp",
+    "ov3d_resnorm_bwd": "lipppppppilllppfpippipipippppip",
     "ov3d_rows_gemm": "iiiplplipplp",
     "ov3d_bn_stats_finalize": "piidppffpppppppp",
     "ov3d_colsum_group": "pipiip",

@@ -115,8 +115,9 @@ def next_step(device):
     """Advance the dropout seed of `device` and snapshot it for this forward (two tiny
     kernels, captured by a hipGraph like any other; call once per training forward)."""
     live = _live(device)
-    live.add_(1)
-    _SNAPS[device] = live.clone()
+    snap = torch.empty_like(live)
+    _native.call("ov3d_seed_next", live, snap, like=live)
+    _SNAPS[device] = snap
 
 
 class PackedMask:

@@ -193,6 +193,22 @@ __global__ void __launch_bounds__(256) multi_copy_kernel(CopyList c) {
 }
 }  // namespace
 
+// the attention / dropout seed of a training forward: live += 1, snapshot = live (one thread)
+namespace {
+__global__ void seed_next_kernel(long long* live, long long* snap) {
+    const long long v = *live + 1;
+    *live = v;
+    *snap = v;
+}
+}  // namespace
+
+extern "C" int ov3d_seed_next(long long* live, long long* snap, void* stream) {
+    if (!live || !snap) return OV3D_EINVAL;
+    seed_next_kernel<<<1, 1, 0, ov3d_stream(stream)>>>(live, snap);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
 extern "C" int ov3d_multi_copy(int n, const void* const* srcs, void* const* dsts,
                                const long long* bytes, void* stream) {
     if (n < 0 || (n > 0 && (!srcs || !dsts || !bytes))) return OV3D_EINVAL;

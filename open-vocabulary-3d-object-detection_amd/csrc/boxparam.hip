@@ -255,18 +255,21 @@ extern "C" int ov3d_box_param_bwd(long long R, int B, int Q, int NB, const float
 
 // ---- Fourier position embedding (models/position_embedding.py:89-118) ----
 // x = xyz (normalised to [0, 1] by the scene range when dmin != NULL) * 2 pi;
-// p = x @ gauss_B (3 x d); out = [sin p | cos p]   (B, N, 2d) fp32, one thread per (point, j)
+// p = x @ gauss_B (3 x d); out = [sin p | cos p]   (B, N, 2d) fp32, one thread per (point, j);
+// seq_first: rows in (N, B) order instead (the transformer's sequence-first layout)
 namespace {
 __global__ void __launch_bounds__(256) fourier_pe_kernel(const float* __restrict__ xyz, long long BN,
-                                                        int N, const float* __restrict__ dmin,
+                                                        int B, int N, const float* __restrict__ dmin,
                                                         const float* __restrict__ dmax,
                                                         const float* __restrict__ gb, int ldb,
-                                                        int d, float two_pi, float* __restrict__ out) {
+                                                        int d, float two_pi, int seq_first,
+                                                        float* __restrict__ out) {
     const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= BN * d) return;
     const long long pt = t / d;
     const int j = (int)(t - pt * d);
     const int b = (int)(pt / N);
+    const long long orow = seq_first ? (pt - (long long)b * N) * B + b : pt;
     float x[3];
     for (int i = 0; i < 3; ++i) {
         float v = xyz[pt * 3 + i];
@@ -274,19 +277,20 @@ __global__ void __launch_bounds__(256) fourier_pe_kernel(const float* __restrict
         x[i] = v * two_pi;
     }
     const float p = fmaf(x[2], gb[2 * ldb + j], fmaf(x[1], gb[ldb + j], x[0] * gb[j]));
-    out[pt * 2 * d + j] = sinf(p);
-    out[pt * 2 * d + d + j] = cosf(p);
+    out[orow * 2 * d + j] = sinf(p);
+    out[orow * 2 * d + d + j] = cosf(p);
 }
 }  // namespace
 
 extern "C" int ov3d_fourier_pe(const float* xyz, int B, int N, const float* dmin, const float* dmax,
-                               const float* gauss_b, int ldb, int d, float* out, void* stream) {
+                               const float* gauss_b, int ldb, int d, int seq_first, float* out,
+                               void* stream) {
     if (!xyz || !gauss_b || !out || B <= 0 || N <= 0 || d <= 0 || ldb < d || (!dmin != !dmax))
         return OV3D_EINVAL;
     const long long n = (long long)B * N * d;
     fourier_pe_kernel<<<ov3d_cdiv(n, 256), 256, 0, ov3d_stream(stream)>>>(
-        xyz, (long long)B * N, N, dmin, dmax, gauss_b, ldb, d, (float)(2.0 * 3.14159265358979323846),
-        out);
+        xyz, (long long)B * N, B, N, dmin, dmax, gauss_b, ldb, d, (float)(2.0 * 3.14159265358979323846),
+        seq_first, out);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

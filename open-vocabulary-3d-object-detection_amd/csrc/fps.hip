@@ -916,12 +916,14 @@ __device__ __forceinline__ u32x4x2 load_sc1_x4x2(const void* p) {
                  "s_waitcnt vmcnt(0)" : "=&v"(r.a), "=&v"(r.b) : "v"(p) : "memory");
     return r;
 }
-// 16-byte store: plain (the line stays in this XCD's L2) or sc1 (written through to memory)
+// 16-byte store: plain (the line stays in this XCD's L2) or sc1 (written through to memory).
+// s_nop 1: a VALU write of the data VGPRs right after a VMEM store of more than 8 bytes needs
+// a wait state, and the compiler's hazard pass does not look inside inline asm
 __device__ __forceinline__ void store_x4(void* p, u32x4 v, bool through) {
     if (through)
-        asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
     else
-        asm volatile("global_store_dwordx4 %0, %1, off" :: "v"(p), "v"(v) : "memory");
+        asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
 }
 
 template <int PPT>
@@ -929,11 +931,12 @@ __global__ __launch_bounds__(kThreads) void fps_pair_kernel(const float* __restr
                                                             int N, int M, int L,
                                                             unsigned long long* __restrict__ xch,
                                                             int32_t* __restrict__ idx,
-                                                            float* __restrict__ new_xyz) {
+                                                            float* __restrict__ new_xyz,
+                                                            int force_mem) {
     constexpr int PW = PPT * 64;
     constexpr int NSORT = 2 * PPT;   // setup slots per thread (the whole scene)
     __shared__ uint32_t s_hist[kCells];
-    __shared__ uint16_t s_perm[kThreads * NSORT];
+    __shared__ __attribute__((aligned(16))) uint16_t s_perm[kThreads * NSORT];
     __shared__ uint16_t s_out[kMaxOutLDS];     // winning point index per iteration
     __shared__ float s_red[6][kWaves];
     __shared__ uint32_t s_scan[kWaves];
@@ -966,81 +969,113 @@ __global__ __launch_bounds__(kThreads) void fps_pair_kernel(const float* __restr
         int through = 1;   // partner silent (spin limit): the memory path
         for (int spin = 0; spin < kPairSpin; ++spin) {
             const u32x4 o = load_sc1_x4(hs_other);
-            if (o[1] == 1u) { through = o[0] != xcc; break; }
+            if (o[1] == 1u) { through = o[0] != xcc || force_mem; break; }
         }
         s_through = through;
+        // the decision, for diagnostics (tools/fps_pair_stress.py reads it after the launch)
+        store_x4(hs_mine + 2, (u32x4){(uint32_t)through, 2u, 0u, 2u}, true);
     }
 
-    // ---- (a) scene bbox, (b) Morton counting sort of all N points (as fps_cull_kernel)
-    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int k = tid; k < N; k += kThreads)
+    // ---- the scene's Morton order.  Both halves must own complementary point sets, and the
+    //      counting sort's order inside a cell follows the LDS atomics' order, which differs
+    //      between two workgroups (a point of the boundary cell could land in both halves or in
+    //      neither): half 0 sorts and publishes the order (sc1 16-byte stores, drained, then a
+    //      flag), half 1 polls the flag and reads it (sc1 loads).  Half 1 sorts by itself only
+    //      if half 0 never answers (spin limit).
+    const int NP = (N + 7) & ~7;
+    uint16_t* const perm_g = reinterpret_cast<uint16_t*>(xch + (size_t)B * 64) + (size_t)b * NP;
+    unsigned long long* const pflag = xch + (size_t)B * 32 + (size_t)b * 2 * 16 + 6;   // half 0's line
+    __shared__ int s_have;
+    if (tid == 0) {
+        int have = 0;
+        if (half)
+            for (int spin = 0; spin < kPairSpin; ++spin)
+                if (load_sc1_x4(pflag)[0] == 1u) { have = 1; break; }
+        s_have = have;
+    }
+    __syncthreads();
+    if (s_have) {
+        for (int c = tid; c < NP / 8; c += kThreads)
+            *reinterpret_cast<u32x4*>(&s_perm[8 * c]) = load_sc1_x4(perm_g + 8 * c);
+    } else {
+        // ---- (a) scene bbox, (b) Morton counting sort of all N points (as fps_cull_kernel)
+        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int k = tid; k < N; k += kThreads)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const float v = p[3 * k + a];
+                lo[a] = fminf(lo[a], v);
+                hi[a] = fmaxf(hi[a], v);
+            }
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            const float v = p[3 * k + a];
-            lo[a] = fminf(lo[a], v);
-            hi[a] = fmaxf(hi[a], v);
+            lo[a] = wave_fmin(lo[a]);
+            hi[a] = wave_fmax(hi[a]);
         }
+        if (lane == 0)
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        lo[a] = wave_fmin(lo[a]);
-        hi[a] = wave_fmax(hi[a]);
-    }
-    if (lane == 0)
-#pragma unroll
-        for (int a = 0; a < 3; ++a) { s_red[a][w] = lo[a]; s_red[3 + a][w] = hi[a]; }
-    for (int i = tid; i < kCells; i += kThreads) s_hist[i] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        float l = s_red[a][0], h = s_red[3 + a][0];
-        for (int q = 1; q < kWaves; ++q) { l = fminf(l, s_red[a][q]); h = fmaxf(h, s_red[3 + a][q]); }
-        lo[a] = l;
-        hi[a] = 16.f / fmaxf(h - l, 1e-6f);
-    }
-    {
-        uint32_t cp[NSORT];
-#pragma unroll
-        for (int i = 0; i < NSORT; ++i) {
-            const int k = tid + i * kThreads;
-            cp[i] = 0xffffffffu;
-            if (k < N) {
-                uint32_t q[3];
-#pragma unroll
-                for (int a = 0; a < 3; ++a) {
-                    const int c = (int)((p[3 * k + a] - lo[a]) * hi[a]);
-                    q[a] = (uint32_t)min(max(c, 0), 15);
-                }
-                const uint32_t code = spread3(q[0]) | (spread3(q[1]) << 1) | (spread3(q[2]) << 2);
-                const uint32_t old = atomicAdd(&s_hist[code], 1u);
-                cp[i] = (code << 16) | old;
-            }
-        }
+            for (int a = 0; a < 3; ++a) { s_red[a][w] = lo[a]; s_red[3 + a][w] = hi[a]; }
+        for (int i = tid; i < kCells; i += kThreads) s_hist[i] = 0;
         __syncthreads();
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            float l = s_red[a][0], h = s_red[3 + a][0];
+            for (int q = 1; q < kWaves; ++q) { l = fminf(l, s_red[a][q]); h = fmaxf(h, s_red[3 + a][q]); }
+            lo[a] = l;
+            hi[a] = 16.f / fmaxf(h - l, 1e-6f);
+        }
         {
-            uint32_t v[4], sum = 0;
+            uint32_t cp[NSORT];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) { v[q] = s_hist[4 * tid + q]; sum += v[q]; }
-            uint32_t inc = sum;
+            for (int i = 0; i < NSORT; ++i) {
+                const int k = tid + i * kThreads;
+                cp[i] = 0xffffffffu;
+                if (k < N) {
+                    uint32_t q[3];
 #pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const uint32_t o = __shfl_up(inc, off);
-                if (lane >= off) inc += o;
+                    for (int a = 0; a < 3; ++a) {
+                        const int c = (int)((p[3 * k + a] - lo[a]) * hi[a]);
+                        q[a] = (uint32_t)min(max(c, 0), 15);
+                    }
+                    const uint32_t code = spread3(q[0]) | (spread3(q[1]) << 1) | (spread3(q[2]) << 2);
+                    const uint32_t old = atomicAdd(&s_hist[code], 1u);
+                    cp[i] = (code << 16) | old;
+                }
             }
-            if (lane == 63) s_scan[w] = inc;
             __syncthreads();
-            uint32_t basew = 0;
-            for (int q = 0; q < w; ++q) basew += s_scan[q];
-            uint32_t run = basew + inc - sum;
+            {
+                uint32_t v[4], sum = 0;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) { s_hist[4 * tid + q] = run; run += v[q]; }
+                for (int q = 0; q < 4; ++q) { v[q] = s_hist[4 * tid + q]; sum += v[q]; }
+                uint32_t inc = sum;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const uint32_t o = __shfl_up(inc, off);
+                    if (lane >= off) inc += o;
+                }
+                if (lane == 63) s_scan[w] = inc;
+                __syncthreads();
+                uint32_t basew = 0;
+                for (int q = 0; q < w; ++q) basew += s_scan[q];
+                uint32_t run = basew + inc - sum;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) { s_hist[4 * tid + q] = run; run += v[q]; }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < NSORT; ++i)
+                if (cp[i] != 0xffffffffu)
+                    s_perm[s_hist[cp[i] >> 16] + (cp[i] & 0xffffu)] = (uint16_t)(tid + i * kThreads);
         }
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < NSORT; ++i)
-            if (cp[i] != 0xffffffffu)
-                s_perm[s_hist[cp[i] >> 16] + (cp[i] & 0xffffu)] = (uint16_t)(tid + i * kThreads);
     }
     __syncthreads();
+    if (half == 0) {
+        for (int c = tid; c < NP / 8; c += kThreads)
+            store_x4(perm_g + 8 * c, *reinterpret_cast<const u32x4*>(&s_perm[8 * c]), true);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) store_x4(pflag, (u32x4){1u, 1u, 1u, 1u}, true);
+    }
 
     // ---- (c) this thread's slots: positions base + w*PW + i*64 + lane (< end), by rank
     uint32_t rk[PPT];
@@ -1214,6 +1249,7 @@ __global__ __launch_bounds__(kThreads) void fps_pair_kernel(const float* __restr
         if (tid == 0) s_out[j] = (uint16_t)pk;
     }
     __syncthreads();
+    if (tid == 0) store_x4(hs_mine + 4, (u32x4){(uint32_t)lost, 3u, 0u, 3u}, true);   // diagnostics
     if (half) return;
     idx += (size_t)b * M;
     if (new_xyz) new_xyz += (size_t)b * M * 3;
@@ -1275,16 +1311,21 @@ extern "C" int ov3d_fps(const float* xyz, int B, int N, int M, int32_t* idx_out,
         const size_t xbytes = (size_t)B * 2 * 2 * 16 * sizeof(unsigned long long);   // slots + XCC_IDs
         if (hipMemsetAsync(workspace, 0, xbytes, s) != hipSuccess) return OV3D_ELAUNCH;
         unsigned long long* xch = reinterpret_cast<unsigned long long*>(workspace);
+        // OV3D_FPS_XCH=mem: candidates through memory even for halves on one XCD (diagnostic)
+        static const int force_mem = [] {
+            const char* e = getenv("OV3D_FPS_XCH");
+            return e && e[0] == 'm' ? 1 : 0;
+        }();
         const int half = (N + 1) / 2, ppt2 = (half + kThreads - 1) / kThreads;
         if (ppt2 <= 12)
             hipLaunchKernelGGL(fps_pair_kernel<12>, dim3(2 * B), dim3(kThreads), 0, s, xyz, B, N, M, L,
-                               xch, idx_out, new_xyz_out);
+                               xch, idx_out, new_xyz_out, force_mem);
         else if (ppt2 <= 16)
             hipLaunchKernelGGL(fps_pair_kernel<16>, dim3(2 * B), dim3(kThreads), 0, s, xyz, B, N, M, L,
-                               xch, idx_out, new_xyz_out);
+                               xch, idx_out, new_xyz_out, force_mem);
         else
             hipLaunchKernelGGL(fps_pair_kernel<20>, dim3(2 * B), dim3(kThreads), 0, s, xyz, B, N, M, L,
-                               xch, idx_out, new_xyz_out);
+                               xch, idx_out, new_xyz_out, force_mem);
     } else if (N <= kThreads * (kPR + kPS) && M <= kMaxOutLDS) {
         if (!workspace) return OV3D_EINVAL;
         // chunk size of the workspace cluster's culling (OV3D_FPS_CHUNK: measurement knob)

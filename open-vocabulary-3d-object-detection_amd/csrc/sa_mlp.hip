@@ -377,14 +377,16 @@ __device__ __forceinline__ void column_totals2(const double* __restrict__ partia
     }
 }
 
+// OutT float: the totals rounded once (a weight gradient consumed in fp32, no cast launch)
+template <typename OutT>
 __global__ __launch_bounds__(1024) void reduce_partials_kernel(const double* __restrict__ partials,
                                                                int nparts, int width,
-                                                               double* __restrict__ totals) {
+                                                               OutT* __restrict__ totals) {
     __shared__ double red[kColPL][2][kColW + 1];
     const int c = blockIdx.x * kColW + (threadIdx.x % kColW), pl = threadIdx.x / kColW;
     double t, unused;
     column_totals2(partials, nparts, width, c, -1, pl, red, t, unused);
-    if (pl == 0 && c < width) totals[c] = t;
+    if (pl == 0 && c < width) totals[c] = (OutT)t;
 }
 
 // f32 column sums of (nparts, width) partials (the SA backward's per-workgroup dW partials):
@@ -835,7 +837,16 @@ extern "C" int ov3d_sa_layer_dy(const void* yprev, const float* scale, const flo
 extern "C" int ov3d_reduce_partials(const double* partials, int nparts, int width, double* totals,
                                     void* stream) {
     if (nparts <= 0 || width <= 0 || !partials || !totals) return OV3D_EINVAL;
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3(ov3d_cdiv(width, kColW)), dim3(1024), 0,
+    hipLaunchKernelGGL(reduce_partials_kernel<double>, dim3(ov3d_cdiv(width, kColW)), dim3(1024), 0,
+                       ov3d_stream(stream), partials, nparts, width, totals);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_reduce_partials_f32(const double* partials, int nparts, int width, float* totals,
+                                        void* stream) {
+    if (nparts <= 0 || width <= 0 || !partials || !totals) return OV3D_EINVAL;
+    hipLaunchKernelGGL(reduce_partials_kernel<float>, dim3(ov3d_cdiv(width, kColW)), dim3(1024), 0,
                        ov3d_stream(stream), partials, nparts, width, totals);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;

@@ -7,6 +7,7 @@ unchanged (reference models/helpers.py:45-112).
 """
 import copy
 
+import torch
 import torch.nn as nn
 
 from .gemm import rows_linear
@@ -76,10 +77,28 @@ class GenericMLP(nn.Module):
         under bf16 autocast: BatchNorm + ReLU (+ Dropout) run as one HIP row pass each way
         (heads.bn_relu_rows)."""
         from . import heads
+        from . import resnorm as rn
         mods = list(self.layers)
         i = 0
         while i < len(mods):
             m = mods[i]
+            if isinstance(m, nn.Conv1d) and i + 2 < len(mods) and isinstance(mods[i + 1], nn.ReLU) \
+                    and isinstance(mods[i + 2], nn.Conv1d) and x.is_cuda:
+                # conv + ReLU + conv (the query projection): the ReLU is the first GEMM's
+                # epilogue forward and the second GEMM's input-gradient epilogue backward
+                m2 = mods[i + 2]
+                w1 = m.weight.view(m.weight.shape[0], m.weight.shape[1])
+                w2 = m2.weight.view(m2.weight.shape[0], m2.weight.shape[1])
+                xb = x.to(torch.bfloat16) if torch.is_autocast_enabled("cuda") else x
+                if rn.ffn_weights_ok(xb, w1, w2):
+                    x = rn.ffn_weights(xb, w1, m.bias, w2, m2.bias)
+                    i += 3
+                    continue
+            if isinstance(m, nn.ReLU) and x.is_cuda and x.dtype == torch.bfloat16 and \
+                    x.shape[-1] % 8 == 0:
+                x = rn.relu_rows(x)
+                i += 1
+                continue
             if isinstance(m, nn.Conv1d):
                 x = rows_linear(x, m.weight.view(m.weight.shape[0], m.weight.shape[1]), m.bias)
             elif isinstance(m, nn.GroupNorm):

@@ -156,12 +156,14 @@ class Model3DETR(nn.Module):
         query_xyz, rows = self._query_rows(encoder_xyz, point_cloud_dims)
         return query_xyz, rows.permute(0, 2, 1)
 
-    def _query_rows(self, encoder_xyz, point_cloud_dims, query_xyz=None):
+    def _query_rows(self, encoder_xyz, point_cloud_dims, query_xyz=None, seq_first=False):
+        """-> query_xyz (B, Q, 3), query embedding (B, Q, C) or, seq_first, (Q, B, C) (the
+        projection is per row: the PE launch writes the rows in the decoder's order)"""
         if query_xyz is None:
             _, query_xyz = pu.furthest_point_sample_gather(encoder_xyz, self.num_queries)
-        pe = self.pos_embedding.rows(query_xyz, input_range=point_cloud_dims)      # (B, Q, C)
-        B, Q, C = pe.shape
-        return query_xyz, self.query_projection.rows(pe.reshape(B * Q, C)).view(B, Q, -1)
+        pe = self.pos_embedding.rows(query_xyz, input_range=point_cloud_dims, seq_first=seq_first)
+        n0, n1, C = pe.shape
+        return query_xyz, self.query_projection.rows(pe.reshape(n0 * n1, C)).view(n0, n1, -1)
 
     @staticmethod
     def _break_up_pc(pc):
@@ -258,8 +260,7 @@ class Model3DETR(nn.Module):
                 pre = heads_mod.fused_heads(self._head_pack, rows, sem=self.mlp_heads["sem_cls_head"],
                                             lq=Q if self.cls_logits_layout == "reference" else 0)
         with torch.autocast(device_type=box_features.device.type, enabled=False):
-            return self._box_predictions(query_xyz.float(), point_cloud_dims, rows.float(),
-                                         (L, Q, B), pre)
+            return self._box_predictions(query_xyz.float(), point_cloud_dims, rows, (L, Q, B), pre)
 
     def _box_predictions(self, query_xyz, point_cloud_dims, rows, dims_lqb, pre=None):
         L, Q, B = dims_lqb
@@ -267,6 +268,9 @@ class Model3DETR(nn.Module):
         if pre is not None and "_raw" in pre and pre["_raw"].is_cuda and \
                 pre["_raw"].dtype == torch.float32 and pre["_raw"].stride(1) == 1:
             return self._box_predictions_fused(query_xyz, point_cloud_dims, pre, L, Q, B)
+
+        if rows is not None:
+            rows = rows.float()   # the heads in fp32 (the decoder's bf16 rows under autocast)
 
         def head(name):
             if pre is not None:
@@ -354,13 +358,27 @@ class Model3DETR(nn.Module):
         if encoder_only:
             return enc_xyz, enc_feats.transpose(0, 1)
         dims = [inputs["point_cloud_dims_min"].float(), inputs["point_cloud_dims_max"].float()]
-        query_xyz, query_embed = self._query_rows(enc_xyz, dims, plan.get("query_xyz"))   # (B, Q, C)
-        enc_pos = self.pos_embedding.rows(enc_xyz, input_range=dims).transpose(0, 1)
-        # (Q, B, C) rows, made contiguous once: every decoder layer reads it twice
-        query_embed = query_embed.transpose(0, 1).contiguous()
-        tgt = torch.zeros_like(query_embed)
+        # (Q, B, C) and (N', B, C) rows, sequence-first as the decoder reads them
+        query_xyz, query_embed = self._query_rows(enc_xyz, dims, plan.get("query_xyz"),
+                                                  seq_first=True)
+        enc_pos = self.pos_embedding.rows(enc_xyz, input_range=dims, seq_first=True)
+        tgt = _zeros_like_cached(query_embed)
         box_features = self.decoder(tgt, enc_feats, query_pos=query_embed, pos=enc_pos)[0]
         return self.get_box_predictions(query_xyz, dims, box_features)
+
+
+_ZERO_TGT = {}
+
+
+def _zeros_like_cached(t):
+    """the decoder's initial target (zeros, read-only): allocated once per shape instead of
+    zero-filled in every step"""
+    key = (tuple(t.shape), t.dtype, t.device)
+    z = _ZERO_TGT.get(key)
+    if z is None:
+        z = torch.zeros_like(t)
+        _ZERO_TGT[key] = z
+    return z
 
 
 # ---------------------------------------------------------------- builders

@@ -28,7 +28,7 @@ class PositionEmbeddingCoordsSine(nn.Module):
             self.register_buffer("gauss_B", torch.empty((d_in, d_pos // 2)).normal_() * gauss_scale)
             self.d_pos = d_pos
 
-    def _fourier(self, xyz, num_channels, input_range):
+    def _fourier(self, xyz, num_channels, input_range, seq_first=False):
         d_in, max_d_out = self.gauss_B.shape
         if num_channels is None:
             num_channels = 2 * max_d_out
@@ -42,16 +42,18 @@ class PositionEmbeddingCoordsSine(nn.Module):
             x = xyz.float().contiguous()
             rng = [t.float().contiguous() for t in input_range] if self.normalize else [None, None]
             gb = self.gauss_B.float().contiguous()
-            out = torch.empty((B, N, 2 * d_out), dtype=torch.float32, device=xyz.device)
-            _native.call("ov3d_fourier_pe", x, B, N, rng[0], rng[1], gb, gb.shape[1], d_out, out,
-                         like=x)
+            shape = (N, B, 2 * d_out) if seq_first else (B, N, 2 * d_out)
+            out = torch.empty(shape, dtype=torch.float32, device=xyz.device)
+            _native.call("ov3d_fourier_pe", x, B, N, rng[0], rng[1], gb, gb.shape[1], d_out,
+                         int(seq_first), out, like=x)
             return out
         x = xyz.float()
         if self.normalize:
             x = shift_scale_points(x, src_range=input_range)
         x = x * (2 * math.pi)
         proj = torch.mm(x.reshape(-1, d_in), self.gauss_B[:, :d_out].float()).view(B, N, d_out)
-        return torch.cat([proj.sin(), proj.cos()], dim=2)   # (B, N, d_pos) channels-last
+        out = torch.cat([proj.sin(), proj.cos()], dim=2)   # (B, N, d_pos) channels-last
+        return out.transpose(0, 1).contiguous() if seq_first else out
 
     def _sine(self, xyz, num_channels, input_range):
         x = xyz.float()
@@ -78,14 +80,16 @@ class PositionEmbeddingCoordsSine(nn.Module):
             prev = cdim
         return torch.cat(outs, dim=2)   # (B, N, d_pos) channels-last
 
-    def rows(self, xyz, num_channels=None, input_range=None):
-        """(B, N, 3) -> (B, N, d_pos) channels-last embedding."""
+    def rows(self, xyz, num_channels=None, input_range=None, seq_first=False):
+        """(B, N, 3) -> (B, N, d_pos) channels-last embedding; seq_first: (N, B, d_pos)
+        contiguous (the transformer's row order, written so by the HIP launch)."""
         if xyz.ndim != 3:
             raise ValueError("xyz must be (B, N, 3)")
         with torch.no_grad(), torch.autocast(device_type=xyz.device.type, enabled=False):
             if self.pos_type == "fourier":
-                return self._fourier(xyz, num_channels, input_range)
-            return self._sine(xyz, num_channels, input_range)
+                return self._fourier(xyz, num_channels, input_range, seq_first)
+            out = self._sine(xyz, num_channels, input_range)
+            return out.transpose(0, 1).contiguous() if seq_first else out
 
     def forward(self, xyz, num_channels=None, input_range=None):
         """Reference layout: (B, d_pos, N)."""

@@ -33,6 +33,7 @@ MI355X path (``region_features``), output-identical up to float rounding:
     0.08 GFLOP per ROI.
 """
 import math
+import os
 from collections import OrderedDict
 
 import torch
@@ -269,9 +270,24 @@ def _conv1x1(x, w, b, relu, residual=None):
 IM2COL_CHUNK_BYTES = 96 << 20
 
 
+# im2col of chunk i + 1 on a side stream while the GEMM of chunk i runs (two column buffers):
+# the byte-moving im2col hides behind the matrix-core GEMM (OV3D_CONV_OVERLAP=0: in series)
+CONV_OVERLAP = os.environ.get("OV3D_CONV_OVERLAP", "1") != "0"
+_SIDE = {}
+
+
+def _side_stream(device):
+    s = _SIDE.get(device)
+    if s is None:
+        s = torch.cuda.Stream(device=device)
+        _SIDE[device] = s
+    return s
+
+
 def _conv3x3(x, w, b, stride=1):
     """3x3 conv (pad 1) + bias + ReLU on NHWC: HIP im2col of a chunk of images / ROIs,
-    then one hipBLASLt GEMM with the ReLU epilogue writing the chunk's output rows."""
+    then one hipBLASLt GEMM with the ReLU epilogue writing the chunk's output rows; with
+    several chunks the next chunk's im2col runs on a side stream beside this chunk's GEMM."""
     N, H, W, C = x.shape
     cout, kpad = w.shape
     Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
@@ -279,14 +295,33 @@ def _conv3x3(x, w, b, stride=1):
     out = torch.empty((N, Ho, Wo, cout), dtype=x.dtype, device=x.device)
     per_img = Ho * Wo * kpad * x.element_size()
     step = max(1, IM2COL_CHUNK_BYTES // per_img)
-    cols = torch.empty((min(step, N) * Ho * Wo, kpad), dtype=x.dtype, device=x.device)
+    starts = list(range(0, N, step))
+    overlap = CONV_OVERLAP and len(starts) > 1
+    cols = [torch.empty((min(step, N) * Ho * Wo, kpad), dtype=x.dtype, device=x.device)
+            for _ in range(2 if overlap else 1)]
     wt = w.t()
-    for n0 in range(0, N, step):
+    main = torch.cuda.current_stream(x.device) if overlap else None
+    side = _side_stream(x.device) if overlap else None
+    freed = [None, None]    # event: the GEMM that last read column buffer j has been issued
+    for ci, n0 in enumerate(starts):
         n = min(step, N - n0)
-        c = cols[: n * Ho * Wo]
-        _native.call("ov3d_im2col3x3", x[n0:n0 + n], x.element_size(), n, H, W, C, stride, kpad, c,
-                     like=x)
+        c = cols[ci % len(cols)][: n * Ho * Wo]
+        if overlap:
+            j = ci % 2
+            with torch.cuda.stream(side):
+                side.wait_event(freed[j]) if freed[j] is not None else side.wait_stream(main)
+                _native.call("ov3d_im2col3x3", x[n0:n0 + n], x.element_size(), n, H, W, C, stride,
+                             kpad, c, like=x)
+                ready = torch.cuda.Event()
+                ready.record(side)
+            main.wait_event(ready)
+        else:
+            _native.call("ov3d_im2col3x3", x[n0:n0 + n], x.element_size(), n, H, W, C, stride, kpad, c,
+                         like=x)
         torch.ops.aten._addmm_activation.out(b, c, wt, out=out[n0:n0 + n].view(-1, cout))
+        if overlap:
+            freed[ci % 2] = torch.cuda.Event()
+            freed[ci % 2].record(main)
     return out
 
 

@@ -98,7 +98,7 @@ def _rows(t, C):
 class _ResNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, meta, src, y, pos, ga, ba, gb, bb):
-        p, site, want_a, want_ap, want_b, eps, shape, fans = meta
+        p, site, want_a, want_ap, want_b, eps, shape, fans, xb_into = meta
         C = shape[-1]
         srcr, yr, posr = _rows(src, C), _rows(y, C), _rows(pos, C)
         R = 1
@@ -111,11 +111,18 @@ class _ResNorm(torch.autograd.Function):
         rstd = torch.empty(R, dtype=torch.float32, device=dev) if norm else None
         xa = torch.empty((R, C), dtype=torch.bfloat16, device=dev) if want_a else None
         xap = torch.empty((R, C), dtype=torch.bfloat16, device=dev) if want_ap else None
-        xb = torch.empty((R, C), dtype=torch.float32, device=dev) if want_b else None
+        xb_map = (0, 0, 0)
+        if want_b and xb_into is not None:
+            # (Q, B, C) rows written as bf16 into layer l of the (L, B, Q, C) heads input
+            out, l = xb_into
+            xb = out[l]
+            xb_map = (shape[1], C, shape[0] * C)
+        else:
+            xb = torch.empty((R, C), dtype=torch.float32, device=dev) if want_b else None
         seed = flash._seed(dev) if p > 0 else None
         _native.call("ov3d_resnorm_fwd", R, C, srcr, _dt_flag(srcr), yr, _dt_flag(yr), float(p),
                      seed, site, ga, ba, posr, _dt_flag(posr), gb, bb, float(eps), s, mean, rstd,
-                     xa, xap, xb, like=s)
+                     xa, xap, xb, _dt_flag(xb), *xb_map, like=s)
         ctx.save_for_backward(s, mean, rstd, ga, gb)
         ctx.seed = seed   # the forward's dropout snapshot (attention._seed)
         ctx.params = (ga, ba, gb, bb)
@@ -124,6 +131,8 @@ class _ResNorm(torch.autograd.Function):
                     y.dtype if y is not None else None, pos.dtype if pos is not None else None)
         ctx.fans = fans
         v = lambda t: t.view(shape) if t is not None else None   # noqa: E731
+        if xb_map[0]:
+            return v(s), v(xa), v(xap), xb.transpose(0, 1)
         return v(s), v(xa), v(xap), v(xb)
 
     @staticmethod
@@ -139,7 +148,7 @@ class _ResNorm(torch.autograd.Function):
         # the decoder's layer outputs reach here as strided (L, B, C) views of the stacked
         # outputs' gradient: read in place (row r at (r // B) * s0 + (r % B) * s1)
         xb_map = (0, 0, 0)
-        if dxb is not None and dxb.dtype == torch.float32 and dxb.dim() == 3 and \
+        if dxb is not None and dxb.dtype in (torch.float32, torch.bfloat16) and dxb.dim() == 3 and \
                 dxb.stride(2) == 1 and not dxb.is_contiguous() and len(shape) == 3 and \
                 tuple(dxb.shape) == tuple(shape) and dxb.stride(0) >= C and dxb.stride(1) >= C:
             xb_map = (shape[1], dxb.stride(0), dxb.stride(1))
@@ -201,7 +210,8 @@ class _ResNorm(torch.autograd.Function):
             if (has_a or has_b) else None
         seed = ctx.seed if (p > 0 and dy is not None) else None
         if dsrc is not None or dy is not None or dpos is not None or has_a or has_b:
-            _native.call("ov3d_resnorm_bwd", R, C, s, mean, rstd, ds, dxa, dxap, dxb, *xb_map, ga, gb,
+            _native.call("ov3d_resnorm_bwd", R, C, s, mean, rstd, ds, dxa, dxap, dxb, _dt_flag(dxb),
+                         *xb_map, ga, gb,
                          float(p) if dy is not None else 0.0, seed, site, dsrc, dy, _dt_flag(dy),
                          dpos, _dt_flag(dpos), partials, nparts, dga, dba,
                          dgb, dbb, acc, like=s)
@@ -220,9 +230,11 @@ class _ResNorm(torch.autograd.Function):
 
 
 def resnorm(pend, norm_a=None, pos=None, want_a=True, want_ap=False, norm_b=None, pos_fan=None,
-            norm_b_fan=None):
+            norm_b_fan=None, xb_into=None):
     """-> (s, xa, xap, xb) for Pending(src, y, p, site); unwanted outputs are None.
-    pos_fan / norm_b_fan: FanIn shared by the calls that read the same pos / norm_b."""
+    pos_fan / norm_b_fan: FanIn shared by the calls that read the same pos / norm_b.
+    xb_into = (out, l): xb of these (Q, B, C) rows is written in bf16 into out[l] of an
+    (L, B, Q, C) buffer (the heads' row order) and returned as that (Q, B, C) view."""
     src, y, p, psite = pend
     ref = y if y is not None else src
     shape = tuple(ref.shape)
@@ -238,14 +250,32 @@ def resnorm(pend, norm_a=None, pos=None, want_a=True, want_ap=False, norm_b=None
     for fan in (pos_fan, norm_b_fan):
         if fan is not None:
             fan.n += 1
+    if norm_b is None or len(shape) != 3:
+        xb_into = None
     meta = (float(p) if y is not None else 0.0, int(psite), bool(want_a), bool(want_ap),
-            norm_b is not None, eps, shape, (pos_fan, norm_b_fan))
+            norm_b is not None, eps, shape, (pos_fan, norm_b_fan), xb_into)
     ga = norm_a.weight if norm_a is not None else None
     ba = norm_a.bias if norm_a is not None else None
     gb = norm_b.weight if norm_b is not None else None
     bb = norm_b.bias if norm_b is not None else None
     with torch.autocast("cuda", enabled=False):
         return _ResNorm.apply(meta, src, y, pos if want_ap else None, ga, ba, gb, bb)
+
+
+class Gather(torch.autograd.Function):
+    """The decoder's layer outputs as ONE (L, Q, B, C) tensor without a copy: every layer's
+    resnorm launch already wrote its rows into `out` (xb_into), so the forward returns
+    out's (L, Q, B, C) view and the backward hands each layer its (Q, B, C) slice of the
+    gradient as a strided view (read in place by the resnorm backward)."""
+
+    @staticmethod
+    def forward(ctx, out, *layers):
+        ctx.n = len(layers)
+        return out.permute(0, 2, 1, 3)
+
+    @staticmethod
+    def backward(ctx, g):
+        return (None,) + tuple(g[l] for l in range(ctx.n))
 
 
 def sites(module, n):
@@ -327,13 +357,21 @@ def _bias(b):
 
 
 def _ffn_ok(x, linear1, linear2, activation):
-    if not (fused_ffn and isinstance(activation, nn.ReLU) and x.is_cuda and x.dtype == torch.bfloat16
+    if not isinstance(activation, nn.ReLU):
+        return False
+    return ffn_weights_ok(x, linear1.weight, linear2.weight)
+
+
+def ffn_weights_ok(x, w1, w2):
+    """the fused two-GEMM path for (R, C) bf16 rows and (F, C) / (N, F) weights"""
+    if not (fused_ffn and x.is_cuda and x.dtype == torch.bfloat16
             and torch.is_autocast_enabled("cuda")
-            and torch.get_autocast_dtype("cuda") == torch.bfloat16 and x.stride(-1) == 1):
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16 and x.stride(-1) == 1
+            and w1.dim() == 2 and w2.dim() == 2):
         return False
     xr = x.reshape(-1, x.shape[-1])
     bf = torch.bfloat16
-    w1c, w2c = gemm.cast_param(linear1.weight, bf), gemm.cast_param(linear2.weight, bf)
+    w1c, w2c = gemm.cast_param(w1, bf), gemm.cast_param(w2, bf)
     if not (gemm._rows_gemm_ok(xr, w1c, True) and w2c.stride(1) == 1 and w2c.stride(0) % 8 == 0
             and w2c.data_ptr() % 16 == 0 and w2c.shape[1] == w1c.shape[0]):
         return False
@@ -352,6 +390,17 @@ def ffn(x, linear1, linear2, activation, dropout, site):
             return _FFN.apply(x, linear1.weight, linear1.bias, linear2.weight, linear2.bias, p, site)
     h = ffn_act(gemm.rows_linear(x, linear1.weight, linear1.bias), activation, dropout, site)
     return gemm.rows_linear(h, linear2.weight, linear2.bias)
+
+
+def ffn_weights(x, w1, b1, w2, b2):
+    """linear2(relu(linear1(x))) on bf16 rows (the query projection's conv pair, no dropout)"""
+    with torch.autocast("cuda", enabled=False):
+        return _FFN.apply(x, w1, b1, w2, b2, 0.0, 0)
+
+
+def relu_rows(y):
+    """relu of bf16 rows on the HIP row kernel (one launch each way)"""
+    return _ReluDropout.apply(y, 0.0, 0)
 
 
 def ffn_act(y, activation, dropout, site):

@@ -291,7 +291,9 @@ class _SAMLPPool(Function):
         parts = torch.empty((NPARTS_ROWS, c1, cin), dtype=torch.float64, device=dev)
         nat.call("ov3d_bn_relu_bwd_cin", 2, dz1, y1, a1, s1, None, None, cA, cB, cC, x0, cin, R, c1,
                  parts, None, NPARTS_ROWS, w1f, like=dout)
-        dw1 = _totals(parts, NPARTS_ROWS, cin * c1, None).view(c1, cin).float().view(w1shape)
+        dw1 = torch.empty(cin * c1, dtype=torch.float32, device=dev)
+        nat.call("ov3d_reduce_partials_f32", parts, NPARTS_ROWS, cin * c1, dw1, like=parts)
+        dw1 = dw1.view(w1shape)
         return (None, dw1, dw2.view(c2, c1), dw3.view(c3, c2), dg1, db1, dg2, db2, dg3, db3, None,
                 None, None)
 

@@ -17,6 +17,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
+from . import _native
 from . import attention as flash
 from . import resnorm as rn
 from . import gemm
@@ -113,17 +114,24 @@ class _MemoryKV(torch.autograd.Function):
         if pos is not None:   # the sum in the inputs' common type, rounded once on the store
             mpos = torch.empty((S * B, C), dtype=bf, device=memory.device)
             torch.add(memory, pos, out=mpos.view(S, B, C))
-        Wk = torch.cat([cast_param(w, bf)[E:2 * E] for w in ws])
-        Wv = torch.cat([cast_param(w, bf)[2 * E:] for w in ws])
-        bk = torch.cat([cast_param(b, bf)[E:2 * E] for b in bs])
-        bv = torch.cat([cast_param(b, bf)[2 * E:] for b in bs])
+        # the K / V row blocks of every layer's bf16 in_proj copy, gathered in one launch
         n = len(ws) * E
+        dev = memory.device
+        Wk, Wv = (torch.empty((n, C), dtype=bf, device=dev) for _ in range(2))
+        bk, bv = (torch.empty(n, dtype=bf, device=dev) for _ in range(2))
+        srcs, dsts = [], []
+        for l, (w, b) in enumerate(zip(ws, bs)):
+            wc, bc = cast_param(w, bf), cast_param(b, bf)
+            rows = slice(l * E, (l + 1) * E)
+            srcs += [wc[E:2 * E], wc[2 * E:], bc[E:2 * E], bc[2 * E:]]
+            dsts += [Wk[rows], Wv[rows], bk[rows], bv[rows]]
+        _native.multi_copy(dsts, srcs)
         K_all = torch.addmm(bk, mpos, Wk.t()).view(S, B, n)
         V_all = torch.addmm(bv, mem, Wv.t()).view(S, B, n)
         dK, dV = torch.empty_like(K_all), torch.empty_like(V_all)
         flash.defer_kv_grads(dK)   # the layers' dK / dV run batched in this op's backward
         token = torch.empty((), dtype=torch.float32, device=memory.device)
-        tok_grad = torch.zeros((), dtype=torch.float32, device=memory.device)
+        tok_grad = _zero_scalar(memory.device)
         ctx.save_for_backward(mem, mpos, Wk, Wv)
         ctx.meta = (E, memory.dtype, pos is not None and pos.requires_grad, len(ws), S * B, C)
         ctx.bufs = (dK, dV)
@@ -141,7 +149,8 @@ class _MemoryKV(torch.autograd.Function):
         params = ctx.params
         with torch.autocast("cuda", enabled=False):
             dmk = dK @ Wk
-            dmem = torch.addmm(dmk, dV, Wv) if not pos_grad else dV @ Wv + dmk
+            # in place when dmk is not also pos's gradient (no copy of dmk into a new output)
+            dmem = dmk.addmm_(dV, Wv) if not pos_grad else dV @ Wv + dmk
             grads = [None] * len(params)
             for l in range(L):
                 w, b = params[2 * l], params[2 * l + 1]
@@ -159,6 +168,18 @@ class _MemoryKV(torch.autograd.Function):
         shape = ctx.bufs[0].shape[:2] + (C,)
         dpos = dmk.view(shape).to(mdt) if pos_grad else None
         return (dmem.view(shape).to(mdt), dpos, None, *grads)
+
+
+_ZEROS = {}
+
+
+def _zero_scalar(device):
+    """a device 0.0 that nothing writes: allocated once (not zero-filled in every step)"""
+    z = _ZEROS.get(device)
+    if z is None:
+        z = torch.zeros((), dtype=torch.float32, device=device)
+        _ZEROS[device] = z
+    return z
 
 
 def memory_kv_ok(layers, memory):
@@ -467,13 +488,19 @@ class TransformerDecoder(nn.Module):
         pend = rn.Pending(tgt, None, 0.0, 0)
         inter = []
         dec_norm = self.norm if self.return_intermediate else None
+        # the layer outputs (decoder norm) go straight into the heads' bf16 (L, B, Q, C) rows
+        outs = None
+        if dec_norm is not None and tgt.dim() == 3:
+            Q, B, C = tgt.shape
+            outs = torch.empty((len(self.layers), B, Q, C), dtype=torch.bfloat16, device=tgt.device)
         # query_pos and the decoder norm are read by many launches: one gradient buffer each
         pos_fan, nb_fan = rn.FanIn(), rn.FanIn()
         for i, layer in enumerate(self.layers):
             s, x, xp, xd = rn.resnorm(pend, layer.norm1, pos=query_pos, want_a=True,
                                       want_ap=query_pos is not None,
                                       norm_b=dec_norm if i > 0 else None, pos_fan=pos_fan,
-                                      norm_b_fan=nb_fan)
+                                      norm_b_fan=nb_fan,
+                                      xb_into=(outs, i - 1) if outs is not None and i > 0 else None)
             if i > 0 and dec_norm is not None:
                 inter.append(xd)
             kvi = None
@@ -481,11 +508,14 @@ class TransformerDecoder(nn.Module):
                 kvi = kv[:5] + ((kv[5] if i == 0 else None),)
             pend = layer.forward_fused(s, x, xp, memory, memory_pos, query_pos, tgt_mask,
                                        memory_mask, kv=kvi, idx=i, pos_fan=pos_fan)
-        s, _, _, xd = rn.resnorm(pend, norm_b=self.norm, norm_b_fan=nb_fan)
+        s, _, _, xd = rn.resnorm(pend, norm_b=self.norm, norm_b_fan=nb_fan,
+                                 xb_into=(outs, len(self.layers) - 1) if outs is not None else None)
         out = xd if self.norm is not None else s
         if self.return_intermediate:
             if self.norm is None:
                 raise NotImplementedError("return_intermediate without a decoder norm")
             inter.append(out)
+            if outs is not None:
+                return rn.Gather.apply(outs, *inter), []
             return torch.stack(inter), []
         return out, []
