@@ -91,6 +91,19 @@ int ov3d_group_bwd_csr(const float* grad_out, const int32_t* offsets, const int3
                        int C, int N, long long feat_sb, long long feat_sn, long long feat_sc,
                        float* grad_features, void* stream);
 
+/* ov3d_group_fwd's rows in bf16 with row stride ldo (a multiple of 8, >= 3 + C; columns
+ * 3 + C .. ldo-1 written as zeros; out 16-byte aligned): the input of an SA MLP's first GEMM
+ * under bf16 autocast, with an aligned K (the masked encoder's interim SA: 259 -> 264). */
+int ov3d_group_rows_bf16(const float* xyz, const float* new_xyz, const float* features,
+                         long long feat_sb, long long feat_sn, long long feat_sc,
+                         const int32_t* idx, int B, int C, int N, int M, int S, float radius,
+                         int normalize, int ldo, void* out, void* stream);
+/* ov3d_group_bwd_csr for bf16 grad rows with row stride ldg (feature columns 3 .. 3+C). */
+int ov3d_group_bwd_csr_bf16(const void* grad_out, long long ldg, const int32_t* offsets,
+                            const int32_t* rows, int B, int C, int N, long long feat_sb,
+                            long long feat_sn, long long feat_sc, float* grad_features,
+                            void* stream);
+
 /* gather_operation (pointnet2_utils): features (B,C,N), idx (B,M) -> out (B,C,M) */
 int ov3d_gather_fwd(const float* features, const int32_t* idx, int B, int C, int N, int M,
                     float* out, void* stream);

@@ -61,6 +61,8 @@ _SIGS = {
     "ov3d_set_loss_fwd_split": "ppppppp",
     "ov3d_group_inverse": "piiiippppp",
     "ov3d_group_bwd_csr": "pppiiilllpp",
+    "ov3d_group_bwd_csr_bf16": "plppiiilllpp",
+    "ov3d_group_rows_bf16": "ppplllpiiiiifiipp",
     "ov3d_nbr_max_bwd": "ppliipp",
     "ov3d_wgrad": "plpliiiplpppip",
     "ov3d_wgrad_group": "pipp",

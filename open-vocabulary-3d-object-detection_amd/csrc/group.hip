@@ -274,7 +274,48 @@ __global__ __launch_bounds__(256) void inv_fill_kernel(const int32_t* __restrict
 
 // gather-form grouping backward: thread per (b, n, c), c fastest (a wave reads 64 channels of
 // one grad row per list entry); every (b, n, c) written (0 when no row refers to n)
-__global__ __launch_bounds__(256) void group_bwd_csr_kernel(const float* __restrict__ gout,
+// The same rows as group_fwd_kernel in bf16 with a padded row stride ldo (a multiple of 8,
+// columns 3 + C .. ldo - 1 zero): the SA MLP's first GEMM reads them directly with an aligned K
+// (bf16 autocast rounds the fp32 rows to these values before the GEMM anyway).  One thread per
+// 8 columns of a row: consecutive threads cover a row left to right (contiguous feature reads
+// for channel-contiguous features), one 16-byte store each.
+__global__ __launch_bounds__(256) void group_rows_bf16_kernel(
+    const float* __restrict__ xyz, const float* __restrict__ new_xyz,
+    const float* __restrict__ feats, long long sb, long long sn, long long sc,
+    const int32_t* __restrict__ idx, int B, int C, int N, int M, int S, float radius,
+    int normalize, int ldo, __bf16* __restrict__ out) {
+    typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    const int chunks = ldo >> 3;
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long rows = (long long)B * M * S;
+    if (t >= rows * chunks) return;
+    const long long row = t / chunks;
+    const int c0 = (int)(t - row * chunks) * 8;
+    const int b = (int)(row / ((long long)M * S));
+    const int m = (int)((row / S) % M);
+    const int k = idx[row];
+    const float* const f = feats ? feats + b * sb + k * sn : nullptr;
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j;
+        float x = 0.f;
+        if (c < 3) {
+            x = xyz[((size_t)b * N + k) * 3 + c] - new_xyz[((size_t)b * M + m) * 3 + c];
+            if (normalize) x = x / radius;
+        } else if (c < 3 + C) {
+            x = f[(c - 3) * sc];
+        }
+        v[j] = (__bf16)x;
+    }
+    *reinterpret_cast<bf16x8*>(out + row * ldo + c0) = v;
+}
+
+// gather-form grouping backward (below) reading the feature columns 3 .. 3 + C of grad rows
+// with row stride ldg (fp32 rows of group_fwd_kernel: ldg = 3 + C; bf16 rows of
+// group_rows_bf16_kernel: ldg = its ldo)
+template <typename GT>
+__global__ __launch_bounds__(256) void group_bwd_csr_kernel(const GT* __restrict__ gout, long long ldg,
                                                             const int32_t* __restrict__ off,
                                                             const int32_t* __restrict__ rows, int B,
                                                             int C, int N, long long sb,
@@ -296,7 +337,7 @@ __global__ __launch_bounds__(256) void group_bwd_csr_kernel(const float* __restr
 #pragma unroll
         for (int u = 0; u < 8; ++u) r[u] = rows[e + u];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = gout[(size_t)r[u] * (3 + C) + 3 + c];
+        for (int u = 0; u < 8; ++u) v[u] = (float)gout[(size_t)r[u] * ldg + 3 + c];
 #pragma unroll
         for (int u = 0; u < 8; ++u) acc += v[u];
     }
@@ -306,7 +347,7 @@ __global__ __launch_bounds__(256) void group_bwd_csr_kernel(const float* __restr
 #pragma unroll
         for (int u = 0; u < 8; ++u) r[u] = e + u < e1 ? rows[e + u] : -1;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = r[u] >= 0 ? gout[(size_t)r[u] * (3 + C) + 3 + c] : 0.f;
+        for (int u = 0; u < 8; ++u) v[u] = r[u] >= 0 ? (float)gout[(size_t)r[u] * ldg + 3 + c] : 0.f;
 #pragma unroll
         for (int u = 0; u < 8; ++u) acc += v[u];
     }
@@ -341,9 +382,43 @@ extern "C" int ov3d_group_bwd_csr(const float* grad_out, const int32_t* offsets,
         return OV3D_EINVAL;
     const long long total = (long long)B * N * C;
     if (total == 0) return OV3D_OK;
-    hipLaunchKernelGGL(group_bwd_csr_kernel, dim3(ov3d_cdiv(total, 256)), dim3(256), 0,
-                       ov3d_stream(stream), grad_out, offsets, rows, B, C, N, feat_sb, feat_sn,
-                       feat_sc, grad_features);
+    hipLaunchKernelGGL(group_bwd_csr_kernel<float>, dim3(ov3d_cdiv(total, 256)), dim3(256), 0,
+                       ov3d_stream(stream), grad_out, (long long)(3 + C), offsets, rows, B, C, N,
+                       feat_sb, feat_sn, feat_sc, grad_features);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_group_bwd_csr_bf16(const void* grad_out, long long ldg, const int32_t* offsets,
+                                       const int32_t* rows, int B, int C, int N, long long feat_sb,
+                                       long long feat_sn, long long feat_sc, float* grad_features,
+                                       void* stream) {
+    if (!grad_out || !offsets || !rows || !grad_features || B < 0 || C < 0 || N <= 0 ||
+        ldg < 3 + C)
+        return OV3D_EINVAL;
+    const long long total = (long long)B * N * C;
+    if (total == 0) return OV3D_OK;
+    hipLaunchKernelGGL(group_bwd_csr_kernel<__bf16>, dim3(ov3d_cdiv(total, 256)), dim3(256), 0,
+                       ov3d_stream(stream), static_cast<const __bf16*>(grad_out), ldg, offsets, rows,
+                       B, C, N, feat_sb, feat_sn, feat_sc, grad_features);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_group_rows_bf16(const float* xyz, const float* new_xyz, const float* features,
+                                    long long feat_sb, long long feat_sn, long long feat_sc,
+                                    const int32_t* idx, int B, int C, int N, int M, int S,
+                                    float radius, int normalize, int ldo, void* out, void* stream) {
+    if (B < 0 || C < 0 || N <= 0 || M < 0 || S <= 0 || !xyz || !new_xyz || !idx || !out ||
+        ldo < 3 + C || (ldo & 7) || ((uintptr_t)out & 15))
+        return OV3D_EINVAL;
+    if (C > 0 && !features) return OV3D_EINVAL;
+    const long long total = (long long)B * M * S * (ldo / 8);
+    if (total == 0) return OV3D_OK;
+    hipLaunchKernelGGL(group_rows_bf16_kernel, dim3(ov3d_cdiv(total, 256)), dim3(256), 0,
+                       ov3d_stream(stream), xyz, new_xyz, C > 0 ? features : nullptr, feat_sb,
+                       feat_sn, feat_sc, idx, B, C, N, M, S, radius, normalize, ldo,
+                       static_cast<__bf16*>(out));
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

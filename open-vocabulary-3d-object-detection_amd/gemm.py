@@ -534,6 +534,44 @@ class _RowsLinear(Function):
         return dx, dw, db
 
 
+class _RowsLinearPadK(Function):
+    """y = x[:, :K] W^T (+ b) for bf16 rows x (R, Kp) whose columns K .. Kp-1 are zero (Kp a
+    multiple of 8, K = W's input width): the GEMM runs on the zero-padded weight (aligned K, the
+    interim SA's 259 -> 264), dW = dy^T x[:, :K] comes from the strided rows directly (deferred
+    like the other weight gradients), dx is (R, Kp) with zero pad columns."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        bf = torch.bfloat16
+        K, Kp = w.shape[1], x.shape[1]
+        wc = cast_param(w, bf)
+        wp = torch.nn.functional.pad(wc, (0, Kp - K))
+        with torch.autocast("cuda", enabled=False):
+            y = _linear(x, wp, cast_param(b, bf))
+        ctx.save_for_backward(x, wp)
+        ctx.meta = (w.dtype, b is not None, K)
+        ctx.params = (w, b)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wp = ctx.saved_tensors
+        wdt, has_b, K = ctx.meta
+        w, b = ctx.params
+        dy = dy.to(torch.bfloat16).contiguous()
+        with torch.autocast("cuda", enabled=False):
+            dx = _dgrad(dy, wp) if ctx.needs_input_grad[0] else None
+            xk = x[:, :K]
+            dw, db = linear_weight_grads(dy, xk, w, b, ctx.needs_input_grad[1],
+                                         has_b and ctx.needs_input_grad[2])
+        return dx, dw, db
+
+
+def rows_linear_padk(x, w, b=None):
+    """rows_linear for bf16 rows with zero-padded columns beyond W's input width"""
+    return _RowsLinearPadK.apply(x, w, b)
+
+
 def rows_linear(x, w, b=None):
     """y = x W^T (+ b) for x (..., Cin); split-K dW on the ROCm device, plain F.linear on CPU."""
     if not x.is_cuda:

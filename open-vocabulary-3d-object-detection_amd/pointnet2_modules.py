@@ -75,9 +75,14 @@ class SharedMLP(nn.Sequential):
         ScanNet SA with colour and the masked encoder's interim SA, which the fused
         3-channel kernels of sa_fused.py do not take)."""
         from . import heads
+        from .gemm import rows_linear_padk
         for layer in self:
             w = layer.conv.weight
-            x = rows_linear(x, w.view(w.shape[0], w.shape[1]), layer.conv.bias)
+            w2 = w.view(w.shape[0], w.shape[1])
+            if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] > w2.shape[1]:
+                x = rows_linear_padk(x, w2, layer.conv.bias)   # zero-padded bf16 group rows
+            else:
+                x = rows_linear(x, w2, layer.conv.bias)
             if hasattr(layer, "bn"):
                 bn = layer.bn.bn
                 if heads.bn_relu_rows_ok(x, bn, layer.activation, None):
@@ -162,8 +167,15 @@ class PointnetSAModuleVotes(nn.Module):
 
     def _mlp_pool(self, xyz, new_xyz, features, ball=None, inverse=None):
         """grouped rows -> SharedMLP -> max over nsample: (B, npoint, Cout)."""
-        g = self.grouper.rows(xyz, new_xyz, features) if ball is None else \
-            self.grouper.rows(xyz, new_xyz, features, idx=ball, inverse=inverse)   # (B,M,S,3+C)
+        # bf16 rows with an aligned width for the GEMM path under bf16 autocast (the masked
+        # encoder's interim SA: 256 features + xyz -> 264 columns); fp32 rows otherwise and for
+        # the fused SA kernels' 3- / 6-channel first layers
+        bf16_rows = (features is not None and features.shape[1] > 3 and xyz.is_cuda
+                     and torch.is_autocast_enabled("cuda")
+                     and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+        kw = {"bf16_rows": True} if bf16_rows else {}
+        g = self.grouper.rows(xyz, new_xyz, features, **kw) if ball is None else \
+            self.grouper.rows(xyz, new_xyz, features, idx=ball, inverse=inverse, **kw)   # (B,M,S,3+C)
         B, M, S, C = g.shape
         rows = g.view(B * M * S, C)
         if self.training and sa_fused.supported(self.mlp_module, rows, S):

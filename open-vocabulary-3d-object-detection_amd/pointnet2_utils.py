@@ -152,6 +152,43 @@ class _Group(Function):
         return None, None, gf, None, None, None, None
 
 
+class _GroupBf16(Function):
+    """_Group's rows in bf16, zero-padded to Cp = round_up(3 + C, 8) columns (aligned GEMM K);
+    the backward gathers the feature columns of the bf16 row gradient through the inverse."""
+
+    @staticmethod
+    def forward(ctx, xyz, new_xyz, features, idx, radius, normalize, inverse=None):
+        B, N, _ = xyz.shape
+        _, M, S = idx.shape
+        C = features.shape[1]
+        strides = _dense_strides(features)
+        if strides is None:
+            features = features.contiguous()
+            strides = _dense_strides(features)
+        cp = (3 + C + 7) // 8 * 8
+        out = torch.empty((B, M, S, cp), dtype=torch.bfloat16, device=xyz.device)
+        nat.call("ov3d_group_rows_bf16", xyz, new_xyz, features, *strides, idx, B, C, N, M, S,
+                 float(radius), int(bool(normalize)), cp, out, like=xyz)
+        ctx.meta = (B, C, N, strides, tuple(features.shape), tuple(features.stride()), cp)
+        ctx.inverse = inverse
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        B, C, N, strides, shape, stride, cp = ctx.meta
+        if not ctx.needs_input_grad[2]:
+            return None, None, None, None, None, None, None
+        if ctx.inverse is None:
+            raise RuntimeError("_GroupBf16: the gradient needs the ball query's inverse")
+        g = g.to(torch.bfloat16)
+        if g.stride(-1) != 1 or g.stride(-2) != cp or not g.view(-1, cp).is_contiguous():
+            g = g.contiguous()
+        gf = torch.empty_strided(shape, stride, dtype=torch.float32, device=g.device)
+        off, rows = ctx.inverse
+        nat.call("ov3d_group_bwd_csr_bf16", g, cp, off, rows, B, C, N, *strides, gf, like=g)
+        return None, None, gf, None, None, None, None
+
+
 def group_inverse(idx, N):
     """(B, M, S) int32 ball-query indices over N points -> (offsets (B*N+1), rows (B*M*S)):
     the rows that read each point (ov3d_group_inverse), for the gather-form backward."""
@@ -192,10 +229,11 @@ class QueryAndGroup(nn.Module):
         self.radius, self.nsample = radius, nsample
         self.use_xyz, self.ret_grouped_xyz, self.normalize_xyz = use_xyz, ret_grouped_xyz, normalize_xyz
 
-    def rows(self, xyz, new_xyz, features=None, idx=None, inverse=None):
+    def rows(self, xyz, new_xyz, features=None, idx=None, inverse=None, bf16_rows=False):
         """Grouped features as channels-last rows (B, npoint, nsample, 3+C).  idx: the
         ball-query indices of (xyz, new_xyz) when computed ahead of time; inverse: its
-        group_inverse (offsets, rows), likewise."""
+        group_inverse (offsets, rows), likewise.  bf16_rows: bf16 rows padded with zero
+        columns to a multiple of 8 (B, npoint, nsample, Cp) for a GEMM (gemm.rows_linear_padk)."""
         if xyz.requires_grad or new_xyz.requires_grad:
             raise NotImplementedError("gradients w.r.t. point coordinates are not on the path")
         if idx is None:
@@ -212,8 +250,10 @@ class QueryAndGroup(nn.Module):
             nat.check_device(features, "features")
         inv = None
         if features is not None and features.requires_grad and torch.is_grad_enabled() and \
-                GATHER_BWD:
+                (GATHER_BWD or bf16_rows):
             inv = inverse if inverse is not None else group_inverse(idx.contiguous(), xyz.shape[1])
+        if bf16_rows and features is not None:
+            return _GroupBf16.apply(xyz, new_xyz, features, idx, self.radius, self.normalize_xyz, inv)
         return _Group.apply(xyz, new_xyz, features, idx, self.radius, self.normalize_xyz, inv)
 
     def forward(self, xyz, new_xyz, features=None):

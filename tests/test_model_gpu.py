@@ -107,7 +107,9 @@ def test_full_size_c4_train_step_properties(cuda):
               "ov3d_nbr_max_bwd", "ov3d_giou3d_bwd", "ov3d_sa_layer_pool_fwd", "ov3d_fps",
               "ov3d_ball_query"):
         assert called.get(k), (k, sorted(called))
-    assert called.get("ov3d_group_bwd_csr") or called.get("ov3d_group_bwd"), sorted(called)
+    # the interim SA's grouped rows: bf16, zero-padded to 264 columns (aligned GEMM K)
+    assert called.get("ov3d_group_rows_bf16"), sorted(called)
+    assert called.get("ov3d_group_bwd_csr_bf16"), sorted(called)
     assert torch.isfinite(loss) and len(ld) == 56
     assert out["outputs"]["sem_cls_logits"].shape[:2] == (8, 256)
     gn = torch.nn.utils.clip_grad_norm_(model.parameters(), 0.1)
