@@ -327,13 +327,17 @@ int ov3d_project_box2d(const float* center, const float* size, const float* head
  *     row-major (R, T) when lq == 0, else the reference's transposed layout of quirk Q8:
  *     (lb, q, t) at lb*lq*T + t*lq + q
  *   box head i (ns <= 4): ws[i] (n[i] <= 32, 256) bf16, bs[i] (n[i]) f32 ->
- *     out_s[:, ocol[i] : ocol[i] + n[i]] of (R, Ns) f32 */
+ *     out_s[:, ocol[i] : ocol[i] + n[i]] of (R, Ns) f32
+ *   work: ov3d_heads_out_workspace(R, T) floats (the column groups' partial logits) */
 int ov3d_heads_out_max_text(void);
+long long ov3d_heads_out_workspace(int R, int T);
 int ov3d_heads_out_fwd(const void* z, long long ldz, int R, const void* wv, const float* bv, int Nv,
                        const float* text, int T, int lq, float* out_v, float* logits, int ns,
                        const void* const* ws, const float* const* bs, const int* n,
-                       const int* kcol, const int* ocol, float* out_s, int Ns, void* stream);
-/* Its backward: gvb = bf16(gv + glog . text) (R, Nv); gsb = bf16(gs) (R, Ns); the box heads'
+                       const int* kcol, const int* ocol, float* out_s, int Ns, float* work,
+                       void* stream);
+/* Its backward: gvb = bf16(gv + glog . text) (R, Nv) (gv may be NULL: zero); gsb = bf16(gs)
+ * (R, Ns); the box heads'
  * input gradient dz[:, kcol[i] + c] = bf16(sum_j gsb[:, ocol[i] + j] ws[i][j, c]), c < 256
  * (dz (R, lddz) bf16; its visual columns are left to the caller's dgrad GEMM on gvb). */
 int ov3d_heads_out_bwd(const float* gv, const float* glog, const float* text, int R, int Nv, int T,

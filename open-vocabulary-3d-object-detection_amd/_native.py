@@ -103,7 +103,7 @@ _SIGS = {
     "ov3d_ap_match": "ppppiiiidpp",
     "ov3d_ap_curve": "plppiplppp",
     "ov3d_project_box2d": "pppliipppppp",
-    "ov3d_heads_out_fwd": "plippipiippippppppip",
+    "ov3d_heads_out_fwd": "plippipiippippppppipp",
     "ov3d_heads_out_bwd": "pppiiiipiippppppplp",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
@@ -113,7 +113,8 @@ EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_
                           "ov3d_resnorm_supported", "ov3d_resnorm_bwd_parts",
                           "ov3d_adamw_chunk", "ov3d_wgrad_group_workspace",
                           "ov3d_rows_gemm_supported", "ov3d_sa_dy_fused_supported",
-                          "ov3d_tile_gemm_supported", "ov3d_sun_range_parts", "ov3d_heads_out_max_text")
+                          "ov3d_tile_gemm_supported", "ov3d_sun_range_parts", "ov3d_heads_out_max_text",
+                          "ov3d_heads_out_workspace")
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_longlong, "f": ctypes.c_float,
        "d": ctypes.c_double}
@@ -176,6 +177,8 @@ def load():
         lib.ov3d_sun_range_parts.restype = ctypes.c_int
         lib.ov3d_heads_out_max_text.argtypes = []
         lib.ov3d_heads_out_max_text.restype = ctypes.c_int
+        lib.ov3d_heads_out_workspace.argtypes = [ctypes.c_int] * 2
+        lib.ov3d_heads_out_workspace.restype = ctypes.c_longlong
         lib.ov3d_version.argtypes = []
         lib.ov3d_version.restype = ctypes.c_char_p
         _lib = lib

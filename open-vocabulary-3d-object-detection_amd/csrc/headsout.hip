@@ -8,21 +8,21 @@
 // heads.py feeds the rows z2 (R, 5*256) bf16: columns [0, 256) are the visual head's hidden
 // features, [256 (1+i), 256 (2+i)) those of box head i.
 //
-// Forward (heads_out_fwd_kernel): a workgroup per 32 rows, 4 waves.  Each 32-channel output
-// tile is one MFMA 32x32x16 chain over K = 256 (A = weight rows, B = the 32 rows, so a lane
-// owns a row and 16 of the tile's channels): the visual head's 20 tiles (5 per wave) and one
-// tile per box head (n_out <= 32, rows past n_out read as zero).  The visual tiles' epilogue
-// writes the fp32 embedding and, with the text embedding staged in LDS, accumulates the fp32
-// logits of the lane's row over its channels (1/4 of the 640 per wave; reduced across the
-// two lane halves and the four waves in LDS) -- the alignment GEMM never re-reads the
-// embedding from HBM.  Logits are written in the caller's layout: row-major (R, T), or with
+// Forward (heads_out_fwd_kernel): six workgroups of 4 waves per 32 rows (see "Column groups"
+// below).  Each 32-channel output tile is one MFMA 32x32x16 chain over K = 256 (A = weight rows,
+// B = the 32 rows, so a lane owns a row and 16 of the tile's channels): the visual head's 20
+// tiles (one per wave of five workgroups) and one tile per box head (n_out <= 32, rows past
+// n_out read as zero).  The visual tiles' epilogue writes the fp32 embedding and, with the
+// group's 128 text columns staged in LDS, the fp32 partial logits of the lane's row over its
+// channels (the alignment GEMM never re-reads the embedding from HBM); a second launch adds
+// the groups' partials.  Logits are written in the caller's layout: row-major (R, T), or with
 // Q > 0 the reference's transposed layout (quirk Q8: element (lb, q, t) of the (L*B, Q, T)
 // result at lb*Q*T + t*Q + q).
 //
-// Backward (heads_out_bwd_kernel): a workgroup per 32 rows: the visual embedding's gradient
+// Backward (heads_out_bwd_kernel): per 32 rows, five workgroups for the visual embedding's gradient
 // plus the alignment's contribution, g_v + g_logits . text, rounded once to bf16 (the operand
-// of the dgrad GEMM and the deferred weight gradient); the box heads' output gradients in
-// bf16; and the box heads' input gradient dz2[:, 256 (1+i) + c] = sum_j g_i[j] W_i[j, c]
+// of the dgrad GEMM and the deferred weight gradient) and one for the box heads' output
+// gradients in bf16 and the box heads' input gradient dz2[:, 256 (1+i) + c] = sum_j g_i[j] W_i[j, c]
 // (n_out <= 32 terms, fp32) into its columns of the caller's dz2.
 #include "common.h"
 
@@ -38,7 +38,6 @@ constexpr int KH = 256;         // hidden width of every head
 constexpr int MAXT = 32;        // text rows (classes) the fused alignment supports
 constexpr int MAXS = 4;         // box heads
 constexpr int NV = 640;         // visual embedding width (clip_embed_length)
-constexpr int VT = NV / 32 / 4; // visual output tiles per wave
 
 struct HeadsOutArgs {
     const bf16* z;              // (R, ldz) bf16
@@ -69,34 +68,8 @@ __device__ __forceinline__ T pick4(const T (&v)[MAXS], int i) {
     return i == 0 ? v[0] : i == 1 ? v[1] : i == 2 ? v[2] : v[3];
 }
 
-// copy n4 float4 from global to LDS with every thread's loads in flight together (a plain
-// load -> store loop waits out one global latency per iteration)
-__device__ __forceinline__ void stage_f4(float4* __restrict__ dst, const float4* __restrict__ src, int n4,
-                                         int tid) {
-    constexpr int U = 8;
-    for (int base = 0; base < n4; base += 256 * U) {
-        float4 v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int i = base + 256 * u + tid;
-            v[u] = src[i < n4 ? i : n4 - 1];   // clamped, unconditional (keeps v in registers)
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int i = base + 256 * u + tid;
-            if (i < n4) dst[i] = v[u];
-        }
-    }
-}
-
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ long long logit_at(const HeadsOutArgs& a, int row, int t) {
-    if (a.lq <= 0) return (long long)row * a.T + t;
-    const int lb = row / a.lq, q = row - lb * a.lq;
-    return ((long long)lb * a.T + t) * a.lq + q;
 }
 
 // one 32-channel tile of rows z (this lane: row r, operand k-half h): acc[e] = channel
@@ -122,115 +95,130 @@ __device__ __forceinline__ f32x16 tile_gemm(const bf16* __restrict__ w, int nrow
     return acc;
 }
 
+// Column groups of the forward (round 3): the visual head's 20 output tiles split over NGV = 5
+// workgroups per 32-row block (one tile per wave), the four box heads in a sixth (one head per
+// wave), so a 32-row block is 6 workgroups of single-tile waves instead of one workgroup walking
+// 5 + 1 tiles per wave with the whole text embedding staged (74 us for 8192 rows, latency-bound).
+// Each visual workgroup stages the block's z rows once in LDS and its 128 text columns, and
+// writes the alignment's partial logits over those 128 channels; ov3d_heads_logits_sum adds the
+// NGV partials in group order.
+constexpr int NGV = NV / 128;   // visual column groups
+constexpr int ZLD = KH + 8;     // padded LDS row of the staged z block (bf16)
+
 // TMAX: the text rows rounded up (8, 16, 24 or 32); rows T..TMAX-1 of the LDS image are zero,
-// so the logit loops are branch-free and their LDS reads batch (a per-row `t < T` branch
-// waited out one LDS round trip per read)
+// so the logit loops are branch-free and their LDS reads batch
 template <int TMAX>
-__global__ void __launch_bounds__(256, 1) heads_out_fwd_kernel(HeadsOutArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    float* textS = smem;                         // (TMAX, Nv), zero rows past T
-    float* red = smem + (size_t)TMAX * a.Nv;     // (4 waves, 32 rows, TMAX)
+__global__ void __launch_bounds__(256) heads_out_fwd_kernel(HeadsOutArgs a, float* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) bf16 zS[RB * ZLD];       // the block's z rows
+    __shared__ __attribute__((aligned(16))) float textS[TMAX * 128];  // (TMAX, 128 channels)
+    __shared__ float red[4][RB][TMAX + 1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int row0 = blockIdx.x * RB;
     const int row = row0 + r;
-    const int rowc = row < a.R ? row : a.R - 1;
-    const bool align = a.text != nullptr;
-    if (align) {
-        stage_f4(reinterpret_cast<float4*>(textS), reinterpret_cast<const float4*>(a.text),
-                 a.T * a.Nv / 4, tid);
-        for (int i = a.T * a.Nv / 4 + tid; i < TMAX * a.Nv / 4; i += 256)
-            reinterpret_cast<float4*>(textS)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-        __syncthreads();
-    }
-    // this lane's row, visual columns [0, 256)
+    const int grp = blockIdx.y;
+    const bool visual = grp < NGV;
+    if (!visual && wave >= a.ns) return;
+    const bool align = visual && a.text != nullptr;
+    const int zcol = visual ? 0 : pick4(a.kcol, wave);
     bf16x8 zf[KH / 16];
-    {
-        const bf16* zr = a.z + (size_t)rowc * a.ldz + 8 * h;
+    if (visual) {
+        // z rows [row0, row0 + 32), columns [0, 256): 1024 16-byte chunks, 4 per thread
 #pragma unroll
-        for (int s = 0; s < KH / 16; ++s) zf[s] = *reinterpret_cast<const bf16x8*>(zr + 16 * s);
+        for (int u = 0; u < 4; ++u) {
+            const int ch = tid + 256 * u, rr = ch >> 5, kc = (ch & 31) * 8;
+            const int rowc = min(row0 + rr, a.R - 1);
+            *reinterpret_cast<bf16x8*>(&zS[rr * ZLD + kc]) =
+                *reinterpret_cast<const bf16x8*>(a.z + (size_t)rowc * a.ldz + kc);
+        }
+        if (align)
+            for (int i = tid; i < TMAX * 32; i += 256) {   // (TMAX, 128) float4 chunks
+                const int t = i >> 5, c4 = i & 31;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (t < a.T) v = *reinterpret_cast<const float4*>(a.text + (size_t)t * a.Nv + grp * 128 + 4 * c4);
+                reinterpret_cast<float4*>(textS)[i] = v;
+            }
+        __syncthreads();
+#pragma unroll
+        for (int s2 = 0; s2 < KH / 16; ++s2) zf[s2] = *reinterpret_cast<const bf16x8*>(&zS[r * ZLD + 16 * s2 + 8 * h]);
+    } else {
+        const int rowc = min(row, a.R - 1);
+        const bf16* zr = a.z + (size_t)rowc * a.ldz + zcol + 8 * h;
+#pragma unroll
+        for (int s2 = 0; s2 < KH / 16; ++s2) zf[s2] = *reinterpret_cast<const bf16x8*>(zr + 16 * s2);
     }
-    // the wave's VT visual tiles (channels 32 (wave + 4k) ..), kept for the logits; the next
-    // tile's weight rows and biases are loaded while this tile's MFMAs run (one wave per SIMD:
-    // nothing else hides the L2 latency)
-    float v[VT][16];
-    bf16x8 wf[2][KH / 16];
-    float4 bq[2][4];
-    auto load_tile = [&](int k, int slot) {
-        const int ct = wave + 4 * k;
-        const bf16* wr = a.wv + ((size_t)ct * 32 + r) * KH + 8 * h;
-#pragma unroll
-        for (int s = 0; s < KH / 16; ++s) wf[slot][s] = *reinterpret_cast<const bf16x8*>(wr + 16 * s);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) bq[slot][g] = *reinterpret_cast<const float4*>(a.bv + 32 * ct + 8 * g + 4 * h);
-    };
-    load_tile(0, 0);
-#pragma unroll
-    for (int k = 0; k < VT; ++k) {
-        const int ct = wave + 4 * k;
-        if (k + 1 < VT) load_tile(k + 1, (k + 1) & 1);
-        f32x16 acc;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-#pragma unroll
-        for (int s = 0; s < KH / 16; ++s) acc = mfma(wf[k & 1][s], zf[s], acc);
+    if (visual) {
+        const int ct = grp * 4 + wave;   // output tile: channels [32 ct, 32 ct + 32)
+        const f32x16 acc = tile_gemm(a.wv + (size_t)ct * 32 * KH, 32, zf, r, h);
+        float v[16];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int ch = 32 * ct + 8 * g + 4 * h;
-            const float4 b4 = bq[k & 1][g];
-            v[k][4 * g] = acc[4 * g] + b4.x;
-            v[k][4 * g + 1] = acc[4 * g + 1] + b4.y;
-            v[k][4 * g + 2] = acc[4 * g + 2] + b4.z;
-            v[k][4 * g + 3] = acc[4 * g + 3] + b4.w;
+            const float4 b4 = *reinterpret_cast<const float4*>(a.bv + ch);
+            v[4 * g] = acc[4 * g] + b4.x;
+            v[4 * g + 1] = acc[4 * g + 1] + b4.y;
+            v[4 * g + 2] = acc[4 * g + 2] + b4.z;
+            v[4 * g + 3] = acc[4 * g + 3] + b4.w;
+            // (staging the group's 32 x 128 outputs in LDS for whole-row stores measured slower:
+            // 36.5 -> 39.2 us, the extra 17 KB of LDS costs occupancy)
             if (row < a.R)
                 *reinterpret_cast<float4*>(a.out_v + (size_t)row * a.Nv + ch) =
-                    make_float4(v[k][4 * g], v[k][4 * g + 1], v[k][4 * g + 2], v[k][4 * g + 3]);
+                    make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
         }
-    }
-    if (align) {
+        if (align) {
 #pragma unroll
-        for (int t = 0; t < TMAX; ++t) {
-            float lg = 0.f;
-#pragma unroll
-            for (int k = 0; k < VT; ++k)
+            for (int t = 0; t < TMAX; ++t) {
+                float lg = 0.f;
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    const int ch = 32 * (wave + 4 * k) + 8 * g + 4 * h;
-                    const float4 tx = *reinterpret_cast<const float4*>(textS + (size_t)t * a.Nv + ch);
-                    lg = fmaf(v[k][4 * g], tx.x, fmaf(v[k][4 * g + 1], tx.y,
-                         fmaf(v[k][4 * g + 2], tx.z, fmaf(v[k][4 * g + 3], tx.w, lg))));
+                    const int cl = 32 * wave + 8 * g + 4 * h;   // channel within the group
+                    const float4 tx = *reinterpret_cast<const float4*>(textS + t * 128 + cl);
+                    lg = fmaf(v[4 * g], tx.x, fmaf(v[4 * g + 1], tx.y,
+                         fmaf(v[4 * g + 2], tx.z, fmaf(v[4 * g + 3], tx.w, lg))));
                 }
-            lg += __shfl_xor(lg, 32);
-            if (h == 0) red[((size_t)wave * RB + r) * TMAX + t] = lg;
-        }
-    }
-    // box head `wave`: its 256 input columns, one tile
-    if (wave < a.ns) {
-        const bf16* zr = a.z + (size_t)rowc * a.ldz + pick4(a.kcol, wave) + 8 * h;
-#pragma unroll
-        for (int s = 0; s < KH / 16; ++s) zf[s] = *reinterpret_cast<const bf16x8*>(zr + 16 * s);
-        const int n = pick4(a.n, wave);
-        const f32x16 acc = tile_gemm(pick4(a.ws, wave), n, zf, r, h);
-        if (row < a.R) {
-            float* o = a.out_s + (size_t)row * a.Ns + pick4(a.ocol, wave);
-            const float* bsw = pick4(a.bs, wave);
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int c = 8 * (e >> 2) + 4 * h + (e & 3);
-                if (c < n) o[c] = acc[e] + bsw[c];
+                lg += __shfl_xor(lg, 32);
+                if (h == 0) red[wave][r][t] = lg;
+            }
+            __syncthreads();
+            // the group's partial logits (R, T) at part[grp], rows of this block
+            for (int i = tid; i < RB * a.T; i += 256) {
+                const int rr = i / a.T, t = i - rr * a.T;
+                if (row0 + rr >= a.R) continue;
+                part[((size_t)grp * a.R + row0 + rr) * a.T + t] =
+                    (red[0][rr][t] + red[1][rr][t]) + (red[2][rr][t] + red[3][rr][t]);
             }
         }
+        return;
     }
-    if (align) {
-        __syncthreads();
-        for (int i = tid; i < RB * a.T; i += 256) {
-            const int rr = i / a.T, t = i - rr * a.T;
-            if (row0 + rr >= a.R) continue;
-            const float s = red[(size_t)rr * TMAX + t] + red[((size_t)RB + rr) * TMAX + t] +
-                            red[((size_t)2 * RB + rr) * TMAX + t] + red[((size_t)3 * RB + rr) * TMAX + t];
-            a.logits[logit_at(a, row0 + rr, t)] = s;
+    // box head `wave`: one tile
+    const int n = pick4(a.n, wave);
+    const f32x16 acc = tile_gemm(pick4(a.ws, wave), n, zf, r, h);
+    if (row < a.R) {
+        float* o = a.out_s + (size_t)row * a.Ns + pick4(a.ocol, wave);
+        const float* bsw = pick4(a.bs, wave);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int c = 8 * (e >> 2) + 4 * h + (e & 3);
+            if (c < n) o[c] = acc[e] + bsw[c];
         }
     }
+}
+
+// logits = the NGV groups' partials added in group order, written in the caller's layout
+__global__ void __launch_bounds__(256) heads_logits_sum_kernel(const float* __restrict__ part, int R,
+                                                              int T, int lq, float* __restrict__ logits) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long long)R * T) return;
+    const int row = (int)(i / T), t = (int)(i - (long long)row * T);
+    float s = part[i];
+#pragma unroll
+    for (int g = 1; g < NGV; ++g) s += part[(size_t)g * R * T + i];
+    long long at = i;
+    if (lq > 0) {
+        const int lb = row / lq, q = row - lb * lq;
+        at = ((long long)lb * T + t) * lq + q;
+    }
+    logits[at] = s;
 }
 
 struct HeadsOutBwdArgs {
@@ -250,73 +238,60 @@ struct HeadsOutBwdArgs {
     long long lddz;
 };
 
-// 320 threads: thread (c4 = tid % 160, half = tid / 160) owns 4 visual columns of 16 rows,
-// its text columns in registers (TMAX float4, zero past T), the rows' logit gradients read
-// from LDS four classes at a time (broadcast); the box heads' part on every thread
-constexpr int BT = 320;
+// Column groups as in the forward: NGV workgroups per 32-row block for the visual gradient
+// (thread: 4 of the group's 128 columns x 4 rows, its text columns in registers, the rows'
+// logit gradients from LDS, broadcast), one per box head (its output gradient in bf16 and its
+// input gradient, weights from LDS).
 template <int TMAX>
-__global__ void __launch_bounds__(BT) heads_out_bwd_kernel(HeadsOutBwdArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    float* gl = smem;                                  // (32 rows, TMAX), zero past T
-    float* gsS = gl + RB * TMAX;                       // (32 rows, MAXS * 32) bf16-rounded
-    bf16* wS = reinterpret_cast<bf16*>(gsS + RB * MAXS * 32);   // box heads' weights (Ns, 256)
+__global__ void __launch_bounds__(256) heads_out_bwd_kernel(HeadsOutBwdArgs a) {
+    __shared__ float gl[RB * TMAX];                  // (32 rows, TMAX), zero past T
+    __shared__ float gsS[RB * 32];                   // the head's bf16-rounded output gradients
+    __shared__ __attribute__((aligned(16))) bf16 wS[32 * KH];   // the head's weights (n, 256)
     const int tid = threadIdx.x;
     const int row0 = blockIdx.x * RB;
     const int nrows = min(RB, a.R - row0);
-    const bool align = a.glog != nullptr;
-    const int c4 = tid % (NV / 4), half = tid / (NV / 4);
-    float4 tx[TMAX];
+    const int grp = blockIdx.y;
+    if (grp < NGV) {
+        const bool align = a.glog != nullptr;
+        const int c4 = tid & 31, rq = tid >> 5;
+        const int col = grp * 128 + 4 * c4;
+        float4 tx[TMAX];
 #pragma unroll
-    for (int t = 0; t < TMAX; ++t) {
-        const int tc = t < a.T ? t : 0;
-        const float4 x = align ? *reinterpret_cast<const float4*>(a.text + (size_t)tc * NV + 4 * c4)
-                               : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float z = t < a.T ? 1.f : 0.f;
-        tx[t] = make_float4(x.x * z, x.y * z, x.z * z, x.w * z);
-    }
-    for (int hi = 0; hi < a.ns; ++hi) {    // (n_i, 256) bf16 rows at row ocol[i]
-        const int n8 = pick4(a.n, hi) * KH / 8;
-        for (int i = tid; i < n8; i += BT)
-            reinterpret_cast<float4*>(wS + (size_t)pick4(a.ocol, hi) * KH)[i] =
-                reinterpret_cast<const float4*>(pick4(a.ws, hi))[i];
-    }
-    for (int i = tid; i < RB * TMAX; i += BT) {
-        const int rr = i / TMAX, t = i - rr * TMAX;
-        const int row = row0 + rr;
-        float g = 0.f;
-        if (align && rr < nrows && t < a.T) {
-            long long at;
-            if (a.lq <= 0) {
-                at = (long long)row * a.T + t;
-            } else {
-                const int lb = row / a.lq, q = row - lb * a.lq;
-                at = ((long long)lb * a.T + t) * a.lq + q;
+        for (int t = 0; t < TMAX; ++t) {
+            const int tc = t < a.T ? t : 0;
+            const float4 x = align ? *reinterpret_cast<const float4*>(a.text + (size_t)tc * NV + col)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float z = t < a.T ? 1.f : 0.f;
+            tx[t] = make_float4(x.x * z, x.y * z, x.z * z, x.w * z);
+        }
+        for (int i = tid; i < RB * TMAX; i += 256) {
+            const int rr = i / TMAX, t = i - rr * TMAX;
+            const int row = row0 + rr;
+            float g = 0.f;
+            if (align && rr < nrows && t < a.T) {
+                long long at;
+                if (a.lq <= 0) {
+                    at = (long long)row * a.T + t;
+                } else {
+                    const int lb = row / a.lq, q = row - lb * a.lq;
+                    at = ((long long)lb * a.T + t) * a.lq + q;
+                }
+                g = a.glog[at];
             }
-            g = a.glog[at];
+            gl[i] = g;
         }
-        gl[i] = g;
-    }
-    for (int i = tid; i < nrows * a.Ns; i += BT) {
-        const int rr = i / a.Ns, j = i - rr * a.Ns;
-        const bf16 v = (bf16)a.gs[(size_t)(row0 + rr) * a.Ns + j];
-        a.gsb[(size_t)(row0 + rr) * a.Ns + j] = v;
-        gsS[rr * (MAXS * 32) + j] = (float)v;
-    }
-    __syncthreads();
-    // visual: g_v + g_logits . text for 16 rows x 4 columns
-    if (half < 2) {
-        // the 16 rows' gradients are loaded up front (clamped rows past R), then combined
-        float4 gvr[RB / 2];
+        float4 gvr[4];   // (gv null: the embedding itself has no consumer, only the logits)
 #pragma unroll
-        for (int k = 0; k < RB / 2; ++k) {
-            const int rr = min(half * (RB / 2) + k, nrows - 1);
-            gvr[k] = *reinterpret_cast<const float4*>(a.gv + (size_t)(row0 + rr) * NV + 4 * c4);
+        for (int k = 0; k < 4; ++k) {
+            const int rr = min(rq * 4 + k, nrows - 1);
+            gvr[k] = a.gv ? *reinterpret_cast<const float4*>(a.gv + (size_t)(row0 + rr) * NV + col)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
         }
+        __syncthreads();
 #pragma unroll
-        for (int k = 0; k < RB / 2; ++k) {
-            const int rr = half * (RB / 2) + k;
+        for (int k = 0; k < 4; ++k) {
+            const int rr = rq * 4 + k;
             if (rr >= nrows) break;
-            const size_t off = (size_t)(row0 + rr) * NV + 4 * c4;
             float4 g = gvr[k];
 #pragma unroll
             for (int t4 = 0; t4 < TMAX / 4; ++t4) {
@@ -336,17 +311,32 @@ __global__ void __launch_bounds__(BT) heads_out_bwd_kernel(HeadsOutBwdArgs a) {
             o[1] = (bf16)g.y;
             o[2] = (bf16)g.z;
             o[3] = (bf16)g.w;
-            *reinterpret_cast<bf16x4*>(a.gvb + off) = o;
+            *reinterpret_cast<bf16x4*>(a.gvb + (size_t)(row0 + rr) * NV + col) = o;
         }
+        return;
     }
-    // box heads' input gradient: 4 columns per item, weights from LDS
-    for (int i = tid; i < nrows * a.ns * (KH / 4); i += BT) {
-        const int cc = i % (KH / 4), hi = (i / (KH / 4)) % a.ns, rr = i / (KH / 4 * a.ns);
+    // box head hi = grp - NGV (one workgroup per head): its output gradient in bf16 and its
+    // input gradient dz[:, kcol + c] = sum_j bf16(g[j]) W[j, c]
+    const int hi = grp - NGV;
+    if (hi >= a.ns) return;
+    const int n = pick4(a.n, hi), oc = pick4(a.ocol, hi);
+    {
+        const int n8 = n * KH / 8;
+        const float4* src = reinterpret_cast<const float4*>(pick4(a.ws, hi));
+        for (int i = tid; i < n8; i += 256) reinterpret_cast<float4*>(wS)[i] = src[i];
+    }
+    for (int i = tid; i < nrows * n; i += 256) {
+        const int rr = i / n, j = i - rr * n;
+        const bf16 v = (bf16)a.gs[(size_t)(row0 + rr) * a.Ns + oc + j];
+        a.gsb[(size_t)(row0 + rr) * a.Ns + oc + j] = v;
+        gsS[rr * 32 + j] = (float)v;
+    }
+    __syncthreads();
+    for (int i = tid; i < nrows * (KH / 4); i += 256) {
+        const int cc = i % (KH / 4), rr = i / (KH / 4);
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
-        const int oc = pick4(a.ocol, hi);
-        const bf16* w = wS + (size_t)oc * KH + 4 * cc;
-        const float* gr = gsS + rr * (MAXS * 32) + oc;
-        const int n = pick4(a.n, hi);
+        const bf16* w = wS + 4 * cc;
+        const float* gr = gsS + rr * 32;
         int j = 0;
         for (; j + 4 <= n; j += 4) {
             bf16x4 wv[4];
@@ -391,9 +381,9 @@ extern "C" int ov3d_heads_out_fwd(const void* z, long long ldz, int R, const voi
                                   int Nv, const float* text, int T, int lq, float* out_v,
                                   float* logits, int ns, const void* const* ws,
                                   const float* const* bs, const int* n, const int* kcol,
-                                  const int* ocol, float* out_s, int Ns, void* stream) {
+                                  const int* ocol, float* out_s, int Ns, float* work, void* stream) {
     if (!z || !wv || !bv || !out_v || !common_ok(R, Nv, text ? T : 0, ns, n) ||
-        (text && (!logits || T <= 0)) || (ns > 0 && (!ws || !bs || !kcol || !ocol || !out_s)))
+        (text && (!logits || T <= 0 || !work)) || (ns > 0 && (!ws || !bs || !kcol || !ocol || !out_s)))
         return OV3D_EINVAL;
     HeadsOutArgs a = {};
     a.z = static_cast<const bf16*>(z);
@@ -421,24 +411,26 @@ extern "C" int ov3d_heads_out_fwd(const void* z, long long ldz, int R, const voi
     a.out_s = out_s;
     a.Ns = Ns;
     const int tm = tmax_of(a.T);
-    const size_t lds = a.T ? ((size_t)tm * Nv + 4 * RB * tm) * sizeof(float) : 0;
-    const void* fn = tm == 8 ? reinterpret_cast<const void*>(heads_out_fwd_kernel<8>)
-                   : tm == 16 ? reinterpret_cast<const void*>(heads_out_fwd_kernel<16>)
-                   : tm == 24 ? reinterpret_cast<const void*>(heads_out_fwd_kernel<24>)
-                              : reinterpret_cast<const void*>(heads_out_fwd_kernel<32>);
-    if (lds > 64 * 1024 &&
-        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-        return OV3D_ELAUNCH;
-    const dim3 grid((unsigned)((R + RB - 1) / RB));
+    const dim3 grid((unsigned)((R + RB - 1) / RB), NGV + 1);
     hipStream_t st = ov3d_stream(stream);
     switch (tm) {
-        case 8: hipLaunchKernelGGL(heads_out_fwd_kernel<8>, grid, dim3(256), lds, st, a); break;
-        case 16: hipLaunchKernelGGL(heads_out_fwd_kernel<16>, grid, dim3(256), lds, st, a); break;
-        case 24: hipLaunchKernelGGL(heads_out_fwd_kernel<24>, grid, dim3(256), lds, st, a); break;
-        default: hipLaunchKernelGGL(heads_out_fwd_kernel<32>, grid, dim3(256), lds, st, a); break;
+        case 8: hipLaunchKernelGGL(heads_out_fwd_kernel<8>, grid, dim3(256), 0, st, a, work); break;
+        case 16: hipLaunchKernelGGL(heads_out_fwd_kernel<16>, grid, dim3(256), 0, st, a, work); break;
+        case 24: hipLaunchKernelGGL(heads_out_fwd_kernel<24>, grid, dim3(256), 0, st, a, work); break;
+        default: hipLaunchKernelGGL(heads_out_fwd_kernel<32>, grid, dim3(256), 0, st, a, work); break;
     }
     OV3D_LAUNCH_CHECK();
+    if (a.T) {
+        hipLaunchKernelGGL(heads_logits_sum_kernel, dim3(ov3d_cdiv((long long)R * a.T, 256)), dim3(256), 0,
+                           st, work, R, a.T, a.lq, logits);
+        OV3D_LAUNCH_CHECK();
+    }
     return OV3D_OK;
+}
+
+/* floats of the forward's workspace (the column groups' partial logits) */
+extern "C" long long ov3d_heads_out_workspace(int R, int T) {
+    return R > 0 && T > 0 ? (long long)NGV * R * T : 0;
 }
 
 extern "C" int ov3d_heads_out_bwd(const float* gv, const float* glog, const float* text, int R, int Nv,
@@ -446,7 +438,7 @@ extern "C" int ov3d_heads_out_bwd(const float* gv, const float* glog, const floa
                                   const void* const* ws, const int* n, const int* kcol,
                                   const int* ocol, void* gvb, void* gsb, void* dz, long long lddz,
                                   void* stream) {
-    if (!gv || !gvb || !common_ok(R, Nv, glog ? T : 0, ns, n) || (glog && (!text || T <= 0)) ||
+    if (!gvb || !common_ok(R, Nv, glog ? T : 0, ns, n) || (glog && (!text || T <= 0)) ||
         (ns > 0 && (!gs || !gsb || !dz || !ws || !kcol || !ocol)) || Ns > MAXS * 32)
         return OV3D_EINVAL;
     HeadsOutBwdArgs a = {};
@@ -473,14 +465,13 @@ extern "C" int ov3d_heads_out_bwd(const float* gv, const float* glog, const floa
     a.dz = static_cast<bf16*>(dz);
     a.lddz = lddz;
     const int tm = tmax_of(a.T);
-    const size_t lds = ((size_t)RB * tm + RB * MAXS * 32) * sizeof(float) + (size_t)a.Ns * KH * sizeof(bf16);
-    const dim3 grid((unsigned)((R + RB - 1) / RB));
+    const dim3 grid((unsigned)((R + RB - 1) / RB), NGV + ns);
     hipStream_t st = ov3d_stream(stream);
     switch (tm) {
-        case 8: hipLaunchKernelGGL(heads_out_bwd_kernel<8>, grid, dim3(BT), lds, st, a); break;
-        case 16: hipLaunchKernelGGL(heads_out_bwd_kernel<16>, grid, dim3(BT), lds, st, a); break;
-        case 24: hipLaunchKernelGGL(heads_out_bwd_kernel<24>, grid, dim3(BT), lds, st, a); break;
-        default: hipLaunchKernelGGL(heads_out_bwd_kernel<32>, grid, dim3(BT), lds, st, a); break;
+        case 8: hipLaunchKernelGGL(heads_out_bwd_kernel<8>, grid, dim3(256), 0, st, a); break;
+        case 16: hipLaunchKernelGGL(heads_out_bwd_kernel<16>, grid, dim3(256), 0, st, a); break;
+        case 24: hipLaunchKernelGGL(heads_out_bwd_kernel<24>, grid, dim3(256), 0, st, a); break;
+        default: hipLaunchKernelGGL(heads_out_bwd_kernel<32>, grid, dim3(256), 0, st, a); break;
     }
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;

@@ -240,10 +240,15 @@ class _Heads(torch.autograd.Function):
         logits = torch.empty((R, T), dtype=torch.float32, device=dev) if text is not None else None
         ws = (ctypes.c_void_p * 4)(*[w.data_ptr() for w in w3[1:]])
         bs = (ctypes.c_void_p * 4)(*[b.data_ptr() for b in b3[1:]])
+        work = torch.empty((max(nat.load().ov3d_heads_out_workspace(R, T), 1),), dtype=torch.float32,
+                           device=dev)
         nat.call("ov3d_heads_out_fwd", z2, H5, R, w3[0], b3[0], Nv, text, T, int(lq), out_v, logits,
                  4, ctypes.addressof(ws), ctypes.addressof(bs), ctypes.addressof(lay["n"]),
-                 ctypes.addressof(lay["kcol"]), ctypes.addressof(lay["ocol"]), out_s, Ns, like=x)
+                 ctypes.addressof(lay["kcol"]), ctypes.addressof(lay["ocol"]), out_s, Ns, work, like=x)
         ctx.save_for_backward(xb, h1, h2, z1, z2, w1, w2, *w3, m1, i1, a1, s1, m2, i2, a2, s2, text)
+        # an output nobody consumed gets no zero-filled gradient (the visual embedding without
+        # the 2D alignment loss: 21 MB of zeros per step)
+        ctx.set_materialize_grads(False)
         ctx.seed = seed   # the forward's dropout snapshot (attention._seed)
         ctx.meta = (pack, float(p1), float(p2), R, x.dtype, int(lq), [w.shape for w in params[-10:-5]])
         if logits is None:
@@ -267,8 +272,9 @@ class _Heads(torch.autograd.Function):
         T = text.shape[0] if text is not None else 0
         # g_v + g_logits . text and the box heads' output gradients in bf16, the box heads'
         # input gradient into dz2[:, H:]: one launch; the visual input gradient on the BLAS
-        gv = gv.contiguous()
-        gs = gs.contiguous()
+        if gv is not None:
+            gv = gv.contiguous()
+        gs = gs.contiguous() if gs is not None else torch.zeros((R, Ns), dtype=torch.float32, device=dev)
         if glog is not None:
             glog = glog.contiguous()
         gvb = torch.empty((R, Nv), dtype=bf, device=dev)

@@ -47,9 +47,10 @@ def test_heads_out_fwd_bwd_match_fp32(cuda, R, T, nb, lq):
     out_v = torch.empty(R, 640, device=cuda)
     out_s = torch.empty(R, Ns, device=cuda)
     logits = torch.empty(R, T, device=cuda)
+    work = torch.empty(nat.load().ov3d_heads_out_workspace(R, T), device=cuda)
     nat.call("ov3d_heads_out_fwd", z, 1280, R, wv, bv, 640, text, T, lq, out_v, logits, 4,
              ctypes.addressof(keep["ws"]), ctypes.addressof(keep["bs"]), ctypes.addressof(keep["n"]),
-             ctypes.addressof(keep["kcol"]), ctypes.addressof(keep["ocol"]), out_s, Ns, like=z)
+             ctypes.addressof(keep["kcol"]), ctypes.addressof(keep["ocol"]), out_s, Ns, work, like=z)
     zf = z.float()
     ref_v = zf[:, :256] @ wv.float().t() + bv
     ref_s = torch.cat([zf[:, 256 * (1 + i):256 * (2 + i)] @ ws[i].float().t() + bs[i] for i in range(4)], 1)
@@ -91,4 +92,4 @@ def test_heads_out_rejects_bad_shapes(cuda):
                  torch.empty(64, 40, device=cuda), 4, ctypes.addressof(keep["ws"]),
                  ctypes.addressof(keep["bs"]), ctypes.addressof(keep["n"]),
                  ctypes.addressof(keep["kcol"]), ctypes.addressof(keep["ocol"]),
-                 torch.empty(64, Ns, device=cuda), Ns, like=z)
+                 torch.empty(64, Ns, device=cuda), Ns, torch.empty(64 * 40 * 5, device=cuda), like=z)

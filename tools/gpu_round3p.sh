@@ -1,0 +1,23 @@
+#!/bin/bash
+# column-parallel heads output kernels: heads / parity / model tests, then every GPU test, bench
+# and a steady-state trace of it
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
+TAG=${TAG:-r03p}
+timeout -k 10 600 python -u -m pytest tests/test_headsout_gpu.py tests/test_heads_gpu.py tests/test_parity_full.py -q -x --timeout 200 --timeout-method thread > $OUT/t_$TAG.log 2>&1
+rc=$?; tail -4 $OUT/t_$TAG.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+rc=$?; tail -3 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python bench.py --steps 30 --warmup 5 --no-cpu-baseline > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { tail -5 $OUT/bench_$TAG.err; exit 1; }
+cut -c1-300 $OUT/bench_$TAG.json
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- \
+    python bench.py --steps 10 --warmup 3 --no-cpu-baseline > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.err || { tail -5 $OUT/prof_$TAG.err; exit 1; }
+f=$(ls $OUT/prof_$TAG/*/run_kernel_trace.csv 2>/dev/null || ls $OUT/prof_$TAG/run_kernel_trace.csv)
+python tools/trace_kernel_avg.py $f "" --steps 8 > $OUT/tr_all_$TAG.json
+python tools/trace_kernel_avg.py $f heads_ > $OUT/tr_heads_$TAG.json
+rm -f $f
+timeout -k 10 300 python tools/gemm_census.py > $OUT/gemm_census.txt 2>&1; grep -v amdgpu $OUT/gemm_census.txt | head -45
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --dp-collectives > $OUT/bench_dp.json 2> $OUT/bench_dp.err || { tail -5 $OUT/bench_dp.err; exit 1; }
+cut -c1-300 $OUT/bench_dp.json
+echo done
