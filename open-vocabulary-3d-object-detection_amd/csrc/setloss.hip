@@ -332,6 +332,260 @@ __global__ void __launch_bounds__(kThreads) set_loss_bwd_kernel(
     }
 }
 
+// ---- 16 lanes per proposal row (the forward split and the backward): the two softmaxes'
+// statistics as lane-parallel reductions, the gradient rows written by consecutive lanes.  One
+// thread per row took 35 us (forward) and 26 us (backward) per SUN step on 32 workgroups: every
+// lane walked its own row serially, every load and store touching 64 rows.
+constexpr int kGrp = 16;                       // lanes per row
+constexpr int kRowsPerWG = kThreads / kGrp;    // 16 rows per workgroup
+constexpr int kGrpMaxN = 2 * kGrp;             // softmax widths served (T, NB)
+constexpr int kTailMaxL = 32;                  // layers the parallel tail serves
+
+// group_softmax_stats == softmax_stats for n <= 32 values spread over the row's 16 lanes (lane
+// j: values j and j + 16): the same maximum and first argmax; the sum in a fixed tree order
+__device__ __forceinline__ void group_softmax_stats(const float* x, int n, int j, float& mx,
+                                                    int& am, float& s) {
+    const float v0 = j < n ? x[j] : -INFINITY;
+    const float v1 = j + kGrp < n ? x[j + kGrp] : -INFINITY;
+    float m = v0;
+    int i = j;
+    if (v1 > m) {
+        m = v1;
+        i = j + kGrp;
+    }
+#pragma unroll
+    for (int o = kGrp / 2; o > 0; o >>= 1) {
+        const float m2 = __shfl_xor(m, o, kGrp);
+        const int i2 = __shfl_xor(i, o, kGrp);
+        if (m2 > m || (m2 == m && i2 < i)) {
+            m = m2;
+            i = i2;
+        }
+    }
+    float e = (j < n ? expf(v0 - m) : 0.f) + (j + kGrp < n ? expf(v1 - m) : 0.f);
+#pragma unroll
+    for (int o = kGrp / 2; o > 0; o >>= 1) e += __shfl_xor(e, o, kGrp);
+    mx = m;
+    am = i;
+    s = e;
+}
+
+// proposal_terms with the two softmaxes over the row's lanes (every lane of the row calls it;
+// lane 0 accumulates)
+__device__ __forceinline__ void proposal_terms_grp(const ov3d_set_loss_desc& d, int l, int p, int P,
+                                                   int j, double* acc, int* cnt) {
+    const int b = p / d.Q;
+    const long long row = (long long)l * P + p;
+    const long long mrow = match_row(d, l, p);
+    const float m = d.matched[mrow];
+    const int g = clampi(d.inds[mrow], d.G - 1);
+    const long long bg = (long long)b * d.G + g;
+    const float* x = d.logits + row * d.ld_logits;
+    float mx, s;
+    int am;
+    group_softmax_stats(x, d.T, j, mx, am, s);
+    const float* a = d.angle_logits + row * d.ld_angle_logits;
+    float ma, sa;
+    int ia;
+    group_softmax_stats(a, d.NB, j, ma, ia, sa);
+    if (j != 0) return;
+    if (am != d.T - 1) atomicAdd(&cnt[b], 1);
+    if (d.flags & OV3D_LOSS_SEM) {
+        const int lab = (m == 0.f) ? d.T - 1 : clampi(d.gt_sem[bg], d.T - 1);
+        const float nll = logf(s) - (x[lab] - mx);
+        const float wt = d.cls_weights[lab];
+        acc[0] += (double)(nll * wt);
+        acc[1] += (double)wt;
+    }
+    {
+        const int gl = clampi(d.gt_angle_cls[bg], d.NB - 1);
+        acc[2] += (double)((logf(sa) - (a[gl] - ma)) * m);
+        const float gr = d.gt_angle_res[bg] * d.res_scale;
+        const float e = d.angle_res[row * d.ld_angle_res + gl] - gr;
+        acc[3] += (double)(huber(e) * m);
+    }
+    if (d.flags & OV3D_LOSS_CENTER) {
+        const float* c = d.center + row * d.ld_center;
+        const float* gc = d.gt_center + bg * 3;
+        const float cl = (fabsf(c[0] - gc[0]) + fabsf(c[1] - gc[1])) + fabsf(c[2] - gc[2]);
+        acc[4] += (double)(cl * m);
+    }
+    if (d.flags & OV3D_LOSS_SIZE) {
+        const float* z = d.size + row * d.ld_size;
+        const float* gz = d.gt_size + bg * 3;
+        const float sl = (fabsf(z[0] - gz[0]) + fabsf(z[1] - gz[1])) + fabsf(z[2] - gz[2]);
+        acc[5] += (double)(sl * m);
+    }
+    if (d.flags & OV3D_LOSS_GIOU) acc[6] += (double)((1.f - d.gious[row * d.G + g]) * m);
+}
+
+// the split forward on 16-row workgroups: chunk partials only.  No last-workgroup ticket: its
+// device-scope fence per workgroup (512 of them) took the launch from 35 to 79 us; the sums
+// and the finalise are a second, one-workgroup launch (set_loss_tail_kernel)
+__global__ void __launch_bounds__(kThreads) set_loss_fwd_grp_kernel(
+    ov3d_set_loss_desc d, double* __restrict__ part) {
+    const int S = gridDim.x, sidx = blockIdx.x, l = blockIdx.y;
+    const int P = d.B * d.Q, W = 7 + d.B;
+    __shared__ int cnt[OV3D_LOSS_MAX_B];
+    __shared__ double gred[kRowsPerWG][7];
+    for (int b = threadIdx.x; b < d.B; b += kThreads) cnt[b] = 0;
+    __syncthreads();
+    double acc[7] = {0, 0, 0, 0, 0, 0, 0};
+    const int j = threadIdx.x & (kGrp - 1);
+    const int p = sidx * kRowsPerWG + threadIdx.x / kGrp;
+    if (p < P) proposal_terms_grp(d, l, p, P, j, acc, cnt);
+    // the groups' sums (lane 0 of each) through LDS, not double wave shuffles
+    if (j == 0) {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) gred[threadIdx.x / kGrp][k] = acc[k];
+    }
+    __syncthreads();
+    double* mine = part + ((size_t)l * S + sidx) * W;
+    if (threadIdx.x < 7) {
+        double t = 0;
+        for (int q = 0; q < kRowsPerWG; ++q) t += gred[q][threadIdx.x];
+        mine[threadIdx.x] = t;
+    }
+    for (int b = threadIdx.x; b < d.B; b += kThreads) mine[7 + b] = (double)cnt[b];
+}
+
+// every (layer, column) summed over the S chunks by one wave (lane c, c + 64, ... then a fixed
+// lane tree: deterministic; a thread per pair walking the chunks serially waited one load
+// round trip per chunk, 34 us); then the per-layer rows and the total (one workgroup, after
+// the partials' launch)
+__global__ void __launch_bounds__(kThreads) set_loss_tail_kernel(
+    ov3d_set_loss_desc d, int S, const double* __restrict__ part, float* raw, float* dict_out,
+    float* total) {
+    const int W = 7 + d.B;
+    __shared__ double tot[kTailMaxL][7 + OV3D_LOSS_MAX_B];
+    // a thread per (layer, column), chunks in chunk order, 16 loads in flight at a time (one
+    // load per chunk step waited a round trip each; a wave tree of double shuffles per pair
+    // was as slow: ~12 ds_bpermute per pair, back to back)
+    const int LW = d.L * W;
+    for (int pc = threadIdx.x; pc < LW; pc += kThreads) {
+        const int ll = pc / W, k = pc - ll * W;
+        const double* pl = part + (size_t)ll * S * W + k;
+        double t = 0;
+        int c = 0;
+        for (; c + 16 <= S; c += 16) {
+            double x[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) x[u] = pl[(size_t)(c + u) * W];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) t += x[u];
+        }
+        for (; c < S; ++c) t += pl[(size_t)c * W];
+        tot[ll][k] = t;
+    }
+    __syncthreads();
+    // the rows in LDS, then every output from there: finalize_total's loads of raw behind its
+    // own stores to dict_out (possible aliases) ran as ~130 serial round trips
+    __shared__ float sraw[kTailMaxL][kRaw];
+    for (int ll = threadIdx.x; ll < d.L; ll += kThreads) {
+        double t[7];
+        for (int k = 0; k < 7; ++k) t[k] = tot[ll][k];
+        float card = 0.f;
+        for (int b = 0; b < d.B; ++b) card += fabsf((float)tot[ll][7 + b] - (float)d.nactual[b]);
+        layer_raw(d, ll, t, card, &sraw[0][0]);
+    }
+    int bad = 0;
+    if (d.match_status)
+        for (int q = threadIdx.x; q < d.n_status; q += kThreads) bad |= d.match_status[q];
+    bad = __syncthreads_or(bad);
+    for (int q = threadIdx.x; q < d.L * kRaw; q += kThreads) raw[q] = (&sraw[0][0])[q];
+    for (int q = threadIdx.x; q < d.L * kCols; q += kThreads) {
+        const int i = q / kCols, k = q - i * kCols;
+        dict_out[q] = sraw[layer_at(d, i)][k] * d.dict_w[k];
+    }
+    if (threadIdx.x != 0) return;
+    float tt = 0.f;   // finalize_total's order
+    for (int i = 0; i < d.L; ++i) {
+        const float* r = sraw[layer_at(d, i)];
+        float ll = 0.f;
+        for (int j = 0; j < d.n_total; ++j) {
+            const int k = d.total_order[j];
+            ll = (j == 0) ? r[k] * d.dict_w[k] : ll + r[k] * d.dict_w[k];
+        }
+        tt = (i == 0) ? ll : tt + ll;
+    }
+    *total = bad ? __int_as_float(0x7fc00000) : tt;   // a refused matching poisons the total
+}
+
+__global__ void __launch_bounds__(kThreads) set_loss_bwd_grp_kernel(
+    ov3d_set_loss_desc d, const float* raw, const float* d_dict, const float* d_total,
+    float* g_logits, float* g_alog, float* g_ares, float* g_center, float* g_size, float* g_gious,
+    float* g_align) {
+    const int P = d.B * d.Q;
+    const int j = threadIdx.x & (kGrp - 1);
+    const long long row = (long long)blockIdx.x * kRowsPerWG + threadIdx.x / kGrp;
+    const float dt = d_total ? *d_total : 0.f;
+    if (blockIdx.x == 0 && threadIdx.x < d.L && g_align) {
+        const int l = threadIdx.x;
+        const float dd = d_dict ? d_dict[dict_pos(d, l) * kCols + 6] : 0.f;
+        g_align[l] = d.dict_w[6] * dd + d.total_w[6] * dt;
+    }
+    if (row >= (long long)d.L * P) return;   // the whole row's group
+    const int l = (int)(row / P);
+    const int b = (int)((row % P) / d.Q);
+    const int i = dict_pos(d, l);
+    float c[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        c[k] = d.dict_w[k] * (d_dict ? d_dict[i * kCols + k] : 0.f) + d.total_w[k] * dt;
+    const float nb = *d.num_boxes;
+    const long long mrow = match_row(d, l, (int)(row % P));
+    const float m = d.matched[mrow];
+    const int g = clampi(d.inds[mrow], d.G - 1);
+    const long long bg = (long long)b * d.G + g;
+    if (g_logits) {
+        const float* x = d.logits + row * d.ld_logits;
+        float* gx = g_logits + row * d.T;
+        float mx, s;
+        int am;
+        group_softmax_stats(x, d.T, j, mx, am, s);
+        const int lab = (m == 0.f) ? d.T - 1 : clampi(d.gt_sem[bg], d.T - 1);
+        const float den = raw[(long long)l * kRaw + 8];
+        const float gn = (c[0] / den) * d.cls_weights[lab];
+        const float inv = 1.f / s;
+        for (int t = j; t < d.T; t += kGrp)
+            gx[t] = gn * (expf(x[t] - mx) * inv - (t == lab ? 1.f : 0.f));
+    }
+    const float* a = d.angle_logits + row * d.ld_angle_logits;
+    const int gl = clampi(d.gt_angle_cls[bg], d.NB - 1);
+    if (g_alog) {
+        float ma, sa;
+        int ia;
+        group_softmax_stats(a, d.NB, j, ma, ia, sa);
+        const float gce = (c[1] / nb) * m;
+        const float inv = 1.f / sa;
+        float* ga = g_alog + row * d.NB;
+        for (int t = j; t < d.NB; t += kGrp)
+            ga[t] = gce * (expf(a[t] - ma) * inv - (t == gl ? 1.f : 0.f));
+    }
+    if (g_ares) {
+        const float gr = d.gt_angle_res[bg] * d.res_scale;
+        const float e = d.angle_res[row * d.ld_angle_res + gl] - gr;
+        const float gh = (c[2] / nb) * m * (sgnf(e) * fminf(fabsf(e), 1.f));
+        float* ga = g_ares + row * d.NB;
+        for (int t = j; t < d.NB; t += kGrp) ga[t] = (t == gl) ? gh : 0.f;
+    }
+    if (g_center && j < 3) {
+        const float* cc = d.center + row * d.ld_center;
+        const float* gc = d.gt_center + bg * 3;
+        g_center[row * 3 + j] = ((c[3] / nb) * m) * sgnf(cc[j] - gc[j]);
+    }
+    if (g_size && j < 3) {
+        const float* z = d.size + row * d.ld_size;
+        const float* gz = d.gt_size + bg * 3;
+        g_size[row * 3 + j] = ((c[4] / nb) * m) * sgnf(z[j] - gz[j]);
+    }
+    if (g_gious) {
+        const float gk = -(c[5] / nb) * m;
+        float* gg = g_gious + row * d.G;
+        for (int t = j; t < d.G; t += kGrp) gg[t] = (t == g) ? gk : 0.f;
+    }
+}
+
 int check_desc(const ov3d_set_loss_desc* d) {
     if (!d || d->L <= 0 || d->B <= 0 || d->Q <= 0 || d->G <= 0 || d->T < 1 || d->NB < 1 ||
         d->B > OV3D_LOSS_MAX_B || !d->logits || !d->angle_logits || !d->angle_res || !d->inds ||
@@ -353,6 +607,11 @@ int check_desc(const ov3d_set_loss_desc* d) {
 
 }  // namespace
 
+// the 16-lanes-per-row kernels serve softmax widths up to 32 and up to 32 layers
+static bool grp_ok(const ov3d_set_loss_desc& d) {
+    return d.T <= kGrpMaxN && d.NB <= kGrpMaxN && d.L <= kTailMaxL;
+}
+
 extern "C" long long ov3d_set_loss_desc_size(void) { return (long long)sizeof(ov3d_set_loss_desc); }
 
 extern "C" int ov3d_set_loss_fwd(const ov3d_set_loss_desc* desc, float* raw, int* ticket,
@@ -367,13 +626,23 @@ extern "C" int ov3d_set_loss_fwd(const ov3d_set_loss_desc* desc, float* raw, int
 /* doubles of scratch ov3d_set_loss_fwd_split needs */
 extern "C" long long ov3d_set_loss_fwd_parts(int L, int B, int Q) {
     if (L <= 0 || B <= 0 || Q <= 0) return 0;
-    return (long long)L * ((B * Q + kThreads - 1) / kThreads) * (7 + B);
+    // the 16-row chunks of the grouped kernel (more than the 256-row chunks of the other)
+    return (long long)L * ((B * Q + kRowsPerWG - 1) / kRowsPerWG) * (7 + B);
 }
 
 extern "C" int ov3d_set_loss_fwd_split(const ov3d_set_loss_desc* desc, float* raw, int* ticket,
                                        float* dict_out, float* total, double* parts, void* stream) {
     if (check_desc(desc) != OV3D_OK || !raw || !ticket || !dict_out || !total || !parts)
         return OV3D_EINVAL;
+    if (grp_ok(*desc)) {
+        const int S = (desc->B * desc->Q + kRowsPerWG - 1) / kRowsPerWG;
+        set_loss_fwd_grp_kernel<<<dim3(S, desc->L), kThreads, 0, ov3d_stream(stream)>>>(*desc, parts);
+        OV3D_LAUNCH_CHECK();
+        set_loss_tail_kernel<<<1, kThreads, 0, ov3d_stream(stream)>>>(*desc, S, parts, raw, dict_out,
+                                                                      total);
+        OV3D_LAUNCH_CHECK();
+        return OV3D_OK;
+    }
     const int S = (desc->B * desc->Q + kThreads - 1) / kThreads;
     set_loss_fwd_split_kernel<<<dim3(S, desc->L), kThreads, 0, ov3d_stream(stream)>>>(
         *desc, raw, ticket, dict_out, total, parts);
@@ -392,6 +661,13 @@ extern "C" int ov3d_set_loss_bwd(const ov3d_set_loss_desc* desc, const float* ra
         (g_align && !(d.flags & OV3D_LOSS_ALIGN)))
         return OV3D_EINVAL;
     const long long rows = (long long)d.L * d.B * d.Q;
+    if (grp_ok(d)) {
+        set_loss_bwd_grp_kernel<<<ov3d_cdiv(rows, kRowsPerWG), kThreads, 0, ov3d_stream(stream)>>>(
+            d, raw, d_dict, d_total, g_logits, g_angle_logits, g_angle_res, g_center, g_size,
+            g_gious, g_align);
+        OV3D_LAUNCH_CHECK();
+        return OV3D_OK;
+    }
     set_loss_bwd_kernel<<<ov3d_cdiv(rows, kThreads), kThreads, 0, ov3d_stream(stream)>>>(
         d, raw, d_dict, d_total, g_logits, g_angle_logits, g_angle_res, g_center, g_size, g_gious,
         g_align);
