@@ -221,18 +221,19 @@ __global__ void __launch_bounds__(256) rows_bn_bwd_kernel(
                     acc[1][j] = fmaf(dt, (xv[j] - mu[j]) * is[j], acc[1][j]);
                 }
             };
-            // 2 rows' loads in flight per round (latency-bound loop otherwise); row order kept
+            // 4 rows' loads in flight per round (latency-bound loop otherwise: the heads' 1280
+            // channels leave one row per block and step; 2 rows measured 14.9 us); row order kept
             const long long step = (long long)gridDim.x * p.rp;
             long long r = (long long)blockIdx.x * p.rp + p.ph;
-            for (; r + step < R; r += 2 * step) {
-                float xv[2][8], zv[2][8];
+            for (; r + 3 * step < R; r += 4 * step) {
+                float xv[4][8], zv[4][8];
 #pragma unroll
-                for (int u = 0; u < 2; ++u) {
+                for (int u = 0; u < 4; ++u) {
                     load8<T>(x, LX, r + u * step, c, xv[u]);
                     load8<bf16>(dz, LZ, r + u * step, c, zv[u]);
                 }
-                row(r, xv[0], zv[0]);
-                row(r + step, xv[1], zv[1]);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) row(r + u * step, xv[u], zv[u]);
             }
             for (; r < R; r += step) {
                 float xv[8], zv[8];
