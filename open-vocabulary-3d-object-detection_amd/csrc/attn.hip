@@ -1071,10 +1071,13 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
         mc[1] = mn[1];
         __syncthreads();
     }
-    if (!kvalid) return;
-    const int kk = k0 + r;
-    bf16* krow = A.dk + ((size_t)kk * a.B + b) * A.sdk + hh * D;
-    bf16* vrow = A.dv + ((size_t)kk * a.B + b) * A.sdv + hh * D;
+    // dK / dV rows through LDS (the Q / dO tiles are free now): a lane holds 4-dim pieces of its
+    // key's rows, stored directly those are 8-byte writes at a row stride (32 rows per
+    // instruction); staged, the workgroup writes whole 128-byte rows, 16 bytes a lane
+    (void)kvalid;
+    bf16* const sk = &Qs[0][0];   // [128 keys][LDK]
+    bf16* const sv = &Ds[0][0];
+    const int kl = wave * 32 + r;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -1085,9 +1088,21 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
                 wk[j] = (bf16)(dkt[dt][4 * g + j] * (A.scale * a.keep_scale));
                 wv[j] = (bf16)(dvt[dt][4 * g + j] * a.keep_scale);
             }
-            *reinterpret_cast<bf16x4*>(krow + 32 * dt + 8 * g + 4 * h) = wk;
-            *reinterpret_cast<bf16x4*>(vrow + 32 * dt + 8 * g + 4 * h) = wv;
+            *reinterpret_cast<bf16x4*>(sk + kl * LDK + 32 * dt + 8 * g + 4 * h) = wk;
+            *reinterpret_cast<bf16x4*>(sv + kl * LDK + 32 * dt + 8 * g + 4 * h) = wv;
         }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = tid + 256 * i, row = c >> 3, d8 = (c & 7) * 8;   // 128 rows x 8 pieces
+        const int key = bx * 128 + row;
+        if (key < a.Lk) {
+            *reinterpret_cast<bf16x8*>(A.dk + ((size_t)key * a.B + b) * A.sdk + hh * D + d8) =
+                *reinterpret_cast<const bf16x8*>(sk + row * LDK + d8);
+            *reinterpret_cast<bf16x8*>(A.dv + ((size_t)key * a.B + b) * A.sdv + hh * D + d8) =
+                *reinterpret_cast<const bf16x8*>(sv + row * LDK + d8);
+        }
+    }
 }
 
 template <bool DROP, bool MASK>
