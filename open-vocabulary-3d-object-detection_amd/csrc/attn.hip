@@ -292,8 +292,10 @@ __global__ void __launch_bounds__(256) attn_dropgen_kernel(AttnArgs a) {
 // BITS: dropout from the words of attn_dropgen_kernel (read, not hashed, not stored)
 template <bool DROP, bool MASK, bool BITS>
 __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
-    __shared__ __attribute__((aligned(16))) bf16 Ks[2][KB * LDK];
-    __shared__ __attribute__((aligned(16))) bf16 Vs[2][KB * LDK];
+    // K and V tiles in one array: its 36 KB also stage the output rows after the loop
+    __shared__ __attribute__((aligned(16))) bf16 KVs[2][2][KB * LDK];
+    bf16 (*const Ks)[KB * LDK] = KVs[0];
+    bf16 (*const Vs)[KB * LDK] = KVs[1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
     int bx, bh;
@@ -535,17 +537,20 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
         PROBE(6);
     }
     PROBE_END;
-    if (!active) return;
-    if (DROP && !BITS && kend > kbeg) store_drop((kend - 1) & ~(KB - 1));
+    if (active && DROP && !BITS && kend > kbeg) store_drop((kend - 1) & ~(KB - 1));
 #ifdef OV3D_ATTN_VALU_ROWSUM
     const float ltot = l + __shfl_xor(l, 32);
 #else
     const float ltot = lacc[0];
 #endif
     const int q = q0 + r;
+    // The workgroup's 128 output rows go through LDS (free after the loop's last barrier): a
+    // lane holds 4-dim pieces of its query's row, stored directly those are 8 / 16-byte writes
+    // at a row stride (32 rows per instruction); staged, whole rows leave 16 bytes a lane.
+    const int ql = wave * QW + r;
     if (a.nsplit == 1) {
         const float inv = ltot > 0.f ? a.keep_scale / ltot : 0.f;
-        bf16* orow = a.o + ((size_t)q * a.B + b) * a.so + hh * D;
+        bf16* const so = &KVs[0][0][0];   // [128 queries][LDK]
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -553,23 +558,41 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
                 bf16x4 w;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) w[j] = (bf16)(o[dt][4 * g + j] * inv);
-                *reinterpret_cast<bf16x4*>(orow + 32 * dt + 8 * g + 4 * h) = w;
+                *reinterpret_cast<bf16x4*>(so + ql * LDK + 32 * dt + 8 * g + 4 * h) = w;
             }
-        if (h == 0) a.lse[(size_t)bh * a.Lq + q] = m * a.scale2 + log2f(ltot);
+        if (active && h == 0) a.lse[(size_t)bh * a.Lq + q] = m * a.scale2 + log2f(ltot);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int c = tid + 256 * i, row = c >> 3, d8 = (c & 7) * 8;
+            const int qq = bx * (4 * QW) + row;
+            if (qq < a.Lq)
+                *reinterpret_cast<bf16x8*>(a.o + ((size_t)qq * a.B + b) * a.so + hh * D + d8) =
+                    *reinterpret_cast<const bf16x8*>(so + row * LDK + d8);
+        }
     } else {
-        const size_t row = ((size_t)blockIdx.z * gridDim.y + bh) * a.Lq + q;
-        float* po = a.part_o + row * D;
+        constexpr int LDF = D + 4;   // fp32 staging row (272 B)
+        float* const sf = reinterpret_cast<float*>(&KVs[0][0][0]);   // [128 queries][LDF]
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                float4 w = make_float4(o[dt][4 * g] * a.keep_scale, o[dt][4 * g + 1] * a.keep_scale,
-                                       o[dt][4 * g + 2] * a.keep_scale, o[dt][4 * g + 3] * a.keep_scale);
-                *reinterpret_cast<float4*>(po + 32 * dt + 8 * g + 4 * h) = w;
-            }
-        if (h == 0) {
-            a.part_ml[2 * row] = m == -INFINITY ? -INFINITY : m * a.scale2;
-            a.part_ml[2 * row + 1] = ltot;
+            for (int g = 0; g < 4; ++g)
+                *reinterpret_cast<float4*>(sf + ql * LDF + 32 * dt + 8 * g + 4 * h) =
+                    make_float4(o[dt][4 * g] * a.keep_scale, o[dt][4 * g + 1] * a.keep_scale,
+                                o[dt][4 * g + 2] * a.keep_scale, o[dt][4 * g + 3] * a.keep_scale);
+        const size_t rbase = ((size_t)blockIdx.z * gridDim.y + bh) * a.Lq;
+        if (active && h == 0) {
+            a.part_ml[2 * (rbase + q)] = m == -INFINITY ? -INFINITY : m * a.scale2;
+            a.part_ml[2 * (rbase + q) + 1] = ltot;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int c = tid + 256 * i, row = c >> 4, d4 = (c & 15) * 4;
+            const int qq = bx * (4 * QW) + row;
+            if (qq < a.Lq)
+                *reinterpret_cast<float4*>(a.part_o + (rbase + qq) * D + d4) =
+                    *reinterpret_cast<const float4*>(sf + row * LDF + d4);
         }
     }
 }
@@ -649,8 +672,10 @@ struct AttnBwdArgs {
 template <bool DROP, bool MASK, bool RAGGED>
 __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
     const AttnArgs& a = A.f;
-    __shared__ __attribute__((aligned(16))) bf16 Ks[2][KB * LDK];
-    __shared__ __attribute__((aligned(16))) bf16 Vs[2][KB * LDK];
+    // K and V tiles in one array: its 36 KB also stage the dQ rows after the loop
+    __shared__ __attribute__((aligned(16))) bf16 KVs[2][2][KB * LDK];
+    bf16 (*const Ks)[KB * LDK] = KVs[0];
+    bf16 (*const Vs)[KB * LDK] = KVs[1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
     int bx, bh;
@@ -815,18 +840,30 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
         mcur = mnext;
         __syncthreads();
     }
-    if (!active) return;
+    // dQ rows through LDS, whole rows 16 bytes a lane (see attn_fwd_kernel)
+    const int ql = wave * QW + r;
     if (a.nsplit > 1) {   // fp32 partial per key split, summed by attn_dq_combine_kernel
-        float* po = a.part_o + (((size_t)blockIdx.z * gridDim.y + bh) * a.Lq + qi) * D;
+        constexpr int LDF = D + 4;
+        float* const sf = reinterpret_cast<float*>(&KVs[0][0][0]);   // [128 queries][LDF]
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
             for (int g = 0; g < 4; ++g)
-                *reinterpret_cast<float4*>(po + 32 * dt + 8 * g + 4 * h) =
+                *reinterpret_cast<float4*>(sf + ql * LDF + 32 * dt + 8 * g + 4 * h) =
                     make_float4(dqt[dt][4 * g], dqt[dt][4 * g + 1], dqt[dt][4 * g + 2], dqt[dt][4 * g + 3]);
+        __syncthreads();
+        const size_t rbase = ((size_t)blockIdx.z * gridDim.y + bh) * a.Lq;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int c = tid + 256 * i, row = c >> 4, d4 = (c & 15) * 4;
+            const int qq = bx * (4 * QW) + row;
+            if (qq < a.Lq)
+                *reinterpret_cast<float4*>(a.part_o + (rbase + qq) * D + d4) =
+                    *reinterpret_cast<const float4*>(sf + row * LDF + d4);
+        }
         return;
     }
-    bf16* row = A.dq + ((size_t)qi * a.B + b) * A.sdq + hh * D;
+    bf16* const sq = &KVs[0][0][0];   // [128 queries][LDK]
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -834,8 +871,17 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
             bf16x4 w;
 #pragma unroll
             for (int j = 0; j < 4; ++j) w[j] = (bf16)(dqt[dt][4 * g + j] * A.scale);
-            *reinterpret_cast<bf16x4*>(row + 32 * dt + 8 * g + 4 * h) = w;
+            *reinterpret_cast<bf16x4*>(sq + ql * LDK + 32 * dt + 8 * g + 4 * h) = w;
         }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = tid + 256 * i, row = c >> 3, d8 = (c & 7) * 8;
+        const int qq = bx * (4 * QW) + row;
+        if (qq < a.Lq)
+            *reinterpret_cast<bf16x8*>(A.dq + ((size_t)qq * a.B + b) * A.sdq + hh * D + d8) =
+                *reinterpret_cast<const bf16x8*>(sq + row * LDK + d8);
+    }
 }
 
 template <bool DROP, bool MASK, bool RAGGED>
