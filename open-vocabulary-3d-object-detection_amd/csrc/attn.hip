@@ -272,7 +272,11 @@ __global__ void __launch_bounds__(256) attn_dropgen_kernel(AttnArgs a) {
                               drop_key(r, h);
     const short ts = (short)((int)a.thresh - 32768);
     const s16x2 tsig = {ts, ts};
-    for (int kt = 0; kt < a.nkt; ++kt) {
+    // blockIdx.z: a range of the key tiles (more waves in flight than one per 32 queries: the
+    // hash chains and the transpose's swizzles are latency, not issue, at 2 waves per SIMD)
+    const int per = (a.nkt + gridDim.z - 1) / gridDim.z;
+    const int kt1 = min(a.nkt, (int)(blockIdx.z + 1) * per);
+    for (int kt = blockIdx.z * per; kt < kt1; ++kt) {
         const uint32_t hb = qh + (uint32_t)(32 * kt) * kPairMul;
         uint32_t dw = 0;
 #pragma unroll
@@ -1301,6 +1305,7 @@ extern "C" int ov3d_attn_small_bwd(int on) {
 // and saves the forward 21.6 us (82.4 -> 60.8 us, profiles/r03_dropgen_trace.json): hashing
 // beside the MFMAs is cheaper than hashing alone.  OV3D_ATTN_DROPGEN_MIN = the query x key
 // count from which the pre-pass runs (0 = always).
+constexpr int kDropgenSplit = 4;   // key-tile ranges of attn_dropgen_kernel (grid.z)
 static bool dropgen_ahead(int Lq, int Lk) {
     const char* e = getenv("OV3D_ATTN_DROPGEN_MIN");   // read per call: tests flip it
     const long long min_pairs = e ? atoll(e) : -1;
@@ -1380,7 +1385,7 @@ extern "C" int ov3d_attn_fwd_masked(const void* q, const void* k, const void* v,
     // short ones (the decoder) hash in the forward, where one more launch would cost more
     const bool bits = a.thresh && dropgen_ahead(Lq, Lk);
     if (bits) {
-        attn_dropgen_kernel<<<dim3(grid.x, grid.y), 256, 0, st>>>(a);
+        attn_dropgen_kernel<<<dim3(grid.x, grid.y, min(a.nkt, kDropgenSplit)), 256, 0, st>>>(a);
         OV3D_LAUNCH_CHECK();
     }
     if (maskbits) {
