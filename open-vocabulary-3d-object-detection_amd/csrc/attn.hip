@@ -602,6 +602,9 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
 }
 
 // merge split-K partials: one 64-lane wave per (b*H+h, query); lane = d
+// NS: the split count rounded up to a power of two (<= kMaxCombine), the loads clamped to the
+// last split (with NS = 16 for every split count, 8 splits loaded each partial twice)
+template <int NS>
 __global__ void __launch_bounds__(256) attn_combine_kernel(AttnArgs a) {
     const int w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, d = threadIdx.x & 63;
     const int BH = a.B * a.H;
@@ -610,12 +613,12 @@ __global__ void __launch_bounds__(256) attn_combine_kernel(AttnArgs a) {
     const int b = bh / a.H, hh = bh - b * a.H;
     float M = -INFINITY;
     float L = 0.f, acc = 0.f;
-    if (a.nsplit <= kMaxCombine) {
+    if (a.nsplit <= NS) {
         // every split's (m, l, o) is loaded up front: the generic loops below are 2·nsplit
         // dependent global round trips
-        float ms[kMaxCombine], ls[kMaxCombine], os[kMaxCombine];
+        float ms[NS], ls[NS], os[NS];
 #pragma unroll
-        for (int s = 0; s < kMaxCombine; ++s) {   // unpredicated loads (split clamped)
+        for (int s = 0; s < NS; ++s) {   // unpredicated loads (split clamped)
             const int sc = s < a.nsplit ? s : a.nsplit - 1;
             const size_t row = ((size_t)sc * BH + bh) * a.Lq + q;
             ms[s] = a.part_ml[2 * row];
@@ -623,12 +626,12 @@ __global__ void __launch_bounds__(256) attn_combine_kernel(AttnArgs a) {
             os[s] = a.part_o[row * D + d];
         }
 #pragma unroll
-        for (int s = 0; s < kMaxCombine; ++s)
+        for (int s = 0; s < NS; ++s)
             if (s >= a.nsplit) ms[s] = -INFINITY;
 #pragma unroll
-        for (int s = 0; s < kMaxCombine; ++s) M = fmaxf(M, ms[s]);
+        for (int s = 0; s < NS; ++s) M = fmaxf(M, ms[s]);
 #pragma unroll
-        for (int s = 0; s < kMaxCombine; ++s) {
+        for (int s = 0; s < NS; ++s) {
             if (ms[s] == -INFINITY) continue;
             const float wgt = exp2f(ms[s] - M);
             L = fmaf(ls[s], wgt, L);
@@ -1405,7 +1408,11 @@ extern "C" int ov3d_attn_fwd_masked(const void* q, const void* k, const void* v,
     OV3D_LAUNCH_CHECK();
     if (nsplit > 1) {
         const long long waves = (long long)B * H * Lq;
-        attn_combine_kernel<<<ov3d_cdiv(waves * 64, 256), 256, 0, st>>>(a);
+        const int nb = ov3d_cdiv(waves * 64, 256);
+        if (nsplit <= 2) attn_combine_kernel<2><<<nb, 256, 0, st>>>(a);
+        else if (nsplit <= 4) attn_combine_kernel<4><<<nb, 256, 0, st>>>(a);
+        else if (nsplit <= 8) attn_combine_kernel<8><<<nb, 256, 0, st>>>(a);
+        else attn_combine_kernel<kMaxCombine><<<nb, 256, 0, st>>>(a);
         OV3D_LAUNCH_CHECK();
     }
     return OV3D_OK;
