@@ -714,34 +714,42 @@ __global__ void __launch_bounds__(256) targets_prep_kernel(int B, int G, int L,
                                                           int64_t* nact64, int32_t* nact32_rep,
                                                           int64_t* total, float* num_boxes,
                                                           int32_t* rotated) {
-    __shared__ long long cnt[256];
-    __shared__ int rot[256];
+    // a wave per scene (lanes over its boxes: the box flags are 0 / 1, so the float count is
+    // exact in any order), the four waves' totals through LDS.  A thread per scene and one
+    // thread adding 256 LDS slots took 9.9 us.
+    __shared__ long long cnt[4];
+    __shared__ int rot[4];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     long long my = 0;
     int r = 0;
-    for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    for (int b = wave; b < B; b += 4) {
         float s = 0.f;
-        for (int g = 0; g < G; ++g) {
+        int rb = 0;
+        for (int g = lane; g < G; g += 64) {
             s += present[(long long)b * G + g];
-            r |= angles[(long long)b * G + g] > 0.f;
+            rb |= angles[(long long)b * G + g] > 0.f;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            s += __shfl_xor(s, o);
+            rb |= __shfl_xor(rb, o);
         }
         const long long n = (long long)s;
-        nact64[b] = n;
-        for (int l = 0; l < L; ++l) nact32_rep[(long long)l * B + b] = (int32_t)n;
+        if (lane == 0) nact64[b] = n;
+        for (int l = lane; l < L; l += 64) nact32_rep[(long long)l * B + b] = (int32_t)n;
         my += n;
+        r |= rb;
     }
-    cnt[threadIdx.x] = my;
-    rot[threadIdx.x] = r;
+    if (lane == 0) {
+        cnt[wave] = my;
+        rot[wave] = r;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        long long t = 0;
-        int rr = 0;
-        for (int i = 0; i < (int)blockDim.x; ++i) {
-            t += cnt[i];
-            rr |= rot[i];
-        }
+        const long long t = (cnt[0] + cnt[1]) + (cnt[2] + cnt[3]);
         *total = t;
         if (num_boxes) *num_boxes = fmaxf((float)t, 1.f);
-        *rotated = rr;
+        *rotated = rot[0] | rot[1] | rot[2] | rot[3];
     }
 }
 
