@@ -272,8 +272,8 @@ __global__ void __launch_bounds__(256) attn_dropgen_kernel(AttnArgs a) {
                               drop_key(r, h);
     const short ts = (short)((int)a.thresh - 32768);
     const s16x2 tsig = {ts, ts};
-    // blockIdx.z: a range of the key tiles (more waves in flight than one per 32 queries: the
-    // hash chains and the transpose's swizzles are latency, not issue, at 2 waves per SIMD)
+    // blockIdx.z: a range of the key tiles (4x the waves of one per 32 queries; measured 33.5 ->
+    // 30.9 us: the pass sits at its vector-issue bound either way)
     const int per = (a.nkt + gridDim.z - 1) / gridDim.z;
     const int kt1 = min(a.nkt, (int)(blockIdx.z + 1) * per);
     for (int kt = blockIdx.z * per; kt < kt1; ++kt) {
@@ -1039,7 +1039,6 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) dkt[0][i] = dkt[1][i] = dvt[0][i] = dvt[1][i] = 0.f;
     // a lane past the last key holds a copy of the last key's row: finite values, never stored
-    const bool kvalid = active && (k0 + r) < a.Lk;
     load(0);
     store(0);
     uint32_t wc[2] = {wn[0], wn[1]};
@@ -1127,7 +1126,6 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
     // dK / dV rows through LDS (the Q / dO tiles are free now): a lane holds 4-dim pieces of its
     // key's rows, stored directly those are 8-byte writes at a row stride (32 rows per
     // instruction); staged, the workgroup writes whole 128-byte rows, 16 bytes a lane
-    (void)kvalid;
     bf16* const sk = &Qs[0][0];   // [128 keys][LDK]
     bf16* const sv = &Ds[0][0];
     const int kl = wave * 32 + r;
