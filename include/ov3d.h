@@ -560,14 +560,18 @@ int ov3d_targets_prep(int B, int G, int L, const float* present, const float* an
 long long ov3d_set_loss_desc_size(void);   /* sizeof(ov3d_set_loss_desc), for FFI layout checks */
 int ov3d_set_loss_fwd(const ov3d_set_loss_desc* desc, float* raw, int* ticket, float* dict_out,
                       float* total, void* stream);
-/* The same with a workgroup per (256 proposals, layer) (the per-layer launch is
- * latency-bound); parts: ov3d_set_loss_fwd_parts(L, B, Q) doubles of scratch.  The chunk sums
- * are added in chunk order: deterministic, equal to the per-layer form up to fp64 rounding. */
+/* The same split over the proposals (the per-layer launch is latency-bound): with T, NB <= 32
+ * and L <= 32, 16 lanes per proposal row on workgroups of 16 rows, then a one-workgroup launch
+ * that adds the chunks and finalises (ticket unused); otherwise a workgroup per (256 proposals,
+ * layer) whose last workgroup finalises.  parts: ov3d_set_loss_fwd_parts(L, B, Q) doubles of
+ * scratch.  The chunk sums are added in chunk order: deterministic, equal to the per-layer form
+ * up to fp64 rounding. */
 long long ov3d_set_loss_fwd_parts(int L, int B, int Q);
 int ov3d_set_loss_fwd_split(const ov3d_set_loss_desc* desc, float* raw, int* ticket,
                             float* dict_out, float* total, double* parts, void* stream);
 /* d_dict (L, 8) or NULL, d_total scalar (device) or NULL; every non-NULL gradient is written
- * in full (contiguous (L*B*Q, n), g_gious (L*B, Q, G), g_align (L,)) */
+ * in full (contiguous (L*B*Q, n), g_gious (L*B, Q, G), g_align (L,)); 16 lanes per proposal
+ * row when T, NB <= 32 and L <= 32, else a thread per row */
 int ov3d_set_loss_bwd(const ov3d_set_loss_desc* desc, const float* raw, const float* d_dict,
                       const float* d_total, float* g_logits, float* g_angle_logits,
                       float* g_angle_res, float* g_center, float* g_size, float* g_gious,
