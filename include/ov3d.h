@@ -662,6 +662,11 @@ int ov3d_seed_next(long long* live, long long* snap, void* stream);
  * per 120 (the step graph's static input batch, the flat gradient buffer) */
 int ov3d_multi_copy(int n, const void* const* srcs, void* const* dsts, const long long* bytes,
                     void* stream);
+/* sum = bf16(a + b) in fp32 (a: fp32, or bf16 when a_bf16; b fp32) and, for a fp32, ac = bf16(a)
+ * (NULL: skipped), n elements (n % 8 == 0, 16-byte aligned): the decoder's memory + pos and
+ * memory rows (transformer._MemoryKV) in one pass */
+int ov3d_add_cast_bf16(const void* a, int a_bf16, const float* b, long long n, void* sum, void* ac,
+                       void* stream);
 /* table[i].grad = grads[i] (host array of device pointers) by kernel arguments: graph-safe */
 int ov3d_adamw_set_grads(ov3d_adamw_tensor* table, int ntensors, float* const* grads, void* stream);
 /* hyper: DEVICE (ngroups, 2) f64 table {lr, weight_decay} per parameter group, read by the

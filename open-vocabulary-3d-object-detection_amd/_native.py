@@ -76,6 +76,7 @@ _SIGS = {
     "ov3d_adamw_step": "pppipfpddfpifpp",
     "ov3d_adamw_set_grads": "pipp",
     "ov3d_multi_copy": "ipppp",
+    "ov3d_add_cast_bf16": "piplppp",
     "ov3d_seed_next": "ppp",
     "ov3d_fourier_pe": "piipppiiipp",
     "ov3d_box_param_fwd": "liiiiplpppppppppppppppp",

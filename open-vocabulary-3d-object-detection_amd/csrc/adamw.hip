@@ -209,6 +209,55 @@ extern "C" int ov3d_seed_next(long long* live, long long* snap, void* stream) {
     return OV3D_OK;
 }
 
+// the decoder's shared memory rows: sum = bf16(a + b) (fp32 add, one rounding, as torch.add
+// into a bf16 output; a fp32 or bf16, b fp32) and ac = bf16(a) for a fp32 (NULL: skipped), 8
+// elements a thread (the add was a mixed-type torch launch, the cast another)
+namespace {
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+template <bool ABF16>
+__global__ void __launch_bounds__(256) add_cast_kernel(const void* __restrict__ a,
+                                                       const float* __restrict__ b, long long n8,
+                                                       bf16* __restrict__ sum, bf16* __restrict__ ac) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n8) return;
+    float av[8];
+    if (ABF16) {
+        const bf16x8_t a8 = reinterpret_cast<const bf16x8_t*>(a)[i];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) av[j] = (float)a8[j];
+    } else {
+        const float4 a0 = reinterpret_cast<const float4*>(a)[2 * i];
+        const float4 a1 = reinterpret_cast<const float4*>(a)[2 * i + 1];
+        av[0] = a0.x; av[1] = a0.y; av[2] = a0.z; av[3] = a0.w;
+        av[4] = a1.x; av[5] = a1.y; av[6] = a1.z; av[7] = a1.w;
+    }
+    const float4 b0 = reinterpret_cast<const float4*>(b)[2 * i];
+    const float4 b1 = reinterpret_cast<const float4*>(b)[2 * i + 1];
+    const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    bf16x8_t s8, c8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        s8[j] = (bf16)(av[j] + bv[j]);
+        c8[j] = (bf16)av[j];
+    }
+    reinterpret_cast<bf16x8_t*>(sum)[i] = s8;
+    if (!ABF16 && ac) reinterpret_cast<bf16x8_t*>(ac)[i] = c8;
+}
+}  // namespace
+
+extern "C" int ov3d_add_cast_bf16(const void* a, int a_bf16, const float* b, long long n,
+                                  void* sum, void* ac, void* stream) {
+    if (n < 0 || (n > 0 && (!a || !b || !sum)) || n % 8 ||
+        (((uintptr_t)a | (uintptr_t)b | (uintptr_t)sum | (uintptr_t)ac) % 16))
+        return OV3D_EINVAL;
+    if (n == 0) return OV3D_OK;
+    const unsigned nb = (unsigned)ov3d_cdiv(n / 8, 256);
+    if (a_bf16) add_cast_kernel<true><<<nb, 256, 0, ov3d_stream(stream)>>>(a, b, n / 8, (bf16*)sum, nullptr);
+    else add_cast_kernel<false><<<nb, 256, 0, ov3d_stream(stream)>>>(a, b, n / 8, (bf16*)sum, (bf16*)ac);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
 extern "C" int ov3d_multi_copy(int n, const void* const* srcs, void* const* dsts,
                                const long long* bytes, void* stream) {
     if (n < 0 || (n > 0 && (!srcs || !dsts || !bytes))) return OV3D_EINVAL;

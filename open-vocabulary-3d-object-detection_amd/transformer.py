@@ -109,11 +109,24 @@ class _MemoryKV(torch.autograd.Function):
         ws, bs = params[0::2], params[1::2]
         S, B, C = memory.shape
         bf = torch.bfloat16
-        mem = memory.reshape(S * B, C).to(bf).contiguous()
-        mpos = mem
-        if pos is not None:   # the sum in the inputs' common type, rounded once on the store
+        if (pos is not None and memory.dtype in (torch.float32, bf) and pos.dtype == torch.float32
+                and memory.is_contiguous() and pos.is_contiguous() and pos.shape == memory.shape
+                and memory.numel() % 8 == 0):
+            # bf16(memory + pos) summed in fp32 and rounded once (torch's GPU add into a bf16
+            # output rounded the fp32 pos to bf16 first), and bf16(memory) for fp32 memory, in
+            # one pass over the rows
+            a_bf16 = memory.dtype == bf
+            mem = memory.view(S * B, C) if a_bf16 else torch.empty((S * B, C), dtype=bf,
+                                                                    device=memory.device)
             mpos = torch.empty((S * B, C), dtype=bf, device=memory.device)
-            torch.add(memory, pos, out=mpos.view(S, B, C))
+            _native.call("ov3d_add_cast_bf16", memory, int(a_bf16), pos, memory.numel(), mpos,
+                         None if a_bf16 else mem, like=memory)
+        else:
+            mem = memory.reshape(S * B, C).to(bf).contiguous()
+            mpos = mem
+            if pos is not None:   # the sum in the inputs' common type, rounded once on the store
+                mpos = torch.empty((S * B, C), dtype=bf, device=memory.device)
+                torch.add(memory, pos, out=mpos.view(S, B, C))
         # the K / V row blocks of every layer's bf16 in_proj copy, gathered in one launch
         n = len(ws) * E
         dev = memory.device

@@ -285,3 +285,23 @@ def test_hungarian_invalid_cost_status(cuda):
     assert mask[1].sum().item() == 0 and mask[0].sum().item() == 4
     with pytest.raises(ValueError, match="invalid numeric"):
         check_status(status)
+
+
+def test_add_cast_bf16_equals_torch(cuda):
+    """ov3d_add_cast_bf16: bf16(a + b) and bf16(a) bit for bit as torch.add into a bf16 output
+    and .to(bfloat16) (transformer._MemoryKV's memory + pos / memory rows)."""
+    from ov3d_amd import _native
+    a = torch.randn(2048, 8, 256, device=cuda) * 3
+    b = torch.randn(2048, 8, 256, device=cuda)
+    s = torch.empty(a.shape, dtype=torch.bfloat16, device=cuda)
+    c = torch.empty(a.shape, dtype=torch.bfloat16, device=cuda)
+    _native.call("ov3d_add_cast_bf16", a, 0, b, a.numel(), s, c, like=a)
+    ref = torch.empty(a.shape, dtype=torch.bfloat16, device=cuda)
+    torch.add(a, b, out=ref)
+    assert torch.equal(s, ref)
+    assert torch.equal(c, a.to(torch.bfloat16))
+    # bf16 memory (the step's encoder output), fp32 pos: the sum in fp32, rounded once (torch's
+    # GPU add into a bf16 output rounds the fp32 operand to bf16 first: two roundings)
+    ab = a.to(torch.bfloat16)
+    _native.call("ov3d_add_cast_bf16", ab, 1, b, a.numel(), s, None, like=a)
+    assert torch.equal(s, (ab.float() + b).to(torch.bfloat16))
