@@ -43,6 +43,12 @@ const char* ov3d_version(void);
 int ov3d_fps(const float* xyz, int B, int N, int M, int32_t* idx_out, float* new_xyz_out,
              float* workspace, void* stream);
 long long ov3d_fps_workspace(int B, int N);
+/* Outcome of the last ov3d_fps on `workspace` (same B, N, M): status (B,) int32 on the device,
+ * 1 where the two-workgroup kernel (20480 < N <= 40960, taken only when its 2B workgroups fit
+ * the device at once) lost its partner workgroup -- that scene's new_xyz_out is NaN --, else 0.
+ * Replaces nothing upstream: its FPS has no such path (it prints and exit()s on launch errors). */
+int ov3d_fps_pair_status(const float* workspace, int B, int N, int M, int32_t* status,
+                         void* stream);
 
 /* Max over the S neighbour rows of each centroid (F.max_pool2d(kernel [1, nsample]) in
  * PointnetSAModuleVotes, models/model_3detr.py:353-362, 385-391) on channels-last bf16 rows:
@@ -82,7 +88,7 @@ int ov3d_group_bwd(const float* grad_out, const int32_t* idx, int B, int C, int 
 
 /* Inverse of a ball-query index, for a gather-form grouping backward (no float atomics):
  *   idx (B,M,S) -> offsets (B*N+1) and rows (B*M*S): the rows r = (b*M + m)*S + s with
- *   idx[r] = n are rows[offsets[b*N+n] .. offsets[b*N+n+1]) (in no particular order).
+ *   idx[r] = n are rows[offsets[b*N+n] .. offsets[b*N+n+1]), ascending (deterministic sums).
  *   cnt, cursor: B*N int32 scratch.  (B*N up to ~10^6: the scan is one workgroup.) */
 int ov3d_group_inverse(const int32_t* idx, int B, int N, int M, int S, int32_t* cnt,
                        int32_t* offsets, int32_t* cursor, int32_t* rows, void* stream);

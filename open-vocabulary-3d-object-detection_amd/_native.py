@@ -22,6 +22,7 @@ _lib = None
 # name -> argtypes ("p" pointer, "i" int, "l" long long, "f" float, "d" double)
 _SIGS = {
     "ov3d_fps": "piiipppp",
+    "ov3d_fps_pair_status": "piiipp",
     "ov3d_ball_query": "ppiiifipp",
     "ov3d_group_fwd": "ppplllpiiiiifipp",
     "ov3d_group_bwd": "ppiiiiilllpp",

@@ -577,6 +577,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     } else {
         constexpr int LDF = D + 4;   // fp32 staging row (272 B)
         float* const sf = reinterpret_cast<float*>(&KVs[0][0][0]);   // [128 queries][LDF]
+        static_assert(sizeof(KVs) >= 128 * LDF * sizeof(float), "fp32 staging rows overrun KVs");
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -852,6 +853,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
     if (a.nsplit > 1) {   // fp32 partial per key split, summed by attn_dq_combine_kernel
         constexpr int LDF = D + 4;
         float* const sf = reinterpret_cast<float*>(&KVs[0][0][0]);   // [128 queries][LDF]
+        static_assert(sizeof(KVs) >= 128 * LDF * sizeof(float), "fp32 staging rows overrun KVs");
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt)
 #pragma unroll

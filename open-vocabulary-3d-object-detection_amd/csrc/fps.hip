@@ -894,7 +894,14 @@ __global__ __launch_bounds__(kThreads) void fps_stream_kernel(const float* __res
 // iteration << 16 | point index) moved by two 16-byte accesses; each granule is read untorn and
 // checked against its tag, so no fences are needed.
 // The exchange slots are zeroed by the host before each launch (tag 0 is never used).
-constexpr int kPairSpin = 1 << 26;   // polls before giving up (a hung partner: garbage, not a hang)
+// polls before giving up on the partner.  A partner that never answers (it was not co-resident:
+// the host only picks this kernel when 2B workgroups fit the device, fps_pair_fits) would
+// otherwise hang the launch; after the limit the half carries on alone, records `lost` in its
+// hand-shake line, and fps_pair_lost_kernel (launched right after) poisons the scene's sampled
+// coordinates with NaN and reports it through ov3d_fps_pair_status: a wrong sample never
+// passes silently.  OV3D_FPS_PAIR_SPIN overrides the limit (tests force the path with a small
+// limit and OV3D_FPS_PAIR_SILENT=1, which makes half 1 return at once).
+constexpr int kPairSpin = 1 << 26;
 
 __device__ __forceinline__ unsigned long long xword(uint32_t v, uint32_t tag) {
     return ((unsigned long long)tag << 32) | v;
@@ -932,7 +939,8 @@ __global__ __launch_bounds__(kThreads) void fps_pair_kernel(const float* __restr
                                                             unsigned long long* __restrict__ xch,
                                                             int32_t* __restrict__ idx,
                                                             float* __restrict__ new_xyz,
-                                                            int force_mem) {
+                                                            int force_mem, int spin_limit,
+                                                            int silent_half1) {
     constexpr int PW = PPT * 64;
     constexpr int NSORT = 2 * PPT;   // setup slots per thread (the whole scene)
     __shared__ uint32_t s_hist[kCells];
@@ -945,6 +953,7 @@ __global__ __launch_bounds__(kThreads) void fps_pair_kernel(const float* __restr
 
     const int b = blockIdx.x % B;
     const int half = blockIdx.x / B;
+    if (silent_half1 && half) return;   // test hook: a partner that never answers
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int w = tid >> 6;
@@ -967,7 +976,7 @@ __global__ __launch_bounds__(kThreads) void fps_pair_kernel(const float* __restr
         const u32x4 hv = {xcc, 1u, 0u, 1u};
         store_x4(hs_mine, hv, true);
         int through = 1;   // partner silent (spin limit): the memory path
-        for (int spin = 0; spin < kPairSpin; ++spin) {
+        for (int spin = 0; spin < spin_limit; ++spin) {
             const u32x4 o = load_sc1_x4(hs_other);
             if (o[1] == 1u) { through = o[0] != xcc || force_mem; break; }
         }
@@ -989,7 +998,7 @@ __global__ __launch_bounds__(kThreads) void fps_pair_kernel(const float* __restr
     if (tid == 0) {
         int have = 0;
         if (half)
-            for (int spin = 0; spin < kPairSpin; ++spin)
+            for (int spin = 0; spin < spin_limit; ++spin)
                 if (load_sc1_x4(pflag)[0] == 1u) { have = 1; break; }
         s_have = have;
     }
@@ -1215,7 +1224,7 @@ __global__ __launch_bounds__(kThreads) void fps_pair_kernel(const float* __restr
         uint32_t ot = 0u;
         if (lane == 0 && !lost) {
             const unsigned long long* const os = other + 8 * buf;
-            for (int spin = 0; spin < kPairSpin; ++spin) {
+            for (int spin = 0; spin < spin_limit; ++spin) {
                 const u32x4x2 g = load_sc1_x4x2(os);
                 const uint32_t t0 = g.a[1];
                 ov[0] = g.a[0]; ov[1] = t0 & 0xffffu; ov[2] = g.a[2]; ov[3] = g.b[0]; ov[4] = g.b[2];
@@ -1249,7 +1258,8 @@ __global__ __launch_bounds__(kThreads) void fps_pair_kernel(const float* __restr
         if (tid == 0) s_out[j] = (uint16_t)pk;
     }
     __syncthreads();
-    if (tid == 0) store_x4(hs_mine + 4, (u32x4){(uint32_t)lost, 3u, 0u, 3u}, true);   // diagnostics
+    // the outcome, read by fps_pair_lost_kernel (poison + status) and the stress tool
+    if (tid == 0) store_x4(hs_mine + 4, (u32x4){(uint32_t)lost, 3u, 0u, 3u}, true);
     if (half) return;
     idx += (size_t)b * M;
     if (new_xyz) new_xyz += (size_t)b * M * 3;
@@ -1263,6 +1273,54 @@ __global__ __launch_bounds__(kThreads) void fps_pair_kernel(const float* __restr
             new_xyz[3 * j + 2] = p[3 * k + 2];
         }
     }
+}
+
+// one thread per scene, after fps_pair_kernel: a scene whose halves did not complete every
+// exchange (either half's `lost`, or a half that never reported: a zero tag) gets NaN sampled
+// coordinates (the forward's loss turns NaN, also inside a captured graph) and status 1
+__global__ void fps_pair_lost_kernel(const unsigned long long* __restrict__ xch, int B, int M,
+                                     float* __restrict__ new_xyz, int32_t* __restrict__ status) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    int bad = 0;
+    for (int half = 0; half < 2; ++half) {
+        const u32x4 o = load_sc1_x4(xch + (size_t)B * 32 + ((size_t)b * 2 + half) * 16 + 4);
+        bad |= o[1] != 3u || o[0] != 0u;
+    }
+    if (status) status[b] = bad;
+    if (bad && new_xyz)
+        for (int j = 0; j < 3 * M; ++j) new_xyz[(size_t)b * M * 3 + j] = __int_as_float(0x7fc00000);
+}
+
+// 2B workgroups of the pair kernel must be resident at once (each half spins on its partner):
+// one 1024-thread workgroup per CU (its LDS), so 2B <= CUs x occupancy
+template <int PPT>
+bool fps_pair_fits(int B) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return false;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fps_pair_kernel<PPT>, kThreads, 0) !=
+        hipSuccess)
+        return false;
+    return 2LL * B <= (long long)cus * per;
+}
+
+int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e && *e ? atoi(e) : dflt;
+}
+
+template <int PPT>
+int launch_pair(const float* xyz, int B, int N, int M, int L, unsigned long long* xch, int32_t* idx,
+                float* nx, int force_mem, hipStream_t s) {
+    const int spin = env_int("OV3D_FPS_PAIR_SPIN", kPairSpin);
+    const int silent = env_int("OV3D_FPS_PAIR_SILENT", 0);
+    hipLaunchKernelGGL(fps_pair_kernel<PPT>, dim3(2 * B), dim3(kThreads), 0, s, xyz, B, N, M, L,
+                       xch, idx, nx, force_mem, spin > 0 ? spin : 1, silent);
+    hipLaunchKernelGGL(fps_pair_lost_kernel, dim3(ov3d_cdiv(B, 64)), dim3(64), 0, s, xch, B, M, nx,
+                       nullptr);
+    return OV3D_OK;
 }
 
 #ifdef OV3D_FPS_PROBE
@@ -1286,6 +1344,15 @@ void launch_cull(const float* xyz, int B, int N, int M, int L, int32_t* idx, flo
                        OV3D_FPS_PROBE_ARG);
 }
 
+int pair_ppt(int N) { return ((N + 1) / 2 + kThreads - 1) / kThreads; }
+
+// the pair kernel's range (20480 < N <= 40960) at a B whose 2B workgroups are co-resident
+bool fps_pair_path(int B, int N) {
+    if (N <= kThreads * kMaxPPT || N > 2 * kThreads * kMaxPPT) return false;
+    const int p = pair_ppt(N);
+    return p <= 12 ? fps_pair_fits<12>(B) : p <= 16 ? fps_pair_fits<16>(B) : fps_pair_fits<20>(B);
+}
+
 }  // namespace
 
 extern "C" int ov3d_fps(const float* xyz, int B, int N, int M, int32_t* idx_out,
@@ -1305,7 +1372,8 @@ extern "C" int ov3d_fps(const float* xyz, int B, int N, int M, int32_t* idx_out,
         else if (ppt <= 12) launch_cull<12>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
         else if (ppt <= 16) launch_cull<16>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
         else launch_cull<20>(xyz, B, N, M, L, idx_out, new_xyz_out, s);
-    } else if (N <= 2 * kThreads * kMaxPPT && M <= kMaxOutLDS && fps_pair_enabled()) {
+    } else if (N <= 2 * kThreads * kMaxPPT && M <= kMaxOutLDS && fps_pair_enabled() &&
+               fps_pair_path(B, N)) {
         // two workgroups per scene, candidates swapped through L2 (fps_pair_kernel)
         if (!workspace) return OV3D_EINVAL;
         const size_t xbytes = (size_t)B * 2 * 2 * 16 * sizeof(unsigned long long);   // slots + XCC_IDs
@@ -1316,16 +1384,13 @@ extern "C" int ov3d_fps(const float* xyz, int B, int N, int M, int32_t* idx_out,
             const char* e = getenv("OV3D_FPS_XCH");
             return e && e[0] == 'm' ? 1 : 0;
         }();
-        const int half = (N + 1) / 2, ppt2 = (half + kThreads - 1) / kThreads;
+        const int ppt2 = pair_ppt(N);
         if (ppt2 <= 12)
-            hipLaunchKernelGGL(fps_pair_kernel<12>, dim3(2 * B), dim3(kThreads), 0, s, xyz, B, N, M, L,
-                               xch, idx_out, new_xyz_out, force_mem);
+            launch_pair<12>(xyz, B, N, M, L, xch, idx_out, new_xyz_out, force_mem, s);
         else if (ppt2 <= 16)
-            hipLaunchKernelGGL(fps_pair_kernel<16>, dim3(2 * B), dim3(kThreads), 0, s, xyz, B, N, M, L,
-                               xch, idx_out, new_xyz_out, force_mem);
+            launch_pair<16>(xyz, B, N, M, L, xch, idx_out, new_xyz_out, force_mem, s);
         else
-            hipLaunchKernelGGL(fps_pair_kernel<20>, dim3(2 * B), dim3(kThreads), 0, s, xyz, B, N, M, L,
-                               xch, idx_out, new_xyz_out, force_mem);
+            launch_pair<20>(xyz, B, N, M, L, xch, idx_out, new_xyz_out, force_mem, s);
     } else if (N <= kThreads * (kPR + kPS) && M <= kMaxOutLDS) {
         if (!workspace) return OV3D_EINVAL;
         // chunk size of the workspace cluster's culling (OV3D_FPS_CHUNK: measurement knob)
@@ -1356,6 +1421,26 @@ extern "C" int ov3d_fps(const float* xyz, int B, int N, int M, int32_t* idx_out,
 // diagnostic entry (probe build only): dbg = B*16*9 u64 phase counters
 extern "C" void ov3d_fps_probe_set(unsigned long long* dbg) { g_probe_dbg = dbg; }
 #endif
+
+/* per-scene outcome of the last ov3d_fps launch on this workspace: status[b] = 1 when the
+ * two-workgroup kernel's halves lost each other (the scene's new_xyz_out was set to NaN), 0
+ * otherwise (and 0 for every scene when (B, N) did not take the two-workgroup path) */
+extern "C" int ov3d_fps_pair_status(const float* workspace, int B, int N, int M, int32_t* status,
+                                    void* stream) {
+    if (B < 0 || N <= 0 || M < 0 || !status) return OV3D_EINVAL;
+    if (B == 0) return OV3D_OK;
+    hipStream_t s = ov3d_stream(stream);
+    if (M == 0 || M > kMaxOutLDS || !fps_pair_enabled() || !fps_pair_path(B, N)) {
+        if (hipMemsetAsync(status, 0, (size_t)B * sizeof(int32_t), s) != hipSuccess)
+            return OV3D_ELAUNCH;
+        return OV3D_OK;
+    }
+    if (!workspace) return OV3D_EINVAL;
+    hipLaunchKernelGGL(fps_pair_lost_kernel, dim3(ov3d_cdiv(B, 64)), dim3(64), 0, s,
+                       reinterpret_cast<const unsigned long long*>(workspace), B, M, nullptr, status);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
 
 /* workspace floats ov3d_fps needs for (B, N) (16-byte aligned) */
 extern "C" long long ov3d_fps_workspace(int B, int N) {

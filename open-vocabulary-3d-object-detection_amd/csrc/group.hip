@@ -272,6 +272,25 @@ __global__ __launch_bounds__(256) void inv_fill_kernel(const int32_t* __restrict
     rows[pos] = (int32_t)t;
 }
 
+// the fill's atomics hand out slots in an arbitrary order; the backward's fp32 sums follow the
+// list order, so each list is sorted by row id (one thread per list, insertion sort: the lists
+// are short and arrive nearly sorted): the gradient is then the same bit for bit in every run
+__global__ __launch_bounds__(256) void inv_sort_kernel(const int32_t* __restrict__ off, long long n,
+                                                       int32_t* __restrict__ rows) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int e0 = off[i], e1 = off[i + 1];
+    for (int j = e0 + 1; j < e1; ++j) {
+        const int32_t v = rows[j];
+        int k = j - 1;
+        while (k >= e0 && rows[k] > v) {
+            rows[k + 1] = rows[k];
+            --k;
+        }
+        rows[k + 1] = v;
+    }
+}
+
 // gather-form grouping backward: thread per (b, n, c), c fastest (a wave reads 64 channels of
 // one grad row per list entry); every (b, n, c) written (0 when no row refers to n)
 // The same rows as group_fwd_kernel in bf16 with a padded row stride ldo (a multiple of 8,
@@ -370,6 +389,8 @@ extern "C" int ov3d_group_inverse(const int32_t* idx, int B, int N, int M, int S
     if (total > 0)
         hipLaunchKernelGGL(inv_fill_kernel, dim3(ov3d_cdiv(total, 256)), dim3(256), 0, s, idx, N,
                            (long long)M * S, total, cursor, rows);
+    if (total > 0)
+        hipLaunchKernelGGL(inv_sort_kernel, dim3(ov3d_cdiv(n, 256)), dim3(256), 0, s, offsets, n, rows);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

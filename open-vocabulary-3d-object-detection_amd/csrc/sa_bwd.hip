@@ -507,6 +507,7 @@ __global__ __launch_bounds__(512, 1) void sa_dy8_kernel(DyFusedArgs p) {
         // the row-block-1 waves hand their partials to the row-block-0 waves of the same channels
         // (4 channel blocks, 64 lanes, 32) floats = 32 KB: DsT (36.9 KB) holds it, As (17 KB) does not
         float* xs = reinterpret_cast<float*>(DsT);
+        static_assert(sizeof(DsT) >= 4 * 64 * 32 * sizeof(float), "stats hand-off overruns DsT");
         if (rbz == 1)
 #pragma unroll
             for (int i = 0; i < 16; ++i) {

@@ -268,6 +268,7 @@ __device__ __forceinline__ void wgrad_seg256(const WgradArgs& a, int bx, int by,
 
     // column sums: 16 row-threads per 8-column group -> LDS -> 256 values
     float* bred = reinterpret_cast<float*>(L);   // 512 x 8 floats, free after the loop
+    static_assert(4 * STG * sizeof(bf16) >= 512 * 8 * sizeof(float), "column-sum staging overruns the stage images");
     if (do_bias) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) bred[tid * 8 + j] = bsum[j];
@@ -401,6 +402,7 @@ __device__ __forceinline__ void wgrad_body(const WgradArgs& a, int bx, int by, i
 
     // column sums of this split: 16 row-threads per 8-column group -> LDS -> 128 values
     float* bred = reinterpret_cast<float*>(&Xs[0][0]);   // 256 x 8 floats, free after the loop
+    static_assert(sizeof(Xs) >= 256 * 8 * sizeof(float), "column-sum staging overruns Xs");
     if (do_bias) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) bred[tid * 8 + j] = bsum[j];

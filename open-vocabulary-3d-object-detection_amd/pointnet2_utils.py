@@ -29,6 +29,30 @@ def _fps_workspace(B, N, device):
     return torch.empty((n,), dtype=torch.float32, device=device) if n > 0 else None
 
 
+def fps_pair_status(ws, B, N, npoint):
+    """(B,) int32 device tensor: 1 where the two-workgroup FPS (20480 < N <= 40960) lost its
+    partner workgroup on the last ov3d_fps of workspace `ws` (that scene's sampled coordinates
+    are NaN), else 0 (ov3d_fps_pair_status)."""
+    st = torch.empty((B,), dtype=torch.int32, device=ws.device if ws is not None else "cuda")
+    nat.call("ov3d_fps_pair_status", ws, B, N, int(npoint), st, like=st)
+    return st
+
+
+class FPSPairLost(RuntimeError):
+    """the two-workgroup FPS lost its partner workgroup: the sampled indices are wrong"""
+
+
+def _check_pair(ws, B, N, npoint, device):
+    """eager callers: raise on a lost exchange (a host sync; skipped inside graph capture, where
+    the NaN sampled coordinates of furthest_point_sample_gather turn the loss NaN)"""
+    if ws is None or torch.cuda.is_current_stream_capturing():
+        return
+    st = fps_pair_status(ws, B, N, npoint)
+    if bool(st.any()):
+        raise FPSPairLost(f"furthest_point_sample: scenes {st.nonzero().flatten().tolist()} lost "
+                          "their partner workgroup (indices invalid)")
+
+
 class FurthestPointSampling(Function):
     @staticmethod
     def forward(ctx, xyz, npoint):
@@ -37,6 +61,7 @@ class FurthestPointSampling(Function):
         idx = torch.empty((B, npoint), dtype=torch.int32, device=xyz.device)
         ws = _fps_workspace(B, N, xyz.device)
         nat.call("ov3d_fps", xyz, B, N, int(npoint), idx, None, ws, like=xyz)
+        _check_pair(ws, B, N, npoint, xyz.device)
         ctx.mark_non_differentiable(idx)
         return idx
 
@@ -48,10 +73,12 @@ class FurthestPointSampling(Function):
 furthest_point_sample = FurthestPointSampling.apply
 
 
-def furthest_point_sample_gather(xyz, npoint):
+def furthest_point_sample_gather(xyz, npoint, check=False):
     """FPS with the gather fused into the sampling kernel: returns
     (idx int32 (B,npoint), new_xyz (B,npoint,3)).  Equals
-    (furthest_point_sample(xyz, n), gather_operation(xyz^T, idx)^T) bit for bit."""
+    (furthest_point_sample(xyz, n), gather_operation(xyz^T, idx)^T) bit for bit.
+    A scene whose two-workgroup sampling lost its partner gets NaN new_xyz (the step's loss
+    turns NaN, no host sync); check=True raises FPSPairLost eagerly instead."""
     with torch.no_grad():
         xyz = _f32(xyz.detach(), "xyz", 3)
         B, N, _ = xyz.shape
@@ -59,6 +86,8 @@ def furthest_point_sample_gather(xyz, npoint):
         new_xyz = torch.empty((B, npoint, 3), dtype=torch.float32, device=xyz.device)
         ws = _fps_workspace(B, N, xyz.device)
         nat.call("ov3d_fps", xyz, B, N, int(npoint), idx, new_xyz, ws, like=xyz)
+        if check:
+            _check_pair(ws, B, N, npoint, xyz.device)
     return idx, new_xyz
 
 

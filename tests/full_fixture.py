@@ -85,6 +85,23 @@ def torch_bf16_path():
             setattr(m, n, v)
 
 
+def step(name, dataset, device, amp=None):
+    """one training step (forward, criterion, backward) on the fixture -> (loss, loss dict,
+    {parameter: gradient})"""
+    from ov3d_amd.criterion import build_criterion
+    fx = fixture(name)
+    model, cfg, args = build(fx, device, dataset)
+    batch = batch_from_fixture(fx, device)
+    inputs = {k: batch[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")}
+    with torch.autocast("cuda", dtype=amp or torch.float32, enabled=amp is not None):
+        out = model(inputs)
+    crit = pin_matcher(build_criterion(args, cfg).to(device), fx, device)
+    loss, ld = crit(out, dict(batch), clip=FakeRegionCLIP())
+    loss.backward()
+    return loss.detach(), {k: v.detach() for k, v in ld.items()}, \
+        {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
+
+
 def run(name, dataset, device, amp=None, f64=False, grad_floor=None):
     """-> dict of error reports (max relative error per group, worst key)"""
     from ov3d_amd.criterion import build_criterion

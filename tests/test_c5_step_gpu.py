@@ -1,0 +1,96 @@
+"""Config C5 (BASELINE.json configs[4]) at its workload: SUN RGB-D --use_image, the
+RegionCLIP RN50x4 ROI path + the 2D-alignment loss (README.md:13-36, weight 2e-4), B=4 scenes
+x 20000 points, 128 queries, 8 decoder layers, 530x730 images, bf16 -- the step bench.py
+--workload sun_image runs.  Reference: criterion.py:366-398 (projection + clip.inference per
+layer), 432-442 (the 8 layers), main.py:96-105.
+
+* one eager training step (forward, criterion, backward, clip + AdamW): finite loss, the 8
+  loss_2dalignment keys finite and positive, ONE batched ROIAlign for all L*B*Q = 4096 boxes
+  (census), every parameter gradient finite;
+* the batched alignment (backbone once, one ROI batch) equals the reference's per-layer
+  clip.inference loop at this size;
+* the captured step (graphs.StepGraph, as the bench replays it): finite losses over 3 replays.
+RegionCLIP is random-init (no checkpoint offline): PARITY UNPINNED against upstream weights.
+"""
+import pytest
+import torch
+
+from helpers import ov3d  # noqa: F401  (registers ov3d_amd)
+
+pytestmark = pytest.mark.gpu
+
+B, Q, L, NPTS = 4, 128, 8, 20000
+
+
+def _setup(cuda):
+    import bench
+    from ov3d_amd import synthetic
+    wl = bench.WORKLOADS["sun_image"]
+    assert wl["batch"] == B and wl["args"]["loss_2dalignment_weight"] == 2e-4
+    args = bench.default_args(**wl["args"])
+    assert (args.nqueries, args.dec_nlayers) == (Q, L)
+    model, crit, opt = bench.build(args, cuda, capturable=True)
+    clip = bench.build_regionclip(cuda)
+    batches = [synthetic.make_batch(B, seed=40 + i, num_points=NPTS, device=cuda, use_image=True)
+               for i in range(2)]
+    return args, model, crit, opt, clip, batches
+
+
+def test_c5_training_step_full_size(cuda):
+    import bench
+    from ov3d_amd import _native
+    args, model, crit, opt, clip, batches = _setup(cuda)
+    b = batches[0]
+    assert b["image"].shape[0] == B and (b["image_height"] == 530).all() and (b["image_width"] == 730).all()
+    _native.census_start()
+    try:
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model({k: b[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")})
+        loss, ld = crit(out, b, clip=clip)
+        loss.backward()
+        torch.cuda.synchronize()
+    finally:
+        called = _native.census_stop()
+    assert torch.isfinite(loss), loss
+    keys = sorted(k for k in ld if k.startswith("loss_2dalignment"))
+    assert len(keys) == L, keys
+    for k in keys:
+        v = ld[k].item()
+        assert v == v and 0 < v < 1e3, (k, v)
+    assert called.get("ov3d_roi_align_fwd") == 1, called.get("ov3d_roi_align_fwd")
+    assert called.get("ov3d_clip_preprocess") == 1, called.get("ov3d_clip_preprocess")
+    bad = [n for n, p in model.named_parameters() if p.grad is not None and not torch.isfinite(p.grad).all()]
+    assert not bad, bad
+    nparam = sum(1 for p in model.parameters() if p.grad is not None)
+    assert nparam > 150
+    opt.step()
+    assert all(torch.isfinite(p).all() for p in model.parameters())
+
+    # batched (one backbone pass, one ROI batch of 4096) == the reference per-layer loop
+    class PerLayer:   # the reference API only: forces the per-layer clip.inference loop
+        def inference(self, *a, **k):
+            return clip.inference(*a, **k)
+
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        out = model({k: b[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")})
+    with torch.no_grad():
+        _, ld_b = crit(out, b, clip=clip)
+        _, ld_r = crit(out, b, clip=PerLayer())
+    for k in keys:
+        r = ld_r[k].item()
+        # the same bf16 kernels on 512- vs 4096-ROI batches: GEMM tilings differ, fp32 sums
+        assert abs(ld_b[k].item() - r) <= 2e-3 * abs(r), (k, ld_b[k].item(), r)
+
+
+def test_c5_captured_step_full_size(cuda):
+    from ov3d_amd.graphs import StepGraph
+    args, model, crit, opt, clip, batches = _setup(cuda)
+    g = StepGraph(model, crit, opt, batches[0], amp_dtype=torch.bfloat16, clip=args.clip_gradient,
+                  regionclip=clip)
+    losses = []
+    for i in range(3):
+        losses.append(g.step(batches[i % 2], batches[(i + 1) % 2]).clone())
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(x) for x in losses), losses
+    assert all(torch.isfinite(p).all() for p in model.parameters())

@@ -20,6 +20,10 @@ from helpers import ROOT
 
 pytestmark = pytest.mark.gpu
 WORLD = 2
+# "small": reduced sizes; "c2": the per-rank C2/C3 workload (BASELINE.json configs[1-2]: 20000
+# points, 2048 pre-encoder points, 128 queries) at 2 scenes per rank, dropout 0
+CONFIGS = {"small": dict(per_rank=1, points=4096, args=dict(preenc_npoints=512, nqueries=64)),
+           "c2": dict(per_rank=2, points=20000, args=dict(preenc_npoints=2048, nqueries=128))}
 
 
 def _free_port():
@@ -28,7 +32,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _setup():
+def _setup(conf):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -38,25 +42,25 @@ def _setup():
     import ov3d_amd
     from ov3d_amd import synthetic
     from ov3d_amd.dataset_config import SunrgbdDatasetConfig
-    args = default_args(enc_dropout=0.0, dec_dropout=0.0, mlp_dropout=0.0, preenc_npoints=512,
-                        nqueries=64)
+    c = CONFIGS[conf]
+    args = default_args(enc_dropout=0.0, dec_dropout=0.0, mlp_dropout=0.0, **c["args"])
     cfg = SunrgbdDatasetConfig()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     model, _ = ov3d_amd.build_model(args, cfg, text_embedding=synthetic.text_embedding())
     model = model.to(dev).train()
     crit = ov3d_amd.build_criterion(args, cfg).to(dev)
-    batch = synthetic.make_batch(WORLD, seed=12, num_points=4096, device=dev)
-    return model, crit, batch, dev
+    batch = synthetic.make_batch(WORLD * c["per_rank"], seed=12, num_points=c["points"], device=dev)
+    return model, crit, batch, dev, c["per_rank"]
 
 
 def _inputs(b):
     return {k: b[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")}
 
 
-def _slice_outputs(out, r):
+def _slice_outputs(out, r, n):
     def one(d):
-        return {k: v[r: r + 1] for k, v in d.items()}
+        return {k: v[r * n: (r + 1) * n] for k, v in d.items()}
     return {"outputs": one(out["outputs"]), "aux_outputs": [one(a) for a in out["aux_outputs"]]}
 
 
@@ -84,16 +88,16 @@ def _recording(crit, rec):
     crit.matcher.forward = fwd
 
 
-def _rank(rank, port, out_dir):
+def _rank(rank, port, out_dir, conf):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(WORLD), LOCAL_RANK="0")
     torch.distributed.init_process_group("gloo", init_method="env://", world_size=WORLD, rank=rank)
-    model, crit, batch, dev = _setup()
+    model, crit, batch, dev, n = _setup(conf)
     from ov3d_amd import dist as pdist
     pinned = torch.load(os.path.join(out_dir, "match.pt"), weights_only=True)[rank]
     _pin(crit, [t.to(dev) for t in pinned])
     model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
-    b = {k: v[rank: rank + 1] for k, v in batch.items()}
+    b = {k: v[rank * n: (rank + 1) * n] for k, v in batch.items()}
     with torch.autocast("cuda", dtype=torch.bfloat16):
         out = model(_inputs(b))
     loss, _ = crit(out, b)
@@ -108,10 +112,11 @@ def _rank(rank, port, out_dir):
     torch.distributed.destroy_process_group()
 
 
-def test_world2_step_equals_global_batch_step(cuda):
+@pytest.mark.parametrize("conf", sorted(CONFIGS))
+def test_world2_step_equals_global_batch_step(cuda, conf):
     from ov3d_amd import criterion as crit_mod
     from ov3d_amd import dist as pdist
-    model, crit, batch, dev = _setup()
+    model, crit, batch, dev, n = _setup(conf)
     rec = {}
     _recording(crit, rec)
     nbox = batch["gt_box_present"].sum(dim=1)
@@ -125,7 +130,7 @@ def test_world2_step_equals_global_batch_step(cuda):
         model.zero_grad(set_to_none=True)
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
             out = model(_inputs(batch))
-        losses = [crit(_slice_outputs(out, r), {k: v[r: r + 1] for k, v in batch.items()})[0]
+        losses = [crit(_slice_outputs(out, r, n), {k: v[r * n: (r + 1) * n] for k, v in batch.items()})[0]
                   for r in range(WORLD)]
         (sum(losses) / WORLD).backward()
         return [x.item() for x in losses], {n: p.grad.float().cpu().clone()
@@ -142,7 +147,7 @@ def test_world2_step_equals_global_batch_step(cuda):
         crit_mod.all_reduce_average, pdist.all_reduce_average, pdist.get_world_size = saved
     with tempfile.TemporaryDirectory() as d:
         torch.save({r: [t.cpu() for t in rec[r]] for r in range(WORLD)}, os.path.join(d, "match.pt"))
-        mp.spawn(_rank, args=(_free_port(), d), nprocs=WORLD, join=True)
+        mp.spawn(_rank, args=(_free_port(), d, conf), nprocs=WORLD, join=True)
         res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(WORLD)]
     for r in range(WORLD):
         assert abs(res[r]["loss"] - losses[r]) <= 5e-3 * abs(losses[r]), r

@@ -52,6 +52,48 @@ def test_fps_two_workgroup_halves_repeated(cuda, B, N, M):
         np.testing.assert_array_equal(idx.cpu().numpy(), ref)
 
 
+def test_fps_two_workgroup_lost_partner_is_an_error(cuda, monkeypatch):
+    """A partner workgroup that never answers (OV3D_FPS_PAIR_SILENT=1: half 1 returns at once;
+    a small OV3D_FPS_PAIR_SPIN so half 0 gives up in milliseconds): the indices are wrong, so
+    the reference API raises, the fused gather returns NaN coordinates (a captured step's loss
+    turns NaN) and ov3d_fps_pair_status reports every scene.  Without the hook: all zeros."""
+    from ov3d_amd import pointnet2_utils as pu
+    B, N, M = 2, 30000, 64
+    xg = torch.from_numpy(np.random.default_rng(5).uniform(-3, 3, (B, N, 3)).astype(np.float32)).to(cuda)
+    ref = O.fps(xg.cpu().numpy(), M)
+    monkeypatch.setenv("OV3D_FPS_PAIR_SPIN", "2000")
+    monkeypatch.setenv("OV3D_FPS_PAIR_SILENT", "1")
+    with pytest.raises(pu.FPSPairLost):
+        pu.furthest_point_sample(xg, M)
+    _, nx = pu.furthest_point_sample_gather(xg, M)
+    assert torch.isnan(nx).all()
+    with pytest.raises(pu.FPSPairLost):
+        pu.furthest_point_sample_gather(xg, M, check=True)
+    monkeypatch.delenv("OV3D_FPS_PAIR_SILENT")
+    monkeypatch.delenv("OV3D_FPS_PAIR_SPIN")
+    idx, nx = pu.furthest_point_sample_gather(xg, M, check=True)
+    np.testing.assert_array_equal(idx.cpu().numpy(), ref)
+    assert torch.isfinite(nx).all()
+    ws = pu._fps_workspace(B, N, cuda)
+    from ov3d_amd import _native as nat
+    out = torch.empty((B, M), dtype=torch.int32, device=cuda)
+    nat.call("ov3d_fps", xg, B, N, M, out, None, ws, like=xg)
+    assert pu.fps_pair_status(ws, B, N, M).cpu().tolist() == [0] * B
+
+
+def test_fps_two_workgroup_range_beyond_coresidency(cuda):
+    """B above CUs / 2 at 20480 < N <= 40960: the 2B workgroups of the pair kernel cannot all be
+    resident (one per CU), so ov3d_fps takes the one-workgroup two-cluster kernel; indices equal
+    the oracle's, status all zero (the pair kernel used to be chosen regardless)."""
+    from ov3d_amd import pointnet2_utils as pu
+    cus = torch.cuda.get_device_properties(cuda).multi_processor_count
+    B, N, M = cus // 2 + 8, 24000, 32
+    xyz = np.random.default_rng(9).uniform(-3, 3, (B, N, 3)).astype(np.float32)
+    ref = O.fps(xyz, M)
+    idx, nx = pu.furthest_point_sample_gather(torch.from_numpy(xyz).to(cuda), M, check=True)
+    np.testing.assert_array_equal(idx.cpu().numpy(), ref)
+
+
 @pytest.mark.parametrize("N", [700, 5000, 30000])
 def test_fps_ties_and_skipped_points(cuda, N):
     """integer grid -> exact distance ties; origin points -> the |p|^2 <= 1e-3 skip."""
@@ -113,7 +155,9 @@ def test_group_fwd_bwd(cuda, C, gather_bwd, monkeypatch):
 
 
 def test_group_inverse_index(cuda):
-    """ov3d_group_inverse: every row appears exactly once, in the list of the point it reads"""
+    """ov3d_group_inverse: every row appears exactly once, in the list of the point it reads,
+    each list ascending (the fill's atomics order is undone: the gather-form backward's fp32
+    sums are then identical in every run) -- i.e. exactly a stable argsort by point"""
     from ov3d_amd import pointnet2_utils as pu
     B, N, M, S = 3, 500, 64, 16
     idx = torch.randint(0, N, (B, M, S), device=cuda, dtype=torch.int32)
@@ -125,6 +169,10 @@ def test_group_inverse_index(cuda):
     for bn in range(B * N):
         r = rows[off[bn]:off[bn + 1]]
         assert np.all(idx[r] == bn % N) and np.all(r // (M * S) == bn // N)
+    key = np.repeat(np.arange(B), M * S) * N + idx
+    np.testing.assert_array_equal(rows, np.argsort(key, kind="stable"))
+    off2, rows2 = pu.group_inverse(torch.from_numpy(idx.reshape(B, M, S)).to(cuda), N)
+    np.testing.assert_array_equal(rows2.cpu().numpy(), rows)
 
 
 def test_gather_fwd_bwd(cuda):

@@ -18,6 +18,9 @@ imports /root/reference/models/model_3detr.py + criterion.py).
   distribution against the same float64 reference is no worse than PyTorch's own bf16
   autocast of the same model (median / 90th percentile within 2x, worst within 2.5x).
 """
+import json
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -25,7 +28,9 @@ import torch
 import full_fixture as F
 from helpers import fixture, ov3d
 
-FLIP_MAX_FRAC = 0.10
+# observed: 0 of 776 (SUN) and 0 of 789 (ScanNet) gradient entries over their bar on the HIP
+# fp32 path (profiles/r04_parity_record.jsonl); the path is deterministic, so none is allowed
+FLIP_MAX_FRAC = 0.0
 FLIP_CAP = 2e-2
 F64_TOL = 1e-6
 
@@ -48,6 +53,15 @@ def test_product_float64_equals_reference_float64(shim, name, ds):
         err, key = F.worst(rep, group)
         # outputs are stored as float32 in the fixture: 1.2e-7 of their max is storage
         assert err <= F64_TOL, (group, key, err)
+
+
+def _record(kind, name, obj):
+    """append a measured figure to the JSON-lines file OV3D_PARITY_RECORD names (the GPU runs
+    whose figures are kept under profiles/)"""
+    path = os.environ.get("OV3D_PARITY_RECORD")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps({"kind": kind, "case": name, **obj}, default=str) + "\n")
 
 
 def _fp32_report(rep, fx):
@@ -73,6 +87,8 @@ def test_fp32_step_matches_float64_reference(cuda, name, ds):
     strict, flips, n = _fp32_report(rep, fx)
     print(f"{name}: {len(flips)} of {n} gradient entries flip-affected; worst:",
           sorted(flips, key=lambda t: -t[2])[:5])
+    _record("fp32_flips", name, {"entries": n, "flip_affected": len(flips),
+                                 "worst": sorted(flips, key=lambda t: -t[2])[:8]})
     assert not strict, strict                          # outputs and losses: 1e-3, no exceptions
     assert len(flips) <= FLIP_MAX_FRAC * n, flips
     assert all(err <= FLIP_CAP for _, _, err, _ in flips), flips
@@ -126,4 +142,23 @@ def test_bf16_step_matches_float64_reference(cuda, name, ds):
                 q[2][0] > max(2.5 * q[2][1], tol[g]):
             bad.append(g)
     print(name, "bf16 hip/torch:\n  " + "\n  ".join(lines))
+    _record("bf16_vs_torch", name, {"lines": lines})
     assert not bad, (bad, lines)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,ds", F.CASES)
+def test_bf16_step_is_deterministic(cuda, name, ds):
+    """The benchmarked bf16 step gives the same loss, loss dict and every parameter gradient bit
+    for bit in two runs.  VERDICT r3 saw the ScanNet bf16 parity cross its bar in one log; that
+    log was the reverted stored-probabilities attention build, and the one
+    run-to-run source on this path was the gather-form grouping backward (the interim SA) summing
+    each point's rows in the order the inverse-index fill's atomics left them -- now sorted
+    (ov3d_group_inverse).  Weight gradients reduce in workgroup order (stream-K slots), the
+    split-K attention partials and the set-loss chunks in index order: no float atomics."""
+    a = F.step(name, ds, cuda, amp=torch.bfloat16)
+    b = F.step(name, ds, cuda, amp=torch.bfloat16)
+    assert torch.equal(a[0], b[0]), (a[0], b[0])
+    assert all(torch.equal(a[1][k], b[1][k]) for k in a[1])
+    diff = [n for n in a[2] if not torch.equal(a[2][n], b[2][n])]
+    assert not diff, diff
