@@ -186,6 +186,85 @@ def attn_launch_timings(B, L, H=4, p=0.1, reps=5):
     return float(np.mean(fwd)), float(np.mean(bwd))
 
 
+def gemm_ceiling(n=8192, reps=10):
+    """measured bf16 GEMM ceiling of this box: hipBLASLt (torch.matmul) n x n x n on random
+    data, HIP events around `reps` back-to-back launches (SURVEY §8d asks for it beside the
+    vendor peak)"""
+    g = torch.Generator(device="cuda").manual_seed(1)
+    a = torch.randn((n, n), device="cuda", dtype=torch.bfloat16, generator=g)
+    b = torch.randn((n, n), device="cuda", dtype=torch.bfloat16, generator=g)
+    for _ in range(3):
+        torch.matmul(a, b)
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    _gpu_busy(1.0)
+    e0.record(st)
+    for _ in range(reps):
+        torch.matmul(a, b)
+    e1.record(st)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    return {"tflops": round(2.0 * n ** 3 / (ms * 1e-3) / 1e12, 1), "shape": f"{n}x{n}x{n} bf16",
+            "ms": round(ms, 4), "how": "torch.matmul (hipBLASLt), random data, HIP events"}
+
+
+def _timed(fn, reps):
+    """HIP events around `reps` back-to-back calls queued behind a spin kernel (kernel time, not
+    host launch gaps) -> ms per call"""
+    fn()
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    _gpu_busy(2.0)
+    e0.record(st)
+    for _ in range(reps):
+        fn()
+    e1.record(st)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def index_kernel_rates(batch, npoint=2048, radius=0.2, nsample=64, L=8, Q=128, reps=5):
+    """Per-kernel HBM figures for the index / geometry kernels (BASELINE.md:62):
+    algorithmic bytes under the streaming formulation / measured time (HIP events, the step's
+    shapes on its batch)."""
+    from ov3d_amd import nms, pointnet2_utils as pu
+    from ov3d_amd.box_util import generalized_box3d_iou
+    xyz = batch["point_clouds"][..., 0:3].contiguous()
+    B, N, _ = xyz.shape
+    _, new_xyz = pu.furthest_point_sample_gather(xyz, npoint)
+    idx = pu.ball_query(radius, nsample, xyz, new_xyz)
+    grouper = pu.QueryAndGroup(radius, nsample, normalize_xyz=True)
+    corners = batch["gt_box_corners"]                                   # (B, G, 8, 3)
+    G = corners.shape[1]
+    g = torch.Generator(device="cuda").manual_seed(3)
+    pred = corners[:, torch.randint(0, G, (Q,), device="cuda", generator=g)]
+    pred = (pred + 0.05 * torch.randn(pred.shape, device="cuda", generator=g)).repeat(L, 1, 1, 1)
+    gt = corners.repeat(L, 1, 1, 1)
+    nums = batch["gt_box_present"].sum(1).int().repeat(L)
+    boxes = nms.nms_boxes_from_corners(pred[:B], torch.rand((B, Q), device="cuda", generator=g),
+                                       torch.randint(0, 10, (B, Q), device="cuda", generator=g))
+    rows = {
+        "ov3d_fps": (lambda: pu.furthest_point_sample_gather(xyz, npoint), B * npoint * N * 16,
+                     f"B={B} N={N} M={npoint}: M*N*16 B per scene (coords + running min, streaming)"),
+        "ov3d_ball_query": (lambda: pu.ball_query(radius, nsample, xyz, new_xyz), B * npoint * N * 12,
+                            f"r={radius} S={nsample}: M*N*12 B per scene (brute-force worst case)"),
+        "ov3d_group_fwd": (lambda: grouper.rows(xyz, new_xyz, None, idx=idx),
+                           B * npoint * nsample * (3 * 4 + 4),
+                           "(B,M,S,3) fp32 rows out + idx in"),
+        "ov3d_giou3d": (lambda: generalized_box3d_iou(pred, gt, nums), L * B * Q * G * (2 * 96 + 4),
+                        f"{L} layers x B x {Q} x {G} pairs x (2*96 + 4) B"),
+        "ov3d_nms3d": (lambda: nms.nms3d_batched(boxes, 0.25), B * Q * Q * 56,
+                       f"B x K^2 x 56 B (K={Q}, fp64 boxes)"),
+    }
+    out = {}
+    for name, (fn, nbytes, what) in rows.items():
+        ms = _timed(fn, reps)
+        out[name] = {"ms": round(ms, 4), "alg_bytes": nbytes, "GBps": round(nbytes / (ms * 1e-3) / 1e9, 1),
+                     "frac_hbm": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "bytes": what}
+    return out
+
+
 def fps_latency_floor(B, M, reps=3):
     """FPS iteration cost with one point per thread (N = M): what the per-iteration barrier /
     reduction / LDS chain costs with (almost) no distance work -- the kernel's latency floor"""
@@ -204,11 +283,13 @@ def fps_latency_floor(B, M, reps=3):
     return float(np.mean(ts))
 
 
-def cpu_baseline(args, samples=((1, 2), (8, 1))):
+def cpu_baseline(args, samples=((1, 5), (8, 1)), anomaly=(1, 2)):
     """The reference step on the host cores: product host code on CPU with the
     C oracle for FPS / ball query / grouping / GIoU (test-infrastructure
     injection, oracle/torch_shim.py), fp32, bounded samples: (batch, steps) pairs, B=1
-    (config C1) and B=8 (the GPU workload's batch), after one B=1 warm-up step."""
+    (config C1, value = scenes / median step time, BASELINE.md:58-60) and B=8 (the GPU
+    workload's batch), after one B=1 warm-up step; plus `anomaly` = (batch, steps) with
+    torch.autograd anomaly detection on, the reference's default (main.py:499, quirk Q7)."""
     from oracle import torch_shim
     ov3d = ov3d_import.load()
     from ov3d_amd import synthetic
@@ -235,20 +316,30 @@ def cpu_baseline(args, samples=((1, 2), (8, 1))):
 
         step(synthetic.make_batch(1, seed=99))  # warm-up
         rates = {}
-        for bs, steps in samples:
-            batches = [synthetic.make_batch(bs, seed=100 + i) for i in range(steps)]
-            t0 = time.perf_counter()
-            for b in batches:
+
+        def timed(bs, steps, seed0):
+            ts = []
+            for i in range(steps):
+                b = synthetic.make_batch(bs, seed=seed0 + i)
+                t0 = time.perf_counter()
                 step(b)
-            rates[bs] = (bs * steps / (time.perf_counter() - t0), steps)
+                ts.append(time.perf_counter() - t0)
+            return bs / float(np.median(ts)), steps, [round(t, 3) for t in ts]
+
+        for bs, steps in samples:
+            rates[f"B={bs}"] = timed(bs, steps, 100)
+        if anomaly:
+            with torch.autograd.detect_anomaly(check_nan=True):
+                rates[f"B={anomaly[0]} anomaly"] = timed(anomaly[0], anomaly[1], 200)
     finally:
         torch_shim.uninstall(saved)
-    b0 = samples[0][0]
+    b0 = f"B={samples[0][0]}"
     return {"value": round(rates[b0][0], 4), "unit": "scenes/s", "cores": threads, "kind": "port",
-            "by_batch": {f"B={b}": {"value": round(r, 4), "steps": n} for b, (r, n) in rates.items()},
-            "sample": "; ".join(f"{n} train step(s) x B={b}" for b, (_, n) in rates.items())
+            "by_batch": {k: {"value": round(r, 4), "steps": n, "step_s": ts} for k, (r, n, ts) in rates.items()},
+            "sample": "; ".join(f"{n} train step(s) x {k}" for k, (_, n, _) in rates.items())
                       + " of 20000-pt scenes, fp32, oracle C for FPS/ball-query/grouping/GIoU + "
-                        "PyTorch-CPU dense layers (value: B=%d)" % b0}
+                        "PyTorch-CPU dense layers (value: %s, scenes / median step time; anomaly: "
+                        "torch.autograd.detect_anomaly, the reference default main.py:499)" % b0}
 
 
 def main():
@@ -328,10 +419,18 @@ def main():
             for i in range(cli.pool)]
 
     graphed = None
+    stamp_buf = None
     if use_graph:
         from ov3d_amd.graphs import StepGraph
-        graphed = StepGraph(model, crit, opt, pool[0], amp_dtype=amp, clip=args.clip_gradient,
-                            prefetch_fps=not cli.no_prefetch, regionclip=clip)
+        # the encoder attention launches captured into the step carry in-kernel wall-clock
+        # stamps (csrc/common.h ov3d_stamp): the roofline kernel is timed inside the step
+        stamp_buf = torch.zeros((1 << 21,), dtype=torch.int64, device=device)
+        _native.stamps_arm(stamp_buf, min_work=1 << 20)
+        try:
+            graphed = StepGraph(model, crit, opt, pool[0], amp_dtype=amp, clip=args.clip_gradient,
+                                prefetch_fps=not cli.no_prefetch, regionclip=clip)
+        finally:
+            _native.stamps_arm(None)
 
     def step(i):
         if graphed is not None:
@@ -356,11 +455,25 @@ def main():
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
+    # in-step kernel times: the last timed step's captured launches, then 5 more replays
+    stamped = []
+    if stamp_buf is not None:
+        stamped.append(_native.stamps_read(stamp_buf))
+        for i in range(5):
+            stamp_buf.zero_()
+            step(cli.steps + i)
+            torch.cuda.synchronize()
+            stamped.append(_native.stamps_read(stamp_buf))
     timings = _native.timing_collect() if graphed is None else fps_launch_timings(pool, cli)
     att = None
-    if rank == 0 and dataset == "sunrgbd":
+    rates = gemm_ref = None
+    if rank == 0 and dataset in ("sunrgbd", "scannet"):
         att = attn_launch_timings(cli.batch, args.preenc_npoints, args.enc_nhead, args.enc_dropout)
         fps_floor_ms = fps_latency_floor(cli.batch, args.preenc_npoints)
+        gemm_ref = gemm_ceiling()
+        if dataset == "sunrgbd":
+            rates = index_kernel_rates(pool[0], npoint=args.preenc_npoints, Q=args.nqueries,
+                                       L=args.dec_nlayers)
     el = torch.tensor([elapsed], device=device, dtype=torch.float64)
     if world > 1:
         torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
@@ -383,23 +496,50 @@ def main():
         L, H, d = args.preenc_npoints, args.enc_nhead, 64
         fwd_ms, bwd_ms = att
         fl_fwd = 4.0 * L * L * d * cli.batch * H
-        ach = fl_fwd / (fwd_ms * 1e-3) / 1e12
+        # in-step launch times (stamps): the encoder layers at L (C4: the first masked layer;
+        # its interim layers run at L/2 and are not averaged in)
+        per = {k: [] for k in _native.STAMP_KINDS}
+        for rec in stamped:
+            for k, ms, work in rec:
+                if work == L * L:
+                    per[k].append(ms)
+        in_step = {k: float(np.mean(v)) for k, v in per.items() if v}
+        fwd_in = in_step.get("fwd")
+        use_ms = fwd_in if fwd_in else fwd_ms
+        ach = fl_fwd / (use_ms * 1e-3) / 1e12
         traffic, tsrc = None, None
         pmc = os.path.join(ROOT, "profiles", "r03_attn_pmc.json")
-        if os.path.exists(pmc) and (cli.batch, L, H) == (8, 2048, 4):
+        if os.path.exists(pmc) and (cli.batch, L, H) == (8, 2048, 4) and dataset == "sunrgbd":
             traffic = json.load(open(pmc)).get("fwd_traffic_bytes_per_launch")
             tsrc = "profiles/r03_attn_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)"
+        kname = "attn_fwd_kernel (encoder self-attention, B=%d H=%d L=%d d=64, dropout %.1f%s)" % (
+            cli.batch, H, L, args.enc_dropout, ", radius mask" if dataset == "scannet" else "")
         roof = {"bound": "mfma", "achieved": round(ach, 1), "peak": BF16_DENSE_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(ach / BF16_DENSE_PEAK_TFLOPS, 4),
-                "traffic": traffic, "traffic_source": tsrc,
-                "kernel": "attn_fwd_kernel (encoder self-attention, B=%d H=%d L=%d d=64, dropout %.1f)"
-                          % (cli.batch, H, L, args.enc_dropout),
-                "flop_per_launch": fl_fwd, "avg_launch_ms": round(fwd_ms, 4), "launches": 5}
+                "traffic": traffic, "traffic_source": tsrc, "kernel": kname,
+                "flop_per_launch": fl_fwd, "avg_launch_ms": round(use_ms, 4),
+                "launches": len(per["fwd"]) if fwd_in else 5,
+                "timing": ("in-step: in-kernel wall-clock stamps (first-wave entry to last-wave exit) "
+                           "of the captured step's launches, the last timed step + 5 replays"
+                           if fwd_in else "standalone relaunch after the timed region, HIP events"),
+                "standalone_relaunch_ms": round(fwd_ms, 4)}
+        if gemm_ref:
+            roof["measured_gemm_ceiling_tflops"] = gemm_ref["tflops"]
+            roof["frac_of_measured_gemm"] = round(ach / gemm_ref["tflops"], 4)
+            extra["gemm_ceiling"] = gemm_ref
         fl_bwd = 2.5 * fl_fwd
+        bwd_in = in_step.get("dq", 0.0) + in_step.get("dkdv", 0.0) if "dq" in in_step else None
+        use_b = bwd_in if bwd_in else bwd_ms
         extra["attn_bwd"] = {"kernels": "attn_bwd_dq_kernel + attn_bwd_dkdv_kernel",
-                             "avg_ms": round(bwd_ms, 4), "flop": fl_bwd,
-                             "achieved_tflops": round(fl_bwd / (bwd_ms * 1e-3) / 1e12, 1),
-                             "frac": round(fl_bwd / (bwd_ms * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS, 4)}
+                             "avg_ms": round(use_b, 4), "flop": fl_bwd,
+                             "dq_ms": round(in_step["dq"], 4) if "dq" in in_step else None,
+                             "dkdv_ms": round(in_step["dkdv"], 4) if "dkdv" in in_step else None,
+                             "achieved_tflops": round(fl_bwd / (use_b * 1e-3) / 1e12, 1),
+                             "frac": round(fl_bwd / (use_b * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS, 4),
+                             "timing": "in-step stamps" if bwd_in else "standalone relaunch",
+                             "standalone_relaunch_ms": round(bwd_ms, 4)}
+    if rates:
+        extra["index_kernels_hbm"] = rates
     # FPS (side stream): a serial chain of M - 1 dependent iterations, reported per iteration
     # against the same kernel's cost with one point per thread (its latency floor)
     fps = timings.get("ov3d_fps", [])
@@ -407,7 +547,8 @@ def main():
     if pre and att is not None:
         B, N, M = pre[0]["shape"]
         avg_ms = float(np.mean([t["ms"] for t in pre]))
-        extra["fps"] = {"kernel": "fps_cull_kernel (pre-encoder, B=%d N=%d M=%d, side stream)" % (B, N, M),
+        kern = "fps_cull_kernel" if N <= 20480 else "fps_pair_kernel"
+        extra["fps"] = {"kernel": "%s (pre-encoder, B=%d N=%d M=%d, side stream)" % (kern, B, N, M),
                         "avg_launch_ms": round(avg_ms, 4),
                         "us_per_iteration": round(avg_ms * 1e3 / (M - 1), 4),
                         "floor_us_per_iteration": round(fps_floor_ms * 1e3 / (M - 1), 4),

@@ -843,6 +843,15 @@ int ov3d_ap_curve(const uint8_t* tp_sorted, long long M, const int32_t* nvalid,
                   const int32_t* npos, int C, int32_t* tp_pos, long long tp_cap, double* ap,
                   double* rec_last, void* stream);
 
+/* In-kernel launch stamps (measurement, bench.py): while armed, each encoder-size attention
+ * launch (Lq * Lk >= min_work) of kind 0 forward, 1 dQ, 2 dK/dV takes 2 words per wave of buf
+ * (entry / exit wall clock of each wave, ov3d_wall_clock_khz ticks), recorded in a host table
+ * (kind, word offset, waves, work = Lq * Lk) captured launches keep replaying into.  buf = NULL disarms.  No reference counterpart. */
+int ov3d_stamps_arm(unsigned long long* buf, long long words, long long min_work);
+int ov3d_stamps_count(void);
+int ov3d_stamps_get(int i, int* kind, long long* word_off, long long* waves, long long* work);
+long long ov3d_wall_clock_khz(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -116,7 +116,8 @@ EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_
                           "ov3d_adamw_chunk", "ov3d_wgrad_group_workspace",
                           "ov3d_rows_gemm_supported", "ov3d_sa_dy_fused_supported",
                           "ov3d_tile_gemm_supported", "ov3d_sun_range_parts", "ov3d_heads_out_max_text",
-                          "ov3d_heads_out_workspace")
+                          "ov3d_heads_out_workspace", "ov3d_stamps_arm", "ov3d_stamps_count",
+                          "ov3d_stamps_get", "ov3d_wall_clock_khz")
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_longlong, "f": ctypes.c_float,
        "d": ctypes.c_double}
@@ -149,6 +150,14 @@ def load():
         lib.ov3d_set_loss_fwd_parts.restype = ctypes.c_longlong
         lib.ov3d_fps_workspace.argtypes = [ctypes.c_int] * 2
         lib.ov3d_fps_workspace.restype = ctypes.c_longlong
+        lib.ov3d_stamps_arm.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_longlong]
+        lib.ov3d_stamps_arm.restype = ctypes.c_int
+        lib.ov3d_stamps_count.argtypes = []
+        lib.ov3d_stamps_count.restype = ctypes.c_int
+        lib.ov3d_stamps_get.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4
+        lib.ov3d_stamps_get.restype = ctypes.c_int
+        lib.ov3d_wall_clock_khz.argtypes = []
+        lib.ov3d_wall_clock_khz.restype = ctypes.c_longlong
         lib.ov3d_attn_small_bwd.argtypes = [ctypes.c_int]
         lib.ov3d_attn_small_bwd.restype = ctypes.c_int
         lib.ov3d_attn_maskbits_words.argtypes = [ctypes.c_int] * 3
@@ -245,6 +254,37 @@ def timing_collect():
 
 # Optional launch census (tests): the set of entry points called while enabled.
 _CALLED = None
+
+
+STAMP_KINDS = ("fwd", "dq", "dkdv")
+
+
+def stamps_arm(buf, min_work=1 << 20):
+    """arm the attention kernels' in-kernel launch stamps into the int64 device tensor buf (None
+    disarms; the launch table stays readable).  Launches captured into a graph while armed keep
+    stamping on every replay."""
+    lib = load()
+    if buf is None:
+        lib.ov3d_stamps_arm(None, 0, 0)
+    else:
+        lib.ov3d_stamps_arm(buf.data_ptr(), buf.numel(), int(min_work))
+
+
+def stamps_read(buf):
+    """-> [(kind, launch duration ms, Lq * Lk)] for every recorded launch whose slots hold
+    stamps: max(exit) - min(entry) over its waves (wall clock, ov3d_wall_clock_khz)."""
+    lib = load()
+    khz = lib.ov3d_wall_clock_khz()
+    host = buf.cpu()
+    out = []
+    for i in range(lib.ov3d_stamps_count()):
+        kind, off, waves, work = ctypes.c_int(), ctypes.c_longlong(), ctypes.c_longlong(), ctypes.c_longlong()
+        lib.ov3d_stamps_get(i, ctypes.byref(kind), ctypes.byref(off), ctypes.byref(waves), ctypes.byref(work))
+        st = host[off.value: off.value + 2 * waves.value].view(-1, 2)
+        if bool((st == 0).any()):
+            continue
+        out.append((STAMP_KINDS[kind.value], (st[:, 1].max() - st[:, 0].min()).item() / khz, work.value))
+    return out
 
 
 def census_start():

@@ -74,6 +74,7 @@ struct AttnArgs {
     int nkt;               // 64-key tiles = ceil(Lk / 64)
     const uint32_t* mq;    // mask bits (1 = not attended), query-major: [nkt][B][Lq][2]
     const uint32_t* mk;    // mask bits, key-major: [Lq/32][B][nkt*64]
+    unsigned long long* stamp;   // in-kernel launch stamps (measurement) or null: ov3d_stamps_arm
 };
 
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
@@ -295,7 +296,7 @@ __global__ void __launch_bounds__(256) attn_dropgen_kernel(AttnArgs a) {
 
 // BITS: dropout from the words of attn_dropgen_kernel (read, not hashed, not stored)
 template <bool DROP, bool MASK, bool BITS>
-__global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
+__device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
     // K and V tiles in one array: its 36 KB also stage the output rows after the loop
     __shared__ __attribute__((aligned(16))) bf16 KVs[2][2][KB * LDK];
     bf16 (*const Ks)[KB * LDK] = KVs[0];
@@ -602,6 +603,13 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     }
 }
 
+template <bool DROP, bool MASK, bool BITS>
+__global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
+    ov3d_stamp(a.stamp, 0);
+    attn_fwd_body<DROP, MASK, BITS>(a);
+    ov3d_stamp(a.stamp, 1);
+}
+
 // merge split-K partials: one 64-lane wave per (b*H+h, query); lane = d
 // NS: the split count rounded up to a power of two (<= kMaxCombine), the loads clamped to the
 // last split (with NS = 16 for every split count, 8 splits loaded each partial twice)
@@ -674,6 +682,7 @@ struct AttnBwdArgs {
     bf16* dv;
     long long sdq, sdk, sdv;
     float scale;
+    unsigned long long* stamp2;   // the dK / dV launch's stamps (f.stamp: the dQ launch's)
 };
 
 // RAGGED: Lk % 64 != 0 (the last key tile is partial); the key check exists only then
@@ -895,7 +904,9 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
 
 template <bool DROP, bool MASK, bool RAGGED>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnBwdArgs A) {
+    ov3d_stamp(A.f.stamp, 0);
     attn_bwd_dq_body<DROP, MASK, RAGGED>(A);
+    ov3d_stamp(A.f.stamp, 1);
 }
 
 // dq = scale * sum over key splits; one thread per (b*H+h, query, 4 dims)
@@ -1160,7 +1171,9 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
 
 template <bool DROP, bool MASK>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnBwdArgs A) {
+    ov3d_stamp(A.stamp2, 0);
     attn_bwd_dkdv_body<DROP, MASK>(A);
+    ov3d_stamp(A.stamp2, 1);
 }
 
 // The whole backward of a short attention (Lq, Lk <= 128, one key split: the decoder's
@@ -1343,6 +1356,59 @@ extern "C" int ov3d_attn_mask_pack(const void* src, int kind, float thr, int B, 
     return OV3D_OK;
 }
 
+// ---- in-kernel launch stamps (bench.py's in-step timing of the roofline kernel).  While armed,
+// every forward / dQ / dK-dV launch of Lq * Lk >= min_work takes 2 words per wave of the buffer
+// (kernel writes: entry and exit wall clock of each wave, see ov3d_stamp); the host reads the
+// launch table back (ov3d_stamps_get) and takes max(exit) - min(entry) per launch.
+namespace {
+unsigned long long* g_stamp_buf = nullptr;
+long long g_stamp_cap = 0, g_stamp_used = 0, g_stamp_min_work = 0;
+constexpr int kStampRecs = 256;
+int g_stamp_n = 0;
+int g_stamp_kind[kStampRecs];
+long long g_stamp_off[kStampRecs], g_stamp_waves[kStampRecs], g_stamp_work[kStampRecs];
+
+unsigned long long* stamp_take(int kind, long long work, long long waves) {
+    if (!g_stamp_buf || work < g_stamp_min_work || g_stamp_n >= kStampRecs ||
+        g_stamp_used + 2 * waves > g_stamp_cap)
+        return nullptr;
+    g_stamp_kind[g_stamp_n] = kind;
+    g_stamp_off[g_stamp_n] = g_stamp_used;
+    g_stamp_waves[g_stamp_n] = waves;
+    g_stamp_work[g_stamp_n] = work;
+    ++g_stamp_n;
+    unsigned long long* p = g_stamp_buf + g_stamp_used;
+    g_stamp_used += 2 * waves;
+    return p;
+}
+}  // namespace
+
+/* kinds: 0 forward, 1 dQ, 2 dK/dV.  buf = null disarms (the table stays readable). */
+extern "C" int ov3d_stamps_arm(unsigned long long* buf, long long words, long long min_work) {
+    g_stamp_buf = buf;
+    g_stamp_cap = buf ? words : 0;
+    g_stamp_min_work = min_work;
+    if (buf) g_stamp_used = g_stamp_n = 0;
+    return OV3D_OK;
+}
+extern "C" int ov3d_stamps_count(void) { return g_stamp_n; }
+extern "C" int ov3d_stamps_get(int i, int* kind, long long* word_off, long long* waves,
+                               long long* work) {
+    if (i < 0 || i >= g_stamp_n || !kind || !word_off || !waves || !work) return OV3D_EINVAL;
+    *kind = g_stamp_kind[i];
+    *word_off = g_stamp_off[i];
+    *waves = g_stamp_waves[i];
+    *work = g_stamp_work[i];
+    return OV3D_OK;
+}
+extern "C" long long ov3d_wall_clock_khz(void) {
+    int dev = 0, khz = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess)
+        return 0;
+    return khz;
+}
+
 extern "C" int ov3d_attn_fwd_masked(const void* q, const void* k, const void* v, long long sq,
                                     long long sk, long long sv, int B, int H, int Lq, int Lk,
                                     float scale, float dropout_p, const int64_t* seed, int site,
@@ -1384,6 +1450,7 @@ extern "C" int ov3d_attn_fwd_masked(const void* q, const void* k, const void* v,
     set_maskbits(a, maskbits);
     hipStream_t st = ov3d_stream(stream);
     dim3 grid((Lq + 4 * QW - 1) / (4 * QW), B * H, nsplit);
+    a.stamp = stamp_take(0, (long long)Lq * Lk, (long long)grid.x * grid.y * grid.z * 4);
     // long attentions take their drop bits from a separate VALU pass (attn_dropgen_kernel);
     // short ones (the decoder) hash in the forward, where one more launch would cost more
     const bool bits = a.thresh && dropgen_ahead(Lq, Lk);
@@ -1495,6 +1562,8 @@ extern "C" int ov3d_attn_bwd_masked(const void* q, const void* k, const void* v,
     a.part_o = workspace;
     set_dropbits(a, (uint32_t*)dropbits);
     set_maskbits(a, maskbits);
+    a.stamp = nullptr;
+    A.stamp2 = nullptr;
     hipStream_t st = ov3d_stream(stream);
     if (dk && !maskbits && nsplit == 1 && Lq <= 4 * QW && Lk <= 128 && fuse_small_bwd()) {
         if (small_bwd_split()) {
@@ -1516,6 +1585,7 @@ extern "C" int ov3d_attn_bwd_masked(const void* q, const void* k, const void* v,
     }
     const dim3 gq((Lq + 4 * QW - 1) / (4 * QW), B * H, nsplit);
     const bool ragged = Lk % KB != 0;
+    a.stamp = stamp_take(1, (long long)Lq * Lk, (long long)gq.x * gq.y * gq.z * 4);
     if (maskbits) {
         if (a.thresh)
             (ragged ? attn_bwd_dq_kernel<true, true, true> : attn_bwd_dq_kernel<true, true, false>)<<<gq, 256, 0, st>>>(A);
@@ -1533,6 +1603,7 @@ extern "C" int ov3d_attn_bwd_masked(const void* q, const void* k, const void* v,
     }
     if (!dk) return OV3D_OK;   // dQ (and D) only: dK / dV follow in ov3d_attn_bwd_dkdv_batch
     const dim3 gk((Lk + 127) / 128, B * H);
+    A.stamp2 = stamp_take(2, (long long)Lq * Lk, (long long)gk.x * gk.y * 4);
     if (maskbits) {
         if (a.thresh)
             attn_bwd_dkdv_kernel<true, true><<<gk, 256, 0, st>>>(A);
@@ -1609,6 +1680,8 @@ extern "C" int ov3d_attn_bwd_dkdv_batch(const ov3d_attn_dkdv_job* jobs, int njob
             A.sdk = J.sdk;
             A.sdv = J.sdv;
             A.scale = scale;
+            a.stamp = nullptr;
+            A.stamp2 = nullptr;
         }
         const dim3 gk((Lk + 127) / 128, B * H, n);
         if (dropout_p > 0.f)

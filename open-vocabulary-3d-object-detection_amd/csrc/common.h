@@ -20,3 +20,13 @@ __device__ __forceinline__ unsigned long long lanemask_lt() {
     const unsigned lane = threadIdx.x & 63u;
     return lane == 0 ? 0ull : (~0ull >> (64u - lane));
 }
+
+// In-kernel launch stamps (measurement only: bench.py's in-step timing of the roofline kernel).
+// Lane 0 of every wave writes the wall clock (100 MHz) at entry (end = 0) and exit (end = 1)
+// into its own 2-word slot of a buffer that nothing else in the kernel reads; st == null: off.
+__device__ __forceinline__ void ov3d_stamp(unsigned long long* st, int end) {
+    if (st && (threadIdx.x & 63) == 0) {
+        const long long wg = blockIdx.x + (long long)gridDim.x * (blockIdx.y + (long long)gridDim.y * blockIdx.z);
+        st[2 * (wg * (blockDim.x >> 6) + (threadIdx.x >> 6)) + end] = wall_clock64();
+    }
+}

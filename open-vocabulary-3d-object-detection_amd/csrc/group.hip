@@ -273,21 +273,43 @@ __global__ __launch_bounds__(256) void inv_fill_kernel(const int32_t* __restrict
 }
 
 // the fill's atomics hand out slots in an arbitrary order; the backward's fp32 sums follow the
-// list order, so each list is sorted by row id (one thread per list, insertion sort: the lists
-// are short and arrive nearly sorted): the gradient is then the same bit for bit in every run
+// list order, so each list is put in ascending row order: the gradient is then the same bit for
+// bit in every run.  One wave per list: the list (row ids are distinct) is staged in LDS and
+// every entry goes to its rank (the number of smaller entries): len^2 / 64 LDS reads per lane,
+// no dependent global round trips (a one-thread insertion sort over global memory took ~1 ms
+// per ScanNet step on its longest lists, ~180 entries).  Lists longer than kSortLds (none at
+// the reference's shapes) take the one-lane insertion sort.
+constexpr int kSortLds = 1024;
 __global__ __launch_bounds__(256) void inv_sort_kernel(const int32_t* __restrict__ off, long long n,
                                                        int32_t* __restrict__ rows) {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int e0 = off[i], e1 = off[i + 1];
-    for (int j = e0 + 1; j < e1; ++j) {
-        const int32_t v = rows[j];
-        int k = j - 1;
-        while (k >= e0 && rows[k] > v) {
-            rows[k + 1] = rows[k];
-            --k;
-        }
-        rows[k + 1] = v;
+    __shared__ int32_t s[4][kSortLds];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const long long i = (long long)blockIdx.x * 4 + w;
+    if (i >= n) return;   // whole waves only; no workgroup barrier below
+    const int e0 = off[i], e1 = off[i + 1], len = e1 - e0;
+    if (len <= 1) return;
+    if (len > kSortLds) {
+        if (lane == 0)
+            for (int j = e0 + 1; j < e1; ++j) {
+                const int32_t v = rows[j];
+                int k = j - 1;
+                while (k >= e0 && rows[k] > v) {
+                    rows[k + 1] = rows[k];
+                    --k;
+                }
+                rows[k + 1] = v;
+            }
+        return;
+    }
+    for (int j = lane; j < len; j += 64) s[w][j] = rows[e0 + j];
+    // one wave's LDS accesses complete in order: its reads below see all its writes
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int j0 = 0; j0 < len; j0 += 64) {
+        const int j = j0 + lane;
+        const int32_t v = j < len ? s[w][j] : 0;
+        int rank = 0;
+        for (int u = 0; u < len; ++u) rank += s[w][u] < v;
+        if (j < len) rows[e0 + rank] = v;
     }
 }
 
@@ -390,7 +412,7 @@ extern "C" int ov3d_group_inverse(const int32_t* idx, int B, int N, int M, int S
         hipLaunchKernelGGL(inv_fill_kernel, dim3(ov3d_cdiv(total, 256)), dim3(256), 0, s, idx, N,
                            (long long)M * S, total, cursor, rows);
     if (total > 0)
-        hipLaunchKernelGGL(inv_sort_kernel, dim3(ov3d_cdiv(n, 256)), dim3(256), 0, s, offsets, n, rows);
+        hipLaunchKernelGGL(inv_sort_kernel, dim3(ov3d_cdiv(n, 4)), dim3(256), 0, s, offsets, n, rows);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

@@ -468,3 +468,39 @@ def test_forward_with_drop_bits_ahead_equals_hashing_forward(cuda, monkeypatch, 
         res.append((o, lse, bits))
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+def test_launch_stamps_time_the_encoder_launches(cuda):
+    """ov3d_stamps_arm: encoder-size launches (Lq * Lk >= min_work) stamp every wave's entry and
+    exit (bench.py's in-step roofline timing); shorter launches take no slot; the kernel outputs
+    are unchanged by the stamps; the stamped duration agrees with HIP events on the same launch."""
+    from ov3d_amd import _native, attention as A
+    L, B, H = 1024, 2, 4
+    E = H * A.HEAD_DIM
+    g = torch.Generator(device="cuda").manual_seed(2)
+    x = torch.randn((L, B, 3 * E), device=cuda, dtype=torch.bfloat16, generator=g).requires_grad_(True)
+    gout = torch.randn((L, B, E), device=cuda, dtype=torch.bfloat16, generator=g)
+    spec = ((0, 0), (0, E), (0, 2 * E))
+    ref = A.attention_packed([x], spec, L, L, H, 0.0)
+    ref.backward(gout)
+    gref = x.grad.clone()
+    x.grad = None
+    buf = torch.zeros((1 << 18,), dtype=torch.int64, device=cuda)
+    _native.stamps_arm(buf, min_work=L * L)
+    try:
+        small = torch.randn((128, B, 3 * E), device=cuda, dtype=torch.bfloat16, generator=g)
+        A.attention_packed([small], spec, 128, 128, H, 0.0)         # below min_work: no slot
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = A.attention_packed([x], spec, L, L, H, 0.0)
+        e1.record()
+        out.backward(gout)
+        torch.cuda.synchronize()
+    finally:
+        _native.stamps_arm(None)
+    assert torch.equal(out, ref) and torch.equal(x.grad, gref)
+    rec = _native.stamps_read(buf)
+    kinds = [k for k, _, _ in rec]
+    assert kinds == ["fwd", "dq", "dkdv"], rec
+    assert all(w == L * L and 0 < ms < 50 for _, ms, w in rec), rec
+    assert rec[0][1] <= e0.elapsed_time(e1) * 1.05 + 0.01, (rec, e0.elapsed_time(e1))

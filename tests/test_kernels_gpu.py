@@ -159,9 +159,10 @@ def test_group_inverse_index(cuda):
     each list ascending (the fill's atomics order is undone: the gather-form backward's fp32
     sums are then identical in every run) -- i.e. exactly a stable argsort by point"""
     from ov3d_amd import pointnet2_utils as pu
-    B, N, M, S = 3, 500, 64, 16
+    B, N, M, S = 3, 500, 128, 16
     idx = torch.randint(0, N, (B, M, S), device=cuda, dtype=torch.int32)
-    idx[1] = 7   # one point read by every row of a scene
+    idx[1] = 7          # one point read by every row of a scene: a 2048-entry list
+    idx[2, :20] = 9     # a ~330-entry list (the wave rank sort's LDS path)
     off, rows = pu.group_inverse(idx, N)
     off, rows, idx = off.cpu().numpy(), rows.cpu().numpy(), idx.cpu().numpy().reshape(-1)
     assert off[0] == 0 and off[-1] == B * M * S and np.all(np.diff(off) >= 0)
