@@ -86,7 +86,7 @@ def regionclip_gflop_per_scene(batch, nqueries=128, layers=8):
 
 
 def build(args, device, ddp=False, capturable=False, sync_bn=False, allreduce=False,
-          dataset="sunrgbd"):
+          dataset="sunrgbd", staged=True):
     """ddp: the reference's DistributedDataParallel + SyncBatchNorm (eager); sync_bn +
     allreduce: the same semantics for the captured step (SyncBatchNorm statistics
     all-reduced inside the fused BN kernels' launches, the gradient mean by ONE collective
@@ -108,12 +108,20 @@ def build(args, device, ddp=False, capturable=False, sync_bn=False, allreduce=Fa
     if getattr(args, "optim", "fused") == "fused":
         # clip_grad_norm_(clip_gradient) + AdamW in three HIP launches (ov3d_amd/optim.py)
         from ov3d_amd.optim import FusedAdamW
-        group = None
+        group = buckets = None
         if allreduce:
             import torch.distributed as tdist
+            from ov3d_amd import dist as pdist
             group = tdist.group.WORLD
+            if staged and hasattr(model, "dp_buckets"):
+                # the decoder side's gradients all-reduced under the encoder / SA backward, on
+                # a communicator of their own (dist.GradBuckets, dist.stage_after_encoder)
+                bgroup = tdist.new_group(ranks=list(range(tdist.get_world_size())))
+                buckets = pdist.GradBuckets(model.dp_buckets(), group=bgroup)
+                pdist.stage_after_encoder(model, buckets)
         opt = FusedAdamW(params, lr=args.base_lr, weight_decay=args.weight_decay,
-                         max_grad_norm=args.clip_gradient, allreduce_group=group)
+                         max_grad_norm=args.clip_gradient, allreduce_group=group,
+                         grad_buckets=buckets)
         return model, crit, opt
     try:
         opt = torch.optim.AdamW(params, lr=args.base_lr, weight_decay=args.weight_decay, fused=True,
@@ -363,6 +371,9 @@ def main():
     p.add_argument("--dp-collectives", action="store_true",
                    help="run the data-parallel collectives (SyncBN statistics, gradient all-reduce) "
                         "even at world size 1 (tests the captured collectives on one GPU)")
+    p.add_argument("--no-staged-allreduce", action="store_true",
+                   help="data parallel: all-reduce every gradient at the end of the step instead of "
+                        "starting the decoder side's bucket under the encoder backward")
     p.add_argument("--no-defer-wgrad", action="store_true",
                    help="compute each linear layer's dW / db inside its backward instead of one "
                         "grouped launch at the end of the backward pass (gemm.DEFER_WGRAD)")
@@ -408,7 +419,8 @@ def main():
     if cli.optim != "fused" and dp:
         raise SystemExit("the captured data-parallel step needs --optim fused")
     model, crit, opt = build(args, device, ddp=world > 1 and not use_graph, capturable=use_graph,
-                             sync_bn=dp, allreduce=dp, dataset=dataset)
+                             sync_bn=dp, allreduce=dp, dataset=dataset,
+                             staged=not cli.no_staged_allreduce)
     if not cli.no_defer_wgrad and not (world > 1 and not use_graph):
         from ov3d_amd import gemm
         gemm.DEFER_WGRAD = True   # one grouped weight-gradient launch per backward (not under DDP)

@@ -251,16 +251,29 @@ class Model3DETR(nn.Module):
         # L*B*Q positions exactly as on the reference's (L*B, C, Q) conv input
         rows = box_features.permute(0, 2, 1, 3).reshape(L * B * Q, C)
         pre = None
-        if self.fuse_heads:
-            if getattr(self, "_head_pack", None) is None:
-                self._head_pack = heads_mod.HeadPack(self.mlp_heads)
-            if heads_mod.supported(self._head_pack, rows):
+        if self._heads_fused_ok(rows):
                 # the text alignment folds into the heads' output launch (Q8 layout written
                 # there when the reference layout is kept)
                 pre = heads_mod.fused_heads(self._head_pack, rows, sem=self.mlp_heads["sem_cls_head"],
                                             lq=Q if self.cls_logits_layout == "reference" else 0)
         with torch.autocast(device_type=box_features.device.type, enabled=False):
             return self._box_predictions(query_xyz.float(), point_cloud_dims, rows, (L, Q, B), pre)
+
+    def dp_buckets(self):
+        """parameters in gradient all-reduce order (dist.GradBuckets): everything downstream of
+        the encoder output (decoder, heads, projections: final when the backward reaches that
+        output), then the encoder and the pre-encoder SA"""
+        early = {id(p) for m in (self.pre_encoder, self.encoder) for p in m.parameters()}
+        ps = [p for p in self.parameters() if p.requires_grad]
+        return [[p for p in ps if id(p) not in early], [p for p in ps if id(p) in early]]
+
+    def _heads_fused_ok(self, x):
+        """True when the five heads run as the fused launch (heads.supported) on x's device"""
+        if not self.fuse_heads:
+            return False
+        if getattr(self, "_head_pack", None) is None:
+            self._head_pack = heads_mod.HeadPack(self.mlp_heads)
+        return heads_mod.supported(self._head_pack, x)
 
     def _box_predictions(self, query_xyz, point_cloud_dims, rows, dims_lqb, pre=None):
         L, Q, B = dims_lqb
@@ -353,6 +366,11 @@ class Model3DETR(nn.Module):
             flash.next_step(pc.device)   # fresh attention-dropout stream for this step
         plan = {k: inputs[k] for k in self.PLAN_KEYS if k in inputs}
         enc_xyz, enc_feats, _ = self.run_encoder(pc, plan=plan)   # (N', B, C)
+        hook = getattr(self, "encoder_grad_hook", None)
+        if hook is not None and enc_feats.requires_grad:
+            # data parallel: the decoder side's gradients are final when this fires (dist.py
+            # stage_after_encoder starts their all-reduce under the encoder's backward)
+            enc_feats.register_hook(lambda g: hook())
         Np, B, C = enc_feats.shape
         enc_feats = self.encoder_to_decoder_projection.rows(enc_feats.reshape(Np * B, C)).view(Np, B, -1)
         if encoder_only:
@@ -363,6 +381,9 @@ class Model3DETR(nn.Module):
                                                   seq_first=True)
         enc_pos = self.pos_embedding.rows(enc_xyz, input_range=dims, seq_first=True)
         tgt = _zeros_like_cached(query_embed)
+        # the fused decoder writes its layer outputs as bf16 rows only for the fused heads
+        # launch; the per-head fp32 path (eval, other head shapes) gets the fp32 rows
+        self.decoder.rows_bf16 = self._heads_fused_ok(tgt)
         box_features = self.decoder(tgt, enc_feats, query_pos=query_embed, pos=enc_pos)[0]
         return self.get_box_predictions(query_xyz, dims, box_features)
 

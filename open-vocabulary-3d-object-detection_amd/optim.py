@@ -46,7 +46,7 @@ class FusedAdamW(torch.optim.Optimizer):
     writes_shadows = True     # step() refreshes gemm.py's bf16 parameter copies
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2,
-                 max_grad_norm=None, allreduce_group=None):
+                 max_grad_norm=None, allreduce_group=None, grad_buckets=None):
         if lr < 0 or eps < 0 or weight_decay < 0 or not (0 <= betas[0] < 1 and 0 <= betas[1] < 1):
             raise ValueError("FusedAdamW: invalid hyper-parameters")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
@@ -55,6 +55,11 @@ class FusedAdamW(torch.optim.Optimizer):
         # one flat buffer (one launch), all-reduced by ONE collective (sum) and averaged by
         # the update kernels (grad_scale = 1/world): DDP's gradient mean, main.py:427-431
         self.allreduce_group = allreduce_group
+        # dist.GradBuckets: the same mean in buckets, the first one started during the backward
+        # (dist.stage_after_encoder); its views replace the single flat buffer
+        self.grad_buckets = grad_buckets
+        if grad_buckets is not None and allreduce_group is None:
+            raise ValueError("FusedAdamW: grad_buckets needs allreduce_group (the world size)")
         self.last_grad_norm = None
         self._key = None
         self._dev = None
@@ -168,7 +173,16 @@ class FusedAdamW(torch.optim.Optimizer):
             self._coefs = torch.empty(4, dtype=torch.float64, device=dev)
             self._key, self._dev = key, dev
         scale = 1.0
-        if self.allreduce_group is not None:
+        if self.grad_buckets is not None:
+            import torch.distributed as dist
+            views = self.grad_buckets.finish()
+            missing = [p for p, _ in items if id(p) not in views]
+            if missing:
+                raise ValueError("FusedAdamW: a parameter with a gradient is in no bucket")
+            self._flat_views = [views[id(p)] for p, _ in items]
+            grad_src = self._flat_views
+            scale = 1.0 / dist.get_world_size(self.allreduce_group)
+        elif self.allreduce_group is not None:
             import torch.distributed as dist
             if getattr(self, "_flat", None) is None or self._flat_key != key:
                 if capturing or self._captured:

@@ -93,17 +93,24 @@ class SceneStore:
     def _stack_extras(self, extras):
         """per-scan dicts of image (H, W, 3) / calib_Rtilt / calib_K / feature_2d ->
         resident tensors: images flattened and zero-padded to MAX_NUM_PIXEL * 3 in their
-        read dtype (the float32 conversion happens per batch, exactly as full_img_1d's)"""
+        read dtype (the float32 conversion happens per batch, exactly as full_img_1d's).
+
+        Memory: S x MAX_NUM_PIXEL x 3 elements on the device (1.16 MB per uint8 image: the
+        5285 SUN v1 training scans are 6.1 GB of the 288 GB HBM).  Each image is copied
+        straight into its row of the preallocated device tensor, so the host never holds
+        more than one padded image beside the decoded ones."""
         dev = self.device
         if "image" in extras[0]:
             imgs = [np.asarray(e["image"]) for e in extras]
             dt = imgs[0].dtype if all(i.dtype == imgs[0].dtype for i in imgs) else np.float32
-            flat = np.zeros((len(imgs), MAX_NUM_PIXEL * 3), dt)
+            flat = torch.zeros((len(imgs), MAX_NUM_PIXEL * 3), dtype=torch.from_numpy(
+                np.zeros(0, dt)).dtype, device=dev)
             for i, im in enumerate(imgs):
                 if im.size > MAX_NUM_PIXEL * 3:
                     raise ValueError("image larger than MAX_NUM_PIXEL (sunrgbd.py:284-285)")
-                flat[i, : im.size] = im.reshape(-1)
-            self.extras["image"] = torch.as_tensor(flat).to(dev)
+                flat[i, : im.size].copy_(torch.from_numpy(
+                    np.ascontiguousarray(im.reshape(-1), dtype=dt)))
+            self.extras["image"] = flat
             self.extras["image_height"] = torch.as_tensor(np.array([i.shape[0] for i in imgs], np.int64)).to(dev)
             self.extras["image_width"] = torch.as_tensor(np.array([i.shape[1] for i in imgs], np.int64)).to(dev)
             for k in ("calib_Rtilt", "calib_K"):

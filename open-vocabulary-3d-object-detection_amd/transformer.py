@@ -503,7 +503,7 @@ class TransformerDecoder(nn.Module):
         dec_norm = self.norm if self.return_intermediate else None
         # the layer outputs (decoder norm) go straight into the heads' bf16 (L, B, Q, C) rows
         outs = None
-        if dec_norm is not None and tgt.dim() == 3:
+        if dec_norm is not None and tgt.dim() == 3 and getattr(self, "rows_bf16", True):
             Q, B, C = tgt.shape
             outs = torch.empty((len(self.layers), B, Q, C), dtype=torch.bfloat16, device=tgt.device)
         # query_pos and the decoder norm are read by many launches: one gradient buffer each

@@ -154,7 +154,7 @@ def _slice_outputs(out, r):
     return {"outputs": one(out["outputs"]), "aux_outputs": [one(a) for a in out["aux_outputs"]]}
 
 
-def _train_rank(rank, port, out_dir):
+def _train_rank(rank, port, out_dir, mode="coalesced"):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -179,18 +179,36 @@ def _train_rank(rank, port, out_dir):
     crit = build_criterion(args, cfg)
     batch = {k: (v.double() if v.is_floating_point() else v)[rank: rank + 1]
              for k, v in bff(fx, "cpu").items()}
+    order = {}
+    if mode == "buckets":
+        # dist.GradBuckets on a group of its own, bucket 0 (decoder side) started by the hook on
+        # the encoder output's gradient; record what was final when it fired
+        gb = pdist.GradBuckets(model.dp_buckets(),
+                               group=torch.distributed.new_group(ranks=list(range(WORLD))))
+
+        def flush():
+            order["enc_grads_at_hook"] = sum(p.grad is not None for p in model.dp_buckets()[1])
+            order["dec_grads_at_hook"] = sum(p.grad is not None for p in model.dp_buckets()[0])
+        pdist.stage_after_encoder(model, gb, flush=flush)
     with float64_host():
         loss = _step(model, crit, batch)
     named = [(n, p) for n, p in model.named_parameters() if p.grad is not None]
-    avg = pdist.all_reduce_coalesced([p.grad for _, p in named], average=True)
+    if mode == "buckets":
+        order["launched_before_step"] = gb.launched(0)
+        views = gb.finish()
+        avg = [views[id(p)] / WORLD for _, p in named]
+    else:
+        avg = pdist.all_reduce_coalesced([p.grad for _, p in named], average=True)
     grads = {n: g.clone() for (n, _), g in zip(named, avg)}
     bufs = {n: b.clone() for n, b in model.named_buffers()}
-    torch.save({"loss": loss.detach(), "grads": grads, "bufs": bufs}, os.path.join(out_dir, f"tr{rank}.pt"))
+    torch.save({"loss": loss.detach(), "grads": grads, "bufs": bufs, "order": order},
+               os.path.join(out_dir, f"tr{rank}.pt"))
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()
 
 
-def test_ddp_syncbn_train_step_equals_global_batch(shim, monkeypatch):
+@pytest.mark.parametrize("mode", ["coalesced", "buckets"])
+def test_ddp_syncbn_train_step_equals_global_batch(shim, monkeypatch, mode):
     """§8(e): 2 ranks x 1 scene (train mode: SyncBatchNorm batch statistics over both ranks,
     the gradient mean by one all-reduce, num_boxes all-reduced) == 1 process x 2 scenes,
     both in float64 (so ReLU / max-pool decisions cannot flip between the two orders of
@@ -221,8 +239,15 @@ def test_ddp_syncbn_train_step_equals_global_batch(shim, monkeypatch):
         (sum(losses) / WORLD).backward()
     ref = {n: p.grad for n, p in model.named_parameters() if p.grad is not None}
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_train_rank, args=(_free_port(), d), nprocs=WORLD, join=True)
+        mp.spawn(_train_rank, args=(_free_port(), d, mode), nprocs=WORLD, join=True)
         res = [torch.load(os.path.join(d, f"tr{r}.pt"), weights_only=True) for r in range(WORLD)]
+    if mode == "buckets":
+        # bucket 0 left during the backward: the decoder side complete, the encoder side not
+        # started (its gradients came after the hook)
+        for r in range(WORLD):
+            o = res[r]["order"]
+            assert o["launched_before_step"] and o["enc_grads_at_hook"] == 0, o
+            assert o["dec_grads_at_hook"] > 50, o
     assert set(res[0]["grads"]) == set(ref)
     checked = 0
     for n, g in ref.items():
@@ -243,3 +268,70 @@ def test_ddp_syncbn_train_step_equals_global_batch(shim, monkeypatch):
             assert torch.equal(res[0]["bufs"][n], res[1]["bufs"][n]), n
             nb += 1
     assert nb >= 16
+
+
+def _syncbn_rank(rank, port, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    import ov3d_import
+    ov3d_import.load()
+    dist = _init(rank, port)
+    res = {}
+    for name, kw in (("cma", dict(momentum=None)), ("noaffine", dict(affine=False)),
+                     ("plain", dict())):
+        g = torch.Generator().manual_seed(5)
+        xs = [torch.randn(2, 7, 6, generator=g, dtype=torch.float64) * 3 + 1 for _ in range(2)]
+        bn = torch.nn.SyncBatchNorm(6, **kw).double()
+        if bn.weight is not None:
+            with torch.no_grad():
+                bn.weight.uniform_(0.5, 1.5, generator=g)
+                bn.bias.uniform_(-1, 1, generator=g)
+        bn.train()
+        outs = []
+        for x in xs:   # two steps: the cumulative-average momentum changes between them
+            xr = x[rank].clone().requires_grad_(True)
+            y = dist.sync_batch_norm_rows(bn, xr)
+            (y * torch.arange(1.0, 7.0, dtype=torch.float64)).sum().backward()
+            outs.append(y.detach())
+        res[name] = dict(y=torch.stack(outs).tolist(), gx=xr.grad.tolist(),
+                         rm=bn.running_mean.tolist(), rv=bn.running_var.tolist(),
+                         gw=None if bn.weight is None else bn.weight.grad.tolist())
+    with open(os.path.join(out_dir, f"sbn{rank}.json"), "w") as f:
+        json.dump(res, f)
+    dist.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_syncbn_rows_momentum_none_and_no_affine_world2():
+    """dist.sync_batch_norm_rows at world 2 equals torch BatchNorm1d on the global batch for
+    momentum=None (cumulative average, 1/num_batches_tracked) and affine=False (ADVICE r3);
+    the weight gradient is rank-local as in torch's SyncBatchNorm (sum over ranks = global)."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_syncbn_rank, args=(_free_port(), d), nprocs=WORLD, join=True)
+        got = [json.load(open(os.path.join(d, f"sbn{r}.json"))) for r in range(WORLD)]
+    for name, kw in (("cma", dict(momentum=None)), ("noaffine", dict(affine=False)),
+                     ("plain", dict())):
+        g = torch.Generator().manual_seed(5)
+        xs = [torch.randn(2, 7, 6, generator=g, dtype=torch.float64) * 3 + 1 for _ in range(2)]
+        bn = torch.nn.BatchNorm1d(6, **kw).double()
+        if bn.weight is not None:
+            with torch.no_grad():
+                bn.weight.uniform_(0.5, 1.5, generator=g)
+                bn.bias.uniform_(-1, 1, generator=g)
+        bn.train()
+        for step, x in enumerate(xs):
+            xr = x.reshape(14, 6).clone().requires_grad_(True)
+            y = bn(xr)
+            (y * torch.arange(1.0, 7.0, dtype=torch.float64)).sum().backward()
+            for r in range(WORLD):
+                np.testing.assert_allclose(got[r][name]["y"][step], y.detach()[7 * r: 7 * r + 7],
+                                           rtol=1e-9, atol=1e-9)
+        for r in range(WORLD):
+            np.testing.assert_allclose(got[r][name]["gx"], xr.grad[7 * r: 7 * r + 7], atol=1e-9)
+            np.testing.assert_allclose(got[r][name]["rm"], bn.running_mean, rtol=1e-9, atol=1e-12)
+            np.testing.assert_allclose(got[r][name]["rv"], bn.running_var, rtol=1e-9, atol=1e-12)
+        if bn.weight is not None:
+            gw = np.add(got[0][name]["gw"], got[1][name]["gw"])
+            np.testing.assert_allclose(gw, bn.weight.grad, rtol=1e-9, atol=1e-9)
+        else:
+            assert got[0][name]["gw"] is None

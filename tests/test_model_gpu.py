@@ -330,3 +330,35 @@ def test_second_forward_does_not_change_first_backward(cuda):
     for n in g1:
         d = (g1[n] - g2[n]).norm() / g1[n].norm().clamp_min(1e-12)
         assert d.item() < 1e-3, (n, d.item())
+
+
+def test_decoder_rows_fp32_unless_fused_heads(cuda):
+    """The fused decoder writes its layer outputs as bf16 rows only when the fused heads
+    launch consumes them (train, bf16 autocast); in eval the per-head fp32 path gets fp32
+    decoder outputs (transformer.py xb_into)."""
+    import ov3d_amd
+    from ov3d_amd import synthetic
+    from ov3d_amd.dataset_config import SunrgbdDatasetConfig
+    from bench import default_args
+    args = default_args()
+    cfg = SunrgbdDatasetConfig()
+    torch.manual_seed(0)
+    model, _ = ov3d_amd.build_model(args, cfg, text_embedding=synthetic.text_embedding())
+    model = model.to(cuda)
+    batch = synthetic.make_batch(2, seed=4, device=cuda)
+    inputs = {k: batch[k] for k in ("point_clouds", "point_cloud_dims_min", "point_cloud_dims_max")}
+    seen = {}
+    orig = model.get_box_predictions
+
+    def spy(qx, dims, feats):
+        seen["feats"] = feats
+        return orig(qx, dims, feats)
+    model.get_box_predictions = spy
+    for mode in ("train", "eval"):
+        getattr(model, mode)()
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            model(inputs)
+        seen[mode] = seen.pop("feats")
+    assert seen["train"].dtype == torch.bfloat16
+    assert seen["eval"].dtype == torch.float32
+    assert torch.isfinite(seen["eval"]).all()
