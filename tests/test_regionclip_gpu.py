@@ -65,7 +65,7 @@ def test_clip_preprocess_bit_exact(cuda):
     from regionclip_ref import preprocess
     ims = [torch.from_numpy(img[i, : hs[i] * ws[i] * 3]).view(hs[i], ws[i], 3).permute(2, 0, 1).to(cuda)
            for i in range(3)]
-    ref = preprocess(m, ims).permute(0, 2, 3, 1)
+    ref = preprocess(m.pixel_mean, m.pixel_std, ims).permute(0, 2, 3, 1)
     torch.testing.assert_close(x, ref, rtol=0, atol=0)
 
 
