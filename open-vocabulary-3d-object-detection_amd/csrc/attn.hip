@@ -67,7 +67,7 @@ struct AttnArgs {
     long long so;
     float* lse;            // (B*H, Lq), log2 domain: m*scale2 + log2(l)
     float* part_o;         // split-K partials (nsplit, B*H, Lq, 64) unnormalised
-    float* part_ml;        // (nsplit, B*H, Lq, 2): m*scale2, l
+    float* part_ml;        // (nsplit, B*H, Lq, 2): m*scale2 (-inf: no attended key), l
     int nsplit, keys_per_split;
     uint32_t* wq;          // drop bits, query-major: [nkt][B*H][Lq][2] (see drop_word)
     uint32_t* wk;          // drop bits, key-major:   [Lq/32][B*H][nkt*64]
@@ -94,16 +94,19 @@ __device__ __forceinline__ uint32_t drop_head_mix(const int64_t* seed, uint32_t 
 __device__ __forceinline__ uint32_t drop_query_base(uint32_t hm, uint32_t q) {
     return mix32(hm ^ (q * 0xC2B2AE35u));
 }
-// Per-element finaliser of the dropout hash: xor-shifts and 24-bit multiplies only
-// (v_mul_u32_u24 issues at the full VALU rate; the 32-bit v_mul_lo_u32 of mix32 is a
-// quarter-rate instruction and dominated the softmax).
-__device__ __forceinline__ uint32_t mix24(uint32_t x) {
+// Per-element finaliser of the dropout hash: two 24-bit multiply rounds; every fold is a
+// 16-bit word or a top byte (x ^ x >> 16 and p ^ x >> 24 are ONE v_xor_b32_sdwa each), so 6
+// vector ops per key pair (round 3's finaliser also folded by 15 bits: 9).  v_mul_u32_u24
+// issues at the full VALU rate (the 32-bit v_mul_lo_u32 of mix32 is quarter rate).  Screened
+// over 16384 queries x 2048 keys x 4 heads at p = 0.1 / 0.3 (tools/drop_hash_screen.py, "b2":
+// drop rate, byte chi2, pair / neighbour / rectangle correlations within noise, as the round-3
+// finaliser; without the first top-byte fold ("b1") the byte chi2 reads 483 on 255 dof).
+__device__ __forceinline__ uint32_t drop_mix(uint32_t x) {
     x ^= x >> 16;
     x = __umul24(x, 0x7feb35u) ^ (x >> 24);
-    x ^= x >> 15;
-    x = __umul24(x, 0x846ca7u) ^ (x >> 24);
     x ^= x >> 16;
-    return x;
+    x = __umul24(x, 0x846ca7u);
+    return x ^ (x >> 16);
 }
 
 // one 32-bit hash per (query, key pair k>>1): its low half decides the even key, the
@@ -164,6 +167,44 @@ __device__ __forceinline__ uint32_t transpose32(uint32_t a, int r) {
 
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// the value of lane ^ 32 combined with this lane's: one v_permlane32_swap (swaps the two
+// 32-lane halves of its operands) instead of a ds_bpermute round trip
+__device__ __forceinline__ float max_halves(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(uint32_t, x),
+                                                    __builtin_bit_cast(uint32_t, x), false, false);
+    return fmaxf(__builtin_bit_cast(float, (uint32_t)r[0]), __builtin_bit_cast(float, (uint32_t)r[1]));
+}
+
+// Operand rows scaled by scale * log2(e) and rounded to bf16 once: the score MFMAs then give
+// log2-domain scores and the softmax needs no multiply per element.  The forward and the dQ
+// pass prescale the query rows identically (the same P); the dK / dV pass prescales its key rows.
+__device__ __forceinline__ bf16x8 prescale8(bf16x8 v, float c) {
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (bf16)((float)v[j] * c);
+    return r;
+}
+
+// Row constants by one more MFMA k-step instead of per-element initial values (a 32x32 tile's
+// 16 accumulators per lane would take 16 v_mov per tile): k-slots 0 and 1 live in the h = 0
+// lanes' elements 0 and 1, every other slot is zero.  One side holds x0, x1, the other 1, 1:
+// the product adds x0 + x1 to every element of the row / column.
+__device__ __forceinline__ bf16x8 kslots(float x0, float x1, bool on) {
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (bf16)0.f;
+    if (on) {
+        r[0] = (bf16)x0;
+        r[1] = (bf16)x1;
+    }
+    return r;
+}
+// x as bf16 hi + lo (x to ~2^-16 relative); +-inf -> (inf, 0)
+__device__ __forceinline__ float bf16_hi(float x) { return (float)(bf16)x; }
+__device__ __forceinline__ float bf16_lo(float x) {
+    return __builtin_isinf(x) ? 0.f : x - bf16_hi(x);
+}
 
 // online-softmax rescale only when a query's running max grows by more than this
 // (log2 units): P stays <= 2^8 between rescales (cdna_hip_programming.md T13)
@@ -285,7 +326,7 @@ __global__ void __launch_bounds__(256) attn_dropgen_kernel(AttnArgs a) {
 #pragma unroll
             for (int i = 0; i < 16; i += 2) {
                 const uint32_t c = 16 * t + ((i & 3) >> 1) + 4 * (i >> 2);
-                const uint32_t dm = drop_halves(mix24(hb + c * kPairMul), tsig);
+                const uint32_t dm = drop_halves(drop_mix(hb + c * kPairMul), tsig);
                 const int jb = 8 * t + (i >> 1);
                 dw |= dm & ((1u << jb) | (1u << (16 + jb)));
             }
@@ -316,7 +357,8 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
         const int qi = active ? q0 + r : 0;
         const bf16* qrow = a.q + ((size_t)qi * a.B + b) * a.sq + hh * D;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qrow + 16 * s + 8 * h);
+        for (int s = 0; s < 4; ++s)
+            qf[s] = prescale8(*reinterpret_cast<const bf16x8*>(qrow + 16 * s + 8 * h), a.scale2);
     }
     // dropout hash input of key pair (kb >> 1) + 2h + c: qh + (kb >> 1) * kPairMul (wave-
     // uniform, once per tile) + c * kPairMul (a constant per unrolled pair)
@@ -380,7 +422,14 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
     f32x16 o[2];
 #pragma unroll
     for (int i = 0; i < 16; ++i) o[0][i] = o[1][i] = 0.f;
-    float m = -INFINITY, l = 0.f;
+    // running max of the lane's query (log2 domain), bf16-exact: the score chains start with
+    // one MFMA k-step that subtracts it (A = 1 in k-slot 0, B = -mb), so S' = S - mb comes out
+    // of the matrix cores; the first tile with an attended key sets it to that tile's max
+    float mb = 0.f;
+    bool unset = true;
+    const bf16x8 k1 = kslots(1.f, 0.f, h == 0);
+    bf16x8 kmb = kslots(0.f, 0.f, false);
+    float l = 0.f;
     // row sums on the matrix cores: an all-ones A operand times the (undropped) P^T packs
     // gives every accumulator row the column sums = each lane's query row sum over the 64 keys
     // of the tile (both lane halves), 4 MFMAs per tile instead of 32 VALU adds (the loop is
@@ -427,6 +476,7 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
 #pragma unroll
                 for (int i = 0; i < 16; ++i)
                     st[t][i] = MASK ? __builtin_bit_cast(float, bit_mask(mw, score_bit(t, i)) & 0xFF800000u) : 0.f;
+                st[t] = mfma(k1, kmb, st[t]);   // - mb
             }
 #pragma unroll
             for (int s = 0; s < 4; ++s)
@@ -456,19 +506,23 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
                     for (int i = 0; i < 16; ++i)
                         if (32 * t + (i & 3) + 8 * (i >> 2) + 4 * h >= nvalid) st[t][i] = -INFINITY;
             }
-            float mx = -INFINITY;
+            float mx = -INFINITY;   // max of S - mb over the lane's keys
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) mx = fmaxf(mx, st[t][i]);
-            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            mx = max_halves(mx);
             PROBE(2);
             // deferred rescale (T13): keep the stale max unless some query's max grew a lot
-            if (__any((mx - m) * a.scale2 > RESCALE_THR)) {
-                const float mnew = fmaxf(m, mx);
-                // (masked: a query with no attended key yet keeps m = -inf and alpha = 1)
-                const float alpha = (MASK && mnew == -INFINITY) ? 1.f : fast_exp2((m - mnew) * a.scale2);
-                m = mnew;
+            const bool seen = mx > -INFINITY;   // some key of the tile attended
+            if (__any(mx > RESCALE_THR || (unset && seen))) {
+                // new stabiliser: the running max rounded to bf16 (nearest: never below mb when
+                // mx > 0); a query's first attended tile sets it up or down
+                const float mn = (mx > 0.f || (unset && seen)) ? bf16_hi(mb + mx) : mb;
+                const float d = mn - mb;
+                // o and the sums of a query with no attended key yet are zero (alpha = 1 keeps
+                // them so even when exp2(-d) would overflow)
+                const float alpha = unset ? 1.f : fast_exp2(-d);
                 l *= alpha;
                 lacc[0] *= alpha;
 #pragma unroll
@@ -476,12 +530,17 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
                     o[0][i] *= alpha;
                     o[1][i] *= alpha;
                 }
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) st[t][i] -= d;
+                mb = mn;
+                kmb = kslots(-mb, 0.f, h == 0);
+                unset = unset && !seen;
             }
-            // p = exp2(s * scale2 - m * scale2), one bf16 pack per key pair; dropout zeroes p
-            // after the row sum.  Scalar f32 ops on purpose: packed v_pk_fma / v_pk_add issue
-            // slower than two scalar ops beside the MFMAs (MI355X_MICROARCH.md cycle table;
-            // the file is built with -fno-slp-vectorize)
-            const float mb = (MASK && m == -INFINITY) ? 0.f : m * a.scale2;
+            // p = exp2(S - mb), one bf16 pack per key pair; dropout zeroes p after the row sum.
+            // Scalar f32 ops on purpose: packed v_pk_* issue slower than two scalar ops beside
+            // the MFMAs (MI355X_MICROARCH.md cycle table; the file is built with -fno-slp-vectorize)
             const uint32_t hb = qh + (uint32_t)(kb >> 1) * kPairMul;
             const short ts = (short)((int)a.thresh - 32768);
             const s16x2 tsig = {ts, ts};
@@ -492,8 +551,8 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int i = 0; i < 16; i += 2) {
-                    float p0 = fast_exp2(fmaf(st[t][i], a.scale2, -mb));
-                    float p1 = fast_exp2(fmaf(st[t][i + 1], a.scale2, -mb));
+                    float p0 = fast_exp2(st[t][i]);
+                    float p1 = fast_exp2(st[t][i + 1]);
 #ifdef OV3D_ATTN_VALU_ROWSUM
                     rs0 += p0;
                     rs1 += p1;
@@ -510,7 +569,7 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
                     } else if (DROP) {
                         // key 32t + (i&3) + 8(i>>2) + 4h (even): pair 16t + (i&3)/2 + 4(i>>2) + 2h
                         const uint32_t c = 16 * t + ((i & 3) >> 1) + 4 * (i >> 2);
-                        const uint32_t dm = drop_halves(mix24(hb + c * kPairMul), tsig);
+                        const uint32_t dm = drop_halves(drop_mix(hb + c * kPairMul), tsig);
                         // 1/(1-p) is applied once to the output (keep_scale below)
                         pk &= ~dm;
                         const int jb = 8 * t + (i >> 1);
@@ -565,7 +624,7 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
                 for (int j = 0; j < 4; ++j) w[j] = (bf16)(o[dt][4 * g + j] * inv);
                 *reinterpret_cast<bf16x4*>(so + ql * LDK + 32 * dt + 8 * g + 4 * h) = w;
             }
-        if (active && h == 0) a.lse[(size_t)bh * a.Lq + q] = m * a.scale2 + log2f(ltot);
+        if (active && h == 0) a.lse[(size_t)bh * a.Lq + q] = mb + log2f(ltot);
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -588,7 +647,7 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
                                 o[dt][4 * g + 2] * a.keep_scale, o[dt][4 * g + 3] * a.keep_scale);
         const size_t rbase = ((size_t)blockIdx.z * gridDim.y + bh) * a.Lq;
         if (active && h == 0) {
-            a.part_ml[2 * (rbase + q)] = m == -INFINITY ? -INFINITY : m * a.scale2;
+            a.part_ml[2 * (rbase + q)] = ltot > 0.f ? mb : -INFINITY;
             a.part_ml[2 * (rbase + q) + 1] = ltot;
         }
         __syncthreads();
@@ -710,7 +769,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
         const bf16* orow = A.o + ((size_t)qi * a.B + b) * a.so + hh * D;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            qf[s] = *reinterpret_cast<const bf16x8*>(qrow + 16 * s + 8 * h);
+            qf[s] = prescale8(*reinterpret_cast<const bf16x8*>(qrow + 16 * s + 8 * h), a.scale2);
             df[s] = *reinterpret_cast<const bf16x8*>(drow + 16 * s + 8 * h);
             const bf16x8 ov = *reinterpret_cast<const bf16x8*>(orow + 16 * s + 8 * h);
 #pragma unroll
@@ -720,12 +779,15 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
     dsum += __shfl_xor(dsum, 32);
     float lse2 = active ? a.lse[(size_t)bh * a.Lq + qi] : 0.f;
     if (MASK && lse2 == -INFINITY) lse2 = INFINITY;   // no attended key: P = 0
-    // row constants as the initial accumulators (the lane's query): S' = S + s_init gives
-    // p' = exp2(S' scale2) = P / (1 - p) directly, dP' = dP + d_init gives
-    // dS = p' (Z ? dP' : d_init) = P (Z dP / (1 - p) - D): no subtraction per element and the
-    // dropout select is one v_bfi_b32
-    const float s_init = (-lse2 + (DROP ? __log2f(a.keep_scale) : 0.f)) / a.scale2;
+    // row constants of the lane's query added by one more MFMA k-step each (kslots): with the
+    // prescaled queries S' = S scale2 + s_init gives p' = exp2(S') = P / (1 - p) directly,
+    // dP' = dP + d_init gives dS = p' (Z ? dP' : d_init) = P (Z dP / (1 - p) - D): no initial
+    // values, multiply or subtraction per element, and the dropout select is one v_bfi_b32
+    const float s_init = -lse2 + (DROP ? __log2f(a.keep_scale) : 0.f);
     const float d_init = -dsum / a.keep_scale;
+    const bf16x8 k11 = kslots(1.f, 1.f, h == 0);
+    const bf16x8 ks = kslots(bf16_hi(s_init), bf16_lo(s_init), h == 0);
+    const bf16x8 kd = kslots(bf16_hi(d_init), bf16_lo(d_init), h == 0);
     if (active && h == 0 && blockIdx.z == 0) A.dvec[(size_t)bh * a.Lq + qi] = dsum;
     // the forward's query-major drop words of this lane, one per 64-key tile (prefetched a
     // tile ahead with the K / V rows)
@@ -805,9 +867,11 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
                 f32x16 st, dpt;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {   // masked keys: -inf initial scores
-                    st[i] = MASK ? neg_inf_if(s_init, mcur, score_bit(t, i)) : s_init;
-                    dpt[i] = d_init;
+                    st[i] = MASK ? neg_inf_if(0.f, mcur, score_bit(t, i)) : 0.f;
+                    dpt[i] = 0.f;
                 }
+                st = mfma(k11, ks, st);
+                dpt = mfma(k11, kd, dpt);
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
                     const bf16x8 ka = *reinterpret_cast<const bf16x8*>(K + (32 * t + r) * LDK + 16 * s + 8 * h);
@@ -823,8 +887,8 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
                 }
 #pragma unroll
                 for (int i = 0; i < 16; i += 2) {
-                    const float p0 = fast_exp2(st[i] * a.scale2);
-                    const float p1 = fast_exp2(st[i + 1] * a.scale2);
+                    const float p0 = fast_exp2(st[i]);
+                    const float p1 = fast_exp2(st[i + 1]);
                     float dp0 = dpt[i], dp1 = dpt[i + 1];
                     if (DROP) {   // keep bits 8t + (i>>1) (even key), 16 + 8t + (i>>1) (odd key)
                         const uint32_t k0 = bit_mask(kcur, 8 * t + (i >> 1));
@@ -946,7 +1010,10 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
     constexpr int QB = 64;   // queries per LDS tile
     __shared__ __attribute__((aligned(16))) bf16 Qs[2][QB * LDK];
     __shared__ __attribute__((aligned(16))) bf16 Ds[2][QB * LDK];
-    __shared__ __attribute__((aligned(16))) float Ls[2][QB];
+    // per query row: the MFMA k-slot images of -lse2 (Xs) and -D (1 - p) (Xd), bf16 hi / lo in
+    // elements 0, 1 and zeros in 2..15 (a lane of half h reads elements 8h..8h+7)
+    __shared__ __attribute__((aligned(16))) bf16 Xs[2][QB][16];
+    __shared__ __attribute__((aligned(16))) bf16 Xd[2][QB][16];
     __shared__ __attribute__((aligned(16))) float Dv[2][QB];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
@@ -971,10 +1038,16 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
         const bf16* krow = a.k + ((size_t)ki * a.B + b) * a.sk + hh * D;
         const bf16* vrow = a.v + ((size_t)ki * a.B + b) * a.sv + hh * D;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            kf[s] = *reinterpret_cast<const bf16x8*>(krow + 16 * s + 8 * h);
+        for (int s = 0; s < 4; ++s) {   // key rows prescaled: log2-domain scores (see prescale8)
+            kf[s] = prescale8(*reinterpret_cast<const bf16x8*>(krow + 16 * s + 8 * h), a.scale2);
             vf[s] = *reinterpret_cast<const bf16x8*>(vrow + 16 * s + 8 * h);
         }
+    }
+    const bf16x8 k11 = kslots(1.f, 1.f, h == 0);
+    {   // the zero halves (elements 8..15) of both k-slot images, both buffers
+        const int row = tid & 63, bb = (tid >> 6) & 1;
+        bf16* const x = (tid >> 7) ? &Xd[bb][row][8] : &Xs[bb][row][8];
+        *reinterpret_cast<bf16x8*>(x) = kslots(0.f, 0.f, false);
     }
     bf16x8 qr[2], dr[2], orr[2];
     float lr = 0.f, dvr = 0.f;
@@ -1009,8 +1082,8 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
             lr = qq < a.Lq ? a.lse[(size_t)bh * a.Lq + qc] : INFINITY;
             if (MASK && lr == -INFINITY) lr = INFINITY;   // query with no attended key
             if (!OWN_D) dvr = A.dvec[(size_t)bh * a.Lq + qc];
-            // the row constants as the S / dP accumulators' initial values (see the loop)
-            lr = -lr / a.scale2;
+            // the row constants added by the k-slot MFMA step (see the loop)
+            lr = -lr;
             if (!OWN_D) dvr = -dvr / a.keep_scale;
         }
         if (DROP && active) {
@@ -1032,8 +1105,11 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
             *reinterpret_cast<bf16x8*>(&Ds[buf][qq * LDK + 8 * ch]) = dr[c];
         }
         if (tid < QB) {
-            Ls[buf][tid] = lr;
-            if (!OWN_D) Dv[buf][tid] = dvr;
+            *reinterpret_cast<bf16x8*>(&Xs[buf][tid][0]) = kslots(bf16_hi(lr), bf16_lo(lr), true);
+            if (!OWN_D) {
+                Dv[buf][tid] = dvr;
+                *reinterpret_cast<bf16x8*>(&Xd[buf][tid][0]) = kslots(bf16_hi(dvr), bf16_lo(dvr), true);
+            }
         }
         if (OWN_D) {   // 8 lanes per query row, 8 of its 64 dims each
 #pragma unroll
@@ -1044,7 +1120,12 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
                 t += __shfl_xor(t, 1);
                 t += __shfl_xor(t, 2);
                 t += __shfl_xor(t, 4);
-                if ((tid & 7) == 0) Dv[buf][(tid >> 3) + 32 * c] = -t / a.keep_scale;
+                if ((tid & 7) == 0) {
+                    const float dd = -t / a.keep_scale;
+                    Dv[buf][(tid >> 3) + 32 * c] = dd;
+                    *reinterpret_cast<bf16x8*>(&Xd[buf][(tid >> 3) + 32 * c][0]) =
+                        kslots(bf16_hi(dd), bf16_lo(dd), true);
+                }
             }
         }
     };
@@ -1066,27 +1147,30 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
             const bf16* DO = Ds[buf];
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
-                // row constants (per element = query row 8g + 4h + j) as the initial
-                // accumulators: S' = S - lse / scale2 gives P = exp2(S' scale2), dP' = dP - D (1-p)
-                // gives dS = P (Z dP / (1-p) - D) = P (Z ? dP' : -D (1-p)) / (1-p), the 1/(1-p)
-                // applied to dK once at the end as it is to dV
-                float lv[16], dv[16];
+                // row constants (per element = query row 8g + 4h + j) by one k-slot MFMA step
+                // each: S' = S scale2 - lse2 gives P = exp2(S'), dP' = dP - D (1-p) gives
+                // dS = P (Z dP / (1-p) - D) = P (Z ? dP' : -D (1-p)) / (1-p), the 1/(1-p)
+                // applied to dK once at the end as it is to dV; -D (1-p) itself (dv) for the
+                // dropped elements
+                float dv[16];
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     const int qrow = 32 * u + 8 * g + 4 * h;      // rows 4g..4g+3 of the tile
-                    const float4 l4 = *reinterpret_cast<const float4*>(&Ls[buf][qrow]);
                     const float4 d4 = *reinterpret_cast<const float4*>(&Dv[buf][qrow]);
-                    lv[4 * g] = l4.x; lv[4 * g + 1] = l4.y; lv[4 * g + 2] = l4.z; lv[4 * g + 3] = l4.w;
                     dv[4 * g] = d4.x; dv[4 * g + 1] = d4.y; dv[4 * g + 2] = d4.z; dv[4 * g + 3] = d4.w;
                 }
+                const bf16x8 xs = *reinterpret_cast<const bf16x8*>(&Xs[buf][32 * u + r][8 * h]);
+                const bf16x8 xd = *reinterpret_cast<const bf16x8*>(&Xd[buf][32 * u + r][8 * h]);
                 // masked (query, key): -inf initial score
                 const uint32_t msh = MASK ? mc[u] >> (4 * h) : 0u;
                 f32x16 st, dpt;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    st[i] = MASK ? neg_inf_if(lv[i], msh, 8 * (i >> 2) + (i & 3)) : lv[i];
-                    dpt[i] = dv[i];
+                    st[i] = MASK ? neg_inf_if(0.f, msh, 8 * (i >> 2) + (i & 3)) : 0.f;
+                    dpt[i] = 0.f;
                 }
+                st = mfma(xs, k11, st);
+                dpt = mfma(xd, k11, dpt);
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
                     const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Q + (32 * u + r) * LDK + 16 * s + 8 * h);
@@ -1103,7 +1187,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int i = 4 * g + j;
-                        const float p = fast_exp2(st[i] * a.scale2);
+                        const float p = fast_exp2(st[i]);
                         float pk = p, dp = dpt[i];
                         if (DROP) {   // 1/(1-p) applied to dV once at the end
                             const uint32_t km = bit_mask(ksh, 8 * g + j);

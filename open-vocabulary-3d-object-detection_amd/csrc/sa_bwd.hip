@@ -339,15 +339,27 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
 template <int K, int N, bool STATS>
 __global__ __launch_bounds__(512, 1) void sa_dy8_kernel(DyFusedArgs p) {
     constexpr int T8 = 512;
-    constexpr int LDK = K + 8;        // padded LDS rows (bf16)
-    constexpr int LDR = kTile + 8;    // DsT row: one channel n, the tile's 64 rows
+    // LDS images and their strides (bf16 elements), each chosen for conflict-free access by
+    // its reads (MI355X_MICROARCH.md §LDS bank rules; round 3's single padded z image read
+    // transposed with 4-way conflicts, 48.6 M conflict cycles per launch):
+    //   As  (z, 68-dword rows): y3 A operand, ds_read_b128 row reads -> 16 distinct slots
+    //   AsT (z again, 80-dword rows = 16 mod 64): dW3 B operand, ds_read_b64_tr_b16 over 4
+    //       consecutive rows x 16 dwords -> disjoint 16-dword windows
+    //   DsT (dy3^T, 34-dword rows): dW3 A operand ds_read_b64 over 32 consecutive channels ->
+    //       34 n mod 64 distinct; dy3 stores (ds_write_b64, 16 lanes) -> 2n mod 32 distinct
+    //   Ys  (raw y2, 66-dword rows): stats ds_read_b64 over 32 consecutive rows -> distinct
+    constexpr int LDK = K + 8;        // As, W3s
+    constexpr int LDT = K + 32;       // AsT
+    constexpr int LDR = kTile + 4;    // DsT row: one channel n, the tile's 64 rows
+    constexpr int LDY = K + 4;        // Ys
     constexpr int LDW = K + 8;        // W3 image row n
     constexpr int KS = K / 16;
     constexpr int NS = N / 16;
     static_assert(K == 128 && N == 256, "8 waves: 32 y3 columns, 32 dz channels x 32 rows, 32 dW rows");
     __shared__ __attribute__((aligned(16))) bf16 As[kTile * LDK];
+    __shared__ __attribute__((aligned(16))) bf16 AsT[kTile * LDT];
     __shared__ __attribute__((aligned(16))) bf16 DsT[N * LDR];
-    __shared__ __attribute__((aligned(16))) bf16 Ys[STATS ? kTile * LDK : 8];
+    __shared__ __attribute__((aligned(16))) bf16 Ys[STATS ? kTile * LDY : 8];
     __shared__ __attribute__((aligned(16))) bf16 W3s[N * LDW];
     __shared__ float sc[K], sh[K], smu[K], sis[K];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r32 = lane & 31, h = lane >> 5;
@@ -408,7 +420,8 @@ __global__ __launch_bounds__(512, 1) void sa_dy8_kernel(DyFusedArgs p) {
             for (int j = 0; j < 8; ++j)
                 z[j] = (bf16)fmaxf(fmaf(sc[kc + j], (float)pre[c][j], sh[kc + j]), 0.f);
             *reinterpret_cast<bf16x8*>(&As[row * LDK + kc]) = z;
-            if constexpr (STATS) *reinterpret_cast<bf16x8*>(&Ys[row * LDK + kc]) = pre[c];
+            *reinterpret_cast<bf16x8*>(&AsT[row * LDT + kc]) = z;
+            if constexpr (STATS) *reinterpret_cast<bf16x8*>(&Ys[row * LDY + kc]) = pre[c];
         }
         // the pooled gradient of this lane's column (issued before the barrier)
         float gv[2];
@@ -476,7 +489,7 @@ __global__ __launch_bounds__(512, 1) void sa_dy8_kernel(DyFusedArgs p) {
                 for (int j = 0; j < 4; ++j) o[j] = (bf16)acc[4 * g + j];
                 *reinterpret_cast<bf16x4*>(p.dz + (row0 + row) * K + k) = o;
                 if constexpr (STATS) {   // bn_relu_bwd pass 0 on the stored values
-                    const bf16x4 y4 = *reinterpret_cast<const bf16x4*>(&Ys[row * LDK + k]);
+                    const bf16x4 y4 = *reinterpret_cast<const bf16x4*>(&Ys[row * LDY + k]);
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const float yy = (float)y4[j];
@@ -496,7 +509,7 @@ __global__ __launch_bounds__(512, 1) void sa_dy8_kernel(DyFusedArgs p) {
             const bf16x4 hi = *reinterpret_cast<const bf16x4*>(dn + 8);
             const bf16x8 ad = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
-            for (int b = 0; b < K / 32; ++b) dw[b] = mfma(ad, col_operand(As, LDK, lane, 32 * b, s), dw[b]);
+            for (int b = 0; b < K / 32; ++b) dw[b] = mfma(ad, col_operand(AsT, LDT, lane, 32 * b, s), dw[b]);
         }
         PROBE(6);
         __syncthreads();   // As / DsT / Ys are rewritten by the next tile
@@ -505,9 +518,11 @@ __global__ __launch_bounds__(512, 1) void sa_dy8_kernel(DyFusedArgs p) {
     PROBE_END;
     if constexpr (STATS) {
         // the row-block-1 waves hand their partials to the row-block-0 waves of the same channels
-        // (4 channel blocks, 64 lanes, 32) floats = 32 KB: DsT (36.9 KB) holds it, As (17 KB) does not
+        // (4 channel blocks, 64 lanes, 32) floats = 32 KB: DsT (34.8 KB) holds it, As (17 KB) does not
         float* xs = reinterpret_cast<float*>(DsT);
         static_assert(sizeof(DsT) >= 4 * 64 * 32 * sizeof(float), "stats hand-off overruns DsT");
+        static_assert(sizeof(As) + sizeof(AsT) + sizeof(DsT) + sizeof(Ys) + sizeof(W3s) +
+                      4 * K * sizeof(float) <= 160 * 1024, "LDS images exceed the CU's 160 KB");
         if (rbz == 1)
 #pragma unroll
             for (int i = 0; i < 16; ++i) {

@@ -222,12 +222,15 @@ class GradBuckets:
     encoder side).  Every parameter has a fixed view in ONE flat fp32 buffer (static for a
     captured step), a bucket's views are contiguous.  ``launch(i)`` copies bucket i's
     gradients into its views (one launch on the GPU) and starts ONE all-reduce (sum) of that
-    region with ``async_op=True`` on ``group`` — a process group of its own (its own RCCL
-    communicator and stream), so the SyncBatchNorm all-reduces the encoder / SA backward issues
-    on the BN's group are not queued behind it.  ``finish()`` launches what is left, waits for
-    every bucket (the current stream waits on the collectives' streams: capturable) and returns
-    {id(param): averaged-by-the-caller summed gradient view}.  A parameter without a gradient
-    contributes zeros."""
+    region on ``group`` — a process group of its own (its own RCCL communicator and stream), so
+    the SyncBatchNorm all-reduces the encoder / SA backward issues on the BN's group are not
+    queued behind it.  On the GPU the collective is issued from a side stream that first waits
+    for the copy (a plain blocking-call all-reduce there: the process group's watchdog never
+    holds an event recorded inside a graph capture); the current stream runs on.  On the CPU
+    (gloo) it is an ``async_op`` work.  ``finish()`` launches what is left, joins (the current
+    stream waits for the side stream: capturable) and returns {id(param): summed gradient
+    view} (the caller divides by the world size).  A parameter without a gradient contributes
+    zeros."""
 
     def __init__(self, buckets, group=None):
         self.buckets = [list(b) for b in buckets]
@@ -235,6 +238,7 @@ class GradBuckets:
         if len(ids) != len(set(ids)):
             raise ValueError("GradBuckets: a parameter is in two buckets")
         self.group = group
+        self.stream = None
         self.flat = None
         self.views = {}
         self.regions = []
@@ -265,12 +269,20 @@ class GradBuckets:
             else:
                 dst.append(v)
                 src.append(p.grad)
-        if dst and dst[0].is_cuda:
+        if self.flat.is_cuda:
             from . import _native
-            _native.multi_copy(dst, src)
-        else:
-            for d, s in zip(dst, src):
-                d.copy_(s)
+            if dst:
+                _native.multi_copy(dst, src)
+            if self.stream is None:
+                self.stream = torch.cuda.Stream(device=self.flat.device)
+            cur = torch.cuda.current_stream(self.flat.device)
+            self.stream.wait_stream(cur)
+            with torch.cuda.stream(self.stream):
+                dist.all_reduce(self.regions[i], group=self.group)
+            self._works[i] = None
+            return
+        for d, s in zip(dst, src):
+            d.copy_(s)
         self._works[i] = dist.all_reduce(self.regions[i], group=self.group, async_op=True)
 
     def launched(self, i):
@@ -280,7 +292,10 @@ class GradBuckets:
         for i in range(len(self.buckets)):
             self.launch(i)
         for w in self._works.values():
-            w.wait()
+            if w is not None:
+                w.wait()
+        if self.stream is not None:
+            torch.cuda.current_stream(self.flat.device).wait_stream(self.stream)
         self._works.clear()
         return self.views
 
@@ -297,6 +312,7 @@ def stage_after_encoder(model, buckets, flush=None):
 
     def hook():
         flush()
-        buckets.launch(0)
+        if buckets is not None:   # None: the staged flush alone (single-process A/B twin)
+            buckets.launch(0)
     model.encoder_grad_hook = hook
     return hook

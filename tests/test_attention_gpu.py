@@ -28,18 +28,18 @@ def _umul24(x, c):
     return ((x & 0xFFFFFF) * (c & 0xFFFFFF)) & M32
 
 
-def _mix24(x):
+def _drop_mix(x):
+    """attn.hip drop_mix: two 24-bit multiply rounds with 16-bit folds"""
     x = x & M32
     x = x ^ (x >> 16)
     x = _umul24(x, 0x7feb35) ^ (x >> 24)
-    x = x ^ (x >> 15)
-    x = _umul24(x, 0x846ca7) ^ (x >> 24)
     x = x ^ (x >> 16)
-    return x
+    x = _umul24(x, 0x846ca7)
+    return x ^ (x >> 16)
 
 
 def keep_mask(seed, site, B, H, Lq, Lk, p, device):
-    """attn.hip drop_head_mix / drop_query_base / drop_pair (mix24, 16-bit half per key), in
+    """attn.hip drop_head_mix / drop_query_base / drop_mix of the pair, 16-bit half per key, in
     int64 torch arithmetic."""
     s = int(seed)
     lo, hi = s & M32, (s >> 32) & M32
@@ -49,7 +49,7 @@ def keep_mask(seed, site, B, H, Lq, Lk, p, device):
     q = torch.arange(Lq, dtype=torch.int64, device=device)
     qb = _mix32(hm[:, None] ^ ((q[None] * 0xC2B2AE35) & M32))                  # (BH, Lq)
     k = torch.arange(Lk, dtype=torch.int64, device=device)
-    hsh = _mix24(qb[:, :, None] + (((k[None, None] >> 1) * 0x27D4EB2F) & M32))   # (BH, Lq, Lk)
+    hsh = _drop_mix(qb[:, :, None] + (((k[None, None] >> 1) * 0x27D4EB2F) & M32))   # (BH, Lq, Lk)
     half = torch.where((k & 1).bool()[None, None], hsh >> 16, hsh & 0xFFFF)
     thresh = min(int(np.rint(np.float32(p) * np.float32(65536.0))), 65535) if p > 0 else 0
     return ((half ^ 0x8000) >= thresh).view(B, H, Lq, Lk)     # int16(half) >= thresh - 32768

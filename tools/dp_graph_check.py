@@ -12,15 +12,20 @@ sys.path.insert(0, ROOT)
 import ov3d_import  # noqa: E402
 
 
-def run(dp, batches):
+def run(dp, batches, staged):
     import bench
-    from ov3d_amd import gemm, sa_fused
+    from ov3d_amd import dist, gemm, sa_fused
     from ov3d_amd.graphs import StepGraph
     sa_fused.FORCE_SYNC = dp
     args = bench.default_args(enc_dropout=0.0, dec_dropout=0.0, mlp_dropout=0.0)
     args.optim = "fused"
     dev = torch.device("cuda", 0)
-    model, crit, opt = bench.build(args, dev, capturable=True, sync_bn=dp, allreduce=dp)
+    model, crit, opt = bench.build(args, dev, capturable=True, sync_bn=dp, allreduce=dp,
+                                   staged=staged)
+    if staged and not dp:
+        # the same two-stage weight-gradient flush without collectives: the grouped launches
+        # then sum the same problems in the same partition as the bucketed run
+        dist.stage_after_encoder(model, None)
     gemm.DEFER_WGRAD = True
     g = StepGraph(model, crit, opt, batches[0], amp_dtype=torch.bfloat16, clip=0.1)
     for i in range(3):
@@ -37,17 +42,19 @@ def main():
     torch.distributed.init_process_group(backend="nccl", init_method="env://", world_size=1, rank=0)
     from ov3d_amd import synthetic
     batches = [synthetic.make_batch(4, seed=30 + i, device="cuda") for i in range(3)]
-    a = run(False, batches)
-    b = run(True, batches)
     worst = 0.0
-    for k in a:
-        # SyncBN at world 1 == BN, the all-reduce of one rank == identity: equal up to the
-        # reduction order of the flat-buffer path (none: same kernels) -> tight tolerance
-        d = ((a[k] - b[k]).norm() / a[k].norm().clamp_min(1e-12)).item()
-        worst = max(worst, d)
-        assert d < 1e-5, (k, d)
+    for staged in (False, True):   # one all-reduce at the end / two buckets (dist.GradBuckets)
+        a = run(False, batches, staged)
+        b = run(True, batches, staged)
+        for k in a:
+            # SyncBN at world 1 == BN, the all-reduce of one rank == identity: equal up to the
+            # reduction order of the flat-buffer path (none: same kernels) -> tight tolerance
+            d = ((a[k] - b[k]).norm() / a[k].norm().clamp_min(1e-12)).item()
+            worst = max(worst, d)
+            assert d < 1e-5, (staged, k, d)
     torch.distributed.destroy_process_group()
-    print(f"OK dp-graph == single-process graph after 3 steps (max rel diff {worst:.2e})")
+    print(f"OK dp-graph == single-process graph after 3 steps, end-of-step and bucketed "
+          f"all-reduce (max rel diff {worst:.2e})")
 
 
 if __name__ == "__main__":
