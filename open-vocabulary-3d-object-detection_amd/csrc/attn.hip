@@ -452,9 +452,11 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
     int buf = 0;
     for (int kb = kbeg; kb < kend; kb += KB, buf ^= 1) {
         const bool more = kb + KB < kend;
-        if (!active && more) load(kb + KB);
         PROBE(0);
-        if (active) {
+        // every wave computes (a wave past Lq on the clamped query row 0, storing nothing): a
+        // branch around the tile would make the accumulators' loop-carried registers a phi of
+        // two paths, and hipcc then copied o / lacc back every tile (dQ: 32 v_mov per tile)
+        {
             const bf16* K = Ks[buf];
             const bf16* V = Vs[buf];
             if (MASK && more) mw_next = mrow[(size_t)((kb >> 6) + 1) * mtile];
@@ -495,7 +497,7 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
             if (more) load(kb + KB);
             // the previous tile's drop word goes out while the score MFMAs run: the lane
             // transpose's swizzle round trips would otherwise sit on this tile's critical path
-            if (DROP && !BITS && kb > kbeg) store_drop(kb - KB);
+            if (DROP && !BITS && kb > kbeg && active) store_drop(kb - KB);
             PROBE(1);
             // keys past Lk (last partial tile) do not take part
             const int nvalid = kend - kb;
@@ -908,7 +910,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
                     for (int s = 0; s < 2; ++s)
                         dqt[dt] = mfma(v_operand(K, lane, dt, t, s), __builtin_bit_cast(bf16x8, dsw[t][s]), dqt[dt]);
         };
-        if (active) {
+        {   // every wave (see attn_fwd_body: no branch around the accumulators)
             if constexpr (RAGGED) {
                 if (kend - kb < KB) tile(std::true_type{});
                 else tile(std::false_type{});
@@ -1142,7 +1144,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
     for (int qb = 0; qb < a.Lq; qb += QB, buf ^= 1) {
         const bool more = qb + QB < a.Lq;
         if (more) load(qb + QB);
-        if (active) {
+        {   // every wave (see attn_fwd_body: no branch around the accumulators)
             const bf16* Q = Qs[buf];
             const bf16* DO = Ds[buf];
 #pragma unroll
