@@ -1012,10 +1012,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
     constexpr int QB = 64;   // queries per LDS tile
     __shared__ __attribute__((aligned(16))) bf16 Qs[2][QB * LDK];
     __shared__ __attribute__((aligned(16))) bf16 Ds[2][QB * LDK];
-    // per query row: the MFMA k-slot images of -lse2 (Xs) and -D (1 - p) (Xd), bf16 hi / lo in
-    // elements 0, 1 and zeros in 2..15 (a lane of half h reads elements 8h..8h+7)
-    __shared__ __attribute__((aligned(16))) bf16 Xs[2][QB][16];
-    __shared__ __attribute__((aligned(16))) bf16 Xd[2][QB][16];
+    __shared__ __attribute__((aligned(16))) float Ls[2][QB];
     __shared__ __attribute__((aligned(16))) float Dv[2][QB];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
@@ -1045,12 +1042,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
             vf[s] = *reinterpret_cast<const bf16x8*>(vrow + 16 * s + 8 * h);
         }
     }
-    const bf16x8 k11 = kslots(1.f, 1.f, h == 0);
-    {   // the zero halves (elements 8..15) of both k-slot images, both buffers
-        const int row = tid & 63, bb = (tid >> 6) & 1;
-        bf16* const x = (tid >> 7) ? &Xd[bb][row][8] : &Xs[bb][row][8];
-        *reinterpret_cast<bf16x8*>(x) = kslots(0.f, 0.f, false);
-    }
+
     bf16x8 qr[2], dr[2], orr[2];
     float lr = 0.f, dvr = 0.f;
     // per-thread offsets of query row tid>>3, advanced per tile by qb * B * s (scalar unit)
@@ -1084,7 +1076,8 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
             lr = qq < a.Lq ? a.lse[(size_t)bh * a.Lq + qc] : INFINITY;
             if (MASK && lr == -INFINITY) lr = INFINITY;   // query with no attended key
             if (!OWN_D) dvr = A.dvec[(size_t)bh * a.Lq + qc];
-            // the row constants added by the k-slot MFMA step (see the loop)
+            // the row constants as the S / dP accumulators' initial values (see the loop); the
+            // key rows are prescaled, so S is in the log2 domain and so is -lse2
             lr = -lr;
             if (!OWN_D) dvr = -dvr / a.keep_scale;
         }
@@ -1107,11 +1100,8 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
             *reinterpret_cast<bf16x8*>(&Ds[buf][qq * LDK + 8 * ch]) = dr[c];
         }
         if (tid < QB) {
-            *reinterpret_cast<bf16x8*>(&Xs[buf][tid][0]) = kslots(bf16_hi(lr), bf16_lo(lr), true);
-            if (!OWN_D) {
-                Dv[buf][tid] = dvr;
-                *reinterpret_cast<bf16x8*>(&Xd[buf][tid][0]) = kslots(bf16_hi(dvr), bf16_lo(dvr), true);
-            }
+            Ls[buf][tid] = lr;
+            if (!OWN_D) Dv[buf][tid] = dvr;
         }
         if (OWN_D) {   // 8 lanes per query row, 8 of its 64 dims each
 #pragma unroll
@@ -1122,12 +1112,7 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
                 t += __shfl_xor(t, 1);
                 t += __shfl_xor(t, 2);
                 t += __shfl_xor(t, 4);
-                if ((tid & 7) == 0) {
-                    const float dd = -t / a.keep_scale;
-                    Dv[buf][(tid >> 3) + 32 * c] = dd;
-                    *reinterpret_cast<bf16x8*>(&Xd[buf][(tid >> 3) + 32 * c][0]) =
-                        kslots(bf16_hi(dd), bf16_lo(dd), true);
-                }
+                if ((tid & 7) == 0) Dv[buf][(tid >> 3) + 32 * c] = -t / a.keep_scale;
             }
         }
     };
@@ -1149,30 +1134,29 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
             const bf16* DO = Ds[buf];
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
-                // row constants (per element = query row 8g + 4h + j) by one k-slot MFMA step
-                // each: S' = S scale2 - lse2 gives P = exp2(S'), dP' = dP - D (1-p) gives
-                // dS = P (Z dP / (1-p) - D) = P (Z ? dP' : -D (1-p)) / (1-p), the 1/(1-p)
-                // applied to dK once at the end as it is to dV; -D (1-p) itself (dv) for the
-                // dropped elements
-                float dv[16];
+                // row constants (per element = query row 8g + 4h + j) as the initial
+                // accumulators: S' = S scale2 - lse2 gives P = exp2(S') (prescaled keys), dP' =
+                // dP - D (1-p) gives dS = P (Z dP / (1-p) - D) = P (Z ? dP' : -D (1-p)) / (1-p),
+                // the 1/(1-p) applied to dK once at the end as it is to dV.  (Here the initial
+                // values stay: the k-slot MFMA step of the dQ pass lengthened this pass's chains
+                // and measured slower, 109 -> 113 us.)
+                float lv[16], dv[16];
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     const int qrow = 32 * u + 8 * g + 4 * h;      // rows 4g..4g+3 of the tile
+                    const float4 l4 = *reinterpret_cast<const float4*>(&Ls[buf][qrow]);
                     const float4 d4 = *reinterpret_cast<const float4*>(&Dv[buf][qrow]);
+                    lv[4 * g] = l4.x; lv[4 * g + 1] = l4.y; lv[4 * g + 2] = l4.z; lv[4 * g + 3] = l4.w;
                     dv[4 * g] = d4.x; dv[4 * g + 1] = d4.y; dv[4 * g + 2] = d4.z; dv[4 * g + 3] = d4.w;
                 }
-                const bf16x8 xs = *reinterpret_cast<const bf16x8*>(&Xs[buf][32 * u + r][8 * h]);
-                const bf16x8 xd = *reinterpret_cast<const bf16x8*>(&Xd[buf][32 * u + r][8 * h]);
                 // masked (query, key): -inf initial score
                 const uint32_t msh = MASK ? mc[u] >> (4 * h) : 0u;
                 f32x16 st, dpt;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    st[i] = MASK ? neg_inf_if(0.f, msh, 8 * (i >> 2) + (i & 3)) : 0.f;
-                    dpt[i] = 0.f;
+                    st[i] = MASK ? neg_inf_if(lv[i], msh, 8 * (i >> 2) + (i & 3)) : lv[i];
+                    dpt[i] = dv[i];
                 }
-                st = mfma(xs, k11, st);
-                dpt = mfma(xd, k11, dpt);
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
                     const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Q + (32 * u + r) * LDK + 16 * s + 8 * h);
