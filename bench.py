@@ -520,10 +520,13 @@ def main():
         use_ms = fwd_in if fwd_in else fwd_ms
         ach = fl_fwd / (use_ms * 1e-3) / 1e12
         traffic, tsrc = None, None
-        pmc = os.path.join(ROOT, "profiles", "r03_attn_pmc.json")
-        if os.path.exists(pmc) and (cli.batch, L, H) == (8, 2048, 4) and dataset == "sunrgbd":
-            traffic = json.load(open(pmc)).get("fwd_traffic_bytes_per_launch")
-            tsrc = "profiles/r03_attn_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)"
+        # the latest PMC record of the shipped kernel (tools/attn_traffic.py over gpu_pmc.sh)
+        for rec_name in ("r04_attn_pmc.json", "r03_attn_pmc.json"):
+            pmc = os.path.join(ROOT, "profiles", rec_name)
+            if os.path.exists(pmc) and (cli.batch, L, H) == (8, 2048, 4) and dataset == "sunrgbd":
+                traffic = json.load(open(pmc)).get("fwd_traffic_bytes_per_launch")
+                tsrc = f"profiles/{rec_name} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)"
+                break
         kname = "attn_fwd_kernel (encoder self-attention, B=%d H=%d L=%d d=64, dropout %.1f%s)" % (
             cli.batch, H, L, args.enc_dropout, ", radius mask" if dataset == "scannet" else "")
         roof = {"bound": "mfma", "achieved": round(ach, 1), "peak": BF16_DENSE_PEAK_TFLOPS,
