@@ -745,12 +745,32 @@ int ov3d_rows_gemm_act(int M, int N, int K, const void* A, long long lda, const 
  * Replaces the library GEMMs under F.linear / the input-gradient matmul of
  * models/transformer.py:262-278 (M = batch * 2048 points).  Same contract as
  * ov3d_rows_gemm (trans_b = 1: C = A W^T + bias; trans_b = 0: C = A W, bias NULL), with a
- * 128 x 128 output tile per workgroup: N % 128 == 0, K % 64 == 0; 16-byte aligned A / W,
- * lda / ldw % 8 == 0; bias (N) bf16 or NULL. */
+ * 128 (or 64) x 128 output tile per workgroup: N % 128 == 0, K % 64 == 0; 16-byte aligned
+ * A / W / C, lda / ldw / ldc % 8 == 0; bias (N) bf16, 8-byte aligned, or NULL.
+ * Also the decoder's memory K/V projections (models/transformer.py:355-379, all layers in one
+ * N = layers x 256 GEMM) and the heads' 8192-row layers. */
 int ov3d_tile_gemm_supported(int M, int N, int K);
 int ov3d_tile_gemm(int M, int N, int K, const void* A, long long lda, const void* W,
                    long long ldw, int trans_b, const void* bias, void* C, long long ldc,
                    void* stream);
+/* with the FFN activation epilogues of ov3d_rows_gemm_act (1: dropout(relu(.)), 2: the
+ * masked input gradient; H 8-byte aligned, ldh % 4 == 0): the encoder's FFN */
+int ov3d_tile_gemm_act(int M, int N, int K, const void* A, long long lda, const void* W,
+                       long long ldw, int trans_b, const void* bias, int epilogue,
+                       float dropout_p, const int64_t* seed, int site, const void* H,
+                       long long ldh, void* C, long long ldc, void* stream);
+/* C = A1 op(W1) + A2 op(W2) in one launch (K1, K2 each a multiple of 64; no bias): the
+ * memory gradient of the decoder's batched K / V projections, d memory = dK Wk + dV Wv
+ * (models/transformer.py:365-372 backward) */
+int ov3d_tile_gemm2(int M, int N, int K1, const void* A1, long long lda1, const void* W1,
+                    long long ldw1, int K2, const void* A2, long long lda2, const void* W2,
+                    long long ldw2, int trans_b, void* C, long long ldc, void* stream);
+/* batch independent products C_b = A_b op(W_b) (no bias), operands at element strides
+ * sA / sW / sC per batch (multiples of 8, sC >= M * ldc): the heads' per-head second layer
+ * and its input gradient (models/helpers.py GenericMLP x 5 heads, torch.bmm in heads.py) */
+int ov3d_tile_gemm_batched(int batch, int M, int N, int K, const void* A, long long lda,
+                           long long sA, const void* W, long long ldw, long long sW, int trans_b,
+                           void* C, long long ldc, long long sC, void* stream);
 
 /* ---- SUN RGB-D training-data pipeline on the device (csrc/sunaug.hip) ----
  * Replaces SunrgbdDetectionDataset.__getitem__ (datasets/sunrgbd.py:256-462, use_color /

@@ -95,6 +95,9 @@ _SIGS = {
     "ov3d_rows_gemm_act": "iiiplplipifpiplplp",
     "ov3d_rows_gemm_group": "iipip",
     "ov3d_tile_gemm": "iiiplplipplp",
+    "ov3d_tile_gemm_act": "iiiplplipifpiplplp",
+    "ov3d_tile_gemm2": "iiiplpliplpliplp",
+    "ov3d_tile_gemm_batched": "iiiipllpllipllp",
     "ov3d_sun_aug_points": "pilippiipippp",
     "ov3d_sun_aug_boxes": "plpppiipipippp",
     "ov3d_sun_cuboid_eval": "piipppiiippippppp",

@@ -121,16 +121,97 @@ def _tile_gemm_ok(a, w, trans_b):
     return bool(_native.load().ov3d_tile_gemm_supported(M, N, K))
 
 
-def tile_gemm(a, w, bias=None, trans_b=True):
-    """as rows_gemm, on the 128 x 128-tile kernel (check _tile_gemm_ok first)"""
+def tile_gemm(a, w, bias=None, trans_b=True, out=None):
+    """as rows_gemm, on the long row-block kernel (check _tile_gemm_ok first); `out` an (M, N)
+    bf16 row view (stride(1) == 1, 16-byte aligned, row stride % 8 == 0) or None"""
+    from . import _native
+    M, K = a.shape
+    N = w.shape[0] if trans_b else w.shape[1]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    if bias is not None and (bias.dtype != torch.bfloat16 or not bias.is_contiguous()
+                             or bias.data_ptr() % 8):   # 8-byte bias pieces
+        bias = bias.to(torch.bfloat16).contiguous().clone()
+    _native.call("ov3d_tile_gemm", M, N, K, a, a.stride(0), w, w.stride(0), int(trans_b), bias,
+                 out, out.stride(0), like=a)
+    return out
+
+
+def tile_out_ok(out):
+    return (out.dtype == torch.bfloat16 and out.dim() == 2 and out.stride(1) == 1
+            and out.stride(0) % 8 == 0 and out.data_ptr() % 16 == 0)
+
+
+def tile_bmm_ok(a, w, trans_b):
+    """a (B, M, K) x w (B, N, K) (trans_b) / (B, K, N) on the long row-block kernel"""
+    if not (TILE_GEMM and a.is_cuda and a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and a.dim() == 3 and w.dim() == 3 and a.shape[0] == w.shape[0]
+            and a.stride(2) == 1 and w.stride(2) == 1):
+        return False
+    B, M, K = a.shape
+    N = w.shape[1] if trans_b else w.shape[2]
+    if M <= ROWS_GEMM_MAX_M or (w.shape[2] if trans_b else w.shape[1]) != K:
+        return False
+    if (a.data_ptr() % 16 or w.data_ptr() % 16 or any(x % 8 for x in a.stride()[:2] + w.stride()[:2])):
+        return False
+    from . import _native
+    return bool(_native.load().ov3d_tile_gemm_supported(M, N, K))
+
+
+def tile_bmm(a, w, trans_b):
+    """torch.bmm(a, w.transpose(1, 2) if trans_b else w) -> (B, M, N) bf16, one launch"""
+    from . import _native
+    B, M, K = a.shape
+    N = w.shape[1] if trans_b else w.shape[2]
+    out = torch.empty((B, M, N), dtype=torch.bfloat16, device=a.device)
+    _native.call("ov3d_tile_gemm_batched", B, M, N, K, a, a.stride(1), a.stride(0), w, w.stride(1),
+                 w.stride(0), int(trans_b), out, N, M * N, like=a)
+    return out
+
+
+def _aligned_bias(b):
+    if b is not None and (b.dtype != torch.bfloat16 or not b.is_contiguous() or b.data_ptr() % 8):
+        b = b.to(torch.bfloat16).contiguous().clone()
+    return b
+
+
+def shape_ok(M, N, K):
+    """a (M, K) x (K, N) product on fresh contiguous bf16 rows runs on rows_gemm or tile_gemm"""
+    from . import _native
+    lib = _native.load()
+    if ROWS_GEMM and M <= ROWS_GEMM_MAX_M:
+        return bool(lib.ov3d_rows_gemm_supported(M, N, K))
+    return TILE_GEMM and M > ROWS_GEMM_MAX_M and bool(lib.ov3d_tile_gemm_supported(M, N, K))
+
+
+def act_gemm_ok(a, w, trans_b):
+    """rows_gemm / tile_gemm can run a (M, K) x w product with an activation epilogue"""
+    return _rows_gemm_ok(a, w, trans_b) or _tile_gemm_ok(a, w, trans_b)
+
+
+def act_gemm(a, w, bias=None, trans_b=True, epilogue=0, p=0.0, seed=None, site=0, h=None):
+    """(M, N) bf16 = a (M, K) x w (w (N, K) when trans_b, else (K, N)) + bias, with the FFN
+    epilogue (0 none, 1 dropout_p(relu(.)), 2 h > 0 ? . / (1 - p) : 0) on the short row-block
+    kernel (M <= ROWS_GEMM_MAX_M) or the long one; check act_gemm_ok first"""
     from . import _native
     M, K = a.shape
     N = w.shape[0] if trans_b else w.shape[1]
     out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
-    if bias is not None and (bias.dtype != torch.bfloat16 or not bias.is_contiguous()):
-        bias = bias.to(torch.bfloat16).contiguous()
-    _native.call("ov3d_tile_gemm", M, N, K, a, a.stride(0), w, w.stride(0), int(trans_b), bias,
+    name = "ov3d_rows_gemm_act" if _rows_gemm_ok(a, w, trans_b) else "ov3d_tile_gemm_act"
+    _native.call(name, M, N, K, a, a.stride(0), w, w.stride(0), int(trans_b), _aligned_bias(bias),
+                 int(epilogue), float(p), seed, int(site), h, h.stride(0) if h is not None else 0,
                  out, N, like=a)
+    return out
+
+
+def tile_gemm2(a1, w1, a2, w2):
+    """a1 w1 + a2 w2 (input-gradient layout: w (K, N)) in one launch of the long row-block
+    kernel (check _tile_gemm_ok on both pairs first)"""
+    from . import _native
+    M, N = a1.shape[0], w1.shape[1]
+    out = torch.empty((M, N), dtype=torch.bfloat16, device=a1.device)
+    _native.call("ov3d_tile_gemm2", M, N, a1.shape[1], a1, a1.stride(0), w1, w1.stride(0),
+                 a2.shape[1], a2, a2.stride(0), w2, w2.stride(0), 0, out, N, like=a1)
     return out
 
 

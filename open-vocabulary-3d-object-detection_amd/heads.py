@@ -212,7 +212,8 @@ class _Heads(torch.autograd.Function):
         w2 = st["w2_bf"].view(5, H, H)
         bn1, bn2 = pack.bns()
         torch._foreach_add_([b.num_batches_tracked for b in bn1 + bn2], 1)
-        h1 = xb @ w1.t()                                                         # (R, 5H)
+        h1 = (gemm.tile_gemm(xb, w1) if gemm._tile_gemm_ok(xb, w1, True)
+              else xb @ w1.t())                                                  # (R, 5H)
         rowmajor = (H5, 0, H5)
         m1, i1, a1, s1 = _stats_finalize(h1, rowmajor, R, H5, st["g1"], st["b1"], bn1, st["rm1"],
                                          st["rv1"])
@@ -223,7 +224,8 @@ class _Heads(torch.autograd.Function):
         z1 = torch.empty((5, R, H), dtype=bf, device=dev)
         nat.call("ov3d_rows_bn_apply", h1, 1, *rowmajor, R, H5, a1, s1, float(p1), seed,
                  pack.sites[0], z1, *headmajor, like=x)
-        h2 = torch.bmm(z1, w2.transpose(1, 2))                                  # (5, R, H)
+        h2 = (gemm.tile_bmm(z1, w2, True) if gemm.tile_bmm_ok(z1, w2, True)
+              else torch.bmm(z1, w2.transpose(1, 2)))                           # (5, R, H)
         m2, i2, a2, s2 = _stats_finalize(h2, headmajor, R, H5, st["g2"], st["b2"], bn2, st["rm2"],
                                          st["rv2"])
         z2 = torch.empty((R, H5), dtype=bf, device=dev)
@@ -285,7 +287,10 @@ class _Heads(torch.autograd.Function):
                  gs, Ns, 4, ctypes.addressof(ws), ctypes.addressof(lay["n"]),
                  ctypes.addressof(lay["kcol"]), ctypes.addressof(lay["ocol"]), gvb, gsb, dz2, H5,
                  like=xb)
-        torch.mm(gvb, w3v, out=dz2[:, :H])
+        if gemm._tile_gemm_ok(gvb, w3v, False) and gemm.tile_out_ok(dz2[:, :H]):
+            gemm.tile_gemm(gvb, w3v, trans_b=False, out=dz2[:, :H])
+        else:
+            torch.mm(gvb, w3v, out=dz2[:, :H])
         # weight gradients: queued for the grouped launch at the end of the backward
         # (gemm.DEFER_WGRAD) as one problem per head parameter, else computed here
         P = pack.parts
@@ -315,7 +320,8 @@ class _Heads(torch.autograd.Function):
             dw2 = torch.empty((5, H, H), dtype=torch.float32, device=dev)
             for i in range(5):
                 fused_weight_grad(dh2[i], z1[i], bias=False, out_w=dw2[i])
-        dz1 = torch.bmm(dh2, w2)                                                 # (5, R, H)
+        dz1 = (gemm.tile_bmm(dh2, w2, False) if gemm.tile_bmm_ok(dh2, w2, False)
+               else torch.bmm(dh2, w2))                                          # (5, R, H)
         dh1 = torch.empty((R, H5), dtype=bf, device=dev)
         dg1, dbe1 = _bn_backward(dz1, headmajor, h1, rowmajor, R, H5, st["g1"], m1, i1, a1, s1, p1,
                                  seed, pack.sites[0], dh1, rowmajor, bn=pack.bns()[0][0])
@@ -324,7 +330,8 @@ class _Heads(torch.autograd.Function):
                 gemm.defer_weight_grad(dh1[:, i * H:(i + 1) * H], xb, P[i][0].weight)
         else:
             dw1, _ = fused_weight_grad(dh1, xb, bias=False)
-        dx = (dh1 @ w1).to(xdt)
+        dx = (gemm.tile_gemm(dh1, w1, trans_b=False) if gemm._tile_gemm_ok(dh1, w1, False)
+              else dh1 @ w1).to(xdt)
         grads = {"g1": dg1, "b1": dbe1, "g2": dg2, "b2": dbe2}
         if not defer:
             grads.update({"w1": dw1.view(-1), "w2": dw2.view(-1)})

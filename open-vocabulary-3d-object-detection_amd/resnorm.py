@@ -325,11 +325,9 @@ class _FFN(torch.autograd.Function):
         w1c, b1c = gemm.cast_param(w1, bf), gemm.cast_param(b1, bf)
         w2c, b2c = gemm.cast_param(w2, bf), gemm.cast_param(b2, bf)
         M, F, N = xc.shape[0], w1c.shape[0], w2c.shape[0]
-        h = torch.empty((M, F), dtype=bf, device=x.device)
         seed = flash._seed(x.device) if p > 0 else None
-        _native.call("ov3d_rows_gemm_act", M, F, C, xc, xc.stride(0), w1c, w1c.stride(0), 1,
-                     _bias(b1c), 1, float(p), seed, site, None, 0, h, F, like=xc)
-        y = gemm.rows_gemm(h, w2c, _bias(b2c), trans_b=True)
+        h = gemm.act_gemm(xc, w1c, _bias(b1c), True, 1, p, seed, site)
+        y = gemm.act_gemm(h, w2c, _bias(b2c), True)
         ctx.save_for_backward(xc, h, w1c, w2c)
         ctx.params = (w1, b1, w2, b2)
         ctx.meta = (float(p), x.shape, x.dtype)
@@ -343,12 +341,10 @@ class _FFN(torch.autograd.Function):
         need = ctx.needs_input_grad
         M, F, N = h.shape[0], h.shape[1], w2c.shape[0]
         dy = dy.reshape(-1, N).to(torch.bfloat16).contiguous()
-        dy1 = torch.empty((M, F), dtype=torch.bfloat16, device=dy.device)
-        _native.call("ov3d_rows_gemm_act", M, F, N, dy, N, w2c, w2c.stride(0), 0, None, 2, float(p),
-                     None, 0, h, F, dy1, F, like=dy)
+        dy1 = gemm.act_gemm(dy, w2c, None, False, 2, p, h=h)
         dw2, db2 = gemm.linear_weight_grads(dy, h, w2, b2, need[3], need[4])
         dw1, db1 = gemm.linear_weight_grads(dy1, xc, w1, b1, need[1], need[2])
-        dx = gemm.rows_gemm(dy1, w1c, trans_b=False).to(xdt).view(xshape) if need[0] else None
+        dx = gemm.act_gemm(dy1, w1c, None, False).to(xdt).view(xshape) if need[0] else None
         return dx, dw1, db1, dw2, db2, None, None
 
 
@@ -372,14 +368,14 @@ def ffn_weights_ok(x, w1, w2):
     xr = x.reshape(-1, x.shape[-1])
     bf = torch.bfloat16
     w1c, w2c = gemm.cast_param(w1, bf), gemm.cast_param(w2, bf)
-    if not (gemm._rows_gemm_ok(xr, w1c, True) and w2c.stride(1) == 1 and w2c.stride(0) % 8 == 0
+    if not (gemm.act_gemm_ok(xr, w1c, True) and w2c.stride(1) == 1 and w2c.stride(0) % 8 == 0
             and w2c.data_ptr() % 16 == 0 and w2c.shape[1] == w1c.shape[0]):
         return False
     # the launches on the fresh (contiguous) h / dy / dy1 rows: linear2, its input gradient
-    # (output F columns over N), linear1's input gradient (C columns over F)
+    # (output F columns over N), linear1's input gradient (C columns over F); the short
+    # row-block kernel or the long one, as gemm.act_gemm picks
     M, C, F, N = xr.shape[0], xr.shape[1], w1c.shape[0], w2c.shape[0]
-    ok = _native.load().ov3d_rows_gemm_supported
-    return bool(ok(M, N, F) and ok(M, F, N) and ok(M, C, F))
+    return gemm.shape_ok(M, N, F) and gemm.shape_ok(M, F, N) and gemm.shape_ok(M, C, F)
 
 
 def ffn(x, linear1, linear2, activation, dropout, site):

@@ -139,8 +139,12 @@ class _MemoryKV(torch.autograd.Function):
             srcs += [wc[E:2 * E], wc[2 * E:], bc[E:2 * E], bc[2 * E:]]
             dsts += [Wk[rows], Wv[rows], bk[rows], bv[rows]]
         _native.multi_copy(dsts, srcs)
-        K_all = torch.addmm(bk, mpos, Wk.t()).view(S, B, n)
-        V_all = torch.addmm(bv, mem, Wv.t()).view(S, B, n)
+        if gemm._tile_gemm_ok(mpos, Wk, True) and gemm._tile_gemm_ok(mem, Wv, True):
+            K_all = gemm.tile_gemm(mpos, Wk, bk, trans_b=True).view(S, B, n)
+            V_all = gemm.tile_gemm(mem, Wv, bv, trans_b=True).view(S, B, n)
+        else:
+            K_all = torch.addmm(bk, mpos, Wk.t()).view(S, B, n)
+            V_all = torch.addmm(bv, mem, Wv.t()).view(S, B, n)
         dK, dV = torch.empty_like(K_all), torch.empty_like(V_all)
         flash.defer_kv_grads(dK)   # the layers' dK / dV run batched in this op's backward
         token = torch.empty((), dtype=torch.float32, device=memory.device)
@@ -161,9 +165,12 @@ class _MemoryKV(torch.autograd.Function):
         dK, dV = (t.view(R, L * E) for t in ctx.bufs)
         params = ctx.params
         with torch.autocast("cuda", enabled=False):
-            dmk = dK @ Wk
-            # in place when dmk is not also pos's gradient (no copy of dmk into a new output)
-            dmem = dmk.addmm_(dV, Wv) if not pos_grad else dV @ Wv + dmk
+            if not pos_grad and gemm._tile_gemm_ok(dK, Wk, False) and gemm._tile_gemm_ok(dV, Wv, False):
+                dmem = gemm.tile_gemm2(dK, Wk, dV, Wv)   # dK Wk + dV Wv in one launch
+            else:
+                dmk = dK @ Wk
+                # in place when dmk is not also pos's gradient (no copy of dmk into a new output)
+                dmem = dmk.addmm_(dV, Wv) if not pos_grad else dV @ Wv + dmk
             grads = [None] * len(params)
             for l in range(L):
                 w, b = params[2 * l], params[2 * l + 1]

@@ -75,3 +75,76 @@ def test_rows_linear_uses_tile_gemm_and_matches_library(cuda, monkeypatch):
     assert res[True][4] == 2 and res[False][4] == 0     # forward + input gradient
     for a, b in zip(res[True][:4], res[False][:4]):
         assert ((a - b).norm() / b.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_tile_gemm_ffn_epilogues_match_row_kernels(cuda, p):
+    """the FFN epilogues (dropout(relu(.)) forward, the masked input gradient backward) equal the
+    plain GEMM followed by the resnorm.hip row kernels bit for bit (same keep hash)"""
+    from ov3d_amd import _native, gemm
+    from ov3d_amd import attention as flash
+    M, C, F = 16384, 256, 128
+    g = torch.Generator(device=cuda).manual_seed(5)
+    x = torch.randn(M, C, device=cuda, generator=g).to(torch.bfloat16)
+    w1 = (torch.randn(F, C, device=cuda, generator=g) / C ** 0.5).to(torch.bfloat16)
+    b1 = torch.randn(F, device=cuda, generator=g).to(torch.bfloat16)
+    seed = flash._seed(cuda) if p > 0 else None
+    site = 1234
+    assert gemm.act_gemm_ok(x, w1, True) and not gemm._rows_gemm_ok(x, w1, True)
+    h = gemm.act_gemm(x, w1, b1, True, 1, p, seed, site)
+    y = gemm.tile_gemm(x, w1, b1, trans_b=True)
+    h_ref = torch.empty_like(y)
+    _native.call("ov3d_relu_dropout_fwd", y, M, F, float(p), seed, site, h_ref, like=y)
+    assert torch.equal(h, h_ref)
+    if p > 0:
+        frac = (h == 0).float().mean().item()
+        assert 0.5 < frac < 0.65   # relu zeros about half, dropout 10 % of the rest
+    # backward: dy (M, C) through linear2 (C, F) -> masked (M, F)
+    w2 = (torch.randn(C, F, device=cuda, generator=g) / F ** 0.5).to(torch.bfloat16)
+    dy = torch.randn(M, C, device=cuda, generator=g).to(torch.bfloat16)
+    d1 = gemm.act_gemm(dy, w2, None, False, 2, p, h=h)
+    raw = gemm.tile_gemm(dy, w2, trans_b=False)
+    d1_ref = torch.empty_like(raw)
+    _native.call("ov3d_relu_dropout_bwd", h, raw, h.numel(), float(p), d1_ref, like=h)
+    assert torch.equal(d1, d1_ref)
+
+
+def test_tile_gemm2_sums_two_products(cuda):
+    """dK Wk + dV Wv in one launch (the decoder memory gradient) vs the fp32 sum"""
+    from ov3d_amd import gemm
+    g = torch.Generator(device=cuda).manual_seed(9)
+    M, N, K = 16384, 256, 2048
+    a1, a2 = (torch.randn(M, K, device=cuda, generator=g).to(torch.bfloat16) for _ in range(2))
+    w1, w2 = ((torch.randn(K, N, device=cuda, generator=g) / K ** 0.5).to(torch.bfloat16)
+              for _ in range(2))
+    out = gemm.tile_gemm2(a1, w1, a2, w2)
+    ref = a1.float() @ w1.float() + a2.float() @ w2.float()
+    lib = (a1 @ w1).addmm_(a2, w2)
+    _check(out, ref, lib)
+
+
+@pytest.mark.parametrize("trans_b", [True, False])
+def test_tile_bmm_heads_shapes(cuda, trans_b):
+    """the heads' per-head second layer (5 x (8192 x 256) x (256 x 256)) and its input gradient
+    as one batched launch vs the fp32 products"""
+    from ov3d_amd import gemm
+    g = torch.Generator(device=cuda).manual_seed(11)
+    a = torch.randn(5, 8192, 256, device=cuda, generator=g).to(torch.bfloat16)
+    w = (torch.randn(5, 256, 256, device=cuda, generator=g) / 16).to(torch.bfloat16)
+    assert gemm.tile_bmm_ok(a, w, trans_b)
+    out = gemm.tile_bmm(a, w, trans_b)
+    wt = w.transpose(1, 2) if trans_b else w
+    _check(out, torch.bmm(a.float(), wt.float()), torch.bmm(a, wt))
+
+
+def test_tile_gemm_into_strided_output(cuda):
+    """the visual head's input gradient written into the first 256 columns of 1280-wide rows"""
+    from ov3d_amd import gemm
+    g = torch.Generator(device=cuda).manual_seed(12)
+    a = torch.randn(8192, 640, device=cuda, generator=g).to(torch.bfloat16)
+    w = (torch.randn(640, 256, device=cuda, generator=g) / 25).to(torch.bfloat16)
+    big = torch.full((8192, 1280), 7.0, device=cuda, dtype=torch.bfloat16)
+    assert gemm._tile_gemm_ok(a, w, False) and gemm.tile_out_ok(big[:, :256])
+    gemm.tile_gemm(a, w, trans_b=False, out=big[:, :256])
+    _check(big[:, :256], a.float() @ w.float(), a @ w)
+    assert bool((big[:, 256:] == 7.0).all())
