@@ -401,6 +401,7 @@ def main():
         os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                           MASTER_PORT=os.environ.get("MASTER_PORT", "29517"))
         torch.cuda.set_device(0)
+        dist.capture_safe_env()
         torch.distributed.init_process_group(backend="nccl", init_method="env://", world_size=1,
                                              rank=0)
     rank, world, local = dist.init_from_env()

@@ -746,7 +746,7 @@ int ov3d_rows_gemm_act(int M, int N, int K, const void* A, long long lda, const 
  * models/transformer.py:262-278 (M = batch * 2048 points).  Same contract as
  * ov3d_rows_gemm (trans_b = 1: C = A W^T + bias; trans_b = 0: C = A W, bias NULL), with a
  * 128 (or 64) x 128 output tile per workgroup: N % 128 == 0, K % 64 == 0; 16-byte aligned
- * A / W / C, lda / ldw / ldc % 8 == 0; bias (N) bf16, 8-byte aligned, or NULL.
+ * A / W / C, lda / ldw / ldc % 8 == 0; bias (N <= 2048) bf16, 8-byte aligned, or NULL.
  * Also the decoder's memory K/V projections (models/transformer.py:355-379, all layers in one
  * N = layers x 256 GEMM) and the heads' 8192-row layers. */
 int ov3d_tile_gemm_supported(int M, int N, int K);
@@ -759,7 +759,8 @@ int ov3d_tile_gemm_act(int M, int N, int K, const void* A, long long lda, const 
                        long long ldw, int trans_b, const void* bias, int epilogue,
                        float dropout_p, const int64_t* seed, int site, const void* H,
                        long long ldh, void* C, long long ldc, void* stream);
-/* C = A1 op(W1) + A2 op(W2) in one launch (K1, K2 each a multiple of 64; no bias): the
+/* C = A1 op(W1) + A2 op(W2) in one launch (K1, K2 each a multiple of 64; lda2 == lda1,
+ * ldw2 == ldw1; no bias): the
  * memory gradient of the decoder's batched K / V projections, d memory = dK Wk + dV Wv
  * (models/transformer.py:365-372 backward) */
 int ov3d_tile_gemm2(int M, int N, int K1, const void* A1, long long lda1, const void* W1,

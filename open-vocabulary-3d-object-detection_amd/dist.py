@@ -51,10 +51,21 @@ def init_distributed(gpu_id, global_rank, world_size, dist_url, dist_backend):
     """reference dist.py:51-64 (dist_url e.g. tcp://127.0.0.1:12345 or env://)."""
     if torch.cuda.is_available() and dist_backend == "nccl":
         torch.cuda.set_device(gpu_id)
+        capture_safe_env()
     dist.init_process_group(backend=dist_backend, init_method=dist_url, world_size=world_size,
                             rank=global_rank)
     dist.barrier()
     setup_print_for_distributed(is_primary())
+
+
+def capture_safe_env():
+    """Process-group settings for collectives captured in a hipGraph, set before the group is
+    created.  ProcessGroupNCCL recycles the events of finished works (its event cache): an
+    event of an eager work (graph warm-up) still on the watchdog's list could be handed to a
+    work recorded during capture, and the watchdog's query of it then aborts the process
+    ("operation not permitted on an event last recorded in a capturing stream").  Without the
+    cache every work owns its events."""
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 
 
 def init_from_env(backend=None):
@@ -69,6 +80,7 @@ def init_from_env(backend=None):
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(local)
+            capture_safe_env()
         dist.init_process_group(backend=backend, init_method="env://", world_size=world, rank=rank)
     return rank, world, local
 

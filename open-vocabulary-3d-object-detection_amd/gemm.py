@@ -101,10 +101,10 @@ def _group_ok(pairs, trans_b):
             and all(_rows_gemm_ok(a, w, trans_b) for a, w in pairs))
 
 
-# Long row blocks (the encoder: batch * 2048 rows) can run on csrc/tilegemm.hip (128 x 128
-# output tiles, the W chunk staged once per workgroup).  Off by default: measured 0.4 %
-# slower per step than hipBLASLt (measured dead ends); OV3D_TILE_GEMM=1 enables it.
-TILE_GEMM = os.environ.get("OV3D_TILE_GEMM", "0") == "1"
+# Long row blocks (the encoder: batch * 2048 rows, the heads: batch * 1024) run on
+# csrc/tilegemm.hip: persistent 64- / 128-row tiles, both operands double-buffered in LDS, the
+# FFN activation as an epilogue (DESIGN.md "Long row-block GEMMs").  OV3D_TILE_GEMM=0: hipBLASLt.
+TILE_GEMM = os.environ.get("OV3D_TILE_GEMM", "1") == "1"
 
 
 def _tile_gemm_ok(a, w, trans_b):
@@ -132,8 +132,11 @@ def tile_gemm(a, w, bias=None, trans_b=True, out=None):
     if bias is not None and (bias.dtype != torch.bfloat16 or not bias.is_contiguous()
                              or bias.data_ptr() % 8):   # 8-byte bias pieces
         bias = bias.to(torch.bfloat16).contiguous().clone()
-    _native.call("ov3d_tile_gemm", M, N, K, a, a.stride(0), w, w.stride(0), int(trans_b), bias,
-                 out, out.stride(0), like=a)
+    wide = bias is not None and N > 2048   # the kernel stages the bias row in LDS (N <= 2048)
+    _native.call("ov3d_tile_gemm", M, N, K, a, a.stride(0), w, w.stride(0), int(trans_b),
+                 None if wide else bias, out, out.stride(0), like=a)
+    if wide:
+        out.add_(bias)
     return out
 
 

@@ -39,6 +39,8 @@ def main():
     os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=os.environ.get("MASTER_PORT", "29519"))
     torch.cuda.set_device(0)
+    from ov3d_amd import dist
+    dist.capture_safe_env()
     torch.distributed.init_process_group(backend="nccl", init_method="env://", world_size=1, rank=0)
     from ov3d_amd import synthetic
     batches = [synthetic.make_batch(4, seed=30 + i, device="cuda") for i in range(3)]

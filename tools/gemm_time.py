@@ -19,21 +19,31 @@ SHAPES = [(16384, 768, 256, 1, 1), (16384, 256, 256, 1, 1), (16384, 256, 256, 1,
 
 
 def timeit(fn, reps):
-    for _ in range(5):
+    """per-call device time: `reps` calls captured in one graph (no host launch overhead),
+    the replay timed with events"""
+    for _ in range(3):
         fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     s.record()
-    for _ in range(reps):
-        fn()
+    for _ in range(3):
+        g.replay()
     e.record()
     torch.cuda.synchronize()
-    return s.elapsed_time(e) * 1e3 / reps
+    return s.elapsed_time(e) * 1e3 / (3 * reps)
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--reps", type=int, default=200)
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--eager", action="store_true", help="no graph (profilers): 3 plain calls each")
+    ap.add_argument("--only", default=None, help="comma list of shape indices")
     a = ap.parse_args()
     ov3d_import.load()
     from ov3d_amd import gemm
@@ -41,7 +51,9 @@ def main():
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(0)
     tot_lib = tot_own = 0.0
-    for M, N, K, tb, hb in SHAPES:
+    for si, (M, N, K, tb, hb) in enumerate(SHAPES):
+        if a.only is not None and str(si) not in a.only.split(","):
+            continue
         x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
         w = (torch.randn(N, K, device=dev, generator=g) if tb else
              torch.randn(K, N, device=dev, generator=g)).div(K ** 0.5).to(torch.bfloat16)
@@ -54,12 +66,18 @@ def main():
         ref = (x.float() @ (w.float().t() if tb else w.float())) + (b.float() if hb else 0)
         d_own = (own().float() - ref).abs().max().item()
         d_lib = (lib().float() - ref).abs().max().item()
+        if a.eager:
+            for _ in range(3):
+                lib()
+                own()
+            torch.cuda.synchronize()
+            continue
         t_lib, t_own = timeit(lib, a.reps), timeit(own, a.reps)
         tot_lib += t_lib
         tot_own += t_own
         mb = (M * K + M * N) * 2 / 1e6
         print(f"M={M:6d} N={N:5d} K={K:5d} tb={tb} bias={hb}  lib {t_lib:7.2f} us  own {t_own:7.2f} us"
-              f"  ({mb / t_own:6.0f} GB/s of A+C)  maxdiff own {d_own:.3g} lib {d_lib:.3g}", flush=True)
+              f"  ({mb / t_own * 1e3:5.0f} GB/s of A+C)  maxdiff own {d_own:.3g} lib {d_lib:.3g}", flush=True)
     print(f"sum lib {tot_lib:.1f} us  own {tot_own:.1f} us")
 
 
