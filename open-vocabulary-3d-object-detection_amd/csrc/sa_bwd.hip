@@ -65,6 +65,17 @@ __device__ unsigned long long* g_sa_probe;
 #define PROBE_END do { } while (0)
 #endif
 
+// buffer resource word 3 for gfx950 raw buffer loads (32-bit data format, no swizzle)
+constexpr int kBufDword3 = 0x00020000;
+
+// the lane index recomputed where it is used (volatile: not hoisted out of the loop, so no
+// loop-invariant copy of it competes for registers)
+__device__ __forceinline__ int lane_fresh() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -396,16 +407,43 @@ __global__ __launch_bounds__(512, 1) void sa_dy8_kernel(DyFusedArgs p) {
     constexpr int CH = kTile * K / 8 / T8;
     static_assert(CH * T8 * 8 == kTile * K, "tile chunks");
     bf16x8 pre[CH];
-    auto fetch = [&](int tile) {
-        const size_t row0 = (size_t)tile * kTile;
+    // Buffer loads (SGPR descriptor + 32-bit lane offset + SGPR tile offset): with global
+    // loads hipcc kept the loop-invariant 64-bit lane addresses in VGPRs, spilled them, and the
+    // spill reloads' vmcnt(0) waited out the prefetch every tile.  The tile's K-wide rows are
+    // contiguous: 16-byte piece ch = tid + c * T8 sits at byte 16 ch.
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.yprev, 0, (int)min((long long)p.R * K * 2, 0x7fffffffLL), kBufDword3);
+    const __amdgpu_buffer_rsrc_t irs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.isel, 0, 0x7fffffff, kBufDword3);
+    const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.gsel, 0, 0x7fffffff, kBufDword3);
+    auto fetch = [&](int tile) __attribute__((always_inline)) {
+        const int soff = tile * kTile * K * 2;
+        const int tf = (wv * 64 + lane_fresh()) * 16;   // = 16 tid
 #pragma unroll
-        for (int c = 0; c < CH; ++c) {
-            const int ch = tid + c * T8;
-            const int row = ch / (K / 8), kc = (ch % (K / 8)) * 8;
-            pre[c] = *reinterpret_cast<const bf16x8*>(p.yprev + (row0 + row) * K + kc);
+        for (int c = 0; c < CH; ++c)
+            pre[c] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    yrs, tf + c * T8 * 16, soff, 0));
+    };
+    // the pooled gradient of this lane's column and the row it came from, one tile ahead
+    // (the loaded values are consumed only in the next tile: any arithmetic on them here would
+    // wait for the loads, and with them for the row prefetch issued before)
+    float gv_n[2] = {0.f, 0.f};
+    uint32_t sv_n[2] = {0u, 0u};
+    auto fetch_g = [&](int tile) __attribute__((always_inline)) {
+        const int nyf = wv * 32 + (lane_fresh() & 31);   // = ny
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+            const int pc0 = (p.S == 64 ? tile : tile * 2 + rb) * N;   // uniform
+            sv_n[rb] = __builtin_amdgcn_raw_buffer_load_b8(irs, nyf, pc0, 0);
+            gv_n[rb] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(grs, nyf * 4, pc0 * 4, 0));
         }
     };
-    if (blockIdx.x < ntiles) fetch(blockIdx.x);
+    if (blockIdx.x < ntiles) {
+        fetch(blockIdx.x);
+        fetch_g(blockIdx.x);
+    }
     __syncthreads();
     PROBE_DECL
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -423,19 +461,15 @@ __global__ __launch_bounds__(512, 1) void sa_dy8_kernel(DyFusedArgs p) {
             *reinterpret_cast<bf16x8*>(&AsT[row * LDT + kc]) = z;
             if constexpr (STATS) *reinterpret_cast<bf16x8*>(&Ys[row * LDY + kc]) = pre[c];
         }
-        // the pooled gradient of this lane's column (issued before the barrier)
-        float gv[2];
-        int sv[2];
-#pragma unroll
-        for (int rb = 0; rb < 2; ++rb) {
-            const size_t pc = (p.S == 64 ? (size_t)tile : (size_t)tile * 2 + rb) * N + ny;
-            sv[rb] = p.isel[pc] + (p.S == 64 ? 0 : 32 * rb);
-            gv[rb] = p.gsel[pc];
-        }
+        const float gv[2] = {gv_n[0], gv_n[1]};
+        const int sv[2] = {(int)sv_n[0], (int)sv_n[1] + (p.S == 64 ? 0 : 32)};
         PROBE(1);
         __syncthreads();
         PROBE(2);
-        if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);   // in flight below
+        if (tile + (int)gridDim.x < ntiles) {   // in flight below
+            fetch_g(tile + gridDim.x);
+            fetch(tile + gridDim.x);
+        }
 
         // y3 = z W3^T for columns 32w.., then dy3 -> DsT
         {
