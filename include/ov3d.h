@@ -441,6 +441,17 @@ int ov3d_attn_fwd_masked(const void* q, const void* k, const void* v, long long 
                          const int64_t* seed, int site, void* o, long long so, float* lse,
                          uint32_t* dropbits, float* workspace, int nsplit,
                          const uint32_t* maskbits, void* stream);
+/* the same forward with this call's drop bits already in dropbits (ov3d_attn_dropgen of the
+ * same seed / site / shape, e.g. on another stream ahead of time): no hash in the forward
+ * (dropout_p > 0 required) */
+int ov3d_attn_fwd_pregen(const void* q, const void* k, const void* v, long long sq, long long sk,
+                         long long sv, int B, int H, int Lq, int Lk, float scale, float dropout_p,
+                         const int64_t* seed, int site, void* o, long long so, float* lse,
+                         uint32_t* dropbits, float* workspace, int nsplit, const uint32_t* maskbits,
+                         void* stream);
+/* the drop bits of an attention forward (both layouts, ov3d_attn_dropbits_words words) */
+int ov3d_attn_dropgen(int B, int H, int Lq, int Lk, float dropout_p, const int64_t* seed, int site,
+                      uint32_t* dropbits, void* stream);
 int ov3d_attn_bwd_masked(const void* q, const void* k, const void* v, long long sq, long long sk,
                          long long sv, const void* o, long long so, const void* dout, long long sdo,
                          const float* lse, int B, int H, int Lq, int Lk, float scale,

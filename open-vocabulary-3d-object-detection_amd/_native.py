@@ -56,6 +56,8 @@ _SIGS = {
     "ov3d_attn_bwd": "ppplllplplpiiiiffppplplplpip",
     "ov3d_attn_bwd_dkdv_batch": "piiiiiffp",
     "ov3d_attn_fwd_masked": "pppllliiiiffpiplpppipp",
+    "ov3d_attn_fwd_pregen": "pppllliiiiffpiplpppipp",
+    "ov3d_attn_dropgen": "iiiifpipp",
     "ov3d_attn_bwd_masked": "ppplllplplpiiiiffppplplplpipp",
     "ov3d_attn_mask_pack": "pifiiipp",
     "ov3d_nbr_max_fwd": "pliippp",

@@ -120,6 +120,53 @@ def next_step(device):
     _SNAPS[device] = snap
 
 
+# Drop bits generated ahead of the attention forward on a side stream (ov3d_attn_dropgen): the
+# hash leaves the forward's vector-issue-bound loop (encoder forward 69 -> 52 us in the step).
+# Off by default: beside the pre-encoder SA the side-stream pass slowed the step 1617 -> 1548
+# scenes/s (same box, tools/ab_env.sh); OV3D_ATTN_PREGEN=1 enables it.
+# (device, site) -> (bits, event, dims)
+PREGEN = os.environ.get("OV3D_ATTN_PREGEN", "0") == "1"
+_PREGEN = {}
+_SIDE = {}
+
+
+def pregen_dropout(device, jobs):
+    """jobs: [(site, B, H, Lq, Lk, p)] of attention forwards later in this forward pass: their
+    drop bits (this forward's seed) on a side stream, joined by the forward that uses them."""
+    lib = _native.load()
+    cur = torch.cuda.current_stream(device)
+    side = _SIDE.get(device)
+    if side is None:
+        side = _SIDE[device] = torch.cuda.Stream(device=device)
+    seed = _seed(device)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        for site, B, H, Lq, Lk, p in jobs:
+            nbits = lib.ov3d_attn_dropbits_words(B, H, Lq, Lk)
+            with torch.cuda.stream(cur):   # allocated on the consumer's stream
+                bits = torch.empty((nbits,), dtype=torch.int32, device=device)
+            bits.record_stream(side)
+            _native.call("ov3d_attn_dropgen", B, H, Lq, Lk, float(p), seed, site, bits, like=bits)
+            ev = torch.cuda.Event()
+            ev.record(side)
+            _PREGEN[(device, site)] = (bits, ev, (B, H, Lq, Lk, float(p)))
+
+
+def _take_pregen(device, site, dims):
+    e = _PREGEN.pop((device, site), None)
+    if e is None:
+        return None
+    bits, ev, d = e
+    if d != dims:
+        return None
+    torch.cuda.current_stream(device).wait_event(ev)
+    return bits
+
+
+def clear_pregen():
+    _PREGEN.clear()
+
+
 class PackedMask:
     """An attention mask shared by the heads, packed for the kernels (ov3d_attn_mask_pack):
     ``words`` int32 (ov3d_attn_maskbits_words(B, Lq, Lk),), bit set = not attended."""
@@ -188,20 +235,24 @@ class _Attention(torch.autograd.Function):
         ws_n = _native.load().ov3d_attn_fwd_workspace(B, H, Lq, Lk, nsplit)
         ws = torch.empty((max(ws_n, 1),), dtype=torch.float32, device=dev)
         seed = _seed(dev)
-        nbits = _native.load().ov3d_attn_dropbits_words(B, H, Lq, Lk) if dropout_p > 0 else 0
-        bits = torch.empty((max(nbits, 1),), dtype=torch.int32, device=dev)
+        bits = _take_pregen(dev, site, (B, H, Lq, Lk, float(dropout_p))) if dropout_p > 0 else None
+        fn = _native.load().ov3d_attn_fwd_pregen
+        if bits is None:
+            nbits = _native.load().ov3d_attn_dropbits_words(B, H, Lq, Lk) if dropout_p > 0 else 0
+            bits = torch.empty((max(nbits, 1),), dtype=torch.int32, device=dev)
+            fn = _native.load().ov3d_attn_fwd_masked
         qp, sq = _rows(q, qo, E)
         kp, sk = _rows(k, ko, E)
         vp, sv = _rows(v, vo, E)
         mw = mask.words if mask is not None else None
-        fn = _native.load().ov3d_attn_fwd_masked
         rc = fn(qp, kp, vp, sq, sk, sv, B, H, Lq, Lk, HEAD_DIM ** -0.5, float(dropout_p),
                 _native._ptr(seed), site, _native._ptr(o), E, _native._ptr(lse), _native._ptr(bits),
                 _native._ptr(ws), nsplit, _native._ptr(mw) if mw is not None else 0,
                 _native._stream(q))
         if rc:
             raise _native.NativeError(f"ov3d_attn_fwd failed with status {rc}")
-        _native.note("ov3d_attn_fwd_masked")
+        _native.note("ov3d_attn_fwd_pregen" if fn is _native.load().ov3d_attn_fwd_pregen
+                     else "ov3d_attn_fwd_masked")
         ctx.save_for_backward(*srcs, o, lse, bits, mw)
         ctx.meta = (spec, dims, H, float(dropout_p), site, len(srcs))
         ctx.ext = ext

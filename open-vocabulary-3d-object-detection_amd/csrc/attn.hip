@@ -1479,12 +1479,13 @@ extern "C" long long ov3d_wall_clock_khz(void) {
     return khz;
 }
 
-extern "C" int ov3d_attn_fwd_masked(const void* q, const void* k, const void* v, long long sq,
-                                    long long sk, long long sv, int B, int H, int Lq, int Lk,
-                                    float scale, float dropout_p, const int64_t* seed, int site,
-                                    void* o, long long so, float* lse, uint32_t* dropbits,
-                                    float* workspace, int nsplit, const uint32_t* maskbits,
-                                    void* stream) {
+// pregen: the drop bits of this forward are already in dropbits (ov3d_attn_dropgen, usually
+// on another stream ahead of time); the forward reads them instead of hashing
+static int attn_fwd_impl(const void* q, const void* k, const void* v, long long sq, long long sk,
+                         long long sv, int B, int H, int Lq, int Lk, float scale, float dropout_p,
+                         const int64_t* seed, int site, void* o, long long so, float* lse,
+                         uint32_t* dropbits, float* workspace, int nsplit, const uint32_t* maskbits,
+                         bool pregen, void* stream) {
     if (!q || !k || !v || !o || !lse || B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || (Lq % QW) ||
         nsplit <= 0 || dropout_p < 0.f || dropout_p >= 1.f ||
         (dropout_p > 0.f && (!seed || !dropbits)) || (nsplit > 1 && !workspace))
@@ -1523,8 +1524,8 @@ extern "C" int ov3d_attn_fwd_masked(const void* q, const void* k, const void* v,
     a.stamp = stamp_take(0, (long long)Lq * Lk, (long long)grid.x * grid.y * grid.z * 4);
     // long attentions take their drop bits from a separate VALU pass (attn_dropgen_kernel);
     // short ones (the decoder) hash in the forward, where one more launch would cost more
-    const bool bits = a.thresh && dropgen_ahead(Lq, Lk);
-    if (bits) {
+    const bool bits = a.thresh && (pregen || dropgen_ahead(Lq, Lk));
+    if (bits && !pregen) {
         attn_dropgen_kernel<<<dim3(grid.x, grid.y, min(a.nkt, kDropgenSplit)), 256, 0, st>>>(a);
         OV3D_LAUNCH_CHECK();
     }
@@ -1552,6 +1553,47 @@ extern "C" int ov3d_attn_fwd_masked(const void* q, const void* k, const void* v,
         else attn_combine_kernel<kMaxCombine><<<nb, 256, 0, st>>>(a);
         OV3D_LAUNCH_CHECK();
     }
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_attn_fwd_masked(const void* q, const void* k, const void* v, long long sq,
+                                    long long sk, long long sv, int B, int H, int Lq, int Lk,
+                                    float scale, float dropout_p, const int64_t* seed, int site,
+                                    void* o, long long so, float* lse, uint32_t* dropbits,
+                                    float* workspace, int nsplit, const uint32_t* maskbits,
+                                    void* stream) {
+    return attn_fwd_impl(q, k, v, sq, sk, sv, B, H, Lq, Lk, scale, dropout_p, seed, site, o, so, lse,
+                         dropbits, workspace, nsplit, maskbits, false, stream);
+}
+
+extern "C" int ov3d_attn_fwd_pregen(const void* q, const void* k, const void* v, long long sq,
+                                    long long sk, long long sv, int B, int H, int Lq, int Lk,
+                                    float scale, float dropout_p, const int64_t* seed, int site,
+                                    void* o, long long so, float* lse, uint32_t* dropbits,
+                                    float* workspace, int nsplit, const uint32_t* maskbits,
+                                    void* stream) {
+    if (!(dropout_p > 0.f)) return OV3D_EINVAL;
+    return attn_fwd_impl(q, k, v, sq, sk, sv, B, H, Lq, Lk, scale, dropout_p, seed, site, o, so, lse,
+                         dropbits, workspace, nsplit, maskbits, true, stream);
+}
+
+extern "C" int ov3d_attn_dropgen(int B, int H, int Lq, int Lk, float dropout_p, const int64_t* seed,
+                                 int site, uint32_t* dropbits, void* stream) {
+    if (!seed || !dropbits || B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || (Lq % QW) ||
+        !(dropout_p > 0.f) || dropout_p >= 1.f)
+        return OV3D_EINVAL;
+    AttnArgs a{};
+    a.B = B;
+    a.H = H;
+    a.Lq = Lq;
+    a.Lk = Lk;
+    a.thresh = (uint32_t)fminf(rintf(dropout_p * 65536.0f), 65535.0f);
+    a.seed = seed;
+    a.site = (uint32_t)site;
+    set_dropbits(a, dropbits);
+    const dim3 grid((Lq + 4 * QW - 1) / (4 * QW), B * H, min(a.nkt, kDropgenSplit));
+    attn_dropgen_kernel<<<grid, 256, 0, ov3d_stream(stream)>>>(a);
+    OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }
 

@@ -360,10 +360,33 @@ class Model3DETR(nn.Module):
         outs = [{k: per_key[k][l] for k in stacked} for l in range(L)]
         return {"outputs": outs[-1], "aux_outputs": outs[:-1], "_layers_stacked": stacked}
 
+    def _pregen_encoder_dropout(self, pc):
+        """The plain encoder's self-attention drop bits for this step, generated on a side
+        stream beside the pre-encoder (attention.pregen_dropout): the layers' forwards read
+        them instead of hashing.  Bit-identical masks (same seed, site and hash)."""
+        from .transformer import TransformerEncoder
+        enc = self.encoder
+        if not (flash.PREGEN and type(enc) is TransformerEncoder and torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+            return
+        L = getattr(self.pre_encoder, "npoint", None)
+        if not L or L % 32:
+            return
+        B = pc.shape[0]
+        jobs = []
+        for layer in enc.layers:
+            a = getattr(layer, "self_attn", None)
+            if a is None or not getattr(a, "site", None) or a.dropout <= 0 or \
+                    a.embed_dim != a.num_heads * flash.HEAD_DIM:
+                return
+            jobs.append((a.site, B, a.num_heads, L, L, float(a.dropout)))
+        flash.pregen_dropout(pc.device, jobs)
+
     def forward(self, inputs, encoder_only=False):
         pc = inputs["point_clouds"]
         if self.training and pc.is_cuda:
             flash.next_step(pc.device)   # fresh attention-dropout stream for this step
+            self._pregen_encoder_dropout(pc)
         plan = {k: inputs[k] for k in self.PLAN_KEYS if k in inputs}
         enc_xyz, enc_feats, _ = self.run_encoder(pc, plan=plan)   # (N', B, C)
         hook = getattr(self, "encoder_grad_hook", None)

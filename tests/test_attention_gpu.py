@@ -504,3 +504,26 @@ def test_launch_stamps_time_the_encoder_launches(cuda):
     assert kinds == ["fwd", "dq", "dkdv"], rec
     assert all(w == L * L and 0 < ms < 50 for _, ms, w in rec), rec
     assert rec[0][1] <= e0.elapsed_time(e1) * 1.05 + 0.01, (rec, e0.elapsed_time(e1))
+
+
+def test_pregen_drop_bits_forward_equals_hashing_forward(cuda):
+    """drop bits generated ahead (ov3d_attn_dropgen on a side stream, attention.pregen_dropout)
+    give the forward and backward of the hashing forward bit for bit"""
+    from ov3d_amd import attention as flash
+    torch.manual_seed(3)
+    B, H, L = 2, 4, 256
+    q, k, v = (torch.randn(L, B, H * 64, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+               for _ in range(3))
+    site = flash.new_site()
+    outs = []
+    for pregen in (False, True):
+        for t in (q, k, v):
+            t.grad = None
+        if pregen:
+            flash.pregen_dropout(cuda, [(site, B, H, L, L, 0.1)])
+        o = flash.attention(q, k, v, H, dropout_p=0.1, site=site)
+        o.float().square().sum().backward()
+        outs.append((o.detach().clone(), q.grad.clone(), k.grad.clone(), v.grad.clone()))
+    assert not flash._PREGEN   # consumed
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
