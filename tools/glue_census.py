@@ -10,7 +10,20 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 import ov3d_import  # noqa: E402
-from op_census import _where  # noqa: E402
+
+
+def _where(ev):
+    """the product source line (forward) or the autograd node (backward) of a profiler event"""
+    for f in ev.stack or []:
+        if "ov3d" in f or "open-vocabulary" in f or "bench.py" in f or "torch/nn/utils" in f \
+                or "torch/optim" in f:
+            return f
+    p = ev.cpu_parent
+    while p is not None:
+        if p.name.startswith("autograd::engine::evaluate_function"):
+            return p.name.split(":")[-1].strip()
+        p = p.cpu_parent
+    return "?"
 
 GLUE = ("at::native", "rocclr", "Memcpy", "Memset", "elementwise", "Fill", "Copy", "copy")
 
