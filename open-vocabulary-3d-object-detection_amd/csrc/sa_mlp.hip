@@ -36,6 +36,13 @@ enum { MODE_STORE = 0, MODE_POOL = 1, MODE_DY = 2 };
 
 __device__ __forceinline__ float relu_bn(float a, float y, float b) { return fmaxf(fmaf(a, y, b), 0.f); }
 
+// x of lane ^ 32 (h = lane >> 5): v_permlane32_swap exchanges the two 32-lane halves of its
+// operands, A = [x_lo, x_lo], B = [x_hi, x_hi]: the partner is B in the low half, A in the high
+__device__ __forceinline__ uint32_t xor32(uint32_t x, int h) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return h ? (uint32_t)r[0] : (uint32_t)r[1];
+}
+
 struct LayerArgs {
     const bf16* yprev;     // (R, K)
     const float* scale;    // (K) previous layer's folded BN: a
@@ -207,9 +214,11 @@ __global__ __launch_bounds__(kThreads, 2) void sa_layer_kernel(LayerArgs p) {
                         if (f > mx[rb]) { mx[rb] = f; imx[rb] = row; }
                         if (f < mn[rb]) { mn[rb] = f; imn[rb] = row; }
                     }
-                    // combine the two lane halves (rows 4h..): value, then lower row
-                    const float omx = __shfl_xor(mx[rb], 32), omn = __shfl_xor(mn[rb], 32);
-                    const int oimx = __shfl_xor(imx[rb], 32), oimn = __shfl_xor(imn[rb], 32);
+                    // combine the two lane halves (rows 4h..): value, then lower row (the
+                    // partner lane's values by v_permlane32_swap, not a ds_bpermute round trip)
+                    const float omx = __builtin_bit_cast(float, xor32(__builtin_bit_cast(uint32_t, mx[rb]), h));
+                    const float omn = __builtin_bit_cast(float, xor32(__builtin_bit_cast(uint32_t, mn[rb]), h));
+                    const int oimx = (int)xor32((uint32_t)imx[rb], h), oimn = (int)xor32((uint32_t)imn[rb], h);
                     if (omx > mx[rb] || (omx == mx[rb] && oimx < imx[rb])) { mx[rb] = omx; imx[rb] = oimx; }
                     if (omn < mn[rb] || (omn == mn[rb] && oimn < imn[rb])) { mn[rb] = omn; imn[rb] = oimn; }
                 }
