@@ -264,15 +264,17 @@ __global__ void __launch_bounds__(256) fourier_pe_kernel(const float* __restrict
                                                         const float* __restrict__ gb, int ldb,
                                                         int d, float two_pi, int seq_first,
                                                         float* __restrict__ out) {
-    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= BN * d) return;
-    const long long pt = t / d;
-    const int j = (int)(t - pt * d);
-    const int b = (int)(pt / N);
-    const long long orow = seq_first ? (pt - (long long)b * N) * B + b : pt;
+    // 32-bit index arithmetic (the host checks BN * d < 2^31): the 64-bit divisions were
+    // most of the kernel's instructions
+    const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (t >= (int)(BN * d)) return;
+    const int pt = t / d;
+    const int j = t - pt * d;
+    const int b = pt / N;
+    const long long orow = seq_first ? (long long)(pt - b * N) * B + b : (long long)pt;
     float x[3];
     for (int i = 0; i < 3; ++i) {
-        float v = xyz[pt * 3 + i];
+        float v = xyz[(long long)pt * 3 + i];
         if (dmin) v = ((v - dmin[b * 3 + i]) * 1.f) / (dmax[b * 3 + i] - dmin[b * 3 + i]) + 0.f;
         x[i] = v * two_pi;
     }
@@ -288,6 +290,7 @@ extern "C" int ov3d_fourier_pe(const float* xyz, int B, int N, const float* dmin
     if (!xyz || !gauss_b || !out || B <= 0 || N <= 0 || d <= 0 || ldb < d || (!dmin != !dmax))
         return OV3D_EINVAL;
     const long long n = (long long)B * N * d;
+    if (n >= (1LL << 31)) return OV3D_EINVAL;
     fourier_pe_kernel<<<ov3d_cdiv(n, 256), 256, 0, ov3d_stream(stream)>>>(
         xyz, (long long)B * N, B, N, dmin, dmax, gauss_b, ldb, d, (float)(2.0 * 3.14159265358979323846),
         seq_first, out);

@@ -598,7 +598,15 @@ __global__ void __launch_bounds__(256) wgrad_group_reduce_kernel(WgradGroup g) {
         const int c = threadIdx.x;
         if (a.db == nullptr || k0 != 0 || n0 + c >= a.N) return;
         float acc = 0.f;
-        for (int sl = 0; sl < nsl; ++sl) acc += ps[(size_t)sl * kSlot + TB * TB + c];
+        int sl = 0;
+        for (; sl + 4 <= nsl; sl += 4) {   // four loads in flight, summed in slot order
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = ps[(size_t)(sl + u) * kSlot + TB * TB + c];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc += v[u];
+        }
+        for (; sl < nsl; ++sl) acc += ps[(size_t)sl * kSlot + TB * TB + c];
         a.db[n0 + c] = acc;
         return;
     }
@@ -606,13 +614,21 @@ __global__ void __launch_bounds__(256) wgrad_group_reduce_kernel(WgradGroup g) {
     const int nl = e / TB, kl = e - nl * TB;
     if (n0 + nl >= a.N || k0 + kl >= a.K) return;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int sl = 0; sl < nsl; ++sl) {
-        const float4 v = *reinterpret_cast<const float4*>(ps + (size_t)sl * kSlot + e);
+    auto add = [&](const float4& v) {
         acc.x += v.x;
         acc.y += v.y;
         acc.z += v.z;
         acc.w += v.w;
+    };
+    int sl = 0;
+    for (; sl + 4 <= nsl; sl += 4) {   // four slots' loads in flight, summed in slot order
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(ps + (size_t)(sl + u) * kSlot + e);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) add(v[u]);
     }
+    for (; sl < nsl; ++sl) add(*reinterpret_cast<const float4*>(ps + (size_t)sl * kSlot + e));
     float* d = a.dW + (size_t)(n0 + nl) * a.ldw + k0 + kl;
     const float o[4] = {acc.x, acc.y, acc.z, acc.w};
     for (int j = 0; j < 4 && k0 + kl + j < a.K; ++j) d[j] = o[j];
