@@ -373,6 +373,21 @@ int ov3d_roi_align_fwd(const void* feat, int is_bf16, int N, int H, int W, int C
 int ov3d_im2col3x3(const void* in, int elem_bytes, int N, int H, int W, int C, int stride,
                    int Kpad, void* out, void* stream);
 
+/* Bottleneck close of the RegionCLIP ModifiedResNet [upstream CLIP Bottleneck.forward:
+ * out = relu(bn3(conv3(out)) + identity); clip.inference, criterion.py:397] after the 1x1
+ * conv3 GEMM, with BN folded into the bias:
+ *   y (rows, cols) <- act(y + bias + residual), in place, fp32 arithmetic, one rounding;
+ *   elem_bytes 2 (bf16) or 4 (f32); cols a multiple of 16/elem_bytes, pointers 16-byte aligned. */
+int ov3d_bias_residual_act(void* y, int elem_bytes, long long rows, int cols, const void* bias,
+                           const void* residual, int relu, void* stream);
+
+/* 2x2 / stride-2 average pool on NHWC [upstream CLIP ModifiedResNet: the nn.AvgPool2d(2) of the
+ * stem and of every strided Bottleneck / downsample; torch avg_pool2d(kernel 2) semantics]:
+ *   in (N, H, W, C) -> out (N, H/2, W/2, C), fp32 sum in torch's NHWC order, / 4, one rounding;
+ *   elem_bytes 2 (bf16) or 4 (f32); C a multiple of 16/elem_bytes, pointers 16-byte aligned. */
+int ov3d_avgpool2_nhwc(const void* in, int elem_bytes, int N, int H, int W, int C, void* out,
+                       void* stream);
+
 /* ---- Flash attention (head_dim 64, bf16, no mask) ----
  * Replaces the nn.MultiheadAttention core of models/transformer.py:223,271 (encoder
  * self-attention) and :307-308,365-372 (decoder self / cross attention): per head

@@ -258,16 +258,19 @@ def _conv1x1(x, w, b, relu, residual=None):
     rows = x.reshape(-1, shp[-1])
     if residual is None:
         y = torch._addmm_activation(b, rows, w.t()) if relu else torch.addmm(b, rows, w.t())
-    else:
-        y = torch.addmm(residual.reshape(-1, w.shape[0]), rows, w.t()).add_(b)
-        if relu:
-            y.relu_()
+    else:   # plain GEMM, then bias + identity + ReLU in one pass
+        y = torch.mm(rows, w.t())
+        res = _native.check(residual.reshape(-1, w.shape[0]), "residual", ndim=2)
+        _native.call("ov3d_bias_residual_act", y, y.element_size(), y.shape[0], y.shape[1], b, res,
+                     int(relu), like=y)
     return y.view(*shp[:-1], w.shape[0])
 
 
-# im2col chunk budget: written by ov3d_im2col3x3 and read back by the GEMM while it is
-# still resident in the 256 MB Infinity Cache (MI355X_MICROARCH.md)
-IM2COL_CHUNK_BYTES = 96 << 20
+# im2col chunk budget.  Whole convolutions (16 GB: res5's first 3x3 over 4096 ROIs is 15.3 GB of
+# columns) beat Infinity-Cache-sized 96 MB chunks: one K = 5760 GEMM reaches ~1130 TFLOP/s where
+# 8100-row chunks ran at ~650, and the columns' HBM round trip costs less than the difference
+# (C5 step 70.3 -> 67.6 ms).  OV3D_IM2COL_CHUNK_MB overrides.
+IM2COL_CHUNK_BYTES = int(os.environ.get("OV3D_IM2COL_CHUNK_MB", "16384")) << 20
 
 
 # im2col of chunk i + 1 on a side stream while the GEMM of chunk i runs (two column buffers):
@@ -326,7 +329,14 @@ def _conv3x3(x, w, b, stride=1):
 
 
 def _avgpool2(x):
-    return _nhwc(F.avg_pool2d(_nchw(x), 2))
+    """nn.AvgPool2d(2) on NHWC rows: HIP (16-byte channel runs), torch's arithmetic."""
+    N, H, W, C = x.shape
+    if C % (16 // x.element_size()):
+        return _nhwc(F.avg_pool2d(_nchw(x), 2))
+    x = _native.check(x.contiguous(), "avgpool input", ndim=4)
+    out = torch.empty((N, H // 2, W // 2, C), dtype=x.dtype, device=x.device)
+    _native.call("ov3d_avgpool2_nhwc", x, x.element_size(), N, H, W, C, out, like=x)
+    return out
 
 
 class RegionCLIP(nn.Module):

@@ -176,3 +176,35 @@ def test_im2col3x3_exact(cuda, dtype, N, H, W, C, stride):
     ref = cols.view(N, C, 9, Ho * Wo).permute(0, 3, 2, 1).reshape(N * Ho * Wo, 9 * C)
     assert torch.equal(out[:, : 9 * C].float(), ref)
     assert (out[:, 9 * C:] == 0).all()
+
+
+@pytest.mark.parametrize("dtype,rows,cols,relu", [(torch.bfloat16, 4 * 81, 2560, 1),
+                                                  (torch.bfloat16, 37, 64, 0),
+                                                  (torch.float32, 50, 36, 1)])
+def test_bias_residual_act_matches_fp32(cuda, dtype, rows, cols, relu):
+    """Bottleneck close after the conv3 GEMM: act((y + bias) + residual) in fp32, one rounding."""
+    from ov3d_amd import _native
+    g = torch.Generator(device=cuda).manual_seed(5)
+    y = torch.randn(rows, cols, device=cuda, generator=g).to(dtype)
+    b = torch.randn(cols, device=cuda, generator=g).to(dtype)
+    r = torch.randn(rows, cols, device=cuda, generator=g).to(dtype)
+    ref = (y.float() + b.float()) + r.float()
+    if relu:
+        ref = ref.relu()
+    out = y.clone()
+    _native.call("ov3d_bias_residual_act", out, out.element_size(), rows, cols, b, r, relu, like=out)
+    assert torch.equal(out, ref.to(dtype))
+
+
+@pytest.mark.parametrize("dtype,N,H,W,C", [(torch.bfloat16, 5, 18, 18, 1280),
+                                           (torch.bfloat16, 2, 17, 23, 80),
+                                           (torch.float32, 3, 8, 6, 12)])
+def test_avgpool2_nhwc_bit_exact(cuda, dtype, N, H, W, C):
+    """The HIP 2x2 pool equals torch's avg_pool2d bit for bit (odd sizes floor)."""
+    import torch.nn.functional as F
+    from ov3d_amd import _native
+    x = torch.randn(N, H, W, C, device=cuda).to(dtype)
+    out = torch.empty((N, H // 2, W // 2, C), dtype=dtype, device=cuda)
+    _native.call("ov3d_avgpool2_nhwc", x, x.element_size(), N, H, W, C, out, like=x)
+    ref = F.avg_pool2d(x.permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1)
+    assert torch.equal(out, ref)
