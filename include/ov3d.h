@@ -388,6 +388,15 @@ int ov3d_bias_residual_act(void* y, int elem_bytes, long long rows, int cols, co
 int ov3d_avgpool2_nhwc(const void* in, int elem_bytes, int N, int H, int W, int C, void* out,
                        void* stream);
 
+/* Token rows of CLIP's AttentionPool2d [upstream CLIP AttentionPool2d.forward: the mean token
+ * concatenated before the spatial tokens, plus the positional embedding; clip.inference,
+ * criterion.py:397]:
+ *   x (R, ntok, C), pos (ntok + 1, C) -> t (R, ntok + 1, C):
+ *   t[r, 0] = T(mean_j x[r, j]) + pos[0] (fp32 mean in token order), t[r, 1 + j] = x[r, j] + pos[1 + j];
+ *   elem_bytes 2 (bf16) or 4 (f32); C a multiple of 16/elem_bytes, pointers 16-byte aligned. */
+int ov3d_attnpool_tokens(const void* x, int elem_bytes, int R, int ntok, int C, const void* pos,
+                         void* t, void* stream);
+
 /* ---- Flash attention (head_dim 64, bf16, no mask) ----
  * Replaces the nn.MultiheadAttention core of models/transformer.py:223,271 (encoder
  * self-attention) and :307-308,365-372 (decoder self / cross attention): per head

@@ -54,6 +54,7 @@ _SIGS = {
     "ov3d_im2col3x3": "piiiiiiipp",
     "ov3d_bias_residual_act": "pilippip",
     "ov3d_avgpool2_nhwc": "piiiiipp",
+    "ov3d_attnpool_tokens": "piiiippp",
     "ov3d_attn_fwd": "pppllliiiiffpiplpppip",
     "ov3d_attn_bwd": "ppplllplplpiiiiffppplplplpip",
     "ov3d_attn_bwd_dkdv_batch": "piiiiiffp",

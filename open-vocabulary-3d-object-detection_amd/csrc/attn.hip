@@ -429,7 +429,6 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
     bool unset = true;
     const bf16x8 k1 = kslots(1.f, 0.f, h == 0);
     bf16x8 kmb = kslots(0.f, 0.f, false);
-    float l = 0.f;
     // row sums on the matrix cores: an all-ones A operand times the (undropped) P^T packs
     // gives every accumulator row the column sums = each lane's query row sum over the 64 keys
     // of the tile (both lane halves), 4 MFMAs per tile instead of 32 VALU adds (the loop is
@@ -525,7 +524,6 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
                 // o and the sums of a query with no attended key yet are zero (alpha = 1 keeps
                 // them so even when exp2(-d) would overflow)
                 const float alpha = unset ? 1.f : fast_exp2(-d);
-                l *= alpha;
                 lacc[0] *= alpha;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
@@ -546,7 +544,6 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
             const uint32_t hb = qh + (uint32_t)(kb >> 1) * kPairMul;
             const short ts = (short)((int)a.thresh - 32768);
             const s16x2 tsig = {ts, ts};
-            float rs0 = 0.f, rs1 = 0.f;
             uint32_t dw = 0;   // this lane's drop word of the tile
             u32x4 pw[2][2], praw[2][2];
 #pragma unroll
@@ -556,8 +553,6 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
                     float p0 = fast_exp2(st[t][i]);
                     float p1 = fast_exp2(st[t][i + 1]);
 #ifdef OV3D_ATTN_VALU_ROWSUM
-                    rs0 += p0;
-                    rs1 += p1;
 #endif
                     uint32_t pk = pack_bf16(p0, p1);
                     praw[t][i >> 3][(i & 7) >> 1] = pk;
@@ -579,7 +574,6 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
                     }
                     pw[t][i >> 3][(i & 7) >> 1] = pk;
                 }
-            l += rs0 + rs1;
             if (DROP && !BITS) dw_prev = dw;
             if (DROP && BITS) dw_cur = dw_next;
             if (MASK) mw_cur = mw_next;

@@ -137,6 +137,46 @@ __global__ void __launch_bounds__(256) avgpool2_kernel(
     reinterpret_cast<V16*>(out)[t] = o;
 }
 
+// Token rows of CLIP's AttentionPool2d in one pass: t[r, 0] = mean_j x[r, j] + pos[0] and
+// t[r, 1 + j] = x[r, j] + pos[1 + j]; one thread per 16-byte channel run of one ROI, fp32 mean
+// (token order) rounded to T before the position add, as mean().to(T) + pos does.
+template <typename T>
+__global__ void __launch_bounds__(256) attnpool_tokens_kernel(
+    const T* __restrict__ x, int ntok, int CV, int total, const T* __restrict__ pos,
+    T* __restrict__ t) {
+    constexpr int E = 16 / sizeof(T);
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= total) return;
+    const int r = g / CV, cv = g - r * CV;
+    const V16* xs = reinterpret_cast<const V16*>(x) + (long long)r * ntok * CV + cv;
+    const V16* ps = reinterpret_cast<const V16*>(pos) + cv;
+    V16* ts = reinterpret_cast<V16*>(t) + (long long)r * (ntok + 1) * CV + cv;
+    float sum[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) sum[e] = 0.f;
+    for (int j = 0; j < ntok; ++j) {
+        const V16 a = xs[(long long)j * CV];
+        const V16 p = ps[(long long)(j + 1) * CV];
+        const T* av = reinterpret_cast<const T*>(&a);
+        const T* pv = reinterpret_cast<const T*>(&p);
+        V16 o;
+        T* ov = reinterpret_cast<T*>(&o);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            sum[e] += to_f(av[e]);
+            ov[e] = (T)(to_f(av[e]) + to_f(pv[e]));
+        }
+        ts[(long long)(j + 1) * CV] = o;
+    }
+    const V16 p0 = ps[0];
+    const T* pv = reinterpret_cast<const T*>(&p0);
+    V16 o;
+    T* ov = reinterpret_cast<T*>(&o);
+#pragma unroll
+    for (int e = 0; e < E; ++e) ov[e] = (T)(to_f((T)(sum[e] / (float)ntok)) + to_f(pv[e]));
+    ts[0] = o;
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) im2col_scalar_kernel(
     const T* __restrict__ in, int H, int W, int C, int stride, int Ho, int Wo, int K, long long rows,
@@ -239,6 +279,27 @@ extern "C" int ov3d_avgpool2_nhwc(const void* in, int elem_bytes, int N, int H, 
     else
         avgpool2_kernel<float><<<ov3d_cdiv(total, 256), 256, 0, s>>>(
             (const float*)in, H, W, CV, Ho, Wo, (int)total, (float*)out);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_attnpool_tokens(const void* x, int elem_bytes, int R, int ntok, int C,
+                                    const void* pos, void* t, void* stream) {
+    if (!x || !pos || !t || R < 0 || ntok <= 0 || C <= 0 || (elem_bytes != 2 && elem_bytes != 4))
+        return OV3D_EINVAL;
+    const int per16 = 16 / elem_bytes;
+    if (C % per16 || ((uintptr_t)x | (uintptr_t)pos | (uintptr_t)t) & 15) return OV3D_EINVAL;
+    const long long total = (long long)R * (C / per16);
+    if (total == 0) return OV3D_OK;
+    if (total > 0x7fffffffLL) return OV3D_EINVAL;
+    hipStream_t s = ov3d_stream(stream);
+    if (elem_bytes == 2)
+        attnpool_tokens_kernel<__hip_bfloat16><<<ov3d_cdiv(total, 256), 256, 0, s>>>(
+            (const __hip_bfloat16*)x, ntok, C / per16, (int)total, (const __hip_bfloat16*)pos,
+            (__hip_bfloat16*)t);
+    else
+        attnpool_tokens_kernel<float><<<ov3d_cdiv(total, 256), 256, 0, s>>>(
+            (const float*)x, ntok, C / per16, (int)total, (const float*)pos, (float*)t);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

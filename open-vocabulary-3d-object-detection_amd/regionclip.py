@@ -218,7 +218,7 @@ class _Folded:
         d = C // H
         f32 = torch.float32
         self.heads, self.head_dim = H, d
-        self.pos = ap.positional_embedding.detach().to(dtype)                       # (T, C)
+        self.pos = ap.positional_embedding.detach().to(dtype).contiguous()          # (T, C)
         self.wq = (ap.q_proj.weight.detach().float() * d ** -0.5).to(dtype)          # scaled q
         self.bq = (ap.q_proj.bias.detach().float() * d ** -0.5).to(dtype)
         self.wk = ap.k_proj.weight.detach().to(dtype).view(H, d, C)                 # (H, d, C)
@@ -521,9 +521,8 @@ class RegionCLIP(nn.Module):
         R, h, w, C = x.shape
         Hh, d = fw.heads, fw.head_dim
         t = torch.empty((R, h * w + 1, C), dtype=x.dtype, device=x.device)
-        t[:, 1:] = x.view(R, h * w, C)
-        t[:, 0] = x.view(R, h * w, C).float().mean(1).to(x.dtype)
-        t += fw.pos
+        x = _native.check(x.contiguous(), "attnpool input", ndim=4)
+        _native.call("ov3d_attnpool_tokens", x, x.element_size(), R, h * w, C, fw.pos, t, like=x)
         q = torch.addmm(fw.bq, t[:, 0], fw.wq.t())                        # (R, C), scaled
         a = torch.bmm(q.view(R, Hh, d).transpose(0, 1), fw.wk)             # (H, R, C)
         s = torch.bmm(a.transpose(0, 1), t.transpose(1, 2))                # (R, H, T)

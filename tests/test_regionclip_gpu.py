@@ -208,3 +208,18 @@ def test_avgpool2_nhwc_bit_exact(cuda, dtype, N, H, W, C):
     _native.call("ov3d_avgpool2_nhwc", x, x.element_size(), N, H, W, C, out, like=x)
     ref = F.avg_pool2d(x.permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1)
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("dtype,R,ntok,C", [(torch.bfloat16, 37, 81, 2560), (torch.float32, 5, 9, 64)])
+def test_attnpool_tokens_matches_torch(cuda, dtype, R, ntok, C):
+    """Token rows of the attention pool: [mean; x] + pos; the spatial rows bit-equal to torch's
+    x + pos, the mean row within one rounding of torch's reduction (summation order)."""
+    from ov3d_amd import _native
+    x = torch.randn(R, ntok, C, device=cuda).to(dtype)
+    pos = torch.randn(ntok + 1, C, device=cuda).to(dtype)
+    t = torch.empty((R, ntok + 1, C), dtype=dtype, device=cuda)
+    _native.call("ov3d_attnpool_tokens", x, x.element_size(), R, ntok, C, pos, t, like=x)
+    ref = torch.cat([x.float().mean(1, keepdim=True).to(dtype), x], 1) + pos
+    assert torch.equal(t[:, 1:], ref[:, 1:])
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    assert torch.allclose(t[:, 0].float(), ref[:, 0].float(), atol=tol, rtol=tol)
