@@ -397,6 +397,18 @@ int ov3d_avgpool2_nhwc(const void* in, int elem_bytes, int N, int H, int W, int 
 int ov3d_attnpool_tokens(const void* x, int elem_bytes, int R, int ntok, int C, const void* pos,
                          void* t, void* stream);
 
+/* conv3 + bottleneck close of the RegionCLIP ModifiedResNet as ONE library GEMM [upstream CLIP
+ * Bottleneck.forward: relu(bn3(conv3(out)) + identity); clip.inference, criterion.py:397]:
+ *   out (M, N) = act(x (M, K) · w (N, K)^T + bias (N) + residual (M, N)), bf16 in and out,
+ *   fp32 accumulation; row-major with leading dimensions ldx, ldw, ldr, ldo (elements);
+ *   hipBLASLt out-of-place C = residual, D = out, bias(+ReLU) epilogue; workspace (16-byte
+ *   aligned, ws_bytes) for its stream-K algorithms.  Returns OV3D_ELAUNCH when hipBLASLt
+ *   finds no algorithm or fails. */
+int ov3d_lt_gemm_bias_residual(long long M, int N, int K, const void* x, long long ldx,
+                               const void* w, long long ldw, const void* bias, const void* residual,
+                               long long ldr, int relu, void* out, long long ldo, void* workspace,
+                               long long ws_bytes, void* stream);
+
 /* ---- Flash attention (head_dim 64, bf16, no mask) ----
  * Replaces the nn.MultiheadAttention core of models/transformer.py:223,271 (encoder
  * self-attention) and :307-308,365-372 (decoder self / cross attention): per head

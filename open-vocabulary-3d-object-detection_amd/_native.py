@@ -55,6 +55,7 @@ _SIGS = {
     "ov3d_bias_residual_act": "pilippip",
     "ov3d_avgpool2_nhwc": "piiiiipp",
     "ov3d_attnpool_tokens": "piiiippp",
+    "ov3d_lt_gemm_bias_residual": "liiplplppliplplp",
     "ov3d_attn_fwd": "pppllliiiiffpiplpppip",
     "ov3d_attn_bwd": "ppplllplplpiiiiffppplplplpip",
     "ov3d_attn_bwd_dkdv_batch": "piiiiiffp",
