@@ -218,14 +218,22 @@ class StepGraph:
         if hasattr(self.opt, "sync_hyper"):
             self.opt.sync_hyper()   # this iteration's lr (engine.py:79) into the graph's table
         keys = list(self.static)
+        dsts = [self.static[k] for k in keys]
         srcs = [batch[k] for k in keys]
-        if all(s.is_cuda and s.is_contiguous() and s.dtype == self.static[k].dtype
-               for k, s in zip(keys, srcs)):
+        nb = next_batch if next_batch is not None else batch
+        if self.prefetch:
+            # the next batch's points ride in the same launch (the previous step's FPS, their
+            # only reader, was joined at its end); a separate copy_ could land on a blit kernel
+            # of ~0.3 ms on the critical path
+            dsts.append(self.next_pc)
+            srcs.append(nb["point_clouds"])
+        if all(s.is_cuda and s.is_contiguous() and s.dtype == d.dtype and s.shape == d.shape
+               for d, s in zip(dsts, srcs)):
             from . import _native
-            _native.multi_copy([self.static[k] for k in keys], srcs)   # one launch
+            _native.multi_copy(dsts, srcs)   # one launch
         else:
-            for k, s in zip(keys, srcs):
-                self.static[k].copy_(s, non_blocking=True)
+            for d, s in zip(dsts, srcs):
+                d.copy_(s, non_blocking=True)
         if not self.prefetch:
             self.graph.replay()
             return self.loss
@@ -236,8 +244,6 @@ class StepGraph:
         if self._expected is None or pc is not self._expected[0] or \
                 pc._version != self._expected[1]:
             self._set_plan(self._sample(self.static["point_clouds"]))
-        nb = next_batch if next_batch is not None else batch
-        self.next_pc.copy_(nb["point_clouds"], non_blocking=True)
         self._expected = (nb["point_clouds"], nb["point_clouds"]._version)
         # the next batch's sampling plan runs on its own stream (own hardware queue),
         # concurrently with this step's graph; the graph reads plan_cur only
