@@ -465,7 +465,9 @@ int ov3d_attn_small_bwd(int on);
  * True = not attended) given to nn.MultiheadAttention.  ov3d_attn_mask_pack packs a
  * (B, Lq, Lk) row-major source, shared by the heads, into ov3d_attn_maskbits_words() uint32
  * words (query-major [nkt][B][Lq][2] then key-major [Lq/32][B][nkt*64]): kind 0 = uint8
- * mask (nonzero = not attended), kind 1 = fp32 distances (not attended iff d >= thr).
+ * mask (nonzero = not attended), kind 1 = fp32 distances (not attended iff d >= thr),
+ * kind 2 = fp32 squared distances g of torch.cdist's matmul form, before its
+ * clamp_min(0).sqrt() (not attended iff sqrt(max(g, 0)) >= thr: the bits of kind 1 on cdist).
  * The _masked entry points take the words (NULL = no mask) and are otherwise
  * ov3d_attn_fwd / ov3d_attn_bwd.  A query with no attended key gets O = 0 and zero
  * gradients (the reference's softmax would give NaN). */

@@ -175,9 +175,11 @@ class PackedMask:
         self.words, self.B, self.Lq, self.Lk = words, B, Lq, Lk
 
 
-def pack_mask(src, thr=None):
+def pack_mask(src, thr=None, squared=False):
     """(B, Lq, Lk) bool mask (True = not attended), or fp32 distances with ``thr`` (not
-    attended iff d >= thr: MaskedTransformerEncoder.compute_mask) -> PackedMask."""
+    attended iff d >= thr: MaskedTransformerEncoder.compute_mask) -> PackedMask.
+    squared: src is cdist's matmul-form squared distances (transformer.euclid_sq), packed as
+    sqrt(max(src, 0)) >= thr — cdist's own clamp and sqrt, fused."""
     B, Lq, Lk = src.shape
     _native.check_device(src, "attention mask")
     lib = _native.load()
@@ -192,7 +194,7 @@ def pack_mask(src, thr=None):
     else:
         if src.dtype != torch.float32:
             raise ValueError("pack_mask: distances must be float32")
-        kind = 1
+        kind = 2 if squared else 1
     words = torch.empty((n,), dtype=torch.int32, device=src.device)
     _native.call("ov3d_attn_mask_pack", src, kind, float(thr), B, Lq, Lk, words, like=src)
     return PackedMask(words, B, Lq, Lk)

@@ -1280,10 +1280,20 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_batch_kernel(AttnBwdBatc
 // Query-major: a thread per (b, q, 64-key tile) reads the tile's 64 contiguous values and
 // writes both halves' words; key-major: a thread per (32-query block, b, key) reads one
 // column (consecutive threads = consecutive keys: coalesced).
+// KIND 0: bool mask; 1: distances, masked iff d >= thr; 2: the squared-distance matrix of
+// torch.cdist's matmul form before its clamp_min(0).sqrt() (ATen _euclidean_dist), masked iff
+// sqrt(max(g, 0)) >= thr — the same correctly rounded sqrt as torch's, so the same bits as
+// packing cdist's output, without the clamp and sqrt passes over the (B, L, L) matrix.
+template <int KIND>
+__device__ __forceinline__ bool masked_value(float v, float thr) {
+    if (KIND == 2) v = sqrtf(fmaxf(v, 0.f));
+    return v >= thr;
+}
+
 template <int KIND>
 __device__ __forceinline__ bool mask_at(const void* src, size_t e, float thr) {
     if (KIND == 0) return ((const uint8_t*)src)[e] != 0;
-    return ((const float*)src)[e] >= thr;
+    return masked_value<KIND>(((const float*)src)[e], thr);
 }
 
 template <int KIND>
@@ -1300,7 +1310,7 @@ __global__ void __launch_bounds__(256) attn_mask_pack_kernel(const void* __restr
         const size_t row = ((size_t)b * Lq + q) * Lk + 64 * kt;
         uint32_t w0 = 0, w1 = 0;
         const bool full = 64 * kt + 64 <= Lk;
-        if (KIND == 1 && full && (row & 3) == 0) {
+        if (KIND != 0 && full && (row & 3) == 0) {
 #pragma unroll
             for (int c = 0; c < 16; ++c) {
                 const float4 v = *reinterpret_cast<const float4*>((const float*)src + row + 4 * c);
@@ -1310,7 +1320,7 @@ __global__ void __launch_bounds__(256) attn_mask_pack_kernel(const void* __restr
                     const int kk = 4 * c + u;   // key offset in the tile -> (half, bit)
                     const int rem = kk & 31;
                     const int bit = (kk & 1) * 16 + (kk >> 5) * 8 + (rem >> 3) * 2 + ((rem >> 1) & 1);
-                    const uint32_t m = vv[u] >= thr ? 1u << bit : 0u;
+                    const uint32_t m = masked_value<KIND>(vv[u], thr) ? 1u << bit : 0u;
                     if ((rem >> 2) & 1) w1 |= m; else w0 |= m;
                 }
             }
@@ -1406,7 +1416,7 @@ extern "C" long long ov3d_attn_maskbits_words(int B, int Lq, int Lk) {
 
 extern "C" int ov3d_attn_mask_pack(const void* src, int kind, float thr, int B, int Lq, int Lk,
                                    uint32_t* words, void* stream) {
-    if (!src || !words || (kind != 0 && kind != 1) || B <= 0 || Lq <= 0 || Lk <= 0 || (Lq % QW))
+    if (!src || !words || kind < 0 || kind > 2 || B <= 0 || Lq <= 0 || Lk <= 0 || (Lq % QW))
         return OV3D_EINVAL;
     const int nkt = (Lk + KB - 1) / KB;
     // threads: B*Lq*nkt query-major (two words each) + W key-major
@@ -1414,8 +1424,10 @@ extern "C" int ov3d_attn_mask_pack(const void* src, int kind, float thr, int B, 
     hipStream_t st = ov3d_stream(stream);
     if (kind == 0)
         attn_mask_pack_kernel<0><<<ov3d_cdiv(n, 256), 256, 0, st>>>(src, thr, B, Lq, Lk, nkt, words);
-    else
+    else if (kind == 1)
         attn_mask_pack_kernel<1><<<ov3d_cdiv(n, 256), 256, 0, st>>>(src, thr, B, Lq, Lk, nkt, words);
+    else
+        attn_mask_pack_kernel<2><<<ov3d_cdiv(n, 256), 256, 0, st>>>(src, thr, B, Lq, Lk, nkt, words);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

@@ -375,6 +375,16 @@ class TransformerEncoder(nn.Module):
         return xb if self.norm is not None else s
 
 
+def euclid_sq(x):
+    """torch.cdist(x, x, p=2) for > 25 points (the matmul form, ATen _euclidean_dist) before its
+    clamp_min(0).sqrt(): the same fp32 operations and GEMM, outside autocast as cdist runs."""
+    with torch.autocast("cuda", enabled=False):
+        x = x.float()
+        xn = x.pow(2).sum(-1, keepdim=True)
+        pad = torch.ones_like(xn)
+        return torch.cat([x.mul(-2), xn, pad], -1).matmul(torch.cat([x, pad, xn], -1).mT)
+
+
 class MaskedTransformerEncoder(TransformerEncoder):
     """Radius-masked encoder with interim SA downsampling after layer 0
     (reference transformer.py:144-209; mask = cdist(xyz) >= radius**2, quirk Q5)."""
@@ -389,17 +399,18 @@ class MaskedTransformerEncoder(TransformerEncoder):
 
     @torch.no_grad()
     def compute_mask(self, xyz, radius, dist=None):
-        if dist is None or dist.shape[1] != xyz.shape[1]:
-            dist = torch.cdist(xyz.float(), xyz.float(), p=2)
-        return dist >= radius, dist
+        if dist is None or dist[0] != "dist" or dist[1].shape[1] != xyz.shape[1]:
+            dist = ("dist", torch.cdist(xyz.float(), xyz.float(), p=2))
+        return dist[1] >= radius, dist
 
     @torch.no_grad()
     def _packed_mask(self, xyz, radius, dist=None):
         """the same mask as compute_mask, packed for the HIP attention kernels straight from
-        the distances (no (B*H, L, L) bool tensor)"""
-        if dist is None or dist.shape[1] != xyz.shape[1]:
-            dist = torch.cdist(xyz.float(), xyz.float(), p=2)
-        return flash.pack_mask(dist, float(radius)), dist
+        cdist's matmul-form squared distances, its clamp and sqrt fused into the packing (no
+        (B, L, L) distance or (B*H, L, L) bool tensor)"""
+        if dist is None or dist[0] != "sq" or dist[1].shape[1] != xyz.shape[1]:
+            dist = ("sq", euclid_sq(xyz))
+        return flash.pack_mask(dist[1], float(radius), squared=True), dist
 
     @staticmethod
     def _packed_ok(layer, src):

@@ -358,6 +358,28 @@ def test_mask_pack_layouts(cuda):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("B,L", [(8, 2048), (3, 1000)])
+def test_squared_distance_mask_equals_cdist_mask(cuda, B, L):
+    """The masked encoder's packing from cdist's matmul-form squared distances (clamp + sqrt
+    fused, transformer.euclid_sq) gives the bits of packing torch.cdist's output, under the
+    step's bf16 autocast as well; the squared form is cdist's own matrix before its sqrt"""
+    from ov3d_amd import attention as A
+    from ov3d_amd import transformer as T
+    g = torch.Generator(device=cuda).manual_seed(3)
+    xyz = torch.rand(B, L, 3, device=cuda, generator=g) * torch.tensor([6.0, 6.0, 3.0], device=cuda)
+    xyz[:, 7] = xyz[:, 3]          # coincident points: clamp at 0
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        sq = T.euclid_sq(xyz)
+        dist = torch.cdist(xyz.float(), xyz.float(), p=2)
+    assert sq.dtype == torch.float32
+    assert torch.equal(sq.clamp_min(0).sqrt(), dist)
+    Lq = L // 32 * 32
+    for r2 in (0.16, 0.64, 1.44):
+        a = A.pack_mask(sq[:, :Lq].contiguous(), r2, squared=True).words
+        b = A.pack_mask(dist[:, :Lq].contiguous(), r2).words
+        assert torch.equal(a, b), r2
+
+
 @pytest.mark.parametrize("with_interim", [False, True])
 def test_masked_encoder_packed_equals_bool_mask_path(cuda, monkeypatch, with_interim):
     """MaskedTransformerEncoder (bf16 fused layers): PackedMask through the HIP kernels vs
@@ -383,7 +405,7 @@ def test_masked_encoder_packed_equals_bool_mask_path(cuda, monkeypatch, with_int
             monkeypatch.setattr(T.MaskedTransformerEncoder, "_packed_ok", staticmethod(lambda *a: False))
         calls = []
         real = T.flash.pack_mask
-        monkeypatch.setattr(T.flash, "pack_mask", lambda *a: calls.append(1) or real(*a))
+        monkeypatch.setattr(T.flash, "pack_mask", lambda *a, **k: calls.append(1) or real(*a, **k))
         src = src0.clone().requires_grad_()
         with torch.autocast("cuda", dtype=torch.bfloat16):
             _, out, inds = twin(src, xyz=xyz)
