@@ -358,7 +358,8 @@ int ov3d_heads_out_bwd(const float* gv, const float* glog, const float* text, in
  *   boxes (R, 4) f32 [x1, y1, x2, y2] in image pixels; roi r samples image
  *   (r / per_image) % nimages  (rows ordered (layer, scene, query))
  *   -> out (R, pooled, pooled, C), same dtype; sampling_ratio <= 0 = adaptive
- *   (ceil(roi_size / pooled)).  fp32 arithmetic in torchvision's order. */
+ *   (ceil(roi_size / pooled)).  fp32 arithmetic in torchvision's order.  feat and out
+ *   16-byte aligned (one 16-byte channel run per corner load). */
 int ov3d_roi_align_fwd(const void* feat, int is_bf16, int N, int H, int W, int C,
                        const float* boxes, int R, int per_image, int nimages, float spatial_scale,
                        int pooled, int sampling_ratio, int aligned, void* out, void* stream);

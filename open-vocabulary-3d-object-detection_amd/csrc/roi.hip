@@ -73,10 +73,15 @@ __device__ __forceinline__ void bilinear_acc(const T* __restrict__ f, int H, int
     const float ly = y - (float)yl, lx = x - (float)xl;
     const float hy = 1.f - ly, hx = 1.f - lx;
     const float w1 = hy * hx, w2 = hy * lx, w3 = ly * hx, w4 = ly * lx;
-    const T* p1 = f + ((size_t)yl * W + xl) * C;
-    const T* p2 = f + ((size_t)yl * W + xh) * C;
-    const T* p3 = f + ((size_t)yh * W + xl) * C;
-    const T* p4 = f + ((size_t)yh * W + xh) * C;
+    // one 16-byte load per corner (VEC * sizeof(T) == 16, channel runs 16-byte aligned)
+    const uint4 u1 = *reinterpret_cast<const uint4*>(f + ((size_t)yl * W + xl) * C);
+    const uint4 u2 = *reinterpret_cast<const uint4*>(f + ((size_t)yl * W + xh) * C);
+    const uint4 u3 = *reinterpret_cast<const uint4*>(f + ((size_t)yh * W + xl) * C);
+    const uint4 u4 = *reinterpret_cast<const uint4*>(f + ((size_t)yh * W + xh) * C);
+    const T* p1 = reinterpret_cast<const T*>(&u1);
+    const T* p2 = reinterpret_cast<const T*>(&u2);
+    const T* p3 = reinterpret_cast<const T*>(&u3);
+    const T* p4 = reinterpret_cast<const T*>(&u4);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
         const float v = w1 * ld(p1 + j) + w2 * ld(p2 + j) + w3 * ld(p3 + j) + w4 * ld(p4 + j);
@@ -85,17 +90,20 @@ __device__ __forceinline__ void bilinear_acc(const T* __restrict__ f, int H, int
 }
 
 // One thread per (roi, ph, pw, channel vector); channel vector fastest.
-template <typename T, int VEC>
+// IDX: the index type of the thread -> (roi, ph, pw, cv) split (int when the grid fits: the
+// 64-bit divisions cost more than the bin's arithmetic).
+template <typename T, int VEC, typename IDX>
 __global__ void __launch_bounds__(256) roi_align_kernel(
     const T* __restrict__ feat, int H, int W, int C, const float* __restrict__ boxes, int R,
     int per_image, int nimages, float scale, int P, int sampling_ratio, int aligned,
     T* __restrict__ out) {
+    static_assert(VEC * sizeof(T) == 16, "one 16-byte channel run per thread");
     const int CV = C / VEC;
-    const long long total = (long long)R * P * P * CV;
-    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const IDX total = (IDX)R * P * P * CV;
+    const IDX t = (IDX)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= total) return;
     const int cv = (int)(t % CV);
-    long long q = t / CV;
+    IDX q = t / CV;
     const int pw = (int)(q % P);
     q /= P;
     const int ph = (int)(q % P);
@@ -113,9 +121,11 @@ __global__ void __launch_bounds__(256) roi_align_kernel(
             bilinear_acc<T, VEC>(f, H, W, C, y, x, acc);
         }
     }
-    T* o = out + (((size_t)r * P + ph) * P + pw) * C + cv * VEC;
+    uint4 ov;
+    T* oe = reinterpret_cast<T*>(&ov);
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) o[j] = (T)(acc[j] / b.count);
+    for (int j = 0; j < VEC; ++j) oe[j] = (T)(acc[j] / b.count);
+    *reinterpret_cast<uint4*>(out + (((size_t)r * P + ph) * P + pw) * C + cv * VEC) = ov;
 }
 
 // CLIPFastRCNN.preprocess_image + ImageList.from_tensors: the (H_b, W_b, 3) view of
@@ -169,12 +179,22 @@ extern "C" int ov3d_roi_align_fwd(const void* feat, int is_bf16, int N, int H, i
     if (total > 0x7fffffffLL * 256) return OV3D_EINVAL;
     const int blocks = ov3d_cdiv(total, 256);
     hipStream_t s = ov3d_stream(stream);
-    if (is_bf16)
-        roi_align_kernel<bf16, 8><<<blocks, 256, 0, s>>>(
+    if ((uintptr_t)feat & 15 || (uintptr_t)out & 15) return OV3D_EINVAL;
+    const bool small = total + 256 <= 0x7fffffffLL;
+    if (is_bf16 && small)
+        roi_align_kernel<bf16, 8, int><<<blocks, 256, 0, s>>>(
             (const bf16*)feat, H, W, C, boxes, R, per_image, nimages, spatial_scale, pooled,
             sampling_ratio, aligned, (bf16*)out);
+    else if (is_bf16)
+        roi_align_kernel<bf16, 8, long long><<<blocks, 256, 0, s>>>(
+            (const bf16*)feat, H, W, C, boxes, R, per_image, nimages, spatial_scale, pooled,
+            sampling_ratio, aligned, (bf16*)out);
+    else if (small)
+        roi_align_kernel<float, 4, int><<<blocks, 256, 0, s>>>(
+            (const float*)feat, H, W, C, boxes, R, per_image, nimages, spatial_scale, pooled,
+            sampling_ratio, aligned, (float*)out);
     else
-        roi_align_kernel<float, 4><<<blocks, 256, 0, s>>>(
+        roi_align_kernel<float, 4, long long><<<blocks, 256, 0, s>>>(
             (const float*)feat, H, W, C, boxes, R, per_image, nimages, spatial_scale, pooled,
             sampling_ratio, aligned, (float*)out);
     OV3D_LAUNCH_CHECK();
