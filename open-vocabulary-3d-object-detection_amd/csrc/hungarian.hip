@@ -32,6 +32,10 @@ __device__ __forceinline__ void lex_min(double& m, int& k, double om, int ok) {
     }
 }
 
+// STAGED: the problem's Q x n costs are copied to LDS in the solver's (row, column) order while
+// the NaN screen reads them, so every augmenting step reads its row from LDS (consecutive lanes,
+// consecutive columns) instead of a strided row of the global matrix at L2 latency.
+template <bool STAGED>
 __global__ __launch_bounds__(64) void hungarian_kernel(const float* __restrict__ cost,
                                                        const int32_t* __restrict__ nactual, int Q,
                                                        int G, int64_t* __restrict__ gt_inds,
@@ -47,22 +51,6 @@ __global__ __launch_bounds__(64) void hungarian_kernel(const float* __restrict__
     int64_t* out_i = gt_inds + (size_t)p * Q;
     float* out_m = matched + (size_t)p * Q;
 
-    // scipy rejects NaN and -inf entries (ValueError) before solving
-    int bad = 0;
-    for (int e = lane; e < Q * n; e += 64) {
-        const float c = C[(size_t)(e / n) * G + e % n];
-        bad |= (c != c) || (c == -__builtin_huge_valf());
-    }
-    const bool invalid = __ballot(bad) != 0ull;
-    if (n == 0 || invalid) {
-        for (int q = lane; q < Q; q += 64) {
-            out_i[q] = 0;
-            out_m[q] = 0.f;
-        }
-        if (status && lane == 0) status[p] = invalid ? -1 : 0;
-        return;
-    }
-
     const bool tr = n < Q;                 // rows = GT boxes, columns = queries
     const int nr = tr ? n : Q, nc = tr ? Q : n;
     const int NC = Q > G ? Q : G, NR = Q < G ? Q : G;   // LDS capacity (host-sized)
@@ -76,6 +64,26 @@ __global__ __launch_bounds__(64) void hungarian_kernel(const float* __restrict__
     int* col4row = pos + NC;
     unsigned char* SC = reinterpret_cast<unsigned char*>(col4row + NR);
     unsigned char* SR = SC + NC;
+    float* Cs = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(SR + NR) + 3) &
+                                         ~(uintptr_t)3);   // STAGED: nr x nc costs
+
+    // scipy rejects NaN and -inf entries (ValueError) before solving
+    int bad = 0;
+    for (int e = lane; e < Q * n; e += 64) {
+        const int q = e / n, g = e - q * n;
+        const float c = C[(size_t)q * G + g];
+        bad |= (c != c) || (c == -__builtin_huge_valf());
+        if (STAGED) Cs[tr ? g * nc + q : q * nc + g] = c;
+    }
+    const bool invalid = __ballot(bad) != 0ull;
+    if (n == 0 || invalid) {
+        for (int q = lane; q < Q; q += 64) {
+            out_i[q] = 0;
+            out_m[q] = 0.f;
+        }
+        if (status && lane == 0) status[p] = invalid ? -1 : 0;
+        return;
+    }
 
     for (int j = lane; j < nc; j += 64) {
         v[j] = 0.0;
@@ -107,7 +115,8 @@ __global__ __launch_bounds__(64) void hungarian_kernel(const float* __restrict__
             int bk = INT_MAX;
             for (int j = lane; j < nc; j += 64) {
                 if (SC[j]) continue;
-                const double c = tr ? (double)C[(size_t)j * G + i] : (double)C[(size_t)i * G + j];
+                const double c = STAGED ? (double)Cs[i * nc + j]
+                                 : tr ? (double)C[(size_t)j * G + i] : (double)C[(size_t)i * G + j];
                 const double r = minv + c - ui - v[j];
                 double s = spc[j];
                 if (r < s) {
@@ -190,9 +199,14 @@ extern "C" int ov3d_hungarian(const float* cost, const int32_t* nactual, int P, 
     if (!cost || !nactual || !gt_inds || !matched) return OV3D_EINVAL;
     const int NC = Q > G ? Q : G, NR = Q < G ? Q : G;
     const size_t lds = (size_t)(2 * NC + NR) * sizeof(double) + (size_t)(4 * NC + NR) * sizeof(int) +
-                       (size_t)(NC + NR);
-    hipLaunchKernelGGL(hungarian_kernel, dim3(P), dim3(64), lds, ov3d_stream(stream), cost, nactual,
-                       Q, G, gt_inds, matched, status);
+                       (size_t)(NC + NR) + 3;
+    const size_t staged = lds + (size_t)Q * G * sizeof(float);
+    if (staged <= (64u << 10))
+        hipLaunchKernelGGL(hungarian_kernel<true>, dim3(P), dim3(64), staged, ov3d_stream(stream),
+                           cost, nactual, Q, G, gt_inds, matched, status);
+    else
+        hipLaunchKernelGGL(hungarian_kernel<false>, dim3(P), dim3(64), lds, ov3d_stream(stream),
+                           cost, nactual, Q, G, gt_inds, matched, status);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

@@ -306,10 +306,12 @@ def test_hungarian_matches_scipy_golden(cuda, case):
     np.testing.assert_array_equal(inds.cpu().numpy(), fx[f"{case}_inds"])
 
 
-def test_hungarian_vs_oracle_random_ties(cuda):
+@pytest.mark.parametrize("P,Q,G", [(96, 128, 64),    # costs staged in LDS (SUN shape)
+                                   (16, 256, 64),    # global-cost path (C4 shape, > 64 KB)
+                                   (24, 32, 48)])    # more GT than queries (transposed solve)
+def test_hungarian_vs_oracle_random_ties(cuda, P, Q, G):
     from ov3d_amd.assignment import hungarian
     rng = np.random.default_rng(11)
-    P, Q, G = 96, 128, 64
     cost = rng.integers(0, 4, (P, Q, G)).astype(np.float32) * 0.5
     cost[: P // 2] = rng.standard_normal((P // 2, Q, G)).astype(np.float32)
     nact = rng.integers(0, G + 1, P).astype(np.int32)
