@@ -539,19 +539,29 @@ class RegionCLIP(nn.Module):
 
     def _attnpool(self, x):
         """AttentionPool2d, first query only, reassociated (module docstring)."""
+        return self._pool_tokens(self._tokens(x))
+
+    def _tokens(self, x):
+        """(R, h, w, C) res5 rows -> (R, h*w + 1, C) token rows [mean; x] + pos (one HIP pass)."""
         fw = self.folded()
         R, h, w, C = x.shape
-        Hh, d = fw.heads, fw.head_dim
         t = torch.empty((R, h * w + 1, C), dtype=x.dtype, device=x.device)
         x = _native.check(x.contiguous(), "attnpool input", ndim=4)
         _native.call("ov3d_attnpool_tokens", x, x.element_size(), R, h * w, C, fw.pos, t, like=x)
+        return t
+
+    def _pool_tokens(self, t):
+        """the pool's first query over the token rows t (R, T, C) -> (R, output_dim) f32"""
+        fw = self.folded()
+        R, _, C = t.shape
+        Hh, d = fw.heads, fw.head_dim
         q = torch.addmm(fw.bq, t[:, 0], fw.wq.t())                        # (R, C), scaled
         a = torch.bmm(q.view(R, Hh, d).transpose(0, 1), fw.wk)             # (H, R, C)
         s = torch.bmm(a.transpose(0, 1), t.transpose(1, 2))                # (R, H, T)
-        p = torch.softmax(s.float(), dim=-1).to(x.dtype)
+        p = torch.softmax(s.float(), dim=-1).to(t.dtype)
         y = torch.bmm(p, t)                                                # (R, H, C)
         o = torch.bmm(y.transpose(0, 1), fw.wvt).transpose(0, 1)           # (R, H, d)
-        o = (o.float() + fw.bv.view(Hh, d)).to(x.dtype).reshape(R, C)
+        o = (o.float() + fw.bv.view(Hh, d)).to(t.dtype).reshape(R, C)
         return torch.addmm(fw.bc, o, fw.wc.t()).float()
 
 

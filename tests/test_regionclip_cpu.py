@@ -98,7 +98,11 @@ def test_reassociated_attnpool_equals_mha():
     m = _small()
     x = torch.randn(5, 1024, 9, 9) * 2             # 32 * width
     ref = m.backbone.attnpool(x)
-    got = m._attnpool(x.permute(0, 2, 3, 1).contiguous())
+    # token rows as ov3d_attnpool_tokens builds them on the GPU ([mean; x] + pos), then the
+    # reassociated first-query pool
+    rows = x.flatten(2).transpose(1, 2)                                  # (R, 81, C)
+    t = torch.cat([rows.mean(1, keepdim=True), rows], 1) + m.folded().pos
+    got = m._pool_tokens(t)
     torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4)
 
 
