@@ -32,6 +32,36 @@ __device__ __forceinline__ void lex_min(double& m, int& k, double om, int ok) {
     }
 }
 
+// one DPP step of the wave reduction: combine with the (value, key) of the lane that dpp_ctrl
+// names; a lane whose source is outside its row (or whose row is masked off) keeps its own
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ void lex_dpp(double& m, int& k) {
+    const long long mb = __double_as_longlong(m);
+    const int lo = (int)mb, hi = (int)(mb >> 32);
+    const int olo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROW_MASK, 0xf, false);
+    const int ohi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROW_MASK, 0xf, false);
+    const int ok = __builtin_amdgcn_update_dpp(k, k, CTRL, ROW_MASK, 0xf, false);
+    lex_min(m, k, __longlong_as_double(((long long)ohi << 32) | (unsigned)olo), ok);
+}
+
+// (value, key) lexicographic minimum over the 64 lanes, returned to every lane: row_shr 1/2/4/8
+// leave each row's minimum in its lane 15, row_bcast 15/31 carry it into lane 63, one readlane
+// broadcasts it (a total order with unique keys: the same result as any reduction order, i.e.
+// as the xor-shuffle tree this replaces, without its LDS-routed permutes)
+__device__ __forceinline__ void wave_lex_min(double& m, int& k) {
+    lex_dpp<0x111, 0xf>(m, k);   // row_shr:1
+    lex_dpp<0x112, 0xf>(m, k);   // row_shr:2
+    lex_dpp<0x114, 0xf>(m, k);   // row_shr:4
+    lex_dpp<0x118, 0xf>(m, k);   // row_shr:8
+    lex_dpp<0x142, 0xa>(m, k);   // row_bcast:15 into rows 1, 3
+    lex_dpp<0x143, 0xc>(m, k);   // row_bcast:31 into rows 2, 3
+    const long long mb = __double_as_longlong(m);
+    const int lo = __builtin_amdgcn_readlane((int)mb, 63);
+    const int hi = __builtin_amdgcn_readlane((int)(mb >> 32), 63);
+    k = __builtin_amdgcn_readlane(k, 63);
+    m = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 // STAGED: the problem's Q x n costs are copied to LDS in the solver's (row, column) order while
 // the NaN screen reads them, so every augmenting step reads its row from LDS (consecutive lanes,
 // consecutive columns) instead of a strided row of the global matrix at L2 latency.
@@ -129,12 +159,7 @@ __global__ __launch_bounds__(64) void hungarian_kernel(const float* __restrict__
                 const int k = row4col[j] < 0 ? (nc - 1 - pos[j]) : (nc + pos[j]);
                 lex_min(bm, bk, s, k);
             }
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                const double om = __shfl_xor(bm, off);
-                const int ok = __shfl_xor(bk, off);
-                lex_min(bm, bk, om, ok);
-            }
+            wave_lex_min(bm, bk);
             minv = bm;
             if (!(bm < INF)) {
                 rc = -2;
