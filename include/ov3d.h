@@ -364,6 +364,14 @@ int ov3d_roi_align_fwd(const void* feat, int is_bf16, int N, int H, int W, int C
                        const float* boxes, int R, int per_image, int nimages, float spatial_scale,
                        int pooled, int sampling_ratio, int aligned, void* out, void* stream);
 
+/* ov3d_roi_align_fwd plus the 2x2 average pool of its output [the AvgPool2d(2) of res5's first
+ * Bottleneck identity path, upstream CLIP ModifiedResNet] in the same launch:
+ *   pooled_out (R, pooled/2, pooled/2, C) = ov3d_avgpool2_nhwc(out), bit for bit; pooled even. */
+int ov3d_roi_align_pool2_fwd(const void* feat, int is_bf16, int N, int H, int W, int C,
+                             const float* boxes, int R, int per_image, int nimages,
+                             float spatial_scale, int pooled, int sampling_ratio, int aligned,
+                             void* out, void* pooled_out, void* stream);
+
 /* NHWC im2col for a 3x3 convolution (pad 1, stride 1|2) of the RegionCLIP
  * ModifiedResNet [upstream CLIP/RegionCLIP; the convolutions of clip.inference,
  * criterion.py:397], so that the convolution is one GEMM against the

@@ -51,6 +51,7 @@ _SIGS = {
     "ov3d_nms_boxes_from_corners": "pppiipp",
     "ov3d_clip_preprocess": "plppiiifffffffipp",
     "ov3d_roi_align_fwd": "piiiiipiiifiiipp",
+    "ov3d_roi_align_pool2_fwd": "piiiiipiiifiiippp",
     "ov3d_im2col3x3": "piiiiiiipp",
     "ov3d_bias_residual_act": "pilippip",
     "ov3d_avgpool2_nhwc": "piiiiipp",

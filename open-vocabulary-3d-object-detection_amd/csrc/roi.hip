@@ -128,6 +128,62 @@ __global__ void __launch_bounds__(256) roi_align_kernel(
     *reinterpret_cast<uint4*>(out + (((size_t)r * P + ph) * P + pw) * C + cv * VEC) = ov;
 }
 
+// The same bins, a 2x2 block of them per thread, plus their 2x2 average pool (the res5 identity
+// path's nn.AvgPool2d(2) over the ROIAlign output, torch's arithmetic as ov3d_avgpool2_nhwc:
+// fp32 (((0 + b00) + b01) + b10) + b11 of the rounded bins, / 4) written beside them, so the
+// pool does not read the (R, P, P, C) output back.  P even, 32-bit indices.
+template <typename T, int VEC>
+__global__ void __launch_bounds__(256) roi_align_pool2_kernel(
+    const T* __restrict__ feat, int H, int W, int C, const float* __restrict__ boxes, int R,
+    int per_image, int nimages, float scale, int P, int sampling_ratio, int aligned,
+    T* __restrict__ out, T* __restrict__ pooled) {
+    static_assert(VEC * sizeof(T) == 16, "one 16-byte channel run per thread");
+    const int CV = C / VEC, P2 = P / 2;
+    const int total = R * P2 * P2 * CV;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= total) return;
+    const int cv = t % CV;
+    int q = t / CV;
+    const int pw2 = q % P2;
+    q /= P2;
+    const int ph2 = q % P2;
+    const int r = q / P2;
+    const int img = (r / per_image) % nimages;
+    const T* f = feat + (size_t)img * H * W * C + cv * VEC;
+    float psum[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) psum[j] = 0.f;
+    for (int dy = 0; dy < 2; ++dy) {
+        for (int dx = 0; dx < 2; ++dx) {
+            const int ph = 2 * ph2 + dy, pw = 2 * pw2 + dx;
+            const Bin b = bin_geometry(boxes + 4 * (size_t)r, scale, aligned, P, ph, pw, sampling_ratio);
+            float acc[VEC];
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+            for (int iy = 0; iy < b.gh; ++iy) {
+                const float y = b.y0 + (float)(iy + .5f) * b.bh / (float)b.gh;
+                for (int ix = 0; ix < b.gw; ++ix) {
+                    const float x = b.x0 + (float)(ix + .5f) * b.bw / (float)b.gw;
+                    bilinear_acc<T, VEC>(f, H, W, C, y, x, acc);
+                }
+            }
+            uint4 ov;
+            T* oe = reinterpret_cast<T*>(&ov);
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) {
+                oe[j] = (T)(acc[j] / b.count);
+                psum[j] += (float)oe[j];
+            }
+            *reinterpret_cast<uint4*>(out + (((size_t)r * P + ph) * P + pw) * C + cv * VEC) = ov;
+        }
+    }
+    uint4 pv;
+    T* pe = reinterpret_cast<T*>(&pv);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) pe[j] = (T)(psum[j] / 4.f);
+    *reinterpret_cast<uint4*>(pooled + (((size_t)r * P2 + ph2) * P2 + pw2) * C + cv * VEC) = pv;
+}
+
 // CLIPFastRCNN.preprocess_image + ImageList.from_tensors: the (H_b, W_b, 3) view of
 // each padded 1-D image buffer (criterion.py:371-375), (v * (1/div) - mean) / std per
 // channel, zero-padded to (Hp, Wp), written NHWC.
@@ -197,6 +253,33 @@ extern "C" int ov3d_roi_align_fwd(const void* feat, int is_bf16, int N, int H, i
         roi_align_kernel<float, 4, long long><<<blocks, 256, 0, s>>>(
             (const float*)feat, H, W, C, boxes, R, per_image, nimages, spatial_scale, pooled,
             sampling_ratio, aligned, (float*)out);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_roi_align_pool2_fwd(const void* feat, int is_bf16, int N, int H, int W, int C,
+                                        const float* boxes, int R, int per_image, int nimages,
+                                        float spatial_scale, int pooled, int sampling_ratio,
+                                        int aligned, void* out, void* pooled_out, void* stream) {
+    if (!feat || !boxes || !out || !pooled_out || N <= 0 || H <= 0 || W <= 0 || C <= 0 || R < 0 ||
+        pooled <= 0 || (pooled & 1) || per_image <= 0 || nimages <= 0 || nimages > N)
+        return OV3D_EINVAL;
+    if (R == 0) return OV3D_OK;
+    const int vec = is_bf16 ? 8 : 4;
+    if (C % vec || ((uintptr_t)feat | (uintptr_t)out | (uintptr_t)pooled_out) & 15) return OV3D_EINVAL;
+    const long long total = (long long)R * (pooled / 2) * (pooled / 2) * (C / vec);
+    if (total + 256 > 0x7fffffffLL || (long long)R * pooled * pooled * C > (1LL << 40))
+        return OV3D_EINVAL;
+    const int blocks = ov3d_cdiv(total, 256);
+    hipStream_t s = ov3d_stream(stream);
+    if (is_bf16)
+        roi_align_pool2_kernel<bf16, 8><<<blocks, 256, 0, s>>>(
+            (const bf16*)feat, H, W, C, boxes, R, per_image, nimages, spatial_scale, pooled,
+            sampling_ratio, aligned, (bf16*)out, (bf16*)pooled_out);
+    else
+        roi_align_pool2_kernel<float, 4><<<blocks, 256, 0, s>>>(
+            (const float*)feat, H, W, C, boxes, R, per_image, nimages, spatial_scale, pooled,
+            sampling_ratio, aligned, (float*)out, (float*)pooled_out);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

@@ -482,7 +482,8 @@ class RegionCLIP(nn.Module):
             x = self._res_layer(x, lname)
         return x
 
-    def _res_layer(self, x, lname):
+    def _res_layer(self, x, lname, x_pooled=None):
+        """x_pooled: _avgpool2(x) when the caller already has it (the ROIAlign launch)"""
         fw = self.folded()
         for i, blk in enumerate(getattr(self.backbone, lname)):
             key = f"{lname}.{i}"
@@ -492,7 +493,10 @@ class RegionCLIP(nn.Module):
             if blk.stride > 1:
                 out = _avgpool2(out)
             if blk.downsample is not None:
-                xi = _avgpool2(x) if blk.stride > 1 else x
+                if blk.stride > 1:
+                    xi = x_pooled if (i == 0 and x_pooled is not None) else _avgpool2(x)
+                else:
+                    xi = x
                 identity = _conv1x1(xi, *c[key + ".down"], relu=False)
             else:
                 identity = x
@@ -531,10 +535,19 @@ class RegionCLIP(nn.Module):
         feats = _native.check(feats.contiguous(), "res4 features", ndim=4)
         boxes = _native.check(boxes.contiguous(), "boxes", dtype=torch.float32, ndim=2)
         x = torch.empty((R, P, P, C), dtype=feats.dtype, device=feats.device)
-        _native.call("ov3d_roi_align_fwd", feats, int(feats.dtype == torch.bfloat16), N, H, W, C,
-                     boxes, R, per_image, nimages, self.spatial_scale, P, self.sampling_ratio, 1, x,
-                     like=feats)
-        x = self._res_layer(x, "layer4")
+        blk0 = self.backbone.layer4[0]
+        xp = None
+        if P % 2 == 0 and blk0.stride > 1 and blk0.downsample is not None:
+            # the first block's identity pool comes out of the ROIAlign launch itself
+            xp = torch.empty((R, P // 2, P // 2, C), dtype=feats.dtype, device=feats.device)
+            _native.call("ov3d_roi_align_pool2_fwd", feats, int(feats.dtype == torch.bfloat16), N, H,
+                         W, C, boxes, R, per_image, nimages, self.spatial_scale, P,
+                         self.sampling_ratio, 1, x, xp, like=feats)
+        else:
+            _native.call("ov3d_roi_align_fwd", feats, int(feats.dtype == torch.bfloat16), N, H, W,
+                         C, boxes, R, per_image, nimages, self.spatial_scale, P,
+                         self.sampling_ratio, 1, x, like=feats)
+        x = self._res_layer(x, "layer4", x_pooled=xp)
         return self._attnpool(x)
 
     def _attnpool(self, x):

@@ -58,7 +58,9 @@ def test_c5_training_step_full_size(cuda):
     for k in keys:
         v = ld[k].item()
         assert v == v and 0 < v < 1e3, (k, v)
-    assert called.get("ov3d_roi_align_fwd") == 1, called.get("ov3d_roi_align_fwd")
+    # one ROIAlign launch for all L*B*Q boxes (with res5's first identity pool fused in)
+    n_roi = called.get("ov3d_roi_align_fwd", 0) + called.get("ov3d_roi_align_pool2_fwd", 0)
+    assert n_roi == 1, called
     assert called.get("ov3d_clip_preprocess") == 1, called.get("ov3d_clip_preprocess")
     bad = [n for n, p in model.named_parameters() if p.grad is not None and not torch.isfinite(p.grad).all()]
     assert not bad, bad

@@ -50,6 +50,15 @@ def test_roi_align_bit_exact(cuda, dtype, C, H, W, R, per, nimg):
         ref = torch.from_numpy(ref).to(torch.bfloat16).float().numpy()
     np.testing.assert_array_equal(out.float().cpu().numpy(), ref)
     assert (out[0] == 0).all()
+    # the fused form: the same bins, plus their 2x2 pool bit-equal to torch's avg_pool2d
+    out2 = torch.empty_like(out)
+    pooled = torch.empty((R, P // 2, P // 2, C), dtype=dtype, device=cuda)
+    _native.call("ov3d_roi_align_pool2_fwd", fg, int(dtype == torch.bfloat16), nimg, H, W, C,
+                 torch.from_numpy(boxes).to(cuda), R, per, nimg, 1.0 / 16, P, 0, 1, out2, pooled,
+                 like=fg)
+    assert torch.equal(out2, out)
+    import torch.nn.functional as F
+    assert torch.equal(pooled, F.avg_pool2d(out.permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1))
 
 
 def test_clip_preprocess_bit_exact(cuda):
