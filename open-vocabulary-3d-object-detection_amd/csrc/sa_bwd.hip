@@ -814,7 +814,11 @@ extern "C" int ov3d_sa_dy_fused(const void* yprev, const float* scale, const flo
         return OV3D_EINVAL;
     DyFusedArgs a{(const bf16*)yprev, scale, shift, (const bf16*)W, R, S, gsel, isel, cA, cB, cC,
                   (bf16*)dz, dwpart, mean, invstd, stats};
-    static const bool four = getenv("OV3D_SA_DY4") != nullptr;   // A/B: the 4-wave kernel
+    static const bool four_env = getenv("OV3D_SA_DY4") != nullptr;   // A/B: the 4-wave kernel
+    // sa_dy8 addresses the previous layer's rows through a buffer resource with 32-bit tile
+    // offsets (num_records clamped to 2^31 - 1 bytes): past that the loads would return zeros.
+    // The 4-wave kernel indexes with 64-bit addresses, so larger inputs go there.
+    const bool four = four_env || (long long)R * K * 2 > 0x7fffffffLL;
     if (four) {
         if (stats)
             hipLaunchKernelGGL((sa_dy_fused_kernel<128, 256, true>), dim3(nwg), dim3(kThreads), 0,

@@ -64,8 +64,14 @@ def capture_safe_env():
     event of an eager work (graph warm-up) still on the watchdog's list could be handed to a
     work recorded during capture, and the watchdog's query of it then aborts the process
     ("operation not permitted on an event last recorded in a capturing stream").  Without the
-    cache every work owns its events."""
-    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+    cache every work owns its events.  Forced, not defaulted: an environment that switches the
+    cache on would re-arm the abort, so it is overridden (with a warning)."""
+    prev = os.environ.get("TORCH_NCCL_CUDA_EVENT_CACHE")
+    if prev not in (None, "0"):
+        import warnings
+        warnings.warn(f"TORCH_NCCL_CUDA_EVENT_CACHE={prev} overridden to 0: the captured step's "
+                      "collectives need every work to own its events (dist.capture_safe_env)")
+    os.environ["TORCH_NCCL_CUDA_EVENT_CACHE"] = "0"
 
 
 def init_from_env(backend=None):

@@ -188,8 +188,10 @@ class StepGraph:
         """-> dict of the step's point-only index work (extra model inputs)"""
         if hasattr(self.model, "sampling_plan"):
             return self.model.sampling_plan(pc)
-        return {"pre_enc_inds": self._pu.furthest_point_sample(pc[..., 0:3].contiguous(),
-                                                               self.npoint)}
+        # the gather form: no host sync on the side stream (furthest_point_sample's eager
+        # two-workgroup status check would block the host until the previous step retired)
+        return {"pre_enc_inds": self._pu.furthest_point_sample_gather(
+            pc[..., 0:3].contiguous(), self.npoint)[0]}
 
     def _set_plan(self, plan):
         from . import _native

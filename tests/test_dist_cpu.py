@@ -335,3 +335,16 @@ def test_syncbn_rows_momentum_none_and_no_affine_world2():
             np.testing.assert_allclose(gw, bn.weight.grad, rtol=1e-9, atol=1e-9)
         else:
             assert got[0][name]["gw"] is None
+
+
+def test_capture_safe_env_forces_event_cache_off(monkeypatch):
+    """dist.capture_safe_env overrides an environment that switched ProcessGroupNCCL's event
+    cache on (a recycled event inside a captured step aborted the process, DESIGN.md Multi-GPU)"""
+    from ov3d_amd import dist as pdist
+    monkeypatch.setenv("TORCH_NCCL_CUDA_EVENT_CACHE", "1")
+    with pytest.warns(UserWarning, match="TORCH_NCCL_CUDA_EVENT_CACHE"):
+        pdist.capture_safe_env()
+    assert os.environ["TORCH_NCCL_CUDA_EVENT_CACHE"] == "0"
+    monkeypatch.delenv("TORCH_NCCL_CUDA_EVENT_CACHE")
+    pdist.capture_safe_env()
+    assert os.environ["TORCH_NCCL_CUDA_EVENT_CACHE"] == "0"

@@ -112,6 +112,160 @@ def _rank(rank, port, out_dir, conf):
     torch.distributed.destroy_process_group()
 
 
+def _rank_bench(rank, port, out_dir, conf):
+    """one rank of the bench's own data-parallel wiring (bench.build(..., sync_bn=True,
+    allreduce=True, staged=True) as bench.main builds it at N > 1): SyncBatchNorm inside the
+    fused BN launches, dist.GradBuckets on a process group of its own with bucket 0 started by
+    dist.stage_after_encoder's hook after the deferred weight-gradient flush, FusedAdamW
+    finishing the buckets, scaling by 1/world, clipping and updating"""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(WORLD), LOCAL_RANK="0")
+    torch.distributed.init_process_group("gloo", init_method="env://", world_size=WORLD, rank=rank)
+    import sys
+    sys.path.insert(0, ROOT)
+    import ov3d_import
+    ov3d_import.load()
+    import bench
+    from ov3d_amd import gemm, synthetic
+    c = CONFIGS[conf]
+    args = bench.default_args(enc_dropout=0.0, dec_dropout=0.0, mlp_dropout=0.0, **c["args"])
+    dev = torch.device("cuda", 0)
+    gemm.DEFER_WGRAD = True
+    model, crit, opt = bench.build(args, dev, sync_bn=True, allreduce=True, staged=True)
+    assert opt.grad_buckets is not None
+    pinned = torch.load(os.path.join(out_dir, "match.pt"), weights_only=True)[rank]
+    _pin(crit, [t.to(dev) for t in pinned])
+    n = c["per_rank"]
+    batch = synthetic.make_batch(WORLD * n, seed=12, num_points=c["points"], device=dev)
+    b = {k: v[rank * n: (rank + 1) * n] for k, v in batch.items()}
+    buckets = model.dp_buckets()
+    order = {}
+    hook = model.encoder_grad_hook
+
+    def spy():
+        order["enc_grads_at_hook"] = sum(p.grad is not None for p in buckets[1])
+        order["dec_grads_at_hook"] = sum(p.grad is not None for p in buckets[0])
+        hook()
+        order["launched_in_hook"] = opt.grad_buckets.launched(0)
+        order["launched_1_in_hook"] = opt.grad_buckets.launched(1)
+    model.encoder_grad_hook = spy
+    loss = bench.train_step(model, crit, opt, b, args, torch.bfloat16)
+    torch.cuda.synchronize()
+    items, _, _ = opt._params()
+    names = {id(p): k for k, p in model.named_parameters()}
+    torch.save({"loss": loss.item(), "order": order,
+                "grad_norm": float(opt.last_grad_norm.item()),
+                "grads": {names[id(p)]: g.float().cpu() for (p, _), g in zip(items, opt.flat_grads())},
+                "params": {k: p.detach().cpu() for k, p in model.named_parameters()},
+                "bufs": {k: t.cpu() for k, t in model.named_buffers()}},
+               os.path.join(out_dir, f"r{rank}.pt"))
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("conf", sorted(CONFIGS))
+def test_world2_bench_dp_path_equals_global_batch_step(cuda, conf):
+    """The code bench.py runs at N > 1, at world 2 (two processes on cuda:0 over gloo): the
+    averaged, clipped gradients the optimizer consumed equal the single-process global-batch
+    step's within the bf16 noise bars of the test above, both ranks hold identical gradients
+    and parameters, the update is AdamW's on those gradients, and bucket 0 (decoder side) left
+    inside the backward, before any encoder gradient existed.  Reference: main.py:427-431
+    (DDP + SyncBatchNorm), utils/dist.py:67-110."""
+    import bench
+    from ov3d_amd import criterion as crit_mod
+    from ov3d_amd import dist as pdist
+    from ov3d_amd import gemm
+    model, crit, batch, dev, n = _setup(conf)
+    p0 = {k: p.detach().clone() for k, p in model.named_parameters()}
+    rec = {}
+    _recording(crit, rec)
+    nbox = batch["gt_box_present"].sum(dim=1)
+    saved = (crit_mod.all_reduce_average, pdist.all_reduce_average, pdist.get_world_size)
+    crit_mod.all_reduce_average = pdist.all_reduce_average = lambda t: nbox.sum() / WORLD
+    pdist.get_world_size = lambda: WORLD
+    saved_defer = gemm.DEFER_WGRAD
+
+    def global_step(amp):
+        model.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            out = model(_inputs(batch))
+        losses = [crit(_slice_outputs(out, r, n), {k: v[r * n: (r + 1) * n] for k, v in batch.items()})[0]
+                  for r in range(WORLD)]
+        (sum(losses) / WORLD).backward()
+        gemm.flush_weight_grads()
+        return [x.item() for x in losses], {k: p.grad.float().clone()
+                                            for k, p in model.named_parameters()
+                                            if p.grad is not None}
+    try:
+        gemm.DEFER_WGRAD = True
+        state = {k: v.clone() for k, v in model.state_dict().items()}
+        _, g32 = global_step(False)
+        model.load_state_dict(state)
+        losses, g16 = global_step(True)
+    finally:
+        crit_mod.all_reduce_average, pdist.all_reduce_average, pdist.get_world_size = saved
+        gemm.DEFER_WGRAD = saved_defer
+    with tempfile.TemporaryDirectory() as d:
+        torch.save({r: [t.cpu() for t in rec[r]] for r in range(WORLD)}, os.path.join(d, "match.pt"))
+        mp.spawn(_rank_bench, args=(_free_port(), d, conf), nprocs=WORLD, join=True)
+        res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(WORLD)]
+    args = bench.default_args(**CONFIGS[conf]["args"])
+    # the staged bucket: launched by the hook, with the decoder side complete and no encoder
+    # gradient yet; the encoder bucket only by the optimizer
+    for r in range(WORLD):
+        o = res[r]["order"]
+        assert o["launched_in_hook"] and not o["launched_1_in_hook"], o
+        assert o["enc_grads_at_hook"] == 0 and o["dec_grads_at_hook"] > 0, o
+        assert abs(res[r]["loss"] - losses[r]) <= 5e-3 * abs(losses[r]), r
+    # clip_grad_norm_(0.1) of the mean gradient (torch's coefficient, clamped at 1)
+    def clipped(g):
+        tot = torch.sqrt(sum((v.double() ** 2).sum() for v in g.values())).item()
+        return {k: v * min(1.0, args.clip_gradient / (tot + 1e-6)) for k, v in g.items()}, tot
+    c16, n16 = clipped(g16)
+    c32, _ = clipped(g32)
+    assert abs(res[0]["grad_norm"] - n16) <= 2e-2 * n16, (res[0]["grad_norm"], n16)
+    checked = 0
+    ratios = []
+    for k, g in c16.items():
+        assert torch.equal(res[0]["grads"][k], res[1]["grads"][k]), k
+        assert torch.equal(res[0]["params"][k], res[1]["params"][k]), k
+        g = g.cpu()
+        if g.norm() > 1e-9:
+            err = ((res[0]["grads"][k] - g).norm() / g.norm()).item()
+            noise = ((g - c32[k].cpu()).norm() / c32[k].cpu().norm().clamp_min(1e-12)).item()
+            bar = max(3e-2, 4.0 * noise)
+            ratios.append((err / max(noise, 1e-3), k, err, noise, bar))
+            checked += 1
+    worst = sorted(ratios, reverse=True)
+    print("largest err/noise:", [("%.1f" % r, k, "%.2e" % e, "%.2e" % z) for r, k, e, z, _ in worst[:12]])
+    bad = [(k, e, z) for r, k, e, z, b in worst if e >= b]
+    assert not bad, bad
+    med = sorted(r for r, *_ in ratios)[len(ratios) // 2]
+    print(f"{checked} clipped gradients checked, median err/noise {med:.2f}")
+    assert med <= 1.5, med
+    assert checked > 100
+    # the update: torch.optim.AdamW's first step on the gradients the optimizer consumed
+    lr, wd, b1, b2, eps = args.base_lr, args.weight_decay, 0.9, 0.999, 1e-8
+    nupd = 0
+    for k, p in p0.items():
+        if k not in res[0]["grads"]:
+            continue
+        g = res[0]["grads"][k].double()
+        x = p.cpu().double() * (1 - lr * wd)
+        denom = (((1 - b2) * g * g).sqrt() / (1 - b2) ** 0.5) + eps
+        want = x - (lr / (1 - b1)) * ((1 - b1) * g) / denom
+        torch.testing.assert_close(res[0]["params"][k].double(), want, rtol=1e-6, atol=1e-7, msg=k)
+        nupd += 1
+    assert nupd >= checked
+    nb = 0
+    for k, t in model.named_buffers():
+        if k.endswith(("running_mean", "running_var")):
+            torch.testing.assert_close(res[0]["bufs"][k], t.cpu(), rtol=2e-2, atol=2e-3, msg=k)
+            torch.testing.assert_close(res[0]["bufs"][k], res[1]["bufs"][k], rtol=0, atol=0, msg=k)
+            nb += 1
+    assert nb >= 16
+
+
 @pytest.mark.parametrize("conf", sorted(CONFIGS))
 def test_world2_step_equals_global_batch_step(cuda, conf):
     from ov3d_amd import criterion as crit_mod
