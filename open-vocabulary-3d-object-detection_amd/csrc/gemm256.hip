@@ -1,0 +1,435 @@
+// Large bf16 GEMM on 256 x 256 output tiles, and the 3x3 convolution as an implicit GEMM on
+// the same main loop, for the RegionCLIP ROI path (res5 of the RN50x4
+// ModifiedResNet over all L*B*Q ROIs, clip.inference at criterion.py:397) and the 3DETR
+// decoder's memory K / V projections (models/transformer.py:369-372):
+//
+//   C (M, N) = act(A (M, K) . B (N, K)^T + bias (N) [+ R (M, N)]),  bf16 in / out, fp32 sums
+//
+// A and B are row-major with K contiguous (activations rows x weight rows: the "NT" product
+// of a linear layer / 1x1 convolution).  In the convolution form A is never materialised: row
+// m of A is output pixel (n, y, x) of an NHWC input (nimg, H, W, C) and column k = (ky*3 +
+// kx)*C + c reads input pixel (y + ky - 1, x + kx - 1), zero outside the image (pad 1,
+// stride 1) -- the (Cout, 3, 3, C) channels-last weight viewed as (Cout, 9C) is B.
+//
+// Main loop (cdna_hip_programming.md §5, "The 256^2 8-phase template"):
+//   * 512 threads = 8 waves, wave (wr, wc) = (wave >> 2, wave & 3) owns output rows
+//     mi*128 + wr*64 + [0, 64) and columns ni*128 + wc*32 + [0, 32), mi, ni in {0, 1};
+//   * K-steps of 64; each operand tile (256 x 64) is held as two halves (rows 0-127 / 128-255)
+//     of 16 KB, two LDS buffers: 128 KB.  Halves are filled by LDS-DMA (buffer_load ... lds,
+//     16 bytes a lane, lane-linear destination; the 16-byte chunks of a 128-byte row are
+//     XOR-swizzled by (row >> 1) & 7 through the per-lane SOURCE offset, which makes the
+//     16x16x32 fragment reads ds_read_b128 conflict-free);
+//   * four phases per K-step, one C quadrant (64 x 32 per wave: 16 MFMAs 16x16x32) each:
+//       P0: read B_lo + A_lo fragments -> Q(lo, lo)      P1: read B_hi -> Q(lo, hi)
+//       P2: read A_hi                  -> Q(hi, hi)      P3: (no reads)  -> Q(hi, lo)
+//     each phase issues ONE half-tile of LDS-DMA (2 instructions a thread) into the buffer
+//     half whose last read is far enough behind: P0 A_hi(t+1), P1 B_lo(t+2), P2 A_lo(t+2),
+//     P3 B_hi(t+2); one counted vmcnt(6) per K-step (P3) retires K-step t+1 and leaves three
+//     half-tiles in flight across the barriers (raw s_barrier, never __syncthreads inside
+//     the loop: its fence would drain the DMA);
+//   * waves 4-7 (wr = 1) run one barrier behind waves 0-3: each SIMD holds one wave of each
+//     group, so one computes while its partner reads and issues (the stagger of §5; every
+//     restage respects the extra barrier: the 1-phase restage of B_lo is ordered by an
+//     lgkmcnt(8) before P0's first barrier, the others are 2 phases behind their last read);
+//   * XCD-aware tile order (consecutive tiles of one row panel on one XCD, bijective remap).
+// Epilogue: per row half, the fp32 quadrants go through LDS ([128][260] f32), then every
+// thread owns 8 consecutive columns of a row: + bias, + residual (fp32), ReLU, one rounding,
+// one 16-byte store.
+#include "common.h"
+
+namespace {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BK = 64;
+constexpr int HALF = 128 * BK * 2;   // bytes of one 128-row half of an operand K-step
+constexpr int BUF = 4 * HALF;        // A_lo, A_hi, B_lo, B_hi
+constexpr int EPI_LD = 260;          // floats per staged epilogue row (+4: conflict-free writes)
+constexpr int LDS_BYTES = 128 * EPI_LD * 4 > 2 * BUF ? 128 * EPI_LD * 4 : 2 * BUF;
+constexpr uint32_t OOB = 0x80000000u;   // buffer offset past num_records: the load returns 0
+
+struct Gemm256Args {
+    const bf16* A;     // dense: (M, K) rows, lda; conv: NHWC input (nimg, H, W, C)
+    long long lda;
+    const bf16* B;     // (N, K) rows, ldb
+    long long ldb;
+    const void* bias;  // (N) bf16 or f32, or null
+    const bf16* R;     // residual (M, N), ldr, or null
+    long long ldr;
+    bf16* C;
+    long long ldc;
+    int M, N, K;
+    int bias_f32, relu;
+    int H, W, Cin;     // conv form
+};
+
+__device__ __forceinline__ f32x4 mfma16(i32x4 a, i32x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+// ds_read_b128 as an asm statement: hipcc would otherwise treat the LDS read as aliasing the
+// in-flight LDS-DMA and wait vmcnt(0) before it.  The result is unprotected until a wait
+// statement names it (lgkm_wait*).
+template <int OFF>
+__device__ __forceinline__ i32x4 lds128(uint32_t addr) {
+    i32x4 r;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF) : "memory");
+    return r;
+}
+
+__device__ __forceinline__ void lgkm_wait12(i32x4 (&a)[8], i32x4 (&b)[4]) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
+                   "+v"(a[6]), "+v"(a[7]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])
+                 :
+                 : "memory");
+}
+__device__ __forceinline__ void lgkm_wait8(i32x4 (&a)[8]) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
+                   "+v"(a[6]), "+v"(a[7])
+                 :
+                 : "memory");
+}
+__device__ __forceinline__ void lgkm_wait4(i32x4 (&b)[4]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]) : : "memory");
+}
+
+__device__ __forceinline__ void barrier() { __builtin_amdgcn_s_barrier(); }
+
+// one quadrant: 4 x 2 tiles of 16 x 16, K = 64 (two 32-deep MFMA steps)
+__device__ __forceinline__ void mma_quad(f32x4 (&acc)[4][2], const i32x4 (&fa)[8], const i32x4 (&fb)[4]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(fa[2 * i + kh], fb[2 * j + kh], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+}
+
+// 8 A fragments of a half (rows wr*64 + 16 i + (lane & 15)), OFF = the half's byte offset
+template <int OFF>
+__device__ __forceinline__ void read_a(i32x4 (&fa)[8], uint32_t p0, uint32_t p1) {
+    fa[0] = lds128<OFF + 0 * 2048>(p0);
+    fa[1] = lds128<OFF + 0 * 2048>(p1);
+    fa[2] = lds128<OFF + 1 * 2048>(p0);
+    fa[3] = lds128<OFF + 1 * 2048>(p1);
+    fa[4] = lds128<OFF + 2 * 2048>(p0);
+    fa[5] = lds128<OFF + 2 * 2048>(p1);
+    fa[6] = lds128<OFF + 3 * 2048>(p0);
+    fa[7] = lds128<OFF + 3 * 2048>(p1);
+}
+template <int OFF>
+__device__ __forceinline__ void read_b(i32x4 (&fb)[4], uint32_t p0, uint32_t p1) {
+    fb[0] = lds128<OFF + 0 * 2048>(p0);
+    fb[1] = lds128<OFF + 0 * 2048>(p1);
+    fb[2] = lds128<OFF + 1 * 2048>(p0);
+    fb[3] = lds128<OFF + 1 * 2048>(p1);
+}
+
+__device__ __forceinline__ void glds(__amdgpu_buffer_rsrc_t rs, char* lds, uint32_t voff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
+    const uint32_t n = bytes > 0x7fffffffLL ? 0x7fffffffu : (uint32_t)(bytes > 0 ? bytes : 0);
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)n, 0x00020000);
+}
+
+template <bool CONV>
+__global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
+    __shared__ __attribute__((aligned(16))) char L[LDS_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave >> 2, wc = wave & 3;
+
+    // XCD-aware tile order: blocks b and b + 8 share an XCD; logical tiles lt are dealt so that
+    // each XCD gets a contiguous range (n fastest: the n tiles of one A row panel together)
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+    const int lt = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+    const int ntn = (a.N + 255) >> 8;
+    const int tm = lt / ntn, tn = lt - tm * ntn;
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int nk = a.K / BK;
+
+    // ---- LDS-DMA sources.  Wave w fills rows 16 w + 8 j + (lane >> 3) of each half (j = 0, 1),
+    // physical chunk lane & 7 <- logical chunk (lane & 7) ^ ((row >> 1) & 7)
+    const int lrow0 = 16 * wave + (lane >> 3);             // j = 0; j = 1: + 8
+    const int lc0 = (lane & 7) ^ ((lane >> 4) & 7);        // (row >> 1) & 7 for j = 0
+    const int lc1 = (lane & 7) ^ (((lane >> 4) + 4) & 7);  // for j = 1
+    const __amdgpu_buffer_rsrc_t rsB =
+        make_rsrc(a.B + (long long)n0 * a.ldb, (long long)(a.N - n0) * a.ldb * 2);
+    uint32_t vB[4];   // [half][j]
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            vB[2 * h + j] = (uint32_t)((128 * h + lrow0 + 8 * j) * a.ldb * 2) + 16u * (j ? lc1 : lc0);
+
+    __amdgpu_buffer_rsrc_t rsA;
+    uint32_t vA[4];
+    // conv form: the row's pixel offset and the validity of its 9 taps
+    uint32_t pix[4] = {0, 0, 0, 0}, tapok[4] = {0, 0, 0, 0};
+    int tap = 0, c0 = 0;
+    if constexpr (!CONV) {
+        rsA = make_rsrc(a.A + (long long)m0 * a.lda, (long long)(a.M - m0) * a.lda * 2);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                vA[2 * h + j] = (uint32_t)((128 * h + lrow0 + 8 * j) * a.lda * 2) + 16u * (j ? lc1 : lc0);
+    } else {
+        const int HW = a.H * a.W;
+        const int img0 = m0 / HW;
+        rsA = make_rsrc(a.A + (long long)img0 * HW * a.Cin, (long long)(a.M - img0 * HW) * a.Cin * 2);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int m = m0 + 128 * h + lrow0 + 8 * j;
+                const int n = m / HW, rem = m - n * HW, y = rem / a.W, x = rem - y * a.W;
+                uint32_t ok = 0;
+                if (m < a.M) {
+#pragma unroll
+                    for (int t = 0; t < 9; ++t) {
+                        const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+                        ok |= (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) ? (1u << t) : 0u;
+                    }
+                }
+                tapok[2 * h + j] = ok;
+                pix[2 * h + j] = (uint32_t)(((n - img0) * HW + rem) * a.Cin * 2) + 16u * (j ? lc1 : lc0);
+            }
+    }
+    // per K-step A offsets of the conv form: tap (ky, kx) and channel block c0 of step kt
+    auto conv_voff = [&](int i, int t, int c) -> uint32_t {
+        const int toff = ((t / 3 - 1) * a.W + (t % 3 - 1)) * a.Cin * 2;
+        return ((tapok[i] >> t) & 1u) ? pix[i] + (uint32_t)(toff + 2 * c) : OOB;
+    };
+
+    // half h (0 A_lo, 1 A_hi, 2 B_lo, 3 B_hi) of K-step kt into LDS buffer kt & 1
+    auto stage = [&](int h, int kt, int ctap, int cc) {
+        char* dst = L + (kt & 1) * BUF + h * HALF + 16 * wave * 128;
+        if (h >= 2) {
+            const uint32_t ko = (uint32_t)kt * (BK * 2);
+            glds(rsB, dst, vB[2 * (h - 2)] + ko);
+            glds(rsB, dst + 8 * 128, vB[2 * (h - 2) + 1] + ko);
+        } else if constexpr (!CONV) {
+            const uint32_t ko = (uint32_t)kt * (BK * 2);
+            glds(rsA, dst, vA[2 * h] + ko);
+            glds(rsA, dst + 8 * 128, vA[2 * h + 1] + ko);
+        } else {
+            glds(rsA, dst, conv_voff(2 * h, ctap, cc));
+            glds(rsA, dst + 8 * 128, conv_voff(2 * h + 1, ctap, cc));
+        }
+    };
+    // (tap, c0) of K-step kt in the conv form, advanced incrementally for kt+1 and kt+2
+    int tap1 = 0, c1 = 0, tap2 = 0, c2 = 0;
+    auto adv = [&](int& t, int& c) {
+        c += BK;
+        if (c >= a.Cin) { c = 0; ++t; }
+    };
+
+    // ---- fragment read bases (bytes): row R = base + 16 i + (lane & 15), chunk q ^ ((R >> 1) & 7)
+    const uint32_t lbase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)L;
+    const int fr = lane & 15, fq = lane >> 4, fs = (fr >> 1) & 7;
+    const uint32_t pa0 = lbase + (uint32_t)((64 * wr + fr) * 128 + 16 * (fq ^ fs));
+    const uint32_t pa1 = lbase + (uint32_t)((64 * wr + fr) * 128 + 16 * ((4 + fq) ^ fs));
+    const uint32_t pb0 = lbase + (uint32_t)((32 * wc + fr) * 128 + 16 * (fq ^ fs));
+    const uint32_t pb1 = lbase + (uint32_t)((32 * wc + fr) * 128 + 16 * ((4 + fq) ^ fs));
+
+    f32x4 acc[2][2][4][2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[x][y][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    i32x4 fa[8], fb0[4], fb1[4];
+
+    // ---- prologue: K-step 0 whole, K-step 1 without A_hi
+    stage(2, 0, 0, 0); stage(0, 0, 0, 0); stage(3, 0, 0, 0); stage(1, 0, 0, 0);
+    if constexpr (CONV) { tap1 = 0; c1 = 0; adv(tap1, c1); }
+    if (nk > 1) {
+        stage(2, 1, tap1, c1); stage(0, 1, tap1, c1); stage(3, 1, tap1, c1);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    barrier();
+    if (wr == 1) barrier();   // stagger: waves 4-7 one barrier behind
+
+    int tap0 = 0, cc0 = 0;    // (tap, c0) of K-step t
+    if constexpr (CONV) { tap2 = tap1; c2 = c1; adv(tap2, c2); }
+    for (int t = 0; t < nk; ++t) {
+        const uint32_t bo = (uint32_t)(t & 1) * BUF;
+        const uint32_t a0 = pa0 + bo, a1 = pa1 + bo, b0 = pb0 + bo, b1 = pb1 + bo;
+        // P0: B_lo, A_lo -> Q(lo, lo); restage A_hi of K-step t+1
+        read_b<2 * HALF>(fb0, b0, b1);
+        read_a<0>(fa, a0, a1);
+        asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");   // B_lo reads done: restaged in P1
+        if (t + 1 < nk) stage(1, t + 1, tap1, c1);
+        barrier();
+        lgkm_wait12(fa, fb0);
+        __builtin_amdgcn_sched_barrier(0);
+        mma_quad(acc[0][0], fa, fb0);
+        __builtin_amdgcn_sched_barrier(0);
+        barrier();
+        // P1: B_hi -> Q(lo, hi); restage B_lo of K-step t+2
+        read_b<3 * HALF>(fb1, b0, b1);
+        if (t + 2 < nk) stage(2, t + 2, tap2, c2);
+        barrier();
+        lgkm_wait4(fb1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma_quad(acc[0][1], fa, fb1);
+        __builtin_amdgcn_sched_barrier(0);
+        barrier();
+        // P2: A_hi -> Q(hi, hi); restage A_lo of K-step t+2
+        read_a<HALF>(fa, a0, a1);
+        if (t + 2 < nk) stage(0, t + 2, tap2, c2);
+        barrier();
+        lgkm_wait8(fa);
+        __builtin_amdgcn_sched_barrier(0);
+        mma_quad(acc[1][1], fa, fb1);
+        __builtin_amdgcn_sched_barrier(0);
+        barrier();
+        // P3: -> Q(hi, lo); restage B_hi of K-step t+2; retire K-step t+1
+        if (t + 2 < nk) {
+            stage(3, t + 2, tap2, c2);
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        mma_quad(acc[1][0], fa, fb0);
+        __builtin_amdgcn_sched_barrier(0);
+        barrier();
+        if constexpr (CONV) {
+            tap0 = tap1; cc0 = c1; tap1 = tap2; c1 = c2; adv(tap2, c2);
+        }
+    }
+    (void)tap0; (void)cc0;
+    if (wr == 0) barrier();   // close the stagger
+    __syncthreads();
+
+    // ---- epilogue
+    const int ecol = 8 * (tid & 31);                 // this thread's 8 columns of the tile
+    const int gcol = n0 + ecol;
+    float bias[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bias[e] = 0.f;
+    if (a.bias && gcol < a.N) {
+        if (a.bias_f32) {
+            const f32x4* bp = reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(a.bias) + gcol);
+            const f32x4 u = bp[0], v = bp[1];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { bias[e] = u[e]; bias[4 + e] = v[e]; }
+        } else {
+            const bf16x8 u = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(a.bias) + gcol);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bias[e] = (float)u[e];
+        }
+    }
+    float* E = reinterpret_cast<float*>(L);
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+        // quadrant rows wr*64 + 16 i + 4 (lane >> 4) + r, columns ni*128 + wc*32 + 16 j + (lane & 15)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        E[(64 * wr + 16 * i + 4 * fq + r) * EPI_LD + 128 * ni + 32 * wc + 16 * j + fr] =
+                            acc[mi][ni][i][j][r];
+        __syncthreads();
+#pragma unroll 2
+        for (int it = 0; it < 8; ++it) {
+            const int row = 16 * it + (tid >> 5);
+            const int grow = m0 + 128 * mi + row;
+            if (grow < a.M && gcol < a.N) {
+                const f32x4 u = *reinterpret_cast<const f32x4*>(&E[row * EPI_LD + ecol]);
+                const f32x4 v = *reinterpret_cast<const f32x4*>(&E[row * EPI_LD + ecol + 4]);
+                float o[8];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { o[e] = u[e] + bias[e]; o[4 + e] = v[e] + bias[4 + e]; }
+                if (a.R) {
+                    const bf16x8 rv = *reinterpret_cast<const bf16x8*>(a.R + (long long)grow * a.ldr + gcol);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) o[e] += (float)rv[e];
+                }
+                bf16x8 ov;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) ov[e] = (bf16)(a.relu ? fmaxf(o[e], 0.f) : o[e]);
+                *reinterpret_cast<bf16x8*>(a.C + (long long)grow * a.ldc + gcol) = ov;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+int launch(const Gemm256Args& a, bool conv, void* stream) {
+    const long long tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256);
+    if (tiles <= 0 || tiles > 0x7fffffffLL) return OV3D_EINVAL;
+    if (conv)
+        hipLaunchKernelGGL(gemm256_kernel<true>, dim3((unsigned)tiles), dim3(512), 0, ov3d_stream(stream), a);
+    else
+        hipLaunchKernelGGL(gemm256_kernel<false>, dim3((unsigned)tiles), dim3(512), 0, ov3d_stream(stream), a);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+bool common_ok(const void* B, long long ldb, const void* bias, const void* R, long long ldr,
+               const void* C, long long ldc, int M, int N, int K) {
+    if (!B || !C || M <= 0 || N <= 0 || K <= 0 || K % BK || N % 8 || ldc % 8 || ldb % 8 || ldb < K ||
+        ldc < N || !aligned16(B) || !aligned16(C))
+        return false;
+    if (bias && !aligned16(bias)) return false;
+    if (R && (ldr % 8 || ldr < N || !aligned16(R))) return false;
+    // 32-bit buffer offsets: one tile's operand rows
+    if (256LL * ldb * 2 + 2LL * K > 0x7fffffffLL) return false;
+    return true;
+}
+
+}  // namespace
+
+extern "C" int ov3d_gemm256(const void* A, long long lda, const void* B, long long ldb,
+                            const void* bias, int bias_f32, const void* R, long long ldr, void* C,
+                            long long ldc, int M, int N, int K, int relu, void* stream) {
+    if (!A || lda % 8 || lda < K || !aligned16(A) || 256LL * lda * 2 + 2LL * K > 0x7fffffffLL ||
+        !common_ok(B, ldb, bias, R, ldr, C, ldc, M, N, K))
+        return OV3D_EINVAL;
+    Gemm256Args a{(const bf16*)A, lda, (const bf16*)B, ldb, bias, (const bf16*)R, ldr, (bf16*)C, ldc,
+                  M, N, K, bias_f32 ? 1 : 0, relu ? 1 : 0, 0, 0, 0};
+    return launch(a, false, stream);
+}
+
+extern "C" int ov3d_conv3x3_gemm256(const void* X, int nimg, int H, int W, int Cin, const void* Wt,
+                                    long long ldb, const void* bias, int bias_f32, const void* R,
+                                    long long ldr, void* Y, long long ldc, int Cout, int relu,
+                                    void* stream) {
+    if (!X || nimg <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cin % BK || !aligned16(X))
+        return OV3D_EINVAL;
+    const long long M = (long long)nimg * H * W;
+    // pixel offsets and the input extent read by one tile in 32-bit buffer arithmetic
+    if (M > 0x7fffffffLL || (long long)(256 + 2 * W + 2 + (long long)H * W) * Cin * 2 > 0x7fffffffLL)
+        return OV3D_EINVAL;
+    const int K = 9 * Cin;
+    if (!common_ok(Wt, ldb, bias, R, ldr, Y, ldc, (int)M, Cout, K)) return OV3D_EINVAL;
+    Gemm256Args a{(const bf16*)X, 0, (const bf16*)Wt, ldb, bias, (const bf16*)R, ldr, (bf16*)Y, ldc,
+                  (int)M, Cout, K, bias_f32 ? 1 : 0, relu ? 1 : 0, H, W, Cin};
+    return launch(a, true, stream);
+}
