@@ -418,6 +418,29 @@ int ov3d_lt_gemm_bias_residual(long long M, int N, int K, const void* x, long lo
                                long long ldr, int relu, void* out, long long ldo, void* workspace,
                                long long ws_bytes, void* stream);
 
+/* Large bf16 GEMM on 256 x 256 tiles (hand-written MFMA, csrc/gemm256.hip) for the RegionCLIP
+ * res5 1x1 convolutions over all L*B*Q ROIs [upstream CLIP ModifiedResNet layer4;
+ * clip.inference, criterion.py:397] and the 3DETR decoder's memory K / V projections
+ * (models/transformer.py:369-372, nn.MultiheadAttention in_proj of the memory):
+ *   C (M, N) = act(A (M, K) . B (N, K)^T + bias (N) + R (M, N)), bf16 in / out, fp32 sums,
+ *   one rounding; bias (N) bf16 (bias_f32 = 0) or f32 (1) or null; R bf16 or null;
+ *   relu: max(., 0) last.  Row-major, K contiguous; K % 64 == 0, N % 8 == 0; lda, ldb, ldr,
+ *   ldc multiples of 8 elements; every pointer 16-byte aligned; 256 * lda * 2 < 2^31. */
+int ov3d_gemm256(const void* A, long long lda, const void* B, long long ldb, const void* bias,
+                 int bias_f32, const void* R, long long ldr, void* C, long long ldc, int M, int N,
+                 int K, int relu, void* stream);
+
+/* 3x3 convolution (pad 1, stride 1) + bias (+ residual) (+ ReLU) as an implicit GEMM on the
+ * same kernel: no column matrix [upstream CLIP ModifiedResNet Bottleneck conv2 of layer3 /
+ * layer4; clip.inference, criterion.py:397]:
+ *   X (nimg, H, W, Cin) NHWC bf16, Wt (Cout, 9*Cin) (ldb) the channels-last weight
+ *   (Cout, ky, kx, Cin) viewed as rows, Y (nimg*H*W, Cout) (ldc) NHWC rows;
+ *   column k = (ky*3 + kx)*Cin + c reads X[n, y+ky-1, x+kx-1, c], zero outside the image.
+ *   Cin % 64 == 0; otherwise as ov3d_gemm256 with M = nimg*H*W, N = Cout, K = 9*Cin. */
+int ov3d_conv3x3_gemm256(const void* X, int nimg, int H, int W, int Cin, const void* Wt,
+                         long long ldb, const void* bias, int bias_f32, const void* R, long long ldr,
+                         void* Y, long long ldc, int Cout, int relu, void* stream);
+
 /* ---- Flash attention (head_dim 64, bf16, no mask) ----
  * Replaces the nn.MultiheadAttention core of models/transformer.py:223,271 (encoder
  * self-attention) and :307-308,365-372 (decoder self / cross attention): per head

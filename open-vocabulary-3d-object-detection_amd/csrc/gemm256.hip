@@ -177,7 +177,6 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
     uint32_t vA[4];
     // conv form: the row's pixel offset and the validity of its 9 taps
     uint32_t pix[4] = {0, 0, 0, 0}, tapok[4] = {0, 0, 0, 0};
-    int tap = 0, c0 = 0;
     if constexpr (!CONV) {
         rsA = make_rsrc(a.A + (long long)m0 * a.lda, (long long)(a.M - m0) * a.lda * 2);
 #pragma unroll
@@ -208,9 +207,10 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
             }
     }
     // per K-step A offsets of the conv form: tap (ky, kx) and channel block c0 of step kt
-    auto conv_voff = [&](int i, int t, int c) -> uint32_t {
-        const int toff = ((t / 3 - 1) * a.W + (t % 3 - 1)) * a.Cin * 2;
-        return ((tapok[i] >> t) & 1u) ? pix[i] + (uint32_t)(toff + 2 * c) : OOB;
+    // (branch-free: an invalid tap's offset is OOB, the DMA then writes zeros)
+    auto conv_voff = [&](int i, int t, uint32_t add) -> uint32_t {
+        const uint32_t keep = 0u - ((tapok[i] >> t) & 1u);
+        return ((pix[i] + add) & keep) | (OOB & ~keep);
     };
 
     // half h (0 A_lo, 1 A_hi, 2 B_lo, 3 B_hi) of K-step kt into LDS buffer kt & 1
@@ -225,8 +225,9 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
             glds(rsA, dst, vA[2 * h] + ko);
             glds(rsA, dst + 8 * 128, vA[2 * h + 1] + ko);
         } else {
-            glds(rsA, dst, conv_voff(2 * h, ctap, cc));
-            glds(rsA, dst + 8 * 128, conv_voff(2 * h + 1, ctap, cc));
+            const uint32_t add = (uint32_t)(((ctap / 3 - 1) * a.W + (ctap % 3 - 1)) * a.Cin * 2 + 2 * cc);
+            glds(rsA, dst, conv_voff(2 * h, ctap, add));
+            glds(rsA, dst + 8 * 128, conv_voff(2 * h + 1, ctap, add));
         }
     };
     // (tap, c0) of K-step kt in the conv form, advanced incrementally for kt+1 and kt+2
@@ -267,7 +268,6 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
     barrier();
     if (wr == 1) barrier();   // stagger: waves 4-7 one barrier behind
 
-    int tap0 = 0, cc0 = 0;    // (tap, c0) of K-step t
     if constexpr (CONV) { tap2 = tap1; c2 = c1; adv(tap2, c2); }
     for (int t = 0; t < nk; ++t) {
         const uint32_t bo = (uint32_t)(t & 1) * BUF;
@@ -314,10 +314,9 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
         __builtin_amdgcn_sched_barrier(0);
         barrier();
         if constexpr (CONV) {
-            tap0 = tap1; cc0 = c1; tap1 = tap2; c1 = c2; adv(tap2, c2);
+            tap1 = tap2; c1 = c2; adv(tap2, c2);
         }
     }
-    (void)tap0; (void)cc0;
     if (wr == 0) barrier();   // close the stagger
     __syncthreads();
 

@@ -218,6 +218,82 @@ def tile_gemm2(a1, w1, a2, w2):
     return out
 
 
+# Large products (the RegionCLIP res5 convolutions over all ROIs, the decoder's memory K / V
+# projections): 256 x 256 tiles on csrc/gemm256.hip, bias / residual / ReLU in the epilogue,
+# and the 3x3 convolution as an implicit GEMM (no column matrix).  OV3D_GEMM256=0: hipBLASLt.
+GEMM256 = os.environ.get("OV3D_GEMM256", "1") == "1"
+
+
+def _rows_ok(t):
+    return (t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0
+            and t.data_ptr() % 16 == 0 and t.is_cuda)
+
+
+def gemm256_ok(a, w, residual=None, out=None):
+    """a (M, K) x w (N, K)^T can run on gemm256 (bf16 rows, K % 64, N % 8, 16-byte rows)"""
+    if not (GEMM256 and _rows_ok(a) and _rows_ok(w)):
+        return False
+    M, K = a.shape
+    N = w.shape[0]
+    if w.shape[1] < K or K % 64 or N % 8 or 256 * max(a.stride(0), w.stride(0)) * 2 + 2 * K >= 2 ** 31:
+        return False
+    if residual is not None and not (_rows_ok(residual) and tuple(residual.shape) == (M, N)):
+        return False
+    return out is None or (_rows_ok(out) and tuple(out.shape) == (M, N))
+
+
+def _bias_arg(bias):
+    if bias is None:
+        return None, 0
+    if bias.dtype == torch.float32:
+        b = bias if bias.is_contiguous() and bias.data_ptr() % 16 == 0 else bias.contiguous().clone()
+        return b, 1
+    b = bias.to(torch.bfloat16)
+    if not b.is_contiguous() or b.data_ptr() % 16:
+        b = b.contiguous().clone()
+    return b, 0
+
+
+def gemm256(a, w, bias=None, residual=None, relu=False, out=None):
+    """act(a w^T + bias + residual) -> (M, N) bf16 on the 256 x 256 tile kernel (check
+    gemm256_ok first); bias bf16 or fp32 (N,), residual (M, N) bf16 rows"""
+    from . import _native
+    M, K = a.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    b, bf32 = _bias_arg(bias)
+    _native.call("ov3d_gemm256", a, a.stride(0), w, w.stride(0), b, bf32, residual,
+                 residual.stride(0) if residual is not None else 0, out, out.stride(0), M, N, K,
+                 int(bool(relu)), like=a)
+    return out
+
+
+def conv3x3_ok(x, w):
+    """x (n, H, W, C) NHWC bf16, w (Cout, >= 9C) bf16 rows: the implicit-GEMM 3x3 convolution"""
+    if not (GEMM256 and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.is_contiguous()
+            and x.data_ptr() % 16 == 0 and _rows_ok(w)):
+        return False
+    n, H, W, C = x.shape
+    return (C % 64 == 0 and w.shape[1] >= 9 * C and w.shape[0] % 8 == 0 and n * H * W < 2 ** 31
+            and (256 + 2 * W + 2 + H * W) * C * 2 < 2 ** 31)
+
+
+def conv3x3_gemm256(x, w, bias=None, residual=None, relu=False):
+    """3x3 convolution (pad 1, stride 1) of NHWC x with the (Cout, 3, 3, C) channels-last weight
+    viewed as (Cout, 9C) rows, + bias (+ residual rows) (+ ReLU) -> (n, H, W, Cout) bf16, as an
+    implicit GEMM (check conv3x3_ok first)"""
+    from . import _native
+    n, H, W, C = x.shape
+    cout = w.shape[0]
+    out = torch.empty((n, H, W, cout), dtype=torch.bfloat16, device=x.device)
+    b, bf32 = _bias_arg(bias)
+    _native.call("ov3d_conv3x3_gemm256", x, n, H, W, C, w, w.stride(0), b, bf32, residual,
+                 residual.stride(0) if residual is not None else 0, out, cout, cout,
+                 int(bool(relu)), like=x)
+    return out
+
+
 def _linear(x, w, b):
     """F.linear on bf16 rows (bias in the epilogue): short row blocks on rowsgemm, long ones
     on tilegemm"""

@@ -1,0 +1,128 @@
+"""The 256 x 256 tile GEMM and the implicit-GEMM 3x3 convolution (csrc/gemm256.hip,
+gemm.gemm256 / gemm.conv3x3_gemm256): the RegionCLIP res5 convolutions over all ROIs
+(clip.inference, criterion.py:397) and the decoder's memory K / V projections
+(models/transformer.py:369-372).  Against the fp32 product / F.conv2d of the same bf16
+operands: the error is that of one bf16 rounding of the output (plus fp32 summation order), as
+for the library GEMM + im2col it replaces.  Ragged M and N (tiles past the matrix), strided
+rows, bias bf16 / fp32, residual, ReLU; convolutions whose tiles straddle images, zero padding
+at every border, K-steps crossing the (ky, kx) taps."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import ov3d  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(out, ref, lib=None):
+    """|out - ref| within one bf16 rounding of ref (2^-8 relative) plus 1e-3 of the scale, and
+    no worse than 1.5x the library's own error when given"""
+    d = (out.float() - ref).abs()
+    scale = ref.abs().max().item()
+    bound = ref.abs() * 2.0 ** -8 + 1e-3 * scale
+    bad = (d > bound).sum().item()
+    assert bad == 0, (bad, d.max().item(), scale)
+    if lib is not None:
+        lib_err = (lib.float() - ref).abs().max().item()
+        assert d.max().item() <= 1.5 * lib_err + 1e-3 * scale, (d.max().item(), lib_err)
+
+
+@pytest.mark.parametrize("M,N,K,bias,res,relu", [
+    (1000, 640, 1280, "bf16", False, True),      # res5 conv1 (ragged rows)
+    (4096, 2560, 640, "bf16", True, True),       # res5 conv3 + identity close
+    (333, 2560, 1280, "bf16", False, False),     # downsample conv
+    (16384, 2048, 256, "f32", False, False),     # decoder memory K / V (8 layers stacked)
+    (300, 40, 64, None, True, False),            # one K-step, N tail inside one tile
+    (513, 264, 128, "f32", False, True),         # two K-steps, N tail past a tile
+    (257, 512, 192, "bf16", True, True),         # three K-steps
+])
+def test_gemm256_matches_fp32(cuda, M, N, K, bias, res, relu):
+    from ov3d_amd import gemm
+    g = torch.Generator(device=cuda).manual_seed(M + 3 * N + 7 * K)
+    wide = torch.randn(M, K + 64, device=cuda, generator=g).to(torch.bfloat16)
+    a = wide[:, 64:64 + K]                               # strided rows (lda = K + 64)
+    w = (torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).to(torch.bfloat16)
+    b = None
+    if bias:
+        b = torch.randn(N, device=cuda, generator=g)
+        b = b.to(torch.bfloat16) if bias == "bf16" else b
+    r = torch.randn(M, N, device=cuda, generator=g).to(torch.bfloat16) if res else None
+    assert gemm.gemm256_ok(a, w, residual=r)
+    out = gemm.gemm256(a, w, bias=b, residual=r, relu=relu)
+    ref = a.float() @ w.float().t()
+    if b is not None:
+        ref = ref + b.float()
+    if r is not None:
+        ref = ref + r.float()
+    if relu:
+        ref = ref.clamp_min(0)
+    assert out.shape == (M, N) and out.dtype == torch.bfloat16
+    lib = torch.nn.functional.linear(a, w, b.to(torch.bfloat16) if b is not None else None)
+    if r is not None:
+        lib = lib + r
+    if relu:
+        lib = lib.clamp_min(0)
+    _check(out, ref, lib)
+
+
+def test_gemm256_exact_integers(cuda):
+    """small-integer operands: every product and sum is exact in fp32 and the outputs are exact
+    in bf16 -- the result must be bit-equal (catches fragment / swizzle / epilogue index errors
+    that a tolerance could hide); asymmetric operands (A = I would hide a transpose)"""
+    from ov3d_amd import gemm
+    g = torch.Generator(device=cuda).manual_seed(5)
+    M, N, K = 700, 520, 320
+    a = torch.randint(-3, 4, (M, K), device=cuda, generator=g).to(torch.bfloat16)
+    w = torch.randint(-2, 3, (N, K), device=cuda, generator=g).to(torch.bfloat16)
+    w[:, 0] = torch.arange(N, device=cuda) % 7      # column-dependent: a swapped C write shows
+    a[:, 1] = torch.arange(M, device=cuda) % 5
+    b = torch.randint(-4, 5, (N,), device=cuda, generator=g).float()
+    out = gemm.gemm256(a, w, bias=b)
+    ref = a.float() @ w.float().t() + b
+    assert ref.abs().max().item() < 256                  # exact in bf16
+    assert torch.equal(out.float(), ref)
+
+
+@pytest.mark.parametrize("n,H,W,C,cout,res", [
+    (5, 18, 18, 640, 640, False),    # res5 block 1 conv2 (ROI 18 x 18), tiles straddle ROIs
+    (13, 9, 9, 640, 640, True),      # res5 blocks 2-6 conv2 (9 x 9: 81 rows per ROI)
+    (2, 34, 46, 320, 320, False),    # layer3 conv2 on an image-sized map
+    (3, 5, 7, 64, 72, False),        # small: one K-step per tap, Cout tail
+])
+def test_conv3x3_gemm256_matches_conv2d(cuda, n, H, W, C, cout, res):
+    from ov3d_amd import gemm
+    g = torch.Generator(device=cuda).manual_seed(n * H * W + C)
+    x = torch.randn(n, H, W, C, device=cuda, generator=g).to(torch.bfloat16)
+    wt = (torch.randn(cout, 3, 3, C, device=cuda, generator=g) / (9 * C) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(cout, device=cuda, generator=g).to(torch.bfloat16)
+    r = torch.randn(n * H * W, cout, device=cuda, generator=g).to(torch.bfloat16) if res else None
+    wm = wt.reshape(cout, 9 * C)
+    assert gemm.conv3x3_ok(x, wm)
+    out = gemm.conv3x3_gemm256(x, wm, bias=b, residual=r, relu=True)
+    ref = F.conv2d(x.permute(0, 3, 1, 2).float(), wt.permute(0, 3, 1, 2).float(), b.float(), padding=1)
+    ref = ref.permute(0, 2, 3, 1)
+    if r is not None:
+        ref = ref + r.float().view(n, H, W, cout)
+    ref = ref.clamp_min(0)
+    assert out.shape == (n, H, W, cout)
+    _check(out, ref)
+
+
+def test_conv3x3_gemm256_border_taps_exact(cuda):
+    """integer input and weights with one nonzero tap per output channel group: each output is
+    one shifted input pixel, so the zero padding at every border and the (ky, kx) order are
+    checked exactly"""
+    from ov3d_amd import gemm
+    n, H, W, C = 3, 9, 9, 64
+    g = torch.Generator(device=cuda).manual_seed(9)
+    x = torch.randint(-8, 9, (n, H, W, C), device=cuda, generator=g).to(torch.bfloat16)
+    cout = 9 * 8
+    wt = torch.zeros(cout, 3, 3, C, device=cuda)
+    for t in range(9):
+        for j in range(8):
+            wt[8 * t + j, t // 3, t % 3, (5 * j + t) % C] = 1.0
+    wt = wt.to(torch.bfloat16)
+    out = gemm.conv3x3_gemm256(x, wt.reshape(cout, 9 * C))
+    ref = F.conv2d(x.permute(0, 3, 1, 2).float(), wt.permute(0, 3, 1, 2).float(), padding=1)
+    assert torch.equal(out.float(), ref.permute(0, 2, 3, 1))

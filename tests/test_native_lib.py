@@ -92,3 +92,36 @@ def test_round4_entries_reject_bad_arguments():
     assert lib.ov3d_lt_gemm_bias_residual(8, 16, 16, fake, 8, fake, 16, fake, fake, 16, 1, fake,
                                           16, None, 0, None) == -1                     # ldx < K
     assert lib.ov3d_attn_mask_pack(fake, 3, 1.0, 1, 32, 64, fake, None) == -1        # kind 3
+
+
+def test_round5_entries_reject_bad_arguments():
+    """ov3d_gemm256 / ov3d_conv3x3_gemm256 validate shapes, strides and alignment before any
+    launch; ov3d_sa_dy_fused keeps its argument checks (its > 2 GiB inputs route to the 64-bit
+    kernel instead of failing).  Host-side checks only."""
+    from ov3d_amd import _native
+    lib = _native.load()
+    p = ctypes.c_void_p(256)      # 16-byte aligned, never dereferenced
+    odd = ctypes.c_void_p(264)    # 8-byte aligned only
+    ok = dict(A=p, lda=128, B=p, ldb=128, bias=None, bf=0, R=None, ldr=0, C=p, ldc=64, M=100,
+              N=64, K=128, relu=0)
+
+    def g(**kw):
+        a = dict(ok, **kw)
+        return lib.ov3d_gemm256(a["A"], a["lda"], a["B"], a["ldb"], a["bias"], a["bf"], a["R"],
+                                a["ldr"], a["C"], a["ldc"], a["M"], a["N"], a["K"], a["relu"], None)
+    assert g(A=None) == -1
+    assert g(K=96) == -1              # K % 64
+    assert g(N=60, ldc=64) == -1      # N % 8
+    assert g(lda=100) == -1           # lda < K
+    assert g(ldb=136 + 4) == -1       # ldb % 8
+    assert g(C=odd) == -1             # 16-byte alignment
+    assert g(R=p, ldr=32) == -1       # ldr < N
+    assert g(M=0) == -1
+    assert lib.ov3d_conv3x3_gemm256(p, 2, 9, 9, 96, p, 864, None, 0, None, 0, p, 64, 64, 1,
+                                    None) == -1   # Cin % 64
+    assert lib.ov3d_conv3x3_gemm256(p, 2, 9, 9, 64, p, 512, None, 0, None, 0, p, 64, 64, 1,
+                                    None) == -1   # ldb < 9 Cin
+    assert lib.ov3d_conv3x3_gemm256(None, 2, 9, 9, 64, p, 576, None, 0, None, 0, p, 64, 64, 1,
+                                    None) == -1
+    assert lib.ov3d_sa_dy_fused(None, None, None, None, 1 << 23, 128, 256, 64, None, None, None,
+                                None, None, None, None, None, None, None, 1, None) == -1
