@@ -35,6 +35,8 @@
 // Epilogue: per row half, the fp32 quadrants go through LDS ([128][260] f32), then every
 // thread owns 8 consecutive columns of a row: + bias, + residual (fp32), ReLU, one rounding,
 // one 16-byte store.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -47,8 +49,6 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 constexpr int BK = 64;
 constexpr int HALF = 128 * BK * 2;   // bytes of one 128-row half of an operand K-step
 constexpr int BUF = 4 * HALF;        // A_lo, A_hi, B_lo, B_hi
-constexpr int EPI_LD = 260;          // floats per staged epilogue row (+4: conflict-free writes)
-constexpr int LDS_BYTES = 128 * EPI_LD * 4 > 2 * BUF ? 128 * EPI_LD * 4 : 2 * BUF;
 constexpr uint32_t OOB = 0x80000000u;   // buffer offset past num_records: the load returns 0
 
 struct Gemm256Args {
@@ -64,6 +64,7 @@ struct Gemm256Args {
     int M, N, K;
     int bias_f32, relu;
     int H, W, Cin;     // conv form
+    int gm;            // row panels per group of the tile order
 };
 
 __device__ __forceinline__ f32x4 mfma16(i32x4 a, i32x4 b, f32x4 c) {
@@ -101,7 +102,8 @@ __device__ __forceinline__ void lgkm_wait4(i32x4 (&b)[4]) {
 
 __device__ __forceinline__ void barrier() { __builtin_amdgcn_s_barrier(); }
 
-// one quadrant: 4 x 2 tiles of 16 x 16, K = 64 (two 32-deep MFMA steps)
+// one quadrant: 4 x 2 tiles of 16 x 16, K = 64 (two 32-deep MFMA steps); B fragments as the
+// A operand: each tile is C^T (the epilogue's row-contiguous layout)
 __device__ __forceinline__ void mma_quad(f32x4 (&acc)[4][2], const i32x4 (&fa)[8], const i32x4 (&fb)[4]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -109,7 +111,7 @@ __device__ __forceinline__ void mma_quad(f32x4 (&acc)[4][2], const i32x4 (&fa)[8
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(fa[2 * i + kh], fb[2 * j + kh], acc[i][j]);
+            for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(fb[2 * j + kh], fa[2 * i + kh], acc[i][j]);
     __builtin_amdgcn_s_setprio(0);
 }
 
@@ -144,73 +146,90 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, lo
 
 template <bool CONV>
 __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
-    __shared__ __attribute__((aligned(16))) char L[LDS_BYTES];
+    __shared__ __attribute__((aligned(16))) char L[2 * BUF];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave >> 2, wc = wave & 3;
-
-    // XCD-aware tile order: blocks b and b + 8 share an XCD; logical tiles lt are dealt so that
-    // each XCD gets a contiguous range (n fastest: the n tiles of one A row panel together)
-    const int nwg = gridDim.x, bid = blockIdx.x;
-    const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
-    const int lt = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
-    const int ntn = (a.N + 255) >> 8;
-    const int tm = lt / ntn, tn = lt - tm * ntn;
-    const int m0 = tm * 256, n0 = tn * 256;
+    const int ntn = (a.N + 255) >> 8, ntm = (a.M + 255) >> 8;
+    const int tiles = ntm * ntn;
     const int nk = a.K / BK;
+
+    // ---- tile schedule.  Persistent (tiles > grid): the tiles of XCD x (blocks b, b % 8 == x)
+    // are one contiguous range of the logical order, taken round robin by its workgroups, so
+    // the tiles in flight on one XCD share A row panels and B column panels in its L2 (the
+    // logical order walks groups of `gm` row panels, columns inside a group).  Otherwise one
+    // tile per block through the same bijective XCD remap.
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7;
+    int lt, lt_end, lt_step;
+    {
+        const int cnt = nwg == tiles ? nwg : tiles;
+        const int q8 = cnt >> 3, r8 = cnt & 7;
+        const int xbeg = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+        if (nwg == tiles) {
+            lt = xbeg + (bid >> 3); lt_end = lt + 1; lt_step = 1;
+        } else {   // nwg % 8 == 0 (host)
+            lt = xbeg + (bid >> 3); lt_end = xbeg + q8 + (xcd < r8 ? 1 : 0); lt_step = nwg >> 3;
+        }
+    }
+    auto coords = [&](int t, int& m0, int& n0) {
+        const int per = a.gm * ntn, g = t / per, first = g * a.gm;
+        const int gs = min(ntm - first, a.gm), rem = t - g * per;
+        m0 = (first + rem % gs) * 256;
+        n0 = (rem / gs) * 256;
+    };
 
     // ---- LDS-DMA sources.  Wave w fills rows 16 w + 8 j + (lane >> 3) of each half (j = 0, 1),
     // physical chunk lane & 7 <- logical chunk (lane & 7) ^ ((row >> 1) & 7)
     const int lrow0 = 16 * wave + (lane >> 3);             // j = 0; j = 1: + 8
     const int lc0 = (lane & 7) ^ ((lane >> 4) & 7);        // (row >> 1) & 7 for j = 0
     const int lc1 = (lane & 7) ^ (((lane >> 4) + 4) & 7);  // for j = 1
-    const __amdgpu_buffer_rsrc_t rsB =
-        make_rsrc(a.B + (long long)n0 * a.ldb, (long long)(a.N - n0) * a.ldb * 2);
-    uint32_t vB[4];   // [half][j]
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-            vB[2 * h + j] = (uint32_t)((128 * h + lrow0 + 8 * j) * a.ldb * 2) + 16u * (j ? lc1 : lc0);
-
-    __amdgpu_buffer_rsrc_t rsA;
-    uint32_t vA[4];
+    __amdgpu_buffer_rsrc_t rsA, rsB;
+    uint32_t vA[4], vB[4];   // [half][j]
     // conv form: the row's pixel offset and the validity of its 9 taps
-    uint32_t pix[4] = {0, 0, 0, 0}, tapok[4] = {0, 0, 0, 0};
-    if constexpr (!CONV) {
-        rsA = make_rsrc(a.A + (long long)m0 * a.lda, (long long)(a.M - m0) * a.lda * 2);
+    uint32_t tapok[4] = {0, 0, 0, 0};
+    auto setup = [&](int m0, int n0) {
+        rsB = make_rsrc(a.B + (long long)n0 * a.ldb, (long long)(a.N - n0) * a.ldb * 2);
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
             for (int j = 0; j < 2; ++j)
-                vA[2 * h + j] = (uint32_t)((128 * h + lrow0 + 8 * j) * a.lda * 2) + 16u * (j ? lc1 : lc0);
-    } else {
-        const int HW = a.H * a.W;
-        const int img0 = m0 / HW;
-        rsA = make_rsrc(a.A + (long long)img0 * HW * a.Cin, (long long)(a.M - img0 * HW) * a.Cin * 2);
+                vB[2 * h + j] = (uint32_t)((128 * h + lrow0 + 8 * j) * a.ldb * 2) + 16u * (j ? lc1 : lc0);
+        if constexpr (!CONV) {
+            rsA = make_rsrc(a.A + (long long)m0 * a.lda, (long long)(a.M - m0) * a.lda * 2);
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+            for (int h = 0; h < 2; ++h)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int m = m0 + 128 * h + lrow0 + 8 * j;
-                const int n = m / HW, rem = m - n * HW, y = rem / a.W, x = rem - y * a.W;
-                uint32_t ok = 0;
-                if (m < a.M) {
+                for (int j = 0; j < 2; ++j)
+                    vA[2 * h + j] = (uint32_t)((128 * h + lrow0 + 8 * j) * a.lda * 2) + 16u * (j ? lc1 : lc0);
+        } else {
+            const int HW = a.H * a.W;
+            const int img0 = m0 / HW;
+            rsA = make_rsrc(a.A + (long long)img0 * HW * a.Cin, (long long)(a.M - img0 * HW) * a.Cin * 2);
 #pragma unroll
-                    for (int t = 0; t < 9; ++t) {
-                        const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
-                        ok |= (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) ? (1u << t) : 0u;
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int m = m0 + 128 * h + lrow0 + 8 * j;
+                    const int n = m / HW, rem = m - n * HW, y = rem / a.W, x = rem - y * a.W;
+                    uint32_t ok = 0;
+                    if (m < a.M) {
+#pragma unroll
+                        for (int t = 0; t < 9; ++t) {
+                            const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+                            ok |= (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) ? (1u << t) : 0u;
+                        }
                     }
+                    tapok[2 * h + j] = ok;
+                    vA[2 * h + j] = (uint32_t)(((n - img0) * HW + rem) * a.Cin * 2) + 16u * (j ? lc1 : lc0);
                 }
-                tapok[2 * h + j] = ok;
-                pix[2 * h + j] = (uint32_t)(((n - img0) * HW + rem) * a.Cin * 2) + 16u * (j ? lc1 : lc0);
-            }
-    }
-    // per K-step A offsets of the conv form: tap (ky, kx) and channel block c0 of step kt
+        }
+    };
+    // per K-step A offsets of the conv form: tap (ky, kx) and channel block c0 of the step
     // (branch-free: an invalid tap's offset is OOB, the DMA then writes zeros)
     auto conv_voff = [&](int i, int t, uint32_t add) -> uint32_t {
         const uint32_t keep = 0u - ((tapok[i] >> t) & 1u);
-        return ((pix[i] + add) & keep) | (OOB & ~keep);
+        return ((vA[i] + add) & keep) | (OOB & ~keep);
     };
 
     // half h (0 A_lo, 1 A_hi, 2 B_lo, 3 B_hi) of K-step kt into LDS buffer kt & 1
@@ -230,11 +249,20 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
             glds(rsA, dst + 8 * 128, conv_voff(2 * h + 1, ctap, add));
         }
     };
-    // (tap, c0) of K-step kt in the conv form, advanced incrementally for kt+1 and kt+2
+    // (tap, c0) of K-steps t+1 and t+2 in the conv form, advanced incrementally
     int tap1 = 0, c1 = 0, tap2 = 0, c2 = 0;
     auto adv = [&](int& t, int& c) {
         c += BK;
         if (c >= a.Cin) { c = 0; ++t; }
+    };
+    // the first two K-steps of a tile: K-step 0 whole, K-step 1 without A_hi (its P0 issues it)
+    auto prologue = [&]() {
+        stage(2, 0, 0, 0); stage(0, 0, 0, 0); stage(3, 0, 0, 0); stage(1, 0, 0, 0);
+        tap1 = 0; c1 = 0;
+        if constexpr (CONV) adv(tap1, c1);
+        if (nk > 1) { stage(2, 1, tap1, c1); stage(0, 1, tap1, c1); stage(3, 1, tap1, c1); }
+        tap2 = tap1; c2 = c1;
+        if constexpr (CONV) adv(tap2, c2);
     };
 
     // ---- fragment read bases (bytes): row R = base + 16 i + (lane & 15), chunk q ^ ((R >> 1) & 7)
@@ -245,148 +273,188 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
     const uint32_t pb0 = lbase + (uint32_t)((32 * wc + fr) * 128 + 16 * (fq ^ fs));
     const uint32_t pb1 = lbase + (uint32_t)((32 * wc + fr) * 128 + 16 * ((4 + fq) ^ fs));
 
-    f32x4 acc[2][2][4][2];
-#pragma unroll
-    for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int y = 0; y < 2; ++y)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j) acc[x][y][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    i32x4 fa[8], fb0[4], fb1[4];
-
-    // ---- prologue: K-step 0 whole, K-step 1 without A_hi
-    stage(2, 0, 0, 0); stage(0, 0, 0, 0); stage(3, 0, 0, 0); stage(1, 0, 0, 0);
-    if constexpr (CONV) { tap1 = 0; c1 = 0; adv(tap1, c1); }
-    if (nk > 1) {
-        stage(2, 1, tap1, c1); stage(0, 1, tap1, c1); stage(3, 1, tap1, c1);
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    barrier();
-    if (wr == 1) barrier();   // stagger: waves 4-7 one barrier behind
-
-    if constexpr (CONV) { tap2 = tap1; c2 = c1; adv(tap2, c2); }
-    for (int t = 0; t < nk; ++t) {
-        const uint32_t bo = (uint32_t)(t & 1) * BUF;
-        const uint32_t a0 = pa0 + bo, a1 = pa1 + bo, b0 = pb0 + bo, b1 = pb1 + bo;
-        // P0: B_lo, A_lo -> Q(lo, lo); restage A_hi of K-step t+1
-        read_b<2 * HALF>(fb0, b0, b1);
-        read_a<0>(fa, a0, a1);
-        asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");   // B_lo reads done: restaged in P1
-        if (t + 1 < nk) stage(1, t + 1, tap1, c1);
-        barrier();
-        lgkm_wait12(fa, fb0);
-        __builtin_amdgcn_sched_barrier(0);
-        mma_quad(acc[0][0], fa, fb0);
-        __builtin_amdgcn_sched_barrier(0);
-        barrier();
-        // P1: B_hi -> Q(lo, hi); restage B_lo of K-step t+2
-        read_b<3 * HALF>(fb1, b0, b1);
-        if (t + 2 < nk) stage(2, t + 2, tap2, c2);
-        barrier();
-        lgkm_wait4(fb1);
-        __builtin_amdgcn_sched_barrier(0);
-        mma_quad(acc[0][1], fa, fb1);
-        __builtin_amdgcn_sched_barrier(0);
-        barrier();
-        // P2: A_hi -> Q(hi, hi); restage A_lo of K-step t+2
-        read_a<HALF>(fa, a0, a1);
-        if (t + 2 < nk) stage(0, t + 2, tap2, c2);
-        barrier();
-        lgkm_wait8(fa);
-        __builtin_amdgcn_sched_barrier(0);
-        mma_quad(acc[1][1], fa, fb1);
-        __builtin_amdgcn_sched_barrier(0);
-        barrier();
-        // P3: -> Q(hi, lo); restage B_hi of K-step t+2; retire K-step t+1
-        if (t + 2 < nk) {
-            stage(3, t + 2, tap2, c2);
-            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        mma_quad(acc[1][0], fa, fb0);
-        __builtin_amdgcn_sched_barrier(0);
-        barrier();
-        if constexpr (CONV) {
-            tap1 = tap2; c1 = c2; adv(tap2, c2);
-        }
-    }
-    if (wr == 0) barrier();   // close the stagger
-    __syncthreads();
-
-    // ---- epilogue
-    const int ecol = 8 * (tid & 31);                 // this thread's 8 columns of the tile
-    const int gcol = n0 + ecol;
-    float bias[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) bias[e] = 0.f;
-    if (a.bias && gcol < a.N) {
-        if (a.bias_f32) {
-            const f32x4* bp = reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(a.bias) + gcol);
-            const f32x4 u = bp[0], v = bp[1];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) { bias[e] = u[e]; bias[4 + e] = v[e]; }
-        } else {
-            const bf16x8 u = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(a.bias) + gcol);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) bias[e] = (float)u[e];
-        }
-    }
-    float* E = reinterpret_cast<float*>(L);
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
-        // quadrant rows wr*64 + 16 i + 4 (lane >> 4) + r, columns ni*128 + wc*32 + 16 j + (lane & 15)
+    // epilogue addressing: the MFMAs compute C^T tiles (B fragments as the A operand), so
+    // accumulator register r of lane l is C[m = .. + (l & 15)][n = .. + 4 (l >> 4) + r]: four
+    // consecutive columns of one row, one 8-byte store
+    const bool has_r = a.R != nullptr;
+    uint2 res[2][4][2];   // residual rows of one row half, [ni][i][j]
+    auto load_res = [&](int mi, int m0, int n0) {
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        E[(64 * wr + 16 * i + 4 * fq + r) * EPI_LD + 128 * ni + 32 * wc + 16 * j + fr] =
-                            acc[mi][ni][i][j][r];
-        __syncthreads();
-#pragma unroll 2
-        for (int it = 0; it < 8; ++it) {
-            const int row = 16 * it + (tid >> 5);
-            const int grow = m0 + 128 * mi + row;
-            if (grow < a.M && gcol < a.N) {
-                const f32x4 u = *reinterpret_cast<const f32x4*>(&E[row * EPI_LD + ecol]);
-                const f32x4 v = *reinterpret_cast<const f32x4*>(&E[row * EPI_LD + ecol + 4]);
-                float o[8];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) { o[e] = u[e] + bias[e]; o[4 + e] = v[e] + bias[4 + e]; }
-                if (a.R) {
-                    const bf16x8 rv = *reinterpret_cast<const bf16x8*>(a.R + (long long)grow * a.ldr + gcol);
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) o[e] += (float)rv[e];
+                for (int j = 0; j < 2; ++j) {
+                    const int m = m0 + 128 * mi + 64 * wr + 16 * i + fr;
+                    const int n = n0 + 128 * ni + 32 * wc + 16 * j + 4 * fq;
+                    res[ni][i][j] = make_uint2(0u, 0u);
+                    if (m < a.M && n < a.N)
+                        res[ni][i][j] = *reinterpret_cast<const uint2*>(a.R + (long long)m * a.ldr + n);
                 }
-                bf16x8 ov;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) ov[e] = (bf16)(a.relu ? fmaxf(o[e], 0.f) : o[e]);
-                *reinterpret_cast<bf16x8*>(a.C + (long long)grow * a.ldc + gcol) = ov;
-            }
+    };
+
+    f32x4 acc[2][2][4][2];
+    i32x4 fa[8], fb0[4], fb1[4];
+    int m0, n0;
+    coords(lt, m0, n0);
+    setup(m0, n0);
+    prologue();
+    bool first = true;
+    while (lt < lt_end) {
+        // K-step 0 landed (every wave's DMA: the barrier); K-step 1's three halves and the
+        // previous tile's 32 epilogue stores may still be in flight
+        if (first) {
+            if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            if (nk > 1) asm volatile("s_waitcnt vmcnt(38)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
         }
-        __syncthreads();
+        first = false;
+        barrier();
+        if (wr == 1) barrier();   // stagger: waves 4-7 one barrier behind
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) acc[x][y][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+        for (int t = 0; t < nk; ++t) {
+            const uint32_t bo = (uint32_t)(t & 1) * BUF;
+            const uint32_t a0 = pa0 + bo, a1 = pa1 + bo, b0 = pb0 + bo, b1 = pb1 + bo;
+            // P0: B_lo, A_lo -> Q(lo, lo); restage A_hi of K-step t+1
+            read_b<2 * HALF>(fb0, b0, b1);
+            read_a<0>(fa, a0, a1);
+            asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");   // B_lo reads done: restaged in P1
+            if (t + 1 < nk) stage(1, t + 1, tap1, c1);
+            barrier();
+            lgkm_wait12(fa, fb0);
+            __builtin_amdgcn_sched_barrier(0);
+            mma_quad(acc[0][0], fa, fb0);
+            __builtin_amdgcn_sched_barrier(0);
+            barrier();
+            // P1: B_hi -> Q(lo, hi); restage B_lo of K-step t+2
+            read_b<3 * HALF>(fb1, b0, b1);
+            if (t + 2 < nk) stage(2, t + 2, tap2, c2);
+            barrier();
+            lgkm_wait4(fb1);
+            __builtin_amdgcn_sched_barrier(0);
+            mma_quad(acc[0][1], fa, fb1);
+            __builtin_amdgcn_sched_barrier(0);
+            barrier();
+            // P2: A_hi -> Q(hi, hi); restage A_lo of K-step t+2
+            read_a<HALF>(fa, a0, a1);
+            if (t + 2 < nk) stage(0, t + 2, tap2, c2);
+            barrier();
+            lgkm_wait8(fa);
+            __builtin_amdgcn_sched_barrier(0);
+            mma_quad(acc[1][1], fa, fb1);
+            __builtin_amdgcn_sched_barrier(0);
+            barrier();
+            // P3: -> Q(hi, lo); restage B_hi of K-step t+2; retire K-step t+1
+            if (t + 2 < nk) {
+                stage(3, t + 2, tap2, c2);
+                asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            mma_quad(acc[1][0], fa, fb0);
+            __builtin_amdgcn_sched_barrier(0);
+            barrier();
+            if constexpr (CONV) { tap1 = tap2; c1 = c2; adv(tap2, c2); }
+        }
+        if (wr == 0) barrier();   // close the stagger: every wave is past its last LDS read
+
+        // ---- epilogue of this tile, the next tile's first two K-steps in flight meanwhile
+        const int em0 = m0, en0 = n0;
+        if (has_r) load_res(0, em0, en0);
+        float bias[2][2][4];
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int n = en0 + 128 * ni + 32 * wc + 16 * j + 4 * fq;
+                f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+                if (a.bias && n < a.N) {
+                    if (a.bias_f32) {
+                        bv = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(a.bias) + n);
+                    } else {
+                        const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(a.bias) + n);
+                        bv = f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                                   __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) bias[ni][j][r] = bv[r];
+            }
+        lt += lt_step;
+        if (lt < lt_end) {
+            coords(lt, m0, n0);
+            setup(m0, n0);
+            prologue();
+        }
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) {
+            if (mi == 1 && has_r) load_res(1, em0, en0);
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const int m = em0 + 128 * mi + 64 * wr + 16 * i + fr;
+                        const int n = en0 + 128 * ni + 32 * wc + 16 * j + 4 * fq;
+                        float o[4];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) o[r] = acc[mi][ni][i][j][r] + bias[ni][j][r];
+                        if (has_r) {
+                            const uint2 u = res[ni][i][j];
+                            o[0] += __uint_as_float(u.x << 16);
+                            o[1] += __uint_as_float(u.x & 0xffff0000u);
+                            o[2] += __uint_as_float(u.y << 16);
+                            o[3] += __uint_as_float(u.y & 0xffff0000u);
+                        }
+                        if (a.relu) {
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) o[r] = fmaxf(o[r], 0.f);
+                        }
+                        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+                        const bf16x4 ov = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+                        if (m < a.M && n < a.N)
+                            *reinterpret_cast<bf16x4*>(a.C + (long long)m * a.ldc + n) = ov;
+                    }
+        }
     }
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-int launch(const Gemm256Args& a, bool conv, void* stream) {
+int launch(Gemm256Args a, bool conv, void* stream) {
     const long long tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256);
     if (tiles <= 0 || tiles > 0x7fffffffLL) return OV3D_EINVAL;
+    // persistent grid: one 512-thread workgroup per CU (128 KB of LDS each)
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        cus &= ~7;
+        if (cus <= 0) cus = 8;
+    }
+    static const int gm_env = getenv("OV3D_GEMM256_GM") ? atoi(getenv("OV3D_GEMM256_GM")) : 0;
+    const int ntn = (a.N + 255) / 256;
+    a.gm = gm_env > 0 ? gm_env : (ntn >= 8 ? 4 : 1);
+    const unsigned grid = (unsigned)(tiles <= cus ? tiles : cus);
     if (conv)
-        hipLaunchKernelGGL(gemm256_kernel<true>, dim3((unsigned)tiles), dim3(512), 0, ov3d_stream(stream), a);
+        hipLaunchKernelGGL(gemm256_kernel<true>, dim3(grid), dim3(512), 0, ov3d_stream(stream), a);
     else
-        hipLaunchKernelGGL(gemm256_kernel<false>, dim3((unsigned)tiles), dim3(512), 0, ov3d_stream(stream), a);
+        hipLaunchKernelGGL(gemm256_kernel<false>, dim3(grid), dim3(512), 0, ov3d_stream(stream), a);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }
@@ -412,7 +480,7 @@ extern "C" int ov3d_gemm256(const void* A, long long lda, const void* B, long lo
         !common_ok(B, ldb, bias, R, ldr, C, ldc, M, N, K))
         return OV3D_EINVAL;
     Gemm256Args a{(const bf16*)A, lda, (const bf16*)B, ldb, bias, (const bf16*)R, ldr, (bf16*)C, ldc,
-                  M, N, K, bias_f32 ? 1 : 0, relu ? 1 : 0, 0, 0, 0};
+                  M, N, K, bias_f32 ? 1 : 0, relu ? 1 : 0, 0, 0, 0, 1};
     return launch(a, false, stream);
 }
 
@@ -429,6 +497,6 @@ extern "C" int ov3d_conv3x3_gemm256(const void* X, int nimg, int H, int W, int C
     const int K = 9 * Cin;
     if (!common_ok(Wt, ldb, bias, R, ldr, Y, ldc, (int)M, Cout, K)) return OV3D_EINVAL;
     Gemm256Args a{(const bf16*)X, 0, (const bf16*)Wt, ldb, bias, (const bf16*)R, ldr, (bf16*)Y, ldc,
-                  (int)M, Cout, K, bias_f32 ? 1 : 0, relu ? 1 : 0, H, W, Cin};
+                  (int)M, Cout, K, bias_f32 ? 1 : 0, relu ? 1 : 0, H, W, Cin, 1};
     return launch(a, true, stream);
 }

@@ -73,10 +73,10 @@ def test_gemm256_exact_integers(cuda):
     from ov3d_amd import gemm
     g = torch.Generator(device=cuda).manual_seed(5)
     M, N, K = 700, 520, 320
-    a = torch.randint(-3, 4, (M, K), device=cuda, generator=g).to(torch.bfloat16)
-    w = torch.randint(-2, 3, (N, K), device=cuda, generator=g).to(torch.bfloat16)
-    w[:, 0] = torch.arange(N, device=cuda) % 7      # column-dependent: a swapped C write shows
-    a[:, 1] = torch.arange(M, device=cuda) % 5
+    a = torch.randint(-1, 2, (M, K), device=cuda, generator=g).to(torch.bfloat16)
+    w = torch.randint(-1, 2, (N, K), device=cuda, generator=g).to(torch.bfloat16)
+    w[:, 0] = torch.arange(N, device=cuda) % 7 - 3   # column-dependent: a swapped C write shows
+    a[:, 1] = torch.arange(M, device=cuda) % 5 - 2
     b = torch.randint(-4, 5, (N,), device=cuda, generator=g).float()
     out = gemm.gemm256(a, w, bias=b)
     ref = a.float() @ w.float().t() + b
