@@ -41,6 +41,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _native
+from . import gemm
 
 # RegionCLIP CLIP configs: PIXEL_MEAN / PIXEL_STD of CLIP, images divided by 255
 CLIP_PIXEL_MEAN = (0.48145466, 0.4578275, 0.40821073)
@@ -256,6 +257,11 @@ def _conv1x1(x, w, b, relu, residual=None):
     bias and ReLU in the GEMM epilogue; with a residual (bf16) the identity is the GEMM's C."""
     shp = x.shape
     rows = x.reshape(-1, shp[-1])
+    if x.dtype == torch.bfloat16 and x.is_cuda:
+        res = residual.reshape(-1, w.shape[0]) if residual is not None else None
+        if gemm.gemm256_ok(rows, w, residual=res):
+            # hand-written 256 x 256 tile kernel: bias, identity and ReLU in its epilogue
+            return gemm.gemm256(rows, w, bias=b, residual=res, relu=relu).view(*shp[:-1], w.shape[0])
     if residual is None:
         y = torch._addmm_activation(b, rows, w.t()) if relu else torch.addmm(b, rows, w.t())
     else:
@@ -317,6 +323,9 @@ def _conv3x3(x, w, b, stride=1):
     cout, kpad = w.shape
     Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
     x = _native.check(x.contiguous(), "conv input", ndim=4)
+    if stride == 1 and gemm.conv3x3_ok(x, w):
+        # implicit GEMM: the 3x3 taps are read straight from the NHWC rows (no column matrix)
+        return gemm.conv3x3_gemm256(x, w, bias=b, relu=True)
     out = torch.empty((N, Ho, Wo, cout), dtype=x.dtype, device=x.device)
     per_img = Ho * Wo * kpad * x.element_size()
     step = max(1, IM2COL_CHUNK_BYTES // per_img)
