@@ -430,6 +430,14 @@ int ov3d_gemm256(const void* A, long long lda, const void* B, long long ldb, con
                  int bias_f32, const void* R, long long ldr, void* C, long long ldc, int M, int N,
                  int K, int relu, void* stream);
 
+/* Two products of one shape in one launch of the same kernel (the decoder's K and V
+ * projections of the memory for all 8 layers, models/transformer.py:369-372):
+ *   C = A B^T + bias, C2 = A2 B2^T + bias2 (no residual, no ReLU); as ov3d_gemm256 otherwise,
+ *   the two problems share M, N, K and the leading dimensions; bias and bias2 both or neither. */
+int ov3d_gemm256_pair(const void* A, const void* A2, long long lda, const void* B, const void* B2,
+                      long long ldb, const void* bias, const void* bias2, int bias_f32, void* C,
+                      void* C2, long long ldc, int M, int N, int K, void* stream);
+
 /* 3x3 convolution (pad 1, stride 1) + bias (+ residual) (+ ReLU) as an implicit GEMM on the
  * same kernel: no column matrix [upstream CLIP ModifiedResNet Bottleneck conv2 of layer3 /
  * layer4; clip.inference, criterion.py:397]:

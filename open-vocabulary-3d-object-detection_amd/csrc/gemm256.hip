@@ -65,6 +65,15 @@ struct Gemm256Args {
     int bias_f32, relu;
     int H, W, Cin;     // conv form
     int gm;            // row panels per group of the tile order
+    int stagger;       // waves 4-7 one barrier behind (1) or in step (0)
+    int delay;         // s_sleep rounds before the first tile of every other workgroup
+    // a second product of the same shape in the same launch (nprob = 2): its tiles follow the
+    // first's in the tile order (the decoder's K and V projections of the memory)
+    int nprob;
+    const bf16* A2;
+    const bf16* B2;
+    const void* bias2;
+    bf16* C2;
 };
 
 __device__ __forceinline__ f32x4 mfma16(i32x4 a, i32x4 b, f32x4 c) {
@@ -151,7 +160,7 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave >> 2, wc = wave & 3;
     const int ntn = (a.N + 255) >> 8, ntm = (a.M + 255) >> 8;
-    const int tiles = ntm * ntn;
+    const int ptiles = ntm * ntn, tiles = ptiles * a.nprob;
     const int nk = a.K / BK;
 
     // ---- tile schedule.  Persistent (tiles > grid): the tiles of XCD x (blocks b, b % 8 == x)
@@ -172,7 +181,14 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
             lt = xbeg + (bid >> 3); lt_end = xbeg + q8 + (xcd < r8 ? 1 : 0); lt_step = nwg >> 3;
         }
     }
+    // the current tile's problem: operand / output pointers (scalar selects)
+    const bf16* pA = a.A;
+    const bf16* pB = a.B;
     auto coords = [&](int t, int& m0, int& n0) {
+        const bool second = t >= ptiles;
+        if (second) t -= ptiles;
+        pA = second ? a.A2 : a.A;
+        pB = second ? a.B2 : a.B;
         const int per = a.gm * ntn, g = t / per, first = g * a.gm;
         const int gs = min(ntm - first, a.gm), rem = t - g * per;
         m0 = (first + rem % gs) * 256;
@@ -189,14 +205,14 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
     // conv form: the row's pixel offset and the validity of its 9 taps
     uint32_t tapok[4] = {0, 0, 0, 0};
     auto setup = [&](int m0, int n0) {
-        rsB = make_rsrc(a.B + (long long)n0 * a.ldb, (long long)(a.N - n0) * a.ldb * 2);
+        rsB = make_rsrc(pB + (long long)n0 * a.ldb, (long long)(a.N - n0) * a.ldb * 2);
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
             for (int j = 0; j < 2; ++j)
                 vB[2 * h + j] = (uint32_t)((128 * h + lrow0 + 8 * j) * a.ldb * 2) + 16u * (j ? lc1 : lc0);
         if constexpr (!CONV) {
-            rsA = make_rsrc(a.A + (long long)m0 * a.lda, (long long)(a.M - m0) * a.lda * 2);
+            rsA = make_rsrc(pA + (long long)m0 * a.lda, (long long)(a.M - m0) * a.lda * 2);
 #pragma unroll
             for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -205,7 +221,7 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
         } else {
             const int HW = a.H * a.W;
             const int img0 = m0 / HW;
-            rsA = make_rsrc(a.A + (long long)img0 * HW * a.Cin, (long long)(a.M - img0 * HW) * a.Cin * 2);
+            rsA = make_rsrc(pA + (long long)img0 * HW * a.Cin, (long long)(a.M - img0 * HW) * a.Cin * 2);
 #pragma unroll
             for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -296,6 +312,11 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
     f32x4 acc[2][2][4][2];
     i32x4 fa[8], fb0[4], fb1[4];
     int m0, n0;
+    // de-phase the workgroups: with equal tiles every CU would reach its epilogue (HBM-bound
+    // stores / residual reads) at the same time and its main loop (MFMA-bound) at the same time
+    if (a.delay && ((bid >> 3) & 1)) {
+        for (int d = 0; d < a.delay; ++d) __builtin_amdgcn_s_sleep(127);
+    }
     coords(lt, m0, n0);
     setup(m0, n0);
     prologue();
@@ -312,7 +333,7 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
         }
         first = false;
         barrier();
-        if (wr == 1) barrier();   // stagger: waves 4-7 one barrier behind
+        if (a.stagger && wr == 1) barrier();   // stagger: waves 4-7 one barrier behind
 #pragma unroll
         for (int x = 0; x < 2; ++x)
 #pragma unroll
@@ -368,10 +389,12 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
             barrier();
             if constexpr (CONV) { tap1 = tap2; c1 = c2; adv(tap2, c2); }
         }
-        if (wr == 0) barrier();   // close the stagger: every wave is past its last LDS read
+        if (a.stagger && wr == 0) barrier();   // close the stagger: every wave is past its last LDS read
 
         // ---- epilogue of this tile, the next tile's first two K-steps in flight meanwhile
         const int em0 = m0, en0 = n0;
+        bf16* const eC = lt >= ptiles && a.nprob > 1 ? a.C2 : a.C;
+        const void* const ebias = lt >= ptiles && a.nprob > 1 ? a.bias2 : a.bias;
         if (has_r) load_res(0, em0, en0);
         float bias[2][2][4];
 #pragma unroll
@@ -380,11 +403,11 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
             for (int j = 0; j < 2; ++j) {
                 const int n = en0 + 128 * ni + 32 * wc + 16 * j + 4 * fq;
                 f32x4 bv = {0.f, 0.f, 0.f, 0.f};
-                if (a.bias && n < a.N) {
+                if (ebias && n < a.N) {
                     if (a.bias_f32) {
-                        bv = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(a.bias) + n);
+                        bv = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(ebias) + n);
                     } else {
-                        const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(a.bias) + n);
+                        const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(ebias) + n);
                         bv = f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
                                    __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
                     }
@@ -404,11 +427,11 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
 #pragma unroll
             for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < 4; ++i) {
+                    const int m = em0 + 128 * mi + 64 * wr + 16 * i + fr;
+                    uint2 pk[2];
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
-                        const int m = em0 + 128 * mi + 64 * wr + 16 * i + fr;
-                        const int n = en0 + 128 * ni + 32 * wc + 16 * j + 4 * fq;
                         float o[4];
 #pragma unroll
                         for (int r = 0; r < 4; ++r) o[r] = acc[mi][ni][i][j][r] + bias[ni][j][r];
@@ -423,11 +446,22 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
 #pragma unroll
                             for (int r = 0; r < 4; ++r) o[r] = fmaxf(o[r], 0.f);
                         }
-                        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-                        const bf16x4 ov = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
-                        if (m < a.M && n < a.N)
-                            *reinterpret_cast<bf16x4*>(a.C + (long long)m * a.ldc + n) = ov;
+                        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+                        const bf16x2 lo = {(bf16)o[0], (bf16)o[1]}, hi = {(bf16)o[2], (bf16)o[3]};
+                        pk[j] = make_uint2(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
                     }
+                    // 16-row groups fq: j = 0 holds columns 4 fq .. +3, j = 1 holds 16 + 4 fq .. +3.
+                    // Swapping the odd groups of j = 0 with the even groups of j = 1 leaves 8
+                    // consecutive columns per lane (fq 0: 0-7, 1: 16-23, 2: 8-15, 3: 24-31): one
+                    // 16-byte store instead of two 8-byte ones (store issue halves)
+                    const auto sx = __builtin_amdgcn_permlane16_swap(pk[0].x, pk[1].x, false, false);
+                    const auto sy = __builtin_amdgcn_permlane16_swap(pk[0].y, pk[1].y, false, false);
+                    const int c = 4 * (fq & 1) * 4 + 8 * (fq >> 1);   // 0, 16, 8, 24
+                    const int n = en0 + 128 * ni + 32 * wc + c;
+                    if (m < a.M && n < a.N)
+                        *reinterpret_cast<uint4*>(eC + (long long)m * a.ldc + n) =
+                            make_uint4(sx[0], sy[0], sx[1], sy[1]);
+                }
         }
     }
 }
@@ -435,7 +469,7 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 int launch(Gemm256Args a, bool conv, void* stream) {
-    const long long tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256);
+    const long long tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256) * a.nprob;
     if (tiles <= 0 || tiles > 0x7fffffffLL) return OV3D_EINVAL;
     // persistent grid: one 512-thread workgroup per CU (128 KB of LDS each)
     static int cus = 0;
@@ -449,7 +483,11 @@ int launch(Gemm256Args a, bool conv, void* stream) {
     }
     static const int gm_env = getenv("OV3D_GEMM256_GM") ? atoi(getenv("OV3D_GEMM256_GM")) : 0;
     const int ntn = (a.N + 255) / 256;
-    a.gm = gm_env > 0 ? gm_env : (ntn >= 8 ? 4 : 1);
+    a.gm = gm_env > 0 ? gm_env : (ntn >= 8 ? 8 : 1);
+    static const int st_env = getenv("OV3D_GEMM256_STAGGER") ? atoi(getenv("OV3D_GEMM256_STAGGER")) : 1;
+    static const int dl_env = getenv("OV3D_GEMM256_DELAY") ? atoi(getenv("OV3D_GEMM256_DELAY")) : 0;
+    a.stagger = st_env;
+    a.delay = dl_env;
     const unsigned grid = (unsigned)(tiles <= cus ? tiles : cus);
     if (conv)
         hipLaunchKernelGGL(gemm256_kernel<true>, dim3(grid), dim3(512), 0, ov3d_stream(stream), a);
@@ -480,7 +518,7 @@ extern "C" int ov3d_gemm256(const void* A, long long lda, const void* B, long lo
         !common_ok(B, ldb, bias, R, ldr, C, ldc, M, N, K))
         return OV3D_EINVAL;
     Gemm256Args a{(const bf16*)A, lda, (const bf16*)B, ldb, bias, (const bf16*)R, ldr, (bf16*)C, ldc,
-                  M, N, K, bias_f32 ? 1 : 0, relu ? 1 : 0, 0, 0, 0, 1};
+                  M, N, K, bias_f32 ? 1 : 0, relu ? 1 : 0, 0, 0, 0, 1, 1, 0, 1, nullptr, nullptr, nullptr, nullptr};
     return launch(a, false, stream);
 }
 
@@ -497,6 +535,21 @@ extern "C" int ov3d_conv3x3_gemm256(const void* X, int nimg, int H, int W, int C
     const int K = 9 * Cin;
     if (!common_ok(Wt, ldb, bias, R, ldr, Y, ldc, (int)M, Cout, K)) return OV3D_EINVAL;
     Gemm256Args a{(const bf16*)X, 0, (const bf16*)Wt, ldb, bias, (const bf16*)R, ldr, (bf16*)Y, ldc,
-                  (int)M, Cout, K, bias_f32 ? 1 : 0, relu ? 1 : 0, H, W, Cin, 1};
+                  (int)M, Cout, K, bias_f32 ? 1 : 0, relu ? 1 : 0, H, W, Cin, 1, 1, 0, 1, nullptr, nullptr, nullptr, nullptr};
     return launch(a, true, stream);
+}
+
+extern "C" int ov3d_gemm256_pair(const void* A, const void* A2, long long lda, const void* B,
+                                 const void* B2, long long ldb, const void* bias, const void* bias2,
+                                 int bias_f32, void* C, void* C2, long long ldc, int M, int N, int K,
+                                 void* stream) {
+    if (!A || !A2 || !B2 || !C2 || lda % 8 || lda < K || !aligned16(A) || !aligned16(A2) ||
+        !aligned16(B2) || !aligned16(C2) || 256LL * lda * 2 + 2LL * K > 0x7fffffffLL ||
+        (bias2 && !aligned16(bias2)) || (!bias) != (!bias2) ||
+        !common_ok(B, ldb, bias, nullptr, 0, C, ldc, M, N, K))
+        return OV3D_EINVAL;
+    Gemm256Args a{(const bf16*)A, lda, (const bf16*)B, ldb, bias, nullptr, 0, (bf16*)C, ldc,
+                  M, N, K, bias_f32 ? 1 : 0, 0, 0, 0, 0, 1, 1, 0, 2, (const bf16*)A2, (const bf16*)B2,
+                  bias2, (bf16*)C2};
+    return launch(a, false, stream);
 }

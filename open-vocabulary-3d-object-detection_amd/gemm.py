@@ -269,6 +269,20 @@ def gemm256(a, w, bias=None, residual=None, relu=False, out=None):
     return out
 
 
+def gemm256_pair(a1, w1, b1, a2, w2, b2):
+    """(a1 w1^T + b1, a2 w2^T + b2) in ONE launch of the tile kernel (same shapes; check
+    gemm256_ok on both pairs and that a1 / a2, w1 / w2 share their row strides first)"""
+    from . import _native
+    M, K = a1.shape
+    N = w1.shape[0]
+    o1 = torch.empty((M, N), dtype=torch.bfloat16, device=a1.device)
+    o2 = torch.empty_like(o1)
+    (bb1, bf32), (bb2, _) = _bias_arg(b1), _bias_arg(b2.to(b1.dtype) if b1 is not None else None)
+    _native.call("ov3d_gemm256_pair", a1, a2, a1.stride(0), w1, w2, w1.stride(0), bb1, bb2, bf32,
+                 o1, o2, N, M, N, K, like=a1)
+    return o1, o2
+
+
 def conv3x3_ok(x, w):
     """x (n, H, W, C) NHWC bf16, w (Cout, >= 9C) bf16 rows: the implicit-GEMM 3x3 convolution"""
     if not (GEMM256 and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.is_contiguous()

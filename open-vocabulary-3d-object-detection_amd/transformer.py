@@ -139,10 +139,15 @@ class _MemoryKV(torch.autograd.Function):
             srcs += [wc[E:2 * E], wc[2 * E:], bc[E:2 * E], bc[2 * E:]]
             dsts += [Wk[rows], Wv[rows], bk[rows], bv[rows]]
         _native.multi_copy(dsts, srcs)
-        # the library GEMM: its 256 x 256 tiles read 4 bytes of operands per output from L2
-        # where the long row-block kernel's 64 x 128 tiles read 12 (N = 2048: 31 vs 40 us)
-        K_all = torch.addmm(bk, mpos, Wk.t()).view(S, B, n)
-        V_all = torch.addmm(bv, mem, Wv.t()).view(S, B, n)
+        # both products in one launch of the 256 x 256 tile kernel (csrc/gemm256.hip; 256 x 256
+        # tiles read 4 bytes of operands per output from L2 where the long row-block kernel's
+        # 64 x 128 tiles read 12); the library GEMMs when it does not apply
+        if gemm.gemm256_ok(mpos, Wk) and gemm.gemm256_ok(mem, Wv) and mpos.stride(0) == mem.stride(0):
+            K_all, V_all = gemm.gemm256_pair(mpos, Wk, bk, mem, Wv, bv)
+            K_all, V_all = K_all.view(S, B, n), V_all.view(S, B, n)
+        else:
+            K_all = torch.addmm(bk, mpos, Wk.t()).view(S, B, n)
+            V_all = torch.addmm(bv, mem, Wv.t()).view(S, B, n)
         dK, dV = torch.empty_like(K_all), torch.empty_like(V_all)
         flash.defer_kv_grads(dK)   # the layers' dK / dV run batched in this op's backward
         token = torch.empty((), dtype=torch.float32, device=memory.device)

@@ -126,3 +126,20 @@ def test_conv3x3_gemm256_border_taps_exact(cuda):
     out = gemm.conv3x3_gemm256(x, wt.reshape(cout, 9 * C))
     ref = F.conv2d(x.permute(0, 3, 1, 2).float(), wt.permute(0, 3, 1, 2).float(), padding=1)
     assert torch.equal(out.float(), ref.permute(0, 2, 3, 1))
+
+
+def test_gemm256_pair_equals_two_products(cuda):
+    """the decoder's K and V projections of the memory (8 layers stacked: 16384 x 2048 x 256) in
+    one launch equal the two single launches bit for bit, and the fp32 products within one
+    rounding (models/transformer.py:369-372)"""
+    from ov3d_amd import gemm
+    g = torch.Generator(device=cuda).manual_seed(11)
+    M, N, K = 16384, 2048, 256
+    a1, a2 = (torch.randn(M, K, device=cuda, generator=g).to(torch.bfloat16) for _ in range(2))
+    w1, w2 = ((torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).to(torch.bfloat16) for _ in range(2))
+    b1, b2 = (torch.randn(N, device=cuda, generator=g).to(torch.bfloat16) for _ in range(2))
+    o1, o2 = gemm.gemm256_pair(a1, w1, b1, a2, w2, b2)
+    assert torch.equal(o1, gemm.gemm256(a1, w1, bias=b1))
+    assert torch.equal(o2, gemm.gemm256(a2, w2, bias=b2))
+    _check(o1, a1.float() @ w1.float().t() + b1.float())
+    _check(o2, a2.float() @ w2.float().t() + b2.float())

@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--json", default=None)
     ap.add_argument("--only", default=None, help="substring filter on the shape names")
+    ap.add_argument("--no-lib", action="store_true", help="time gemm256 only")
     a = ap.parse_args()
     ov3d_import.load()
     from ov3d_amd import _native, gemm
@@ -66,8 +67,9 @@ def main():
             if r is not None:
                 y += r
             return y.relu_() if relu else y
-        t_own, t_lib = timed(own, a.reps), timed(lib, a.reps)
-        d = (own().float() - lib().float()).abs().max().item()
+        t_own = timed(own, a.reps)
+        t_lib = float('nan') if a.no_lib else timed(lib, a.reps)
+        d = float('nan') if a.no_lib else (own().float() - lib().float()).abs().max().item()
         fl = 2.0 * M * N * K
         rows.append({"shape": name, "M": M, "N": N, "K": K, "ms_gemm256": round(t_own, 4),
                      "ms_library": round(t_lib, 4), "tflops_gemm256": round(fl / t_own / 1e9, 1),
@@ -75,6 +77,21 @@ def main():
         print(rows[-1], flush=True)
         del x, w, r
         torch.cuda.empty_cache()
+    if not a.only or a.only in "decoder memory K/V pair":
+        M, N, K = 16384, 2048, 256
+        x1, x2 = (torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16) for _ in range(2))
+        w1, w2 = ((torch.randn(N, K, device=dev, generator=g) / 16).to(torch.bfloat16) for _ in range(2))
+        b1, b2 = (torch.randn(N, device=dev, generator=g).to(torch.bfloat16) for _ in range(2))
+        own = lambda: gemm.gemm256_pair(x1, w1, b1, x2, w2, b2)
+        lib = lambda: (torch.addmm(b1, x1, w1.t()), torch.addmm(b2, x2, w2.t()))
+        t_own = timed(own, a.reps)
+        t_lib = float('nan') if a.no_lib else timed(lib, a.reps)
+        fl = 4.0 * M * N * K
+        rows.append({"shape": "decoder memory K/V pair (one launch vs two addmm)", "M": M, "N": N,
+                     "K": K, "ms_gemm256": round(t_own, 4), "ms_library": round(t_lib, 4),
+                     "tflops_gemm256": round(fl / t_own / 1e9, 1),
+                     "tflops_library": round(fl / t_lib / 1e9, 1)})
+        print(rows[-1], flush=True)
     for name, n, H, W, C, cout in CONVS:
         if a.only and a.only not in name:
             continue
@@ -88,8 +105,9 @@ def main():
         def lib():
             _native.call("ov3d_im2col3x3", x, 2, n, H, W, C, 1, 9 * C, cols, like=x)
             return torch._addmm_activation(b, cols, wm.t())
-        t_own, t_lib = timed(own, a.reps), timed(lib, a.reps)
-        d = (own().reshape(M, cout).float() - lib().float()).abs().max().item()
+        t_own = timed(own, a.reps)
+        t_lib = float('nan') if a.no_lib else timed(lib, a.reps)
+        d = float('nan') if a.no_lib else (own().reshape(M, cout).float() - lib().float()).abs().max().item()
         fl = 2.0 * M * cout * 9 * C
         rows.append({"shape": name, "M": M, "N": cout, "K": 9 * C, "ms_gemm256": round(t_own, 4),
                      "ms_library": round(t_lib, 4), "library": "ov3d_im2col3x3 + hipBLASLt",
