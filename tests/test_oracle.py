@@ -232,3 +232,27 @@ def test_lsap_rejects_invalid_entries():
     c[1, 1] = np.nan
     with pytest.raises(ValueError):
         O.lsap(c)
+
+
+def test_bench_ball_query_scanned_count_matches_the_reference_scan():
+    """bench.py's ball-query byte count (the points the reference scan actually
+    reads) from the oracle's indices equals a direct simulation of the Appendix A.2 scan
+    (stop after the S-th strict d^2 < r^2 hit, else N), incl. centroids with no / few hits"""
+    import torch
+    import bench
+    rng = np.random.default_rng(4)
+    B, N, M, S, r = 2, 700, 40, 8, 0.2
+    xyz = rng.uniform(-1, 1, (B, N, 3)).astype(np.float32)
+    new = xyz[:, rng.choice(N, M, replace=False)].copy()
+    new[0, 0] = (5.0, 5.0, 5.0)         # no neighbour: scans all N
+    new[1, 1] = xyz[1, -1] + 0.01         # few neighbours near the end
+    idx = O.ball_query(xyz, new, r, S)
+    want = 0
+    r2 = np.float32(r) * np.float32(r)
+    for b in range(B):
+        for m in range(M):
+            d = xyz[b] - new[b, m]
+            d2 = (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]
+            hits = np.nonzero(d2 < r2)[0]
+            want += hits[S - 1] + 1 if len(hits) >= S else N
+    assert bench.ball_query_scanned(torch.from_numpy(idx), N) == want
