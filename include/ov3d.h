@@ -425,10 +425,12 @@ int ov3d_lt_gemm_bias_residual(long long M, int N, int K, const void* x, long lo
  *   C (M, N) = act(A (M, K) . B (N, K)^T + bias (N) + R (M, N)), bf16 in / out, fp32 sums,
  *   one rounding; bias (N) bf16 (bias_f32 = 0) or f32 (1) or null; R bf16 or null;
  *   relu: max(., 0) last.  Row-major, K contiguous; K % 64 == 0, N % 8 == 0; lda, ldb, ldr,
- *   ldc multiples of 8 elements; every pointer 16-byte aligned; 256 * lda * 2 < 2^31. */
+ *   ldc multiples of 8 elements; every pointer 16-byte aligned; 256 * lda * 2 < 2^31.
+ *   ctr: caller workspace of 8 ints (16-byte aligned) for the dynamic tile schedule (zeroed on
+ *   the stream by the call; one launch at a time per buffer), or null: static schedule. */
 int ov3d_gemm256(const void* A, long long lda, const void* B, long long ldb, const void* bias,
                  int bias_f32, const void* R, long long ldr, void* C, long long ldc, int M, int N,
-                 int K, int relu, void* stream);
+                 int K, int relu, void* ctr, void* stream);
 
 /* Two products of one shape in one launch of the same kernel (the decoder's K and V
  * projections of the memory for all 8 layers, models/transformer.py:369-372):
@@ -436,7 +438,7 @@ int ov3d_gemm256(const void* A, long long lda, const void* B, long long ldb, con
  *   the two problems share M, N, K and the leading dimensions; bias and bias2 both or neither. */
 int ov3d_gemm256_pair(const void* A, const void* A2, long long lda, const void* B, const void* B2,
                       long long ldb, const void* bias, const void* bias2, int bias_f32, void* C,
-                      void* C2, long long ldc, int M, int N, int K, void* stream);
+                      void* C2, long long ldc, int M, int N, int K, void* ctr, void* stream);
 
 /* 3x3 convolution (pad 1, stride 1) + bias (+ residual) (+ ReLU) as an implicit GEMM on the
  * same kernel: no column matrix [upstream CLIP ModifiedResNet Bottleneck conv2 of layer3 /
@@ -447,7 +449,7 @@ int ov3d_gemm256_pair(const void* A, const void* A2, long long lda, const void* 
  *   Cin % 64 == 0; otherwise as ov3d_gemm256 with M = nimg*H*W, N = Cout, K = 9*Cin. */
 int ov3d_conv3x3_gemm256(const void* X, int nimg, int H, int W, int Cin, const void* Wt,
                          long long ldb, const void* bias, int bias_f32, const void* R, long long ldr,
-                         void* Y, long long ldc, int Cout, int relu, void* stream);
+                         void* Y, long long ldc, int Cout, int relu, void* ctr, void* stream);
 
 /* ---- Flash attention (head_dim 64, bf16, no mask) ----
  * Replaces the nn.MultiheadAttention core of models/transformer.py:223,271 (encoder

@@ -117,9 +117,9 @@ _SIGS = {
     "ov3d_project_box2d": "pppliipppppp",
     "ov3d_heads_out_fwd": "plippipiippippppppipp",
     "ov3d_heads_out_bwd": "pppiiiipiippppppplp",
-    "ov3d_gemm256": "plplpiplpliiiip",
-    "ov3d_conv3x3_gemm256": "piiiiplpiplpliip",
-    "ov3d_gemm256_pair": "pplpplppippliiip",
+    "ov3d_gemm256": "plplpiplpliiiipp",
+    "ov3d_conv3x3_gemm256": "piiiiplpiplpliipp",
+    "ov3d_gemm256_pair": "pplpplppippliiipp",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
                           "ov3d_attn_dropbits_words", "ov3d_attn_maskbits_words", "ov3d_fps_workspace", "ov3d_attn_small_bwd", "ov3d_set_loss_fwd_parts",
