@@ -424,7 +424,8 @@ int ov3d_lt_gemm_bias_residual(long long M, int N, int K, const void* x, long lo
  * (models/transformer.py:369-372, nn.MultiheadAttention in_proj of the memory):
  *   C (M, N) = act(A (M, K) . B (N, K)^T + bias (N) + R (M, N)), bf16 in / out, fp32 sums,
  *   one rounding; bias (N) bf16 (bias_f32 = 0) or f32 (1) or null; R bf16 or null;
- *   relu: max(., 0) last.  Row-major, K contiguous; K % 64 == 0, N % 8 == 0; lda, ldb, ldr,
+ *   relu: max(., 0) last.  Row-major, K contiguous; K % 8 == 0 (a K tail past the last multiple
+ *   of 64 reads zeros), N % 8 == 0; lda, ldb, ldr,
  *   ldc multiples of 8 elements; every pointer 16-byte aligned; 256 * lda * 2 < 2^31.
  *   ctr: caller workspace of 8 ints (16-byte aligned) for the dynamic tile schedule (zeroed on
  *   the stream by the call; one launch at a time per buffer), or null: static schedule. */

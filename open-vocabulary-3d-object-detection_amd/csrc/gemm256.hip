@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
     const int wr = wave >> 2, wc = wave & 3;
     const int ntn = (a.N + 255) >> 8, ntm = (a.M + 255) >> 8;
     const int ptiles = ntm * ntn, tiles = ptiles * a.nprob;
-    const int nk = a.K / BK;
+    const int nk = (a.K + BK - 1) / BK;   // a K tail (K % 64 != 0, K % 8 == 0) reads zeros
 
     // ---- tile schedule.  Persistent (tiles > grid): the tiles of XCD x (blocks b, b % 8 == x)
     // are one contiguous range of the logical order, taken round robin by its workgroups, so
@@ -272,16 +272,25 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
     };
 
     // half h (0 A_lo, 1 A_hi, 2 B_lo, 3 B_hi) of K-step kt into LDS buffer kt & 1
+    // the K tail: chunks at k >= K read zeros (OOB) in both operands of the last K-step
+    auto ktail = [&](uint32_t v, int kt, int lc) -> uint32_t {
+        return kt * BK + 8 * lc < a.K ? v : OOB;
+    };
     auto stage = [&](int h, int kt, int ctap, int cc) {
         char* dst = L + (kt & 1) * BUF + h * HALF + 16 * wave * 128;
+        const bool tail = (kt + 1) * BK > a.K;   // wave-uniform
         if (h >= 2) {
             const uint32_t ko = (uint32_t)kt * (BK * 2);
-            glds(rsB, dst, vB[2 * (h - 2)] + ko);
-            glds(rsB, dst + 8 * 128, vB[2 * (h - 2) + 1] + ko);
+            uint32_t v0 = vB[2 * (h - 2)] + ko, v1 = vB[2 * (h - 2) + 1] + ko;
+            if (tail) { v0 = ktail(v0, kt, lc0); v1 = ktail(v1, kt, lc1); }
+            glds(rsB, dst, v0);
+            glds(rsB, dst + 8 * 128, v1);
         } else if constexpr (!CONV) {
             const uint32_t ko = (uint32_t)kt * (BK * 2);
-            glds(rsA, dst, vA[2 * h] + ko);
-            glds(rsA, dst + 8 * 128, vA[2 * h + 1] + ko);
+            uint32_t v0 = vA[2 * h] + ko, v1 = vA[2 * h + 1] + ko;
+            if (tail) { v0 = ktail(v0, kt, lc0); v1 = ktail(v1, kt, lc1); }
+            glds(rsA, dst, v0);
+            glds(rsA, dst + 8 * 128, v1);
         } else {
             const uint32_t add = (uint32_t)(((ctap / 3 - 1) * a.W + (ctap % 3 - 1)) * a.Cin * 2 + 2 * cc);
             glds(rsA, dst, conv_voff(2 * h, ctap, add));
@@ -539,7 +548,7 @@ int launch(Gemm256Args a, bool conv, void* stream) {
 
 bool common_ok(const void* B, long long ldb, const void* bias, const void* R, long long ldr,
                const void* C, long long ldc, int M, int N, int K) {
-    if (!B || !C || M <= 0 || N <= 0 || K <= 0 || K % BK || N % 8 || ldc % 8 || ldb % 8 || ldb < K ||
+    if (!B || !C || M <= 0 || N <= 0 || K <= 0 || K % 8 || N % 8 || ldc % 8 || ldb % 8 || ldb < K ||
         ldc < N || !aligned16(B) || !aligned16(C))
         return false;
     if (bias && !aligned16(bias)) return false;

@@ -230,12 +230,12 @@ def _rows_ok(t):
 
 
 def gemm256_ok(a, w, residual=None, out=None):
-    """a (M, K) x w (N, K)^T can run on gemm256 (bf16 rows, K % 64, N % 8, 16-byte rows)"""
+    """a (M, K) x w (N, K)^T can run on gemm256 (bf16 rows, K % 8, N % 8, 16-byte rows)"""
     if not (GEMM256 and _rows_ok(a) and _rows_ok(w)):
         return False
     M, K = a.shape
     N = w.shape[0]
-    if w.shape[1] < K or K % 64 or N % 8 or 256 * max(a.stride(0), w.stride(0)) * 2 + 2 * K >= 2 ** 31:
+    if w.shape[1] < K or K % 8 or N % 8 or 256 * max(a.stride(0), w.stride(0)) * 2 + 2 * K >= 2 ** 31:
         return False
     if residual is not None and not (_rows_ok(residual) and tuple(residual.shape) == (M, N)):
         return False

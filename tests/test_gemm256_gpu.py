@@ -36,6 +36,9 @@ def _check(out, ref, lib=None):
     (300, 40, 64, None, True, False),            # one K-step, N tail inside one tile
     (513, 264, 128, "f32", False, True),         # two K-steps, N tail past a tile
     (257, 512, 192, "bf16", True, True),         # three K-steps
+    (1300, 320, 80, "bf16", True, True),         # K tail: layer1 conv3 (80 channels)
+    (700, 640, 160, "bf16", False, True),        # K tail after two full steps (layer2, 160)
+    (300, 96, 8, None, False, False),            # a single 8-wide chunk
 ])
 def test_gemm256_matches_fp32(cuda, M, N, K, bias, res, relu):
     from ov3d_amd import gemm

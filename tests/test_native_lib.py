@@ -110,7 +110,7 @@ def test_round5_entries_reject_bad_arguments():
         return lib.ov3d_gemm256(a["A"], a["lda"], a["B"], a["ldb"], a["bias"], a["bf"], a["R"],
                                 a["ldr"], a["C"], a["ldc"], a["M"], a["N"], a["K"], a["relu"], None, None)
     assert g(A=None) == -1
-    assert g(K=96) == -1              # K % 64
+    assert g(K=100) == -1             # K % 8
     assert g(N=60, ldc=64) == -1      # N % 8
     assert g(lda=100) == -1           # lda < K
     assert g(ldb=136 + 4) == -1       # ldb % 8
