@@ -426,12 +426,10 @@ int ov3d_lt_gemm_bias_residual(long long M, int N, int K, const void* x, long lo
  *   one rounding; bias (N) bf16 (bias_f32 = 0) or f32 (1) or null; R bf16 or null;
  *   relu: max(., 0) last.  Row-major, K contiguous; K % 8 == 0 (a K tail past the last multiple
  *   of 64 reads zeros), N % 8 == 0; lda, ldb, ldr,
- *   ldc multiples of 8 elements; every pointer 16-byte aligned; 256 * lda * 2 < 2^31.
- *   ctr: caller workspace of 8 ints (16-byte aligned) for the dynamic tile schedule (zeroed on
- *   the stream by the call; one launch at a time per buffer), or null: static schedule. */
+ *   ldc multiples of 8 elements; every pointer 16-byte aligned; 256 * lda * 2 < 2^31. */
 int ov3d_gemm256(const void* A, long long lda, const void* B, long long ldb, const void* bias,
                  int bias_f32, const void* R, long long ldr, void* C, long long ldc, int M, int N,
-                 int K, int relu, void* ctr, void* stream);
+                 int K, int relu, void* stream);
 
 /* Two products of one shape in one launch of the same kernel (the decoder's K and V
  * projections of the memory for all 8 layers, models/transformer.py:369-372):
@@ -439,7 +437,7 @@ int ov3d_gemm256(const void* A, long long lda, const void* B, long long ldb, con
  *   the two problems share M, N, K and the leading dimensions; bias and bias2 both or neither. */
 int ov3d_gemm256_pair(const void* A, const void* A2, long long lda, const void* B, const void* B2,
                       long long ldb, const void* bias, const void* bias2, int bias_f32, void* C,
-                      void* C2, long long ldc, int M, int N, int K, void* ctr, void* stream);
+                      void* C2, long long ldc, int M, int N, int K, void* stream);
 
 /* 3x3 convolution (pad 1, stride 1) + bias (+ residual) (+ ReLU) as an implicit GEMM on the
  * same kernel: no column matrix [upstream CLIP ModifiedResNet Bottleneck conv2 of layer3 /
@@ -450,7 +448,22 @@ int ov3d_gemm256_pair(const void* A, const void* A2, long long lda, const void* 
  *   Cin % 64 == 0; otherwise as ov3d_gemm256 with M = nimg*H*W, N = Cout, K = 9*Cin. */
 int ov3d_conv3x3_gemm256(const void* X, int nimg, int H, int W, int Cin, const void* Wt,
                          long long ldb, const void* bias, int bias_f32, const void* R, long long ldr,
-                         void* Y, long long ldc, int Cout, int relu, void* ctr, void* stream);
+                         void* Y, long long ldc, int Cout, int relu, void* stream);
+
+/* Output projection + residual + dropout + LayerNorm in ONE launch (forward) [models/
+ * transformer.py: out_proj (nn.MultiheadAttention, 223 / 307-308) or linear2 (275-277 /
+ * 375-377), then x + dropout(branch) and the next sub-layer's norm (forward_pre 262-280 /
+ * 355-379)]: y = bf16(x (R, K) . w (256, K)^T + bias) (bf16 rows / weight / bias) replaces the
+ * y operand of ov3d_resnorm_fwd (same outputs, same dropout hash and rounding; y itself is not
+ * written).  ov3d_linres_supported(Cout, K): Cout == 256, K % 32 == 0, K <= 256.  x, w, s and
+ * src 16-byte aligned, ldx / ldw multiples of 8 elements, bias 8-byte aligned or null. */
+int ov3d_linres_supported(int Cout, int K);
+int ov3d_linres_fwd(long long R, int K, const void* x, long long ldx, const void* w, long long ldw,
+                    const void* bias, const void* src, int src_bf16, float dropout_p,
+                    const int64_t* seed, int site, const float* ga, const float* ba,
+                    const void* pos, int pos_bf16, const float* gb, const float* bb, float eps,
+                    float* s, float* mean, float* rstd, void* xa, void* xap, void* xb, int xb_bf16,
+                    long long xb_inner, long long xb_s0, long long xb_s1, void* stream);
 
 /* ---- Flash attention (head_dim 64, bf16, no mask) ----
  * Replaces the nn.MultiheadAttention core of models/transformer.py:223,271 (encoder

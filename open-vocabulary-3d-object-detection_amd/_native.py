@@ -117,9 +117,10 @@ _SIGS = {
     "ov3d_project_box2d": "pppliipppppp",
     "ov3d_heads_out_fwd": "plippipiippippppppipp",
     "ov3d_heads_out_bwd": "pppiiiipiippppppplp",
-    "ov3d_gemm256": "plplpiplpliiiipp",
-    "ov3d_conv3x3_gemm256": "piiiiplpiplpliipp",
-    "ov3d_gemm256_pair": "pplpplppippliiipp",
+    "ov3d_gemm256": "plplpiplpliiiip",
+    "ov3d_conv3x3_gemm256": "piiiiplpiplpliip",
+    "ov3d_gemm256_pair": "pplpplppippliiip",
+    "ov3d_linres_fwd": "liplplppifpipppippfppppppilllp",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
                           "ov3d_attn_dropbits_words", "ov3d_attn_maskbits_words", "ov3d_fps_workspace", "ov3d_attn_small_bwd", "ov3d_set_loss_fwd_parts",
@@ -130,7 +131,7 @@ EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_
                           "ov3d_rows_gemm_supported", "ov3d_sa_dy_fused_supported",
                           "ov3d_tile_gemm_supported", "ov3d_sun_range_parts", "ov3d_heads_out_max_text",
                           "ov3d_heads_out_workspace", "ov3d_stamps_arm", "ov3d_stamps_count",
-                          "ov3d_stamps_get", "ov3d_wall_clock_khz")
+                          "ov3d_stamps_get", "ov3d_wall_clock_khz", "ov3d_linres_supported")
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_longlong, "f": ctypes.c_float,
        "d": ctypes.c_double}
@@ -201,6 +202,8 @@ def load():
         lib.ov3d_sun_range_parts.restype = ctypes.c_int
         lib.ov3d_heads_out_max_text.argtypes = []
         lib.ov3d_heads_out_max_text.restype = ctypes.c_int
+        lib.ov3d_linres_supported.argtypes = [ctypes.c_int] * 2
+        lib.ov3d_linres_supported.restype = ctypes.c_int
         lib.ov3d_heads_out_workspace.argtypes = [ctypes.c_int] * 2
         lib.ov3d_heads_out_workspace.restype = ctypes.c_longlong
         lib.ov3d_version.argtypes = []

@@ -70,7 +70,6 @@ struct Gemm256Args {
     // a second product of the same shape in the same launch (nprob = 2): its tiles follow the
     // first's in the tile order (the decoder's K and V projections of the memory)
     int nprob;
-    int* ctr;          // 8 per-XCD tile counters, zero at launch (dynamic schedule), or null
     const bf16* A2;
     const bf16* B2;
     const void* bias2;
@@ -154,9 +153,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, lo
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)n, 0x00020000);
 }
 
-template <bool CONV>
+template <bool CONV, bool TAIL>   // TAIL: K % 64 != 0 (its own instance: the checks cost registers)
 __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
-    __shared__ __attribute__((aligned(16))) char L[2 * BUF + 16];   // + the next-tile slot
+    __shared__ __attribute__((aligned(16))) char L[2 * BUF];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave >> 2, wc = wave & 3;
@@ -183,27 +182,6 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
             lt = xbeg + (bid >> 3); lt_end = xbeg + q8 + (xcd < r8 ? 1 : 0); lt_step = nwg >> 3;
         }
     }
-    // Dynamic schedule (a.ctr): after its first tile a workgroup takes the next untaken tile of
-    // its XCD's range (one relaxed agent-scope atomic on that XCD's counter), then of the other
-    // ranges: a workgroup that starts late (its CU busy with a concurrent kernel, e.g. the
-    // step's side-stream FPS) leaves its share to the others instead of finishing last.
-    const bool dyn = a.ctr != nullptr && nwg != tiles;
-    int* const slot = reinterpret_cast<int*>(L + 2 * BUF);
-    auto dequeue = [&]() -> int {   // wave 0 only (lane 0 adds: a vector atomic)
-        const int per_x = nwg >> 3;
-        for (int k = 0; k < 8; ++k) {
-            const int x = (xcd + k) & 7;
-            const int len = q8 + (x < r8 ? 1 : 0) - per_x;   // tiles beyond the first round
-            if (len <= 0) continue;
-            int got = 0;
-            if (lane == 0)   // one add per wave (the other lanes read lane 0's result)
-                got = __hip_atomic_fetch_add(a.ctr + x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            got = __shfl(got, 0);
-            if (got < len) return xbeg_of(x) + per_x + got;
-        }
-        return tiles;   // none left
-    };
-    int nxt = tiles;
     // the current tile's problem: operand / output pointers (scalar selects)
     const bf16* pA = a.A;
     const bf16* pB = a.B;
@@ -278,7 +256,7 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
     };
     auto stage = [&](int h, int kt, int ctap, int cc) {
         char* dst = L + (kt & 1) * BUF + h * HALF + 16 * wave * 128;
-        const bool tail = (kt + 1) * BK > a.K;   // wave-uniform
+        const bool tail = TAIL && (kt + 1) * BK > a.K;   // wave-uniform
         if (h >= 2) {
             const uint32_t ko = (uint32_t)kt * (BK * 2);
             uint32_t v0 = vB[2 * (h - 2)] + ko, v1 = vB[2 * (h - 2) + 1] + ko;
@@ -366,8 +344,6 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
         first = false;
         barrier();
         if (a.stagger && wr == 1) barrier();   // stagger: waves 4-7 one barrier behind
-        // the next tile, asked for now and read after the K loop (its latency hides there)
-        if (dyn && wave == 0) nxt = dequeue();
 #pragma unroll
         for (int x = 0; x < 2; ++x)
 #pragma unroll
@@ -423,12 +399,7 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
             barrier();
             if constexpr (CONV) { tap1 = tap2; c1 = c2; adv(tap2, c2); }
         }
-        if (dyn && wave == 0 && lane == 0) {
-            *slot = nxt;
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
         if (a.stagger && wr == 0) barrier();   // close the stagger: every wave is past its last LDS read
-        if (dyn && !a.stagger) barrier();
 
         // ---- epilogue of this tile, the next tile's first two K-steps in flight meanwhile
         const int em0 = m0, en0 = n0;
@@ -454,12 +425,7 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) bias[ni][j][r] = bv[r];
             }
-        if (dyn) {
-            lt = *slot;
-            lt_end = tiles;
-        } else {
-            lt += lt_step;
-        }
+        lt += lt_step;
         if (lt < lt_end) {
             coords(lt, m0, n0);
             setup(m0, n0);
@@ -533,15 +499,12 @@ int launch(Gemm256Args a, bool conv, void* stream) {
     a.stagger = st_env;
     a.delay = dl_env;
     const unsigned grid = (unsigned)(tiles <= cus ? tiles : cus);
-    if (a.ctr) {
-        if ((long long)grid == tiles) a.ctr = nullptr;   // one tile per workgroup: nothing to take
-        else if (hipMemsetAsync(a.ctr, 0, 8 * sizeof(int), ov3d_stream(stream)) != hipSuccess)
-            return OV3D_ELAUNCH;
-    }
-    if (conv)
-        hipLaunchKernelGGL(gemm256_kernel<true>, dim3(grid), dim3(512), 0, ov3d_stream(stream), a);
+    if (conv)   // Cin % 64 == 0: no K tail
+        hipLaunchKernelGGL((gemm256_kernel<true, false>), dim3(grid), dim3(512), 0, ov3d_stream(stream), a);
+    else if (a.K % BK)
+        hipLaunchKernelGGL((gemm256_kernel<false, true>), dim3(grid), dim3(512), 0, ov3d_stream(stream), a);
     else
-        hipLaunchKernelGGL(gemm256_kernel<false>, dim3(grid), dim3(512), 0, ov3d_stream(stream), a);
+        hipLaunchKernelGGL((gemm256_kernel<false, false>), dim3(grid), dim3(512), 0, ov3d_stream(stream), a);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }
@@ -562,19 +525,19 @@ bool common_ok(const void* B, long long ldb, const void* bias, const void* R, lo
 
 extern "C" int ov3d_gemm256(const void* A, long long lda, const void* B, long long ldb,
                             const void* bias, int bias_f32, const void* R, long long ldr, void* C,
-                            long long ldc, int M, int N, int K, int relu, void* ctr, void* stream) {
+                            long long ldc, int M, int N, int K, int relu, void* stream) {
     if (!A || lda % 8 || lda < K || !aligned16(A) || 256LL * lda * 2 + 2LL * K > 0x7fffffffLL ||
         !common_ok(B, ldb, bias, R, ldr, C, ldc, M, N, K))
         return OV3D_EINVAL;
     Gemm256Args a{(const bf16*)A, lda, (const bf16*)B, ldb, bias, (const bf16*)R, ldr, (bf16*)C, ldc,
-                  M, N, K, bias_f32 ? 1 : 0, relu ? 1 : 0, 0, 0, 0, 1, 1, 0, 1, (int*)ctr, nullptr, nullptr, nullptr, nullptr};
+                  M, N, K, bias_f32 ? 1 : 0, relu ? 1 : 0, 0, 0, 0, 1, 1, 0, 1, nullptr, nullptr, nullptr, nullptr};
     return launch(a, false, stream);
 }
 
 extern "C" int ov3d_conv3x3_gemm256(const void* X, int nimg, int H, int W, int Cin, const void* Wt,
                                     long long ldb, const void* bias, int bias_f32, const void* R,
                                     long long ldr, void* Y, long long ldc, int Cout, int relu,
-                                    void* ctr, void* stream) {
+                                    void* stream) {
     if (!X || nimg <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cin % BK || !aligned16(X))
         return OV3D_EINVAL;
     const long long M = (long long)nimg * H * W;
@@ -584,21 +547,21 @@ extern "C" int ov3d_conv3x3_gemm256(const void* X, int nimg, int H, int W, int C
     const int K = 9 * Cin;
     if (!common_ok(Wt, ldb, bias, R, ldr, Y, ldc, (int)M, Cout, K)) return OV3D_EINVAL;
     Gemm256Args a{(const bf16*)X, 0, (const bf16*)Wt, ldb, bias, (const bf16*)R, ldr, (bf16*)Y, ldc,
-                  (int)M, Cout, K, bias_f32 ? 1 : 0, relu ? 1 : 0, H, W, Cin, 1, 1, 0, 1, (int*)ctr, nullptr, nullptr, nullptr, nullptr};
+                  (int)M, Cout, K, bias_f32 ? 1 : 0, relu ? 1 : 0, H, W, Cin, 1, 1, 0, 1, nullptr, nullptr, nullptr, nullptr};
     return launch(a, true, stream);
 }
 
 extern "C" int ov3d_gemm256_pair(const void* A, const void* A2, long long lda, const void* B,
                                  const void* B2, long long ldb, const void* bias, const void* bias2,
                                  int bias_f32, void* C, void* C2, long long ldc, int M, int N, int K,
-                                 void* ctr, void* stream) {
+                                 void* stream) {
     if (!A || !A2 || !B2 || !C2 || lda % 8 || lda < K || !aligned16(A) || !aligned16(A2) ||
         !aligned16(B2) || !aligned16(C2) || 256LL * lda * 2 + 2LL * K > 0x7fffffffLL ||
         (bias2 && !aligned16(bias2)) || (!bias) != (!bias2) ||
         !common_ok(B, ldb, bias, nullptr, 0, C, ldc, M, N, K))
         return OV3D_EINVAL;
     Gemm256Args a{(const bf16*)A, lda, (const bf16*)B, ldb, bias, nullptr, 0, (bf16*)C, ldc,
-                  M, N, K, bias_f32 ? 1 : 0, 0, 0, 0, 0, 1, 1, 0, 2, (int*)ctr, (const bf16*)A2, (const bf16*)B2,
+                  M, N, K, bias_f32 ? 1 : 0, 0, 0, 0, 0, 1, 1, 0, 2, (const bf16*)A2, (const bf16*)B2,
                   bias2, (bf16*)C2};
     return launch(a, false, stream);
 }

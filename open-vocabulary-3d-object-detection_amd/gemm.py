@@ -242,25 +242,6 @@ def gemm256_ok(a, w, residual=None, out=None):
     return out is None or (_rows_ok(out) and tuple(out.shape) == (M, N))
 
 
-_CTRS = {}
-# dynamic tile schedule of gemm256 (per-XCD counters in an 8-int workspace); OV3D_GEMM256_DYN=0:
-# the static persistent schedule
-GEMM256_DYN = os.environ.get("OV3D_GEMM256_DYN", "1") != "0"
-
-
-def _ctr(device):
-    """the gemm256 launches' tile counters on `device` (8 ints, zeroed by every launch on its
-    stream: launches on one stream serialise, so one buffer per stream serves them all)"""
-    if not GEMM256_DYN:
-        return None
-    key = (device, torch.cuda.current_stream(device).cuda_stream)   # one buffer per stream
-    c = _CTRS.get(key)
-    if c is None:
-        c = torch.zeros((16,), dtype=torch.int32, device=device)
-        _CTRS[key] = c
-    return c
-
-
 def _bias_arg(bias):
     if bias is None:
         return None, 0
@@ -284,7 +265,7 @@ def gemm256(a, w, bias=None, residual=None, relu=False, out=None):
     b, bf32 = _bias_arg(bias)
     _native.call("ov3d_gemm256", a, a.stride(0), w, w.stride(0), b, bf32, residual,
                  residual.stride(0) if residual is not None else 0, out, out.stride(0), M, N, K,
-                 int(bool(relu)), _ctr(a.device), like=a)
+                 int(bool(relu)), like=a)
     return out
 
 
@@ -298,7 +279,7 @@ def gemm256_pair(a1, w1, b1, a2, w2, b2):
     o2 = torch.empty_like(o1)
     (bb1, bf32), (bb2, _) = _bias_arg(b1), _bias_arg(b2.to(b1.dtype) if b1 is not None else None)
     _native.call("ov3d_gemm256_pair", a1, a2, a1.stride(0), w1, w2, w1.stride(0), bb1, bb2, bf32,
-                 o1, o2, N, M, N, K, _ctr(a1.device), like=a1)
+                 o1, o2, N, M, N, K, like=a1)
     return o1, o2
 
 
@@ -323,7 +304,7 @@ def conv3x3_gemm256(x, w, bias=None, residual=None, relu=False):
     b, bf32 = _bias_arg(bias)
     _native.call("ov3d_conv3x3_gemm256", x, n, H, W, C, w, w.stride(0), b, bf32, residual,
                  residual.stride(0) if residual is not None else 0, out, cout, cout,
-                 int(bool(relu)), _ctr(x.device), like=x)
+                 int(bool(relu)), like=x)
     return out
 
 

@@ -27,6 +27,11 @@ from . import attention as flash
 from . import gemm
 
 Pending = namedtuple("Pending", "src y p site")
+# a branch output not yet computed: y = x w^T + b (the sub-layer's output projection / FFN
+# linear2); resnorm() runs it inside the residual + LayerNorm launch (csrc/linres.hip)
+LinY = namedtuple("LinY", "x w b relu_p", defaults=(None,))
+# relu_p (FFN linear2): x is dropout_p(relu(h)); the input gradient then takes the FFN's
+# activation mask in its epilogue (dx = x > 0 ? dy w / (1 - p) : 0), as _FFN's backward does
 
 
 class FanIn:
@@ -55,6 +60,11 @@ class FanIn:
 enabled = True   # False: the plain module code under autocast as well (tests compare the two)
 fan_in = True    # False: every call returns its own pos / norm_b gradient (autograd sums them)
 fused_ffn = os.environ.get("OV3D_FUSED_FFN", "1") != "0"   # _FFN on short row blocks
+# output projection + residual + dropout + LayerNorm in one launch (csrc/linres.hip).  Off by
+# default: measured slower in the SUN step than rows GEMM + resnorm_fwd (decoder 1024-row blocks
+# 10.8 vs 5.0 + 5.1 us, encoder 16384 rows 33 vs 20 us: every 16-row workgroup re-reads the whole
+# 256 x K weight); OV3D_LINRES=1 turns it on
+linres = os.environ.get("OV3D_LINRES", "0") == "1"
 
 
 def supported(x, *norms):
@@ -137,96 +147,220 @@ class _ResNorm(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, ds, dxa, dxap, dxb):
-        p, site, R, C, shape, src_dt, y_dt, pos_dt = ctx.meta
-        s, mean, rstd, ga, gb = ctx.saved_tensors
-        need = ctx.needs_input_grad   # meta, src, y, pos, ga, ba, gb, bb
-        dev = s.device
+        return (None,) + _bwd_core(ctx, ds, dxa, dxap, dxb, ctx.needs_input_grad)
 
-        def g(t, dt):
-            return t.reshape(R, C).to(dt).contiguous() if t is not None else None
 
-        # the decoder's layer outputs reach here as strided (L, B, C) views of the stacked
-        # outputs' gradient: read in place (row r at (r // B) * s0 + (r % B) * s1)
+def _bwd_core(ctx, ds, dxa, dxap, dxb, need):
+    """the resnorm backward launch; need = needs_input_grad over (meta, src, y, pos, ga, ba,
+    gb, bb) -> (dsrc, dy, dpos, dga, dba, dgb, dbb) (views of the forward's shapes)"""
+    p, site, R, C, shape, src_dt, y_dt, pos_dt = ctx.meta
+    s, mean, rstd, ga, gb = ctx.saved_tensors[:5]
+    dev = s.device
+
+    def g(t, dt):
+        return t.reshape(R, C).to(dt).contiguous() if t is not None else None
+
+    # the decoder's layer outputs reach here as strided (L, B, C) views of the stacked
+    # outputs' gradient: read in place (row r at (r // B) * s0 + (r % B) * s1)
+    xb_map = (0, 0, 0)
+    if dxb is not None and dxb.dtype in (torch.float32, torch.bfloat16) and dxb.dim() == 3 and \
+            dxb.stride(2) == 1 and not dxb.is_contiguous() and len(shape) == 3 and \
+            tuple(dxb.shape) == tuple(shape) and dxb.stride(0) >= C and dxb.stride(1) >= C:
+        xb_map = (shape[1], dxb.stride(0), dxb.stride(1))
+    ds, dxa, dxap = g(ds, torch.float32), g(dxa, torch.bfloat16), g(dxap, torch.bfloat16)
+    if not xb_map[0]:
+        dxb = g(dxb, torch.float32)
+    if ga is None:
+        dxa = dxap = None
+    if gb is None:
+        dxb = None
+    dsrc = torch.empty((R, C), dtype=torch.float32, device=dev) if need[1] else None
+    dy = torch.empty((R, C), dtype=y_dt, device=dev) if need[2] else None
+    dpos = torch.empty((R, C), dtype=pos_dt, device=dev) if (need[3] and dxap is not None) else None
+    has_a = dxa is not None or dxap is not None
+    has_b = dxb is not None
+    dga = torch.empty(C, dtype=torch.float32, device=dev) if (need[4] and has_a) else None
+    dba = torch.empty(C, dtype=torch.float32, device=dev) if (need[5] and has_a) else None
+    dgb = torch.empty(C, dtype=torch.float32, device=dev) if (need[6] and has_b) else None
+    dbb = torch.empty(C, dtype=torch.float32, device=dev) if (need[7] and has_b) else None
+    acc = 0
+    pos_fan, nb_fan = ctx.fans
+    # LayerNorm weight / bias gradients: deferred to one grouped launch at the end of the
+    # backward (with the weight gradients, gemm.DEFER_WGRAD) from this call's partials
+    params = ctx.params
+    defer_norm = gemm.DEFER_WGRAD and not torch.is_grad_enabled() and (has_a or has_b) and all(
+        t is None or gemm._leaf_param(t) is t for t in params)
+    slots = []
+    if defer_norm:
+        for k, (nd, have) in enumerate(((need[4], has_a), (need[5], has_a),
+                                        (need[6], has_b), (need[7], has_b))):
+            if nd and have:
+                slots.append((k, params[k]))
+        dga = dba = dgb = dbb = None
+        nb_fan = None
+    ret_pos = ret_nb = True
+    if pos_fan is not None and need[3]:
+        first, ret_pos = pos_fan.take()
+        if first:   # this call's gradient (or zeros) starts the sum
+            pos_fan.bufs = dpos if dpos is not None else \
+                torch.zeros((R, C), dtype=pos_dt, device=dev)
+        elif dpos is not None:
+            dpos, acc = pos_fan.bufs, acc | 1
+        if ret_pos:
+            dpos_ret, pos_fan.bufs = pos_fan.bufs, None
+    if nb_fan is not None and (need[6] or need[7]):
+        first, ret_nb = nb_fan.take()
+        if first:
+            z = lambda t, n: t if t is not None or not n else \
+                torch.zeros(C, dtype=torch.float32, device=dev)   # noqa: E731
+            nb_fan.bufs = (z(dgb, need[6]), z(dbb, need[7]))
+        elif has_b:
+            dgb, dbb = nb_fan.bufs
+            acc |= 4
+        if ret_nb:
+            nb_ret, nb_fan.bufs = nb_fan.bufs, None
+    lib = _native.load()
+    nparts = lib.ov3d_resnorm_bwd_parts(R, C)
+    partials = torch.empty((nparts, 4, C), dtype=torch.float32, device=dev) \
+        if (has_a or has_b) else None
+    seed = ctx.seed if (p > 0 and dy is not None) else None
+    if dsrc is not None or dy is not None or dpos is not None or has_a or has_b:
+        _native.call("ov3d_resnorm_bwd", R, C, s, mean, rstd, ds, dxa, dxap, dxb, _dt_flag(dxb),
+                     *xb_map, ga, gb,
+                     float(p) if dy is not None else 0.0, seed, site, dsrc, dy, _dt_flag(dy),
+                     dpos, _dt_flag(dpos), partials, nparts, dga, dba,
+                     dgb, dbb, acc, like=s)
+    if slots:
+        gemm.defer_norm_grads(partials, nparts, C, slots)
+    v = lambda t: t.view(shape) if t is not None else None   # noqa: E731
+    if dsrc is not None and src_dt != torch.float32:
+        dsrc = dsrc.to(src_dt)
+    if pos_fan is not None and need[3]:
+        dpos = dpos_ret if ret_pos else None
+    if nb_fan is not None and (need[6] or need[7]):
+        dgb, dbb = nb_ret if ret_nb else (None, None)
+    if defer_norm:
+        dga = dba = dgb = dbb = None
+    return v(dsrc), v(dy), v(dpos), dga, dba, dgb, dbb
+
+
+class _LinResNorm(torch.autograd.Function):
+    """resnorm with the branch output computed in the same launch: y = bf16(x w^T + b)
+    (csrc/linres.hip).  Backward: the resnorm backward launch gives dy (bf16), then the linear's
+    input gradient dx = dy w (rowsgemm) and its weight / bias gradients (deferred with the
+    others when gemm.DEFER_WGRAD)."""
+
+    @staticmethod
+    def forward(ctx, meta, src, x, w, b, pos, ga, ba, gb, bb, relu_p=None):
+        p, site, want_a, want_ap, want_b, eps, shape, fans, xb_into = meta
+        C = w.shape[0]
+        K = x.shape[-1]
+        bf = torch.bfloat16
+        xr = x.reshape(-1, K)
+        wc, bc = gemm.cast_param(w, bf), gemm.cast_param(b, bf) if b is not None else None
+        srcr, posr = _rows(src, C), _rows(pos, C)
+        R = xr.shape[0]
+        dev = x.device
+        s = torch.empty((R, C), dtype=torch.float32, device=dev)
+        norm = want_a or want_ap or want_b
+        mean = torch.empty(R, dtype=torch.float32, device=dev) if norm else None
+        rstd = torch.empty(R, dtype=torch.float32, device=dev) if norm else None
+        xa = torch.empty((R, C), dtype=bf, device=dev) if want_a else None
+        xap = torch.empty((R, C), dtype=bf, device=dev) if want_ap else None
         xb_map = (0, 0, 0)
-        if dxb is not None and dxb.dtype in (torch.float32, torch.bfloat16) and dxb.dim() == 3 and \
-                dxb.stride(2) == 1 and not dxb.is_contiguous() and len(shape) == 3 and \
-                tuple(dxb.shape) == tuple(shape) and dxb.stride(0) >= C and dxb.stride(1) >= C:
-            xb_map = (shape[1], dxb.stride(0), dxb.stride(1))
-        ds, dxa, dxap = g(ds, torch.float32), g(dxa, torch.bfloat16), g(dxap, torch.bfloat16)
-        if not xb_map[0]:
-            dxb = g(dxb, torch.float32)
-        if ga is None:
-            dxa = dxap = None
-        if gb is None:
-            dxb = None
-        dsrc = torch.empty((R, C), dtype=torch.float32, device=dev) if need[1] else None
-        dy = torch.empty((R, C), dtype=y_dt, device=dev) if need[2] else None
-        dpos = torch.empty((R, C), dtype=pos_dt, device=dev) if (need[3] and dxap is not None) else None
-        has_a = dxa is not None or dxap is not None
-        has_b = dxb is not None
-        dga = torch.empty(C, dtype=torch.float32, device=dev) if (need[4] and has_a) else None
-        dba = torch.empty(C, dtype=torch.float32, device=dev) if (need[5] and has_a) else None
-        dgb = torch.empty(C, dtype=torch.float32, device=dev) if (need[6] and has_b) else None
-        dbb = torch.empty(C, dtype=torch.float32, device=dev) if (need[7] and has_b) else None
-        acc = 0
-        pos_fan, nb_fan = ctx.fans
-        # LayerNorm weight / bias gradients: deferred to one grouped launch at the end of the
-        # backward (with the weight gradients, gemm.DEFER_WGRAD) from this call's partials
-        params = ctx.params
-        defer_norm = gemm.DEFER_WGRAD and not torch.is_grad_enabled() and (has_a or has_b) and all(
-            t is None or gemm._leaf_param(t) is t for t in params)
-        slots = []
-        if defer_norm:
-            for k, (nd, have) in enumerate(((need[4], has_a), (need[5], has_a),
-                                            (need[6], has_b), (need[7], has_b))):
-                if nd and have:
-                    slots.append((k, params[k]))
-            dga = dba = dgb = dbb = None
-            nb_fan = None
-        ret_pos = ret_nb = True
-        if pos_fan is not None and need[3]:
-            first, ret_pos = pos_fan.take()
-            if first:   # this call's gradient (or zeros) starts the sum
-                pos_fan.bufs = dpos if dpos is not None else \
-                    torch.zeros((R, C), dtype=pos_dt, device=dev)
-            elif dpos is not None:
-                dpos, acc = pos_fan.bufs, acc | 1
-            if ret_pos:
-                dpos_ret, pos_fan.bufs = pos_fan.bufs, None
-        if nb_fan is not None and (need[6] or need[7]):
-            first, ret_nb = nb_fan.take()
-            if first:
-                z = lambda t, n: t if t is not None or not n else \
-                    torch.zeros(C, dtype=torch.float32, device=dev)   # noqa: E731
-                nb_fan.bufs = (z(dgb, need[6]), z(dbb, need[7]))
-            elif has_b:
-                dgb, dbb = nb_fan.bufs
-                acc |= 4
-            if ret_nb:
-                nb_ret, nb_fan.bufs = nb_fan.bufs, None
-        lib = _native.load()
-        nparts = lib.ov3d_resnorm_bwd_parts(R, C)
-        partials = torch.empty((nparts, 4, C), dtype=torch.float32, device=dev) \
-            if (has_a or has_b) else None
-        seed = ctx.seed if (p > 0 and dy is not None) else None
-        if dsrc is not None or dy is not None or dpos is not None or has_a or has_b:
-            _native.call("ov3d_resnorm_bwd", R, C, s, mean, rstd, ds, dxa, dxap, dxb, _dt_flag(dxb),
-                         *xb_map, ga, gb,
-                         float(p) if dy is not None else 0.0, seed, site, dsrc, dy, _dt_flag(dy),
-                         dpos, _dt_flag(dpos), partials, nparts, dga, dba,
-                         dgb, dbb, acc, like=s)
-        if slots:
-            gemm.defer_norm_grads(partials, nparts, C, slots)
+        if want_b and xb_into is not None:
+            out, l = xb_into
+            xb = out[l]
+            xb_map = (shape[1], C, shape[0] * C)
+        else:
+            xb = torch.empty((R, C), dtype=torch.float32, device=dev) if want_b else None
+        seed = flash._seed(dev) if p > 0 else None
+        _native.call("ov3d_linres_fwd", R, K, xr, xr.stride(0), wc, wc.stride(0), bc, srcr,
+                     _dt_flag(srcr), float(p), seed, site, ga, ba, posr, _dt_flag(posr), gb, bb,
+                     float(eps), s, mean, rstd, xa, xap, xb, _dt_flag(xb), *xb_map, like=s)
+        ctx.save_for_backward(s, mean, rstd, ga, gb, xr, wc)
+        ctx.seed = seed
+        ctx.params = (ga, ba, gb, bb)
+        ctx.lin = (w, b)
+        ctx.set_materialize_grads(False)
+        ctx.meta = (p, site, R, C, shape, src.dtype if src is not None else None, bf,
+                    pos.dtype if pos is not None else None)
+        ctx.xshape, ctx.xdt = x.shape, x.dtype
+        ctx.relu_p = relu_p
+        ctx.fans = fans
         v = lambda t: t.view(shape) if t is not None else None   # noqa: E731
-        if dsrc is not None and src_dt != torch.float32:
-            dsrc = dsrc.to(src_dt)
-        if pos_fan is not None and need[3]:
-            dpos = dpos_ret if ret_pos else None
-        if nb_fan is not None and (need[6] or need[7]):
-            dgb, dbb = nb_ret if ret_nb else (None, None)
-        if defer_norm:
-            dga = dba = dgb = dbb = None
-        return None, v(dsrc), v(dy), v(dpos), dga, dba, dgb, dbb
+        if xb_map[0]:
+            return v(s), v(xa), v(xap), xb.transpose(0, 1)
+        return v(s), v(xa), v(xap), v(xb)
+
+    @staticmethod
+    def backward(ctx, ds, dxa, dxap, dxb):
+        nig = ctx.needs_input_grad   # meta, src, x, w, b, pos, ga, ba, gb, bb
+        need_y = nig[2] or nig[3] or nig[4]
+        need = (False, nig[1], need_y, nig[5], nig[6], nig[7], nig[8], nig[9])
+        dsrc, dy, dpos, dga, dba, dgb, dbb = _bwd_core(ctx, ds, dxa, dxap, dxb, need)
+        dx = dw = db = None
+        if dy is not None:
+            xr, wc = ctx.saved_tensors[5:7]
+            w, b = ctx.lin
+            dyr = dy.reshape(-1, wc.shape[0])
+            with torch.autocast("cuda", enabled=False):
+                if nig[2] and ctx.relu_p is not None:   # the FFN's ReLU + dropout mask
+                    dx = gemm.act_gemm(dyr, wc, None, False, 2, ctx.relu_p, h=xr).view(ctx.xshape)
+                elif nig[2]:
+                    dx = gemm._dgrad(dyr, wc).to(ctx.xdt).view(ctx.xshape)
+                if nig[3] or (b is not None and nig[4]):
+                    dw, db = gemm.linear_weight_grads(dyr, xr, w, b, nig[3], nig[4])
+        return None, dsrc, dx, dw, db, dpos, dga, dba, dgb, dbb, None
+
+
+def linres_ok(y, C):
+    """the LinY branch y can run inside the resnorm launch (csrc/linres.hip)"""
+    if not (linres and isinstance(y, LinY) and y.x.is_cuda and y.x.dtype == torch.bfloat16):
+        return False
+    x = y.x
+    K = x.shape[-1]
+    if not (x.stride(-1) == 1 and x.is_contiguous() and x.data_ptr() % 16 == 0 and y.w.dim() == 2
+            and tuple(y.w.shape) == (C, K)):
+        return False
+    return bool(_native.load().ov3d_linres_supported(C, K))
+
+
+def resolve(y):
+    """a LinY branch computed on its own (rows GEMM); other values unchanged"""
+    if isinstance(y, LinY):
+        return gemm.rows_linear(y.x, y.w, y.b)
+    return y
+
+
+class _FFN1(torch.autograd.Function):
+    """h = dropout_p(relu(x w1^T + b1)) (linear1 with its activation epilogue) of an FFN whose
+    linear2 runs inside the next resnorm launch (LinY with relu_p): the gradient arriving here
+    already carries the activation mask (the LinY backward's dgrad epilogue)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, p, site):
+        bf = torch.bfloat16
+        C = x.shape[-1]
+        xc = x.reshape(-1, C)
+        w1c, b1c = gemm.cast_param(w1, bf), gemm.cast_param(b1, bf)
+        seed = flash._seed(x.device) if p > 0 else None
+        h = gemm.act_gemm(xc, w1c, _bias(b1c), True, 1, p, seed, site)
+        ctx.save_for_backward(xc, w1c)
+        ctx.params = (w1, b1)
+        ctx.meta = (x.shape, x.dtype)
+        return h
+
+    @staticmethod
+    def backward(ctx, dy1):
+        xc, w1c = ctx.saved_tensors
+        w1, b1 = ctx.params
+        xshape, xdt = ctx.meta
+        need = ctx.needs_input_grad
+        dy1 = dy1.reshape(-1, w1c.shape[0]).to(torch.bfloat16).contiguous()
+        dw1, db1 = gemm.linear_weight_grads(dy1, xc, w1, b1, need[1], need[2])
+        dx = gemm.act_gemm(dy1, w1c, None, False).to(xdt).view(xshape) if need[0] else None
+        return dx, dw1, db1, None, None
 
 
 def resnorm(pend, norm_a=None, pos=None, want_a=True, want_ap=False, norm_b=None, pos_fan=None,
@@ -236,7 +370,10 @@ def resnorm(pend, norm_a=None, pos=None, want_a=True, want_ap=False, norm_b=None
     xb_into = (out, l): xb of these (Q, B, C) rows is written in bf16 into out[l] of an
     (L, B, Q, C) buffer (the heads' row order) and returned as that (Q, B, C) view."""
     src, y, p, psite = pend
-    ref = y if y is not None else src
+    fuse = isinstance(y, LinY) and src is not None and linres_ok(y, y.w.shape[0])
+    if isinstance(y, LinY) and not fuse:
+        y = resolve(y)
+    ref = src if fuse else (y if y is not None else src)
     shape = tuple(ref.shape)
     if norm_a is None:
         want_a = want_ap = False
@@ -259,6 +396,9 @@ def resnorm(pend, norm_a=None, pos=None, want_a=True, want_ap=False, norm_b=None
     gb = norm_b.weight if norm_b is not None else None
     bb = norm_b.bias if norm_b is not None else None
     with torch.autocast("cuda", enabled=False):
+        if fuse:
+            return _LinResNorm.apply(meta, src, y.x, y.w, y.b, pos if want_ap else None,
+                                     ga, ba, gb, bb, y.relu_p)
         return _ResNorm.apply(meta, src, y, pos if want_ap else None, ga, ba, gb, bb)
 
 
@@ -378,8 +518,15 @@ def ffn_weights_ok(x, w1, w2):
     return gemm.shape_ok(M, N, F) and gemm.shape_ok(M, F, N) and gemm.shape_ok(M, C, F)
 
 
-def ffn(x, linear1, linear2, activation, dropout, site):
-    """linear2(dropout(activation(linear1(x)))) of a transformer layer (bf16 rows)."""
+def ffn(x, linear1, linear2, activation, dropout, site, defer=False):
+    """linear2(dropout(activation(linear1(x)))) of a transformer layer (bf16 rows); defer: a
+    LinY whose linear2 the next resnorm launch computes (csrc/linres.hip)"""
+    if defer and linres and _ffn_ok(x, linear1, linear2, activation) and \
+            _native.load().ov3d_linres_supported(linear2.weight.shape[0], linear2.weight.shape[1]):
+        p = dropout.p if dropout.training else 0.0
+        with torch.autocast("cuda", enabled=False):
+            h = _FFN1.apply(x, linear1.weight, linear1.bias, p, site)
+        return LinY(h.view(*x.shape[:-1], h.shape[-1]), linear2.weight, linear2.bias, p)
     if _ffn_ok(x, linear1, linear2, activation):
         p = dropout.p if dropout.training else 0.0
         with torch.autocast("cuda", enabled=False):

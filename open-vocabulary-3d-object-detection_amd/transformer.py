@@ -44,7 +44,13 @@ class MultiheadAttention(nn.Module):
     def _heads(self, x, L, B):
         return x.view(L, B, self.num_heads, self.head_dim).permute(1, 2, 0, 3)
 
-    def forward(self, query, key, value, attn_mask: Optional[Tensor] = None):
+    def _out(self, out, defer):
+        """the output projection, or (defer) a resnorm.LinY the next resnorm launch computes"""
+        if defer:
+            return rn.LinY(out, self.out_proj.weight, self.out_proj.bias)
+        return rows_linear(out, self.out_proj.weight, self.out_proj.bias)
+
+    def forward(self, query, key, value, attn_mask: Optional[Tensor] = None, defer_out=False):
         L, B, E = query.shape
         S = key.shape[0]
         w, bias = self.in_proj_weight, self.in_proj_bias
@@ -64,7 +70,7 @@ class MultiheadAttention(nn.Module):
             out = flash.attention_packed(srcs, spec, L, S, self.num_heads,
                                          dropout_p=self.dropout if self.training else 0.0,
                                          site=self.site, mask=attn_mask if packed else None)
-            return rows_linear(out, self.out_proj.weight, self.out_proj.bias)
+            return self._out(out, defer_out)
         if packed:
             raise ValueError("a PackedMask needs the HIP attention path (bf16, head_dim 64)")
         q, k, v = (srcs[i][..., off:off + E] for i, off in spec)
@@ -79,7 +85,7 @@ class MultiheadAttention(nn.Module):
         return rows_linear(out, self.out_proj.weight, self.out_proj.bias)
 
 
-    def forward_kv(self, query, kv, idx):
+    def forward_kv(self, query, kv, idx, defer_out=False):
         """Cross attention whose K / V projections of the memory were computed for all decoder
         layers at once (MemoryKV): kv = (K_all, V_all, dK_all, dV_all, token, token_grad),
         this layer's block = columns idx*E .. (idx+1)*E."""
@@ -91,7 +97,7 @@ class MultiheadAttention(nn.Module):
             [q, K_all, V_all], ((0, 0), (1, idx * E), (2, idx * E)), L, S, self.num_heads,
             dropout_p=self.dropout if self.training else 0.0, site=self.site,
             ext=((None, dK, dV), token, tok_grad))
-        return rows_linear(out, self.out_proj.weight, self.out_proj.bias)
+        return self._out(out, defer_out)
 
 
 class _MemoryKV(torch.autograd.Function):
@@ -260,11 +266,12 @@ class TransformerEncoderLayer(nn.Module):
         site1, site2, site_ffn = rn.sites(self, 3)
         s, x, xp, _ = rn.resnorm(pend, self.norm1, pos=pos, want_a=True, want_ap=pos is not None)
         qk = xp if pos is not None else x
-        y = self.self_attn(qk, qk, x, attn_mask=src_mask)
+        y = self.self_attn(qk, qk, x, attn_mask=src_mask, defer_out=self.use_ffn)
         if not self.use_ffn:
             return rn.Pending(s, y, p1, site1)
         s, x, _, _ = rn.resnorm(rn.Pending(s, y, p1, site1), self.norm2)
-        y = rn.ffn(x, self.linear1, self.linear2, self.activation, self.dropout, site_ffn)
+        y = rn.ffn(x, self.linear1, self.linear2, self.activation, self.dropout, site_ffn,
+                   defer=True)
         return rn.Pending(s, y, p2, site2)
 
     def fused_ok(self, x):
@@ -317,17 +324,18 @@ class TransformerDecoderLayer(nn.Module):
                       else (0.0, 0.0, 0.0))
         site1, site2, site3, site_ffn = rn.sites(self, 4)
         qk = xp if query_pos is not None else x
-        y = self.self_attn(qk, qk, x, attn_mask=tgt_mask)
+        y = self.self_attn(qk, qk, x, attn_mask=tgt_mask, defer_out=True)
         s, x2, q, _ = rn.resnorm(rn.Pending(s, y, p1, site1), self.norm2, pos=query_pos,
                                  want_a=query_pos is None, want_ap=query_pos is not None,
                                  pos_fan=pos_fan)
         qx = q if query_pos is not None else x2
         if kv is not None and memory_mask is None:
-            y = self.multihead_attn.forward_kv(qx, kv, idx)
+            y = self.multihead_attn.forward_kv(qx, kv, idx, defer_out=True)
         else:
-            y = self.multihead_attn(qx, memory_pos, memory, attn_mask=memory_mask)
+            y = self.multihead_attn(qx, memory_pos, memory, attn_mask=memory_mask, defer_out=True)
         s, x3, _, _ = rn.resnorm(rn.Pending(s, y, p2, site2), self.norm3)
-        y = rn.ffn(x3, self.linear1, self.linear2, self.activation, self.dropout, site_ffn)
+        y = rn.ffn(x3, self.linear1, self.linear2, self.activation, self.dropout, site_ffn,
+                   defer=True)
         return rn.Pending(s, y, p3, site3)
 
     def fused_ok(self, x):

@@ -108,7 +108,7 @@ def test_round5_entries_reject_bad_arguments():
     def g(**kw):
         a = dict(ok, **kw)
         return lib.ov3d_gemm256(a["A"], a["lda"], a["B"], a["ldb"], a["bias"], a["bf"], a["R"],
-                                a["ldr"], a["C"], a["ldc"], a["M"], a["N"], a["K"], a["relu"], None, None)
+                                a["ldr"], a["C"], a["ldc"], a["M"], a["N"], a["K"], a["relu"], None)
     assert g(A=None) == -1
     assert g(K=100) == -1             # K % 8
     assert g(N=60, ldc=64) == -1      # N % 8
@@ -118,10 +118,10 @@ def test_round5_entries_reject_bad_arguments():
     assert g(R=p, ldr=32) == -1       # ldr < N
     assert g(M=0) == -1
     assert lib.ov3d_conv3x3_gemm256(p, 2, 9, 9, 96, p, 864, None, 0, None, 0, p, 64, 64, 1,
-                                    None, None) == -1   # Cin % 64
+                                    None) == -1   # Cin % 64
     assert lib.ov3d_conv3x3_gemm256(p, 2, 9, 9, 64, p, 512, None, 0, None, 0, p, 64, 64, 1,
-                                    None, None) == -1   # ldb < 9 Cin
+                                    None) == -1   # ldb < 9 Cin
     assert lib.ov3d_conv3x3_gemm256(None, 2, 9, 9, 64, p, 576, None, 0, None, 0, p, 64, 64, 1,
-                                    None, None) == -1
+                                    None) == -1
     assert lib.ov3d_sa_dy_fused(None, None, None, None, 1 << 23, 128, 256, 64, None, None, None,
                                 None, None, None, None, None, None, None, 1, None) == -1
