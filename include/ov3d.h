@@ -406,6 +406,20 @@ int ov3d_avgpool2_nhwc(const void* in, int elem_bytes, int N, int H, int W, int 
 int ov3d_attnpool_tokens(const void* x, int elem_bytes, int R, int ntok, int C, const void* pos,
                          void* t, void* stream);
 
+/* The same pool's first query without the token rows (csrc/attnpool.hip) [upstream CLIP
+ * AttentionPool2d.forward, x[0] only; clip.inference, criterion.py:397; regionclip._pool_tokens]:
+ * ov3d_attnpool_mean: x (R, ntok, C) bf16, pos (ntok + 1, C) -> t0 (R, C) = bf16(bf16(mean_j x[r, j])
+ *   + pos[0]) (fp32 mean in token order: row 0 of ov3d_attnpool_tokens);
+ * ov3d_attnpool_fused: with a (r, h, c) at a[h * sa_h + r * sa_r + c] (= Wk_h^T q[r, h], bf16),
+ *   token rows t[r, 0] = t0[r], t[r, 1 + j] = bf16(x[r, j] + pos[1 + j]) built on chip:
+ *   s = bf16(a t^T) (fp32 sums), p = bf16(softmax_j(s)) (fp32), y (H, R, C) = bf16(p t) (fp32 sums).
+ * ov3d_attnpool_fused_supported(ntok, C, H): ntok + 1 <= 96, C % 64 == 0, H <= 48.  bf16 only;
+ * every pointer 16-byte aligned, sa_h and sa_r multiples of 8 elements. */
+int ov3d_attnpool_mean(const void* x, int R, int ntok, int C, const void* pos, void* t0, void* stream);
+int ov3d_attnpool_fused_supported(int ntok, int C, int H);
+int ov3d_attnpool_fused(const void* x, const void* t0, const void* pos, const void* a, long long sa_h,
+                        long long sa_r, int R, int ntok, int C, int H, void* y, void* stream);
+
 /* conv3 + bottleneck close of the RegionCLIP ModifiedResNet as ONE library GEMM [upstream CLIP
  * Bottleneck.forward: relu(bn3(conv3(out)) + identity); clip.inference, criterion.py:397]:
  *   out (M, N) = act(x (M, K) · w (N, K)^T + bias (N) + residual (M, N)), bf16 in and out,
@@ -438,6 +452,17 @@ int ov3d_gemm256(const void* A, long long lda, const void* B, long long ldb, con
 int ov3d_gemm256_pair(const void* A, const void* A2, long long lda, const void* B, const void* B2,
                       long long ldb, const void* bias, const void* bias2, int bias_f32, void* C,
                       void* C2, long long ldc, int M, int N, int K, void* stream);
+
+/* nbatch products of one shape in one launch (the RegionCLIP attention pool's per-head
+ * products: a_h = q_h Wk_h, o_h = y_h Wv_h^T, regionclip._pool_fused; upstream CLIP
+ * AttentionPool2d k / v projections, clip.inference, criterion.py:397): problem p is
+ *   C + p sC = act(A + p sA  .  (B + p sB)^T + bias + p sbias) (no residual),
+ * strides in elements (multiples of 8; sbias of 4 for f32, 8 for bf16 bias); as ov3d_gemm256
+ * otherwise. */
+int ov3d_gemm256_batched(const void* A, long long lda, long long sA, const void* B, long long ldb,
+                         long long sB, const void* bias, long long sbias, int bias_f32, void* C,
+                         long long ldc, long long sC, int M, int N, int K, int nbatch, int relu,
+                         void* stream);
 
 /* 3x3 convolution (pad 1, stride 1) + bias (+ residual) (+ ReLU) as an implicit GEMM on the
  * same kernel: no column matrix [upstream CLIP ModifiedResNet Bottleneck conv2 of layer3 /

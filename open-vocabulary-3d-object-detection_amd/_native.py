@@ -56,6 +56,8 @@ _SIGS = {
     "ov3d_bias_residual_act": "pilippip",
     "ov3d_avgpool2_nhwc": "piiiiipp",
     "ov3d_attnpool_tokens": "piiiippp",
+    "ov3d_attnpool_mean": "piiippp",
+    "ov3d_attnpool_fused": "pppplliiiipp",
     "ov3d_lt_gemm_bias_residual": "liiplplppliplplp",
     "ov3d_attn_fwd": "pppllliiiiffpiplpppip",
     "ov3d_attn_bwd": "ppplllplplpiiiiffppplplplpip",
@@ -120,6 +122,7 @@ _SIGS = {
     "ov3d_gemm256": "plplpiplpliiiip",
     "ov3d_conv3x3_gemm256": "piiiiplpiplpliip",
     "ov3d_gemm256_pair": "pplpplppippliiip",
+    "ov3d_gemm256_batched": "pllpllpliplliiiiip",
     "ov3d_linres_fwd": "liplplppifpipppippfppppppilllp",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
@@ -131,7 +134,8 @@ EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_
                           "ov3d_rows_gemm_supported", "ov3d_sa_dy_fused_supported",
                           "ov3d_tile_gemm_supported", "ov3d_sun_range_parts", "ov3d_heads_out_max_text",
                           "ov3d_heads_out_workspace", "ov3d_stamps_arm", "ov3d_stamps_count",
-                          "ov3d_stamps_get", "ov3d_wall_clock_khz", "ov3d_linres_supported")
+                          "ov3d_stamps_get", "ov3d_wall_clock_khz", "ov3d_linres_supported",
+                          "ov3d_attnpool_fused_supported")
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_longlong, "f": ctypes.c_float,
        "d": ctypes.c_double}
@@ -204,6 +208,8 @@ def load():
         lib.ov3d_heads_out_max_text.restype = ctypes.c_int
         lib.ov3d_linres_supported.argtypes = [ctypes.c_int] * 2
         lib.ov3d_linres_supported.restype = ctypes.c_int
+        lib.ov3d_attnpool_fused_supported.argtypes = [ctypes.c_int] * 3
+        lib.ov3d_attnpool_fused_supported.restype = ctypes.c_int
         lib.ov3d_heads_out_workspace.argtypes = [ctypes.c_int] * 2
         lib.ov3d_heads_out_workspace.restype = ctypes.c_longlong
         lib.ov3d_version.argtypes = []

@@ -67,13 +67,11 @@ struct Gemm256Args {
     int gm;            // row panels per group of the tile order
     int stagger;       // waves 4-7 one barrier behind (1) or in step (0)
     int delay;         // s_sleep rounds before the first tile of every other workgroup
-    // a second product of the same shape in the same launch (nprob = 2): its tiles follow the
-    // first's in the tile order (the decoder's K and V projections of the memory)
+    // nprob products of the same shape in the same launch, problem p at A + p sA, B + p sB,
+    // bias + p sbias, C + p sC (elements); its tiles follow problem p - 1's in the tile order
+    // (the decoder's K and V projections of the memory; the attention pool's per-head products)
     int nprob;
-    const bf16* A2;
-    const bf16* B2;
-    const void* bias2;
-    bf16* C2;
+    long long sA, sB, sbias, sC;
 };
 
 __device__ __forceinline__ f32x4 mfma16(i32x4 a, i32x4 b, f32x4 c) {
@@ -186,10 +184,10 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
     const bf16* pA = a.A;
     const bf16* pB = a.B;
     auto coords = [&](int t, int& m0, int& n0) {
-        const bool second = t >= ptiles;
-        if (second) t -= ptiles;
-        pA = second ? a.A2 : a.A;
-        pB = second ? a.B2 : a.B;
+        const int p = t / ptiles;
+        t -= p * ptiles;
+        pA = a.A + p * a.sA;
+        pB = a.B + p * a.sB;
         const int per = a.gm * ntn, g = t / per, first = g * a.gm;
         const int gs = min(ntm - first, a.gm), rem = t - g * per;
         m0 = (first + rem % gs) * 256;
@@ -403,8 +401,10 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
 
         // ---- epilogue of this tile, the next tile's first two K-steps in flight meanwhile
         const int em0 = m0, en0 = n0;
-        bf16* const eC = lt >= ptiles && a.nprob > 1 ? a.C2 : a.C;
-        const void* const ebias = lt >= ptiles && a.nprob > 1 ? a.bias2 : a.bias;
+        const int ep = lt / ptiles;
+        bf16* const eC = a.C + ep * a.sC;
+        const void* const ebias = a.bias ? reinterpret_cast<const char*>(a.bias) + ep * a.sbias * (a.bias_f32 ? 4 : 2)
+                                         : nullptr;
         if (has_r) load_res(0, em0, en0);
         float bias[2][2][4];
 #pragma unroll
@@ -478,7 +478,7 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-int launch(Gemm256Args a, bool conv, void* stream) {
+int launch(Gemm256Args a, bool conv, void* stream, bool one_tile = false) {
     const long long tiles = (long long)((a.M + 255) / 256) * ((a.N + 255) / 256) * a.nprob;
     if (tiles <= 0 || tiles > 0x7fffffffLL) return OV3D_EINVAL;
     // persistent grid: one 512-thread workgroup per CU (128 KB of LDS each)
@@ -498,7 +498,14 @@ int launch(Gemm256Args a, bool conv, void* stream) {
     static const int dl_env = getenv("OV3D_GEMM256_DELAY") ? atoi(getenv("OV3D_GEMM256_DELAY")) : 0;
     a.stagger = st_env;
     a.delay = dl_env;
-    const unsigned grid = (unsigned)(tiles <= cus ? tiles : cus);
+    // The two-problem launch (the decoder's memory K / V inside the SUN step) runs one tile per
+    // workgroup: the step's side-stream FPS holds 8 CUs for milliseconds, and a persistent grid's
+    // workgroups queued behind it took their whole tile ranges late (99 us in the step vs 57 us
+    // alone, profiles/r05_trace_steady_v1.json); hardware dispatch hands single tiles to the free
+    // CUs instead.  OV3D_GEMM256_PAIR_PERSIST=1 keeps the persistent grid.
+    static const int pp_env = getenv("OV3D_GEMM256_PAIR_PERSIST") ? atoi(getenv("OV3D_GEMM256_PAIR_PERSIST")) : 0;
+    one_tile = one_tile && !pp_env;
+    const unsigned grid = (unsigned)(tiles <= cus || one_tile ? tiles : cus);
     if (conv)   // Cin % 64 == 0: no K tail
         hipLaunchKernelGGL((gemm256_kernel<true, false>), dim3(grid), dim3(512), 0, ov3d_stream(stream), a);
     else if (a.K % BK)
@@ -530,7 +537,7 @@ extern "C" int ov3d_gemm256(const void* A, long long lda, const void* B, long lo
         !common_ok(B, ldb, bias, R, ldr, C, ldc, M, N, K))
         return OV3D_EINVAL;
     Gemm256Args a{(const bf16*)A, lda, (const bf16*)B, ldb, bias, (const bf16*)R, ldr, (bf16*)C, ldc,
-                  M, N, K, bias_f32 ? 1 : 0, relu ? 1 : 0, 0, 0, 0, 1, 1, 0, 1, nullptr, nullptr, nullptr, nullptr};
+                  M, N, K, bias_f32 ? 1 : 0, relu ? 1 : 0, 0, 0, 0, 1, 1, 0, 1, 0, 0, 0, 0};
     return launch(a, false, stream);
 }
 
@@ -547,8 +554,13 @@ extern "C" int ov3d_conv3x3_gemm256(const void* X, int nimg, int H, int W, int C
     const int K = 9 * Cin;
     if (!common_ok(Wt, ldb, bias, R, ldr, Y, ldc, (int)M, Cout, K)) return OV3D_EINVAL;
     Gemm256Args a{(const bf16*)X, 0, (const bf16*)Wt, ldb, bias, (const bf16*)R, ldr, (bf16*)Y, ldc,
-                  (int)M, Cout, K, bias_f32 ? 1 : 0, relu ? 1 : 0, H, W, Cin, 1, 1, 0, 1, nullptr, nullptr, nullptr, nullptr};
+                  (int)M, Cout, K, bias_f32 ? 1 : 0, relu ? 1 : 0, H, W, Cin, 1, 1, 0, 1, 0, 0, 0, 0};
     return launch(a, true, stream);
+}
+
+// element offset of q from p (both bf16 / f32 pointers of one address space)
+static long long elem_diff(const void* q, const void* p, int esz) {
+    return ((long long)(uintptr_t)q - (long long)(uintptr_t)p) / esz;
 }
 
 extern "C" int ov3d_gemm256_pair(const void* A, const void* A2, long long lda, const void* B,
@@ -561,7 +573,20 @@ extern "C" int ov3d_gemm256_pair(const void* A, const void* A2, long long lda, c
         !common_ok(B, ldb, bias, nullptr, 0, C, ldc, M, N, K))
         return OV3D_EINVAL;
     Gemm256Args a{(const bf16*)A, lda, (const bf16*)B, ldb, bias, nullptr, 0, (bf16*)C, ldc,
-                  M, N, K, bias_f32 ? 1 : 0, 0, 0, 0, 0, 1, 1, 0, 2, (const bf16*)A2, (const bf16*)B2,
-                  bias2, (bf16*)C2};
+                  M, N, K, bias_f32 ? 1 : 0, 0, 0, 0, 0, 1, 1, 0, 2, elem_diff(A2, A, 2), elem_diff(B2, B, 2),
+                  bias ? elem_diff(bias2, bias, bias_f32 ? 4 : 2) : 0, elem_diff(C2, C, 2)};
+    return launch(a, false, stream, true);
+}
+
+extern "C" int ov3d_gemm256_batched(const void* A, long long lda, long long sA, const void* B,
+                                    long long ldb, long long sB, const void* bias, long long sbias,
+                                    int bias_f32, void* C, long long ldc, long long sC, int M, int N,
+                                    int K, int nbatch, int relu, void* stream) {
+    if (!A || nbatch <= 0 || lda % 8 || lda < K || !aligned16(A) || sA % 8 || sB % 8 || sC % 8 ||
+        (bias && sbias % (bias_f32 ? 4 : 8)) || 256LL * lda * 2 + 2LL * K > 0x7fffffffLL ||
+        !common_ok(B, ldb, bias, nullptr, 0, C, ldc, M, N, K))
+        return OV3D_EINVAL;
+    Gemm256Args a{(const bf16*)A, lda, (const bf16*)B, ldb, bias, nullptr, 0, (bf16*)C, ldc,
+                  M, N, K, bias_f32 ? 1 : 0, relu ? 1 : 0, 0, 0, 0, 1, 1, 0, nbatch, sA, sB, sbias, sC};
     return launch(a, false, stream);
 }

@@ -283,6 +283,20 @@ def gemm256_pair(a1, w1, b1, a2, w2, b2):
     return o1, o2
 
 
+def gemm256_batched(A, lda, sA, B, ldb, sB, C, ldc, sC, M, N, K, nbatch, bias=None, sbias=0,
+                    relu=False, like=None):
+    """nbatch products in one launch of the tile kernel: problem p reads A + p sA, B + p sB (bf16
+    rows, K contiguous), bias + p sbias (bf16 or f32, or None) and writes C + p sC (bf16); all
+    offsets and leading dimensions in elements of the given base tensors (no shape checks here:
+    the C entry validates strides and alignment)"""
+    from . import _native
+    bf32 = 0
+    if bias is not None:
+        bf32 = int(bias.dtype == torch.float32)
+    _native.call("ov3d_gemm256_batched", A, lda, sA, B, ldb, sB, bias, sbias, bf32, C, ldc, sC, M, N,
+                 K, nbatch, int(bool(relu)), like=like if like is not None else A)
+
+
 def conv3x3_ok(x, w):
     """x (n, H, W, C) NHWC bf16, w (Cout, >= 9C) bf16 rows: the implicit-GEMM 3x3 convolution"""
     if not (GEMM256 and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.is_contiguous()

@@ -24,13 +24,17 @@ MI355X path (``region_features``), output-identical up to float rounding:
     the convolution weights;
   * ROIAlign for all L*B*Q boxes is one HIP launch (``ov3d_roi_align_fwd``)
     writing the (R,18,18,1280) rows the res5 GEMMs read;
-  * res5 runs once over all L*B*Q ROIs (1x1 convs as hipBLASLt GEMMs on rows,
-    3x3 convs on MIOpen channels-last), bf16 with fp32 accumulation;
+  * res5 runs once over all L*B*Q ROIs on the hand-written 256 x 256 tile kernel
+    (csrc/gemm256.hip: 1x1 convs as GEMMs on rows with bias / identity / ReLU in the
+    epilogue, 3x3 convs as implicit GEMMs over the NHWC rows), bf16 with fp32
+    accumulation; the backbone's narrow 3x3 convs (Cin % 64 != 0) as HIP im2col +
+    the same kernel;
   * the attention pool only ever needs its first query (``x[0]``): with
     a_h = Wk_h^T q_h the scores are a_h . t_j (the q_h . bk_h term is constant
     over j and cancels in the softmax) and the output is Wv_h (sum_j p_hj t_j)
     + bv_h, so neither K nor V is projected for the 82 tokens: 2.2 GFLOP ->
-    0.08 GFLOP per ROI.
+    0.08 GFLOP per ROI; the scores, softmax and p.t of all heads are one HIP
+    launch that builds the token rows on chip (csrc/attnpool.hip).
 """
 import math
 import os
@@ -223,6 +227,8 @@ class _Folded:
         self.wq = (ap.q_proj.weight.detach().float() * d ** -0.5).to(dtype)          # scaled q
         self.bq = (ap.q_proj.bias.detach().float() * d ** -0.5).to(dtype)
         self.wk = ap.k_proj.weight.detach().to(dtype).view(H, d, C)                 # (H, d, C)
+        self.wkt = self.wk.transpose(1, 2).contiguous()                              # (H, C, d)
+        self.wv = ap.v_proj.weight.detach().to(dtype).contiguous()                   # (H*d, C)
         self.wvt = ap.v_proj.weight.detach().to(dtype).view(H, d, C).transpose(1, 2).contiguous()
         self.bv = ap.v_proj.bias.detach().to(f32)
         self.wc = ap.c_proj.weight.detach().to(dtype)
@@ -304,6 +310,10 @@ IM2COL_CHUNK_BYTES = int(os.environ.get("OV3D_IM2COL_CHUNK_MB", "16384")) << 20
 # im2col of chunk i + 1 on a side stream while the GEMM of chunk i runs (two column buffers):
 # the byte-moving im2col hides behind the matrix-core GEMM (OV3D_CONV_OVERLAP=0: in series)
 CONV_OVERLAP = os.environ.get("OV3D_CONV_OVERLAP", "1") != "0"
+
+# the attention pool's scores / softmax / p.t in one launch over on-chip token rows
+# (csrc/attnpool.hip); OV3D_FUSED_POOL=0: the token rows + library bmm's (_pool_tokens)
+FUSED_POOL = os.environ.get("OV3D_FUSED_POOL", "1") != "0"
 _SIDE = {}
 
 
@@ -352,7 +362,11 @@ def _conv3x3(x, w, b, stride=1):
         else:
             _native.call("ov3d_im2col3x3", x[n0:n0 + n], x.element_size(), n, H, W, C, stride, kpad, c,
                          like=x)
-        torch.ops.aten._addmm_activation.out(b, c, wt, out=out[n0:n0 + n].view(-1, cout))
+        o = out[n0:n0 + n].view(-1, cout)
+        if gemm.gemm256_ok(c, w, out=o):   # the columns on the tile kernel, ReLU in its epilogue
+            gemm.gemm256(c, w, bias=b, relu=True, out=o)
+        else:
+            torch.ops.aten._addmm_activation.out(b, c, wt, out=o)
         if overlap:
             freed[ci % 2] = torch.cuda.Event()
             freed[ci % 2].record(main)
@@ -544,6 +558,14 @@ class RegionCLIP(nn.Module):
         feats = _native.check(feats.contiguous(), "res4 features", ndim=4)
         boxes = _native.check(boxes.contiguous(), "boxes", dtype=torch.float32, ndim=2)
         x = torch.empty((R, P, P, C), dtype=feats.dtype, device=feats.device)
+        if os.environ.get("OV3D_ROI_STATS") == "1" and not torch.cuda.is_current_stream_capturing():
+            # diagnostic: ROI extents in feature pixels and ROIAlign samples per bin (host sync)
+            wh = (boxes[:, 2:] - boxes[:, :2]).float() * self.spatial_scale
+            g = torch.ceil(wh / P).clamp(min=1)
+            qs = torch.tensor([0.1, 0.5, 0.9, 1.0], device=boxes.device)
+            print("ROI_STATS R=%d map=%dx%d w_q=%s h_q=%s samples/bin mean=%.2f" % (
+                R, H, W, torch.quantile(wh[:, 0], qs).tolist(), torch.quantile(wh[:, 1], qs).tolist(),
+                (g[:, 0] * g[:, 1]).mean().item()), flush=True)
         blk0 = self.backbone.layer4[0]
         xp = None
         if P % 2 == 0 and blk0.stride > 1 and blk0.downsample is not None:
@@ -561,7 +583,45 @@ class RegionCLIP(nn.Module):
 
     def _attnpool(self, x):
         """AttentionPool2d, first query only, reassociated (module docstring)."""
+        if self._fused_pool_ok(x):
+            return self._pool_fused(x)
         return self._pool_tokens(self._tokens(x))
+
+    def _fused_pool_ok(self, x):
+        fw = self.folded()
+        R, h, w, C = x.shape
+        return (FUSED_POOL and x.is_cuda and x.dtype == torch.bfloat16 and fw.pos.dtype == torch.bfloat16
+                and bool(_native.load().ov3d_attnpool_fused_supported(h * w, C, fw.heads)))
+
+    def _pool_fused(self, x):
+        """_pool_tokens without the token rows (csrc/attnpool.hip): the mean token t0, q and
+        a = Wk_h^T q_h as before, then scores, softmax and p.t for all heads in one launch that
+        builds the token rows on chip; the value / output projections as before."""
+        fw = self.folded()
+        R, h, w, C = x.shape
+        Hh, d = fw.heads, fw.head_dim
+        x = _native.check(x.contiguous(), "attnpool input", ndim=4)
+        t0 = torch.empty((R, C), dtype=x.dtype, device=x.device)
+        _native.call("ov3d_attnpool_mean", x, R, h * w, C, fw.pos, t0, like=x)
+        tiles = gemm.gemm256_ok(t0, fw.wq) and d % 8 == 0
+        q = (gemm.gemm256(t0, fw.wq, bias=fw.bq) if tiles
+             else torch.addmm(fw.bq, t0, fw.wq.t()))                     # (R, C), scaled
+        a = torch.empty((Hh, R, C), dtype=x.dtype, device=x.device)
+        if tiles:   # a_h = q_h Wk_h for every head in one tile-kernel launch (K = d)
+            gemm.gemm256_batched(q, C, d, fw.wkt, d, C * d, a, C, R * C, R, C, d, Hh)
+        else:
+            torch.bmm(q.view(R, Hh, d).transpose(0, 1), fw.wk, out=a)
+        y = torch.empty((Hh, R, C), dtype=x.dtype, device=x.device)
+        _native.call("ov3d_attnpool_fused", x, t0, fw.pos, a, a.stride(0), a.stride(1), R, h * w, C,
+                     Hh, y, like=x)
+        if tiles:   # o_h = y_h Wv_h^T + bv_h, one launch, written as (R, H*d) rows
+            o = torch.empty((R, C), dtype=x.dtype, device=x.device)
+            gemm.gemm256_batched(y, C, R * C, fw.wv, C, d * C, o, C, d, R, d, C, Hh, bias=fw.bv,
+                                 sbias=d)
+            return gemm.gemm256(o, fw.wc, bias=fw.bc).float()
+        o = torch.bmm(y, fw.wvt).transpose(0, 1)                         # (R, H, d)
+        o = (o.float() + fw.bv.view(Hh, d)).to(x.dtype).reshape(R, C)
+        return torch.addmm(fw.bc, o, fw.wc.t()).float()
 
     def _tokens(self, x):
         """(R, h, w, C) res5 rows -> (R, h*w + 1, C) token rows [mean; x] + pos (one HIP pass)."""

@@ -146,3 +146,28 @@ def test_gemm256_pair_equals_two_products(cuda):
     assert torch.equal(o2, gemm.gemm256(a2, w2, bias=b2))
     _check(o1, a1.float() @ w1.float().t() + b1.float())
     _check(o2, a2.float() @ w2.float().t() + b2.float())
+
+
+@pytest.mark.parametrize("R,C,H,d", [(4096, 2560, 40, 64), (300, 384, 6, 64)])
+def test_gemm256_batched_attnpool_products(cuda, R, C, H, d):
+    """the attention pool's per-head products in one launch each (regionclip._pool_fused):
+    a_h = q_h Wk_h (K = d, strided A columns, (H, R, C) output) and o_h = y_h Wv_h^T + bv_h
+    (N = d, f32 bias, column-block output): equal to the per-problem single launches bit for
+    bit and within one rounding of the fp32 bmm"""
+    from ov3d_amd import gemm
+    g = torch.Generator(device=cuda).manual_seed(R + H)
+    q = torch.randn(R, C, device=cuda, generator=g).to(torch.bfloat16)
+    wkt = (torch.randn(H, C, d, device=cuda, generator=g) / d ** 0.5).to(torch.bfloat16)
+    a = torch.empty((H, R, C), dtype=torch.bfloat16, device=cuda)
+    gemm.gemm256_batched(q, C, d, wkt, d, C * d, a, C, R * C, R, C, d, H)
+    ref = torch.bmm(q.float().view(R, H, d).transpose(0, 1), wkt.float().transpose(1, 2))
+    _check(a, ref)
+    for h in (0, H - 1):
+        assert torch.equal(a[h], gemm.gemm256(q[:, h * d:(h + 1) * d].contiguous(), wkt[h].contiguous()))
+    y = torch.randn(H, R, C, device=cuda, generator=g).to(torch.bfloat16)
+    wv = (torch.randn(H * d, C, device=cuda, generator=g) / C ** 0.5).to(torch.bfloat16)
+    bv = torch.randn(H * d, device=cuda, generator=g)
+    o = torch.full((R, H * d), 7.0, dtype=torch.bfloat16, device=cuda)
+    gemm.gemm256_batched(y, C, R * C, wv, C, d * C, o, H * d, d, R, d, C, H, bias=bv, sbias=d)
+    ref = torch.bmm(y.float(), wv.float().view(H, d, C).transpose(1, 2)) + bv.view(H, 1, d)
+    _check(o.view(R, H, d).transpose(0, 1), ref)

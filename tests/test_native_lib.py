@@ -125,3 +125,13 @@ def test_round5_entries_reject_bad_arguments():
                                     None) == -1
     assert lib.ov3d_sa_dy_fused(None, None, None, None, 1 << 23, 128, 256, 64, None, None, None,
                                 None, None, None, None, None, None, None, 1, None) == -1
+    # the fused attention pool: shape limits, strides and alignment
+    assert lib.ov3d_attnpool_fused_supported(81, 2560, 40) == 1
+    assert lib.ov3d_attnpool_fused_supported(96, 2560, 40) == 0      # ntok + 1 > 96
+    assert lib.ov3d_attnpool_fused_supported(81, 2560, 49) == 0      # H > 48
+    assert lib.ov3d_attnpool_fused_supported(81, 2500, 40) == 0      # C % 64
+    assert lib.ov3d_attnpool_fused(p, p, p, p, 40 * 2560, 2560, 4, 81, 2560, 49, p, None) == -1
+    assert lib.ov3d_attnpool_fused(p, p, p, p, 40 * 2560, 2564, 4, 81, 2560, 40, p, None) == -1
+    assert lib.ov3d_attnpool_fused(p, p, p, odd, 40 * 2560, 2560, 4, 81, 2560, 40, p, None) == -1
+    assert lib.ov3d_attnpool_mean(p, 4, 81, 2564, p, p, None) == -1          # C % 8
+    assert lib.ov3d_attnpool_mean(None, 4, 81, 2560, p, p, None) == -1

@@ -234,6 +234,58 @@ def test_attnpool_tokens_matches_torch(cuda, dtype, R, ntok, C):
     assert torch.allclose(t[:, 0].float(), ref[:, 0].float(), atol=tol, rtol=tol)
 
 
+@pytest.mark.parametrize("R,ntok,C,H", [(37, 81, 2560, 40), (5, 9, 128, 13), (3, 94, 64, 48)])
+def test_attnpool_fused_matches_token_path(cuda, R, ntok, C, H):
+    """ov3d_attnpool_mean is row 0 of ov3d_attnpool_tokens bit for bit; ov3d_attnpool_fused
+    (token rows on chip, scores, softmax, p.t in one launch) equals the token rows + bmm +
+    softmax + bmm composition of regionclip._pool_tokens up to the bmm's summation order
+    (scores rounded to bf16 on both sides), and stays within bf16 rounding of fp32."""
+    from ov3d_amd import _native
+    g = torch.Generator(device=cuda).manual_seed(R + ntok)
+    x = torch.randn(R, ntok, C, device=cuda, generator=g).to(torch.bfloat16)
+    pos = (0.5 * torch.randn(ntok + 1, C, device=cuda, generator=g)).to(torch.bfloat16)
+    a = (torch.randn(H, R, C, device=cuda, generator=g) / C ** 0.5).to(torch.bfloat16)
+    t = torch.empty((R, ntok + 1, C), dtype=torch.bfloat16, device=cuda)
+    _native.call("ov3d_attnpool_tokens", x, 2, R, ntok, C, pos, t, like=x)
+    t0 = torch.empty((R, C), dtype=torch.bfloat16, device=cuda)
+    _native.call("ov3d_attnpool_mean", x, R, ntok, C, pos, t0, like=x)
+    assert torch.equal(t0, t[:, 0])
+    y = torch.empty((H, R, C), dtype=torch.bfloat16, device=cuda)
+    _native.call("ov3d_attnpool_fused", x, t0, pos, a, a.stride(0), a.stride(1), R, ntok, C, H, y,
+                 like=x)
+    s = torch.bmm(a.transpose(0, 1), t.transpose(1, 2))                  # (R, H, T) bf16
+    p = torch.softmax(s.float(), dim=-1).to(torch.bfloat16)
+    ref = torch.bmm(p, t).transpose(0, 1)                                # (H, R, C)
+    err = (y.float() - ref.float()).abs()
+    assert err.max().item() < 3e-2 * ref.float().abs().max().item(), err.max().item()
+    assert _rel(y.float(), ref.float()) < 4e-3, _rel(y.float(), ref.float())
+    s32 = torch.bmm(a.transpose(0, 1).float(), t.float().transpose(1, 2))
+    ref32 = torch.bmm(torch.softmax(s32, dim=-1), t.float()).transpose(0, 1)
+    assert _rel(y.float(), ref32) < 1e-2, _rel(y.float(), ref32)
+    # a strided (R, H, C) view of the same values gives the same result
+    a2 = a.transpose(0, 1).contiguous().transpose(0, 1)
+    y2 = torch.empty_like(y)
+    _native.call("ov3d_attnpool_fused", x, t0, pos, a2, a2.stride(0), a2.stride(1), R, ntok, C, H,
+                 y2, like=x)
+    assert torch.equal(y2, y)
+
+
+def test_attnpool_fused_module_equals_token_path(cuda):
+    """RegionCLIP._attnpool through the fused launch vs through the token rows (RN50x4 pool
+    shapes: 81 tokens, 2560 channels, 40 heads)."""
+    from ov3d_amd import regionclip as rc
+    m, _ = rc.build_regionclip(compute_dtype=torch.bfloat16)
+    m = m.to(cuda)
+    g = torch.Generator(device=cuda).manual_seed(4)
+    x = torch.randn(24, 9, 9, 2560, device=cuda, generator=g).relu().to(torch.bfloat16)
+    assert m._fused_pool_ok(x)
+    got = m._attnpool(x)
+    ref = m._pool_tokens(m._tokens(x))
+    cos = torch.nn.functional.cosine_similarity(got, ref, dim=-1)
+    assert cos.min().item() > 0.9999, cos.min().item()
+    assert _rel(got, ref) < 1e-2
+
+
 @pytest.mark.parametrize("M,N,K,relu", [(4 * 81, 2560, 640, 1), (1000, 256, 64, 0)])
 def test_lt_gemm_bias_residual_matches_fp32(cuda, M, N, K, relu):
     """conv3 + bottleneck close as one hipBLASLt matmul vs the fp32 formula (bf16 output:
