@@ -257,10 +257,12 @@ def index_kernel_rates(batch, npoint=2048, radius=0.2, nsample=64, L=8, Q=128, r
     # reported as microseconds per sampling iteration against its latency floor ("fps" below),
     # not as a byte rate
     rows = {
-        "ov3d_ball_query": (lambda: pu.ball_query(radius, nsample, xyz, new_xyz), scanned * 12,
-                            f"r={radius} S={nsample}: 12 B per point actually scanned "
-                            f"({scanned} points over the B*M centroids: each scan stops at the "
-                            f"S-th in-radius point, SURVEY Appendix A.2)"),
+        "ov3d_ball_query": (lambda: pu.ball_query(radius, nsample, xyz, new_xyz),
+                            B * N * 12 + B * npoint * nsample * 4,
+                            f"r={radius} S={nsample}: the scene's points read from HBM once (B*N*12 B) + "
+                            f"the indices written (B*M*S*4 B); the scans themselves ({scanned} points "
+                            f"over the B*M centroids, each stopping at the S-th in-radius point, SURVEY "
+                            f"Appendix A.2) re-read the L2-resident scene: see scan_points_per_s"),
         "ov3d_group_fwd": (lambda: grouper.rows(xyz, new_xyz, None, idx=idx),
                            B * npoint * nsample * (3 * 4 + 4),
                            "(B,M,S,3) fp32 rows out + idx in"),
@@ -274,6 +276,12 @@ def index_kernel_rates(batch, npoint=2048, radius=0.2, nsample=64, L=8, Q=128, r
         ms = _timed(fn, reps)
         out[name] = {"ms": round(ms, 4), "alg_bytes": nbytes, "GBps": round(nbytes / (ms * 1e-3) / 1e9, 1),
                      "frac_hbm": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "bytes": what}
+    # ball query is bound by the distance tests over the L2-resident scene, not by HBM: the
+    # reference scan's point count per second (points each centroid's scan reads until its S-th
+    # hit) is its throughput figure
+    bq = out["ov3d_ball_query"]
+    bq["scanned_points"] = scanned
+    bq["scan_points_per_s"] = round(scanned / (bq["ms"] * 1e-3), 1)
     return out
 
 

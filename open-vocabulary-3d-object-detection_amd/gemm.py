@@ -329,6 +329,9 @@ def _linear(x, w, b):
         return rows_gemm(x, w, b, trans_b=True)
     if _tile_gemm_ok(x, w, True):
         return tile_gemm(x, w, b, trans_b=True)
+    if x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and gemm256_ok(x, w):
+        # K % 64 != 0 (the masked encoder's interim SA: 256 features + xyz padded to 264)
+        return gemm256(x, w, bias=b)
     return torch.nn.functional.linear(x, w, b)
 
 
@@ -353,6 +356,10 @@ def _dgrad(dy, w):
         return rows_gemm(dy, w, trans_b=False)
     if _tile_gemm_ok(dy, w, False):
         return tile_gemm(dy, w, trans_b=False)
+    if dy.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and dy.shape[0] > ROWS_GEMM_MAX_M:
+        wt = w.t().contiguous()   # (K, N) rows: dx = dy wt^T on the tile kernel
+        if gemm256_ok(dy, wt):
+            return gemm256(dy, wt)
     return dy @ w
 
 

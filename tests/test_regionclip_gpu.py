@@ -34,9 +34,15 @@ def _boxes(rng, n, H, W):
 
 @pytest.mark.parametrize("dtype,C,H,W,R,per,nimg", [(torch.float32, 64, 33, 45, 40, 10, 4),
                                                     (torch.bfloat16, 128, 33, 45, 48, 12, 2),
-                                                    (torch.float32, 8, 7, 5, 16, 4, 4)])
-def test_roi_align_bit_exact(cuda, dtype, C, H, W, R, per, nimg):
+                                                    (torch.float32, 8, 7, 5, 16, 4, 4),
+                                                    # LDS-window form: 16-ROI groups, a partial one
+                                                    (torch.bfloat16, 64, 33, 45, 80, 40, 2),
+                                                    # windows past 1536 pixels: global reads
+                                                    (torch.bfloat16, 32, 40, 45, 20, 20, 1)])
+@pytest.mark.parametrize("lds", ["0", "1"])
+def test_roi_align_bit_exact(cuda, monkeypatch, dtype, C, H, W, R, per, nimg, lds):
     from ov3d_amd import _native
+    monkeypatch.setenv("OV3D_ROI_LDS", lds)   # the LDS-window form of the fused pool (bf16)
     rng = np.random.default_rng(C + R)
     feat = torch.from_numpy(rng.standard_normal((nimg, H, W, C)).astype(np.float32)).to(dtype)
     boxes = _boxes(rng, R, H * 16, W * 16)
