@@ -497,35 +497,6 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
             // the previous tile's drop word goes out while the score MFMAs run: the lane
             // transpose's swizzle round trips would otherwise sit on this tile's critical path
             if (DROP && !BITS && kb > kbeg && active) store_drop(kb - KB);
-            // the tile's dropout masks before its scores are back: the hash needs only the query
-            // and key indices, so its ~160 vector instructions (16 independent chains) issue while
-            // the score MFMAs are in flight instead of after the row max (round 4 ran them in the
-            // softmax loop, behind the rescale branch)
-            const short ts = (short)((int)a.thresh - 32768);
-            const s16x2 tsig = {ts, ts};
-            uint32_t dw = 0;   // this lane's drop word of the tile
-            uint32_t dmk[16];
-            if (DROP && !BITS) {
-                const uint32_t hb = qh + (uint32_t)(kb >> 1) * kPairMul;
-#pragma unroll
-                for (int t = 0; t < 2; ++t)
-#pragma unroll
-                    for (int i = 0; i < 16; i += 2) {
-                        // key 32t + (i&3) + 8(i>>2) + 4h (even): pair 16t + (i&3)/2 + 4(i>>2) + 2h
-                        const uint32_t c = 16 * t + ((i & 3) >> 1) + 4 * (i >> 2);
-                        const uint32_t dm = drop_halves(drop_mix(hb + c * kPairMul), tsig);
-                        const int jb = 8 * t + (i >> 1);
-                        dmk[jb] = dm;
-                        dw |= dm & ((1u << jb) | (1u << (16 + jb)));
-                    }
-                // pin the masks here: left alone, hipcc sinks the hash past the rescale branch into
-                // the softmax loop (its only use), behind the score MFMAs' results again
-                // (not in the masked form: its mask words take the registers, and it spilled)
-                if constexpr (!MASK) {
-#pragma unroll
-                    for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(dmk[j]));
-                }
-            }
             PROBE(1);
             // keys past Lk (last partial tile) do not take part
             const int nvalid = kend - kb;
@@ -570,6 +541,10 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
             // p = exp2(S - mb), one bf16 pack per key pair; dropout zeroes p after the row sum.
             // Scalar f32 ops on purpose: packed v_pk_* issue slower than two scalar ops beside
             // the MFMAs (MI355X_MICROARCH.md cycle table; the file is built with -fno-slp-vectorize)
+            const uint32_t hb = qh + (uint32_t)(kb >> 1) * kPairMul;
+            const short ts = (short)((int)a.thresh - 32768);
+            const s16x2 tsig = {ts, ts};
+            uint32_t dw = 0;   // this lane's drop word of the tile
             u32x4 pw[2][2], praw[2][2];
 #pragma unroll
             for (int t = 0; t < 2; ++t)
@@ -589,8 +564,13 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
                         const s16x2 kh = __builtin_bit_cast(s16x2, kwin << (15 - jb));
                         pk &= __builtin_bit_cast(uint32_t, (s16x2)(kh >> (s16x2){15, 15}));
                     } else if (DROP) {
+                        // key 32t + (i&3) + 8(i>>2) + 4h (even): pair 16t + (i&3)/2 + 4(i>>2) + 2h
+                        const uint32_t c = 16 * t + ((i & 3) >> 1) + 4 * (i >> 2);
+                        const uint32_t dm = drop_halves(drop_mix(hb + c * kPairMul), tsig);
                         // 1/(1-p) is applied once to the output (keep_scale below)
-                        pk &= ~dmk[8 * t + (i >> 1)];
+                        pk &= ~dm;
+                        const int jb = 8 * t + (i >> 1);
+                        dw |= dm & ((1u << jb) | (1u << (16 + jb)));
                     }
                     pw[t][i >> 3][(i & 7) >> 1] = pk;
                 }

@@ -325,6 +325,19 @@ def _side_stream(device):
     return s
 
 
+_BUDGET = {}
+
+
+def _im2col_budget(device):
+    """the column-buffer budget: IM2COL_CHUNK_BYTES, at most an eighth of the device's memory
+    (two buffers are live when the chunks overlap; the caching allocator keeps them)"""
+    b = _BUDGET.get(device)
+    if b is None:
+        total = torch.cuda.get_device_properties(device).total_memory
+        b = _BUDGET[device] = min(IM2COL_CHUNK_BYTES, total // 8)
+    return b
+
+
 def _conv3x3(x, w, b, stride=1):
     """3x3 conv (pad 1) + bias + ReLU on NHWC: HIP im2col of a chunk of images / ROIs,
     then one hipBLASLt GEMM with the ReLU epilogue writing the chunk's output rows; with
@@ -338,7 +351,7 @@ def _conv3x3(x, w, b, stride=1):
         return gemm.conv3x3_gemm256(x, w, bias=b, relu=True)
     out = torch.empty((N, Ho, Wo, cout), dtype=x.dtype, device=x.device)
     per_img = Ho * Wo * kpad * x.element_size()
-    step = max(1, IM2COL_CHUNK_BYTES // per_img)
+    step = max(1, _im2col_budget(x.device) // per_img)
     starts = list(range(0, N, step))
     overlap = CONV_OVERLAP and len(starts) > 1
     cols = [torch.empty((min(step, N) * Ho * Wo, kpad), dtype=x.dtype, device=x.device)
