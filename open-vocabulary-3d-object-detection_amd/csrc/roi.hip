@@ -169,22 +169,33 @@ __global__ void __launch_bounds__(256) roi_align_kernel(
 // path's nn.AvgPool2d(2) over the ROIAlign output, torch's arithmetic as ov3d_avgpool2_nhwc:
 // fp32 (((0 + b00) + b01) + b10) + b11 of the rounded bins, / 4) written beside them, so the
 // pool does not read the (R, P, P, C) output back.  P even, 32-bit indices.
+// affine (grid % 8 == 0, R % per_image == 0, (R / per_image) % nimages == 0): image-affine XCD
+// order.  Workgroup b runs on XCD b % 8 (the dispatcher's round robin; an assumption for speed
+// only, any placement is correct): work item L = (b >> 3) + (b & 7) * (grid / 8), items ordered
+// image-major, so each XCD's L2 serves the ROIs of one image (a 45 x 33 x 1280 bf16 res4 map is
+// 3.8 MB) instead of all of them (the gathers of a whole-map ROI re-read its image ~75 times).
 template <typename T, int VEC>
 __global__ void __launch_bounds__(256) roi_align_pool2_kernel(
     const T* __restrict__ feat, int H, int W, int C, const float* __restrict__ boxes, int R,
     int per_image, int nimages, float scale, int P, int sampling_ratio, int aligned,
-    T* __restrict__ out, T* __restrict__ pooled) {
+    T* __restrict__ out, T* __restrict__ pooled, int affine) {
     static_assert(VEC * sizeof(T) == 16, "one 16-byte channel run per thread");
     const int CV = C / VEC, P2 = P / 2;
     const int total = R * P2 * P2 * CV;
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = affine ? (blockIdx.x >> 3) + (blockIdx.x & 7) * (gridDim.x >> 3) : blockIdx.x;
+    const int t = b * blockDim.x + threadIdx.x;
     if (t >= total) return;
     const int cv = t % CV;
     int q = t / CV;
     const int pw2 = q % P2;
     q /= P2;
     const int ph2 = q % P2;
-    const int r = q / P2;
+    int r = q / P2;
+    if (affine) {   // image-major rank -> ROI: image i owns runs i, i + nimages, ...
+        const int per_img_rois = R / nimages, i = r / per_img_rois, rem = r - i * per_img_rois;
+        const int k = rem / per_image;
+        r = (i + k * nimages) * per_image + (rem - k * per_image);
+    }
     const int img = (r / per_image) % nimages;
     const T* f = feat + (size_t)img * H * W * C + cv * VEC;
     float psum[VEC];
@@ -449,14 +460,22 @@ extern "C" int ov3d_roi_align_pool2_fwd(const void* feat, int is_bf16, int N, in
         roi_align_pool2_lds_kernel<<<grid, 512, 0, s>>>(
             (const bf16*)feat, H, W, C, boxes, R, per_image, nimages, spatial_scale, pooled,
             sampling_ratio, aligned, (int)nwork, (bf16*)out, (bf16*)pooled_out);
-    } else if (is_bf16)
-        roi_align_pool2_kernel<bf16, 8><<<blocks, 256, 0, s>>>(
-            (const bf16*)feat, H, W, C, boxes, R, per_image, nimages, spatial_scale, pooled,
-            sampling_ratio, aligned, (bf16*)out, (bf16*)pooled_out);
-    else
-        roi_align_pool2_kernel<float, 4><<<blocks, 256, 0, s>>>(
-            (const float*)feat, H, W, C, boxes, R, per_image, nimages, spatial_scale, pooled,
-            sampling_ratio, aligned, (float*)out, (float*)pooled_out);
+    } else {
+        // image-affine XCD order, opt-in (OV3D_ROI_AFFINE=1; read per call): measured no gain at C5
+        // (51.2 vs 50.9 ms median, profiles/r05_c5_roi_affine_ab.json)
+        const int aff_env = getenv("OV3D_ROI_AFFINE") ? atoi(getenv("OV3D_ROI_AFFINE")) : 0;
+        const int affine = aff_env && R % per_image == 0 && (R / per_image) % nimages == 0 &&
+                           (long long)(blocks + 7) / 8 * 8 * 256 <= 0x7fffffffLL;
+        const int grid = affine ? (blocks + 7) / 8 * 8 : blocks;
+        if (is_bf16)
+            roi_align_pool2_kernel<bf16, 8><<<grid, 256, 0, s>>>(
+                (const bf16*)feat, H, W, C, boxes, R, per_image, nimages, spatial_scale, pooled,
+                sampling_ratio, aligned, (bf16*)out, (bf16*)pooled_out, affine);
+        else
+            roi_align_pool2_kernel<float, 4><<<grid, 256, 0, s>>>(
+                (const float*)feat, H, W, C, boxes, R, per_image, nimages, spatial_scale, pooled,
+                sampling_ratio, aligned, (float*)out, (float*)pooled_out, affine);
+    }
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

@@ -175,14 +175,16 @@ class _SAMLPPool(Function):
         world = [dist.get_world_size(g) if g is not None else 1 for g in groups]
         x0 = x0.contiguous()
         bf = torch.bfloat16
-        # z1 is kept for the backward only when that does not recompute it (sa_dy2_fused), and
-        # then y1 is not stored either: every consumer recomputes it from x0 (12 B per row
-        # instead of 128 B: the (R, 64) first-layer output never reaches HBM)
-        fused_bwd2 = FUSED_BWD and cin == 3 and c1 == 64 and c2 == 128 and \
+        # z1 is kept for the backward only when that does not recompute it (sa_dy2_fused); with
+        # the 3 xyz inputs y1 is not stored either: every consumer recomputes it from x0 (12 B
+        # per row instead of 128 B: the (R, 64) first-layer output never reaches HBM).  With
+        # colour (ScanNet, cin = 6) y1 is stored and sa_dy2_fused reads it.
+        fused_bwd2 = FUSED_BWD and c1 == 64 and c2 == 128 and \
             bool(nat.load().ov3d_sa_dy_fused_supported(c2, w3.shape[0]))
+        recompute_y1 = fused_bwd2 and cin == 3
         w1f = w1.float().contiguous()
         # layer 1 (statistics only when y1 is recomputed)
-        y1 = None if fused_bwd2 else torch.empty((R, c1), dtype=bf, device=dev)
+        y1 = None if recompute_y1 else torch.empty((R, c1), dtype=bf, device=dev)
         parts = torch.empty((NPARTS_ROWS, 2, c1), dtype=torch.float64, device=dev)
         nat.call("ov3d_sa_l1_fwd_cin", x0, cin, w1f, R, c1, y1, parts, NPARTS_ROWS, like=x0)
         st1 = _bn_stats(parts, NPARTS_ROWS, c1, groups[0], R * world[0], bns[0])
@@ -191,7 +193,7 @@ class _SAMLPPool(Function):
         z1 = None if fused_bwd2 else torch.empty((R, c1), dtype=bf, device=dev)
         y2 = torch.empty((R, c2), dtype=bf, device=dev)
         parts = torch.empty((NPARTS_LAYER, 2, c2), dtype=torch.float64, device=dev)
-        if fused_bwd2:
+        if recompute_y1:
             nat.call("ov3d_sa_layer_fwd_x0", x0, w1f, st1[2], st1[3], w2b, R, c1, c2, y2, parts,
                      NPARTS_LAYER, like=x0)
         else:

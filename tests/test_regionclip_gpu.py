@@ -39,10 +39,11 @@ def _boxes(rng, n, H, W):
                                                     (torch.bfloat16, 64, 33, 45, 80, 40, 2),
                                                     # windows past 1536 pixels: global reads
                                                     (torch.bfloat16, 32, 40, 45, 20, 20, 1)])
-@pytest.mark.parametrize("lds", ["0", "1"])
-def test_roi_align_bit_exact(cuda, monkeypatch, dtype, C, H, W, R, per, nimg, lds):
+@pytest.mark.parametrize("lds,affine", [("0", "1"), ("0", "0"), ("1", "1")])
+def test_roi_align_bit_exact(cuda, monkeypatch, dtype, C, H, W, R, per, nimg, lds, affine):
     from ov3d_amd import _native
-    monkeypatch.setenv("OV3D_ROI_LDS", lds)   # the LDS-window form of the fused pool (bf16)
+    monkeypatch.setenv("OV3D_ROI_LDS", lds)         # the LDS-window form of the fused pool (bf16)
+    monkeypatch.setenv("OV3D_ROI_AFFINE", affine)   # image-affine XCD order of the global form
     rng = np.random.default_rng(C + R)
     feat = torch.from_numpy(rng.standard_normal((nimg, H, W, C)).astype(np.float32)).to(dtype)
     boxes = _boxes(rng, R, H * 16, W * 16)
