@@ -490,6 +490,46 @@ int ov3d_linres_fwd(long long R, int K, const void* x, long long ldx, const void
                     float* s, float* mean, float* rstd, void* xa, void* xap, void* xb, int xb_bf16,
                     long long xb_inner, long long xb_s0, long long xb_s1, void* stream);
 
+/* LayerNorm boundary + the adjacent row GEMM in one launch (csrc/lngemm.hip), the decoder's
+ * short row blocks [models/transformer.py TransformerDecoderLayer.forward_pre 355-379].
+ * ov3d_lngemm_fwd: the ov3d_resnorm_fwd row pass (same arguments and outputs; C = 256, y bf16
+ * or null, mean / rstd / ga / ba required) followed by out_i = epi(xsel_i W_i^T + bias_i) for
+ * nprob <= 2 problems over the same rows (sel 0: xa, 1: xap; W_i (N_i, 256) bf16 rows,
+ * N_i % 128 == 0; epilogue 0 none, 1 dropout_p2(relu(.)) with seed2 / site2 as
+ * ov3d_rows_gemm_act).  ov3d_lngemm_bwd: the ov3d_resnorm_bwd row pass (dy bf16 required,
+ * partials (ov3d_lngemm_bwd_parts(R), 4, 256) as resnorm_bwd's per-8-row blocks; the column
+ * sums are left to ov3d_colsum_group) followed by dx = epi(dy W) for W (256, N) rows (the
+ * branch linear's weight; epilogue 0 none, 2 the FFN mask h > 0 ? . / (1 - p2) : 0).
+ * R % 32 == 0; the outputs equal the two-launch path's (resnorm + rows GEMM). */
+typedef struct {
+    const void* W;
+    long long ldw;
+    const void* bias;
+    void* out;
+    long long ldo;
+    int N;
+    int sel;
+} ov3d_lngemm_problem;
+int ov3d_lngemm_supported(int R, int C, int N);
+int ov3d_lngemm_fwd(int R, const void* src, int src_bf16, const void* y, float dropout_p,
+                    const int64_t* seed, int site, const float* ga, const float* ba,
+                    const void* pos, int pos_bf16, const float* gb, const float* bb, float eps,
+                    float* s, float* mean, float* rstd, void* xa, void* xap, void* xb, int xb_bf16,
+                    long long xb_inner, long long xb_s0, long long xb_s1, int nprob,
+                    const ov3d_lngemm_problem* probs, int epilogue, float dropout_p2,
+                    const int64_t* seed2, int site2, void* stream);
+int ov3d_lngemm_bwd_parts(int R);
+/* measurement only: ov3d_lngemm_fwd launches after this write 5 per-wave phase clocks
+ * (s_memtime) into buf, 8 words a wave; NULL disarms */
+int ov3d_lngemm_stamps_arm(void* buf);
+int ov3d_lngemm_bwd(int R, const float* s, const float* mean, const float* rstd, const float* ds,
+                    const void* dxa, const void* dxap, const void* dxb, int dxb_bf16,
+                    long long dxb_inner, long long dxb_s0, long long dxb_s1, const float* ga,
+                    const float* gb, float dropout_p, const int64_t* seed, int site, float* dsrc,
+                    void* dy, void* dpos, int dpos_bf16, float* partials, int accumulate,
+                    const void* W, long long ldw, int N, int epilogue, float dropout_p2,
+                    const void* H, long long ldh, void* dx, long long lddx, void* stream);
+
 /* ---- Flash attention (head_dim 64, bf16, no mask) ----
  * Replaces the nn.MultiheadAttention core of models/transformer.py:223,271 (encoder
  * self-attention) and :307-308,365-372 (decoder self / cross attention): per head

@@ -124,6 +124,8 @@ _SIGS = {
     "ov3d_gemm256_pair": "pplpplppippliiip",
     "ov3d_gemm256_batched": "pllpllpliplliiiiip",
     "ov3d_linres_fwd": "liplplppifpipppippfppppppilllp",
+    "ov3d_lngemm_fwd": "ipipfpipppippfppppppilllipifpip",
+    "ov3d_lngemm_bwd": "ipppppppilllppfpipppipipliifplplp",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
                           "ov3d_attn_dropbits_words", "ov3d_attn_maskbits_words", "ov3d_fps_workspace", "ov3d_attn_small_bwd", "ov3d_set_loss_fwd_parts",
@@ -135,7 +137,8 @@ EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_
                           "ov3d_tile_gemm_supported", "ov3d_sun_range_parts", "ov3d_heads_out_max_text",
                           "ov3d_heads_out_workspace", "ov3d_stamps_arm", "ov3d_stamps_count",
                           "ov3d_stamps_get", "ov3d_wall_clock_khz", "ov3d_linres_supported",
-                          "ov3d_attnpool_fused_supported")
+                          "ov3d_attnpool_fused_supported", "ov3d_lngemm_supported",
+                          "ov3d_lngemm_bwd_parts", "ov3d_lngemm_stamps_arm")
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_longlong, "f": ctypes.c_float,
        "d": ctypes.c_double}
@@ -210,6 +213,12 @@ def load():
         lib.ov3d_linres_supported.restype = ctypes.c_int
         lib.ov3d_attnpool_fused_supported.argtypes = [ctypes.c_int] * 3
         lib.ov3d_attnpool_fused_supported.restype = ctypes.c_int
+        lib.ov3d_lngemm_supported.argtypes = [ctypes.c_int] * 3
+        lib.ov3d_lngemm_supported.restype = ctypes.c_int
+        lib.ov3d_lngemm_bwd_parts.argtypes = [ctypes.c_int]
+        lib.ov3d_lngemm_bwd_parts.restype = ctypes.c_int
+        lib.ov3d_lngemm_stamps_arm.argtypes = [ctypes.c_void_p]
+        lib.ov3d_lngemm_stamps_arm.restype = ctypes.c_int
         lib.ov3d_heads_out_workspace.argtypes = [ctypes.c_int] * 2
         lib.ov3d_heads_out_workspace.restype = ctypes.c_longlong
         lib.ov3d_version.argtypes = []

@@ -71,6 +71,13 @@ class _RgProblem(ctypes.Structure):
                 ("ldc", ctypes.c_longlong), ("N", ctypes.c_int), ("K", ctypes.c_int)]
 
 
+class _LnProblem(ctypes.Structure):
+    """mirror of ov3d_lngemm_problem (include/ov3d.h)"""
+    _fields_ = [("W", ctypes.c_void_p), ("ldw", ctypes.c_longlong), ("bias", ctypes.c_void_p),
+                ("out", ctypes.c_void_p), ("ldo", ctypes.c_longlong), ("N", ctypes.c_int),
+                ("sel", ctypes.c_int)]
+
+
 def rows_gemm_group(problems, trans_b=True):
     """[(a, w, bias)] over the same rows -> [outputs], one launch (every pair must pass
     _rows_gemm_ok; at most 4)"""

@@ -150,9 +150,11 @@ class _ResNorm(torch.autograd.Function):
         return (None,) + _bwd_core(ctx, ds, dxa, dxap, dxb, ctx.needs_input_grad)
 
 
-def _bwd_core(ctx, ds, dxa, dxap, dxb, need):
+def _bwd_core(ctx, ds, dxa, dxap, dxb, need, fused=None):
     """the resnorm backward launch; need = needs_input_grad over (meta, src, y, pos, ga, ba,
-    gb, bb) -> (dsrc, dy, dpos, dga, dba, dgb, dbb) (views of the forward's shapes)"""
+    gb, bb) -> (dsrc, dy, dpos, dga, dba, dgb, dbb) (views of the forward's shapes).
+    fused = (w, relu_p, h, dx): the branch y = h w^T + b's input gradient dx = epi(dy w) is
+    computed in the same launch (csrc/lngemm.hip) into dx; dy is then always produced."""
     p, site, R, C, shape, src_dt, y_dt, pos_dt = ctx.meta
     s, mean, rstd, ga, gb = ctx.saved_tensors[:5]
     dev = s.device
@@ -220,11 +222,23 @@ def _bwd_core(ctx, ds, dxa, dxap, dxb, need):
         if ret_nb:
             nb_ret, nb_fan.bufs = nb_fan.bufs, None
     lib = _native.load()
-    nparts = lib.ov3d_resnorm_bwd_parts(R, C)
+    nparts = lib.ov3d_lngemm_bwd_parts(R) if fused is not None else lib.ov3d_resnorm_bwd_parts(R, C)
     partials = torch.empty((nparts, 4, C), dtype=torch.float32, device=dev) \
         if (has_a or has_b) else None
     seed = ctx.seed if (p > 0 and dy is not None) else None
-    if dsrc is not None or dy is not None or dpos is not None or has_a or has_b:
+    if fused is not None:
+        w, relu_p, h, dx = fused
+        if dy is None:
+            dy = torch.empty((R, C), dtype=torch.bfloat16, device=dev)
+        seed = ctx.seed if p > 0 else None
+        _native.call("ov3d_lngemm_bwd", R, s, mean, rstd, ds, dxa, dxap, dxb, _dt_flag(dxb),
+                     *xb_map, ga, gb, float(p), seed, site, dsrc, dy, dpos, _dt_flag(dpos),
+                     partials, acc, w, w.stride(0), w.shape[1], 2 if relu_p is not None else 0,
+                     float(relu_p or 0.0), h, h.stride(0) if h is not None else 0, dx, dx.stride(0),
+                     like=s)
+        if not slots and (dga is not None or dba is not None or dgb is not None or dbb is not None):
+            _colsums(partials, nparts, C, (dga, dba, dgb, dbb), acc)
+    elif dsrc is not None or dy is not None or dpos is not None or has_a or has_b:
         _native.call("ov3d_resnorm_bwd", R, C, s, mean, rstd, ds, dxa, dxap, dxb, _dt_flag(dxb),
                      *xb_map, ga, gb,
                      float(p) if dy is not None else 0.0, seed, site, dsrc, dy, _dt_flag(dy),
@@ -242,6 +256,275 @@ def _bwd_core(ctx, ds, dxa, dxap, dxb, need):
     if defer_norm:
         dga = dba = dgb = dbb = None
     return v(dsrc), v(dy), v(dpos), dga, dba, dgb, dbb
+
+
+def _colsums(partials, nparts, C, outs, acc):
+    """LayerNorm parameter gradients (dga, dba, dgb, dbb) from (nparts, 4, C) partials in
+    one ov3d_colsum_group launch (the fixed summation order of resnorm_bwd's own column
+    pass); acc bits 2 / 4: add into dga / dba, dgb / dbb (gradient fan-in)."""
+    from .gemm import _ColSeg, _ColOut
+    import ctypes
+    tmp = torch.empty((4, C), dtype=torch.float32, device=partials.device)
+    segs = (_ColSeg * 4)(*[_ColSeg(partials.data_ptr(), nparts, k) for k in range(4)])
+    oa = (_ColOut * 4)(*[_ColOut(tmp[k].data_ptr(), k, 1) for k in range(4)])
+    _native.call("ov3d_colsum_group", ctypes.addressof(segs), 4, ctypes.addressof(oa), 4, C,
+                 like=partials)
+    for k, o in enumerate(outs):
+        if o is None:
+            continue
+        if acc & (2 if k < 2 else 4):
+            o.add_(tmp[k])
+        else:
+            o.copy_(tmp[k])
+
+
+class _RowsLinearMask(torch.autograd.Function):
+    """y = h w^T + b for the FFN's linear2 whose input h = dropout_p(relu(.)) came from a
+    relu-drop epilogue (LinY with relu_p): the input gradient takes the activation mask in
+    its epilogue (dx = h > 0 ? dy w / (1 - p) : 0), the convention of _FFN1 / _LnGemm."""
+
+    @staticmethod
+    def forward(ctx, h, w, b, relu_p):
+        bf = torch.bfloat16
+        hr = h.reshape(-1, h.shape[-1])
+        wc, bc = gemm.cast_param(w, bf), gemm.cast_param(b, bf)
+        with torch.autocast("cuda", enabled=False):
+            y = gemm.act_gemm(hr, wc, _bias(bc), True)
+        ctx.save_for_backward(hr, wc)
+        ctx.params = (w, b)
+        ctx.meta = (h.shape, float(relu_p))
+        return y.view(*h.shape[:-1], wc.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        hr, wc = ctx.saved_tensors
+        w, b = ctx.params
+        hshape, relu_p = ctx.meta
+        need = ctx.needs_input_grad
+        dyr = dy.reshape(-1, wc.shape[0]).to(torch.bfloat16).contiguous()
+        with torch.autocast("cuda", enabled=False):
+            dx = gemm.act_gemm(dyr, wc, None, False, 2, relu_p, h=hr).view(hshape) \
+                if need[0] else None
+            dw, db = gemm.linear_weight_grads(dyr, hr, w, b, need[1], b is not None and need[2])
+        return dx, dw, db, None
+
+
+# LayerNorm boundary + the following row GEMM in one launch each way (csrc/lngemm.hip), the
+# decoder's sub-layer boundaries; OV3D_LNGEMM=0: the resnorm + rows-GEMM launches
+lngemm = os.environ.get("OV3D_LNGEMM", "1") != "0"
+
+
+class _LnGemm(torch.autograd.Function):
+    """resnorm(Pending(src, y, p, site)) feeding a linear layer directly:
+        s = src + dropout_p(y);  xa = norm_a(s);  xap = xa + pos;  xb = norm_b(s)
+        out_i = epi(xsel_i W[r0_i:r1_i]^T + b[r0_i:r1_i])       (xsel: xa or xap)
+    y is a LinY (x w_y^T + b_y, computed here by a rows GEMM launch, its input gradient then
+    fused into the resnorm backward launch) or a bf16 tensor or None.  The outputs are s, xb
+    (None unless norm_b) and the out_i; xa / xap stay internal (saved for the backward).
+    Forward: [y GEMM] + ONE lngemm launch; backward: the out_i input gradients (one rows-GEMM
+    launch) + ONE lngemm launch (resnorm backward + dx of y's linear) — the two-launch
+    resnorm / GEMM pairs of models/transformer.py:355-379's boundaries each become one."""
+
+    @staticmethod
+    def forward(ctx, meta, src, yx, yw, yb, pos, ga, ba, gb, bb, gw, gbias):
+        p, site, eps, shape, fans, xb_into, relu_p, spec, epi = meta
+        bf = torch.bfloat16
+        C = shape[-1]
+        R = 1
+        for d in shape[:-1]:
+            R *= d
+        dev = ga.device
+        lin = yw is not None
+        ywc = gemm.cast_param(yw, bf) if lin else None
+        if lin:
+            yr = yx.reshape(-1, yx.shape[-1])
+            with torch.autocast("cuda", enabled=False):
+                y = gemm.act_gemm(yr, ywc, _bias(gemm.cast_param(yb, bf)), True)
+        else:
+            yr = None
+            y = _rows(yx, C).to(bf).contiguous() if yx is not None else None
+        srcr, posr = _rows(src, C), _rows(pos, C)
+        s = torch.empty((R, C), dtype=torch.float32, device=dev)
+        mean = torch.empty(R, dtype=torch.float32, device=dev)
+        rstd = torch.empty(R, dtype=torch.float32, device=dev)
+        use_a = any(sel == 0 for sel, _, _ in spec)
+        use_ap = any(sel == 1 for sel, _, _ in spec)
+        xa = torch.empty((R, C), dtype=bf, device=dev) if use_a else None
+        xap = torch.empty((R, C), dtype=bf, device=dev) if use_ap else None
+        want_b = gb is not None
+        xb_map = (0, 0, 0)
+        if want_b and xb_into is not None:
+            out, l = xb_into
+            xb = out[l]
+            xb_map = (shape[1], C, shape[0] * C)
+        else:
+            xb = torch.empty((R, C), dtype=torch.float32, device=dev) if want_b else None
+        gwc, gbc = gemm.cast_param(gw, bf), gemm.cast_param(gbias, bf)
+        outs, probs = [], []
+        from .gemm import _LnProblem
+        import ctypes
+        for sel, r0, r1 in spec:
+            o = torch.empty((R, r1 - r0), dtype=bf, device=dev)
+            w_i = gwc[r0:r1]
+            b_i = gbc[r0:r1] if gbc is not None else None
+            outs.append(o)
+            probs.append(_LnProblem(w_i.data_ptr(), w_i.stride(0),
+                                    b_i.data_ptr() if b_i is not None else None,
+                                    o.data_ptr(), o.stride(0), r1 - r0, sel))
+        arr = (_LnProblem * len(probs))(*probs)
+        seed = flash._seed(dev) if (p > 0 or (epi is not None and epi[0] > 0)) else None
+        ep, esite = (float(epi[0]), int(epi[1])) if epi is not None else (0.0, 0)
+        _native.call("ov3d_lngemm_fwd", R, srcr, _dt_flag(srcr), y, float(p) if y is not None else 0.0,
+                     seed if p > 0 else None, site, ga, ba, posr, _dt_flag(posr), gb, bb, float(eps),
+                     s, mean, rstd, xa, xap, xb, _dt_flag(xb), *xb_map, len(probs),
+                     ctypes.addressof(arr), 1 if epi is not None else 0, ep,
+                     seed if ep > 0 else None, esite, like=s)
+        ctx.save_for_backward(s, mean, rstd, ga, gb, xa, xap, yr, ywc, gwc)
+        ctx.seed = seed
+        ctx.params = (ga, ba, gb, bb)
+        ctx.lin = (yw, yb, gw, gbias)
+        ctx.set_materialize_grads(False)
+        ctx.meta = (p if y is not None else 0.0, site, R, C, shape,
+                    src.dtype if src is not None else None, bf if y is not None else None,
+                    pos.dtype if pos is not None else None)
+        ctx.spec = spec
+        ctx.relu_p = relu_p
+        ctx.ydt = (yx.shape, yx.dtype) if yx is not None else None
+        ctx.fans = fans
+        v = lambda t: t.view(shape) if t is not None else None   # noqa: E731
+        xbo = xb.transpose(0, 1) if xb_map[0] else v(xb)
+        return (v(s), xbo) + tuple(o.view(*shape[:-1], o.shape[1]) for o in outs)
+
+    @staticmethod
+    def backward(ctx, ds, dxb, *douts):
+        s, mean, rstd, ga, gb, xa, xap, yr, ywc, gwc = ctx.saved_tensors
+        yw, yb, gw, gbias = ctx.lin
+        nig = ctx.needs_input_grad   # meta, src, yx, yw, yb, pos, ga, ba, gb, bb, gw, gbias
+        p, site, R, C, shape = ctx.meta[:5]
+        spec = ctx.spec
+        bf = torch.bfloat16
+        dev = s.device
+        with torch.autocast("cuda", enabled=False):
+            d = [dd.reshape(R, -1).to(bf).contiguous() if dd is not None else None for dd in douts]
+            # the linear's input gradients: dxa (sel 0 problems), dxap (sel 1), one launch
+            pairs = [(d[i], gwc[r0:r1], sel) for i, (sel, r0, r1) in enumerate(spec)
+                     if d[i] is not None]
+            dsel = {0: None, 1: None}
+            if len(pairs) > 1 and gemm._group_ok([(a, w) for a, w, _ in pairs], False) and \
+                    len({sel for _, _, sel in pairs}) == len(pairs):
+                for (_, _, sel), o in zip(pairs, gemm.rows_gemm_group(
+                        [(a, w, None) for a, w, _ in pairs], trans_b=False)):
+                    dsel[sel] = o
+            else:
+                for a, w, sel in pairs:
+                    o = gemm._dgrad(a, w)
+                    dsel[sel] = o if dsel[sel] is None else dsel[sel] + o
+            lin = ywc is not None
+            need_y = lin and (nig[2] or nig[3] or nig[4])
+            need = (False, nig[1], need_y or (not lin and nig[2]), nig[5], nig[6], nig[7], nig[8],
+                    nig[9])
+            dx = None
+            fused = None
+            if lin and nig[2]:
+                dx = torch.empty((R, ywc.shape[1]), dtype=bf, device=dev)
+                fused = (ywc, ctx.relu_p, yr if ctx.relu_p is not None else None, dx)
+            if dsel[0] is None and dsel[1] is None and dxb is None:
+                fused = None   # nothing reaches the norm: plain resnorm backward
+            dsrc, dy, dpos, dga, dba, dgb, dbb = _bwd_core(ctx, ds, dsel[0], dsel[1], dxb, need,
+                                                           fused=fused)
+            dyw = dyb = None
+            if lin:
+                dyr = dy.reshape(R, C) if dy is not None else None
+                if fused is None and nig[2] and dyr is not None:
+                    if ctx.relu_p is not None:
+                        dx = gemm.act_gemm(dyr, ywc, None, False, 2, ctx.relu_p, h=yr)
+                    else:
+                        dx = gemm._dgrad(dyr, ywc)
+                if dyr is not None and (nig[3] or (yb is not None and nig[4])):
+                    dyw, dyb = gemm.linear_weight_grads(dyr, yr, yw, yb, nig[3], nig[4])
+                dyx = dx.view(ctx.ydt[0]).to(ctx.ydt[1]) if dx is not None else None
+            else:
+                dyx = dy
+            # the linear's weight / bias gradients (row blocks of one weight, as _InProj)
+            dgw = dgbias = None
+            want_b = gbias is not None and nig[11]
+            if nig[10] or want_b:
+                items = [(d[i], xap if sel == 1 else xa, (r0, r1))
+                         for i, (sel, r0, r1) in enumerate(spec) if d[i] is not None]
+                if nig[10] and all(gemm.can_defer(x, gw, gbias if want_b else None)
+                                   for _, x, _ in items):
+                    for dd, x, rows in items:
+                        gemm.defer_weight_grad(dd, x, gw, gbias if want_b else None, rows=rows)
+                else:
+                    dgw = torch.zeros(gw.shape, dtype=torch.float32, device=dev) if nig[10] else None
+                    dgbias = torch.zeros(gbias.shape, dtype=torch.float32, device=dev) \
+                        if want_b else None
+                    for dd, x, (r0, r1) in items:
+                        if dgw is not None and gemm._fused_ok(dd, x):
+                            gemm.fused_weight_grad(dd, x, bias=dgbias is not None,
+                                                   out_w=dgw[r0:r1],
+                                                   out_b=dgbias[r0:r1] if dgbias is not None else None)
+                            continue
+                        if dgw is not None:
+                            gemm.weight_grad(dd, x, out=dgw[r0:r1])
+                        if dgbias is not None:
+                            torch.sum(dd, dim=0, dtype=torch.float32, out=dgbias[r0:r1])
+                    dgw = dgw.to(gw.dtype) if dgw is not None else None
+                    dgbias = dgbias.to(gbias.dtype) if dgbias is not None else None
+        return (None, dsrc, dyx, dyw, dyb, dpos, dga, dba, dgb, dbb, dgw, dgbias)
+
+
+def resnorm_gemm(pend, norm_a, w, b, spec, pos=None, norm_b=None, pos_fan=None, norm_b_fan=None,
+                 xb_into=None, epi=None):
+    """-> (s, xb, [out_i]) of _LnGemm, or None when the fused launches do not apply (the
+    caller then runs resnorm() and the linear layer).  spec: ((sel, r0, r1), ...) with sel
+    0 = norm_a(s), 1 = norm_a(s) + pos as the input of out_i = xsel W[r0:r1]^T + b[r0:r1];
+    epi = (p, site): out = dropout_p(relu(.)) (one problem)."""
+    src, y, p, psite = pend
+    if not (lngemm and enabled and src is not None and norm_a is not None and len(spec) <= 2):
+        return None
+    ref = src
+    shape = tuple(ref.shape)
+    C = shape[-1]
+    R = ref.numel() // C
+    lib = _native.load()
+    if not (ref.is_cuda and w.is_cuda and w.dim() == 2 and w.shape[1] == C
+            and all(lib.ov3d_lngemm_supported(R, C, r1 - r0) for _, r0, r1 in spec)):
+        return None
+    if any(sel == 1 for sel, _, _ in spec) and pos is None:
+        return None
+    if isinstance(y, LinY):
+        x = y.x
+        if not (x.dtype == torch.bfloat16 and tuple(y.w.shape) == (C, x.shape[-1])
+                and lib.ov3d_lngemm_supported(R, C, x.shape[-1])
+                and gemm.act_gemm_ok(x.reshape(-1, x.shape[-1]), gemm.cast_param(y.w, torch.bfloat16), True)):
+            return None
+        yx, yw, yb, relu_p = x, y.w, y.b, y.relu_p
+    else:
+        if y is not None and (tuple(y.shape) != shape or y.dtype != torch.bfloat16):
+            return None
+        yx, yw, yb, relu_p = y, None, None, None
+    eps = norm_a.eps
+    if norm_b is not None and norm_b.eps != eps:
+        return None
+    want_ap = any(sel == 1 for sel, _, _ in spec)
+    if not (fan_in and want_ap and pos is not None and pos.requires_grad):
+        pos_fan = None
+    if norm_b is None or not fan_in:
+        norm_b_fan = None
+    for fan in (pos_fan, norm_b_fan):
+        if fan is not None:
+            fan.n += 1
+    if norm_b is None or len(shape) != 3:
+        xb_into = None
+    meta = (float(p) if y is not None else 0.0, int(psite), eps, shape, (pos_fan, norm_b_fan),
+            xb_into, relu_p, tuple(spec), epi)
+    gb_ = norm_b.weight if norm_b is not None else None
+    bb_ = norm_b.bias if norm_b is not None else None
+    with torch.autocast("cuda", enabled=False):
+        r = _LnGemm.apply(meta, src, yx, yw, yb, pos if want_ap else None, norm_a.weight,
+                          norm_a.bias, gb_, bb_, w, b)
+    return r[0], r[1], list(r[2:])
 
 
 class _LinResNorm(torch.autograd.Function):
@@ -329,6 +612,9 @@ def linres_ok(y, C):
 def resolve(y):
     """a LinY branch computed on its own (rows GEMM); other values unchanged"""
     if isinstance(y, LinY):
+        if y.relu_p is not None:   # its gradient must carry the FFN mask (_RowsLinearMask)
+            with torch.autocast("cuda", enabled=False):
+                return _RowsLinearMask.apply(y.x, y.w, y.b, y.relu_p)
         return gemm.rows_linear(y.x, y.w, y.b)
     return y
 

@@ -85,14 +85,24 @@ class MultiheadAttention(nn.Module):
         return rows_linear(out, self.out_proj.weight, self.out_proj.bias)
 
 
-    def forward_kv(self, query, kv, idx, defer_out=False):
+    def attend(self, srcs, spec, L, S, defer_out=False):
+        """the flash path on already-projected rows (srcs / spec as attention.attention_packed:
+        the in-projection ran elsewhere, e.g. inside the norm's launch, resnorm.resnorm_gemm)"""
+        out = flash.attention_packed(srcs, spec, L, S, self.num_heads,
+                                     dropout_p=self.dropout if self.training else 0.0,
+                                     site=self.site)
+        return self._out(out, defer_out)
+
+    def forward_kv(self, query, kv, idx, defer_out=False, q=None):
         """Cross attention whose K / V projections of the memory were computed for all decoder
         layers at once (MemoryKV): kv = (K_all, V_all, dK_all, dV_all, token, token_grad),
-        this layer's block = columns idx*E .. (idx+1)*E."""
+        this layer's block = columns idx*E .. (idx+1)*E.  q: the query projection when it was
+        already computed (then `query` only gives the shape)."""
         L, B, E = query.shape
         K_all, V_all, dK, dV, token, tok_grad = kv
         S = K_all.shape[0]
-        q = in_projection(self.in_proj_weight, self.in_proj_bias, ((query, 0, E),))[0]
+        if q is None:
+            q = in_projection(self.in_proj_weight, self.in_proj_bias, ((query, 0, E),))[0]
         out = flash.attention_packed(
             [q, K_all, V_all], ((0, 0), (1, idx * E), (2, idx * E)), L, S, self.num_heads,
             dropout_p=self.dropout if self.training else 0.0, site=self.site,
@@ -341,6 +351,56 @@ class TransformerDecoderLayer(nn.Module):
     def fused_ok(self, x):
         return rn.supported(x, self.norm1, self.norm2, self.norm3)
 
+    def ln_ok(self, tgt, query_pos, tgt_mask, memory_mask, kv):
+        """forward_fused_ln applies: the fused boundary launches (csrc/lngemm.hip), flash
+        shapes, batched memory K / V, the FFN's ReLU, bf16 row widths the kernels take"""
+        sa, ca = self.self_attn, self.multihead_attn
+        E = sa.embed_dim
+        R = tgt.shape[0] * tgt.shape[1] if tgt.dim() == 3 else 0
+        if not (rn.lngemm and kv is not None and tgt_mask is None and memory_mask is None
+                and tgt.dim() == 3 and isinstance(self.activation, nn.ReLU)
+                and sa.in_proj_bias is not None and ca.in_proj_bias is not None
+                and self.linear1.bias is not None and self.linear2.bias is not None
+                and flash.supported(tgt, E, sa.num_heads, None)):
+            return False
+        lib = _native.load()
+        F = self.linear1.out_features
+        return all(lib.ov3d_lngemm_supported(R, E, n) for n in (E, 2 * E, 3 * E, F)) and \
+            self.linear2.out_features == E and self.linear1.in_features == E and \
+            bool(lib.ov3d_lngemm_supported(R, E, self.linear2.in_features))
+
+    def forward_fused_ln(self, pend, query_pos, kv, idx, pos_fan, norm_b=None, norm_b_fan=None,
+                         xb_into=None):
+        """bf16 step of the whole layer from the previous layer's Pending residual, every
+        norm fused with the linear layer after it (norm1 -> in-projection, norm2 -> the cross
+        attention's query projection, norm3 -> linear1 + ReLU + dropout: resnorm.resnorm_gemm)
+        and linear2 left to the next boundary's launch (LinY).  norm_b: the decoder norm of
+        the previous layer's output, computed by norm1's launch.  -> (Pending, xb)."""
+        sa, ca = self.self_attn, self.multihead_attn
+        E = sa.embed_dim
+        p1, p2, p3, pf = ((self.dropout1.p, self.dropout2.p, self.dropout3.p, self.dropout.p)
+                          if self.training else (0.0, 0.0, 0.0, 0.0))
+        site1, site2, site3, site_ffn = rn.sites(self, 4)
+        hp = query_pos is not None
+        spec = ((1, 0, 2 * E), (0, 2 * E, 3 * E)) if hp else ((0, 0, 3 * E),)
+        r = rn.resnorm_gemm(pend, self.norm1, sa.in_proj_weight, sa.in_proj_bias, spec,
+                            pos=query_pos, norm_b=norm_b, pos_fan=pos_fan, norm_b_fan=norm_b_fan,
+                            xb_into=xb_into)
+        if r is None:
+            return None
+        s, xd, outs = r
+        L = s.shape[0]
+        aspec = ((0, 0), (0, E), (1, 0)) if hp else ((0, 0), (0, E), (0, 2 * E))
+        y = sa.attend(outs, aspec, L, L, defer_out=True)
+        s, _, (q,) = rn.resnorm_gemm(rn.Pending(s, y, p1, site1), self.norm2, ca.in_proj_weight,
+                                     ca.in_proj_bias, ((1 if hp else 0, 0, E),), pos=query_pos,
+                                     pos_fan=pos_fan)
+        y = ca.forward_kv(s, kv, idx, defer_out=True, q=q.view(s.shape))
+        F = self.linear1.out_features
+        s, _, (h,) = rn.resnorm_gemm(rn.Pending(s, y, p2, site2), self.norm3, self.linear1.weight,
+                                     self.linear1.bias, ((0, 0, F),), epi=(pf, site_ffn))
+        return rn.Pending(s, rn.LinY(h, self.linear2.weight, self.linear2.bias, pf), p3, site3), xd
+
 
 class TransformerEncoder(nn.Module):
     def __init__(self, encoder_layer, num_layers, norm=None, weight_init_name="xavier_uniform"):
@@ -538,18 +598,28 @@ class TransformerDecoder(nn.Module):
         # query_pos and the decoder norm are read by many launches: one gradient buffer each
         pos_fan, nb_fan = rn.FanIn(), rn.FanIn()
         for i, layer in enumerate(self.layers):
-            s, x, xp, xd = rn.resnorm(pend, layer.norm1, pos=query_pos, want_a=True,
-                                      want_ap=query_pos is not None,
-                                      norm_b=dec_norm if i > 0 else None, pos_fan=pos_fan,
-                                      norm_b_fan=nb_fan,
-                                      xb_into=(outs, i - 1) if outs is not None and i > 0 else None)
-            if i > 0 and dec_norm is not None:
-                inter.append(xd)
             kvi = None
             if kv is not None:   # the token gradient is returned once (by layer 0)
                 kvi = kv[:5] + ((kv[5] if i == 0 else None),)
-            pend = layer.forward_fused(s, x, xp, memory, memory_pos, query_pos, tgt_mask,
-                                       memory_mask, kv=kvi, idx=i, pos_fan=pos_fan)
+            xb_into = (outs, i - 1) if outs is not None and i > 0 else None
+            r = None
+            if layer.ln_ok(tgt, query_pos, tgt_mask, memory_mask, kvi):
+                # every norm fused with the linear layer after it (csrc/lngemm.hip)
+                r = layer.forward_fused_ln(pend, query_pos, kvi, i, pos_fan,
+                                           norm_b=dec_norm if i > 0 else None, norm_b_fan=nb_fan,
+                                           xb_into=xb_into)
+            if r is not None:
+                pend, xd = r
+            else:
+                s, x, xp, xd = rn.resnorm(pend, layer.norm1, pos=query_pos, want_a=True,
+                                          want_ap=query_pos is not None,
+                                          norm_b=dec_norm if i > 0 else None, pos_fan=pos_fan,
+                                          norm_b_fan=nb_fan, xb_into=xb_into)
+            if i > 0 and dec_norm is not None:
+                inter.append(xd)
+            if r is None:
+                pend = layer.forward_fused(s, x, xp, memory, memory_pos, query_pos, tgt_mask,
+                                           memory_mask, kv=kvi, idx=i, pos_fan=pos_fan)
         s, _, _, xd = rn.resnorm(pend, norm_b=self.norm, norm_b_fan=nb_fan,
                                  xb_into=(outs, len(self.layers) - 1) if outs is not None else None)
         out = xd if self.norm is not None else s

@@ -237,6 +237,7 @@ def test_linres_matches_unfused(cuda, R, K, p, want_b):
     pos0 = torch.randn(R, 1, C, device=cuda)
     site = flash.new_site()
     outs, grads = [], []
+    old = rn.linres
     for fused in (True, False):
         rn.linres = fused
         src = src0.clone().requires_grad_()
@@ -257,10 +258,162 @@ def test_linres_matches_unfused(cuda, R, K, p, want_b):
         outs.append([t.detach().float() for t in o])
         grads.append([t.grad.float() for t in (x, src, pos)] +
                      [p_.grad.float() for m in (lin, na) + ((nb,) if want_b else ()) for p_ in m.parameters()])
-    rn.linres = True
+    rn.linres = old
     for a, b in zip(*outs):
         d = (a - b).abs()
         assert d.max().item() <= 0.05 * b.abs().max().item() + 1e-2, d.max().item()
         assert _rel(a, b) < 5e-3, _rel(a, b)
     for a, b in zip(*grads):
         assert _rel(a, b) < 2e-2, _rel(a, b)
+
+
+@pytest.mark.parametrize("qpos_kind", ["f32", "bf16", "none"])
+def test_lngemm_decoder_equals_unfused_bitwise(cuda, qpos_kind):
+    """every decoder norm fused with the linear layer after it (csrc/lngemm.hip,
+    resnorm.resnorm_gemm: norm1 -> in-projection, norm2 -> query projection, norm3 -> linear1
+    + ReLU + dropout, linear2 into the next launch) against the resnorm + rows-GEMM launches:
+    outputs, query_pos and every parameter gradient bit for bit (same arithmetic, same
+    order), dropout 0.1"""
+    from ov3d_amd import attention as flash
+    from ov3d_amd import resnorm as rn
+    from ov3d_amd.transformer import TransformerDecoder, TransformerDecoderLayer
+    torch.manual_seed(5)
+    dec = TransformerDecoder(TransformerDecoderLayer(256, 4, 256, dropout=0.1), 3,
+                             return_intermediate=True)
+    with torch.no_grad():
+        for m in dec.modules():
+            if isinstance(m, torch.nn.LayerNorm):
+                m.weight.normal_(1, 0.1)
+                m.bias.normal_(0, 0.1)
+    dec = dec.to(cuda).train()
+    flash.next_step(cuda)
+    tgt = torch.zeros(128, 2, 256, device=cuda)
+    mem = torch.randn(256, 2, 256, device=cuda)
+    qpos = None if qpos_kind == "none" else torch.randn(128, 2, 256, device=cuda).to(
+        torch.bfloat16 if qpos_kind == "bf16" else torch.float32)
+    mpos = torch.randn(256, 2, 256, device=cuda)
+    g = torch.randn((3, 2, 128, 256), device=cuda)
+    res = {}
+    for mode in ("fused", "unfused"):
+        rn.lngemm = mode == "fused"
+        try:
+            dec.zero_grad(set_to_none=True)
+            q = qpos.clone().requires_grad_() if qpos is not None else None
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                assert dec.layers[0].ln_ok(tgt, q, None, None, (None,)) == (mode == "fused")
+                out, _ = dec(tgt, mem, query_pos=q, pos=mpos)        # (L, Q, B, C)
+            (out.permute(0, 2, 1, 3).reshape(-1, 256) * g.reshape(-1, 256)).sum().backward()
+            res[mode] = [out.detach().clone()] + ([q.grad.clone()] if q is not None else []) + \
+                [p.grad.clone() for p in dec.parameters()]
+        finally:
+            rn.lngemm = True
+    names = ["out"] + (["qpos"] if qpos is not None else []) + [n for n, _ in dec.named_parameters()]
+    bad = [(n, (a.float() - b.float()).abs().max().item())
+           for n, a, b in zip(names, res["fused"], res["unfused"]) if not torch.equal(a, b)]
+    assert not bad, bad
+
+
+def _report(pairs):
+    bad = []
+    for n, a, b in pairs:
+        if a is None and b is None:
+            continue
+        if not torch.equal(a, b):
+            d = (a.float() - b.float()).abs()
+            bad.append((n, int((d > 0).sum().item()), d.max().item(), b.float().abs().max().item()))
+    return bad
+
+
+@pytest.mark.parametrize("p,epi", [(0.0, 0), (0.1, 1)])
+def test_lngemm_kernels_equal_two_launch_path(cuda, p, epi):
+    """ov3d_lngemm_fwd / _bwd against ov3d_resnorm_fwd + ov3d_rows_gemm(_act) and
+    ov3d_resnorm_bwd + ov3d_rows_gemm_act on the same operands: every output bit for bit"""
+    import ctypes
+    from ov3d_amd import _native, gemm
+    from ov3d_amd import attention as flash
+    torch.manual_seed(7)
+    R, C = 1024, 256
+    bf = torch.bfloat16
+    dev = cuda
+    flash.next_step(dev)
+    seed = flash._seed(dev)
+    src = torch.randn(R, C, device=dev)
+    y = torch.randn(R, C, device=dev).to(bf)
+    pos = torch.randn(R, C, device=dev)
+    ga, ba, gb, bb = (1 + 0.1 * torch.randn(C, device=dev), 0.1 * torch.randn(C, device=dev),
+                      1 + 0.1 * torch.randn(C, device=dev), 0.1 * torch.randn(C, device=dev))
+    W0 = (0.05 * torch.randn(512, C, device=dev)).to(bf)
+    b0 = (0.1 * torch.randn(512, device=dev)).to(bf)
+    W1 = (0.05 * torch.randn(256, C, device=dev)).to(bf)
+    b1 = (0.1 * torch.randn(256, device=dev)).to(bf)
+    site, site2 = 11, 12
+    outs = {}
+    for mode in ("two", "one"):
+        s = torch.empty(R, C, device=dev)
+        mean = torch.empty(R, device=dev)
+        rstd = torch.empty(R, device=dev)
+        xa = torch.empty(R, C, device=dev, dtype=bf)
+        xap = torch.empty(R, C, device=dev, dtype=bf)
+        xb = torch.empty(R, C, device=dev)
+        o0 = torch.empty(R, 512, device=dev, dtype=bf)
+        o1 = torch.empty(R, 256, device=dev, dtype=bf)
+        if mode == "two":
+            _native.call("ov3d_resnorm_fwd", R, C, src, 0, y, 1, float(p), seed, site, ga, ba, pos,
+                         0, gb, bb, 1e-5, s, mean, rstd, xa, xap, xb, 0, 0, 0, 0, like=s)
+            _native.call("ov3d_rows_gemm_act", R, 512, C, xap, C, W0, C, 1, b0, 0, 0.0, None, 0,
+                         None, 0, o0, 512, like=s)
+            _native.call("ov3d_rows_gemm_act", R, 256, C, xa, C, W1, C, 1, b1, epi, float(p), seed,
+                         site2, None, 0, o1, 256, like=s)
+        else:
+            probs = [gemm._LnProblem(W0.data_ptr(), C, b0.data_ptr(), o0.data_ptr(), 512, 512, 1),
+                     gemm._LnProblem(W1.data_ptr(), C, b1.data_ptr(), o1.data_ptr(), 256, 256, 0)]
+            if epi:   # the activation epilogue applies to every problem: one problem a launch
+                arr = (gemm._LnProblem * 1)(probs[0])
+                _native.call("ov3d_lngemm_fwd", R, src, 0, y, float(p), seed, site, ga, ba, pos, 0,
+                             gb, bb, 1e-5, s, mean, rstd, xa, xap, xb, 0, 0, 0, 0, 1,
+                             ctypes.addressof(arr), 0, 0.0, None, 0, like=s)
+                arr2 = (gemm._LnProblem * 1)(probs[1])
+                s2 = torch.empty_like(s)
+                _native.call("ov3d_lngemm_fwd", R, src, 0, y, float(p), seed, site, ga, ba, pos, 0,
+                             gb, bb, 1e-5, s2, torch.empty_like(mean), torch.empty_like(rstd),
+                             None, None, None, 0, 0, 0, 0, 1, ctypes.addressof(arr2), 1, float(p),
+                             seed, site2, like=s)
+            else:
+                arr = (gemm._LnProblem * 2)(*probs)
+                _native.call("ov3d_lngemm_fwd", R, src, 0, y, float(p), seed, site, ga, ba, pos, 0,
+                             gb, bb, 1e-5, s, mean, rstd, xa, xap, xb, 0, 0, 0, 0, 2,
+                             ctypes.addressof(arr), 0, 0.0, None, 0, like=s)
+        outs[mode] = dict(s=s, mean=mean, rstd=rstd, xa=xa, xap=xap, xb=xb, o0=o0, o1=o1)
+    fwd_bad = _report([(k, outs["one"][k], outs["two"][k]) for k in outs["two"]])
+    # backward: dy = dropout(resnorm_bwd(...)); dx = epi(dy W) with W (256, 256) = (out, in)
+    s, mean, rstd = outs["two"]["s"], outs["two"]["mean"], outs["two"]["rstd"]
+    ds = torch.randn(R, C, device=dev)
+    dxa = torch.randn(R, C, device=dev).to(bf)
+    dxap = torch.randn(R, C, device=dev).to(bf)
+    Wy = (0.05 * torch.randn(C, 256, device=dev)).to(bf)
+    H = torch.relu(torch.randn(R, 256, device=dev)).to(bf)
+    res = {}
+    for mode in ("two", "one"):
+        dsrc = torch.empty(R, C, device=dev)
+        dy = torch.empty(R, C, device=dev, dtype=bf)
+        dpos = torch.empty(R, C, device=dev)
+        dx = torch.empty(R, 256, device=dev, dtype=bf)
+        if mode == "two":
+            nparts = _native.load().ov3d_resnorm_bwd_parts(R, C)
+            part = torch.empty(nparts, 4, C, device=dev)
+            _native.call("ov3d_resnorm_bwd", R, C, s, mean, rstd, ds, dxa, dxap, None, 0, 0, 0, 0,
+                         ga, None, float(p), seed, site, dsrc, dy, 1, dpos, 0, part, nparts,
+                         None, None, None, None, 0, like=s)
+            _native.call("ov3d_rows_gemm_act", R, 256, C, dy, C, Wy, 256, 0, None,
+                         2 if epi else 0, float(p), None, 0, H if epi else None, 256 if epi else 0,
+                         dx, 256, like=s)
+        else:
+            nparts = _native.load().ov3d_lngemm_bwd_parts(R)
+            part = torch.empty(nparts, 4, C, device=dev)
+            _native.call("ov3d_lngemm_bwd", R, s, mean, rstd, ds, dxa, dxap, None, 0, 0, 0, 0, ga,
+                         None, float(p), seed, site, dsrc, dy, dpos, 0, part, 0, Wy, 256, 256,
+                         2 if epi else 0, float(p), H if epi else None, 256 if epi else 0, dx, 256,
+                         like=s)
+        res[mode] = dict(dsrc=dsrc, dy=dy, dpos=dpos, dx=dx, part=part)
+    bwd_bad = _report([(k, res["one"][k], res["two"][k]) for k in res["two"]])
+    assert not fwd_bad and not bwd_bad, (fwd_bad, bwd_bad)
