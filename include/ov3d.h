@@ -588,7 +588,10 @@ int ov3d_attn_small_bwd(int on);
  * words (query-major [nkt][B][Lq][2] then key-major [Lq/32][B][nkt*64]): kind 0 = uint8
  * mask (nonzero = not attended), kind 1 = fp32 distances (not attended iff d >= thr),
  * kind 2 = fp32 squared distances g of torch.cdist's matmul form, before its
- * clamp_min(0).sqrt() (not attended iff sqrt(max(g, 0)) >= thr: the bits of kind 1 on cdist).
+ * clamp_min(0).sqrt() (not attended iff sqrt(max(g, 0)) >= thr: the bits of kind 1 on cdist),
+ * kind 3 = the same bits from the points: src (B, L, 4) fp32 rows (x, y, z, |p|^2 as
+ * x.pow(2).sum(-1)), Lq == Lk == L, 16-byte aligned; g formed as the fma chain of cdist's
+ * K = 5 GEMM (bit-identical to it), no (B, L, L) distance matrix.
  * The _masked entry points take the words (NULL = no mask) and are otherwise
  * ov3d_attn_fwd / ov3d_attn_bwd.  A query with no attended key gets O = 0 and zero
  * gradients (the reference's softmax would give NaN). */

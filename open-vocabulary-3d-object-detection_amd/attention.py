@@ -200,6 +200,24 @@ def pack_mask(src, thr=None, squared=False):
     return PackedMask(words, B, Lq, Lk)
 
 
+def pack_mask_points(xyz, thr):
+    """(B, L, 3) points -> PackedMask of cdist(xyz, xyz) >= thr computed in the packing launch
+    (kind 3): the squared distances as cdist's matmul form, bit for bit, without the (B, L, L)
+    distance matrix or its fp32 GEMM (MaskedTransformerEncoder.compute_mask)."""
+    B, L, _ = xyz.shape
+    _native.check_device(xyz, "attention mask points")
+    lib = _native.load()
+    n = lib.ov3d_attn_maskbits_words(B, L, L)
+    if n <= 0:
+        raise ValueError("pack_mask_points: point count must be a multiple of 32")
+    with torch.autocast("cuda", enabled=False):
+        x = xyz.float()
+        pts = torch.cat([x, x.pow(2).sum(-1, keepdim=True)], -1).contiguous()   # euclid_sq's norms
+    words = torch.empty((n,), dtype=torch.int32, device=xyz.device)
+    _native.call("ov3d_attn_mask_pack", pts, 3, float(thr), B, L, L, words, like=pts)
+    return PackedMask(words, B, L, L)
+
+
 def supported(q_src, embed_dim, num_heads, attn_mask):
     """the HIP kernels: head_dim 64, no mask or a PackedMask, query length a multiple of 32"""
     return (q_src.is_cuda and (attn_mask is None or isinstance(attn_mask, PackedMask))

@@ -1290,9 +1290,30 @@ __device__ __forceinline__ bool masked_value(float v, float thr) {
     return v >= thr;
 }
 
+// KIND 3: the distances from the points themselves, src = (B, L, 4) fp32 rows (x, y, z,
+// |p|^2) with Lq == Lk == L: the squared distance as cdist's matmul form computes it, one fma
+// per term of [-2 p_q, |p_q|^2, 1] . [p_k, 1, |p_k|^2] in that order (the fp32 GEMM's
+// accumulation: bit for bit the library result, tools/cdist_probe.py), then KIND 2's clamp and
+// sqrt folded into the bound: sqrt(max(g, 0)) >= thr  <=>  g >= g0, g0 the least float whose
+// (correctly rounded) sqrt reaches thr, found on the host.  No (B, L, L) distance matrix, no GEMM.
+__device__ __forceinline__ float point_sqdist(const float4 pq, const float4 pk) {
+    float acc = 0.f;
+    acc = fmaf(-2.f * pq.x, pk.x, acc);
+    acc = fmaf(-2.f * pq.y, pk.y, acc);
+    acc = fmaf(-2.f * pq.z, pk.z, acc);
+    acc = fmaf(pq.w, 1.f, acc);
+    acc = fmaf(1.f, pk.w, acc);
+    return acc;
+}
+
 template <int KIND>
-__device__ __forceinline__ bool mask_at(const void* src, size_t e, float thr) {
+__device__ __forceinline__ bool mask_at(const void* src, size_t e, float thr, int Lk = 0) {
     if (KIND == 0) return ((const uint8_t*)src)[e] != 0;
+    if (KIND == 3) {
+        const size_t bq = e / (size_t)Lk, k = e - bq * (size_t)Lk, b = bq / (size_t)Lk;
+        const float4* pts = (const float4*)src;
+        return point_sqdist(pts[bq], pts[b * Lk + k]) >= thr;   // thr: the squared-form bound
+    }
     return masked_value<KIND>(((const float*)src)[e], thr);
 }
 
@@ -1310,7 +1331,18 @@ __global__ void __launch_bounds__(256) attn_mask_pack_kernel(const void* __restr
         const size_t row = ((size_t)b * Lq + q) * Lk + 64 * kt;
         uint32_t w0 = 0, w1 = 0;
         const bool full = 64 * kt + 64 <= Lk;
-        if (KIND != 0 && full && (row & 3) == 0) {
+        if (KIND == 3 && full) {   // the query point once, the 64 key points of the tile
+            const float4* pts = (const float4*)src;
+            const float4 pq = pts[(size_t)b * Lq + q];
+            const float4* pk = pts + (size_t)b * Lk + 64 * kt;
+#pragma unroll 8
+            for (int kk = 0; kk < 64; ++kk) {
+                const int rem = kk & 31;
+                const int bit = (kk & 1) * 16 + (kk >> 5) * 8 + (rem >> 3) * 2 + ((rem >> 1) & 1);
+                const uint32_t m = point_sqdist(pq, pk[kk]) >= thr ? 1u << bit : 0u;
+                if ((rem >> 2) & 1) w1 |= m; else w0 |= m;
+            }
+        } else if (KIND != 0 && KIND != 3 && full && (row & 3) == 0) {
 #pragma unroll
             for (int c = 0; c < 16; ++c) {
                 const float4 v = *reinterpret_cast<const float4*>((const float*)src + row + 4 * c);
@@ -1328,7 +1360,7 @@ __global__ void __launch_bounds__(256) attn_mask_pack_kernel(const void* __restr
             for (int kk = 0; kk < 64 && 64 * kt + kk < Lk; ++kk) {
                 const int rem = kk & 31;
                 const int bit = (kk & 1) * 16 + (kk >> 5) * 8 + (rem >> 3) * 2 + ((rem >> 1) & 1);
-                const uint32_t m = mask_at<KIND>(src, row + kk, thr) ? 1u << bit : 0u;
+                const uint32_t m = mask_at<KIND>(src, row + kk, thr, Lk) ? 1u << bit : 0u;
                 if ((rem >> 2) & 1) w1 |= m; else w0 |= m;
             }
         }
@@ -1343,9 +1375,71 @@ __global__ void __launch_bounds__(256) attn_mask_pack_kernel(const void* __restr
     const int b = (int)(qb % B), q0 = 32 * (int)(qb / B);
     uint32_t w = 0;
     if (k < Lk) {
+        if (KIND == 3) {   // the key point once, the block's 32 query points
+            const float4* pts = (const float4*)src;
+            const float4 pk = pts[(size_t)b * Lk + k];
+#pragma unroll 8
+            for (int n = 0; n < 32; ++n)
+                if (q0 + n < Lq && point_sqdist(pts[(size_t)b * Lq + q0 + n], pk) >= thr)
+                    w |= 1u << n;
+        } else {
+#pragma unroll 8
+            for (int n = 0; n < 32; ++n)
+                if (q0 + n < Lq && mask_at<KIND>(src, ((size_t)b * Lq + q0 + n) * Lk + k, thr)) w |= 1u << n;
+        }
+    }
+    words[W + u] = w;
+}
+
+// Kind 3 with the points staged in LDS: every query-major word of a (scene, 64-key tile)
+// block reads the tile's 64 key points from LDS (broadcast) instead of 1 KB from L2 per
+// thread, every key-major word of a (scene, 32-query block) reads the block's 32 query points.
+// Blocks [0, nA): query-major, (kt, b, 256-query chunk); blocks [nA, ...): key-major, 256
+// consecutive words of one (32-query block, scene) row ((nkt * 64) % 256 == 0).
+__global__ void __launch_bounds__(256) attn_mask_points_kernel(const float4* __restrict__ pts,
+                                                               float g0, int B, int L, int nkt,
+                                                               int nA, uint32_t* __restrict__ words) {
+    __shared__ float4 sp[64];
+    const int tid = threadIdx.x;
+    const int qchunks = (L + 255) / 256;
+    if ((int)blockIdx.x < nA) {
+        const int blk = blockIdx.x;
+        const int qc = blk % qchunks, rest = blk / qchunks;
+        const int b = rest % B, kt = rest / B;
+        if (tid < 64) {
+            const int k = min(64 * kt + tid, L - 1);
+            sp[tid] = pts[(size_t)b * L + k];
+        }
+        __syncthreads();
+        const int q = qc * 256 + tid;
+        if (q >= L) return;
+        const float4 pq = pts[(size_t)b * L + q];
+        const int nk = min(64, L - 64 * kt);
+        uint32_t w0 = 0, w1 = 0;
+#pragma unroll 8
+        for (int kk = 0; kk < 64; ++kk) {
+            const int rem = kk & 31;
+            const int bit = (kk & 1) * 16 + (kk >> 5) * 8 + (rem >> 3) * 2 + ((rem >> 1) & 1);
+            const uint32_t m = (kk < nk && point_sqdist(pq, sp[kk]) >= g0) ? 1u << bit : 0u;
+            if ((rem >> 2) & 1) w1 |= m; else w0 |= m;
+        }
+        *reinterpret_cast<uint2*>(words + (((size_t)kt * B + b) * L + q) * 2) = make_uint2(w0, w1);
+        return;
+    }
+    const long long W = (long long)nkt * B * L * 2;
+    const long long u = (long long)(blockIdx.x - nA) * 256 + tid;
+    const long long row = (long long)nkt * 64;
+    const long long qb = ((long long)(blockIdx.x - nA) * 256) / row;   // uniform over the block
+    const int b = (int)(qb % B), q0 = 32 * (int)(qb / B);
+    if (tid < 32) sp[tid] = pts[(size_t)b * L + min(q0 + tid, L - 1)];
+    __syncthreads();
+    const int k = (int)(u % row);
+    uint32_t w = 0;
+    if (k < L) {
+        const float4 pk = pts[(size_t)b * L + k];
 #pragma unroll 8
         for (int n = 0; n < 32; ++n)
-            if (q0 + n < Lq && mask_at<KIND>(src, ((size_t)b * Lq + q0 + n) * Lk + k, thr)) w |= 1u << n;
+            if (q0 + n < L && point_sqdist(sp[n], pk) >= g0) w |= 1u << n;
     }
     words[W + u] = w;
 }
@@ -1416,8 +1510,9 @@ extern "C" long long ov3d_attn_maskbits_words(int B, int Lq, int Lk) {
 
 extern "C" int ov3d_attn_mask_pack(const void* src, int kind, float thr, int B, int Lq, int Lk,
                                    uint32_t* words, void* stream) {
-    if (!src || !words || kind < 0 || kind > 2 || B <= 0 || Lq <= 0 || Lk <= 0 || (Lq % QW))
+    if (!src || !words || kind < 0 || kind > 3 || B <= 0 || Lq <= 0 || Lk <= 0 || (Lq % QW))
         return OV3D_EINVAL;
+    if (kind == 3 && (Lq != Lk || ((uintptr_t)src & 15))) return OV3D_EINVAL;   // self pairs, float4 rows
     const int nkt = (Lk + KB - 1) / KB;
     // threads: B*Lq*nkt query-major (two words each) + W key-major
     const long long n = (long long)B * Lq * nkt + ov3d_attn_maskbits_words(B, Lq, Lk) / 2;
@@ -1426,8 +1521,26 @@ extern "C" int ov3d_attn_mask_pack(const void* src, int kind, float thr, int B, 
         attn_mask_pack_kernel<0><<<ov3d_cdiv(n, 256), 256, 0, st>>>(src, thr, B, Lq, Lk, nkt, words);
     else if (kind == 1)
         attn_mask_pack_kernel<1><<<ov3d_cdiv(n, 256), 256, 0, st>>>(src, thr, B, Lq, Lk, nkt, words);
-    else
+    else if (kind == 2)
         attn_mask_pack_kernel<2><<<ov3d_cdiv(n, 256), 256, 0, st>>>(src, thr, B, Lq, Lk, nkt, words);
+    else {
+        // the squared-form bound of kind 3: the least g0 with sqrtf(g0) >= thr (sqrtf is
+        // monotonic and correctly rounded on host and device), -inf when every key is masked
+        float g0 = -INFINITY;
+        if (thr > 0.f) {
+            g0 = thr * thr;
+            while (sqrtf(g0) < thr) g0 = nextafterf(g0, INFINITY);
+            while (g0 > 0.f && sqrtf(nextafterf(g0, -INFINITY)) >= thr) g0 = nextafterf(g0, -INFINITY);
+        }
+        if ((nkt * 64) % 256 == 0) {
+            const int nA = nkt * B * ((Lq + 255) / 256);
+            const long long nBk = ov3d_attn_maskbits_words(B, Lq, Lk) / 2 / 256;   // key-major words / 256
+            attn_mask_points_kernel<<<(unsigned)(nA + nBk), 256, 0, st>>>((const float4*)src, g0, B, Lq,
+                                                                        nkt, nA, words);
+        } else {
+            attn_mask_pack_kernel<3><<<ov3d_cdiv(n, 256), 256, 0, st>>>(src, g0, B, Lq, Lk, nkt, words);
+        }
+    }
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

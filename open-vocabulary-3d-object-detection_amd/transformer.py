@@ -11,6 +11,7 @@ checkpoints load.  Differences that do not change results:
     (need_weights=True by default, transformer.py:271-272, 365-372);
   * ``memory + pos`` is formed once and shared by the 8 decoder layers.
 """
+import os
 from typing import Optional
 
 import torch
@@ -448,6 +449,11 @@ class TransformerEncoder(nn.Module):
         return xb if self.norm is not None else s
 
 
+# the masked encoder's mask straight from the points (attention.pack_mask_points); 0: cdist's
+# squared-distance GEMM + the kind-2 packing
+POINT_MASK = os.environ.get("OV3D_POINT_MASK", "1") != "0"
+
+
 def euclid_sq(x):
     """torch.cdist(x, x, p=2) for > 25 points (the matmul form, ATen _euclidean_dist) before its
     clamp_min(0).sqrt(): the same fp32 operations and GEMM, outside autocast as cdist runs."""
@@ -481,6 +487,8 @@ class MaskedTransformerEncoder(TransformerEncoder):
         """the same mask as compute_mask, packed for the HIP attention kernels straight from
         cdist's matmul-form squared distances, its clamp and sqrt fused into the packing (no
         (B, L, L) distance or (B*H, L, L) bool tensor)"""
+        if POINT_MASK:   # the distances inside the packing launch (no GEMM, no L x L matrix)
+            return flash.pack_mask_points(xyz, float(radius)), ("pts", None)
         if dist is None or dist[0] != "sq" or dist[1].shape[1] != xyz.shape[1]:
             dist = ("sq", euclid_sq(xyz))
         return flash.pack_mask(dist[1], float(radius), squared=True), dist

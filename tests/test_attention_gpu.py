@@ -380,6 +380,23 @@ def test_squared_distance_mask_equals_cdist_mask(cuda, B, L):
         assert torch.equal(a, b), r2
 
 
+@pytest.mark.parametrize("B,L,scale", [(8, 2048, (6.0, 6.0, 3.0)), (3, 1024, (6.0, 6.0, 3.0)),
+                                       (2, 2048, (0.5, 0.5, 0.5))])
+def test_point_mask_equals_cdist_mask(cuda, B, L, scale):
+    """The masked encoder's mask packed straight from the points (kind 3: the squared distance
+    as the fma chain of cdist's K = 5 matmul form, attention.pack_mask_points) gives the bits of
+    packing torch.cdist's output (coincident points included): no distance matrix, no GEMM"""
+    from ov3d_amd import attention as A
+    g = torch.Generator(device=cuda).manual_seed(4)
+    xyz = torch.rand(B, L, 3, device=cuda, generator=g) * torch.tensor(scale, device=cuda)
+    xyz[:, 7] = xyz[:, 3]
+    dist = torch.cdist(xyz.float(), xyz.float(), p=2)
+    for r2 in (0.16, 0.64, 1.44, 0.05):
+        a = A.pack_mask_points(xyz, r2).words
+        b = A.pack_mask(dist, r2).words
+        assert torch.equal(a, b), r2
+
+
 @pytest.mark.parametrize("with_interim", [False, True])
 def test_masked_encoder_packed_equals_bool_mask_path(cuda, monkeypatch, with_interim):
     """MaskedTransformerEncoder (bf16 fused layers): PackedMask through the HIP kernels vs
@@ -404,8 +421,10 @@ def test_masked_encoder_packed_equals_bool_mask_path(cuda, monkeypatch, with_int
         if not packed:
             monkeypatch.setattr(T.MaskedTransformerEncoder, "_packed_ok", staticmethod(lambda *a: False))
         calls = []
-        real = T.flash.pack_mask
+        real, real_pts = T.flash.pack_mask, T.flash.pack_mask_points
         monkeypatch.setattr(T.flash, "pack_mask", lambda *a, **k: calls.append(1) or real(*a, **k))
+        monkeypatch.setattr(T.flash, "pack_mask_points",
+                            lambda *a, **k: calls.append(1) or real_pts(*a, **k))
         src = src0.clone().requires_grad_()
         with torch.autocast("cuda", dtype=torch.bfloat16):
             _, out, inds = twin(src, xyz=xyz)
