@@ -329,11 +329,19 @@ def conv3x3_gemm256(x, w, bias=None, residual=None, relu=False):
     return out
 
 
+# products over this many rows and more (the masked encoder's interim SA: 2^18 rows) run on the
+# 256 x 256 tile kernel (gemm256, ~1 PF/s there) rather than the long row-block kernel (~0.5)
+GEMM256_MIN_M = int(os.environ.get("OV3D_GEMM256_MIN_M", str(1 << 17)))
+
+
 def _linear(x, w, b):
     """F.linear on bf16 rows (bias in the epilogue): short row blocks on rowsgemm, long ones
-    on tilegemm"""
+    on tilegemm, the longest on gemm256"""
     if _rows_gemm_ok(x, w, True):
         return rows_gemm(x, w, b, trans_b=True)
+    if x.shape[0] >= GEMM256_MIN_M and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 \
+            and gemm256_ok(x, w):
+        return gemm256(x, w, bias=b)
     if _tile_gemm_ok(x, w, True):
         return tile_gemm(x, w, b, trans_b=True)
     if x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and gemm256_ok(x, w):
@@ -361,6 +369,10 @@ def _dgrad(dy, w):
     """dy (M, N) @ w (N, K) for the input gradient of a linear layer"""
     if _rows_gemm_ok(dy, w, False):
         return rows_gemm(dy, w, trans_b=False)
+    if dy.shape[0] >= GEMM256_MIN_M and dy.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
+        wt = w.t().contiguous()   # (K, N) rows: dx = dy wt^T on the 256 x 256 tile kernel
+        if gemm256_ok(dy, wt):
+            return gemm256(dy, wt)
     if _tile_gemm_ok(dy, w, False):
         return tile_gemm(dy, w, trans_b=False)
     if dy.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and dy.shape[0] > ROWS_GEMM_MAX_M:

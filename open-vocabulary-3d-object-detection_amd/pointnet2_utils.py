@@ -7,6 +7,8 @@ Same names, argument meaning and return types as the upstream module:
 ``gather_operation``, ``ball_query``, ``grouping_operation``, ``QueryAndGroup``.
 Semantics: SURVEY.md Appendix A (FPS tie rule: DESIGN.md §FPS).
 """
+import os
+
 import torch
 import torch.nn as nn
 from torch.autograd import Function
@@ -181,8 +183,15 @@ class _Group(Function):
         return None, None, gf, None, None, None, None
 
 
+# column alignment of the bf16 group rows (the masked encoder's interim SA: 3 + 256 -> 264).
+# 64 (K = 320, whole K chunks for gemm256) measured slower at C4: 7.33 vs 7.29 ms median, the
+# wider rows cost the grouping, the GEMMs and the dgrad more than the K tail costs gemm256
+ROW_ALIGN = int(os.environ.get("OV3D_GROUP_ROW_ALIGN", "8"))
+
+
 class _GroupBf16(Function):
-    """_Group's rows in bf16, zero-padded to Cp = round_up(3 + C, 8) columns (aligned GEMM K);
+    """_Group's rows in bf16, zero-padded to Cp = round_up(3 + C, ROW_ALIGN) columns (aligned
+    GEMM K);
     the backward gathers the feature columns of the bf16 row gradient through the inverse."""
 
     @staticmethod
@@ -194,7 +203,7 @@ class _GroupBf16(Function):
         if strides is None:
             features = features.contiguous()
             strides = _dense_strides(features)
-        cp = (3 + C + 7) // 8 * 8
+        cp = (3 + C + ROW_ALIGN - 1) // ROW_ALIGN * ROW_ALIGN
         out = torch.empty((B, M, S, cp), dtype=torch.bfloat16, device=xyz.device)
         nat.call("ov3d_group_rows_bf16", xyz, new_xyz, features, *strides, idx, B, C, N, M, S,
                  float(radius), int(bool(normalize)), cp, out, like=xyz)
