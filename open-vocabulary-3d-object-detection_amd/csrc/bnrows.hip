@@ -136,32 +136,105 @@ __global__ void __launch_bounds__(256) rows_bn_stats_kernel(const T* __restrict_
     }
 }
 
+// Element passes: a thread owns one 8-channel run (its per-channel coefficients loaded once and
+// its layout offset computed once) and RPT rows of it, the rows' loads in flight together; the
+// grid covers R in (256 / runs) * RPT-row slabs.  (One run per thread per launch cost ~60 %
+// more than the HBM floor at 2^18 x 256: ten coefficient loads, three runtime divisions of the
+// layout and 64-bit index math for each 16 bytes of data.)
+constexpr int RPT = 4;
+
+__device__ __forceinline__ long long coff(const RowsLayout& L, int c) {
+    return (long long)(c / L.cb) * L.bstride + (c % L.cb);
+}
+
+template <typename T>
+__device__ __forceinline__ void load8o(const T* base, long long off, float* v);
+template <>
+__device__ __forceinline__ void load8o<bf16>(const bf16* base, long long off, float* v) {
+    const bf16x8 x = *reinterpret_cast<const bf16x8*>(base + off);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)x[j];
+}
+template <>
+__device__ __forceinline__ void load8o<float>(const float* base, long long off, float* v) {
+    const float4 a = *reinterpret_cast<const float4*>(base + off);
+    const float4 b = *reinterpret_cast<const float4*>(base + off + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void ld8f(const float* p, float* v) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// the run / rows of this thread: rows r0 + k * rstep (k < RPT), channel c
+struct Slab {
+    int c;
+    long long r0, rstep;
+    bool active;
+};
+__device__ __forceinline__ Slab slab(int C) {
+    Slab q;
+    const int runs = C / 8;
+    const int tpr = runs < 256 ? runs : 256;       // threads per row
+    const int rpb = 256 / tpr;                      // rows per block pass
+    const int ph = threadIdx.x / tpr;
+    const int chunks = (runs + tpr - 1) / tpr;      // C > 2048: several thread rows per row
+    const int chunk = blockIdx.x % chunks;
+    const long long blk = blockIdx.x / chunks;
+    q.c = (chunk * tpr + threadIdx.x % tpr) * 8;
+    q.r0 = blk * (long long)rpb * RPT + ph;
+    q.rstep = rpb;
+    q.active = ph < rpb && q.c < C;
+    return q;
+}
+__host__ __device__ inline long long slab_blocks(long long R, int C) {
+    const int runs = C / 8;
+    const int tpr = runs < 256 ? runs : 256;
+    const int rpb = 256 / tpr;
+    return ((R + (long long)rpb * RPT - 1) / ((long long)rpb * RPT)) * ((runs + tpr - 1) / tpr);
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) rows_bn_apply_kernel(
     const T* __restrict__ x, RowsLayout L, long long R, int C, const float* __restrict__ scale,
     const float* __restrict__ shift, uint32_t thresh, float keep_scale, const int64_t* seed,
     uint32_t site, bf16* __restrict__ out, RowsLayout LO) {
-    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const int runs = C / 8;
-    if (t >= R * runs) return;
-    const long long r = t / runs;
-    const int c = (int)(t - r * runs) * 8;
-    float v[8];
-    load8<T>(x, L, r, c, v);
-    bool keep[8];
+    const Slab q = slab(C);
+    if (!q.active) return;
+    const int c = q.c;
+    float sc[8], sh[8];
+    ld8f(scale + c, sc);
+    ld8f(shift + c, sh);
+    const long long ox = coff(L, c), oo = coff(LO, c);
+    uint32_t sm = 0;
     if (thresh) {
         const uint64_t s = (uint64_t)*seed;
-        const uint32_t sm = mix32((uint32_t)s ^ mix32((uint32_t)(s >> 32) + site * 0x9E3779B9u));
-        keep8(row_base(sm, r), c, thresh, keep);
+        sm = mix32((uint32_t)s ^ mix32((uint32_t)(s >> 32) + site * 0x9E3779B9u));
     }
-    bf16x8 o;
+    float v[RPT][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        float z = fmaxf(fmaf(v[j], scale[c + j], shift[c + j]), 0.f);
-        if (thresh) z = keep[j] ? z * keep_scale : 0.f;
-        o[j] = (bf16)z;
+    for (int k = 0; k < RPT; ++k) {
+        const long long r = q.r0 + k * q.rstep;
+        if (r < R) load8o<T>(x, ox + r * L.ld, v[k]);
     }
-    *reinterpret_cast<bf16x8*>(out + addr(LO, r, c)) = o;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const long long r = q.r0 + k * q.rstep;
+        if (r >= R) break;
+        bool keep[8];
+        if (thresh) keep8(row_base(sm, r), c, thresh, keep);
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float z = fmaxf(fmaf(v[k][j], sc[j], sh[j]), 0.f);
+            if (thresh) z = keep[j] ? z * keep_scale : 0.f;
+            o[j] = (bf16)z;
+        }
+        *reinterpret_cast<bf16x8*>(out + oo + r * LO.ld) = o;
+    }
 }
 
 template <int PASS, typename T>
@@ -178,24 +251,40 @@ __global__ void __launch_bounds__(256) rows_bn_bwd_kernel(
         sm = mix32((uint32_t)s ^ mix32((uint32_t)(s >> 32) + site * 0x9E3779B9u));
     }
     if (PASS == 1) {
-        const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-        const int runs = C / 8;
-        if (t >= R * runs) return;
-        const long long r = t / runs;
-        const int c = (int)(t - r * runs) * 8;
-        float xv[8], zv[8];
-        load8<T>(x, LX, r, c, xv);
-        load8<bf16>(dz, LZ, r, c, zv);
-        bool keep[8];
-        if (thresh) keep8(row_base(sm, r), c, thresh, keep);
-        bf16x8 o;
+        const Slab q = slab(C);
+        if (!q.active) return;
+        const int c = q.c;
+        float sc[8], sh[8], a[8], b[8], cc[8];
+        ld8f(scale + c, sc);
+        ld8f(shift + c, sh);
+        ld8f(cA + c, a);
+        ld8f(cB + c, b);
+        ld8f(cC + c, cc);
+        const long long ox = coff(LX, c), oz = coff(LZ, c), od = coff(LD, c);
+        float xv[RPT][8], zv[RPT][8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            float dt = fmaf(xv[j], scale[c + j], shift[c + j]) > 0.f ? zv[j] : 0.f;
-            if (thresh) dt = keep[j] ? dt * keep_scale : 0.f;
-            o[j] = (bf16)fmaf(cA[c + j], dt, fmaf(cB[c + j], xv[j], cC[c + j]));
+        for (int k = 0; k < RPT; ++k) {
+            const long long r = q.r0 + k * q.rstep;
+            if (r < R) {
+                load8o<T>(x, ox + r * LX.ld, xv[k]);
+                load8o<bf16>(dz, oz + r * LZ.ld, zv[k]);
+            }
         }
-        *reinterpret_cast<bf16x8*>(dx + addr(LD, r, c)) = o;
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) {
+            const long long r = q.r0 + k * q.rstep;
+            if (r >= R) break;
+            bool keep[8];
+            if (thresh) keep8(row_base(sm, r), c, thresh, keep);
+            bf16x8 o;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float dt = fmaf(xv[k][j], sc[j], sh[j]) > 0.f ? zv[k][j] : 0.f;
+                if (thresh) dt = keep[j] ? dt * keep_scale : 0.f;
+                o[j] = (bf16)fmaf(a[j], dt, fmaf(b[j], xv[k][j], cc[j]));
+            }
+            *reinterpret_cast<bf16x8*>(dx + od + r * LD.ld) = o;
+        }
         return;
     }
     const Phase p = phase(C);
@@ -278,15 +367,15 @@ extern "C" int ov3d_rows_bn_apply(const void* x, int is_bf16, long long ld, long
     if (!x || !scale || !shift || !out || R <= 0 || C <= 0 || C % 8 || !layout_ok(L, C) ||
         !layout_ok(LO, C) || dropout_p < 0.f || dropout_p >= 1.f || (dropout_p > 0.f && !seed))
         return OV3D_EINVAL;
-    const long long n = R * (C / 8);
+    const long long nb = slab_blocks(R, C);
     hipStream_t s = ov3d_stream(stream);
     const uint32_t th = drop_thresh(dropout_p);
     const float ks = 1.f / (1.f - dropout_p);
     if (is_bf16)
-        rows_bn_apply_kernel<bf16><<<ov3d_cdiv(n, 256), 256, 0, s>>>(
+        rows_bn_apply_kernel<bf16><<<(unsigned)nb, 256, 0, s>>>(
             (const bf16*)x, L, R, C, scale, shift, th, ks, seed, (uint32_t)site, (bf16*)out, LO);
     else
-        rows_bn_apply_kernel<float><<<ov3d_cdiv(n, 256), 256, 0, s>>>(
+        rows_bn_apply_kernel<float><<<(unsigned)nb, 256, 0, s>>>(
             (const float*)x, L, R, C, scale, shift, th, ks, seed, (uint32_t)site, (bf16*)out, LO);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
@@ -319,13 +408,13 @@ extern "C" int ov3d_rows_bn_bwd(int pass, const void* dz, long long ldz, long lo
                 (const bf16*)dz, LZ, (const float*)x, LX, R, C, scale, shift, mean, invstd, cA, cB,
                 cC, th, ks, seed, (uint32_t)site, partials, (bf16*)dx, LD);
     } else {
-        const long long n = R * (C / 8);
+        const long long nb = slab_blocks(R, C);
         if (x_bf16)
-            rows_bn_bwd_kernel<1, bf16><<<ov3d_cdiv(n, 256), 256, 0, s>>>(
+            rows_bn_bwd_kernel<1, bf16><<<(unsigned)nb, 256, 0, s>>>(
                 (const bf16*)dz, LZ, (const bf16*)x, LX, R, C, scale, shift, mean, invstd, cA, cB,
                 cC, th, ks, seed, (uint32_t)site, partials, (bf16*)dx, LD);
         else
-            rows_bn_bwd_kernel<1, float><<<ov3d_cdiv(n, 256), 256, 0, s>>>(
+            rows_bn_bwd_kernel<1, float><<<(unsigned)nb, 256, 0, s>>>(
                 (const bf16*)dz, LZ, (const float*)x, LX, R, C, scale, shift, mean, invstd, cA, cB,
                 cC, th, ks, seed, (uint32_t)site, partials, (bf16*)dx, LD);
     }
