@@ -221,10 +221,13 @@ int ov3d_sa_dy2_fused(const void* y1, const float* x0, const float* W1, const fl
                       const void* dz2, const float* cA, const float* cB, const float* cC,
                       const void* W, const float* mean1, const float* invstd1, int R, int K, int N,
                       void* dz1, float* dwpart, double* stats, int nwg, void* stream);
+/* (ysel (P, N): the pooled y3 value at the isel row, as ov3d_sa_pool_fwd wrote it; the dy of
+ * that row is cA*g + cB*ysel + cC, every other row's cB*y + cC) */
 int ov3d_sa_dy_fused(const void* yprev, const float* scale, const float* shift, const void* W,
                      int R, int K, int N, int S, const float* gsel, const uint8_t* isel,
-                     const float* cA, const float* cB, const float* cC, void* dz, float* dwpart,
-                     const float* mean, const float* invstd, double* stats, int nwg, void* stream);
+                     const float* ysel, const float* cA, const float* cB, const float* cC,
+                     void* dz, float* dwpart, const float* mean, const float* invstd,
+                     double* stats, int nwg, void* stream);
 /* (nparts, width) fp64 -> (width) sums */
 int ov3d_reduce_partials(const double* partials, int nparts, int width, double* totals,
                          void* stream);

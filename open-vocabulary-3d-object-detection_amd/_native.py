@@ -98,7 +98,7 @@ _SIGS = {
     "ov3d_rows_gemm": "iiiplplipplp",
     "ov3d_bn_stats_finalize": "piidppffpppppppp",
     "ov3d_colsum_group": "pipiip",
-    "ov3d_sa_dy_fused": "ppppiiiippppppppppip",
+    "ov3d_sa_dy_fused": "ppppiiiipppppppppppip",
     "ov3d_sa_dy2_fused": "pppppppppppppppiiipppip",
     "ov3d_bn_bwd_stats_finalize": "piidppppppppp",
     "ov3d_rows_gemm_act": "iiiplplipifpiplplp",

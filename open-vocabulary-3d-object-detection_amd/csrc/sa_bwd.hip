@@ -41,6 +41,7 @@ struct DyFusedArgs {
     int R, S;
     const float* gsel;     // (P, N) pooled gradient after the ReLU mask
     const uint8_t* isel;   // (P, N) row of the pooled value within its centroid
+    const float* ysel;     // (P, N) the pooled y3 value (the forward's, at the isel row)
     const float* cA;       // (N) dy3 = cA*g + cB*y3 + cC
     const float* cB;
     const float* cC;
@@ -593,6 +594,331 @@ __global__ __launch_bounds__(512, 1) void sa_dy8_kernel(DyFusedArgs p) {
         }
 }
 
+// sa_dy9's LDS images.  Rows / lines are unpadded and XOR-swizzled in 16- or 8-byte pieces, so
+// that every access below is free of bank conflicts (MI355X_MICROARCH.md §LDS lane groups;
+// tools/lds_banks_dy9.py enumerates them):
+//   As  (z: 64 rows x 128 k): 16-byte piece c of row r at c ^ zsw(r).  Read row-wise by the y3 A
+//       operand (ds_read_b128, lanes = rows) and transposed by the dW3 B operand
+//       (ds_read_b64_tr_b16 over 4 rows x 16 k): one image serves both (sa_dy8 kept two).
+//   DsT (dy3^T: 256 lines x 64 rows): 8-byte piece c (4 rows) of line n at c ^ dsw(n).  Written
+//       by the y3 epilogue (ds_write_b64, 16 consecutive lines per lane group), read transposed
+//       by the dz A operand (4 lines x 16 rows) and by the dW3 A operand (ds_read_b64 over 32
+//       consecutive lines).  sa_dy8's padded 34-dword lines left the dz reads 2-way conflicted.
+__device__ __forceinline__ int dsw(int n) {
+    return (((n >> 1) & 1) << 3) | (((n >> 3) & 1) << 2) | (((n >> 2) & 1) << 1) | ((n ^ (n >> 4)) & 1);
+}
+__device__ __forceinline__ int zsw(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+
+// sa_dy8 restructured so its three MFMA chains are fed two steps ahead.  sa_dy8 held, per lane,
+// 16 channels x 2 statistics partials (32 VGPRs) next to the W3^T fragments (64) and the dW3
+// accumulators (64): at the 256-VGPR cap every MFMA waited for the LDS read issued just before
+// it.  Here the dz product is computed transposed, dz[row][k] = dy3 W3 with dy3 as the A
+// operand: a lane holds ONE channel (kz = kbz + r32) of 16 rows, so the statistics partials are
+// 2 registers and the channel's BN constants 4; the freed registers carry the operands ahead.
+// The dz values are staged in LDS (Dz, 2-byte writes) and stored as 16-byte rows by the next
+// tile's prologue.  dy3 is cB*y3 + cC everywhere but at the pooled row of each centroid, whose
+// value comes from the pooled y3 (ysel, the forward's value at that row, which the recompute
+// reproduces bit for bit): one 2-byte LDS write per lane over the 8-byte row stores.
+// Same roles per wave and output layouts as sa_dy8; the statistics are summed over a lane's
+// rows in a different order (fp32 per lane, fp64 across lanes and workgroups).
+template <int K, int N, bool STATS>
+__global__ __launch_bounds__(512, 1) void sa_dy9_kernel(DyFusedArgs p) {
+    constexpr int T8 = 512;
+    constexpr int LDR = kTile;        // DsT line (swizzled, unpadded)
+    constexpr int LDY = K + 32;       // Ys: ds_read_b64_tr_b16 column reads (80 dwords)
+    constexpr int KS = K / 16;
+    constexpr int NS = N / 16;
+    constexpr int NWL = 6;            // dz k-steps whose W3 fragments are read from W3s, not held
+    static_assert(K == 128 && N == 256, "8 waves: 32 y3 columns, 32 dz channels x 32 rows, 32 dW rows");
+    __shared__ __attribute__((aligned(256))) bf16 As[kTile * K];
+    __shared__ __attribute__((aligned(128))) bf16 DsT[N * LDR];
+    __shared__ __attribute__((aligned(16))) bf16 Dz[kTile * K];
+    __shared__ __attribute__((aligned(16))) bf16 Ys[STATS ? kTile * LDY : 8];
+    __shared__ __attribute__((aligned(256))) bf16 W3s[N * K];   // swizzled as As (zsw of the row n)
+    __shared__ float sc[K], sh[K];
+    static_assert(sizeof(As) + sizeof(DsT) + sizeof(Dz) + sizeof(Ys) + sizeof(W3s) +
+                  2 * K * sizeof(float) <= 160 * 1024, "LDS images exceed the CU's 160 KB");
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r32 = lane & 31, h = lane >> 5;
+
+    for (int k = tid; k < K; k += T8) {
+        sc[k] = p.scale[k];
+        sh[k] = p.shift[k];
+    }
+    for (int i = tid; i < N * K / 8; i += T8) {   // W3 (N, K) -> swizzled LDS rows
+        const int n = i / (K / 8), c = i % (K / 8);
+        *reinterpret_cast<bf16x8*>(&W3s[n * K + 8 * (c ^ zsw(n))]) = *reinterpret_cast<const bf16x8*>(p.W + (size_t)n * K + 8 * c);
+    }
+    const int kbz = (wave & 3) * 32, rbz = wave >> 2;   // dz: channel block, row block
+    const int kz = kbz + r32;                           // dz: this lane's channel
+    // W3 fragments (B operand of dz = dy3 W3): channel kz, n in col_operand's order; the first
+    // NWL k-steps' come from W3s in the dz loop (registers for the operands read ahead)
+    bf16x8 wt[NS];
+#pragma unroll
+    for (int s = NWL; s < NS; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            wt[s][j] = p.W[(size_t)(16 * s + 8 * (j >> 2) + 4 * h + (j & 3)) * K + kz];
+    float zsc = 0.f, zsh = 0.f, zmu = 0.f, zis = 0.f;   // layer 2's BN of channel kz
+    if constexpr (STATS) {
+        zsc = p.scale[kz];
+        zsh = p.shift[kz];
+        zmu = p.mean[kz];
+        zis = p.invstd[kz];
+    }
+    const int ny = wave * 32 + r32;   // y3 column / dW3 row of this lane
+    const float cA = p.cA[ny], cB = p.cB[ny], cC = p.cC[ny];
+    float st1 = 0.f, st2 = 0.f;
+    f32x16 dw[K / 32];
+#pragma unroll
+    for (int b = 0; b < K / 32; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dw[b][i] = 0.f;
+
+    // element offsets.  As, y3 A operand: row r32 (+32), piece 2s + h -> ya ^ 16s.
+    const int zt = zsw(r32);
+    const int ya = r32 * K + 8 * (h ^ zt);
+    const int wy = ny * K + 8 * (h ^ zt);   // W3s, y3 B operand: row ny (zsw(ny) = zsw(r32))
+    // As, dW3 B operand (col_operand's lane pattern): rows 16s + rl (+8), k = 32b + 16(g&1) +
+    // 4(i&3); zsw(16s + rl) = zsw(rl), so (base ^ 32b) + 16K s.  The same pattern reads the
+    // dz B operand from W3s (rows n = 16s + rl, k = kbz + ...): (base ^ kbz) + 16K s.
+    const int g4 = lane >> 4, i16 = lane & 15;
+    const int rl = 4 * (g4 >> 1) + (i16 >> 2);
+    const int kq = 2 * (g4 & 1) + ((i16 >> 1) & 1);   // 16-byte piece within the 64-byte column run
+    const int zl = zsw(rl), zh = zsw(rl + 8);
+    const int xlo = rl * K + 32 * (zl >> 2) + 8 * (kq ^ (zl & 3)) + 4 * (i16 & 1);
+    const int xhi = (rl + 8) * K + 32 * (zh >> 2) + 8 * (kq ^ (zh & 3)) + 4 * (i16 & 1);
+    // DsT.  y3 stores / dW3 reads: line ny, piece c at 4 (c ^ dsw(ny)); the pieces 8rb + 2q + h
+    // and 4s + h (+2) are oy ^ (32rb + 8q) and oy ^ 16s (^ 8).  dz reads: lines 16s + nl (+8),
+    // pieces pc; dsw(16s + nl) = dsw(nl) ^ (s & 1): two bases per half and an immediate 1024 s.
+    const int sgy = dsw(r32);
+    const int oy = ny * LDR + 4 * (h ^ sgy);
+    const int pc = rbz * 8 + 4 * (g4 & 1) + (i16 & 3);
+    const int nl = 4 * (g4 >> 1) + (i16 >> 2);
+    const int zl0 = nl * LDR + 4 * (pc ^ dsw(nl));
+    const int zh0 = (nl + 8) * LDR + 4 * (pc ^ dsw(nl + 8));
+    const bf16* zlo[2] = {DsT + zl0, DsT + (zl0 ^ 4)};
+    const bf16* zhi[2] = {DsT + zh0, DsT + (zh0 ^ 4)};
+
+    const int ntiles = p.R / kTile;
+    constexpr int CH = kTile * K / 8 / T8;
+    static_assert(CH * T8 * 8 == kTile * K, "tile chunks");
+    bf16x8 pre[CH];
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.yprev, 0, (int)min((long long)p.R * K * 2, 0x7fffffffLL), kBufDword3);
+    const __amdgpu_buffer_rsrc_t irs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.isel, 0, 0x7fffffff, kBufDword3);
+    const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.gsel, 0, 0x7fffffff, kBufDword3);
+    const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.ysel, 0, 0x7fffffff, kBufDword3);
+    auto fetch = [&](int tile) __attribute__((always_inline)) {
+        const int soff = tile * kTile * K * 2;
+        const int tf = (wv * 64 + lane_fresh()) * 16;
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+            pre[c] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    yrs, tf + c * T8 * 16, soff, 0));
+    };
+    // the pooled gradient, value and row of this lane's column, one tile ahead
+    float gv_n[2] = {0.f, 0.f}, yv_n[2] = {0.f, 0.f};
+    uint32_t sv_n[2] = {0u, 0u};
+    auto fetch_g = [&](int tile) __attribute__((always_inline)) {
+        const int nyf = wv * 32 + (lane_fresh() & 31);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+            const int pc0 = (p.S == 64 ? tile : tile * 2 + rb) * N;
+            sv_n[rb] = __builtin_amdgcn_raw_buffer_load_b8(irs, nyf, pc0, 0);
+            gv_n[rb] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(grs, nyf * 4, pc0 * 4, 0));
+            yv_n[rb] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vrs, nyf * 4, pc0 * 4, 0));
+        }
+    };
+    // a finished tile's dz rows (staged in Dz by its dz phase) -> HBM as 16-byte row pieces
+    auto flush_dz = [&](size_t prow0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const int ch = tid + c * T8;
+            const int row = ch / (K / 8), kc = (ch % (K / 8)) * 8;
+            *reinterpret_cast<bf16x8*>(p.dz + (prow0 + row) * K + kc) =
+                *reinterpret_cast<const bf16x8*>(&Dz[row * K + kc]);
+        }
+    };
+    if (blockIdx.x < ntiles) {
+        fetch(blockIdx.x);
+        fetch_g(blockIdx.x);
+    }
+    __syncthreads();
+    PROBE_DECL
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const size_t row0 = (size_t)tile * kTile;
+        PROBE(0);
+        if (tile != (int)blockIdx.x) flush_dz(row0 - (size_t)gridDim.x * kTile);
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const int ch = tid + c * T8;
+            const int row = ch / (K / 8), kc = (ch % (K / 8)) * 8;
+            bf16x8 z;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                z[j] = (bf16)fmaxf(fmaf(sc[kc + j], (float)pre[c][j], sh[kc + j]), 0.f);
+            *reinterpret_cast<bf16x8*>(&As[row * K + 8 * ((kc >> 3) ^ zsw(row))]) = z;
+            if constexpr (STATS) *reinterpret_cast<bf16x8*>(&Ys[row * LDY + kc]) = pre[c];
+        }
+        const float gv[2] = {gv_n[0], gv_n[1]}, yv[2] = {yv_n[0], yv_n[1]};
+        const int sv[2] = {(int)sv_n[0], (int)sv_n[1] + (p.S == 64 ? 0 : 32)};
+        PROBE(1);
+        __syncthreads();
+        PROBE(2);
+        if (tile + (int)gridDim.x < ntiles) {   // in flight below
+            fetch_g(tile + gridDim.x);
+            fetch(tile + gridDim.x);
+        }
+
+        // y3 = z W3^T for columns 32w.., then dy3 -> DsT; operands two k-steps ahead
+        {
+            bf16x8 bq[KS], a0q[KS], a1q[KS];
+            auto ld = [&](int s) __attribute__((always_inline)) {
+                bq[s] = *reinterpret_cast<const bf16x8*>(&W3s[wy ^ (16 * s)]);
+                a0q[s] = *reinterpret_cast<const bf16x8*>(&As[ya ^ (16 * s)]);
+                a1q[s] = *reinterpret_cast<const bf16x8*>(&As[(ya ^ (16 * s)) + 32 * K]);
+            };
+            f32x16 acc[2];
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[rb][i] = 0.f;
+            ld(0);
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                if (s + 1 < KS) ld(s + 1);
+                acc[0] = mfma(a0q[s], bq[s], acc[0]);
+                acc[1] = mfma(a1q[s], bq[s], acc[1]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {   // rows rb*32 + 8q + 4h + (0..3): piece 8rb + 2q + h
+                    bf16x4 d4;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        d4[j] = (bf16)fmaf(cB, (float)(bf16)acc[rb][4 * q + j], cC);
+                    *reinterpret_cast<bf16x4*>(&DsT[oy ^ (32 * rb + 8 * q)]) = d4;
+                }
+            }
+            // the pooled row of each centroid (one per tile at S = 64, per row block at 32)
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb) {
+                const int r = sv[rb];
+                if ((rb == 0 || p.S == 32) && h == ((r >> 2) & 1))
+                    DsT[ny * LDR + 4 * ((r >> 2) ^ sgy) + (r & 3)] = (bf16)fmaf(cA, gv[rb], fmaf(cB, yv[rb], cC));
+            }
+        }
+        PROBE(3);
+        __syncthreads();
+        PROBE(4);
+
+        // dz[row][k] = dy3 W3 for rows rbz*32.., channel kz: A = dy3 rows (transposed DsT reads)
+        {
+            bf16x8 aq[NS];
+            auto ld = [&](int s) __attribute__((always_inline)) {
+                const bf16x4 lo = tr16(zlo[s & 1] + 16 * LDR * s);
+                const bf16x4 hi = tr16(zhi[s & 1] + 16 * LDR * s);
+                aq[s] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                if (s < NWL) {
+                    const bf16x4 wl = tr16(W3s + (xlo ^ kbz) + 16 * K * s);
+                    const bf16x4 wh = tr16(W3s + (xhi ^ kbz) + 16 * K * s);
+                    wt[s] = bf16x8{wl[0], wl[1], wl[2], wl[3], wh[0], wh[1], wh[2], wh[3]};
+                }
+            };
+            f32x16 acc;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+            ld(0);
+            ld(1);
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                if (s + 2 < NS) ld(s + 2);
+                acc = mfma(aq[s], wt[s], acc);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            bf16x8 yq[2];   // layer 2's raw rows of this lane's channel (the statistics)
+            if constexpr (STATS) {
+                yq[0] = col_operand(Ys, LDY, lane, kbz, 2 * rbz);
+                yq[1] = col_operand(Ys, LDY, lane, kbz, 2 * rbz + 1);
+            }
+            // element i: row rbz*32 + (i&3) + 8(i>>2) + 4h of channel kz
+            bf16* dzl = &Dz[(rbz * 32 + 4 * h) * K + kz];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const bf16 o = (bf16)acc[i];
+                dzl[((i & 3) + 8 * (i >> 2)) * K] = o;
+                if constexpr (STATS) {   // bn_relu_bwd pass 0 on the stored value
+                    const float yy = (float)yq[i >> 3][i & 7];
+                    const float dt = fmaf(zsc, yy, zsh) > 0.f ? (float)o : 0.f;
+                    st1 += dt;
+                    st2 = fmaf(dt, (yy - zmu) * zis, st2);
+                }
+            }
+        }
+        PROBE(5);
+
+        // dW3 rows 32w.. += dy3^T z over this tile's rows; operands two products ahead
+        {
+            bf16x8 adq[kTile / 16], bzq[kTile / 16 * (K / 32)];
+            auto ld = [&](int t) __attribute__((always_inline)) {
+                const int s = t >> 2, b = t & 3;
+                if (b == 0) {
+                    const bf16x4 lo = *reinterpret_cast<const bf16x4*>(&DsT[oy ^ (16 * s)]);
+                    const bf16x4 hi = *reinterpret_cast<const bf16x4*>(&DsT[oy ^ 8 ^ (16 * s)]);
+                    adq[s] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                }
+                const bf16x4 lo = tr16(As + (xlo ^ (32 * b)) + 16 * K * s);
+                const bf16x4 hi = tr16(As + (xhi ^ (32 * b)) + 16 * K * s);
+                bzq[t] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            };
+            constexpr int NT = kTile / 16 * (K / 32);
+            ld(0);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                if (t + 1 < NT) ld(t + 1);
+                dw[t & 3] = mfma(adq[t >> 2], bzq[t], dw[t & 3]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        PROBE(6);
+        __syncthreads();   // As / DsT / Ys / Dz are rewritten / stored by the next tile
+        PROBE(7);
+    }
+    PROBE_END;
+    if (blockIdx.x < ntiles)   // the last tile's dz rows
+        flush_dz((size_t)(blockIdx.x + (ntiles - 1 - blockIdx.x) / gridDim.x * gridDim.x) * kTile);
+    if constexpr (STATS) {
+        // channel kz: the two lane halves (rows 4h..), then row block 1 handed to row block 0
+        const double s1 = (double)st1 + (double)__shfl_xor(st1, 32);
+        const double s2 = (double)st2 + (double)__shfl_xor(st2, 32);
+        double* xs = reinterpret_cast<double*>(DsT);
+        if (rbz == 1 && h == 0) {
+            xs[((wave & 3) * 32 + r32) * 2] = s1;
+            xs[((wave & 3) * 32 + r32) * 2 + 1] = s2;
+        }
+        __syncthreads();
+        if (rbz == 0 && h == 0) {
+            p.stats[(size_t)blockIdx.x * 2 * K + kz] = s1 + xs[(wave * 32 + r32) * 2];
+            p.stats[(size_t)blockIdx.x * 2 * K + K + kz] = s2 + xs[(wave * 32 + r32) * 2 + 1];
+        }
+    }
+    // dW3 partial: element (b, i) = dW[n][k], n = 32w + (i&3) + 8(i>>2) + 4h, k = 32b + r32
+    float* out = p.dwpart + (size_t)blockIdx.x * N * K;
+#pragma unroll
+    for (int b = 0; b < K / 32; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int n = wave * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+            out[(size_t)n * K + 32 * b + r32] = dw[b][i];
+        }
+}
+
 // The middle layer's backward in one pass (sa_dy2_fused_kernel), after the pooled layer's
 // (which produced dz2 and this layer's BN-backward coefficients cA2 / cB2 / cC2):
 //   per 64-row tile:  z1 = relu(a1*y1 + b1) -> LDS (and raw y1 for the statistics)
@@ -805,16 +1131,18 @@ extern "C" void ov3d_sa_probe_set(unsigned long long* dbg) {
 
 extern "C" int ov3d_sa_dy_fused(const void* yprev, const float* scale, const float* shift,
                                 const void* W, int R, int K, int N, int S, const float* gsel,
-                                const uint8_t* isel, const float* cA, const float* cB,
-                                const float* cC, void* dz, float* dwpart, const float* mean,
-                                const float* invstd, double* stats, int nwg, void* stream) {
+                                const uint8_t* isel, const float* ysel, const float* cA,
+                                const float* cB, const float* cC, void* dz, float* dwpart,
+                                const float* mean, const float* invstd, double* stats, int nwg,
+                                void* stream) {
     if (!ov3d_sa_dy_fused_supported(K, N) || R <= 0 || R % kTile || (S != 32 && S != 64) ||
-        !yprev || !scale || !shift || !W || !gsel || !isel || !cA || !cB || !cC || !dz ||
+        !yprev || !scale || !shift || !W || !gsel || !isel || !ysel || !cA || !cB || !cC || !dz ||
         !dwpart || nwg <= 0 || (stats && (!mean || !invstd)))
         return OV3D_EINVAL;
-    DyFusedArgs a{(const bf16*)yprev, scale, shift, (const bf16*)W, R, S, gsel, isel, cA, cB, cC,
-                  (bf16*)dz, dwpart, mean, invstd, stats};
+    DyFusedArgs a{(const bf16*)yprev, scale, shift, (const bf16*)W, R, S, gsel, isel, ysel, cA, cB,
+                  cC, (bf16*)dz, dwpart, mean, invstd, stats};
     static const bool four_env = getenv("OV3D_SA_DY4") != nullptr;   // A/B: the 4-wave kernel
+    static const bool dy8_env = getenv("OV3D_SA_DY8") != nullptr;    // A/B: the round-4 8-wave kernel
     // sa_dy8 addresses the previous layer's rows through a buffer resource with 32-bit tile
     // offsets (num_records clamped to 2^31 - 1 bytes): past that the loads would return zeros.
     // The 4-wave kernel indexes with 64-bit addresses, so larger inputs go there.
@@ -826,11 +1154,18 @@ extern "C" int ov3d_sa_dy_fused(const void* yprev, const float* scale, const flo
         else
             hipLaunchKernelGGL((sa_dy_fused_kernel<128, 256, false>), dim3(nwg), dim3(kThreads), 0,
                                ov3d_stream(stream), a);
+    } else if (dy8_env) {
+        if (stats)
+            hipLaunchKernelGGL((sa_dy8_kernel<128, 256, true>), dim3(nwg), dim3(512), 0,
+                               ov3d_stream(stream), a);
+        else
+            hipLaunchKernelGGL((sa_dy8_kernel<128, 256, false>), dim3(nwg), dim3(512), 0,
+                               ov3d_stream(stream), a);
     } else if (stats) {
-        hipLaunchKernelGGL((sa_dy8_kernel<128, 256, true>), dim3(nwg), dim3(512), 0,
+        hipLaunchKernelGGL((sa_dy9_kernel<128, 256, true>), dim3(nwg), dim3(512), 0,
                            ov3d_stream(stream), a);
     } else {
-        hipLaunchKernelGGL((sa_dy8_kernel<128, 256, false>), dim3(nwg), dim3(512), 0,
+        hipLaunchKernelGGL((sa_dy9_kernel<128, 256, false>), dim3(nwg), dim3(512), 0,
                            ov3d_stream(stream), a);
     }
     OV3D_LAUNCH_CHECK();

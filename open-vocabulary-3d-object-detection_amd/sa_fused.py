@@ -244,7 +244,7 @@ class _SAMLPPool(Function):
             # + layer 2's ReLU + BN backward partials (the stats pass over dz2 and y2)
             parts2 = torch.empty((nwg, 2, c2), dtype=torch.float64, device=dev) \
                 if FUSED_STATS else None
-            nat.call("ov3d_sa_dy_fused", y2, a2, s2, w3b, R, c2, c3, S, gsel, isel, cA, cB, cC, dz2,
+            nat.call("ov3d_sa_dy_fused", y2, a2, s2, w3b, R, c2, c3, S, gsel, isel, ysel, cA, cB, cC, dz2,
                      part, m2, i2, parts2, nwg, like=dout)
             dw3 = _colsum(part)
             del part

@@ -124,7 +124,7 @@ def test_round5_entries_reject_bad_arguments():
     assert lib.ov3d_conv3x3_gemm256(None, 2, 9, 9, 64, p, 576, None, 0, None, 0, p, 64, 64, 1,
                                     None) == -1
     assert lib.ov3d_sa_dy_fused(None, None, None, None, 1 << 23, 128, 256, 64, None, None, None,
-                                None, None, None, None, None, None, None, 1, None) == -1
+                                None, None, None, None, None, None, None, None, 1, None) == -1
     # the fused attention pool: shape limits, strides and alignment
     assert lib.ov3d_attnpool_fused_supported(81, 2560, 40) == 1
     assert lib.ov3d_attnpool_fused_supported(96, 2560, 40) == 0      # ntok + 1 > 96

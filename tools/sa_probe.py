@@ -1,4 +1,5 @@
-"""Phase stamps of the SA layer-3 backward kernel (sa_dy8_kernel; OV3D_SA_DY4=1: the 4-wave
+"""Phase stamps of the SA layer-3 backward kernel (sa_dy9_kernel; OV3D_SA_DY8=1: sa_dy8_kernel,
+OV3D_SA_DY4=1: the 4-wave
 sa_dy_fused_kernel) on the GPU.
 
     python tools/sa_probe.py build     # (CPU) tools/probe/libov3d_saprobe.so, sa_bwd.hip with -DOV3D_SA_PROBE
@@ -16,7 +17,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "open-vocabulary-3d-object-detection_amd", "csrc")
-OUT = os.path.join(ROOT, "tools", "probe")
+OUT = os.path.join(ROOT, "tools", "saprobe")   # travels to the GPU box (tools/probe does not)
 LIB = os.path.join(OUT, "libov3d_saprobe.so")
 PHASES = ["loop", "prologue", "barrier1", "y3+dy3", "barrier2", "dz+stats", "dW", "barrier3"]
 
@@ -28,7 +29,8 @@ def build():
     subprocess.run(["/opt/rocm/bin/hipcc", *flags, "-DOV3D_SA_PROBE", "-c",
                     os.path.join(CSRC, "sa_bwd.hip"), "-o", obj], check=True)
     others = [o for o in glob.glob(os.path.join(CSRC, "*.o")) if not o.endswith("sa_bwd.o")]
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-o", LIB, obj, *others],
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-o", LIB, obj, *others,
+                    "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib", "-lhipblaslt"],
                    check=True)
     print("built", LIB)
 
