@@ -192,10 +192,13 @@ int ov3d_sa_layer_fwd_x0(const float* x0, const float* W1, const float* scale, c
                          int nparts, void* stream);
 /* last layer + pool: as ov3d_sa_layer_fwd but y is not stored; per centroid (S rows,
  * S in {32,64}) and channel: max/min of y (bf16 values) and their rows. */
+/* gamma (N) or NULL: the layer's BN weight.  Given, a channel with gamma >= 0 gets only its
+ * max (pmax, imax) and one with gamma < 0 only its min (pmin, imin), the one extreme
+ * ov3d_sa_pool_fwd reads (a = gamma * invstd has gamma's sign); NULL: both. */
 int ov3d_sa_layer_pool_fwd(const void* yprev, const float* scale, const float* shift,
                            const void* W, int R, int K, int N, int S, void* zout, float* pmax,
-                           float* pmin, uint8_t* imax, uint8_t* imin, double* partials,
-                           int nparts, void* stream);
+                           float* pmin, uint8_t* imax, uint8_t* imin, const float* gamma,
+                           double* partials, int nparts, void* stream);
 /* backward of the last layer: recompute y, dy = cA*g + cB*y + cC with g = gsel at
  * row isel of each centroid (0 elsewhere) -> dyout (R,N) bf16. */
 int ov3d_sa_layer_dy(const void* yprev, const float* scale, const float* shift, const void* W,

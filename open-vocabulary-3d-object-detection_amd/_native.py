@@ -36,7 +36,7 @@ _SIGS = {
     "ov3d_sa_l1_fwd_cin": "pipiippip",
     "ov3d_sa_layer_fwd": "ppppiiipppip",
     "ov3d_sa_layer_fwd_x0": "pppppiiippip",
-    "ov3d_sa_layer_pool_fwd": "ppppiiiippppppip",
+    "ov3d_sa_layer_pool_fwd": "ppppiiiipppppppip",
     "ov3d_sa_layer_dy": "ppppiiiippppppip",
     "ov3d_reduce_partials": "piipp",
     "ov3d_reduce_partials_f32": "piipp",

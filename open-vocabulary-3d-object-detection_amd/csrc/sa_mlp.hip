@@ -18,10 +18,17 @@
 //     non-increasing for a < 0, also after rounding), max_s relu(a*y_s + b) ==
 //     relu(a * (a >= 0 ? max_s y : min_s y) + b): the last layer's activations
 //     are never written (2^20 x 256 values per step).
+//     MODE_POOL1: MODE_POOL given the sign of the layer's BN weight (the sign of a = gamma *
+//                 invstd, known before the statistics): a channel needs only one extreme,
+//                 so y is negated where gamma < 0 and one max (value, first row) is kept;
+//                 the sums of the negated values are negated back once (exact), the squares
+//                 are unchanged: the same bits as MODE_POOL's chosen extreme and partials.
 //     MODE_DY   : backward recompute of y_k fused with the BN backward:
 //                 dy = cA*g + cB*y + cC, g = pooled gradient at the arg row.
 // BN statistics are reduced per workgroup (fp32 per lane over its rows, fp64
 // across lanes / workgroups) and finalised on the device.
+#include <limits.h>
+
 #include "common.h"
 
 namespace {
@@ -30,9 +37,24 @@ typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+#ifdef OV3D_SA_PROBE
+// diagnostic build only (tools/sa_probe.py fwd): per-wave s_memtime totals of the layer
+// kernel's tile phases (MODE_POOL launches)
+__device__ unsigned long long* g_sal_probe;
+#define LPROBE_DECL unsigned long long pr_t = __builtin_amdgcn_s_memtime(), pr_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define LPROBE(i) do { if (MODE == MODE_POOL || MODE == MODE_POOL1) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); pr_acc[i] += t_ - pr_t; pr_t = t_; } } while (0)
+#define LPROBE_END do { if ((MODE == MODE_POOL || MODE == MODE_POOL1) && (threadIdx.x & 63) == 0 && g_sal_probe) { \
+    unsigned long long* o_ = g_sal_probe + ((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8; \
+    for (int i_ = 0; i_ < 8; ++i_) o_[i_] = pr_acc[i_]; } } while (0)
+#else
+#define LPROBE_DECL
+#define LPROBE(i) do { } while (0)
+#define LPROBE_END do { } while (0)
+#endif
+
 constexpr int kTile = 64;      // rows per tile
 constexpr int kThreads = 256;  // 4 waves
-enum { MODE_STORE = 0, MODE_POOL = 1, MODE_DY = 2 };
+enum { MODE_STORE = 0, MODE_POOL = 1, MODE_DY = 2, MODE_POOL1 = 3 };
 
 __device__ __forceinline__ float relu_bn(float a, float y, float b) { return fmaxf(fmaf(a, y, b), 0.f); }
 
@@ -58,6 +80,7 @@ struct LayerArgs {
     uint8_t* imin;
     const float* gsel;     // MODE_DY: (P, N) pooled gradient after the ReLU mask
     const uint8_t* isel;   // (P, N) row of the pooled value within its centroid
+    const float* gamma;    // MODE_POOL1: (N) the layer's BN weight (its sign picks the extreme)
     const float* cA;       // (N) dy = cA*g + cB*y + cC
     const float* cB;
     const float* cC;
@@ -100,6 +123,10 @@ __global__ __launch_bounds__(kThreads, 2) void sa_layer_kernel(LayerArgs p) {
     float ssum[NB], ssq[NB];
 #pragma unroll
     for (int cb = 0; cb < NB; ++cb) ssum[cb] = ssq[cb] = 0.f;
+    uint32_t fm[NB];   // MODE_POOL1: sign mask of this lane's columns (gamma < 0: negated)
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb)
+        fm[cb] = (MODE == MODE_POOL1 && p.gamma[wave * (N / 4) + cb * 32 + r32] < 0.f) ? 0x80000000u : 0u;
     float cA[NB], cB[NB], cC[NB];
     if constexpr (MODE == MODE_DY) {
 #pragma unroll
@@ -137,8 +164,10 @@ __global__ __launch_bounds__(kThreads, 2) void sa_layer_kernel(LayerArgs p) {
         if (tid < 3 * kTile / 4) reinterpret_cast<float4*>(x0s)[tid] = prex;
         __syncthreads();
     }
+    LPROBE_DECL
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const size_t row0 = (size_t)tile * kTile;
+        LPROBE(0);
         // prologue: previous layer's BN + ReLU of the prefetched rows, to bf16, into LDS
         // (and optionally HBM)
 #pragma unroll
@@ -156,7 +185,9 @@ __global__ __launch_bounds__(kThreads, 2) void sa_layer_kernel(LayerArgs p) {
             *reinterpret_cast<bf16x8*>(&As[row * LDK + kc]) = z;
             if (p.zout) *reinterpret_cast<bf16x8*>(p.zout + (row0 + row) * K + kc) = z;
         }
+        LPROBE(1);
         __syncthreads();
+        LPROBE(2);
         if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);   // in flight during the MFMAs
         f32x16 acc[2][NB];
 #pragma unroll
@@ -179,7 +210,9 @@ __global__ __launch_bounds__(kThreads, 2) void sa_layer_kernel(LayerArgs p) {
             if (tid < 3 * kTile / 4 && tile + (int)gridDim.x < ntiles)
                 reinterpret_cast<float4*>(x0s)[tid] = prex;
         }
+        LPROBE(3);
         __syncthreads();   // As (and x0s) are rewritten by the next tile's prologue
+        LPROBE(4);
 
         // epilogue: element (rb, cb, i) is row rb*32 + (i&3) + 8*(i>>2) + 4h, column n
 #pragma unroll
@@ -241,6 +274,50 @@ __global__ __launch_bounds__(kThreads, 2) void sa_layer_kernel(LayerArgs p) {
                         }
                     }
                 }
+            } else if constexpr (MODE == MODE_POOL1) {
+                // one integer max per row block, no compare / select chain: the flipped value's
+                // bits made order-preserving as an int (t, low 16 bits zero: bf16 values), plus
+                // 63 - row in the low bits, so ties go to the first row
+                int key[2];
+#pragma unroll
+                for (int rb = 0; rb < 2; ++rb) {
+                    key[rb] = INT_MIN;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {       // row rb*32 + (i&3) + 8(i>>2) + 4h
+                        const uint32_t u = __builtin_bit_cast(uint32_t, (float)(bf16)acc[rb][cb][i]) ^ fm[cb];
+                        const float f = __builtin_bit_cast(float, u);
+                        ssum[cb] += f;
+                        ssq[cb] = fmaf(f, f, ssq[cb]);
+                        const int t = (int)(u ^ ((uint32_t)((int)u >> 31) & 0x7fff0000u));
+                        key[rb] = max(key[rb], t + (63 - rb * 32 - (i & 3) - 8 * (i >> 2)) - 4 * h);
+                    }
+                    key[rb] = max(key[rb], (int)xor32((uint32_t)key[rb], h));
+                }
+                float mx[2];
+                int imx[2];
+#pragma unroll
+                for (int rb = 0; rb < 2; ++rb) {
+                    const int t = key[rb] & (int)0xffff0000;
+                    mx[rb] = __builtin_bit_cast(float, (uint32_t)t ^ ((uint32_t)(t >> 31) & 0x7fff0000u));
+                    imx[rb] = 63 - (key[rb] & 63);
+                }
+                if (h == 0) {
+                    float* pv = fm[cb] ? p.pmin : p.pmax;
+                    uint8_t* pi = fm[cb] ? p.imin : p.imax;
+                    if (p.S == 64) {
+                        const int c0 = key[1] > key[0] ? 1 : 0;
+                        const size_t o = (size_t)tile * N + n;
+                        pv[o] = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, mx[c0]) ^ fm[cb]);
+                        pi[o] = (uint8_t)imx[c0];
+                    } else {   // S == 32: one centroid per row block
+#pragma unroll
+                        for (int rb = 0; rb < 2; ++rb) {
+                            const size_t o = ((size_t)tile * 2 + rb) * N + n;
+                            pv[o] = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, mx[rb]) ^ fm[cb]);
+                            pi[o] = (uint8_t)(imx[rb] - 32 * rb);
+                        }
+                    }
+                }
             } else {   // MODE_DY
 #pragma unroll
                 for (int rb = 0; rb < 2; ++rb) {
@@ -258,12 +335,15 @@ __global__ __launch_bounds__(kThreads, 2) void sa_layer_kernel(LayerArgs p) {
                 }
             }
         }
+        LPROBE(5);
     }
+    LPROBE_END;
 
     if constexpr (MODE != MODE_DY) {
         // per-column totals of this workgroup: both lane halves hold the same column
 #pragma unroll
         for (int cb = 0; cb < NB; ++cb) {
+            ssum[cb] = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, ssum[cb]) ^ fm[cb]);
             const double s = (double)ssum[cb] + (double)__shfl_xor(ssum[cb], 32);
             const double q = (double)ssq[cb] + (double)__shfl_xor(ssq[cb], 32);
             if (h == 0) {
@@ -823,10 +903,17 @@ extern "C" int ov3d_sa_layer_fwd_x0(const float* x0, const float* W1, const floa
     return OV3D_OK;
 }
 
+#ifdef OV3D_SA_PROBE
+extern "C" void ov3d_sal_probe_set(unsigned long long* dbg) {
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sal_probe), &dbg, sizeof(dbg));
+}
+#endif
+
 extern "C" int ov3d_sa_layer_pool_fwd(const void* yprev, const float* scale, const float* shift,
                                       const void* W, int R, int K, int N, int S, void* zout,
                                       float* pmax, float* pmin, uint8_t* imax, uint8_t* imin,
-                                      double* partials, int nparts, void* stream) {
+                                      const float* gamma, double* partials, int nparts,
+                                      void* stream) {
     if (R < 0 || R % kTile || (S != 32 && S != 64) || !yprev || !scale || !shift || !W || !pmax ||
         !pmin || !imax || !imin || !partials || nparts <= 0)
         return OV3D_EINVAL;
@@ -843,6 +930,8 @@ extern "C" int ov3d_sa_layer_pool_fwd(const void* yprev, const float* scale, con
     a.pmin = pmin;
     a.imax = imax;
     a.imin = imin;
+    a.gamma = gamma;
+    if (gamma) return launch_layer<MODE_POOL1>(a, K, N, nparts, ov3d_stream(stream));
     return launch_layer<MODE_POOL>(a, K, N, nparts, ov3d_stream(stream));
 }
 

@@ -42,6 +42,9 @@ NPARTS_POOL = 1024    # pooled-gradient pass: 16 centroids per thread at P = 163
 # last layer's backward in one pass (csrc/sa_bwd.hip): one persistent workgroup per CU
 FUSED_BWD = os.environ.get("OV3D_SA_FUSED_BWD", "1") != "0"
 NWG_DY_FUSED = int(os.environ.get("OV3D_SA_DY_NWG", "256"))
+# layer 3's pooling tracks one extreme per channel, chosen by the sign of its BN weight
+# (OV3D_SA_POOL_BOTH=1: both, as before round 5)
+POOL_ONE_EXTREME = os.environ.get("OV3D_SA_POOL_BOTH", "0") == "0"
 FUSED_STATS = os.environ.get("OV3D_SA_FUSED_STATS", "1") != "0"   # + layer 2's BN-bwd stats
 
 
@@ -207,8 +210,10 @@ class _SAMLPPool(Function):
         pmax, pmin = (torch.empty((P, c3), dtype=torch.float32, device=dev) for _ in range(2))
         imax, imin = (torch.empty((P, c3), dtype=torch.uint8, device=dev) for _ in range(2))
         parts = torch.empty((NPARTS_LAYER, 2, c3), dtype=torch.float64, device=dev)
+        # the BN weight's sign picks each channel's extreme (POOL_ONE_EXTREME; None: both)
+        g3s = g3.detach().float().contiguous() if (POOL_ONE_EXTREME and g3 is not None) else None
         nat.call("ov3d_sa_layer_pool_fwd", y2, st2[2], st2[3], w3b, R, c2, c3, S, z2, pmax, pmin,
-                 imax, imin, parts, NPARTS_LAYER, like=x0)
+                 imax, imin, g3s, parts, NPARTS_LAYER, like=x0)
         st3 = _bn_stats(parts, NPARTS_LAYER, c3, groups[2], R * world[2], bns[2])
         out = torch.empty((P, c3), dtype=torch.float32, device=dev)
         ysel = torch.empty((P, c3), dtype=torch.float32, device=dev)

@@ -63,8 +63,8 @@ def test_pool_kernel_max_min_rows(cuda, S):
     imax, imin = (torch.empty(P, N, dtype=torch.uint8, device=cuda) for _ in range(2))
     parts = torch.empty(32, 2, N, dtype=torch.float64, device=cuda)
     z = torch.empty(R, K, dtype=torch.bfloat16, device=cuda)
-    nat.call("ov3d_sa_layer_pool_fwd", y, sc, sh, W, R, K, N, S, z, pmax, pmin, imax, imin, parts,
-             32, like=y)
+    nat.call("ov3d_sa_layer_pool_fwd", y, sc, sh, W, R, K, N, S, z, pmax, pmin, imax, imin, None,
+             parts, 32, like=y)
     yf = (z.float() @ W.float().t()).to(torch.bfloat16).float().view(P, S, N)
     assert _rel(pmax, yf.max(1).values) < 8e-3
     assert _rel(pmin, yf.min(1).values) < 8e-3
@@ -74,6 +74,38 @@ def test_pool_kernel_max_min_rows(cuda, S):
     assert (at_max - pmax).abs().max().item() <= 0.02 * pmax.abs().max().item()
     assert (at_min - pmin).abs().max().item() <= 0.02 * pmin.abs().max().item()
     assert int(imax.max()) < S and int(imin.max()) < S
+
+
+@pytest.mark.parametrize("S", [64, 32])
+def test_pool_one_extreme_equals_both(cuda, S):
+    """Given the BN weight, the layer-3 pool kernel keeps only the extreme its sign selects
+    (MODE_POOL1): those values, rows and the BN partial sums are the bits the two-extreme
+    kernel produces."""
+    from ov3d_amd import _native as nat
+    g = torch.Generator(device="cpu").manual_seed(3)
+    R, K, N = 64 * 256, 128, 256
+    y = torch.randn(R, K, generator=g).to(torch.bfloat16).to(cuda)
+    sc = torch.rand(K, generator=g).to(cuda) + 0.5
+    sh = torch.randn(K, generator=g).to(cuda) * 0.1
+    W = (torch.randn(N, K, generator=g) * 0.1).to(torch.bfloat16).to(cuda)
+    gamma = torch.randn(N, generator=g).to(cuda)
+    gamma[:8] = 0.0
+    gamma[8:16] = -0.0
+    P = R // S
+    out = []
+    for gm in (None, gamma):
+        pmax, pmin = (torch.full((P, N), float("nan"), device=cuda) for _ in range(2))
+        imax, imin = (torch.full((P, N), 255, dtype=torch.uint8, device=cuda) for _ in range(2))
+        parts = torch.empty(64, 2, N, dtype=torch.float64, device=cuda)
+        nat.call("ov3d_sa_layer_pool_fwd", y, sc, sh, W, R, K, N, S, None, pmax, pmin, imax, imin,
+                 gm, parts, 64, like=y)
+        out.append((pmax, pmin, imax, imin, parts))
+    up = ~(gamma < 0)        # ov3d_sa_pool_fwd's a >= 0 (a = gamma * invstd)
+    (amx, amn, aix, ain, ap), (bmx, bmn, bix, bin_, bp) = out
+    assert torch.equal(torch.where(up, amx, amn), torch.where(up, bmx, bmn))
+    assert torch.equal(torch.where(up, aix, ain), torch.where(up, bix, bin_))
+    assert torch.equal(ap, bp)
+    assert int(up.sum()) not in (0, N)
 
 
 def _sa_copies(cuda, n, seed=0):

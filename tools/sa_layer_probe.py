@@ -38,7 +38,7 @@ def main():
                 res.append(("store", us, R * (2 * K + 2 * K + 2 * N)))
             else:
                 f = lambda: nat.call("ov3d_sa_layer_pool_fwd", y, sc, sh, W, R, K, N, S, z, pmax, pmin,  # noqa
-                                     imax, imin, parts, nparts, like=y)
+                                     imax, imin, None, parts, nparts, like=y)
                 us = t(f, 10)
                 res.append(("pool", us, R * (2 * K + 2 * K)))
                 f = lambda: nat.call("ov3d_sa_layer_dy", y, sc, sh, W, R, K, N, S, gsel, imax, cA, cB, cC,  # noqa
