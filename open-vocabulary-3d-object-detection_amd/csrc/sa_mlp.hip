@@ -144,6 +144,16 @@ __global__ __launch_bounds__(kThreads, 2) void sa_layer_kernel(LayerArgs p) {
     // MFMA phase and epilogue run (CH 16-byte chunks per thread)
     constexpr int CH = kTile * K / 8 / kThreads;
     static_assert(CH * kThreads * 8 == kTile * K, "tile chunks");
+    // a thread's chunks all start at channel kc0 (kThreads % (K / 8) == 0): its 8 BN
+    // coefficients are read from LDS once, not per chunk and tile
+    static_assert(kThreads % (K / 8) == 0, "chunk channel fixed per thread");
+    const int kc0 = (tid % (K / 8)) * 8;
+    float scv[8], shv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        scv[j] = sc[kc0 + j];
+        shv[j] = sh[kc0 + j];
+    }
     bf16x8 pre[X0 ? 1 : CH];
     float4 prex = make_float4(0.f, 0.f, 0.f, 0.f);   // X0: 16 bytes of the tile's 768 B of x0
     auto fetch = [&](int tile) {
@@ -180,7 +190,7 @@ __global__ __launch_bounds__(kThreads, 2) void sa_layer_kernel(LayerArgs p) {
                 float yv;
                 if constexpr (X0) yv = l1_value(&w1s[3 * (kc + j)], &x0s[3 * row]);
                 else yv = (float)pre[c][j];
-                z[j] = (bf16)relu_bn(sc[kc + j], yv, sh[kc + j]);
+                z[j] = (bf16)relu_bn(scv[j], yv, shv[j]);
             }
             *reinterpret_cast<bf16x8*>(&As[row * LDK + kc]) = z;
             if (p.zout) *reinterpret_cast<bf16x8*>(p.zout + (row0 + row) * K + kc) = z;
