@@ -620,7 +620,9 @@ __device__ __forceinline__ int zsw(int r) { return ((r & 3) << 2) | ((r >> 2) & 
 // value comes from the pooled y3 (ysel, the forward's value at that row, which the recompute
 // reproduces bit for bit): one 2-byte LDS write per lane over the 8-byte row stores.
 // Same roles per wave and output layouts as sa_dy8; the statistics are summed over a lane's
-// rows in a different order (fp32 per lane, fp64 across lanes and workgroups).
+// rows in a different order: fp32 over a tile's 16 rows, fp64 across tiles, lanes and
+// workgroups (a lane sees 16x the rows sa_dy8's did: fp32 across tiles lost precision on the
+// near-cancelling sum of dt).
 template <int K, int N, bool STATS>
 __global__ __launch_bounds__(512, 1) void sa_dy9_kernel(DyFusedArgs p) {
     constexpr int T8 = 512;
@@ -667,7 +669,7 @@ __global__ __launch_bounds__(512, 1) void sa_dy9_kernel(DyFusedArgs p) {
     }
     const int ny = wave * 32 + r32;   // y3 column / dW3 row of this lane
     const float cA = p.cA[ny], cB = p.cB[ny], cC = p.cC[ny];
-    float st1 = 0.f, st2 = 0.f;
+    double st1 = 0.0, st2 = 0.0;   // fp32 over a tile's 16 rows, fp64 across tiles
     f32x16 dw[K / 32];
 #pragma unroll
     for (int b = 0; b < K / 32; ++b)
@@ -849,6 +851,7 @@ __global__ __launch_bounds__(512, 1) void sa_dy9_kernel(DyFusedArgs p) {
             }
             // element i: row rbz*32 + (i&3) + 8(i>>2) + 4h of channel kz
             bf16* dzl = &Dz[(rbz * 32 + 4 * h) * K + kz];
+            float t1 = 0.f, t2 = 0.f;
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const bf16 o = (bf16)acc[i];
@@ -856,9 +859,13 @@ __global__ __launch_bounds__(512, 1) void sa_dy9_kernel(DyFusedArgs p) {
                 if constexpr (STATS) {   // bn_relu_bwd pass 0 on the stored value
                     const float yy = (float)yq[i >> 3][i & 7];
                     const float dt = fmaf(zsc, yy, zsh) > 0.f ? (float)o : 0.f;
-                    st1 += dt;
-                    st2 = fmaf(dt, (yy - zmu) * zis, st2);
+                    t1 += dt;
+                    t2 = fmaf(dt, (yy - zmu) * zis, t2);
                 }
+            }
+            if constexpr (STATS) {
+                st1 += (double)t1;
+                st2 += (double)t2;
             }
         }
         PROBE(5);
@@ -895,8 +902,8 @@ __global__ __launch_bounds__(512, 1) void sa_dy9_kernel(DyFusedArgs p) {
         flush_dz((size_t)(blockIdx.x + (ntiles - 1 - blockIdx.x) / gridDim.x * gridDim.x) * kTile);
     if constexpr (STATS) {
         // channel kz: the two lane halves (rows 4h..), then row block 1 handed to row block 0
-        const double s1 = (double)st1 + (double)__shfl_xor(st1, 32);
-        const double s2 = (double)st2 + (double)__shfl_xor(st2, 32);
+        const double s1 = st1 + __shfl_xor(st1, 32);
+        const double s2 = st2 + __shfl_xor(st2, 32);
         double* xs = reinterpret_cast<double*>(DsT);
         if (rbz == 1 && h == 0) {
             xs[((wave & 3) * 32 + r32) * 2] = s1;
@@ -1119,6 +1126,231 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy2_fused_kernel(Dy2Args p) {
         }
 }
 
+// (Opt-in, OV3D_SA_DY2B=1; one workgroup per CU.)  With two co-resident workgroups per CU its
+// gradients differ run to run (tools/sa_bwd_check.py: dW2 / dW1 off by ~1e-2; one per CU they
+// equal sa_dy2_fused's to every printed digit); the cause is not found yet.
+// sa_dy2_fused restructured as sa_dy9: dz1 computed transposed (dy2 rows as the A operand), so
+// a lane holds ONE layer-1 channel (kz = kbase + r32) of 16 rows and the layer-1 statistics
+// partials are 2 registers instead of 32; the dz1 tile is staged in LDS (Dz) and stored as
+// 16-byte rows by the next tile's prologue; the per-thread BN coefficients of the prologue are
+// read once; operands are read ahead of their MFMAs.  The registers fit two workgroups per CU
+// (sa_dy2_fused needed ~300 with its AGPRs: one 4-wave workgroup per CU).  LDS images:
+//   As, Ys (z1, raw y1; 64 rows x 64): 48-dword rows, read transposed (4 rows x 16 dwords per
+//       32 lanes -> disjoint bank windows) by the dW2 B operand / the statistics;
+//   Ds (dy2; 64 rows x 128): unpadded, 16-byte pieces swizzled by zsw(row) as sa_dy9's As: row
+//       reads (dz1 A operand) and transposed reads (dW2 A operand) both conflict-free.
+template <int K, int N, bool X0>
+__global__ __launch_bounds__(kThreads, 2) void sa_dy2b_kernel(Dy2Args p) {
+    static_assert(K == 64 && N == 128, "4 waves = 2 x 2 dz tiles, 32 dW rows each");
+    constexpr int LDA = K + 32;
+    __shared__ __attribute__((aligned(16))) bf16 As[kTile * LDA];   // z1
+    __shared__ __attribute__((aligned(16))) bf16 Ys[kTile * LDA];   // raw y1
+    __shared__ __attribute__((aligned(256))) bf16 Ds[kTile * N];    // dy2, swizzled rows
+    __shared__ __attribute__((aligned(16))) bf16 Dz[kTile * K];     // dz1 tile
+    __shared__ float w1s[X0 ? 3 * K : 1];
+    __shared__ __attribute__((aligned(16))) float x0s[X0 ? 3 * kTile : 4];   // the tile's x0 rows
+    __shared__ __attribute__((aligned(16))) float cAs[N], cBs[N], cCs[N];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r32 = lane & 31, h = lane >> 5;
+    for (int n = tid; n < N; n += kThreads) {
+        cAs[n] = p.cA[n];
+        cBs[n] = p.cB[n];
+        cCs[n] = p.cC[n];
+    }
+    if constexpr (X0)
+        for (int k = tid; k < 3 * K; k += kThreads) w1s[k] = p.W1[k];
+    // dz1 tile of this wave: rows rb*32 .. +31, channel kz of this lane
+    const int kbase = (wave & 1) * 32, rb = wave >> 1;
+    const int kz = kbase + r32;
+    constexpr int NS = N / 16;
+    bf16x8 wt[NS];   // W2 fragments (B operand of dz1 = dy2 W2): channel kz, n = 16s + 8h + j
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) wt[s][j] = p.W[(size_t)(16 * s + 8 * h + j) * K + kz];
+    const float zsc = p.a1[kz], zsh = p.b1[kz], zmu = p.mean1[kz], zis = p.invstd1[kz];
+    // a thread's prologue chunks all start at one channel: its coefficients once
+    const int kc0 = (tid % (K / 8)) * 8, nc0 = (tid % (N / 8)) * 8;
+    static_assert(kThreads % (K / 8) == 0 && kThreads % (N / 8) == 0, "chunk channel fixed");
+    float a1v[8], b1v[8], a2v[8], b2v[8];   // (the dy2 coefficients stay in LDS: registers)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        a1v[j] = p.a1[kc0 + j];
+        b1v[j] = p.b1[kc0 + j];
+        a2v[j] = p.a2[nc0 + j];
+        b2v[j] = p.b2[nc0 + j];
+    }
+    f32x16 dw[2];    // dW2 rows wave*32 .. +31, columns 0..31 / 32..63
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dw[b][i] = 0.f;
+    double st1 = 0.0, st2 = 0.0;   // fp32 over a tile's 16 rows, fp64 across tiles
+    // Ds element offsets: dz1 A operand row rb*32 + r32, piece 2s + h -> ya ^ 16s; dW2 A operand
+    // (col_operand's pattern over columns 32 wave ..): (xlo ^ 32 wave) + 16 N s, as sa_dy9
+    const int ya = (rb * 32 + r32) * N + 8 * (h ^ zsw(r32));
+    const int g4 = lane >> 4, i16 = lane & 15;
+    const int rl = 4 * (g4 >> 1) + (i16 >> 2);
+    const int kq = 2 * (g4 & 1) + ((i16 >> 1) & 1);
+    const int zl = zsw(rl), zh = zsw(rl + 8);
+    const int xlo = (rl * N + 32 * (zl >> 2) + 8 * (kq ^ (zl & 3)) + 4 * (i16 & 1)) ^ (32 * wave);
+    const int xhi = ((rl + 8) * N + 32 * (zh >> 2) + 8 * (kq ^ (zh & 3)) + 4 * (i16 & 1)) ^ (32 * wave);
+    __syncthreads();
+
+    const int ntiles = p.R / kTile;
+    constexpr int C1 = kTile * K / 8 / kThreads;   // 16-byte chunks per thread: y1, dz1
+    constexpr int C2 = kTile * N / 8 / kThreads;   // y2, dz2
+    bf16x8 py1[X0 ? 1 : C1], py2[C2], pdz[C2];
+    float4 px0 = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto fetch = [&](int tile) {
+        const size_t row0 = (size_t)tile * kTile;
+        if constexpr (X0) {
+            if (tid < 3 * kTile / 4) px0 = reinterpret_cast<const float4*>(p.x0 + row0 * 3)[tid];
+        } else {
+#pragma unroll
+            for (int c = 0; c < C1; ++c) {
+                const int ch = tid + c * kThreads, row = ch / (K / 8);
+                py1[c] = *reinterpret_cast<const bf16x8*>(p.y1 + (row0 + row) * K + kc0);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < C2; ++c) {
+            const int ch = tid + c * kThreads, row = ch / (N / 8);
+            py2[c] = *reinterpret_cast<const bf16x8*>(p.y2 + (row0 + row) * N + nc0);
+            pdz[c] = *reinterpret_cast<const bf16x8*>(p.dz2 + (row0 + row) * N + nc0);
+        }
+    };
+    auto flush_dz = [&](size_t prow0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int c = 0; c < C1; ++c) {
+            const int ch = tid + c * kThreads, row = ch / (K / 8);
+            *reinterpret_cast<bf16x8*>(p.dz1 + (prow0 + row) * K + kc0) =
+                *reinterpret_cast<const bf16x8*>(&Dz[row * K + kc0]);
+        }
+    };
+    if (blockIdx.x < ntiles) fetch(blockIdx.x);
+    if constexpr (X0) {   // x0 of the first tile -> LDS (read in the first prologue)
+        if (tid < 3 * kTile / 4) reinterpret_cast<float4*>(x0s)[tid] = px0;
+        __syncthreads();
+    }
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const size_t row0 = (size_t)tile * kTile;
+        if (tile != (int)blockIdx.x) flush_dz(row0 - (size_t)gridDim.x * kTile);
+#pragma unroll
+        for (int c = 0; c < C1; ++c) {
+            const int ch = tid + c * kThreads, row = ch / (K / 8);
+            bf16x8 y1v;
+            if constexpr (X0) {
+                const float* xr = &x0s[3 * row];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {   // sa_l1_kernel's value, bit for bit
+                    const float* w = &w1s[3 * (kc0 + j)];
+                    y1v[j] = (bf16)fmaf(w[2], xr[2], fmaf(w[1], xr[1], w[0] * xr[0]));
+                }
+            } else {
+                y1v = py1[c];
+            }
+            bf16x8 z;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) z[j] = (bf16)fmaxf(fmaf(a1v[j], (float)y1v[j], b1v[j]), 0.f);
+            *reinterpret_cast<bf16x8*>(&As[row * LDA + kc0]) = z;
+            *reinterpret_cast<bf16x8*>(&Ys[row * LDA + kc0]) = y1v;
+        }
+#pragma unroll
+        for (int c = 0; c < C2; ++c) {   // bn_relu_bwd_kernel pass 1 arithmetic
+            const int ch = tid + c * kThreads, row = ch / (N / 8);
+            bf16x8 d;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float yy = (float)py2[c][j];
+                const float dt = fmaf(a2v[j], yy, b2v[j]) > 0.f ? (float)pdz[c][j] : 0.f;
+                d[j] = (bf16)fmaf(cAs[nc0 + j], dt, fmaf(cBs[nc0 + j], yy, cCs[nc0 + j]));
+            }
+            *reinterpret_cast<bf16x8*>(&Ds[row * N + 8 * ((nc0 >> 3) ^ zsw(row))]) = d;
+        }
+        __syncthreads();
+        if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);   // in flight below
+
+        // dz1[row][k] = dy2 W2 for rows rb*32.., channel kz; A = dy2 rows, read one step ahead
+        {
+            bf16x8 aq[NS];
+            auto ld = [&](int s) __attribute__((always_inline)) {
+                aq[s] = *reinterpret_cast<const bf16x8*>(&Ds[ya ^ (16 * s)]);
+            };
+            f32x16 acc;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+            ld(0);
+            ld(1);
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                if (s + 2 < NS) ld(s + 2);
+                acc = mfma(aq[s], wt[s], acc);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            const bf16x8 yq[2] = {col_operand(Ys, LDA, lane, kbase, 2 * rb),
+                                  col_operand(Ys, LDA, lane, kbase, 2 * rb + 1)};
+            // element i: row rb*32 + (i&3) + 8(i>>2) + 4h of channel kz
+            bf16* dzl = &Dz[(rb * 32 + 4 * h) * K + kz];
+            float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const bf16 o = (bf16)acc[i];
+                dzl[((i & 3) + 8 * (i >> 2)) * K] = o;
+                const float yy = (float)yq[i >> 3][i & 7];   // bn_relu_bwd pass 0 of layer 1
+                const float dt = fmaf(zsc, yy, zsh) > 0.f ? (float)o : 0.f;
+                t1 += dt;
+                t2 = fmaf(dt, (yy - zmu) * zis, t2);
+            }
+            st1 += (double)t1;
+            st2 += (double)t2;
+        }
+        // dW2 += dy2^T z1 over the tile's rows; operands one product ahead
+        {
+            bf16x8 adq[kTile / 16], bzq[kTile / 16 * 2];
+            auto ld = [&](int t) __attribute__((always_inline)) {
+                const int s = t >> 1, b = t & 1;
+                if (b == 0) {
+                    const bf16x4 lo = tr16(Ds + xlo + 16 * N * s);
+                    const bf16x4 hi = tr16(Ds + xhi + 16 * N * s);
+                    adq[s] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                }
+                bzq[t] = col_operand(As, LDA, lane, 32 * b, s);
+            };
+            constexpr int NT = kTile / 16 * 2;
+            ld(0);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                if (t + 1 < NT) ld(t + 1);
+                dw[t & 1] = mfma(adq[t >> 1], bzq[t], dw[t & 1]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if constexpr (X0) {   // the next tile's x0 (its prologue reads it after the barrier)
+            if (tid < 3 * kTile / 4 && tile + (int)gridDim.x < ntiles)
+                reinterpret_cast<float4*>(x0s)[tid] = px0;
+        }
+        __syncthreads();   // As / Ys / Ds / Dz (and x0s) are rewritten / stored by the next tile
+    }
+    if (blockIdx.x < ntiles)   // the last tile's dz1 rows
+        flush_dz((size_t)(blockIdx.x + (ntiles - 1 - blockIdx.x) / gridDim.x * gridDim.x) * kTile);
+    {   // channel kz, rows of row block rb: the two lane halves, one slot per row block
+        const double s1 = st1 + __shfl_xor(st1, 32);
+        const double s2 = st2 + __shfl_xor(st2, 32);
+        if (h == 0) {
+            p.stats[((size_t)blockIdx.x * 2 + rb) * 2 * K + kz] = s1;
+            p.stats[((size_t)blockIdx.x * 2 + rb) * 2 * K + K + kz] = s2;
+        }
+    }
+    float* out = p.dwpart + (size_t)blockIdx.x * N * K;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int n = wave * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+            out[(size_t)n * K + 32 * b + r32] = dw[b][i];
+        }
+}
+
 }  // namespace
 
 extern "C" int ov3d_sa_dy_fused_supported(int K, int N) { return K == 128 && N == 256; }
@@ -1184,6 +1416,20 @@ extern "C" int ov3d_sa_dy2_fused(const void* y1, const float* x0, const float* W
         return OV3D_EINVAL;
     Dy2Args a{(const bf16*)y1, a1, b1, (const bf16*)y2, a2, b2, (const bf16*)dz2, cA, cB, cC,
               (const bf16*)W, mean1, invstd1, R, (bf16*)dz1, dwpart, stats, x0, W1};
+    // sa_dy2b is opt-in (OV3D_SA_DY2B=1): two co-resident workgroups per CU corrupt its results
+    // (DESIGN.md, round 5), so its launch reserves dynamic LDS that leaves one per CU
+    static const bool b_env = getenv("OV3D_SA_DY2B") != nullptr;
+    static const int lds_pad = getenv("OV3D_SA_DY2_LDSPAD") ? atoi(getenv("OV3D_SA_DY2_LDSPAD")) : 65536;
+    if (b_env) {
+        if (y1)
+            hipLaunchKernelGGL((sa_dy2b_kernel<64, 128, false>), dim3(nwg), dim3(kThreads), lds_pad,
+                               ov3d_stream(stream), a);
+        else
+            hipLaunchKernelGGL((sa_dy2b_kernel<64, 128, true>), dim3(nwg), dim3(kThreads), lds_pad,
+                               ov3d_stream(stream), a);
+        OV3D_LAUNCH_CHECK();
+        return OV3D_OK;
+    }
     if (y1)
         hipLaunchKernelGGL((sa_dy2_fused_kernel<64, 128, false>), dim3(nwg), dim3(kThreads), 0,
                            ov3d_stream(stream), a);

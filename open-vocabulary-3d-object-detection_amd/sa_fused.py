@@ -42,6 +42,8 @@ NPARTS_POOL = 1024    # pooled-gradient pass: 16 centroids per thread at P = 163
 # last layer's backward in one pass (csrc/sa_bwd.hip): one persistent workgroup per CU
 FUSED_BWD = os.environ.get("OV3D_SA_FUSED_BWD", "1") != "0"
 NWG_DY_FUSED = int(os.environ.get("OV3D_SA_DY_NWG", "256"))
+# the layer-2 backward's workgroups (one 4-wave workgroup per CU)
+NWG_DY2 = int(os.environ.get("OV3D_SA_DY2_NWG", "256"))
 # layer 3's pooling tracks one extreme per channel, chosen by the sign of its BN weight
 # (OV3D_SA_POOL_BOTH=1: both, as before round 5)
 POOL_ONE_EXTREME = os.environ.get("OV3D_SA_POOL_BOTH", "0") == "0"
@@ -271,7 +273,7 @@ class _SAMLPPool(Function):
                      parts, None, NPARTS_ROWS, None, like=dout)
         cA, cB, cC, dg2, db2 = bn_bwd_affine(parts, nparts, c2, groups[1], R * world[1], g2, m2, i2)
         if fused_bwd2:   # dy2 -> dz1, dW2 and layer 1's statistics in one pass
-            nwg2 = min(NWG_DY_FUSED, R // 64)
+            nwg2 = min(NWG_DY2, R // 64)
             dz1 = torch.empty((R, c1), dtype=bf, device=dev)
             part = torch.empty((nwg2, c2, c1), dtype=torch.float32, device=dev)
             parts, nparts = torch.empty((2 * nwg2, 2, c1), dtype=torch.float64, device=dev), \
