@@ -948,6 +948,9 @@ struct Dy2Args {
     double* stats;      // (gridDim.x, 2, K)
     const float* x0;    // X0 variant (y1 == NULL): y1 = bf16(x0 W1^T) recomputed, (R, 3)
     const float* W1;    // (K, 3)
+    int dbg;            // sa_dy2b diagnostics (OV3D_SA_DY2B_DBG bits): 1 barrier after the dz1
+                        // flush, 2 barrier between its dz1 and dW2 phases, 4 dz1 stored directly,
+                        // 8 every counter drained before the next tile's x0 rows reach LDS
 };
 
 template <int K, int N, bool X0>
@@ -1234,7 +1237,8 @@ __global__ __launch_bounds__(kThreads, 2) void sa_dy2b_kernel(Dy2Args p) {
     }
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const size_t row0 = (size_t)tile * kTile;
-        if (tile != (int)blockIdx.x) flush_dz(row0 - (size_t)gridDim.x * kTile);
+        if (tile != (int)blockIdx.x && !(p.dbg & 4)) flush_dz(row0 - (size_t)gridDim.x * kTile);
+        if (p.dbg & 1) __syncthreads();
 #pragma unroll
         for (int c = 0; c < C1; ++c) {
             const int ch = tid + c * kThreads, row = ch / (K / 8);
@@ -1295,7 +1299,8 @@ __global__ __launch_bounds__(kThreads, 2) void sa_dy2b_kernel(Dy2Args p) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const bf16 o = (bf16)acc[i];
-                dzl[((i & 3) + 8 * (i >> 2)) * K] = o;
+                if (p.dbg & 4) p.dz1[(row0 + rb * 32 + 4 * h + (i & 3) + 8 * (i >> 2)) * K + kz] = o;
+                else dzl[((i & 3) + 8 * (i >> 2)) * K] = o;
                 const float yy = (float)yq[i >> 3][i & 7];   // bn_relu_bwd pass 0 of layer 1
                 const float dt = fmaf(zsc, yy, zsh) > 0.f ? (float)o : 0.f;
                 t1 += dt;
@@ -1304,6 +1309,7 @@ __global__ __launch_bounds__(kThreads, 2) void sa_dy2b_kernel(Dy2Args p) {
             st1 += (double)t1;
             st2 += (double)t2;
         }
+        if (p.dbg & 2) __syncthreads();
         // dW2 += dy2^T z1 over the tile's rows; operands one product ahead
         {
             bf16x8 adq[kTile / 16], bzq[kTile / 16 * 2];
@@ -1326,12 +1332,13 @@ __global__ __launch_bounds__(kThreads, 2) void sa_dy2b_kernel(Dy2Args p) {
             }
         }
         if constexpr (X0) {   // the next tile's x0 (its prologue reads it after the barrier)
+            if (p.dbg & 8) __builtin_amdgcn_s_waitcnt(0);
             if (tid < 3 * kTile / 4 && tile + (int)gridDim.x < ntiles)
                 reinterpret_cast<float4*>(x0s)[tid] = px0;
         }
         __syncthreads();   // As / Ys / Ds / Dz (and x0s) are rewritten / stored by the next tile
     }
-    if (blockIdx.x < ntiles)   // the last tile's dz1 rows
+    if (blockIdx.x < ntiles && !(p.dbg & 4))   // the last tile's dz1 rows
         flush_dz((size_t)(blockIdx.x + (ntiles - 1 - blockIdx.x) / gridDim.x * gridDim.x) * kTile);
     {   // channel kz, rows of row block rb: the two lane halves, one slot per row block
         const double s1 = st1 + __shfl_xor(st1, 32);
@@ -1414,8 +1421,9 @@ extern "C" int ov3d_sa_dy2_fused(const void* y1, const float* x0, const float* W
         !a2 || !b2 || !dz2 || !cA || !cB || !cC || !W || !mean1 || !invstd1 || !dz1 || !dwpart ||
         !stats || nwg <= 0)
         return OV3D_EINVAL;
+    static const int dbg = getenv("OV3D_SA_DY2B_DBG") ? atoi(getenv("OV3D_SA_DY2B_DBG")) : 0;
     Dy2Args a{(const bf16*)y1, a1, b1, (const bf16*)y2, a2, b2, (const bf16*)dz2, cA, cB, cC,
-              (const bf16*)W, mean1, invstd1, R, (bf16*)dz1, dwpart, stats, x0, W1};
+              (const bf16*)W, mean1, invstd1, R, (bf16*)dz1, dwpart, stats, x0, W1, dbg};
     // sa_dy2b is opt-in (OV3D_SA_DY2B=1): two co-resident workgroups per CU corrupt its results
     // (DESIGN.md, round 5), so its launch reserves dynamic LDS that leaves one per CU
     static const bool b_env = getenv("OV3D_SA_DY2B") != nullptr;

@@ -16,9 +16,10 @@ def main():
     from ov3d_amd import sa_fused, synthetic
     from ov3d_amd.pointnet2_modules import PointnetSAModuleVotes
     cuda = torch.device("cuda")
+    feat = int(os.environ.get("SA_CHECK_FEATURES", "0"))   # 3: colour input (stored y1 rows)
     for nsample in (64, 32):
         torch.manual_seed(3)
-        sa = PointnetSAModuleVotes(radius=0.2, nsample=nsample, npoint=2048, mlp=[0, 64, 128, 256],
+        sa = PointnetSAModuleVotes(radius=0.2, nsample=nsample, npoint=2048, mlp=[feat, 64, 128, 256],
                                    normalize_xyz=True).to(cuda).train()
         with torch.no_grad():
             for layer in sa.mlp_module:
@@ -31,8 +32,10 @@ def main():
         for fused in (True, False, True):
             sa_fused.FUSED_BWD = fused
             twin = copy.deepcopy(sa)
+            feats = torch.rand(xyz.shape[0], feat, xyz.shape[1], device=cuda,
+                               generator=torch.Generator(device=cuda).manual_seed(5)) if feat else None
             with torch.autocast("cuda", dtype=torch.bfloat16):
-                _, f, _ = twin(xyz[..., :3].contiguous())
+                _, f, _ = twin(xyz[..., :3].contiguous(), feats)
             (f.float() * gw).sum().backward()
             res.setdefault(fused, []).append({n: p.grad.clone() for n, p in twin.named_parameters()})
         sa_fused.FUSED_BWD = True
