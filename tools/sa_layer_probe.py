@@ -7,7 +7,19 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import ov3d_import  # noqa: E402
-from wgrad_probe import t  # noqa: E402
+
+
+def t(f, n):
+    """average microseconds of f() over n launches (after one warm-up)"""
+    f()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        f()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / n
 
 
 def main():
@@ -37,8 +49,9 @@ def main():
                 us = t(f, 10)
                 res.append(("store", us, R * (2 * K + 2 * K + 2 * N)))
             else:
-                f = lambda: nat.call("ov3d_sa_layer_pool_fwd", y, sc, sh, W, R, K, N, S, z, pmax, pmin,  # noqa
-                                     imax, imin, None, parts, nparts, like=y)
+                gam = torch.randn(N, device=dev)
+                f = lambda: nat.call("ov3d_sa_layer_pool_fwd", y, sc, sh, W, R, K, N, S, None, pmax, pmin,  # noqa
+                                     imax, imin, gam, parts, nparts, like=y)
                 us = t(f, 10)
                 res.append(("pool", us, R * (2 * K + 2 * K)))
                 f = lambda: nat.call("ov3d_sa_layer_dy", y, sc, sh, W, R, K, N, S, gsel, imax, cA, cB, cC,  # noqa
@@ -46,7 +59,7 @@ def main():
                 us = t(f, 10)
                 res.append(("dy", us, R * (2 * K + 2 * N)))
             print(f"K={K} N={N} nparts={nparts}: " + "  ".join(
-                f"{m} {us:7.1f} us {b / us / 1e3:5.2f} TB/s" for m, us, b in res), flush=True)
+                f"{m} {us:7.1f} us {b / us / 1e3:7.1f} GB/s" for m, us, b in res), flush=True)
 
 
 if __name__ == "__main__":
