@@ -820,7 +820,11 @@ __global__ __launch_bounds__(512, 1) void sa_dy9_kernel(DyFusedArgs p) {
         __syncthreads();
         PROBE(4);
 
-        // dz[row][k] = dy3 W3 for rows rbz*32.., channel kz: A = dy3 rows (transposed DsT reads)
+        // dz[row][k] = dy3 W3 for rows rbz*32.., channel kz: A = dy3 rows (transposed DsT reads).
+        // Its epilogue (bf16 values to Dz, the layer-2 statistics) runs one element per dW3
+        // MFMA below, in that chain's shadow (dW3 does not depend on dz).
+        f32x16 acc;
+        bf16x8 yq[2];   // layer 2's raw rows of this lane's channel (the statistics)
         {
             bf16x8 aq[NS];
             auto ld = [&](int s) __attribute__((always_inline)) {
@@ -833,7 +837,6 @@ __global__ __launch_bounds__(512, 1) void sa_dy9_kernel(DyFusedArgs p) {
                     wt[s] = bf16x8{wl[0], wl[1], wl[2], wl[3], wh[0], wh[1], wh[2], wh[3]};
                 }
             };
-            f32x16 acc;
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[i] = 0.f;
             ld(0);
@@ -844,33 +847,15 @@ __global__ __launch_bounds__(512, 1) void sa_dy9_kernel(DyFusedArgs p) {
                 acc = mfma(aq[s], wt[s], acc);
                 __builtin_amdgcn_sched_barrier(0);
             }
-            bf16x8 yq[2];   // layer 2's raw rows of this lane's channel (the statistics)
             if constexpr (STATS) {
                 yq[0] = col_operand(Ys, LDY, lane, kbz, 2 * rbz);
                 yq[1] = col_operand(Ys, LDY, lane, kbz, 2 * rbz + 1);
             }
-            // element i: row rbz*32 + (i&3) + 8(i>>2) + 4h of channel kz
-            bf16* dzl = &Dz[(rbz * 32 + 4 * h) * K + kz];
-            float t1 = 0.f, t2 = 0.f;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const bf16 o = (bf16)acc[i];
-                dzl[((i & 3) + 8 * (i >> 2)) * K] = o;
-                if constexpr (STATS) {   // bn_relu_bwd pass 0 on the stored value
-                    const float yy = (float)yq[i >> 3][i & 7];
-                    const float dt = fmaf(zsc, yy, zsh) > 0.f ? (float)o : 0.f;
-                    t1 += dt;
-                    t2 = fmaf(dt, (yy - zmu) * zis, t2);
-                }
-            }
-            if constexpr (STATS) {
-                st1 += (double)t1;
-                st2 += (double)t2;
-            }
         }
         PROBE(5);
 
-        // dW3 rows 32w.. += dy3^T z over this tile's rows; operands two products ahead
+        // dW3 rows 32w.. += dy3^T z over this tile's rows; operands one product ahead; dz
+        // element t (row rbz*32 + (t&3) + 8(t>>2) + 4h of channel kz) beside product t
         {
             bf16x8 adq[kTile / 16], bzq[kTile / 16 * (K / 32)];
             auto ld = [&](int t) __attribute__((always_inline)) {
@@ -885,12 +870,27 @@ __global__ __launch_bounds__(512, 1) void sa_dy9_kernel(DyFusedArgs p) {
                 bzq[t] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
             };
             constexpr int NT = kTile / 16 * (K / 32);
+            static_assert(NT == 16, "one dz element per dW3 product");
+            bf16* dzl = &Dz[(rbz * 32 + 4 * h) * K + kz];
+            float t1 = 0.f, t2 = 0.f;
             ld(0);
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
                 if (t + 1 < NT) ld(t + 1);
                 dw[t & 3] = mfma(adq[t >> 2], bzq[t], dw[t & 3]);
+                const bf16 o = (bf16)acc[t];
+                dzl[((t & 3) + 8 * (t >> 2)) * K] = o;
+                if constexpr (STATS) {   // bn_relu_bwd pass 0 on the stored value
+                    const float yy = (float)yq[t >> 3][t & 7];
+                    const float dt = fmaf(zsc, yy, zsh) > 0.f ? (float)o : 0.f;
+                    t1 += dt;
+                    t2 = fmaf(dt, (yy - zmu) * zis, t2);
+                }
                 __builtin_amdgcn_sched_barrier(0);
+            }
+            if constexpr (STATS) {
+                st1 += (double)t1;
+                st2 += (double)t2;
             }
         }
         PROBE(6);
