@@ -950,7 +950,8 @@ struct Dy2Args {
     const float* W1;    // (K, 3)
     int dbg;            // sa_dy2b diagnostics (OV3D_SA_DY2B_DBG bits): 1 barrier after the dz1
                         // flush, 2 barrier between its dz1 and dW2 phases, 4 dz1 stored directly,
-                        // 8 every counter drained before the next tile's x0 rows reach LDS
+                        // 8 every counter drained before the next tile's x0 rows reach LDS,
+                        // 16 x0 rows / 32 W1 read from global memory instead of LDS
 };
 
 template <int K, int N, bool X0>
@@ -1244,10 +1245,10 @@ __global__ __launch_bounds__(kThreads, 2) void sa_dy2b_kernel(Dy2Args p) {
             const int ch = tid + c * kThreads, row = ch / (K / 8);
             bf16x8 y1v;
             if constexpr (X0) {
-                const float* xr = &x0s[3 * row];
+                const float* xr = (p.dbg & 16) ? p.x0 + (row0 + row) * 3 : &x0s[3 * row];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {   // sa_l1_kernel's value, bit for bit
-                    const float* w = &w1s[3 * (kc0 + j)];
+                    const float* w = (p.dbg & 32) ? p.W1 + 3 * (kc0 + j) : &w1s[3 * (kc0 + j)];
                     y1v[j] = (bf16)fmaf(w[2], xr[2], fmaf(w[1], xr[1], w[0] * xr[0]));
                 }
             } else {
