@@ -23,6 +23,7 @@ eager results (same kernels, same order); dropout draws from the graph-safe
 Philox generator.
 """
 import os
+import time
 
 import torch
 import torch.nn as nn
@@ -139,8 +140,16 @@ class StepGraph:
         self.opt.zero_grad(set_to_none=True)
         # with a process group the RCCL collectives are captured too; the watchdog thread of
         # the process group must not invalidate the capture ("thread_local" capture mode)
-        mode = "thread_local" if (torch.distributed.is_available()
-                                  and torch.distributed.is_initialized()) else "global"
+        pg = torch.distributed.is_available() and torch.distributed.is_initialized()
+        mode = "thread_local" if pg else "global"
+        if pg:
+            # Let the watchdog retire the warm-up's collectives before any process group's
+            # stream joins the capture.  Its polling loop sleeps ~100 ms between passes.  Once
+            # in a while (1 of ~10 full GPU suites) its query of a warm-up work's event aborted
+            # the process with "operation not permitted on an event last recorded in a
+            # capturing stream" (PG ID 1, the gradient buckets' group).
+            torch.cuda.synchronize()
+            time.sleep(0.5)
         if not self.split:
             with torch.cuda.graph(self.graph, capture_error_mode=mode):
                 self.loss = self._body(gemm)
