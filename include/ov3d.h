@@ -852,6 +852,11 @@ int ov3d_multi_copy(int n, const void* const* srcs, void* const* dsts, const lon
  * memory rows (transformer._MemoryKV) in one pass */
 int ov3d_add_cast_bf16(const void* a, int a_bf16, const float* b, long long n, void* sum, void* ac,
                        void* stream);
+/* *out = a new non-blocking HIP stream owned by the caller (never destroyed by the library).
+ * Replaces nothing in the reference (torch.cuda.Stream() hands out pool streams, which recycle):
+ * graphs.StepGraph and dist.GradBuckets use streams of their own so that no stream that carried
+ * an eager collective ever joins a graph capture (the watchdog abort). */
+int ov3d_stream_create(void** out);
 /* table[i].grad = grads[i] (host array of device pointers) by kernel arguments: graph-safe */
 int ov3d_adamw_set_grads(ov3d_adamw_tensor* table, int ntensors, float* const* grads, void* stream);
 /* hyper: DEVICE (ngroups, 2) f64 table {lr, weight_decay} per parameter group, read by the

@@ -138,7 +138,7 @@ EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_
                           "ov3d_heads_out_workspace", "ov3d_stamps_arm", "ov3d_stamps_count",
                           "ov3d_stamps_get", "ov3d_wall_clock_khz", "ov3d_linres_supported",
                           "ov3d_attnpool_fused_supported", "ov3d_lngemm_supported",
-                          "ov3d_lngemm_bwd_parts", "ov3d_lngemm_stamps_arm")
+                          "ov3d_lngemm_bwd_parts", "ov3d_lngemm_stamps_arm", "ov3d_stream_create")
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_longlong, "f": ctypes.c_float,
        "d": ctypes.c_double}
@@ -221,6 +221,8 @@ def load():
         lib.ov3d_lngemm_stamps_arm.restype = ctypes.c_int
         lib.ov3d_heads_out_workspace.argtypes = [ctypes.c_int] * 2
         lib.ov3d_heads_out_workspace.restype = ctypes.c_longlong
+        lib.ov3d_stream_create.argtypes = [ctypes.c_void_p]
+        lib.ov3d_stream_create.restype = ctypes.c_int
         lib.ov3d_version.argtypes = []
         lib.ov3d_version.restype = ctypes.c_char_p
         _lib = lib
@@ -229,6 +231,18 @@ def load():
 
 def version():
     return load().ov3d_version().decode()
+
+
+def stream_create(device):
+    """-> torch.cuda.ExternalStream over a new HIP stream of the caller's own (ov3d_stream_create):
+    unlike torch.cuda.Stream() it never comes from (or returns to) PyTorch's recycled pool.  The
+    stream lives for the process."""
+    with torch.cuda.device(device):
+        h = ctypes.c_void_p()
+        rc = load().ov3d_stream_create(ctypes.byref(h))
+        if rc != 0 or not h.value:
+            raise NativeError(f"ov3d_stream_create failed with status {rc}")
+        return torch.cuda.ExternalStream(h.value, device=device)
 
 
 def _stream(t):

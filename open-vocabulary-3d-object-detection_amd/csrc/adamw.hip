@@ -280,3 +280,14 @@ extern "C" int ov3d_multi_copy(int n, const void* const* srcs, void* const* dsts
     }
     return OV3D_OK;
 }
+
+/* A HIP stream of the caller's own (non-blocking, never handed out by PyTorch's stream pool):
+ * graphs.StepGraph / dist.GradBuckets keep the streams that join a graph capture apart from the
+ * streams that carry eager collectives (dist.dedicated_stream). */
+extern "C" int ov3d_stream_create(void** out) {
+    if (!out) return OV3D_EINVAL;
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return OV3D_ELAUNCH;
+    *out = (void*)s;
+    return OV3D_OK;
+}

@@ -74,6 +74,40 @@ def capture_safe_env():
     os.environ["TORCH_NCCL_CUDA_EVENT_CACHE"] = "0"
 
 
+_DEDICATED = {}
+
+
+def dedicated_stream(device, role):
+    """The process's stream for `role` on `device`: "eager" (StepGraph's warm-up, which issues
+    eager collectives), "capture" (the stream a step graph is captured on), "bucket_eager" /
+    "bucket_capture" (GradBuckets' side stream outside / inside a capture).
+
+    Why (round 6, tools/pg_capture_probe.py on the GPU): a blocking (async_op=False) collective
+    runs on the CURRENT stream and ProcessGroupNCCL records the work's end event there; the
+    work stays on the group's watchdog list until a watchdog pass (~100 ms apart) sees the event
+    complete.  If that stream joins a graph capture before that pass, HIP refuses the query
+    (hipErrorCapturedEvent: "operation not permitted on an event last recorded in a capturing
+    stream"), the watchdog rethrows and the process aborts.  Round 5's abort was exactly this:
+    GradBuckets' one side stream carried the warm-up's eager bucket all-reduce and then joined
+    the capture.  The probe aborts deterministically when eager works are issued from the stream
+    that is then captured (whatever group the captured collective uses) and passes when they
+    are issued from another stream.  So streams are dedicated by role: a stream that carried an
+    eager collective never joins a capture.  They are HIP streams of their own
+    (_native.stream_create), not torch.cuda.Stream() pool streams, which are recycled (32 per
+    priority) and could alias across roles."""
+    if role not in ("eager", "capture", "bucket_eager", "bucket_capture"):
+        raise ValueError(f"dedicated_stream: unknown role {role!r}")
+    device = torch.device(device)
+    if device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    key = (device.index, role)
+    s = _DEDICATED.get(key)
+    if s is None:
+        from . import _native
+        s = _DEDICATED[key] = _native.stream_create(device)
+    return s
+
+
 def init_from_env(backend=None):
     """torchrun-style init (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* in the env)."""
     if is_distributed():
@@ -240,11 +274,13 @@ class GradBuckets:
     encoder side).  Every parameter has a fixed view in ONE flat fp32 buffer (static for a
     captured step), a bucket's views are contiguous.  ``launch(i)`` copies bucket i's
     gradients into its views (one launch on the GPU) and starts ONE all-reduce (sum) of that
-    region on ``group`` — a process group of its own (its own RCCL communicator and stream), so
-    the SyncBatchNorm all-reduces the encoder / SA backward issues on the BN's group are not
+    region on ``group`` — a process group of its own (its own RCCL communicator), so the
+    SyncBatchNorm all-reduces the encoder / SA backward issues on the BN's group are not
     queued behind it.  On the GPU the collective is issued from a side stream that first waits
-    for the copy (a plain blocking-call all-reduce there: the process group's watchdog never
-    holds an event recorded inside a graph capture); the current stream runs on.  On the CPU
+    for the copy (a plain blocking-call all-reduce there: inside a capture it enqueues no work
+    on the watchdog's list); the current stream runs on.  The side stream is
+    ``dedicated_stream(.., "bucket_eager")`` outside a capture and ``"bucket_capture"`` inside
+    one, so no stream that carried an eager bucket all-reduce joins a capture.  On the CPU
     (gloo) it is an ``async_op`` work.  ``finish()`` launches what is left, joins (the current
     stream waits for the side stream: capturable) and returns {id(param): summed gradient
     view} (the caller divides by the world size).  A parameter without a gradient contributes
@@ -291,8 +327,11 @@ class GradBuckets:
             from . import _native
             if dst:
                 _native.multi_copy(dst, src)
-            if self.stream is None:
-                self.stream = torch.cuda.Stream(device=self.flat.device)
+            # inside a capture the collective goes out on a stream that never carried an eager
+            # one (dedicated_stream: an eager work's end event on a capturing stream aborts the
+            # watchdog)
+            role = "bucket_capture" if torch.cuda.is_current_stream_capturing() else "bucket_eager"
+            self.stream = dedicated_stream(self.flat.device, role)
             cur = torch.cuda.current_stream(self.flat.device)
             self.stream.wait_stream(cur)
             with torch.cuda.stream(self.stream):

@@ -23,7 +23,6 @@ eager results (same kernels, same order); dropout draws from the graph-safe
 Philox generator.
 """
 import os
-import time
 
 import torch
 import torch.nn as nn
@@ -128,7 +127,14 @@ class StepGraph:
         self.split = bool(self.prefetch and want and hasattr(model, "run_encoder"))
         self.mid_event = torch.cuda.Event() if self.split else None
         self.graph2 = None
-        self.side = torch.cuda.Stream()
+        # warm-up and capture on streams dedicated to each role (dist.dedicated_stream): the
+        # warm-up's eager collectives record their end events on the current stream, and a
+        # stream holding one the process group's watchdog has not retired yet must never join
+        # the capture (hipErrorCapturedEvent on the watchdog's query aborts the process)
+        from . import dist as _dist
+        dev = self.static["point_clouds"].device
+        self.side = _dist.dedicated_stream(dev, "eager")
+        cap = _dist.dedicated_stream(dev, "capture")
         self.side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.side):
             for _ in range(warmup_iters):
@@ -142,22 +148,13 @@ class StepGraph:
         # the process group must not invalidate the capture ("thread_local" capture mode)
         pg = torch.distributed.is_available() and torch.distributed.is_initialized()
         mode = "thread_local" if pg else "global"
-        if pg:
-            # Let the watchdog retire the warm-up's collectives before any process group's
-            # stream joins the capture.  Its polling loop sleeps ~100 ms between passes.  Once
-            # in a while (1 of ~10 full GPU suites) its query of a warm-up work's event aborted
-            # the process with "operation not permitted on an event last recorded in a
-            # capturing stream" (PG ID 1, the gradient buckets' group).
-            torch.cuda.synchronize()
-            time.sleep(0.5)
         if not self.split:
-            with torch.cuda.graph(self.graph, capture_error_mode=mode):
+            with torch.cuda.graph(self.graph, stream=cap, capture_error_mode=mode):
                 self.loss = self._body(gemm)
             return
         # split capture (the torch.cuda.graph context's steps, done by hand so the capture
         # can switch graphs in the middle of the forward)
         self.graph2 = torch.cuda.CUDAGraph()
-        cap = torch.cuda.Stream()
         torch.cuda.synchronize()
         cap.wait_stream(torch.cuda.current_stream())
         switched = []

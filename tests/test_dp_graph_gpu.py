@@ -31,3 +31,16 @@ def test_bench_dp_collectives_one_json_line():
     assert len(lines) == 1, r.stdout
     res = json.loads(lines[0])
     assert res["value"] > 0 and res["n_gpus"] == 1
+
+
+def test_capture_after_eager_collectives_on_dedicated_streams():
+    """Round 6: the watchdog abort's mechanism (tools/pg_capture_probe.py: an eager blocking
+    collective's end event sits on the stream it was issued from; if that stream joins a capture
+    before the watchdog retired the work, the watchdog's query aborts the process) and its fix
+    (dist.dedicated_stream: eager and capture roles never share a stream).  The probe issues
+    eager collectives and immediately captures the same collectives, holding the capture open
+    across ~15 watchdog passes: with the product's streams it must not abort."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pg_capture_probe.py"),
+                        "product"], capture_output=True, text=True, timeout=180, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "product: ok" in r.stdout
