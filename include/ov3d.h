@@ -426,18 +426,6 @@ int ov3d_attnpool_fused_supported(int ntok, int C, int H);
 int ov3d_attnpool_fused(const void* x, const void* t0, const void* pos, const void* a, long long sa_h,
                         long long sa_r, int R, int ntok, int C, int H, void* y, void* stream);
 
-/* conv3 + bottleneck close of the RegionCLIP ModifiedResNet as ONE library GEMM [upstream CLIP
- * Bottleneck.forward: relu(bn3(conv3(out)) + identity); clip.inference, criterion.py:397]:
- *   out (M, N) = act(x (M, K) · w (N, K)^T + bias (N) + residual (M, N)), bf16 in and out,
- *   fp32 accumulation; row-major with leading dimensions ldx, ldw, ldr, ldo (elements);
- *   hipBLASLt out-of-place C = residual, D = out, bias(+ReLU) epilogue; workspace (16-byte
- *   aligned, ws_bytes) for its stream-K algorithms.  Returns OV3D_ELAUNCH when hipBLASLt
- *   finds no algorithm or fails. */
-int ov3d_lt_gemm_bias_residual(long long M, int N, int K, const void* x, long long ldx,
-                               const void* w, long long ldw, const void* bias, const void* residual,
-                               long long ldr, int relu, void* out, long long ldo, void* workspace,
-                               long long ws_bytes, void* stream);
-
 /* Large bf16 GEMM on 256 x 256 tiles (hand-written MFMA, csrc/gemm256.hip) for the RegionCLIP
  * res5 1x1 convolutions over all L*B*Q ROIs [upstream CLIP ModifiedResNet layer4;
  * clip.inference, criterion.py:397] and the 3DETR decoder's memory K / V projections
@@ -480,21 +468,6 @@ int ov3d_gemm256_batched(const void* A, long long lda, long long sA, const void*
 int ov3d_conv3x3_gemm256(const void* X, int nimg, int H, int W, int Cin, const void* Wt,
                          long long ldb, const void* bias, int bias_f32, const void* R, long long ldr,
                          void* Y, long long ldc, int Cout, int relu, void* stream);
-
-/* Output projection + residual + dropout + LayerNorm in ONE launch (forward) [models/
- * transformer.py: out_proj (nn.MultiheadAttention, 223 / 307-308) or linear2 (275-277 /
- * 375-377), then x + dropout(branch) and the next sub-layer's norm (forward_pre 262-280 /
- * 355-379)]: y = bf16(x (R, K) . w (256, K)^T + bias) (bf16 rows / weight / bias) replaces the
- * y operand of ov3d_resnorm_fwd (same outputs, same dropout hash and rounding; y itself is not
- * written).  ov3d_linres_supported(Cout, K): Cout == 256, K % 32 == 0, K <= 256.  x, w, s and
- * src 16-byte aligned, ldx / ldw multiples of 8 elements, bias 8-byte aligned or null. */
-int ov3d_linres_supported(int Cout, int K);
-int ov3d_linres_fwd(long long R, int K, const void* x, long long ldx, const void* w, long long ldw,
-                    const void* bias, const void* src, int src_bf16, float dropout_p,
-                    const int64_t* seed, int site, const float* ga, const float* ba,
-                    const void* pos, int pos_bf16, const float* gb, const float* bb, float eps,
-                    float* s, float* mean, float* rstd, void* xa, void* xap, void* xb, int xb_bf16,
-                    long long xb_inner, long long xb_s0, long long xb_s1, void* stream);
 
 /* LayerNorm boundary + the adjacent row GEMM in one launch (csrc/lngemm.hip), the decoder's
  * short row blocks [models/transformer.py TransformerDecoderLayer.forward_pre 355-379].

@@ -58,7 +58,6 @@ _SIGS = {
     "ov3d_attnpool_tokens": "piiiippp",
     "ov3d_attnpool_mean": "piiippp",
     "ov3d_attnpool_fused": "pppplliiiipp",
-    "ov3d_lt_gemm_bias_residual": "liiplplppliplplp",
     "ov3d_attn_fwd": "pppllliiiiffpiplpppip",
     "ov3d_attn_bwd": "ppplllplplpiiiiffppplplplpip",
     "ov3d_attn_bwd_dkdv_batch": "piiiiiffp",
@@ -123,7 +122,6 @@ _SIGS = {
     "ov3d_conv3x3_gemm256": "piiiiplpiplpliip",
     "ov3d_gemm256_pair": "pplpplppippliiip",
     "ov3d_gemm256_batched": "pllpllpliplliiiiip",
-    "ov3d_linres_fwd": "liplplppifpipppippfppppppilllp",
     "ov3d_lngemm_fwd": "ipipfpipppippfppppppilllipifpip",
     "ov3d_lngemm_bwd": "ipppppppilllppfpipppipipliifplplp",
 }
@@ -136,7 +134,7 @@ EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_
                           "ov3d_rows_gemm_supported", "ov3d_sa_dy_fused_supported",
                           "ov3d_tile_gemm_supported", "ov3d_sun_range_parts", "ov3d_heads_out_max_text",
                           "ov3d_heads_out_workspace", "ov3d_stamps_arm", "ov3d_stamps_count",
-                          "ov3d_stamps_get", "ov3d_wall_clock_khz", "ov3d_linres_supported",
+                          "ov3d_stamps_get", "ov3d_wall_clock_khz",
                           "ov3d_attnpool_fused_supported", "ov3d_lngemm_supported",
                           "ov3d_lngemm_bwd_parts", "ov3d_lngemm_stamps_arm", "ov3d_stream_create")
 
@@ -209,8 +207,6 @@ def load():
         lib.ov3d_sun_range_parts.restype = ctypes.c_int
         lib.ov3d_heads_out_max_text.argtypes = []
         lib.ov3d_heads_out_max_text.restype = ctypes.c_int
-        lib.ov3d_linres_supported.argtypes = [ctypes.c_int] * 2
-        lib.ov3d_linres_supported.restype = ctypes.c_int
         lib.ov3d_attnpool_fused_supported.argtypes = [ctypes.c_int] * 3
         lib.ov3d_attnpool_fused_supported.restype = ctypes.c_int
         lib.ov3d_lngemm_supported.argtypes = [ctypes.c_int] * 3

@@ -336,280 +336,23 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy_fused_kernel(DyFusedArgs p)
             }
 }
 
-// The same pass with 8 waves (512 threads, two waves per SIMD): each wave owns half the
-// columns of each product, so its accumulators and operand registers halve (dW3 64 instead of
-// 128 VGPRs) and the kernel fits 256 registers: the matrix work of one wave overlaps the
-// VALU epilogue / LDS work of its SIMD partner, which the 4-wave kernel (512 registers, one
-// wave per SIMD) serialises.  Roles per tile:
-//   y3 + dy3 : wave w, columns n = 32w .. 32w+31, both 32-row blocks; W3 rows read from an
-//              LDS image of W3 (ds_read_b128)
-//   dz       : wave w, channels k = 32(w&3) .. +31, rows 32(w>>2) .. +31; W3^T fragments in
-//              VGPRs
-//   dW3      : wave w, rows n = 32w .. +31 of dW3, all K
-// Stats (layer 2's ReLU + BN backward partials): the two row halves' lanes meet in LDS after
-// the loop.  Output layouts are the 4-wave kernel's (dwpart (nwg, N, K), stats (nwg, 2, K)).
-template <int K, int N, bool STATS>
-__global__ __launch_bounds__(512, 1) void sa_dy8_kernel(DyFusedArgs p) {
-    constexpr int T8 = 512;
-    // LDS images and their strides (bf16 elements), each chosen for conflict-free access by
-    // its reads (MI355X_MICROARCH.md §LDS bank rules; round 3's single padded z image read
-    // transposed with 4-way conflicts, 48.6 M conflict cycles per launch):
-    //   As  (z, 68-dword rows): y3 A operand, ds_read_b128 row reads -> 16 distinct slots
-    //   AsT (z again, 80-dword rows = 16 mod 64): dW3 B operand, ds_read_b64_tr_b16 over 4
-    //       consecutive rows x 16 dwords -> disjoint 16-dword windows
-    //   DsT (dy3^T, 34-dword rows): dW3 A operand ds_read_b64 over 32 consecutive channels ->
-    //       34 n mod 64 distinct; dy3 stores (ds_write_b64, 16 lanes) -> 2n mod 32 distinct
-    //   Ys  (raw y2, 66-dword rows): stats ds_read_b64 over 32 consecutive rows -> distinct
-    constexpr int LDK = K + 8;        // As, W3s
-    constexpr int LDT = K + 32;       // AsT
-    constexpr int LDR = kTile + 4;    // DsT row: one channel n, the tile's 64 rows
-    constexpr int LDY = K + 4;        // Ys
-    constexpr int LDW = K + 8;        // W3 image row n
-    constexpr int KS = K / 16;
-    constexpr int NS = N / 16;
-    static_assert(K == 128 && N == 256, "8 waves: 32 y3 columns, 32 dz channels x 32 rows, 32 dW rows");
-    __shared__ __attribute__((aligned(16))) bf16 As[kTile * LDK];
-    __shared__ __attribute__((aligned(16))) bf16 AsT[kTile * LDT];
-    __shared__ __attribute__((aligned(16))) bf16 DsT[N * LDR];
-    __shared__ __attribute__((aligned(16))) bf16 Ys[STATS ? kTile * LDY : 8];
-    __shared__ __attribute__((aligned(16))) bf16 W3s[N * LDW];
-    __shared__ float sc[K], sh[K], smu[K], sis[K];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r32 = lane & 31, h = lane >> 5;
-
-    for (int k = tid; k < K; k += T8) {
-        sc[k] = p.scale[k];
-        sh[k] = p.shift[k];
-        smu[k] = STATS ? p.mean[k] : 0.f;
-        sis[k] = STATS ? p.invstd[k] : 0.f;
-    }
-    for (int i = tid; i < N * K / 8; i += T8) {   // W3 (N, K) -> padded LDS rows
-        const int n = i / (K / 8), kc = (i % (K / 8)) * 8;
-        *reinterpret_cast<bf16x8*>(&W3s[n * LDW + kc]) = *reinterpret_cast<const bf16x8*>(p.W + (size_t)n * K + kc);
-    }
-    const int kbz = (wave & 3) * 32, rbz = wave >> 2;   // dz: channel block, row block
-    bf16x8 wt[NS];   // W3^T fragments: lane row k = kbz + r32, channels in col_operand's order
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            wt[s][j] = p.W[(size_t)(16 * s + 8 * (j >> 2) + 4 * h + (j & 3)) * K + kbz + r32];
-    const int ny = wave * 32 + r32;   // y3 column / dW3 row of this lane
-    const float cA = p.cA[ny], cB = p.cB[ny], cC = p.cC[ny];
-    float st1[STATS ? 16 : 1], st2[STATS ? 16 : 1];
-#pragma unroll
-    for (int i = 0; i < (STATS ? 16 : 1); ++i) st1[i] = st2[i] = 0.f;
-    f32x16 dw[K / 32];
-#pragma unroll
-    for (int b = 0; b < K / 32; ++b)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) dw[b][i] = 0.f;
-
-    const int ntiles = p.R / kTile;
-    constexpr int CH = kTile * K / 8 / T8;
-    static_assert(CH * T8 * 8 == kTile * K, "tile chunks");
-    bf16x8 pre[CH];
-    // Buffer loads (SGPR descriptor + 32-bit lane offset + SGPR tile offset): with global
-    // loads hipcc kept the loop-invariant 64-bit lane addresses in VGPRs, spilled them, and the
-    // spill reloads' vmcnt(0) waited out the prefetch every tile.  The tile's K-wide rows are
-    // contiguous: 16-byte piece ch = tid + c * T8 sits at byte 16 ch.
-    const int wv = __builtin_amdgcn_readfirstlane(wave);
-    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)p.yprev, 0, (int)min((long long)p.R * K * 2, 0x7fffffffLL), kBufDword3);
-    const __amdgpu_buffer_rsrc_t irs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)p.isel, 0, 0x7fffffff, kBufDword3);
-    const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)p.gsel, 0, 0x7fffffff, kBufDword3);
-    auto fetch = [&](int tile) __attribute__((always_inline)) {
-        const int soff = tile * kTile * K * 2;
-        const int tf = (wv * 64 + lane_fresh()) * 16;   // = 16 tid
-#pragma unroll
-        for (int c = 0; c < CH; ++c)
-            pre[c] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                                                    yrs, tf + c * T8 * 16, soff, 0));
-    };
-    // the pooled gradient of this lane's column and the row it came from, one tile ahead
-    // (the loaded values are consumed only in the next tile: any arithmetic on them here would
-    // wait for the loads, and with them for the row prefetch issued before)
-    float gv_n[2] = {0.f, 0.f};
-    uint32_t sv_n[2] = {0u, 0u};
-    auto fetch_g = [&](int tile) __attribute__((always_inline)) {
-        const int nyf = wv * 32 + (lane_fresh() & 31);   // = ny
-#pragma unroll
-        for (int rb = 0; rb < 2; ++rb) {
-            const int pc0 = (p.S == 64 ? tile : tile * 2 + rb) * N;   // uniform
-            sv_n[rb] = __builtin_amdgcn_raw_buffer_load_b8(irs, nyf, pc0, 0);
-            gv_n[rb] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(grs, nyf * 4, pc0 * 4, 0));
-        }
-    };
-    if (blockIdx.x < ntiles) {
-        fetch(blockIdx.x);
-        fetch_g(blockIdx.x);
-    }
-    __syncthreads();
-    PROBE_DECL
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const size_t row0 = (size_t)tile * kTile;
-        PROBE(0);
-#pragma unroll
-        for (int c = 0; c < CH; ++c) {
-            const int ch = tid + c * T8;
-            const int row = ch / (K / 8), kc = (ch % (K / 8)) * 8;
-            bf16x8 z;
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                z[j] = (bf16)fmaxf(fmaf(sc[kc + j], (float)pre[c][j], sh[kc + j]), 0.f);
-            *reinterpret_cast<bf16x8*>(&As[row * LDK + kc]) = z;
-            *reinterpret_cast<bf16x8*>(&AsT[row * LDT + kc]) = z;
-            if constexpr (STATS) *reinterpret_cast<bf16x8*>(&Ys[row * LDY + kc]) = pre[c];
-        }
-        const float gv[2] = {gv_n[0], gv_n[1]};
-        const int sv[2] = {(int)sv_n[0], (int)sv_n[1] + (p.S == 64 ? 0 : 32)};
-        PROBE(1);
-        __syncthreads();
-        PROBE(2);
-        if (tile + (int)gridDim.x < ntiles) {   // in flight below
-            fetch_g(tile + gridDim.x);
-            fetch(tile + gridDim.x);
-        }
-
-        // y3 = z W3^T for columns 32w.., then dy3 -> DsT
-        {
-            f32x16 acc[2];
-#pragma unroll
-            for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) acc[rb][i] = 0.f;
-#pragma unroll
-            for (int s = 0; s < KS; ++s) {
-                const bf16x8 b = *reinterpret_cast<const bf16x8*>(&W3s[ny * LDW + 16 * s + 8 * h]);
-#pragma unroll
-                for (int rb = 0; rb < 2; ++rb) {
-                    const bf16x8 a = *reinterpret_cast<const bf16x8*>(&As[(rb * 32 + r32) * LDK + 16 * s + 8 * h]);
-                    acc[rb] = mfma(a, b, acc[rb]);
-                }
-            }
-#pragma unroll
-            for (int rb = 0; rb < 2; ++rb) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {   // rows rb*32 + 8q + 4h + (0..3)
-                    bf16x4 d4;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int row = rb * 32 + 8 * q + 4 * h + j;
-                        const float y = (float)(bf16)acc[rb][4 * q + j];
-                        const float gi = row == sv[rb] ? gv[rb] : 0.f;
-                        d4[j] = (bf16)fmaf(cA, gi, fmaf(cB, y, cC));
-                    }
-                    *reinterpret_cast<bf16x4*>(&DsT[ny * LDR + rb * 32 + 8 * q + 4 * h]) = d4;
-                }
-            }
-        }
-        PROBE(3);
-        __syncthreads();
-        PROBE(4);
-
-        // dz^T = W3^T dy3^T for channels kbz.., rows rbz*32.. -> HBM
-        {
-            f32x16 acc;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-#pragma unroll
-            for (int s = 0; s < NS; ++s) acc = mfma(wt[s], col_operand(DsT, LDR, lane, rbz * 32, s), acc);
-            const int row = rbz * 32 + r32;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int k = kbz + 8 * g + 4 * h;
-                bf16x4 o;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) o[j] = (bf16)acc[4 * g + j];
-                *reinterpret_cast<bf16x4*>(p.dz + (row0 + row) * K + k) = o;
-                if constexpr (STATS) {   // bn_relu_bwd pass 0 on the stored values
-                    const bf16x4 y4 = *reinterpret_cast<const bf16x4*>(&Ys[row * LDY + k]);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const float yy = (float)y4[j];
-                        const float dt = fmaf(sc[k + j], yy, sh[k + j]) > 0.f ? (float)o[j] : 0.f;
-                        st1[4 * g + j] += dt;
-                        st2[4 * g + j] = fmaf(dt, (yy - smu[k + j]) * sis[k + j], st2[4 * g + j]);
-                    }
-                }
-            }
-        }
-        PROBE(5);
-        // dW3 rows 32w.. += dy3^T z over this tile's rows
-#pragma unroll
-        for (int s = 0; s < kTile / 16; ++s) {
-            const bf16* dn = DsT + ny * LDR + 16 * s + 4 * h;
-            const bf16x4 lo = *reinterpret_cast<const bf16x4*>(dn);
-            const bf16x4 hi = *reinterpret_cast<const bf16x4*>(dn + 8);
-            const bf16x8 ad = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-            for (int b = 0; b < K / 32; ++b) dw[b] = mfma(ad, col_operand(AsT, LDT, lane, 32 * b, s), dw[b]);
-        }
-        PROBE(6);
-        __syncthreads();   // As / DsT / Ys are rewritten by the next tile
-        PROBE(7);
-    }
-    PROBE_END;
-    if constexpr (STATS) {
-        // the row-block-1 waves hand their partials to the row-block-0 waves of the same channels
-        // (4 channel blocks, 64 lanes, 32) floats = 32 KB: DsT (34.8 KB) holds it, As (17 KB) does not
-        float* xs = reinterpret_cast<float*>(DsT);
-        static_assert(sizeof(DsT) >= 4 * 64 * 32 * sizeof(float), "stats hand-off overruns DsT");
-        static_assert(sizeof(As) + sizeof(AsT) + sizeof(DsT) + sizeof(Ys) + sizeof(W3s) +
-                      4 * K * sizeof(float) <= 160 * 1024, "LDS images exceed the CU's 160 KB");
-        if (rbz == 1)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                xs[((wave & 3) * 64 + lane) * 32 + i] = st1[i];
-                xs[((wave & 3) * 64 + lane) * 32 + 16 + i] = st2[i];
-            }
-        __syncthreads();
-        if (rbz == 0) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                double s1 = (double)st1[i] + (double)xs[(wave * 64 + lane) * 32 + i];
-                double s2 = (double)st2[i] + (double)xs[(wave * 64 + lane) * 32 + 16 + i];
-#pragma unroll
-                for (int o = 16; o > 0; o >>= 1) {
-                    s1 += __shfl_xor(s1, o, 64);
-                    s2 += __shfl_xor(s2, o, 64);
-                }
-                if (r32 == 0) {
-                    const int k = kbz + 8 * (i >> 2) + 4 * h + (i & 3);
-                    p.stats[(size_t)blockIdx.x * 2 * K + k] = s1;
-                    p.stats[(size_t)blockIdx.x * 2 * K + K + k] = s2;
-                }
-            }
-        }
-    }
-    // dW3 partial: element (b, i) = dW[n][k], n = 32w + (i&3) + 8(i>>2) + 4h, k = 32b + r32
-    float* out = p.dwpart + (size_t)blockIdx.x * N * K;
-#pragma unroll
-    for (int b = 0; b < K / 32; ++b)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int n = wave * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-            out[(size_t)n * K + 32 * b + r32] = dw[b][i];
-        }
-}
-
 // sa_dy9's LDS images.  Rows / lines are unpadded and XOR-swizzled in 16- or 8-byte pieces, so
 // that every access below is free of bank conflicts (MI355X_MICROARCH.md §LDS lane groups;
 // tools/lds_banks_dy9.py enumerates them):
 //   As  (z: 64 rows x 128 k): 16-byte piece c of row r at c ^ zsw(r).  Read row-wise by the y3 A
 //       operand (ds_read_b128, lanes = rows) and transposed by the dW3 B operand
-//       (ds_read_b64_tr_b16 over 4 rows x 16 k): one image serves both (sa_dy8 kept two).
+//       (ds_read_b64_tr_b16 over 4 rows x 16 k): one image serves both (round 4's sa_dy8 kept two).
 //   DsT (dy3^T: 256 lines x 64 rows): 8-byte piece c (4 rows) of line n at c ^ dsw(n).  Written
 //       by the y3 epilogue (ds_write_b64, 16 consecutive lines per lane group), read transposed
 //       by the dz A operand (4 lines x 16 rows) and by the dW3 A operand (ds_read_b64 over 32
-//       consecutive lines).  sa_dy8's padded 34-dword lines left the dz reads 2-way conflicted.
+//       consecutive lines).  Round 4's padded 34-dword lines left the dz reads 2-way conflicted.
 __device__ __forceinline__ int dsw(int n) {
     return (((n >> 1) & 1) << 3) | (((n >> 3) & 1) << 2) | (((n >> 2) & 1) << 1) | ((n ^ (n >> 4)) & 1);
 }
 __device__ __forceinline__ int zsw(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
 
-// sa_dy8 restructured so its three MFMA chains are fed two steps ahead.  sa_dy8 held, per lane,
+// The round-4 8-wave kernel (sa_dy8) restructured so its three MFMA chains are fed two steps
+// ahead.  sa_dy8 held, per lane,
 // 16 channels x 2 statistics partials (32 VGPRs) next to the W3^T fragments (64) and the dW3
 // accumulators (64): at the 256-VGPR cap every MFMA waited for the LDS read issued just before
 // it.  Here the dz product is computed transposed, dz[row][k] = dy3 W3 with dy3 as the A
@@ -948,10 +691,6 @@ struct Dy2Args {
     double* stats;      // (gridDim.x, 2, K)
     const float* x0;    // X0 variant (y1 == NULL): y1 = bf16(x0 W1^T) recomputed, (R, 3)
     const float* W1;    // (K, 3)
-    int dbg;            // sa_dy2b diagnostics (OV3D_SA_DY2B_DBG bits): 1 barrier after the dz1
-                        // flush, 2 barrier between its dz1 and dW2 phases, 4 dz1 stored directly,
-                        // 8 every counter drained before the next tile's x0 rows reach LDS,
-                        // 16 x0 rows / 32 W1 read from global memory instead of LDS
 };
 
 template <int K, int N, bool X0>
@@ -1130,235 +869,6 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy2_fused_kernel(Dy2Args p) {
         }
 }
 
-// (Opt-in, OV3D_SA_DY2B=1; one workgroup per CU.)  With two co-resident workgroups per CU its
-// gradients differ run to run (tools/sa_bwd_check.py: dW2 / dW1 off by ~1e-2; one per CU they
-// equal sa_dy2_fused's to every printed digit); the cause is not found yet.
-// sa_dy2_fused restructured as sa_dy9: dz1 computed transposed (dy2 rows as the A operand), so
-// a lane holds ONE layer-1 channel (kz = kbase + r32) of 16 rows and the layer-1 statistics
-// partials are 2 registers instead of 32; the dz1 tile is staged in LDS (Dz) and stored as
-// 16-byte rows by the next tile's prologue; the per-thread BN coefficients of the prologue are
-// read once; operands are read ahead of their MFMAs.  The registers fit two workgroups per CU
-// (sa_dy2_fused needed ~300 with its AGPRs: one 4-wave workgroup per CU).  LDS images:
-//   As, Ys (z1, raw y1; 64 rows x 64): 48-dword rows, read transposed (4 rows x 16 dwords per
-//       32 lanes -> disjoint bank windows) by the dW2 B operand / the statistics;
-//   Ds (dy2; 64 rows x 128): unpadded, 16-byte pieces swizzled by zsw(row) as sa_dy9's As: row
-//       reads (dz1 A operand) and transposed reads (dW2 A operand) both conflict-free.
-template <int K, int N, bool X0>
-__global__ __launch_bounds__(kThreads, 2) void sa_dy2b_kernel(Dy2Args p) {
-    static_assert(K == 64 && N == 128, "4 waves = 2 x 2 dz tiles, 32 dW rows each");
-    constexpr int LDA = K + 32;
-    __shared__ __attribute__((aligned(16))) bf16 As[kTile * LDA];   // z1
-    __shared__ __attribute__((aligned(16))) bf16 Ys[kTile * LDA];   // raw y1
-    __shared__ __attribute__((aligned(256))) bf16 Ds[kTile * N];    // dy2, swizzled rows
-    __shared__ __attribute__((aligned(16))) bf16 Dz[kTile * K];     // dz1 tile
-    __shared__ float w1s[X0 ? 3 * K : 1];
-    __shared__ __attribute__((aligned(16))) float x0s[X0 ? 3 * kTile : 4];   // the tile's x0 rows
-    __shared__ __attribute__((aligned(16))) float cAs[N], cBs[N], cCs[N];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r32 = lane & 31, h = lane >> 5;
-    for (int n = tid; n < N; n += kThreads) {
-        cAs[n] = p.cA[n];
-        cBs[n] = p.cB[n];
-        cCs[n] = p.cC[n];
-    }
-    if constexpr (X0)
-        for (int k = tid; k < 3 * K; k += kThreads) w1s[k] = p.W1[k];
-    // dz1 tile of this wave: rows rb*32 .. +31, channel kz of this lane
-    const int kbase = (wave & 1) * 32, rb = wave >> 1;
-    const int kz = kbase + r32;
-    constexpr int NS = N / 16;
-    bf16x8 wt[NS];   // W2 fragments (B operand of dz1 = dy2 W2): channel kz, n = 16s + 8h + j
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) wt[s][j] = p.W[(size_t)(16 * s + 8 * h + j) * K + kz];
-    const float zsc = p.a1[kz], zsh = p.b1[kz], zmu = p.mean1[kz], zis = p.invstd1[kz];
-    // a thread's prologue chunks all start at one channel: its coefficients once
-    const int kc0 = (tid % (K / 8)) * 8, nc0 = (tid % (N / 8)) * 8;
-    static_assert(kThreads % (K / 8) == 0 && kThreads % (N / 8) == 0, "chunk channel fixed");
-    float a1v[8], b1v[8], a2v[8], b2v[8];   // (the dy2 coefficients stay in LDS: registers)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        a1v[j] = p.a1[kc0 + j];
-        b1v[j] = p.b1[kc0 + j];
-        a2v[j] = p.a2[nc0 + j];
-        b2v[j] = p.b2[nc0 + j];
-    }
-    f32x16 dw[2];    // dW2 rows wave*32 .. +31, columns 0..31 / 32..63
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) dw[b][i] = 0.f;
-    double st1 = 0.0, st2 = 0.0;   // fp32 over a tile's 16 rows, fp64 across tiles
-    // Ds element offsets: dz1 A operand row rb*32 + r32, piece 2s + h -> ya ^ 16s; dW2 A operand
-    // (col_operand's pattern over columns 32 wave ..): (xlo ^ 32 wave) + 16 N s, as sa_dy9
-    const int ya = (rb * 32 + r32) * N + 8 * (h ^ zsw(r32));
-    const int g4 = lane >> 4, i16 = lane & 15;
-    const int rl = 4 * (g4 >> 1) + (i16 >> 2);
-    const int kq = 2 * (g4 & 1) + ((i16 >> 1) & 1);
-    const int zl = zsw(rl), zh = zsw(rl + 8);
-    const int xlo = (rl * N + 32 * (zl >> 2) + 8 * (kq ^ (zl & 3)) + 4 * (i16 & 1)) ^ (32 * wave);
-    const int xhi = ((rl + 8) * N + 32 * (zh >> 2) + 8 * (kq ^ (zh & 3)) + 4 * (i16 & 1)) ^ (32 * wave);
-    __syncthreads();
-
-    const int ntiles = p.R / kTile;
-    constexpr int C1 = kTile * K / 8 / kThreads;   // 16-byte chunks per thread: y1, dz1
-    constexpr int C2 = kTile * N / 8 / kThreads;   // y2, dz2
-    bf16x8 py1[X0 ? 1 : C1], py2[C2], pdz[C2];
-    float4 px0 = make_float4(0.f, 0.f, 0.f, 0.f);
-    auto fetch = [&](int tile) {
-        const size_t row0 = (size_t)tile * kTile;
-        if constexpr (X0) {
-            if (tid < 3 * kTile / 4) px0 = reinterpret_cast<const float4*>(p.x0 + row0 * 3)[tid];
-        } else {
-#pragma unroll
-            for (int c = 0; c < C1; ++c) {
-                const int ch = tid + c * kThreads, row = ch / (K / 8);
-                py1[c] = *reinterpret_cast<const bf16x8*>(p.y1 + (row0 + row) * K + kc0);
-            }
-        }
-#pragma unroll
-        for (int c = 0; c < C2; ++c) {
-            const int ch = tid + c * kThreads, row = ch / (N / 8);
-            py2[c] = *reinterpret_cast<const bf16x8*>(p.y2 + (row0 + row) * N + nc0);
-            pdz[c] = *reinterpret_cast<const bf16x8*>(p.dz2 + (row0 + row) * N + nc0);
-        }
-    };
-    auto flush_dz = [&](size_t prow0) __attribute__((always_inline)) {
-#pragma unroll
-        for (int c = 0; c < C1; ++c) {
-            const int ch = tid + c * kThreads, row = ch / (K / 8);
-            *reinterpret_cast<bf16x8*>(p.dz1 + (prow0 + row) * K + kc0) =
-                *reinterpret_cast<const bf16x8*>(&Dz[row * K + kc0]);
-        }
-    };
-    if (blockIdx.x < ntiles) fetch(blockIdx.x);
-    if constexpr (X0) {   // x0 of the first tile -> LDS (read in the first prologue)
-        if (tid < 3 * kTile / 4) reinterpret_cast<float4*>(x0s)[tid] = px0;
-        __syncthreads();
-    }
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const size_t row0 = (size_t)tile * kTile;
-        if (tile != (int)blockIdx.x && !(p.dbg & 4)) flush_dz(row0 - (size_t)gridDim.x * kTile);
-        if (p.dbg & 1) __syncthreads();
-#pragma unroll
-        for (int c = 0; c < C1; ++c) {
-            const int ch = tid + c * kThreads, row = ch / (K / 8);
-            bf16x8 y1v;
-            if constexpr (X0) {
-                const float* xr = (p.dbg & 16) ? p.x0 + (row0 + row) * 3 : &x0s[3 * row];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {   // sa_l1_kernel's value, bit for bit
-                    const float* w = (p.dbg & 32) ? p.W1 + 3 * (kc0 + j) : &w1s[3 * (kc0 + j)];
-                    y1v[j] = (bf16)fmaf(w[2], xr[2], fmaf(w[1], xr[1], w[0] * xr[0]));
-                }
-            } else {
-                y1v = py1[c];
-            }
-            bf16x8 z;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) z[j] = (bf16)fmaxf(fmaf(a1v[j], (float)y1v[j], b1v[j]), 0.f);
-            *reinterpret_cast<bf16x8*>(&As[row * LDA + kc0]) = z;
-            *reinterpret_cast<bf16x8*>(&Ys[row * LDA + kc0]) = y1v;
-        }
-#pragma unroll
-        for (int c = 0; c < C2; ++c) {   // bn_relu_bwd_kernel pass 1 arithmetic
-            const int ch = tid + c * kThreads, row = ch / (N / 8);
-            bf16x8 d;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float yy = (float)py2[c][j];
-                const float dt = fmaf(a2v[j], yy, b2v[j]) > 0.f ? (float)pdz[c][j] : 0.f;
-                d[j] = (bf16)fmaf(cAs[nc0 + j], dt, fmaf(cBs[nc0 + j], yy, cCs[nc0 + j]));
-            }
-            *reinterpret_cast<bf16x8*>(&Ds[row * N + 8 * ((nc0 >> 3) ^ zsw(row))]) = d;
-        }
-        __syncthreads();
-        if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);   // in flight below
-
-        // dz1[row][k] = dy2 W2 for rows rb*32.., channel kz; A = dy2 rows, read one step ahead
-        {
-            bf16x8 aq[NS];
-            auto ld = [&](int s) __attribute__((always_inline)) {
-                aq[s] = *reinterpret_cast<const bf16x8*>(&Ds[ya ^ (16 * s)]);
-            };
-            f32x16 acc;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-            ld(0);
-            ld(1);
-#pragma unroll
-            for (int s = 0; s < NS; ++s) {
-                if (s + 2 < NS) ld(s + 2);
-                acc = mfma(aq[s], wt[s], acc);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            const bf16x8 yq[2] = {col_operand(Ys, LDA, lane, kbase, 2 * rb),
-                                  col_operand(Ys, LDA, lane, kbase, 2 * rb + 1)};
-            // element i: row rb*32 + (i&3) + 8(i>>2) + 4h of channel kz
-            bf16* dzl = &Dz[(rb * 32 + 4 * h) * K + kz];
-            float t1 = 0.f, t2 = 0.f;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const bf16 o = (bf16)acc[i];
-                if (p.dbg & 4) p.dz1[(row0 + rb * 32 + 4 * h + (i & 3) + 8 * (i >> 2)) * K + kz] = o;
-                else dzl[((i & 3) + 8 * (i >> 2)) * K] = o;
-                const float yy = (float)yq[i >> 3][i & 7];   // bn_relu_bwd pass 0 of layer 1
-                const float dt = fmaf(zsc, yy, zsh) > 0.f ? (float)o : 0.f;
-                t1 += dt;
-                t2 = fmaf(dt, (yy - zmu) * zis, t2);
-            }
-            st1 += (double)t1;
-            st2 += (double)t2;
-        }
-        if (p.dbg & 2) __syncthreads();
-        // dW2 += dy2^T z1 over the tile's rows; operands one product ahead
-        {
-            bf16x8 adq[kTile / 16], bzq[kTile / 16 * 2];
-            auto ld = [&](int t) __attribute__((always_inline)) {
-                const int s = t >> 1, b = t & 1;
-                if (b == 0) {
-                    const bf16x4 lo = tr16(Ds + xlo + 16 * N * s);
-                    const bf16x4 hi = tr16(Ds + xhi + 16 * N * s);
-                    adq[s] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                }
-                bzq[t] = col_operand(As, LDA, lane, 32 * b, s);
-            };
-            constexpr int NT = kTile / 16 * 2;
-            ld(0);
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                if (t + 1 < NT) ld(t + 1);
-                dw[t & 1] = mfma(adq[t >> 1], bzq[t], dw[t & 1]);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        if constexpr (X0) {   // the next tile's x0 (its prologue reads it after the barrier)
-            if (p.dbg & 8) __builtin_amdgcn_s_waitcnt(0);
-            if (tid < 3 * kTile / 4 && tile + (int)gridDim.x < ntiles)
-                reinterpret_cast<float4*>(x0s)[tid] = px0;
-        }
-        __syncthreads();   // As / Ys / Ds / Dz (and x0s) are rewritten / stored by the next tile
-    }
-    if (blockIdx.x < ntiles && !(p.dbg & 4))   // the last tile's dz1 rows
-        flush_dz((size_t)(blockIdx.x + (ntiles - 1 - blockIdx.x) / gridDim.x * gridDim.x) * kTile);
-    {   // channel kz, rows of row block rb: the two lane halves, one slot per row block
-        const double s1 = st1 + __shfl_xor(st1, 32);
-        const double s2 = st2 + __shfl_xor(st2, 32);
-        if (h == 0) {
-            p.stats[((size_t)blockIdx.x * 2 + rb) * 2 * K + kz] = s1;
-            p.stats[((size_t)blockIdx.x * 2 + rb) * 2 * K + K + kz] = s2;
-        }
-    }
-    float* out = p.dwpart + (size_t)blockIdx.x * N * K;
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int n = wave * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-            out[(size_t)n * K + 32 * b + r32] = dw[b][i];
-        }
-}
-
 }  // namespace
 
 extern "C" int ov3d_sa_dy_fused_supported(int K, int N) { return K == 128 && N == 256; }
@@ -1381,25 +891,15 @@ extern "C" int ov3d_sa_dy_fused(const void* yprev, const float* scale, const flo
         return OV3D_EINVAL;
     DyFusedArgs a{(const bf16*)yprev, scale, shift, (const bf16*)W, R, S, gsel, isel, ysel, cA, cB,
                   cC, (bf16*)dz, dwpart, mean, invstd, stats};
-    static const bool four_env = getenv("OV3D_SA_DY4") != nullptr;   // A/B: the 4-wave kernel
-    static const bool dy8_env = getenv("OV3D_SA_DY8") != nullptr;    // A/B: the round-4 8-wave kernel
-    // sa_dy8 addresses the previous layer's rows through a buffer resource with 32-bit tile
+    // sa_dy9 addresses the previous layer's rows through a buffer resource with 32-bit tile
     // offsets (num_records clamped to 2^31 - 1 bytes): past that the loads would return zeros.
     // The 4-wave kernel indexes with 64-bit addresses, so larger inputs go there.
-    const bool four = four_env || (long long)R * K * 2 > 0x7fffffffLL;
-    if (four) {
+    if ((long long)R * K * 2 > 0x7fffffffLL) {
         if (stats)
             hipLaunchKernelGGL((sa_dy_fused_kernel<128, 256, true>), dim3(nwg), dim3(kThreads), 0,
                                ov3d_stream(stream), a);
         else
             hipLaunchKernelGGL((sa_dy_fused_kernel<128, 256, false>), dim3(nwg), dim3(kThreads), 0,
-                               ov3d_stream(stream), a);
-    } else if (dy8_env) {
-        if (stats)
-            hipLaunchKernelGGL((sa_dy8_kernel<128, 256, true>), dim3(nwg), dim3(512), 0,
-                               ov3d_stream(stream), a);
-        else
-            hipLaunchKernelGGL((sa_dy8_kernel<128, 256, false>), dim3(nwg), dim3(512), 0,
                                ov3d_stream(stream), a);
     } else if (stats) {
         hipLaunchKernelGGL((sa_dy9_kernel<128, 256, true>), dim3(nwg), dim3(512), 0,
@@ -1422,23 +922,8 @@ extern "C" int ov3d_sa_dy2_fused(const void* y1, const float* x0, const float* W
         !a2 || !b2 || !dz2 || !cA || !cB || !cC || !W || !mean1 || !invstd1 || !dz1 || !dwpart ||
         !stats || nwg <= 0)
         return OV3D_EINVAL;
-    static const int dbg = getenv("OV3D_SA_DY2B_DBG") ? atoi(getenv("OV3D_SA_DY2B_DBG")) : 0;
     Dy2Args a{(const bf16*)y1, a1, b1, (const bf16*)y2, a2, b2, (const bf16*)dz2, cA, cB, cC,
-              (const bf16*)W, mean1, invstd1, R, (bf16*)dz1, dwpart, stats, x0, W1, dbg};
-    // sa_dy2b is opt-in (OV3D_SA_DY2B=1): two co-resident workgroups per CU corrupt its results
-    // (DESIGN.md, round 5), so its launch reserves dynamic LDS that leaves one per CU
-    static const bool b_env = getenv("OV3D_SA_DY2B") != nullptr;
-    static const int lds_pad = getenv("OV3D_SA_DY2_LDSPAD") ? atoi(getenv("OV3D_SA_DY2_LDSPAD")) : 65536;
-    if (b_env) {
-        if (y1)
-            hipLaunchKernelGGL((sa_dy2b_kernel<64, 128, false>), dim3(nwg), dim3(kThreads), lds_pad,
-                               ov3d_stream(stream), a);
-        else
-            hipLaunchKernelGGL((sa_dy2b_kernel<64, 128, true>), dim3(nwg), dim3(kThreads), lds_pad,
-                               ov3d_stream(stream), a);
-        OV3D_LAUNCH_CHECK();
-        return OV3D_OK;
-    }
+              (const bf16*)W, mean1, invstd1, R, (bf16*)dz1, dwpart, stats, x0, W1};
     if (y1)
         hipLaunchKernelGGL((sa_dy2_fused_kernel<64, 128, false>), dim3(nwg), dim3(kThreads), 0,
                            ov3d_stream(stream), a);

@@ -260,44 +260,29 @@ def _nhwc(x):
 
 def _conv1x1(x, w, b, relu, residual=None):
     """1x1 conv on NHWC rows as one GEMM: (rows, Cin) @ (Cout, Cin)^T + b (+ residual), the
-    bias and ReLU in the GEMM epilogue; with a residual (bf16) the identity is the GEMM's C."""
+    bias and ReLU in the GEMM epilogue; with a residual (bf16) the identity is the GEMM's C.
+
+    bf16 on the device (the product path) has ONE backend, the hand-written 256 x 256 tile
+    kernel (csrc/gemm256.hip); a shape it rejects raises instead of falling back to a library
+    GEMM.  fp32 (the parity tests' restatement dtype) runs torch's GEMM + ov3d_bias_residual_act."""
     shp = x.shape
     rows = x.reshape(-1, shp[-1])
+    res = residual.reshape(-1, w.shape[0]) if residual is not None else None
     if x.dtype == torch.bfloat16 and x.is_cuda:
-        res = residual.reshape(-1, w.shape[0]) if residual is not None else None
-        if gemm.gemm256_ok(rows, w, residual=res):
-            # hand-written 256 x 256 tile kernel: bias, identity and ReLU in its epilogue
-            return gemm.gemm256(rows, w, bias=b, residual=res, relu=relu).view(*shp[:-1], w.shape[0])
-    if residual is None:
+        if not gemm.gemm256_ok(rows, w, residual=res):
+            raise _native.NativeError(
+                f"regionclip 1x1 conv: gemm256 rejects rows {tuple(rows.shape)} stride "
+                f"{rows.stride()} x weight {tuple(w.shape)} stride {w.stride()} (bf16 rows, "
+                "K % 8 == 0, N % 8 == 0, 16-byte aligned; OV3D_GEMM256=1)")
+        return gemm.gemm256(rows, w, bias=b, residual=res, relu=relu).view(*shp[:-1], w.shape[0])
+    if res is None:
         y = torch._addmm_activation(b, rows, w.t()) if relu else torch.addmm(b, rows, w.t())
     else:
-        res = _native.check(residual.reshape(-1, w.shape[0]), "residual", ndim=2)
-        rows = _native.check(rows.contiguous(), "conv3 input", ndim=2)
-        if x.dtype == torch.bfloat16:
-            # one hipBLASLt matmul: C = identity, D = out, bias + ReLU epilogue
-            y = torch.empty((rows.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
-            ws = _lt_workspace(x.device)
-            _native.call("ov3d_lt_gemm_bias_residual", rows.shape[0], w.shape[0], w.shape[1], rows,
-                         rows.stride(0), w, w.stride(0), b, res, res.stride(0), int(relu), y,
-                         y.stride(0), ws, ws.numel(), like=x)
-        else:   # fp32: plain GEMM, then bias + identity + ReLU in one pass
-            y = torch.mm(rows, w.t())
-            _native.call("ov3d_bias_residual_act", y, y.element_size(), y.shape[0], y.shape[1], b,
-                         res, int(relu), like=y)
+        res = _native.check(res, "residual", ndim=2)
+        y = torch.mm(rows, w.t())
+        _native.call("ov3d_bias_residual_act", y, y.element_size(), y.shape[0], y.shape[1], b,
+                     res, int(relu), like=y)
     return y.view(*shp[:-1], w.shape[0])
-
-
-# hipBLASLt workspace of the fused conv3 GEMM (its stream-K algorithms), one per device
-LT_WORKSPACE_BYTES = 64 << 20
-_LT_WS = {}
-
-
-def _lt_workspace(device):
-    ws = _LT_WS.get(device)
-    if ws is None:
-        ws = torch.empty((LT_WORKSPACE_BYTES,), dtype=torch.uint8, device=device)
-        _LT_WS[device] = ws
-    return ws
 
 
 # im2col chunk budget.  Whole convolutions (16 GB: res5's first 3x3 over 4096 ROIs is 15.3 GB of

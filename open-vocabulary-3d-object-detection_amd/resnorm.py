@@ -28,7 +28,8 @@ from . import gemm
 
 Pending = namedtuple("Pending", "src y p site")
 # a branch output not yet computed: y = x w^T + b (the sub-layer's output projection / FFN
-# linear2); resnorm() runs it inside the residual + LayerNorm launch (csrc/linres.hip)
+# linear2); the decoder's lngemm launch (resnorm_gemm) computes it in place of a y operand, the
+# plain resnorm() resolves it with a rows GEMM first
 LinY = namedtuple("LinY", "x w b relu_p", defaults=(None,))
 # relu_p (FFN linear2): x is dropout_p(relu(h)); the input gradient then takes the FFN's
 # activation mask in its epilogue (dx = x > 0 ? dy w / (1 - p) : 0), as _FFN's backward does
@@ -60,11 +61,6 @@ class FanIn:
 enabled = True   # False: the plain module code under autocast as well (tests compare the two)
 fan_in = True    # False: every call returns its own pos / norm_b gradient (autograd sums them)
 fused_ffn = os.environ.get("OV3D_FUSED_FFN", "1") != "0"   # _FFN on short row blocks
-# output projection + residual + dropout + LayerNorm in one launch (csrc/linres.hip).  Off by
-# default: measured slower in the SUN step than rows GEMM + resnorm_fwd (decoder 1024-row blocks
-# 10.8 vs 5.0 + 5.1 us, encoder 16384 rows 33 vs 20 us: every 16-row workgroup re-reads the whole
-# 256 x K weight); OV3D_LINRES=1 turns it on
-linres = os.environ.get("OV3D_LINRES", "0") == "1"
 
 
 def supported(x, *norms):
@@ -281,7 +277,7 @@ def _colsums(partials, nparts, C, outs, acc):
 class _RowsLinearMask(torch.autograd.Function):
     """y = h w^T + b for the FFN's linear2 whose input h = dropout_p(relu(.)) came from a
     relu-drop epilogue (LinY with relu_p): the input gradient takes the activation mask in
-    its epilogue (dx = h > 0 ? dy w / (1 - p) : 0), the convention of _FFN1 / _LnGemm."""
+    its epilogue (dx = h > 0 ? dy w / (1 - p) : 0), the convention of _LnGemm."""
 
     @staticmethod
     def forward(ctx, h, w, b, relu_p):
@@ -527,88 +523,6 @@ def resnorm_gemm(pend, norm_a, w, b, spec, pos=None, norm_b=None, pos_fan=None, 
     return r[0], r[1], list(r[2:])
 
 
-class _LinResNorm(torch.autograd.Function):
-    """resnorm with the branch output computed in the same launch: y = bf16(x w^T + b)
-    (csrc/linres.hip).  Backward: the resnorm backward launch gives dy (bf16), then the linear's
-    input gradient dx = dy w (rowsgemm) and its weight / bias gradients (deferred with the
-    others when gemm.DEFER_WGRAD)."""
-
-    @staticmethod
-    def forward(ctx, meta, src, x, w, b, pos, ga, ba, gb, bb, relu_p=None):
-        p, site, want_a, want_ap, want_b, eps, shape, fans, xb_into = meta
-        C = w.shape[0]
-        K = x.shape[-1]
-        bf = torch.bfloat16
-        xr = x.reshape(-1, K)
-        wc, bc = gemm.cast_param(w, bf), gemm.cast_param(b, bf) if b is not None else None
-        srcr, posr = _rows(src, C), _rows(pos, C)
-        R = xr.shape[0]
-        dev = x.device
-        s = torch.empty((R, C), dtype=torch.float32, device=dev)
-        norm = want_a or want_ap or want_b
-        mean = torch.empty(R, dtype=torch.float32, device=dev) if norm else None
-        rstd = torch.empty(R, dtype=torch.float32, device=dev) if norm else None
-        xa = torch.empty((R, C), dtype=bf, device=dev) if want_a else None
-        xap = torch.empty((R, C), dtype=bf, device=dev) if want_ap else None
-        xb_map = (0, 0, 0)
-        if want_b and xb_into is not None:
-            out, l = xb_into
-            xb = out[l]
-            xb_map = (shape[1], C, shape[0] * C)
-        else:
-            xb = torch.empty((R, C), dtype=torch.float32, device=dev) if want_b else None
-        seed = flash._seed(dev) if p > 0 else None
-        _native.call("ov3d_linres_fwd", R, K, xr, xr.stride(0), wc, wc.stride(0), bc, srcr,
-                     _dt_flag(srcr), float(p), seed, site, ga, ba, posr, _dt_flag(posr), gb, bb,
-                     float(eps), s, mean, rstd, xa, xap, xb, _dt_flag(xb), *xb_map, like=s)
-        ctx.save_for_backward(s, mean, rstd, ga, gb, xr, wc)
-        ctx.seed = seed
-        ctx.params = (ga, ba, gb, bb)
-        ctx.lin = (w, b)
-        ctx.set_materialize_grads(False)
-        ctx.meta = (p, site, R, C, shape, src.dtype if src is not None else None, bf,
-                    pos.dtype if pos is not None else None)
-        ctx.xshape, ctx.xdt = x.shape, x.dtype
-        ctx.relu_p = relu_p
-        ctx.fans = fans
-        v = lambda t: t.view(shape) if t is not None else None   # noqa: E731
-        if xb_map[0]:
-            return v(s), v(xa), v(xap), xb.transpose(0, 1)
-        return v(s), v(xa), v(xap), v(xb)
-
-    @staticmethod
-    def backward(ctx, ds, dxa, dxap, dxb):
-        nig = ctx.needs_input_grad   # meta, src, x, w, b, pos, ga, ba, gb, bb
-        need_y = nig[2] or nig[3] or nig[4]
-        need = (False, nig[1], need_y, nig[5], nig[6], nig[7], nig[8], nig[9])
-        dsrc, dy, dpos, dga, dba, dgb, dbb = _bwd_core(ctx, ds, dxa, dxap, dxb, need)
-        dx = dw = db = None
-        if dy is not None:
-            xr, wc = ctx.saved_tensors[5:7]
-            w, b = ctx.lin
-            dyr = dy.reshape(-1, wc.shape[0])
-            with torch.autocast("cuda", enabled=False):
-                if nig[2] and ctx.relu_p is not None:   # the FFN's ReLU + dropout mask
-                    dx = gemm.act_gemm(dyr, wc, None, False, 2, ctx.relu_p, h=xr).view(ctx.xshape)
-                elif nig[2]:
-                    dx = gemm._dgrad(dyr, wc).to(ctx.xdt).view(ctx.xshape)
-                if nig[3] or (b is not None and nig[4]):
-                    dw, db = gemm.linear_weight_grads(dyr, xr, w, b, nig[3], nig[4])
-        return None, dsrc, dx, dw, db, dpos, dga, dba, dgb, dbb, None
-
-
-def linres_ok(y, C):
-    """the LinY branch y can run inside the resnorm launch (csrc/linres.hip)"""
-    if not (linres and isinstance(y, LinY) and y.x.is_cuda and y.x.dtype == torch.bfloat16):
-        return False
-    x = y.x
-    K = x.shape[-1]
-    if not (x.stride(-1) == 1 and x.is_contiguous() and x.data_ptr() % 16 == 0 and y.w.dim() == 2
-            and tuple(y.w.shape) == (C, K)):
-        return False
-    return bool(_native.load().ov3d_linres_supported(C, K))
-
-
 def resolve(y):
     """a LinY branch computed on its own (rows GEMM); other values unchanged"""
     if isinstance(y, LinY):
@@ -619,36 +533,6 @@ def resolve(y):
     return y
 
 
-class _FFN1(torch.autograd.Function):
-    """h = dropout_p(relu(x w1^T + b1)) (linear1 with its activation epilogue) of an FFN whose
-    linear2 runs inside the next resnorm launch (LinY with relu_p): the gradient arriving here
-    already carries the activation mask (the LinY backward's dgrad epilogue)."""
-
-    @staticmethod
-    def forward(ctx, x, w1, b1, p, site):
-        bf = torch.bfloat16
-        C = x.shape[-1]
-        xc = x.reshape(-1, C)
-        w1c, b1c = gemm.cast_param(w1, bf), gemm.cast_param(b1, bf)
-        seed = flash._seed(x.device) if p > 0 else None
-        h = gemm.act_gemm(xc, w1c, _bias(b1c), True, 1, p, seed, site)
-        ctx.save_for_backward(xc, w1c)
-        ctx.params = (w1, b1)
-        ctx.meta = (x.shape, x.dtype)
-        return h
-
-    @staticmethod
-    def backward(ctx, dy1):
-        xc, w1c = ctx.saved_tensors
-        w1, b1 = ctx.params
-        xshape, xdt = ctx.meta
-        need = ctx.needs_input_grad
-        dy1 = dy1.reshape(-1, w1c.shape[0]).to(torch.bfloat16).contiguous()
-        dw1, db1 = gemm.linear_weight_grads(dy1, xc, w1, b1, need[1], need[2])
-        dx = gemm.act_gemm(dy1, w1c, None, False).to(xdt).view(xshape) if need[0] else None
-        return dx, dw1, db1, None, None
-
-
 def resnorm(pend, norm_a=None, pos=None, want_a=True, want_ap=False, norm_b=None, pos_fan=None,
             norm_b_fan=None, xb_into=None):
     """-> (s, xa, xap, xb) for Pending(src, y, p, site); unwanted outputs are None.
@@ -656,10 +540,9 @@ def resnorm(pend, norm_a=None, pos=None, want_a=True, want_ap=False, norm_b=None
     xb_into = (out, l): xb of these (Q, B, C) rows is written in bf16 into out[l] of an
     (L, B, Q, C) buffer (the heads' row order) and returned as that (Q, B, C) view."""
     src, y, p, psite = pend
-    fuse = isinstance(y, LinY) and src is not None and linres_ok(y, y.w.shape[0])
-    if isinstance(y, LinY) and not fuse:
+    if isinstance(y, LinY):
         y = resolve(y)
-    ref = src if fuse else (y if y is not None else src)
+    ref = y if y is not None else src
     shape = tuple(ref.shape)
     if norm_a is None:
         want_a = want_ap = False
@@ -682,9 +565,6 @@ def resnorm(pend, norm_a=None, pos=None, want_a=True, want_ap=False, norm_b=None
     gb = norm_b.weight if norm_b is not None else None
     bb = norm_b.bias if norm_b is not None else None
     with torch.autocast("cuda", enabled=False):
-        if fuse:
-            return _LinResNorm.apply(meta, src, y.x, y.w, y.b, pos if want_ap else None,
-                                     ga, ba, gb, bb, y.relu_p)
         return _ResNorm.apply(meta, src, y, pos if want_ap else None, ga, ba, gb, bb)
 
 
@@ -804,15 +684,8 @@ def ffn_weights_ok(x, w1, w2):
     return gemm.shape_ok(M, N, F) and gemm.shape_ok(M, F, N) and gemm.shape_ok(M, C, F)
 
 
-def ffn(x, linear1, linear2, activation, dropout, site, defer=False):
-    """linear2(dropout(activation(linear1(x)))) of a transformer layer (bf16 rows); defer: a
-    LinY whose linear2 the next resnorm launch computes (csrc/linres.hip)"""
-    if defer and linres and _ffn_ok(x, linear1, linear2, activation) and \
-            _native.load().ov3d_linres_supported(linear2.weight.shape[0], linear2.weight.shape[1]):
-        p = dropout.p if dropout.training else 0.0
-        with torch.autocast("cuda", enabled=False):
-            h = _FFN1.apply(x, linear1.weight, linear1.bias, p, site)
-        return LinY(h.view(*x.shape[:-1], h.shape[-1]), linear2.weight, linear2.bias, p)
+def ffn(x, linear1, linear2, activation, dropout, site):
+    """linear2(dropout(activation(linear1(x)))) of a transformer layer (bf16 rows)"""
     if _ffn_ok(x, linear1, linear2, activation):
         p = dropout.p if dropout.training else 0.0
         with torch.autocast("cuda", enabled=False):

@@ -281,8 +281,7 @@ class TransformerEncoderLayer(nn.Module):
         if not self.use_ffn:
             return rn.Pending(s, y, p1, site1)
         s, x, _, _ = rn.resnorm(rn.Pending(s, y, p1, site1), self.norm2)
-        y = rn.ffn(x, self.linear1, self.linear2, self.activation, self.dropout, site_ffn,
-                   defer=True)
+        y = rn.ffn(x, self.linear1, self.linear2, self.activation, self.dropout, site_ffn)
         return rn.Pending(s, y, p2, site2)
 
     def fused_ok(self, x):
@@ -345,8 +344,7 @@ class TransformerDecoderLayer(nn.Module):
         else:
             y = self.multihead_attn(qx, memory_pos, memory, attn_mask=memory_mask, defer_out=True)
         s, x3, _, _ = rn.resnorm(rn.Pending(s, y, p2, site2), self.norm3)
-        y = rn.ffn(x3, self.linear1, self.linear2, self.activation, self.dropout, site_ffn,
-                   defer=True)
+        y = rn.ffn(x3, self.linear1, self.linear2, self.activation, self.dropout, site_ffn)
         return rn.Pending(s, y, p3, site3)
 
     def fused_ok(self, x):

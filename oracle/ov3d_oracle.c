@@ -22,6 +22,14 @@
  *       (box_intersection, K2 = rect2.shape[2] bug), and utils/box_util.py:517-618
  *       (TorchScript path, float32, all K2).
  *   NMS   : utils/nms.py:79-162 (nms_3d_faster / nms_3d_faster_samecls).
+ *   gather: un-vendored pointnet2 gather_operation (model_3detr.py:174-186, 355-361).
+ *   2D projection: utils/image_util.py:117-134, 286-298 + criterion.py:386-391.
+ *   SA MLP + max-pool: upstream SharedMLP / PointnetSAModuleVotes (model_3detr.py:353-362),
+ *       float64 (a tolerance checker of the bf16 path, not bit-exact).
+ * The §8(b) boundary's entry points have twins here with the suffix _cpu and no stream argument:
+ * fps, ball_query, group (+ bwd), gather (+ bwd), sa_mlp (+ bwd), giou3d, nms3d, project_box2d,
+ * roi_align (and lsap for the matcher).  Not twinned: the GIoU backward (checked against the
+ * reference's own autograd through tests/golden/giou.npz instead).
  */
 #include <math.h>
 #include <stdint.h>
@@ -136,6 +144,25 @@ int ov3d_group_cpu(const float* feats, const int32_t* idx, int B, int C, int N, 
                     int k = idx[((size_t)b * M + j) * S + s];
                     out[(((size_t)b * C + c) * M + j) * S + s] =
                         (k >= 0 && k < N) ? feats[((size_t)b * C + c) * N + k] : 0.f;
+                }
+    return 0;
+}
+
+/* its backward (grouping_operation's, the interim SA's input gradient): grad_out (B,C,M,S) ->
+ * grad_features (B,C,N), zero-filled, added in (j, s) order.  Twin of ov3d_group_bwd (equal
+ * up to float summation order where a point has several (centroid, slot) hits). */
+int ov3d_group_bwd_cpu(const float* grad_out, const int32_t* idx, int B, int C, int N, int M,
+                       int S, float* grad_feats) {
+    if (B < 0 || C < 0 || N < 0 || M < 0 || S < 0) return -1;
+    memset(grad_feats, 0, sizeof(float) * (size_t)B * C * N);
+    for (int b = 0; b < B; ++b)
+        for (int c = 0; c < C; ++c)
+            for (int j = 0; j < M; ++j)
+                for (int s = 0; s < S; ++s) {
+                    int k = idx[((size_t)b * M + j) * S + s];
+                    if (k >= 0 && k < N)
+                        grad_feats[((size_t)b * C + c) * N + k] +=
+                            grad_out[(((size_t)b * C + c) * M + j) * S + s];
                 }
     return 0;
 }
@@ -564,5 +591,321 @@ int ov3d_roi_align_cpu(const float* feat, int N, int H, int W, int C, const floa
                     out[(((size_t)r * P + ph) * P + pw) * C + c] = acc / count;
                 }
     }
+    return 0;
+}
+
+/* ------------------------------------------------------- gather (pointnet2 gather_operation) */
+
+/* gather_operation [upstream pointnet2, called at models/model_3detr.py:355-361 through the SA
+ * module and :174-186 for the query points]: features (B,C,N), idx (B,M) -> out (B,C,M); an
+ * index outside [0, N) reads 0 (the HIP kernel's guard).  Twin of ov3d_gather_fwd. */
+int ov3d_gather_fwd_cpu(const float* feats, const int32_t* idx, int B, int C, int N, int M,
+                        float* out) {
+    if (B < 0 || C < 0 || N < 0 || M < 0) return -1;
+    for (int b = 0; b < B; ++b)
+        for (int c = 0; c < C; ++c)
+            for (int j = 0; j < M; ++j) {
+                int k = idx[(size_t)b * M + j];
+                out[((size_t)b * C + c) * M + j] =
+                    (k >= 0 && k < N) ? feats[((size_t)b * C + c) * N + k] : 0.f;
+            }
+    return 0;
+}
+
+/* its backward: grad_out (B,C,M) -> grad_features (B,C,N), zero-filled, then added in index
+ * order j = 0..M-1 (the upstream kernel's atomicAdd has no fixed order: equal to the HIP
+ * result whenever the indices of a scene are distinct, as FPS indices are).  Twin of
+ * ov3d_gather_bwd. */
+int ov3d_gather_bwd_cpu(const float* grad_out, const int32_t* idx, int B, int C, int N, int M,
+                        float* grad_feats) {
+    if (B < 0 || C < 0 || N < 0 || M < 0) return -1;
+    memset(grad_feats, 0, sizeof(float) * (size_t)B * C * N);
+    for (int b = 0; b < B; ++b)
+        for (int c = 0; c < C; ++c)
+            for (int j = 0; j < M; ++j) {
+                int k = idx[(size_t)b * M + j];
+                if (k >= 0 && k < N)
+                    grad_feats[((size_t)b * C + c) * N + k] += grad_out[((size_t)b * C + c) * M + j];
+            }
+    return 0;
+}
+
+/* ------------------------------------------------------------- 2D projection (a14) */
+
+/* NaN-propagating min / max (torch's min / max reductions: once NaN, stay NaN) */
+static float nmin_f(float a, float b) { return ((b < a || b != b) && a == a) ? b : a; }
+static float nmax_f(float a, float b) { return ((b > a || b != b) && a == a) ? b : a; }
+
+/* 3D box -> clamped 2D image box of the RegionCLIP alignment branch: utils/image_util.py:117-134
+ * (project_box_3d_cuda: rotz(-heading), corners with the FULL size as half-extent, quirk Q4),
+ * :286-298 (SUNRGBD_Calibration_cuda: Rtilt^T p, flip_axis_to_camera (x, -z, y), K, divide),
+ * :131-133 ([min v, min u, max v, max u]) and criterion.py:386-391 (clamp to [0, (w,h,w,h)]).
+ * float32 arithmetic in the reference's order.  Rows ordered (.., scene, query): scene of row r
+ * = (r / Q) % B.  Twin of ov3d_project_box2d (the HIP kernel evaluates the same expressions;
+ * cosf / sinf are libm's here, ocml's there: equal to ~1 ulp). */
+int ov3d_project_box2d_cpu(const float* center, const float* size, const float* heading,
+                           long long n, int Q, int B, const float* Rt, const float* Kc,
+                           const int64_t* img_h, const int64_t* img_w, float* out) {
+    if (n < 0 || Q <= 0 || B <= 0) return -1;
+    for (long long r = 0; r < n; ++r) {
+        const int b = (int)((r / Q) % B);
+        const float cx = center[3 * r], cy = center[3 * r + 1], cz = center[3 * r + 2];
+        const float l = size[3 * r], w = size[3 * r + 1], h = size[3 * r + 2];
+        const float a = -heading[r];
+        const float c = cosf(a), s = sinf(a);
+        const float* R = Rt + 9 * b;
+        const float* K = Kc + 9 * b;
+        float umin = INFINITY, umax = -INFINITY, vmin = INFINITY, vmax = -INFINITY;
+        for (int k = 0; k < 8; ++k) {
+            /* x [-l,l,l,-l,-l,l,l,-l], y [w,w,-w,-w,w,w,-w,-w], z [h,h,h,h,-h,-h,-h,-h] */
+            const float x = ((k + 1) & 2) ? l : -l;
+            const float y = (k & 2) ? -w : w;
+            const float z = (k & 4) ? -h : h;
+            const float X = c * x - s * y + cx;
+            const float Y = s * x + c * y + cy;
+            const float Z = z + cz;
+            const float dx = R[0] * X + R[3] * Y + R[6] * Z;
+            const float dy = R[1] * X + R[4] * Y + R[7] * Z;
+            const float dz = R[2] * X + R[5] * Y + R[8] * Z;
+            const float px = dx, py = -dz, pz = dy;
+            const float uu = K[0] * px + K[1] * py + K[2] * pz;
+            const float vv = K[3] * px + K[4] * py + K[5] * pz;
+            const float ww = K[6] * px + K[7] * py + K[8] * pz;
+            const float u = uu / ww, v = vv / ww;
+            umin = nmin_f(umin, u);
+            umax = nmax_f(umax, u);
+            vmin = nmin_f(vmin, v);
+            vmax = nmax_f(vmax, v);
+        }
+        const float wf = (float)img_w[b], hf = (float)img_h[b];
+        const float box[4] = {vmin, umin, vmax, umax};
+        const float lim[4] = {wf, hf, wf, hf};
+        for (int i = 0; i < 4; ++i) {
+            float v = box[i] < 0.f ? 0.f : box[i];
+            v = v > lim[i] ? lim[i] : v;
+            out[4 * r + i] = v;
+        }
+    }
+    return 0;
+}
+
+/* ------------------------------------------------- SA MLP + max-pool (a4), float64 checker */
+
+#define SA_MAX_LAYERS 4
+
+typedef struct {
+    long long R;
+    int S, nl, ch[SA_MAX_LAYERS + 1];
+    double* xhat[SA_MAX_LAYERS];   /* (R, ch[l+1]) normalised pre-activations */
+    double* z[SA_MAX_LAYERS];      /* (R, ch[l+1]) layer outputs relu(gamma xhat + beta) */
+    double* invstd[SA_MAX_LAYERS];
+} sa_state;
+
+static void sa_free(sa_state* st) {
+    for (int l = 0; l < SA_MAX_LAYERS; ++l) {
+        free(st->xhat[l]);
+        free(st->z[l]);
+        free(st->invstd[l]);
+    }
+}
+
+/* the forward of every layer, kept for the backward */
+static int sa_forward(const float* x0, long long R, int S, int nl, const int* ch,
+                      const float* const* W, const float* const* gamma, const float* const* beta,
+                      double eps, sa_state* st, double* mean_out, double* var_out) {
+    memset(st, 0, sizeof(*st));
+    if (R <= 0 || S <= 0 || R % S || nl < 1 || nl > SA_MAX_LAYERS || !x0 || !W) return -1;
+    st->R = R;
+    st->S = S;
+    st->nl = nl;
+    for (int l = 0; l <= nl; ++l) {
+        if (ch[l] <= 0) return -1;
+        st->ch[l] = ch[l];
+    }
+    size_t moff = 0;
+    for (int l = 0; l < nl; ++l) {
+        const int K = ch[l], C = ch[l + 1];
+        st->xhat[l] = (double*)malloc(sizeof(double) * (size_t)R * C);
+        st->z[l] = (double*)malloc(sizeof(double) * (size_t)R * C);
+        st->invstd[l] = (double*)malloc(sizeof(double) * (size_t)C);
+        double* mean = (double*)calloc((size_t)C, sizeof(double));
+        double* var = (double*)calloc((size_t)C, sizeof(double));
+        if (!st->xhat[l] || !st->z[l] || !st->invstd[l] || !mean || !var) {
+            free(mean);
+            free(var);
+            sa_free(st);
+            return -1;
+        }
+        double* y = st->xhat[l];
+        for (long long r = 0; r < R; ++r)
+            for (int c = 0; c < C; ++c) {
+                double acc = 0.0;
+                for (int k = 0; k < K; ++k) {
+                    const double xv = l == 0 ? (double)x0[r * K + k] : st->z[l - 1][r * K + k];
+                    acc += xv * (double)W[l][(size_t)c * K + k];
+                }
+                y[r * C + c] = acc;
+                mean[c] += acc;
+            }
+        for (int c = 0; c < C; ++c) mean[c] /= (double)R;
+        for (long long r = 0; r < R; ++r)
+            for (int c = 0; c < C; ++c) {
+                const double d = y[r * C + c] - mean[c];
+                var[c] += d * d;
+            }
+        for (int c = 0; c < C; ++c) {
+            var[c] /= (double)R;   /* biased: BatchNorm's normalisation in train mode */
+            st->invstd[l][c] = 1.0 / sqrt(var[c] + eps);
+            if (mean_out) mean_out[moff + c] = mean[c];
+            if (var_out) var_out[moff + c] = var[c];
+        }
+        for (long long r = 0; r < R; ++r)
+            for (int c = 0; c < C; ++c) {
+                const double xh = (y[r * C + c] - mean[c]) * st->invstd[l][c];
+                y[r * C + c] = xh;
+                const double g = gamma && gamma[l] ? (double)gamma[l][c] : 1.0;
+                const double bb = beta && beta[l] ? (double)beta[l][c] : 0.0;
+                const double t = g * xh + bb;
+                st->z[l][r * C + c] = t > 0.0 ? t : 0.0;
+            }
+        moff += (size_t)C;
+        free(mean);
+        free(var);
+    }
+    return 0;
+}
+
+/* SharedMLP(ch) + max over S of PointnetSAModuleVotes in train mode [upstream pointnet2
+ * pointnet2_modules.py; configured at models/model_3detr.py:353-362]: per layer a 1x1 Conv2d
+ * without bias (y = x W^T), BatchNorm2d with the batch statistics (biased variance in the
+ * normalisation), ReLU; then F.max_pool2d over the S neighbours of each centroid.
+ *   x0 (R, ch[0]) rows, centroid-major (row = p*S + s), R % S == 0; W[l] (ch[l+1], ch[l]);
+ *   gamma[l] / beta[l] (ch[l+1]) or NULL (1 / 0); nl <= 4 layers.
+ *   out (R/S, ch[nl]) f32; mean / var (sum of ch[1..nl]) f64 per layer, concatenated, or NULL;
+ *   argmax (R/S, ch[nl]) int32 the first s attaining the maximum, or NULL.
+ * float64 throughout: the checker of the fp32 / bf16 device path (ov3d_sa_layer_* kernels via
+ * sa_fused.py), compared within tolerance, not a bit-exact twin. */
+int ov3d_sa_mlp_fwd_cpu(const float* x0, long long R, int S, int nl, const int* ch,
+                        const float* const* W, const float* const* gamma,
+                        const float* const* beta, double eps, float* out, double* mean,
+                        double* var, int32_t* argmax) {
+    sa_state st;
+    if (sa_forward(x0, R, S, nl, ch, W, gamma, beta, eps, &st, mean, var)) return -1;
+    const int C = ch[nl];
+    const double* z = st.z[nl - 1];
+    for (long long p = 0; p < R / S; ++p)
+        for (int c = 0; c < C; ++c) {
+            int best = 0;
+            double v = z[(p * S) * C + c];
+            for (int s = 1; s < S; ++s) {
+                const double u = z[(p * S + s) * C + c];
+                if (u > v) {
+                    v = u;
+                    best = s;
+                }
+            }
+            out[p * C + c] = (float)v;
+            if (argmax) argmax[p * C + c] = best;
+        }
+    sa_free(&st);
+    return 0;
+}
+
+/* Gradients of sum(out * dout) (dout (R/S, ch[nl]) f32) for the forward above: the max-pool
+ * routes each centroid's gradient to its first maximum, ReLU passes where gamma xhat + beta > 0,
+ * BatchNorm's train-mode backward (batch statistics), the conv's dW = dy^T x.
+ *   dW[l] (ch[l+1], ch[l]) f32; dgamma[l] / dbeta[l] (ch[l+1]) f32, or NULL arrays / entries. */
+int ov3d_sa_mlp_bwd_cpu(const float* x0, long long R, int S, int nl, const int* ch,
+                        const float* const* W, const float* const* gamma,
+                        const float* const* beta, double eps, const float* dout,
+                        float* const* dW, float* const* dgamma, float* const* dbeta) {
+    sa_state st;
+    if (sa_forward(x0, R, S, nl, ch, W, gamma, beta, eps, &st, NULL, NULL)) return -1;
+    int Cmax = 0;
+    for (int l = 0; l <= nl; ++l) Cmax = ch[l] > Cmax ? ch[l] : Cmax;
+    double* dz = (double*)calloc((size_t)R * Cmax, sizeof(double));
+    double* dy = (double*)malloc(sizeof(double) * (size_t)R * Cmax);
+    double* s1 = (double*)malloc(sizeof(double) * (size_t)Cmax);
+    double* s2 = (double*)malloc(sizeof(double) * (size_t)Cmax);
+    if (!dz || !dy || !s1 || !s2) {
+        free(dz);
+        free(dy);
+        free(s1);
+        free(s2);
+        sa_free(&st);
+        return -1;
+    }
+    {   /* max-pool backward into dz of the last layer */
+        const int C = ch[nl];
+        const double* z = st.z[nl - 1];
+        for (long long p = 0; p < R / S; ++p)
+            for (int c = 0; c < C; ++c) {
+                int best = 0;
+                double v = z[(p * S) * C + c];
+                for (int s = 1; s < S; ++s) {
+                    const double u = z[(p * S + s) * C + c];
+                    if (u > v) {
+                        v = u;
+                        best = s;
+                    }
+                }
+                dz[(p * S + best) * C + c] = (double)dout[p * C + c];
+            }
+    }
+    for (int l = nl - 1; l >= 0; --l) {
+        const int K = ch[l], C = ch[l + 1];
+        const double* xh = st.xhat[l];
+        for (int c = 0; c < C; ++c) s1[c] = s2[c] = 0.0;
+        /* dt = dz * relu'(t); dxhat = gamma dt; s1 = sum dxhat, s2 = sum dxhat xhat */
+        for (long long r = 0; r < R; ++r)
+            for (int c = 0; c < C; ++c) {
+                const double g = gamma && gamma[l] ? (double)gamma[l][c] : 1.0;
+                const double dt = st.z[l][r * C + c] > 0.0 ? dz[r * C + c] : 0.0;
+                dy[r * C + c] = dt;   /* dt kept for dgamma / dbeta */
+                s1[c] += g * dt;
+                s2[c] += g * dt * xh[r * C + c];
+            }
+        if (dgamma && dgamma[l])
+            for (int c = 0; c < C; ++c) {
+                double a = 0.0;
+                for (long long r = 0; r < R; ++r) a += dy[r * C + c] * xh[r * C + c];
+                dgamma[l][c] = (float)a;
+            }
+        if (dbeta && dbeta[l])
+            for (int c = 0; c < C; ++c) {
+                double a = 0.0;
+                for (long long r = 0; r < R; ++r) a += dy[r * C + c];
+                dbeta[l][c] = (float)a;
+            }
+        for (long long r = 0; r < R; ++r)
+            for (int c = 0; c < C; ++c) {
+                const double g = gamma && gamma[l] ? (double)gamma[l][c] : 1.0;
+                const double dxh = g * dy[r * C + c];
+                dy[r * C + c] = st.invstd[l][c] / (double)R *
+                                ((double)R * dxh - s1[c] - xh[r * C + c] * s2[c]);
+            }
+        if (dW && dW[l])
+            for (int c = 0; c < C; ++c)
+                for (int k = 0; k < K; ++k) {
+                    double a = 0.0;
+                    for (long long r = 0; r < R; ++r) {
+                        const double xv = l == 0 ? (double)x0[r * K + k] : st.z[l - 1][r * K + k];
+                        a += dy[r * C + c] * xv;
+                    }
+                    dW[l][(size_t)c * K + k] = (float)a;
+                }
+        if (l > 0)   /* dz of the layer below = dy W */
+            for (long long r = 0; r < R; ++r)
+                for (int k = 0; k < K; ++k) {
+                    double a = 0.0;
+                    for (int c = 0; c < C; ++c) a += dy[r * C + c] * (double)W[l][(size_t)c * K + k];
+                    dz[r * K + k] = a;
+                }
+    }
+    free(dz);
+    free(dy);
+    free(s1);
+    free(s2);
+    sa_free(&st);
     return 0;
 }

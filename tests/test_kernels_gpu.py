@@ -189,6 +189,22 @@ def test_gather_fwd_bwd(cuda):
     torch.testing.assert_close(f.grad, exp)
 
 
+def test_gather_matches_cpu_twin_bit_exact(cuda):
+    """ov3d_gather_fwd / _bwd against the boundary's CPU twins (ov3d_gather_fwd_cpu / _bwd_cpu):
+    bit-exact on FPS-style distinct indices (no summation-order freedom in the backward)"""
+    from ov3d_amd import pointnet2_utils as pu
+    g = torch.Generator(device="cpu").manual_seed(12)
+    B, C, N, M = 3, 7, 5000, 512
+    f = torch.randn((B, C, N), generator=g)
+    idx = torch.stack([torch.randperm(N, generator=g)[:M] for _ in range(B)]).int()
+    gout = torch.randn((B, C, M), generator=g)
+    fd = f.to(cuda).requires_grad_()
+    out = pu.gather_operation(fd, idx.to(cuda))
+    out.backward(gout.to(cuda))
+    assert np.array_equal(out.detach().cpu().numpy(), O.gather(f.numpy(), idx.numpy()))
+    assert np.array_equal(fd.grad.cpu().numpy(), O.gather_bwd(gout.numpy(), idx.numpy(), N))
+
+
 # ------------------------------------------------------------------ GIoU
 @pytest.mark.parametrize("tag", ["rot", "aligned"])
 @pytest.mark.parametrize("rflag", [True, False])

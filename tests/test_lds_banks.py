@@ -1,4 +1,4 @@
-"""CPU check of the LDS layouts of csrc/sa_bwd.hip's sa_dy9 / sa_dy2b kernels: every access
+"""CPU check of the LDS layouts of csrc/sa_bwd.hip's sa_dy9 kernel: every access
 pattern of their swizzled / padded images is free of bank conflicts under the lane groups of
 MI355X_MICROARCH.md §LDS (tools/lds_banks_dy9.py enumerates them), and the swizzles are
 bijections."""
@@ -18,7 +18,7 @@ def _tool():
 
 def test_sa_bwd_lds_images_conflict_free():
     res = _tool().main()
-    assert len(res) >= 9
+    assert len(res) >= 8
     assert all(v == 0 for v in res.values()), res
 
 

@@ -77,7 +77,7 @@ def test_package_exports_drop_in_modules():
 
 
 def test_round4_entries_reject_bad_arguments():
-    """The RegionCLIP close / pool / token / library-GEMM entries and the squared-distance mask
+    """The RegionCLIP close / pool / token entries and the squared-distance mask
     kind validate before touching the device (host-side checks; no GPU needed)."""
     from ov3d_amd import _native
     lib = _native.load()
@@ -87,10 +87,6 @@ def test_round4_entries_reject_bad_arguments():
     assert lib.ov3d_avgpool2_nhwc(None, 2, 1, 4, 4, 8, None, None) == -1
     assert lib.ov3d_avgpool2_nhwc(fake, 3, 1, 4, 4, 8, fake, None) == -1            # elem bytes
     assert lib.ov3d_attnpool_tokens(None, 2, 1, 81, 64, None, None, None) == -1
-    assert lib.ov3d_lt_gemm_bias_residual(8, 16, 16, None, 16, None, 16, None, None, 16, 1, None,
-                                          16, None, 0, None) == -1
-    assert lib.ov3d_lt_gemm_bias_residual(8, 16, 16, fake, 8, fake, 16, fake, fake, 16, 1, fake,
-                                          16, None, 0, None) == -1                     # ldx < K
     assert lib.ov3d_attn_mask_pack(fake, 3, 1.0, 1, 32, 64, fake, None) == -1        # kind 3
 
 

@@ -52,3 +52,28 @@ def test_projection_matches_host_restatement(cuda):
     d = torch.where(ok, dev, torch.zeros_like(dev))
     assert (d >= 0).all() and (d <= lim).all()
     assert (d == 0).any() and (d == lim).any()
+
+
+def test_projection_matches_cpu_twin(cuda):
+    """ov3d_project_box2d against its CPU twin (oracle ov3d_project_box2d_cpu, pinned to the
+    reference golden in tests/test_oracle_twins.py): the same float32 expressions in the same
+    order, so equal but for cosf / sinf (ocml vs libm, ~1 ulp) and what that moves"""
+    from ov3d_amd.image_util import project_boxes_2d
+    from oracle import oracle
+    g = torch.Generator().manual_seed(5)
+    L, B, Q = 8, 4, 128
+    n = L * B
+    center = torch.rand((n, Q, 3), generator=g) * torch.tensor([6.0, 6.0, 3.0]) - torch.tensor([3.0, -0.5, 1.0])
+    size = torch.rand((n, Q, 3), generator=g) * 2 + 0.05
+    heading = (torch.rand((n, Q), generator=g) - 0.5) * 2 * np.pi
+    rt = torch.eye(3) + 0.05 * torch.randn((B, 3, 3), generator=g)
+    kk = torch.tensor([[529.5, 0, 365.0], [0, 529.5, 265.0], [0, 0, 1]]).repeat(B, 1, 1)
+    ih, iw = torch.tensor([530, 427, 530, 441]), torch.tensor([730, 561, 681, 591])
+    rep = (lambda t: t.repeat((L,) + (1,) * (t.dim() - 1)))
+    dev = project_boxes_2d(center.to(cuda), size.to(cuda), heading.to(cuda), rep(rt).to(cuda),
+                           rep(kk).to(cuda), rep(ih).to(cuda), rep(iw).to(cuda)).cpu().numpy()
+    twin = oracle.project_box2d(center.numpy(), size.numpy(), heading.numpy(), Q, B, rt.numpy(),
+                                kk.numpy(), ih.numpy(), iw.numpy()).reshape(dev.shape)
+    np.testing.assert_allclose(dev, twin, rtol=2e-5, atol=2e-3)
+    assert (dev == twin).mean() > 0.5   # most boxes: the identical bits
+

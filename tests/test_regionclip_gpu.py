@@ -291,24 +291,3 @@ def test_attnpool_fused_module_equals_token_path(cuda):
     cos = torch.nn.functional.cosine_similarity(got, ref, dim=-1)
     assert cos.min().item() > 0.9999, cos.min().item()
     assert _rel(got, ref) < 1e-2
-
-
-@pytest.mark.parametrize("M,N,K,relu", [(4 * 81, 2560, 640, 1), (1000, 256, 64, 0)])
-def test_lt_gemm_bias_residual_matches_fp32(cuda, M, N, K, relu):
-    """conv3 + bottleneck close as one hipBLASLt matmul vs the fp32 formula (bf16 output:
-    within two roundings of the exact value)."""
-    from ov3d_amd import _native, regionclip
-    g = torch.Generator(device=cuda).manual_seed(9)
-    x = torch.randn(M, K, device=cuda, generator=g).to(torch.bfloat16)
-    w = (torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).to(torch.bfloat16)
-    b = torch.randn(N, device=cuda, generator=g).to(torch.bfloat16)
-    r = torch.randn(M, N, device=cuda, generator=g).to(torch.bfloat16)
-    out = torch.empty((M, N), dtype=torch.bfloat16, device=cuda)
-    ws = regionclip._lt_workspace(cuda)
-    _native.call("ov3d_lt_gemm_bias_residual", M, N, K, x, K, w, K, b, r, N, relu, out, N, ws,
-                 ws.numel(), like=x)
-    ref = x.float() @ w.float().t() + b.float() + r.float()
-    if relu:
-        ref = ref.relu()
-    err = (out.float() - ref).abs()
-    assert (err <= 2 ** -7 * ref.abs() + 1e-2).all(), err.max()

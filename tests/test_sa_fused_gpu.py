@@ -312,3 +312,95 @@ def test_colsum_f32_equals_torch_sum(cuda, nparts, shape):
     assert got.shape == ref.shape
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5 * nparts ** 0.5)
     assert torch.equal(got, sa_fused._colsum(part))
+
+
+@pytest.mark.parametrize("nwg", [256, 1024])
+def test_fused_backward_is_run_to_run_deterministic(cuda, monkeypatch, nwg):
+    """the fused SA backward (sa_dy9 for layer 3, sa_dy2_fused for layer 2 with y1 recomputed from
+    x0) gives bit-identical gradients run to run, at the default workgroup count and at 1024
+    workgroups (four per CU's worth of work queued: any co-residency the register budget allows).
+    Round 5's opt-in sa_dy2b failed exactly this at two workgroups per CU and was removed in
+    round 6 (Fused SA MLP)."""
+    from ov3d_amd import sa_fused, synthetic
+    from ov3d_amd.pointnet2_modules import PointnetSAModuleVotes
+    monkeypatch.setattr(sa_fused, "NWG_DY2", nwg)
+    monkeypatch.setattr(sa_fused, "NWG_DY_FUSED", nwg)
+    torch.manual_seed(4)
+    sa = PointnetSAModuleVotes(radius=0.2, nsample=64, npoint=2048, mlp=[0, 64, 128, 256],
+                               normalize_xyz=True).to(cuda).train()
+    xyz = synthetic.make_batch(8, seed=11, device=cuda)["point_clouds"][..., :3].contiguous()
+    gw = torch.randn(8, 256, 2048, device=cuda)
+    runs = []
+    for _ in range(3):
+        twin = copy.deepcopy(sa)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            _, f, _ = twin(xyz)
+        (f.float() * gw).sum().backward()
+        runs.append({n: p.grad.clone() for n, p in twin.named_parameters()})
+    for r in runs[1:]:
+        for n in runs[0]:
+            assert torch.equal(r[n], runs[0][n]), n
+
+
+def test_fused_sa_matches_cpu_twin(cuda):
+    """the fused bf16 SA MLP + max-pool (sa_fused.sa_mlp_pool over the HIP kernels) against the
+    boundary's CPU twin (oracle ov3d_sa_mlp_fwd_cpu / _bwd_cpu, float64, pinned to torch's
+    Conv2d + BatchNorm2d + ReLU + max_pool2d in tests/test_oracle_twins.py): output and every
+    weight / BN-affine gradient no further from the twin than PyTorch's own bf16 autocast of the
+    same layers (x2, or within 3e-2)"""
+    import torch.nn.functional as F
+    from ov3d_amd import sa_fused
+    from ov3d_amd.pointnet2_modules import PointnetSAModuleVotes
+    from oracle import oracle
+    torch.manual_seed(7)
+    sa = PointnetSAModuleVotes(radius=0.2, nsample=64, npoint=256, mlp=[0, 64, 128, 256],
+                               normalize_xyz=True).to(cuda).train()
+    with torch.no_grad():
+        for layer in sa.mlp_module:
+            bn = layer.bn.bn
+            bn.weight.copy_(torch.randn_like(bn.weight) * 0.5 + 0.6)
+            bn.bias.copy_(torch.randn_like(bn.bias) * 0.2)
+    S, P = 64, 256
+    g = torch.Generator(device="cpu").manual_seed(8)
+    x0 = (torch.rand((P * S, 3), generator=g) * 2 - 1).to(cuda)
+    dout = torch.randn((P, 256), generator=g).to(cuda)
+    layers = list(sa.mlp_module)
+    ws = [l.conv.weight.detach().view(l.conv.weight.shape[0], -1) for l in layers]
+    gs = [l.bn.bn.weight.detach() for l in layers]
+    bs = [l.bn.bn.bias.detach() for l in layers]
+    cpu = lambda ts: [t.float().cpu().numpy() for t in ts]   # noqa: E731
+    out_t, _, _, _ = oracle.sa_mlp(x0.cpu().numpy(), S, cpu(ws), cpu(gs), cpu(bs))
+    dW_t, dg_t, db_t = oracle.sa_mlp_bwd(x0.cpu().numpy(), S, cpu(ws), dout.cpu().numpy(),
+                                         cpu(gs), cpu(bs))
+    twin = [torch.from_numpy(a) for a in [out_t] + dW_t + dg_t + db_t]
+
+    def grads_of(params):
+        return [p.grad.detach().float().cpu().view(p.shape[0], -1).squeeze(-1) if p.dim() > 1
+                else p.grad.detach().float().cpu() for p in params]
+
+    # fused HIP path
+    for p in sa.parameters():
+        p.grad = None
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = sa_fused.sa_mlp_pool(sa.mlp_module, x0, S)
+    (out.float() * dout).sum().backward()
+    params = [l.conv.weight for l in layers] + [l.bn.bn.weight for l in layers] + \
+        [l.bn.bn.bias for l in layers]
+    fused = [out.detach().float().cpu()] + grads_of(params)
+    # PyTorch's own bf16 autocast of the same layers (the reference modules' ops)
+    wt = [w.clone().requires_grad_() for w in ws]
+    gt = [t.clone().requires_grad_() for t in gs]
+    bt = [t.clone().requires_grad_() for t in bs]
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        x = x0.T.reshape(1, 3, P, S)
+        for w, gm, bb in zip(wt, gt, bt):
+            x = F.relu(F.batch_norm(F.conv2d(x, w[:, :, None, None]), None, None, gm, bb,
+                                    training=True))
+        ref = F.max_pool2d(x, kernel_size=[1, S]).squeeze(-1)[0].T
+    (ref.float() * dout).sum().backward()
+    torchbf = [ref.detach().float().cpu()] + [t.grad.float().cpu() for t in wt + gt + bt]
+    names = ["out"] + [f"dW{i}" for i in range(3)] + [f"dgamma{i}" for i in range(3)] + \
+        [f"dbeta{i}" for i in range(3)]
+    for n, f, tb, tw in zip(names, fused, torchbf, twin):
+        ef, et = _rel(f, tw.view(f.shape)), _rel(tb, tw.view(f.shape))
+        assert ef <= max(2.0 * et, 3e-2), (n, ef, et)

@@ -122,25 +122,6 @@ def main():
             a = {lane: 2 * 8 * (w * 64 + lane + 512 * c) for lane in range(64)}
             t += extra(B128, a, 4, 64)
     res["Dz writes + reads"] = t
-    t = 0   # sa_dy2b: As / Ys (64 wide, 96-element rows) read transposed, columns 0 / 32
-    for c0 in (0, 32):
-        for s in range(4):
-            for hi in (0, 1):
-                a = {}
-                for lane in range(64):
-                    k0, d0 = tr16_lane(lane, c0, s, hi)
-                    a[lane] = 2 * (k0 * 96 + d0)
-                t += extra(HALVES, a, 2, 64)
-    for w in range(4):   # dz1 tile: 2-byte writes (row, channel 32(w&1) + r32), 64-wide rows
-        for i in range(16):
-            a = {lane: 2 * ((32 * (w >> 1) + 4 * (lane >> 5) + (i & 3) + 8 * (i >> 2)) * 64 + 32 * (w & 1) + (lane & 31))
-                 for lane in range(64)}
-            t += extra(HALVES, {k: v - v % 4 for k, v in a.items()}, 1, 32)
-    for c in range(2):   # and its 16-byte reads in the next prologue
-        for w in range(4):
-            a = {lane: 2 * 8 * (w * 64 + lane + 256 * c) for lane in range(64)}
-            t += extra(B128, a, 4, 64)
-    res["sa_dy2b As/Ys/Dz"] = t
     assert sorted(zimg(r, k) for r in range(64) for k in range(128)) == list(range(64 * 128))
     seen = {dst(n, r) for n in range(256) for r in range(64)}
     assert len(seen) == 256 * 64 and min(seen) == 0 and max(seen) == 256 * 64 - 1

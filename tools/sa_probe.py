@@ -1,6 +1,4 @@
-"""Phase stamps of the SA layer-3 backward kernel (sa_dy9_kernel; OV3D_SA_DY8=1: sa_dy8_kernel,
-OV3D_SA_DY4=1: the 4-wave
-sa_dy_fused_kernel) on the GPU.
+"""Phase stamps of the SA layer-3 backward kernel (sa_dy9_kernel) on the GPU.
 
     python tools/sa_probe.py build     # (CPU) tools/probe/libov3d_saprobe.so, sa_bwd.hip with -DOV3D_SA_PROBE
     python tools/sa_probe.py run       # (GPU) one eager SUN training step, per-phase cycles per tile
@@ -58,7 +56,7 @@ def run():
     torch.cuda.synchronize()
     fwd = len(sys.argv) > 2 and sys.argv[2] == "fwd"   # the layer-3 forward (sa_layer_kernel POOL)
     nwg = sa_fused.NPARTS_LAYER if fwd else sa_fused.NWG_DY_FUSED
-    waves = 4 if (fwd or os.environ.get("OV3D_SA_DY4")) else 8
+    waves = 4 if fwd else 8
     dbg = torch.zeros(nwg * waves * 8, dtype=torch.int64, device=dev)
     setter = lib.ov3d_sal_probe_set if fwd else lib.ov3d_sa_probe_set
     setter.argtypes = [ctypes.c_void_p]
