@@ -297,7 +297,7 @@ def timing_collect():
 _CALLED = None
 
 
-STAMP_KINDS = ("fwd", "dq", "dkdv")
+STAMP_KINDS = ("fwd", "dq", "dkdv", "gemm256")
 
 
 def stamps_arm(buf, min_work=1 << 20):

@@ -1557,7 +1557,9 @@ int g_stamp_n = 0;
 int g_stamp_kind[kStampRecs];
 long long g_stamp_off[kStampRecs], g_stamp_waves[kStampRecs], g_stamp_work[kStampRecs];
 
-unsigned long long* stamp_take(int kind, long long work, long long waves) {
+}  // namespace
+
+unsigned long long* ov3d_stamp_take(int kind, long long work, long long waves) {
     if (!g_stamp_buf || work < g_stamp_min_work || g_stamp_n >= kStampRecs ||
         g_stamp_used + 2 * waves > g_stamp_cap)
         return nullptr;
@@ -1570,9 +1572,8 @@ unsigned long long* stamp_take(int kind, long long work, long long waves) {
     g_stamp_used += 2 * waves;
     return p;
 }
-}  // namespace
 
-/* kinds: 0 forward, 1 dQ, 2 dK/dV.  buf = null disarms (the table stays readable). */
+/* kinds: 0 forward, 1 dQ, 2 dK/dV, 3 gemm256 (work = flops).  buf = null disarms (the table stays readable). */
 extern "C" int ov3d_stamps_arm(unsigned long long* buf, long long words, long long min_work) {
     g_stamp_buf = buf;
     g_stamp_cap = buf ? words : 0;
@@ -1640,7 +1641,7 @@ static int attn_fwd_impl(const void* q, const void* k, const void* v, long long 
     set_maskbits(a, maskbits);
     hipStream_t st = ov3d_stream(stream);
     dim3 grid((Lq + 4 * QW - 1) / (4 * QW), B * H, nsplit);
-    a.stamp = stamp_take(0, (long long)Lq * Lk, (long long)grid.x * grid.y * grid.z * 4);
+    a.stamp = ov3d_stamp_take(0, (long long)Lq * Lk, (long long)grid.x * grid.y * grid.z * 4);
     // long attentions take their drop bits from a separate VALU pass (attn_dropgen_kernel);
     // short ones (the decoder) hash in the forward, where one more launch would cost more
     const bool bits = a.thresh && (pregen || dropgen_ahead(Lq, Lk));
@@ -1816,7 +1817,7 @@ extern "C" int ov3d_attn_bwd_masked(const void* q, const void* k, const void* v,
     }
     const dim3 gq((Lq + 4 * QW - 1) / (4 * QW), B * H, nsplit);
     const bool ragged = Lk % KB != 0;
-    a.stamp = stamp_take(1, (long long)Lq * Lk, (long long)gq.x * gq.y * gq.z * 4);
+    a.stamp = ov3d_stamp_take(1, (long long)Lq * Lk, (long long)gq.x * gq.y * gq.z * 4);
     if (maskbits) {
         if (a.thresh)
             (ragged ? attn_bwd_dq_kernel<true, true, true> : attn_bwd_dq_kernel<true, true, false>)<<<gq, 256, 0, st>>>(A);
@@ -1834,7 +1835,7 @@ extern "C" int ov3d_attn_bwd_masked(const void* q, const void* k, const void* v,
     }
     if (!dk) return OV3D_OK;   // dQ (and D) only: dK / dV follow in ov3d_attn_bwd_dkdv_batch
     const dim3 gk((Lk + 127) / 128, B * H);
-    A.stamp2 = stamp_take(2, (long long)Lq * Lk, (long long)gk.x * gk.y * 4);
+    A.stamp2 = ov3d_stamp_take(2, (long long)Lq * Lk, (long long)gk.x * gk.y * 4);
     if (maskbits) {
         if (a.thresh)
             attn_bwd_dkdv_kernel<true, true><<<gk, 256, 0, st>>>(A);

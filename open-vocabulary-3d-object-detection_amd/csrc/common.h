@@ -21,6 +21,11 @@ __device__ __forceinline__ unsigned long long lanemask_lt() {
     return lane == 0 ? 0ull : (~0ull >> (64u - lane));
 }
 
+// host: reserve 2 stamp words per wave of the next launch while stamps are armed (attn.hip
+// ov3d_stamps_arm); kind 0 / 1 / 2 attention fwd / dQ / dK-dV, 3 gemm256; null when disarmed,
+// below the armed min_work, or out of space
+unsigned long long* ov3d_stamp_take(int kind, long long work, long long waves);
+
 // In-kernel launch stamps (measurement only: bench.py's in-step timing of the roofline kernel).
 // Lane 0 of every wave writes the wall clock (100 MHz) at entry (end = 0) and exit (end = 1)
 // into its own 2-word slot of a buffer that nothing else in the kernel reads; st == null: off.

@@ -72,6 +72,7 @@ struct Gemm256Args {
     // (the decoder's K and V projections of the memory; the attention pool's per-head products)
     int nprob;
     long long sA, sB, sbias, sC;
+    unsigned long long* stamp;   // in-kernel launch stamps (bench.py's C5 roofline) or null
 };
 
 __device__ __forceinline__ f32x4 mfma16(i32x4 a, i32x4 b, f32x4 c) {
@@ -154,6 +155,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, lo
 template <bool CONV, bool TAIL>   // TAIL: K % 64 != 0 (its own instance: the checks cost registers)
 __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
     __shared__ __attribute__((aligned(16))) char L[2 * BUF];
+    // launch stamp (measurement only, a.stamp != null): each wave's entry clock waits in LDS and
+    // both words leave in one vector store at the exit -- nothing stays live in registers across
+    // the kernel (ov3d_stamp's entry store kept an address live: at the 256-VGPR cap that spilled)
+    __shared__ unsigned long long s_t0[8];
+    if ((threadIdx.x & 63) == 0) s_t0[threadIdx.x >> 6] = wall_clock64();
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave >> 2, wc = wave & 3;
@@ -474,6 +480,11 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
                 }
         }
     }
+    if (a.stamp && lane == 0) {
+        const long long slot = (long long)blockIdx.x * 8 + (tid >> 6);
+        const unsigned long long t_exit = wall_clock64();
+        *reinterpret_cast<ulonglong2*>(a.stamp + 2 * slot) = make_ulonglong2(s_t0[tid >> 6], t_exit);
+    }
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -506,6 +517,8 @@ int launch(Gemm256Args a, bool conv, void* stream, bool one_tile = false) {
     static const int pp_env = getenv("OV3D_GEMM256_PAIR_PERSIST") ? atoi(getenv("OV3D_GEMM256_PAIR_PERSIST")) : 0;
     one_tile = one_tile && !pp_env;
     const unsigned grid = (unsigned)(tiles <= cus || one_tile ? tiles : cus);
+    // kind 3, work = the launch's flops (2 M N K per problem)
+    a.stamp = ov3d_stamp_take(3, 2LL * a.M * a.N * a.K * a.nprob, (long long)grid * 8);
     if (conv)   // Cin % 64 == 0: no K tail
         hipLaunchKernelGGL((gemm256_kernel<true, false>), dim3(grid), dim3(512), 0, ov3d_stream(stream), a);
     else if (a.K % BK)

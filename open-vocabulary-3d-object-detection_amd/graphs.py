@@ -101,7 +101,7 @@ class StepGraph:
     the table the captured update reads (FusedAdamW.sync_hyper)."""
 
     def __init__(self, model, crit, opt, sample, amp_dtype=torch.bfloat16, clip=0.1,
-                 warmup_iters=3, prefetch_fps=True, regionclip=None):
+                 warmup_iters=3, prefetch_fps=True, regionclip=None, before_capture=None):
         from . import gemm
         from . import pointnet2_utils as pu
         self.model, self.crit, self.opt = model, crit, opt
@@ -142,6 +142,8 @@ class StepGraph:
         torch.cuda.current_stream().wait_stream(self.side)
         if self.prefetch:
             self._set_plan(self._sample(self.static["point_clouds"]))
+        if before_capture is not None:   # e.g. bench.py arms the in-kernel launch stamps here
+            before_capture()
         self.graph = torch.cuda.CUDAGraph()
         self.opt.zero_grad(set_to_none=True)
         # with a process group the RCCL collectives are captured too; the watchdog thread of
