@@ -217,12 +217,15 @@ constexpr int kMaxCombine = 16;
 // diagnostic build only (tools/attn_probe_phases.py): per-wave s_memtime totals of the tile
 // phases of attn_fwd_kernel
 __device__ unsigned long long* g_attn_probe;
-#define PROBE_DECL unsigned long long pr_t = __builtin_amdgcn_s_memtime(), pr_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PROBE_ENTRY const unsigned long long pr_entry = __builtin_amdgcn_s_memtime();
+#define PROBE_DECL unsigned long long pr_t = __builtin_amdgcn_s_memtime(), pr_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
+    pr_acc[7] = pr_t - pr_entry;
 #define PROBE(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); pr_acc[i] += t_ - pr_t; pr_t = t_; } while (0)
 #define PROBE_END do { if ((threadIdx.x & 63) == 0 && g_attn_probe) { \
     unsigned long long* o_ = g_attn_probe + (((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 32 + (threadIdx.x >> 6) * 8; \
     for (int i_ = 0; i_ < 8; ++i_) o_[i_] = pr_acc[i_]; } } while (0)
 #else
+#define PROBE_ENTRY
 #define PROBE_DECL
 #define PROBE(i) do { } while (0)
 #define PROBE_END do { } while (0)
@@ -338,6 +341,7 @@ __global__ void __launch_bounds__(256) attn_dropgen_kernel(AttnArgs a) {
 // BITS: dropout from the words of attn_dropgen_kernel (read, not hashed, not stored)
 template <bool DROP, bool MASK, bool BITS>
 __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
+    PROBE_ENTRY
     // K and V tiles in one array: its 36 KB also stage the output rows after the loop
     __shared__ __attribute__((aligned(16))) bf16 KVs[2][2][KB * LDK];
     bf16 (*const Ks)[KB * LDK] = KVs[0];
