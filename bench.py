@@ -260,9 +260,11 @@ def index_kernel_rates(batch, npoint=2048, radius=0.2, nsample=64, L=8, Q=128, r
         "ov3d_ball_query": (lambda: pu.ball_query(radius, nsample, xyz, new_xyz),
                             B * N * 12 + B * npoint * nsample * 4,
                             f"r={radius} S={nsample}: the scene's points read from HBM once (B*N*12 B) + "
-                            f"the indices written (B*M*S*4 B); the scans themselves ({scanned} points "
+                            f"the indices written (B*M*S*4 B); the reference's scans ({scanned} points "
                             f"over the B*M centroids, each stopping at the S-th in-radius point, SURVEY "
-                            f"Appendix A.2) re-read the L2-resident scene: see scan_points_per_s"),
+                            f"Appendix A.2) are replaced by a per-scene cell index (csrc/group.hip "
+                            f"bq_cells_*: 27 cells per centroid, L2-resident): scan_points_per_s is "
+                            f"the reference-scan-equivalent rate"),
         "ov3d_group_fwd": (lambda: grouper.rows(xyz, new_xyz, None, idx=idx),
                            B * npoint * nsample * (3 * 4 + 4),
                            "(B,M,S,3) fp32 rows out + idx in"),

@@ -67,6 +67,16 @@ int ov3d_nbr_max_bwd(const void* g, const uint8_t* arg, long long P, int S, int 
 int ov3d_ball_query(const float* xyz, const float* new_xyz, int B, int N, int M, float radius,
                     int S, int32_t* idx_out, void* stream);
 
+/* The same output from a uniform-grid index of each scene (two launches: a per-scene counting
+ * sort into ws, then one wave per centroid over the 27 cells around it) instead of a scan of
+ * the whole scene.  ws: >= ov3d_ball_query_ws_bytes(B, N) bytes of device memory, 16-B aligned,
+ * owned by the stream until the call's work is done.  N < 8192 (the scan is cheaper there),
+ * N >= 65536 or S > 64: the scan above. */
+long long ov3d_ball_query_ws_bytes(int B, int N);
+int ov3d_ball_query_cells(const float* xyz, const float* new_xyz, int B, int N, int M,
+                          float radius, int S, int32_t* idx_out, void* ws, long long ws_bytes,
+                          void* stream);
+
 /* QueryAndGroup output with use_xyz=True (pointnet2_utils.QueryAndGroup.forward),
  * written as channels-last rows (the GEMM layout of the SA MLP):
  *   out[b,m,s, 0:3]   = (xyz[b,idx] - new_xyz[b,m]) (/ radius if normalize)

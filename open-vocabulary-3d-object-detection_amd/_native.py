@@ -24,6 +24,7 @@ _SIGS = {
     "ov3d_fps": "piiipppp",
     "ov3d_fps_pair_status": "piiipp",
     "ov3d_ball_query": "ppiiifipp",
+    "ov3d_ball_query_cells": "ppiiifipplp",
     "ov3d_group_fwd": "ppplllpiiiiifipp",
     "ov3d_group_bwd": "ppiiiiilllpp",
     "ov3d_gather_fwd": "ppiiiipp",
@@ -136,7 +137,8 @@ EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_
                           "ov3d_heads_out_workspace", "ov3d_stamps_arm", "ov3d_stamps_count",
                           "ov3d_stamps_get", "ov3d_wall_clock_khz",
                           "ov3d_attnpool_fused_supported", "ov3d_lngemm_supported",
-                          "ov3d_lngemm_bwd_parts", "ov3d_lngemm_stamps_arm", "ov3d_stream_create")
+                          "ov3d_lngemm_bwd_parts", "ov3d_lngemm_stamps_arm", "ov3d_stream_create",
+                          "ov3d_ball_query_ws_bytes")
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_longlong, "f": ctypes.c_float,
        "d": ctypes.c_double}
@@ -218,6 +220,8 @@ def load():
         lib.ov3d_heads_out_workspace.argtypes = [ctypes.c_int] * 2
         lib.ov3d_heads_out_workspace.restype = ctypes.c_longlong
         lib.ov3d_stream_create.argtypes = [ctypes.c_void_p]
+        lib.ov3d_ball_query_ws_bytes.argtypes = [ctypes.c_int] * 2
+        lib.ov3d_ball_query_ws_bytes.restype = ctypes.c_longlong
         lib.ov3d_stream_create.restype = ctypes.c_int
         lib.ov3d_version.argtypes = []
         lib.ov3d_version.restype = ctypes.c_char_p

@@ -155,6 +155,364 @@ void launch_bq_multi(bool aligned, hipStream_t s, const float* xyz, const float*
                            dim3(64 * kBQWavesPerBlock), 0, s, xyz, new_xyz, B, N, M, r2, S, idx);
 }
 
+// ---------------------------------------------------------------------------
+// Cell-indexed ball query (ov3d_ball_query_cells): the same output as the scan above, from
+// a uniform grid instead of a scan of the whole scene.
+//
+// Build (one 1024-thread workgroup per scene): bbox of the finite points, cube cells of side
+// csz = max(1.001 r, extent / (kBQDim - 1)) (at most kBQDim^3 cells), a counting sort in LDS
+// (16-bit counters, N < 65536), the cells' start offsets and the scene's points in cell order
+// as float4 (x, y, z, index bits) into the workspace.
+// Query (one wave per centroid): every point within r of the centroid lies in the 3 x 3 x 3
+// cells around the centroid's cell (csz >= 1.001 r covers the rounding of d2 and of the cell
+// coordinates), i.e. in 9 contiguous runs of 3 cells.  The wave tests those runs' points with
+// the reference's d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx)) < r^2 (dx = centre - point), keeps
+// the hits' indices in LDS and outputs the S smallest in ascending order -- exactly the first S
+// hits of the upstream index-order scan -- padded with the smallest (upstream: the first hit),
+// or zeros without a hit.  A centroid with more than kBQCap hits in its runs falls back to the
+// index-order scan on its wave (exact either way).
+constexpr int kBQDim = 40;
+constexpr int kBQCells = kBQDim * kBQDim * kBQDim;   // 64000 16-bit counters = 125 KiB LDS
+constexpr int kBQCap = 1024;                          // hits kept per wave (4 KiB LDS)
+constexpr int kBQParams = 8;                          // lo xyz, inv, dims xyz, pad (4-byte words)
+// measured (tools/bq_time.py): B=8, M=2048, r=0.2, S=64: N=20000 scan 107 us, cells 50 (build,
+// 8 workgroups) + 23 (query); N=40000 205 vs 106; B=8, N=2048, M=1024, r=0.4: scan 13-16 us,
+// cells 13 + 8
+constexpr int kBQCellsMinN = 8192;
+
+struct BQLayout {
+    float* params;      // [B][kBQParams]
+    uint32_t* cstart;   // [B][kBQCells + 1]
+    float4* pts;        // [B][N]
+};
+
+__host__ __device__ inline long long bq_ws_bytes(int B, int N) {
+    return (long long)B * kBQParams * 4 + (long long)B * (kBQCells + 1) * 4 +
+           (long long)B * N * 16 + 64;
+}
+
+__host__ __device__ inline BQLayout bq_layout(void* ws, int B, int N) {
+    char* c = static_cast<char*>(ws);
+    BQLayout l;
+    l.params = reinterpret_cast<float*>(c);
+    c += (long long)B * kBQParams * 4;
+    l.cstart = reinterpret_cast<uint32_t*>(c);
+    c += (long long)B * (kBQCells + 1) * 4;
+    c = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(c) + 15) & ~uintptr_t(15));
+    l.pts = reinterpret_cast<float4*>(c);
+    return l;
+}
+
+__device__ __forceinline__ bool bq_finite(float x, float y, float z) {
+    return fabsf(x) <= 3.0e38f && fabsf(y) <= 3.0e38f && fabsf(z) <= 3.0e38f;
+}
+
+// the point's cell coordinate on one axis (build and query evaluate the same expression)
+__device__ __forceinline__ int bq_axis(float v, float lo, float inv, int dim) {
+    const float f = floorf((v - lo) * inv);
+    return f < 0.f ? -1 : (f >= (float)dim ? dim : (int)f);
+}
+
+__device__ __forceinline__ float bq_wave_fmin(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fminf(v, __shfl_xor(v, off));
+    return v;
+}
+__device__ __forceinline__ float bq_wave_fmax(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+    return v;
+}
+
+// the scene's points as PPT register slots per thread (point k = tid + 1024 i), all loads in
+// flight at once; PPT = 0: a loop over global memory per pass (N > 32768)
+template <int PPT>
+struct BQPoints {
+    float x[PPT], y[PPT], z[PPT];
+    __device__ __forceinline__ void load(const float* __restrict__ p, int N, int tid) {
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) {
+            const int k = tid + 1024 * i;
+            x[i] = k < N ? p[3 * k] : NAN;
+            y[i] = k < N ? p[3 * k + 1] : NAN;
+            z[i] = k < N ? p[3 * k + 2] : NAN;
+        }
+    }
+    template <class F>
+    __device__ __forceinline__ void each(const float* __restrict__, int, int tid, F&& f) const {
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) f(tid + 1024 * i, x[i], y[i], z[i]);
+    }
+};
+template <>
+struct BQPoints<0> {
+    __device__ __forceinline__ void load(const float* __restrict__, int, int) {}
+    template <class F>
+    __device__ __forceinline__ void each(const float* __restrict__ p, int N, int tid, F&& f) const {
+        for (int k = tid; k < N; k += 1024) f(k, p[3 * k], p[3 * k + 1], p[3 * k + 2]);
+    }
+};
+
+template <int PPT>
+__global__ __launch_bounds__(1024) void bq_cells_build_kernel(const float* __restrict__ xyz, int N,
+                                                              float radius, BQLayout L) {
+    __shared__ uint32_t s_cnt[kBQCells / 2];   // two 16-bit counters per word
+    __shared__ float s_red[6][16];
+    __shared__ uint32_t s_tot[16];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const float* __restrict__ p = xyz + (size_t)b * N * 3;
+    BQPoints<PPT> P;
+    P.load(p, N, tid);
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    P.each(p, N, tid, [&](int, float x, float y, float z) {
+        if (!bq_finite(x, y, z)) return;
+        lo[0] = fminf(lo[0], x); lo[1] = fminf(lo[1], y); lo[2] = fminf(lo[2], z);
+        hi[0] = fmaxf(hi[0], x); hi[1] = fmaxf(hi[1], y); hi[2] = fmaxf(hi[2], z);
+    });
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { lo[a] = bq_wave_fmin(lo[a]); hi[a] = bq_wave_fmax(hi[a]); }
+    if (lane == 0)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) { s_red[a][w] = lo[a]; s_red[3 + a][w] = hi[a]; }
+    for (int i = tid; i < kBQCells / 2; i += 1024) s_cnt[i] = 0u;
+    __syncthreads();
+    float ext = 0.f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        float l = s_red[a][0], h = s_red[3 + a][0];
+        for (int q = 1; q < 16; ++q) { l = fminf(l, s_red[a][q]); h = fmaxf(h, s_red[3 + a][q]); }
+        if (!(l <= h)) { l = 0.f; h = 0.f; }   // no finite point
+        lo[a] = l;
+        hi[a] = h - l;                          // extent
+        ext = fmaxf(ext, hi[a]);
+    }
+    const float csz = fmaxf(fmaxf(fabsf(radius) * 1.001f, ext / (float)(kBQDim - 1)), 1e-30f);
+    const float inv = 1.f / csz;
+    int dim[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) dim[a] = min((int)floorf(hi[a] * inv) + 1, kBQDim);
+    const int ncell = dim[0] * dim[1] * dim[2];
+    if (tid == 0) {
+        float* prm = L.params + (size_t)b * kBQParams;
+        prm[0] = lo[0]; prm[1] = lo[1]; prm[2] = lo[2]; prm[3] = inv;
+        prm[4] = __int_as_float(dim[0]); prm[5] = __int_as_float(dim[1]);
+        prm[6] = __int_as_float(dim[2]); prm[7] = 0.f;
+    }
+    auto cell = [&](float x, float y, float z) {
+        return (min(bq_axis(z, lo[2], inv, dim[2]), dim[2] - 1) * dim[1] +
+                min(bq_axis(y, lo[1], inv, dim[1]), dim[1] - 1)) * dim[0] +
+               min(bq_axis(x, lo[0], inv, dim[0]), dim[0] - 1);
+    };
+    // counts (the old counter value is not kept: positions come from the second pass)
+    P.each(p, N, tid, [&](int, float x, float y, float z) {
+        if (!bq_finite(x, y, z)) return;
+        const int c = cell(x, y, z);
+        atomicAdd(&s_cnt[c >> 1], 1u << (16 * (c & 1)));
+    });
+    __syncthreads();
+    // exclusive scan of the counters: 32 words (64 cells) per thread, in place, and the
+    // starts (+ the end) into the workspace
+    uint32_t* __restrict__ cs = L.cstart + (size_t)b * (kBQCells + 1);
+    const int nw = (ncell + 1) >> 1;
+    constexpr int WPT = kBQCells / 2 / 1024 + 1;   // 32 words
+    const int w0 = tid * WPT;
+    uint32_t sum = 0;
+    for (int i = 0; i < WPT; ++i) {
+        const int wi = w0 + i;
+        if (wi < nw) { const uint32_t v = s_cnt[wi]; sum += (v & 0xffffu) + (v >> 16); }
+    }
+    uint32_t inc = sum;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(inc, off);
+        if (lane >= off) inc += o;
+    }
+    if (lane == 63) s_tot[w] = inc;
+    __syncthreads();
+    uint32_t run = inc - sum;
+    for (int q = 0; q < w; ++q) run += s_tot[q];
+    for (int i = 0; i < WPT; ++i) {
+        const int wi = w0 + i;
+        if (wi >= nw) break;
+        const uint32_t v = s_cnt[wi];
+        const uint32_t a0 = run, a1 = run + (v & 0xffffu);
+        run = a1 + (v >> 16);
+        s_cnt[wi] = a0 | (a1 << 16);
+        if (2 * wi < ncell) cs[2 * wi] = a0;
+        if (2 * wi + 1 < ncell) cs[2 * wi + 1] = a1;
+    }
+    if (tid == 1023) {
+        uint32_t t = 0;
+        for (int q = 0; q < 16; ++q) t += s_tot[q];
+        cs[ncell] = t;
+    }
+    __syncthreads();
+    // scatter: the counter of the point's cell hands out its position (16-bit adds never carry:
+    // every running value stays below the scene's finite-point count < 65536)
+    float4* __restrict__ dst = L.pts + (size_t)b * N;
+    P.each(p, N, tid, [&](int k, float x, float y, float z) {
+        if (!bq_finite(x, y, z)) return;
+        const int c = cell(x, y, z);
+        const uint32_t old = atomicAdd(&s_cnt[c >> 1], 1u << (16 * (c & 1)));
+        const uint32_t pos = (old >> (16 * (c & 1))) & 0xffffu;
+        dst[pos] = make_float4(x, y, z, __int_as_float(k));
+    });
+}
+
+// ascending bitonic sort of one value per lane across the wave
+__device__ __forceinline__ int wave_sort_asc(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const int o = __shfl_xor(v, j);
+            const bool up = (lane & k) == 0;
+            const bool low = (lane & j) == 0;
+            v = (low == up) ? min(v, o) : max(v, o);
+        }
+    return v;
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+constexpr int kBQQWaves = 4;
+
+__global__ __launch_bounds__(64 * kBQQWaves) void bq_cells_query_kernel(
+    const float* __restrict__ xyz, const float* __restrict__ new_xyz, int B, int N, int M, float r2,
+    int S, BQLayout L, int32_t* __restrict__ idx) {
+    __shared__ int s_hit[kBQQWaves][kBQCap];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int c0 = blockIdx.x * kBQQWaves + wv;
+    if (c0 >= B * M) return;   // wave-uniform; no block barrier below
+    const int b = c0 / M;
+    int* __restrict__ hits = s_hit[wv];
+    int32_t* __restrict__ out = idx + (size_t)c0 * S;
+    const float cx = new_xyz[(size_t)c0 * 3], cy = new_xyz[(size_t)c0 * 3 + 1],
+                cz = new_xyz[(size_t)c0 * 3 + 2];
+    const float* __restrict__ prm = L.params + (size_t)b * kBQParams;
+    const float lox = prm[0], loy = prm[1], loz = prm[2], inv = prm[3];
+    const int dx = __float_as_int(prm[4]), dy = __float_as_int(prm[5]), dz = __float_as_int(prm[6]);
+    const uint32_t* __restrict__ cs = L.cstart + (size_t)b * (kBQCells + 1);
+    const float4* __restrict__ pts = L.pts + (size_t)b * N;
+    // the 9 runs: lane r < 9 holds run r = (z, y) row, cells x-1 .. x+1 (clipped)
+    int rbeg = 0, rlen = 0;
+    if (bq_finite(cx, cy, cz)) {
+        const int ix = bq_axis(cx, lox, inv, dx), iy = bq_axis(cy, loy, inv, dy),
+                  iz = bq_axis(cz, loz, inv, dz);
+        if (lane < 9) {
+            const int yy = iy + lane % 3 - 1, zz = iz + lane / 3 - 1;
+            const int x0 = max(ix - 1, 0), x1 = min(ix + 1, dx - 1);
+            if (yy >= 0 && yy < dy && zz >= 0 && zz < dz && x0 <= x1) {
+                const int row = (zz * dy + yy) * dx;
+                rbeg = (int)cs[row + x0];
+                rlen = (int)cs[row + x1 + 1] - rbeg;
+            }
+        }
+    }
+    // inclusive prefix of the run lengths over lanes 0..8
+    int pre = rlen;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) {
+        const int o = __shfl_up(pre, off);
+        if (lane >= off) pre += o;
+    }
+    // wave-uniform run table: P[q] = end of run q in the flattened candidate list, OFF[q] =
+    // its cell-order position minus its flattened start
+    int P[9], OFF[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+        P[q] = __builtin_amdgcn_readlane(pre, q);
+        OFF[q] = __builtin_amdgcn_readlane(rbeg, q) - P[q] + __builtin_amdgcn_readlane(rlen, q);
+    }
+    const int total = P[8];
+    int cnt = 0;
+    bool overflow = false;
+    const unsigned long long below = lanemask_lt();
+    for (int f0 = 0; f0 < total; f0 += 64) {
+        const int f = f0 + lane;
+        bool hit = false;
+        int k = 0;
+        if (f < total) {
+            int off = OFF[0];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) off = P[q] <= f ? OFF[q + 1] : off;
+            const float4 v = pts[f + off];
+            const float ddx = cx - v.x, ddy = cy - v.y, ddz = cz - v.z;
+            const float d2 = fmaf(ddz, ddz, fmaf(ddy, ddy, ddx * ddx));
+            hit = d2 < r2;
+            k = __float_as_int(v.w);
+        }
+        const unsigned long long m = __ballot(hit);
+        const int n = __popcll(m);
+        if (cnt + n > kBQCap) { overflow = true; break; }
+        if (hit) hits[cnt + __popcll(m & below)] = k;
+        cnt += n;
+    }
+    if (overflow) {
+        // index-order scan of the whole scene (the reference's loop), one point per lane
+        int filled = 0, first = 0;
+        for (int base = 0; base < N && filled < S; base += 64) {
+            const int k = base + lane;
+            bool hit = false;
+            if (k < N) {
+                const float ddx = cx - xyz[((size_t)b * N + k) * 3],
+                            ddy = cy - xyz[((size_t)b * N + k) * 3 + 1],
+                            ddz = cz - xyz[((size_t)b * N + k) * 3 + 2];
+                hit = fmaf(ddz, ddz, fmaf(ddy, ddy, ddx * ddx)) < r2;
+            }
+            const unsigned long long m = __ballot(hit);
+            if (!m) continue;
+            if (filled == 0) first = base + __ffsll((long long)m) - 1;
+            const int pos = filled + __popcll(m & below);
+            if (hit && pos < S) out[pos] = k;
+            filled += __popcll(m);
+        }
+        const int fill = filled > 0 ? first : 0;
+        for (int s = (filled < S ? filled : S) + lane; s < S; s += 64) out[s] = fill;
+        return;
+    }
+    if (cnt == 0) {
+        for (int s = lane; s < S; s += 64) out[s] = 0;
+        return;
+    }
+    int v;
+    if (cnt <= 64) {
+        v = lane < cnt ? hits[lane] : INT_MAX;
+    } else {
+        // the S-th smallest hit index t - 1: the least t with #(hits < t) >= S (indices are
+        // distinct), by bisection over [0, N]
+        int tlo = 0, thi = N;   // #(< tlo) < S <= #(< thi)
+        while (thi - tlo > 1) {
+            const int mid = (tlo + thi) >> 1;
+            int c = 0;
+            for (int i = lane; i < cnt; i += 64) c += hits[i] < mid ? 1 : 0;
+            if (wave_sum(c) >= S) thi = mid; else tlo = mid;
+        }
+        // the S hits below thi, compacted in place to the front of the list: chunk i0's kept
+        // values land in [base, base + n) with base + n <= i0 + 64, i.e. on entries this wave
+        // has already read (its LDS operations retire in order)
+        int base = 0;
+        for (int i0 = 0; i0 < cnt; i0 += 64) {
+            const int i = i0 + lane;
+            const int h = i < cnt ? hits[i] : INT_MAX;
+            const bool keep = h < thi;
+            const unsigned long long m = __ballot(keep);
+            if (keep) hits[base + __popcll(m & below)] = h;
+            base += __popcll(m);
+        }
+        v = lane < S ? hits[lane] : INT_MAX;
+    }
+    v = wave_sort_asc(v);
+    const int smallest = __shfl(v, 0);
+    const int have = cnt < S ? cnt : S;
+    for (int s = lane; s < S; s += 64) out[s] = s < have ? v : smallest;
+}
+
 // out (B,M,S,3+C) channels-last rows: thread per output element (row, channel);
 // features addressed through (sb, sn, sc) element strides, so both the reference
 // (B,C,N) layout and the encoder's seq-first (N,B,C) layout are read in place.
@@ -478,6 +836,38 @@ extern "C" int ov3d_ball_query(const float* xyz, const float* new_xyz, int B, in
     else if (cpw == 4) launch_bq_multi<4>(aligned, s, xyz, new_xyz, B, N, M, r2, S, idx_out);
     else if (cpw == 8) launch_bq_multi<8>(aligned, s, xyz, new_xyz, B, N, M, r2, S, idx_out);
     else launch_bq_multi<1>(aligned, s, xyz, new_xyz, B, N, M, r2, S, idx_out);
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" long long ov3d_ball_query_ws_bytes(int B, int N) {
+    return B > 0 && N > 0 ? bq_ws_bytes(B, N) : 0;
+}
+
+extern "C" int ov3d_ball_query_cells(const float* xyz, const float* new_xyz, int B, int N, int M,
+                                     float radius, int S, int32_t* idx_out, void* ws,
+                                     long long ws_bytes, void* stream) {
+    if (B < 0 || N < 0 || M < 0 || S <= 0 || !xyz || !new_xyz || !idx_out) return OV3D_EINVAL;
+    if ((long long)B * M == 0) return OV3D_OK;
+    // the grid's 16-bit cell counters and the one-value-per-lane sort: N < 65536, S <= 64;
+    // beyond that, and below kBQCellsMinN points (the scan of a small scene is cheaper than
+    // the build's ~13 us of single-workgroup phases), the index-order scan (same output)
+    if (N >= 65536 || N < kBQCellsMinN || S > 64)
+        return ov3d_ball_query(xyz, new_xyz, B, N, M, radius, S, idx_out, stream);
+    if (!ws || ws_bytes < bq_ws_bytes(B, N) || (reinterpret_cast<uintptr_t>(ws) & 15))
+        return OV3D_EINVAL;
+    hipStream_t s = ov3d_stream(stream);
+    const BQLayout L = bq_layout(ws, B, N);
+    if (N <= 20480)
+        hipLaunchKernelGGL(bq_cells_build_kernel<20>, dim3(B), dim3(1024), 0, s, xyz, N, radius, L);
+    else if (N <= 32768)
+        hipLaunchKernelGGL(bq_cells_build_kernel<32>, dim3(B), dim3(1024), 0, s, xyz, N, radius, L);
+    else
+        hipLaunchKernelGGL(bq_cells_build_kernel<0>, dim3(B), dim3(1024), 0, s, xyz, N, radius, L);
+    OV3D_LAUNCH_CHECK();
+    hipLaunchKernelGGL(bq_cells_query_kernel, dim3(ov3d_cdiv((long long)B * M, kBQQWaves)),
+                       dim3(64 * kBQQWaves), 0, s, xyz, new_xyz, B, N, M, radius * radius, S, L,
+                       idx_out);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

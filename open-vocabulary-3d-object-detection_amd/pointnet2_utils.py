@@ -126,7 +126,12 @@ def ball_query(radius, nsample, xyz, new_xyz):
     B, N, _ = xyz.shape
     M = new_xyz.shape[1]
     idx = torch.empty((B, M, nsample), dtype=torch.int32, device=xyz.device)
-    nat.call("ov3d_ball_query", xyz, new_xyz, B, N, M, float(radius), int(nsample), idx, like=xyz)
+    # the per-scene cell index (csrc/group.hip bq_cells_*): a stream-ordered temporary from the
+    # caching allocator (a graph's private pool under capture)
+    nbytes = int(nat.load().ov3d_ball_query_ws_bytes(B, N))
+    ws = torch.empty((max(nbytes, 16),), dtype=torch.uint8, device=xyz.device)
+    nat.call("ov3d_ball_query_cells", xyz, new_xyz, B, N, M, float(radius), int(nsample), idx,
+             ws, nbytes, like=xyz)
     return idx
 
 

@@ -128,6 +128,73 @@ def test_ball_query_bit_exact(cuda, B, N, M, r, S, uniform):
     np.testing.assert_array_equal(got, ref)
 
 
+def _bq_case(name, rs):
+    """(xyz (B,N,3), centroids (B,M,3), r, S) for the cell-index edge cases"""
+    B, N, M = 3, 9000, 257   # N >= 8192: the cell path (kBQCellsMinN)
+    xyz = rs.uniform(-2.0, 2.0, (B, N, 3)).astype(np.float32)
+    r, S = 0.2, 64
+    if name == "dense_cluster":      # > 1024 hits in one centroid's runs: the scan fallback
+        xyz[:, :3000] = rs.uniform(0.0, 0.05, (B, 3000, 3))
+    elif name == "mid_density":      # 65 .. 1024 hits: bisection for the S-th smallest index
+        xyz = rs.uniform(0.0, 1.0, (B, N, 3)).astype(np.float32)
+    elif name == "wide_extent":      # one scene 400 m wide: cells far larger than r
+        xyz[1, :10] *= 100.0
+    elif name == "nonfinite":        # NaN / inf points never hit; NaN centroid: no hit
+        xyz[:, 5] = np.nan
+        xyz[:, 6] = np.inf
+        xyz[:, 7, 1] = -np.inf
+    elif name == "huge_radius":      # every point a candidate
+        r = 50.0
+    elif name == "zero_radius":
+        r = 0.0
+    elif name == "negative_radius":  # the reference squares it
+        r = -0.3
+    elif name == "one_point_scene":  # zero extent
+        xyz[:] = 0.5
+    elif name == "S_above_64":       # the index-order scan
+        S = 100
+    elif name == "S_1":
+        S = 1
+    elif name == "boundary":         # lattice of spacing r: neighbours at d2 ~ r^2 (rounding edge)
+        xyz = (rs.randint(-5, 6, (B, N, 3)) * np.float32(0.2)).astype(np.float32)
+    cen = xyz[:, rs.choice(N, M, replace=False)].copy()
+    cen[:, 0] += 100.0               # no neighbour at all
+    cen[:, 1] = xyz[:, 0] + np.float32(abs(r) * 0.999)   # just inside / outside the sphere
+    cen[:, 2] = np.nan if name == "nonfinite" else cen[:, 2]
+    cen[:, 3] = -100.0               # far outside the grid on the low side
+    return xyz, cen, r, S
+
+
+@pytest.mark.parametrize("name", ["dense_cluster", "mid_density", "wide_extent", "nonfinite",
+                                  "huge_radius", "zero_radius", "negative_radius",
+                                  "one_point_scene", "S_above_64", "S_1", "boundary"])
+def test_ball_query_cells_edge_cases(cuda, name):
+    """ov3d_ball_query_cells (the product's ball query: a per-scene cell index, 27 cells per
+    centroid, the S smallest hit indices) equals the index-order scan of the oracle on the
+    inputs that stress it: more hits than the wave keeps (scan fallback), the bisection path,
+    cells far wider than r, non-finite points and centroids, radii 0 / negative / larger than the
+    scene, a zero-extent scene, S > 64, points on cell boundaries"""
+    from ov3d_amd import pointnet2_utils as pu
+    xyz, cen, r, S = _bq_case(name, np.random.RandomState(7))
+    ref = O.ball_query(xyz, cen, r, S)
+    got = pu.ball_query(r, S, torch.from_numpy(xyz).to(cuda), torch.from_numpy(cen).to(cuda))
+    np.testing.assert_array_equal(got.cpu().numpy(), ref)
+
+
+def test_ball_query_cells_equals_scan_at_full_size(cuda):
+    """size-independent check at N = 65535 (the largest the 16-bit cell counters take) and the
+    fallback above it: cells == the scan entry point ov3d_ball_query"""
+    from ov3d_amd import _native as nat, pointnet2_utils as pu
+    for N in (65535, 65536):
+        xyz = scene_batch(2, N, seed=N)
+        xg = xyz.to(cuda)
+        cen = xg[:, ::N // 1024][:, :1024].contiguous()
+        got = pu.ball_query(0.2, 64, xg, cen)
+        scan = torch.empty_like(got)
+        nat.call("ov3d_ball_query", xg, cen, 2, N, 1024, 0.2, 64, scan, like=xg)
+        assert torch.equal(got, scan)
+
+
 # -------------------------------------------------------------- grouping
 @pytest.mark.parametrize("C", [0, 3, 256])
 @pytest.mark.parametrize("gather_bwd", [True, False])

@@ -32,7 +32,7 @@ def build():
     others = [o for o in glob.glob(os.path.join(CSRC, "*.o"))
               if not o.endswith(("sa_bwd.o", "sa_mlp.o"))]
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-o", LIB, *objs, *others,
-                    "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib", "-lhipblaslt"],
+                    "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib"],
                    check=True)
     print("built", LIB)
 
