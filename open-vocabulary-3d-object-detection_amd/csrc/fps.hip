@@ -28,6 +28,8 @@
 
 namespace {
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 constexpr int kThreads = 1024;
 constexpr int kWaves = kThreads / 64;
 constexpr int kMaxPPT = 20;  // 4 VGPRs per slot: 118 VGPRs at PPT=20, spills beyond
@@ -335,17 +337,21 @@ __global__ __launch_bounds__(kThreads) void fps_cull_kernel(const float* __restr
             rk[i] = min(a, c);
             rk[i + 1] = max(a, c);
         }
-    float px[PPT], py[PPT], pz[PPT], td[PPT];
+    // coordinates as packed pairs (slot 2j, 2j+1): the distance update runs on v_pk_add /
+    // v_pk_mul / v_pk_fma, two points per instruction; an odd PPT pads one dead slot
+    constexpr int NP = (PPT + 1) / 2;
+    f32x2 px[NP], py[NP], pz[NP];
+    float td[2 * NP];
     float wlo[3] = {INFINITY, INFINITY, INFINITY}, whi[3] = {-INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
-    for (int i = 0; i < PPT; ++i) {
+    for (int i = 0; i < 2 * NP; ++i) {
         const int pos = w * PW + i * 64 + lane;
-        if (rk[i] != 0xffffffffu) {
+        if (i < PPT && rk[i] != 0xffffffffu) {
             const int k = fps_unrank(rk[i], L);
             s_perm[pos] = (uint16_t)k;
             const float x = p[3 * k], y = p[3 * k + 1], z = p[3 * k + 2];
             const float mag = fmaf(z, z, fmaf(y, y, x * x));
-            px[i] = x; py[i] = y; pz[i] = z;
+            px[i >> 1][i & 1] = x; py[i >> 1][i & 1] = y; pz[i >> 1][i & 1] = z;
             const bool skip = (double)mag <= 1e-3;
             td[i] = skip ? -1.f : 1e10f;
             if (!skip) {
@@ -353,7 +359,8 @@ __global__ __launch_bounds__(kThreads) void fps_cull_kernel(const float* __restr
                 whi[0] = fmaxf(whi[0], x); whi[1] = fmaxf(whi[1], y); whi[2] = fmaxf(whi[2], z);
             }
         } else {
-            px[i] = 0.f; py[i] = 0.f; pz[i] = 0.f; td[i] = -1.f;
+            px[i >> 1][i & 1] = 0.f; py[i >> 1][i & 1] = 0.f; pz[i >> 1][i & 1] = 0.f;
+            td[i] = -1.f;
         }
     }
 #pragma unroll
@@ -389,19 +396,18 @@ __global__ __launch_bounds__(kThreads) void fps_cull_kernel(const float* __restr
 #ifdef OV3D_FPS_PROBE
             pr_did = true;
 #endif
+            // per point: the packed distance (3 pk ops per pair), min into the running
+            // distance, and max3 into the lane's best -- the slot of the best is found after
+            // the wave reduction, on the winning lane only
+            const f32x2 cx = {x1, x1}, cy = {y1, y1}, cz = {z1, z1};
             float best = -1.f;
-            int bi = 0;
-            float sx = 0.f, sy = 0.f, sz = 0.f;  // this lane's best point, carried along
 #pragma unroll
-            for (int i = 0; i < PPT; ++i) {
-                const float dx = px[i] - x1, dy = py[i] - y1, dz = pz[i] - z1;
-                const float d = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                const float d2 = fminf(d, td[i]);  // no NaN canonicalisation: built non-IEEE (Makefile)
-                td[i] = d2;
-                const bool gt = d2 > best;
-                best = gt ? d2 : best;
-                bi = gt ? i : bi;
-                sx = gt ? px[i] : sx; sy = gt ? py[i] : sy; sz = gt ? pz[i] : sz;
+            for (int j = 0; j < NP; ++j) {
+                const f32x2 dx = px[j] - cx, dy = py[j] - cy, dz = pz[j] - cz;
+                const f32x2 d = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
+                td[2 * j] = fminf(d.x, td[2 * j]);   // no NaN canonicalisation: built non-IEEE (Makefile)
+                td[2 * j + 1] = fminf(d.y, td[2 * j + 1]);
+                best = fmaxf(best, fmaxf(td[2 * j], td[2 * j + 1]));
             }
 #ifdef OV3D_FPS_PROBE
             pr_loop += __builtin_amdgcn_s_memtime() - pt0;
@@ -412,19 +418,44 @@ __global__ __launch_bounds__(kThreads) void fps_cull_kernel(const float* __restr
             wtmax = __int_as_float(wm);
             if (wm >= 0) {
                 const unsigned long long cand = __ballot(bb == wm);
-                int wl;
+                int wl, slot;
                 if (__popcll(cand) == 1) {
                     wl = __ffsll((long long)cand) - 1;
+                    // the winning lane's first slot holding wm (slots are in rank order: the
+                    // upstream tie rule inside a thread): one independent compare per slot
+                    // into a lane mask, bit wl tested on the scalar unit
+                    slot = 0;
+#pragma unroll
+                    for (int i = 2 * NP - 1; i >= 0; --i)
+                        slot = ((__ballot(__float_as_int(td[i]) == wm) >> wl) & 1ull) ? i : slot;
                 } else {  // distance tie inside the wave: smallest rank wins
+                    int bi = 0;
+#pragma unroll
+                    for (int i = 2 * NP - 1; i >= 0; --i) bi = __float_as_int(td[i]) == wm ? i : bi;
                     uint32_t my = 0xffffffffu;
                     if (bb == wm) my = fps_rank(s_perm[w * PW + bi * 64 + lane], L);
                     const uint32_t mr = wave_min_u32(my);
                     wl = __ffsll((long long)__ballot(my == mr)) - 1;
+                    slot = __builtin_amdgcn_readlane(bi, wl);
                 }
-                wx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sx), wl));
-                wy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sy), wl));
-                wz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sz), wl));
-                wpos = w * PW + __builtin_amdgcn_readlane(bi, wl) * 64 + wl;
+                // the winner's coordinates: slot is wave-uniform, one branch of the switch
+                switch (slot >> 1) {
+#define OV3D_FPS_PICK(J)                                                                              \
+    case J:                                                                                          \
+        if (J < NP) {                                                                                \
+            const int h_ = slot & 1;                                                                 \
+            wx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(px[J < NP ? J : 0][h_]), wl)); \
+            wy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(py[J < NP ? J : 0][h_]), wl)); \
+            wz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pz[J < NP ? J : 0][h_]), wl)); \
+        }                                                                                            \
+        break;
+                    OV3D_FPS_PICK(0) OV3D_FPS_PICK(1) OV3D_FPS_PICK(2) OV3D_FPS_PICK(3)
+                    OV3D_FPS_PICK(4) OV3D_FPS_PICK(5) OV3D_FPS_PICK(6) OV3D_FPS_PICK(7)
+                    OV3D_FPS_PICK(8) OV3D_FPS_PICK(9)
+#undef OV3D_FPS_PICK
+                    default: break;
+                }
+                wpos = w * PW + slot * 64 + wl;
             }
         }
 #ifdef OV3D_FPS_PROBE

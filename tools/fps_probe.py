@@ -17,7 +17,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "open-vocabulary-3d-object-detection_amd", "csrc")
-OUT = os.path.join(ROOT, "tools", "probe")
+OUT = os.path.join(ROOT, "tools", "fpsprobe")   # travels to the GPU box (tools/probe is gpurun-ignored)
 NONIEEE = ["-mno-amdgpu-ieee", "-fno-honor-nans"]   # the product's fps.o flags (csrc/Makefile)
 FPS = os.path.join(CSRC, "fps.hip")
 BASE = os.path.join(OUT, "fps_base.hip")      # a saved earlier fps.hip to A/B against (optional)
@@ -35,7 +35,7 @@ def build():
         if not os.path.exists(src):
             continue
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17",
-               "-ffp-contract=off", "-shared", *flags, src,
+               "-ffp-contract=off", "-shared", f"-I{CSRC}", *flags, src,
                "-o", os.path.join(OUT, f"libfps_{name}.so")]
         subprocess.run(cmd, check=True)
         print("built", name)

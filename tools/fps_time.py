@@ -1,5 +1,8 @@
-"""Time ov3d_fps (HIP events, median) at the SUN (B=8, N=20000) and ScanNet (B=8, N=40000)
-pre-encoder shapes, M=2048: ms per launch and us per sampling iteration."""
+"""FPS launch times (HIP events) on the steps' shapes: B=8, N=20000 -> 2048 (SUN pre-encoder),
+2048 -> 128 (query FPS), N=40000 -> 2048 (ScanNet, the two-workgroup kernel).
+
+    python tools/fps_time.py      # (GPU) one JSON line per shape: ms per launch, us per iteration
+"""
 import json
 import os
 import sys
@@ -11,17 +14,24 @@ import ov3d_import  # noqa: E402
 
 ov3d_import.load()
 from ov3d_amd import pointnet2_utils as pu, synthetic  # noqa: E402
-from bench_kernels import timeit  # noqa: E402
 
 
 def main():
-    dev = torch.device("cuda", 0)
-    res = {}
-    for n in (20000, 40000):
-        xyz = synthetic.make_batch(8, seed=1, num_points=n, device=dev)["point_clouds"][..., :3].contiguous()
-        ms = timeit(lambda: pu.furthest_point_sample_gather(xyz, 2048), reps=10, warm=2)
-        res[f"fps_B8_N{n}_M2048"] = {"ms": round(ms, 3), "us_per_iter": round(ms * 1e3 / 2048, 3)}
-    print(json.dumps(res))
+    for (B, N, M) in [(8, 20000, 2048), (8, 2048, 128), (8, 40000, 2048)]:
+        xyz = synthetic.make_batch(B, seed=2, num_points=N, device="cuda")["point_clouds"][..., :3].contiguous()
+        pu.furthest_point_sample(xyz, M)
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            pu.furthest_point_sample(xyz, M)
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        ms = sorted(ts)[len(ts) // 2]
+        print(json.dumps({"B": B, "N": N, "M": M, "ms": round(ms, 4),
+                          "us_per_iter": round(ms * 1e3 / (M - 1), 4)}), flush=True)
 
 
 if __name__ == "__main__":
