@@ -105,7 +105,7 @@ def test_full_size_c4_train_step_properties(cuda):
         called = _native.census_stop()
     for k in ("ov3d_attn_mask_pack", "ov3d_attn_fwd_masked", "ov3d_attn_bwd_masked", "ov3d_nbr_max_fwd",
               "ov3d_nbr_max_bwd", "ov3d_giou3d_bwd", "ov3d_sa_layer_pool_fwd", "ov3d_fps",
-              "ov3d_ball_query"):
+              "ov3d_ball_query_cells"):
         assert called.get(k), (k, sorted(called))
     # the interim SA's grouped rows: bf16, zero-padded to 264 columns (aligned GEMM K)
     assert called.get("ov3d_group_rows_bf16"), sorted(called)

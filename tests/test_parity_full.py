@@ -128,7 +128,9 @@ def test_bf16_step_matches_float64_reference(cuda, name, ds):
         rep = F.run(name, ds, cuda, amp=torch.bfloat16, grad_floor=F.BF16_GRAD_FLOOR)
     finally:
         called = _native.census_stop()
-    missing = [k for k in BF16_KERNELS[ds] if not called.get(k)]
+    # ball query: the index-order scan below 8192 points, the cell index above (same results)
+    missing = [k for k in BF16_KERNELS[ds]
+               if not (called.get(k) or (k == "ov3d_ball_query" and called.get("ov3d_ball_query_cells")))]
     assert not missing, (missing, sorted(called))
     with F.torch_bf16_path():
         base = F.run(name, ds, cuda, amp=torch.bfloat16, grad_floor=F.BF16_GRAD_FLOOR)
