@@ -378,7 +378,7 @@ __global__ __launch_bounds__(kThreads) void fps_cull_kernel(const float* __restr
 
 #ifdef OV3D_FPS_PROBE
     // diagnostic build only (tools/fps_probe.py): per-wave phase cycle totals
-    unsigned long long pr_loop = 0, pr_upd = 0, pr_nupd = 0, pr_cupd = 0, pr_cnupd = 0, pr_bar = 0, pr_post = 0;
+    unsigned long long pr_wm = 0, pr_slot = 0, pr_xyz = 0, pr_loop = 0, pr_upd = 0, pr_nupd = 0, pr_cupd = 0, pr_cnupd = 0, pr_bar = 0, pr_post = 0;
     const unsigned long long pr_rt0 = __builtin_amdgcn_s_memrealtime();
     const unsigned long long pr_c0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -413,49 +413,47 @@ __global__ __launch_bounds__(kThreads) void fps_cull_kernel(const float* __restr
             pr_loop += __builtin_amdgcn_s_memtime() - pt0;
 #endif
             const int bb = __float_as_int(best);
+            // the slot of the lane's best: the first pair whose max is the best, then the first
+            // slot of that pair holding it (slots are in rank order: the upstream tie rule inside
+            // a thread); a 10-step select chain, independent of the wave reduction below
+            int bi = 0;
+#pragma unroll
+            for (int j = NP - 1; j >= 0; --j) {
+                const int in_pair = __float_as_int(td[2 * j]) == bb ? 2 * j : 2 * j + 1;
+                bi = __float_as_int(fmaxf(td[2 * j], td[2 * j + 1])) == bb ? in_pair : bi;
+            }
             const int wm = wave_max_i32(bb);
+#ifdef OV3D_FPS_PROBE
+            unsigned long long pq = __builtin_amdgcn_s_memtime();
+            pr_wm += pq - pt0;
+#endif
             wdist = wm;
             wtmax = __int_as_float(wm);
             if (wm >= 0) {
                 const unsigned long long cand = __ballot(bb == wm);
-                int wl, slot;
+                int wl;
                 if (__popcll(cand) == 1) {
                     wl = __ffsll((long long)cand) - 1;
-                    // the winning lane's first slot holding wm (slots are in rank order: the
-                    // upstream tie rule inside a thread): one independent compare per slot
-                    // into a lane mask, bit wl tested on the scalar unit
-                    slot = 0;
-#pragma unroll
-                    for (int i = 2 * NP - 1; i >= 0; --i)
-                        slot = ((__ballot(__float_as_int(td[i]) == wm) >> wl) & 1ull) ? i : slot;
                 } else {  // distance tie inside the wave: smallest rank wins
-                    int bi = 0;
-#pragma unroll
-                    for (int i = 2 * NP - 1; i >= 0; --i) bi = __float_as_int(td[i]) == wm ? i : bi;
                     uint32_t my = 0xffffffffu;
                     if (bb == wm) my = fps_rank(s_perm[w * PW + bi * 64 + lane], L);
                     const uint32_t mr = wave_min_u32(my);
                     wl = __ffsll((long long)__ballot(my == mr)) - 1;
-                    slot = __builtin_amdgcn_readlane(bi, wl);
                 }
-                // the winner's coordinates: slot is wave-uniform, one branch of the switch
-                switch (slot >> 1) {
-#define OV3D_FPS_PICK(J)                                                                              \
-    case J:                                                                                          \
-        if (J < NP) {                                                                                \
-            const int h_ = slot & 1;                                                                 \
-            wx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(px[J < NP ? J : 0][h_]), wl)); \
-            wy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(py[J < NP ? J : 0][h_]), wl)); \
-            wz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pz[J < NP ? J : 0][h_]), wl)); \
-        }                                                                                            \
-        break;
-                    OV3D_FPS_PICK(0) OV3D_FPS_PICK(1) OV3D_FPS_PICK(2) OV3D_FPS_PICK(3)
-                    OV3D_FPS_PICK(4) OV3D_FPS_PICK(5) OV3D_FPS_PICK(6) OV3D_FPS_PICK(7)
-                    OV3D_FPS_PICK(8) OV3D_FPS_PICK(9)
-#undef OV3D_FPS_PICK
-                    default: break;
-                }
+                const int slot = __builtin_amdgcn_readlane(bi, wl);
+#ifdef OV3D_FPS_PROBE
+                { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); pr_slot += t_ - pq; pq = t_; }
+#endif
+                // the winner's coordinates: slot is wave-uniform, so hipcc reads them from a
+                // private copy of the slot arrays at a scalar offset (three loads, no branches;
+                // round 5's uniform switch over the slots was 0.11 us per iteration slower)
+                wx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(px[slot >> 1][slot & 1]), wl));
+                wy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(py[slot >> 1][slot & 1]), wl));
+                wz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pz[slot >> 1][slot & 1]), wl));
                 wpos = w * PW + slot * 64 + wl;
+#ifdef OV3D_FPS_PROBE
+                pr_xyz += __builtin_amdgcn_s_memtime() - pq;
+#endif
             }
         }
 #ifdef OV3D_FPS_PROBE
@@ -508,9 +506,10 @@ __global__ __launch_bounds__(kThreads) void fps_cull_kernel(const float* __restr
         const unsigned long long c1 = __builtin_amdgcn_s_memtime();
         const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
         if (lane == 0) {
-            unsigned long long* o = dbg + ((size_t)b * kWaves + w) * 9;
+            unsigned long long* o = dbg + ((size_t)b * kWaves + w) * 12;
             o[0] = pr_upd; o[1] = pr_cupd; o[2] = pr_nupd; o[3] = pr_cnupd;
             o[4] = pr_bar; o[5] = pr_post; o[6] = c1 - pr_c0; o[7] = rt1 - pr_rt0; o[8] = pr_loop;
+            o[9] = pr_wm; o[10] = pr_slot; o[11] = pr_xyz;
         }
     }
 #endif
@@ -1449,7 +1448,7 @@ extern "C" int ov3d_fps(const float* xyz, int B, int N, int M, int32_t* idx_out,
 }
 
 #ifdef OV3D_FPS_PROBE
-// diagnostic entry (probe build only): dbg = B*16*9 u64 phase counters
+// diagnostic entry (probe build only): dbg = B*16*12 u64 phase counters
 extern "C" void ov3d_fps_probe_set(unsigned long long* dbg) { g_probe_dbg = dbg; }
 #endif
 

@@ -23,7 +23,6 @@ FPS = os.path.join(CSRC, "fps.hip")
 BASE = os.path.join(OUT, "fps_base.hip")      # a saved earlier fps.hip to A/B against (optional)
 VARIANTS = {                                   # name -> (source, extra flags)
     "stamps": (FPS, ["-DOV3D_FPS_PROBE", *NONIEEE]),
-    "base_stamps": (BASE, ["-DOV3D_FPS_PROBE", *NONIEEE]),
     "base": (BASE, [*NONIEEE]),
     "cur": (FPS, [*NONIEEE]),
 }
@@ -73,7 +72,7 @@ def run():
                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
             dbg = None
             if name.endswith("stamps"):
-                dbg = torch.zeros(B * 16 * 9, dtype=torch.int64, device=dev)
+                dbg = torch.zeros(B * 16 * 12, dtype=torch.int64, device=dev)
                 lib.ov3d_fps_probe_set.argtypes = [ctypes.c_void_p]
                 lib.ov3d_fps_probe_set(dbg.data_ptr())
             idx = torch.empty_like(ref)
@@ -91,8 +90,8 @@ def run():
             us = ev[0].elapsed_time(ev[1]) * 1e3 / reps
             r = {"us": round(us, 1), "us_per_iter": round(us / (M - 1), 4), "bitexact": same}
             if dbg is not None:
-                d = dbg.view(B, 16, 9).double().cpu()
-                upd, cupd, nupd, cnupd, bar, post, cyc, rt, loop = [d[..., i] for i in range(9)]
+                d = dbg.view(B, 16, 12).double().cpu()
+                upd, cupd, nupd, cnupd, bar, post, cyc, rt, loop, pwm, pslot, pxyz = [d[..., i] for i in range(12)]
                 it = (upd + nupd)[0, 0].item()
                 r.update({
                     "clock_ghz": round((cyc / rt * 0.1).median().item(), 3),
@@ -104,6 +103,9 @@ def run():
                     "cyc_publish_barrier_min_wave": round((bar / it).min(1).values.median().item(), 1),
                     "cyc_post": round((post / it).median().item(), 1),
                     "cyc_update_loop_when_updating": round((loop.sum() / upd.sum().clamp(min=1)).item(), 1),
+                    "cyc_to_wave_max_when_updating": round((pwm.sum() / upd.sum().clamp(min=1)).item(), 1),
+                    "cyc_wave_max_to_slot": round((pslot.sum() / upd.sum().clamp(min=1)).item(), 1),
+                    "cyc_slot_to_coords": round((pxyz.sum() / upd.sum().clamp(min=1)).item(), 1),
                     "barrier_wait_by_wave": [round(x, 1) for x in (bar / it).median(0).values.tolist()],
                     "update_frac_by_wave": [round(x, 3) for x in (upd / it).median(0).values.tolist()],
                 })
