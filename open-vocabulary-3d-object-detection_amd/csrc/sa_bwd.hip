@@ -693,13 +693,24 @@ struct Dy2Args {
     const float* W1;    // (K, 3)
 };
 
+// sa_dy2_fused's LDS images (round 6), conflict-free for every access of the kernel under the
+// MI355X lane-group rules (tools/lds_banks_dy9.py enumerates them):
+//   Ds (dy2: 64 rows x 128 n, 256-byte rows): 16-byte piece c of row r at c ^ zsw(r).  Read
+//      row-wise by the dz1 B operand (ds_read_b128, lanes = rows) and transposed by the dW2 A
+//      operand (ds_read_b64_tr_b16 over 4 rows x 16 n).  Padded 272-byte rows were 4-way on the
+//      transposed reads.
+//   As (z1: 64 rows x 64 k, 128-byte rows): piece c of row r at c ^ asw(r) (rows r and r ^ 2 of
+//      a transposed read share a 32-bank half: the XOR moves one to the other 16 banks).
+//   Ys (raw y1, read by rows, 4 channels a lane): 66-dword rows, two rows per bank pair window.
+__device__ __forceinline__ int asw(int r) { return ((r >> 1) & 1) << 2; }
+
 template <int K, int N, bool X0>
 __global__ __launch_bounds__(kThreads, 1) void sa_dy2_fused_kernel(Dy2Args p) {
     static_assert(K == 64 && N == 128, "4 waves = 2 x 2 dz tiles, 32 dW rows each");
-    constexpr int LDK = K + 8, LDN = N + 8;
-    __shared__ __attribute__((aligned(16))) bf16 As[kTile * LDK];   // z1
-    __shared__ __attribute__((aligned(16))) bf16 Ys[kTile * LDK];   // raw y1
-    __shared__ __attribute__((aligned(16))) bf16 Ds[kTile * LDN];   // dy2, row-major
+    constexpr int LDY = K + 68;   // Ys row: 66 dwords
+    __shared__ __attribute__((aligned(256))) bf16 As[kTile * K];   // z1, swizzled (asw)
+    __shared__ __attribute__((aligned(16))) bf16 Ys[kTile * LDY];  // raw y1
+    __shared__ __attribute__((aligned(256))) bf16 Ds[kTile * N];   // dy2, swizzled (zsw)
     __shared__ float a1s[K], b1s[K], mus[K], iss[K], a2s[N], b2s[N], cAs[N], cBs[N], cCs[N];
     __shared__ float w1s[X0 ? 3 * K : 1];
     __shared__ __attribute__((aligned(16))) float x0s[X0 ? 3 * kTile : 4];   // the tile's x0 rows
@@ -737,7 +748,38 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy2_fused_kernel(Dy2Args p) {
     for (int i = 0; i < 16; ++i) st1[i] = st2[i] = 0.f;
     __syncthreads();
 
+    // a thread's coefficients, invariant over the tiles (its chunks all start at the same
+    // channel): from LDS once per launch, not per chunk and tile (the prologue's and the
+    // epilogue's LDS reads were ~40 % of the kernel's LDS instructions)
+    const int kc0 = (tid % (K / 8)) * 8, nc0 = (tid % (N / 8)) * 8;
+    float ca1[8], cb1[8], ca2[8], cb2[8], cca[8], ccb[8], ccc[8], cw1[X0 ? 24 : 1];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        ca1[j] = a1s[kc0 + j]; cb1[j] = b1s[kc0 + j];
+        ca2[j] = a2s[nc0 + j]; cb2[j] = b2s[nc0 + j];
+        cca[j] = cAs[nc0 + j]; ccb[j] = cBs[nc0 + j]; ccc[j] = cCs[nc0 + j];
+    }
+    if constexpr (X0)
+#pragma unroll
+        for (int j = 0; j < 24; ++j) cw1[j] = w1s[3 * kc0 + j];
+    float ea1[16], eb1[16], emu[16], eis[16];   // the epilogue's 16 channels kbase + 8g + 4h + j
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int kk = kbase + 8 * (i >> 2) + 4 * h + (i & 3);
+        ea1[i] = a1s[kk]; eb1[i] = b1s[kk]; emu[i] = mus[kk]; eis[i] = iss[kk];
+    }
     const int ntiles = p.R / kTile;
+    // swizzled element offsets.  dz1 B operand (Ds rows rb*32 + r32): zsw(r) depends on r & 15.
+    const int zr = zsw(r32);
+    // dW2 operands in col_operand's lane pattern (rows 16s + rl (+8), columns c0 + 16(g&1) +
+    // 4(i&3)): piece cq of the 32-column run, 4 elements at eq; the swizzles do not depend on s
+    const int g4 = lane >> 4, i16 = lane & 15;
+    const int rl = 4 * (g4 >> 1) + (i16 >> 2);
+    const int cq = 2 * (g4 & 1) + ((i16 & 3) >> 1), eq = 4 * (i16 & 1);
+    const int dlo = rl * N + 8 * ((4 * wave + cq) ^ zsw(rl)) + eq;
+    const int dhi = (rl + 8) * N + 8 * ((4 * wave + cq) ^ zsw(rl + 8)) + eq;
+    const int alo = rl * K + 8 * (cq ^ asw(rl)) + eq;         // column run 32b: ^ 32b
+    const int ahi = (rl + 8) * K + 8 * (cq ^ asw(rl + 8)) + eq;
     constexpr int C1 = kTile * K / 8 / kThreads;   // 16-byte chunks per thread: y1
     constexpr int C2 = kTile * N / 8 / kThreads;   // y2, dz2
     bf16x8 py1[X0 ? 1 : C1], py2[C2], pdz[C2];
@@ -769,13 +811,13 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy2_fused_kernel(Dy2Args p) {
         const size_t row0 = (size_t)tile * kTile;
 #pragma unroll
         for (int c = 0; c < C1; ++c) {
-            const int ch = tid + c * kThreads, row = ch / (K / 8), kc = (ch % (K / 8)) * 8;
+            const int ch = tid + c * kThreads, row = ch / (K / 8), kc = kc0;
             bf16x8 y1v;
             if constexpr (X0) {
                 const float* xr = &x0s[3 * row];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {   // sa_l1_kernel's value, bit for bit
-                    const float* w = &w1s[3 * (kc + j)];
+                    const float* w = &cw1[3 * j];
                     y1v[j] = (bf16)fmaf(w[2], xr[2], fmaf(w[1], xr[1], w[0] * xr[0]));
                 }
             } else {
@@ -784,21 +826,22 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy2_fused_kernel(Dy2Args p) {
             bf16x8 z;
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-                z[j] = (bf16)fmaxf(fmaf(a1s[kc + j], (float)y1v[j], b1s[kc + j]), 0.f);
-            *reinterpret_cast<bf16x8*>(&As[row * LDK + kc]) = z;
-            *reinterpret_cast<bf16x8*>(&Ys[row * LDK + kc]) = y1v;
+                z[j] = (bf16)fmaxf(fmaf(ca1[j], (float)y1v[j], cb1[j]), 0.f);
+            *reinterpret_cast<bf16x8*>(&As[row * K + 8 * ((kc >> 3) ^ asw(row))]) = z;
+            *reinterpret_cast<bf16x4*>(&Ys[row * LDY + kc]) = bf16x4{y1v[0], y1v[1], y1v[2], y1v[3]};
+            *reinterpret_cast<bf16x4*>(&Ys[row * LDY + kc + 4]) = bf16x4{y1v[4], y1v[5], y1v[6], y1v[7]};
         }
 #pragma unroll
         for (int c = 0; c < C2; ++c) {   // bn_relu_bwd_kernel pass 1 arithmetic
-            const int ch = tid + c * kThreads, row = ch / (N / 8), nc = (ch % (N / 8)) * 8;
+            const int ch = tid + c * kThreads, row = ch / (N / 8), nc = nc0;
             bf16x8 d;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const float yy = (float)py2[c][j];
-                const float dt = fmaf(a2s[nc + j], yy, b2s[nc + j]) > 0.f ? (float)pdz[c][j] : 0.f;
-                d[j] = (bf16)fmaf(cAs[nc + j], dt, fmaf(cBs[nc + j], yy, cCs[nc + j]));
+                const float dt = fmaf(ca2[j], yy, cb2[j]) > 0.f ? (float)pdz[c][j] : 0.f;
+                d[j] = (bf16)fmaf(cca[j], dt, fmaf(ccb[j], yy, ccc[j]));
             }
-            *reinterpret_cast<bf16x8*>(&Ds[row * LDN + nc]) = d;
+            *reinterpret_cast<bf16x8*>(&Ds[row * N + 8 * ((nc >> 3) ^ zsw(row))]) = d;
         }
         __syncthreads();
         if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);   // in flight below
@@ -810,7 +853,7 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy2_fused_kernel(Dy2Args p) {
             for (int i = 0; i < 16; ++i) acc[i] = 0.f;
 #pragma unroll
             for (int s = 0; s < NS; ++s) {
-                const bf16x8 b = *reinterpret_cast<const bf16x8*>(&Ds[(rb * 32 + r32) * LDN + 16 * s + 8 * h]);
+                const bf16x8 b = *reinterpret_cast<const bf16x8*>(&Ds[(rb * 32 + r32) * N + 8 * ((2 * s + h) ^ zr)]);
                 acc = mfma(wt[s], b, acc);
             }
             const int row = rb * 32 + r32;
@@ -821,22 +864,27 @@ __global__ __launch_bounds__(kThreads, 1) void sa_dy2_fused_kernel(Dy2Args p) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) o[j] = (bf16)acc[4 * g + j];
                 *reinterpret_cast<bf16x4*>(p.dz1 + (row0 + row) * K + k) = o;
-                const bf16x4 y4 = *reinterpret_cast<const bf16x4*>(&Ys[row * LDK + k]);
+                const bf16x4 y4 = *reinterpret_cast<const bf16x4*>(&Ys[row * LDY + k]);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {   // bn_relu_bwd pass 0 of layer 1
                     const float yy = (float)y4[j];
-                    const float dt = fmaf(a1s[k + j], yy, b1s[k + j]) > 0.f ? (float)o[j] : 0.f;
+                    const float dt = fmaf(ea1[4 * g + j], yy, eb1[4 * g + j]) > 0.f ? (float)o[j] : 0.f;
                     st1[4 * g + j] += dt;
-                    st2[4 * g + j] = fmaf(dt, (yy - mus[k + j]) * iss[k + j], st2[4 * g + j]);
+                    st2[4 * g + j] = fmaf(dt, (yy - emu[4 * g + j]) * eis[4 * g + j], st2[4 * g + j]);
                 }
             }
         }
         // dW2 += dy2^T z1 over the tile's rows
 #pragma unroll
         for (int s = 0; s < kTile / 16; ++s) {
-            const bf16x8 ad = col_operand(Ds, LDN, lane, wave * 32, s);
+            const bf16x4 dl = tr16(Ds + dlo + 16 * N * s), dh = tr16(Ds + dhi + 16 * N * s);
+            const bf16x8 ad = bf16x8{dl[0], dl[1], dl[2], dl[3], dh[0], dh[1], dh[2], dh[3]};
 #pragma unroll
-            for (int b = 0; b < 2; ++b) dw[b] = mfma(ad, col_operand(As, LDK, lane, 32 * b, s), dw[b]);
+            for (int b = 0; b < 2; ++b) {
+                const bf16x4 al = tr16(As + (alo ^ (32 * b)) + 16 * K * s);
+                const bf16x4 ah = tr16(As + (ahi ^ (32 * b)) + 16 * K * s);
+                dw[b] = mfma(ad, bf16x8{al[0], al[1], al[2], al[3], ah[0], ah[1], ah[2], ah[3]}, dw[b]);
+            }
         }
         if constexpr (X0) {   // the next tile's x0 (its prologue reads it after the barrier)
             if (tid < 3 * kTile / 4 && tile + (int)gridDim.x < ntiles)

@@ -74,12 +74,16 @@ class GraphedModel:
         return {"outputs": layers[0], "aux_outputs": layers[1:]}
 
 
-# "auto": split when the plan is short against the step (the register-resident FPS, N <= 20480
-# points: SUN); ScanNet's 40000-point plan (~8.7 ms) must start with the step or it becomes
-# the bound (C4: 10.5 ms at the start vs 11.9 ms after the encoder)
-MID_START = os.environ.get("OV3D_PLAN_MID_START", "auto")
+# "1" / "auto": split the step so that the plan starts after the encoder ("auto": only for the
+# register-resident FPS, N <= 20480 points).  Default "0": the plan starts with the step.  Round 6
+# (FPS 2.46 -> 2.25 ms): started after the encoder it ran into the encoder BACKWARD (attention
+# dQ / dK/dV 68 / 95 -> 95-103 / 146-148 us beside it, the K = 2048 memory-gradient GEMM
+# ~30 -> 94 us); started with the step it overlaps the SA / encoder forward instead and ends
+# within the decoder: 1633-1636 -> 1642-1645 scenes/s (A/B on one box, tools/ab_plan_start.sh).
+# ScanNet's 40000-point plan (~3.6 ms) must start with the step either way.
+MID_START = os.environ.get("OV3D_PLAN_MID_START", "0")
 MID_START_MAX_POINTS = 20480
-SPLIT_AT = os.environ.get("OV3D_PLAN_SPLIT_AT", "encoder")   # or "memory_kv"
+SPLIT_AT = os.environ.get("OV3D_PLAN_SPLIT_AT", "encoder")   # or "memory_kv", "pre_encoder"
 
 
 class StepGraph:
@@ -170,8 +174,12 @@ class StepGraph:
         # full-grid GEMMs that lose a tail round beside the FPS: 34 -> 53 us each), else
         # after the encoder
         dec = getattr(self.model, "decoder", None)
-        target, attr = (dec, "after_memory_kv") if hasattr(dec, "_forward_fused") and \
-            SPLIT_AT == "memory_kv" else (self.model, "after_encoder")
+        if SPLIT_AT == "pre_encoder":
+            target, attr = self.model, "after_pre_encoder"
+        elif hasattr(dec, "_forward_fused") and SPLIT_AT == "memory_kv":
+            target, attr = dec, "after_memory_kv"
+        else:
+            target, attr = self.model, "after_encoder"
         setattr(target, attr, switch)
         try:
             with torch.cuda.stream(cap):

@@ -222,6 +222,9 @@ class Model3DETR(nn.Module):
             xyz, feats, inds=pre_enc_inds,
             new_xyz=plan.get("pre_enc_xyz") if pre_enc_inds is not None else None,
             ball=plan.get("pre_enc_ball") if pre_enc_inds is not None else None)
+        hook = getattr(self, "after_pre_encoder", None)
+        if hook is not None:   # graphs.StepGraph (OV3D_PLAN_SPLIT_AT=pre_encoder)
+            hook()
         # (B, C, M) view of channels-last rows -> seq-first (M, B, C)
         src = pre_feats.permute(2, 0, 1).contiguous()
         if "interim_inds" in plan:

@@ -29,3 +29,13 @@ def test_swizzles_match_kernel_formulas():
     assert [t.dsw(n) for n in range(8)] == [0, 1, 8, 9, 2, 3, 10, 11]
     assert t.dsw(16) == 1 and t.dsw(17) == 0
     assert [t.zsw(r) for r in range(6)] == [0, 4, 8, 12, 1, 5]
+
+
+def test_sa_dy2_lds_images_conflict_free():
+    """csrc/sa_bwd.hip sa_dy2_fused (round 6): the swizzled Ds / As images and the 66-dword Ys
+    rows leave every access of the kernel conflict-free (the padded round-5 rows did not)"""
+    t = _tool()
+    res = t.dy2_census(True)
+    assert len(res) == 4 and all(v == 0 for v in res.values()), res
+    assert sum(t.dy2_census(False).values()) > 0
+    assert [t.asw(r) for r in range(8)] == [0, 0, 4, 4, 0, 0, 4, 4]

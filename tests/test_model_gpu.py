@@ -206,11 +206,18 @@ def test_step_has_no_host_sync_and_matcher_equals_scipy(cuda):
     assert len(asg) == cost.shape[0] and len(asg[0]) in (0, 2)
 
 
-def test_step_graph_equals_eager_step(cuda):
+@pytest.mark.parametrize("mid_start,split_at", [("0", "encoder"), ("1", "encoder"),
+                                                ("1", "pre_encoder")])
+def test_step_graph_equals_eager_step(cuda, monkeypatch, mid_start, split_at):
     """graphs.StepGraph (whole step captured once: forward, criterion, backward, clip, fused
-    AdamW) replays the eager step: same loss, same updated parameters and BN statistics."""
+    AdamW) replays the eager step: same loss, same updated parameters and BN statistics.  Also
+    as two graphs with the sampling plan released between them (OV3D_PLAN_MID_START=1), split
+    after the encoder or after the pre-encoder SA."""
     import copy
     import ov3d_amd
+    from ov3d_amd import graphs
+    monkeypatch.setattr(graphs, "MID_START", mid_start)
+    monkeypatch.setattr(graphs, "SPLIT_AT", split_at)
     from ov3d_amd import synthetic
     from ov3d_amd.dataset_config import SunrgbdDatasetConfig
     from ov3d_amd.graphs import StepGraph
@@ -232,6 +239,7 @@ def test_step_graph_equals_eager_step(cuda):
     b2 = synthetic.make_batch(2, seed=5, num_points=4096, device=cuda)
     amp = torch.bfloat16
     sg = StepGraph(twin, crit, opt_g, b1, amp_dtype=amp, clip=args.clip_gradient, warmup_iters=1)
+    assert (sg.graph2 is not None) == (mid_start == "1")
     # start the eager side from the graph side's state (parameters, BN buffers, AdamW state):
     # one step then differs only by run-to-run noise of atomics-based kernels
     model.load_state_dict(twin.state_dict())

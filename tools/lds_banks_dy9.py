@@ -130,5 +130,74 @@ def main():
     return res
 
 
+def asw(r):
+    return ((r >> 1) & 1) << 2
+
+
+def dy2_census(swizzled=True):
+    """sa_dy2_fused (K = 64 layer-1 channels, N = 128 layer-2 channels, 4 waves): extra LDS cycles
+    per tile of each access pattern; swizzled=False: the round-5 padded rows (72 / 136 bf16)."""
+    K, N = 64, 128
+    if swizzled:
+        def ds(r, n): return r * N + 8 * ((n >> 3) ^ zsw(r)) + (n & 7)
+        def az(r, k): return r * K + 8 * ((k >> 3) ^ asw(r)) + (k & 7)
+        def ys(r, k): return r * (K + 68) + k
+    else:
+        def ds(r, n): return r * (N + 8) + n
+        def az(r, k): return r * (K + 8) + k
+        def ys(r, k): return r * (K + 8) + k
+    res = {}
+    t = 0   # prologue writes: As / Ds ds_write_b128 (8-lane groups, 32 banks), Ys 2 x ds_write_b64
+    for w in range(4):
+        for c in range(2):
+            a = {l: 2 * az((w * 64 + l + 256 * c) // 8, 8 * ((w * 64 + l + 256 * c) % 8)) for l in range(64)}
+            t += extra(EIGHTS, a, 4, 32)
+            for half in (0, 4):
+                a = {l: 2 * ys((w * 64 + l + 256 * c) // 8, 8 * ((w * 64 + l + 256 * c) % 8) + half)
+                     for l in range(64)}
+                t += extra(QUARTERS, a, 2, 32)
+        for c in range(4):
+            a = {l: 2 * ds((w * 64 + l + 256 * c) // 16, 8 * ((w * 64 + l + 256 * c) % 16)) for l in range(64)}
+            t += extra(EIGHTS, a, 4, 32)
+    res["prologue writes"] = t
+    t = 0   # dz1 B operand: Ds rows rb*32 + r32, n = 16s + 8h (ds_read_b128)
+    for w in range(4):
+        rb = w >> 1
+        for s in range(8):
+            a = {l: 2 * ds(rb * 32 + (l & 31), 16 * s + 8 * (l >> 5)) for l in range(64)}
+            t += extra(B128, a, 4, 64)
+    res["dz1 b128 reads of Ds"] = t
+    t = 0   # layer-1 statistics: Ys row rb*32 + r32, channels kbase + 8g + 4h (ds_read_b64)
+    for w in range(4):
+        kbase, rb = (w & 1) * 32, w >> 1
+        for g in range(4):
+            a = {l: 2 * ys(rb * 32 + (l & 31), kbase + 8 * g + 4 * (l >> 5)) for l in range(64)}
+            t += extra(HALVES, a, 2, 64)
+    res["Ys b64 reads"] = t
+    t = 0   # dW2: A = Ds transposed (columns 32w..), B = As transposed (columns 32b..), tr16
+    for w in range(4):
+        for s in range(4):
+            for hi in (0, 1):
+                a = {}
+                for l in range(64):
+                    r, n = tr16_lane(l, 32 * w, s, hi)
+                    a[l] = 2 * ds(r, n)
+                t += extra(HALVES, a, 2, 64)
+                for b in (0, 1):
+                    a = {}
+                    for l in range(64):
+                        r, k = tr16_lane(l, 32 * b, s, hi)
+                        a[l] = 2 * az(r, k)
+                    t += extra(HALVES, a, 2, 64)
+    res["dW2 tr16 reads of Ds / As"] = t
+    if swizzled:
+        assert sorted(ds(r, n) for r in range(64) for n in range(N)) == list(range(64 * N))
+        assert sorted(az(r, k) for r in range(64) for k in range(K)) == list(range(64 * K))
+    return res
+
+
 if __name__ == "__main__":
     main()
+    for sw in (False, True):
+        for k, v in dy2_census(sw).items():
+            print(f"sa_dy2 {'swizzled' if sw else 'padded  '} {k:28s} extra cycles per tile: {v}")
