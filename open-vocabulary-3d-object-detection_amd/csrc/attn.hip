@@ -50,7 +50,17 @@ typedef short s16x2 __attribute__((ext_vector_type(2)));
 constexpr int D = 64;     // head dim
 constexpr int KB = 64;    // keys per LDS tile
 constexpr int QW = 32;    // queries per wave
-constexpr int LDK = 72;   // padded LDS row, bf16 elements (144 B)
+constexpr int LDK = 72;   // padded LDS row of the output staging images, bf16 elements (144 B)
+
+// K / V / Q / dO tile images (round 6): unpadded 128-byte rows, 16-byte piece c of row r at
+// c ^ isw(r).  One image serves the row reads (ds_read_b128, lanes = rows 32t + r, pieces 2s + h)
+// and the transposed reads (ds_read_b64_tr_b16 over 4 rows x 16 columns, v_operand): isw takes
+// bits 1-3 of the row so that the 8 same-parity rows of a b128 lane group land on 8 different
+// pieces and rows r, r + 2 of a transposed read on opposite 16-bank halves.  Every access is
+// conflict-free under the MI355X lane groups (the padded 144-byte rows left the transposed reads
+// 2-way: 32 extra LDS cycles per tile and wave; tools/lds_banks_dy9.py attn_census).
+__device__ __forceinline__ int isw(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
+__device__ __forceinline__ int img(int r, int c) { return r * D + 8 * ((c >> 3) ^ isw(r)) + (c & 7); }
 
 struct AttnArgs {
     const bf16* q;
@@ -247,8 +257,8 @@ __device__ __forceinline__ bf16x8 v_operand(const bf16* Vs, int lane, int dt, in
     const int g = lane >> 4, i = lane & 15;
     const int d0 = 32 * dt + 16 * (g & 1) + 4 * (i & 3);
     const int k0 = 32 * t + 16 * s + 4 * (g >> 1) + (i >> 2);
-    const bf16x4 lo = tr16(Vs + k0 * LDK + d0);
-    const bf16x4 hi = tr16(Vs + (k0 + 8) * LDK + d0);
+    const bf16x4 lo = tr16(Vs + img(k0, d0));
+    const bf16x4 hi = tr16(Vs + img(k0 + 8, d0));
     bf16x8 a;
     a[0] = lo[0]; a[1] = lo[1]; a[2] = lo[2]; a[3] = lo[3];
     a[4] = hi[0]; a[5] = hi[1]; a[6] = hi[2]; a[7] = hi[3];
@@ -418,8 +428,8 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             const int idx = tid + 256 * c, key = idx >> 3, ch = idx & 7;
-            *reinterpret_cast<bf16x8*>(&Ks[buf][key * LDK + 8 * ch]) = kr[c];
-            *reinterpret_cast<bf16x8*>(&Vs[buf][key * LDK + 8 * ch]) = vr[c];
+            *reinterpret_cast<bf16x8*>(&Ks[buf][img(key, 8 * ch)]) = kr[c];
+            *reinterpret_cast<bf16x8*>(&Vs[buf][img(key, 8 * ch)]) = vr[c];
         }
     };
 
@@ -473,7 +483,7 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a) {
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int s = 0; s < 4; ++s)
-                    ka[t][s] = *reinterpret_cast<const bf16x8*>(K + (32 * t + r) * LDK + 16 * s + 8 * h);
+                    ka[t][s] = *reinterpret_cast<const bf16x8*>(K + img(32 * t + r, 16 * s + 8 * h));
             // masked keys (MASK): -inf initial scores, so the MFMA results carry the mask
             f32x16 st[2];
 #pragma unroll
@@ -830,8 +840,8 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             const int idx = tid + 256 * c, key = idx >> 3, ch = idx & 7;
-            *reinterpret_cast<bf16x8*>(&Ks[buf][key * LDK + 8 * ch]) = kr[c];
-            *reinterpret_cast<bf16x8*>(&Vs[buf][key * LDK + 8 * ch]) = vr[c];
+            *reinterpret_cast<bf16x8*>(&Ks[buf][img(key, 8 * ch)]) = kr[c];
+            *reinterpret_cast<bf16x8*>(&Vs[buf][img(key, 8 * ch)]) = vr[c];
         }
     };
     f32x16 dqt[2];
@@ -874,8 +884,8 @@ __device__ __forceinline__ void attn_bwd_dq_body(const AttnBwdArgs& A) {
                 dpt = mfma(k11, kd, dpt);
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
-                    const bf16x8 ka = *reinterpret_cast<const bf16x8*>(K + (32 * t + r) * LDK + 16 * s + 8 * h);
-                    const bf16x8 va = *reinterpret_cast<const bf16x8*>(V + (32 * t + r) * LDK + 16 * s + 8 * h);
+                    const bf16x8 ka = *reinterpret_cast<const bf16x8*>(K + img(32 * t + r, 16 * s + 8 * h));
+                    const bf16x8 va = *reinterpret_cast<const bf16x8*>(V + img(32 * t + r, 16 * s + 8 * h));
                     st = mfma(ka, qf[s], st);
                     dpt = mfma(va, df[s], dpt);
                 }
@@ -1094,8 +1104,8 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             const int idx = tid + 256 * c, qq = idx >> 3, ch = idx & 7;
-            *reinterpret_cast<bf16x8*>(&Qs[buf][qq * LDK + 8 * ch]) = qr[c];
-            *reinterpret_cast<bf16x8*>(&Ds[buf][qq * LDK + 8 * ch]) = dr[c];
+            *reinterpret_cast<bf16x8*>(&Qs[buf][img(qq, 8 * ch)]) = qr[c];
+            *reinterpret_cast<bf16x8*>(&Ds[buf][img(qq, 8 * ch)]) = dr[c];
         }
         if (tid < QB) {
             Ls[buf][tid] = lr;
@@ -1157,8 +1167,8 @@ __device__ __forceinline__ void attn_bwd_dkdv_body(const AttnBwdArgs& A) {
                 }
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
-                    const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Q + (32 * u + r) * LDK + 16 * s + 8 * h);
-                    const bf16x8 da = *reinterpret_cast<const bf16x8*>(DO + (32 * u + r) * LDK + 16 * s + 8 * h);
+                    const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Q + img(32 * u + r, 16 * s + 8 * h));
+                    const bf16x8 da = *reinterpret_cast<const bf16x8*>(DO + img(32 * u + r, 16 * s + 8 * h));
                     st = mfma(qa, kf[s], st);
                     dpt = mfma(da, vf[s], dpt);
                 }

@@ -39,3 +39,13 @@ def test_sa_dy2_lds_images_conflict_free():
     assert len(res) == 4 and all(v == 0 for v in res.values()), res
     assert sum(t.dy2_census(False).values()) > 0
     assert [t.asw(r) for r in range(8)] == [0, 0, 4, 4, 0, 0, 4, 4]
+
+
+def test_attention_tile_images_conflict_free():
+    """csrc/attn.hip (round 6): the swizzled K / V / Q / dO images serve the row reads, the
+    transposed v_operand reads and the tile stores without bank conflicts (the padded 72-element
+    rows left the transposed reads 2-way)"""
+    t = _tool()
+    assert all(v == 0 for v in t.attn_census(True).values())
+    assert t.attn_census(False)["transposed reads"] > 0
+    assert [t.isw(r) for r in range(8)] == [0, 0, 4, 4, 1, 1, 5, 5]

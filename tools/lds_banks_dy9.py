@@ -196,8 +196,48 @@ def dy2_census(swizzled=True):
     return res
 
 
+def isw(r):
+    return (((r >> 1) & 1) << 2) | ((r >> 2) & 3)
+
+
+def attn_census(swizzled=True):
+    """csrc/attn.hip K / V / Q / dO tile images (64 rows x 64 bf16): extra LDS cycles per tile and
+    wave of the row reads (ds_read_b128, rows 32t + r, columns 16s + 8h), the transposed reads of
+    v_operand (ds_read_b64_tr_b16) and the tile stores (ds_write_b128, 8 lanes a row);
+    swizzled=False: the round-5 padded 72-element rows."""
+    if swizzled:
+        def f(r, c): return r * 64 + 8 * ((c >> 3) ^ isw(r)) + (c & 7)
+    else:
+        def f(r, c): return r * 72 + c
+    res = {"row reads": 0, "transposed reads": 0, "stores": 0}
+    for t in (0, 1):
+        for s in range(4):
+            a = {l: 2 * f(32 * t + (l & 31), 16 * s + 8 * (l >> 5)) for l in range(64)}
+            res["row reads"] += extra(B128, a, 4, 64)
+    for dt in (0, 1):
+        for t in (0, 1):
+            for s in (0, 1):
+                for hi in (0, 1):
+                    a = {}
+                    for l in range(64):
+                        g, i = l >> 4, l & 15
+                        a[l] = 2 * f(32 * t + 16 * s + 4 * (g >> 1) + (i >> 2) + 8 * hi,
+                                     32 * dt + 16 * (g & 1) + 4 * (i & 3))
+                    res["transposed reads"] += extra(HALVES, a, 2, 64)
+    for c in (0, 1):
+        for w in range(4):
+            a = {l: 2 * f((w * 64 + l + 256 * c) >> 3, 8 * ((w * 64 + l + 256 * c) & 7)) for l in range(64)}
+            res["stores"] += extra(EIGHTS, a, 4, 32)
+    if swizzled:
+        assert sorted(f(r, c) for r in range(64) for c in range(64)) == list(range(64 * 64))
+    return res
+
+
 if __name__ == "__main__":
     main()
+    for sw in (False, True):
+        for k, v in attn_census(sw).items():
+            print(f"attn {'swizzled' if sw else 'padded  '} {k:18s} extra cycles per tile and wave: {v}")
     for sw in (False, True):
         for k, v in dy2_census(sw).items():
             print(f"sa_dy2 {'swizzled' if sw else 'padded  '} {k:28s} extra cycles per tile: {v}")
