@@ -36,6 +36,7 @@
 // thread owns 8 consecutive columns of a row: + bias, + residual (fp32), ReLU, one rounding,
 // one 16-byte store.
 #include <stdlib.h>
+#include <type_traits>
 
 #include "common.h"
 
@@ -357,6 +358,12 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
 #pragma unroll
                     for (int j = 0; j < 2; ++j) acc[x][y][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+        // a column tile with only its first 128 columns inside N (N = 640 = 2.5 tiles: the res5
+        // 3x3 / 1x1 convolutions with 640 outputs): B_hi is all zeros, so the two quadrants
+        // against it (P1, P2) are skipped -- their barriers and the A_hi read stay (tile-uniform)
+        const bool bhalf = n0 + 128 >= a.N;
+        auto kloop = [&](auto bh_) __attribute__((always_inline)) {
+        constexpr bool BH = decltype(bh_)::value;
         for (int t = 0; t < nk; ++t) {
             const uint32_t bo = (uint32_t)(t & 1) * BUF;
             const uint32_t a0 = pa0 + bo, a1 = pa1 + bo, b0 = pb0 + bo, b1 = pb1 + bo;
@@ -372,22 +379,26 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
             __builtin_amdgcn_sched_barrier(0);
             barrier();
             // P1: B_hi -> Q(lo, hi); restage B_lo of K-step t+2
-            read_b<3 * HALF>(fb1, b0, b1);
+            if (!BH) read_b<3 * HALF>(fb1, b0, b1);
             if (t + 2 < nk) stage(2, t + 2, tap2, c2);
             barrier();
-            lgkm_wait4(fb1);
-            __builtin_amdgcn_sched_barrier(0);
-            mma_quad(acc[0][1], fa, fb1);
-            __builtin_amdgcn_sched_barrier(0);
+            if (!BH) {
+                lgkm_wait4(fb1);
+                __builtin_amdgcn_sched_barrier(0);
+                mma_quad(acc[0][1], fa, fb1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
             barrier();
             // P2: A_hi -> Q(hi, hi); restage A_lo of K-step t+2
             read_a<HALF>(fa, a0, a1);
             if (t + 2 < nk) stage(0, t + 2, tap2, c2);
             barrier();
             lgkm_wait8(fa);
-            __builtin_amdgcn_sched_barrier(0);
-            mma_quad(acc[1][1], fa, fb1);
-            __builtin_amdgcn_sched_barrier(0);
+            if (!BH) {
+                __builtin_amdgcn_sched_barrier(0);
+                mma_quad(acc[1][1], fa, fb1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
             barrier();
             // P3: -> Q(hi, lo); restage B_hi of K-step t+2; retire K-step t+1
             if (t + 2 < nk) {
@@ -403,6 +414,9 @@ __global__ void __launch_bounds__(512, 2) gemm256_kernel(Gemm256Args a) {
             barrier();
             if constexpr (CONV) { tap1 = tap2; c1 = c2; adv(tap2, c2); }
         }
+        };
+        if (bhalf) kloop(std::true_type{});
+        else kloop(std::false_type{});
         if (a.stagger && wr == 0) barrier();   // close the stagger: every wave is past its last LDS read
 
         // ---- epilogue of this tile, the next tile's first two K-steps in flight meanwhile
