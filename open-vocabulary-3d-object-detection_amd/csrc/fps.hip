@@ -446,7 +446,8 @@ __global__ __launch_bounds__(kThreads) void fps_cull_kernel(const float* __restr
 #endif
                 // the winner's coordinates: slot is wave-uniform, so hipcc reads them from a
                 // private copy of the slot arrays at a scalar offset (three loads, no branches;
-                // round 5's uniform switch over the slots was 0.11 us per iteration slower)
+                // round 5's uniform switch over the slots was 0.11 us per iteration slower, the
+                // slots as vector values indexed by the GPR-index mode 0.08 us slower)
                 wx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(px[slot >> 1][slot & 1]), wl));
                 wy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(py[slot >> 1][slot & 1]), wl));
                 wz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pz[slot >> 1][slot & 1]), wl));
@@ -474,7 +475,10 @@ __global__ __launch_bounds__(kThreads) void fps_cull_kernel(const float* __restr
         // every row of the wave reads the 16 wave slots (lane & 15): the row reduction
         // leaves the maximum in every lane, no lane masking
         const float4 v = s_pub[buf][lane & (kWaves - 1)];
-        const int vp = s_pos[buf][lane & (kWaves - 1)];
+        int vp = s_pos[buf][lane & (kWaves - 1)];
+        // both LDS reads in flight together (hipcc would sink the position read below the
+        // branch: a second LDS round trip on the iteration's serial chain)
+        asm volatile("" : "+v"(vp));
         const int dv = __float_as_int(v.w);
         const int dm = __builtin_amdgcn_readfirstlane(row_max_i32(dv));
         int pj;
