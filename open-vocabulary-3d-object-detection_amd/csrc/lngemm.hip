@@ -50,6 +50,13 @@ constexpr int LDW = 40;           // LDS row of a transposed-read W tile slice (
 constexpr int LDR = RB + 1;       // fp32 partial-product rows [column][row]
 constexpr int MAXP = 2;
 constexpr int BNB = 64;           // backward: output columns per workgroup
+// backward LDS strides (round 6; every read conflict-free under the MI355X lane groups, the
+// padded forward strides left 3.9 conflict cycles per LDS instruction, tools/lds_banks_dy9.py):
+constexpr int LDXB = C + 4;       // dy rows: 130 dwords (16 rows of a read on distinct bank pairs)
+constexpr int LDWB = 32;          // W slice rows unpadded: 4 rows of a transposed read on 4 16-bank windows
+constexpr int LDRB = RB + 4;      // partial products [column][row]: 20 dwords
+constexpr int CRB = C + 32;       // LayerNorm column terms: 4 pad dwords per 32 columns
+__device__ __forceinline__ int redix(int row, int col) { return row * CRB + col + 4 * (col >> 5); }
 enum { EPI_NONE = 0, EPI_RELU_DROP = 1, EPI_MASK = 2 };
 
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
@@ -364,10 +371,10 @@ struct LnBwdArgs {
 
 template <int EPI>
 __global__ void __launch_bounds__(NT) lngemm_bwd_kernel(LnBwdArgs a) {
-    __shared__ __attribute__((aligned(16))) bf16 img[RB * LDX];        // dy rows
-    __shared__ __attribute__((aligned(16))) bf16 wsm[2][C * LDW];      // W (k, 32 columns) x 2
-    __shared__ float red[4][RB * C];                                   // LayerNorm column terms
-    __shared__ float pr[4][BNB * LDR];                                 // per K quarter products
+    __shared__ __attribute__((aligned(16))) bf16 img[RB * LDXB];       // dy rows
+    __shared__ __attribute__((aligned(16))) bf16 wsm[2][C * LDWB];     // W (k, 32 columns) x 2
+    __shared__ __attribute__((aligned(16))) float red[4][RB * CRB];    // LayerNorm column terms
+    __shared__ float pr[4][BNB * LDRB];                                // per K quarter products
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
     const int m0 = blockIdx.x * RB;
     const bool writer = blockIdx.y == 0;
@@ -408,14 +415,16 @@ __global__ void __launch_bounds__(NT) lngemm_bwd_kernel(LnBwdArgs a) {
     const Raw8 rdb = ldraw(orz(a.dxb), a.dxb_bf16, ob);
     const Raw8 rold = ldraw(acc_pos ? a.dpos : (const void*)g_zero, a.dpos_bf16, acc_pos ? off : c);
     // the epilogue's activation values (EPI_MASK), fetched with the rest
-    const int em = tid / (BNB / 4), cg = tid % (BNB / 4);
+    // the epilogue's row / 4-column group: consecutive lanes take consecutive rows of a column
+    // group (the partial-product reads conflict-free; the 8-byte stores hit 16 rows)
+    const int em = tid % RB, cg = tid / RB;
     const bool eact = tid < RB * BNB / 4;
     bf16x4 hv;
     if (EPI == EPI_MASK)
-        hv = *reinterpret_cast<const bf16x4*>(a.H + (long long)(m0 + (eact ? em : 0)) * a.ldh + nb + 4 * cg);
+        hv = *reinterpret_cast<const bf16x4*>(a.H + (long long)(m0 + (eact ? em : 0)) * a.ldh + nb + 4 * (eact ? cg : 0));
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-        *reinterpret_cast<bf16x8*>(&wsm[cs][(64 * kq + 16 * i + (lane >> 2)) * LDW + 8 * (lane & 3)]) = wr[i];
+        *reinterpret_cast<bf16x8*>(&wsm[cs][(64 * kq + 16 * i + (lane >> 2)) * LDWB + 8 * (lane & 3)]) = wr[i];
 
     float g[8], sv[8], da[8], db[8], tv[8];
     cvt8(rds, 0, g);                 // zeros without ds
@@ -433,16 +442,28 @@ __global__ void __launch_bounds__(NT) lngemm_bwd_kernel(LnBwdArgs a) {
     for (int j = 0; j < 8; ++j) da[j] = has_ap ? da[j] + tv[j] : da[j];
     cvt8(rdb, a.dxb_bf16, db);       // zeros without dxb
     float xh[8], dxh[8], s1 = 0.f, s2 = 0.f;
+    float t0[8], t1[8], t2[8], t3[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         xh[j] = (sv[j] - mu) * rs;
         dxh[j] = da[j] * ga[j] + db[j] * gb[j];
         s1 += dxh[j];
         s2 += dxh[j] * xh[j];
-        red[0][lr * C + c + j] = 0.f + da[j] * xh[j];
-        red[1][lr * C + c + j] = 0.f + da[j];
-        red[2][lr * C + c + j] = 0.f + db[j] * xh[j];
-        red[3][lr * C + c + j] = 0.f + db[j];
+        t0[j] = 0.f + da[j] * xh[j];
+        t1[j] = 0.f + da[j];
+        t2[j] = 0.f + db[j] * xh[j];
+        t3[j] = 0.f + db[j];
+    }
+    {   // 16-byte stores (the padded offset is a multiple of 4 floats)
+        const int ro = redix(lr, c);
+        float4* const r0 = reinterpret_cast<float4*>(&red[0][ro]);
+        float4* const r1 = reinterpret_cast<float4*>(&red[1][ro]);
+        float4* const r2 = reinterpret_cast<float4*>(&red[2][ro]);
+        float4* const r3 = reinterpret_cast<float4*>(&red[3][ro]);
+        r0[0] = make_float4(t0[0], t0[1], t0[2], t0[3]); r0[1] = make_float4(t0[4], t0[5], t0[6], t0[7]);
+        r1[0] = make_float4(t1[0], t1[1], t1[2], t1[3]); r1[1] = make_float4(t1[4], t1[5], t1[6], t1[7]);
+        r2[0] = make_float4(t2[0], t2[1], t2[2], t2[3]); r2[1] = make_float4(t2[4], t2[5], t2[6], t2[7]);
+        r3[0] = make_float4(t3[0], t3[1], t3[2], t3[3]); r3[1] = make_float4(t3[4], t3[5], t3[6], t3[7]);
     }
     s1 = row_sum32(s1) / (float)C;
     s2 = row_sum32(s2) / (float)C;
@@ -454,7 +475,8 @@ __global__ void __launch_bounds__(NT) lngemm_bwd_kernel(LnBwdArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) d[j] = keep[j] ? g[j] * a.keep_scale : 0.f;   // g * 1 at p = 0
     const bf16x8 dv = pack8(d);
-    *reinterpret_cast<bf16x8*>(&img[lr * LDX + c]) = dv;
+    *reinterpret_cast<bf16x4*>(&img[lr * LDXB + c]) = bf16x4{dv[0], dv[1], dv[2], dv[3]};
+    *reinterpret_cast<bf16x4*>(&img[lr * LDXB + c + 4]) = bf16x4{dv[4], dv[5], dv[6], dv[7]};
     if (writer) {
         if (a.dsrc) st8f(a.dsrc, off, g);
         *reinterpret_cast<bf16x8*>(a.dy + off) = dv;
@@ -477,14 +499,14 @@ __global__ void __launch_bounds__(NT) lngemm_bwd_kernel(LnBwdArgs a) {
             const int k = rem / C, col = rem - k * C;
             float tt = 0.f;
 #pragma unroll
-            for (int p = 0; p < 8; ++p) tt += red[k][(8 * blk + p) * C + col];
+            for (int p = 0; p < 8; ++p) tt += red[k][redix(8 * blk + p, col)];
             a.partials[(long long)(m0 / 8 + blk) * 4 * C + rem] = tt;
         }
     }
 
     // ---- dx = dy W: A = the dy image (rowsgemm's trans_b = 0 k order), W read transposed
     {
-        const bf16* ar = &img[(r & 15) * LDX];
+        const bf16* ar = &img[(r & 15) * LDXB];
         const bf16* ws = wsm[cs];
         const int gq = lane >> 4, i16 = lane & 15;
         const int d0 = 16 * (gq & 1) + 4 * (i16 & 3);
@@ -498,15 +520,15 @@ __global__ void __launch_bounds__(NT) lngemm_bwd_kernel(LnBwdArgs a) {
             const bf16x4 hi = *reinterpret_cast<const bf16x4*>(ar + 16 * ks + 8 + 4 * h);
             const bf16x8 av = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
             const int k0 = 16 * ks + 4 * (gq >> 1) + (i16 >> 2);
-            const bf16x4 wl = tr16(ws + k0 * LDW + d0);
-            const bf16x4 wh = tr16(ws + (k0 + 8) * LDW + d0);
+            const bf16x4 wl = tr16(ws + k0 * LDWB + d0);
+            const bf16x4 wh = tr16(ws + (k0 + 8) * LDWB + d0);
             const bf16x8 bv = bf16x8{wl[0], wl[1], wl[2], wl[3], wh[0], wh[1], wh[2], wh[3]};
             acc = mfma(bv, av, acc);
         }
         if (r < RB) {
 #pragma unroll
             for (int v = 0; v < 16; ++v)
-                pr[kq][(32 * cs + 8 * (v >> 2) + 4 * h + (v & 3)) * LDR + r] = acc[v];
+                pr[kq][(32 * cs + 8 * (v >> 2) + 4 * h + (v & 3)) * LDRB + r] = acc[v];
         }
     }
     __syncthreads();
@@ -517,8 +539,8 @@ __global__ void __launch_bounds__(NT) lngemm_bwd_kernel(LnBwdArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int n = 4 * cg + e;
-            const float tt = (pr[0][n * LDR + em] + pr[1][n * LDR + em]) +
-                             (pr[2][n * LDR + em] + pr[3][n * LDR + em]);
+            const float tt = (pr[0][n * LDRB + em] + pr[1][n * LDRB + em]) +
+                             (pr[2][n * LDRB + em] + pr[3][n * LDRB + em]);
             const bf16 yv = (bf16)tt;
             if (EPI == EPI_MASK)
                 o[e] = (float)hv[e] > 0.f ? (bf16)((float)yv * a.keep_scale2) : (bf16)0.f;

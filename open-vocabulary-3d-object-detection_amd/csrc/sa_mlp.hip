@@ -36,6 +36,18 @@ namespace {
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+// two fp32 -> two bf16 in one dword (one v_cvt_pk_bf16_f32), the first in the low half
+__device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
+}
+// the two bf16 halves of a dword as fp32 (exact)
+__device__ __forceinline__ f32x2 unpack_bf16(uint32_t u) {
+    return f32x2{__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xffff0000u)};
+}
 
 #ifdef OV3D_SA_PROBE
 // diagnostic build only (tools/sa_probe.py fwd): per-wave s_memtime totals of the layer
@@ -123,6 +135,11 @@ __global__ __launch_bounds__(kThreads, 2) void sa_layer_kernel(LayerArgs p) {
     float ssum[NB], ssq[NB];
 #pragma unroll
     for (int cb = 0; cb < NB; ++cb) ssum[cb] = ssq[cb] = 0.f;
+    // the pool modes sum a column's values in two interleaved fp32 chains (even / odd rows of
+    // a lane: packed v_pk_add / v_pk_fma over the bf16 pairs), joined at the end
+    f32x2 ssum2[NB], ssq2[NB];
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb) ssum2[cb] = ssq2[cb] = f32x2{0.f, 0.f};
     uint32_t fm[NB];   // MODE_POOL1: sign mask of this lane's columns (gamma < 0: negated)
 #pragma unroll
     for (int cb = 0; cb < NB; ++cb)
@@ -249,13 +266,17 @@ __global__ __launch_bounds__(kThreads, 2) void sa_layer_kernel(LayerArgs p) {
                     mn[rb] = __builtin_huge_valf();
                     imx[rb] = imn[rb] = 0;
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) {       // rows increase with i (fixed h)
-                        const int row = rb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                        const float f = (float)(bf16)acc[rb][cb][i];
-                        ssum[cb] += f;
-                        ssq[cb] = fmaf(f, f, ssq[cb]);
-                        if (f > mx[rb]) { mx[rb] = f; imx[rb] = row; }
-                        if (f < mn[rb]) { mn[rb] = f; imn[rb] = row; }
+                    for (int i = 0; i < 16; i += 2) {    // rows increase with i (fixed h)
+                        const f32x2 f2 = unpack_bf16(pack_bf16(acc[rb][cb][i], acc[rb][cb][i + 1]));
+                        ssum2[cb] += f2;
+                        ssq2[cb] = __builtin_elementwise_fma(f2, f2, ssq2[cb]);
+#pragma unroll
+                        for (int e = 0; e < 2; ++e) {
+                            const int row = rb * 32 + ((i + e) & 3) + 8 * ((i + e) >> 2) + 4 * h;
+                            const float f = f2[e];
+                            if (f > mx[rb]) { mx[rb] = f; imx[rb] = row; }
+                            if (f < mn[rb]) { mn[rb] = f; imn[rb] = row; }
+                        }
                     }
                     // combine the two lane halves (rows 4h..): value, then lower row (the
                     // partner lane's values by v_permlane32_swap, not a ds_bpermute round trip)
@@ -287,20 +308,31 @@ __global__ __launch_bounds__(kThreads, 2) void sa_layer_kernel(LayerArgs p) {
             } else if constexpr (MODE == MODE_POOL1) {
                 // one integer max per row block, no compare / select chain: the flipped value's
                 // bits made order-preserving as an int (t, low 16 bits zero: bf16 values), plus
-                // 63 - row in the low bits, so ties go to the first row
+                // 63 - row in the low bits, so ties go to the first row.  Two values per dword
+                // (round 6): one v_cvt_pk_bf16_f32, one sign flip, the order-preserving map on
+                // both 16-bit halves at once (v_pk_ashrrev_i16), the statistics as packed f32
+                // ops, the two keys into one v_max3_i32 (9.4 -> ~6 vector ops per value)
+                const uint32_t fm2 = fm[cb] | (fm[cb] >> 16);
                 int key[2];
 #pragma unroll
                 for (int rb = 0; rb < 2; ++rb) {
                     key[rb] = INT_MIN;
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) {       // row rb*32 + (i&3) + 8(i>>2) + 4h
-                        const uint32_t u = __builtin_bit_cast(uint32_t, (float)(bf16)acc[rb][cb][i]) ^ fm[cb];
-                        const float f = __builtin_bit_cast(float, u);
-                        ssum[cb] += f;
-                        ssq[cb] = fmaf(f, f, ssq[cb]);
-                        const int t = (int)(u ^ ((uint32_t)((int)u >> 31) & 0x7fff0000u));
-                        key[rb] = max(key[rb], t + (63 - rb * 32 - (i & 3) - 8 * (i >> 2)) - 4 * h);
+                    for (int i = 0; i < 16; i += 2) {    // rows rb*32 + (i&3) + 8(i>>2) + 4h (+1)
+                        const uint32_t u2 = pack_bf16(acc[rb][cb][i], acc[rb][cb][i + 1]) ^ fm2;
+                        const f32x2 f2 = unpack_bf16(u2);
+                        ssum2[cb] += f2;
+                        ssq2[cb] = __builtin_elementwise_fma(f2, f2, ssq2[cb]);
+                        const s16x2 sg = __builtin_bit_cast(s16x2, u2) >> (s16x2){15, 15};
+                        const uint32_t t2 = u2 ^ (__builtin_bit_cast(uint32_t, sg) & 0x7fff7fffu);
+                        // low bits 63 - row without the lane half's 4h: compile-time constants;
+                        // all of a lane's rows share h, so it is subtracted after the max
+                        const uint32_t c0 = 63 - rb * 32 - (i & 3) - 8 * (i >> 2);
+                        const int k0 = (int)((t2 << 16) | c0);
+                        const int k1 = (int)((t2 & 0xffff0000u) | (c0 - 1u));
+                        key[rb] = max(key[rb], max(k0, k1));
                     }
+                    key[rb] -= 4 * h;   // low bits >= 63 - 59 - 4 = 0: no borrow into the value
                     key[rb] = max(key[rb], (int)xor32((uint32_t)key[rb], h));
                 }
                 float mx[2];
@@ -353,6 +385,10 @@ __global__ __launch_bounds__(kThreads, 2) void sa_layer_kernel(LayerArgs p) {
         // per-column totals of this workgroup: both lane halves hold the same column
 #pragma unroll
         for (int cb = 0; cb < NB; ++cb) {
+            if constexpr (MODE == MODE_POOL || MODE == MODE_POOL1) {
+                ssum[cb] = ssum2[cb][0] + ssum2[cb][1];
+                ssq[cb] = ssq2[cb][0] + ssq2[cb][1];
+            }
             ssum[cb] = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, ssum[cb]) ^ fm[cb]);
             const double s = (double)ssum[cb] + (double)__shfl_xor(ssum[cb], 32);
             const double q = (double)ssq[cb] + (double)__shfl_xor(ssq[cb], 32);
