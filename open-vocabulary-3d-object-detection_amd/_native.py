@@ -124,6 +124,7 @@ _SIGS = {
     "ov3d_gemm256_pair": "pplpplppippliiip",
     "ov3d_gemm256_batched": "pllpllpliplliiiiip",
     "ov3d_lngemm_fwd": "ipipfpipppippfppppppilllipifpip",
+    "ov3d_rows256": "plplpllpp",
     "ov3d_lngemm_bwd": "ipppppppilllppfpipppipipliifplplp",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",
@@ -138,7 +139,7 @@ EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_
                           "ov3d_stamps_get", "ov3d_wall_clock_khz",
                           "ov3d_attnpool_fused_supported", "ov3d_lngemm_supported",
                           "ov3d_lngemm_bwd_parts", "ov3d_lngemm_stamps_arm", "ov3d_stream_create",
-                          "ov3d_ball_query_ws_bytes")
+                          "ov3d_ball_query_ws_bytes", "ov3d_rows256_supported")
 
 _CT = {"p": ctypes.c_void_p, "i": ctypes.c_int, "l": ctypes.c_longlong, "f": ctypes.c_float,
        "d": ctypes.c_double}
@@ -202,6 +203,8 @@ def load():
         lib.ov3d_sa_dy_fused_supported.argtypes = [ctypes.c_int] * 2
         lib.ov3d_sa_dy_fused_supported.restype = ctypes.c_int
         lib.ov3d_rows_gemm_supported.argtypes = [ctypes.c_int] * 3
+        lib.ov3d_rows256_supported.argtypes = [ctypes.c_longlong, ctypes.c_int, ctypes.c_int]
+        lib.ov3d_rows256_supported.restype = ctypes.c_int
         lib.ov3d_rows_gemm_supported.restype = ctypes.c_int
         lib.ov3d_tile_gemm_supported.argtypes = [ctypes.c_int] * 3
         lib.ov3d_tile_gemm_supported.restype = ctypes.c_int

@@ -46,8 +46,6 @@ constexpr int C = 256;            // model width: the LayerNorm rows and the GEM
 constexpr int RB = 16;            // rows per workgroup
 constexpr int NT = 512;           // threads (8 waves)
 constexpr int LDX = C + 8;        // LDS row of the row / W images (bf16): 528 bytes
-constexpr int LDW = 40;           // LDS row of a transposed-read W tile slice (bf16)
-constexpr int LDR = RB + 1;       // fp32 partial-product rows [column][row]
 constexpr int MAXP = 2;
 constexpr int BNB = 64;           // backward: output columns per workgroup
 // backward LDS strides (round 6; every read conflict-free under the MI355X lane groups, the

@@ -334,11 +334,46 @@ def conv3x3_gemm256(x, w, bias=None, residual=None, relu=False):
 GEMM256_MIN_M = int(os.environ.get("OV3D_GEMM256_MIN_M", str(1 << 17)))
 
 
+# (M, 256) x (256, 256)^T products over this many rows and more, without bias (the masked
+# encoder's interim SA layers and their input gradients), on the streaming kernel
+# (csrc/rows256.hip: W resident per CU, equal to gemm256's outputs bit for bit); "0": gemm256
+ROWS256 = os.environ.get("OV3D_ROWS256", "1") != "0"
+
+
+def rows256_ok(a, w, bias=None):
+    from . import _native
+    return (ROWS256 and bias is None and a.shape[0] >= GEMM256_MIN_M and _rows_ok(a) and _rows_ok(w)
+            and tuple(a.shape[1:]) == (256,) and tuple(w.shape) == (256, 256)
+            and bool(_native.load().ov3d_rows256_supported(a.shape[0], 256, 256)))
+
+
+def rows256(a, w):
+    """a (M, 256) w (256, 256)^T -> (M, 256) bf16 (check rows256_ok first)"""
+    from . import _native
+    out = torch.empty((a.shape[0], 256), dtype=torch.bfloat16, device=a.device)
+    _native.call("ov3d_rows256", a, a.stride(0), w, w.stride(0), out, out.stride(0), a.shape[0],
+                 _rows256_counters(a.device), like=a)
+    return out
+
+
+_R256_COUNTERS = {}
+
+
+def _rows256_counters(device):
+    c = _R256_COUNTERS.get(device)
+    if c is None:   # tile claims of csrc/rows256.hip: zero, and left zero by every launch
+        c = torch.zeros(2, dtype=torch.int32, device=device)
+        _R256_COUNTERS[device] = c
+    return c
+
+
 def _linear(x, w, b):
     """F.linear on bf16 rows (bias in the epilogue): short row blocks on rowsgemm, long ones
-    on tilegemm, the longest on gemm256"""
+    on tilegemm, the longest on rows256 (256 x 256 weights) or gemm256"""
     if _rows_gemm_ok(x, w, True):
         return rows_gemm(x, w, b, trans_b=True)
+    if x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and rows256_ok(x, w, b):
+        return rows256(x, w)
     if x.shape[0] >= GEMM256_MIN_M and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 \
             and gemm256_ok(x, w):
         return gemm256(x, w, bias=b)
@@ -371,6 +406,8 @@ def _dgrad(dy, w):
         return rows_gemm(dy, w, trans_b=False)
     if dy.shape[0] >= GEMM256_MIN_M and dy.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
         wt = w.t().contiguous()   # (K, N) rows: dx = dy wt^T on the 256 x 256 tile kernel
+        if rows256_ok(dy, wt):
+            return rows256(dy, wt)
         if gemm256_ok(dy, wt):
             return gemm256(dy, wt)
     if _tile_gemm_ok(dy, w, False):

@@ -171,3 +171,48 @@ def test_gemm256_batched_attnpool_products(cuda, R, C, H, d):
     gemm.gemm256_batched(y, C, R * C, wv, C, d * C, o, H * d, d, R, d, C, H, bias=bv, sbias=d)
     ref = torch.bmm(y.float(), wv.float().view(H, d, C).transpose(1, 2)) + bv.view(H, 1, d)
     _check(o.view(R, H, d).transpose(0, 1), ref)
+
+
+@pytest.mark.parametrize("M,ldx", [(262144, 256), (131072 + 37, 264), (200, 256), (5, 320)])
+def test_rows256_equals_gemm256_bitwise(M, ldx):
+    """csrc/rows256.hip (the masked encoder's interim SA products: W resident per CU, X streamed
+    through LDS) against gemm256 on the same bf16 operands, no bias: every output bit, with a
+    ragged last tile and strided rows; and the fp32 product within one bf16 rounding"""
+    from ov3d_amd import _native, gemm
+    torch.manual_seed(3)
+    dev = torch.device("cuda", 0)
+    xb = torch.randn(M, ldx, device=dev).to(torch.bfloat16)
+    x = xb[:, :256]
+    w = (0.06 * torch.randn(256, 256, device=dev)).to(torch.bfloat16)
+    y = torch.full((M, 256), float("nan"), device=dev, dtype=torch.bfloat16)
+    _native.call("ov3d_rows256", x, x.stride(0), w, w.stride(0), y, y.stride(0), M,
+                 gemm._rows256_counters(dev), like=x)
+    ref = gemm.gemm256(x, w)
+    assert torch.equal(y, ref)
+    _check(y[:4096], x[:4096].float() @ w.float().t())
+
+
+def test_rows256_routes_interim_sa_products():
+    """_linear / _dgrad send the 2^18-row 256 x 256 products to rows256 (and equal gemm256's)"""
+    from ov3d_amd import _native, gemm
+    torch.manual_seed(4)
+    dev = torch.device("cuda", 0)
+    x = torch.randn(1 << 17, 256, device=dev).to(torch.bfloat16)
+    w = (0.06 * torch.randn(256, 256, device=dev)).to(torch.bfloat16)
+    assert gemm.rows256_ok(x, w) and not gemm.rows256_ok(x[:1000], w)
+    seen = []
+    orig = _native.call
+
+    def spy(name, *a, **k):
+        seen.append(name)
+        return orig(name, *a, **k)
+
+    _native.call = spy
+    try:
+        y = gemm._linear(x, w, None)
+        dx = gemm._dgrad(x, w)
+    finally:
+        _native.call = orig
+    assert seen.count("ov3d_rows256") == 2, seen
+    assert torch.equal(y, gemm.gemm256(x, w))
+    assert torch.equal(dx, gemm.gemm256(x, w.t().contiguous()))

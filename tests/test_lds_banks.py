@@ -49,3 +49,11 @@ def test_attention_tile_images_conflict_free():
     assert all(v == 0 for v in t.attn_census(True).values())
     assert t.attn_census(False)["transposed reads"] > 0
     assert [t.isw(r) for r in range(8)] == [0, 0, 4, 4, 1, 1, 5, 5]
+
+
+def test_rows256_tile_image_conflict_free():
+    """csrc/rows256.hip: the row & 15 chunk swizzle serves every 16-lane group of the fragment
+    reads from distinct banks (plain 512-byte rows would put all 16 rows on the same banks)"""
+    t = _tool()
+    assert t.rows256_census(True) == 0
+    assert t.rows256_census(False) > 0

@@ -233,11 +233,31 @@ def attn_census(swizzled=True):
     return res
 
 
+def rows256_census(swizzled=True):
+    """csrc/rows256.hip X tile image (128 rows x 256 bf16, 512-byte rows, 16-byte chunk c of row r
+    at c ^ (r & 15)): extra LDS cycles per tile and wave of the fragment reads (ds_read_b128:
+    lane l reads row 16 rb + (l & 15), logical chunk 4 ks + (l >> 4)); the image is written by
+    LDS-DMA (lane-linear 1 KB pieces, no bank rule).  swizzled=False: plain rows."""
+    def f(r, c):   # byte address of logical 16-byte chunk c of row r
+        return r * 512 + 16 * ((c ^ (r & 15)) if swizzled else c)
+    cyc = 0
+    for rb in range(8):
+        for ks in range(8):
+            a = {l: f(16 * rb + (l & 15), 4 * ks + (l >> 4)) for l in range(64)}
+            cyc += extra(B128, a, 4, 64)
+    if swizzled:
+        assert sorted(f(r, c) // 16 for r in range(128) for c in range(32)) == list(range(128 * 32))
+    return cyc
+
+
 if __name__ == "__main__":
     main()
     for sw in (False, True):
         for k, v in attn_census(sw).items():
             print(f"attn {'swizzled' if sw else 'padded  '} {k:18s} extra cycles per tile and wave: {v}")
+    for sw in (False, True):
+        print(f"rows256 {'swizzled' if sw else 'plain   '} fragment reads extra cycles per tile and wave: "
+              f"{rows256_census(sw)}")
     for sw in (False, True):
         for k, v in dy2_census(sw).items():
             print(f"sa_dy2 {'swizzled' if sw else 'padded  '} {k:28s} extra cycles per tile: {v}")
