@@ -59,6 +59,10 @@ int ov3d_nbr_max_fwd(const void* y, long long P, int S, int C, void* out, uint8_
                      void* stream);
 int ov3d_nbr_max_bwd(const void* g, const uint8_t* arg, long long P, int S, int C, void* dy,
                      void* stream);
+/* ov3d_nbr_max_fwd of z = bf16(relu(y * scale + shift)) (the ov3d_rows_bn_apply arithmetic, no
+ * dropout) without storing z: y (P*S, C) bf16 rows of the last SA layer before its BatchNorm */
+int ov3d_nbr_max_bnrelu_fwd(const void* y, long long P, int S, int C, const float* scale,
+                            const float* shift, void* out, uint8_t* arg, void* stream);
 
 /* Ball query: first S point indices (ascending) with |p - c|^2 < radius^2,
  * padded with the first hit, zeros if none.
@@ -672,6 +676,14 @@ int ov3d_rows_bn_bwd(int pass, const void* dz, long long ldz, long long bstride_
                      const float* invstd, const float* cA, const float* cB, const float* cC,
                      float dropout_p, const int64_t* seed, int site, double* partials, int nparts,
                      void* dx, long long ldd, long long bstride_d, int cbd, void* stream);
+/* ov3d_rows_bn_bwd (row-major bf16 x, no dropout) with dz the dense gradient of the neighbour
+ * max-pool rebuilt from its pooled gradient g (P, C) bf16 and arg rows (P, C) uint8 (row
+ * p * S + s takes g[p] where arg == s): the backward of ov3d_nbr_max_bnrelu_fwd */
+int ov3d_rows_bn_bwd_pooled(int pass, const void* g, const uint8_t* arg, int S, const void* x,
+                            long long R, int C, const float* scale, const float* shift,
+                            const float* mean, const float* invstd, const float* cA,
+                            const float* cB, const float* cC, double* partials, int nparts,
+                            void* dx, void* stream);
 
 
 /* ---- Set-criterion losses (criterion.py SetCriterion.forward, all decoder layers) ----

@@ -74,6 +74,8 @@ _SIGS = {
     "ov3d_group_bwd_csr_bf16": "plppiiilllpp",
     "ov3d_group_rows_bf16": "ppplllpiiiiifiipp",
     "ov3d_nbr_max_bwd": "ppliipp",
+    "ov3d_nbr_max_bnrelu_fwd": "pliippppp",
+    "ov3d_rows_bn_bwd_pooled": "ippiplippppppppipp",
     "ov3d_wgrad": "plpliiiplpppip",
     "ov3d_wgrad_group": "pipp",
     "ov3d_rows_bn_stats": "pillilipip",

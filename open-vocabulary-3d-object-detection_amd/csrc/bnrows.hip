@@ -237,14 +237,34 @@ __global__ void __launch_bounds__(256) rows_bn_apply_kernel(
     }
 }
 
-template <int PASS, typename T>
+// the dz run (row r, channels c .. c+7): read, or (POOLED) rebuilt from the neighbour max-pool's
+// pooled gradient g (P, C) and arg rows (P, C) uint8 -- row r = p * S + s takes g[p] where
+// arg[p] == s, else 0 (exactly the dense gradient ov3d_nbr_max_bwd would have written)
+typedef uint8_t u8x8 __attribute__((ext_vector_type(8)));
+template <bool POOLED>
+__device__ __forceinline__ void load_dz(const bf16* dz, const RowsLayout& LZ, long long r, int c,
+                                        const uint8_t* parg, int pS, int C, float* v) {
+    if constexpr (!POOLED) {
+        load8<bf16>(dz, LZ, r, c, v);
+    } else {
+        const long long p = r / pS;
+        const int s = (int)(r - p * pS);
+        float g[8];
+        load8<bf16>(dz, LZ, p, c, g);
+        const u8x8 a = *reinterpret_cast<const u8x8*>(parg + p * C + c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = a[j] == s ? g[j] : 0.f;
+    }
+}
+
+template <int PASS, typename T, bool POOLED = false>
 __global__ void __launch_bounds__(256) rows_bn_bwd_kernel(
     const bf16* __restrict__ dz, RowsLayout LZ, const T* __restrict__ x, RowsLayout LX, long long R,
     int C, const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ cA,
     const float* __restrict__ cB, const float* __restrict__ cC, uint32_t thresh, float keep_scale,
     const int64_t* seed, uint32_t site, double* __restrict__ partials, bf16* __restrict__ dx,
-    RowsLayout LD) {
+    RowsLayout LD, const uint8_t* __restrict__ parg = nullptr, int pS = 1) {
     uint32_t sm = 0;
     if (thresh) {
         const uint64_t s = (uint64_t)*seed;
@@ -267,7 +287,8 @@ __global__ void __launch_bounds__(256) rows_bn_bwd_kernel(
             const long long r = q.r0 + k * q.rstep;
             if (r < R) {
                 load8o<T>(x, ox + r * LX.ld, xv[k]);
-                load8o<bf16>(dz, oz + r * LZ.ld, zv[k]);
+                if constexpr (POOLED) load_dz<true>(dz, LZ, r, c, parg, pS, C, zv[k]);
+                else load8o<bf16>(dz, oz + r * LZ.ld, zv[k]);
             }
         }
 #pragma unroll
@@ -319,7 +340,7 @@ __global__ void __launch_bounds__(256) rows_bn_bwd_kernel(
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     load8<T>(x, LX, r + u * step, c, xv[u]);
-                    load8<bf16>(dz, LZ, r + u * step, c, zv[u]);
+                    load_dz<POOLED>(dz, LZ, r + u * step, c, parg, pS, C, zv[u]);
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) row(r + u * step, xv[u], zv[u]);
@@ -327,7 +348,7 @@ __global__ void __launch_bounds__(256) rows_bn_bwd_kernel(
             for (; r < R; r += step) {
                 float xv[8], zv[8];
                 load8<T>(x, LX, r, c, xv);
-                load8<bf16>(dz, LZ, r, c, zv);
+                load_dz<POOLED>(dz, LZ, r, c, parg, pS, C, zv);
                 row(r, xv, zv);
             }
         }
@@ -418,6 +439,34 @@ extern "C" int ov3d_rows_bn_bwd(int pass, const void* dz, long long ldz, long lo
                 (const bf16*)dz, LZ, (const float*)x, LX, R, C, scale, shift, mean, invstd, cA, cB,
                 cC, th, ks, seed, (uint32_t)site, partials, (bf16*)dx, LD);
     }
+    OV3D_LAUNCH_CHECK();
+    return OV3D_OK;
+}
+
+extern "C" int ov3d_rows_bn_bwd_pooled(int pass, const void* g, const uint8_t* arg, int S,
+                                       const void* x, long long R, int C, const float* scale,
+                                       const float* shift, const float* mean, const float* invstd,
+                                       const float* cA, const float* cB, const float* cC,
+                                       double* partials, int nparts, void* dx, void* stream) {
+    // row-major bf16 (P * S, C) rows x, (P, C) pooled gradient g and arg; no dropout (the SA
+    // layers' BatchNorm + ReLU)
+    RowsLayout L{C, 0, C};
+    if (!g || !arg || !x || S <= 0 || S > 256 || R <= 0 || R % S || C <= 0 || C % 8 ||
+        ((uintptr_t)g | (uintptr_t)x) % 16 || (uintptr_t)arg % 8 || (pass != 0 && pass != 1))
+        return OV3D_EINVAL;
+    if (pass == 0 && (!partials || nparts <= 0 || !mean || !invstd || !scale || !shift))
+        return OV3D_EINVAL;
+    if (pass == 1 && (!dx || !cA || !cB || !cC || !scale || !shift || (uintptr_t)dx % 16))
+        return OV3D_EINVAL;
+    hipStream_t s = ov3d_stream(stream);
+    if (pass == 0)
+        rows_bn_bwd_kernel<0, bf16, true><<<nparts, 256, 0, s>>>(
+            (const bf16*)g, L, (const bf16*)x, L, R, C, scale, shift, mean, invstd, cA, cB, cC, 0u,
+            1.f, nullptr, 0u, partials, (bf16*)dx, L, arg, S);
+    else
+        rows_bn_bwd_kernel<1, bf16, true><<<(unsigned)slab_blocks(R, C), 256, 0, s>>>(
+            (const bf16*)g, L, (const bf16*)x, L, R, C, scale, shift, mean, invstd, cA, cB, cC, 0u,
+            1.f, nullptr, 0u, partials, (bf16*)dx, L, arg, S);
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

@@ -21,6 +21,7 @@ exist without a per-step concatenation.  Dropout masks come from a counter-based
 to bf16 rounding (tests/test_heads_gpu.py).
 """
 import ctypes
+import os
 
 import torch
 import torch.nn as nn
@@ -468,3 +469,65 @@ def bn_relu_rows(h, bn, drop=None):
         h = h.contiguous()
     with torch.autocast("cuda", enabled=False):
         return _BnReluRows.apply(h, bn.weight, bn.bias, bn, p, site)
+
+
+# ----------------------------------------------------------- BN + ReLU + neighbour max-pool
+# the last SharedMLP layer of an SA module on the rows path (the masked encoder's interim SA)
+# straight into the max over its nsample rows: the activated rows z are never stored (forward:
+# csrc/pool.hip ov3d_nbr_max_bnrelu_fwd; backward: ov3d_rows_bn_bwd_pooled rebuilds the dense
+# pooled gradient row by row); OV3D_BN_POOL=0: bn_relu_rows + the plain pool
+BN_POOL = os.environ.get("OV3D_BN_POOL", "1") != "0"
+
+
+class _BnReluPoolRows(torch.autograd.Function):
+    """max over S neighbour rows of relu(bn(h)) (training BN, batch statistics + running-stat
+    update, no dropout): the _BnReluRows arithmetic followed by pointnet2_modules._NbrMax's,
+    without the (R, C) activation in between; bit-equal to the two"""
+
+    @staticmethod
+    def forward(ctx, h, gamma, beta, bn, S):
+        R, C = h.shape
+        dev = h.device
+        nbt = bn.num_batches_tracked if (bn.track_running_stats and
+                                         bn.num_batches_tracked is not None) else None
+        rowmajor = (C, 0, C)
+        mean, invstd, scale, shift = _stats_finalize(h, rowmajor, R, C, gamma, beta, [bn],
+                                                     bn.running_mean, bn.running_var, nbt)
+        P = R // S
+        out = torch.empty((P, C), dtype=torch.bfloat16, device=dev)
+        arg = torch.empty((P, C), dtype=torch.uint8, device=dev)
+        nat.call("ov3d_nbr_max_bnrelu_fwd", h, P, S, C, scale, shift, out, arg, like=h)
+        ctx.save_for_backward(h, gamma, mean, invstd, scale, shift, arg)
+        ctx.S = S
+        ctx.bn = bn
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        h, gamma, mean, invstd, scale, shift, arg = ctx.saved_tensors
+        S = ctx.S
+        R, C = h.shape
+        dev = h.device
+        g = g.to(torch.bfloat16).contiguous()
+        parts = torch.empty((NPARTS, 2, C), dtype=torch.float64, device=dev)
+        nat.call("ov3d_rows_bn_bwd_pooled", 0, g, arg, S, h, R, C, scale, shift, mean, invstd, None,
+                 None, None, parts, NPARTS, None, like=h)
+        group, world = _group_world(ctx.bn)
+        cA, cB, cC, dg, db = bn_bwd_affine(parts, NPARTS, C, group, R * world, gamma, mean, invstd)
+        dh = torch.empty((R, C), dtype=torch.bfloat16, device=dev)
+        nat.call("ov3d_rows_bn_bwd_pooled", 1, g, arg, S, h, R, C, scale, shift, mean, invstd, cA, cB,
+                 cC, None, 0, dh, like=h)
+        return dh, dg, db, None, None
+
+
+def bn_relu_pool_ok(h, bn, relu, S):
+    """the fused BN + ReLU + max-pool rows path applies (bf16 contiguous rows, no dropout)"""
+    return (BN_POOL and bn_relu_rows_ok(h, bn, relu, None) and h.dtype == torch.bfloat16
+            and h.is_contiguous() and h.data_ptr() % 16 == 0 and 0 < S <= 256
+            and h.shape[0] % S == 0 and h.shape[1] % 8 == 0)
+
+
+def bn_relu_pool_rows(h, bn, S):
+    """(R, C) training rows h -> (R / S, C) bf16: max over each S rows of relu(bn(h))"""
+    with torch.autocast("cuda", enabled=False):
+        return _BnReluPoolRows.apply(h, bn.weight, bn.bias, bn, S)

@@ -68,15 +68,17 @@ class SharedMLP(nn.Sequential):
         for i in range(len(args) - 1):
             self.add_module(f"{name}layer{i}", _ConvBNReLU(args[i], args[i + 1], bn=bn))
 
-    def rows(self, x):
+    def rows(self, x, pool=None):
         """The 1x1-conv stack on channels-last rows (R, Cin) -> (R, Cout): each layer is one
-        GEMM (hipBLASLt) + BN over rows + ReLU; no NCHW<->NHWC transposes.  Training under
-        bf16 autocast: BN + ReLU as one HIP row pass each way (heads.bn_relu_rows; the
-        ScanNet SA with colour and the masked encoder's interim SA, which the fused
-        3-channel kernels of sa_fused.py do not take)."""
+        GEMM + BN over rows + ReLU; no NCHW<->NHWC transposes.  Training under bf16 autocast:
+        BN + ReLU as one HIP row pass each way (heads.bn_relu_rows; the ScanNet SA with colour
+        and the masked encoder's interim SA, which the fused 3-channel kernels of sa_fused.py
+        do not take).  pool=S: -> (y, pooled); pooled: the last layer's BN + ReLU went straight
+        into the max over each S rows (heads.bn_relu_pool_rows), y is (R / S, Cout)."""
         from . import heads
         from .gemm import rows_linear_padk
-        for layer in self:
+        last = len(self) - 1
+        for i, layer in enumerate(self):
             w = layer.conv.weight
             w2 = w.view(w.shape[0], w.shape[1])
             if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] > w2.shape[1]:
@@ -85,12 +87,15 @@ class SharedMLP(nn.Sequential):
                 x = rows_linear(x, w2, layer.conv.bias)
             if hasattr(layer, "bn"):
                 bn = layer.bn.bn
+                if pool is not None and i == last and heads.bn_relu_pool_ok(x, bn, layer.activation,
+                                                                              pool):
+                    return heads.bn_relu_pool_rows(x, bn, pool), True
                 if heads.bn_relu_rows_ok(x, bn, layer.activation, None):
                     x = heads.bn_relu_rows(x, bn)
                     continue
                 x = batch_norm_rows(bn, x)
             x = torch.relu(x)
-        return x
+        return (x, False) if pool is not None else x
 
 
 def _nbr_max_ok(y, S):
@@ -186,7 +191,9 @@ class PointnetSAModuleVotes(nn.Module):
                 return sa_fused.sa_mlp_pool(self.mlp_module, rows, S, seq_m=M).view(
                     M, B, -1).transpose(0, 1)
             return sa_fused.sa_mlp_pool(self.mlp_module, rows, S).view(B, M, -1)
-        y = self.mlp_module.rows(rows)
+        y, pooled = self.mlp_module.rows(rows, pool=S)
+        if pooled:   # the last BN + ReLU fused into the pool (heads.bn_relu_pool_rows)
+            return y.view(B, M, -1)
         # == F.max_pool2d(kernel [1, nsample]) of the reference
         if _nbr_max_ok(y, S):
             return _NbrMax.apply(y, S).view(B, M, -1)

@@ -103,10 +103,13 @@ def test_full_size_c4_train_step_properties(cuda):
         torch.cuda.synchronize()
     finally:
         called = _native.census_stop()
-    for k in ("ov3d_attn_mask_pack", "ov3d_attn_fwd_masked", "ov3d_attn_bwd_masked", "ov3d_nbr_max_fwd",
-              "ov3d_nbr_max_bwd", "ov3d_giou3d_bwd", "ov3d_sa_layer_pool_fwd", "ov3d_fps",
-              "ov3d_ball_query_cells"):
+    for k in ("ov3d_attn_mask_pack", "ov3d_attn_fwd_masked", "ov3d_attn_bwd_masked",
+              "ov3d_giou3d_bwd", "ov3d_sa_layer_pool_fwd", "ov3d_fps", "ov3d_ball_query_cells",
+              "ov3d_rows256"):
         assert called.get(k), (k, sorted(called))
+    # the interim SA's last BN + ReLU inside its neighbour max-pool (heads.bn_relu_pool_rows)
+    assert called.get("ov3d_nbr_max_bnrelu_fwd") and called.get("ov3d_rows_bn_bwd_pooled"), \
+        sorted(called)
     # the interim SA's grouped rows: bf16, zero-padded to 264 columns (aligned GEMM K)
     assert called.get("ov3d_group_rows_bf16"), sorted(called)
     assert called.get("ov3d_group_bwd_csr_bf16"), sorted(called)

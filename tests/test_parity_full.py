@@ -129,8 +129,9 @@ def test_bf16_step_matches_float64_reference(cuda, name, ds):
     finally:
         called = _native.census_stop()
     # ball query: the index-order scan below 8192 points, the cell index above (same results)
-    missing = [k for k in BF16_KERNELS[ds]
-               if not (called.get(k) or (k == "ov3d_ball_query" and called.get("ov3d_ball_query_cells")))]
+    alt = {"ov3d_ball_query": "ov3d_ball_query_cells",        # the cell-index form
+           "ov3d_nbr_max_fwd": "ov3d_nbr_max_bnrelu_fwd"}      # the pool with the BN + ReLU fused
+    missing = [k for k in BF16_KERNELS[ds] if not (called.get(k) or called.get(alt.get(k, k)))]
     assert not missing, (missing, sorted(called))
     with F.torch_bf16_path():
         base = F.run(name, ds, cuda, amp=torch.bfloat16, grad_floor=F.BF16_GRAD_FLOOR)
