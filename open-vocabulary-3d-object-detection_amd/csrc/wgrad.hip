@@ -38,7 +38,7 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int TN = 128, TK = 128;  // output tile (rows of dW = N, cols = K)
 constexpr int RS = 32;             // rows of dy / x per LDS stage
-constexpr int kGroupMax = 28;      // problems per grouped launch (kernel argument space)
+constexpr int kGroupMax = 28;      // problems per 128 x 128 grouped launch (kernel argument space)
 constexpr int LDT = TN + 32;       // padded LDS row (bf16): conflict-free tr16 reads
 
 struct WgradArgs {
@@ -119,7 +119,8 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // (n - n0, k - k0) when `local`) and the bias column sums (tiles with by == 0) to bdst.
 // Problems here have N, K % 8 == 0, 16-byte aligned rows and R % BK == 0 (sk_ok); the rest
 // take the 128 x 128 register-staged group kernel.
-__device__ __forceinline__ void wgrad_seg256(const WgradArgs& a, int bx, int by, int rbeg, int rend,
+template <typename A>   // WgradArgs or the stream-K launch's WgradSK
+__device__ __forceinline__ void wgrad_seg256(const A& a, int bx, int by, int rbeg, int rend,
                                              float* dst, size_t ld, bool local, float* bdst,
                                              bf16* L) {
     // the wave index in a scalar register: every per-wave LDS / row base below stays scalar
@@ -522,19 +523,36 @@ __global__ void __launch_bounds__(256) wgrad_group128_reduce_kernel(WgradGroup12
 // Several independent weight gradients in one launch (the deferred dW / db of a whole
 // backward pass, gemm.py), stream-K over the units (problem, 256 x 256 tile, 64-row stage).
 constexpr int kSlot = TB * TB + TB;   // floats of one partial slot: tile + bias columns
+// a stream-K launch's problem: WgradArgs without the split fields, 32-bit strides (64 bytes),
+// so 48 problems fit the argument space (28 with WgradArgs: the step's ~100 deferred weight
+// gradients took 4 launches + 4 reductions)
+struct WgradSK {
+    const bf16* dy;
+    const bf16* x;
+    float* dW;
+    float* db;
+    int ldy, ldx, ldw;
+    int R, N, K;
+    int vec_dy, vec_x;
+};
+static_assert(sizeof(WgradSK) == 64, "compact stream-K problem");
+constexpr int kSKMax = 48;   // problems per stream-K launch
 struct WgradGroup {
-    WgradArgs p[kGroupMax];
-    long long ubeg[kGroupMax + 1];   // first unit of problem i
-    int sbeg[kGroupMax + 1];         // first partial slot of problem i
-    int tbeg[kGroupMax + 1];         // first tile of problem i (reduction grid)
+    WgradSK p[kSKMax];
+    long long ubeg[kSKMax + 1];   // first unit of problem i
+    int sbeg[kSKMax + 1];         // first partial slot of problem i
+    int tbeg[kSKMax + 1];         // first tile of problem i (reduction grid)
     int n, G;
-    float* part;                     // partial slots, kSlot floats each
+    float* part;                  // partial slots, kSlot floats each
 };
 static_assert(sizeof(WgradGroup) <= 4000, "kernel argument space");
 
-__host__ __device__ inline int sk_tiles_n(const WgradArgs& a) { return (a.N + TB - 1) / TB; }
-__host__ __device__ inline int sk_tiles(const WgradArgs& a) { return sk_tiles_n(a) * ((a.K + TB - 1) / TB); }
-__host__ __device__ inline int sk_stages(const WgradArgs& a) { return (a.R + BK - 1) / BK; }
+template <typename A>
+__host__ __device__ inline int sk_tiles_n(const A& a) { return (a.N + TB - 1) / TB; }
+template <typename A>
+__host__ __device__ inline int sk_tiles(const A& a) { return sk_tiles_n(a) * ((a.K + TB - 1) / TB); }
+template <typename A>
+__host__ __device__ inline int sk_stages(const A& a) { return (a.R + BK - 1) / BK; }
 // first unit of workgroup w / the workgroup owning unit u (ranges floor(U w / G))
 __host__ __device__ inline long long sk_start(long long U, int G, int w) { return U * w / G; }
 __host__ __device__ inline int sk_owner(long long U, int G, long long u) {
@@ -558,7 +576,7 @@ __global__ void __launch_bounds__(512, 1) wgrad_group_kernel(WgradGroup g) {
     int i = 0;
     while (u < u1) {
         while (u >= g.ubeg[i + 1]) ++i;
-        const WgradArgs& a = g.p[i];
+        const WgradSK& a = g.p[i];
         const int st = sk_stages(a), tn = sk_tiles_n(a);
         const long long local = u - g.ubeg[i];
         const int t = (int)(local / st), s0 = (int)(local - (long long)t * st);
@@ -585,7 +603,7 @@ __global__ void __launch_bounds__(256) wgrad_group_reduce_kernel(WgradGroup g) {
     const int gt = blockIdx.x / 65, sub = blockIdx.x - gt * 65;
     int i = 0;
     while (i + 1 < g.n && gt >= g.tbeg[i + 1]) ++i;
-    const WgradArgs& a = g.p[i];
+    const WgradSK& a = g.p[i];
     const int t = gt - g.tbeg[i];
     const int nsl = sk_tile_slots(g, i, t, U);
     if (nsl == 0) return;
@@ -714,6 +732,20 @@ static int cu_count() {
     return cus;
 }
 
+// problems per stream-K launch: kSKMax; OV3D_WGRAD_SK_MAX (1 .. kSKMax) for A/B runs (28: the
+// round-5 split)
+static int sk_max() {
+    static int m = 0;
+    if (!m) {
+        m = kSKMax;
+        if (const char* e = getenv("OV3D_WGRAD_SK_MAX")) {
+            const int v = atoi(e);
+            if (v >= 1 && v <= kSKMax) m = v;
+        }
+    }
+    return m;
+}
+
 static bool sk_ok(const ov3d_wgrad_problem& q) {
     (void)q;   // every problem: the stream-K kernel loads unaligned / narrow rows per element
     return true;
@@ -722,14 +754,18 @@ static bool sk_ok(const ov3d_wgrad_problem& q) {
 // stream-K plan of the problems idx[first .. first + g.n): units, slot and tile prefixes, grid
 static int plan_group(WgradGroup& g, const ov3d_wgrad_problem* probs, const int* idx, int first,
                       int n, long long& slots) {
-    g.n = n - first < kGroupMax ? n - first : kGroupMax;
+    g.n = n - first < sk_max() ? n - first : sk_max();
     long long U = 0;
     int tiles = 0;
     for (int j = 0; j < g.n; ++j) {
         const ov3d_wgrad_problem& q = probs[idx[first + j]];
-        const int rc = make_args(g.p[j], q.dy, q.ldy, q.x, q.ldx, q.R, q.N, q.K, q.dW, q.ldw, q.db,
+        WgradArgs f;
+        const int rc = make_args(f, q.dy, q.ldy, q.x, q.ldx, q.R, q.N, q.K, q.dW, q.ldw, q.db,
                                  nullptr, 1);
         if (rc != OV3D_OK) return rc;
+        if (f.ldy >= (1LL << 31) || f.ldx >= (1LL << 31) || f.ldw >= (1LL << 31)) return OV3D_EINVAL;
+        g.p[j] = WgradSK{f.dy, f.x, f.dW, f.db, (int)f.ldy, (int)f.ldx, (int)f.ldw, f.R, f.N, f.K,
+                         f.vec_dy, f.vec_x};
         g.ubeg[j] = U;
         g.tbeg[j] = tiles;
         U += (long long)sk_tiles(g.p[j]) * sk_stages(g.p[j]);
@@ -757,7 +793,7 @@ static long long group_space(const ov3d_wgrad_problem* probs, int n, long long* 
         else fb += ov3d_wgrad_workspace(probs[i].R, probs[i].N, probs[i].K, probs[i].nsplit);
     }
     long long most = 0;
-    for (int first = 0; first < (int)sk.size(); first += kGroupMax) {
+    for (int first = 0; first < (int)sk.size(); first += sk_max()) {
         WgradGroup g;
         long long slots = 0;
         if (plan_group(g, probs, sk.data(), first, (int)sk.size(), slots) != OV3D_OK) return -1;
@@ -785,7 +821,7 @@ extern "C" int ov3d_wgrad_group(const ov3d_wgrad_problem* probs, int n, float* w
     if (need > 0 && !workspace) return OV3D_EINVAL;
     std::vector<int> sk, fb;
     for (int i = 0; i < n; ++i) (sk_ok(probs[i]) ? sk : fb).push_back(i);
-    for (int first = 0; first < (int)sk.size(); first += kGroupMax) {
+    for (int first = 0; first < (int)sk.size(); first += sk_max()) {
         WgradGroup g;
         long long slots = 0;
         const int rc = plan_group(g, probs, sk.data(), first, (int)sk.size(), slots);
