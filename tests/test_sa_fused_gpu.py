@@ -249,9 +249,11 @@ def test_sa_rows_bn_relu_path_vs_fp32(cuda, monkeypatch, kind):
             monkeypatch.setattr(heads, "bn_relu_rows_ok", lambda *a: False)
         if not rows or kind != "scannet_colour":
             monkeypatch.setattr(sa_fused, "supported", lambda *a: False)
-        calls, fcalls = [], []
-        real, freal = heads.bn_relu_rows, sa_fused.sa_mlp_pool
+        calls, fcalls, pcalls = [], [], []
+        real, freal, preal = heads.bn_relu_rows, sa_fused.sa_mlp_pool, heads.bn_relu_pool_rows
         monkeypatch.setattr(heads, "bn_relu_rows", lambda *a, **k: calls.append(1) or real(*a, **k))
+        monkeypatch.setattr(heads, "bn_relu_pool_rows",
+                            lambda *a, **k: pcalls.append(1) or preal(*a, **k))
         monkeypatch.setattr(sa_fused, "sa_mlp_pool", lambda *a, **k: fcalls.append(1) or freal(*a, **k))
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
             _, f, _ = twin(xyz, feats)
@@ -261,7 +263,11 @@ def test_sa_rows_bn_relu_path_vs_fp32(cuda, monkeypatch, kind):
         (f.float() * gw).sum().backward()
         fused = name == "hip" and kind == "scannet_colour"
         assert len(fcalls) == (1 if fused else 0), (name, len(fcalls))
-        assert len(calls) == (3 if name == "hip" and not fused else 0), (name, len(calls))
+        # the rows path: layers 1-2 on bn_relu_rows, the last BN + ReLU inside the pool
+        # (heads.bn_relu_pool_rows) unless OV3D_BN_POOL=0
+        rows_hip = name == "hip" and not fused
+        assert len(pcalls) == (1 if rows_hip and heads.BN_POOL else 0), (name, len(pcalls))
+        assert len(calls) + len(pcalls) == (3 if rows_hip else 0), (name, len(calls))
         g = {n: p.grad.clone() for n, p in twin.named_parameters()}
         if feats.requires_grad:
             g["features"] = feats.grad.clone()
