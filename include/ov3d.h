@@ -492,6 +492,12 @@ int ov3d_conv3x3_gemm256(const void* X, int nimg, int H, int W, int Cin, const v
 int ov3d_rows256_supported(long long M, int N, int K);
 int ov3d_rows256(const void* X, long long ldx, const void* W, long long ldw, void* Y, long long ldy,
                  long long M, unsigned int* counters, void* stream);
+/* ov3d_rows256 of Z = bf16(relu(X * scale + shift)) (the previous layer's BatchNorm + ReLU, the
+ * ov3d_rows_bn_apply arithmetic without dropout; scale / shift (256) fp32) with Z also written
+ * (ldz % 8; the weight gradient's input): Y equals ov3d_rows_bn_apply followed by ov3d_rows256 */
+int ov3d_rows256_bn(const void* X, long long ldx, const float* scale, const float* shift,
+                    const void* W, long long ldw, void* Y, long long ldy, void* Z, long long ldz,
+                    long long M, unsigned int* counters, void* stream);
 
 /* LayerNorm boundary + the adjacent row GEMM in one launch (csrc/lngemm.hip), the decoder's
  * short row blocks [models/transformer.py TransformerDecoderLayer.forward_pre 355-379].

@@ -127,6 +127,7 @@ _SIGS = {
     "ov3d_gemm256_batched": "pllpllpliplliiiiip",
     "ov3d_lngemm_fwd": "ipipfpipppippfppppppilllipifpip",
     "ov3d_rows256": "plplpllpp",
+    "ov3d_rows256_bn": "plppplplpllpp",
     "ov3d_lngemm_bwd": "ipppppppilllppfpipppipipliifplplp",
 }
 EXPORTS = tuple(_SIGS) + ("ov3d_version", "ov3d_sa_layer_supported", "ov3d_attn_fwd_workspace",

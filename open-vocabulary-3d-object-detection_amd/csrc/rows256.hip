@@ -88,8 +88,18 @@ struct Rows256Args {
     long long M;
     int tiles;
     unsigned int* ctr;   // [next tile, workgroups done]: zero, and left zero by every launch
+    // BNIN: X holds the previous layer's pre-BatchNorm rows; the product's input is
+    // Z = bf16(relu(X * scale + shift)) (the ov3d_rows_bn_apply arithmetic), written to Z
+    const float* scale; const float* shift;
+    bf16* Z; long long ldz;
 };
 
+// ds_write_b128 as asm (a plain LDS store would wait for every DMA in flight)
+__device__ __forceinline__ void lds_write128(uint32_t addr, i32x4 v) {
+    asm volatile("ds_write_b128 %0, %1" : : "v"(addr), "v"(v) : "memory");
+}
+
+template <bool BNIN>
 __global__ void __launch_bounds__(NT, 1) rows256_kernel(Rows256Args a) {
     __shared__ __attribute__((aligned(16))) char L[2 * TILE_BYTES];
     __shared__ int s_claim[2];
@@ -136,6 +146,20 @@ __global__ void __launch_bounds__(NT, 1) rows256_kernel(Rows256Args a) {
     const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)L;
     const uint32_t rowoff = (uint32_t)(li * KD * 2);
 
+    // BNIN: this thread's 8 channels 8 (tid & 31) .. + 7 are the same in every tile
+    float bsc[BNIN ? 8 : 1], bsh[BNIN ? 8 : 1];
+    if constexpr (BNIN) {
+        const int c8 = 8 * (tid & 31);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            bsc[j] = a.scale[c8 + j];
+            bsh[j] = a.shift[c8 + j];
+        }
+    }
+    // VMEM operations a lane issues per tile after its DMA: the output stores (8), with BNIN
+    // also the Z stores (8)
+    constexpr int SPT = BNIN ? 16 : 8;
+
     __syncthreads();   // the first claims (nothing in flight yet but the W loads)
     int t = s_claim[0], tn = s_claim[1];
     if (t < a.tiles) issue(t, 0);
@@ -150,10 +174,38 @@ __global__ void __launch_bounds__(NT, 1) rows256_kernel(Rows256Args a) {
         if (has_next) issue(tn, buf ^ 1);
         // this tile's DMA landed: later VMEM ops (the previous tile's 8 stores, the claim, the
         // next tile's 8 DMA pieces) may stay in flight
-        if (has_next && prev_stores) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        else if (prev_stores || has_next) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        if (has_next && prev_stores) asm volatile("s_waitcnt vmcnt(%0)" : : "n"(SPT + 8) : "memory");
+        else if (prev_stores) asm volatile("s_waitcnt vmcnt(%0)" : : "n"(SPT) : "memory");
+        else if (has_next) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+        if constexpr (BNIN) {
+            // the tile in place: z = bf16(relu(x * scale + shift)), also stored to Z (the
+            // weight gradient's input); thread = 8 rows of one 8-channel chunk
+            const uint32_t tbuf = lds0 + buf * TILE_BYTES;
+            const long long zm0 = (long long)t * TM;
+            const int c = tid & 31;
+            i32x4 rv[RB];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int r = (tid >> 5) + 16 * i;
+                rv[i] = lds128(tbuf + r * KD * 2 + 16 * (c ^ (r & 15)));
+            }
+            lgkm_wait8(rv);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int r = (tid >> 5) + 16 * i;
+                const bf16x8 v = __builtin_bit_cast(bf16x8, rv[i]);
+                bf16x8 o;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) o[j] = (bf16)fmaxf(fmaf((float)v[j], bsc[j], bsh[j]), 0.f);
+                const i32x4 ov = __builtin_bit_cast(i32x4, o);
+                lds_write128(tbuf + r * KD * 2 + 16 * (c ^ (r & 15)), ov);
+                if (zm0 + r < a.M) *reinterpret_cast<i32x4*>(a.Z + (zm0 + r) * a.ldz + 8 * c) = ov;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
 
         f32x4 acc[RB][2];
 #pragma unroll
@@ -209,8 +261,8 @@ __global__ void __launch_bounds__(NT, 1) rows256_kernel(Rows256Args a) {
         }
         prev_stores = true;
         if (tid == 0 && has_next) {
-            // the claim returned: younger are the next tile's 8 DMA pieces and this tile's 8 stores
-            asm volatile("s_waitcnt vmcnt(16)" : "+v"(claim) : : "memory");
+            // the claim returned: younger are the next tile's 8 DMA pieces and this tile's stores
+            asm volatile("s_waitcnt vmcnt(%1)" : "+v"(claim) : "n"(SPT + 8) : "memory");
             s_claim[buf] = (int)claim;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -237,8 +289,12 @@ extern "C" int ov3d_rows256_supported(long long M, int N, int K) {
            M * KD * 2 < (1LL << 40);
 }
 
-extern "C" int ov3d_rows256(const void* X, long long ldx, const void* W, long long ldw, void* Y,
-                            long long ldy, long long M, unsigned int* counters, void* stream) {
+namespace {
+struct BnIn {
+    const float* scale; const float* shift; void* Z; long long ldz;
+};
+int rows256_launch(const void* X, long long ldx, const void* W, long long ldw, void* Y, long long ldy,
+                   long long M, unsigned int* counters, const BnIn* bn, void* stream) {
     if (!ov3d_rows256_supported(M, KD, KD) || !X || !W || !Y || !counters || ldx < KD || ldw < KD ||
         ldy < KD || ldx % 8 || ldw % 8 || ldy % 8 || ((uintptr_t)X | (uintptr_t)W | (uintptr_t)Y) % 16 ||
         (uintptr_t)counters % 8)
@@ -253,9 +309,30 @@ extern "C" int ov3d_rows256(const void* X, long long ldx, const void* W, long lo
             g_cus = 256;
     }
     Rows256Args a{(const bf16*)X, ldx, (const bf16*)W, ldw, (bf16*)Y, ldy, M, (int)((M + TM - 1) / TM),
-                  counters};
+                  counters, nullptr, nullptr, nullptr, 0};
     const int grid = a.tiles < g_cus ? a.tiles : g_cus;
-    rows256_kernel<<<grid, NT, 0, ov3d_stream(stream)>>>(a);
+    if (bn) {
+        if (!bn->scale || !bn->shift || !bn->Z || bn->ldz < KD || bn->ldz % 8 ||
+            ((uintptr_t)bn->scale | (uintptr_t)bn->shift | (uintptr_t)bn->Z) % 16)
+            return OV3D_EINVAL;
+        a.scale = bn->scale; a.shift = bn->shift; a.Z = (bf16*)bn->Z; a.ldz = bn->ldz;
+        rows256_kernel<true><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
+    } else {
+        rows256_kernel<false><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
+    }
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
+}
+}  // namespace
+
+extern "C" int ov3d_rows256(const void* X, long long ldx, const void* W, long long ldw, void* Y,
+                            long long ldy, long long M, unsigned int* counters, void* stream) {
+    return rows256_launch(X, ldx, W, ldw, Y, ldy, M, counters, nullptr, stream);
+}
+
+extern "C" int ov3d_rows256_bn(const void* X, long long ldx, const float* scale, const float* shift,
+                               const void* W, long long ldw, void* Y, long long ldy, void* Z,
+                               long long ldz, long long M, unsigned int* counters, void* stream) {
+    const BnIn bn{scale, shift, Z, ldz};
+    return rows256_launch(X, ldx, W, ldw, Y, ldy, M, counters, &bn, stream);
 }

@@ -531,3 +531,78 @@ def bn_relu_pool_rows(h, bn, S):
     """(R, C) training rows h -> (R / S, C) bf16: max over each S rows of relu(bn(h))"""
     with torch.autocast("cuda", enabled=False):
         return _BnReluPoolRows.apply(h, bn.weight, bn.bias, bn, S)
+
+
+# ------------------------------------------------------------- BN + ReLU into the next GEMM
+# a SharedMLP layer's BatchNorm + ReLU applied while the next layer's 256 x 256 product stages
+# its rows (csrc/rows256.hip ov3d_rows256_bn, the masked encoder's interim SA: 2^18 rows): no
+# separate apply pass; the activation rows are still written (the weight gradient's input).
+# OV3D_BN_GEMM=0: bn_relu_rows + the product
+BN_GEMM = os.environ.get("OV3D_BN_GEMM", "1") != "0"
+
+
+class _BnReluLinearRows(torch.autograd.Function):
+    """y = relu(bn(h)) w^T (training BN, no dropout, no bias): the _BnReluRows and
+    gemm._RowsLinear arithmetic in their order, bit-equal to the two (and the weight gradient
+    deferred the same way)"""
+
+    @staticmethod
+    def forward(ctx, h, gamma, beta, bn, w):
+        R, C = h.shape
+        dev = h.device
+        nbt = bn.num_batches_tracked if (bn.track_running_stats and
+                                         bn.num_batches_tracked is not None) else None
+        rowmajor = (C, 0, C)
+        mean, invstd, scale, shift = _stats_finalize(h, rowmajor, R, C, gamma, beta, [bn],
+                                                     bn.running_mean, bn.running_var, nbt)
+        wc = gemm.cast_param(w, torch.bfloat16)
+        z = torch.empty((R, C), dtype=torch.bfloat16, device=dev)
+        y = torch.empty((R, wc.shape[0]), dtype=torch.bfloat16, device=dev)
+        nat.call("ov3d_rows256_bn", h, h.stride(0), scale, shift, wc, wc.stride(0), y, y.stride(0), z,
+                 z.stride(0), R, gemm._rows256_counters(dev), like=h)
+        ctx.save_for_backward(h, gamma, mean, invstd, scale, shift, z, wc)
+        ctx.bn = bn
+        ctx.w = w
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        h, gamma, mean, invstd, scale, shift, z, wc = ctx.saved_tensors
+        w = ctx.w
+        R, C = h.shape
+        dev = h.device
+        dy = dy.to(torch.bfloat16).contiguous()
+        dw = None
+        with torch.autocast("cuda", enabled=False):
+            dz = gemm._dgrad(dy, wc)                      # gemm._RowsLinear's input gradient
+            if gemm.can_defer(z, w):
+                gemm.defer_weight_grad(dy, z, w)
+            elif gemm._fused_ok(dy, z):
+                dw = gemm.fused_weight_grad(dy, z, bias=False)[0].to(w.dtype)
+            else:
+                dw = gemm.weight_grad(dy, z).to(w.dtype)
+        rowmajor = (C, 0, C)
+        parts = torch.empty((NPARTS, 2, C), dtype=torch.float64, device=dev)
+        nat.call("ov3d_rows_bn_bwd", 0, dz, *rowmajor, h, 1, *rowmajor, R, C, scale, shift, mean,
+                 invstd, None, None, None, 0.0, None, 0, parts, NPARTS, None, 0, 0, 8, like=h)
+        group, world = _group_world(ctx.bn)
+        cA, cB, cC, dg, db = bn_bwd_affine(parts, NPARTS, C, group, R * world, gamma, mean, invstd)
+        dh = torch.empty((R, C), dtype=torch.bfloat16, device=dev)
+        nat.call("ov3d_rows_bn_bwd", 1, dz, *rowmajor, h, 1, *rowmajor, R, C, scale, shift, mean,
+                 invstd, cA, cB, cC, 0.0, None, 0, None, 0, dh, *rowmajor, like=h)
+        return dh, dg, db, None, dw
+
+
+def bn_relu_linear_ok(h, bn, relu, w, b):
+    """the fused BN + ReLU -> 256 x 256 product applies (bf16 contiguous rows on rows256)"""
+    return (BN_GEMM and gemm.ROWS256 and b is None and bn_relu_rows_ok(h, bn, relu, None)
+            and h.dtype == torch.bfloat16 and h.is_contiguous() and h.data_ptr() % 16 == 0
+            and h.shape[1] == 256 and h.shape[0] >= gemm.GEMM256_MIN_M
+            and tuple(w.shape[:2]) == (256, 256) and w.numel() == 256 * 256 and w.is_contiguous()
+            and bool(nat.load().ov3d_rows256_supported(h.shape[0], 256, 256)))
+
+
+def bn_relu_linear_rows(h, bn, w):
+    """(R, 256) training rows h -> relu(bn(h)) w^T (R, 256) bf16"""
+    with torch.autocast("cuda", enabled=False):
+        return _BnReluLinearRows.apply(h, bn.weight, bn.bias, bn, w)

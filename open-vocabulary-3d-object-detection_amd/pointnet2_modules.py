@@ -74,14 +74,21 @@ class SharedMLP(nn.Sequential):
         BN + ReLU as one HIP row pass each way (heads.bn_relu_rows; the ScanNet SA with colour
         and the masked encoder's interim SA, which the fused 3-channel kernels of sa_fused.py
         do not take).  pool=S: -> (y, pooled); pooled: the last layer's BN + ReLU went straight
-        into the max over each S rows (heads.bn_relu_pool_rows), y is (R / S, Cout)."""
+        into the max over each S rows (heads.bn_relu_pool_rows), y is (R / S, Cout).  A BN + ReLU
+        followed by a 256 x 256 product over >= 2^17 rows runs inside it
+        (heads.bn_relu_linear_rows)."""
         from . import heads
         from .gemm import rows_linear_padk
-        last = len(self) - 1
-        for i, layer in enumerate(self):
+        layers = list(self)
+        last = len(layers) - 1
+        pend = None   # a layer output whose BN + ReLU runs inside this layer's product
+        for i, layer in enumerate(layers):
             w = layer.conv.weight
             w2 = w.view(w.shape[0], w.shape[1])
-            if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] > w2.shape[1]:
+            if pend is not None:
+                x = heads.bn_relu_linear_rows(x, pend, w2)
+                pend = None
+            elif x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] > w2.shape[1]:
                 x = rows_linear_padk(x, w2, layer.conv.bias)   # zero-padded bf16 group rows
             else:
                 x = rows_linear(x, w2, layer.conv.bias)
@@ -90,6 +97,11 @@ class SharedMLP(nn.Sequential):
                 if pool is not None and i == last and heads.bn_relu_pool_ok(x, bn, layer.activation,
                                                                               pool):
                     return heads.bn_relu_pool_rows(x, bn, pool), True
+                if i < last:   # the next 256 x 256 product applies this BN + ReLU as it loads
+                    nxt = layers[i + 1].conv
+                    if heads.bn_relu_linear_ok(x, bn, layer.activation, nxt.weight, nxt.bias):
+                        pend = bn
+                        continue
                 if heads.bn_relu_rows_ok(x, bn, layer.activation, None):
                     x = heads.bn_relu_rows(x, bn)
                     continue

@@ -45,3 +45,42 @@ def test_bn_relu_pool_equals_two_passes(P, S, C):
     bad = [(n, (a.float() - b.float()).abs().max().item()) for n, a, b in zip(names, *res)
            if not torch.equal(a, b)]
     assert not bad, bad
+
+
+def test_bn_relu_into_rows256_equals_two_passes():
+    """heads.bn_relu_linear_rows (csrc/rows256.hip ov3d_rows256_bn: the previous layer's BN +
+    ReLU applied while the next 256 x 256 product stages its rows, the activation rows still
+    written for the weight gradient) against heads.bn_relu_rows + gemm.rows_linear: output, input
+    / gamma / beta / weight gradients and running statistics bit for bit (2^17 + 64 rows: a
+    ragged last tile)"""
+    from ov3d_amd import gemm, heads
+    torch.manual_seed(12)
+    dev = torch.device("cuda", 0)
+    R, C = (1 << 17) + 64, 256
+    h = torch.randn(R, C, device=dev).to(torch.bfloat16)
+    bn1 = torch.nn.BatchNorm2d(C).to(dev).train()
+    with torch.no_grad():
+        bn1.weight.normal_(1, 0.2)
+        bn1.bias.normal_(0, 0.2)
+        bn1.bias[:3] = -50.0                                 # dead channels
+    bn2 = copy.deepcopy(bn1)
+    conv1 = torch.nn.Conv2d(C, C, 1, bias=False).to(dev)
+    conv2 = copy.deepcopy(conv1)
+    g = torch.randn(R, C, device=dev).to(torch.bfloat16)
+    res = []
+    for fused, bn, conv in ((True, bn1, conv1), (False, bn2, conv2)):
+        x = h.clone().requires_grad_()
+        w2 = conv.weight.view(C, C)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            if fused:
+                assert heads.bn_relu_linear_ok(x, bn, torch.nn.ReLU(), conv.weight, None)
+                y = heads.bn_relu_linear_rows(x, bn, w2)
+            else:
+                y = gemm.rows_linear(heads.bn_relu_rows(x, bn), w2)
+        y.backward(g)
+        res.append([y.detach(), x.grad, bn.weight.grad, bn.bias.grad, conv.weight.grad,
+                    bn.running_mean.clone(), bn.running_var.clone()])
+    names = ["y", "dh", "dgamma", "dbeta", "dW", "running_mean", "running_var"]
+    bad = [(n, (a.float() - b.float()).abs().max().item()) for n, a, b in zip(names, *res)
+           if not torch.equal(a, b)]
+    assert not bad, bad
