@@ -1,4 +1,4 @@
-// Streaming product Y (M, 256) = X (M, 256) . W (256, 256)^T for very long row sets: the
+// Streaming product Y (M, 256) = X (M, K) . W (256, K)^T, K = 256 or 264, for very long row sets: the
 // masked encoder's interim set abstraction in ScanNet training (models/model_3detr.py:377-399
 // build_preencoder / interim downsampling, PointnetSAModuleVotes' SharedMLP 1x1 convolutions
 // over npoint * nsample = 2^18 grouped rows, mlp widths 256 -> 256 -> 256) forward, and the
@@ -38,6 +38,7 @@ constexpr int TM = 128;                 // rows a tile
 constexpr int KD = 256;                 // K = N
 constexpr int TILE_BYTES = TM * KD * 2; // 64 KB
 constexpr int RB = TM / 16;             // 16-row blocks a tile
+constexpr int TAIL_BYTES = TM * 16;     // KT: the K = 256 .. 263 chunk of a tile's rows
 
 __device__ __forceinline__ f32x4 mfma16(i32x4 a, i32x4 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
@@ -99,9 +100,12 @@ __device__ __forceinline__ void lds_write128(uint32_t addr, i32x4 v) {
     asm volatile("ds_write_b128 %0, %1" : : "v"(addr), "v"(v) : "memory");
 }
 
-template <bool BNIN>
+// KT: K = 264 (the interim SA's first layer: 256 features + xyz, zero-padded): gemm256's tail
+// K-step (k 256 .. 319, zeros past 264) as two more 32-deep MFMA steps, the rows' chunk 32 in a
+// tail image filled by two more DMA pieces (waves 6 and 7)
+template <bool BNIN, bool KT>
 __global__ void __launch_bounds__(NT, 1) rows256_kernel(Rows256Args a) {
-    __shared__ __attribute__((aligned(16))) char L[2 * TILE_BYTES];
+    __shared__ __attribute__((aligned(16))) char L[2 * TILE_BYTES + (KT ? 2 * TAIL_BYTES : 0)];
     __shared__ int s_claim[2];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -122,6 +126,14 @@ __global__ void __launch_bounds__(NT, 1) rows256_kernel(Rows256Args a) {
         for (int ks = 0; ks < 8; ++ks)
             wf[cb][ks] = *reinterpret_cast<const i32x4*>(a.W + (size_t)(32 * w + 16 * cb + li) * a.ldw +
                                                          32 * ks + 8 * lg);
+    const i32x4 zero4 = {0, 0, 0, 0};
+    i32x4 wt[2] = {zero4, zero4};   // KT: k = 256 + 8 lg .. (lg = 0 only; zeros past 264)
+    if constexpr (KT) {
+        if (lg == 0)
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb)
+                wt[cb] = *reinterpret_cast<const i32x4*>(a.W + (size_t)(32 * w + 16 * cb + li) * a.ldw + 256);
+    }
 
     // LDS-DMA of a tile: wave w fills rows 16 w + 2 i + (lane >> 5) (i = 0..7), physical chunk
     // lane & 31 <- logical chunk (lane & 31) ^ (row & 15)
@@ -140,6 +152,15 @@ __global__ void __launch_bounds__(NT, 1) rows256_kernel(Rows256Args a) {
         for (int i = 0; i < 8; ++i)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
                 rs, (__attribute__((address_space(3))) void*)(base + i * 2 * KD * 2), 16, voff[i], 0, 0, 0);
+        if constexpr (KT) {
+            if (w >= 6) {   // rows 64 (w - 6) + lane, chunk 32, lane-linear into the tail image
+                const int r = 64 * (w - 6) + lane;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (__attribute__((address_space(3))) void*)(L + 2 * TILE_BYTES + buf * TAIL_BYTES +
+                                                                   64 * (w - 6) * 16),
+                    16, (uint32_t)(r * a.ldx * 2) + 512u, 0, 0, 0);
+            }
+        }
     };
 
     // fragment reads: row 16 rb + li, logical chunk 4 ks + lg at physical (4 ks + lg) ^ li
@@ -225,6 +246,25 @@ __global__ void __launch_bounds__(NT, 1) rows256_kernel(Rows256Args a) {
 #pragma unroll
                 for (int cb = 0; cb < 2; ++cb) acc[rb][cb] = mfma16(wf[cb][ks], xf[rb], acc[rb][cb]);
         }
+        if constexpr (KT) {
+            // k 256 .. 287: chunk 32 from the tail image (lg = 0), zeros (lg > 0); then k 288 ..
+            // 319, all zeros: gemm256's K-tail step, both halves
+            i32x4 xf[RB];
+            const uint32_t tt = lds0 + 2 * TILE_BYTES + buf * TAIL_BYTES + li * 16;
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb) xf[rb] = lds128(tt + rb * 16 * 16);
+            lgkm_wait8(xf);
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb) {
+                const i32x4 x = lg == 0 ? xf[rb] : zero4;
+#pragma unroll
+                for (int cb = 0; cb < 2; ++cb) acc[rb][cb] = mfma16(wt[cb], x, acc[rb][cb]);
+            }
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+                for (int cb = 0; cb < 2; ++cb) acc[rb][cb] = mfma16(zero4, zero4, acc[rb][cb]);
+        }
         // the tile's bf16 image into the buffer just read (row-major, chunk c of row r at
         // c ^ (r & 15)), then every thread stores 8 whole 16-byte chunks (2 rows a wave): the
         // 8-byte stores straight from the accumulators ran at 68 vs 54 us (tools/rows256_probe.py)
@@ -285,7 +325,7 @@ int g_cus = 0;
 }  // namespace
 
 extern "C" int ov3d_rows256_supported(long long M, int N, int K) {
-    return M > 0 && N == KD && K == KD && (M + TM - 1) / TM < (1LL << 31) &&
+    return M > 0 && N == KD && (K == KD || K == KD + 8) && (M + TM - 1) / TM < (1LL << 31) &&
            M * KD * 2 < (1LL << 40);
 }
 
@@ -293,9 +333,10 @@ namespace {
 struct BnIn {
     const float* scale; const float* shift; void* Z; long long ldz;
 };
-int rows256_launch(const void* X, long long ldx, const void* W, long long ldw, void* Y, long long ldy,
-                   long long M, unsigned int* counters, const BnIn* bn, void* stream) {
-    if (!ov3d_rows256_supported(M, KD, KD) || !X || !W || !Y || !counters || ldx < KD || ldw < KD ||
+int rows256_launch(const void* X, long long ldx, int K, const void* W, long long ldw, void* Y,
+                   long long ldy, long long M, unsigned int* counters, const BnIn* bn, void* stream) {
+    if (!ov3d_rows256_supported(M, KD, K) || (bn && K != KD) || !X || !W || !Y || !counters ||
+        ldx < K || ldw < K ||
         ldy < KD || ldx % 8 || ldw % 8 || ldy % 8 || ((uintptr_t)X | (uintptr_t)W | (uintptr_t)Y) % 16 ||
         (uintptr_t)counters % 8)
         return OV3D_EINVAL;
@@ -316,23 +357,26 @@ int rows256_launch(const void* X, long long ldx, const void* W, long long ldw, v
             ((uintptr_t)bn->scale | (uintptr_t)bn->shift | (uintptr_t)bn->Z) % 16)
             return OV3D_EINVAL;
         a.scale = bn->scale; a.shift = bn->shift; a.Z = (bf16*)bn->Z; a.ldz = bn->ldz;
-        rows256_kernel<true><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
+        rows256_kernel<true, false><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
+    } else if (K == KD) {
+        rows256_kernel<false, false><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
     } else {
-        rows256_kernel<false><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
+        rows256_kernel<false, true><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
     }
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }
 }  // namespace
 
-extern "C" int ov3d_rows256(const void* X, long long ldx, const void* W, long long ldw, void* Y,
-                            long long ldy, long long M, unsigned int* counters, void* stream) {
-    return rows256_launch(X, ldx, W, ldw, Y, ldy, M, counters, nullptr, stream);
+extern "C" int ov3d_rows256(const void* X, long long ldx, int K, const void* W, long long ldw,
+                            void* Y, long long ldy, long long M, unsigned int* counters,
+                            void* stream) {
+    return rows256_launch(X, ldx, K, W, ldw, Y, ldy, M, counters, nullptr, stream);
 }
 
 extern "C" int ov3d_rows256_bn(const void* X, long long ldx, const float* scale, const float* shift,
                                const void* W, long long ldw, void* Y, long long ldy, void* Z,
                                long long ldz, long long M, unsigned int* counters, void* stream) {
     const BnIn bn{scale, shift, Z, ldz};
-    return rows256_launch(X, ldx, W, ldw, Y, ldy, M, counters, &bn, stream);
+    return rows256_launch(X, ldx, KD, W, ldw, Y, ldy, M, counters, &bn, stream);
 }

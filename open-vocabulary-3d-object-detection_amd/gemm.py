@@ -334,25 +334,27 @@ def conv3x3_gemm256(x, w, bias=None, residual=None, relu=False):
 GEMM256_MIN_M = int(os.environ.get("OV3D_GEMM256_MIN_M", str(1 << 17)))
 
 
-# (M, 256) x (256, 256)^T products over this many rows and more, without bias (the masked
-# encoder's interim SA layers and their input gradients), on the streaming kernel
+# (M, 256 or 264) x (256, K)^T products over this many rows and more, without bias (the masked
+# encoder's interim SA layers and their 256-wide input gradients), on the streaming kernel
 # (csrc/rows256.hip: W resident per CU, equal to gemm256's outputs bit for bit); "0": gemm256
 ROWS256 = os.environ.get("OV3D_ROWS256", "1") != "0"
 
 
 def rows256_ok(a, w, bias=None):
+    """a (M, K) x w (256, K)^T, K = 256 or 264 (the zero-padded first layer), runs on rows256"""
     from . import _native
+    K = a.shape[1] if a.dim() == 2 else 0
     return (ROWS256 and bias is None and a.shape[0] >= GEMM256_MIN_M and _rows_ok(a) and _rows_ok(w)
-            and tuple(a.shape[1:]) == (256,) and tuple(w.shape) == (256, 256)
-            and bool(_native.load().ov3d_rows256_supported(a.shape[0], 256, 256)))
+            and K in (256, 264) and tuple(w.shape) == (256, K)
+            and bool(_native.load().ov3d_rows256_supported(a.shape[0], 256, K)))
 
 
 def rows256(a, w):
-    """a (M, 256) w (256, 256)^T -> (M, 256) bf16 (check rows256_ok first)"""
+    """a (M, K) w (256, K)^T -> (M, 256) bf16 (check rows256_ok first)"""
     from . import _native
     out = torch.empty((a.shape[0], 256), dtype=torch.bfloat16, device=a.device)
-    _native.call("ov3d_rows256", a, a.stride(0), w, w.stride(0), out, out.stride(0), a.shape[0],
-                 _rows256_counters(a.device), like=a)
+    _native.call("ov3d_rows256", a, a.stride(0), a.shape[1], w, w.stride(0), out, out.stride(0),
+                 a.shape[0], _rows256_counters(a.device), like=a)
     return out
 
 

@@ -185,7 +185,7 @@ def test_rows256_equals_gemm256_bitwise(M, ldx):
     x = xb[:, :256]
     w = (0.06 * torch.randn(256, 256, device=dev)).to(torch.bfloat16)
     y = torch.full((M, 256), float("nan"), device=dev, dtype=torch.bfloat16)
-    _native.call("ov3d_rows256", x, x.stride(0), w, w.stride(0), y, y.stride(0), M,
+    _native.call("ov3d_rows256", x, x.stride(0), 256, w, w.stride(0), y, y.stride(0), M,
                  gemm._rows256_counters(dev), like=x)
     ref = gemm.gemm256(x, w)
     assert torch.equal(y, ref)
@@ -216,3 +216,23 @@ def test_rows256_routes_interim_sa_products():
     assert seen.count("ov3d_rows256") == 2, seen
     assert torch.equal(y, gemm.gemm256(x, w))
     assert torch.equal(dx, gemm.gemm256(x, w.t().contiguous()))
+
+
+@pytest.mark.parametrize("M", [262144, 131072 + 37, 77])
+def test_rows256_k264_equals_gemm256_bitwise(M):
+    """the interim SA's first layer: 259 inputs zero-padded to 264 columns (rows and weight), on
+    rows256's K-tail mode against gemm256's K-tail step, every output bit (rows with all-zero
+    inputs included: the zero steps are the same instructions)"""
+    from ov3d_amd import _native, gemm
+    torch.manual_seed(5)
+    dev = torch.device("cuda", 0)
+    x = torch.randn(M, 264, device=dev).to(torch.bfloat16)
+    x[:, 259:] = 0
+    x[:3] = 0
+    w = torch.nn.functional.pad((0.06 * torch.randn(256, 259, device=dev)).to(torch.bfloat16), (0, 5))
+    y = torch.full((M, 256), float("nan"), device=dev, dtype=torch.bfloat16)
+    _native.call("ov3d_rows256", x, x.stride(0), 264, w, w.stride(0), y, y.stride(0), M,
+                 gemm._rows256_counters(dev), like=x)
+    assert torch.equal(y, gemm.gemm256(x, w))
+    if M >= gemm.GEMM256_MIN_M:
+        assert gemm.rows256_ok(x, w) and torch.equal(gemm._linear(x, w, None), y)
