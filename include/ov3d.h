@@ -495,7 +495,7 @@ int ov3d_rows256(const void* X, long long ldx, int K, const void* W, long long l
                  long long ldy, long long M, unsigned int* counters, void* stream);
 /* ov3d_rows256 of Z = bf16(relu(X * scale + shift)) (the previous layer's BatchNorm + ReLU, the
  * ov3d_rows_bn_apply arithmetic without dropout; scale / shift (256) fp32) with Z also written
- * (ldz % 8; the weight gradient's input): Y equals ov3d_rows_bn_apply followed by ov3d_rows256 */
+ * when Z != NULL (ldz % 8): Y equals ov3d_rows_bn_apply followed by ov3d_rows256 */
 int ov3d_rows256_bn(const void* X, long long ldx, const float* scale, const float* shift,
                     const void* W, long long ldw, void* Y, long long ldy, void* Z, long long ldz,
                     long long M, unsigned int* counters, void* stream);
@@ -642,6 +642,12 @@ int ov3d_attn_bwd_masked(const void* q, const void* k, const void* v, long long 
 int ov3d_wgrad(const void* dy, long long ldy, const void* x, long long ldx, int R, int N, int K,
                float* dW, long long ldw, float* db, float* workspace, int* counters, int nsplit,
                void* stream);
+/* ov3d_wgrad with x = bf16(relu(x_stored * scale + shift)) per input channel (the previous
+ * layer's BatchNorm + ReLU applied on load, ov3d_rows_bn_apply's arithmetic; K % 8 == 0, 16-byte
+ * aligned x rows): the weight gradient of ov3d_rows256_bn's product without its Z rows */
+int ov3d_wgrad_bn(const void* dy, long long ldy, const void* x, long long ldx, int R, int N, int K,
+                  const float* scale, const float* shift, float* dW, long long ldw, float* db,
+                  float* workspace, int* counters, int nsplit, void* stream);
 long long ov3d_wgrad_workspace(int R, int N, int K, int nsplit);
 /* several independent weight gradients in one launch (+ one split reduction launch) per
  * 28 problems: the deferred dW / db of a backward pass (gemm.py).  256 x 256 tiles,

@@ -77,6 +77,7 @@ _SIGS = {
     "ov3d_nbr_max_bnrelu_fwd": "pliippppp",
     "ov3d_rows_bn_bwd_pooled": "ippiplippppppppipp",
     "ov3d_wgrad": "plpliiiplpppip",
+    "ov3d_wgrad_bn": "plpliiippplpppip",
     "ov3d_wgrad_group": "pipp",
     "ov3d_rows_bn_stats": "pillilipip",
     "ov3d_rows_bn_apply": "pillilippfpipllip",

@@ -103,7 +103,9 @@ __device__ __forceinline__ void lds_write128(uint32_t addr, i32x4 v) {
 // KT: K = 264 (the interim SA's first layer: 256 features + xyz, zero-padded): gemm256's tail
 // K-step (k 256 .. 319, zeros past 264) as two more 32-deep MFMA steps, the rows' chunk 32 in a
 // tail image filled by two more DMA pieces (waves 6 and 7)
-template <bool BNIN, bool KT>
+// BNIN: 0 none, 1 BN + ReLU on the staged rows and Z stored, 2 the same without Z (its weight
+// gradient applies the BN on load: ov3d_wgrad_bn)
+template <int BNIN, bool KT>
 __global__ void __launch_bounds__(NT, 1) rows256_kernel(Rows256Args a) {
     __shared__ __attribute__((aligned(16))) char L[2 * TILE_BYTES + (KT ? 2 * TAIL_BYTES : 0)];
     __shared__ int s_claim[2];
@@ -179,7 +181,7 @@ __global__ void __launch_bounds__(NT, 1) rows256_kernel(Rows256Args a) {
     }
     // VMEM operations a lane issues per tile after its DMA: the output stores (8), with BNIN
     // also the Z stores (8)
-    constexpr int SPT = BNIN ? 16 : 8;
+    constexpr int SPT = BNIN == 1 ? 16 : 8;
 
     __syncthreads();   // the first claims (nothing in flight yet but the W loads)
     int t = s_claim[0], tn = s_claim[1];
@@ -222,7 +224,8 @@ __global__ void __launch_bounds__(NT, 1) rows256_kernel(Rows256Args a) {
                 for (int j = 0; j < 8; ++j) o[j] = (bf16)fmaxf(fmaf((float)v[j], bsc[j], bsh[j]), 0.f);
                 const i32x4 ov = __builtin_bit_cast(i32x4, o);
                 lds_write128(tbuf + r * KD * 2 + 16 * (c ^ (r & 15)), ov);
-                if (zm0 + r < a.M) *reinterpret_cast<i32x4*>(a.Z + (zm0 + r) * a.ldz + 8 * c) = ov;
+                if constexpr (BNIN == 1)
+                    if (zm0 + r < a.M) *reinterpret_cast<i32x4*>(a.Z + (zm0 + r) * a.ldz + 8 * c) = ov;
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
@@ -353,15 +356,16 @@ int rows256_launch(const void* X, long long ldx, int K, const void* W, long long
                   counters, nullptr, nullptr, nullptr, 0};
     const int grid = a.tiles < g_cus ? a.tiles : g_cus;
     if (bn) {
-        if (!bn->scale || !bn->shift || !bn->Z || bn->ldz < KD || bn->ldz % 8 ||
+        if (!bn->scale || !bn->shift || (bn->Z && (bn->ldz < KD || bn->ldz % 8)) ||
             ((uintptr_t)bn->scale | (uintptr_t)bn->shift | (uintptr_t)bn->Z) % 16)
             return OV3D_EINVAL;
         a.scale = bn->scale; a.shift = bn->shift; a.Z = (bf16*)bn->Z; a.ldz = bn->ldz;
-        rows256_kernel<true, false><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
+        if (bn->Z) rows256_kernel<1, false><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
+        else rows256_kernel<2, false><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
     } else if (K == KD) {
-        rows256_kernel<false, false><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
+        rows256_kernel<0, false><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
     } else {
-        rows256_kernel<false, true><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
+        rows256_kernel<0, true><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
     }
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;

@@ -52,6 +52,10 @@ struct WgradArgs {
     float* part;      // (nsplit, N, K) + (nsplit, N) split partials
     int nsplit, rows_per_split;
     int vec_dy, vec_x;  // 16-byte row segments are aligned (row strides % 8 == 0)
+    // x = bf16(relu(x_stored * xs + xh)) per channel when xs != null (ov3d_wgrad_bn: the layer's
+    // input is the previous layer's BatchNorm + ReLU, applied on load instead of stored)
+    const float* xs;
+    const float* xh;
 };
 
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
@@ -311,6 +315,20 @@ __device__ __forceinline__ void wgrad_body(const WgradArgs& a, int bx, int by, i
     // rows on the VALU (thread: 8 adjacent columns x 2 rows per stage)
     const bool do_bias = a.db != nullptr && by == 0;
 
+    // ov3d_wgrad_bn: the thread's 8 x channels (k0 + 8 (tid & 15) ..) are the same in every
+    // stage: their BN coefficients in registers (zeros past K: those columns are never stored)
+    float xsc[8], xsh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xsc[j] = xsh[j] = 0.f;
+    if (a.xs) {
+        const int kx = k0 + 8 * (tid & 15);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (kx + j < a.K) {
+                xsc[j] = a.xs[kx + j];
+                xsh[j] = a.xh[kx + j];
+            }
+    }
     // stage loader: RS rows x 16 chunks (16 B) per operand = 512 chunks, 2 per thread.
     // Two register sets: stage n+2 is in flight while stage n is computed and stage n+1
     // waits in the other set (a stage is only 4-6 MFMAs per wave, too short to cover a
@@ -337,12 +355,20 @@ __device__ __forceinline__ void wgrad_body(const WgradArgs& a, int bx, int by, i
             xr[c] = zx;
         }
     };
-    auto store = [&](const bf16x8 (&dr)[2], const bf16x8 (&xr)[2], int buf) {
+    // ov3d_wgrad_bn: the BN + ReLU (ov3d_rows_bn_apply's arithmetic) here, when the stage's
+    // registers have long landed (in the loader it would wait for every load at once); rows past
+    // rend stay zero
+    auto store = [&](const bf16x8 (&dr)[2], const bf16x8 (&xr)[2], int buf, int r0) {
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             const int idx = tid + 256 * c, row = idx >> 4, ch = idx & 15;
+            bf16x8 xv = xr[c];
+            if (a.xs && r0 + row < rend) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) xv[j] = (bf16)fmaxf(fmaf((float)xv[j], xsc[j], xsh[j]), 0.f);
+            }
             *reinterpret_cast<bf16x8*>(&Ds[buf][row * LDT + 8 * ch]) = dr[c];
-            *reinterpret_cast<bf16x8*>(&Xs[buf][row * LDT + 8 * ch]) = xr[c];
+            *reinterpret_cast<bf16x8*>(&Xs[buf][row * LDT + 8 * ch]) = xv;
         }
     };
 
@@ -381,7 +407,7 @@ __device__ __forceinline__ void wgrad_body(const WgradArgs& a, int bx, int by, i
     bf16x8 dA[2], xA[2], dB[2], xB[2];
     if (rbeg < rend) {
         load(dA, xA, rbeg);
-        store(dA, xA, 0);
+        store(dA, xA, 0, rbeg);
         if (rbeg + RS < rend) load(dA, xA, rbeg + RS);
     }
     __syncthreads();
@@ -389,14 +415,14 @@ __device__ __forceinline__ void wgrad_body(const WgradArgs& a, int bx, int by, i
         // LDS buffer 0 holds stage r, set A holds stage r + RS
         if (r + 2 * RS < rend) load(dB, xB, r + 2 * RS);
         compute(0);
-        if (r + RS < rend) store(dA, xA, 1);
+        if (r + RS < rend) store(dA, xA, 1, r + RS);
         __syncthreads();
         r += RS;
         if (r >= rend) break;
         // LDS buffer 1 holds stage r, set B holds stage r + RS
         if (r + 2 * RS < rend) load(dA, xA, r + 2 * RS);
         compute(1);
-        if (r + RS < rend) store(dB, xB, 0);
+        if (r + RS < rend) store(dB, xB, 0, r + RS);
         __syncthreads();
         r += RS;
     }
@@ -689,16 +715,23 @@ static int make_args(WgradArgs& a, const void* dy, long long ldy, const void* x,
     a.rows_per_split = rps;
     a.vec_dy = (ldy % 8 == 0) && ((uintptr_t)dy % 16 == 0);
     a.vec_x = (ldx % 8 == 0) && ((uintptr_t)x % 16 == 0);
+    a.xs = nullptr;
+    a.xh = nullptr;
     return OV3D_OK;
 }
 
-extern "C" int ov3d_wgrad(const void* dy, long long ldy, const void* x, long long ldx, int R, int N,
-                          int K, float* dW, long long ldw, float* db, float* workspace,
-                          int* counters, int nsplit, void* stream) {
-    (void)counters;
+namespace {
+int wgrad_launch(const void* dy, long long ldy, const void* x, long long ldx, int R, int N, int K,
+                 float* dW, long long ldw, float* db, float* workspace, int nsplit,
+                 const float* xs, const float* xh, void* stream) {
     WgradArgs a;
     const int rc = make_args(a, dy, ldy, x, ldx, R, N, K, dW, ldw, db, workspace, nsplit);
     if (rc != OV3D_OK) return rc;
+    if (xs || xh) {
+        if (!xs || !xh || K % 8 || !a.vec_x) return OV3D_EINVAL;
+        a.xs = xs;
+        a.xh = xh;
+    }
     nsplit = a.nsplit;
     dim3 grid((N + TN - 1) / TN, (K + TK - 1) / TK, nsplit);
     hipStream_t st = ov3d_stream(stream);
@@ -710,6 +743,25 @@ extern "C" int ov3d_wgrad(const void* dy, long long ldy, const void* x, long lon
         OV3D_LAUNCH_CHECK();
     }
     return OV3D_OK;
+}
+}  // namespace
+
+extern "C" int ov3d_wgrad(const void* dy, long long ldy, const void* x, long long ldx, int R, int N,
+                          int K, float* dW, long long ldw, float* db, float* workspace,
+                          int* counters, int nsplit, void* stream) {
+    (void)counters;
+    return wgrad_launch(dy, ldy, x, ldx, R, N, K, dW, ldw, db, workspace, nsplit, nullptr, nullptr,
+                        stream);
+}
+
+extern "C" int ov3d_wgrad_bn(const void* dy, long long ldy, const void* x, long long ldx, int R,
+                             int N, int K, const float* scale, const float* shift, float* dW,
+                             long long ldw, float* db, float* workspace, int* counters, int nsplit,
+                             void* stream) {
+    (void)counters;
+    if (!scale || !shift) return OV3D_EINVAL;
+    return wgrad_launch(dy, ldy, x, ldx, R, N, K, dW, ldw, db, workspace, nsplit, scale, shift,
+                        stream);
 }
 
 // stream-K plan of problems [first, first + g.n): units, slot and tile prefixes, grid

@@ -466,10 +466,11 @@ def _fused_ok(dy, x):
             and dy.dim() == 2 and x.dim() == 2 and dy.stride(1) == 1 and x.stride(1) == 1)
 
 
-def fused_weight_grad(dy, x, bias=True, out_w=None, out_b=None):
+def fused_weight_grad(dy, x, bias=True, out_w=None, out_b=None, bn=None):
     """dW = dy^T x (fp32, (N, K)) and db = column sums of dy (fp32, (N,)) in ONE HIP launch
     (csrc/wgrad.hip, ov3d_wgrad); dy (R, N), x (R, K) bf16 rows (row strides taken from the
-    tensors).  out_w / out_b: optional fp32 destinations (row slices of a larger gradient)."""
+    tensors).  out_w / out_b: optional fp32 destinations (row slices of a larger gradient).
+    bn=(scale, shift): x is relu(x * scale + shift) in bf16, applied on load (ov3d_wgrad_bn)."""
     from . import _native
     R, N = dy.shape
     K = x.shape[1]
@@ -486,8 +487,12 @@ def fused_weight_grad(dy, x, bias=True, out_w=None, out_b=None):
         raise ValueError("fused_weight_grad: too many output tiles")
     ws_n = lib.ov3d_wgrad_workspace(R, N, K, nsplit)
     ws = torch.empty((max(ws_n, 1),), dtype=torch.float32, device=dev)
-    _native.call("ov3d_wgrad", dy, dy.stride(0), x, x.stride(0), R, N, K, dw, dw.stride(0), db, ws,
-                 _wg_counters(dev), nsplit, like=dy)
+    if bn is not None:
+        _native.call("ov3d_wgrad_bn", dy, dy.stride(0), x, x.stride(0), R, N, K, bn[0], bn[1], dw,
+                     dw.stride(0), db, ws, _wg_counters(dev), nsplit, like=dy)
+    else:
+        _native.call("ov3d_wgrad", dy, dy.stride(0), x, x.stride(0), R, N, K, dw, dw.stride(0), db,
+                     ws, _wg_counters(dev), nsplit, like=dy)
     return dw, db
 
 
@@ -591,12 +596,13 @@ def can_defer(x, w, b=None):
             and _leaf_param(w) is not None and (b is None or _leaf_param(b) is not None))
 
 
-def defer_weight_grad(dy, x, w, b=None, rows=None):
+def defer_weight_grad(dy, x, w, b=None, rows=None, bn=None):
     """queue dW = dy^T x (+ db = sum dy) for parameter w (and bias b); rows=(r0, r1): the
-    block of w's rows this pair produces (nn.MultiheadAttention in_proj)."""
+    block of w's rows this pair produces (nn.MultiheadAttention in_proj); bn=(scale, shift):
+    the input is relu(x * scale + shift) (its own ov3d_wgrad_bn launch)."""
     _ensure_flush()
     _PENDING.append((dy, x, _leaf_param(w), w.shape, _leaf_param(b) if b is not None else None,
-                     rows))
+                     rows, bn))
 
 
 def flush_weight_grads():
@@ -618,7 +624,7 @@ def flush_weight_grads():
             bufs[id(param)] = e
         return e
 
-    for dy, x, wp, wshape, bp, rows in items:
+    for dy, x, wp, wshape, bp, rows, _ in items:
         r0, r1 = rows if rows is not None else (0, wshape[0])
         buf(wp)[2] += r1 - r0
         if bp is not None:
@@ -627,17 +633,17 @@ def flush_weight_grads():
         full = e[2] == e[0].shape[0]
         e[1] = (torch.empty if full else torch.zeros)(e[0].shape, dtype=torch.float32,
                                                        device=e[0].device)
-    for dy, x, wp, wshape, bp, rows in items:
+    for dy, x, wp, wshape, bp, rows, bn in items:
         R, N = dy.shape
         K = x.shape[1]
         r0, r1 = rows if rows is not None else (0, wshape[0])
         dw = bufs[id(wp)][1].view(wshape)[r0:r1].reshape(r1 - r0, K)
         db = bufs[id(bp)][1][r0:r1] if bp is not None else None
-        if R >= WGRAD_SINGLE_MIN_R:
+        if R >= WGRAD_SINGLE_MIN_R or bn is not None:
             # long problems (the masked encoder's interim SA, R = 2^18) run on their own
             # launch: the grouped stream-K split gives them hundreds of partial slots
             # (tools/wgrad_big.py: 104 vs 140 us at R = 2^18, N = K = 256)
-            fused_weight_grad(dy, x, bias=db is not None, out_w=dw, out_b=db)
+            fused_weight_grad(dy, x, bias=db is not None, out_w=dw, out_b=db, bn=bn)
             continue
         probs.append(_WgProblem(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), R, N, K,
                                 _wg_group_splits(R), dw.data_ptr(), dw.stride(0),

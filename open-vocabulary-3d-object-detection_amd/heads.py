@@ -536,15 +536,15 @@ def bn_relu_pool_rows(h, bn, S):
 # ------------------------------------------------------------- BN + ReLU into the next GEMM
 # a SharedMLP layer's BatchNorm + ReLU applied while the next layer's 256 x 256 product stages
 # its rows (csrc/rows256.hip ov3d_rows256_bn, the masked encoder's interim SA: 2^18 rows): no
-# separate apply pass; the activation rows are still written (the weight gradient's input).
-# OV3D_BN_GEMM=0: bn_relu_rows + the product
+# separate apply pass and no activation rows -- the weight gradient applies the same BN + ReLU
+# as it loads the pre-BN rows (ov3d_wgrad_bn).  OV3D_BN_GEMM=0: bn_relu_rows + the product
 BN_GEMM = os.environ.get("OV3D_BN_GEMM", "1") != "0"
 
 
 class _BnReluLinearRows(torch.autograd.Function):
     """y = relu(bn(h)) w^T (training BN, no dropout, no bias): the _BnReluRows and
-    gemm._RowsLinear arithmetic in their order, bit-equal to the two (and the weight gradient
-    deferred the same way)"""
+    gemm._RowsLinear arithmetic in their order, bit-equal to the two; the weight gradient
+    dy^T relu(bn(h)) is deferred the same way, its input rebuilt from h on load"""
 
     @staticmethod
     def forward(ctx, h, gamma, beta, bn, w):
@@ -556,18 +556,17 @@ class _BnReluLinearRows(torch.autograd.Function):
         mean, invstd, scale, shift = _stats_finalize(h, rowmajor, R, C, gamma, beta, [bn],
                                                      bn.running_mean, bn.running_var, nbt)
         wc = gemm.cast_param(w, torch.bfloat16)
-        z = torch.empty((R, C), dtype=torch.bfloat16, device=dev)
         y = torch.empty((R, wc.shape[0]), dtype=torch.bfloat16, device=dev)
-        nat.call("ov3d_rows256_bn", h, h.stride(0), scale, shift, wc, wc.stride(0), y, y.stride(0), z,
-                 z.stride(0), R, gemm._rows256_counters(dev), like=h)
-        ctx.save_for_backward(h, gamma, mean, invstd, scale, shift, z, wc)
+        nat.call("ov3d_rows256_bn", h, h.stride(0), scale, shift, wc, wc.stride(0), y, y.stride(0),
+                 None, 0, R, gemm._rows256_counters(dev), like=h)
+        ctx.save_for_backward(h, gamma, mean, invstd, scale, shift, wc)
         ctx.bn = bn
         ctx.w = w
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        h, gamma, mean, invstd, scale, shift, z, wc = ctx.saved_tensors
+        h, gamma, mean, invstd, scale, shift, wc = ctx.saved_tensors
         w = ctx.w
         R, C = h.shape
         dev = h.device
@@ -575,12 +574,11 @@ class _BnReluLinearRows(torch.autograd.Function):
         dw = None
         with torch.autocast("cuda", enabled=False):
             dz = gemm._dgrad(dy, wc)                      # gemm._RowsLinear's input gradient
-            if gemm.can_defer(z, w):
-                gemm.defer_weight_grad(dy, z, w)
-            elif gemm._fused_ok(dy, z):
-                dw = gemm.fused_weight_grad(dy, z, bias=False)[0].to(w.dtype)
+            # its weight gradient dy^T relu(bn(h)), the activation applied on load
+            if gemm.can_defer(h, w):
+                gemm.defer_weight_grad(dy, h, w, bn=(scale, shift))
             else:
-                dw = gemm.weight_grad(dy, z).to(w.dtype)
+                dw = gemm.fused_weight_grad(dy, h, bias=False, bn=(scale, shift))[0].to(w.dtype)
         rowmajor = (C, 0, C)
         parts = torch.empty((NPARTS, 2, C), dtype=torch.float64, device=dev)
         nat.call("ov3d_rows_bn_bwd", 0, dz, *rowmajor, h, 1, *rowmajor, R, C, scale, shift, mean,

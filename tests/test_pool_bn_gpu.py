@@ -47,13 +47,16 @@ def test_bn_relu_pool_equals_two_passes(P, S, C):
     assert not bad, bad
 
 
-def test_bn_relu_into_rows256_equals_two_passes():
+@pytest.mark.parametrize("defer", [False, True])
+def test_bn_relu_into_rows256_equals_two_passes(monkeypatch, defer):
     """heads.bn_relu_linear_rows (csrc/rows256.hip ov3d_rows256_bn: the previous layer's BN +
-    ReLU applied while the next 256 x 256 product stages its rows, the activation rows still
-    written for the weight gradient) against heads.bn_relu_rows + gemm.rows_linear: output, input
-    / gamma / beta / weight gradients and running statistics bit for bit (2^17 + 64 rows: a
-    ragged last tile)"""
+    ReLU applied while the next 256 x 256 product stages its rows; its weight gradient
+    ov3d_wgrad_bn applies the same BN + ReLU as it loads the pre-BN rows) against
+    heads.bn_relu_rows + gemm.rows_linear: output, input / gamma / beta / weight gradients and
+    running statistics bit for bit (2^17 + 64 rows: a ragged last tile), the weight gradient
+    immediate or deferred to the end of the backward (gemm.DEFER_WGRAD)"""
     from ov3d_amd import gemm, heads
+    monkeypatch.setattr(gemm, "DEFER_WGRAD", defer)
     torch.manual_seed(12)
     dev = torch.device("cuda", 0)
     R, C = (1 << 17) + 64, 256
