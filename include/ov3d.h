@@ -483,15 +483,16 @@ int ov3d_conv3x3_gemm256(const void* X, int nimg, int H, int W, int Cin, const v
                          long long ldb, const void* bias, int bias_f32, const void* R, long long ldr,
                          void* Y, long long ldc, int Cout, int relu, void* stream);
 
-/* Streaming Y (M, 256) = X (M, K) . W (256, K)^T, K = 256 or 264 (the first layer's zero-padded
- * 259 inputs), for long row sets (csrc/rows256.hip): the
+/* Streaming Y (M, N) = X (M, K) . W (N, K)^T, K = 256 or 264 (the first layer's zero-padded
+ * 259 inputs), N = 256 or 264 (with K = 256: that layer's input gradient), for long row sets
+ * (csrc/rows256.hip): the
  * masked encoder's interim SA 1x1 convolutions [models/model_3detr.py:377-399,
  * third_party/pointnet2/pointnet2_modules.py PointnetSAModuleVotes mlp] and their input
  * gradients.  bf16 rows, 16-byte aligned X / W / Y, ld % 8; equals ov3d_gemm256 with no bias,
  * residual or ReLU bit for bit.  counters: 2 device uints, zero, left zero by every launch (one
  * launch at a time per counter pair). */
 int ov3d_rows256_supported(long long M, int N, int K);
-int ov3d_rows256(const void* X, long long ldx, int K, const void* W, long long ldw, void* Y,
+int ov3d_rows256(const void* X, long long ldx, int K, int N, const void* W, long long ldw, void* Y,
                  long long ldy, long long M, unsigned int* counters, void* stream);
 /* ov3d_rows256 of Z = bf16(relu(X * scale + shift)) (the previous layer's BatchNorm + ReLU, the
  * ov3d_rows_bn_apply arithmetic without dropout; scale / shift (256) fp32) with Z also written

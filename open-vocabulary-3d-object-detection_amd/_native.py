@@ -127,7 +127,7 @@ _SIGS = {
     "ov3d_gemm256_pair": "pplpplppippliiip",
     "ov3d_gemm256_batched": "pllpllpliplliiiiip",
     "ov3d_lngemm_fwd": "ipipfpipppippfppppppilllipifpip",
-    "ov3d_rows256": "pliplpllpp",
+    "ov3d_rows256": "pliiplpllpp",
     "ov3d_rows256_bn": "plppplplpllpp",
     "ov3d_lngemm_bwd": "ipppppppilllppfpipppipipliifplplp",
 }

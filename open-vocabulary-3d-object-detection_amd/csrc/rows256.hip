@@ -39,6 +39,7 @@ constexpr int KD = 256;                 // K = N
 constexpr int TILE_BYTES = TM * KD * 2; // 64 KB
 constexpr int RB = TM / 16;             // 16-row blocks a tile
 constexpr int TAIL_BYTES = TM * 16;     // KT: the K = 256 .. 263 chunk of a tile's rows
+constexpr int WX_BYTES = 16 * KD * 2;   // NX: W rows 256 .. 271 (zeros past 263), swizzled
 
 __device__ __forceinline__ f32x4 mfma16(i32x4 a, i32x4 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
@@ -104,10 +105,14 @@ __device__ __forceinline__ void lds_write128(uint32_t addr, i32x4 v) {
 // K-step (k 256 .. 319, zeros past 264) as two more 32-deep MFMA steps, the rows' chunk 32 in a
 // tail image filled by two more DMA pieces (waves 6 and 7)
 // BNIN: 0 none, 1 BN + ReLU on the staged rows and Z stored, 2 the same without Z (its weight
-// gradient applies the BN on load: ov3d_wgrad_bn)
-template <int BNIN, bool KT>
+// gradient applies the BN on load: ov3d_wgrad_bn).
+// NX: N = 264 (the first layer's input gradient, 259 + 5 zero columns): every wave also
+// computes output columns 256 .. 271 (W rows past 263 zero) of its own 16-row block, W's rows
+// 256 .. 271 read from an LDS image; the 8 real columns leave through a 2 KB tail image
+template <int BNIN, bool KT, bool NX>
 __global__ void __launch_bounds__(NT, 1) rows256_kernel(Rows256Args a) {
-    __shared__ __attribute__((aligned(16))) char L[2 * TILE_BYTES + (KT ? 2 * TAIL_BYTES : 0)];
+    __shared__ __attribute__((aligned(16))) char L[2 * TILE_BYTES + (KT ? 2 * TAIL_BYTES : 0) +
+                                                   (NX ? WX_BYTES + TAIL_BYTES : 0)];
     __shared__ int s_claim[2];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -129,6 +134,12 @@ __global__ void __launch_bounds__(NT, 1) rows256_kernel(Rows256Args a) {
             wf[cb][ks] = *reinterpret_cast<const i32x4*>(a.W + (size_t)(32 * w + 16 * cb + li) * a.ldw +
                                                          32 * ks + 8 * lg);
     const i32x4 zero4 = {0, 0, 0, 0};
+    if constexpr (NX) {   // W rows 256 .. 271 -> the WX image (chunk c of row j at c ^ j)
+        const int j = tid >> 5, c = tid & 31;
+        const i32x4 v = 256 + j < 264
+            ? *reinterpret_cast<const i32x4*>(a.W + (size_t)(256 + j) * a.ldw + 8 * c) : zero4;
+        *reinterpret_cast<i32x4*>(L + 2 * TILE_BYTES + j * KD * 2 + 16 * (c ^ j)) = v;
+    }
     i32x4 wt[2] = {zero4, zero4};   // KT: k = 256 + 8 lg .. (lg = 0 only; zeros past 264)
     if constexpr (KT) {
         if (lg == 0)
@@ -237,6 +248,7 @@ __global__ void __launch_bounds__(NT, 1) rows256_kernel(Rows256Args a) {
 #pragma unroll
             for (int cb = 0; cb < 2; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
         const uint32_t tb = lds0 + buf * TILE_BYTES + rowoff;
+        f32x4 accx = {0.f, 0.f, 0.f, 0.f};   // NX: columns 256 .. 271 of rows 16 w + li
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks) {
             i32x4 xf[RB];
@@ -248,6 +260,13 @@ __global__ void __launch_bounds__(NT, 1) rows256_kernel(Rows256Args a) {
             for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
                 for (int cb = 0; cb < 2; ++cb) acc[rb][cb] = mfma16(wf[cb][ks], xf[rb], acc[rb][cb]);
+            if constexpr (NX) {
+                i32x4 xe[2];
+                xe[0] = lds128(tb + w * 16 * KD * 2 + co);                       // rows 16 w + li
+                xe[1] = lds128(lds0 + 2 * TILE_BYTES + li * KD * 2 + co);        // W row 256 + li
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xe[0]), "+v"(xe[1]) : : "memory");
+                accx = mfma16(xe[1], xe[0], accx);
+            }
         }
         if constexpr (KT) {
             // k 256 .. 287: chunk 32 from the tail image (lg = 0), zeros (lg > 0); then k 288 ..
@@ -286,6 +305,15 @@ __global__ void __launch_bounds__(NT, 1) rows256_kernel(Rows256Args a) {
                 lds_write64(ib + r * KD * 2 + 16 * (c ^ li) + 8 * (lg & 1), o);
             }
         }
+        const uint32_t ot = lds0 + 2 * TILE_BYTES + WX_BYTES;   // NX: columns 256 .. 263
+        if constexpr (NX) {
+            if (lg < 2) {
+                bf16x4 o;
+#pragma unroll
+                for (int v = 0; v < 4; ++v) o[v] = (bf16)accx[v];
+                lds_write64(ot + (16 * w + li) * 16 + 8 * lg, o);
+            }
+        }
         // LDS writes done, then the raw barrier (__syncthreads' fence would also wait for the
         // next tile's DMA)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -301,6 +329,15 @@ __global__ void __launch_bounds__(NT, 1) rows256_kernel(Rows256Args a) {
         for (int i = 0; i < 8; ++i) {
             const int q = tid + NT * i, r = q >> 5, c = q & 31;
             if (m0 + r < a.M) *reinterpret_cast<i32x4*>(a.Y + (m0 + r) * a.ldy + 8 * c) = sv[i];
+        }
+        if constexpr (NX) {   // waves 6, 7 (wave 0's claim wait stays exact): row tid - 384
+            if (tid >= 384) {
+                const int r = tid - 384;
+                i32x4 v[RB];
+                v[0] = lds128(ot + r * 16);
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]) : : "memory");
+                if (m0 + r < a.M) *reinterpret_cast<i32x4*>(a.Y + (m0 + r) * a.ldy + 256) = v[0];
+            }
         }
         prev_stores = true;
         if (tid == 0 && has_next) {
@@ -328,19 +365,19 @@ int g_cus = 0;
 }  // namespace
 
 extern "C" int ov3d_rows256_supported(long long M, int N, int K) {
-    return M > 0 && N == KD && (K == KD || K == KD + 8) && (M + TM - 1) / TM < (1LL << 31) &&
-           M * KD * 2 < (1LL << 40);
+    return M > 0 && (N == KD || (N == KD + 8 && K == KD)) && (K == KD || K == KD + 8) &&
+           (M + TM - 1) / TM < (1LL << 31) && M * KD * 2 < (1LL << 40);
 }
 
 namespace {
 struct BnIn {
     const float* scale; const float* shift; void* Z; long long ldz;
 };
-int rows256_launch(const void* X, long long ldx, int K, const void* W, long long ldw, void* Y,
+int rows256_launch(const void* X, long long ldx, int K, int N, const void* W, long long ldw, void* Y,
                    long long ldy, long long M, unsigned int* counters, const BnIn* bn, void* stream) {
-    if (!ov3d_rows256_supported(M, KD, K) || (bn && K != KD) || !X || !W || !Y || !counters ||
-        ldx < K || ldw < K ||
-        ldy < KD || ldx % 8 || ldw % 8 || ldy % 8 || ((uintptr_t)X | (uintptr_t)W | (uintptr_t)Y) % 16 ||
+    if (!ov3d_rows256_supported(M, N, K) || (bn && (K != KD || N != KD)) || !X || !W || !Y ||
+        !counters || ldx < K || ldw < K ||
+        ldy < N || ldx % 8 || ldw % 8 || ldy % 8 || ((uintptr_t)X | (uintptr_t)W | (uintptr_t)Y) % 16 ||
         (uintptr_t)counters % 8)
         return OV3D_EINVAL;
     // the buffer resource of a tile covers at most 2 GB from its first row
@@ -360,27 +397,29 @@ int rows256_launch(const void* X, long long ldx, int K, const void* W, long long
             ((uintptr_t)bn->scale | (uintptr_t)bn->shift | (uintptr_t)bn->Z) % 16)
             return OV3D_EINVAL;
         a.scale = bn->scale; a.shift = bn->shift; a.Z = (bf16*)bn->Z; a.ldz = bn->ldz;
-        if (bn->Z) rows256_kernel<1, false><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
-        else rows256_kernel<2, false><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
+        if (bn->Z) rows256_kernel<1, false, false><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
+        else rows256_kernel<2, false, false><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
+    } else if (N != KD) {
+        rows256_kernel<0, false, true><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
     } else if (K == KD) {
-        rows256_kernel<0, false><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
+        rows256_kernel<0, false, false><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
     } else {
-        rows256_kernel<0, true><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
+        rows256_kernel<0, true, false><<<grid, NT, 0, ov3d_stream(stream)>>>(a);
     }
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }
 }  // namespace
 
-extern "C" int ov3d_rows256(const void* X, long long ldx, int K, const void* W, long long ldw,
+extern "C" int ov3d_rows256(const void* X, long long ldx, int K, int N, const void* W, long long ldw,
                             void* Y, long long ldy, long long M, unsigned int* counters,
                             void* stream) {
-    return rows256_launch(X, ldx, K, W, ldw, Y, ldy, M, counters, nullptr, stream);
+    return rows256_launch(X, ldx, K, N, W, ldw, Y, ldy, M, counters, nullptr, stream);
 }
 
 extern "C" int ov3d_rows256_bn(const void* X, long long ldx, const float* scale, const float* shift,
                                const void* W, long long ldw, void* Y, long long ldy, void* Z,
                                long long ldz, long long M, unsigned int* counters, void* stream) {
     const BnIn bn{scale, shift, Z, ldz};
-    return rows256_launch(X, ldx, KD, W, ldw, Y, ldy, M, counters, &bn, stream);
+    return rows256_launch(X, ldx, KD, KD, W, ldw, Y, ldy, M, counters, &bn, stream);
 }

@@ -341,19 +341,22 @@ ROWS256 = os.environ.get("OV3D_ROWS256", "1") != "0"
 
 
 def rows256_ok(a, w, bias=None):
-    """a (M, K) x w (256, K)^T, K = 256 or 264 (the zero-padded first layer), runs on rows256"""
+    """a (M, K) x w (N, K)^T runs on rows256: (K, N) = (256, 256), (264, 256) (the zero-padded
+    first layer) or (256, 264) (its input gradient)"""
     from . import _native
     K = a.shape[1] if a.dim() == 2 else 0
+    N = w.shape[0] if w.dim() == 2 else 0
     return (ROWS256 and bias is None and a.shape[0] >= GEMM256_MIN_M and _rows_ok(a) and _rows_ok(w)
-            and K in (256, 264) and tuple(w.shape) == (256, K)
-            and bool(_native.load().ov3d_rows256_supported(a.shape[0], 256, K)))
+            and (K, N) in ((256, 256), (264, 256), (256, 264)) and w.shape[1] == K
+            and bool(_native.load().ov3d_rows256_supported(a.shape[0], N, K)))
 
 
 def rows256(a, w):
-    """a (M, K) w (256, K)^T -> (M, 256) bf16 (check rows256_ok first)"""
+    """a (M, K) w (N, K)^T -> (M, N) bf16 (check rows256_ok first)"""
     from . import _native
-    out = torch.empty((a.shape[0], 256), dtype=torch.bfloat16, device=a.device)
-    _native.call("ov3d_rows256", a, a.stride(0), a.shape[1], w, w.stride(0), out, out.stride(0),
+    N = w.shape[0]
+    out = torch.empty((a.shape[0], N), dtype=torch.bfloat16, device=a.device)
+    _native.call("ov3d_rows256", a, a.stride(0), a.shape[1], N, w, w.stride(0), out, out.stride(0),
                  a.shape[0], _rows256_counters(a.device), like=a)
     return out
 

@@ -185,7 +185,7 @@ def test_rows256_equals_gemm256_bitwise(M, ldx):
     x = xb[:, :256]
     w = (0.06 * torch.randn(256, 256, device=dev)).to(torch.bfloat16)
     y = torch.full((M, 256), float("nan"), device=dev, dtype=torch.bfloat16)
-    _native.call("ov3d_rows256", x, x.stride(0), 256, w, w.stride(0), y, y.stride(0), M,
+    _native.call("ov3d_rows256", x, x.stride(0), 256, 256, w, w.stride(0), y, y.stride(0), M,
                  gemm._rows256_counters(dev), like=x)
     ref = gemm.gemm256(x, w)
     assert torch.equal(y, ref)
@@ -231,8 +231,27 @@ def test_rows256_k264_equals_gemm256_bitwise(M):
     x[:3] = 0
     w = torch.nn.functional.pad((0.06 * torch.randn(256, 259, device=dev)).to(torch.bfloat16), (0, 5))
     y = torch.full((M, 256), float("nan"), device=dev, dtype=torch.bfloat16)
-    _native.call("ov3d_rows256", x, x.stride(0), 264, w, w.stride(0), y, y.stride(0), M,
+    _native.call("ov3d_rows256", x, x.stride(0), 264, 256, w, w.stride(0), y, y.stride(0), M,
                  gemm._rows256_counters(dev), like=x)
     assert torch.equal(y, gemm.gemm256(x, w))
     if M >= gemm.GEMM256_MIN_M:
         assert gemm.rows256_ok(x, w) and torch.equal(gemm._linear(x, w, None), y)
+
+
+@pytest.mark.parametrize("M", [262144, 131072 + 37, 150])
+def test_rows256_n264_equals_gemm256_bitwise(M):
+    """the first interim SA layer's input gradient dy (M, 256) . W (256, 264): 264 output columns
+    (the 8 past 256 from an extra 16-column block per wave) against gemm256, every bit; routed
+    from gemm._dgrad"""
+    from ov3d_amd import _native, gemm
+    torch.manual_seed(6)
+    dev = torch.device("cuda", 0)
+    dy = torch.randn(M, 256, device=dev).to(torch.bfloat16)
+    w = torch.nn.functional.pad((0.06 * torch.randn(256, 259, device=dev)).to(torch.bfloat16), (0, 5))
+    wt = w.t().contiguous()                        # (264, 256) rows
+    y = torch.full((M, 264), float("nan"), device=dev, dtype=torch.bfloat16)
+    _native.call("ov3d_rows256", dy, dy.stride(0), 256, 264, wt, wt.stride(0), y, y.stride(0), M,
+                 gemm._rows256_counters(dev), like=dy)
+    assert torch.equal(y, gemm.gemm256(dy, wt))
+    if M >= gemm.GEMM256_MIN_M:
+        assert gemm.rows256_ok(dy, wt) and torch.equal(gemm._dgrad(dy, w), y)

@@ -24,7 +24,7 @@ def main():
     res = {}
 
     def run_rows():
-        _native.call("ov3d_rows256", x, 256, 256, w, 256, y, 256, M, gemm._rows256_counters(dev), like=x)
+        _native.call("ov3d_rows256", x, 256, 256, 256, w, 256, y, 256, M, gemm._rows256_counters(dev), like=x)
 
     def run_g256():
         gemm.gemm256(x, w, out=y)
