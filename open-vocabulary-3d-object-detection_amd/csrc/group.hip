@@ -678,6 +678,10 @@ __global__ __launch_bounds__(256) void inv_sort_kernel(const int32_t* __restrict
 // (bf16 autocast rounds the fp32 rows to these values before the GEMM anyway).  One thread per
 // 8 columns of a row: consecutive threads cover a row left to right (contiguous feature reads
 // for channel-contiguous features), one 16-byte store each.
+// VEC: channel-contiguous feature rows (sc = 1, C % 4 == 0, 16-byte aligned rows): the 8
+// feature values of a chunk (channels c0 - 3 .. c0 + 4) from three aligned 16-byte loads
+// instead of eight misaligned 4-byte ones (same values)
+template <bool VEC>
 __global__ __launch_bounds__(256) void group_rows_bf16_kernel(
     const float* __restrict__ xyz, const float* __restrict__ new_xyz,
     const float* __restrict__ feats, long long sb, long long sn, long long sc,
@@ -694,6 +698,16 @@ __global__ __launch_bounds__(256) void group_rows_bf16_kernel(
     const int m = (int)((row / S) % M);
     const int k = idx[row];
     const float* const f = feats ? feats + b * sb + k * sn : nullptr;
+    float fv[12];   // VEC: features c0 - 4 .. c0 + 7 (zeros outside 0 .. C - 1)
+    if constexpr (VEC) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int e = c0 - 4 + 4 * q;
+            float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (e >= 0 && e + 4 <= C) u = *reinterpret_cast<const float4*>(f + e);
+            fv[4 * q] = u.x; fv[4 * q + 1] = u.y; fv[4 * q + 2] = u.z; fv[4 * q + 3] = u.w;
+        }
+    }
     bf16x8 v;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -703,7 +717,8 @@ __global__ __launch_bounds__(256) void group_rows_bf16_kernel(
             x = xyz[((size_t)b * N + k) * 3 + c] - new_xyz[((size_t)b * M + m) * 3 + c];
             if (normalize) x = x / radius;
         } else if (c < 3 + C) {
-            x = f[(c - 3) * sc];
+            if constexpr (VEC) x = fv[j + 1];   // channel c - 3 = (c0 - 4) + (j + 1)
+            else x = f[(c - 3) * sc];
         }
         v[j] = (__bf16)x;
     }
@@ -816,10 +831,17 @@ extern "C" int ov3d_group_rows_bf16(const float* xyz, const float* new_xyz, cons
     if (C > 0 && !features) return OV3D_EINVAL;
     const long long total = (long long)B * M * S * (ldo / 8);
     if (total == 0) return OV3D_OK;
-    hipLaunchKernelGGL(group_rows_bf16_kernel, dim3(ov3d_cdiv(total, 256)), dim3(256), 0,
-                       ov3d_stream(stream), xyz, new_xyz, C > 0 ? features : nullptr, feat_sb,
-                       feat_sn, feat_sc, idx, B, C, N, M, S, radius, normalize, ldo,
-                       static_cast<__bf16*>(out));
+    const bool vec = C > 0 && feat_sc == 1 && C % 4 == 0 && feat_sb % 4 == 0 && feat_sn % 4 == 0 &&
+                     ((uintptr_t)features & 15) == 0;
+    if (vec)
+        hipLaunchKernelGGL(group_rows_bf16_kernel<true>, dim3(ov3d_cdiv(total, 256)), dim3(256), 0,
+                           ov3d_stream(stream), xyz, new_xyz, features, feat_sb, feat_sn, feat_sc,
+                           idx, B, C, N, M, S, radius, normalize, ldo, static_cast<__bf16*>(out));
+    else
+        hipLaunchKernelGGL(group_rows_bf16_kernel<false>, dim3(ov3d_cdiv(total, 256)), dim3(256), 0,
+                           ov3d_stream(stream), xyz, new_xyz, C > 0 ? features : nullptr, feat_sb,
+                           feat_sn, feat_sc, idx, B, C, N, M, S, radius, normalize, ldo,
+                           static_cast<__bf16*>(out));
     OV3D_LAUNCH_CHECK();
     return OV3D_OK;
 }

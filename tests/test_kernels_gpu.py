@@ -439,3 +439,34 @@ def test_add_cast_bf16_equals_torch(cuda):
     ab = a.to(torch.bfloat16)
     _native.call("ov3d_add_cast_bf16", ab, 1, b, a.numel(), s, None, like=a)
     assert torch.equal(s, (ab.float() + b).to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("C,layout", [(256, "nbc"), (256, "bcn"), (20, "nbc"), (0, "nbc")])
+def test_group_rows_bf16_bit_exact(cuda, C, layout):
+    """ov3d_group_rows_bf16 (the interim SA's grouped rows: (xyz[idx] - centroid) / r, then the
+    features, bf16, zero-padded to a multiple of 8 columns) against the same fp32 arithmetic in
+    torch, every bit: channel-contiguous features of the encoder's (N, B, C) rows (three aligned
+    16-byte loads per chunk), channel-strided (B, C, N) rows and C % 4 != 0 (per-element loads)"""
+    from ov3d_amd import _native
+    torch.manual_seed(8)
+    B, N, M, S, r = 2, 1024, 128, 32, 0.4
+    xyz = torch.rand(B, N, 3, device=cuda) * 2
+    nxyz = xyz[:, :M].contiguous()
+    idx = torch.randint(0, N, (B, M, S), device=cuda, dtype=torch.int32)
+    if layout == "nbc":
+        feats = torch.randn(N, B, max(C, 1), device=cuda)[..., :C].permute(1, 2, 0)   # (B, C, N) view
+    else:
+        feats = torch.randn(B, max(C, 1), N, device=cuda)[:, :C]
+    cp = (3 + C + 7) // 8 * 8
+    out = torch.empty((B, M, S, cp), dtype=torch.bfloat16, device=cuda)
+    st = feats.stride()
+    _native.call("ov3d_group_rows_bf16", xyz, nxyz, feats if C else None, st[0], st[2], st[1], idx,
+                 B, C, N, M, S, r, 1, cp, out, like=xyz)
+    il = idx.long()
+    gx = torch.gather(xyz, 1, il.view(B, -1, 1).expand(-1, -1, 3)).view(B, M, S, 3)
+    ref = torch.zeros((B, M, S, cp), device=cuda)
+    ref[..., :3] = (gx - nxyz[:, :, None, :]) / r
+    if C:
+        ft = feats.transpose(1, 2)                                          # (B, N, C)
+        ref[..., 3:3 + C] = torch.gather(ft, 1, il.view(B, -1, 1).expand(-1, -1, C)).view(B, M, S, C)
+    assert torch.equal(out, ref.to(torch.bfloat16))
