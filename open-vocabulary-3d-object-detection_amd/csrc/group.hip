@@ -768,6 +768,69 @@ __global__ __launch_bounds__(256) void group_bwd_csr_kernel(const GT* __restrict
     gfeat[b * sb + n * sn + c * sc] = acc;
 }
 
+typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+
+// the same gather over bf16 rows with ldg % 8 == 0 and 16-byte aligned rows: a thread owns
+// the 16-byte chunk q of each row it reads (columns 8q .. 8q+7 = channels 8q-3 .. 8q+4), one
+// row id and one 16-byte load per entry instead of one of each per channel.  Each channel sums
+// its entries in the scalar kernel's order (8 a round, a zero-padded tail round): bit-equal.
+__global__ __launch_bounds__(256) void group_bwd_csr_vec_kernel(const __bf16* __restrict__ gout,
+                                                                long long ldg,
+                                                                const int32_t* __restrict__ off,
+                                                                const int32_t* __restrict__ rows,
+                                                                int B, int C, int N, int nq,
+                                                                long long sb, long long sn,
+                                                                long long sc,
+                                                                float* __restrict__ gfeat) {
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long long)B * N * nq) return;
+    const int q = (int)(t % nq);
+    const long long bn = t / nq;
+    const int b = (int)(bn / N), n = (int)(bn - (long long)b * N);
+    const int e0 = off[bn], e1 = off[bn + 1];
+    const __bf16* g = gout + 8 * q;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    int e = e0;
+    for (; e + 8 <= e1; e += 8) {
+        int r[8];
+        bf16x8v v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) r[u] = rows[e + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const bf16x8v*>(g + (size_t)r[u] * ldg);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[j] += (float)v[u][j];
+    }
+    if (e < e1) {
+        int r[8];
+        bf16x8v v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) r[u] = e + u < e1 ? rows[e + u] : -1;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (r[u] >= 0) {
+                v[u] = *reinterpret_cast<const bf16x8v*>(g + (size_t)r[u] * ldg);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[u][j] = (__bf16)0.f;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[j] += (float)v[u][j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int c = 8 * q + j - 3;
+        if (c >= 0 && c < C) gfeat[b * sb + n * sn + c * sc] = acc[j];
+    }
+}
+
 }  // namespace
 
 extern "C" int ov3d_group_inverse(const int32_t* idx, int B, int N, int M, int S, int32_t* cnt,
@@ -814,6 +877,15 @@ extern "C" int ov3d_group_bwd_csr_bf16(const void* grad_out, long long ldg, cons
         return OV3D_EINVAL;
     const long long total = (long long)B * N * C;
     if (total == 0) return OV3D_OK;
+    if (ldg % 8 == 0 && reinterpret_cast<uintptr_t>(grad_out) % 16 == 0) {
+        const int nq = (3 + C + 7) / 8;   // <= ldg / 8
+        const long long tv = (long long)B * N * nq;
+        hipLaunchKernelGGL(group_bwd_csr_vec_kernel, dim3(ov3d_cdiv(tv, 256)), dim3(256), 0,
+                           ov3d_stream(stream), static_cast<const __bf16*>(grad_out), ldg, offsets,
+                           rows, B, C, N, nq, feat_sb, feat_sn, feat_sc, grad_features);
+        OV3D_LAUNCH_CHECK();
+        return OV3D_OK;
+    }
     hipLaunchKernelGGL(group_bwd_csr_kernel<__bf16>, dim3(ov3d_cdiv(total, 256)), dim3(256), 0,
                        ov3d_stream(stream), static_cast<const __bf16*>(grad_out), ldg, offsets, rows,
                        B, C, N, feat_sb, feat_sn, feat_sc, grad_features);

@@ -470,3 +470,37 @@ def test_group_rows_bf16_bit_exact(cuda, C, layout):
         ft = feats.transpose(1, 2)                                          # (B, N, C)
         ref[..., 3:3 + C] = torch.gather(ft, 1, il.view(B, -1, 1).expand(-1, -1, C)).view(B, M, S, C)
     assert torch.equal(out, ref.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("C,ldg_kind", [(256, "cp"), (20, "cp"), (256, "odd"), (20, "odd")])
+def test_group_bwd_csr_bf16_bit_exact(cuda, C, ldg_kind):
+    """ov3d_group_bwd_csr_bf16 (the interim SA grouping's gather-form backward over bf16 row
+    gradients) against a torch sum in the inverse's entry order, every bit: the 16-byte chunk
+    kernel (ldg = cp, a multiple of 8) and the per-channel kernel (ldg = 3 + C, odd)"""
+    from ov3d_amd import _native
+    from ov3d_amd import pointnet2_utils as pu
+    torch.manual_seed(9)
+    B, N, M, S = 2, 512, 256, 16
+    idx = torch.randint(0, N, (B, M, S), device=cuda, dtype=torch.int32)
+    idx[0, :8] = 7                                   # a point with many entries (> 8 rounds)
+    off, rows = pu.group_inverse(idx, N)
+    ldg = (3 + C + 7) // 8 * 8 if ldg_kind == "cp" else 3 + C + (0 if (3 + C) % 2 else 1)
+    g = torch.randn(B * M * S, ldg, device=cuda).to(torch.bfloat16)
+    gf = torch.full((N, B, C), float("nan"), device=cuda).permute(1, 2, 0)   # (B, C, N) view
+    st = gf.stride()
+    _native.call("ov3d_group_bwd_csr_bf16", g, ldg, off, rows, B, C, N, st[0], st[2], st[1], gf,
+                 like=g)
+    offc, rowsc = off.cpu().long(), rows.cpu().long()
+    deg = offc[1:] - offc[:-1]
+    D = int(deg.max())
+    ent = torch.full((B * N, D), -1, dtype=torch.long)
+    for p in range(B * N):
+        ent[p, :deg[p]] = rowsc[offc[p]:offc[p + 1]]
+    feat = g[:, 3:3 + C].float()
+    acc = torch.zeros((B * N, C), device=cuda)
+    ent = ent.to(cuda)
+    for k in range(D):
+        e = ent[:, k]
+        acc = acc + torch.where((e >= 0)[:, None], feat[e.clamp(min=0)], torch.zeros((), device=cuda))
+    ref = acc.view(B, N, C).transpose(1, 2)
+    assert torch.equal(gf, ref)
